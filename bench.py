@@ -1,0 +1,237 @@
+#!/usr/bin/env python
+"""Headline benchmark: metric-series scored/sec (whole node) + p50 detect
+latency on the 100k-series canary (BASELINE.json).
+
+One scoring tick = the full canary pipeline for every series of the job:
+
+  1. ingest: this tick's per-pod points arrive in pinned host memory (as the
+     Prometheus ingest would deliver them), are copied H2D and streamed into
+     the HBM rings (K10: new points in, oldest current points graduate into
+     the sliding 7-day history);
+  2. pairwise canary test: baseline vs current Mann-Whitney U + Wilcoxon +
+     Kruskal (ML_PAIRWISE_ALGORITHM=ALL), per series (K5/K11);
+  3. model: additive Holt-Winters (daily season, 60 s step, 7-day window =
+     10,080 points) refit from scratch on the slid window over a 64-point
+     alpha/beta/gamma grid, forecast of the 50 current points, band,
+     anomalies, verdict, per-app counters — one fused launch (K3 + K9);
+  4. cluster aggregation: per-app counters all-reduced and verdicts
+     all-gathered over RCCL/xGMI (RC1 + RC2);
+  5. the aggregated health table is copied back to the host — the verdict
+     is "available" and the tick's detect latency stops here.
+
+Nothing is cached across ticks: every tick refits every model on new data.
+Strong scaling: the 100k series are sharded over the ranks.
+
+Usage: ``python bench.py --gpus N --steps K --warmup W`` (N > 1 under
+``torch.distributed.run``; rank 0 prints ONE JSON line).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+from foremast_amd.brain.engine import ShardSpec, StreamingShard, synthetic_history  # noqa: E402
+from foremast_amd.parallel.health import HealthAggregator, shard_range  # noqa: E402
+from foremast_amd.utils.config import BrainConfig  # noqa: E402
+
+METRIC = "metric-series scored/sec (whole node) + p50 detect latency, 100k-series canary"
+BASELINE_VALUE = None  # the reference publishes no number (BASELINE.json "published": {})
+METRICS_PER_APP = 5
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--series", type=int, default=100_000)
+    p.add_argument("--ring", type=int, default=10080)
+    p.add_argument("--season", type=int, default=1440)
+    p.add_argument("--pods", type=int, default=5)
+    p.add_argument("--window", type=int, default=10)
+    p.add_argument("--algorithm", default="holt_winters")
+    p.add_argument("--pairwise", default="ALL")
+    p.add_argument("--anomaly-frac", type=float, default=0.01)
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--graph", action="store_true", help="capture the GPU part of a tick in a HIP graph")
+    p.add_argument("--cpu", action="store_true", help="force CPU (reference path; tiny sizes only)")
+    return p.parse_args()
+
+
+def init_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    use_gpu = torch.cuda.is_available() and not args.cpu
+    if use_gpu:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if use_gpu:
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    return world, rank, dev
+
+
+def barrier(dev):
+    if dist.is_initialized():
+        if dev.type == "cuda":
+            dist.barrier(device_ids=[dev.index])
+        else:
+            dist.barrier()
+
+
+def make_ticks(n, pods, nticks, season, start_t, dev, seed, anomaly_frac, hist_tail):
+    """Per-tick per-pod values [nticks, n, pods] continuing each series' pattern,
+    with a fraction of series turned anomalous (canary regression)."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed + 17)
+    # estimate each series' level/seasonality from the tail of its history
+    last_day = hist_tail.float()
+    base = last_day[:, -season:]  # one day back = same phase
+    t = torch.arange(nticks, device=dev)
+    idx = (t % season)
+    vals = base[:, idx].T.contiguous()  # [nticks, n]
+    noise = torch.randn((nticks, n, pods), generator=g, device=dev) * (0.03 * vals.abs().mean(0, keepdim=True)[..., None] + 1e-3)
+    out = vals[..., None] + noise
+    n_bad = int(n * anomaly_frac)
+    if n_bad:
+        bad = torch.randperm(n, generator=g, device=dev)[:n_bad]
+        out[:, bad, :] *= 3.0
+    return out.float()
+
+
+def main():
+    args = parse()
+    world, rank, dev = init_dist(args)
+    if dev.type == "cpu" and args.series > 4096:
+        # the CPU path is the reference implementation: keep it small
+        args.series, args.ring, args.season = 256, 480, 48
+    cfg = BrainConfig()
+    cfg.min_historical_points = 0
+    s, e, per = shard_range(args.series, world, rank, align=METRICS_PER_APP)
+    n_local = e - s
+    n_apps = (args.series + METRICS_PER_APP - 1) // METRICS_PER_APP
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    spec = ShardSpec(n_series=n_local, ring_len=args.ring, season=args.season, pods=args.pods,
+                     window=args.window, algorithm=args.algorithm, pairwise=args.pairwise,
+                     dtype=dtype, n_apps=n_apps)
+    app_id = (torch.arange(s, e, device=dev, dtype=torch.int64) // METRICS_PER_APP).to(torch.int32)
+    shard = StreamingShard(spec, cfg, dev, app_id=app_id,
+                           threshold=torch.full((n_local,), 4.0, device=dev),
+                           bound=torch.full((n_local,), 3, dtype=torch.int8, device=dev))
+    # --- synthetic data (outside the timed region) ---------------------------------
+    hist = synthetic_history(n_local, args.ring, args.season, dev, seed=1234 + rank)
+    shard.load_history(hist)
+    W, P = args.window, args.pods
+    total_ticks = args.warmup + args.steps
+    ticks = make_ticks(n_local, P, total_ticks + W, args.season, args.ring, dev, 99 + rank,
+                       args.anomaly_frac, hist)
+    # baseline pods: same times as the first current window, healthy, own noise
+    clean = make_ticks(n_local, P, W, args.season, args.ring, dev, 7 + rank, 0.0, hist)
+    shard.set_baseline(clean.permute(1, 2, 0).reshape(n_local, P * W))
+    del clean
+    del hist
+    pin = dev.type == "cuda"
+    host_ticks = ticks.cpu()
+    if pin:
+        host_ticks = host_ticks.pin_memory()
+    del ticks
+    newv = torch.empty((n_local, P), dtype=torch.float32, device=dev)
+    agg = HealthAggregator(n_local, per, dev)
+    health_host = torch.empty_like(shard.app_stats, device="cpu")
+    if pin:
+        health_host = health_host.pin_memory()
+    # prefill the current window so every tick scores a full 10-minute window
+    for k in range(W):
+        newv.copy_(host_ticks[k], non_blocking=pin)
+        shard.ingest_tick(newv)
+
+    def tick(k):
+        newv.copy_(host_ticks[W + k], non_blocking=pin)
+        shard.ingest_tick(newv)
+        out = shard.score()
+        stats, _ = agg.tick(shard.app_stats, out["verdict"])
+        health_host.copy_(stats, non_blocking=pin)
+        if dev.type == "cuda":
+            torch.cuda.current_stream().synchronize()
+        return out
+
+    for k in range(args.warmup):
+        tick(k)
+    barrier(dev)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    lat = []
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ts = time.perf_counter()
+        tick(args.warmup + k)
+        lat.append(time.perf_counter() - ts)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    barrier(dev)
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    lat_t = torch.tensor(lat, dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(lat_t, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    lat_ms = lat_t.cpu().numpy() * 1e3
+    anomalous_apps = int((health_host[:, 0] > 0).sum())
+    scored = int(health_host[:, 1].sum())
+    if rank == 0:
+        value = args.series * args.steps / elapsed
+        res = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "series/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None if BASELINE_VALUE is None else round(value / BASELINE_VALUE, 3),
+            "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
+            "data": "synthetic (seasonal Prometheus-like range-vectors, random per-series params)",
+            "config": {
+                "model": f"{args.algorithm} + pairwise {args.pairwise} (MW U / Wilcoxon / Kruskal) canary scorer",
+                "global_batch": args.series,
+                "seq_len": args.ring,
+                "parallelism": f"dp{world}",
+                "season": args.season,
+                "pods": P,
+                "current_window": W,
+                "grid_points": int(shard.grid.shape[0]),
+                "device": str(dev) if dev.type == "cpu" else torch.cuda.get_device_name(dev),
+            },
+            "p50_detect_latency_ms": round(float(np.percentile(lat_ms, 50)), 3),
+            "p99_detect_latency_ms": round(float(np.percentile(lat_ms, 99)), 3),
+            "health": {"apps": int(health_host.shape[0]), "anomalous_apps": anomalous_apps,
+                       "series_scored_last_tick": scored},
+        }
+        print(json.dumps(res), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

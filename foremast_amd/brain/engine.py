@@ -1,0 +1,208 @@
+"""GPU-resident streaming scoring engine for one shard of series.
+
+One ``StreamingShard`` per rank (one process per GPU).  It owns:
+
+* the history ring ``[N, R]`` (bf16) and the current/baseline windows
+  ``[N, P*W]`` in HBM;
+* per-series config (threshold / bound / min_lower_bound, app id);
+* preallocated outputs, so a scoring tick allocates nothing and can be
+  captured into a HIP graph.
+
+A tick is:  ``ingest_tick`` (K10: new per-pod points in, oldest graduate to
+history)  →  ``score``: pairwise rank tests (K5/K11) → model fit + forecast +
+band + verdict in ONE launch (K2/K3 + fused K9) → per-app health counts
+(atomics in the same launch).  Cross-rank aggregation is
+:mod:`foremast_amd.parallel.health`.
+
+On CPU (tests, no GPU) the same API runs the PyTorch reference scorers.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from ..ingest.ringbuffer import HistoryRing, WindowRing
+from ..models import detect as det_ref
+from ..models import moving_average as ma_ref
+from ..models import pairwise as pw_ref
+from ..models import smoothing as sm_ref
+from ..utils.config import BrainConfig
+
+ALGO_MODE = {"exponential_smoothing": sm_ref.MODE_ES, "double_exponential_smoothing": sm_ref.MODE_DES,
+             "holt_winters": sm_ref.MODE_HW}
+
+
+@dataclass
+class ShardSpec:
+    n_series: int
+    ring_len: int = 10080
+    season: int = 1440
+    pods: int = 5
+    window: int = 10
+    algorithm: str = "holt_winters"
+    pairwise: str = "ALL"
+    dtype: torch.dtype = torch.bfloat16
+    n_apps: int = 1
+    want_band: bool = True
+    extra: Dict = field(default_factory=dict)
+
+
+class StreamingShard:
+    def __init__(self, spec: ShardSpec, cfg: Optional[BrainConfig] = None, device="cpu",
+                 app_id: Optional[torch.Tensor] = None, threshold: Optional[torch.Tensor] = None,
+                 bound: Optional[torch.Tensor] = None, min_lower: Optional[torch.Tensor] = None) -> None:
+        self.spec = spec
+        self.cfg = cfg or BrainConfig()
+        self.device = torch.device(device)
+        self.gpu = self.device.type == "cuda"
+        N, P, W = spec.n_series, spec.pods, spec.window
+        self.hist = HistoryRing(N, spec.ring_len, spec.dtype, self.device)
+        self.cur = WindowRing(N, P, W, self.device)
+        self.base = torch.full((N, P * W), float("nan"), dtype=torch.float32, device=self.device)
+        kw = dict(device=self.device)
+        self.threshold = (threshold if threshold is not None
+                          else torch.full((N,), self.cfg.threshold, dtype=torch.float32, **kw))
+        self.bound = bound if bound is not None else torch.full((N,), self.cfg.bound, dtype=torch.int8, **kw)
+        self.min_lower = (min_lower if min_lower is not None
+                          else torch.full((N,), self.cfg.min_lower_bound, dtype=torch.float32, **kw))
+        self.app_id = app_id if app_id is not None else torch.zeros(N, dtype=torch.int32, **kw)
+        self.app_stats = torch.zeros((max(spec.n_apps, 1), 2), dtype=torch.int32, **kw)
+        self.algorithm = spec.algorithm
+        self.mode = ALGO_MODE.get(spec.algorithm)
+        self.pw_mode = pw_ref.PW_BY_NAME.get(spec.pairwise.upper(), pw_ref.PW_ALL)
+        g = sm_ref.make_grid(self.mode if self.mode is not None else sm_ref.MODE_HW,
+                             self.cfg.hw_alpha, self.cfg.hw_beta, self.cfg.hw_gamma)
+        self.grid = g.to(self.device)
+        C = P * W
+        self.horizons = torch.tensor(self.cur.horizons(), dtype=torch.int32, device=self.device)
+        if self.gpu:
+            self._h_pinned = torch.empty(C, dtype=torch.int32).pin_memory()
+        self.out: Dict[str, torch.Tensor] = {}
+        self.pw_out: Dict[str, torch.Tensor] = {}
+
+    # ------------------------------------------------------------------ data in
+    def load_history(self, values: torch.Tensor) -> None:
+        self.hist.load(values.to(self.device))
+
+    def set_baseline(self, values: torch.Tensor) -> None:
+        self.base.copy_(values.to(self.device, torch.float32))
+
+    def _refresh_horizons(self) -> None:
+        h = self.cur.horizons()
+        if self.gpu:
+            self._h_pinned.copy_(torch.from_numpy(h))
+            self.horizons.copy_(self._h_pinned, non_blocking=True)
+        else:
+            self.horizons.copy_(torch.from_numpy(h))
+
+    def ingest_tick(self, newv: torch.Tensor) -> None:
+        """``newv``: ``[N, P]`` float32 on the shard's device."""
+        graduate = self.cur.ticks >= self.cur.W
+        if self.gpu:
+            from ..ops import kernels as K
+            K.tick_ingest(self.hist.data, self.hist.next_col(), self.cur.data, self.cur.P, self.cur.W,
+                          self.cur.slot(), newv, graduate=graduate)
+            self.cur.ticks += 1
+        else:
+            old = self.cur.push_(newv)
+            if graduate:
+                self.hist.data[:, self.hist.next_col()] = old.to(self.hist.data.dtype)
+        if graduate:
+            self.hist.advance(1)
+        self._refresh_horizons()
+
+    # ------------------------------------------------------------------ scoring
+    def score(self) -> Dict[str, torch.Tensor]:
+        self.app_stats.zero_()
+        if self.gpu:
+            return self._score_gpu()
+        return self._score_cpu()
+
+    def _score_gpu(self) -> Dict[str, torch.Tensor]:
+        from ..ops import kernels as K
+        cfg = self.cfg
+        differs = None
+        if self.pw_mode != pw_ref.PW_NONE:
+            self.pw_out = K.rank_tests(self.base, self.cur.data, self.pw_mode, cfg.pairwise_threshold,
+                                       cfg.min_mann_white, cfg.min_wilcoxon, cfg.min_kruskal,
+                                       want_pvals=True, out=self.pw_out)
+            differs = self.pw_out["differs"]
+        spec = K.DetectSpec(horizons=self.horizons, threshold=self.threshold, bound=self.bound,
+                            min_lower=self.min_lower, cur=self.cur.data, differs=differs,
+                            pw_scale=cfg.pairwise_scale, min_valid=cfg.min_historical_points,
+                            want_band=self.spec.want_band, app_id=self.app_id, app_stats=self.app_stats)
+        h = self.hist
+        if self.mode is not None:
+            self.out = K.smoothing_fit(h.data, h.head, h.length, self.mode, self.spec.season, self.grid,
+                                       spec, out=self.out)
+        elif self.algorithm in ("moving_average_all", "moving_average"):
+            length = h.length
+            head = h.head
+            if self.algorithm == "moving_average" and cfg.ma_window < length:
+                head = (h.head + length - cfg.ma_window) % h.R
+                length = cfg.ma_window
+            self.out = K.window_stats(h.data, head, length, spec, out=self.out)
+        else:
+            raise ValueError(f"algorithm {self.algorithm!r} is not a streaming univariate scorer")
+        return self.out
+
+    def _score_cpu(self) -> Dict[str, torch.Tensor]:
+        cfg = self.cfg
+        y = self.hist.logical().float()
+        differs = None
+        if self.pw_mode != pw_ref.PW_NONE:
+            res = pw_ref.rank_tests(self.base, self.cur.data)
+            differs = pw_ref.pairwise_differs(res, self.pw_mode, cfg.pairwise_threshold, cfg.min_mann_white,
+                                              cfg.min_wilcoxon, cfg.min_kruskal)
+            self.pw_out = {"differs": differs.to(torch.uint8),
+                           "pvals": torch.stack([res.p_mw, res.p_wilcoxon, res.p_kruskal], 1).float()}
+        h = self.horizons.long()
+        valid_hist = (~torch.isnan(y)).sum(1)
+        if self.mode is not None:
+            fit = sm_ref.fit_smoothing(y, self.mode, self.grid.cpu(), m=self.spec.season)
+            f = sm_ref.forecast(fit, h)
+            sigma = fit.sigma
+            n_valid = fit.n_valid
+            extra = {"level": fit.level, "trend": fit.trend, "sigma": sigma, "best": fit.best.int()}
+        else:
+            win = cfg.ma_window if self.algorithm == "moving_average" else None
+            st = ma_ref.window_stats(y, win)
+            f = st.mean[:, None].expand(-1, h.shape[0])
+            sigma = st.std
+            n_valid = st.count
+            extra = {"mean": st.mean, "std": st.std}
+        ok = n_valid >= cfg.min_historical_points
+        d = det_ref.detect(f, sigma, self.cur.data, self.threshold, self.bound, self.min_lower,
+                           differs=differs, pairwise_scale=cfg.pairwise_scale, model_ok=ok)
+        v = d.verdict.long()
+        self.app_stats.index_put_((self.app_id.long(), torch.zeros_like(v)), (v == 1).int(), accumulate=True)
+        self.app_stats.index_put_((self.app_id.long(), torch.ones_like(v)), (v >= 0).int(), accumulate=True)
+        del valid_hist
+        self.out = dict(extra, forecast=f, upper=d.upper, lower=d.lower, count=d.count,
+                        verdict=d.verdict, score=d.score)
+        return self.out
+
+
+def synthetic_history(N: int, T: int, season: int, device, seed: int = 0, dtype=torch.float32,
+                      chunk: int = 8192) -> torch.Tensor:
+    """Seasonal synthetic series (level, daily seasonality, slight trend, noise)
+    generated on ``device`` in chunks; returns ``[N, T]`` in ``dtype``."""
+    out = torch.empty((N, T), dtype=dtype, device=device)
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    t = torch.arange(T, device=device, dtype=torch.float32)
+    for s in range(0, N, chunk):
+        e = min(N, s + chunk)
+        n = e - s
+        lvl = torch.rand((n, 1), generator=g, device=device) * 95 + 5
+        amp = (torch.rand((n, 1), generator=g, device=device) * 0.25 + 0.05) * lvl
+        ph = torch.rand((n, 1), generator=g, device=device) * 6.283
+        tr = (torch.rand((n, 1), generator=g, device=device) - 0.5) * 1e-4 * lvl
+        noise = torch.randn((n, T), generator=g, device=device) * (0.03 * lvl)
+        y = lvl + tr * t + amp * torch.sin(2 * np.pi * t / season + ph) + noise
+        out[s:e] = y.to(dtype)
+    return out

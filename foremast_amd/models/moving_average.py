@@ -1,0 +1,49 @@
+"""Moving-average band (``ML_ALGORITHM=moving_average_all`` / ``moving_average``).
+
+Reference semantics for the ``window_stats`` kernel (K1).  The brain's
+default model (``deploy/foremast/3_brain/foremast-brain.yaml:24-25``):
+centre = mean of the historical window, spread = population standard
+deviation; the band is ``mean ± threshold·std`` (the threshold/bound are
+applied by :mod:`foremast_amd.models.detect`).
+
+* ``moving_average_all`` — statistics over the whole history;
+* ``moving_average``     — statistics over the last ``window`` positions.
+
+NaNs are ignored.  Accumulation is fp32 with a per-series shift (the first
+valid value) to avoid catastrophic cancellation in ``E[x²] − E[x]²``.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+
+@dataclass
+class WindowStats:
+    mean: torch.Tensor   # [N]
+    std: torch.Tensor    # [N]
+    count: torch.Tensor  # [N]
+
+
+def window_stats(y: torch.Tensor, window: Optional[int] = None) -> WindowStats:
+    y = y.float()
+    if window is not None and window < y.shape[1]:
+        y = y[:, -window:]
+    valid = ~torch.isnan(y)
+    cnt = valid.sum(1).float()
+    # shift by the first valid value
+    first = torch.where(valid.any(1), valid.float().argmax(1), torch.zeros_like(cnt, dtype=torch.long))
+    shift = y.gather(1, first[:, None]).squeeze(1)
+    shift = torch.where(torch.isnan(shift), torch.zeros_like(shift), shift)
+    d = torch.where(valid, y - shift[:, None], torch.zeros_like(y))
+    s1 = d.sum(1)
+    s2 = (d * d).sum(1)
+    n = cnt.clamp(min=1)
+    mean_d = s1 / n
+    var = (s2 / n - mean_d * mean_d).clamp(min=0)
+    mean = torch.where(cnt > 0, mean_d + shift, torch.full_like(cnt, float("nan")))
+    std = torch.where(cnt > 0, torch.sqrt(var), torch.full_like(cnt, float("nan")))
+    return WindowStats(mean=mean, std=std, count=cnt)

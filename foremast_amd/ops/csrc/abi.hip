@@ -1,0 +1,23 @@
+// ABI introspection for the ctypes binding (sizeof / offsetof of the arg structs).
+#include <hip/hip_runtime.h>
+#include "args.h"
+
+#define FM_OFF(S, f) if (!__builtin_strcmp(field, #f)) return (long long)offsetof(S, f)
+
+extern "C" long long fm_abi_sizeof(const char* name) {
+  if (!__builtin_strcmp(name, "DetectArgs")) return sizeof(DetectArgs);
+  if (!__builtin_strcmp(name, "SmoothArgs")) return sizeof(SmoothArgs);
+  if (!__builtin_strcmp(name, "RankArgs")) return sizeof(RankArgs);
+  if (!__builtin_strcmp(name, "WindowArgs")) return sizeof(WindowArgs);
+  if (!__builtin_strcmp(name, "BivArgs")) return sizeof(BivArgs);
+  return -1;
+}
+
+extern "C" long long fm_abi_offsetof(const char* name, const char* field) {
+  if (!__builtin_strcmp(name, "SmoothArgs")) { FM_OFF(SmoothArgs, det); FM_OFF(SmoothArgs, season_out); FM_OFF(SmoothArgs, grid); }
+  if (!__builtin_strcmp(name, "DetectArgs")) { FM_OFF(DetectArgs, pw_scale); FM_OFF(DetectArgs, app_stats); FM_OFF(DetectArgs, ld_cur); }
+  if (!__builtin_strcmp(name, "RankArgs")) { FM_OFF(RankArgs, pvals); FM_OFF(RankArgs, alpha); }
+  if (!__builtin_strcmp(name, "WindowArgs")) { FM_OFF(WindowArgs, det); }
+  if (!__builtin_strcmp(name, "BivArgs")) { FM_OFF(BivArgs, eps); FM_OFF(BivArgs, app_stats); }
+  return -1;
+}

@@ -1,0 +1,106 @@
+// Kernel argument structs (C ABI shared with foremast_amd/ops/_native.py).
+//
+// Field order/types here and the ctypes Structures in _native.py must agree;
+// tests/test_ops_abi.py checks sizeof/offsetof through fm_abi_* exports.
+#pragma once
+#include <stddef.h>
+
+struct DetectArgs {
+  const int* horizons;          // [C]
+  int C;
+  int min_valid;
+  const float* cur;             // [N, ld_cur] (NaN = missing) or null
+  long long ld_cur;
+  const float* threshold;       // [N]
+  const signed char* bound;     // [N]
+  const float* min_lower;       // [N]
+  const unsigned char* differs; // [N] or null
+  float pw_scale;
+  int _pad0;
+  float* forecast;              // [N, C] or null
+  float* upper;                 // [N, C] or null
+  float* lower;                 // [N, C] or null
+  int* count;                   // [N]
+  signed char* verdict;         // [N]
+  float* score;                 // [N]
+  const int* app_id;            // [N] or null
+  int* app_stats;               // [A, 2] (anomalous, scored) or null
+};
+
+struct SmoothArgs {
+  const void* hist;     // [N, ld] ring buffer (float or bf16)
+  long long ld;         // row stride (elements)
+  int ring_len;         // R (physical columns)
+  int head;             // physical column of logical t = 0
+  int T;                // logical window length
+  int Tp;               // padded length (multiple of seg)
+  int pad;              // front padding (Tp - T)
+  int m;                // season (HW) or 1
+  int K;                // steps per lane per segment
+  int seg;              // segment length (HW: m; ES/DES: 64*K)
+  const float* grid;    // [G, 3] (alpha, beta, gamma)
+  int G;
+  int N;
+  float* level;         // [N]
+  float* trend;         // [N]
+  float* sigma;         // [N]
+  int* best;            // [N]
+  float* season_out;    // [N, m] or null
+  DetectArgs det;
+};
+
+struct RankArgs {
+  const float* base;
+  long long ld_base;
+  const float* cur;
+  long long ld_cur;
+  int nb;
+  int nc;
+  int N;
+  int mode;       // 0 none, 1 ALL, 2 ANY, 3 MW, 4 WILCOXON, 5 KRUSKAL
+  float alpha;
+  int min_mw;
+  int min_wilcoxon;
+  int min_kruskal;
+  float* pvals;            // [N, 3] (mw, wilcoxon, kruskal) or null
+  unsigned char* differs;  // [N]
+  float* counts;           // [N, 3] (n_base, n_cur, n_pairs) or null
+};
+
+struct WindowArgs {
+  const void* hist;
+  long long ld;
+  int ring_len;
+  int head;      // physical column of the first sample of the window
+  int len;       // window length (logical samples)
+  int N;
+  float* mean;   // [N]
+  float* stdv;   // [N]
+  float* count;  // [N]
+  DetectArgs det;
+};
+
+struct BivArgs {
+  const void* hx;       // [N, ld] metric 0 ring
+  const void* hy;       // [N, ld] metric 1 ring
+  long long ld;
+  int ring_len;
+  int head;
+  int len;
+  int N;
+  const float* cur;     // [N, C, 2]
+  int C;
+  int min_valid;
+  const float* threshold;       // [N]
+  const unsigned char* differs; // [N] or null
+  float pw_scale;
+  float eps;
+  float* mean;          // [N, 2]
+  float* cov;           // [N, 3]
+  float* d2;            // [N, C] or null
+  int* count;           // [N]
+  signed char* verdict; // [N]
+  float* score;         // [N] max d
+  const int* app_id;
+  int* app_stats;
+};

@@ -1,0 +1,45 @@
+// K10 tick ingest: one launch per scoring tick for a shard of series.
+//
+// Streaming layout (foremast_amd/ingest/ringbuffer.py):
+//   hist [N, R]      7-day history ring (bf16 or f32), one point per minute;
+//   cur  [N, P*W]    current window, P pods x W slots (slot = tick mod W);
+//   newv [N, P]      this tick's per-pod values (from the host ingest, H2D).
+// Per series: the slot being overwritten holds the oldest current points
+// (age W); their pod-mean graduates into history at column hist_col, then
+// the new per-pod values take the slot.  One thread per series; everything
+// the tick needs is touched once.
+#include "common.h"
+
+template <typename TH>
+__global__ __launch_bounds__(256) void tick_ingest_kernel(TH* __restrict__ hist, long long ld_h, int hist_col,
+                                                          float* __restrict__ cur, long long ld_c, int P, int W,
+                                                          int slot, const float* __restrict__ newv,
+                                                          long long ld_n, int N, int graduate) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f, c = 0.f;
+  float* row = cur + (long long)n * ld_c;
+  const float* nv = newv + (long long)n * ld_n;
+  for (int p = 0; p < P; ++p) {
+    const int col = p * W + slot;
+    const float old = row[col];
+    if (old == old) { s += old; c += 1.f; }
+    row[col] = nv[p];
+  }
+  if (graduate) hist[(long long)n * ld_h + hist_col] = from_f32<TH>(c > 0.f ? s / c : fm_nan());
+}
+
+extern "C" int fm_tick_ingest(void* hist, long long ld_h, int hist_col, float* cur, long long ld_c, int P,
+                              int W, int slot, const float* newv, long long ld_n, int N, int graduate,
+                              int bf16, hipStream_t st) {
+  if (N <= 0) return 0;
+  if (P <= 0 || W <= 0 || slot < 0 || slot >= W || hist_col < 0) return (int)hipErrorInvalidValue;
+  dim3 grid((N + 255) / 256), block(256);
+  if (bf16)
+    hipLaunchKernelGGL(tick_ingest_kernel<bf16_t>, grid, block, 0, st, (bf16_t*)hist, ld_h, hist_col, cur,
+                       ld_c, P, W, slot, newv, ld_n, N, graduate);
+  else
+    hipLaunchKernelGGL(tick_ingest_kernel<float>, grid, block, 0, st, (float*)hist, ld_h, hist_col, cur, ld_c,
+                       P, W, slot, newv, ld_n, N, graduate);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,167 @@
+// K5 + K11: batched Mann-Whitney U / Wilcoxon signed-rank / Kruskal-Wallis
+// and the pairwise "do baseline and current differ" decision.
+//
+// Semantics: foremast_amd/models/pairwise.py (scipy asymptotic forms).
+// One 64-lane wave per series; four series per 256-thread workgroup.  The
+// pooled sample (n <= 1024) is staged in the wave's LDS slice and ranked by
+// exact pairwise counting: rank_i = #(x_j < x_i) + (#(x_j == x_i) + 1) / 2,
+// which gives average ranks under ties and the tie term sum(t^3 - t) =
+// sum_i (eq_i^2 - 1) in the same sweep.  All lanes read the same x_j per
+// iteration (an LDS broadcast), so the sweep is conflict-free.  For canary
+// windows (n ~ 20-200) this beats a sort: no data-dependent control flow.
+#include "common.h"
+#include "args.h"
+
+
+
+extern __shared__ __attribute__((aligned(16))) char fm_rank_smem[];
+
+// Rank the valid entries of x[0..n) (NaN = invalid); returns per-lane partial
+// sums: sum of ranks for entries with group flag set, and the tie term.
+template <typename GroupFn>
+__device__ __forceinline__ void rank_sweep(const float* x, int n, GroupFn in_group,
+                                           float& rsum_g, float& tie, float& rsum_o) {
+  const int lane = lane_id();
+  rsum_g = 0.f; rsum_o = 0.f; tie = 0.f;
+  for (int i = lane; i < n; i += FM_WAVE) {
+    const float xi = x[i];
+    if (xi != xi) continue;
+    float less = 0.f, eq = 0.f;
+    int j = 0;
+    for (; j + 4 <= n; j += 4) {
+      const v4f q = *(const v4f*)(x + j);
+      less += (q.x < xi) ? 1.f : 0.f; eq += (q.x == xi) ? 1.f : 0.f;
+      less += (q.y < xi) ? 1.f : 0.f; eq += (q.y == xi) ? 1.f : 0.f;
+      less += (q.z < xi) ? 1.f : 0.f; eq += (q.z == xi) ? 1.f : 0.f;
+      less += (q.w < xi) ? 1.f : 0.f; eq += (q.w == xi) ? 1.f : 0.f;
+    }
+    for (; j < n; ++j) {
+      const float q = x[j];
+      less += (q < xi) ? 1.f : 0.f;
+      eq += (q == xi) ? 1.f : 0.f;
+    }
+    const float r = less + (eq + 1.f) * 0.5f;
+    if (in_group(i)) rsum_g += r; else rsum_o += r;
+    tie += eq * eq - 1.f;
+  }
+  rsum_g = wave_sum(rsum_g);
+  rsum_o = wave_sum(rsum_o);
+  tie = wave_sum(tie);
+}
+
+__global__ __launch_bounds__(256) void rank_tests_kernel(const RankArgs a) {
+  const int w = wave_id(), lane = lane_id();
+  const int n = blockIdx.x * (blockDim.x / FM_WAVE) + w;
+  const int npool = a.nb + a.nc;
+  const int npool4 = (npool + 3) & ~3;
+  const int k = a.nb < a.nc ? a.nb : a.nc;
+  const int k4 = (k + 3) & ~3;
+  float* x = (float*)fm_rank_smem + (size_t)w * (npool4 + k4);
+  float* dabs = x + npool4;
+  if (n >= a.N) return;  // wave-uniform; no block barrier below
+
+  // stage pooled sample (NaN pads the vector tail) and |d| of aligned pairs
+  const float* b = a.base + (long long)n * a.ld_base;
+  const float* c = a.cur + (long long)n * a.ld_cur;
+  float cnt_b = 0.f, cnt_c = 0.f;
+  for (int i = lane; i < npool4; i += FM_WAVE) {
+    float v = fm_nan();
+    if (i < a.nb) v = b[i];
+    else if (i < npool) v = c[i - a.nb];
+    x[i] = v;
+    if (v == v) { if (i < a.nb) cnt_b += 1.f; else cnt_c += 1.f; }
+  }
+  float npairs = 0.f;
+  for (int i = lane; i < k4; i += FM_WAVE) {
+    float v = fm_nan();
+    if (i < k) {
+      const float d = c[i] - b[i];
+      if (d == d && d != 0.f) { v = fabsf(d); npairs += 1.f; }
+    }
+    dabs[i] = v;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  const float n1 = wave_sum(cnt_b), n2 = wave_sum(cnt_c), np = wave_sum(npairs);
+  const float nn = n1 + n2;
+
+  // --- MW / Kruskal share the pooled ranks
+  float R1, tie, R2;
+  const int nbv = a.nb;
+  rank_sweep(x, npool4, [nbv](int i) { return i < nbv; }, R1, tie, R2);
+
+  // --- Wilcoxon: ranks of |d| over nonzero pairs, group = positive d
+  float Tp, wtie, Tm;
+  rank_sweep(dabs, k4, [c, b](int i) { return (c[i] - b[i]) > 0.f; }, Tp, wtie, Tm);
+
+  if (lane != 0) return;
+  // Mann-Whitney U (two-sided, continuity, tie-corrected)
+  float p_mw = 1.f;
+  if (n1 > 0.f && n2 > 0.f) {
+    const float U1 = R1 - n1 * (n1 + 1.f) * 0.5f;
+    const float U = fmaxf(U1, n1 * n2 - U1);
+    const float mu = n1 * n2 * 0.5f;
+    const float var = n1 * n2 / 12.f * ((nn + 1.f) - tie / fmaxf(nn * (nn - 1.f), 1.f));
+    const float sd = sqrtf(fmaxf(var, 0.f));
+    if (sd > 0.f) p_mw = fminf(2.f * norm_sf((U - mu - 0.5f) / sd), 1.f);
+  }
+  // Kruskal-Wallis, 2 groups → chi^2(1)
+  float p_kw = 1.f;
+  if (n1 > 0.f && n2 > 0.f) {
+    const float H = 12.f / fmaxf(nn * (nn + 1.f), 1.f) * (R1 * R1 / n1 + R2 * R2 / n2) - 3.f * (nn + 1.f);
+    const float corr = 1.f - tie / fmaxf(nn * nn * nn - nn, 1.f);
+    if (corr > 0.f) p_kw = fminf(erfcf(sqrtf(fmaxf(H / corr, 0.f) * 0.5f)), 1.f);
+  }
+  // Wilcoxon signed-rank (approx, no continuity correction)
+  float p_w = 1.f;
+  if (np > 0.f) {
+    const float T = fminf(Tp, Tm);
+    const float mu = np * (np + 1.f) * 0.25f;
+    const float var = np * (np + 1.f) * (2.f * np + 1.f) / 24.f - wtie / 48.f;
+    const float sd = sqrtf(fmaxf(var, 0.f));
+    if (sd > 0.f) p_w = fminf(2.f * norm_sf(fabsf((T - mu) / sd)), 1.f);
+  }
+  const float nsmall = fminf(n1, n2);
+  const bool ran_mw = nsmall >= (float)a.min_mw;
+  const bool ran_w = np >= (float)a.min_wilcoxon;
+  const bool ran_k = nsmall >= (float)a.min_kruskal;
+  const bool rej_mw = ran_mw && p_mw < a.alpha;
+  const bool rej_w = ran_w && p_w < a.alpha;
+  const bool rej_k = ran_k && p_kw < a.alpha;
+  bool d = false;
+  switch (a.mode) {
+    case 1: d = (ran_mw || ran_w || ran_k) && (!ran_mw || rej_mw) && (!ran_w || rej_w) && (!ran_k || rej_k); break;
+    case 2: d = rej_mw || rej_w || rej_k; break;
+    case 3: d = rej_mw; break;
+    case 4: d = rej_w; break;
+    case 5: d = rej_k; break;
+    default: d = false;
+  }
+  a.differs[n] = d ? 1 : 0;
+  if (a.pvals) {
+    a.pvals[3 * (long long)n + 0] = p_mw;
+    a.pvals[3 * (long long)n + 1] = p_w;
+    a.pvals[3 * (long long)n + 2] = p_kw;
+  }
+  if (a.counts) {
+    a.counts[3 * (long long)n + 0] = n1;
+    a.counts[3 * (long long)n + 1] = n2;
+    a.counts[3 * (long long)n + 2] = np;
+  }
+}
+
+extern "C" size_t fm_rank_lds_bytes(int nb, int nc) {
+  const int npool4 = (nb + nc + 3) & ~3;
+  const int k = nb < nc ? nb : nc;
+  const int k4 = (k + 3) & ~3;
+  return (size_t)4 * (npool4 + k4) * 4;
+}
+
+extern "C" int fm_rank_tests(const RankArgs* a, hipStream_t st) {
+  if (a->N <= 0) return 0;
+  const size_t lds = fm_rank_lds_bytes(a->nb, a->nc);
+  if (lds > 64 * 1024 || a->nb <= 0 || a->nc <= 0) return (int)hipErrorInvalidValue;
+  dim3 grid((a->N + 3) / 4), block(256);
+  hipLaunchKernelGGL(rank_tests_kernel, grid, block, lds, st, *a);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,338 @@
+// K2/K3 (+ fused K9 epilogue): exponential smoothing / Holt (double ES) /
+// additive Holt-Winters — batched grid fit, forecast, band and verdict.
+//
+// Semantics: foremast_amd/models/smoothing.py (+ models/detect.py for the
+// epilogue).  The brain fits one model per series serially on a 100m CPU;
+// here one 256-thread workgroup owns one series and fits the whole
+// alpha x beta x gamma grid:
+//
+//  * the series (<= 64 KB) is staged once into LDS (ring-buffer rotation and
+//    front padding are resolved while loading);
+//  * the level/trend recurrence is an affine map x_t = A_t x_{t-1} + c_t u_t,
+//    so a 64-lane wave walks one *segment* (one season for HW) in parallel:
+//    lane j owns K consecutive steps/phases, composes its local affine map,
+//    a Kogge-Stone scan over the 64 lanes composes the prefixes
+//    (time-axis parallel scan), then each lane replays its
+//    steps from its true start state, accumulating SSE and updating the
+//    seasonal state it owns in registers (phase j*K+i is always lane j);
+//  * each lane carries TWO grid points (float2 → v_pk_* packed FP32);
+//  * NaN-free segments use the precomputed local power A^len (pass 1 only
+//    propagates the vector part); segments with gaps take the general path;
+//  * the best combo's state is kept per wave, arg-min across waves, and the
+//    epilogue forecasts the current window, builds the band and the verdict
+//    without another launch.
+#include "common.h"
+#include "detect.h"
+#include "args.h"
+
+
+
+enum { MODE_ES = 0, MODE_DES = 1, MODE_HW = 2 };
+
+extern __shared__ __attribute__((aligned(16))) char fm_smem[];
+
+template <int KMAX, int MODE, typename TIN>
+__global__ __launch_bounds__(256) void smooth_fit_kernel(const SmoothArgs a) {
+  const int n = blockIdx.x;
+  const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+  const int nwaves = blockDim.x / FM_WAVE;
+
+  // ---- LDS carve: ys[Tp] | sfinal[m] | segnan[nseg] | red[64] | best[8] ----------
+  size_t off = ((size_t)a.Tp * sizeof(TIN) + 15) & ~(size_t)15;
+  TIN* ys = (TIN*)fm_smem;
+  float* sfinal = (float*)(fm_smem + off);
+  off += ((size_t)a.m * 4 + 15) & ~(size_t)15;
+  const int nseg = a.Tp / a.seg;
+  int* segnan = (int*)(fm_smem + off);
+  off += ((size_t)nseg * 4 + 15) & ~(size_t)15;
+  float* red = (float*)(fm_smem + off);
+  off += 64 * 4;
+  float* wbest = (float*)(fm_smem + off);  // [nwaves][4]: sse, idx, l, b
+
+  for (int i = tid; i < nseg; i += blockDim.x) segnan[i] = 0;
+  __syncthreads();
+
+  // ---- stage the logical window into LDS ---------------------------------------------
+  const TIN* row = (const TIN*)a.hist + (long long)n * a.ld;
+  const int t0 = (MODE == MODE_HW) ? a.m : 0;
+  float nv_local = 0.f;
+  for (int i = tid; i < a.Tp; i += blockDim.x) {
+    const int t = i - a.pad;
+    float v;
+    if (t < 0) {
+      v = fm_nan();
+    } else {
+      int c = a.head + t;
+      if (c >= a.ring_len) c -= a.ring_len;
+      v = to_f32<TIN>(row[c]);
+    }
+    ys[i] = from_f32<TIN>(v);
+    const bool isn = (v != v);
+    if (isn) atomicOr(&segnan[i / a.seg], 1);
+    if (!isn && i >= t0) nv_local += 1.f;
+  }
+  const float n_valid = blk_sum(nv_local, red);  // includes __syncthreads
+
+  // ---- initial state ---------------------------------------------------------------
+  float l0 = 0.f, b0 = 0.f;
+  if (MODE == MODE_HW) {
+    float s0 = 0.f, c0 = 0.f, s1 = 0.f, c1 = 0.f;
+    for (int i = tid; i < a.m; i += blockDim.x) {
+      float y0 = to_f32<TIN>(ys[i]);
+      float y1 = to_f32<TIN>(ys[a.m + i]);
+      if (y0 == y0) { s0 += y0; c0 += 1.f; }
+      if (y1 == y1) { s1 += y1; c1 += 1.f; }
+    }
+    s0 = blk_sum(s0, red);
+    c0 = blk_sum(c0, red);
+    s1 = blk_sum(s1, red);
+    c1 = blk_sum(c1, red);
+    l0 = c0 > 0.f ? s0 / c0 : 0.f;
+    const float l1 = c1 > 0.f ? s1 / c1 : 0.f;
+    b0 = (l1 - l0) / (float)a.m;
+  } else {
+    // first valid value (wave-uniform ballot scan, every wave redundantly)
+    int first = -1;
+    for (int base = 0; base < a.Tp && first < 0; base += FM_WAVE) {
+      const int i = base + lane;
+      const float y = i < a.Tp ? to_f32<TIN>(ys[i]) : fm_nan();
+      const unsigned long long mask = __ballot(y == y);
+      if (mask) first = base + __ffsll((long long)mask) - 1;
+    }
+    l0 = first >= 0 ? to_f32<TIN>(ys[first]) : 0.f;
+    b0 = 0.f;
+  }
+
+  // ---- per-lane geometry -------------------------------------------------------------
+  const int myStart = lane * a.K;
+  int myLen = a.seg - myStart;
+  myLen = myLen < 0 ? 0 : (myLen > a.K ? a.K : myLen);
+
+  float s0r[KMAX];
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    float v = 0.f;
+    if (MODE == MODE_HW && i < myLen) {
+      const float y = to_f32<TIN>(ys[myStart + i]);
+      v = (y == y) ? y - l0 : 0.f;
+    }
+    s0r[i] = v;
+  }
+
+  float bestSSE = __builtin_huge_valf();
+  int bestIdx = 0x7fffffff;
+  float bestL = l0, bestB = b0;
+  float bests[KMAX];
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) bests[i] = s0r[i];
+
+  const int npairs = (a.G + 1) / 2;
+  const int seg0 = (MODE == MODE_HW) ? 1 : 0;
+
+  for (int pi = w; pi < npairs; pi += nwaves) {
+    const int c0 = 2 * pi;
+    const int c1 = (2 * pi + 1 < a.G) ? 2 * pi + 1 : c0;
+    v2f al, be, ga;
+    al.x = a.grid[3 * c0 + 0]; al.y = a.grid[3 * c1 + 0];
+    be.x = a.grid[3 * c0 + 1]; be.y = a.grid[3 * c1 + 1];
+    ga.x = a.grid[3 * c0 + 2]; ga.y = a.grid[3 * c1 + 2];
+    const v2f one = splat2(1.f), zero = splat2(0.f);
+    const v2f ab = al * be;
+    const v2f oma = one - al;
+    const v2f omab = one - ab;
+    const v2f g1a = ga * oma;
+
+    // local power A^myLen for NaN-free segments: A = [[1-a, 1-a], [-ab, 1-ab]]
+    v2f P11 = one, P12 = zero, P21 = zero, P22 = one;
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) {
+      if (i < myLen) {
+        const v2f n11 = oma * (P11 + P21), n12 = oma * (P12 + P22);
+        const v2f n21 = omab * P21 - ab * P11, n22 = omab * P22 - ab * P12;
+        P11 = n11; P12 = n12; P21 = n21; P22 = n22;
+      }
+    }
+
+    v2f s[KMAX];
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) s[i] = splat2(s0r[i]);
+    v2f L = splat2(l0), B = splat2(b0), sse = zero;
+
+    for (int sg = seg0; sg < nseg; ++sg) {
+      const int base = sg * a.seg + myStart;
+      float yr[KMAX];
+#pragma unroll
+      for (int i = 0; i < KMAX; ++i) yr[i] = (i < myLen) ? to_f32<TIN>(ys[base + i]) : 0.f;
+
+      // -- pass 1: local affine map (M, v) of my steps, from the zero state
+      v2f M11, M12, M21, M22, v1 = zero, v2 = zero;
+      if (!segnan[sg]) {
+        M11 = P11; M12 = P12; M21 = P21; M22 = P22;
+#pragma unroll
+        for (int i = 0; i < KMAX; ++i) {
+          if (i < myLen) {
+            const v2f e = (splat2(yr[i]) - s[i]) - v1 - v2;
+            v1 = v1 + v2 + al * e;
+            v2 = v2 + ab * e;
+          }
+        }
+      } else {
+        M11 = one; M12 = zero; M21 = zero; M22 = one;
+#pragma unroll
+        for (int i = 0; i < KMAX; ++i) {
+          if (i < myLen) {
+            const float y = yr[i];
+            const bool ok = (y == y);
+            const v2f a11 = ok ? oma : one;
+            const v2f a21 = ok ? -ab : zero;
+            const v2f a22 = ok ? omab : one;
+            const v2f u = ok ? (splat2(y) - s[i]) : zero;
+            const v2f n11 = a11 * (M11 + M21), n12 = a11 * (M12 + M22);
+            const v2f n21 = a21 * M11 + a22 * M21, n22 = a21 * M12 + a22 * M22;
+            M11 = n11; M12 = n12; M21 = n21; M22 = n22;
+            const v2f nv1 = a11 * (v1 + v2) + (ok ? al * u : zero);
+            const v2f nv2 = a21 * v1 + a22 * v2 + (ok ? ab * u : zero);
+            v1 = nv1; v2 = nv2;
+          }
+        }
+      }
+
+      // -- inclusive Kogge-Stone scan of affine maps across the wave
+#pragma unroll
+      for (int d = 1; d < FM_WAVE; d <<= 1) {
+        const v2f q11 = shfl_up2(M11, d), q12 = shfl_up2(M12, d);
+        const v2f q21 = shfl_up2(M21, d), q22 = shfl_up2(M22, d);
+        const v2f qv1 = shfl_up2(v1, d), qv2 = shfl_up2(v2, d);
+        if (lane >= d) {
+          const v2f nv1 = M11 * qv1 + M12 * qv2 + v1;
+          const v2f nv2 = M21 * qv1 + M22 * qv2 + v2;
+          const v2f n11 = M11 * q11 + M12 * q21, n12 = M11 * q12 + M12 * q22;
+          const v2f n21 = M21 * q11 + M22 * q21, n22 = M21 * q12 + M22 * q22;
+          M11 = n11; M12 = n12; M21 = n21; M22 = n22; v1 = nv1; v2 = nv2;
+        }
+      }
+      // exclusive prefix → my start state
+      {
+        v2f e11 = shfl_up2(M11, 1), e12 = shfl_up2(M12, 1), e21 = shfl_up2(M21, 1),
+            e22 = shfl_up2(M22, 1), ev1 = shfl_up2(v1, 1), ev2 = shfl_up2(v2, 1);
+        if (lane == 0) { e11 = one; e12 = zero; e21 = zero; e22 = one; ev1 = zero; ev2 = zero; }
+        v1 = e11 * L + e12 * B + ev1;
+        v2 = e21 * L + e22 * B + ev2;
+      }
+      // -- pass 2: replay with the true start state
+#pragma unroll
+      for (int i = 0; i < KMAX; ++i) {
+        if (i < myLen) {
+          const float y = yr[i];
+          const bool ok = (y == y);
+          v2f e = (splat2(y) - s[i]) - v1 - v2;
+          e = ok ? e : zero;
+          v1 = v1 + v2 + al * e;
+          v2 = v2 + ab * e;
+          if (MODE == MODE_HW) s[i] = s[i] + g1a * e;
+          sse = sse + e * e;
+        }
+      }
+      L = shfl2(v1, FM_WAVE - 1);
+      B = shfl2(v2, FM_WAVE - 1);
+    }
+    sse = wave_sum2(sse);
+    if (sse.x < bestSSE || (sse.x == bestSSE && c0 < bestIdx)) {
+      bestSSE = sse.x; bestIdx = c0; bestL = L.x; bestB = B.x;
+#pragma unroll
+      for (int i = 0; i < KMAX; ++i) bests[i] = s[i].x;
+    }
+    if (c1 != c0 && (sse.y < bestSSE || (sse.y == bestSSE && c1 < bestIdx))) {
+      bestSSE = sse.y; bestIdx = c1; bestL = L.y; bestB = B.y;
+#pragma unroll
+      for (int i = 0; i < KMAX; ++i) bests[i] = s[i].y;
+    }
+  }
+
+  // ---- arg-min across waves ---------------------------------------------------------
+  if (lane == 0) {
+    wbest[4 * w + 0] = bestSSE;
+    wbest[4 * w + 1] = __int_as_float(bestIdx);
+    wbest[4 * w + 2] = bestL;
+    wbest[4 * w + 3] = bestB;
+  }
+  __syncthreads();
+  int win = 0;
+  for (int i = 1; i < nwaves; ++i) {
+    const float si = wbest[4 * i], sw = wbest[4 * win];
+    const int ii = __float_as_int(wbest[4 * i + 1]), iw = __float_as_int(wbest[4 * win + 1]);
+    if (si < sw || (si == sw && ii < iw)) win = i;
+  }
+  const float gSSE = wbest[4 * win];
+  const int gIdx = __float_as_int(wbest[4 * win + 1]);
+  const float gL = wbest[4 * win + 2], gB = wbest[4 * win + 3];
+  if (MODE == MODE_HW && w == win) {
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i)
+      if (i < myLen) sfinal[myStart + i] = bests[i];
+  }
+  __syncthreads();
+
+  const float sig = sqrtf(gSSE / fmaxf(n_valid, 1.f));
+  if (tid == 0) {
+    a.level[n] = gL;
+    a.trend[n] = gB;
+    a.sigma[n] = sig;
+    a.best[n] = gIdx;
+  }
+  if (MODE == MODE_HW && a.season_out) {
+    for (int p = tid; p < a.m; p += blockDim.x) a.season_out[(long long)n * a.m + p] = sfinal[p];
+  }
+
+  // ---- fused epilogue: forecast, band, anomalies, verdict ----------------------------
+  const int Tp = a.Tp, m = a.m;
+  detect_epilogue(a.det, n, sig, n_valid,
+                  [&](int h) {
+                    float f = gL + (float)h * gB;
+                    if (MODE == MODE_HW) {
+                      int ph = (Tp - 1 + h) % m;
+                      if (ph < 0) ph += m;
+                      f += sfinal[ph];
+                    }
+                    return f;
+                  },
+                  red);
+}
+
+template <int KMAX, int MODE>
+static hipError_t launch_t(const SmoothArgs& a, int bf16, size_t lds, hipStream_t st) {
+  dim3 grid(a.N), block(256);
+  if (bf16)
+    hipLaunchKernelGGL((smooth_fit_kernel<KMAX, MODE, bf16_t>), grid, block, lds, st, a);
+  else
+    hipLaunchKernelGGL((smooth_fit_kernel<KMAX, MODE, float>), grid, block, lds, st, a);
+  return hipGetLastError();
+}
+
+template <int MODE>
+static hipError_t launch_k(const SmoothArgs& a, int bf16, size_t lds, hipStream_t st) {
+  if (a.K <= 8) return launch_t<8, MODE>(a, bf16, lds, st);
+  if (a.K <= 16) return launch_t<16, MODE>(a, bf16, lds, st);
+  if (a.K <= 24) return launch_t<24, MODE>(a, bf16, lds, st);
+  return launch_t<32, MODE>(a, bf16, lds, st);
+}
+
+extern "C" size_t fm_smooth_lds_bytes(int Tp, int m, int seg, int bf16) {
+  size_t off = ((size_t)Tp * (bf16 ? 2 : 4) + 15) & ~(size_t)15;
+  off += ((size_t)m * 4 + 15) & ~(size_t)15;
+  off += ((size_t)(Tp / seg) * 4 + 15) & ~(size_t)15;
+  off += 64 * 4 + 16 * 4;
+  return off;
+}
+
+extern "C" int fm_smooth_fit(const SmoothArgs* a, int mode, int bf16, hipStream_t st) {
+  if (a->N <= 0) return 0;
+  if (a->K < 1 || a->K > 32 || a->seg > 64 * a->K || a->Tp % a->seg != 0) return (int)hipErrorInvalidValue;
+  const size_t lds = fm_smooth_lds_bytes(a->Tp, a->m, a->seg, bf16);
+  if (lds > 64 * 1024) return (int)hipErrorInvalidValue;
+  hipError_t e;
+  if (mode == MODE_ES) e = launch_k<MODE_ES>(*a, bf16, lds, st);
+  else if (mode == MODE_DES) e = launch_k<MODE_DES>(*a, bf16, lds, st);
+  else e = launch_k<MODE_HW>(*a, bf16, lds, st);
+  return (int)e;
+}

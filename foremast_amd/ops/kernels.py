@@ -1,0 +1,345 @@
+"""PyTorch-facing launchers for the gfx950 kernels.
+
+Every launcher validates shapes, dtypes, strides and devices on the host
+*before* launching (a bad shape must never reach a kernel), allocates any
+output not supplied in ``out`` and launches on the current HIP stream.  No
+host synchronisation happens here, so the launchers can be captured into a
+HIP graph.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import torch
+
+from . import _native as nat
+
+MODE_ES, MODE_DES, MODE_HW = 0, 1, 2
+DEFAULT_ES_K = 16  # steps per lane per segment for ES/DES (segment = 1024)
+LDS_LIMIT = 64 * 1024
+
+
+class KernelShapeError(ValueError):
+    pass
+
+
+def _need(cond: bool, msg: str) -> None:
+    if not cond:
+        raise KernelShapeError(msg)
+
+
+def _cuda(t: torch.Tensor, name: str) -> None:
+    _need(t.is_cuda, f"{name} must be a GPU tensor")
+
+
+def _vec(t: Optional[torch.Tensor], n: int, dtype, name: str, device) -> Optional[torch.Tensor]:
+    if t is None:
+        return None
+    _need(t.dim() == 1 and t.shape[0] == n, f"{name} must be [{n}], got {tuple(t.shape)}")
+    _need(t.dtype == dtype, f"{name} must be {dtype}, got {t.dtype}")
+    _need(t.is_contiguous(), f"{name} must be contiguous")
+    _need(t.device == device, f"{name} on {t.device}, expected {device}")
+    return t
+
+
+@dataclass
+class DetectSpec:
+    """Inputs of the fused detection epilogue (see models/detect.py)."""
+
+    horizons: torch.Tensor                 # int32 [C]
+    threshold: torch.Tensor                # float32 [N]
+    bound: torch.Tensor                    # int8 [N]
+    min_lower: torch.Tensor                # float32 [N]
+    cur: Optional[torch.Tensor] = None     # float32 [N, C] (row stride free)
+    differs: Optional[torch.Tensor] = None  # uint8 [N]
+    pw_scale: float = 0.5
+    min_valid: int = 0
+    want_band: bool = True
+    app_id: Optional[torch.Tensor] = None   # int32 [N]
+    app_stats: Optional[torch.Tensor] = None  # int32 [A, 2]
+
+
+def _fill_detect(d: nat.DetectArgs, spec: DetectSpec, N: int, device, out: Dict[str, torch.Tensor]) -> None:
+    C = int(spec.horizons.shape[0])
+    _need(spec.horizons.dtype == torch.int32 and spec.horizons.is_contiguous() and spec.horizons.dim() == 1,
+          "horizons must be contiguous int32 [C]")
+    _need(spec.horizons.device == device, "horizons on wrong device")
+    _vec(spec.threshold, N, torch.float32, "threshold", device)
+    _vec(spec.bound, N, torch.int8, "bound", device)
+    _vec(spec.min_lower, N, torch.float32, "min_lower", device)
+    _vec(spec.differs, N, torch.uint8, "differs", device)
+    if spec.cur is not None:
+        c = spec.cur
+        _need(c.dim() == 2 and c.shape[0] == N and c.shape[1] == C,
+              f"cur must be [{N}, {C}], got {tuple(c.shape)}")
+        _need(c.dtype == torch.float32 and c.stride(1) == 1, "cur must be float32 with unit inner stride")
+        _need(c.device == device, "cur on wrong device")
+    if spec.app_id is not None:
+        _vec(spec.app_id, N, torch.int32, "app_id", device)
+        _need(spec.app_stats is not None and spec.app_stats.dtype == torch.int32
+              and spec.app_stats.is_contiguous() and spec.app_stats.dim() == 2
+              and spec.app_stats.shape[1] == 2, "app_stats must be contiguous int32 [A, 2]")
+    kw = dict(dtype=torch.float32, device=device)
+    if spec.want_band and C > 0:
+        for k in ("forecast", "upper", "lower"):
+            if k not in out:
+                out[k] = torch.empty((N, C), **kw)
+    if "count" not in out:
+        out["count"] = torch.empty(N, dtype=torch.int32, device=device)
+    if "verdict" not in out:
+        out["verdict"] = torch.empty(N, dtype=torch.int8, device=device)
+    if "score" not in out:
+        out["score"] = torch.empty(N, **kw)
+    d.horizons = nat.ptr(spec.horizons)
+    d.C = C
+    d.min_valid = int(spec.min_valid)
+    d.cur = nat.ptr(spec.cur)
+    d.ld_cur = int(spec.cur.stride(0)) if spec.cur is not None else 0
+    d.threshold = nat.ptr(spec.threshold)
+    d.bound = nat.ptr(spec.bound)
+    d.min_lower = nat.ptr(spec.min_lower)
+    d.differs = nat.ptr(spec.differs)
+    d.pw_scale = float(spec.pw_scale)
+    d.forecast = nat.ptr(out.get("forecast"))
+    d.upper = nat.ptr(out.get("upper"))
+    d.lower = nat.ptr(out.get("lower"))
+    d.count = nat.ptr(out["count"])
+    d.verdict = nat.ptr(out["verdict"])
+    d.score = nat.ptr(out["score"])
+    d.app_id = nat.ptr(spec.app_id)
+    d.app_stats = nat.ptr(spec.app_stats)
+
+
+def _hist_check(hist: torch.Tensor, head: int, length: int) -> None:
+    _cuda(hist, "hist")
+    _need(hist.dim() == 2, "hist must be [N, R]")
+    _need(hist.dtype in (torch.float32, torch.bfloat16), "hist must be float32 or bfloat16")
+    _need(hist.stride(1) == 1, "hist rows must be contiguous")
+    R = hist.shape[1]
+    _need(0 <= head < R, f"head {head} out of [0, {R})")
+    _need(0 < length <= R, f"length {length} out of (0, {R}]")
+
+
+def smoothing_geometry(mode: int, T: int, m: int, K: Optional[int] = None):
+    """Return (Tp, pad, K, seg) for the smoothing kernel."""
+    if mode == MODE_HW:
+        _need(m >= 2, "season must be >= 2")
+        k = (m + 63) // 64
+        _need(k <= 32, f"season {m} too long for the register-resident kernel (max 2048)")
+        seg = m
+        Tp = ((T + m - 1) // m) * m
+        _need(Tp // m >= 2, f"holt_winters needs >= 2 seasons (T={T}, m={m})")
+    else:
+        k = K or DEFAULT_ES_K
+        _need(1 <= k <= 32, "K out of range")
+        seg = 64 * k
+        Tp = ((T + seg - 1) // seg) * seg
+    return Tp, Tp - T, k, seg
+
+
+def smoothing_supported(mode: int, T: int, m: int, bf16: bool) -> bool:
+    try:
+        Tp, _, k, seg = smoothing_geometry(mode, T, m)
+    except KernelShapeError:
+        return False
+    lib = nat.load()
+    if lib is None:
+        return False
+    return lib.fm_smooth_lds_bytes(Tp, m if mode == MODE_HW else 1, seg, int(bf16)) <= LDS_LIMIT
+
+
+def smoothing_fit(hist: torch.Tensor, head: int, length: int, mode: int, m: int,
+                  grid: torch.Tensor, det: DetectSpec, K: Optional[int] = None,
+                  want_season: bool = False, out: Optional[Dict[str, torch.Tensor]] = None
+                  ) -> Dict[str, torch.Tensor]:
+    lib = nat.require()
+    _hist_check(hist, head, length)
+    dev = hist.device
+    N = hist.shape[0]
+    _need(grid.dim() == 2 and grid.shape[1] == 3 and grid.dtype == torch.float32
+          and grid.is_contiguous() and grid.device == dev, "grid must be contiguous float32 [G, 3] on device")
+    G = grid.shape[0]
+    _need(G >= 1, "empty grid")
+    mm = m if mode == MODE_HW else 1
+    Tp, pad, k, seg = smoothing_geometry(mode, length, mm, K)
+    bf16 = hist.dtype == torch.bfloat16
+    lds = lib.fm_smooth_lds_bytes(Tp, mm, seg, int(bf16))
+    _need(lds <= LDS_LIMIT, f"series too long for LDS staging ({lds} bytes)")
+    out = {} if out is None else out
+    f32 = dict(dtype=torch.float32, device=dev)
+    for kname in ("level", "trend", "sigma"):
+        if kname not in out:
+            out[kname] = torch.empty(N, **f32)
+    if "best" not in out:
+        out["best"] = torch.empty(N, dtype=torch.int32, device=dev)
+    if want_season and mode == MODE_HW and "season" not in out:
+        out["season"] = torch.empty((N, mm), **f32)
+    a = nat.SmoothArgs()
+    a.hist = nat.ptr(hist)
+    a.ld = hist.stride(0)
+    a.ring_len = hist.shape[1]
+    a.head = int(head)
+    a.T = int(length)
+    a.Tp = Tp
+    a.pad = pad
+    a.m = mm
+    a.K = k
+    a.seg = seg
+    a.grid = nat.ptr(grid)
+    a.G = G
+    a.N = N
+    a.level = nat.ptr(out["level"])
+    a.trend = nat.ptr(out["trend"])
+    a.sigma = nat.ptr(out["sigma"])
+    a.best = nat.ptr(out["best"])
+    a.season_out = nat.ptr(out.get("season")) if (want_season and mode == MODE_HW) else 0
+    _fill_detect(a.det, det, N, dev, out)
+    nat.check(lib.fm_smooth_fit(a, int(mode), int(bf16), nat.stream_handle(dev)), "fm_smooth_fit")
+    return out
+
+
+def window_stats(hist: torch.Tensor, head: int, length: int, det: DetectSpec,
+                 out: Optional[Dict[str, torch.Tensor]] = None) -> Dict[str, torch.Tensor]:
+    lib = nat.require()
+    _hist_check(hist, head, length)
+    dev = hist.device
+    N = hist.shape[0]
+    bf16 = hist.dtype == torch.bfloat16
+    _need(hist.stride(0) % (8 if bf16 else 4) == 0 and hist.data_ptr() % 16 == 0,
+          "hist rows must be 16-byte aligned for vector loads")
+    out = {} if out is None else out
+    for k in ("mean", "std", "count_hist"):
+        if k not in out:
+            out[k] = torch.empty(N, dtype=torch.float32, device=dev)
+    a = nat.WindowArgs()
+    a.hist = nat.ptr(hist)
+    a.ld = hist.stride(0)
+    a.ring_len = hist.shape[1]
+    a.head = int(head)
+    a.len = int(length)
+    a.N = N
+    a.mean = nat.ptr(out["mean"])
+    a.stdv = nat.ptr(out["std"])
+    a.count = nat.ptr(out["count_hist"])
+    _fill_detect(a.det, det, N, dev, out)
+    nat.check(lib.fm_window_stats(a, int(bf16), nat.stream_handle(dev)), "fm_window_stats")
+    return out
+
+
+def rank_tests(base: torch.Tensor, cur: torch.Tensor, mode: int, alpha: float, min_mw: int = 20,
+               min_wilcoxon: int = 20, min_kruskal: int = 5, want_pvals: bool = True,
+               out: Optional[Dict[str, torch.Tensor]] = None) -> Dict[str, torch.Tensor]:
+    lib = nat.require()
+    _cuda(base, "base")
+    _need(base.dim() == 2 and cur.dim() == 2 and base.shape[0] == cur.shape[0],
+          "base/cur must be [N, nb] / [N, nc]")
+    _need(base.dtype == torch.float32 and cur.dtype == torch.float32, "base/cur must be float32")
+    _need(base.stride(1) == 1 and cur.stride(1) == 1, "base/cur rows must be contiguous")
+    _need(cur.device == base.device, "base/cur on different devices")
+    N, nb = base.shape
+    nc = cur.shape[1]
+    _need(nb >= 1 and nc >= 1, "empty windows")
+    _need(lib.fm_rank_lds_bytes(nb, nc) <= LDS_LIMIT, "windows too large for the rank kernel")
+    dev = base.device
+    out = {} if out is None else out
+    if "differs" not in out:
+        out["differs"] = torch.empty(N, dtype=torch.uint8, device=dev)
+    if want_pvals:
+        if "pvals" not in out:
+            out["pvals"] = torch.empty((N, 3), dtype=torch.float32, device=dev)
+        if "counts" not in out:
+            out["counts"] = torch.empty((N, 3), dtype=torch.float32, device=dev)
+    a = nat.RankArgs()
+    a.base = nat.ptr(base)
+    a.ld_base = base.stride(0)
+    a.cur = nat.ptr(cur)
+    a.ld_cur = cur.stride(0)
+    a.nb, a.nc, a.N, a.mode = nb, nc, N, int(mode)
+    a.alpha = float(alpha)
+    a.min_mw, a.min_wilcoxon, a.min_kruskal = int(min_mw), int(min_wilcoxon), int(min_kruskal)
+    a.pvals = nat.ptr(out.get("pvals")) if want_pvals else 0
+    a.counts = nat.ptr(out.get("counts")) if want_pvals else 0
+    a.differs = nat.ptr(out["differs"])
+    nat.check(lib.fm_rank_tests(a, nat.stream_handle(dev)), "fm_rank_tests")
+    return out
+
+
+def bivariate(hx: torch.Tensor, hy: torch.Tensor, head: int, length: int, cur: torch.Tensor,
+              threshold: torch.Tensor, differs: Optional[torch.Tensor] = None, pw_scale: float = 0.5,
+              min_valid: int = 0, eps: float = 1e-9, app_id=None, app_stats=None,
+              out: Optional[Dict[str, torch.Tensor]] = None) -> Dict[str, torch.Tensor]:
+    lib = nat.require()
+    _hist_check(hx, head, length)
+    _need(hy.shape == hx.shape and hy.dtype == hx.dtype and hy.stride() == hx.stride(),
+          "hx/hy must share geometry")
+    dev = hx.device
+    N = hx.shape[0]
+    _need(cur.dim() == 3 and cur.shape[0] == N and cur.shape[2] == 2 and cur.is_contiguous()
+          and cur.dtype == torch.float32, "cur must be contiguous float32 [N, C, 2]")
+    _vec(threshold, N, torch.float32, "threshold", dev)
+    _vec(differs, N, torch.uint8, "differs", dev)
+    C = cur.shape[1]
+    out = {} if out is None else out
+    f32 = dict(dtype=torch.float32, device=dev)
+    out.setdefault("mean", torch.empty((N, 2), **f32))
+    out.setdefault("cov", torch.empty((N, 3), **f32))
+    out.setdefault("d2", torch.empty((N, C), **f32))
+    out.setdefault("count", torch.empty(N, dtype=torch.int32, device=dev))
+    out.setdefault("verdict", torch.empty(N, dtype=torch.int8, device=dev))
+    out.setdefault("score", torch.empty(N, **f32))
+    a = nat.BivArgs()
+    a.hx, a.hy = nat.ptr(hx), nat.ptr(hy)
+    a.ld = hx.stride(0)
+    a.ring_len = hx.shape[1]
+    a.head, a.len, a.N = int(head), int(length), N
+    a.cur = nat.ptr(cur)
+    a.C = C
+    a.min_valid = int(min_valid)
+    a.threshold = nat.ptr(threshold)
+    a.differs = nat.ptr(differs)
+    a.pw_scale = float(pw_scale)
+    a.eps = float(eps)
+    for k in ("mean", "cov", "d2", "count", "verdict", "score"):
+        setattr(a, k, nat.ptr(out[k]))
+    a.app_id = nat.ptr(app_id)
+    a.app_stats = nat.ptr(app_stats)
+    nat.check(lib.fm_bivariate(a, int(hx.dtype == torch.bfloat16), nat.stream_handle(dev)), "fm_bivariate")
+    return out
+
+
+def ring_append(dst: torch.Tensor, col0: int, src: torch.Tensor) -> None:
+    """``dst[n, (col0 + j) % R] = src[n, j]`` (dst may be float32 or bf16)."""
+    lib = nat.require()
+    _cuda(dst, "dst")
+    _need(dst.dim() == 2 and src.dim() == 2 and dst.shape[0] == src.shape[0], "shape mismatch")
+    _need(dst.stride(1) == 1 and src.stride(1) == 1, "rows must be contiguous")
+    _need(src.dtype == torch.float32 and dst.dtype in (torch.float32, torch.bfloat16), "dtype mismatch")
+    _need(src.device == dst.device, "device mismatch")
+    R = dst.shape[1]
+    _need(src.shape[1] <= R, "append wider than the ring")
+    nat.check(lib.fm_ring_append(nat.ptr(dst), dst.stride(0), R, int(col0) % R, src.shape[1],
+                                 nat.ptr(src), src.stride(0), dst.shape[0],
+                                 int(dst.dtype == torch.bfloat16), nat.stream_handle(dst.device)),
+              "fm_ring_append")
+
+
+def tick_ingest(hist: torch.Tensor, hist_col: int, cur: torch.Tensor, P: int, W: int, slot: int,
+                newv: torch.Tensor, graduate: bool = True) -> None:
+    """Per-tick streaming ingest (see csrc/ingest.hip)."""
+    lib = nat.require()
+    _cuda(hist, "hist")
+    N = hist.shape[0]
+    _need(hist.dim() == 2 and hist.stride(1) == 1, "hist must be [N, R] row-contiguous")
+    _need(hist.dtype in (torch.float32, torch.bfloat16), "hist dtype")
+    _need(cur.dim() == 2 and cur.shape[0] == N and cur.shape[1] == P * W and cur.stride(1) == 1
+          and cur.dtype == torch.float32, f"cur must be float32 [N, {P * W}]")
+    _need(newv.dim() == 2 and newv.shape[0] == N and newv.shape[1] == P and newv.stride(1) == 1
+          and newv.dtype == torch.float32, f"newv must be float32 [N, {P}]")
+    _need(cur.device == hist.device and newv.device == hist.device, "device mismatch")
+    _need(0 <= slot < W and 0 <= hist_col < hist.shape[1], "slot/hist_col out of range")
+    nat.check(lib.fm_tick_ingest(nat.ptr(hist), hist.stride(0), int(hist_col), nat.ptr(cur), cur.stride(0),
+                                 int(P), int(W), int(slot), nat.ptr(newv), newv.stride(0), N, int(graduate),
+                                 int(hist.dtype == torch.bfloat16), nat.stream_handle(hist.device)),
+              "fm_tick_ingest")

@@ -1,0 +1,276 @@
+"""Job store with Elasticsearch-document semantics.
+
+The reference keeps every analysis job as a document in the ES index
+``documents`` (``foremast-service/pkg/search/elasticsearchstore.go``); the
+service creates it with ``status: "initial"`` and the brain moves it through
+the state diagram.  This module provides that table behind one interface:
+
+* :class:`MemoryJobStore` — in-process (tests, single-process deployments);
+* :class:`SqliteJobStore` — durable, shareable by several brain processes on
+  one host (checkpoint/resume: a restarted brain re-claims open jobs);
+* ``foremast_amd.store.es.ElasticJobStore`` — talks to a real ES 6.x so the
+  engine can replace the reference brain next to the reference service.
+
+Job ids are content addressed: HMAC-SHA256 with an empty key over the
+concatenated request fields (``foremast-service/pkg/common/stringutils.go:11-17``),
+so an identical request returns the same job (idempotent create).
+
+Claims are lease based: a worker may take a job whose status
+is open (``initial``/``reprogress``) or that has been in progress longer than
+``MAX_STUCK_IN_SECONDS`` (stuck-job takeover, ``foremast-brain.yaml:80-81``).
+"""
+
+from __future__ import annotations
+
+import abc
+import copy
+import hashlib
+import hmac
+import json
+import os
+import sqlite3
+import threading
+import time
+from typing import Any, Dict, Iterable, List, Optional
+
+from ..api import rest as r
+from ..utils.timeutil import format_rfc3339_nano, parse_rfc3339
+
+
+def job_id_for(req: r.DocumentRequest) -> str:
+    """``UUIDGen(ConvertDocumentRequestToString(doc))``."""
+    return hmac.new(b"", req.hash_input().encode("utf-8"), hashlib.sha256).hexdigest()
+
+
+def new_document(req: r.DocumentRequest, job_id: str, now: Optional[float] = None) -> Dict[str, Any]:
+    """Build the ES document (``elasticsearchstore.go:37-53``).
+
+    Raises :class:`~foremast_amd.utils.timeutil.TimeFormatError` on a bad
+    start/end time (the reference crashes the process — Q5).
+    """
+    now = time.time() if now is None else now
+    start = parse_rfc3339(req.start_time) if req.start_time else None
+    end = parse_rfc3339(req.end_time) if req.end_time else None
+    ts = format_rfc3339_nano(now)
+    return {
+        "id": job_id,
+        "appName": req.app_name,
+        "created_at": ts,
+        "startTime": format_rfc3339_nano(start.timestamp()) if start else "0001-01-01T00:00:00Z",
+        "endTime": format_rfc3339_nano(end.timestamp()) if end else "0001-01-01T00:00:00Z",
+        "modified_at": ts,
+        "currentConfig": req.current_config,
+        "baselineConfig": req.baseline_config,
+        "historicalConfig": req.historical_config,
+        "currentMetricStore": req.current_metric_store,
+        "baselineMetricStore": req.baseline_metric_store,
+        "historicalMetricStore": req.historical_metric_store,
+        "status": r.ST_INITIAL,
+        "statusCode": req.status_code,
+        "strategy": req.strategy,
+        "reason": "",
+        "processingContent": "",
+        "anomalyInfo": "",
+        # engine-side lease bookkeeping (ignored by the reference service)
+        "claimed_by": "",
+        "claimed_at": 0.0,
+        "modified_ts": now,
+    }
+
+
+def is_claimable(doc: Dict[str, Any], now: float, max_stuck_s: float) -> bool:
+    st = doc.get("status")
+    if st in r.OPEN_STATUSES:
+        return float(doc.get("not_before", 0.0) or 0.0) <= now
+    if st in r.INPROGRESS_STATUSES:
+        return now - float(doc.get("modified_ts", 0.0) or 0.0) > max_stuck_s
+    return False
+
+
+class JobStore(abc.ABC):
+    """The shared job table."""
+
+    @abc.abstractmethod
+    def get(self, job_id: str) -> Optional[Dict[str, Any]]: ...
+
+    @abc.abstractmethod
+    def _insert_if_absent(self, doc: Dict[str, Any]) -> bool: ...
+
+    @abc.abstractmethod
+    def update(self, job_id: str, fields: Dict[str, Any],
+               expect_claimed_by: Optional[str] = None) -> bool:
+        """Patch a document; with ``expect_claimed_by`` the write only lands if
+        the caller still holds the lease (lost-update protection)."""
+
+    @abc.abstractmethod
+    def claim(self, worker: str, now: Optional[float] = None, max_stuck_s: float = 90.0,
+              limit: int = 64) -> List[Dict[str, Any]]: ...
+
+    @abc.abstractmethod
+    def all(self) -> List[Dict[str, Any]]: ...
+
+    def create(self, req: r.DocumentRequest, now: Optional[float] = None) -> str:
+        job_id = job_id_for(req)
+        if self.get(job_id) is None:
+            self._insert_if_absent(new_document(req, job_id, now))
+        return job_id
+
+    def by_status(self, statuses: Iterable[str]) -> List[Dict[str, Any]]:
+        s = set(statuses)
+        return [d for d in self.all() if d.get("status") in s]
+
+    def close(self) -> None:
+        pass
+
+
+class MemoryJobStore(JobStore):
+    def __init__(self) -> None:
+        self._docs: Dict[str, Dict[str, Any]] = {}
+        self._lock = threading.RLock()
+
+    def get(self, job_id):
+        with self._lock:
+            d = self._docs.get(job_id)
+            return copy.deepcopy(d) if d is not None else None
+
+    def _insert_if_absent(self, doc):
+        with self._lock:
+            if doc["id"] in self._docs:
+                return False
+            self._docs[doc["id"]] = copy.deepcopy(doc)
+            return True
+
+    def update(self, job_id, fields, expect_claimed_by=None):
+        with self._lock:
+            d = self._docs.get(job_id)
+            if d is None:
+                return False
+            if expect_claimed_by is not None and d.get("claimed_by") != expect_claimed_by:
+                return False
+            d.update(copy.deepcopy(fields))
+            now = time.time()
+            d["modified_ts"] = fields.get("modified_ts", now)
+            d["modified_at"] = format_rfc3339_nano(d["modified_ts"])
+            return True
+
+    def claim(self, worker, now=None, max_stuck_s=90.0, limit=64):
+        now = time.time() if now is None else now
+        out = []
+        with self._lock:
+            for d in sorted(self._docs.values(), key=lambda x: x.get("modified_ts", 0.0)):
+                if len(out) >= limit:
+                    break
+                if is_claimable(d, now, max_stuck_s):
+                    d["status"] = r.ST_PREPROCESS_INPROGRESS
+                    d["claimed_by"] = worker
+                    d["claimed_at"] = now
+                    d["modified_ts"] = now
+                    d["modified_at"] = format_rfc3339_nano(now)
+                    out.append(copy.deepcopy(d))
+        return out
+
+    def all(self):
+        with self._lock:
+            return [copy.deepcopy(d) for d in self._docs.values()]
+
+
+class SqliteJobStore(JobStore):
+    """Durable store; safe across processes (``BEGIN IMMEDIATE`` claims)."""
+
+    def __init__(self, path: str) -> None:
+        self.path = path
+        d = os.path.dirname(os.path.abspath(path))
+        os.makedirs(d, exist_ok=True)
+        self._local = threading.local()
+        with self._conn() as c:
+            c.execute("PRAGMA journal_mode=WAL")
+            c.execute("CREATE TABLE IF NOT EXISTS documents ("
+                      "id TEXT PRIMARY KEY, status TEXT, modified_ts REAL, doc TEXT)")
+            c.execute("CREATE INDEX IF NOT EXISTS documents_status ON documents(status)")
+
+    def _conn(self) -> sqlite3.Connection:
+        c = getattr(self._local, "conn", None)
+        if c is None:
+            c = sqlite3.connect(self.path, timeout=30.0, isolation_level=None)
+            self._local.conn = c
+        return c
+
+    def get(self, job_id):
+        row = self._conn().execute("SELECT doc FROM documents WHERE id=?", (job_id,)).fetchone()
+        return json.loads(row[0]) if row else None
+
+    def _insert_if_absent(self, doc):
+        cur = self._conn().execute(
+            "INSERT OR IGNORE INTO documents(id, status, modified_ts, doc) VALUES (?,?,?,?)",
+            (doc["id"], doc["status"], doc["modified_ts"], json.dumps(doc)))
+        return cur.rowcount == 1
+
+    def update(self, job_id, fields, expect_claimed_by=None):
+        c = self._conn()
+        c.execute("BEGIN IMMEDIATE")
+        try:
+            row = c.execute("SELECT doc FROM documents WHERE id=?", (job_id,)).fetchone()
+            if row is None:
+                c.execute("ROLLBACK")
+                return False
+            d = json.loads(row[0])
+            if expect_claimed_by is not None and d.get("claimed_by") != expect_claimed_by:
+                c.execute("ROLLBACK")
+                return False
+            d.update(fields)
+            d["modified_ts"] = fields.get("modified_ts", time.time())
+            d["modified_at"] = format_rfc3339_nano(d["modified_ts"])
+            c.execute("UPDATE documents SET status=?, modified_ts=?, doc=? WHERE id=?",
+                      (d["status"], d["modified_ts"], json.dumps(d), job_id))
+            c.execute("COMMIT")
+            return True
+        except Exception:
+            c.execute("ROLLBACK")
+            raise
+
+    def claim(self, worker, now=None, max_stuck_s=90.0, limit=64):
+        now = time.time() if now is None else now
+        c = self._conn()
+        c.execute("BEGIN IMMEDIATE")
+        try:
+            rows = c.execute(
+                "SELECT doc FROM documents WHERE status IN (?,?,?,?,?) ORDER BY modified_ts",
+                r.OPEN_STATUSES + r.INPROGRESS_STATUSES).fetchall()
+            out = []
+            for (raw,) in rows:
+                if len(out) >= limit:
+                    break
+                d = json.loads(raw)
+                if not is_claimable(d, now, max_stuck_s):
+                    continue
+                d.update(status=r.ST_PREPROCESS_INPROGRESS, claimed_by=worker, claimed_at=now,
+                         modified_ts=now, modified_at=format_rfc3339_nano(now))
+                c.execute("UPDATE documents SET status=?, modified_ts=?, doc=? WHERE id=?",
+                          (d["status"], now, json.dumps(d), d["id"]))
+                out.append(d)
+            c.execute("COMMIT")
+            return out
+        except Exception:
+            c.execute("ROLLBACK")
+            raise
+
+    def all(self):
+        return [json.loads(x[0]) for x in self._conn().execute("SELECT doc FROM documents")]
+
+    def close(self):
+        c = getattr(self._local, "conn", None)
+        if c is not None:
+            c.close()
+            self._local.conn = None
+
+
+def open_store(url: Optional[str]) -> JobStore:
+    """``memory://`` | ``sqlite:///path`` | ``http(s)://es-host:9200`` (ES)."""
+    if not url or url.startswith("memory"):
+        return MemoryJobStore()
+    if url.startswith("sqlite://"):
+        return SqliteJobStore(url[len("sqlite://"):] or "foremast_jobs.db")
+    if url.startswith("http://") or url.startswith("https://"):
+        from .es import ElasticJobStore
+        return ElasticJobStore(url)
+    return SqliteJobStore(url)

@@ -1,0 +1,27 @@
+#!/bin/bash
+# GPU round script: each GPU step under its own time limit; a test FAILURE (rc 1)
+# does not stop later steps, but a fault / abort / timeout (any other rc) does.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+run() {
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 5 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+STEPS=${STEPS:-"tests smoke bench prof"}
+for s in $STEPS; do
+  case $s in
+    tests) run gpu_tests 900 python -m pytest tests -m gpu -x -q ;;
+    smoke) run smoke 300 python __graft_entry__.py smoke ;;
+    bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
+    prof)
+      export TMPDIR=/tmp
+      run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof" -o run -- python3 "$PWD/bench.py" --steps 5 --warmup 2 ;;
+  esac
+done

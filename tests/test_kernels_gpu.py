@@ -1,0 +1,181 @@
+"""Numerics of the gfx950 kernels against the fp32 PyTorch references."""
+
+import numpy as np
+import pytest
+import torch
+
+from foremast_amd.models import bivariate as biv_ref
+from foremast_amd.models import detect as det_ref
+from foremast_amd.models import moving_average as ma_ref
+from foremast_amd.models import pairwise as pw_ref
+from foremast_amd.models import smoothing as sm_ref
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def K():
+    from foremast_amd.ops import _native, kernels
+    _native.require()
+    return kernels
+
+
+def _series(N, T, m, seed=0, nan_frac=0.0):
+    rng = np.random.default_rng(seed)
+    t = np.arange(T)
+    amp = rng.uniform(1, 5, (N, 1))
+    lvl = rng.uniform(5, 50, (N, 1))
+    slope = rng.uniform(-0.01, 0.01, (N, 1))
+    y = lvl + slope * t + amp * np.sin(2 * np.pi * t / m + rng.uniform(0, 6, (N, 1))) \
+        + rng.normal(0, 0.3, (N, T))
+    if nan_frac:
+        mask = rng.random((N, T)) < nan_frac
+        y[mask] = np.nan
+    return y.astype(np.float32)
+
+
+def _ring(y, R, head):
+    """Place logical series y [N, T] into a ring [N, R] starting at column head."""
+    N, T = y.shape
+    ring = np.full((N, R), 7.0, dtype=np.float32)
+    cols = (head + np.arange(T)) % R
+    ring[:, cols] = y
+    return ring
+
+
+def _det_spec(K, N, C, dev, cur=None, thr=2.0, bound=3):
+    return K.DetectSpec(
+        horizons=torch.arange(1, C + 1, dtype=torch.int32, device=dev),
+        threshold=torch.full((N,), thr, device=dev), bound=torch.full((N,), bound, dtype=torch.int8, device=dev),
+        min_lower=torch.full((N,), -1e30, device=dev), cur=cur)
+
+
+@pytest.mark.parametrize("mode,m,T,nan", [
+    (sm_ref.MODE_HW, 24, 24 * 5 + 7, 0.0),
+    (sm_ref.MODE_HW, 24, 24 * 6, 0.02),
+    (sm_ref.MODE_HW, 100, 100 * 4, 0.0),
+    (sm_ref.MODE_ES, 1, 3000, 0.0),
+    (sm_ref.MODE_DES, 1, 2500, 0.01),
+])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_smoothing_kernel_matches_reference(K, mode, m, T, nan, dtype):
+    dev = torch.device("cuda:0")
+    N, C = 48, 12
+    y = _series(N, T, max(m, 24), seed=T + mode, nan_frac=nan)
+    R, head = T + 37, 29
+    ring = torch.tensor(_ring(y, R, head), device=dev).to(dtype)
+    yl = ring.float().cpu().numpy()[:, (head + np.arange(T)) % R]  # bf16-rounded logical
+    grid = sm_ref.make_grid(mode, (0.1, 0.3, 0.6), (0.0, 0.05), (0.1, 0.4))
+    cur = torch.tensor(y[:, -C:] * 1.05, device=dev)
+    spec = _det_spec(K, N, C, dev, cur=cur)
+    out = K.smoothing_fit(ring, head, T, mode, m, grid.to(dev), spec, want_season=True)
+    torch.cuda.synchronize()
+    ref = sm_ref.fit_smoothing(torch.tensor(yl, dtype=torch.float64), mode, grid.double(), m=m)
+    # the kernel's chosen combo must be (near-)optimal under the reference SSE
+    ref_all = []
+    for g in range(grid.shape[0]):
+        fg = sm_ref.fit_smoothing(torch.tensor(yl, dtype=torch.float64), mode, grid[g:g + 1].double(), m=m)
+        ref_all.append(fg.sse)
+    sse_all = torch.stack(ref_all, 1)  # [N, G]
+    kb = out["best"].cpu().long()
+    chosen = sse_all.gather(1, kb[:, None]).squeeze(1)
+    assert torch.all(chosen <= ref.sse * (1 + 1e-4) + 1e-6), "kernel picked a sub-optimal grid point"
+    same = kb == ref.best
+    assert same.float().mean() > 0.9
+    np.testing.assert_allclose(out["sigma"].cpu().numpy()[same.numpy()], ref.sigma.numpy()[same.numpy()],
+                               rtol=2e-3, atol=1e-4)
+    np.testing.assert_allclose(out["level"].cpu().numpy()[same.numpy()], ref.level.numpy()[same.numpy()],
+                               rtol=1e-3, atol=2e-3)
+    f_ref = sm_ref.forecast(ref, torch.arange(1, C + 1))
+    np.testing.assert_allclose(out["forecast"].cpu().numpy()[same.numpy()], f_ref.numpy()[same.numpy()],
+                               rtol=2e-3, atol=5e-3)
+    d = det_ref.detect(torch.tensor(out["forecast"].cpu()), out["sigma"].cpu(), cur.cpu(),
+                       torch.full((N,), 2.0), torch.full((N,), 3, dtype=torch.int8), torch.full((N,), -1e30))
+    assert torch.equal(d.count, out["count"].cpu())
+    assert torch.equal(d.verdict, out["verdict"].cpu())
+
+
+def test_smoothing_kernel_flagship_shape(K):
+    """T = 10080 (7 days at 60 s), season 1440 (daily), bf16 ring."""
+    dev = torch.device("cuda:0")
+    N, T, m, C = 16, 10080, 1440, 50
+    y = _series(N, T, m, seed=5)
+    ring = torch.tensor(y, device=dev).to(torch.bfloat16)
+    grid = sm_ref.make_grid(sm_ref.MODE_HW, (0.1, 0.3, 0.5, 0.8), (0.0, 0.01, 0.05, 0.1), (0.05, 0.1, 0.3, 0.5))
+    spec = _det_spec(K, N, C, dev, cur=torch.tensor(y[:, :C], device=dev))
+    out = K.smoothing_fit(ring, 0, T, sm_ref.MODE_HW, m, grid.to(dev), spec)
+    torch.cuda.synchronize()
+    ref = sm_ref.fit_smoothing(ring.float().cpu(), sm_ref.MODE_HW, grid, m=m)
+    same = (out["best"].cpu().long() == ref.best)
+    assert same.float().mean() >= 0.75
+    np.testing.assert_allclose(out["sigma"].cpu().numpy(), ref.sigma.numpy(), rtol=5e-3)
+
+
+def test_window_stats_kernel(K):
+    dev = torch.device("cuda:0")
+    N, T, C = 40, 1000, 8
+    y = _series(N, T, 24, seed=11, nan_frac=0.05)
+    for dtype in (torch.float32, torch.bfloat16):
+        R, head = 1024, 1000  # wraps
+        ring = torch.tensor(_ring(y, R, head), device=dev).to(dtype)
+        yl = ring.float().cpu()[:, (head + np.arange(T)) % R]
+        cur = torch.tensor(y[:, :C] + 3.0, device=dev)
+        spec = _det_spec(K, N, C, dev, cur=cur)
+        out = K.window_stats(ring, head, T, spec)
+        torch.cuda.synchronize()
+        st = ma_ref.window_stats(yl)
+        np.testing.assert_allclose(out["mean"].cpu().numpy(), st.mean.numpy(), rtol=1e-5, atol=1e-4)
+        np.testing.assert_allclose(out["std"].cpu().numpy(), st.std.numpy(), rtol=1e-4, atol=1e-4)
+        d = det_ref.detect(st.mean[:, None].expand(N, C), st.std, cur.cpu(), torch.full((N,), 2.0),
+                           torch.full((N,), 3, dtype=torch.int8), torch.full((N,), -1e30))
+        assert torch.equal(d.verdict, out["verdict"].cpu())
+
+
+def test_rank_tests_kernel(K):
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(3)
+    N, nb, nc = 300, 50, 40
+    b = rng.normal(0, 1, (N, nb)).astype(np.float32)
+    c = (rng.normal(0, 1, (N, nc)) + rng.choice([0, 0.8], (N, 1))).astype(np.float32)
+    b[::7] = np.round(b[::7])
+    c[::7] = np.round(c[::7])
+    b[5, 30:] = np.nan
+    c[9, :4] = b[9, :4]
+    out = K.rank_tests(torch.tensor(b, device=dev), torch.tensor(c, device=dev), pw_ref.PW_ALL, 0.05)
+    torch.cuda.synchronize()
+    ref = pw_ref.rank_tests(torch.tensor(b, dtype=torch.float64), torch.tensor(c, dtype=torch.float64))
+    p = out["pvals"].cpu().double()
+    np.testing.assert_allclose(p[:, 0].numpy(), ref.p_mw.numpy(), rtol=2e-3, atol=1e-5)
+    np.testing.assert_allclose(p[:, 1].numpy(), ref.p_wilcoxon.numpy(), rtol=2e-3, atol=1e-5)
+    np.testing.assert_allclose(p[:, 2].numpy(), ref.p_kruskal.numpy(), rtol=2e-3, atol=1e-5)
+    dref = pw_ref.pairwise_differs(ref, pw_ref.PW_ALL, 0.05)
+    agree = (out["differs"].cpu().bool() == dref).float().mean()
+    assert agree > 0.99
+
+
+def test_bivariate_kernel(K):
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(4)
+    N, T, C = 32, 2000, 6
+    h = rng.multivariate_normal([1, 2], [[1.0, 0.6], [0.6, 2.0]], size=(N, T)).astype(np.float32)
+    h[3, 10:20, 0] = np.nan
+    hx = torch.tensor(h[..., 0], device=dev)
+    hy = torch.tensor(h[..., 1], device=dev)
+    cur = torch.tensor(rng.normal(1, 2, (N, C, 2)).astype(np.float32), device=dev)
+    out = K.bivariate(hx, hy, 0, T, cur, torch.full((N,), 3.0, device=dev))
+    torch.cuda.synchronize()
+    fit = biv_ref.fit_bivariate(torch.tensor(h))
+    d2 = biv_ref.mahalanobis2(fit, cur.cpu())
+    np.testing.assert_allclose(out["d2"].cpu().numpy(), d2.numpy(), rtol=2e-3, atol=1e-3)
+    assert torch.equal((d2 > 9.0).sum(1).int(), out["count"].cpu())
+
+
+def test_ring_append(K):
+    dev = torch.device("cuda:0")
+    for dtype in (torch.float32, torch.bfloat16):
+        dst = torch.zeros((10, 16), device=dev, dtype=dtype)
+        src = torch.arange(50, dtype=torch.float32, device=dev).view(10, 5)
+        K.ring_append(dst, 14, src)
+        torch.cuda.synchronize()
+        cols = [14, 15, 0, 1, 2]
+        assert torch.equal(dst[:, cols].float(), src)

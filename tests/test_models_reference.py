@@ -1,0 +1,158 @@
+"""Oracle tests for the reference scorers: scipy for the rank tests, a
+textbook (non error-correction) numpy Holt-Winters for the smoothing family."""
+
+import math
+
+import numpy as np
+import pytest
+import scipy.stats as ss
+import torch
+
+from foremast_amd.models import bivariate, detect, moving_average, pairwise, smoothing
+
+
+def _textbook_hw(y, m, a, b, g, mode):
+    """Textbook additive Holt-Winters one-step SSE (numpy, float64)."""
+    y = np.asarray(y, dtype=np.float64)
+    T = len(y)
+    if mode == smoothing.MODE_HW:
+        Tp = ((T + m - 1) // m) * m
+        y = np.concatenate([np.full(Tp - T, np.nan), y])
+        l = np.nanmean(y[:m])
+        bb = (np.nanmean(y[m:2 * m]) - l) / m
+        s = np.where(np.isnan(y[:m]), 0.0, y[:m] - l)
+        t0 = m
+    else:
+        Tp = T
+        first = np.argmax(~np.isnan(y))
+        l = y[first]
+        bb = 0.0
+        s = np.zeros(1)
+        m = 1
+        t0 = 0
+    sse = 0.0
+    n = 0
+    for t in range(t0, Tp):
+        p = t % m
+        sp = s[p] if mode == smoothing.MODE_HW else 0.0
+        yhat = l + bb + sp
+        yt = y[t]
+        if np.isnan(yt):
+            yt = yhat
+        else:
+            sse += (yt - yhat) ** 2
+            n += 1
+        ln = a * (yt - sp) + (1 - a) * (l + bb)
+        bn = b * (ln - l) + (1 - b) * bb
+        if mode == smoothing.MODE_HW:
+            s[p] = g * (yt - ln) + (1 - g) * sp
+        l, bb = ln, bn
+    return sse, n, l, bb, s, Tp
+
+
+@pytest.mark.parametrize("mode", [smoothing.MODE_ES, smoothing.MODE_DES, smoothing.MODE_HW])
+def test_smoothing_matches_textbook(mode):
+    rng = np.random.default_rng(0)
+    m = 12
+    N, T = 5, 5 * m + 7
+    t = np.arange(T)
+    y = (10 + 0.05 * t + 3 * np.sin(2 * np.pi * t / m))[None, :] + rng.normal(0, 0.5, (N, T))
+    y[1, 5] = np.nan
+    y[2, 30:33] = np.nan
+    grid = smoothing.make_grid(mode, (0.2, 0.6), (0.0, 0.1), (0.1, 0.4))
+    fit = smoothing.fit_smoothing(torch.tensor(y, dtype=torch.float32), mode, grid, m=m)
+    for i in range(N):
+        best = None
+        for gi, (a, b, g) in enumerate(grid.tolist()):
+            sse, n, l, bb, s, Tp = _textbook_hw(y[i], m, a, b, g, mode)
+            if best is None or sse < best[0]:
+                best = (sse, n, l, bb, s, gi, Tp)
+        sse, n, l, bb, s, gi, Tp = best
+        assert int(fit.best[i]) == gi
+        assert fit.sigma[i].item() == pytest.approx(math.sqrt(sse / n), rel=1e-4)
+        assert fit.level[i].item() == pytest.approx(l, rel=1e-4, abs=1e-4)
+        assert fit.trend[i].item() == pytest.approx(bb, rel=1e-3, abs=1e-4)
+        h = torch.tensor([1, 2, 5])
+        f = smoothing.forecast(fit, h)[i].numpy()
+        sp = [s[(Tp - 1 + k) % len(s)] if mode == smoothing.MODE_HW else 0.0 for k in (1, 2, 5)]
+        exp = [l + k * bb + sp[j] for j, k in enumerate((1, 2, 5))]
+        np.testing.assert_allclose(f, exp, rtol=1e-4, atol=1e-3)
+
+
+def test_rank_tests_vs_scipy():
+    rng = np.random.default_rng(1)
+    N, nb, nc = 12, 30, 25
+    b = rng.normal(0, 1, (N, nb))
+    c = rng.normal(0.3, 1, (N, nc))
+    # ties and a NaN-padded row
+    b[0] = np.round(b[0], 0)
+    c[0] = np.round(c[0], 0)
+    b[3, 20:] = np.nan
+    c[4, :5] = np.round(b[4, :5], 1)
+    b[4, :5] = np.round(b[4, :5], 1)
+    res = pairwise.rank_tests(torch.tensor(b, dtype=torch.float64), torch.tensor(c, dtype=torch.float64))
+    for i in range(N):
+        bi = b[i][~np.isnan(b[i])]
+        ci = c[i][~np.isnan(c[i])]
+        mw = ss.mannwhitneyu(bi, ci, alternative="two-sided", use_continuity=True, method="asymptotic")
+        assert res.p_mw[i].item() == pytest.approx(mw.pvalue, rel=1e-4, abs=1e-6)
+        kw = ss.kruskal(bi, ci)
+        assert res.p_kruskal[i].item() == pytest.approx(kw.pvalue, rel=1e-4, abs=1e-6)
+        k = min(nb, nc)
+        d = c[i, :k] - b[i, :k]
+        ok = ~np.isnan(d)
+        bw, cw = b[i, :k][ok], c[i, :k][ok]
+        w = ss.wilcoxon(cw, bw, zero_method="wilcox", correction=False, method="approx")
+        assert res.p_wilcoxon[i].item() == pytest.approx(w.pvalue, rel=1e-4, abs=1e-6)
+
+
+def test_friedman_vs_scipy():
+    rng = np.random.default_rng(2)
+    g = rng.normal(0, 1, (3, 10, 4))
+    g[1] = np.round(g[1])
+    p = pairwise.friedman(torch.tensor(g, dtype=torch.float64))
+    for i in range(3):
+        exp = ss.friedmanchisquare(*[g[i, :, j] for j in range(4)]).pvalue
+        assert p[i].item() == pytest.approx(exp, rel=1e-4)
+
+
+def test_pairwise_decision_modes():
+    N = 4
+    r = pairwise.PairwiseResult(
+        p_mw=torch.tensor([0.01, 0.01, 0.5, 0.01]), p_wilcoxon=torch.tensor([0.01, 0.5, 0.5, 0.01]),
+        p_kruskal=torch.tensor([0.01, 0.01, 0.5, 0.01]), n_base=torch.tensor([30., 30., 30., 3.]),
+        n_cur=torch.tensor([30., 30., 30., 3.]), n_pairs=torch.tensor([30., 30., 30., 3.]))
+    assert pairwise.pairwise_differs(r, pairwise.PW_ALL, 0.05).tolist() == [True, False, False, False]
+    assert pairwise.pairwise_differs(r, pairwise.PW_ANY, 0.05).tolist() == [True, True, False, False]
+    assert pairwise.pairwise_differs(r, pairwise.PW_MANN_WHITE, 0.05).tolist() == [True, True, False, False]
+
+
+def test_window_stats_and_detect():
+    rng = np.random.default_rng(3)
+    y = rng.normal(5, 2, (6, 200)).astype(np.float32)
+    y[2, :50] = np.nan
+    st = moving_average.window_stats(torch.tensor(y))
+    np.testing.assert_allclose(st.mean.numpy(), np.nanmean(y, 1), rtol=1e-5)
+    np.testing.assert_allclose(st.std.numpy(), np.nanstd(y, 1), rtol=1e-4)
+    stw = moving_average.window_stats(torch.tensor(y), window=60)
+    np.testing.assert_allclose(stw.mean.numpy(), np.nanmean(y[:, -60:], 1), rtol=1e-5)
+    f = st.mean[:, None].expand(6, 4)
+    x = torch.tensor(np.array([[5, 5, 5, 100]] * 6, dtype=np.float32))
+    x[5] = float("nan")
+    d = detect.detect(f, st.std, x, torch.full((6,), 2.0), torch.tensor([1, 2, 3, 1, 1, 1]),
+                      torch.zeros(6))
+    assert d.verdict.tolist() == [1, 0, 1, 1, 1, -1]
+
+
+def test_bivariate():
+    rng = np.random.default_rng(4)
+    cov = np.array([[1.0, 0.6], [0.6, 2.0]])
+    h = rng.multivariate_normal([1, 2], cov, size=(3, 4000))
+    fit = bivariate.fit_bivariate(torch.tensor(h))
+    x = torch.tensor([[[1.0, 2.0], [4.0, -1.0]]] * 3)
+    d2 = bivariate.mahalanobis2(fit, x)
+    inv = np.linalg.inv(np.cov(h[0].T, bias=True))
+    dv = np.array([3.0, -3.0]) - (h[0].mean(0) - np.array([1, 2]))
+    exp = dv @ inv @ dv
+    assert d2[0, 1].item() == pytest.approx(exp, rel=1e-3)
+    assert d2[0, 0].item() < 0.1

@@ -1,0 +1,39 @@
+"""The ctypes argument structs must match the C structs in csrc/args.h
+(runs on CPU: loading the library does not need a device)."""
+
+import ctypes as C
+
+import pytest
+
+from foremast_amd.ops import _native as nat
+from foremast_amd.ops import build
+
+
+@pytest.fixture(scope="module")
+def lib():
+    try:
+        build.build()
+    except RuntimeError as e:  # pragma: no cover
+        pytest.skip(f"no HIP toolchain: {e}")
+    lib = nat.load()
+    if lib is None:
+        pytest.skip("library failed to load")
+    lib.fm_abi_sizeof.restype = C.c_longlong
+    lib.fm_abi_offsetof.restype = C.c_longlong
+    return lib
+
+
+@pytest.mark.parametrize("name", ["DetectArgs", "SmoothArgs", "RankArgs", "WindowArgs", "BivArgs"])
+def test_struct_sizes(lib, name):
+    assert lib.fm_abi_sizeof(name.encode()) == C.sizeof(getattr(nat, name))
+
+
+@pytest.mark.parametrize("name,field", [
+    ("SmoothArgs", "det"), ("SmoothArgs", "season_out"), ("SmoothArgs", "grid"),
+    ("DetectArgs", "pw_scale"), ("DetectArgs", "app_stats"), ("DetectArgs", "ld_cur"),
+    ("RankArgs", "pvals"), ("RankArgs", "alpha"), ("WindowArgs", "det"),
+    ("BivArgs", "eps"), ("BivArgs", "app_stats"),
+])
+def test_struct_offsets(lib, name, field):
+    cls = getattr(nat, name)
+    assert lib.fm_abi_offsetof(name.encode(), field.encode()) == getattr(cls, field).offset
