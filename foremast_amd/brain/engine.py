@@ -71,6 +71,10 @@ class StreamingShard:
                           else torch.full((N,), self.cfg.min_lower_bound, dtype=torch.float32, **kw))
         self.app_id = app_id if app_id is not None else torch.zeros(N, dtype=torch.int32, **kw)
         self.app_stats = torch.zeros((max(spec.n_apps, 1), 2), dtype=torch.int32, **kw)
+        if N and app_id is not None:
+            lo, hi = int(self.app_id.min()), int(self.app_id.max())  # one-time sync at setup
+            if lo < 0 or hi >= self.app_stats.shape[0]:
+                raise ValueError(f"app_id range [{lo}, {hi}] outside the app table of {self.app_stats.shape[0]}")
         self.algorithm = spec.algorithm
         self.mode = ALGO_MODE.get(spec.algorithm)
         self.pw_mode = pw_ref.PW_BY_NAME.get(spec.pairwise.upper(), pw_ref.PW_ALL)

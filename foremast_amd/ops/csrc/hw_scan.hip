@@ -1,0 +1,486 @@
+// K2/K3 fast path: branch-free time-parallel smoothing fit for geometries
+// where every active lane owns exactly K steps of a segment (seg = L*K,
+// L <= 64), e.g. Holt-Winters with a daily season of 1440 = 60 lanes x 24.
+//
+// Same semantics and outputs as smooth_fit_kernel (smoothing.hip); what
+// differs is the schedule:
+//  * the staged series lives in LDS lane-chunked ([seg][64][KP]) so each
+//    lane pulls its K values of a segment with 16-byte ds_reads
+//    (48-byte lane stride for K=24 bf16: conflict-free);
+//  * the per-step loops carry no per-lane guards (idle lanes >= L compute
+//    garbage that is masked once per segment), so a whole segment is one
+//    basic block the scheduler can interleave;
+//  * pass 1 of season k+1 (its local affine map, which needs season k's
+//    updated seasonal state) is fused into pass 2 of season k: two
+//    independent dependency chains per step;
+//  * the cross-lane affine scan uses DPP (row_shr 1/2/4/8, row_bcast 15/31,
+//    wave_shr 1) instead of LDS permutes, end-of-segment state is a
+//    v_readlane;
+//  * per-wave best seasonal state is kept in LDS, not registers.
+#include "common.h"
+#include "detect.h"
+#include "args.h"
+
+#include <type_traits>
+
+extern __shared__ __attribute__((aligned(16))) char fm_hw_smem[];
+
+namespace {
+
+enum { MODE_ES = 0, MODE_DES = 1, MODE_HW = 2 };
+
+template <int CTRL, int RM>
+__device__ __forceinline__ float dppf(float old, float src) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src), CTRL, RM, 0xf, false));
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ v2f dpp2(float old, v2f src) {
+  v2f r;
+  r.x = dppf<CTRL, RM>(old, src.x);
+  r.y = dppf<CTRL, RM>(old, src.y);
+  return r;
+}
+__device__ __forceinline__ float rdlane(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+template <typename V> __device__ __forceinline__ V splatv(float a);
+template <> __device__ __forceinline__ float splatv<float>(float a) { return a; }
+template <> __device__ __forceinline__ v2f splatv<v2f>(float a) { return splat2(a); }
+
+template <int CTRL, int RM>
+__device__ __forceinline__ float dppv(float old, float src) { return dppf<CTRL, RM>(old, src); }
+template <int CTRL, int RM>
+__device__ __forceinline__ v2f dppv(float old, v2f src) { return dpp2<CTRL, RM>(old, src); }
+
+__device__ __forceinline__ float rdlanev(float v, int l) { return rdlane(v, l); }
+__device__ __forceinline__ v2f rdlanev(v2f v, int l) { v2f r; r.x = rdlane(v.x, l); r.y = rdlane(v.y, l); return r; }
+__device__ __forceinline__ float wave_sumv(float v) { return wave_sum(v); }
+__device__ __forceinline__ v2f wave_sumv(v2f v) { return wave_sum2(v); }
+__device__ __forceinline__ float compv(float v, int) { return v; }
+__device__ __forceinline__ float compv(v2f v, int c) { return c ? v.y : v.x; }
+
+template <typename V>
+struct Aff {
+  V m11, m12, m21, m22, v1, v2;
+};
+
+// this = this ∘ q  (apply q first)
+template <typename V>
+__device__ __forceinline__ void compose(Aff<V>& a, const Aff<V>& q) {
+  const V nv1 = a.m11 * q.v1 + a.m12 * q.v2 + a.v1;
+  const V nv2 = a.m21 * q.v1 + a.m22 * q.v2 + a.v2;
+  const V n11 = a.m11 * q.m11 + a.m12 * q.m21, n12 = a.m11 * q.m12 + a.m12 * q.m22;
+  const V n21 = a.m21 * q.m11 + a.m22 * q.m21, n22 = a.m21 * q.m12 + a.m22 * q.m22;
+  a.m11 = n11; a.m12 = n12; a.m21 = n21; a.m22 = n22; a.v1 = nv1; a.v2 = nv2;
+}
+
+template <int CTRL, int RM, typename V>
+__device__ __forceinline__ void scan_round(Aff<V>& a) {
+  Aff<V> q;
+  q.m11 = dppv<CTRL, RM>(1.f, a.m11);
+  q.m12 = dppv<CTRL, RM>(0.f, a.m12);
+  q.m21 = dppv<CTRL, RM>(0.f, a.m21);
+  q.m22 = dppv<CTRL, RM>(1.f, a.m22);
+  q.v1 = dppv<CTRL, RM>(0.f, a.v1);
+  q.v2 = dppv<CTRL, RM>(0.f, a.v2);
+  compose(a, q);
+}
+
+// inclusive wave scan of affine maps (lane j: f_j ∘ ... ∘ f_0), then shift by
+// one lane (exclusive); lane 0 gets the identity.
+template <typename V>
+__device__ __forceinline__ void wave_exclusive_scan(Aff<V>& a) {
+  scan_round<0x111, 0xf>(a);  // row_shr:1
+  scan_round<0x112, 0xf>(a);  // row_shr:2
+  scan_round<0x114, 0xf>(a);  // row_shr:4
+  scan_round<0x118, 0xf>(a);  // row_shr:8
+  scan_round<0x142, 0xa>(a);  // row_bcast:15 → rows 1, 3
+  scan_round<0x143, 0xc>(a);  // row_bcast:31 → rows 2, 3
+  a.m11 = dppv<0x138, 0xf>(1.f, a.m11);  // wave_shr:1
+  a.m12 = dppv<0x138, 0xf>(0.f, a.m12);
+  a.m21 = dppv<0x138, 0xf>(0.f, a.m21);
+  a.m22 = dppv<0x138, 0xf>(1.f, a.m22);
+  a.v1 = dppv<0x138, 0xf>(0.f, a.v1);
+  a.v2 = dppv<0x138, 0xf>(0.f, a.v2);
+}
+
+// ---- register image of one lane's K values of a segment ---------------------------
+template <typename TIN, int K>
+struct YRegs {
+  static constexpr int KP = (sizeof(TIN) == 2) ? ((K + 7) / 8) * 8 : ((K + 3) / 4) * 4;
+  static constexpr int NW = KP * sizeof(TIN) / 4;  // 32-bit words
+  unsigned w[NW];
+  __device__ __forceinline__ void load(const TIN* lds) {
+    const uint4* p = (const uint4*)lds;
+#pragma unroll
+    for (int q = 0; q < NW / 4; ++q) {
+      const uint4 v = p[q];
+      w[4 * q + 0] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+    }
+  }
+  __device__ __forceinline__ float get(int i) const {
+    if (sizeof(TIN) == 2) {
+      const unsigned x = w[i >> 1];
+      return __uint_as_float((i & 1) ? (x & 0xffff0000u) : (x << 16));
+    }
+    return __uint_as_float(w[i]);
+  }
+};
+
+template <int K, typename Y, typename V>
+__device__ __forceinline__ void pass1_fast(const Y& y, const V* s, V al, V ab, V& v1, V& v2) {
+  v1 = splatv<V>(0.f);
+  v2 = splatv<V>(0.f);
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    const V t = v1 + v2;
+    const V e = (splatv<V>(y.get(i)) - s[i]) - t;
+    v1 = t + al * e;
+    v2 = v2 + ab * e;
+  }
+}
+
+// general local map (segment contains NaN): NaN steps are x' = [[1,1],[0,1]] x
+template <int K, typename Y, typename V>
+__device__ __forceinline__ void pass1_slow(const Y& y, const V* s, V al, V ab, V oma, V omab, Aff<V>& a) {
+  const V one = splatv<V>(1.f), zero = splatv<V>(0.f);
+  a.m11 = one; a.m12 = zero; a.m21 = zero; a.m22 = one; a.v1 = zero; a.v2 = zero;
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    const float yi = y.get(i);
+    const bool ok = (yi == yi);
+    const V a11 = ok ? oma : one;
+    const V a21 = ok ? -ab : zero;
+    const V a22 = ok ? omab : one;
+    const V u = ok ? (splatv<V>(yi) - s[i]) : zero;
+    const V n11 = a11 * (a.m11 + a.m21), n12 = a11 * (a.m12 + a.m22);
+    const V n21 = a21 * a.m11 + a22 * a.m21, n22 = a21 * a.m12 + a22 * a.m22;
+    const V nv1 = a11 * (a.v1 + a.v2) + (ok ? al * u : zero);
+    const V nv2 = a21 * a.v1 + a22 * a.v2 + (ok ? ab * u : zero);
+    a.m11 = n11; a.m12 = n12; a.m21 = n21; a.m22 = n22; a.v1 = nv1; a.v2 = nv2;
+  }
+}
+
+// pass 2 of this segment (true start state x1/x2), optionally fused with the
+// fast pass 1 of the next segment.
+template <int K, int MODE, bool MASK, bool FUSE, typename Y, typename V>
+__device__ __forceinline__ void pass2(const Y& y, const Y& yn, V* s, V al, V ab, V g1a, V& x1, V& x2, V& sse,
+                                      V& p1, V& p2) {
+  if (FUSE) { p1 = splatv<V>(0.f); p2 = splatv<V>(0.f); }
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    const V t = x1 + x2;
+    const float yi = y.get(i);
+    V e = (splatv<V>(yi) - s[i]) - t;
+    if (MASK) e = (yi == yi) ? e : splatv<V>(0.f);
+    x1 = t + al * e;
+    x2 = x2 + ab * e;
+    if (MODE == MODE_HW) s[i] = s[i] + g1a * e;
+    sse = sse + e * e;
+    if (FUSE) {
+      const V tn = p1 + p2;
+      const V en = (splatv<V>(yn.get(i)) - s[i]) - tn;
+      p1 = tn + al * en;
+      p2 = p2 + ab * en;
+    }
+  }
+}
+
+}  // namespace
+
+template <int K, int MODE, typename TIN, int NC, int MINW>
+__global__ __launch_bounds__(256, MINW) void hw_scan_kernel(const SmoothArgs a) {
+  using V = typename std::conditional<NC == 2, v2f, float>::type;
+  using YR = YRegs<TIN, K>;
+  constexpr int KP = YR::KP;
+  const int n = blockIdx.x;
+  const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+  const int nwaves = blockDim.x / FM_WAVE;
+  const int seg = a.seg;
+  const int L = seg / K;  // active lanes
+  const int nseg = a.Tp / seg;
+
+  // ---- LDS carve: ys[nseg][64][KP] | bests[nwaves][64][KP] f32 | segnan | red | wbest ----
+  size_t off = 0;
+  TIN* ys = (TIN*)(fm_hw_smem + off);
+  off += ((size_t)nseg * 64 * KP * sizeof(TIN) + 15) & ~(size_t)15;
+  float* bests = (float*)(fm_hw_smem + off);
+  if (MODE == MODE_HW) off += (size_t)nwaves * 64 * KP * 4;
+  int* segnan = (int*)(fm_hw_smem + off);
+  off += ((size_t)nseg * 4 + 15) & ~(size_t)15;
+  float* red = (float*)(fm_hw_smem + off);
+  off += 64 * 4;
+  float* wbest = (float*)(fm_hw_smem + off);
+
+  for (int i = tid; i < nseg; i += blockDim.x) segnan[i] = 0;
+  __syncthreads();
+
+  // ---- stage: logical padded index p = sg*seg + j*K + i → ys[sg][j][i] ----------------
+  const TIN* row = (const TIN*)a.hist + (long long)n * a.ld;
+  const int t0 = (MODE == MODE_HW) ? a.m : 0;
+  float nv_local = 0.f;
+  const int total = nseg * 64 * KP;
+  for (int idx = tid; idx < total; idx += blockDim.x) {
+    const int i = idx % KP;
+    const int j = (idx / KP) & 63;
+    const int sg = idx / (KP * 64);
+    float v = fm_nan();
+    if (i < K && j < L) {
+      const int p = sg * seg + j * K + i;
+      const int t = p - a.pad;
+      if (t >= 0) {
+        int c = a.head + t;
+        if (c >= a.ring_len) c -= a.ring_len;
+        v = to_f32<TIN>(row[c]);
+      }
+      const bool isn = (v != v);
+      if (isn) atomicOr(&segnan[sg], 1);
+      if (!isn && p >= t0) nv_local += 1.f;
+    }
+    ys[idx] = from_f32<TIN>(v);
+  }
+  const float n_valid = blk_sum(nv_local, red);
+
+  // ---- initial state ----------------------------------------------------------------
+  float l0 = 0.f, b0 = 0.f;
+  if (MODE == MODE_HW) {
+    float s0 = 0.f, c0 = 0.f, s1 = 0.f, c1 = 0.f;
+    for (int q = tid; q < seg; q += blockDim.x) {
+      const int j = q / K, i = q % K;
+      const float y0 = to_f32<TIN>(ys[(0 * 64 + j) * KP + i]);
+      const float y1 = to_f32<TIN>(ys[(1 * 64 + j) * KP + i]);
+      if (y0 == y0) { s0 += y0; c0 += 1.f; }
+      if (y1 == y1) { s1 += y1; c1 += 1.f; }
+    }
+    s0 = blk_sum(s0, red);
+    c0 = blk_sum(c0, red);
+    s1 = blk_sum(s1, red);
+    c1 = blk_sum(c1, red);
+    l0 = c0 > 0.f ? s0 / c0 : 0.f;
+    b0 = ((c1 > 0.f ? s1 / c1 : 0.f) - l0) / (float)a.m;
+  } else {
+    // first valid value in logical order (segments, then lanes, then steps)
+    int first = 0x7fffffff;
+    for (int q = tid; q < nseg * seg; q += blockDim.x) {
+      const int sg = q / seg, r = q % seg, j = r / K, i = r % K;
+      const float y = to_f32<TIN>(ys[(sg * 64 + j) * KP + i]);
+      if (y == y && q < first) first = q;
+    }
+    float f = (float)first;
+    f = -blk_max(-f, red);
+    const int fi = (int)f;
+    if (fi < nseg * seg) {
+      const int sg = fi / seg, r = fi % seg;
+      l0 = to_f32<TIN>(ys[(sg * 64 + r / K) * KP + r % K]);
+    }
+  }
+
+  const bool active = lane < L;
+  float bestSSE = __builtin_huge_valf();
+  int bestIdx = 0x7fffffff;
+  float bestL = l0, bestB = b0;
+  float* mybest = bests + ((size_t)w * 64 + lane) * KP;
+  const int npairs = (a.G + NC - 1) / NC;
+  const int sgA = (MODE == MODE_HW) ? 1 : 0;
+
+  for (int pi = w; pi < npairs; pi += nwaves) {
+    const int c0 = NC * pi;
+    const int c1 = (NC == 2 && NC * pi + 1 < a.G) ? NC * pi + 1 : c0;
+    V al, be, ga;
+    if constexpr (NC == 2) {
+      al.x = a.grid[3 * c0 + 0]; al.y = a.grid[3 * c1 + 0];
+      be.x = a.grid[3 * c0 + 1]; be.y = a.grid[3 * c1 + 1];
+      ga.x = a.grid[3 * c0 + 2]; ga.y = a.grid[3 * c1 + 2];
+    } else {
+      al = a.grid[3 * c0 + 0]; be = a.grid[3 * c0 + 1]; ga = a.grid[3 * c0 + 2];
+    }
+    const V one = splatv<V>(1.f), zero = splatv<V>(0.f);
+    const V ab = al * be, oma = one - al, omab = one - ab, g1a = ga * oma;
+
+    // A^K for a full NaN-free lane chunk
+    Aff<V> P;
+    P.m11 = one; P.m12 = zero; P.m21 = zero; P.m22 = one;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      const V n11 = oma * (P.m11 + P.m21), n12 = oma * (P.m12 + P.m22);
+      const V n21 = omab * P.m21 - ab * P.m11, n22 = omab * P.m22 - ab * P.m12;
+      P.m11 = n11; P.m12 = n12; P.m21 = n21; P.m22 = n22;
+    }
+
+    // seasonal state: my phases of season 0, minus l0
+    V s[K];
+    {
+      YR y0;
+      y0.load(ys + ((size_t)0 * 64 + lane) * KP);
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        const float y = y0.get(i);
+        s[i] = splatv<V>((MODE == MODE_HW && y == y) ? y - l0 : 0.f);
+      }
+    }
+    V Lv = splatv<V>(l0), Bv = splatv<V>(b0), sse = zero;
+
+    // prologue: pass 1 of the first fitted segment
+    YR ycur, ynext;
+    ycur.load(ys + ((size_t)sgA * 64 + lane) * KP);
+    Aff<V> loc;
+    bool locfast = !segnan[sgA];
+    if (locfast) {
+      pass1_fast<K>(ycur, s, al, ab, loc.v1, loc.v2);
+    } else {
+      pass1_slow<K>(ycur, s, al, ab, oma, omab, loc);
+    }
+
+    for (int sg = sgA; sg < nseg; ++sg) {
+      if (locfast) { loc.m11 = P.m11; loc.m12 = P.m12; loc.m21 = P.m21; loc.m22 = P.m22; }
+      wave_exclusive_scan(loc);
+      V x1 = loc.m11 * Lv + loc.m12 * Bv + loc.v1;
+      V x2 = loc.m21 * Lv + loc.m22 * Bv + loc.v2;
+      const bool has_next = sg + 1 < nseg;
+      if (has_next) ynext.load(ys + ((size_t)(sg + 1) * 64 + lane) * KP);
+      const bool mask = segnan[sg] != 0;
+      const bool next_fast = has_next && !segnan[sg + 1];
+      if (next_fast) {
+        if (mask) pass2<K, MODE, true, true>(ycur, ynext, s, al, ab, g1a, x1, x2, sse, loc.v1, loc.v2);
+        else pass2<K, MODE, false, true>(ycur, ynext, s, al, ab, g1a, x1, x2, sse, loc.v1, loc.v2);
+        locfast = true;
+      } else {
+        V d1, d2;
+        if (mask) pass2<K, MODE, true, false>(ycur, ynext, s, al, ab, g1a, x1, x2, sse, d1, d2);
+        else pass2<K, MODE, false, false>(ycur, ynext, s, al, ab, g1a, x1, x2, sse, d1, d2);
+        if (has_next) pass1_slow<K>(ynext, s, al, ab, oma, omab, loc);
+        locfast = false;
+      }
+      Lv = rdlanev(x1, L - 1);
+      Bv = rdlanev(x2, L - 1);
+      ycur = ynext;
+    }
+    sse = active ? sse : zero;
+    sse = wave_sumv(sse);
+    const float s0v = compv(sse, 0), s1v = compv(sse, 1);
+    bool upd0 = (s0v < bestSSE || (s0v == bestSSE && c0 < bestIdx));
+    if (upd0) { bestSSE = s0v; bestIdx = c0; bestL = compv(Lv, 0); bestB = compv(Bv, 0); }
+    const bool upd1 = (c1 != c0) && (s1v < bestSSE || (s1v == bestSSE && c1 < bestIdx));
+    if (upd1) { bestSSE = s1v; bestIdx = c1; bestL = compv(Lv, 1); bestB = compv(Bv, 1); }
+    if (MODE == MODE_HW && (upd0 || upd1)) {
+#pragma unroll
+      for (int i = 0; i < K; ++i) mybest[i] = compv(s[i], upd1 ? 1 : 0);
+    }
+  }
+
+  // ---- arg-min across waves ---------------------------------------------------------
+  if (lane == 0) {
+    wbest[4 * w + 0] = bestSSE;
+    wbest[4 * w + 1] = __int_as_float(bestIdx);
+    wbest[4 * w + 2] = bestL;
+    wbest[4 * w + 3] = bestB;
+  }
+  __syncthreads();
+  int win = 0;
+  for (int i = 1; i < nwaves; ++i) {
+    const float si = wbest[4 * i], sw = wbest[4 * win];
+    const int ii = __float_as_int(wbest[4 * i + 1]), iw = __float_as_int(wbest[4 * win + 1]);
+    if (si < sw || (si == sw && ii < iw)) win = i;
+  }
+  const float gSSE = wbest[4 * win];
+  const int gIdx = __float_as_int(wbest[4 * win + 1]);
+  const float gL = wbest[4 * win + 2], gB = wbest[4 * win + 3];
+  const float sig = sqrtf(gSSE / fmaxf(n_valid, 1.f));
+  if (tid == 0) {
+    a.level[n] = gL;
+    a.trend[n] = gB;
+    a.sigma[n] = sig;
+    a.best[n] = gIdx;
+  }
+  const float* sfin = bests + (size_t)win * 64 * KP;  // [lane][KP]: phase p → (p/K, p%K)
+  if (MODE == MODE_HW && a.season_out) {
+    for (int p = tid; p < a.m; p += blockDim.x) a.season_out[(long long)n * a.m + p] = sfin[(p / K) * KP + p % K];
+  }
+  const int Tp = a.Tp, m = a.m;
+  detect_epilogue(a.det, n, sig, n_valid,
+                  [&](int h) {
+                    float f = gL + (float)h * gB;
+                    if (MODE == MODE_HW) {
+                      int ph = (Tp - 1 + h) % m;
+                      if (ph < 0) ph += m;
+                      f += sfin[(ph / K) * KP + ph % K];
+                    }
+                    return f;
+                  },
+                  red);
+}
+
+template <int K>
+static constexpr int kp_of(int bf16) {
+  return bf16 ? ((K + 7) / 8) * 8 : ((K + 3) / 4) * 4;
+}
+
+extern "C" size_t fm_hw_scan_lds_bytes(int Tp, int seg, int K, int mode, int bf16) {
+  int KP;
+  switch (K) {
+    case 8: KP = 8; break;
+    case 12: KP = bf16 ? 16 : 12; break;
+    case 16: KP = 16; break;
+    case 24: KP = 24; break;
+    case 32: KP = 32; break;
+    default: return (size_t)-1;
+  }
+  const int nseg = Tp / seg;
+  size_t off = ((size_t)nseg * 64 * KP * (bf16 ? 2 : 4) + 15) & ~(size_t)15;
+  if (mode == MODE_HW) off += (size_t)4 * 64 * KP * 4;
+  off += ((size_t)nseg * 4 + 15) & ~(size_t)15;
+  off += 64 * 4 + 16 * 4;
+  return off;
+}
+
+// variant: 0 = 1 combo/lane, >=3 waves/SIMD; 1 = 1 combo/lane, 2 waves/SIMD;
+//          2 = 2 combos/lane (packed FP32), 2 waves/SIMD
+template <int K, int MODE, int NC, int MINW>
+static hipError_t launch_v(const SmoothArgs& a, int bf16, size_t lds, hipStream_t st) {
+  if (bf16)
+    hipLaunchKernelGGL((hw_scan_kernel<K, MODE, bf16_t, NC, MINW>), dim3(a.N), dim3(256), lds, st, a);
+  else
+    hipLaunchKernelGGL((hw_scan_kernel<K, MODE, float, NC, MINW>), dim3(a.N), dim3(256), lds, st, a);
+  return hipGetLastError();
+}
+
+template <int K, int MODE>
+static hipError_t launch_fast(const SmoothArgs& a, int bf16, size_t lds, hipStream_t st, int variant) {
+  switch (variant) {
+    case 1: return launch_v<K, MODE, 1, 2>(a, bf16, lds, st);
+    case 2: return launch_v<K, MODE, 2, 2>(a, bf16, lds, st);
+    default: return launch_v<K, MODE, 1, 3>(a, bf16, lds, st);
+  }
+}
+
+template <int K, int MODE>
+static hipError_t launch_fast0(const SmoothArgs& a, int bf16, size_t lds, hipStream_t st, int) {
+  return launch_v<K, MODE, 1, 3>(a, bf16, lds, st);
+}
+
+// Returns hipErrorNotSupported when the geometry is not uniform (caller falls back).
+extern "C" int fm_hw_scan_fit(const SmoothArgs* a, int mode, int bf16, int variant, hipStream_t st) {
+  const int K = a->K;
+  if (a->seg % K != 0 || a->seg / K > 64 || a->Tp % a->seg != 0) return (int)hipErrorNotSupported;
+  const size_t lds = fm_hw_scan_lds_bytes(a->Tp, a->seg, K, mode, bf16);
+  if (lds == (size_t)-1 || lds > 64 * 1024) return (int)hipErrorNotSupported;
+  if (a->N <= 0) return 0;
+  hipError_t e = hipErrorNotSupported;
+  if (mode == MODE_HW) {
+    switch (K) {
+      case 8: e = launch_fast0<8, MODE_HW>(*a, bf16, lds, st, variant); break;
+      case 12: e = launch_fast0<12, MODE_HW>(*a, bf16, lds, st, variant); break;
+      case 16: e = launch_fast0<16, MODE_HW>(*a, bf16, lds, st, variant); break;
+      case 24: e = launch_fast<24, MODE_HW>(*a, bf16, lds, st, variant); break;
+      case 32: e = launch_fast0<32, MODE_HW>(*a, bf16, lds, st, variant); break;
+      default: return (int)hipErrorNotSupported;
+    }
+  } else if (K == 16) {
+    e = (mode == MODE_ES) ? launch_fast<16, MODE_ES>(*a, bf16, lds, st, variant)
+                          : launch_fast<16, MODE_DES>(*a, bf16, lds, st, variant);
+  } else {
+    return (int)hipErrorNotSupported;
+  }
+  return (int)e;
+}

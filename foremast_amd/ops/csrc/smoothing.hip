@@ -325,7 +325,22 @@ extern "C" size_t fm_smooth_lds_bytes(int Tp, int m, int seg, int bf16) {
   return off;
 }
 
-extern "C" int fm_smooth_fit(const SmoothArgs* a, int mode, int bf16, hipStream_t st) {
+extern "C" int fm_hw_scan_fit(const SmoothArgs* a, int mode, int bf16, int variant, hipStream_t st);
+
+// generic (guarded) path only
+extern "C" int fm_smooth_fit_generic(const SmoothArgs* a, int mode, int bf16, hipStream_t st);
+
+// variant < 0: generic kernel; otherwise try the uniform fast kernel first.
+extern "C" int fm_smooth_fit(const SmoothArgs* a, int mode, int bf16, int variant, hipStream_t st) {
+  if (a->N <= 0) return 0;
+  if (variant >= 0) {
+    const int e = fm_hw_scan_fit(a, mode, bf16, variant, st);
+    if (e != (int)hipErrorNotSupported) return e;
+  }
+  return fm_smooth_fit_generic(a, mode, bf16, st);
+}
+
+extern "C" int fm_smooth_fit_generic(const SmoothArgs* a, int mode, int bf16, hipStream_t st) {
   if (a->N <= 0) return 0;
   if (a->K < 1 || a->K > 32 || a->seg > 64 * a->K || a->Tp % a->seg != 0) return (int)hipErrorInvalidValue;
   const size_t lds = fm_smooth_lds_bytes(a->Tp, a->m, a->seg, bf16);

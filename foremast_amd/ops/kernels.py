@@ -9,6 +9,7 @@ HIP graph.
 
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Dict, Optional
 
@@ -122,11 +123,18 @@ def _hist_check(hist: torch.Tensor, head: int, length: int) -> None:
     _need(0 < length <= R, f"length {length} out of (0, {R}]")
 
 
+UNIFORM_K = (8, 12, 16, 24, 32)
+
+
 def smoothing_geometry(mode: int, T: int, m: int, K: Optional[int] = None):
-    """Return (Tp, pad, K, seg) for the smoothing kernel."""
+    """Return (Tp, pad, K, seg) for the smoothing kernel.  For Holt-Winters a K
+    that divides the season exactly (<= 64 lanes) selects the branch-free
+    uniform kernel (1440 = 60 x 24); otherwise K = ceil(m / 64) (guarded)."""
     if mode == MODE_HW:
         _need(m >= 2, "season must be >= 2")
-        k = (m + 63) // 64
+        k = next((c for c in UNIFORM_K if m % c == 0 and m // c <= 64), None) if K is None else K
+        if k is None:
+            k = (m + 63) // 64
         _need(k <= 32, f"season {m} too long for the register-resident kernel (max 2048)")
         seg = m
         Tp = ((T + m - 1) // m) * m
@@ -152,8 +160,8 @@ def smoothing_supported(mode: int, T: int, m: int, bf16: bool) -> bool:
 
 def smoothing_fit(hist: torch.Tensor, head: int, length: int, mode: int, m: int,
                   grid: torch.Tensor, det: DetectSpec, K: Optional[int] = None,
-                  want_season: bool = False, out: Optional[Dict[str, torch.Tensor]] = None
-                  ) -> Dict[str, torch.Tensor]:
+                  want_season: bool = False, out: Optional[Dict[str, torch.Tensor]] = None,
+                  variant: Optional[int] = None) -> Dict[str, torch.Tensor]:
     lib = nat.require()
     _hist_check(hist, head, length)
     dev = hist.device
@@ -165,8 +173,16 @@ def smoothing_fit(hist: torch.Tensor, head: int, length: int, mode: int, m: int,
     mm = m if mode == MODE_HW else 1
     Tp, pad, k, seg = smoothing_geometry(mode, length, mm, K)
     bf16 = hist.dtype == torch.bfloat16
-    lds = lib.fm_smooth_lds_bytes(Tp, mm, seg, int(bf16))
-    _need(lds <= LDS_LIMIT, f"series too long for LDS staging ({lds} bytes)")
+    if variant is None:
+        variant = int(os.environ.get("FOREMAST_HW_VARIANT", "0"))
+    fast_lds = lib.fm_hw_scan_lds_bytes(Tp, seg, k, int(mode), int(bf16))
+    if variant >= 0 and not (seg % k == 0 and seg // k <= 64 and fast_lds <= LDS_LIMIT):
+        variant = -1
+    if variant < 0:
+        if mode == MODE_HW and k not in (8, 16, 24, 32):
+            k = (mm + 63) // 64
+        lds = lib.fm_smooth_lds_bytes(Tp, mm, seg, int(bf16))
+        _need(lds <= LDS_LIMIT, f"series too long for LDS staging ({lds} bytes)")
     out = {} if out is None else out
     f32 = dict(dtype=torch.float32, device=dev)
     for kname in ("level", "trend", "sigma"):
@@ -196,7 +212,7 @@ def smoothing_fit(hist: torch.Tensor, head: int, length: int, mode: int, m: int,
     a.best = nat.ptr(out["best"])
     a.season_out = nat.ptr(out.get("season")) if (want_season and mode == MODE_HW) else 0
     _fill_detect(a.det, det, N, dev, out)
-    nat.check(lib.fm_smooth_fit(a, int(mode), int(bf16), nat.stream_handle(dev)), "fm_smooth_fit")
+    nat.check(lib.fm_smooth_fit(a, int(mode), int(bf16), int(variant), nat.stream_handle(dev)), "fm_smooth_fit")
     return out
 
 

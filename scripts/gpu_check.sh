@@ -20,6 +20,7 @@ for s in $STEPS; do
     tests) run gpu_tests 900 python -m pytest tests -m gpu -x -q ;;
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
+    kbench) run kbench 600 python scripts/bench_kernels.py ;;
     prof)
       export TMPDIR=/tmp
       run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof" -o run -- python3 "$PWD/bench.py" --steps 5 --warmup 2 ;;
