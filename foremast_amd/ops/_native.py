@@ -46,7 +46,7 @@ class SmoothArgs(C.Structure):
         ("hist", P), ("ld", LL), ("ring_len", I), ("head", I), ("T", I), ("Tp", I),
         ("pad", I), ("m", I), ("K", I), ("seg", I), ("grid", P), ("G", I), ("N", I),
         ("level", P), ("trend", P), ("sigma", P), ("best", P), ("season_out", P),
-        ("det", DetectArgs),
+        ("pair_tab", P), ("det", DetectArgs),
     ]
 
 

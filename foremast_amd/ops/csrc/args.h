@@ -46,6 +46,7 @@ struct SmoothArgs {
   float* sigma;         // [N]
   int* best;            // [N]
   float* season_out;    // [N, m] or null
+  const float* pair_tab;  // per combo-pair precomputed table (hw_scan variant 3) or null
   DetectArgs det;
 };
 

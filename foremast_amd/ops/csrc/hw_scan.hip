@@ -128,36 +128,40 @@ struct YRegs {
   }
 };
 
+// State in (f, b) coordinates: f = level + trend (the one-step forecast),
+// b = trend.  Update:  e = u - f;  f' = (f + b) + c1 e;  b' = b + c2 e  with
+// c1 = alpha (1 + beta), c2 = alpha beta — a 2-deep dependency per step
+// (t = f + b issues beside e = u - f).
 template <int K, typename Y, typename V>
-__device__ __forceinline__ void pass1_fast(const Y& y, const V* s, V al, V ab, V& v1, V& v2) {
+__device__ __forceinline__ void pass1_fast(const Y& y, const V* s, V c1, V c2, V& v1, V& v2) {
   v1 = splatv<V>(0.f);
   v2 = splatv<V>(0.f);
 #pragma unroll
   for (int i = 0; i < K; ++i) {
     const V t = v1 + v2;
-    const V e = (splatv<V>(y.get(i)) - s[i]) - t;
-    v1 = t + al * e;
-    v2 = v2 + ab * e;
+    const V e = (splatv<V>(y.get(i)) - s[i]) - v1;
+    v1 = t + c1 * e;
+    v2 = v2 + c2 * e;
   }
 }
 
 // general local map (segment contains NaN): NaN steps are x' = [[1,1],[0,1]] x
 template <int K, typename Y, typename V>
-__device__ __forceinline__ void pass1_slow(const Y& y, const V* s, V al, V ab, V oma, V omab, Aff<V>& a) {
+__device__ __forceinline__ void pass1_slow(const Y& y, const V* s, V c1, V c2, Aff<V>& a) {
   const V one = splatv<V>(1.f), zero = splatv<V>(0.f);
+  const V omc1 = one - c1;
   a.m11 = one; a.m12 = zero; a.m21 = zero; a.m22 = one; a.v1 = zero; a.v2 = zero;
 #pragma unroll
   for (int i = 0; i < K; ++i) {
     const float yi = y.get(i);
     const bool ok = (yi == yi);
-    const V a11 = ok ? oma : one;
-    const V a21 = ok ? -ab : zero;
-    const V a22 = ok ? omab : one;
+    const V a11 = ok ? omc1 : one;  // a12 = a22 = 1
+    const V a21 = ok ? -c2 : zero;
     const V u = ok ? (splatv<V>(yi) - s[i]) : zero;
-    const V n11 = a11 * (a.m11 + a.m21), n12 = a11 * (a.m12 + a.m22);
-    const V n21 = a21 * a.m11 + a22 * a.m21, n22 = a21 * a.m12 + a22 * a.m22;
-    const V nv1 = a11 * (a.v1 + a.v2) + (ok ? al * u : zero);
-    const V nv2 = a21 * a.v1 + a22 * a.v2 + (ok ? ab * u : zero);
+    const V n11 = a11 * a.m11 + a.m21, n12 = a11 * a.m12 + a.m22;
+    const V n21 = a21 * a.m11 + a.m21, n22 = a21 * a.m12 + a.m22;
+    const V nv1 = a11 * a.v1 + a.v2 + (ok ? c1 * u : zero);
+    const V nv2 = a21 * a.v1 + a.v2 + (ok ? c2 * u : zero);
     a.m11 = n11; a.m12 = n12; a.m21 = n21; a.m22 = n22; a.v1 = nv1; a.v2 = nv2;
   }
 }
@@ -165,32 +169,128 @@ __device__ __forceinline__ void pass1_slow(const Y& y, const V* s, V al, V ab, V
 // pass 2 of this segment (true start state x1/x2), optionally fused with the
 // fast pass 1 of the next segment.
 template <int K, int MODE, bool MASK, bool FUSE, typename Y, typename V>
-__device__ __forceinline__ void pass2(const Y& y, const Y& yn, V* s, V al, V ab, V g1a, V& x1, V& x2, V& sse,
+__device__ __forceinline__ void pass2(const Y& y, const Y& yn, V* s, V c1, V c2, V g1a, V& x1, V& x2, V& sse,
                                       V& p1, V& p2) {
   if (FUSE) { p1 = splatv<V>(0.f); p2 = splatv<V>(0.f); }
 #pragma unroll
   for (int i = 0; i < K; ++i) {
     const V t = x1 + x2;
     const float yi = y.get(i);
-    V e = (splatv<V>(yi) - s[i]) - t;
+    V e = (splatv<V>(yi) - s[i]) - x1;
     if (MASK) e = (yi == yi) ? e : splatv<V>(0.f);
-    x1 = t + al * e;
-    x2 = x2 + ab * e;
+    x1 = t + c1 * e;
+    x2 = x2 + c2 * e;
     if (MODE == MODE_HW) s[i] = s[i] + g1a * e;
     sse = sse + e * e;
     if (FUSE) {
       const V tn = p1 + p2;
-      const V en = (splatv<V>(yn.get(i)) - s[i]) - tn;
-      p1 = tn + al * en;
-      p2 = p2 + ab * en;
+      const V en = (splatv<V>(yn.get(i)) - s[i]) - p1;
+      p1 = tn + c1 * en;
+      p2 = p2 + c2 * en;
     }
+  }
+}
+
+
+// ---- table-driven fast path (variant 3) ---------------------------------------------
+// Per combo pair the host precomputes (float, [combo0, combo1] interleaved):
+//   [0..5]            c1, c2, g1a
+//   [6 .. 6+4K)       W_i = A^(K-1-i) c  as (W1_i, W2_i) pairs   (pass-1 weights)
+//   [6+4K .. +40)     B^1, B^2, B^4, B^8, B^16 (B = A^K), each m11 m12 m21 m22
+// so pass 1 is  v = sum_i W_i u_i  (3 ops/step) and the cross-lane scan only
+// carries the state vector with wave-uniform matrices.
+template <int K>
+struct PairTab {
+  static constexpr int W0 = 6;
+  static constexpr int B0 = 6 + 4 * K;
+  static constexpr int SIZE = ((B0 + 40) + 15) / 16 * 16;
+};
+
+__device__ __forceinline__ v2f ldv2(const float* p) { return *(const v2f*)p; }
+
+struct Mat2 { v2f a, b, c, d; };
+__device__ __forceinline__ Mat2 ldmat(const float* p) {
+  Mat2 m; m.a = ldv2(p); m.b = ldv2(p + 2); m.c = ldv2(p + 4); m.d = ldv2(p + 6); return m;
+}
+__device__ __forceinline__ void matvec(const Mat2& m, v2f x1, v2f x2, v2f& y1, v2f& y2) {
+  y1 = m.a * x1 + m.b * x2;
+  y2 = m.c * x1 + m.d * x2;
+}
+__device__ __forceinline__ Mat2 matmul(const Mat2& p, const Mat2& q) {
+  Mat2 r;
+  r.a = p.a * q.a + p.b * q.c; r.b = p.a * q.b + p.b * q.d;
+  r.c = p.c * q.a + p.d * q.c; r.d = p.c * q.b + p.d * q.d;
+  return r;
+}
+
+template <int CTRL>
+__device__ __forceinline__ void row_round(v2f& w1, v2f& w2, const Mat2& Bd) {
+  const v2f q1 = dpp2<CTRL, 0xf>(0.f, w1);
+  const v2f q2 = dpp2<CTRL, 0xf>(0.f, w2);
+  w1 = w1 + Bd.a * q1 + Bd.b * q2;
+  w2 = w2 + Bd.c * q1 + Bd.d * q2;
+}
+
+// Exclusive scan of X_j = B X_{j-1} + v_j over lanes (X_{-1} = x0); returns the
+// start state of this lane.  Bj = B^(lane & 15) (per lane, precomputed).
+__device__ __forceinline__ void uniform_exclusive_scan(const float* tab_b, v2f v1, v2f v2, v2f x01, v2f x02,
+                                                       const Mat2& Bj, int lane, v2f& s1, v2f& s2) {
+  const Mat2 B1 = ldmat(tab_b), B2 = ldmat(tab_b + 8), B4 = ldmat(tab_b + 16), B8 = ldmat(tab_b + 24),
+             B16 = ldmat(tab_b + 32);
+  // within-row exclusive prefix
+  v2f w1 = dpp2<0x111, 0xf>(0.f, v1);
+  v2f w2 = dpp2<0x111, 0xf>(0.f, v2);
+  row_round<0x111>(w1, w2, B1);
+  row_round<0x112>(w1, w2, B2);
+  row_round<0x114>(w1, w2, B4);
+  row_round<0x118>(w1, w2, B8);
+  // row-end states from zero: E = B w + v at lanes 15, 31, 47
+  v2f e1, e2;
+  matvec(B1, w1, w2, e1, e2);
+  e1 = e1 + v1;
+  e2 = e2 + v2;
+  v2f Y01 = x01, Y02 = x02, t1, t2;
+  const int row = lane >> 4;
+  v2f p1 = x01, p2 = x02;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const v2f E1 = rdlanev(e1, 16 * r + 15), E2 = rdlanev(e2, 16 * r + 15);
+    matvec(B16, Y01, Y02, t1, t2);
+    Y01 = t1 + E1;
+    Y02 = t2 + E2;
+    if (row == r + 1) { p1 = Y01; p2 = Y02; }
+  }
+  matvec(Bj, p1, p2, s1, s2);
+  s1 = s1 + w1;
+  s2 = s2 + w2;
+}
+
+template <int K, int MODE, bool MASK, typename Y>
+__device__ __forceinline__ void pass2_tab(const Y& y, const Y& yn, v2f* s, v2f c1, v2f c2, v2f g1a,
+                                          const float* W, v2f& x1, v2f& x2, v2f& sse, v2f& p1, v2f& p2) {
+  p1 = splat2(0.f);
+  p2 = splat2(0.f);
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    const v2f t = x1 + x2;
+    const float yi = y.get(i);
+    v2f e = (splat2(yi) - s[i]) - x1;
+    if (MASK) e = (yi == yi) ? e : splat2(0.f);
+    x1 = t + c1 * e;
+    x2 = x2 + c2 * e;
+    if (MODE == MODE_HW) s[i] = s[i] + g1a * e;
+    sse = sse + e * e;
+    const v2f un = splat2(yn.get(i)) - s[i];
+    p1 = p1 + ldv2(W + 4 * i) * un;
+    p2 = p2 + ldv2(W + 4 * i + 2) * un;
   }
 }
 
 }  // namespace
 
-template <int K, int MODE, typename TIN, int NC, int MINW>
+template <int K, int MODE, typename TIN, int NC, int MINW, bool TAB = false>
 __global__ __launch_bounds__(256, MINW) void hw_scan_kernel(const SmoothArgs a) {
+  static_assert(!TAB || NC == 2, "table path is packed-pair only");
   using V = typename std::conditional<NC == 2, v2f, float>::type;
   using YR = YRegs<TIN, K>;
   constexpr int KP = YR::KP;
@@ -286,25 +386,39 @@ __global__ __launch_bounds__(256, MINW) void hw_scan_kernel(const SmoothArgs a) 
 
   for (int pi = w; pi < npairs; pi += nwaves) {
     const int c0 = NC * pi;
-    const int c1 = (NC == 2 && NC * pi + 1 < a.G) ? NC * pi + 1 : c0;
+    const int c1i = (NC == 2 && NC * pi + 1 < a.G) ? NC * pi + 1 : c0;
     V al, be, ga;
     if constexpr (NC == 2) {
-      al.x = a.grid[3 * c0 + 0]; al.y = a.grid[3 * c1 + 0];
-      be.x = a.grid[3 * c0 + 1]; be.y = a.grid[3 * c1 + 1];
-      ga.x = a.grid[3 * c0 + 2]; ga.y = a.grid[3 * c1 + 2];
+      al.x = a.grid[3 * c0 + 0]; al.y = a.grid[3 * c1i + 0];
+      be.x = a.grid[3 * c0 + 1]; be.y = a.grid[3 * c1i + 1];
+      ga.x = a.grid[3 * c0 + 2]; ga.y = a.grid[3 * c1i + 2];
     } else {
       al = a.grid[3 * c0 + 0]; be = a.grid[3 * c0 + 1]; ga = a.grid[3 * c0 + 2];
     }
     const V one = splatv<V>(1.f), zero = splatv<V>(0.f);
-    const V ab = al * be, oma = one - al, omab = one - ab, g1a = ga * oma;
+    const V c2 = al * be, c1 = al + c2, g1a = ga * (one - al), omc1 = one - c1;
+    const float* tab = nullptr;
+    Mat2 Bj;
+    if constexpr (TAB) {
+      tab = a.pair_tab + (size_t)__builtin_amdgcn_readfirstlane(pi) * PairTab<K>::SIZE;
+      // Bj = B^(lane & 15) by binary powering
+      const float* tb = tab + PairTab<K>::B0;
+      Bj.a = one; Bj.b = zero; Bj.c = zero; Bj.d = one;
+#pragma unroll
+      for (int bit = 0; bit < 4; ++bit) {
+        const Mat2 Bb = ldmat(tb + 8 * bit);
+        const Mat2 r = matmul(Bj, Bb);
+        if ((lane >> bit) & 1) Bj = r;
+      }
+    }
 
-    // A^K for a full NaN-free lane chunk
+    // A'^K for a full NaN-free lane chunk, A' = [[1-c1, 1], [-c2, 1]]
     Aff<V> P;
     P.m11 = one; P.m12 = zero; P.m21 = zero; P.m22 = one;
 #pragma unroll
     for (int i = 0; i < K; ++i) {
-      const V n11 = oma * (P.m11 + P.m21), n12 = oma * (P.m12 + P.m22);
-      const V n21 = omab * P.m21 - ab * P.m11, n22 = omab * P.m22 - ab * P.m12;
+      const V n11 = omc1 * P.m11 + P.m21, n12 = omc1 * P.m12 + P.m22;
+      const V n21 = P.m21 - c2 * P.m11, n22 = P.m22 - c2 * P.m12;
       P.m11 = n11; P.m12 = n12; P.m21 = n21; P.m22 = n22;
     }
 
@@ -319,7 +433,7 @@ __global__ __launch_bounds__(256, MINW) void hw_scan_kernel(const SmoothArgs a) 
         s[i] = splatv<V>((MODE == MODE_HW && y == y) ? y - l0 : 0.f);
       }
     }
-    V Lv = splatv<V>(l0), Bv = splatv<V>(b0), sse = zero;
+    V Lv = splatv<V>(l0 + b0), Bv = splatv<V>(b0), sse = zero;  // (f, b)
 
     // prologue: pass 1 of the first fitted segment
     YR ycur, ynext;
@@ -327,29 +441,49 @@ __global__ __launch_bounds__(256, MINW) void hw_scan_kernel(const SmoothArgs a) 
     Aff<V> loc;
     bool locfast = !segnan[sgA];
     if (locfast) {
-      pass1_fast<K>(ycur, s, al, ab, loc.v1, loc.v2);
+      if constexpr (TAB) {
+        loc.v1 = zero; loc.v2 = zero;
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+          const V un = splatv<V>(ycur.get(i)) - s[i];
+          loc.v1 = loc.v1 + ldv2(tab + PairTab<K>::W0 + 4 * i) * un;
+          loc.v2 = loc.v2 + ldv2(tab + PairTab<K>::W0 + 4 * i + 2) * un;
+        }
+      } else {
+        pass1_fast<K>(ycur, s, c1, c2, loc.v1, loc.v2);
+      }
     } else {
-      pass1_slow<K>(ycur, s, al, ab, oma, omab, loc);
+      pass1_slow<K>(ycur, s, c1, c2, loc);
     }
 
     for (int sg = sgA; sg < nseg; ++sg) {
-      if (locfast) { loc.m11 = P.m11; loc.m12 = P.m12; loc.m21 = P.m21; loc.m22 = P.m22; }
-      wave_exclusive_scan(loc);
-      V x1 = loc.m11 * Lv + loc.m12 * Bv + loc.v1;
-      V x2 = loc.m21 * Lv + loc.m22 * Bv + loc.v2;
+      V x1, x2;
+      if (TAB && locfast) {
+        if constexpr (TAB) uniform_exclusive_scan(tab + PairTab<K>::B0, loc.v1, loc.v2, Lv, Bv, Bj, lane, x1, x2);
+      } else {
+        if (locfast) { loc.m11 = P.m11; loc.m12 = P.m12; loc.m21 = P.m21; loc.m22 = P.m22; }
+        wave_exclusive_scan(loc);
+        x1 = loc.m11 * Lv + loc.m12 * Bv + loc.v1;
+        x2 = loc.m21 * Lv + loc.m22 * Bv + loc.v2;
+      }
       const bool has_next = sg + 1 < nseg;
       if (has_next) ynext.load(ys + ((size_t)(sg + 1) * 64 + lane) * KP);
       const bool mask = segnan[sg] != 0;
       const bool next_fast = has_next && !segnan[sg + 1];
       if (next_fast) {
-        if (mask) pass2<K, MODE, true, true>(ycur, ynext, s, al, ab, g1a, x1, x2, sse, loc.v1, loc.v2);
-        else pass2<K, MODE, false, true>(ycur, ynext, s, al, ab, g1a, x1, x2, sse, loc.v1, loc.v2);
+        if constexpr (TAB) {
+          if (mask) pass2_tab<K, MODE, true>(ycur, ynext, s, c1, c2, g1a, tab + PairTab<K>::W0, x1, x2, sse, loc.v1, loc.v2);
+          else pass2_tab<K, MODE, false>(ycur, ynext, s, c1, c2, g1a, tab + PairTab<K>::W0, x1, x2, sse, loc.v1, loc.v2);
+        } else {
+          if (mask) pass2<K, MODE, true, true>(ycur, ynext, s, c1, c2, g1a, x1, x2, sse, loc.v1, loc.v2);
+          else pass2<K, MODE, false, true>(ycur, ynext, s, c1, c2, g1a, x1, x2, sse, loc.v1, loc.v2);
+        }
         locfast = true;
       } else {
         V d1, d2;
-        if (mask) pass2<K, MODE, true, false>(ycur, ynext, s, al, ab, g1a, x1, x2, sse, d1, d2);
-        else pass2<K, MODE, false, false>(ycur, ynext, s, al, ab, g1a, x1, x2, sse, d1, d2);
-        if (has_next) pass1_slow<K>(ynext, s, al, ab, oma, omab, loc);
+        if (mask) pass2<K, MODE, true, false>(ycur, ynext, s, c1, c2, g1a, x1, x2, sse, d1, d2);
+        else pass2<K, MODE, false, false>(ycur, ynext, s, c1, c2, g1a, x1, x2, sse, d1, d2);
+        if (has_next) pass1_slow<K>(ynext, s, c1, c2, loc);
         locfast = false;
       }
       Lv = rdlanev(x1, L - 1);
@@ -360,9 +494,9 @@ __global__ __launch_bounds__(256, MINW) void hw_scan_kernel(const SmoothArgs a) 
     sse = wave_sumv(sse);
     const float s0v = compv(sse, 0), s1v = compv(sse, 1);
     bool upd0 = (s0v < bestSSE || (s0v == bestSSE && c0 < bestIdx));
-    if (upd0) { bestSSE = s0v; bestIdx = c0; bestL = compv(Lv, 0); bestB = compv(Bv, 0); }
-    const bool upd1 = (c1 != c0) && (s1v < bestSSE || (s1v == bestSSE && c1 < bestIdx));
-    if (upd1) { bestSSE = s1v; bestIdx = c1; bestL = compv(Lv, 1); bestB = compv(Bv, 1); }
+    if (upd0) { bestSSE = s0v; bestIdx = c0; bestL = compv(Lv, 0) - compv(Bv, 0); bestB = compv(Bv, 0); }
+    const bool upd1 = (c1i != c0) && (s1v < bestSSE || (s1v == bestSSE && c1i < bestIdx));
+    if (upd1) { bestSSE = s1v; bestIdx = c1i; bestL = compv(Lv, 1) - compv(Bv, 1); bestB = compv(Bv, 1); }
     if (MODE == MODE_HW && (upd0 || upd1)) {
 #pragma unroll
       for (int i = 0; i < K; ++i) mybest[i] = compv(s[i], upd1 ? 1 : 0);
@@ -436,12 +570,12 @@ extern "C" size_t fm_hw_scan_lds_bytes(int Tp, int seg, int K, int mode, int bf1
 
 // variant: 0 = 1 combo/lane, >=3 waves/SIMD; 1 = 1 combo/lane, 2 waves/SIMD;
 //          2 = 2 combos/lane (packed FP32), 2 waves/SIMD
-template <int K, int MODE, int NC, int MINW>
+template <int K, int MODE, int NC, int MINW, bool TAB = false>
 static hipError_t launch_v(const SmoothArgs& a, int bf16, size_t lds, hipStream_t st) {
   if (bf16)
-    hipLaunchKernelGGL((hw_scan_kernel<K, MODE, bf16_t, NC, MINW>), dim3(a.N), dim3(256), lds, st, a);
+    hipLaunchKernelGGL((hw_scan_kernel<K, MODE, bf16_t, NC, MINW, TAB>), dim3(a.N), dim3(256), lds, st, a);
   else
-    hipLaunchKernelGGL((hw_scan_kernel<K, MODE, float, NC, MINW>), dim3(a.N), dim3(256), lds, st, a);
+    hipLaunchKernelGGL((hw_scan_kernel<K, MODE, float, NC, MINW, TAB>), dim3(a.N), dim3(256), lds, st, a);
   return hipGetLastError();
 }
 
@@ -450,6 +584,9 @@ static hipError_t launch_fast(const SmoothArgs& a, int bf16, size_t lds, hipStre
   switch (variant) {
     case 1: return launch_v<K, MODE, 1, 2>(a, bf16, lds, st);
     case 2: return launch_v<K, MODE, 2, 2>(a, bf16, lds, st);
+    case 3:
+      if (!a.pair_tab) return hipErrorInvalidValue;
+      return launch_v<K, MODE, 2, 2, true>(a, bf16, lds, st);
     default: return launch_v<K, MODE, 1, 3>(a, bf16, lds, st);
   }
 }

@@ -147,6 +147,57 @@ def smoothing_geometry(mode: int, T: int, m: int, K: Optional[int] = None):
     return Tp, Tp - T, k, seg
 
 
+_PAIR_TAB_CACHE: Dict[tuple, torch.Tensor] = {}
+
+
+def pair_table(grid: torch.Tensor, K: int) -> torch.Tensor:
+    """Per combo-pair precomputed table for the table-driven HW kernel
+    (hw_scan.hip ``PairTab``): c1, c2, g1a; pass-1 weights W_i = A^(K-1-i) c;
+    B^1, B^2, B^4, B^8, B^16 with B = A^K — all in (forecast, trend)
+    coordinates, A = [[1-c1, 1], [-c2, 1]], c = (c1, c2), computed in float64."""
+    key = (grid.data_ptr(), tuple(grid.shape), K, grid.device)
+    t = _PAIR_TAB_CACHE.get(key)
+    if t is not None:
+        return t
+    import numpy as np
+    g = grid.detach().cpu().double().numpy()
+    G = g.shape[0]
+    npairs = (G + 1) // 2
+    size = ((6 + 4 * K + 40) + 15) // 16 * 16
+    tab = np.zeros((npairs, size), dtype=np.float64)
+    for p in range(npairs):
+        for comp, ci in enumerate((2 * p, 2 * p + 1 if 2 * p + 1 < G else 2 * p)):
+            al, be, ga = g[ci]
+            c2 = al * be
+            c1 = al + c2
+            A = np.array([[1 - c1, 1.0], [-c2, 1.0]])
+            c = np.array([c1, c2])
+            tab[p, 0 + comp] = c1
+            tab[p, 2 + comp] = c2
+            tab[p, 4 + comp] = ga * (1 - al)
+            Ap = np.eye(2)
+            pows = [np.eye(2)]
+            for _ in range(K):
+                Ap = A @ Ap
+                pows.append(Ap)
+            for i in range(K):
+                Wi = pows[K - 1 - i] @ c
+                tab[p, 6 + 4 * i + comp] = Wi[0]
+                tab[p, 6 + 4 * i + 2 + comp] = Wi[1]
+            B = pows[K]
+            Bp = B
+            for r in range(5):
+                base = 6 + 4 * K + 8 * r
+                for q, v in enumerate((Bp[0, 0], Bp[0, 1], Bp[1, 0], Bp[1, 1])):
+                    tab[p, base + 2 * q + comp] = v
+                Bp = Bp @ Bp
+    t = torch.tensor(tab, dtype=torch.float32, device=grid.device).contiguous()
+    if len(_PAIR_TAB_CACHE) > 64:
+        _PAIR_TAB_CACHE.clear()
+    _PAIR_TAB_CACHE[key] = t
+    return t
+
+
 def smoothing_supported(mode: int, T: int, m: int, bf16: bool) -> bool:
     try:
         Tp, _, k, seg = smoothing_geometry(mode, T, m)
@@ -174,7 +225,7 @@ def smoothing_fit(hist: torch.Tensor, head: int, length: int, mode: int, m: int,
     Tp, pad, k, seg = smoothing_geometry(mode, length, mm, K)
     bf16 = hist.dtype == torch.bfloat16
     if variant is None:
-        variant = int(os.environ.get("FOREMAST_HW_VARIANT", "0"))
+        variant = int(os.environ.get("FOREMAST_HW_VARIANT", "3"))
     fast_lds = lib.fm_hw_scan_lds_bytes(Tp, seg, k, int(mode), int(bf16))
     if variant >= 0 and not (seg % k == 0 and seg // k <= 64 and fast_lds <= LDS_LIMIT):
         variant = -1
@@ -211,6 +262,7 @@ def smoothing_fit(hist: torch.Tensor, head: int, length: int, mode: int, m: int,
     a.sigma = nat.ptr(out["sigma"])
     a.best = nat.ptr(out["best"])
     a.season_out = nat.ptr(out.get("season")) if (want_season and mode == MODE_HW) else 0
+    a.pair_tab = nat.ptr(pair_table(grid, k)) if variant == 3 else 0
     _fill_detect(a.det, det, N, dev, out)
     nat.check(lib.fm_smooth_fit(a, int(mode), int(bf16), int(variant), nat.stream_handle(dev)), "fm_smooth_fit")
     return out

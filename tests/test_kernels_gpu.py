@@ -58,7 +58,7 @@ def _det_spec(K, N, C, dev, cur=None, thr=2.0, bound=3):
     (sm_ref.MODE_DES, 1, 2500, 0.01),
 ])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("variant", [-1, 0, 2])
+@pytest.mark.parametrize("variant", [-1, 0, 2, 3])
 def test_smoothing_kernel_matches_reference(K, mode, m, T, nan, dtype, variant):
     dev = torch.device("cuda:0")
     N, C = 48, 12
@@ -96,7 +96,7 @@ def test_smoothing_kernel_matches_reference(K, mode, m, T, nan, dtype, variant):
     assert torch.equal(d.verdict, out["verdict"].cpu())
 
 
-@pytest.mark.parametrize("variant", [-1, 0, 1, 2])
+@pytest.mark.parametrize("variant", [-1, 0, 1, 2, 3])
 def test_smoothing_kernel_flagship_shape(K, variant):
     """T = 10080 (7 days at 60 s), season 1440 (daily), bf16 ring."""
     dev = torch.device("cuda:0")
