@@ -4,10 +4,10 @@ latency on the 100k-series canary (BASELINE.json).
 
 One scoring tick = the full canary pipeline for every series of the job:
 
-  1. ingest: this tick's per-pod points arrive in pinned host memory (as the
-     Prometheus ingest would deliver them), are copied H2D and streamed into
-     the HBM rings (K10: new points in, oldest current points graduate into
-     the sliding 7-day history);
+  1. ingest: this tick's canary-pod and baseline-pod points arrive in pinned
+     host memory (as the Prometheus ingest would deliver them), are copied
+     H2D and streamed into the HBM rings (K10: new points in, oldest current
+     points graduate into the sliding 7-day history);
   2. pairwise canary test: baseline vs current Mann-Whitney U + Wilcoxon +
      Kruskal (ML_PAIRWISE_ALGORITHM=ALL), per series (K5/K11);
   3. model: additive Holt-Winters (daily season, 60 s step, 7-day window =
@@ -141,31 +141,32 @@ def main():
     shard.load_history(hist)
     W, P = args.window, args.pods
     total_ticks = args.warmup + args.steps
-    ticks = make_ticks(n_local, P, total_ticks + W, args.season, args.ring, dev, 99 + rank,
+    # per tick: P canary-pod values (a fraction of series regressed) and P
+    # baseline-pod values (healthy, same times) -> [ticks, N, 2P]
+    cur_t = make_ticks(n_local, P, total_ticks + W, args.season, args.ring, dev, 99 + rank,
                        args.anomaly_frac, hist)
-    # baseline pods: same times as the first current window, healthy, own noise
-    clean = make_ticks(n_local, P, W, args.season, args.ring, dev, 7 + rank, 0.0, hist)
-    shard.set_baseline(clean.permute(1, 2, 0).reshape(n_local, P * W))
-    del clean
-    del hist
+    base_t = make_ticks(n_local, P, total_ticks + W, args.season, args.ring, dev, 7 + rank, 0.0, hist)
+    ticks = torch.cat([cur_t, base_t], 2)
+    del cur_t, base_t, hist
     pin = dev.type == "cuda"
     host_ticks = ticks.cpu()
     if pin:
         host_ticks = host_ticks.pin_memory()
     del ticks
-    newv = torch.empty((n_local, P), dtype=torch.float32, device=dev)
+    newvb = torch.empty((n_local, 2 * P), dtype=torch.float32, device=dev)
+    newv, newb = newvb[:, :P], newvb[:, P:]
     agg = HealthAggregator(n_local, per, dev)
     health_host = torch.empty_like(shard.app_stats, device="cpu")
     if pin:
         health_host = health_host.pin_memory()
     # prefill the current window so every tick scores a full 10-minute window
     for k in range(W):
-        newv.copy_(host_ticks[k], non_blocking=pin)
-        shard.ingest_tick(newv)
+        newvb.copy_(host_ticks[k], non_blocking=pin)
+        shard.ingest_tick(newv, newb)
 
     def tick(k):
-        newv.copy_(host_ticks[W + k], non_blocking=pin)
-        shard.ingest_tick(newv)
+        newvb.copy_(host_ticks[W + k], non_blocking=pin)
+        shard.ingest_tick(newv, newb)
         out = shard.score()
         stats, _ = agg.tick(shard.app_stats, out["verdict"])
         health_host.copy_(stats, non_blocking=pin)

@@ -103,15 +103,21 @@ class StreamingShard:
         else:
             self.horizons.copy_(torch.from_numpy(h))
 
-    def ingest_tick(self, newv: torch.Tensor) -> None:
-        """``newv``: ``[N, P]`` float32 on the shard's device."""
+    def ingest_tick(self, newv: torch.Tensor, newb: Optional[torch.Tensor] = None) -> None:
+        """``newv``: ``[N, P]`` float32 current-pod values on the shard's device;
+        ``newb`` (optional, same shape): baseline-pod values streamed into the
+        baseline window at the same slot (continuous canary)."""
         graduate = self.cur.ticks >= self.cur.W
         if self.gpu:
             from ..ops import kernels as K
             K.tick_ingest(self.hist.data, self.hist.next_col(), self.cur.data, self.cur.P, self.cur.W,
-                          self.cur.slot(), newv, graduate=graduate)
+                          self.cur.slot(), newv, graduate=graduate,
+                          base=self.base if newb is not None else None, newb=newb)
             self.cur.ticks += 1
         else:
+            if newb is not None:
+                cols = torch.arange(self.cur.P, device=self.device) * self.cur.W + self.cur.slot()
+                self.base[:, cols] = newb.float()
             old = self.cur.push_(newv)
             if graduate:
                 self.hist.data[:, self.hist.next_col()] = old.to(self.hist.data.dtype)

@@ -1,0 +1,156 @@
+"""Python binding of the native Prometheus matrix decoder (``csrc/prom_parse.cpp``).
+
+``parse_matrix(body)`` → list of ``(labels, ts, values)``;
+``parse_dense(body, start, step, T, out, row0)`` scatters straight into a
+dense float32 matrix (e.g. a pinned host staging buffer for the GPU ring).
+Falls back to ``json`` when the native library cannot be built (no g++).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+import shutil
+import subprocess
+import threading
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "csrc", "prom_parse.cpp")
+LIBDIR = os.path.join(HERE, "_lib")
+LIB = os.path.join(LIBDIR, "libforemast_ingest.so")
+
+_lock = threading.Lock()
+_lib: Optional[C.CDLL] = None
+
+
+class ParseError(ValueError):
+    pass
+
+
+def build(verbose: bool = False) -> str:
+    os.makedirs(LIBDIR, exist_ok=True)
+    if os.path.exists(LIB) and os.path.getmtime(LIB) >= os.path.getmtime(SRC):
+        return LIB
+    cxx = os.environ.get("CXX") or shutil.which("g++") or shutil.which("clang++")
+    if not cxx:
+        raise RuntimeError("no C++ compiler for the ingest parser")
+    cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-o", LIB + ".tmp", SRC]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"ingest parser build failed:\n{r.stderr}")
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+def _load() -> Optional[C.CDLL]:
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        try:
+            build()
+            lib = C.CDLL(LIB)
+        except (RuntimeError, OSError):
+            return None
+        LL, P = C.c_longlong, C.c_void_p
+        lib.fm_prom_scan.argtypes = [C.c_char_p, LL, LL, P, P, P, P]
+        lib.fm_prom_scan.restype = LL
+        lib.fm_prom_fill.argtypes = [C.c_char_p, LL, P, P, LL]
+        lib.fm_prom_fill.restype = LL
+        lib.fm_prom_dense.argtypes = [C.c_char_p, LL, C.c_double, C.c_double, LL, P, LL, LL, LL, P]
+        lib.fm_prom_dense.restype = LL
+        _lib = lib
+        return lib
+
+
+def available() -> bool:
+    return _load() is not None
+
+
+def _check_status(body: bytes) -> None:
+    head = body[:256]
+    if b'"status"' in head and b'"error"' in head and b'"success"' not in head:
+        try:
+            d = json.loads(body)
+            raise ParseError(d.get("error", "prometheus error"))
+        except ValueError:
+            raise ParseError("prometheus error")
+
+
+def parse_matrix(body: bytes) -> List[Tuple[Dict[str, str], np.ndarray, np.ndarray]]:
+    if isinstance(body, str):
+        body = body.encode()
+    _check_status(body)
+    lib = _load()
+    if lib is None:
+        return _parse_py(body)
+    n = lib.fm_prom_scan(body, len(body), 0, None, None, None, None)
+    if n < 0:
+        raise ParseError(f"malformed query_range body (code {n})")
+    off = np.zeros(n, dtype=np.int64)
+    ln = np.zeros(n, dtype=np.int32)
+    cnt = np.zeros(n, dtype=np.int64)
+    tot = C.c_longlong(0)
+    lib.fm_prom_scan(body, len(body), n, off.ctypes.data, ln.ctypes.data, cnt.ctypes.data, C.byref(tot))
+    ts = np.empty(tot.value, dtype=np.float64)
+    vals = np.empty(tot.value, dtype=np.float32)
+    k = lib.fm_prom_fill(body, len(body), ts.ctypes.data, vals.ctypes.data, tot.value)
+    if k < 0:
+        raise ParseError(f"malformed query_range body (code {k})")
+    out = []
+    pos = 0
+    for i in range(n):
+        labels = json.loads(body[off[i]: off[i] + ln[i]]) if off[i] >= 0 and ln[i] > 0 else {}
+        c = int(cnt[i])
+        out.append((labels, ts[pos:pos + c], vals[pos:pos + c]))
+        pos += c
+    return out
+
+
+def parse_dense(body: bytes, start: float, step: float, T: int, out: np.ndarray, row0: int = 0) -> Tuple[int, int]:
+    """Scatter series into ``out[row0 + s, :]`` (float32, pre-filled with NaN).
+    Returns (n_series, n_dropped_points)."""
+    if isinstance(body, str):
+        body = body.encode()
+    _check_status(body)
+    if out.dtype != np.float32 or out.ndim != 2 or out.shape[1] < T or not out.flags.c_contiguous:
+        raise ValueError("out must be a C-contiguous float32 [rows, >=T] array")
+    lib = _load()
+    if lib is None:
+        series = _parse_py(body)
+        dropped = 0
+        for s, (_, ts, v) in enumerate(series):
+            if row0 + s >= out.shape[0]:
+                dropped += len(ts)
+                continue
+            fi = (ts - start) / step
+            i = np.rint(fi).astype(np.int64)
+            ok = (i >= 0) & (i < T) & (np.abs(fi - i) < 1e-6)
+            out[row0 + s, i[ok]] = v[ok]
+            dropped += int((~ok).sum())
+        return len(series), dropped
+    dropped = C.c_longlong(0)
+    n = lib.fm_prom_dense(body, len(body), float(start), float(step), int(T), out.ctypes.data, out.shape[1],
+                          int(row0), out.shape[0], C.byref(dropped))
+    if n < 0:
+        raise ParseError(f"malformed query_range body (code {n})")
+    return int(n), int(dropped.value)
+
+
+def _parse_py(body: bytes):
+    d = json.loads(body)
+    if d.get("status") != "success":
+        raise ParseError(d.get("error", "prometheus error"))
+    out = []
+    for r in d.get("data", {}).get("result", []):
+        pts = r.get("values") or ([r["value"]] if "value" in r else [])
+        ts = np.array([float(p[0]) for p in pts], dtype=np.float64)
+        vals = np.array([float(p[1]) for p in pts], dtype=np.float32)
+        out.append((r.get("metric", {}), ts, vals))
+    return out

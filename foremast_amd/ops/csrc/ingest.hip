@@ -3,7 +3,9 @@
 // Streaming layout (foremast_amd/ingest/ringbuffer.py):
 //   hist [N, R]      7-day history ring (bf16 or f32), one point per minute;
 //   cur  [N, P*W]    current window, P pods x W slots (slot = tick mod W);
-//   newv [N, P]      this tick's per-pod values (from the host ingest, H2D).
+//   newv [N, P]      this tick's per-pod values (from the host ingest, H2D);
+//   base [N, P*W]    optional baseline (old-pod) window, streamed the same way
+//   newb [N, P]      (no graduation: the model history is the app aggregate).
 // Per series: the slot being overwritten holds the oldest current points
 // (age W); their pod-mean graduates into history at column hist_col, then
 // the new per-pod values take the slot.  One thread per series; everything
@@ -14,9 +16,15 @@ template <typename TH>
 __global__ __launch_bounds__(256) void tick_ingest_kernel(TH* __restrict__ hist, long long ld_h, int hist_col,
                                                           float* __restrict__ cur, long long ld_c, int P, int W,
                                                           int slot, const float* __restrict__ newv,
-                                                          long long ld_n, int N, int graduate) {
+                                                          long long ld_n, int N, int graduate,
+                                                          float* __restrict__ base, const float* __restrict__ newb) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
+  if (base) {
+    float* brow = base + (long long)n * ld_c;
+    const float* nb = newb + (long long)n * ld_n;
+    for (int p = 0; p < P; ++p) brow[p * W + slot] = nb[p];
+  }
   float s = 0.f, c = 0.f;
   float* row = cur + (long long)n * ld_c;
   const float* nv = newv + (long long)n * ld_n;
@@ -31,15 +39,15 @@ __global__ __launch_bounds__(256) void tick_ingest_kernel(TH* __restrict__ hist,
 
 extern "C" int fm_tick_ingest(void* hist, long long ld_h, int hist_col, float* cur, long long ld_c, int P,
                               int W, int slot, const float* newv, long long ld_n, int N, int graduate,
-                              int bf16, hipStream_t st) {
+                              float* base, const float* newb, int bf16, hipStream_t st) {
   if (N <= 0) return 0;
   if (P <= 0 || W <= 0 || slot < 0 || slot >= W || hist_col < 0) return (int)hipErrorInvalidValue;
   dim3 grid((N + 255) / 256), block(256);
   if (bf16)
     hipLaunchKernelGGL(tick_ingest_kernel<bf16_t>, grid, block, 0, st, (bf16_t*)hist, ld_h, hist_col, cur,
-                       ld_c, P, W, slot, newv, ld_n, N, graduate);
+                       ld_c, P, W, slot, newv, ld_n, N, graduate, base, newb);
   else
     hipLaunchKernelGGL(tick_ingest_kernel<float>, grid, block, 0, st, (float*)hist, ld_h, hist_col, cur, ld_c,
-                       P, W, slot, newv, ld_n, N, graduate);
+                       P, W, slot, newv, ld_n, N, graduate, base, newb);
   return (int)hipGetLastError();
 }

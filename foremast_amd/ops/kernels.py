@@ -394,8 +394,10 @@ def ring_append(dst: torch.Tensor, col0: int, src: torch.Tensor) -> None:
 
 
 def tick_ingest(hist: torch.Tensor, hist_col: int, cur: torch.Tensor, P: int, W: int, slot: int,
-                newv: torch.Tensor, graduate: bool = True) -> None:
-    """Per-tick streaming ingest (see csrc/ingest.hip)."""
+                newv: torch.Tensor, graduate: bool = True, base: Optional[torch.Tensor] = None,
+                newb: Optional[torch.Tensor] = None) -> None:
+    """Per-tick streaming ingest (see csrc/ingest.hip); ``newv``/``newb`` are
+    ``[N, P]`` (same row stride) current/baseline pod values."""
     lib = nat.require()
     _cuda(hist, "hist")
     N = hist.shape[0]
@@ -407,7 +409,13 @@ def tick_ingest(hist: torch.Tensor, hist_col: int, cur: torch.Tensor, P: int, W:
           and newv.dtype == torch.float32, f"newv must be float32 [N, {P}]")
     _need(cur.device == hist.device and newv.device == hist.device, "device mismatch")
     _need(0 <= slot < W and 0 <= hist_col < hist.shape[1], "slot/hist_col out of range")
+    if base is not None:
+        _need(newb is not None and base.shape == cur.shape and base.stride() == cur.stride()
+              and base.dtype == torch.float32 and base.device == cur.device, "base must match cur")
+        _need(newb.shape == newv.shape and newb.stride() == newv.stride() and newb.dtype == torch.float32
+              and newb.device == newv.device, "newb must match newv")
     nat.check(lib.fm_tick_ingest(nat.ptr(hist), hist.stride(0), int(hist_col), nat.ptr(cur), cur.stride(0),
                                  int(P), int(W), int(slot), nat.ptr(newv), newv.stride(0), N, int(graduate),
+                                 nat.ptr(base), nat.ptr(newb) if base is not None else 0,
                                  int(hist.dtype == torch.bfloat16), nat.stream_handle(hist.device)),
               "fm_tick_ingest")

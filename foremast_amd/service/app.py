@@ -25,6 +25,10 @@ import logging
 import os
 from typing import Any, Callable, Dict, Optional
 
+import httpx
+from fastapi import FastAPI, Request
+from fastapi.responses import JSONResponse, PlainTextResponse
+
 from ..api import rest as r
 from ..api import status as st
 from ..store import JobStore, open_store
@@ -37,7 +41,6 @@ DEFAULT_QUERY_ENDPOINT = "http://prometheus-k8s.monitoring.svc.cluster.local:909
 
 
 def _err(code: int, msg: str):
-    from fastapi.responses import JSONResponse
     return JSONResponse(status_code=code, content={"error": msg})
 
 
@@ -115,10 +118,6 @@ def create_app(store: Optional[JobStore] = None, query_endpoint: Optional[str] =
 
     ``proxy_transport`` lets tests route the proxy to an in-process ASGI app.
     """
-    from fastapi import FastAPI, Request
-    from fastapi.responses import JSONResponse, PlainTextResponse
-    import httpx
-
     if store is None:
         store = open_store(os.environ.get("FOREMAST_JOB_STORE") or os.environ.get("ELASTIC_URL"))
     qe = query_endpoint or os.environ.get("QUERY_SERVICE_ENDPOINT") or DEFAULT_QUERY_ENDPOINT

@@ -1,0 +1,84 @@
+import asyncio
+import json
+
+import httpx
+import numpy as np
+import pytest
+
+from foremast_amd.ingest import native
+from foremast_amd.promql import synth
+from foremast_amd.promql.client import PromClient
+from foremast_amd.promql.fake import FakePrometheus
+from foremast_amd.promql.selector import SelectorError, parse_selector
+
+
+def test_selector_matching():
+    s = parse_selector('namespace_pod:http_server_requests_error_5xx{namespace="ns",pod=~"a-1|b-2"}')
+    assert s.name == "namespace_pod:http_server_requests_error_5xx"
+    base = {"__name__": s.name, "namespace": "ns"}
+    assert s.matches(dict(base, pod="a-1"))
+    assert not s.matches(dict(base, pod="a-10"))  # anchored regex
+    assert not s.matches(dict(base, pod="c"))
+    s2 = parse_selector('m{app!="x",pod!~"z.*"}')
+    assert s2.matches({"__name__": "m", "app": "y", "pod": "a"})
+    with pytest.raises(SelectorError):
+        parse_selector("sum(rate(x[1m]))")
+
+
+BODY = (b'{"status":"success","data":{"resultType":"matrix","result":['
+        b'{"metric":{"__name__":"m","pod":"a"},"values":[[1700000000,"1.5"],[1700000060,"NaN"],[1700000120,"2"]]},'
+        b'{"metric":{},"values":[]},'
+        b'{"metric":{"pod":"b\\"q"},"values":[[1700000060.5,"+Inf"],[1700000180,"-3e-2"]]}]}}')
+
+
+def test_native_parser_matches_json():
+    out = native.parse_matrix(BODY)
+    ref = native._parse_py(BODY)
+    assert len(out) == len(ref) == 3
+    for (l1, t1, v1), (l2, t2, v2) in zip(out, ref):
+        assert l1 == l2
+        np.testing.assert_array_equal(t1, t2)
+        np.testing.assert_array_equal(v1, v2)
+    assert out[2][0]["pod"] == 'b"q'
+
+
+def test_native_dense_scatter():
+    dense = np.full((4, 5), np.nan, dtype=np.float32)
+    n, dropped = native.parse_dense(BODY, 1700000000, 60, 5, dense, row0=1)
+    assert n == 3
+    assert dropped == 1  # the off-grid 1700000060.5 sample
+    assert dense[1, 0] == 1.5 and np.isnan(dense[1, 1]) and dense[1, 2] == 2.0
+    assert dense[3, 3] == pytest.approx(-0.03)
+
+
+def test_parser_errors():
+    with pytest.raises(native.ParseError):
+        native.parse_matrix(b'{"status":"error","errorType":"bad_data","error":"x"}')
+    with pytest.raises(native.ParseError):
+        native.parse_matrix(b'{"status":"success","data":{"result":[{"metric":{},"values":[[1,}]}}')
+
+
+def test_fake_prometheus_and_client_roundtrip():
+    prom = FakePrometheus(clock=lambda: 1_700_100_000)
+    prom.add("namespace_pod:lat", {"namespace": "ns", "pod": "p1"}, synth.seasonal(level=10, amp=1, noise=0.1))
+    prom.add("namespace_pod:lat", {"namespace": "ns", "pod": "p2"}, synth.seasonal(level=12, amp=1, noise=0.1))
+    prom.add("namespace_pod:lat", {"namespace": "other", "pod": "p1"}, synth.seasonal())
+    transport = httpx.ASGITransport(app=prom.asgi_app())
+    client = PromClient(transport=transport)
+    url = ("http://prom:9090/api/v1/query_range?query=" + "namespace_pod%3Alat%7Bnamespace%3D%22ns%22%2Cpod%3D~%22p1%7Cp2%22%7D"
+           + "&start=1700000000&end=1700003540&step=60")
+    res = asyncio.run(client.fetch_many([url]))[0]
+    assert len(res) == 2
+    assert all(len(s.ts) == 60 for s in res)
+    assert {s.labels["pod"] for s in res} == {"p1", "p2"}
+    # late data: nothing newer than now - lag
+    prom.faults.lag_seconds = 1_700_100_000 - 1_700_001_000
+    res = asyncio.run(client.fetch_many([url]))[0]
+    assert all(s.ts.max() <= 1_700_001_000 for s in res)
+
+
+def test_error_rate_spikes():
+    f = synth.error_rate(spikes=[600.0, 1800.0])
+    v = f(np.arange(0, 3600, 60.0))
+    assert v[10] > 30 and v[30] > 30
+    assert np.all(v[[0, 5, 20, 40]] < 2)
