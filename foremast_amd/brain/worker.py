@@ -1,0 +1,260 @@
+"""The brain job loop (foremast-brain, absent from the reference repo).
+
+Reconstructed from ``docs/guides/design.md:33-43`` and the request state
+diagram::
+
+    claim   : status in {initial, reprogress}, or in progress longer than
+              MAX_STUCK_IN_SECONDS (takeover)   → preprocess_inprogress
+    fetch   : historical / baseline / current range vectors (concurrent)
+    score   : one batched GPU pass over every (job, metric) of the cycle
+    verdict : anomaly                  → completed_unhealth   (fail fast)
+              endTime reached, healthy → completed_health
+              no current data at end   → completed_unknown
+              otherwise                → reprogress (re-claimed next cycle)
+    export  : foremastbrain:<metric>_{upper,lower,anomaly} gauges
+
+Writes go through the job store with ``expect_claimed_by`` so a worker that
+lost its lease (stuck-job takeover by another brain) cannot overwrite the
+new owner's result.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import json
+import logging
+import os
+import socket
+import time
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Tuple
+
+import numpy as np
+
+from ..api import rest as r
+from ..promql.client import FetchError, PromClient, Series
+from ..promql.selector import SelectorError, parse_selector
+from ..service import urls
+from ..store import JobStore
+from ..utils.config import BrainConfig
+from ..utils.metrics import BrainMetrics
+from ..utils.timeutil import TimeFormatError, parse_rfc3339
+from .batch import BatchScorer, MetricTask, TaskResult
+
+log = logging.getLogger("foremast.brain")
+
+
+@dataclass
+class JobPlan:
+    doc: Dict[str, Any]
+    end_ts: float
+    current: Dict[str, str] = field(default_factory=dict)
+    baseline: Dict[str, str] = field(default_factory=dict)
+    historical: Dict[str, str] = field(default_factory=dict)
+    sources: Dict[str, str] = field(default_factory=dict)
+    error: str = ""
+
+
+def _selector_info(url: str) -> Tuple[str, str, str]:
+    try:
+        q = urls.parse_prometheus_url(url)["query"]
+        sel = parse_selector(str(q))
+    except (urls.ConfigError, SelectorError):
+        return "", "", ""
+    labels = {k: v for k, op, v in sel.matchers if op == "="}
+    return sel.name, labels.get("namespace", ""), labels.get("app", "")
+
+
+def _grid(url: str) -> Tuple[float, float, float]:
+    p = urls.parse_prometheus_url(url)
+    return float(p["start"]), float(p["end"]), float(p["step"])
+
+
+class BrainWorker:
+    def __init__(self, store: JobStore, cfg: Optional[BrainConfig] = None, prom: Optional[PromClient] = None,
+                 scorer: Optional[BatchScorer] = None, worker_id: Optional[str] = None,
+                 clock=time.time, metrics: Optional[BrainMetrics] = None, batch_limit: int = 256) -> None:
+        self.store = store
+        self.cfg = cfg or BrainConfig.from_env()
+        self.prom = prom or PromClient()
+        self.scorer = scorer or BatchScorer(self.cfg)
+        self.worker_id = worker_id or f"{socket.gethostname()}-{os.getpid()}"
+        self.clock = clock
+        self.metrics = metrics or BrainMetrics()
+        self.batch_limit = batch_limit
+
+    # ------------------------------------------------------------------ planning
+    def plan(self, doc: Dict[str, Any]) -> JobPlan:
+        try:
+            end_ts = parse_rfc3339(doc.get("endTime", "")).timestamp()
+        except TimeFormatError:
+            end_ts = 0.0
+        p = JobPlan(doc=doc, end_ts=end_ts)
+        try:
+            p.current = urls.parse_config(doc.get("currentConfig", ""))
+            p.baseline = urls.parse_config(doc.get("baselineConfig", ""))
+            p.historical = urls.parse_config(doc.get("historicalConfig", ""))
+            p.sources = urls.parse_config(doc.get("currentMetricStore", ""))
+        except urls.ConfigError as e:
+            p.error = f"bad config: {e}"
+        if not p.current and not p.error:
+            p.error = "no current metric config"
+        unsupported = [a for a, s in p.sources.items() if s and s != r.DATASOURCE_PROMETHEUS]
+        if unsupported and not p.error:
+            p.error = "unsupported data source for " + ",".join(sorted(unsupported))
+        return p
+
+    # ------------------------------------------------------------------ one cycle
+    async def cycle(self) -> int:
+        t0 = time.perf_counter()
+        now = self.clock()
+        docs = self.store.claim(self.worker_id, now=now, max_stuck_s=self.cfg.max_stuck_seconds,
+                                limit=self.batch_limit)
+        if not docs:
+            return 0
+        plans = [self.plan(d) for d in docs]
+        # fetch everything concurrently
+        reqs: List[Tuple[int, str, str, str]] = []  # (plan, category, alias, url)
+        for i, p in enumerate(plans):
+            if p.error:
+                continue
+            for cat, m in (("current", p.current), ("baseline", p.baseline), ("historical", p.historical)):
+                for alias, url in m.items():
+                    reqs.append((i, cat, alias, url))
+        fetched = await self.prom.fetch_many([u for _, _, _, u in reqs])
+        data: Dict[Tuple[int, str, str], Any] = {}
+        for (i, cat, alias, _), res in zip(reqs, fetched):
+            data[(i, cat, alias)] = res
+        tasks: List[MetricTask] = []
+        owners: List[int] = []
+        fetch_errors: Dict[int, List[str]] = {}
+        for i, p in enumerate(plans):
+            if p.error:
+                continue
+            for alias in sorted(p.current):
+                task = self._build_task(i, p, alias, data, fetch_errors)
+                if task is not None:
+                    tasks.append(task)
+                    owners.append(i)
+        results: List[TaskResult] = self.scorer.score(tasks) if tasks else []
+        per_job: Dict[int, List[Tuple[MetricTask, TaskResult]]] = {}
+        for t, res, i in zip(tasks, results, owners):
+            per_job.setdefault(i, []).append((t, res))
+        self._multivariate(plans, per_job)
+        for i, p in enumerate(plans):
+            self._finish(p, per_job.get(i, []), fetch_errors.get(i, []), now)
+        self.metrics.detect_latency.observe(time.perf_counter() - t0)
+        self.metrics.series_scored.inc(len(tasks))
+        return len(docs)
+
+    def _build_task(self, i: int, p: JobPlan, alias: str, data, errors) -> Optional[MetricTask]:
+        cur = data.get((i, "current", alias))
+        hist = data.get((i, "historical", alias))
+        base = data.get((i, "baseline", alias))
+        if isinstance(cur, Exception):
+            errors.setdefault(i, []).append(f"{alias}: current fetch failed")
+            cur = []
+        if isinstance(hist, Exception) or hist is None:
+            errors.setdefault(i, []).append(f"{alias}: historical fetch failed")
+            return None
+        hurl = p.historical.get(alias, "")
+        metric, ns, app = _selector_info(hurl)
+        start, end, step = _grid(hurl)
+        T = int(round((end - start) / step)) + 1
+        sums = np.zeros(T)
+        cnt = np.zeros(T)
+        for s in hist:  # several series (e.g. per pod) → mean per timestamp
+            idx = np.rint((s.ts - start) / step).astype(np.int64)
+            ok = (idx >= 0) & (idx < T) & ~np.isnan(s.values)
+            np.add.at(cnt, idx[ok], 1)
+            np.add.at(sums, idx[ok], s.values[ok].astype(np.float64))
+        h = np.where(cnt > 0, sums / np.maximum(cnt, 1), np.nan).astype(np.float32)
+        cts, cvs, tags = [], [], []
+        for s in cur or []:
+            cts.append(s.ts)
+            cvs.append(s.values)
+            tags += [s.labels.get("pod", s.labels.get("app", ""))] * len(s.ts)
+        cur_ts = np.concatenate(cts) if cts else np.zeros(0)
+        cur_vals = np.concatenate(cvs).astype(np.float32) if cvs else np.zeros(0, dtype=np.float32)
+        base_vals = None
+        if base is not None and not isinstance(base, Exception) and base:
+            base_vals = np.concatenate([s.values for s in base]).astype(np.float32)
+        th = self.cfg.for_metric(alias, metric)
+        return MetricTask(job_id=p.doc["id"], alias=alias, metric=metric or alias, namespace=ns, app=app,
+                          step=step, hist=h, hist_end=start + (T - 1) * step, cur_ts=cur_ts, cur_vals=cur_vals,
+                          cur_tags=tags, base_vals=base_vals, threshold=th.threshold, bound=th.bound,
+                          min_lower=th.min_lower_bound)
+
+    def _multivariate(self, plans: List[JobPlan], per_job) -> None:
+        algo = self.cfg.algorithm
+        if algo != "bivariate_normal":
+            return
+        pairs, owners = [], []
+        for i, items in per_job.items():
+            if len(items) >= 2:
+                (ta, _), (tb, _) = items[0], items[1]
+                pairs.append((ta, tb))
+                owners.append(i)
+        for i, (verdict, idx) in zip(owners, self.scorer.score_bivariate(pairs)):
+            ta, ra = per_job[i][0]
+            tb, rb = per_job[i][1]
+            if verdict == 1:
+                ra.verdict = max(ra.verdict, 1)
+                ra.anomalies = [(float(ta.cur_ts[j]), float(ta.cur_vals[j]),
+                                 ta.cur_tags[j] if j < len(ta.cur_tags) else "") for j in idx]
+                ra.model = rb.model = "bivariate_normal"
+
+    def _finish(self, p: JobPlan, items: List[Tuple[MetricTask, TaskResult]], errors: List[str], now: float):
+        doc_id = p.doc["id"]
+        if p.error:
+            self._write(doc_id, r.ST_PREPROCESS_FAILED, p.error)
+            return
+        anomaly: Dict[str, Dict[str, Any]] = {}
+        any_current = False
+        for t, res in items:
+            any_current |= bool(len(t.cur_vals))
+            if len(res.upper) and t.namespace:
+                last_anom = res.anomalies[-1][0] if res.anomalies else None
+                self.metrics.export_band(t.metric, t.namespace, t.app, float(res.upper[-1]),
+                                         float(res.lower[-1]), last_anom)
+            if res.verdict == 1 and res.anomalies:
+                vals: List[float] = []
+                for ts, v, _ in sorted(res.anomalies):
+                    vals += [ts, v]
+                tags = ",".join(sorted({tag for _, _, tag in res.anomalies if tag}))
+                anomaly[t.alias] = {"tags": tags, "values": vals}
+        if anomaly:
+            self._write(doc_id, r.ST_COMPLETED_UNHEALTH,
+                        "anomaly detected in " + ",".join(sorted(anomaly)), anomaly)
+            return
+        if now >= p.end_ts:
+            if any_current and not errors:
+                self._write(doc_id, r.ST_COMPLETED_HEALTH, "")
+            else:
+                reason = "; ".join(errors) or "no current metric data"
+                self._write(doc_id, r.ST_COMPLETED_UNKNOWN, reason)
+            return
+        self._write(doc_id, r.ST_REPROGRESS, "; ".join(errors),
+                    not_before=now + self.cfg.poll_seconds)
+
+    def _write(self, doc_id: str, status: str, reason: str, anomaly: Optional[Dict] = None,
+               not_before: float = 0.0) -> None:
+        fields: Dict[str, Any] = {"status": status, "reason": reason, "not_before": not_before,
+                                  "processingContent": f"scored by {self.worker_id}"}
+        if anomaly:
+            fields["anomalyInfo"] = json.dumps(anomaly)
+        if status in r.TERMINAL_STATUSES:
+            fields["claimed_by"] = ""
+        ok = self.store.update(doc_id, fields, expect_claimed_by=self.worker_id)
+        if ok and status in r.TERMINAL_STATUSES:
+            self.metrics.jobs.labels(status=status).inc()
+
+    async def run_forever(self, stop: Optional[asyncio.Event] = None) -> None:
+        while stop is None or not stop.is_set():
+            try:
+                n = await self.cycle()
+            except Exception as e:  # noqa: BLE001 - keep the loop alive
+                log.exception("brain cycle failed: %s", e)
+                n = 0
+            if n == 0:
+                await asyncio.sleep(min(self.cfg.poll_seconds, 1.0))

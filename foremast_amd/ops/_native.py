@@ -32,7 +32,7 @@ F = C.c_float
 
 class DetectArgs(C.Structure):
     _fields_ = [
-        ("horizons", P), ("C", I), ("min_valid", I),
+        ("horizons", P), ("h_ld", LL), ("C", I), ("min_valid", I),
         ("cur", P), ("ld_cur", LL),
         ("threshold", P), ("bound", P), ("min_lower", P), ("differs", P),
         ("pw_scale", F), ("_pad0", I),

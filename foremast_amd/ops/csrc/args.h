@@ -6,7 +6,8 @@
 #include <stddef.h>
 
 struct DetectArgs {
-  const int* horizons;          // [C]
+  const int* horizons;          // [C] (h_ld = 0) or [N, h_ld]
+  long long h_ld;               // horizon row stride; 0 = shared across series
   int C;
   int min_valid;
   const float* cur;             // [N, ld_cur] (NaN = missing) or null

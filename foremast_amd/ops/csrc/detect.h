@@ -42,7 +42,7 @@ __device__ __forceinline__ void detect_epilogue(const DetectArgs& d, int n, floa
   const bool model_ok = n_valid >= (float)d.min_valid;
   float cnt = 0.f, anyv = 0.f, sc = 0.f;
   for (int c = tid; c < d.C; c += blockDim.x) {
-    const int h = d.horizons[c];
+    const int h = d.horizons[d.h_ld * n + c];
     const float f = fcast(h);
     const float up = f + thr * sig;
     const float lo = fmaxf(f - thr * sig, mlow);

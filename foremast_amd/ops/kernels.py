@@ -49,7 +49,7 @@ def _vec(t: Optional[torch.Tensor], n: int, dtype, name: str, device) -> Optiona
 class DetectSpec:
     """Inputs of the fused detection epilogue (see models/detect.py)."""
 
-    horizons: torch.Tensor                 # int32 [C]
+    horizons: torch.Tensor                 # int32 [C] (shared) or [N, C] (per series)
     threshold: torch.Tensor                # float32 [N]
     bound: torch.Tensor                    # int8 [N]
     min_lower: torch.Tensor                # float32 [N]
@@ -63,9 +63,12 @@ class DetectSpec:
 
 
 def _fill_detect(d: nat.DetectArgs, spec: DetectSpec, N: int, device, out: Dict[str, torch.Tensor]) -> None:
-    C = int(spec.horizons.shape[0])
-    _need(spec.horizons.dtype == torch.int32 and spec.horizons.is_contiguous() and spec.horizons.dim() == 1,
-          "horizons must be contiguous int32 [C]")
+    hz = spec.horizons
+    _need(hz.dtype == torch.int32 and hz.stride(-1) == 1 and hz.dim() in (1, 2),
+          "horizons must be int32 [C] or [N, C] with unit inner stride")
+    C = int(hz.shape[-1])
+    if hz.dim() == 2:
+        _need(hz.shape[0] == N, f"per-series horizons must be [{N}, C]")
     _need(spec.horizons.device == device, "horizons on wrong device")
     _vec(spec.threshold, N, torch.float32, "threshold", device)
     _vec(spec.bound, N, torch.int8, "bound", device)
@@ -94,6 +97,7 @@ def _fill_detect(d: nat.DetectArgs, spec: DetectSpec, N: int, device, out: Dict[
     if "score" not in out:
         out["score"] = torch.empty(N, **kw)
     d.horizons = nat.ptr(spec.horizons)
+    d.h_ld = int(hz.stride(0)) if hz.dim() == 2 else 0
     d.C = C
     d.min_valid = int(spec.min_valid)
     d.cur = nat.ptr(spec.cur)

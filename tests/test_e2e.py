@@ -1,0 +1,216 @@
+"""End-to-end: rollout of a faulty v2 → job → brain detects the
+5xx spike → DeploymentMonitor Unhealthy with anomaly values → AutoRollback
+on the fake cluster; band gauges exported.  Runs on CPU (reference scorers)
+and, on a GPU box, through the HIP kernels."""
+
+import asyncio
+import json
+
+import httpx
+import numpy as np
+import pytest
+
+from foremast_amd.api import crd
+from foremast_amd.brain.batch import BatchScorer
+from foremast_amd.brain.worker import BrainWorker
+from foremast_amd.controller.analyst import AnalystClient
+from foremast_amd.controller.barrelman import Barrelman
+from foremast_amd.controller.monitor import MonitorController
+from foremast_amd.k8s.fake import FakeCluster
+from foremast_amd.promql import synth
+from foremast_amd.promql.client import PromClient
+from foremast_amd.promql.fake import FakePrometheus
+from foremast_amd.service.app import create_app
+from foremast_amd.store import MemoryJobStore
+from foremast_amd.utils.config import BrainConfig, reference_default_env
+from foremast_amd.utils.metrics import BrainMetrics
+
+NS = "foremast-examples"
+T0 = 1_700_000_000.0  # rollout time (aligned to the minute)
+METRIC = "http_server_requests_error_5xx"
+
+
+class Clock:
+    def __init__(self, t):
+        self.t = t
+
+    def __call__(self):
+        return self.t
+
+
+def metadata(namespace="foremast"):
+    return {
+        "apiVersion": "deployment.foremast.ai/v1alpha1", "kind": "DeploymentMetadata",
+        "metadata": {"name": "spring-boot", "namespace": namespace},
+        "spec": {"analyst": {"endpoint": "http://foremast-service:8099/v1/healthcheck/"},
+                 "metrics": {"dataSourceType": "prometheus", "endpoint": "http://prometheus:9090/api/v1/",
+                             "monitoring": [{"metricName": METRIC, "metricType": "counter",
+                                             "metricAlias": "error5xx"}]}},
+    }
+
+
+def build_world(algorithm="moving_average_all", strategy_canary=False):
+    clock = Clock(T0)
+    kube = FakeCluster()
+    kube.add_namespace(NS)
+    kube.add_namespace("foremast")
+    kube.create_sync("deploymentmetadatas", metadata())
+    # user pre-creates the monitor to opt into AutoRollback (examples/demo/0_service.yaml)
+    kube.create_sync("deploymentmonitors", {"metadata": {"name": "demo", "namespace": NS},
+                                            "spec": {"remediation": {"option": "AutoRollback"}}})
+    prom = FakePrometheus(clock=clock)
+    prom.add("namespace_app_per_pod:" + METRIC, {"namespace": NS, "app": "demo"},
+             synth.error_rate(base=0.3, spread=0.2, seed=1))
+    store = MemoryJobStore()
+    service = create_app(store, query_endpoint="http://prometheus:9090/")
+    svc_transport = httpx.ASGITransport(app=service)
+    prom_transport = httpx.ASGITransport(app=prom.asgi_app())
+    barrel = Barrelman(kube, namespace="foremast", clock=clock, poll_seconds=0, pod_retry_sleep=0,
+                       analyst_factory=lambda ep: AnalystClient(ep, transport=svc_transport))
+    mc = MonitorController(kube, barrel)
+    env = reference_default_env()
+    env["ML_ALGORITHM"] = algorithm
+    env["MIN_HISTORICAL_DATA_POINT_TO_MEASURE"] = "10"
+    cfg = BrainConfig.from_env(env)
+    metrics = BrainMetrics()
+    brain = BrainWorker(store, cfg, prom=PromClient(transport=prom_transport), scorer=BatchScorer(cfg),
+                        worker_id="brain-0", clock=clock, metrics=metrics)
+    return clock, kube, prom, store, barrel, mc, brain, metrics
+
+
+def register_pod_series(kube, prom, old_rs_hash, spike_at, spread=0.2):
+    for p in kube.list_sync("pods", NS):
+        h = p["metadata"]["labels"]["pod-template-hash"]
+        gen = synth.error_rate(base=0.3, spread=spread, seed=sum(map(ord, p["metadata"]["name"])))
+        if h != old_rs_hash:
+            gen = synth.step_change(gen, at=spike_at, factor=0.0, add=40.0)  # v2: 5xx storm
+        prom.add("namespace_pod:" + METRIC, {"namespace": NS, "pod": p["metadata"]["name"]}, gen)
+
+
+async def _drive_rollout(world):
+    clock, kube, prom, store, barrel, mc, brain, metrics = world
+    v1 = kube.apply_deployment(NS, "demo", "demo", "foremast/demo:v1", replicas=2,
+                               labels={"appType": "spring-boot"})
+    await barrel.on_deployment_added(v1)
+    mon = crd.DeploymentMonitor.from_dict(kube.get_sync("deploymentmonitors", NS, "demo"))
+    assert mon.status.phase == crd.PHASE_HEALTHY
+    assert mon.spec.remediation.option == "AutoRollback"  # preserved from the user's object
+    old_hash = kube.list_sync("replicasets", NS)[0]["metadata"]["labels"]["pod-template-hash"]
+    v1 = kube.get_sync("deployments", NS, "demo")
+    v2 = kube.apply_deployment(NS, "demo", "demo", "foremast/demo:v2", replicas=2,
+                               labels={"appType": "spring-boot"})
+    register_pod_series(kube, prom, old_hash, spike_at=T0 + 120)
+    task = await barrel.on_deployment_updated(v1, v2)
+    await barrel.drain()
+    mon = crd.DeploymentMonitor.from_dict(kube.get_sync("deploymentmonitors", NS, "demo"))
+    assert mon.status.phase == crd.PHASE_RUNNING and mon.status.job_id
+    assert mon.spec.rollback_revision == 1
+    doc = store.get(mon.status.job_id)
+    assert doc["status"] == "initial"
+    assert "namespace_pod%3Ahttp_server_requests_error_5xx" in doc["currentConfig"]
+    return mon
+
+
+@pytest.mark.parametrize("algorithm", ["moving_average_all", "holt_winters"])
+def test_rollout_spike_rolls_back(algorithm):
+    world = build_world(algorithm)
+    clock, kube, prom, store, barrel, mc, brain, metrics = world
+
+    async def go():
+        mon = await _drive_rollout(world)
+        # 5 minutes into the watch window the brain runs a cycle
+        clock.t = T0 + 300
+        n = await brain.cycle()
+        assert n == 1
+        doc = store.get(mon.status.job_id)
+        assert doc["status"] == "completed_unhealth", doc["reason"]
+        info = json.loads(doc["anomalyInfo"])
+        assert info["error5xx"]["values"][1] > 30  # the 40/s storm
+        # barrelman polls the service
+        before = kube.get_sync("deploymentmonitors", NS, "demo")
+        await barrel.check_running_status()
+        after = kube.get_sync("deploymentmonitors", NS, "demo")
+        m2 = crd.DeploymentMonitor.from_dict(after)
+        assert m2.status.phase == crd.PHASE_UNHEALTHY
+        assert m2.status.anomaly.anomalous_metrics[0].name == "error5xx"
+        assert m2.status.anomaly.anomalous_metrics[0].values[0].value > 30
+        # MonitorController remediates
+        await mc.on_monitor_updated(before, after)
+        await barrel.drain()
+        assert kube.actions and kube.actions[-1]["action"] == "rollback" and kube.actions[-1]["revision"] == 1
+        m3 = crd.DeploymentMonitor.from_dict(kube.get_sync("deploymentmonitors", NS, "demo"))
+        assert m3.status.remediation_taken
+        depl = kube.get_sync("deployments", NS, "demo")
+        assert depl["spec"]["template"]["spec"]["containers"][0]["image"] == "foremast/demo:v1"
+        # the rollback rollout itself must not start a new job (revision == rollbackRevision... new rev 3)
+        text = metrics.render().decode()
+        assert "foremastbrain:namespace_app_per_pod:http_server_requests_error_5xx_upper" in text
+        assert "foremastbrain:namespace_app_per_pod:http_server_requests_error_5xx_anomaly" in text
+    asyncio.run(go())
+
+
+def test_healthy_rollout_completes_healthy():
+    world = build_world()
+    clock, kube, prom, store, barrel, mc, brain, metrics = world
+
+    async def go():
+        v1 = kube.apply_deployment(NS, "demo", "demo", "foremast/demo:v1", replicas=2,
+                                   labels={"appType": "spring-boot"})
+        await barrel.on_deployment_added(v1)
+        old_hash = kube.list_sync("replicasets", NS)[0]["metadata"]["labels"]["pod-template-hash"]
+        v1 = kube.get_sync("deployments", NS, "demo")
+        v2 = kube.apply_deployment(NS, "demo", "demo", "foremast/demo:v2", replicas=2,
+                                   labels={"appType": "spring-boot"})
+        register_pod_series(kube, prom, old_hash, spike_at=T0 + 10 ** 9, spread=0.02)  # never spikes
+        await barrel.on_deployment_updated(v1, v2)
+        await barrel.drain()
+        mon = crd.DeploymentMonitor.from_dict(kube.get_sync("deploymentmonitors", NS, "demo"))
+        clock.t = T0 + 300
+        await brain.cycle()
+        assert store.get(mon.status.job_id)["status"] == "reprogress"
+        clock.t = T0 + 302  # not yet eligible again (not_before = +poll_seconds)
+        assert await brain.cycle() == 0
+        clock.t = T0 + 11 * 60 + 30  # past endTime
+        await brain.cycle()
+        assert store.get(mon.status.job_id)["status"] == "completed_health"
+        await barrel.check_running_status()
+        m2 = crd.DeploymentMonitor.from_dict(kube.get_sync("deploymentmonitors", NS, "demo"))
+        assert m2.status.phase == crd.PHASE_HEALTHY
+        assert not kube.actions
+    asyncio.run(go())
+
+
+def test_stuck_job_takeover_and_lease():
+    world = build_world()
+    clock, kube, prom, store, barrel, mc, brain, metrics = world
+
+    async def go():
+        await _drive_rollout(world)
+        clock.t = T0 + 300
+        claimed = store.claim("dead-brain", now=clock.t, max_stuck_s=90)
+        assert len(claimed) == 1
+        assert await brain.cycle() == 0  # still leased
+        clock.t += 91  # past MAX_STUCK_IN_SECONDS → takeover
+        assert await brain.cycle() == 1
+        jid = claimed[0]["id"]
+        assert store.get(jid)["status"] == "completed_unhealth"
+        # the dead brain's late write is rejected by the lease check
+        assert not store.update(jid, {"status": "completed_health"}, expect_claimed_by="dead-brain")
+    asyncio.run(go())
+
+
+def test_unknown_when_no_current_data():
+    world = build_world()
+    clock, kube, prom, store, barrel, mc, brain, metrics = world
+
+    async def go():
+        mon = await _drive_rollout(world)
+        prom.remove("namespace_pod:" + METRIC)
+        clock.t = T0 + 12 * 60
+        await brain.cycle()
+        doc = store.get(mon.status.job_id)
+        assert doc["status"] == "completed_unknown"
+        await barrel.check_running_status()
+        m2 = crd.DeploymentMonitor.from_dict(kube.get_sync("deploymentmonitors", NS, "demo"))
+        assert m2.status.phase == crd.PHASE_ABORT  # service maps completed_unknown → abort (Q4)
+    asyncio.run(go())
