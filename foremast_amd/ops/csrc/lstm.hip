@@ -1,0 +1,287 @@
+// K6: fused LSTM-autoencoder inference on MFMA (bf16, or fp8 e4m3 OCP).
+//
+// Semantics: foremast_amd/models/lstm_ae.py (encoder LSTM(F→H), decoder with
+// zero input starting from the encoder's final (h, c), linear read-out,
+// reconstruction MSE → z-score vs calibration → verdict).  H = 64.
+//
+// Layout (one 64-lane wave = 32 series, a workgroup = 4 waves = 128 series):
+//  * gates^T [256 x 32] = Waug^T [256 x 80] · [h; x_t; 1] [80 x 32] on
+//    v_mfma_f32_32x32x16 (8 row tiles x 5 k-steps = 40 MFMAs per step).  The
+//    input projection and bias ride in the 5th k-step (x at k=64..64+F-1,
+//    bias at k=71), so no VALU matmul is needed for them.
+//  * The 256 gate rows are permuted host-side so that in tile t, accumulator
+//    register 4*gate+q of lane half hh holds gate `gate` of hidden unit
+//    u = 16(t>>1) + 8hh + 4(t&1) + q: each lane has i,f,g,o of its units
+//    (cell update is lane-local) AND the new h lands exactly where the next
+//    step's B operand needs unit 16s + 8hh + j (s = t>>1, j = 4(t&1)+q) —
+//    h never leaves registers across time steps, no LDS transpose.
+//  * Weights are pre-packed into A-fragment order [tile][kstep][lane][8] and
+//    staged in LDS once per phase (encoder, then decoder): one 16-byte
+//    ds_read per MFMA, lane-contiguous (conflict-free).
+#include "common.h"
+#include "args.h"
+
+#include <type_traits>
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+struct LstmArgs {
+  const float* x;          // [N, T, F] normalised windows
+  int N;
+  int T;
+  int F;                   // 1..7
+  int fp8;                 // 0 bf16, 1 fp8 e4m3
+  const void* w_enc;       // packed A fragments [8][5][64][8] (bf16 or fp8)
+  const void* w_dec;
+  const float* w_out;      // [F][64]
+  const float* b_out;      // [F]
+  float scale_w_enc;       // fp8 dequant scales (1 for bf16)
+  float scale_w_dec;
+  float scale_act;         // fp8 activation scale for h / x (1 for bf16)
+  float mu;                // calibration
+  float sigma;
+  const float* threshold;  // [N] or null (→ thr_default)
+  float thr_default;
+  float* err;              // [N]
+  float* zscore;           // [N] or null
+  signed char* verdict;    // [N] or null
+  float* recon;            // [N, T, F] or null
+  const int* app_id;       // [N] or null
+  int* app_stats;          // [A, 2] or null
+};
+
+extern __shared__ __attribute__((aligned(16))) char fm_lstm_smem[];
+
+namespace {
+
+constexpr int H = 64;
+constexpr int TILES = 8;
+constexpr int KSTEPS = 5;
+constexpr int FRAG_BYTES_BF16 = TILES * KSTEPS * 64 * 16;  // 40 KB
+constexpr int FRAG_BYTES_FP8 = TILES * KSTEPS * 64 * 8;    // 20 KB
+
+__device__ __forceinline__ float sigm(float v) { return __frcp_rn(1.f + __expf(-v)); }
+__device__ __forceinline__ float tanh_f(float v) { return 2.f * __frcp_rn(1.f + __expf(-2.f * v)) - 1.f; }
+
+__device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
+  return (unsigned)f32_to_bf16(lo) | ((unsigned)f32_to_bf16(hi) << 16);
+}
+
+__device__ __forceinline__ unsigned pack_fp8x4(float a, float b, float c, float d) {
+  int v = 0;
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, v, false);
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
+  return (unsigned)v;
+}
+
+template <bool FP8>
+struct Frag {
+  // bf16: 8 x bf16 = uint4; fp8: 8 x fp8 = uint2
+  typedef typename std::conditional<FP8, uint2, uint4>::type T;
+};
+
+template <bool FP8>
+__device__ __forceinline__ f32x16 mfma(const typename Frag<FP8>::T& a, const typename Frag<FP8>::T& b, f32x16 c) {
+  if constexpr (FP8) {
+    long av, bv;
+    __builtin_memcpy(&av, &a, 8);
+    __builtin_memcpy(&bv, &b, 8);
+    return __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(av, bv, c, 0, 0, 0);
+  } else {
+    bf16x8_t av, bv;
+    __builtin_memcpy(&av, &a, 16);
+    __builtin_memcpy(&bv, &b, 16);
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, c, 0, 0, 0);
+  }
+}
+
+// Build the B fragment for a k-step from 8 fp32 values (already scaled).
+template <bool FP8>
+__device__ __forceinline__ typename Frag<FP8>::T make_b(const float (&v)[8]) {
+  typename Frag<FP8>::T r;
+  if constexpr (FP8) {
+    r.x = pack_fp8x4(v[0], v[1], v[2], v[3]);
+    r.y = pack_fp8x4(v[4], v[5], v[6], v[7]);
+  } else {
+    r.x = pack_bf16x2(v[0], v[1]);
+    r.y = pack_bf16x2(v[2], v[3]);
+    r.z = pack_bf16x2(v[4], v[5]);
+    r.w = pack_bf16x2(v[6], v[7]);
+  }
+  return r;
+}
+
+// One LSTM recurrence over T steps for this wave's 32 series.
+// ENC: input x_t at k=64..64+F-1; DEC: zero input, read-out + error.
+template <bool FP8, bool ENC>
+__device__ __forceinline__ void run_phase(const LstmArgs& a, const typename Frag<FP8>::T* wlds,
+                                          const float* wout_lds, long long series, bool valid, int hh,
+                                          float (&hreg)[32], float (&creg)[32], float& errsum) {
+  using FT = typename Frag<FP8>::T;
+  const float sw = ENC ? a.scale_w_enc : a.scale_w_dec;
+  const float sa = a.scale_act;
+  const float deq = sw * sa;  // acc → real gates
+  const int lane = lane_id();
+  const float* xrow = a.x + series * (long long)a.T * a.F;
+  for (int t = 0; t < a.T; ++t) {
+    // B fragments: h (4 k-steps) and the input/bias k-step
+    FT hb[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = hreg[(2 * s + (j >> 2)) * 4 + (j & 3)] * (1.f / sa);
+      hb[s] = make_b<FP8>(v);
+    }
+    FT xb;
+    {
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (hh == 0) {
+        if (ENC && valid) {
+#pragma unroll
+          for (int f = 0; f < 7; ++f)
+            if (f < a.F) v[f] = xrow[t * a.F + f] * (1.f / sa);
+        }
+        v[7] = 1.f / sa;
+      }
+      xb = make_b<FP8>(v);
+    }
+    // tiles in pairs: two independent accumulator chains, 32 accumulator regs live.
+    // bf16: keep the A fragments in LDS (an opaque lane offset per step stops the
+    // compiler hoisting all 40 fragments = 160 VGPRs out of the time loop);
+    // fp8 fragments (80 VGPRs) may stay register-resident.
+    int lo = lane;
+    if constexpr (!FP8) asm volatile("" : "+v"(lo));
+#pragma unroll
+    for (int tp = 0; tp < TILES; tp += 2) {
+      f32x16 acc0 = (f32x16){}, acc1 = (f32x16){};
+#pragma unroll
+      for (int s = 0; s < KSTEPS; ++s) {
+        const FT bfr = (s < 4) ? hb[s] : xb;
+        acc0 = mfma<FP8>(wlds[(tp * KSTEPS + s) * 64 + lo], bfr, acc0);
+        acc1 = mfma<FP8>(wlds[((tp + 1) * KSTEPS + s) * 64 + lo], bfr, acc1);
+      }
+      // cell update (lane-local): unit (tt, q) <-> acc[4*gate + q]
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const f32x16& acc = e ? acc1 : acc0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float gi = acc[q] * deq, gf = acc[4 + q] * deq;
+          const float gg = acc[8 + q] * deq, go = acc[12 + q] * deq;
+          const int u = (tp + e) * 4 + q;
+          const float c = sigm(gf) * creg[u] + sigm(gi) * tanh_f(gg);
+          creg[u] = c;
+          hreg[u] = sigm(go) * tanh_f(c);
+        }
+      }
+    }
+    if (!ENC) {
+      // read-out y_f = sum_u h_u W_out[f][u] + b_out[f]; halves hold 32 units each
+#pragma unroll
+      for (int f = 0; f < 7; ++f) {
+        if (f >= a.F) break;
+        float p = 0.f;
+#pragma unroll
+        for (int tt = 0; tt < TILES; ++tt)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int unit = 16 * (tt >> 1) + 8 * hh + 4 * (tt & 1) + q;
+            p += hreg[tt * 4 + q] * wout_lds[f * H + unit];
+          }
+        p += __shfl_xor(p, 32, FM_WAVE);
+        const float y = p + a.b_out[f];
+        if (valid && hh == 0) {
+          const float d = y - xrow[t * a.F + f];
+          errsum += d * d;
+          if (a.recon) a.recon[(series * a.T + t) * a.F + f] = y;
+        }
+      }
+    }
+  }
+}
+
+template <bool FP8>
+__global__ __launch_bounds__(256, 2) void lstm_ae_kernel(const LstmArgs a) {
+  using FT = typename Frag<FP8>::T;
+  const int w = wave_id(), lane = lane_id();
+  const int hh = lane >> 5;
+  const long long series = ((long long)blockIdx.x * 4 + w) * 32 + (lane & 31);
+  const bool valid = series < a.N;
+  const long long sidx = valid ? series : 0;
+  constexpr int FB = FP8 ? FRAG_BYTES_FP8 : FRAG_BYTES_BF16;
+  FT* wlds = (FT*)fm_lstm_smem;
+  float* wout = (float*)(fm_lstm_smem + FB);
+
+  // stage encoder weights + read-out
+  {
+    const uint4* src = (const uint4*)a.w_enc;
+    uint4* dst = (uint4*)fm_lstm_smem;
+    for (int i = threadIdx.x; i < FB / 16; i += blockDim.x) dst[i] = src[i];
+    for (int i = threadIdx.x; i < a.F * H; i += blockDim.x) wout[i] = a.w_out[i];
+  }
+  __syncthreads();
+  float hreg[32], creg[32];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) { hreg[i] = 0.f; creg[i] = 0.f; }
+  float errsum = 0.f;
+  run_phase<FP8, true>(a, wlds, wout, sidx, valid, hh, hreg, creg, errsum);
+  __syncthreads();
+  {
+    const uint4* src = (const uint4*)a.w_dec;
+    uint4* dst = (uint4*)fm_lstm_smem;
+    for (int i = threadIdx.x; i < FB / 16; i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+  run_phase<FP8, false>(a, wlds, wout, sidx, valid, hh, hreg, creg, errsum);
+  if (valid && hh == 0) {
+    const float err = errsum / (float)(a.T * a.F);
+    a.err[series] = err;
+    const float z = (err - a.mu) / fmaxf(a.sigma, 1e-12f);
+    if (a.zscore) a.zscore[series] = z;
+    const float thr = a.threshold ? a.threshold[series] : a.thr_default;
+    const int v = z > thr ? 1 : 0;
+    if (a.verdict) a.verdict[series] = (signed char)v;
+    if (a.app_id) {
+      const int app = a.app_id[series];
+      if (v) atomicAdd(&a.app_stats[2 * app], 1);
+      atomicAdd(&a.app_stats[2 * app + 1], 1);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" size_t fm_lstm_lds_bytes(int F, int fp8) {
+  return (size_t)(fp8 ? FRAG_BYTES_FP8 : FRAG_BYTES_BF16) + (size_t)F * H * 4;
+}
+
+extern "C" int fm_lstm_ae(const LstmArgs* a, hipStream_t st) {
+  if (a->N <= 0) return 0;
+  if (a->F < 1 || a->F > 7 || a->T < 1) return (int)hipErrorInvalidValue;
+  const size_t lds = fm_lstm_lds_bytes(a->F, a->fp8);
+  dim3 grid((unsigned)((a->N + 127) / 128)), block(256);
+  if (a->fp8)
+    hipLaunchKernelGGL(lstm_ae_kernel<true>, grid, block, lds, st, *a);
+  else
+    hipLaunchKernelGGL(lstm_ae_kernel<false>, grid, block, lds, st, *a);
+  return (int)hipGetLastError();
+}
+
+extern "C" long long fm_lstm_args_size() { return (long long)sizeof(LstmArgs); }
+
+// debug helper: convert floats to fp8 e4m3 with the device instruction (for host-side agreement tests)
+__global__ void fp8_cvt_kernel(const float* in, unsigned char* out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const int v = __builtin_amdgcn_cvt_pk_fp8_f32(in[i], 0.f, 0, false);
+    out[i] = (unsigned char)(v & 0xff);
+  }
+}
+
+extern "C" int fm_fp8_convert(const float* in, unsigned char* out, int n, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(fp8_cvt_kernel, dim3((n + 255) / 256), dim3(256), 0, st, in, out, n);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,154 @@
+"""Host side of the fused LSTM-AE kernel (``csrc/lstm.hip``): weight packing
+into MFMA A-fragment order, fp8 quantisation, launcher."""
+
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import torch
+
+from . import _native as nat
+from .kernels import KernelShapeError, _need
+
+H = 64
+TILES, KSTEPS, KAUG = 8, 5, 80
+BIAS_K = 71  # bias column of the augmented weight (k-step 4, lane half 0, element 7)
+FP8_MAX = 448.0
+
+
+class LstmArgs(C.Structure):
+    _fields_ = [
+        ("x", C.c_void_p), ("N", C.c_int), ("T", C.c_int), ("F", C.c_int), ("fp8", C.c_int),
+        ("w_enc", C.c_void_p), ("w_dec", C.c_void_p), ("w_out", C.c_void_p), ("b_out", C.c_void_p),
+        ("scale_w_enc", C.c_float), ("scale_w_dec", C.c_float), ("scale_act", C.c_float),
+        ("mu", C.c_float), ("sigma", C.c_float), ("threshold", C.c_void_p), ("thr_default", C.c_float),
+        ("err", C.c_void_p), ("zscore", C.c_void_p), ("verdict", C.c_void_p), ("recon", C.c_void_p),
+        ("app_id", C.c_void_p), ("app_stats", C.c_void_p),
+    ]
+
+
+nat.register("fm_lstm_ae", [C.POINTER(LstmArgs), C.c_void_p])
+nat.register("fm_lstm_lds_bytes", [C.c_int, C.c_int], C.c_size_t)
+nat.register("fm_lstm_args_size", [], C.c_longlong)
+nat.register("fm_fp8_convert", [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p])
+
+
+def gate_row_perm() -> torch.Tensor:
+    """Row permutation: packed row (tile t, r) → PyTorch gate row ``gate*H + unit``."""
+    rows = []
+    for t in range(TILES):
+        for r in range(32):
+            gate, hh, q = r >> 3, (r >> 2) & 1, r & 3
+            u = 16 * (t >> 1) + 8 * hh + 4 * (t & 1) + q
+            rows.append(gate * H + u)
+    return torch.tensor(rows, dtype=torch.long)
+
+
+def _augment(w_hh: torch.Tensor, b: torch.Tensor, w_ih: Optional[torch.Tensor], F: int) -> torch.Tensor:
+    A = torch.zeros(4 * H, KAUG, dtype=torch.float32)
+    A[:, :H] = w_hh.detach().float().cpu()
+    if w_ih is not None:
+        A[:, H:H + F] = w_ih.detach().float().cpu()
+    A[:, BIAS_K] = b.detach().float().cpu()
+    return A
+
+
+def pack_fragments(A: torch.Tensor) -> torch.Tensor:
+    """``[256, 80]`` augmented weight → ``[TILES, KSTEPS, 64, 8]`` A fragments
+    (lane l: row (l & 31) of the permuted tile, k = 16 s + 8 (l >> 5) + j)."""
+    P = A[gate_row_perm()]  # [256, 80] permuted rows
+    out = torch.empty(TILES, KSTEPS, 64, 8, dtype=A.dtype)
+    lanes = torch.arange(64)
+    for t in range(TILES):
+        rows = P[32 * t + (lanes & 31)]  # [64, 80]
+        for s in range(KSTEPS):
+            k0 = 16 * s + 8 * (lanes >> 5)  # [64]
+            idx = k0[:, None] + torch.arange(8)[None, :]
+            out[t, s] = rows.gather(1, idx)
+    return out
+
+
+@dataclass
+class LstmPacked:
+    F: int
+    fp8: bool
+    w_enc: torch.Tensor
+    w_dec: torch.Tensor
+    w_out: torch.Tensor
+    b_out: torch.Tensor
+    scale_w_enc: float = 1.0
+    scale_w_dec: float = 1.0
+    scale_act: float = 1.0
+
+
+def pack(model, fp8: bool = False, device="cuda", act_scale: float = 1.0 / 32) -> LstmPacked:
+    F = model.F
+    if model.H != H:
+        raise KernelShapeError(f"fused LSTM kernel is built for H={H}")
+    if not 1 <= F <= 7:
+        raise KernelShapeError("fused LSTM kernel supports 1..7 features")
+    Ae = pack_fragments(_augment(model.enc_w_hh, model.enc_b, model.enc_w_ih, F))
+    Ad = pack_fragments(_augment(model.dec_w_hh, model.dec_b, None, F))
+    if fp8:
+        se = float(Ae.abs().max()) / FP8_MAX or 1.0
+        sd = float(Ad.abs().max()) / FP8_MAX or 1.0
+        qe = (Ae / se).to(torch.float8_e4m3fn).view(torch.uint8)
+        qd = (Ad / sd).to(torch.float8_e4m3fn).view(torch.uint8)
+        return LstmPacked(F=F, fp8=True, w_enc=qe.contiguous().to(device), w_dec=qd.contiguous().to(device),
+                          w_out=model.out_w.detach().float().contiguous().to(device),
+                          b_out=model.out_b.detach().float().contiguous().to(device),
+                          scale_w_enc=se, scale_w_dec=sd, scale_act=act_scale)
+    return LstmPacked(F=F, fp8=False, w_enc=Ae.to(torch.bfloat16).contiguous().to(device),
+                      w_dec=Ad.to(torch.bfloat16).contiguous().to(device),
+                      w_out=model.out_w.detach().float().contiguous().to(device),
+                      b_out=model.out_b.detach().float().contiguous().to(device))
+
+
+def lstm_score(p: LstmPacked, x: torch.Tensor, mu: float = 0.0, sigma: float = 1.0,
+               threshold: Optional[torch.Tensor] = None, thr_default: float = 3.0, want_recon: bool = False,
+               app_id: Optional[torch.Tensor] = None, app_stats: Optional[torch.Tensor] = None,
+               out: Optional[Dict[str, torch.Tensor]] = None) -> Dict[str, torch.Tensor]:
+    lib = nat.require()
+    _need(x.is_cuda and x.dtype == torch.float32 and x.dim() == 3 and x.is_contiguous(),
+          "x must be a contiguous float32 [N, T, F] GPU tensor")
+    N, T, F = x.shape
+    _need(F == p.F, f"feature mismatch {F} vs {p.F}")
+    dev = x.device
+    if threshold is not None:
+        _need(threshold.shape == (N,) and threshold.dtype == torch.float32 and threshold.is_contiguous()
+              and threshold.device == dev, "threshold must be float32 [N]")
+    if app_id is not None:
+        _need(app_id.shape == (N,) and app_id.dtype == torch.int32 and app_stats is not None
+              and app_stats.dtype == torch.int32 and app_stats.is_contiguous(), "app_id/app_stats")
+    out = {} if out is None else out
+    out.setdefault("err", torch.empty(N, dtype=torch.float32, device=dev))
+    out.setdefault("zscore", torch.empty(N, dtype=torch.float32, device=dev))
+    out.setdefault("verdict", torch.empty(N, dtype=torch.int8, device=dev))
+    if want_recon:
+        out.setdefault("recon", torch.empty((N, T, F), dtype=torch.float32, device=dev))
+    a = LstmArgs()
+    a.x = x.data_ptr()
+    a.N, a.T, a.F, a.fp8 = N, T, F, int(p.fp8)
+    a.w_enc, a.w_dec = p.w_enc.data_ptr(), p.w_dec.data_ptr()
+    a.w_out, a.b_out = p.w_out.data_ptr(), p.b_out.data_ptr()
+    a.scale_w_enc, a.scale_w_dec, a.scale_act = p.scale_w_enc, p.scale_w_dec, p.scale_act
+    a.mu, a.sigma = float(mu), float(sigma)
+    a.threshold = nat.ptr(threshold)
+    a.thr_default = float(thr_default)
+    a.err, a.zscore, a.verdict = nat.ptr(out["err"]), nat.ptr(out["zscore"]), nat.ptr(out["verdict"])
+    a.recon = nat.ptr(out.get("recon")) if want_recon else 0
+    a.app_id, a.app_stats = nat.ptr(app_id), nat.ptr(app_stats)
+    nat.check(lib.fm_lstm_ae(C.byref(a), nat.stream_handle(dev)), "fm_lstm_ae")
+    return out
+
+
+def device_fp8(values: torch.Tensor) -> torch.Tensor:
+    """Convert with the device's ``v_cvt_pk_fp8_f32`` (format agreement tests)."""
+    lib = nat.require()
+    v = values.float().contiguous()
+    out = torch.empty(v.numel(), dtype=torch.uint8, device=v.device)
+    nat.check(lib.fm_fp8_convert(v.data_ptr(), out.data_ptr(), v.numel(), nat.stream_handle(v.device)),
+              "fm_fp8_convert")
+    return out

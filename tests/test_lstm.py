@@ -1,0 +1,150 @@
+"""LSTM autoencoder: reference model, DP training loop, fused-kernel layout.
+
+The CPU tests emulate the documented gfx950 ``v_mfma_f32_32x32x16`` lane maps
+(A: lane l holds A[l&31][8(l>>5)+j]; B: B[8(l>>5)+j][l&31]; C: col l&31,
+row (r&3)+8(r>>2)+4(l>>5)) to check the host packing and the kernel's
+register plan (gates lane-local, new h = next B operand) before any GPU run.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from foremast_amd.models import lstm_ae
+from foremast_amd.ops import lstm as L
+
+
+def _emulate_mfma(afrag, bfrag, c):
+    """afrag/bfrag: [64, 8] per-lane operand elements; c: [64, 16] accumulators."""
+    A = np.zeros((32, 16))
+    B = np.zeros((16, 32))
+    for l in range(64):
+        for j in range(8):
+            A[l & 31, 8 * (l >> 5) + j] = afrag[l, j]
+            B[8 * (l >> 5) + j, l & 31] = bfrag[l, j]
+    Cm = A @ B
+    out = c.copy()
+    for l in range(64):
+        for r in range(16):
+            out[l, r] += Cm[(r & 3) + 8 * (r >> 2) + 4 * (l >> 5), l & 31]
+    return out
+
+
+def _sig(x):
+    return 1 / (1 + np.exp(-x))
+
+
+def test_register_plan_matches_reference_step():
+    torch.manual_seed(0)
+    F = 3
+    m = lstm_ae.LSTMAutoencoder(F, 64).double()
+    frag = L.pack_fragments(L._augment(m.enc_w_hh, m.enc_b, m.enc_w_ih, F)).double().numpy()
+    B = 32
+    x = torch.randn(B, F, dtype=torch.float64)
+    h0 = torch.randn(B, 64, dtype=torch.float64) * 0.5
+    c0 = torch.randn(B, 64, dtype=torch.float64) * 0.5
+    # reference one step
+    gates = x @ m.enc_w_ih.t() + h0 @ m.enc_w_hh.t() + m.enc_b
+    h_ref, c_ref = m._cell(gates, c0)
+    # kernel register plan: lane l -> series l&31, half hh = l>>5 owns units 16s+8hh+4e+q
+    hreg = np.zeros((64, 32))
+    creg = np.zeros((64, 32))
+    for l in range(64):
+        hh = l >> 5
+        for t in range(8):
+            for q in range(4):
+                u = 16 * (t >> 1) + 8 * hh + 4 * (t & 1) + q
+                hreg[l, 4 * t + q] = h0[l & 31, u]
+                creg[l, 4 * t + q] = c0[l & 31, u]
+    hb = np.zeros((4, 64, 8))
+    for s in range(4):
+        for j in range(8):
+            hb[s, :, j] = hreg[:, (2 * s + (j >> 2)) * 4 + (j & 3)]
+    xb = np.zeros((64, 8))
+    for l in range(32):
+        xb[l, :F] = x[l].numpy()
+        xb[l, 7] = 1.0
+    hnew = np.zeros_like(hreg)
+    for t in range(8):
+        acc = np.zeros((64, 16))
+        for s in range(5):
+            acc = _emulate_mfma(frag[t, s], hb[s] if s < 4 else xb, acc)
+        for q in range(4):
+            gi, gf, gg, go = acc[:, q], acc[:, 4 + q], acc[:, 8 + q], acc[:, 12 + q]
+            c = _sig(gf) * creg[:, 4 * t + q] + _sig(gi) * np.tanh(gg)
+            hnew[:, 4 * t + q] = _sig(go) * np.tanh(c)
+    for l in range(64):
+        hh = l >> 5
+        for t in range(8):
+            for q in range(4):
+                u = 16 * (t >> 1) + 8 * hh + 4 * (t & 1) + q
+                assert abs(hnew[l, 4 * t + q] - h_ref[l & 31, u].item()) < 1e-9
+
+
+def test_lstm_ae_trains_and_scores():
+    torch.manual_seed(1)
+    N, Lh, F, T = 16, 300, 2, 16
+    t = torch.arange(Lh, dtype=torch.float32)
+    base = torch.stack([torch.sin(2 * np.pi * t / 24 + i) for i in range(N)])
+    series = torch.stack([base, 0.5 * base + 0.1 * torch.randn(N, Lh)], 2)
+    z, mu, sd = lstm_ae.normalize(series)
+    m = lstm_ae.LSTMAutoencoder(F, 32)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-2)
+    g = torch.Generator().manual_seed(0)
+    first = None
+    for it in range(60):
+        w = lstm_ae.make_windows(z, T, 64, g)
+        loss = m.recon_error(w).mean()
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        first = first if first is not None else float(loss)
+    assert float(loss) < 0.6 * first
+    with torch.no_grad():
+        normal = lstm_ae.make_windows(z, T, 64, g)
+        cal = lstm_ae.calibrate(m.recon_error(normal))
+        spike = normal.clone()
+        spike[:, T // 2:, 0] += 6.0
+        e = m.recon_error(spike)
+    zs = (e - cal.mu) / cal.sigma
+    assert float(zs.min()) > 3.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fp8", [False, True])
+def test_fused_lstm_kernel_matches_reference(fp8):
+    torch.manual_seed(2)
+    dev = torch.device("cuda:0")
+    N, T, F = 300, 24, 3
+    m = lstm_ae.LSTMAutoencoder(F, 64)
+    x = torch.randn(N, T, F)
+    x[:40, 10:14] += 4.0
+    with torch.no_grad():
+        ref_err = m.recon_error(x)
+        ref_y = m(x)
+    p = L.pack(m, fp8=fp8, device=dev)
+    out = L.lstm_score(p, x.to(dev).contiguous(), mu=float(ref_err.mean()), sigma=float(ref_err.std()),
+                       want_recon=True)
+    torch.cuda.synchronize()
+    err = out["err"].cpu()
+    y = out["recon"].cpu()
+    if not fp8:
+        np.testing.assert_allclose(y.numpy(), ref_y.numpy(), atol=3e-2, rtol=3e-2)
+        np.testing.assert_allclose(err.numpy(), ref_err.numpy(), rtol=5e-2, atol=1e-3)
+    else:
+        corr = np.corrcoef(err.numpy(), ref_err.numpy())[0, 1]
+        assert corr > 0.98
+        assert (y - ref_y).abs().mean() < 0.08
+    # ranking: the perturbed windows are the highest errors in both
+    top_ref = set(torch.topk(ref_err, 40).indices.tolist())
+    top_k = set(torch.topk(err, 40).indices.tolist())
+    assert len(top_ref & top_k) >= 36
+
+
+@pytest.mark.gpu
+def test_device_fp8_matches_torch_ocp():
+    dev = torch.device("cuda:0")
+    v = torch.tensor([0.0, 1.0, -1.5, 0.3, 447.0, -240.0, 1e-3, 3.14159], device=dev)
+    got = L.device_fp8(v).cpu()
+    exp = v.cpu().to(torch.float8_e4m3fn).view(torch.uint8)
+    assert torch.equal(got, exp)

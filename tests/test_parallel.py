@@ -1,0 +1,100 @@
+"""Multi-process paths on CPU (gloo): health aggregation, sharding and the
+bench's distributed contract (rank 0 prints ONE JSON line)."""
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from foremast_amd.parallel.health import HealthAggregator, shard_range
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n_total, A = 23, 5
+        s, e, per = shard_range(n_total, world, rank, align=5)
+        n = e - s
+        agg = HealthAggregator(n, per, "cpu")
+        stats = torch.zeros((A, 2), dtype=torch.int32)
+        app = torch.arange(s, e) // 5
+        verdict = torch.tensor([1 if (i % 7 == 0) else 0 for i in range(s, e)], dtype=torch.int8)
+        for a, v in zip(app.tolist(), verdict.tolist()):
+            stats[a, 0] += int(v == 1)
+            stats[a, 1] += 1
+        red, allv = agg.tick(stats, verdict)
+        q.put((rank, red.tolist(), allv.tolist(), per))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_health_aggregation_gloo():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    exp = [[0, 0] for _ in range(5)]
+    for i in range(23):
+        exp[i // 5][0] += int(i % 7 == 0)
+        exp[i // 5][1] += 1
+    for rank, red, allv, per in res:
+        assert red == exp
+        # gathered verdict table: rank blocks of `per` padded with -1
+        flat = [v for v in allv]
+        got = [flat[r * per + j] for r in range(world) for j in range(per)]
+        valid = [g for g in got if g != -1]
+        assert len(valid) == 23
+
+
+def test_shard_range_alignment():
+    world = 8
+    spans = [shard_range(100_000, world, r, align=5) for r in range(world)]
+    assert spans[0][0] == 0 and spans[-1][1] == 100_000
+    for (s, e, per), (s2, _, _) in zip(spans, spans[1:]):
+        assert e == s2 and s % 5 == 0
+    assert sum(e - s for s, e, _ in spans) == 100_000
+
+
+@pytest.mark.slow
+def test_bench_distributed_cpu():
+    port = _free_port()
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--cpu", "--series", "200", "--ring", "480",
+           "--season", "48"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["config"]["parallelism"] == "dp2"
+    assert d["health"]["series_scored_last_tick"] == 200
+    for k in ("metric", "value", "unit", "ms_per_step", "higher_is_better", "scaling", "vs_baseline", "dtype",
+              "data", "config"):
+        assert k in d
