@@ -22,6 +22,14 @@ One scoring tick = the full canary pipeline for every series of the job:
 Nothing is cached across ticks: every tick refits every model on new data.
 Strong scaling: the 100k series are sharded over the ranks.
 
+Other BASELINE configs (same metric/JSON contract, ``--config``):
+
+* ``lstm`` (config 3): 100k univariate series, LSTM autoencoder; every tick
+  runs one DP Adam step (gradient all-reduce over RCCL) and re-scores every
+  series' latest window with the fused MFMA kernel;
+* ``multivariate`` (config 5): 50k entities x (latency, error-rate) = 100k
+  metric-series, LSTM-AE scored with fp8 e4m3 MFMA.
+
 Usage: ``python bench.py --gpus N --steps K --warmup W`` (N > 1 under
 ``torch.distributed.run``; rank 0 prints ONE JSON line).
 """
@@ -67,6 +75,13 @@ def parse():
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--graph", action="store_true", help="capture the GPU part of a tick in a HIP graph")
     p.add_argument("--cpu", action="store_true", help="force CPU (reference path; tiny sizes only)")
+    p.add_argument("--config", default="canary", choices=["canary", "lstm", "multivariate"],
+                   help="canary = headline (BASELINE configs 2/4 at 100k); lstm = config 3; "
+                        "multivariate = config 5 (fp8 LSTM, latency + error-rate)")
+    p.add_argument("--lstm-window", type=int, default=32)
+    p.add_argument("--lstm-train-batch", type=int, default=4096)
+    p.add_argument("--lstm-train-every", type=int, default=1)
+    p.add_argument("--lstm-pretrain", type=int, default=10)
     return p.parse_args()
 
 
@@ -117,9 +132,8 @@ def make_ticks(n, pods, nticks, season, start_t, dev, seed, anomaly_frac, hist_t
     return out.float()
 
 
-def main():
-    args = parse()
-    world, rank, dev = init_dist(args)
+def setup_canary(args, world, rank, dev):
+    """Config 4 / headline: HW + pairwise canary scorer over the sharded 100k series."""
     if dev.type == "cpu" and args.series > 4096:
         # the CPU path is the reference implementation: keep it small
         args.series, args.ring, args.season = 256, 480, 48
@@ -174,6 +188,98 @@ def main():
             torch.cuda.current_stream().synchronize()
         return out
 
+    meta = {
+        "model": f"{args.algorithm} + pairwise {args.pairwise} (MW U / Wilcoxon / Kruskal) canary scorer",
+        "global_batch": args.series,
+        "seq_len": args.ring,
+        "season": args.season,
+        "pods": P,
+        "current_window": W,
+        "grid_points": int(shard.grid.shape[0]),
+    }
+    dt = "bf16" if dtype == torch.bfloat16 else "fp32"
+    return tick, health_host, meta, dt, args.series
+
+
+def setup_lstm(args, world, rank, dev, n_features, fp8):
+    """Config 3 (univariate LSTM-AE, DP training + scoring) and config 5
+    (multivariate latency + error-rate entities, fp8 MFMA scoring).
+
+    Per tick: ingest one point per metric-series, one DP training step
+    (gradient all-reduce over RCCL), device-side weight repack, fused LSTM-AE
+    scoring of every entity's latest window, cluster aggregation, D2H."""
+    from foremast_amd.brain.lstm_engine import LstmShard
+    F = n_features
+    if dev.type == "cpu" and args.series > 4096:
+        args.series, args.ring, args.season, args.lstm_train_batch = 256, 480, 48, 64
+    n_ent = args.series // F  # entities; each has F metric-series
+    s, e, per = shard_range(n_ent, world, rank, align=1)
+    n_local = e - s
+    ent_per_app = max(1, METRICS_PER_APP // F)
+    n_apps = (n_ent + ent_per_app - 1) // ent_per_app
+    app_id = (torch.arange(s, e, device=dev, dtype=torch.int64) // ent_per_app).to(torch.int32)
+    shard = LstmShard(n_local, args.ring, F, window=args.lstm_window, hidden=64, fp8=fp8, device=dev,
+                      app_id=app_id, n_apps=n_apps, threshold=4.0, train_batch=args.lstm_train_batch,
+                      lr=1e-3, seed=0)
+    hist = [synthetic_history(n_local, args.ring, args.season, dev, seed=1234 + 7 * f + 101 * rank)
+            for f in range(F)]
+    shard.load_history(hist)
+    total = args.warmup + args.steps
+    ticks = torch.stack([make_ticks(n_local, 1, total, args.season, args.ring, dev, 99 + rank + 13 * f,
+                                    args.anomaly_frac, hist[f])[..., 0] for f in range(F)], 2)  # [ticks, n, F]
+    del hist
+    pin = dev.type == "cuda"
+    host_ticks = ticks.cpu()
+    if pin:
+        host_ticks = host_ticks.pin_memory()
+    del ticks
+    newx = torch.empty((n_local, F), dtype=torch.float32, device=dev)
+    agg = HealthAggregator(n_local, per, dev)
+    health_host = torch.empty_like(shard.app_stats, device="cpu")
+    if pin:
+        health_host = health_host.pin_memory()
+    # model initialisation (outside the timed region): a few DP steps + calibration
+    for _ in range(args.lstm_pretrain):
+        shard.train_step()
+    shard.calibrate(args.lstm_train_batch)
+
+    def tick(k):
+        newx.copy_(host_ticks[k], non_blocking=pin)
+        shard.ingest_tick(newx)
+        if k % args.lstm_train_every == 0:
+            shard.train_step()
+        out = shard.score()
+        stats, _ = agg.tick(shard.app_stats, out["verdict"])
+        health_host.copy_(stats, non_blocking=pin)
+        if dev.type == "cuda":
+            torch.cuda.current_stream().synchronize()
+        return out
+
+    meta = {
+        "model": f"LSTM autoencoder (F={F}, H=64, window {args.lstm_window}), DP Adam step "
+                 f"(batch {args.lstm_train_batch}/rank) every {args.lstm_train_every} tick(s) + fused scoring",
+        "global_batch": n_ent,
+        "seq_len": args.lstm_window,
+        "history": args.ring,
+        "entities": n_ent,
+        "features": F,
+        "train_batch_per_rank": args.lstm_train_batch,
+        "scoring_dtype": "fp8_e4m3" if fp8 else "bf16",
+    }
+    dt = "bf16"  # training fp32 master / bf16 MFMA scoring (fp8 weights+activations for config 5)
+    return tick, health_host, meta, dt, n_ent * F
+
+
+def main():
+    args = parse()
+    world, rank, dev = init_dist(args)
+    if args.config == "canary":
+        tick, health_host, meta, dtype_name, n_series = setup_canary(args, world, rank, dev)
+    elif args.config == "lstm":
+        tick, health_host, meta, dtype_name, n_series = setup_lstm(args, world, rank, dev, 1, False)
+    else:
+        tick, health_host, meta, dtype_name, n_series = setup_lstm(args, world, rank, dev, 2, True)
+
     for k in range(args.warmup):
         tick(k)
     barrier(dev)
@@ -199,7 +305,11 @@ def main():
     anomalous_apps = int((health_host[:, 0] > 0).sum())
     scored = int(health_host[:, 1].sum())
     if rank == 0:
-        value = args.series * args.steps / elapsed
+        value = n_series * args.steps / elapsed
+        config = {"model": meta.pop("model"), "global_batch": meta.pop("global_batch"),
+                  "seq_len": meta.pop("seq_len"), "parallelism": f"dp{world}", "bench_config": args.config}
+        config.update(meta)
+        config["device"] = str(dev) if dev.type == "cpu" else torch.cuda.get_device_name(dev)
         res = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -211,19 +321,9 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None if BASELINE_VALUE is None else round(value / BASELINE_VALUE, 3),
-            "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
-            "data": "synthetic (seasonal Prometheus-like range-vectors, random per-series params)",
-            "config": {
-                "model": f"{args.algorithm} + pairwise {args.pairwise} (MW U / Wilcoxon / Kruskal) canary scorer",
-                "global_batch": args.series,
-                "seq_len": args.ring,
-                "parallelism": f"dp{world}",
-                "season": args.season,
-                "pods": P,
-                "current_window": W,
-                "grid_points": int(shard.grid.shape[0]),
-                "device": str(dev) if dev.type == "cpu" else torch.cuda.get_device_name(dev),
-            },
+            "dtype": dtype_name,
+            "data": "synthetic (seasonal Prometheus-like range-vectors, random per-series params; random-init weights)",
+            "config": config,
             "p50_detect_latency_ms": round(float(np.percentile(lat_ms, 50)), 3),
             "p99_detect_latency_ms": round(float(np.percentile(lat_ms, 99)), 3),
             "health": {"apps": int(health_host.shape[0]), "anomalous_apps": anomalous_apps,

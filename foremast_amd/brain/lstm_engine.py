@@ -1,0 +1,163 @@
+"""Streaming LSTM-autoencoder scoring for one shard (BASELINE configs 3 and 5).
+
+Per tick:
+
+1. ingest one new point per (series, metric) into the per-metric HBM rings;
+2. one data-parallel training step of the shared LSTM-AE on a minibatch of
+   history windows sampled from this rank's shard (gradient all-reduce over
+   RCCL, :mod:`foremast_amd.parallel.dp`);
+3. repack the updated weights into MFMA fragment order on the device;
+4. score every series' latest window with the fused kernel (bf16, or fp8
+   e4m3 for the multivariate service-mesh config) → reconstruction z-score
+   → verdict → per-app counters.
+
+Per-series normalisation statistics (mean/std per metric) come from the
+``window_stats`` kernel over the history ring and are refreshed every
+``restat_every`` ticks.
+"""
+
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..ingest.ringbuffer import HistoryRing
+from ..models.lstm_ae import LSTMAutoencoder
+from ..parallel.dp import DPTrainer
+
+
+class LstmShard:
+    def __init__(self, n_series: int, ring_len: int, n_features: int, window: int = 32, hidden: int = 64,
+                 fp8: bool = False, device="cuda", app_id: Optional[torch.Tensor] = None, n_apps: int = 1,
+                 threshold: float = 4.0, train_batch: int = 4096, lr: float = 1e-3, restat_every: int = 16,
+                 seed: int = 0, dtype=torch.bfloat16) -> None:
+        self.n, self.R, self.F, self.T = n_series, ring_len, n_features, window
+        self.device = torch.device(device)
+        self.gpu = self.device.type == "cuda"
+        self.rings: List[HistoryRing] = [HistoryRing(n_series, ring_len, dtype, self.device)
+                                         for _ in range(n_features)]
+        torch.manual_seed(seed)
+        self.model = LSTMAutoencoder(n_features, hidden).to(self.device)
+        self.trainer = DPTrainer(self.model, lr=lr)
+        self.fp8 = fp8
+        self.train_batch = train_batch
+        self.threshold = threshold
+        self.restat_every = restat_every
+        self.app_id = app_id if app_id is not None else torch.zeros(n_series, dtype=torch.int32,
+                                                                    device=self.device)
+        self.app_stats = torch.zeros((max(n_apps, 1), 2), dtype=torch.int32, device=self.device)
+        self.mean = torch.zeros(n_series, n_features, device=self.device)
+        self.std = torch.ones(n_series, n_features, device=self.device)
+        self.mu, self.sigma = 0.0, 1.0
+        self.ticks = 0
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(seed + 1)
+        self.packed = None
+        self.out: Dict[str, torch.Tensor] = {}
+        self._ar = torch.arange(window, device=self.device)
+        self._det = None
+        self._ws: Dict[str, torch.Tensor] = {}
+        self._all = torch.arange(n_series, device=self.device)
+        self._zero_off = torch.zeros(n_series, dtype=torch.long, device=self.device)
+
+    # ------------------------------------------------------------------ data
+    def load_history(self, values) -> None:
+        """``values``: ``[n, T_hist, F]`` or a list of F ``[n, T_hist]`` tensors."""
+        for f, ring in enumerate(self.rings):
+            ring.load(values[f] if isinstance(values, (list, tuple)) else values[..., f])
+        self.refresh_stats()
+
+    def refresh_stats(self) -> None:
+        """Per-series mean/std of each metric over the whole history ring
+        (``window_stats`` kernel on the GPU: one HBM pass, no fp32 copy)."""
+        if self.gpu:
+            from ..ops import kernels as K
+            if self._det is None:
+                n, dev = self.n, self.device
+                self._det = K.DetectSpec(horizons=torch.ones(1, dtype=torch.int32, device=dev),
+                                         threshold=torch.zeros(n, device=dev),
+                                         bound=torch.zeros(n, dtype=torch.int8, device=dev),
+                                         min_lower=torch.zeros(n, device=dev), want_band=False)
+            for f, ring in enumerate(self.rings):
+                o = K.window_stats(ring.data, ring.head, ring.length, self._det, out=self._ws)
+                self.mean[:, f] = o["mean"]
+                self.std[:, f] = o["std"].clamp(min=1e-6)
+            return
+        for f, ring in enumerate(self.rings):
+            yf = ring.logical().float()
+            self.mean[:, f] = yf.mean(1)
+            self.std[:, f] = yf.std(1, unbiased=False).clamp(min=1e-6)
+
+    def ingest_tick(self, newv: torch.Tensor) -> None:
+        """``newv``: ``[n, F]`` float32."""
+        for f, ring in enumerate(self.rings):
+            col = ring.next_col()
+            if self.gpu:
+                from ..ops import kernels as K
+                K.ring_append(ring.data, col, newv[:, f:f + 1])
+            else:
+                ring.data[:, col] = newv[:, f].to(ring.data.dtype)
+            ring.advance(1)
+        self.ticks += 1
+        if self.ticks % self.restat_every == 0:
+            self.refresh_stats()
+
+    def _gather(self, series_idx: torch.Tensor, end_offsets: torch.Tensor) -> torch.Tensor:
+        """Windows ending ``end_offsets`` samples before the newest one → ``[B, T, F]`` normalised."""
+        ring0 = self.rings[0]
+        L = ring0.length
+        start = L - self.T - end_offsets  # logical start index
+        cols = (ring0.head + start[:, None] + self._ar[None, :]) % ring0.R  # [B, T]
+        feats = [ring.data[series_idx[:, None], cols].float() for ring in self.rings]
+        x = torch.stack(feats, 2)  # [B, T, F]
+        return ((x - self.mean[series_idx][:, None, :]) / self.std[series_idx][:, None, :]).contiguous()
+
+    # ------------------------------------------------------------------ train / score
+    def _sample(self, B: int) -> torch.Tensor:
+        L = self.rings[0].length
+        si = torch.randint(0, self.n, (B,), generator=self.gen, device=self.device)
+        off = torch.randint(0, max(1, L - self.T), (B,), generator=self.gen, device=self.device)
+        return self._gather(si, off)
+
+    def train_step(self) -> torch.Tensor:
+        """One DP step on ``train_batch`` history windows of this shard."""
+        return self.trainer.step(self._sample(self.train_batch))
+
+    def calibrate(self, n: int = 4096) -> None:
+        """Reconstruction-error mean/std over ``n`` history windows per rank,
+        combined across ranks (one 3-float all-reduce) so every rank applies
+        the same threshold."""
+        with torch.no_grad():
+            e = self.model.recon_error(self._sample(n)).double()
+        mom = torch.stack([e.sum(), (e * e).sum(), torch.tensor(float(e.numel()), dtype=torch.float64,
+                                                                device=e.device)])
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            dist.all_reduce(mom)
+        s1, s2, cnt = mom.tolist()
+        self.mu = s1 / cnt
+        self.sigma = max(s2 / cnt - self.mu * self.mu, 0.0) ** 0.5 + 1e-12
+
+    def score(self) -> Dict[str, torch.Tensor]:
+        self.app_stats.zero_()
+        x = self._gather(self._all, self._zero_off)
+        if self.gpu:
+            from ..ops import lstm as L
+            if self.packed is None:
+                self.packed = L.pack(self.model, fp8=self.fp8, device=self.device)
+            else:
+                L.repack_into(self.packed, self.model)
+            self.out = L.lstm_score(self.packed, x, self.mu, self.sigma, thr_default=self.threshold,
+                                    app_id=self.app_id, app_stats=self.app_stats, out=self.out)
+            return self.out
+        with torch.no_grad():
+            err = self.model.recon_error(x)
+        z = (err - self.mu) / max(self.sigma, 1e-12)
+        v = (z > self.threshold).to(torch.int8)
+        ids = self.app_id.long()
+        self.app_stats.index_put_((ids, torch.zeros_like(ids)), v.int(), accumulate=True)
+        self.app_stats.index_put_((ids, torch.ones_like(ids)), torch.ones_like(v, dtype=torch.int32),
+                                  accumulate=True)
+        self.out = {"err": err, "zscore": z, "verdict": v}
+        return self.out

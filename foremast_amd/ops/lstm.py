@@ -70,6 +70,58 @@ def pack_fragments(A: torch.Tensor) -> torch.Tensor:
     return out
 
 
+_IDX_CACHE: Dict[str, torch.Tensor] = {}
+
+
+def _frag_index(device) -> torch.Tensor:
+    """Flat gather index into a row-major [256, 80] augmented weight that
+    produces the A-fragment layout (device-side repacking every train step)."""
+    key = str(device)
+    idx = _IDX_CACHE.get(key)
+    if idx is None:
+        rows = gate_row_perm()
+        lanes = torch.arange(64)
+        out = torch.empty(TILES, KSTEPS, 64, 8, dtype=torch.long)
+        for t in range(TILES):
+            r = rows[32 * t + (lanes & 31)]
+            for s in range(KSTEPS):
+                k = 16 * s + 8 * (lanes >> 5)
+                out[t, s] = r[:, None] * KAUG + k[:, None] + torch.arange(8)[None, :]
+        idx = out.flatten().to(device)
+        _IDX_CACHE[key] = idx
+    return idx
+
+
+def _augment_dev(w_hh, b, w_ih, F) -> torch.Tensor:
+    A = torch.zeros(4 * H, KAUG, dtype=torch.float32, device=w_hh.device)
+    A[:, :H] = w_hh.detach()
+    if w_ih is not None:
+        A[:, H:H + F] = w_ih.detach()
+    A[:, BIAS_K] = b.detach()
+    return A
+
+
+def repack_into(p: "LstmPacked", model) -> "LstmPacked":
+    """Refresh ``p`` in place from (device) model parameters: one gather per
+    matrix, no host round trip except the fp8 scale."""
+    F = model.F
+    idx = _frag_index(p.w_enc.device)
+    Ae = _augment_dev(model.enc_w_hh, model.enc_b, model.enc_w_ih, F).flatten()[idx]
+    Ad = _augment_dev(model.dec_w_hh, model.dec_b, None, F).flatten()[idx]
+    if p.fp8:
+        m = torch.stack([Ae.abs().max(), Ad.abs().max()]).clamp(min=1e-30) / FP8_MAX
+        se, sd = m.tolist()
+        p.w_enc.copy_((Ae / se).to(torch.float8_e4m3fn).view(torch.uint8).view_as(p.w_enc))
+        p.w_dec.copy_((Ad / sd).to(torch.float8_e4m3fn).view(torch.uint8).view_as(p.w_dec))
+        p.scale_w_enc, p.scale_w_dec = se, sd
+    else:
+        p.w_enc.copy_(Ae.to(torch.bfloat16).view_as(p.w_enc))
+        p.w_dec.copy_(Ad.to(torch.bfloat16).view_as(p.w_dec))
+    p.w_out.copy_(model.out_w.detach())
+    p.b_out.copy_(model.out_b.detach())
+    return p
+
+
 @dataclass
 class LstmPacked:
     F: int

@@ -148,3 +148,58 @@ def test_device_fp8_matches_torch_ocp():
     got = L.device_fp8(v).cpu()
     exp = v.cpu().to(torch.float8_e4m3fn).view(torch.uint8)
     assert torch.equal(got, exp)
+
+
+def _toy_history(n, R, F, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    t = torch.arange(R, dtype=torch.float32)
+    ph = torch.rand(n, 1, generator=g) * 6.28
+    return [10 + 3 * torch.sin(2 * np.pi * t / 48 + ph + f) + 0.1 * torch.randn(n, R, generator=g)
+            for f in range(F)]
+
+
+def test_lstm_shard_cpu_streaming():
+    from foremast_amd.brain.lstm_engine import LstmShard
+    n, R, F = 40, 200, 2
+    sh = LstmShard(n, R, F, window=12, device="cpu", app_id=(torch.arange(n) // 4).int(), n_apps=10,
+                   train_batch=32, lr=1e-2)
+    sh.load_history(_toy_history(n, R, F))
+    l0 = float(sh.train_step())
+    for k in range(25):
+        sh.ingest_tick(torch.randn(n, F) * 0.1 + 10)
+        l1 = float(sh.train_step())
+    assert l1 < l0
+    sh.calibrate(64)
+    out = sh.score()
+    assert out["verdict"].shape == (n,) and int(sh.app_stats[:, 1].sum()) == n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fp8", [False, True])
+def test_lstm_shard_gpu_matches_model(fp8):
+    """Streaming shard on the GPU: rings + window_stats + device repack +
+    fused kernel agree with the PyTorch model on the same windows."""
+    from foremast_amd.brain.lstm_engine import LstmShard
+    dev = torch.device("cuda:0")
+    n, R, F = 512, 300, 2
+    sh = LstmShard(n, R, F, window=16, device=dev, fp8=fp8, app_id=(torch.arange(n, device=dev) // 4).int(),
+                   n_apps=128, train_batch=256, lr=1e-2)
+    sh.load_history([h.to(dev) for h in _toy_history(n, R, F)])
+    # stats from the native window_stats kernel equal torch's
+    ref_mean = torch.stack([r.logical().float().mean(1) for r in sh.rings], 1)
+    assert torch.allclose(sh.mean, ref_mean, rtol=1e-4, atol=1e-3)
+    for k in range(5):
+        sh.ingest_tick(torch.full((n, F), 10.0, device=dev))
+        sh.train_step()
+    sh.calibrate(512)
+    out = sh.score()
+    torch.cuda.synchronize()
+    x = sh._gather(sh._all, sh._zero_off)
+    with torch.no_grad():
+        ref = sh.model.recon_error(x)
+    err = out["err"]
+    if fp8:
+        assert np.corrcoef(err.cpu().numpy(), ref.cpu().numpy())[0, 1] > 0.95
+    else:
+        assert torch.allclose(err, ref, rtol=5e-2, atol=2e-3)
+    assert int(sh.app_stats[:, 1].sum()) == n

@@ -7,6 +7,7 @@ import socket
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -81,20 +82,77 @@ def test_shard_range_alignment():
 
 
 @pytest.mark.slow
-def test_bench_distributed_cpu():
+@pytest.mark.parametrize("config", ["canary", "lstm"])
+def test_bench_distributed_cpu(config):
     port = _free_port()
     env = dict(os.environ, OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "2", "--warmup", "1", "--cpu", "--series", "200", "--ring", "480",
-           "--season", "48"]
+           "--season", "48", "--config", config, "--lstm-train-batch", "32", "--lstm-pretrain", "2"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["steps"] == 2 and d["config"]["parallelism"] == "dp2"
+    assert d["config"]["bench_config"] == config
     assert d["health"]["series_scored_last_tick"] == 200
     for k in ("metric", "value", "unit", "ms_per_step", "higher_is_better", "scaling", "vs_baseline", "dtype",
               "data", "config"):
         assert k in d
+
+
+def _dp_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from foremast_amd.models.lstm_ae import LSTMAutoencoder
+        from foremast_amd.parallel.dp import DPTrainer
+        torch.manual_seed(100 + rank)  # different init per rank → broadcast must align them
+        m = LSTMAutoencoder(2, 16)
+        tr = DPTrainer(m, lr=1e-2, bucket_bytes=2048)  # several buckets
+        g = torch.Generator().manual_seed(rank)
+        for _ in range(3):
+            x = torch.randn(8, 6, 2, generator=g)
+            tr.step(x)
+        flat = torch.cat([p.detach().flatten() for p in m.parameters()])
+        q.put((rank, flat.numpy().tolist(), len(tr.buckets.buckets)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_trainer_keeps_replicas_identical():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, p0, nb), (r1, p1, _) = res
+    assert nb > 1
+    assert np.allclose(p0, p1, atol=1e-6)
+
+
+def test_dp_single_process_matches_plain_adam():
+    from foremast_amd.models.lstm_ae import LSTMAutoencoder
+    from foremast_amd.parallel.dp import DPTrainer
+    torch.manual_seed(0)
+    a = LSTMAutoencoder(1, 8)
+    b = LSTMAutoencoder(1, 8)
+    b.load_state_dict(a.state_dict())
+    tr = DPTrainer(a, lr=1e-2)
+    opt = torch.optim.Adam(b.parameters(), lr=1e-2)
+    x = torch.randn(4, 5, 1)
+    for _ in range(3):
+        tr.step(x)
+        opt.zero_grad()
+        b.recon_error(x).mean().backward()
+        opt.step()
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        assert torch.allclose(pa, pb, atol=1e-6)
