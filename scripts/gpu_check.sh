@@ -21,6 +21,12 @@ for s in $STEPS; do
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
     kbench) run kbench 600 python scripts/bench_kernels.py ;;
+    lstm) run bench_lstm 600 python bench.py --config lstm --steps 20 --warmup 5 ;;
+    mv) run bench_mv 600 python bench.py --config multivariate --steps 20 --warmup 5 ;;
+    lstmtests) run lstm_tests 600 python -m pytest tests/test_lstm.py -m gpu -x -q ;;
+    proflstm)
+      export TMPDIR=/tmp
+      run proflstm 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/proflstm" -o run -- python3 "$PWD/bench.py" --config lstm --steps 5 --warmup 2 ;;
     prof)
       export TMPDIR=/tmp
       run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof" -o run -- python3 "$PWD/bench.py" --steps 5 --warmup 2 ;;
