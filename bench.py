@@ -50,7 +50,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-from foremast_amd.brain.engine import ShardSpec, StreamingShard, synthetic_history  # noqa: E402
+from foremast_amd.brain.engine import (ShardSpec, StreamingShard, synthetic_eval,  # noqa: E402
+                                       synthetic_history, synthetic_params)
 from foremast_amd.parallel.health import HealthAggregator, shard_range  # noqa: E402
 from foremast_amd.utils.config import BrainConfig  # noqa: E402
 
@@ -112,19 +113,16 @@ def barrier(dev):
             dist.barrier()
 
 
-def make_ticks(n, pods, nticks, season, start_t, dev, seed, anomaly_frac, hist_tail):
-    """Per-tick per-pod values [nticks, n, pods] continuing each series' pattern,
-    with a fraction of series turned anomalous (canary regression)."""
+def make_ticks(params, pods, nticks, season, t0, seed, anomaly_frac):
+    """Per-tick per-pod values ``[nticks, n, pods]`` continuing each series'
+    synthetic model past the history (same noise level as the history), with a
+    fraction of series turned anomalous (canary regression: values x3)."""
+    lvl = params["lvl"]
+    n, dev = lvl.shape[0], lvl.device
     g = torch.Generator(device=dev)
     g.manual_seed(seed + 17)
-    # estimate each series' level/seasonality from the tail of its history
-    last_day = hist_tail.float()
-    base = last_day[:, -season:]  # one day back = same phase
-    t = torch.arange(nticks, device=dev)
-    idx = (t % season)
-    vals = base[:, idx].T.contiguous()  # [nticks, n]
-    noise = torch.randn((nticks, n, pods), generator=g, device=dev) * (0.03 * vals.abs().mean(0, keepdim=True)[..., None] + 1e-3)
-    out = vals[..., None] + noise
+    vals = synthetic_eval(params, t0, nticks, season, None).T.contiguous()  # [nticks, n]
+    out = vals[..., None] + torch.randn((nticks, n, pods), generator=g, device=dev) * (0.03 * lvl[:, 0])[None, :, None]
     n_bad = int(n * anomaly_frac)
     if n_bad:
         bad = torch.randperm(n, generator=g, device=dev)[:n_bad]
@@ -151,17 +149,18 @@ def setup_canary(args, world, rank, dev):
                            threshold=torch.full((n_local,), 4.0, device=dev),
                            bound=torch.full((n_local,), 3, dtype=torch.int8, device=dev))
     # --- synthetic data (outside the timed region) ---------------------------------
-    hist = synthetic_history(n_local, args.ring, args.season, dev, seed=1234 + rank)
+    params = synthetic_params(n_local, dev, seed=1234 + rank)
+    hist = synthetic_eval(params, 0, args.ring, args.season, noise_seed=4321 + rank)
     shard.load_history(hist)
+    del hist
     W, P = args.window, args.pods
     total_ticks = args.warmup + args.steps
     # per tick: P canary-pod values (a fraction of series regressed) and P
     # baseline-pod values (healthy, same times) -> [ticks, N, 2P]
-    cur_t = make_ticks(n_local, P, total_ticks + W, args.season, args.ring, dev, 99 + rank,
-                       args.anomaly_frac, hist)
-    base_t = make_ticks(n_local, P, total_ticks + W, args.season, args.ring, dev, 7 + rank, 0.0, hist)
+    cur_t = make_ticks(params, P, total_ticks + W, args.season, args.ring, 99 + rank, args.anomaly_frac)
+    base_t = make_ticks(params, P, total_ticks + W, args.season, args.ring, 7 + rank, 0.0)
     ticks = torch.cat([cur_t, base_t], 2)
-    del cur_t, base_t, hist
+    del cur_t, base_t
     pin = dev.type == "cuda"
     host_ticks = ticks.cpu()
     if pin:
@@ -221,13 +220,13 @@ def setup_lstm(args, world, rank, dev, n_features, fp8):
     shard = LstmShard(n_local, args.ring, F, window=args.lstm_window, hidden=64, fp8=fp8, device=dev,
                       app_id=app_id, n_apps=n_apps, threshold=4.0, train_batch=args.lstm_train_batch,
                       lr=1e-3, seed=0)
-    hist = [synthetic_history(n_local, args.ring, args.season, dev, seed=1234 + 7 * f + 101 * rank)
-            for f in range(F)]
-    shard.load_history(hist)
+    params = [synthetic_params(n_local, dev, seed=1234 + 7 * f + 101 * rank) for f in range(F)]
+    shard.load_history([synthetic_eval(p, 0, args.ring, args.season, noise_seed=555 + f + 101 * rank)
+                        for f, p in enumerate(params)])
     total = args.warmup + args.steps
-    ticks = torch.stack([make_ticks(n_local, 1, total, args.season, args.ring, dev, 99 + rank + 13 * f,
-                                    args.anomaly_frac, hist[f])[..., 0] for f in range(F)], 2)  # [ticks, n, F]
-    del hist
+    # the same entities regress on every metric (seed shared across features)
+    ticks = torch.stack([make_ticks(p, 1, total, args.season, args.ring, 99 + rank, args.anomaly_frac)[..., 0]
+                         for p in params], 2)  # [ticks, n, F]
     pin = dev.type == "cuda"
     host_ticks = ticks.cpu()
     if pin:

@@ -197,22 +197,42 @@ class StreamingShard:
         return self.out
 
 
+def synthetic_params(N: int, device, seed: int = 0) -> Dict[str, torch.Tensor]:
+    """Per-series parameters of the synthetic seasonal model: level, daily
+    amplitude, phase, linear trend (each ``[N, 1]``)."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    lvl = torch.rand((N, 1), generator=g, device=device) * 95 + 5
+    amp = (torch.rand((N, 1), generator=g, device=device) * 0.25 + 0.05) * lvl
+    ph = torch.rand((N, 1), generator=g, device=device) * 6.283
+    tr = (torch.rand((N, 1), generator=g, device=device) - 0.5) * 1e-4 * lvl
+    return {"lvl": lvl, "amp": amp, "ph": ph, "tr": tr}
+
+
+def synthetic_eval(params: Dict[str, torch.Tensor], t0: int, T: int, season: int, noise_seed: Optional[int],
+                   dtype=torch.float32, chunk: int = 8192, noise: float = 0.03) -> torch.Tensor:
+    """Values of the synthetic model at times ``t0 .. t0+T-1`` → ``[N, T]``;
+    i.i.d. Gaussian noise of ``noise * level`` unless ``noise_seed`` is None."""
+    lvl = params["lvl"]
+    N, dev = lvl.shape[0], lvl.device
+    out = torch.empty((N, T), dtype=dtype, device=dev)
+    gn = None
+    if noise_seed is not None:
+        gn = torch.Generator(device=dev)
+        gn.manual_seed(noise_seed)
+    t = torch.arange(t0, t0 + T, device=dev, dtype=torch.float32)
+    for s in range(0, N, chunk):
+        e = min(N, s + chunk)
+        y = lvl[s:e] + params["tr"][s:e] * t + params["amp"][s:e] * torch.sin(2 * np.pi * t / season + params["ph"][s:e])
+        if gn is not None:
+            y = y + torch.randn((e - s, T), generator=gn, device=dev) * (noise * lvl[s:e])
+        out[s:e] = y.to(dtype)
+    return out
+
+
 def synthetic_history(N: int, T: int, season: int, device, seed: int = 0, dtype=torch.float32,
                       chunk: int = 8192) -> torch.Tensor:
     """Seasonal synthetic series (level, daily seasonality, slight trend, noise)
-    generated on ``device`` in chunks; returns ``[N, T]`` in ``dtype``."""
-    out = torch.empty((N, T), dtype=dtype, device=device)
-    g = torch.Generator(device=device)
-    g.manual_seed(seed)
-    t = torch.arange(T, device=device, dtype=torch.float32)
-    for s in range(0, N, chunk):
-        e = min(N, s + chunk)
-        n = e - s
-        lvl = torch.rand((n, 1), generator=g, device=device) * 95 + 5
-        amp = (torch.rand((n, 1), generator=g, device=device) * 0.25 + 0.05) * lvl
-        ph = torch.rand((n, 1), generator=g, device=device) * 6.283
-        tr = (torch.rand((n, 1), generator=g, device=device) - 0.5) * 1e-4 * lvl
-        noise = torch.randn((n, T), generator=g, device=device) * (0.03 * lvl)
-        y = lvl + tr * t + amp * torch.sin(2 * np.pi * t / season + ph) + noise
-        out[s:e] = y.to(dtype)
-    return out
+    generated on ``device`` in chunks; returns ``[N, T]`` in ``dtype``.
+    Continue a series with ``synthetic_eval(synthetic_params(N, dev, seed), T, ...)``."""
+    return synthetic_eval(synthetic_params(N, device, seed), 0, T, season, seed + 1_000_003, dtype, chunk)
