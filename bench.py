@@ -83,6 +83,7 @@ def parse():
     p.add_argument("--lstm-train-batch", type=int, default=4096)
     p.add_argument("--lstm-train-every", type=int, default=1)
     p.add_argument("--lstm-pretrain", type=int, default=10)
+    p.add_argument("--lstm-autograd", action="store_true", help="train with autograd instead of the fused K7 kernel")
     return p.parse_args()
 
 
@@ -219,7 +220,7 @@ def setup_lstm(args, world, rank, dev, n_features, fp8):
     app_id = (torch.arange(s, e, device=dev, dtype=torch.int64) // ent_per_app).to(torch.int32)
     shard = LstmShard(n_local, args.ring, F, window=args.lstm_window, hidden=64, fp8=fp8, device=dev,
                       app_id=app_id, n_apps=n_apps, threshold=4.0, train_batch=args.lstm_train_batch,
-                      lr=1e-3, seed=0)
+                      lr=1e-3, seed=0, fused_train=not args.lstm_autograd)
     params = [synthetic_params(n_local, dev, seed=1234 + 7 * f + 101 * rank) for f in range(F)]
     shard.load_history([synthetic_eval(p, 0, args.ring, args.season, noise_seed=555 + f + 101 * rank)
                         for f, p in enumerate(params)])
@@ -264,6 +265,7 @@ def setup_lstm(args, world, rank, dev, n_features, fp8):
         "features": F,
         "train_batch_per_rank": args.lstm_train_batch,
         "scoring_dtype": "fp8_e4m3" if fp8 else "bf16",
+        "training": "fused K7 kernel + hipBLASLt weight-grad GEMMs" if shard.fused_train else "autograd",
     }
     dt = "bf16"  # training fp32 master / bf16 MFMA scoring (fp8 weights+activations for config 5)
     return tick, health_host, meta, dt, n_ent * F

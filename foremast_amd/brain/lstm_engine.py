@@ -32,7 +32,7 @@ class LstmShard:
     def __init__(self, n_series: int, ring_len: int, n_features: int, window: int = 32, hidden: int = 64,
                  fp8: bool = False, device="cuda", app_id: Optional[torch.Tensor] = None, n_apps: int = 1,
                  threshold: float = 4.0, train_batch: int = 4096, lr: float = 1e-3, restat_every: int = 16,
-                 seed: int = 0, dtype=torch.bfloat16) -> None:
+                 seed: int = 0, dtype=torch.bfloat16, fused_train: bool = True) -> None:
         self.n, self.R, self.F, self.T = n_series, ring_len, n_features, window
         self.device = torch.device(device)
         self.gpu = self.device.type == "cuda"
@@ -40,7 +40,13 @@ class LstmShard:
                                          for _ in range(n_features)]
         torch.manual_seed(seed)
         self.model = LSTMAutoencoder(n_features, hidden).to(self.device)
-        self.trainer = DPTrainer(self.model, lr=lr)
+        grad_fn = None
+        if self.gpu and fused_train and train_batch % 32 == 0:
+            from ..ops.lstm_train import FusedLstmGrad
+            fg = FusedLstmGrad(train_batch, window, n_features, self.device)
+            grad_fn = fg.grads
+        self.fused_train = grad_fn is not None
+        self.trainer = DPTrainer(self.model, lr=lr, grad_fn=grad_fn)
         self.fp8 = fp8
         self.train_batch = train_batch
         self.threshold = threshold

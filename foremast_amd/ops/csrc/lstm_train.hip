@@ -1,0 +1,320 @@
+// K7: fused LSTM-autoencoder training pass (forward + backward through time)
+// on MFMA, for the data-parallel trainer (foremast_amd/parallel/dp.py).
+//
+// Semantics = foremast_amd/models/lstm_ae.py, loss = mean over the batch of
+// the per-window reconstruction MSE.  One 64-lane wave owns 32 windows
+// (lane l: window l&31, hidden-unit half l>>5), exactly as the inference
+// kernel (lstm.hip), and runs four phases back to back:
+//
+//   1. encoder forward  (40 MFMA / step, x + bias in the 5th k-step)
+//   2. decoder forward  (+ read-out y_t, dL/dy_t)
+//   3. decoder backward (t = T-1 .. 0)
+//   4. encoder backward (t = T-1 .. 0), seeded by the decoder's dh/dc at t=0
+//
+// Forward saves the activated gates (i, f, g, o) and c_t per step in a
+// lane-major fp32 scratch (one coalesced 256 B row per register).  Backward
+// recomputes nothing: per unit the cell gradient is lane-local, and
+//   dh_{t-1} = W_hh^T · dgates_t
+// is 32 MFMAs (2 M-tiles x 16 k-steps) whose B operand is the lane's own
+// dgates (k ordered as the forward accumulator registers) and whose A
+// operand is W_hh^T packed host-side so that the accumulator lands in the
+// h register layout — no LDS transpose anywhere in the recurrence.
+//
+// Weight gradients are NOT reduced in the kernel: it streams dgates
+// (bf16, PyTorch gate-row order) and the augmented inputs [h_{t-1}; x_t; 1]
+// (bf16) to HBM as [rows, T*B] matrices, and the host forms
+//   dW_aug = G · Haug^T   (one hipBLASLt GEMM per LSTM, K = T*B)
+// which is the plain library GEMM the recurrence cannot use.
+#include "common.h"
+#include "lstm_common.h"
+
+struct LstmTrainArgs {
+  const float* x;        // [B, T, F] normalised windows; B % 32 == 0
+  int B;
+  int T;
+  int F;                 // 1..7
+  int _pad;
+  const uint4* w_enc;    // forward A fragments [8][5][64] (bf16 x 8)
+  const uint4* w_dec;
+  const uint4* wt_enc;   // backward (W_hh^T) A fragments [2][16][64]
+  const uint4* wt_dec;
+  const float* w_out;    // [F][64]
+  const float* b_out;    // [F]
+  float* scratch;        // [waves][2][T][160][64] fp32
+  bf16_t* g_enc;         // [256][T*B]  dL/dgates, PyTorch row order
+  bf16_t* g_dec;         // [256][T*B]
+  bf16_t* h_enc;         // [80][T*B]   rows 0..63 h_{t-1}, 64..64+F-1 x_t (row 71 = 1 preset by host)
+  bf16_t* h_dec;         // [80][(T+1)*B] block 0 = encoder final h, block t+1 = decoder h_t
+  float* dy;             // [F][T*B]    dL/dy
+  float* err;            // [B]         per-window reconstruction MSE
+  float loss_scale;      // 2 / (B*T*F)
+};
+
+extern __shared__ __attribute__((aligned(16))) char fm_lstm_train_smem[];
+
+namespace {
+
+using namespace fm_lstm;
+
+constexpr int SREGS = 160;  // 32 units x (i, f, g, o, c)
+constexpr int WT_FRAGS = 2 * 16;
+
+__device__ __forceinline__ int unit_of(int tile, int hh, int q) {
+  return 16 * (tile >> 1) + 8 * hh + 4 * (tile & 1) + q;
+}
+
+__device__ __forceinline__ bf16x8_t as_bf16x8(const uint4& v) {
+  bf16x8_t r;
+  __builtin_memcpy(&r, &v, 16);
+  return r;
+}
+
+__device__ __forceinline__ f32x16 mfma_bf16(const uint4& a, const uint4& b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a), as_bf16x8(b), c, 0, 0, 0);
+}
+
+__device__ __forceinline__ uint4 pack8(const float (&v)[8]) {
+  uint4 r;
+  r.x = pack_bf16x2(v[0], v[1]);
+  r.y = pack_bf16x2(v[2], v[3]);
+  r.z = pack_bf16x2(v[4], v[5]);
+  r.w = pack_bf16x2(v[6], v[7]);
+  return r;
+}
+
+__device__ __forceinline__ void stage(uint4* dst, const uint4* src, int n16) {
+  for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+}
+
+// ---------------------------------------------------------------- forward
+template <bool ENC>
+__device__ __forceinline__ void fwd_phase(const LstmTrainArgs& a, const uint4* wlds, const float* wout,
+                                          float* scr, long long b, int hh, long long KB,
+                                          float (&hreg)[32], float (&creg)[32], float& errsum) {
+  const int lane = lane_id();
+  const float* xrow = a.x + b * (long long)a.T * a.F;
+  bf16_t* hbuf = ENC ? a.h_enc : a.h_dec;
+  const long long ldh = ENC ? KB : KB + a.B;
+  for (int t = 0; t < a.T; ++t) {
+    const long long col = (long long)t * a.B + b;
+    // augmented input [h_{t-1}; x_t; 1] for the weight-gradient GEMM
+    if (ENC || t == 0) {
+#pragma unroll
+      for (int tt = 0; tt < TILES; ++tt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          hbuf[(long long)unit_of(tt, hh, q) * ldh + col] = f32_to_bf16(hreg[4 * tt + q]);
+    }
+    uint4 hb[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = hreg[(2 * s + (j >> 2)) * 4 + (j & 3)];
+      hb[s] = pack8(v);
+    }
+    uint4 xb;
+    {
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (hh == 0) {
+        if (ENC) {
+#pragma unroll
+          for (int f = 0; f < 7; ++f)
+            if (f < a.F) {
+              v[f] = xrow[t * a.F + f];
+              a.h_enc[(long long)(64 + f) * KB + col] = f32_to_bf16(v[f]);
+            }
+        }
+        v[7] = 1.f;
+      }
+      xb = pack8(v);
+    }
+    int lo = lane;
+    asm volatile("" : "+v"(lo));
+    float* srow = scr + (long long)t * SREGS * 64 + lane;
+#pragma unroll
+    for (int tp = 0; tp < TILES; tp += 2) {
+      f32x16 acc0 = (f32x16){}, acc1 = (f32x16){};
+#pragma unroll
+      for (int s = 0; s < KSTEPS; ++s) {
+        const uint4 bfr = (s < 4) ? hb[s] : xb;
+        acc0 = mfma_bf16(wlds[(tp * KSTEPS + s) * 64 + lo], bfr, acc0);
+        acc1 = mfma_bf16(wlds[((tp + 1) * KSTEPS + s) * 64 + lo], bfr, acc1);
+      }
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const f32x16& acc = e ? acc1 : acc0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float gi = sigm(acc[q]), gf = sigm(acc[4 + q]);
+          const float gg = tanh_f(acc[8 + q]), go = sigm(acc[12 + q]);
+          const int u = (tp + e) * 4 + q;
+          const float c = gf * creg[u] + gi * gg;
+          creg[u] = c;
+          hreg[u] = go * tanh_f(c);
+          float* sp = srow + (long long)(u * 5) * 64;
+          sp[0] = gi;
+          sp[64] = gf;
+          sp[128] = gg;
+          sp[192] = go;
+          sp[256] = c;
+        }
+      }
+    }
+    if (!ENC) {
+      // decoder output block t+1 (h_t) for dW_dec (as h_prev of step t+1) and dW_out
+      const long long col1 = (long long)(t + 1) * a.B + b;
+#pragma unroll
+      for (int tt = 0; tt < TILES; ++tt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          a.h_dec[(long long)unit_of(tt, hh, q) * ldh + col1] = f32_to_bf16(hreg[4 * tt + q]);
+#pragma unroll
+      for (int f = 0; f < 7; ++f) {
+        if (f >= a.F) break;
+        float p = 0.f;
+#pragma unroll
+        for (int tt = 0; tt < TILES; ++tt)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) p += hreg[tt * 4 + q] * wout[f * H + unit_of(tt, hh, q)];
+        p += __shfl_xor(p, 32, FM_WAVE);
+        const float d = p + a.b_out[f] - xrow[t * a.F + f];
+        if (hh == 0) {
+          errsum += d * d;
+          a.dy[(long long)f * KB + col] = d * a.loss_scale;
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- backward
+// c_prev of step t: scratch c of step t-1, or `c0` (per-unit registers) at t = 0.
+template <bool ENC>
+__device__ __forceinline__ void bwd_phase(const LstmTrainArgs& a, const uint4* wt, const float* wout,
+                                          const float* scr, const float (&c0)[32], long long b, int hh,
+                                          long long KB, float (&dh)[32], float (&dc)[32]) {
+  const int lane = lane_id();
+  bf16_t* gbuf = ENC ? a.g_enc : a.g_dec;
+  for (int t = a.T - 1; t >= 0; --t) {
+    const long long col = (long long)t * a.B + b;
+    if (!ENC) {
+      // dL/dh_t += W_out^T dL/dy_t
+#pragma unroll
+      for (int f = 0; f < 7; ++f) {
+        if (f >= a.F) break;
+        const float dyf = a.dy[(long long)f * KB + col];
+#pragma unroll
+        for (int tt = 0; tt < TILES; ++tt)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) dh[4 * tt + q] += dyf * wout[f * H + unit_of(tt, hh, q)];
+      }
+    }
+    const float* srow = scr + (long long)t * SREGS * 64 + lane;
+    const float* sprev = scr + (long long)(t - 1) * SREGS * 64 + lane;
+    int lo = lane;
+    asm volatile("" : "+v"(lo));
+    f32x16 acc0 = (f32x16){}, acc1 = (f32x16){};  // dh_{t-1}: units of M-tile 0 / 1
+#pragma unroll
+    for (int tt = 0; tt < TILES; ++tt) {
+      float dg[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int u = 4 * tt + q;
+        const float* sp = srow + (long long)(u * 5) * 64;
+        const float gi = sp[0], gf = sp[64], gg = sp[128], go = sp[192], c = sp[256];
+        const float cp = (t > 0) ? sprev[(long long)(u * 5 + 4) * 64] : c0[u];
+        const float tc = tanh_f(c);
+        const float dcu = dc[u] + dh[u] * go * (1.f - tc * tc);
+        dg[q] = dcu * gg * gi * (1.f - gi);            // i
+        dg[4 + q] = dcu * cp * gf * (1.f - gf);        // f
+        dg[8 + q] = dcu * gi * (1.f - gg * gg);        // g
+        dg[12 + q] = dh[u] * tc * go * (1.f - go);     // o
+        dc[u] = dcu * gf;
+      }
+      // dgates → HBM (bf16, PyTorch gate-row order: gate*64 + unit)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        gbuf[(long long)((r >> 2) * H + unit_of(tt, hh, r & 3)) * KB + col] = f32_to_bf16(dg[r]);
+      // dh_{t-1} += W_hh^T[:, rows of this tile] · dgates (2 k-steps x 2 M-tiles)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = dg[8 * e + j];
+        const uint4 bfr = pack8(v);
+        const int ks = 2 * tt + e;
+        acc0 = mfma_bf16(wt[(0 * 16 + ks) * 64 + lo], bfr, acc0);
+        acc1 = mfma_bf16(wt[(1 * 16 + ks) * 64 + lo], bfr, acc1);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      dh[r] = acc0[r];
+      dh[16 + r] = acc1[r];
+    }
+  }
+}
+
+__global__ __launch_bounds__(64, 1) void lstm_ae_train_kernel(const LstmTrainArgs a) {
+  const int lane = lane_id();
+  const int hh = lane >> 5;
+  const long long wave = blockIdx.x;
+  const long long b = wave * 32 + (lane & 31);  // host guarantees B % 32 == 0
+  const long long KB = (long long)a.T * a.B;
+  uint4* wlds = (uint4*)fm_lstm_train_smem;
+  float* wout = (float*)(fm_lstm_train_smem + FRAG_BYTES_BF16);
+  float* scr_enc = a.scratch + wave * 2 * (long long)a.T * SREGS * 64;
+  float* scr_dec = scr_enc + (long long)a.T * SREGS * 64;
+
+  for (int i = threadIdx.x; i < a.F * H; i += blockDim.x) wout[i] = a.w_out[i];
+  stage(wlds, a.w_enc, FRAG_BYTES_BF16 / 16);
+  __syncthreads();
+  float hreg[32], creg[32];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) { hreg[i] = 0.f; creg[i] = 0.f; }
+  float errsum = 0.f;
+  fwd_phase<true>(a, wlds, wout, scr_enc, b, hh, KB, hreg, creg, errsum);
+  float c_enc[32];  // encoder final c = decoder c_prev at t = 0
+#pragma unroll
+  for (int i = 0; i < 32; ++i) c_enc[i] = creg[i];
+  __syncthreads();
+  stage(wlds, a.w_dec, FRAG_BYTES_BF16 / 16);
+  __syncthreads();
+  fwd_phase<false>(a, wlds, wout, scr_dec, b, hh, KB, hreg, creg, errsum);
+  if (hh == 0) a.err[b] = errsum / (float)(a.T * a.F);
+
+  // backward: decoder, then encoder
+  __syncthreads();
+  stage(wlds, a.wt_dec, WT_FRAGS * 64);
+  __syncthreads();
+  float dh[32], dc[32];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) { dh[i] = 0.f; dc[i] = 0.f; }
+  bwd_phase<false>(a, wlds, wout, scr_dec, c_enc, b, hh, KB, dh, dc);
+  __syncthreads();
+  stage(wlds, a.wt_enc, WT_FRAGS * 64);
+  __syncthreads();
+  float zero[32];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) zero[i] = 0.f;
+  bwd_phase<true>(a, wlds, wout, scr_enc, zero, b, hh, KB, dh, dc);
+}
+
+}  // namespace
+
+extern "C" size_t fm_lstm_train_lds_bytes(int F) { return (size_t)FRAG_BYTES_BF16 + (size_t)F * H * 4; }
+
+extern "C" long long fm_lstm_train_scratch_floats(int B, int T) {
+  return (long long)(B / 32) * 2 * T * SREGS * 64;
+}
+
+extern "C" long long fm_lstm_train_args_size() { return (long long)sizeof(LstmTrainArgs); }
+
+extern "C" int fm_lstm_ae_train(const LstmTrainArgs* a, hipStream_t st) {
+  if (a->B <= 0) return 0;
+  if (a->B % 32 || a->F < 1 || a->F > 7 || a->T < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(lstm_ae_train_kernel, dim3((unsigned)(a->B / 32)), dim3(64),
+                     fm_lstm_train_lds_bytes(a->F), st, *a);
+  return (int)hipGetLastError();
+}

@@ -74,15 +74,16 @@ class GradBuckets:
             b["ready"] = 0
 
     def finish(self) -> None:
-        """Complete the reduction (average over ranks)."""
+        """Complete the reduction (average over ranks).  Buckets whose hooks
+        did not fire (gradients written directly, e.g. by the fused LSTM
+        training kernel) are all-reduced here."""
         if self.world > 1:
-            if self.overlap:
-                for h in self._handles:
-                    h.wait()
-                self._handles.clear()
-            else:
-                for b in self.buckets:
-                    dist.all_reduce(b["flat"], group=self.group)
+            for b in self.buckets:
+                if not self.overlap or b["ready"] < len(b["params"]):
+                    self._handles.append(dist.all_reduce(b["flat"], group=self.group, async_op=True))
+            for h in self._handles:
+                h.wait()
+            self._handles.clear()
             for b in self.buckets:
                 b["flat"].div_(self.world)
 
@@ -97,17 +98,25 @@ class DPTrainer:
     """Adam on the reconstruction loss with bucketed gradient all-reduce."""
 
     def __init__(self, model: torch.nn.Module, lr: float = 1e-3, group=None, bucket_bytes: int = 4 << 20,
-                 overlap: bool = True) -> None:
+                 overlap: bool = True, grad_fn=None) -> None:
+        """``grad_fn(model, windows) -> loss`` (optional) writes ``p.grad`` itself
+        (fused kernel path) instead of autograd."""
         self.model = model
+        self.grad_fn = grad_fn
         broadcast_params(model, 0, group)
         self.buckets = GradBuckets(list(model.parameters()), bucket_bytes, group, overlap)
-        self.opt = torch.optim.Adam(model.parameters(), lr=lr)
+        on_gpu = next(model.parameters()).is_cuda
+        # fused multi-tensor Adam on the GPU: one launch for all parameters
+        self.opt = torch.optim.Adam(model.parameters(), lr=lr, fused=on_gpu or None)
         self.steps = 0
 
     def step(self, windows: torch.Tensor) -> torch.Tensor:
         self.buckets.zero()
-        loss = self.model.recon_error(windows).mean()
-        loss.backward()
+        if self.grad_fn is not None:
+            loss = self.grad_fn(self.model, windows)
+        else:
+            loss = self.model.recon_error(windows).mean()
+            loss.backward()
         self.buckets.finish()
         self.opt.step()
         self.steps += 1

@@ -23,6 +23,7 @@ for s in $STEPS; do
     kbench) run kbench 600 python scripts/bench_kernels.py ;;
     lstm) run bench_lstm 600 python bench.py --config lstm --steps 20 --warmup 5 ;;
     mv) run bench_mv 600 python bench.py --config multivariate --steps 20 --warmup 5 ;;
+    lstmauto) run bench_lstm_autograd 600 python bench.py --config lstm --steps 20 --warmup 5 --lstm-autograd ;;
     lstmtests) run lstm_tests 600 python -m pytest tests/test_lstm.py -m gpu -x -q ;;
     proflstm)
       export TMPDIR=/tmp

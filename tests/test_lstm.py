@@ -203,3 +203,58 @@ def test_lstm_shard_gpu_matches_model(fp8):
     else:
         assert torch.allclose(err, ref, rtol=5e-2, atol=2e-3)
     assert int(sh.app_stats[:, 1].sum()) == n
+
+
+def test_backward_register_plan_matches_wT_dgates():
+    """CPU emulation of the K7 backward recurrence step: dh_{t-1} = W_hh^T dgates
+    from lane-local dgates (forward accumulator order) through the packed W^T
+    fragments lands in the h register layout."""
+    from foremast_amd.ops import lstm_train as LT
+    rng = np.random.default_rng(0)
+    W = rng.standard_normal((256, 64))
+    d = rng.standard_normal((32, 256))  # [series, pytorch gate row]
+    frag = W.flatten()[LT.transposed_frag_index().numpy()].reshape(2, 16, 64, 8)
+
+    def unit(t, hh, q):
+        return 16 * (t >> 1) + 8 * hh + 4 * (t & 1) + q
+
+    acc = [np.zeros((64, 16)), np.zeros((64, 16))]
+    for ks in range(16):
+        tt, e = ks >> 1, ks & 1
+        b = np.zeros((64, 8))
+        for l in range(64):
+            for j in range(8):
+                r = 8 * e + j
+                b[l, j] = d[l & 31, (r >> 2) * 64 + unit(tt, l >> 5, r & 3)]
+        for mt in range(2):
+            acc[mt] = _emulate_mfma(frag[mt, ks], b, acc[mt])
+    ref = d @ W  # [series, unit] = (W^T d)^T
+    for l in range(64):
+        for mt in range(2):
+            for r in range(16):
+                u = unit(4 * mt + (r >> 2), l >> 5, r & 3)
+                assert abs(acc[mt][l, r] - ref[l & 31, u]) < 1e-9
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("F", [1, 3])
+def test_fused_lstm_training_grads_match_autograd(F):
+    from foremast_amd.ops.lstm_train import FusedLstmGrad
+    torch.manual_seed(5)
+    dev = torch.device("cuda:0")
+    B, T = 64, 12
+    m = lstm_ae.LSTMAutoencoder(F, 64).to(dev)
+    x = torch.randn(B, T, F, device=dev)
+    loss = m.recon_error(x).mean()
+    ref = torch.autograd.grad(loss, list(m.parameters()))
+    fg = FusedLstmGrad(B, T, F, dev)
+    with torch.no_grad():
+        err_ref = m.recon_error(x)
+    got_loss = fg.grads(m, x)
+    torch.cuda.synchronize()
+    assert torch.allclose(fg.err, err_ref, rtol=3e-2, atol=1e-3)
+    assert abs(float(got_loss) - float(loss)) < 3e-2 * abs(float(loss))
+    for (name, p), g in zip(m.named_parameters(), ref):
+        cos = torch.nn.functional.cosine_similarity(p.grad.flatten(), g.flatten(), dim=0)
+        rel = (p.grad - g).norm() / g.norm().clamp(min=1e-12)
+        assert cos > 0.99 and rel < 0.08, (name, float(cos), float(rel))
