@@ -84,6 +84,8 @@ def parse():
     p.add_argument("--lstm-train-every", type=int, default=1)
     p.add_argument("--lstm-pretrain", type=int, default=10)
     p.add_argument("--lstm-autograd", action="store_true", help="train with autograd instead of the fused K7 kernel")
+    p.add_argument("--lstm-no-overlap", action="store_true",
+                   help="run the training step and scoring back to back instead of on two HIP streams")
     return p.parse_args()
 
 
@@ -245,10 +247,7 @@ def setup_lstm(args, world, rank, dev, n_features, fp8):
 
     def tick(k):
         newx.copy_(host_ticks[k], non_blocking=pin)
-        shard.ingest_tick(newx)
-        if k % args.lstm_train_every == 0:
-            shard.train_step()
-        out = shard.score()
+        out = shard.tick(newx, train=(k % args.lstm_train_every == 0), overlap=not args.lstm_no_overlap)
         stats, _ = agg.tick(shard.app_stats, out["verdict"])
         health_host.copy_(stats, non_blocking=pin)
         if dev.type == "cuda":
@@ -266,6 +265,7 @@ def setup_lstm(args, world, rank, dev, n_features, fp8):
         "train_batch_per_rank": args.lstm_train_batch,
         "scoring_dtype": "fp8_e4m3" if fp8 else "bf16",
         "training": "fused K7 kernel + hipBLASLt weight-grad GEMMs" if shard.fused_train else "autograd",
+        "train_score_overlap": not args.lstm_no_overlap,
     }
     dt = "bf16"  # training fp32 master / bf16 MFMA scoring (fp8 weights+activations for config 5)
     return tick, health_host, meta, dt, n_ent * F

@@ -64,6 +64,7 @@ class LstmShard:
         self.out: Dict[str, torch.Tensor] = {}
         self._ar = torch.arange(window, device=self.device)
         self._det = None
+        self._side = None
         self._ws: Dict[str, torch.Tensor] = {}
         self._all = torch.arange(n_series, device=self.device)
         self._zero_off = torch.zeros(n_series, dtype=torch.long, device=self.device)
@@ -145,18 +146,52 @@ class LstmShard:
         self.mu = s1 / cnt
         self.sigma = max(s2 / cnt - self.mu * self.mu, 0.0) ** 0.5 + 1e-12
 
-    def score(self) -> Dict[str, torch.Tensor]:
+    def _pack_scoring(self) -> None:
+        from ..ops import lstm as L
+        if self.packed is None:
+            self.packed = L.pack(self.model, fp8=self.fp8, device=self.device)
+        else:
+            L.repack_into(self.packed, self.model)
+
+    def _score_packed(self, x: torch.Tensor) -> Dict[str, torch.Tensor]:
+        from ..ops import lstm as L
         self.app_stats.zero_()
+        self.out = L.lstm_score(self.packed, x, self.mu, self.sigma, thr_default=self.threshold,
+                                app_id=self.app_id, app_stats=self.app_stats, out=self.out)
+        return self.out
+
+    def tick(self, newx: torch.Tensor, train: bool = True, overlap: bool = True) -> Dict[str, torch.Tensor]:
+        """Ingest + (optional) DP training step + scoring of every series.
+
+        On the GPU with ``overlap`` the training step runs on a side HIP stream
+        concurrently with scoring (the training kernel occupies B/32 SIMDs,
+        scoring fills the rest); scoring uses the weights from before this
+        tick's update (a one-step model lag) and the tick joins both streams."""
+        self.ingest_tick(newx)
+        if not (train and overlap and self.gpu):
+            if train:
+                self.train_step()
+            return self.score()
+        xs = self._gather(self._all, self._zero_off)
+        xt = self._sample(self.train_batch)
+        self._pack_scoring()
+        main = torch.cuda.current_stream(self.device)
+        if self._side is None:
+            self._side = torch.cuda.Stream(self.device)
+        self._side.wait_stream(main)
+        xt.record_stream(self._side)
+        with torch.cuda.stream(self._side):
+            self.trainer.step(xt)
+        out = self._score_packed(xs)
+        main.wait_stream(self._side)
+        return out
+
+    def score(self) -> Dict[str, torch.Tensor]:
         x = self._gather(self._all, self._zero_off)
         if self.gpu:
-            from ..ops import lstm as L
-            if self.packed is None:
-                self.packed = L.pack(self.model, fp8=self.fp8, device=self.device)
-            else:
-                L.repack_into(self.packed, self.model)
-            self.out = L.lstm_score(self.packed, x, self.mu, self.sigma, thr_default=self.threshold,
-                                    app_id=self.app_id, app_stats=self.app_stats, out=self.out)
-            return self.out
+            self._pack_scoring()
+            return self._score_packed(x)
+        self.app_stats.zero_()
         with torch.no_grad():
             err = self.model.recon_error(x)
         z = (err - self.mu) / max(self.sigma, 1e-12)

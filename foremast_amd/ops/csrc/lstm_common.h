@@ -17,8 +17,16 @@ constexpr int KSTEPS = 5;
 constexpr int FRAG_BYTES_BF16 = TILES * KSTEPS * 64 * 16;  // 40 KB
 constexpr int FRAG_BYTES_FP8 = TILES * KSTEPS * 64 * 8;    // 20 KB
 
-__device__ __forceinline__ float sigm(float v) { return __frcp_rn(1.f + __expf(-v)); }
-__device__ __forceinline__ float tanh_f(float v) { return 2.f * __frcp_rn(1.f + __expf(-2.f * v)) - 1.f; }
+// v_exp_f32 (2^x) + v_rcp_f32 (1 ulp): two transcendental issues per
+// activation.  (__frcp_rn / '/' lower to the ~10-instruction IEEE division
+// sequence.)  Saturates cleanly: exp2 → inf gives rcp → 0.
+constexpr float LOG2E = 1.4426950408889634f;
+__device__ __forceinline__ float sigm(float v) {
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-LOG2E * v));
+}
+__device__ __forceinline__ float tanh_f(float v) {
+  return 2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-2.f * LOG2E * v)) - 1.f;
+}
 
 __device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
   return (unsigned)f32_to_bf16(lo) | ((unsigned)f32_to_bf16(hi) << 16);

@@ -12,7 +12,7 @@
 //   4. encoder backward (t = T-1 .. 0), seeded by the decoder's dh/dc at t=0
 //
 // Forward saves the activated gates (i, f, g, o) and c_t per step in a
-// lane-major fp32 scratch (one coalesced 256 B row per register).  Backward
+// lane-major fp32 scratch (layout below).  Backward
 // recomputes nothing: per unit the cell gradient is lane-local, and
 //   dh_{t-1} = W_hh^T · dgates_t
 // is 32 MFMAs (2 M-tiles x 16 k-steps) whose B operand is the lane's own
@@ -20,11 +20,17 @@
 // operand is W_hh^T packed host-side so that the accumulator lands in the
 // h register layout — no LDS transpose anywhere in the recurrence.
 //
-// Weight gradients are NOT reduced in the kernel: it streams dgates
-// (bf16, PyTorch gate-row order) and the augmented inputs [h_{t-1}; x_t; 1]
-// (bf16) to HBM as [rows, T*B] matrices, and the host forms
+// Weight gradients are NOT reduced in the kernel: it streams dgates (bf16,
+// PyTorch gate-row order) and the augmented inputs [h_{t-1}; x_t; 1] (bf16)
+// to HBM as K-contiguous [rows, T*B] matrices (a wave's 32 windows write 64
+// contiguous bytes per row), and the host forms
 //   dW_aug = G · Haug^T   (one hipBLASLt GEMM per LSTM, K = T*B)
-// which is the plain library GEMM the recurrence cannot use.
+// in the "both operands K-contiguous" form hipBLASLt runs fastest.
+// (A row-per-(t, window) layout with 16-byte stores made the kernel no
+// faster and the GEMM 3.5x slower: measured, scripts/bench_lstm_kernels.py.)
+// Scratch is float4-vectorised: per step a lane owns 40 float4 (gates i,f,g,o
+// of unit u at float4 u, c of units 4k..4k+3 at float4 32+k), and every
+// scratch access of a wave is one contiguous 1 KB segment.
 #include "common.h"
 #include "lstm_common.h"
 
@@ -33,14 +39,14 @@ struct LstmTrainArgs {
   int B;
   int T;
   int F;                 // 1..7
-  int _pad;
+  int phases;            // bitmask (profiling): 1 enc fwd, 2 dec fwd, 4 dec bwd, 8 enc bwd; 0 = all
   const uint4* w_enc;    // forward A fragments [8][5][64] (bf16 x 8)
   const uint4* w_dec;
   const uint4* wt_enc;   // backward (W_hh^T) A fragments [2][16][64]
   const uint4* wt_dec;
   const float* w_out;    // [F][64]
   const float* b_out;    // [F]
-  float* scratch;        // [waves][2][T][160][64] fp32
+  float* scratch;        // [waves][2][T][40][64] float4
   bf16_t* g_enc;         // [256][T*B]  dL/dgates, PyTorch row order
   bf16_t* g_dec;         // [256][T*B]
   bf16_t* h_enc;         // [80][T*B]   rows 0..63 h_{t-1}, 64..64+F-1 x_t (row 71 = 1 preset by host)
@@ -56,7 +62,7 @@ namespace {
 
 using namespace fm_lstm;
 
-constexpr int SREGS = 160;  // 32 units x (i, f, g, o, c)
+constexpr int SV4 = 40;  // float4 per lane per step: 32 units x (i, f, g, o) + 32 c
 constexpr int WT_FRAGS = 2 * 16;
 
 __device__ __forceinline__ int unit_of(int tile, int hh, int q) {
@@ -89,21 +95,21 @@ __device__ __forceinline__ void stage(uint4* dst, const uint4* src, int n16) {
 // ---------------------------------------------------------------- forward
 template <bool ENC>
 __device__ __forceinline__ void fwd_phase(const LstmTrainArgs& a, const uint4* wlds, const float* wout,
-                                          float* scr, long long b, int hh, long long KB,
+                                          float4* scr, long long b, int hh, long long KB,
                                           float (&hreg)[32], float (&creg)[32], float& errsum) {
   const int lane = lane_id();
   const float* xrow = a.x + b * (long long)a.T * a.F;
   bf16_t* hbuf = ENC ? a.h_enc : a.h_dec;
   const long long ldh = ENC ? KB : KB + a.B;
   for (int t = 0; t < a.T; ++t) {
-    const long long col = (long long)t * a.B + b;
+    const long long row = (long long)t * a.B + b;  // column of the [rows, T*B] matrices
     // augmented input [h_{t-1}; x_t; 1] for the weight-gradient GEMM
     if (ENC || t == 0) {
 #pragma unroll
       for (int tt = 0; tt < TILES; ++tt)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          hbuf[(long long)unit_of(tt, hh, q) * ldh + col] = f32_to_bf16(hreg[4 * tt + q]);
+          hbuf[(long long)unit_of(tt, hh, q) * ldh + row] = f32_to_bf16(hreg[4 * tt + q]);
     }
     uint4 hb[4];
 #pragma unroll
@@ -122,7 +128,7 @@ __device__ __forceinline__ void fwd_phase(const LstmTrainArgs& a, const uint4* w
           for (int f = 0; f < 7; ++f)
             if (f < a.F) {
               v[f] = xrow[t * a.F + f];
-              a.h_enc[(long long)(64 + f) * KB + col] = f32_to_bf16(v[f]);
+              a.h_enc[(long long)(64 + f) * KB + row] = f32_to_bf16(v[f]);
             }
         }
         v[7] = 1.f;
@@ -131,7 +137,7 @@ __device__ __forceinline__ void fwd_phase(const LstmTrainArgs& a, const uint4* w
     }
     int lo = lane;
     asm volatile("" : "+v"(lo));
-    float* srow = scr + (long long)t * SREGS * 64 + lane;
+    float4* srow = scr + (long long)t * SV4 * 64 + lane;
 #pragma unroll
     for (int tp = 0; tp < TILES; tp += 2) {
       f32x16 acc0 = (f32x16){}, acc1 = (f32x16){};
@@ -144,6 +150,7 @@ __device__ __forceinline__ void fwd_phase(const LstmTrainArgs& a, const uint4* w
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const f32x16& acc = e ? acc1 : acc0;
+        float4 cv;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const float gi = sigm(acc[q]), gf = sigm(acc[4 + q]);
@@ -152,23 +159,20 @@ __device__ __forceinline__ void fwd_phase(const LstmTrainArgs& a, const uint4* w
           const float c = gf * creg[u] + gi * gg;
           creg[u] = c;
           hreg[u] = go * tanh_f(c);
-          float* sp = srow + (long long)(u * 5) * 64;
-          sp[0] = gi;
-          sp[64] = gf;
-          sp[128] = gg;
-          sp[192] = go;
-          sp[256] = c;
+          srow[u * 64] = make_float4(gi, gf, gg, go);
+          (&cv.x)[q] = c;
         }
+        srow[(32 + tp + e) * 64] = cv;
       }
     }
     if (!ENC) {
       // decoder output block t+1 (h_t) for dW_dec (as h_prev of step t+1) and dW_out
-      const long long col1 = (long long)(t + 1) * a.B + b;
+      const long long row1 = (long long)(t + 1) * a.B + b;
 #pragma unroll
       for (int tt = 0; tt < TILES; ++tt)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          a.h_dec[(long long)unit_of(tt, hh, q) * ldh + col1] = f32_to_bf16(hreg[4 * tt + q]);
+          a.h_dec[(long long)unit_of(tt, hh, q) * ldh + row1] = f32_to_bf16(hreg[4 * tt + q]);
 #pragma unroll
       for (int f = 0; f < 7; ++f) {
         if (f >= a.F) break;
@@ -181,7 +185,7 @@ __device__ __forceinline__ void fwd_phase(const LstmTrainArgs& a, const uint4* w
         const float d = p + a.b_out[f] - xrow[t * a.F + f];
         if (hh == 0) {
           errsum += d * d;
-          a.dy[(long long)f * KB + col] = d * a.loss_scale;
+          a.dy[(long long)f * KB + row] = d * a.loss_scale;
         }
       }
     }
@@ -192,38 +196,42 @@ __device__ __forceinline__ void fwd_phase(const LstmTrainArgs& a, const uint4* w
 // c_prev of step t: scratch c of step t-1, or `c0` (per-unit registers) at t = 0.
 template <bool ENC>
 __device__ __forceinline__ void bwd_phase(const LstmTrainArgs& a, const uint4* wt, const float* wout,
-                                          const float* scr, const float (&c0)[32], long long b, int hh,
+                                          const float4* scr, const float (&c0)[32], long long b, int hh,
                                           long long KB, float (&dh)[32], float (&dc)[32]) {
   const int lane = lane_id();
   bf16_t* gbuf = ENC ? a.g_enc : a.g_dec;
   for (int t = a.T - 1; t >= 0; --t) {
-    const long long col = (long long)t * a.B + b;
+    const long long row = (long long)t * a.B + b;
     if (!ENC) {
       // dL/dh_t += W_out^T dL/dy_t
 #pragma unroll
       for (int f = 0; f < 7; ++f) {
         if (f >= a.F) break;
-        const float dyf = a.dy[(long long)f * KB + col];
+        const float dyf = a.dy[(long long)f * KB + row];
 #pragma unroll
         for (int tt = 0; tt < TILES; ++tt)
 #pragma unroll
           for (int q = 0; q < 4; ++q) dh[4 * tt + q] += dyf * wout[f * H + unit_of(tt, hh, q)];
       }
     }
-    const float* srow = scr + (long long)t * SREGS * 64 + lane;
-    const float* sprev = scr + (long long)(t - 1) * SREGS * 64 + lane;
+    const float4* srow = scr + (long long)t * SV4 * 64 + lane;
+    const float4* sprev = scr + (long long)(t - 1) * SV4 * 64 + lane;
     int lo = lane;
     asm volatile("" : "+v"(lo));
     f32x16 acc0 = (f32x16){}, acc1 = (f32x16){};  // dh_{t-1}: units of M-tile 0 / 1
 #pragma unroll
     for (int tt = 0; tt < TILES; ++tt) {
       float dg[16];
+      const float4 cv = srow[(32 + tt) * 64];
+      float4 cpv;
+      if (t > 0) cpv = sprev[(32 + tt) * 64];
+      else cpv = make_float4(c0[4 * tt], c0[4 * tt + 1], c0[4 * tt + 2], c0[4 * tt + 3]);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int u = 4 * tt + q;
-        const float* sp = srow + (long long)(u * 5) * 64;
-        const float gi = sp[0], gf = sp[64], gg = sp[128], go = sp[192], c = sp[256];
-        const float cp = (t > 0) ? sprev[(long long)(u * 5 + 4) * 64] : c0[u];
+        const float4 gv = srow[u * 64];
+        const float gi = gv.x, gf = gv.y, gg = gv.z, go = gv.w;
+        const float c = (&cv.x)[q], cp = (&cpv.x)[q];
         const float tc = tanh_f(c);
         const float dcu = dc[u] + dh[u] * go * (1.f - tc * tc);
         dg[q] = dcu * gg * gi * (1.f - gi);            // i
@@ -232,10 +240,10 @@ __device__ __forceinline__ void bwd_phase(const LstmTrainArgs& a, const uint4* w
         dg[12 + q] = dh[u] * tc * go * (1.f - go);     // o
         dc[u] = dcu * gf;
       }
-      // dgates → HBM (bf16, PyTorch gate-row order: gate*64 + unit)
+      // dgates → HBM (PyTorch gate-row order: gate*64 + unit)
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        gbuf[(long long)((r >> 2) * H + unit_of(tt, hh, r & 3)) * KB + col] = f32_to_bf16(dg[r]);
+        gbuf[(long long)((r >> 2) * H + unit_of(tt, hh, r & 3)) * KB + row] = f32_to_bf16(dg[r]);
       // dh_{t-1} += W_hh^T[:, rows of this tile] · dgates (2 k-steps x 2 M-tiles)
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -264,8 +272,8 @@ __global__ __launch_bounds__(64, 1) void lstm_ae_train_kernel(const LstmTrainArg
   const long long KB = (long long)a.T * a.B;
   uint4* wlds = (uint4*)fm_lstm_train_smem;
   float* wout = (float*)(fm_lstm_train_smem + FRAG_BYTES_BF16);
-  float* scr_enc = a.scratch + wave * 2 * (long long)a.T * SREGS * 64;
-  float* scr_dec = scr_enc + (long long)a.T * SREGS * 64;
+  float4* scr_enc = (float4*)a.scratch + wave * 2 * (long long)a.T * SV4 * 64;
+  float4* scr_dec = scr_enc + (long long)a.T * SV4 * 64;
 
   for (int i = threadIdx.x; i < a.F * H; i += blockDim.x) wout[i] = a.w_out[i];
   stage(wlds, a.w_enc, FRAG_BYTES_BF16 / 16);
@@ -274,14 +282,15 @@ __global__ __launch_bounds__(64, 1) void lstm_ae_train_kernel(const LstmTrainArg
 #pragma unroll
   for (int i = 0; i < 32; ++i) { hreg[i] = 0.f; creg[i] = 0.f; }
   float errsum = 0.f;
-  fwd_phase<true>(a, wlds, wout, scr_enc, b, hh, KB, hreg, creg, errsum);
+  const int ph = a.phases ? a.phases : 15;
+  if (ph & 1) fwd_phase<true>(a, wlds, wout, scr_enc, b, hh, KB, hreg, creg, errsum);
   float c_enc[32];  // encoder final c = decoder c_prev at t = 0
 #pragma unroll
   for (int i = 0; i < 32; ++i) c_enc[i] = creg[i];
   __syncthreads();
   stage(wlds, a.w_dec, FRAG_BYTES_BF16 / 16);
   __syncthreads();
-  fwd_phase<false>(a, wlds, wout, scr_dec, b, hh, KB, hreg, creg, errsum);
+  if (ph & 2) fwd_phase<false>(a, wlds, wout, scr_dec, b, hh, KB, hreg, creg, errsum);
   if (hh == 0) a.err[b] = errsum / (float)(a.T * a.F);
 
   // backward: decoder, then encoder
@@ -291,14 +300,14 @@ __global__ __launch_bounds__(64, 1) void lstm_ae_train_kernel(const LstmTrainArg
   float dh[32], dc[32];
 #pragma unroll
   for (int i = 0; i < 32; ++i) { dh[i] = 0.f; dc[i] = 0.f; }
-  bwd_phase<false>(a, wlds, wout, scr_dec, c_enc, b, hh, KB, dh, dc);
+  if (ph & 4) bwd_phase<false>(a, wlds, wout, scr_dec, c_enc, b, hh, KB, dh, dc);
   __syncthreads();
   stage(wlds, a.wt_enc, WT_FRAGS * 64);
   __syncthreads();
   float zero[32];
 #pragma unroll
   for (int i = 0; i < 32; ++i) zero[i] = 0.f;
-  bwd_phase<true>(a, wlds, wout, scr_enc, zero, b, hh, KB, dh, dc);
+  if (ph & 8) bwd_phase<true>(a, wlds, wout, scr_enc, zero, b, hh, KB, dh, dc);
 }
 
 }  // namespace
@@ -306,7 +315,7 @@ __global__ __launch_bounds__(64, 1) void lstm_ae_train_kernel(const LstmTrainArg
 extern "C" size_t fm_lstm_train_lds_bytes(int F) { return (size_t)FRAG_BYTES_BF16 + (size_t)F * H * 4; }
 
 extern "C" long long fm_lstm_train_scratch_floats(int B, int T) {
-  return (long long)(B / 32) * 2 * T * SREGS * 64;
+  return (long long)(B / 32) * 2 * T * SV4 * 64 * 4;
 }
 
 extern "C" long long fm_lstm_train_args_size() { return (long long)sizeof(LstmTrainArgs); }

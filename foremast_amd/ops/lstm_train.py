@@ -23,7 +23,7 @@ from .lstm import BIAS_K, H, KAUG, _augment_dev, _frag_index
 
 class LstmTrainArgs(C.Structure):
     _fields_ = [
-        ("x", C.c_void_p), ("B", C.c_int), ("T", C.c_int), ("F", C.c_int), ("_pad", C.c_int),
+        ("x", C.c_void_p), ("B", C.c_int), ("T", C.c_int), ("F", C.c_int), ("phases", C.c_int),
         ("w_enc", C.c_void_p), ("w_dec", C.c_void_p), ("wt_enc", C.c_void_p), ("wt_dec", C.c_void_p),
         ("w_out", C.c_void_p), ("b_out", C.c_void_p), ("scratch", C.c_void_p),
         ("g_enc", C.c_void_p), ("g_dec", C.c_void_p), ("h_enc", C.c_void_p), ("h_dec", C.c_void_p),
@@ -94,6 +94,7 @@ class FusedLstmGrad:
         self.device = dev
         KB = T * B
         self.scratch = torch.empty(int(lib.fm_lstm_train_scratch_floats(B, T)), dtype=torch.float32, device=dev)
+        # K-contiguous [rows, T*B] operands of the weight-gradient GEMMs
         self.g_enc = torch.empty((4 * H, KB), dtype=torch.bfloat16, device=dev)
         self.g_dec = torch.empty((4 * H, KB), dtype=torch.bfloat16, device=dev)
         self.h_enc = torch.zeros((KAUG, KB), dtype=torch.bfloat16, device=dev)
@@ -116,6 +117,8 @@ class FusedLstmGrad:
         self.wt_enc.copy_(model.enc_w_hh.detach().flatten()[tidx])
         self.wt_dec.copy_(model.dec_w_hh.detach().flatten()[tidx])
 
+    phases = 0  # profiling only: restrict the kernel to a subset of its four phases
+
     def launch(self, model, x: torch.Tensor) -> torch.Tensor:
         """Run the fused forward+backward; returns per-window errors ``[B]``."""
         lib = nat.require()
@@ -128,6 +131,7 @@ class FusedLstmGrad:
         a = LstmTrainArgs()
         a.x = x.data_ptr()
         a.B, a.T, a.F = self.B, self.T, self.F
+        a.phases = int(self.phases)
         a.w_enc, a.w_dec = self.w_enc.data_ptr(), self.w_dec.data_ptr()
         a.wt_enc, a.wt_dec = self.wt_enc.data_ptr(), self.wt_dec.data_ptr()
         a.w_out, a.b_out = w_out.data_ptr(), b_out.data_ptr()

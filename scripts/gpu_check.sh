@@ -24,6 +24,7 @@ for s in $STEPS; do
     lstm) run bench_lstm 600 python bench.py --config lstm --steps 20 --warmup 5 ;;
     mv) run bench_mv 600 python bench.py --config multivariate --steps 20 --warmup 5 ;;
     lstmauto) run bench_lstm_autograd 600 python bench.py --config lstm --steps 20 --warmup 5 --lstm-autograd ;;
+    lstmk) run lstm_kbench 300 python scripts/bench_lstm_kernels.py ;;
     lstmtests) run lstm_tests 600 python -m pytest tests/test_lstm.py -m gpu -x -q ;;
     proflstm)
       export TMPDIR=/tmp

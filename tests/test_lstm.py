@@ -203,6 +203,12 @@ def test_lstm_shard_gpu_matches_model(fp8):
     else:
         assert torch.allclose(err, ref, rtol=5e-2, atol=2e-3)
     assert int(sh.app_stats[:, 1].sum()) == n
+    # overlapped tick (training on a side stream, scoring with the pre-step weights)
+    before = [p.detach().clone() for p in sh.model.parameters()]
+    out = sh.tick(torch.full((n, F), 10.0, device=dev))
+    torch.cuda.synchronize()
+    assert int(sh.app_stats[:, 1].sum()) == n and torch.isfinite(out["err"]).all()
+    assert any(not torch.equal(b, p) for b, p in zip(before, sh.model.parameters()))
 
 
 def test_backward_register_plan_matches_wT_dgates():
@@ -258,3 +264,4 @@ def test_fused_lstm_training_grads_match_autograd(F):
         cos = torch.nn.functional.cosine_similarity(p.grad.flatten(), g.flatten(), dim=0)
         rel = (p.grad - g).norm() / g.norm().clamp(min=1e-12)
         assert cos > 0.99 and rel < 0.08, (name, float(cos), float(rel))
+
