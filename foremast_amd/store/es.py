@@ -1,0 +1,145 @@
+"""Elasticsearch 6.x job store (index ``documents``, type ``document``).
+
+Drop-in for the reference deployment: the reference service writes job docs
+into ES (``foremast-service/pkg/search/elasticsearchstore.go:17-18,37-53``)
+and brains poll them.  This store speaks the same REST surface so the engine
+can run next to the reference service, or the reference brain next to our
+service:
+
+* create  — ``PUT /documents/document/<id>/_create`` (409 ⇒ already exists,
+  i.e. idempotent create of a content-addressed job);
+* get     — ``GET /documents/document/<id>`` (``_source`` + ``_version``);
+* update  — read-modify-write with ``?version=<v>`` (ES internal optimistic
+  concurrency, available on 6.x) so two brains never both win a claim and a
+  worker that lost its lease cannot overwrite the new owner's result;
+* claim   — ``_search`` for open / in-progress docs, then one versioned
+  write per candidate; only writes that land are returned.
+
+The reference reconnects to ES every 3 s until it is up
+(``foremast-service/cmd/manager/main.go:248-260``); :meth:`wait_ready` does
+the same with a deadline instead of looping forever.
+"""
+
+from __future__ import annotations
+
+import json
+import time
+from typing import Any, Dict, List, Optional, Tuple
+
+import httpx
+
+from ..api import rest as r
+from ..utils.timeutil import format_rfc3339_nano
+from .jobstore import JobStore, is_claimable
+
+INDEX = "documents"
+DOC_TYPE = "document"
+
+
+class ElasticJobStore(JobStore):
+    def __init__(self, url: str, index: str = INDEX, doc_type: str = DOC_TYPE, timeout: float = 10.0,
+                 transport: Optional[httpx.BaseTransport] = None, refresh: str = "true") -> None:
+        self.base = url.rstrip("/")
+        self.index, self.doc_type = index, doc_type
+        self.refresh = refresh
+        kw: Dict[str, Any] = {"timeout": timeout}
+        if transport is not None:
+            kw["transport"] = transport
+        self.http = httpx.Client(**kw)
+
+    # ------------------------------------------------------------------ plumbing
+    def _doc_url(self, job_id: str, suffix: str = "") -> str:
+        return f"{self.base}/{self.index}/{self.doc_type}/{job_id}{suffix}"
+
+    def wait_ready(self, deadline_s: float = 60.0, every_s: float = 3.0) -> None:
+        t_end = time.time() + deadline_s
+        while True:
+            try:
+                if self.http.get(self.base + "/").status_code < 500:
+                    return
+            except httpx.HTTPError:
+                pass
+            if time.time() >= t_end:
+                raise ConnectionError(f"elasticsearch at {self.base} not reachable")
+            time.sleep(every_s)
+
+    def _get_versioned(self, job_id: str) -> Tuple[Optional[Dict[str, Any]], int]:
+        resp = self.http.get(self._doc_url(job_id))
+        if resp.status_code == 404:
+            return None, 0
+        resp.raise_for_status()
+        body = resp.json()
+        if not body.get("found", False):
+            return None, 0
+        return body["_source"], int(body.get("_version", 1))
+
+    def _put_versioned(self, doc: Dict[str, Any], version: int) -> bool:
+        resp = self.http.put(self._doc_url(doc["id"]), params={"version": version, "refresh": self.refresh},
+                             content=json.dumps(doc), headers={"Content-Type": "application/json"})
+        if resp.status_code == 409:
+            return False
+        resp.raise_for_status()
+        return True
+
+    # ------------------------------------------------------------------ JobStore
+    def get(self, job_id):
+        return self._get_versioned(job_id)[0]
+
+    def _insert_if_absent(self, doc):
+        resp = self.http.put(self._doc_url(doc["id"], "/_create"), params={"refresh": self.refresh},
+                             content=json.dumps(doc), headers={"Content-Type": "application/json"})
+        if resp.status_code == 409:
+            return False
+        resp.raise_for_status()
+        return True
+
+    def update(self, job_id, fields, expect_claimed_by=None, retries: int = 5):
+        for _ in range(retries):
+            d, ver = self._get_versioned(job_id)
+            if d is None:
+                return False
+            if expect_claimed_by is not None and d.get("claimed_by") != expect_claimed_by:
+                return False
+            d.update(fields)
+            d["modified_ts"] = fields.get("modified_ts", time.time())
+            d["modified_at"] = format_rfc3339_nano(d["modified_ts"])
+            if self._put_versioned(d, ver):
+                return True
+        return False
+
+    def _search(self, statuses, size: int = 1000) -> List[Tuple[Dict[str, Any], int]]:
+        body = {"query": {"bool": {"filter": [{"terms": {"status": list(statuses)}}]}},
+                "size": size, "version": True, "sort": [{"modified_ts": {"order": "asc"}}]}
+        resp = self.http.post(f"{self.base}/{self.index}/{self.doc_type}/_search", content=json.dumps(body),
+                              headers={"Content-Type": "application/json"})
+        if resp.status_code == 404:  # index not created yet
+            return []
+        resp.raise_for_status()
+        hits = resp.json().get("hits", {}).get("hits", [])
+        return [(h["_source"], int(h.get("_version", 1))) for h in hits]
+
+    def claim(self, worker, now=None, max_stuck_s=90.0, limit=64):
+        now = time.time() if now is None else now
+        out = []
+        for d, ver in self._search(r.OPEN_STATUSES + r.INPROGRESS_STATUSES):
+            if len(out) >= limit:
+                break
+            if not is_claimable(d, now, max_stuck_s):
+                continue
+            d.update(status=r.ST_PREPROCESS_INPROGRESS, claimed_by=worker, claimed_at=now,
+                     modified_ts=now, modified_at=format_rfc3339_nano(now))
+            if self._put_versioned(d, ver):  # lost races simply drop out
+                out.append(d)
+        return out
+
+    def all(self):
+        body = {"query": {"match_all": {}}, "size": 10000}
+        resp = self.http.post(f"{self.base}/{self.index}/{self.doc_type}/_search", content=json.dumps(body),
+                              headers={"Content-Type": "application/json"})
+        if resp.status_code == 404:
+            return []
+        resp.raise_for_status()
+        return [h["_source"] for h in resp.json().get("hits", {}).get("hits", [])]
+
+    def close(self):
+        self.http.close()

@@ -1,0 +1,110 @@
+"""In-process fake of the Elasticsearch 6.x REST subset the job store uses
+(WSGI app; mount with ``httpx.WSGITransport`` in tests, or serve it with any
+WSGI server for local runs).
+
+Supported: ``GET /``, ``GET|PUT /<index>/<type>/<id>`` (``?version=`` for
+optimistic concurrency → 409 on mismatch), ``PUT .../<id>/_create`` (409 if
+present), ``POST /<index>/<type>/_search`` with ``match_all`` or a
+``bool.filter[terms.status]`` query, ``size``, ``version`` and a single-key
+``sort``.  Documents are versioned per id exactly like ES internal versions.
+"""
+
+from __future__ import annotations
+
+import json
+import threading
+from typing import Any, Dict, List, Tuple
+from urllib.parse import parse_qs
+
+
+class FakeElasticsearch:
+    def __init__(self) -> None:
+        self.docs: Dict[Tuple[str, str], Tuple[Dict[str, Any], int]] = {}
+        self.lock = threading.Lock()
+        self.requests: List[str] = []
+        self.fail_next = 0  # fault injection: return 503 for the next N requests
+
+    # ------------------------------------------------------------------ WSGI
+    def __call__(self, environ, start_response):
+        method = environ["REQUEST_METHOD"]
+        path = environ.get("PATH_INFO", "/")
+        qs = {k: v[-1] for k, v in parse_qs(environ.get("QUERY_STRING", "")).items()}
+        n = int(environ.get("CONTENT_LENGTH") or 0)
+        raw = environ["wsgi.input"].read(n) if n else b""
+        self.requests.append(f"{method} {path}")
+        if self.fail_next > 0:
+            self.fail_next -= 1
+            return self._reply(start_response, 503, {"error": "injected"})
+        try:
+            status, body = self.handle(method, path, qs, json.loads(raw) if raw else None)
+        except (ValueError, KeyError) as e:
+            status, body = 400, {"error": str(e)}
+        return self._reply(start_response, status, body)
+
+    @staticmethod
+    def _reply(start_response, status, body):
+        data = json.dumps(body).encode()
+        reason = {200: "OK", 201: "Created", 400: "Bad Request", 404: "Not Found", 409: "Conflict",
+                  503: "Service Unavailable"}.get(status, "")
+        start_response(f"{status} {reason}", [("Content-Type", "application/json"),
+                                              ("Content-Length", str(len(data)))])
+        return [data]
+
+    # ------------------------------------------------------------------ API
+    def handle(self, method: str, path: str, qs: Dict[str, str], body: Any):
+        parts = [p for p in path.split("/") if p]
+        if not parts:
+            return 200, {"version": {"number": "6.4.2"}, "tagline": "You Know, for Search"}
+        if len(parts) == 3 and parts[2] == "_search" and method in ("GET", "POST"):
+            return self._search(parts[0], body or {})
+        if len(parts) == 4 and parts[3] == "_create" and method in ("PUT", "POST"):
+            return self._put(parts[0], parts[2], body, create=True, version=None)
+        if len(parts) == 3:
+            idx, _typ, did = parts
+            if method == "GET":
+                with self.lock:
+                    cur = self.docs.get((idx, did))
+                if cur is None:
+                    return 404, {"_index": idx, "_id": did, "found": False}
+                return 200, {"_index": idx, "_type": _typ, "_id": did, "_version": cur[1], "found": True,
+                             "_source": cur[0]}
+            if method in ("PUT", "POST"):
+                ver = int(qs["version"]) if "version" in qs else None
+                return self._put(idx, did, body, create=False, version=ver)
+        return 400, {"error": f"unsupported {method} {path}"}
+
+    def _put(self, idx: str, did: str, doc: Any, create: bool, version):
+        with self.lock:
+            cur = self.docs.get((idx, did))
+            if create and cur is not None:
+                return 409, {"error": {"type": "version_conflict_engine_exception"}}
+            if version is not None and (cur is None or cur[1] != version):
+                return 409, {"error": {"type": "version_conflict_engine_exception"}}
+            ver = 1 if cur is None else cur[1] + 1
+            self.docs[(idx, did)] = (json.loads(json.dumps(doc)), ver)
+        return (201 if ver == 1 else 200), {"_index": idx, "_id": did, "_version": ver,
+                                            "result": "created" if ver == 1 else "updated"}
+
+    def _search(self, idx: str, body: Dict[str, Any]):
+        with self.lock:
+            items = [(did, d, v) for (i, did), (d, v) in self.docs.items() if i == idx]
+        if not any(True for (i, _d) in self.docs if i == idx):
+            return 404, {"error": {"type": "index_not_found_exception"}}
+        q = body.get("query", {"match_all": {}})
+        statuses = None
+        for f in q.get("bool", {}).get("filter", []):
+            if "terms" in f and "status" in f["terms"]:
+                statuses = set(f["terms"]["status"])
+        if statuses is not None:
+            items = [x for x in items if x[1].get("status") in statuses]
+        for s in body.get("sort", []):
+            (key, spec), = s.items()
+            items.sort(key=lambda x: x[1].get(key, 0), reverse=spec.get("order") == "desc")
+        items = items[: int(body.get("size", 10))]
+        hits = []
+        for did, d, v in items:
+            h = {"_index": idx, "_id": did, "_source": json.loads(json.dumps(d))}
+            if body.get("version"):
+                h["_version"] = v
+            hits.append(h)
+        return 200, {"hits": {"total": len(hits), "hits": hits}}

@@ -127,9 +127,20 @@ def _req(strategy="canary", **kw):
                 "start": 1577836860, "end": 1577837460, "step": 60}}}, **kw}}
 
 
-@pytest.mark.parametrize("store_kind", ["memory", "sqlite"])
+def _make_store(kind, tmp_path):
+    if kind == "memory":
+        return MemoryJobStore()
+    if kind == "sqlite":
+        return SqliteJobStore(str(tmp_path / "jobs.db"))
+    import httpx
+    from foremast_amd.store.es import ElasticJobStore
+    from foremast_amd.store.fake_es import FakeElasticsearch
+    return ElasticJobStore("http://es:9200", transport=httpx.WSGITransport(app=FakeElasticsearch()))
+
+
+@pytest.mark.parametrize("store_kind", ["memory", "sqlite", "es"])
 def test_register_and_lookup(tmp_path, store_kind):
-    store = MemoryJobStore() if store_kind == "memory" else SqliteJobStore(str(tmp_path / "jobs.db"))
+    store = _make_store(store_kind, tmp_path)
     code, body = svc.register(store, _req())
     assert code == 200 and body["status"] == "new" and body["statusCode"] == 200 and "reason" not in body
     code2, body2 = svc.register(store, _req())
@@ -195,3 +206,46 @@ def test_service_http_and_proxy():
             r = await c.get("/api/v1/query_range?" + q + "&raw=1")
             assert r.json()["status"] == "success"
     asyncio.run(go())
+
+
+@pytest.mark.parametrize("store_kind", ["memory", "sqlite", "es"])
+def test_store_claim_lease_semantics(tmp_path, store_kind):
+    """Claims are exclusive, stuck jobs are taken over after MAX_STUCK_IN_SECONDS,
+    and a worker that lost its lease cannot overwrite the new owner's result."""
+    store = _make_store(store_kind, tmp_path)
+    ids = [svc.register(store, _req(strategy=s))[1]["jobId"] for s in ("canary", "rollover", "continuous")]
+    a = store.claim("A", now=1000.0, limit=2)
+    b = store.claim("B", now=1000.0)
+    got_a, got_b = {d["id"] for d in a}, {d["id"] for d in b}
+    assert len(got_a) == 2 and len(got_b) == 1 and not (got_a & got_b) and (got_a | got_b) == set(ids)
+    assert store.claim("C", now=1010.0) == []            # in progress, not stuck yet
+    stolen = store.claim("C", now=10_000.0, max_stuck_s=90.0)
+    assert {d["id"] for d in stolen} == set(ids)          # stuck-job takeover
+    jid = a[0]["id"]
+    assert not store.update(jid, {"status": "completed_health"}, expect_claimed_by="A")
+    assert store.update(jid, {"status": "completed_health"}, expect_claimed_by="C")
+    assert store.get(jid)["status"] == "completed_health"
+
+
+def test_es_store_conflicts_and_faults():
+    import httpx
+    from foremast_amd.store.es import ElasticJobStore
+    from foremast_amd.store.fake_es import FakeElasticsearch
+    from foremast_amd.store.jobstore import open_store
+    fake = FakeElasticsearch()
+    s1 = ElasticJobStore("http://es:9200", transport=httpx.WSGITransport(app=fake))
+    s2 = ElasticJobStore("http://es:9200", transport=httpx.WSGITransport(app=fake))
+    assert s1.all() == [] and s1.claim("x") == []        # index does not exist yet
+    jid = svc.register(s1, _req())[1]["jobId"]
+    assert s2.get(jid)["status"] == "initial"
+    # interleaved read-modify-write: s2's stale version is rejected, then retried
+    d, v = s1._get_versioned(jid)
+    assert s2.update(jid, {"reason": "from s2"})
+    d["reason"] = "stale"
+    assert not s1._put_versioned(d, v)
+    assert s1.get(jid)["reason"] == "from s2"
+    fake.fail_next = 1
+    with pytest.raises(httpx.HTTPStatusError):
+        s1.get(jid)
+    s1.wait_ready(deadline_s=1.0)
+    assert isinstance(open_store("http://es:9200"), ElasticJobStore)
