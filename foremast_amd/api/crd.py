@@ -45,6 +45,9 @@ REMEDIATIONS = (REMEDIATION_NONE, REMEDIATION_AUTO_ROLLBACK, REMEDIATION_AUTO_PA
 
 # Annotations / naming (Barrelman.go:56-62, MonitorController.go:168)
 ANNOTATION_DEPLOYMENT_NAME = "deployment.kubernetes.io/name"
+# set by our rollback on the Deployment (a fresh value per rollback): the
+# rollout it triggers is the remediation itself and must not start a new job
+ANNOTATION_ROLLBACK_ID = "deployment.foremast.ai/rollback-id"
 ANNOTATION_STRATEGY = "deployment.foremast.ai/strategy"
 ANNOTATION_MONITORING = "foremast.ai/monitoring"
 ANNOTATION_ROLLBACK_MESSAGE = "deployment.foremast.ai/rollbackMessage"

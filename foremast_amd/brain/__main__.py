@@ -1,0 +1,64 @@
+"""``python -m foremast_amd.brain`` — the scoring worker process.
+
+Replaces the foremast-brain container (``deploy/foremast/3_brain/foremast-brain.yaml``):
+same environment variables (``ES_ENDPOINT``, ``ML_ALGORITHM``, ``threshold``,
+``bound``, ``metric_type{i}`` …, ``MAX_STUCK_IN_SECONDS``; parsed by
+:class:`~foremast_amd.utils.config.BrainConfig`), same Prometheus exposition
+on :8000 (``foremastbrain:<metric>_{upper,lower,anomaly}`` plus engine
+metrics).  ``FOREMAST_JOB_STORE`` (``sqlite:///…`` / ``memory://``) overrides
+``ES_ENDPOINT``.  Several processes can share one store: claims are leases.
+"""
+
+from __future__ import annotations
+
+import argparse
+import asyncio
+import logging
+import os
+import signal
+
+from ..store.jobstore import open_store
+from ..utils.config import BrainConfig
+from ..utils.metrics import BrainMetrics
+from .worker import BrainWorker
+
+
+def parse(argv=None):
+    p = argparse.ArgumentParser(prog="foremast-brain")
+    p.add_argument("--store", default=os.environ.get("FOREMAST_JOB_STORE") or os.environ.get("ES_ENDPOINT"))
+    p.add_argument("--metrics-port", type=int, default=int(os.environ.get("FOREMAST_METRICS_PORT", "8000")))
+    p.add_argument("--worker-id", default=None)
+    p.add_argument("--run-seconds", type=float, default=None)
+    return p.parse_args(argv)
+
+
+async def run(args) -> BrainWorker:
+    cfg = BrainConfig.from_env()
+    store = open_store(args.store)
+    metrics = BrainMetrics()
+    if args.metrics_port:
+        from prometheus_client import start_http_server
+        start_http_server(args.metrics_port, registry=metrics.registry)
+    worker = BrainWorker(store, cfg, worker_id=args.worker_id, metrics=metrics)
+    stop = asyncio.Event()
+    loop = asyncio.get_running_loop()
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        try:
+            loop.add_signal_handler(sig, stop.set)
+        except (NotImplementedError, RuntimeError):
+            pass
+    if args.run_seconds is not None:
+        loop.call_later(args.run_seconds, stop.set)
+    await worker.run_forever(stop)
+    store.close()
+    return worker
+
+
+def main(argv=None) -> None:
+    logging.basicConfig(level=os.environ.get("FOREMAST_LOG_LEVEL", "INFO"),
+                        format="%(asctime)s %(name)s %(levelname)s %(message)s")
+    asyncio.run(run(parse(argv)))
+
+
+if __name__ == "__main__":
+    main()

@@ -271,6 +271,11 @@ class Barrelman:
                       for a, b in zip(oc, nc))
         if not changed and strategy != r.STRATEGY_CANARY:
             return None
+        rb_new = (new.get("metadata", {}).get("annotations") or {}).get(crd.ANNOTATION_ROLLBACK_ID)
+        rb_old = (old.get("metadata", {}).get("annotations") or {}).get(crd.ANNOTATION_ROLLBACK_ID)
+        if rb_new and rb_new != rb_old:
+            return None  # the rollout our own rollback triggered (revision numbers move on, so
+            #              the reference's `revision == rollbackRevision` test cannot see it)
         name = new.get("metadata", {}).get("name", "")
         mon = await self._get_monitor(ns, name)
         not_found = mon is None

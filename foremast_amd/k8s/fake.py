@@ -285,8 +285,10 @@ class FakeCluster:
         tpl = copy.deepcopy(target["spec"]["template"])
         tpl.get("metadata", {}).get("labels", {}).pop("pod-template-hash", None)
         depl["spec"]["template"] = tpl
+        ann = depl["metadata"].setdefault("annotations", {})
+        ann["deployment.foremast.ai/rollback-id"] = f"{revision}-{time.time_ns()}"
         if message:
-            depl["metadata"].setdefault("annotations", {})["deployment.foremast.ai/rollbackMessage"] = message
+            ann["deployment.foremast.ai/rollbackMessage"] = message
         depl["metadata"].pop("resourceVersion", None)
         self.actions.append({"action": "rollback", "namespace": namespace, "name": name,
                              "revision": revision, "message": message})

@@ -214,3 +214,48 @@ def test_unknown_when_no_current_data():
         m2 = crd.DeploymentMonitor.from_dict(kube.get_sync("deploymentmonitors", NS, "demo"))
         assert m2.status.phase == crd.PHASE_ABORT  # service maps completed_unknown → abort (Q4)
     asyncio.run(go())
+
+
+def test_live_loops_rollout_to_rollback():
+    """The real run loops (deployment informer, status poller, monitor
+    informer, sync work queue, brain worker) wired together: a faulty v2
+    rollout ends in a rollback with nobody calling handlers by hand."""
+    from foremast_amd.controller import __main__ as cli
+    world = build_world("moving_average_all")
+    clock, kube, prom, store, barrel, mc, brain, metrics = world
+    args = cli.parse(["--namespace", "foremast", "--poll-seconds", "0.05", "--workers", "2"])
+    svc_transport = barrel.analyst_factory("x").http._transport if hasattr(barrel.analyst_factory("x"), "http") \
+        else None
+
+    async def go():
+        stop = asyncio.Event()
+        ctl = asyncio.create_task(cli.run(args, kube=kube, stop=stop, clock=clock, pod_retry_sleep=0,
+                                          analyst_factory=barrel.analyst_factory))
+        brain_task = asyncio.create_task(brain.run_forever(stop))
+        await asyncio.sleep(0.2)
+        kube.apply_deployment(NS, "demo", "demo", "foremast/demo:v1", replicas=2, labels={"appType": "spring-boot"})
+        await asyncio.sleep(0.3)
+        old_hash = kube.list_sync("replicasets", NS)[0]["metadata"]["labels"]["pod-template-hash"]
+        kube.apply_deployment(NS, "demo", "demo", "foremast/demo:v2", replicas=2, labels={"appType": "spring-boot"})
+        register_pod_series(kube, prom, old_hash, spike_at=T0 + 120)
+        for _ in range(100):
+            mon = kube.get_sync("deploymentmonitors", NS, "demo")
+            if (mon.get("status") or {}).get("jobId"):
+                break
+            await asyncio.sleep(0.05)
+        clock.t = T0 + 300  # the brain may score now (data for the watch window exists)
+        for _ in range(200):
+            if any(a["action"] == "rollback" for a in kube.actions):
+                break
+            await asyncio.sleep(0.05)
+        stop.set()
+        bm = await asyncio.wait_for(ctl, 10)
+        await asyncio.wait_for(brain_task, 10)
+        rb = [a for a in kube.actions if a["action"] == "rollback"]
+        assert rb and rb[0]["revision"] == 1
+        assert any(e["reason"] == "Synced" for e in bm.events)
+        mon = crd.DeploymentMonitor.from_dict(kube.get_sync("deploymentmonitors", NS, "demo"))
+        assert mon.status.phase == crd.PHASE_UNHEALTHY and mon.status.remediation_taken
+
+    del svc_transport
+    asyncio.run(go())
