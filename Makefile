@@ -1,0 +1,34 @@
+# foremast-amd build / test entry points (reference C33: generate → fmt → vet → test → build)
+PY ?= python
+GPURUN ?= /usr/local/graft/bin/gpurun
+
+.PHONY: all build native test test-gpu bench deploy lint clean image
+
+all: build test
+
+build:            ## compile every HIP kernel for gfx950 + the C++ ingest parser, import the package
+	$(PY) -c "import __graft_entry__ as g; g.build()"
+
+native: build
+
+test:             ## CPU suite (gloo for the multi-process paths)
+	$(PY) -m pytest tests -x -q -m "not gpu"
+
+test-gpu:         ## GPU suite on an MI355X (run on the box)
+	$(PY) -m pytest tests -x -q -m gpu
+
+bench:            ## headline benchmark, 1 GPU
+	$(PY) bench.py
+
+deploy:           ## regenerate the Kubernetes bundle from the code's type/query tables
+	$(PY) -m foremast_amd.deploy deploy/foremast
+
+lint:
+	$(PY) -m compileall -q foremast_amd tests bench.py __graft_entry__.py
+
+image:
+	docker build -t foremast-amd:latest .
+
+clean:
+	rm -rf foremast_amd/ops/_lib foremast_amd/ingest/_lib
+	find . -name __pycache__ -prune -exec rm -rf {} +

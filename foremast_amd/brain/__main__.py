@@ -32,13 +32,27 @@ def parse(argv=None):
     return p.parse_args(argv)
 
 
+def _bind_gpu() -> int:
+    """One scorer process per GPU under torchrun: bind LOCAL_RANK's device.
+    Ranks share nothing but the job store (lease-based claims)."""
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local % torch.cuda.device_count())
+    except ImportError:
+        pass
+    return local
+
+
 async def run(args) -> BrainWorker:
+    local = _bind_gpu()
     cfg = BrainConfig.from_env()
     store = open_store(args.store)
     metrics = BrainMetrics()
     if args.metrics_port:
         from prometheus_client import start_http_server
-        start_http_server(args.metrics_port, registry=metrics.registry)
+        start_http_server(args.metrics_port + local, registry=metrics.registry)
     worker = BrainWorker(store, cfg, worker_id=args.worker_id, metrics=metrics)
     stop = asyncio.Event()
     loop = asyncio.get_running_loop()
