@@ -29,6 +29,8 @@ def parse(argv=None):
     p.add_argument("--metrics-port", type=int, default=int(os.environ.get("FOREMAST_METRICS_PORT", "8000")))
     p.add_argument("--worker-id", default=None)
     p.add_argument("--run-seconds", type=float, default=None)
+    p.add_argument("--model-cache", default=os.environ.get("FOREMAST_MODEL_CACHE"),
+                   help="safetensors checkpoint of the LSTM model cache (loaded at start, saved at exit)")
     return p.parse_args(argv)
 
 
@@ -54,6 +56,13 @@ async def run(args) -> BrainWorker:
         from prometheus_client import start_http_server
         start_http_server(args.metrics_port + local, registry=metrics.registry)
     worker = BrainWorker(store, cfg, worker_id=args.worker_id, metrics=metrics)
+    cache_path = None
+    if args.model_cache:
+        from .multivariate import LstmJobScorer, ModelCache
+        cache_path = args.model_cache.replace("{rank}", str(local))
+        if os.path.exists(cache_path):
+            cache = ModelCache.load(cache_path, cfg.max_cache_size, device=worker.scorer.device)
+            worker.lstm = LstmJobScorer(device=worker.scorer.device, cache=cache, threshold=cfg.lstm_threshold)
     stop = asyncio.Event()
     loop = asyncio.get_running_loop()
     for sig in (signal.SIGTERM, signal.SIGINT):
@@ -64,6 +73,8 @@ async def run(args) -> BrainWorker:
     if args.run_seconds is not None:
         loop.call_later(args.run_seconds, stop.set)
     await worker.run_forever(stop)
+    if cache_path and worker.lstm is not None:
+        worker.lstm.cache.save(cache_path)
     store.close()
     return worker
 

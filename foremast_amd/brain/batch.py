@@ -29,6 +29,7 @@ from ..models import bivariate as biv_ref
 from ..models import detect as det_ref
 from ..models import moving_average as ma_ref
 from ..models import pairwise as pw_ref
+from ..models import prophet_lite as pl_ref
 from ..models import smoothing as sm_ref
 from ..utils.config import BrainConfig
 
@@ -113,8 +114,8 @@ class BatchScorer:
             m = self._season_points(t.step)
             if algo == "holt_winters" and np.count_nonzero(~np.isnan(t.hist)) and len(t.hist) < 2 * m:
                 algo = "double_exponential_smoothing"
-            if algo in ("bivariate_normal", "lstm", "prophet"):
-                algo = "moving_average_all"  # multivariate handled by score_multivariate
+            if algo in ("bivariate_normal", "lstm", "auto"):
+                algo = "moving_average_all"  # per-metric part; the joint model runs in the worker
             groups.setdefault((algo, m if algo == "holt_winters" else 0), []).append(i)
         for (algo, m), idx in groups.items():
             sub = [tasks[i] for i in idx]
@@ -153,7 +154,26 @@ class BatchScorer:
         t_hz = torch.from_numpy(hz).to(dev)
         t_hist = torch.from_numpy(hist).to(dev)
         mode = sm_ref.MODE_BY_NAME.get(algo)
-        if self.gpu:
+        if algo == "prophet":
+            # batched additive trend + Fourier seasonality (one [B, P, P] solve; torch on the device)
+            C = t_cur.shape[1]
+            cts = np.zeros((B, C), dtype=np.float64)
+            for i, t in enumerate(tasks):
+                n = len(t.cur_ts)
+                if n:
+                    cts[i, :n] = t.cur_ts
+                    cts[i, n:] = t.cur_ts[-1]
+                else:
+                    cts[i, :] = t.hist_end
+            ends = torch.tensor([t.hist_end for t in tasks], dtype=torch.float64, device=dev)
+            steps = torch.tensor([t.step for t in tasks], dtype=torch.float64, device=dev)
+            fit = pl_ref.fit_prophet(t_hist.float(), ends, steps)
+            f = pl_ref.forecast(fit, torch.from_numpy(cts).to(dev))
+            d = det_ref.detect(f, fit.sigma.float(), t_cur, t_thr, t_bnd, t_low, differs=differs,
+                               pairwise_scale=cfg.pairwise_scale,
+                               model_ok=fit.n_valid >= cfg.min_historical_points)
+            upper, lower, verdict, anom = d.upper, d.lower, d.verdict, d.anomaly
+        elif self.gpu:
             from ..ops import kernels as K
             spec = K.DetectSpec(horizons=t_hz, threshold=t_thr, bound=t_bnd, min_lower=t_low, cur=t_cur,
                                 differs=differs, pw_scale=cfg.pairwise_scale, min_valid=cfg.min_historical_points)

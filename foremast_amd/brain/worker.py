@@ -82,6 +82,7 @@ class BrainWorker:
         self.clock = clock
         self.metrics = metrics or BrainMetrics()
         self.batch_limit = batch_limit
+        self.lstm = None  # LstmJobScorer, created on first multivariate LSTM job
 
     # ------------------------------------------------------------------ planning
     def plan(self, doc: Dict[str, Any]) -> JobPlan:
@@ -186,12 +187,22 @@ class BrainWorker:
                           min_lower=th.min_lower_bound)
 
     def _multivariate(self, plans: List[JobPlan], per_job) -> None:
+        """Joint models on top of the per-metric verdicts: ``bivariate_normal``
+        (>= 2 metrics, first two aliases), ``lstm`` (>= 2 metrics), or
+        ``auto`` = the design doc's dispatch (2 metrics → bivariate normal,
+        3+ → LSTM autoencoder; ``docs/guides/design.md:76-84``)."""
         algo = self.cfg.algorithm
-        if algo != "bivariate_normal":
+        if algo not in ("bivariate_normal", "lstm", "auto"):
+            return
+        lstm_jobs = [i for i, items in per_job.items()
+                     if (algo == "lstm" and len(items) >= 2) or (algo == "auto" and len(items) >= 3)]
+        if lstm_jobs:
+            self._score_lstm(per_job, lstm_jobs)
+        if algo == "lstm":
             return
         pairs, owners = [], []
         for i, items in per_job.items():
-            if len(items) >= 2:
+            if len(items) == 2 or (algo == "bivariate_normal" and len(items) >= 2):
                 (ta, _), (tb, _) = items[0], items[1]
                 pairs.append((ta, tb))
                 owners.append(i)
@@ -203,6 +214,23 @@ class BrainWorker:
                 ra.anomalies = [(float(ta.cur_ts[j]), float(ta.cur_vals[j]),
                                  ta.cur_tags[j] if j < len(ta.cur_tags) else "") for j in idx]
                 ra.model = rb.model = "bivariate_normal"
+
+    def _score_lstm(self, per_job, jobs: List[int]) -> None:
+        from .multivariate import LstmJobScorer, ModelCache, align_job
+        if self.lstm is None:
+            self.lstm = LstmJobScorer(device=self.scorer.device, cache=ModelCache(self.cfg.max_cache_size),
+                                      threshold=self.cfg.lstm_threshold)
+        for i in jobs:
+            items = sorted(per_job[i], key=lambda tr: tr[0].alias)
+            tasks = [t for t, _ in items]
+            hist, cts, cur = align_job(tasks)
+            key = self.lstm.cache.key(tasks[0].namespace, tasks[0].app, [t.alias for t in tasks])
+            verdict, bad, _z = self.lstm.score_job(key, hist, cts, cur, now=self.clock())
+            for f, (t, res) in enumerate(items):
+                res.model = "lstm"
+                if verdict == 1:
+                    res.verdict = 1
+                    res.anomalies = [(float(cts[j]), float(cur[j, f]), "") for j in bad]
 
     def _finish(self, p: JobPlan, items: List[Tuple[MetricTask, TaskResult]], errors: List[str], now: float):
         doc_id = p.doc["id"]

@@ -61,6 +61,7 @@ class BrainConfig:
     pairwise_threshold: float = 0.05
     min_historical_points: int = 60
     max_cache_size: int = 1000
+    lstm_threshold: float = 4.0  # z-score of the joint reconstruction error (ML_LSTM_THRESHOLD)
     # --- MI355X engine knobs -------------------------------------------------------
     dtype: str = "bf16"
     device: str = "auto"
@@ -123,6 +124,7 @@ class BrainConfig:
         c.min_historical_points = int(f("MIN_HISTORICAL_DATA_POINT_TO_MEASURE",
                                         c.min_historical_points, int))
         c.max_cache_size = int(f("MAX_CACHE_SIZE", c.max_cache_size, int))
+        c.lstm_threshold = f("ML_LSTM_THRESHOLD", c.lstm_threshold)
         c.dtype = e.get("FOREMAST_DTYPE", c.dtype)
         c.device = e.get("FOREMAST_DEVICE", c.device)
         c.ring_len = int(f("FOREMAST_RING_LEN", c.ring_len, int))

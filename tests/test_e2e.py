@@ -111,7 +111,7 @@ async def _drive_rollout(world):
     return mon
 
 
-@pytest.mark.parametrize("algorithm", ["moving_average_all", "holt_winters"])
+@pytest.mark.parametrize("algorithm", ["moving_average_all", "holt_winters", "prophet"])
 def test_rollout_spike_rolls_back(algorithm):
     world = build_world(algorithm)
     clock, kube, prom, store, barrel, mc, brain, metrics = world

@@ -156,3 +156,29 @@ def test_bivariate():
     exp = dv @ inv @ dv
     assert d2[0, 1].item() == pytest.approx(exp, rel=1e-3)
     assert d2[0, 0].item() < 0.1
+
+
+def test_prophet_lite_recovers_trend_and_seasonality():
+    """Parity unpinned (the prophet package is not installed): checks the
+    batched ridge fit against the generating model, gap handling, and that a
+    batch equals independent per-series fits."""
+    import math
+    from foremast_amd.models import prophet_lite as P
+    torch.manual_seed(0)
+    B, T, step = 3, 3 * 1440, 60.0
+    end = torch.full((B,), 1.7e9, dtype=torch.float64)
+    j = torch.arange(T, dtype=torch.float64)
+    ts = end[:, None] - (T - 1 - j) * step
+
+    def truth(t):
+        return 20 + 4 * torch.sin(2 * math.pi * t / 86400 + torch.arange(B)[:, None]) + 2e-5 * (t - 1.69e9)
+    y = truth(ts) + 0.2 * torch.randn(B, T, dtype=torch.float64)
+    y[1, 500:900] = float("nan")
+    fit = P.fit_prophet(y.float(), end, torch.full((B,), step))
+    assert fit.seasons and fit.seasons[0][0] == P.DAY
+    assert torch.allclose(fit.sigma, torch.full((B,), 0.2), atol=0.03)
+    cts = end[:, None] + torch.arange(1, 31, dtype=torch.float64)[None, :] * step
+    f = P.forecast(fit, cts)
+    assert float((f - truth(cts)).abs().max()) < 0.15
+    one = P.fit_prophet(y[1:2].float(), end[1:2], torch.full((1,), step))
+    assert torch.allclose(P.forecast(one, cts[1:2]), f[1:2], atol=1e-4)

@@ -1,0 +1,120 @@
+"""Joint multi-metric scoring: LSTM autoencoder per job (3+ metrics under
+ML_ALGORITHM=auto), the LRU model cache and its safetensors checkpoint."""
+
+import asyncio
+import json
+
+import httpx
+import numpy as np
+import torch
+
+from foremast_amd.brain.multivariate import LstmJobScorer, ModelCache, align_job
+from foremast_amd.models.lstm_ae import LSTMAutoencoder
+
+
+def _hist(T=600, F=3, seed=0):
+    rng = np.random.default_rng(seed)
+    t = np.arange(T)
+    base = np.sin(2 * np.pi * t / 60)[:, None]
+    h = np.concatenate([1 + 0.5 * base, 2 + 0.3 * base, 5 - base], 1)[:, :F]
+    return (h + 0.05 * rng.standard_normal((T, F))).astype(np.float32)
+
+
+def test_lstm_job_scorer_flags_joint_anomaly_and_caches():
+    sc = LstmJobScorer(device="cpu", cache=ModelCache(2), train_steps=60, train_batch=64, threshold=4.0)
+    h = _hist()
+    T = len(h)
+    cts = np.arange(T, T + 10, dtype=np.float64)
+    t = np.arange(T, T + 10)
+    normal = np.stack([1 + 0.5 * np.sin(2 * np.pi * t / 60), 2 + 0.3 * np.sin(2 * np.pi * t / 60),
+                       5 - np.sin(2 * np.pi * t / 60)], 1).astype(np.float32)
+    v, bad, z = sc.score_job("ns/app/a,b,c", h, cts, normal, now=0.0)
+    assert v == 0 and bad == []
+    spiky = normal.copy()
+    spiky[6:, 0] += 40.0
+    v, bad, z = sc.score_job("ns/app/a,b,c", h, cts, spiky, now=1.0)
+    assert v == 1 and bad and min(bad) >= 6 and sc.trained == 1  # second call hit the cache
+    assert sc.cache.hits == 1
+    sc.score_job("k2", h, cts, normal, now=2.0)
+    sc.score_job("k3", h, cts, normal, now=3.0)
+    assert len(sc.cache) == 2 and sc.cache.evictions == 1 and "ns/app/a,b,c" not in sc.cache.keys()
+
+
+def test_model_cache_checkpoint_roundtrip(tmp_path):
+    c = ModelCache(10)
+    from foremast_amd.brain.multivariate import CachedModel
+    torch.manual_seed(0)
+    m = LSTMAutoencoder(3, 16)
+    c.put("a/b/x,y,z", CachedModel(model=m, mu=0.5, sigma=0.1, mean=np.ones(3, np.float32),
+                                   std=np.full(3, 2, np.float32), window=16, trained_at=123.0))
+    path = str(tmp_path / "models" / "cache.safetensors")
+    c.save(path)
+    c2 = ModelCache.load(path)
+    e = c2.get("a/b/x,y,z")
+    assert e.mu == 0.5 and e.window == 16 and e.trained_at == 123.0
+    x = torch.randn(4, 16, 3)
+    with torch.no_grad():
+        assert torch.allclose(e.model.recon_error(x), m.recon_error(x))
+
+
+def test_align_job_common_timestamps():
+    from foremast_amd.brain.batch import MetricTask
+    def task(alias, vals, ts):
+        return MetricTask(job_id="j", alias=alias, metric=alias, namespace="ns", app="a", step=60.0,
+                          hist=np.arange(10, dtype=np.float32), hist_end=0.0, cur_ts=np.array(ts, np.float64),
+                          cur_vals=np.array(vals, np.float32))
+    a = task("a", [1, 3, 5], [60, 60, 120])       # two pods at t=60 → mean 2
+    b = task("b", [7, 9], [60, 180])
+    hist, cts, cur = align_job([a, b])
+    assert hist.shape == (10, 2) and list(cts) == [60.0] and cur.tolist() == [[2.0, 7.0]]
+
+
+def test_worker_auto_routes_three_metrics_to_lstm():
+    """Brain worker, ML_ALGORITHM=auto, a job with 3 metrics: the joint LSTM
+    flags the 5xx storm of a faulty rollout."""
+    from foremast_amd.brain.batch import BatchScorer
+    from foremast_amd.brain.worker import BrainWorker
+    from foremast_amd.promql import synth
+    from foremast_amd.promql.client import PromClient
+    from foremast_amd.promql.fake import FakePrometheus
+    from foremast_amd.service import app as svc
+    from foremast_amd.store import MemoryJobStore
+    from foremast_amd.utils.config import BrainConfig, reference_default_env
+
+    T0 = 1_700_000_000.0
+    clock = lambda: T0 + 300  # noqa: E731
+    prom = FakePrometheus(clock=clock)
+    metrics = {"error5xx": "http_server_requests_error_5xx", "error4xx": "http_server_requests_error_4xx",
+               "latency": "http_server_requests_latency"}
+    for i, (alias, m) in enumerate(metrics.items()):
+        prom.add("namespace_app_per_pod:" + m, {"namespace": "ns", "app": "demo"},
+                 synth.error_rate(base=0.3 + i, spread=0.05, seed=i))
+        gen = synth.error_rate(base=0.3 + i, spread=0.05, seed=10 + i)
+        if alias == "error5xx":
+            gen = synth.step_change(gen, at=T0 + 60, factor=0.0, add=40.0)
+        prom.add("namespace_pod:" + m, {"namespace": "ns", "pod": "demo-v2-1"}, gen)
+    store = MemoryJobStore()
+    cur, hist = {}, {}
+    for alias, m in metrics.items():
+        params = {"endpoint": "http://prometheus:9090/api/v1/", "step": 60}
+        cur[alias] = {"dataSourceType": "prometheus", "parameters": dict(
+            params, query=f'namespace_pod:{m}{{namespace="ns",pod="demo-v2-1"}}', start=int(T0), end=int(T0 + 600))}
+        hist[alias] = {"dataSourceType": "prometheus", "parameters": dict(
+            params, query=f'namespace_app_per_pod:{m}{{namespace="ns",app="demo"}}',
+            start=int(T0 - 2 * 86400), end=int(T0))}
+    code, body = svc.register(store, {"appName": "demo", "startTime": "2023-11-14T22:13:20Z",
+                                      "endTime": "2023-11-14T22:23:20Z", "strategy": "rollingupdate",
+                                      "metrics": {"current": cur, "historical": hist}})
+    assert code == 200, body
+    env = reference_default_env()
+    env.update(ML_ALGORITHM="auto", MIN_HISTORICAL_DATA_POINT_TO_MEASURE="10", threshold="1000",
+               threshold0="1000", threshold1="1000", threshold2="1000")  # univariate models can't fire
+    cfg = BrainConfig.from_env(env)
+    brain = BrainWorker(store, cfg, prom=PromClient(transport=httpx.ASGITransport(app=prom.asgi_app())),
+                        scorer=BatchScorer(cfg, device=torch.device("cpu")), worker_id="b0", clock=clock)
+    assert asyncio.run(brain.cycle()) == 1
+    doc = store.get(body["jobId"])
+    assert doc["status"] == "completed_unhealth", doc["reason"]
+    info = json.loads(doc["anomalyInfo"])
+    assert set(info) == set(metrics) and max(info["error5xx"]["values"][1::2]) > 30
+    assert brain.lstm is not None and brain.lstm.trained == 1
