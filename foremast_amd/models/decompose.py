@@ -1,0 +1,69 @@
+"""Classical additive seasonal decomposition (reference for the K4 kernel).
+
+``y = trend + seasonal + resid`` per series, the textbook moving-average
+method (the one ``statsmodels.tsa.seasonal_decompose(model="additive")``
+implements), made NaN-aware for scraped metrics with gaps:
+
+* trend: centred moving average of one season — for an even period m the
+  2 x m MA (weights 1/2m at both ends, 1/m inside), for odd m the plain m MA;
+  over missing points the weighted mean of the valid ones, NaN when fewer
+  than half the window is valid; NaN in the first/last ``m // 2`` samples;
+* seasonal: per-phase mean of ``y - trend`` over the periods where it is
+  defined, centred so the m phase means sum to zero, tiled over time;
+* resid: ``y - trend - seasonal``.
+
+Used for Holt-Winters seasonal initialisation, and exposed for dashboards
+("seasonality decomposition" in BASELINE.json).
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+
+@dataclass
+class Decomposition:
+    trend: torch.Tensor        # [N, T]
+    seasonal: torch.Tensor     # [N, T]
+    resid: torch.Tensor        # [N, T]
+    phase_means: torch.Tensor  # [N, m] (centred)
+
+
+def ma_weights(m: int, dtype=torch.float64) -> torch.Tensor:
+    if m % 2 == 0:
+        w = torch.ones(m + 1, dtype=dtype) / m
+        w[0] = w[-1] = 0.5 / m
+    else:
+        w = torch.ones(m, dtype=dtype) / m
+    return w
+
+
+def seasonal_decompose(y: torch.Tensor, m: int) -> Decomposition:
+    """``y [N, T]`` (NaN = missing), period ``m`` (2 <= m <= T // 2)."""
+    N, T = y.shape
+    yd = y.double()
+    valid = ~torch.isnan(yd)
+    y0 = torch.nan_to_num(yd)
+    w = ma_weights(m).to(y.device)
+    L = w.numel()
+    h = L // 2
+    num = torch.nn.functional.conv1d((y0 * valid).unsqueeze(1), w.view(1, 1, -1)).squeeze(1)  # [N, T-L+1]
+    den = torch.nn.functional.conv1d(valid.double().unsqueeze(1), w.view(1, 1, -1)).squeeze(1)
+    tr = torch.where(den >= 0.5, num / den.clamp(min=1e-300), torch.full_like(num, float("nan")))
+    trend = torch.full((N, T), float("nan"), dtype=torch.float64, device=y.device)
+    trend[:, h:h + tr.shape[1]] = tr
+    det = yd - trend
+    ok = ~torch.isnan(det)
+    P = (T + m - 1) // m
+    pad = P * m - T
+    dpad = torch.nn.functional.pad(torch.nan_to_num(det) * ok, (0, pad)).view(N, P, m)
+    cpad = torch.nn.functional.pad(ok.double(), (0, pad)).view(N, P, m)
+    cnt = cpad.sum(1)
+    pm = torch.where(cnt > 0, dpad.sum(1) / cnt.clamp(min=1), torch.zeros_like(cnt))
+    pm = pm - pm.mean(1, keepdim=True)
+    seasonal = pm.repeat(1, P)[:, :T]
+    resid = yd - trend - seasonal
+    f = y.dtype if y.dtype.is_floating_point and y.dtype != torch.bfloat16 else torch.float32
+    return Decomposition(trend.to(f), seasonal.to(f), resid.to(f), pm.to(f))

@@ -1,0 +1,193 @@
+// K4: classical additive seasonal decomposition (trend / seasonal / resid)
+// of every series of a history ring, one workgroup per series.
+//
+// Semantics: foremast_amd/models/decompose.py (NaN-aware 2 x m centred MA
+// trend, centred per-phase means of the detrended series, residual).
+//
+// Schedule (256 threads, series staged once through LDS):
+//  1. block mean of the valid values (offset that keeps fp32 prefix sums
+//     small — the MA is a difference of two prefix sums);
+//  2. exclusive prefix sums of valid*(y - mean) and of the valid count in
+//     LDS: per-thread contiguous chunks, wave DPP-free shuffles + one LDS
+//     round for the 4 wave totals;
+//  3. per phase p (strided over threads): mean over periods of y - trend,
+//     trend evaluated on the fly from the prefix sums (O(1) per sample);
+//  4. one coalesced output pass: trend, seasonal = phase_mean[t mod m],
+//     resid.  Everything else is in LDS: 2 x (T+1) floats + m floats.
+#include "common.h"
+
+struct DecompArgs {
+  const void* hist;   // [N, ld] ring (bf16 or fp32)
+  long long ld;
+  int ring_len;
+  int head;
+  int T;              // samples (logical order from head)
+  int N;
+  int m;              // period
+  int bf16;
+  float* trend;       // [N, T] or null
+  float* seasonal;    // [N, T] or null
+  float* resid;       // [N, T] or null
+  float* phase_means; // [N, m] or null
+};
+
+extern __shared__ __attribute__((aligned(16))) char fm_dec_smem[];
+
+namespace {
+
+constexpr int BLOCK = 256;
+
+template <typename TIN>
+__device__ __forceinline__ float load_y(const DecompArgs& a, const TIN* row, int i) {
+  int c = a.head + i;
+  if (c >= a.ring_len) c -= a.ring_len;
+  return to_f32<TIN>(row[c]);
+}
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x / FM_WAVE;
+  __syncthreads();
+  if (lane_id() == 0) red[w] = v;
+  __syncthreads();
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < BLOCK / FM_WAVE; ++i) s += red[i];
+  return s;
+}
+
+// exclusive block scan of one value per thread
+__device__ __forceinline__ v2f block_exscan2(v2f v, float* red) {
+  const int lane = lane_id(), w = threadIdx.x / FM_WAVE;
+  v2f inc = v;
+#pragma unroll
+  for (int o = 1; o < FM_WAVE; o <<= 1) {
+    const v2f t = shfl_up2(inc, o);
+    if (lane >= o) inc += t;
+  }
+  __syncthreads();
+  if (lane == FM_WAVE - 1) {
+    red[2 * w] = inc.x;
+    red[2 * w + 1] = inc.y;
+  }
+  __syncthreads();
+  v2f off = {0.f, 0.f};
+  for (int i = 0; i < w; ++i) {
+    off.x += red[2 * i];
+    off.y += red[2 * i + 1];
+  }
+  return off + inc - v;
+}
+
+template <typename TIN>
+__global__ __launch_bounds__(BLOCK) void decompose_kernel(const DecompArgs a) {
+  const int n = blockIdx.x;
+  const TIN* row = (const TIN*)a.hist + (long long)n * a.ld;
+  const int T = a.T, m = a.m, tid = threadIdx.x;
+  float* S = (float*)fm_dec_smem;    // [T+1] prefix of valid*(y - ybar)
+  float* Cn = S + (T + 1);           // [T+1] prefix of valid
+  float* pm = Cn + (T + 1);          // [m]
+  float* red = pm + m;               // [2 * waves]
+
+  // 1. mean of valid values
+  float sv = 0.f, cv = 0.f;
+  for (int i = tid; i < T; i += BLOCK) {
+    const float y = load_y<TIN>(a, row, i);
+    if (y == y) { sv += y; cv += 1.f; }
+  }
+  const float ssum = block_sum(sv, red);
+  const float csum = block_sum(cv, red);
+  const float ybar = csum > 0.f ? ssum / csum : 0.f;
+
+  // 2. prefix sums, contiguous chunk per thread
+  const int chunk = (T + BLOCK - 1) / BLOCK;
+  const int i0 = min(T, tid * chunk), i1 = min(T, i0 + chunk);
+  v2f loc = {0.f, 0.f};
+  for (int i = i0; i < i1; ++i) {
+    const float y = load_y<TIN>(a, row, i);
+    if (y == y) { loc.x += y - ybar; loc.y += 1.f; }
+  }
+  v2f run = block_exscan2(loc, red);
+  for (int i = i0; i < i1; ++i) {
+    S[i] = run.x;
+    Cn[i] = run.y;
+    const float y = load_y<TIN>(a, row, i);
+    if (y == y) { run.x += y - ybar; run.y += 1.f; }
+  }
+  if (tid == BLOCK - 1) { S[T] = run.x; Cn[T] = run.y; }
+  __syncthreads();
+
+  const int h = m / 2;
+  const bool even = (m & 1) == 0;
+  const float inv_m = 1.f / (float)m;
+  // trend at t (NaN at the edges / when < half the window is valid)
+  auto trend_at = [&](int t) -> float {
+    if (t < h || t + h > T - 1) return fm_nan();
+    float num, den;
+    if (even) {
+      num = (S[t + h] - S[t - h + 1]);
+      den = (Cn[t + h] - Cn[t - h + 1]);
+      const float ca = Cn[t - h + 1] - Cn[t - h], cb = Cn[t + h + 1] - Cn[t + h];
+      num += 0.5f * ((S[t - h + 1] - S[t - h]) + (S[t + h + 1] - S[t + h]));
+      den += 0.5f * (ca + cb);
+    } else {
+      num = S[t + h + 1] - S[t - h];
+      den = Cn[t + h + 1] - Cn[t - h];
+    }
+    num *= inv_m;
+    den *= inv_m;
+    return den >= 0.5f ? ybar + num / den : fm_nan();
+  };
+
+  // 3. phase means of the detrended series
+  for (int p = tid; p < m; p += BLOCK) {
+    float s = 0.f, c = 0.f;
+    for (int t = p; t < T; t += m) {
+      const float y = load_y<TIN>(a, row, t);
+      const float tr = trend_at(t);
+      const float d = y - tr;
+      if (d == d) { s += d; c += 1.f; }
+    }
+    pm[p] = c > 0.f ? s / c : 0.f;
+  }
+  __syncthreads();
+  float ps = 0.f;
+  for (int p = tid; p < m; p += BLOCK) ps += pm[p];
+  const float pmean = block_sum(ps, red) / (float)m;
+  for (int p = tid; p < m; p += BLOCK) {
+    pm[p] -= pmean;
+    if (a.phase_means) a.phase_means[(long long)n * m + p] = pm[p];
+  }
+  __syncthreads();
+
+  // 4. outputs
+  const long long base = (long long)n * T;
+  for (int t = tid; t < T; t += BLOCK) {
+    const float tr = trend_at(t);
+    const float se = pm[t % m];
+    if (a.trend) a.trend[base + t] = tr;
+    if (a.seasonal) a.seasonal[base + t] = se;
+    if (a.resid) a.resid[base + t] = load_y<TIN>(a, row, t) - tr - se;
+  }
+}
+
+}  // namespace
+
+extern "C" size_t fm_decompose_lds_bytes(int T, int m) {
+  return (size_t)(2 * (T + 1) + m + 2 * (BLOCK / FM_WAVE)) * sizeof(float);
+}
+
+extern "C" long long fm_decompose_args_size() { return (long long)sizeof(DecompArgs); }
+
+extern "C" int fm_seasonal_decompose(const DecompArgs* a, hipStream_t st) {
+  if (a->N <= 0) return 0;
+  if (a->m < 2 || a->T < 2 * a->m || a->T > a->ring_len || a->head < 0 || a->head >= a->ring_len)
+    return (int)hipErrorInvalidValue;
+  const size_t lds = fm_decompose_lds_bytes(a->T, a->m);
+  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  if (a->bf16)
+    hipLaunchKernelGGL(decompose_kernel<bf16_t>, dim3(a->N), dim3(BLOCK), lds, st, *a);
+  else
+    hipLaunchKernelGGL(decompose_kernel<float>, dim3(a->N), dim3(BLOCK), lds, st, *a);
+  return (int)hipGetLastError();
+}

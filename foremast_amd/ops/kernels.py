@@ -9,6 +9,7 @@ HIP graph.
 
 from __future__ import annotations
 
+import ctypes as C
 import os
 from dataclasses import dataclass
 from typing import Dict, Optional
@@ -19,7 +20,8 @@ from . import _native as nat
 
 MODE_ES, MODE_DES, MODE_HW = 0, 1, 2
 DEFAULT_ES_K = 16  # steps per lane per segment for ES/DES (segment = 1024)
-LDS_LIMIT = 64 * 1024
+LDS_LIMIT = 64 * 1024          # budget of the tiled kernels (keeps >= 2 workgroups per CU)
+LDS_MAX_WG = 160 * 1024        # gfx950: one workgroup may own the whole 160 KiB
 
 
 class KernelShapeError(ValueError):
@@ -423,3 +425,48 @@ def tick_ingest(hist: torch.Tensor, hist_col: int, cur: torch.Tensor, P: int, W:
                                  nat.ptr(base), nat.ptr(newb) if base is not None else 0,
                                  int(hist.dtype == torch.bfloat16), nat.stream_handle(hist.device)),
               "fm_tick_ingest")
+
+
+# ---------------------------------------------------------------------------------
+# K4: seasonal decomposition
+# ---------------------------------------------------------------------------------
+
+class DecompArgs(C.Structure):
+    _fields_ = [("hist", C.c_void_p), ("ld", C.c_longlong), ("ring_len", C.c_int), ("head", C.c_int),
+                ("T", C.c_int), ("N", C.c_int), ("m", C.c_int), ("bf16", C.c_int),
+                ("trend", C.c_void_p), ("seasonal", C.c_void_p), ("resid", C.c_void_p),
+                ("phase_means", C.c_void_p)]
+
+
+nat.register("fm_seasonal_decompose", [C.POINTER(DecompArgs), C.c_void_p])
+nat.register("fm_decompose_lds_bytes", [C.c_int, C.c_int], C.c_size_t)
+nat.register("fm_decompose_args_size", [], C.c_longlong)
+
+
+def seasonal_decompose(hist: torch.Tensor, head: int, length: int, m: int, want=("trend", "seasonal", "resid"),
+                       out: Optional[Dict[str, torch.Tensor]] = None) -> Dict[str, torch.Tensor]:
+    """Classical additive decomposition of the ring's logical window
+    ``[head, head+length)`` (see models/decompose.py); returns float32
+    ``trend/seasonal/resid [N, length]`` (those in ``want``) and
+    ``phase_means [N, m]``."""
+    lib = nat.require()
+    _hist_check(hist, head, length)
+    _need(2 <= m and 2 * m <= length, f"period {m} needs at least two seasons of history")
+    _need(lib.fm_decompose_lds_bytes(length, m) <= LDS_MAX_WG, "window too long for the decomposition kernel")
+    N, dev = hist.shape[0], hist.device
+    out = {} if out is None else out
+    for k in want:
+        if k not in out:
+            out[k] = torch.empty((N, length), dtype=torch.float32, device=dev)
+    if "phase_means" not in out:
+        out["phase_means"] = torch.empty((N, m), dtype=torch.float32, device=dev)
+    a = DecompArgs()
+    a.hist, a.ld, a.ring_len, a.head, a.T, a.N, a.m = nat.ptr(hist), hist.stride(0), hist.shape[1], int(head), \
+        int(length), N, int(m)
+    a.bf16 = int(hist.dtype == torch.bfloat16)
+    a.trend = nat.ptr(out.get("trend"))
+    a.seasonal = nat.ptr(out.get("seasonal"))
+    a.resid = nat.ptr(out.get("resid"))
+    a.phase_means = nat.ptr(out["phase_means"])
+    nat.check(lib.fm_seasonal_decompose(C.byref(a), nat.stream_handle(dev)), "fm_seasonal_decompose")
+    return out

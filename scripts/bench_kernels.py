@@ -74,6 +74,9 @@ def main():
     jobs["rank_tests"] = lambda: rk.update(K.rank_tests(base, cur + 0.1, 1, 0.05, out=rk))
     ws = {}
     jobs["window_stats"] = lambda: ws.update(K.window_stats(hist, 0, R, spec, out=ws))
+    dc = {}
+    if not args.only or "decompose" in args.only:
+        jobs["seasonal_decompose"] = lambda: dc.update(K.seasonal_decompose(hist, 0, R, m, out=dc))
     for name, fn in jobs.items():  # warm-up / compile
         fn()
     torch.cuda.synchronize()

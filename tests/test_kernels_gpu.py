@@ -183,3 +183,28 @@ def test_ring_append(K):
         torch.cuda.synchronize()
         cols = [14, 15, 0, 1, 2]
         assert torch.equal(dst[:, cols].float(), src)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,m,T", [(torch.float32, 24, 24 * 9 + 5), (torch.bfloat16, 1440, 10080)])
+def test_seasonal_decompose_kernel_matches_reference(K, dtype, m, T):
+    from foremast_amd.models.decompose import seasonal_decompose as ref
+    from foremast_amd.brain.engine import synthetic_history
+    dev = torch.device("cuda:0")
+    N, R = 64, T + 37
+    y = synthetic_history(N, T, m, dev, seed=5)
+    y[3, 100:140] = float("nan")
+    ring = torch.full((N, R), float("nan"), device=dev, dtype=dtype)
+    head = 29
+    cols = (head + torch.arange(T, device=dev)) % R
+    ring[:, cols] = y.to(dtype)
+    out = K.seasonal_decompose(ring, head, T, m)
+    torch.cuda.synchronize()
+    d = ref(ring[:, cols].float().cpu(), m)
+    scale = float(torch.nan_to_num(y.float()).abs().max())
+    for k, r in (("trend", d.trend), ("seasonal", d.seasonal), ("resid", d.resid)):
+        got = out[k].cpu()
+        assert torch.equal(torch.isnan(got), torch.isnan(r)), k
+        ok = ~torch.isnan(r)
+        assert float((got[ok] - r[ok]).abs().max()) < 2e-4 * scale, k
+    assert torch.allclose(out["phase_means"].cpu(), d.phase_means, atol=2e-4 * scale)

@@ -182,3 +182,27 @@ def test_prophet_lite_recovers_trend_and_seasonality():
     assert float((f - truth(cts)).abs().max()) < 0.15
     one = P.fit_prophet(y[1:2].float(), end[1:2], torch.full((1,), step))
     assert torch.allclose(P.forecast(one, cts[1:2]), f[1:2], atol=1e-4)
+
+
+def test_seasonal_decompose_reference():
+    import math
+    from foremast_amd.models.decompose import seasonal_decompose
+    torch.manual_seed(1)
+    N, m, P = 3, 24, 8
+    T = m * P
+    t = torch.arange(T, dtype=torch.float64)
+    season = torch.sin(2 * math.pi * t / m)
+    y = 5 + 0.01 * t + 2 * season + 0.01 * torch.randn(N, T, dtype=torch.float64)
+    d = seasonal_decompose(y, m)
+    h = m // 2
+    assert torch.isnan(d.trend[:, :h]).all() and torch.isnan(d.trend[:, T - h:]).all()
+    mid = slice(h, T - h)
+    assert torch.allclose(d.trend[:, mid], (5 + 0.01 * t[mid]).expand(N, -1), atol=0.02)
+    assert torch.allclose(d.seasonal, 2 * season.expand(N, -1), atol=0.03)
+    assert abs(float(d.phase_means.sum(1).abs().max())) < 1e-9
+    assert float(d.resid[:, mid].abs().max()) < 0.06
+    # gaps: still defined where at least half of the window is valid
+    y2 = y.clone()
+    y2[:, 50:55] = float("nan")
+    d2 = seasonal_decompose(y2, m)
+    assert torch.isfinite(d2.trend[:, 52]).all() and torch.allclose(d2.seasonal, d.seasonal, atol=0.05)

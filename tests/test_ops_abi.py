@@ -37,3 +37,13 @@ def test_struct_sizes(lib, name):
 def test_struct_offsets(lib, name, field):
     cls = getattr(nat, name)
     assert lib.fm_abi_offsetof(name.encode(), field.encode()) == getattr(cls, field).offset
+
+
+def test_module_local_struct_sizes(lib):
+    """Structs declared next to their kernels (lstm / lstm_train / decompose)."""
+    from foremast_amd.ops import kernels, lstm, lstm_train
+    for sym, cls in (("fm_lstm_args_size", lstm.LstmArgs), ("fm_lstm_train_args_size", lstm_train.LstmTrainArgs),
+                     ("fm_decompose_args_size", kernels.DecompArgs)):
+        f = getattr(lib, sym)
+        f.restype = C.c_longlong
+        assert f() == C.sizeof(cls), sym
