@@ -20,6 +20,7 @@ the GPU ranks, when a brain publishes one into the service).
 
 from __future__ import annotations
 
+import html
 import json
 import logging
 import os
@@ -27,7 +28,7 @@ from typing import Any, Callable, Dict, Optional
 
 import httpx
 from fastapi import FastAPI, Request
-from fastapi.responses import JSONResponse, PlainTextResponse
+from fastapi.responses import HTMLResponse, JSONResponse, PlainTextResponse
 
 from ..api import rest as r
 from ..api import status as st
@@ -147,6 +148,18 @@ def create_app(store: Optional[JobStore] = None, query_endpoint: Optional[str] =
     @app.get("/healthz")
     async def healthz():
         return PlainTextResponse("ok")
+
+    @app.get("/ui/{namespace}/{app_name}")
+    async def dashboard(namespace: str, app_name: str):
+        from . import ui
+        return HTMLResponse(ui.page(namespace, app_name))
+
+    @app.get("/ui")
+    async def dashboard_index():
+        apps = sorted({d.get("appName", "") for d in store.all() if d.get("appName")})
+        items = "".join(f"<li>{html.escape(a)}</li>" for a in apps)
+        return HTMLResponse("<!doctype html><title>Foremast</title><h1>Foremast jobs</h1>"
+                            "<p>open <code>/ui/&lt;namespace&gt;/&lt;app&gt;</code></p><ul>" + items + "</ul>")
 
     @app.get("/api/v1/{queryproxy}")
     async def query_proxy(queryproxy: str, request: Request):

@@ -249,3 +249,22 @@ def test_es_store_conflicts_and_faults():
         s1.get(jid)
     s1.wait_ready(deadline_s=1.0)
     assert isinstance(open_store("http://es:9200"), ElasticJobStore)
+
+
+def test_dashboard_page():
+    from fastapi.testclient import TestClient
+    from foremast_amd.service import ui
+    store = MemoryJobStore()
+    svc.register(store, _req())
+    client = TestClient(svc.create_app(store, query_endpoint="http://prom:9090/"))
+    r = client.get("/ui/foremast-examples/demo")
+    assert r.status_code == 200 and r.headers["content-type"].startswith("text/html")
+    body = r.text
+    q = ui.queries("foremast-examples", "demo")
+    upper = q["http_server_requests_error_5xx"]["upper"]
+    assert "foremastbrain:namespace_app_per_pod:http_server_requests_error_5xx_upper" in upper
+    assert "exported_namespace" in body and "/api/v1/query_range?query=" in body and "<script>" in body
+    idx = client.get("/ui")
+    assert "demo" in idx.text
+    xss = client.get("/ui/%3Cscript%3E/x")
+    assert "<script>alert" not in xss.text and "&lt;script&gt;" in xss.text
