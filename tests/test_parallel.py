@@ -6,6 +6,7 @@ import os
 import socket
 import subprocess
 import sys
+import time
 
 import numpy as np
 import pytest
@@ -156,3 +157,52 @@ def test_dp_single_process_matches_plain_adam():
         opt.step()
     for pa, pb in zip(a.parameters(), b.parameters()):
         assert torch.allclose(pa, pb, atol=1e-6)
+
+
+def _elastic_worker(mid, members, port, q, die_after):
+    import datetime as _dt
+    from torch.distributed import TCPStore
+    from foremast_amd.parallel.elastic import ElasticWorld
+    store = TCPStore("127.0.0.1", port, is_master=False, timeout=_dt.timedelta(seconds=60))
+    ew = ElasticWorld(store, mid, members, backend="gloo", heartbeat_timeout_s=1.0, collective_timeout_s=5)
+    ew.start_heartbeat(0.2)
+    ew.form()
+    n_total = 1000
+    log = []
+    for tick in range(6):
+        if die_after is not None and tick == die_after:
+            os._exit(0)  # simulated crash: no cleanup, heartbeats stop
+
+        def work():
+            s, e, _ = shard_range(n_total, ew.world, ew.rank, align=5)
+            t = torch.tensor([e - s], dtype=torch.int64)
+            dist.all_reduce(t)
+            return int(t.item())
+        total = ew.run_tick(work)
+        log.append((tick, ew.world, total))
+        time.sleep(0.3)
+    ew.stop_heartbeat()
+    q.put((mid, log, ew.reforms))
+    dist.destroy_process_group()
+
+
+def test_elastic_recovery_reshards_after_rank_death():
+    import datetime as _dt
+    from torch.distributed import TCPStore
+    port = _free_port()
+    store = TCPStore("127.0.0.1", port, is_master=True, wait_for_workers=False, timeout=_dt.timedelta(seconds=60))
+    members = ["m0", "m1", "m2"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_elastic_worker, args=(m, members, port, q, 2 if m == "m2" else None))
+             for m in members]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    del store
+    for mid, log, reforms in res:
+        assert [t for t, _, _ in log] == list(range(6))
+        assert all(total == 1000 for _, _, total in log), log   # every series scored every tick
+        assert log[0][1] == 3 and log[-1][1] == 2 and reforms == 1, log
