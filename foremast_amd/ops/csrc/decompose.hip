@@ -4,16 +4,18 @@
 // Semantics: foremast_amd/models/decompose.py (NaN-aware 2 x m centred MA
 // trend, centred per-phase means of the detrended series, residual).
 //
-// Schedule (256 threads, series staged once through LDS):
-//  1. block mean of the valid values (offset that keeps fp32 prefix sums
-//     small — the MA is a difference of two prefix sums);
-//  2. exclusive prefix sums of valid*(y - mean) and of the valid count in
-//     LDS: per-thread contiguous chunks, wave DPP-free shuffles + one LDS
-//     round for the 4 wave totals;
-//  3. per phase p (strided over threads): mean over periods of y - trend,
-//     trend evaluated on the fly from the prefix sums (O(1) per sample);
+// Schedule (512 threads, the series read from HBM exactly once):
+//  0. coalesced staging of the ring window into LDS as fp32 (+ block mean of
+//     the valid values: the offset that keeps the fp32 prefix sums small —
+//     the MA is a difference of two prefix sums);
+//  1. exclusive prefix sums of valid*(y - mean) and of the valid count, in
+//     LDS: per-thread contiguous chunks + one shuffle scan + one LDS round;
+//  2. trend per sample from the prefix sums (O(1) each), kept in registers;
+//     the detrended series overwrites the prefix array;
+//  3. per phase p (strided over threads): mean over periods of y - trend;
 //  4. one coalesced output pass: trend, seasonal = phase_mean[t mod m],
-//     resid.  Everything else is in LDS: 2 x (T+1) floats + m floats.
+//     resid.  LDS: 3 x (T+1) + m floats (127 KiB at T = 10080, m = 1440 —
+//     gfx950 lets one workgroup own up to 160 KiB).
 #include "common.h"
 
 struct DecompArgs {
@@ -35,7 +37,8 @@ extern __shared__ __attribute__((aligned(16))) char fm_dec_smem[];
 
 namespace {
 
-constexpr int BLOCK = 256;
+constexpr int BLOCK = 512;
+constexpr int MAX_ITEMS = 32;  // samples per thread held in registers: T <= 16384
 
 template <typename TIN>
 __device__ __forceinline__ float load_y(const DecompArgs& a, const TIN* row, int i) {
@@ -84,37 +87,39 @@ __global__ __launch_bounds__(BLOCK) void decompose_kernel(const DecompArgs a) {
   const int n = blockIdx.x;
   const TIN* row = (const TIN*)a.hist + (long long)n * a.ld;
   const int T = a.T, m = a.m, tid = threadIdx.x;
-  float* S = (float*)fm_dec_smem;    // [T+1] prefix of valid*(y - ybar)
+  float* Y = (float*)fm_dec_smem;    // [T+1] staged series (NaN = missing)
+  float* S = Y + (T + 1);            // [T+1] prefix of valid*(y - ybar)
   float* Cn = S + (T + 1);           // [T+1] prefix of valid
   float* pm = Cn + (T + 1);          // [m]
   float* red = pm + m;               // [2 * waves]
 
-  // 1. mean of valid values
+  // 0. stage (coalesced) + mean of valid values
   float sv = 0.f, cv = 0.f;
   for (int i = tid; i < T; i += BLOCK) {
     const float y = load_y<TIN>(a, row, i);
+    Y[i] = y;
     if (y == y) { sv += y; cv += 1.f; }
   }
   const float ssum = block_sum(sv, red);
   const float csum = block_sum(cv, red);
   const float ybar = csum > 0.f ? ssum / csum : 0.f;
 
-  // 2. prefix sums, contiguous chunk per thread
+  // 1. prefix sums, contiguous chunk per thread (reads the staged copy)
   const int chunk = (T + BLOCK - 1) / BLOCK;
   const int i0 = min(T, tid * chunk), i1 = min(T, i0 + chunk);
   v2f loc = {0.f, 0.f};
   for (int i = i0; i < i1; ++i) {
-    const float y = load_y<TIN>(a, row, i);
+    const float y = Y[i];
     if (y == y) { loc.x += y - ybar; loc.y += 1.f; }
   }
   v2f run = block_exscan2(loc, red);
   for (int i = i0; i < i1; ++i) {
     S[i] = run.x;
     Cn[i] = run.y;
-    const float y = load_y<TIN>(a, row, i);
+    const float y = Y[i];
     if (y == y) { run.x += y - ybar; run.y += 1.f; }
   }
-  if (tid == BLOCK - 1) { S[T] = run.x; Cn[T] = run.y; }
+  if (i1 == T && i0 < i1) { S[T] = run.x; Cn[T] = run.y; }
   __syncthreads();
 
   const int h = m / 2;
@@ -139,13 +144,28 @@ __global__ __launch_bounds__(BLOCK) void decompose_kernel(const DecompArgs a) {
     return den >= 0.5f ? ybar + num / den : fm_nan();
   };
 
+  // 2. trend once per sample into registers (t = tid + k*BLOCK); after a
+  //    barrier S is free and becomes the detrended series D
+  float tr_r[MAX_ITEMS];
+#pragma unroll
+  for (int k = 0; k < MAX_ITEMS; ++k) {
+    const int t = tid + k * BLOCK;
+    tr_r[k] = t < T ? trend_at(t) : 0.f;
+  }
+  __syncthreads();
+  float* D = S;
+#pragma unroll
+  for (int k = 0; k < MAX_ITEMS; ++k) {
+    const int t = tid + k * BLOCK;
+    if (t < T) D[t] = Y[t] - tr_r[k];
+  }
+  __syncthreads();
+
   // 3. phase means of the detrended series
   for (int p = tid; p < m; p += BLOCK) {
     float s = 0.f, c = 0.f;
     for (int t = p; t < T; t += m) {
-      const float y = load_y<TIN>(a, row, t);
-      const float tr = trend_at(t);
-      const float d = y - tr;
+      const float d = D[t];
       if (d == d) { s += d; c += 1.f; }
     }
     pm[p] = c > 0.f ? s / c : 0.f;
@@ -160,28 +180,32 @@ __global__ __launch_bounds__(BLOCK) void decompose_kernel(const DecompArgs a) {
   }
   __syncthreads();
 
-  // 4. outputs
+  // 4. outputs (coalesced)
   const long long base = (long long)n * T;
-  for (int t = tid; t < T; t += BLOCK) {
-    const float tr = trend_at(t);
-    const float se = pm[t % m];
-    if (a.trend) a.trend[base + t] = tr;
-    if (a.seasonal) a.seasonal[base + t] = se;
-    if (a.resid) a.resid[base + t] = load_y<TIN>(a, row, t) - tr - se;
+#pragma unroll
+  for (int k = 0; k < MAX_ITEMS; ++k) {
+    const int t = tid + k * BLOCK;
+    if (t < T) {
+      const float se = pm[t % m];
+      if (a.trend) a.trend[base + t] = tr_r[k];
+      if (a.seasonal) a.seasonal[base + t] = se;
+      if (a.resid) a.resid[base + t] = D[t] - se;
+    }
   }
 }
 
 }  // namespace
 
 extern "C" size_t fm_decompose_lds_bytes(int T, int m) {
-  return (size_t)(2 * (T + 1) + m + 2 * (BLOCK / FM_WAVE)) * sizeof(float);
+  return (size_t)(3 * (T + 1) + m + 2 * (BLOCK / FM_WAVE)) * sizeof(float);
 }
 
 extern "C" long long fm_decompose_args_size() { return (long long)sizeof(DecompArgs); }
 
 extern "C" int fm_seasonal_decompose(const DecompArgs* a, hipStream_t st) {
   if (a->N <= 0) return 0;
-  if (a->m < 2 || a->T < 2 * a->m || a->T > a->ring_len || a->head < 0 || a->head >= a->ring_len)
+  if (a->m < 2 || a->T < 2 * a->m || a->T > a->ring_len || a->head < 0 || a->head >= a->ring_len ||
+      a->T > BLOCK * MAX_ITEMS)
     return (int)hipErrorInvalidValue;
   const size_t lds = fm_decompose_lds_bytes(a->T, a->m);
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
