@@ -95,22 +95,24 @@ def init_dist(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_gpu = torch.cuda.is_available() and not args.cpu
     if use_gpu:
+        local = local % max(1, torch.cuda.device_count())  # >1 rank per GPU only in gloo tests
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
     else:
         dev = torch.device("cpu")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if use_gpu:
-            dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("FOREMAST_DIST_BACKEND", "nccl" if use_gpu else "gloo")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group(backend)  # gloo: CPU runs, or several ranks sharing one GPU in tests
     return world, rank, dev
 
 
 def barrier(dev):
     if dist.is_initialized():
-        if dev.type == "cuda":
+        if dev.type == "cuda" and dist.get_backend() == "nccl":
             dist.barrier(device_ids=[dev.index])
         else:
             dist.barrier()
