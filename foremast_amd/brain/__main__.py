@@ -29,6 +29,9 @@ def parse(argv=None):
     p.add_argument("--metrics-port", type=int, default=int(os.environ.get("FOREMAST_METRICS_PORT", "8000")))
     p.add_argument("--worker-id", default=None)
     p.add_argument("--run-seconds", type=float, default=None)
+    p.add_argument("--streaming", action="store_true",
+                   default=os.environ.get("FOREMAST_STREAMING", "0") not in ("0", "", "false"),
+                   help="serve continuous jobs from the resident streaming engine")
     p.add_argument("--model-cache", default=os.environ.get("FOREMAST_MODEL_CACHE"),
                    help="safetensors checkpoint of the LSTM model cache (loaded at start, saved at exit)")
     return p.parse_args(argv)
@@ -55,7 +58,8 @@ async def run(args) -> BrainWorker:
     if args.metrics_port:
         from prometheus_client import start_http_server
         start_http_server(args.metrics_port + local, registry=metrics.registry)
-    worker = BrainWorker(store, cfg, worker_id=args.worker_id, metrics=metrics)
+    worker = BrainWorker(store, cfg, worker_id=args.worker_id, metrics=metrics,
+                         exclude_strategies=("continuous",) if args.streaming else ())
     cache_path = None
     if args.model_cache:
         from .multivariate import LstmJobScorer, ModelCache
@@ -72,7 +76,13 @@ async def run(args) -> BrainWorker:
             pass
     if args.run_seconds is not None:
         loop.call_later(args.run_seconds, stop.set)
-    await worker.run_forever(stop)
+    tasks = [worker.run_forever(stop)]
+    if args.streaming:
+        from .streaming import StreamingMonitor
+        mon = StreamingMonitor(store, cfg, device=worker.scorer.device, metrics=metrics,
+                               worker_id=f"{worker.worker_id}-stream")
+        tasks.append(mon.run_forever(stop))
+    await asyncio.gather(*tasks)
     if cache_path and worker.lstm is not None:
         worker.lstm.cache.save(cache_path)
     store.close()

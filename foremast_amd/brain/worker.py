@@ -73,7 +73,8 @@ def _grid(url: str) -> Tuple[float, float, float]:
 class BrainWorker:
     def __init__(self, store: JobStore, cfg: Optional[BrainConfig] = None, prom: Optional[PromClient] = None,
                  scorer: Optional[BatchScorer] = None, worker_id: Optional[str] = None,
-                 clock=time.time, metrics: Optional[BrainMetrics] = None, batch_limit: int = 256) -> None:
+                 clock=time.time, metrics: Optional[BrainMetrics] = None, batch_limit: int = 256,
+                 exclude_strategies: Tuple[str, ...] = ()) -> None:
         self.store = store
         self.cfg = cfg or BrainConfig.from_env()
         self.prom = prom or PromClient()
@@ -82,6 +83,8 @@ class BrainWorker:
         self.clock = clock
         self.metrics = metrics or BrainMetrics()
         self.batch_limit = batch_limit
+        # strategies another component owns (the streaming monitor takes "continuous")
+        self.exclude = {x.lower() for x in exclude_strategies}
         self.lstm = None  # LstmJobScorer, created on first multivariate LSTM job
 
     # ------------------------------------------------------------------ planning
@@ -109,8 +112,9 @@ class BrainWorker:
     async def cycle(self) -> int:
         t0 = time.perf_counter()
         now = self.clock()
+        only = (lambda d: (d.get("strategy") or "").lower() not in self.exclude) if self.exclude else None
         docs = self.store.claim(self.worker_id, now=now, max_stuck_s=self.cfg.max_stuck_seconds,
-                                limit=self.batch_limit)
+                                limit=self.batch_limit, only=only)
         if not docs:
             return 0
         plans = [self.plan(d) for d in docs]

@@ -118,13 +118,13 @@ class ElasticJobStore(JobStore):
         hits = resp.json().get("hits", {}).get("hits", [])
         return [(h["_source"], int(h.get("_version", 1))) for h in hits]
 
-    def claim(self, worker, now=None, max_stuck_s=90.0, limit=64):
+    def claim(self, worker, now=None, max_stuck_s=90.0, limit=64, only=None):
         now = time.time() if now is None else now
         out = []
         for d, ver in self._search(r.OPEN_STATUSES + r.INPROGRESS_STATUSES):
             if len(out) >= limit:
                 break
-            if not is_claimable(d, now, max_stuck_s):
+            if not is_claimable(d, now, max_stuck_s) or (only is not None and not only(d)):
                 continue
             d.update(status=r.ST_PREPROCESS_INPROGRESS, claimed_by=worker, claimed_at=now,
                      modified_ts=now, modified_at=format_rfc3339_nano(now))

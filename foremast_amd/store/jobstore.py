@@ -104,7 +104,9 @@ class JobStore(abc.ABC):
 
     @abc.abstractmethod
     def claim(self, worker: str, now: Optional[float] = None, max_stuck_s: float = 90.0,
-              limit: int = 64) -> List[Dict[str, Any]]: ...
+              limit: int = 64, only=None) -> List[Dict[str, Any]]:
+        """Lease up to ``limit`` claimable documents (``only(doc)`` filters,
+        e.g. by strategy: the streaming monitor takes continuous jobs)."""
 
     @abc.abstractmethod
     def all(self) -> List[Dict[str, Any]]: ...
@@ -153,14 +155,14 @@ class MemoryJobStore(JobStore):
             d["modified_at"] = format_rfc3339_nano(d["modified_ts"])
             return True
 
-    def claim(self, worker, now=None, max_stuck_s=90.0, limit=64):
+    def claim(self, worker, now=None, max_stuck_s=90.0, limit=64, only=None):
         now = time.time() if now is None else now
         out = []
         with self._lock:
             for d in sorted(self._docs.values(), key=lambda x: x.get("modified_ts", 0.0)):
                 if len(out) >= limit:
                     break
-                if is_claimable(d, now, max_stuck_s):
+                if is_claimable(d, now, max_stuck_s) and (only is None or only(d)):
                     d["status"] = r.ST_PREPROCESS_INPROGRESS
                     d["claimed_by"] = worker
                     d["claimed_at"] = now
@@ -228,7 +230,7 @@ class SqliteJobStore(JobStore):
             c.execute("ROLLBACK")
             raise
 
-    def claim(self, worker, now=None, max_stuck_s=90.0, limit=64):
+    def claim(self, worker, now=None, max_stuck_s=90.0, limit=64, only=None):
         now = time.time() if now is None else now
         c = self._conn()
         c.execute("BEGIN IMMEDIATE")
@@ -241,7 +243,7 @@ class SqliteJobStore(JobStore):
                 if len(out) >= limit:
                     break
                 d = json.loads(raw)
-                if not is_claimable(d, now, max_stuck_s):
+                if not is_claimable(d, now, max_stuck_s) or (only is not None and not only(d)):
                     continue
                 d.update(status=r.ST_PREPROCESS_INPROGRESS, claimed_by=worker, claimed_at=now,
                          modified_ts=now, modified_at=format_rfc3339_nano(now))
