@@ -79,9 +79,11 @@ def build_world(algorithm="moving_average_all", strategy_canary=False):
 
 
 def register_pod_series(kube, prom, old_rs_hash, spike_at, spread=0.2):
-    for p in kube.list_sync("pods", NS):
+    pods = sorted(kube.list_sync("pods", NS), key=lambda p: (p["metadata"]["labels"]["pod-template-hash"] != old_rs_hash,
+                                                               p["metadata"]["name"]))
+    for i, p in enumerate(pods):  # seeds by position: pod names carry random suffixes
         h = p["metadata"]["labels"]["pod-template-hash"]
-        gen = synth.error_rate(base=0.3, spread=spread, seed=sum(map(ord, p["metadata"]["name"])))
+        gen = synth.error_rate(base=0.3, spread=spread, seed=101 + i)
         if h != old_rs_hash:
             gen = synth.step_change(gen, at=spike_at, factor=0.0, add=40.0)  # v2: 5xx storm
         prom.add("namespace_pod:" + METRIC, {"namespace": NS, "pod": p["metadata"]["name"]}, gen)
