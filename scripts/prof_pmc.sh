@@ -1,14 +1,28 @@
 #!/bin/bash
-# PMC counter profile of the HW kernel (kernel-trace + counters only; no sys/runtime trace).
+# PMC counter profiles (kernel-trace + counters only; never combined with
+# sys/runtime traces).  TARGET selects the workload:
+#   hw    — Holt-Winters scan kernel (default variant) on 20k x 10080
+#   lstm  — LSTM training (per phase) + scoring kernels
+#   dec   — seasonal decomposition
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out/pmc
+TARGET=${TARGET:-hw}
+OUT="$PWD/gpurun_out/pmc_$TARGET"
+mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -k 10 120 rocprofv3 -L > gpurun_out/pmc/avail.txt 2>&1 || true
-for C in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" "SQ_INST_CYCLES_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY"; do
+case $TARGET in
+  hw)   CMD=("$PWD/scripts/bench_kernels.py" --series 20000 --rounds 1 --only hw --variants=3) ;;
+  dec)  CMD=("$PWD/scripts/bench_kernels.py" --series 20000 --rounds 1 --only decompose --variants=3) ;;
+  lstm) CMD=("$PWD/scripts/bench_lstm_kernels.py") ;;
+esac
+SETS=("SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS"
+      "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU"
+      "SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"
+      "FETCH_SIZE WRITE_SIZE")
+for C in "${SETS[@]}"; do
   tag=$(echo $C | tr ' ' '_' | cut -c1-40)
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $C --output-format csv -d "$PWD/gpurun_out/pmc/$tag" -o run -- python3 "$PWD/scripts/bench_kernels.py" --series 20000 --rounds 1 --only hw --variants 2 > "gpurun_out/pmc/$tag.log" 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $C --output-format csv -d "$OUT/$tag" -o run -- python3 "${CMD[@]}" > "$OUT/$tag.log" 2>&1
   rc=$?; echo "$tag rc=$rc"
-  if [ $rc -ne 0 ]; then tail -5 "gpurun_out/pmc/$tag.log"; fi
-  if [ $rc -gt 1 ] && [ $rc -ne 2 ]; then exit $rc; fi
+  if [ $rc -ne 0 ]; then tail -5 "$OUT/$tag.log"; fi
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 done
