@@ -54,6 +54,7 @@ struct LstmTrainArgs {
   float* dy;             // [F][T*B]    dL/dy
   float* err;            // [B]         per-window reconstruction MSE
   float loss_scale;      // 2 / (B*T*F)
+  int variant;           // 0: one wave per 32 windows; 1: two waves (hidden units split, LDS exchange)
 };
 
 extern __shared__ __attribute__((aligned(16))) char fm_lstm_train_smem[];
@@ -310,9 +311,283 @@ __global__ __launch_bounds__(64, 1) void lstm_ae_train_kernel(const LstmTrainArg
   if (ph & 8) bwd_phase<true>(a, wlds, wout, scr_enc, zero, b, hh, KB, dh, dc);
 }
 
+
+// ================================================================ variant 1
+// Two waves per 32 windows: wave w owns gate tiles 4w..4w+3, i.e. hidden units
+// 32w..32w+31 (both lane halves).  Per time step each wave issues half the
+// MFMAs and half the cell math; the halves meet once per step through a
+// double-buffered LDS exchange:
+//  * forward: each wave publishes its two h B-fragments (k-steps 2w, 2w+1) and
+//    its partial read-out; after one barrier the other wave's fragments
+//    complete the next step's B operand;
+//  * backward: each wave forms dh partials for BOTH M-tiles from its own
+//    dgates k-steps, keeps its own M-tile and hands the other one over.
+// Twice the waves in flight and half the dependency chain per wave per step.
+constexpr int SV4H = 20;  // per wave per step: 16 units x (i,f,g,o) + 16 c
+
+struct Xch {
+  uint4* hb;    // [2 buf][2 wave][2 frag][64]
+  float* y;     // [2 buf][2 wave][8][64]
+  float* dh;    // [2 buf][2 wave][16][64]
+};
+
+template <bool ENC>
+__device__ __forceinline__ void fwd_phase2(const LstmTrainArgs& a, const uint4* wlds, const float* wout, float4* scr,
+                                           long long b, int hh, int w, long long KB, float (&hreg)[16],
+                                           float (&creg)[16], float& errsum, const Xch& x) {
+  const int lane = lane_id();
+  const int TB = 4 * w;
+  const float* xrow = a.x + b * (long long)a.T * a.F;
+  bf16_t* hbuf = ENC ? a.h_enc : a.h_dec;
+  const long long ldh = ENC ? KB : KB + a.B;
+  // prologue: publish the initial h (zeros for the encoder, the encoder's final h for the decoder)
+  uint4 hb[4];
+  auto publish_h = [&](int buf) {
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = hreg[(2 * sl + (j >> 2)) * 4 + (j & 3)];
+      const uint4 f = pack8(v);
+      hb[2 * w + sl] = f;
+      x.hb[((buf * 2 + w) * 2 + sl) * 64 + lane] = f;
+    }
+  };
+  auto collect_h = [&](int buf) {
+    const int o = 1 - w;
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) hb[2 * o + sl] = x.hb[((buf * 2 + o) * 2 + sl) * 64 + lane];
+  };
+  publish_h(1);
+  __syncthreads();
+  collect_h(1);
+  for (int t = 0; t < a.T; ++t) {
+    const int buf = t & 1;
+    const long long row = (long long)t * a.B + b;
+    if (ENC || t == 0) {
+#pragma unroll
+      for (int tl = 0; tl < 4; ++tl)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          hbuf[(long long)unit_of(TB + tl, hh, q) * ldh + row] = f32_to_bf16(hreg[4 * tl + q]);
+    }
+    uint4 xb;
+    {
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (hh == 0) {
+        if (ENC) {
+#pragma unroll
+          for (int f = 0; f < 7; ++f)
+            if (f < a.F) {
+              v[f] = xrow[t * a.F + f];
+              if (w == 0) a.h_enc[(long long)(64 + f) * KB + row] = f32_to_bf16(v[f]);
+            }
+        }
+        v[7] = 1.f;
+      }
+      xb = pack8(v);
+    }
+    int lo = lane;
+    asm volatile("" : "+v"(lo));
+    float4* srow = scr + (long long)t * SV4H * 64 + lane;
+#pragma unroll
+    for (int tp = 0; tp < 4; tp += 2) {
+      f32x16 acc0 = (f32x16){}, acc1 = (f32x16){};
+#pragma unroll
+      for (int s = 0; s < KSTEPS; ++s) {
+        const uint4 bfr = (s < 4) ? hb[s] : xb;
+        acc0 = mfma_bf16(wlds[((TB + tp) * KSTEPS + s) * 64 + lo], bfr, acc0);
+        acc1 = mfma_bf16(wlds[((TB + tp + 1) * KSTEPS + s) * 64 + lo], bfr, acc1);
+      }
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const f32x16& acc = e ? acc1 : acc0;
+        float4 cv;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float gi = sigm(acc[q]), gf = sigm(acc[4 + q]);
+          const float gg = tanh_f(acc[8 + q]), go = sigm(acc[12 + q]);
+          const int u = (tp + e) * 4 + q;
+          const float c = gf * creg[u] + gi * gg;
+          creg[u] = c;
+          hreg[u] = go * tanh_f(c);
+          srow[u * 64] = make_float4(gi, gf, gg, go);
+          (&cv.x)[q] = c;
+        }
+        srow[(16 + tp + e) * 64] = cv;
+      }
+    }
+    float py[7];
+    if (!ENC) {
+      const long long row1 = (long long)(t + 1) * a.B + b;
+#pragma unroll
+      for (int tl = 0; tl < 4; ++tl)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          a.h_dec[(long long)unit_of(TB + tl, hh, q) * ldh + row1] = f32_to_bf16(hreg[4 * tl + q]);
+#pragma unroll
+      for (int f = 0; f < 7; ++f) {
+        py[f] = 0.f;
+        if (f >= a.F) continue;
+        float p = 0.f;
+#pragma unroll
+        for (int tl = 0; tl < 4; ++tl)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) p += hreg[tl * 4 + q] * wout[f * H + unit_of(TB + tl, hh, q)];
+        p += __shfl_xor(p, 32, FM_WAVE);
+        py[f] = p;
+        x.y[((buf * 2 + w) * 8 + f) * 64 + lane] = p;
+      }
+    }
+    publish_h(buf);
+    __syncthreads();
+    collect_h(buf);
+    if (!ENC) {
+#pragma unroll
+      for (int f = 0; f < 7; ++f) {
+        if (f >= a.F) break;
+        const float y = py[f] + x.y[((buf * 2 + (1 - w)) * 8 + f) * 64 + lane] + a.b_out[f];
+        const float d = y - xrow[t * a.F + f];
+        if (w == 0 && hh == 0) {
+          errsum += d * d;
+          a.dy[(long long)f * KB + row] = d * a.loss_scale;
+        }
+      }
+    }
+  }
+}
+
+template <bool ENC>
+__device__ __forceinline__ void bwd_phase2(const LstmTrainArgs& a, const uint4* wt, const float* wout,
+                                           const float4* scr, const float (&c0)[16], long long b, int hh, int w,
+                                           long long KB, float (&dh)[16], float (&dc)[16], const Xch& x) {
+  const int lane = lane_id();
+  const int TB = 4 * w;
+  bf16_t* gbuf = ENC ? a.g_enc : a.g_dec;
+  for (int t = a.T - 1; t >= 0; --t) {
+    const int buf = t & 1;
+    const long long row = (long long)t * a.B + b;
+    if (!ENC) {  // dy was written by wave 0 during the forward; phase barriers made it visible
+#pragma unroll
+      for (int f = 0; f < 7; ++f) {
+        if (f >= a.F) break;
+        const float dyf = a.dy[(long long)f * KB + row];
+#pragma unroll
+        for (int tl = 0; tl < 4; ++tl)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) dh[4 * tl + q] += dyf * wout[f * H + unit_of(TB + tl, hh, q)];
+      }
+    }
+    const float4* srow = scr + (long long)t * SV4H * 64 + lane;
+    const float4* sprev = scr + (long long)(t - 1) * SV4H * 64 + lane;
+    int lo = lane;
+    asm volatile("" : "+v"(lo));
+    f32x16 acc0 = (f32x16){}, acc1 = (f32x16){};
+#pragma unroll
+    for (int tl = 0; tl < 4; ++tl) {
+      const int tt = TB + tl;
+      float dg[16];
+      const float4 cv = srow[(16 + tl) * 64];
+      float4 cpv;
+      if (t > 0) cpv = sprev[(16 + tl) * 64];
+      else cpv = make_float4(c0[4 * tl], c0[4 * tl + 1], c0[4 * tl + 2], c0[4 * tl + 3]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int u = 4 * tl + q;
+        const float4 gv = srow[u * 64];
+        const float gi = gv.x, gf = gv.y, gg = gv.z, go = gv.w;
+        const float c = (&cv.x)[q], cp = (&cpv.x)[q];
+        const float tc = tanh_f(c);
+        const float dcu = dc[u] + dh[u] * go * (1.f - tc * tc);
+        dg[q] = dcu * gg * gi * (1.f - gi);
+        dg[4 + q] = dcu * cp * gf * (1.f - gf);
+        dg[8 + q] = dcu * gi * (1.f - gg * gg);
+        dg[12 + q] = dh[u] * tc * go * (1.f - go);
+        dc[u] = dcu * gf;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        gbuf[(long long)((r >> 2) * H + unit_of(tt, hh, r & 3)) * KB + row] = f32_to_bf16(dg[r]);
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = dg[8 * e + j];
+        const uint4 bfr = pack8(v);
+        const int ks = 2 * tt + e;
+        acc0 = mfma_bf16(wt[(0 * 16 + ks) * 64 + lo], bfr, acc0);
+        acc1 = mfma_bf16(wt[(1 * 16 + ks) * 64 + lo], bfr, acc1);
+      }
+    }
+    // keep my M-tile (units 32w..), hand the other partial to the other wave
+    const f32x16& mine = w ? acc1 : acc0;
+    const f32x16& theirs = w ? acc0 : acc1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) x.dh[((buf * 2 + w) * 16 + r) * 64 + lane] = theirs[r];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dh[r] = mine[r] + x.dh[((buf * 2 + (1 - w)) * 16 + r) * 64 + lane];
+  }
+}
+
+__global__ __launch_bounds__(128, 1) void lstm_ae_train_kernel2(const LstmTrainArgs a) {
+  const int lane = lane_id();
+  const int hh = lane >> 5;
+  const int w = wave_id();
+  const long long grp = blockIdx.x;
+  const long long b = grp * 32 + (lane & 31);
+  const long long KB = (long long)a.T * a.B;
+  char* smem = fm_lstm_train_smem;
+  uint4* wlds = (uint4*)smem;
+  float* wout = (float*)(smem + FRAG_BYTES_BF16);
+  Xch x;
+  x.hb = (uint4*)(smem + FRAG_BYTES_BF16 + 7 * H * 4);
+  x.y = (float*)(x.hb + 2 * 2 * 2 * 64);
+  x.dh = x.y + 2 * 2 * 8 * 64;
+  float4* base = (float4*)a.scratch + grp * 2 * 2 * (long long)a.T * SV4H * 64;
+  float4* scr_enc = base + (0 * 2 + w) * (long long)a.T * SV4H * 64;
+  float4* scr_dec = base + (1 * 2 + w) * (long long)a.T * SV4H * 64;
+
+  for (int i = threadIdx.x; i < a.F * H; i += blockDim.x) wout[i] = a.w_out[i];
+  stage(wlds, a.w_enc, FRAG_BYTES_BF16 / 16);
+  __syncthreads();
+  float hreg[16], creg[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { hreg[i] = 0.f; creg[i] = 0.f; }
+  float errsum = 0.f;
+  const int ph = a.phases ? a.phases : 15;
+  if (ph & 1) fwd_phase2<true>(a, wlds, wout, scr_enc, b, hh, w, KB, hreg, creg, errsum, x);
+  float c_enc[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) c_enc[i] = creg[i];
+  __syncthreads();
+  stage(wlds, a.w_dec, FRAG_BYTES_BF16 / 16);
+  __syncthreads();
+  if (ph & 2) fwd_phase2<false>(a, wlds, wout, scr_dec, b, hh, w, KB, hreg, creg, errsum, x);
+  if (w == 0 && hh == 0) a.err[b] = errsum / (float)(a.T * a.F);
+  __syncthreads();
+  stage(wlds, a.wt_dec, WT_FRAGS * 64);
+  __syncthreads();
+  float dh[16], dc[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { dh[i] = 0.f; dc[i] = 0.f; }
+  if (ph & 4) bwd_phase2<false>(a, wlds, wout, scr_dec, c_enc, b, hh, w, KB, dh, dc, x);
+  __syncthreads();
+  stage(wlds, a.wt_enc, WT_FRAGS * 64);
+  __syncthreads();
+  float zero[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) zero[i] = 0.f;
+  if (ph & 8) bwd_phase2<true>(a, wlds, wout, scr_enc, zero, b, hh, w, KB, dh, dc, x);
+}
+
 }  // namespace
 
 extern "C" size_t fm_lstm_train_lds_bytes(int F) { return (size_t)FRAG_BYTES_BF16 + (size_t)F * H * 4; }
+
+static size_t lds_bytes_v1() {
+  return (size_t)FRAG_BYTES_BF16 + 7 * H * 4 + 2 * 2 * 2 * 64 * 16 + (2 * 2 * 8 * 64 + 2 * 2 * 16 * 64) * 4;
+}
 
 extern "C" long long fm_lstm_train_scratch_floats(int B, int T) {
   return (long long)(B / 32) * 2 * T * SV4 * 64 * 4;
@@ -323,7 +598,10 @@ extern "C" long long fm_lstm_train_args_size() { return (long long)sizeof(LstmTr
 extern "C" int fm_lstm_ae_train(const LstmTrainArgs* a, hipStream_t st) {
   if (a->B <= 0) return 0;
   if (a->B % 32 || a->F < 1 || a->F > 7 || a->T < 1) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(lstm_ae_train_kernel, dim3((unsigned)(a->B / 32)), dim3(64),
-                     fm_lstm_train_lds_bytes(a->F), st, *a);
+  if (a->variant == 1)
+    hipLaunchKernelGGL(lstm_ae_train_kernel2, dim3((unsigned)(a->B / 32)), dim3(128), lds_bytes_v1(), st, *a);
+  else
+    hipLaunchKernelGGL(lstm_ae_train_kernel, dim3((unsigned)(a->B / 32)), dim3(64),
+                       fm_lstm_train_lds_bytes(a->F), st, *a);
   return (int)hipGetLastError();
 }

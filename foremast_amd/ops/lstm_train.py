@@ -12,7 +12,8 @@ backward recurrence).
 from __future__ import annotations
 
 import ctypes as C
-from typing import Dict
+import os
+from typing import Dict, Optional
 
 import torch
 
@@ -27,7 +28,7 @@ class LstmTrainArgs(C.Structure):
         ("w_enc", C.c_void_p), ("w_dec", C.c_void_p), ("wt_enc", C.c_void_p), ("wt_dec", C.c_void_p),
         ("w_out", C.c_void_p), ("b_out", C.c_void_p), ("scratch", C.c_void_p),
         ("g_enc", C.c_void_p), ("g_dec", C.c_void_p), ("h_enc", C.c_void_p), ("h_dec", C.c_void_p),
-        ("dy", C.c_void_p), ("err", C.c_void_p), ("loss_scale", C.c_float),
+        ("dy", C.c_void_p), ("err", C.c_void_p), ("loss_scale", C.c_float), ("variant", C.c_int),
     ]
 
 
@@ -83,7 +84,10 @@ def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 class FusedLstmGrad:
     """Reusable buffers + launcher for one (B, T, F) training shape."""
 
-    def __init__(self, B: int, T: int, F: int, device) -> None:
+    def __init__(self, B: int, T: int, F: int, device, variant: Optional[int] = None) -> None:
+        """``variant`` 0: one wave per 32 windows; 1 (default): two waves per 32
+        windows splitting the hidden units (env ``FOREMAST_LSTM_TRAIN_VARIANT``)."""
+        self.variant = int(os.environ.get("FOREMAST_LSTM_TRAIN_VARIANT", "1")) if variant is None else int(variant)
         if B % 32:
             raise KernelShapeError("fused LSTM training needs B % 32 == 0")
         if not 1 <= F <= 7:
@@ -140,6 +144,7 @@ class FusedLstmGrad:
         a.h_enc, a.h_dec = self.h_enc.data_ptr(), self.h_dec.data_ptr()
         a.dy, a.err = self.dy.data_ptr(), self.err.data_ptr()
         a.loss_scale = 2.0 / (self.B * self.T * self.F)
+        a.variant = self.variant
         nat.check(lib.fm_lstm_ae_train(C.byref(a), nat.stream_handle(self.device)), "fm_lstm_ae_train")
         return self.err
 

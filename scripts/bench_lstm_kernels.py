@@ -33,12 +33,15 @@ def main():
     B, T, F = int(os.environ.get("B", 4096)), int(os.environ.get("T", 32)), int(os.environ.get("F", 1))
     m = LSTMAutoencoder(F, 64).to(dev)
     x = torch.randn(B, T, F, device=dev)
-    fg = FusedLstmGrad(B, T, F, dev)
-    for ph, name in [(15, "all"), (1, "enc_fwd"), (2, "dec_fwd"), (3, "fwd"), (4, "dec_bwd"), (8, "enc_bwd")]:
-        fg.phases = ph
-        print(json.dumps({"kernel": "lstm_train", "phases": name, "B": B, "T": T, "ms": round(timeit(lambda: fg.launch(m, x)), 4)}))
-    fg.phases = 0
-    print(json.dumps({"kernel": "lstm_train+gemms", "B": B, "T": T, "ms": round(timeit(lambda: fg.grads(m, x)), 4)}))
+    for variant in (0, 1):
+        fg = FusedLstmGrad(B, T, F, dev, variant=variant)
+        for ph, name in [(15, "all"), (1, "enc_fwd"), (2, "dec_fwd"), (3, "fwd"), (4, "dec_bwd"), (8, "enc_bwd")]:
+            fg.phases = ph
+            print(json.dumps({"kernel": "lstm_train", "variant": variant, "phases": name, "B": B, "T": T,
+                              "ms": round(timeit(lambda: fg.launch(m, x)), 4)}))
+        fg.phases = 0
+        print(json.dumps({"kernel": "lstm_train+gemms", "variant": variant, "B": B, "T": T,
+                          "ms": round(timeit(lambda: fg.grads(m, x)), 4)}))
     N = int(os.environ.get("N", 100000))
     xs = torch.randn(N, T, F, device=dev)
     for fp8 in (False, True):

@@ -243,8 +243,8 @@ def test_backward_register_plan_matches_wT_dgates():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("F", [1, 3])
-def test_fused_lstm_training_grads_match_autograd(F):
+@pytest.mark.parametrize("F,variant", [(1, 0), (3, 0), (1, 1), (3, 1)])
+def test_fused_lstm_training_grads_match_autograd(F, variant):
     from foremast_amd.ops.lstm_train import FusedLstmGrad
     torch.manual_seed(5)
     dev = torch.device("cuda:0")
@@ -253,7 +253,7 @@ def test_fused_lstm_training_grads_match_autograd(F):
     x = torch.randn(B, T, F, device=dev)
     loss = m.recon_error(x).mean()
     ref = torch.autograd.grad(loss, list(m.parameters()))
-    fg = FusedLstmGrad(B, T, F, dev)
+    fg = FusedLstmGrad(B, T, F, dev, variant=variant)
     with torch.no_grad():
         err_ref = m.recon_error(x)
     got_loss = fg.grads(m, x)
