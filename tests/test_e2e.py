@@ -49,7 +49,7 @@ def metadata(namespace="foremast"):
     }
 
 
-def build_world(algorithm="moving_average_all", strategy_canary=False):
+def build_world(algorithm="moving_average_all", strategy_canary=False, device="cpu"):
     clock = Clock(T0)
     kube = FakeCluster()
     kube.add_namespace(NS)
@@ -73,7 +73,9 @@ def build_world(algorithm="moving_average_all", strategy_canary=False):
     env["MIN_HISTORICAL_DATA_POINT_TO_MEASURE"] = "10"
     cfg = BrainConfig.from_env(env)
     metrics = BrainMetrics()
-    brain = BrainWorker(store, cfg, prom=PromClient(transport=prom_transport), scorer=BatchScorer(cfg),
+    import torch
+    brain = BrainWorker(store, cfg, prom=PromClient(transport=prom_transport),
+                        scorer=BatchScorer(cfg, device=torch.device(device)),
                         worker_id="brain-0", clock=clock, metrics=metrics)
     return clock, kube, prom, store, barrel, mc, brain, metrics
 
@@ -113,9 +115,15 @@ async def _drive_rollout(world):
     return mon
 
 
-@pytest.mark.parametrize("algorithm", ["moving_average_all", "holt_winters", "prophet"])
-def test_rollout_spike_rolls_back(algorithm):
-    world = build_world(algorithm)
+@pytest.mark.parametrize("algorithm,device", [
+    ("moving_average_all", "cpu"), ("holt_winters", "cpu"), ("prophet", "cpu"),
+    # the same scenario through the HIP kernels (rank tests, window stats / HW scan, fused epilogue)
+    pytest.param("moving_average_all", "cuda", marks=pytest.mark.gpu),
+    pytest.param("holt_winters", "cuda", marks=pytest.mark.gpu),
+    pytest.param("prophet", "cuda", marks=pytest.mark.gpu),
+])
+def test_rollout_spike_rolls_back(algorithm, device):
+    world = build_world(algorithm, device=device)
     clock, kube, prom, store, barrel, mc, brain, metrics = world
 
     async def go():

@@ -69,7 +69,11 @@ def test_align_job_common_timestamps():
     assert hist.shape == (10, 2) and list(cts) == [60.0] and cur.tolist() == [[2.0, 7.0]]
 
 
-def test_worker_auto_routes_three_metrics_to_lstm():
+import pytest
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_worker_auto_routes_three_metrics_to_lstm(device):
     """Brain worker, ML_ALGORITHM=auto, a job with 3 metrics: the joint LSTM
     flags the 5xx storm of a faulty rollout."""
     from foremast_amd.brain.batch import BatchScorer
@@ -111,7 +115,7 @@ def test_worker_auto_routes_three_metrics_to_lstm():
                threshold0="1000", threshold1="1000", threshold2="1000")  # univariate models can't fire
     cfg = BrainConfig.from_env(env)
     brain = BrainWorker(store, cfg, prom=PromClient(transport=httpx.ASGITransport(app=prom.asgi_app())),
-                        scorer=BatchScorer(cfg, device=torch.device("cpu")), worker_id="b0", clock=clock)
+                        scorer=BatchScorer(cfg, device=torch.device(device)), worker_id="b0", clock=clock)
     assert asyncio.run(brain.cycle()) == 1
     doc = store.get(body["jobId"])
     assert doc["status"] == "completed_unhealth", doc["reason"]
