@@ -80,6 +80,7 @@ class BatchScorer:
     def _pack(self, tasks: List[MetricTask]):
         B = len(tasks)
         T = max(len(t.hist) for t in tasks)
+        T = (T + 7) // 8 * 8  # rows 16/32-byte aligned for the kernels' vector loads (front NaN pad)
         C = max(1, max(len(t.cur_vals) for t in tasks))
         hist = np.full((B, T), np.nan, dtype=np.float32)
         cur = np.full((B, C), np.nan, dtype=np.float32)
