@@ -79,6 +79,9 @@ def parse():
     p.add_argument("--config", default="canary", choices=["canary", "lstm", "multivariate"],
                    help="canary = headline (BASELINE configs 2/4 at 100k); lstm = config 3; "
                         "multivariate = config 5 (fp8 LSTM, latency + error-rate)")
+    p.add_argument("--multi-cluster", action="store_true",
+                   help="config 4 layout: each rank scrapes the baseline cluster of its neighbour's shard; "
+                        "baseline windows reach their owner through one RCCL all-to-all per tick")
     p.add_argument("--lstm-window", type=int, default=32)
     p.add_argument("--lstm-train-batch", type=int, default=4096)
     p.add_argument("--lstm-train-every", type=int, default=1)
@@ -163,27 +166,58 @@ def setup_canary(args, world, rank, dev):
     # per tick: P canary-pod values (a fraction of series regressed) and P
     # baseline-pod values (healthy, same times) -> [ticks, N, 2P]
     cur_t = make_ticks(params, P, total_ticks + W, args.season, args.ring, 99 + rank, args.anomaly_frac)
-    base_t = make_ticks(params, P, total_ticks + W, args.season, args.ring, 7 + rank, 0.0)
-    ticks = torch.cat([cur_t, base_t], 2)
-    del cur_t, base_t
+    exch = None
+    if args.multi_cluster:
+        # this rank scrapes the baseline pods of the neighbour's shard
+        from foremast_amd.parallel import canary
+        r_ids = canary.remote_baseline_ids(args.series, world, rank, align=METRICS_PER_APP).to(dev)
+        r_rank = (rank + 1) % world
+        r_params = synthetic_params(int(r_ids.numel()), dev, seed=1234 + r_rank)
+        base_t = make_ticks(r_params, P, total_ticks + W, args.season, args.ring, 7 + r_rank, 0.0)
+        owner = canary.owner_of(r_ids, canary.shard_starts(args.series, world, METRICS_PER_APP, dev))
+        exch = canary.WindowExchanger(r_ids, owner, P)
+        local_rows = (exch.recv_ids - s).long()
+        if int(local_rows.numel()) != n_local:
+            raise RuntimeError("multi-cluster exchange does not cover the shard")
+        ticks = cur_t
+        base_host = base_t.cpu()
+        if dev.type == "cuda":
+            base_host = base_host.pin_memory()
+        base_dev = torch.empty((base_t.shape[1], P), dtype=torch.float32, device=dev)
+        del base_t
+    else:
+        base_t = make_ticks(params, P, total_ticks + W, args.season, args.ring, 7 + rank, 0.0)
+        ticks = torch.cat([cur_t, base_t], 2)
+        del base_t
+    del cur_t
     pin = dev.type == "cuda"
     host_ticks = ticks.cpu()
     if pin:
         host_ticks = host_ticks.pin_memory()
     del ticks
-    newvb = torch.empty((n_local, 2 * P), dtype=torch.float32, device=dev)
-    newv, newb = newvb[:, :P], newvb[:, P:]
+    if exch is None:
+        newvb = torch.empty((n_local, 2 * P), dtype=torch.float32, device=dev)
+        newv, newb = newvb[:, :P], newvb[:, P:]
+    else:
+        newvb = torch.empty((n_local, P), dtype=torch.float32, device=dev)
+        newv, newb = newvb, torch.empty((n_local, P), dtype=torch.float32, device=dev)
+
+    def load_tick(k):
+        newvb.copy_(host_ticks[k], non_blocking=pin)
+        if exch is not None:
+            base_dev.copy_(base_host[k], non_blocking=pin)
+            newb.index_copy_(0, local_rows, exch(base_dev))  # RC5: baseline windows to their owners
     agg = HealthAggregator(n_local, per, dev)
     health_host = torch.empty_like(shard.app_stats, device="cpu")
     if pin:
         health_host = health_host.pin_memory()
     # prefill the current window so every tick scores a full 10-minute window
     for k in range(W):
-        newvb.copy_(host_ticks[k], non_blocking=pin)
+        load_tick(k)
         shard.ingest_tick(newv, newb)
 
     def tick(k):
-        newvb.copy_(host_ticks[W + k], non_blocking=pin)
+        load_tick(W + k)
         shard.ingest_tick(newv, newb)
         out = shard.score()
         stats, _ = agg.tick(shard.app_stats, out["verdict"])
@@ -200,8 +234,10 @@ def setup_canary(args, world, rank, dev):
         "pods": P,
         "current_window": W,
         "grid_points": int(shard.grid.shape[0]),
+        "multi_cluster": bool(args.multi_cluster),
     }
     dt = "bf16" if dtype == torch.bfloat16 else "fp32"
+    meta["_agg"] = agg
     return tick, health_host, meta, dt, args.series
 
 
@@ -270,6 +306,7 @@ def setup_lstm(args, world, rank, dev, n_features, fp8):
         "train_score_overlap": not args.lstm_no_overlap,
     }
     dt = "bf16"  # training fp32 master / bf16 MFMA scoring (fp8 weights+activations for config 5)
+    meta["_agg"] = agg
     return tick, health_host, meta, dt, n_ent * F
 
 
@@ -283,8 +320,12 @@ def main():
     else:
         tick, health_host, meta, dtype_name, n_series = setup_lstm(args, world, rank, dev, 2, True)
 
+    agg = meta.pop("_agg", None)
     for k in range(args.warmup):
         tick(k)
+    if agg is not None:
+        agg.flush_timings()
+        agg.timings_ms.clear()
     barrier(dev)
     if dev.type == "cuda":
         torch.cuda.synchronize()
@@ -305,6 +346,7 @@ def main():
         dist.all_reduce(lat_t, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
     lat_ms = lat_t.cpu().numpy() * 1e3
+    coll_ms = agg.flush_timings() if agg is not None else []
     anomalous_apps = int((health_host[:, 0] > 0).sum())
     scored = int(health_host[:, 1].sum())
     if rank == 0:
@@ -329,6 +371,8 @@ def main():
             "config": config,
             "p50_detect_latency_ms": round(float(np.percentile(lat_ms, 50)), 3),
             "p99_detect_latency_ms": round(float(np.percentile(lat_ms, 99)), 3),
+            # device time of the per-tick health collectives (RC2 all-reduce + RC1 all-gather), rank 0
+            "collective_ms_p50": round(float(np.percentile(coll_ms, 50)), 4) if coll_ms else None,
             "health": {"apps": int(health_host.shape[0]), "anomalous_apps": anomalous_apps,
                        "series_scored_last_tick": scored},
         }

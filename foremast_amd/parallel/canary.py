@@ -78,3 +78,36 @@ def remote_baseline_ids(n_total: int, world: int, rank: int, align: int = 1) -> 
     s, e, _ = shard_range(n_total, world, (rank + 1) % world, align)
     return torch.arange(s, e, dtype=torch.int64)
 
+
+
+class WindowExchanger:
+    """Fixed routing for the per-tick baseline exchange: the (ids, owner)
+    layout does not change between ticks, so the counts all-to-all and the
+    destination sort run once; each tick is ONE payload ``all_to_all_single``."""
+
+    def __init__(self, ids: torch.Tensor, owner: torch.Tensor, width: int, group=None) -> None:
+        self.group = group
+        self.world = _world(group)
+        self.width = width
+        self.order = torch.argsort(owner, stable=True)
+        dev = ids.device
+        if self.world == 1:
+            self.recv_ids = ids
+            return
+        send_counts = torch.bincount(owner.long(), minlength=self.world).to(torch.int64)
+        recv_counts = torch.empty_like(send_counts)
+        dist.all_to_all_single(recv_counts, send_counts, group=group)
+        self.sc, self.rc = send_counts.tolist(), recv_counts.tolist()
+        ids_s = ids[self.order].contiguous()
+        self.recv_ids = torch.empty(int(sum(self.rc)), dtype=ids.dtype, device=dev)
+        dist.all_to_all_single(self.recv_ids, ids_s, self.rc, self.sc, group=group)
+        self.recv = torch.empty((int(sum(self.rc)), width), dtype=torch.float32, device=dev)
+
+    def __call__(self, values: torch.Tensor) -> torch.Tensor:
+        if self.world == 1:
+            return values
+        send = values[self.order].contiguous()
+        W = self.width
+        dist.all_to_all_single(self.recv.view(-1), send.view(-1), [c * W for c in self.rc],
+                               [c * W for c in self.sc], group=self.group)
+        return self.recv

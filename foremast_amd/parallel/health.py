@@ -18,7 +18,8 @@ code on CPU for tests.
 
 from __future__ import annotations
 
-from typing import Optional
+import time
+from typing import List, Optional
 
 import torch
 import torch.distributed as dist
@@ -30,8 +31,11 @@ def _active() -> bool:
 
 class HealthAggregator:
     def __init__(self, n_series_local: int, n_series_padded: Optional[int] = None, device="cpu",
-                 group=None) -> None:
+                 group=None, metrics=None) -> None:
         self.group = group
+        self.metrics = metrics          # BrainMetrics: foremast_collective_seconds histogram
+        self.timings_ms: List[float] = []  # per tick, resolved one tick late (no host sync)
+        self._pending = None
         self.world = dist.get_world_size(group) if _active() else 1
         self.rank = dist.get_rank(group) if _active() else 0
         self.n_local = n_series_local
@@ -60,8 +64,44 @@ class HealthAggregator:
             dist.all_gather_into_tensor(self.verdict_all, v, group=self.group)
         return self.verdict_all
 
+    def _resolve(self, wait: bool = False) -> None:
+        p = self._pending
+        if p is None:
+            return
+        if isinstance(p, tuple) and p[0] == "cpu":
+            ms = p[1]
+        else:
+            if not wait and not p[1].query():
+                return
+            p[1].synchronize()
+            ms = p[0].elapsed_time(p[1])
+        self._pending = None
+        self.timings_ms.append(ms)
+        if self.metrics is not None:
+            self.metrics.collective.observe(ms / 1e3)
+
     def tick(self, app_stats: torch.Tensor, verdict: torch.Tensor):
-        return self.reduce_apps(app_stats), self.gather_verdicts(verdict)
+        """RC2 + RC1 for one scoring tick.  Their duration (device time between
+        events around the two collectives) is recorded without a host sync and
+        read back on the next tick (``timings_ms``, ``foremast_collective_seconds``)."""
+        self._resolve()
+        cuda = app_stats.is_cuda
+        if cuda:
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        else:
+            t0 = time.perf_counter()
+        out = self.reduce_apps(app_stats), self.gather_verdicts(verdict)
+        if cuda:
+            ev1.record()
+            self._pending = (ev0, ev1)
+        else:
+            self._pending = ("cpu", (time.perf_counter() - t0) * 1e3)
+        return out
+
+    def flush_timings(self) -> List[float]:
+        self._resolve(wait=True)
+        return self.timings_ms
 
 
 def shard_range(n_total: int, world: int, rank: int, align: int = 1):

@@ -83,14 +83,16 @@ def test_shard_range_alignment():
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("config", ["canary", "lstm"])
+@pytest.mark.parametrize("config", ["canary", "lstm", "multicluster"])
 def test_bench_distributed_cpu(config):
+    extra = ["--multi-cluster"] if config == "multicluster" else []
+    config = "canary" if config == "multicluster" else config
     port = _free_port()
     env = dict(os.environ, OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "2", "--warmup", "1", "--cpu", "--series", "200", "--ring", "480",
-           "--season", "48", "--config", config, "--lstm-train-batch", "32", "--lstm-pretrain", "2"]
+           "--season", "48", "--config", config, "--lstm-train-batch", "32", "--lstm-pretrain", "2"] + extra
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
@@ -99,6 +101,8 @@ def test_bench_distributed_cpu(config):
     assert d["n_gpus"] == 2 and d["steps"] == 2 and d["config"]["parallelism"] == "dp2"
     assert d["config"]["bench_config"] == config
     assert d["health"]["series_scored_last_tick"] == 200
+    if extra:
+        assert d["config"]["multi_cluster"] is True
     for k in ("metric", "value", "unit", "ms_per_step", "higher_is_better", "scaling", "vs_baseline", "dtype",
               "data", "config"):
         assert k in d
