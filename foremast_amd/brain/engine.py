@@ -87,6 +87,13 @@ class StreamingShard:
             self._h_pinned = torch.empty(C, dtype=torch.int32).pin_memory()
         self.out: Dict[str, torch.Tensor] = {}
         self.pw_out: Dict[str, torch.Tensor] = {}
+        # K9: compacted anomalous points of the current window (GPU), enabled via enable_anomaly_list()
+        self.anomalies = None
+
+    def enable_anomaly_list(self, cap: int) -> None:
+        if self.gpu:
+            from ..ops import kernels as K
+            self.anomalies = K.AnomalyBuffer(cap, self.device)
 
     # ------------------------------------------------------------------ data in
     def load_history(self, values: torch.Tensor) -> None:
@@ -144,7 +151,10 @@ class StreamingShard:
         spec = K.DetectSpec(horizons=self.horizons, threshold=self.threshold, bound=self.bound,
                             min_lower=self.min_lower, cur=self.cur.data, differs=differs,
                             pw_scale=cfg.pairwise_scale, min_valid=cfg.min_historical_points,
-                            want_band=self.spec.want_band, app_id=self.app_id, app_stats=self.app_stats)
+                            want_band=self.spec.want_band, app_id=self.app_id, app_stats=self.app_stats,
+                            anomalies=self.anomalies)
+        if self.anomalies is not None:
+            self.anomalies.reset()
         h = self.hist
         if self.mode is not None:
             self.out = K.smoothing_fit(h.data, h.head, h.length, self.mode, self.spec.season, self.grid,

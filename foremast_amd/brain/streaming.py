@@ -187,6 +187,7 @@ class StreamingMonitor:
             threshold=torch.tensor([t.threshold for t in th], dtype=torch.float32, device=dev),
             bound=torch.tensor([t.bound for t in th], dtype=torch.int8, device=dev),
             min_lower=torch.tensor([t.min_lower_bound for t in th], dtype=torch.float32, device=dev))
+        self.shard.enable_anomaly_list(cap=max(1024, 4 * N))
         self.shard.load_history(torch.from_numpy(np.ascontiguousarray(grid[:, :self.R])))
         for k in range(self.W):
             self.shard.ingest_tick(torch.from_numpy(np.ascontiguousarray(grid[:, self.R + k:self.R + k + 1])).to(dev))
@@ -215,7 +216,24 @@ class StreamingMonitor:
         verdict = out["verdict"].cpu().numpy()
         upper = out["upper"][:, col].float().cpu().numpy() if "upper" in out else None
         lower = out["lower"][:, col].float().cpu().numpy() if "lower" in out else None
-        latest = self.shard.cur.data[:, col].float().cpu().numpy()
+        # anomalous points of the current window per series: (timestamp, value) pairs
+        points: Dict[int, List[Tuple[float, float]]] = {}
+        ab = self.shard.anomalies
+        overflow = False
+        if ab is not None:  # K9 device-side compaction: only the anomalies come back
+            rows, cols, vals, overflow = ab.fetch()
+        if ab is None or overflow:
+            x = self.shard.cur.data.float().cpu().numpy()
+            up = out["upper"].float().cpu().numpy()
+            lo = out["lower"].float().cpu().numpy()
+            b = self.shard.bound.cpu().numpy().astype(np.int64)[:, None]
+            flag = (((b & 1) != 0) & (x > up)) | (((b & 2) != 0) & (x < lo))
+            flag &= (verdict == 1)[:, None]
+            rows, cols = np.nonzero(flag)
+            vals = x[rows, cols]
+        for rr, cc, vv in zip(rows.tolist(), cols.tolist(), vals.tolist()):
+            age = (col - cc) % C
+            points.setdefault(rr, []).append((self.t_last - age * self.step, vv))
         self.ticks += 1
         self.metrics.tick.observe(time.perf_counter() - t0)
         self.metrics.series_scored.inc(len(self.keys))
@@ -227,7 +245,10 @@ class StreamingMonitor:
                     self.metrics.export_band(metric, ns, app, float(upper[row]), float(lower[row]),
                                              self.t_last if verdict[row] == 1 else None)
                 if verdict[row] == 1:
-                    anomaly[alias] = {"tags": "", "values": [self.t_last, float(latest[row])]}
+                    flat: List[float] = []
+                    for ts, v in sorted(points.get(row, [])):
+                        flat += [ts, float(v)]
+                    anomaly[alias] = {"tags": "", "values": flat}
             if anomaly:
                 status, reason = r.ST_COMPLETED_UNHEALTH, "anomaly detected in " + ",".join(sorted(anomaly))
             elif now >= job.end_ts:

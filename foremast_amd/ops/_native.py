@@ -38,6 +38,7 @@ class DetectArgs(C.Structure):
         ("pw_scale", F), ("_pad0", I),
         ("forecast", P), ("upper", P), ("lower", P), ("count", P), ("verdict", P),
         ("score", P), ("app_id", P), ("app_stats", P),
+        ("anom_count", P), ("anom_series", P), ("anom_col", P), ("anom_val", P), ("anom_cap", I), ("_pad1", I),
     ]
 
 

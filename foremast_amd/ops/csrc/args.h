@@ -26,6 +26,14 @@ struct DetectArgs {
   float* score;                 // [N]
   const int* app_id;            // [N] or null
   int* app_stats;               // [A, 2] (anomalous, scored) or null
+  // K9 compaction (optional): every anomalous (series, column, value) is
+  // appended at slot atomicAdd(anom_count, 1) while slot < anom_cap
+  int* anom_count;              // [1] (zeroed by the caller) or null
+  int* anom_series;             // [anom_cap]
+  int* anom_col;                // [anom_cap]
+  float* anom_val;              // [anom_cap]
+  int anom_cap;
+  int _pad1;
 };
 
 struct SmoothArgs {

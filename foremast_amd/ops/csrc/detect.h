@@ -56,6 +56,14 @@ __device__ __forceinline__ void detect_epilogue(const DetectArgs& d, int n, floa
         anyv = 1.f;
         const bool an = model_ok && (((bnd & 1) && x > up) || ((bnd & 2) && x < lo));
         cnt += an ? 1.f : 0.f;
+        if (an && d.anom_count) {  // anomalies are rare: one atomic per anomalous point
+          const int slot = atomicAdd(d.anom_count, 1);
+          if (slot < d.anom_cap) {
+            d.anom_series[slot] = n;
+            d.anom_col[slot] = c;
+            d.anom_val[slot] = x;
+          }
+        }
         sc = fmaxf(sc, fabsf(x - f) / fmaxf(sig, 1e-12f));
       }
     }

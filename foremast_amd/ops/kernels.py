@@ -62,6 +62,36 @@ class DetectSpec:
     want_band: bool = True
     app_id: Optional[torch.Tensor] = None   # int32 [N]
     app_stats: Optional[torch.Tensor] = None  # int32 [A, 2]
+    anomalies: Optional["AnomalyBuffer"] = None  # K9 compaction of anomalous points
+
+
+class AnomalyBuffer:
+    """Device-side compacted list of anomalous points (K9): the detection
+    epilogue appends ``(series, column, value)`` triples; the host copies back
+    only ``count`` and the used prefix instead of whole ``[N, C]`` bands."""
+
+    def __init__(self, cap: int, device) -> None:
+        dev = torch.device(device)
+        self.cap = int(cap)
+        self.count = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.series = torch.empty(self.cap, dtype=torch.int32, device=dev)
+        self.col = torch.empty(self.cap, dtype=torch.int32, device=dev)
+        self.val = torch.empty(self.cap, dtype=torch.float32, device=dev)
+
+    def reset(self) -> None:
+        self.count.zero_()
+
+    def fetch(self):
+        """(series, col, val) numpy arrays sorted by (series, col), and whether
+        the buffer overflowed (more anomalies than ``cap``)."""
+        import numpy as np
+        n_all = int(self.count.item())
+        n = min(n_all, self.cap)
+        s = self.series[:n].cpu().numpy()
+        c = self.col[:n].cpu().numpy()
+        v = self.val[:n].cpu().numpy()
+        order = np.lexsort((c, s))
+        return s[order], c[order], v[order], n_all > self.cap
 
 
 def _fill_detect(d: nat.DetectArgs, spec: DetectSpec, N: int, device, out: Dict[str, torch.Tensor]) -> None:
@@ -98,6 +128,12 @@ def _fill_detect(d: nat.DetectArgs, spec: DetectSpec, N: int, device, out: Dict[
         out["verdict"] = torch.empty(N, dtype=torch.int8, device=device)
     if "score" not in out:
         out["score"] = torch.empty(N, **kw)
+    ab = spec.anomalies
+    if ab is not None:
+        _need(ab.count.device == device, "anomaly buffer on wrong device")
+        d.anom_count, d.anom_series, d.anom_col, d.anom_val = (nat.ptr(ab.count), nat.ptr(ab.series),
+                                                               nat.ptr(ab.col), nat.ptr(ab.val))
+        d.anom_cap = ab.cap
     d.horizons = nat.ptr(spec.horizons)
     d.h_ld = int(hz.stride(0)) if hz.dim() == 2 else 0
     d.C = C

@@ -208,3 +208,40 @@ def test_seasonal_decompose_kernel_matches_reference(K, dtype, m, T):
         ok = ~torch.isnan(r)
         assert float((got[ok] - r[ok]).abs().max()) < 2e-4 * scale, k
     assert torch.allclose(out["phase_means"].cpu(), d.phase_means, atol=2e-4 * scale)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", ["window_stats", "holt_winters"])
+def test_anomaly_compaction_matches_band_flags(K, which):
+    """K9: the compacted (series, col, value) list equals the points outside
+    the enabled side of the band, computed on the host from the full bands."""
+    from foremast_amd.brain.engine import synthetic_history
+    dev = torch.device("cuda:0")
+    N, T, m, C = 3000, 2 * 1440, 1440, 20
+    hist = synthetic_history(N, T, m, dev, seed=11).to(torch.bfloat16)
+    cur = hist[:, -C:].float().contiguous()
+    cur[::7, 5] += 1000.0  # spikes
+    cur[::11, 9] -= 1000.0
+    bound = torch.tensor([1, 2, 3], dtype=torch.int8, device=dev).repeat(N // 3)
+    spec = K.DetectSpec(horizons=torch.arange(1, C + 1, dtype=torch.int32, device=dev),
+                        threshold=torch.full((N,), 3.0, device=dev), bound=bound,
+                        min_lower=torch.full((N,), -1e9, device=dev), cur=cur,
+                        anomalies=K.AnomalyBuffer(4096, dev))
+    spec.anomalies.reset()
+    if which == "window_stats":
+        out = K.window_stats(hist, 0, T, spec)
+    else:
+        grid = sm_ref.make_grid(sm_ref.MODE_HW, (0.1, 0.5), (0.0, 0.1), (0.1, 0.5)).to(dev)
+        out = K.smoothing_fit(hist, 0, T, sm_ref.MODE_HW, m, grid, spec)
+    torch.cuda.synchronize()
+    s, c, v, overflow = spec.anomalies.fetch()
+    assert not overflow
+    up, lo, x = out["upper"].cpu(), out["lower"].cpu(), cur.cpu()
+    b = bound.cpu().long()[:, None]
+    flag = (((b & 1) != 0) & (x > up)) | (((b & 2) != 0) & (x < lo))
+    flag &= (out["verdict"].cpu()[:, None] >= 0)
+    exp = flag.nonzero().numpy()
+    assert len(exp) == len(s) and len(s) > 0
+    assert (exp[:, 0] == s).all() and (exp[:, 1] == c).all()
+    assert np.allclose(v, x.numpy()[s, c])
+    assert (np.bincount(s, minlength=N) == out["count"].cpu().numpy()).all()

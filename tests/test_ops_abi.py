@@ -31,6 +31,7 @@ def test_struct_sizes(lib, name):
 @pytest.mark.parametrize("name,field", [
     ("SmoothArgs", "det"), ("SmoothArgs", "season_out"), ("SmoothArgs", "grid"),
     ("DetectArgs", "pw_scale"), ("DetectArgs", "app_stats"), ("DetectArgs", "ld_cur"),
+    ("DetectArgs", "anom_count"), ("DetectArgs", "anom_cap"),
     ("RankArgs", "pvals"), ("RankArgs", "alpha"), ("WindowArgs", "det"),
     ("BivArgs", "eps"), ("BivArgs", "app_stats"),
 ])
