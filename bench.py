@@ -76,9 +76,10 @@ def parse():
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--graph", action="store_true", help="capture the GPU part of a tick in a HIP graph")
     p.add_argument("--cpu", action="store_true", help="force CPU (reference path; tiny sizes only)")
-    p.add_argument("--config", default="canary", choices=["canary", "lstm", "multivariate"],
-                   help="canary = headline (BASELINE configs 2/4 at 100k); lstm = config 3; "
-                        "multivariate = config 5 (fp8 LSTM, latency + error-rate)")
+    p.add_argument("--config", default="canary", choices=["canary", "single", "hw10k", "lstm", "multivariate"],
+                   help="canary = headline (BASELINE configs 2/4 at 100k); single = config 1 (one latency "
+                        "series, moving average, CPU brain plumbing end to end); hw10k = config 2 (10k series); "
+                        "lstm = config 3; multivariate = config 5 (fp8 LSTM, latency + error-rate)")
     p.add_argument("--multi-cluster", action="store_true",
                    help="config 4 layout: each rank scrapes the baseline cluster of its neighbour's shard; "
                         "baseline windows reach their owner through one RCCL all-to-all per tick")
@@ -310,10 +311,86 @@ def setup_lstm(args, world, rank, dev, n_features, fp8):
     return tick, health_host, meta, dt, n_ent * F
 
 
+def setup_single(args, world, rank, dev):
+    """Config 1: one ``http_server_requests_latency`` series per rank, moving
+    average on CPU, through the whole brain path per step: register a job via
+    the service API, claim, fetch the three windows from (fake) Prometheus
+    over HTTP/ASGI, parse, score, write the verdict and export the band."""
+    import asyncio
+    import httpx
+    from foremast_amd.brain.batch import BatchScorer
+    from foremast_amd.brain.worker import BrainWorker
+    from foremast_amd.promql import synth
+    from foremast_amd.promql.client import PromClient
+    from foremast_amd.promql.fake import FakePrometheus
+    from foremast_amd.service import app as svc
+    from foremast_amd.store import MemoryJobStore
+    from foremast_amd.utils.config import reference_default_env
+    from foremast_amd.utils.timeutil import format_rfc3339
+    metric = "http_server_requests_latency"
+    t0 = 1_700_000_000.0
+    state = {"now": t0}
+    prom = FakePrometheus(clock=lambda: state["now"])
+    prom.add("namespace_app_per_pod:" + metric, {"namespace": "ns", "app": "demo"},
+             synth.seasonal(level=0.12, amp=0.02, noise=0.004, seed=rank))
+    prom.add("namespace_pod:" + metric, {"namespace": "ns", "pod": "demo-v2"},
+             synth.seasonal(level=0.12, amp=0.02, noise=0.004, seed=100 + rank))
+    store = MemoryJobStore()
+    env = reference_default_env()
+    env["ML_ALGORITHM"] = "moving_average_all"
+    cfg = BrainConfig.from_env(env)
+    loop = asyncio.new_event_loop()
+    brain = BrainWorker(store, cfg, prom=PromClient(transport=httpx.ASGITransport(app=prom.asgi_app())),
+                        scorer=BatchScorer(cfg, device=torch.device("cpu")), worker_id=f"bench-{rank}",
+                        clock=lambda: state["now"])
+
+    def job(k):
+        start = t0 + 600 * k
+        q = {"endpoint": "http://prometheus:9090/api/v1/", "step": 60}
+        return {"appName": "demo", "startTime": format_rfc3339(start), "endTime": format_rfc3339(start + 600),
+                "strategy": "rollingupdate", "metrics": {
+                    "current": {"latency": {"dataSourceType": "prometheus", "parameters": dict(
+                        q, query=f'namespace_pod:{metric}{{namespace="ns",pod="demo-v2"}}',
+                        start=int(start), end=int(start + 600))}},
+                    "historical": {"latency": {"dataSourceType": "prometheus", "parameters": dict(
+                        q, query=f'namespace_app_per_pod:{metric}{{namespace="ns",app="demo"}}',
+                        start=int(start - 7 * 86400), end=int(start))}}}}
+
+    last = {}
+
+    def tick(k):
+        state["now"] = t0 + 600 * k + 660  # the window is over: the job finishes this cycle
+        code, body = svc.register(store, job(k))
+        assert code == 200, body
+        n = loop.run_until_complete(brain.cycle())
+        assert n == 1
+        last["status"] = store.get(body["jobId"])["status"]
+        return last
+
+    health = torch.zeros((1, 2), dtype=torch.int32)
+
+    def tick_and_health(k):
+        out = tick(k)
+        health[0, 0] = int(out["status"] == "completed_unhealth")
+        health[0, 1] = 1
+        return out
+
+    meta = {"model": "moving_average_all on one http_server_requests_latency series (CPU brain, end to end)",
+            "global_batch": world, "seq_len": 10080, "path": "service register -> claim -> Prometheus HTTP -> "
+            "native parse -> score -> verdict write"}
+    return tick_and_health, health, meta, "fp32", world
+
+
 def main():
     args = parse()
+    if args.config == "hw10k":
+        args.series = 10_000  # BASELINE config 2: same pipeline as the headline at 10k series
+        args.config = "canary"
+        args.config_name = "hw10k"
     world, rank, dev = init_dist(args)
-    if args.config == "canary":
+    if args.config == "single":
+        tick, health_host, meta, dtype_name, n_series = setup_single(args, world, rank, dev)
+    elif args.config == "canary":
         tick, health_host, meta, dtype_name, n_series = setup_canary(args, world, rank, dev)
     elif args.config == "lstm":
         tick, health_host, meta, dtype_name, n_series = setup_lstm(args, world, rank, dev, 1, False)
@@ -352,7 +429,8 @@ def main():
     if rank == 0:
         value = n_series * args.steps / elapsed
         config = {"model": meta.pop("model"), "global_batch": meta.pop("global_batch"),
-                  "seq_len": meta.pop("seq_len"), "parallelism": f"dp{world}", "bench_config": args.config}
+                  "seq_len": meta.pop("seq_len"), "parallelism": f"dp{world}",
+                  "bench_config": getattr(args, "config_name", args.config)}
         config.update(meta)
         config["device"] = str(dev) if dev.type == "cpu" else torch.cuda.get_device_name(dev)
         res = {

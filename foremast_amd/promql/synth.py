@@ -70,3 +70,29 @@ def gaps(base: Gen, every: int = 17) -> Gen:
         v[idx] = np.nan
         return v
     return f
+
+
+def replay(rates: Sequence[float], start: float, step: float = 60.0, before: Optional[Gen] = None,
+           loop: bool = False) -> Gen:
+    """Replay a recorded rate file (one value per ``step`` from ``start``), like
+    the reference demo's ``FileErrorGenerator``; before ``start`` the ``before``
+    generator (history), after the end NaN (or wrap around with ``loop``)."""
+    r = np.asarray(rates, dtype=np.float64)
+
+    def f(ts):
+        ts = np.asarray(ts, dtype=np.float64)
+        k = np.floor((ts - start) / step).astype(np.int64)
+        if loop:
+            k = np.where(k >= 0, k % len(r), k)
+        inside = (k >= 0) & (k < len(r))
+        out = np.full(ts.shape, np.nan)
+        out[inside] = r[k[inside]]
+        if before is not None:
+            out = np.where(k < 0, before(ts), out)
+        return out
+    return f
+
+
+def read_rates(path: str) -> list:
+    with open(path) as fh:
+        return [float(x) for x in (ln.strip() for ln in fh) if x and not x.startswith("#")]

@@ -269,3 +269,40 @@ def test_live_loops_rollout_to_rollback():
 
     del svc_transport
     asyncio.run(go())
+
+
+def test_config1_single_latency_series_replay():
+    """BASELINE config 1 / SURVEY §7.3: one series, moving-average baseline on
+    CPU; the current window replays the demo's spike file (our own
+    examples/demo/data/spike_rates.txt) through the fake Prometheus."""
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    rates = synth.read_rates(os.path.join(root, "examples", "demo", "data", "spike_rates.txt"))
+    world = build_world("moving_average_all")
+    clock, kube, prom, store, barrel, mc, brain, metrics = world
+
+    async def go():
+        v1 = kube.apply_deployment(NS, "demo", "demo", "foremast/demo:v1", replicas=1,
+                                   labels={"appType": "spring-boot"})
+        await barrel.on_deployment_added(v1)
+        old_hash = kube.list_sync("replicasets", NS)[0]["metadata"]["labels"]["pod-template-hash"]
+        v1 = kube.get_sync("deployments", NS, "demo")
+        v2 = kube.apply_deployment(NS, "demo", "demo", "foremast/demo:v2", replicas=1,
+                                   labels={"appType": "spring-boot"})
+        for p in kube.list_sync("pods", NS):
+            base = synth.error_rate(base=0.4, spread=0.3, seed=5)
+            if p["metadata"]["labels"]["pod-template-hash"] != old_hash:
+                # replay starts at the beginning of the watch window (T0 + 60 s)
+                base = synth.replay(rates, start=T0 + 60, step=60.0, before=base)
+            prom.add("namespace_pod:" + METRIC, {"namespace": NS, "pod": p["metadata"]["name"]}, base)
+        await barrel.on_deployment_updated(v1, v2)
+        await barrel.drain()
+        mon = crd.DeploymentMonitor.from_dict(kube.get_sync("deploymentmonitors", NS, "demo"))
+        clock.t = T0 + 300
+        assert await brain.cycle() == 1
+        doc = store.get(mon.status.job_id)
+        assert doc["status"] == "completed_unhealth"
+        vals = json.loads(doc["anomalyInfo"])["error5xx"]["values"]
+        assert max(vals[1::2]) > 40  # the replayed ~40/s bursts (file lines 2-3)
+
+    asyncio.run(go())
