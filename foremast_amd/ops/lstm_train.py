@@ -73,6 +73,22 @@ def _t_index(device) -> torch.Tensor:
     return _T_IDX[k]
 
 
+def _bmm_sum_f32(a: torch.Tensor, b: torch.Tensor, chunks: int) -> torch.Tensor:
+    """``a [M, K] @ b [K, N]`` as a strided-batched GEMM over ``chunks`` K-slices
+    summed in fp32: the K = T*B reduction of the weight gradients is far too
+    deep for one tall-skinny GEMM to fill the GPU; T slices of K = B run as one
+    batched launch (no copies: the slices are strided views)."""
+    M, K = a.shape
+    N = b.shape[1]
+    kc = K // chunks
+    av = a.as_strided((chunks, M, kc), (kc, a.stride(0), a.stride(1)))
+    bv = b.as_strided((chunks, kc, N), (kc * b.stride(0), b.stride(0), b.stride(1)))
+    try:
+        return torch.bmm(av, bv, out_dtype=torch.float32).sum(0)
+    except (RuntimeError, TypeError, NotImplementedError):
+        return torch.bmm(av.float(), bv.float()).sum(0)
+
+
 def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     """bf16 x bf16 → fp32 GEMM (hipBLASLt) without rounding the result to bf16."""
     try:
@@ -122,6 +138,7 @@ class FusedLstmGrad:
         self.wt_dec.copy_(model.dec_w_hh.detach().flatten()[tidx])
 
     phases = 0  # profiling only: restrict the kernel to a subset of its four phases
+    batched_gemm = True  # weight-grad reduction as a strided-batched GEMM over time slices
 
     def launch(self, model, x: torch.Tensor) -> torch.Tensor:
         """Run the fused forward+backward; returns per-window errors ``[B]``."""
@@ -151,9 +168,13 @@ class FusedLstmGrad:
     def grads(self, model, x: torch.Tensor) -> torch.Tensor:
         """Fill ``p.grad`` of every model parameter (overwrite); returns the loss."""
         err = self.launch(model, x)
-        F, KB, B = self.F, self.T * self.B, self.B
-        dwe = _mm_f32(self.g_enc, self.h_enc.t())           # [256, 80]
-        dwd = _mm_f32(self.g_dec, self.h_dec[:, :KB].t())   # [256, 80]
+        F, KB, B, T = self.F, self.T * self.B, self.B, self.T
+        if self.batched_gemm:
+            dwe = _bmm_sum_f32(self.g_enc, self.h_enc.t(), T)           # [256, 80]
+            dwd = _bmm_sum_f32(self.g_dec, self.h_dec[:, :KB].t(), T)   # [256, 80]
+        else:
+            dwe = _mm_f32(self.g_enc, self.h_enc.t())
+            dwd = _mm_f32(self.g_dec, self.h_dec[:, :KB].t())
         dwo = _mm_f32(self.dy.to(torch.bfloat16), self.h_dec[:H, B:].t())  # [F, 64]
         grads = {
             "enc_w_hh": dwe[:, :H], "enc_w_ih": dwe[:, H:H + F], "enc_b": dwe[:, BIAS_K],

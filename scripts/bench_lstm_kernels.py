@@ -40,8 +40,10 @@ def main():
             print(json.dumps({"kernel": "lstm_train", "variant": variant, "phases": name, "B": B, "T": T,
                               "ms": round(timeit(lambda: fg.launch(m, x)), 4)}))
         fg.phases = 0
-        print(json.dumps({"kernel": "lstm_train+gemms", "variant": variant, "B": B, "T": T,
-                          "ms": round(timeit(lambda: fg.grads(m, x)), 4)}))
+        for bg in (False, True):
+            fg.batched_gemm = bg
+            print(json.dumps({"kernel": "lstm_train+gemms", "variant": variant, "batched_gemm": bg, "B": B, "T": T,
+                              "ms": round(timeit(lambda: fg.grads(m, x)), 4)}))
     N = int(os.environ.get("N", 100000))
     xs = torch.randn(N, T, F, device=dev)
     for fp8 in (False, True):
