@@ -43,8 +43,8 @@ class LstmShard:
         grad_fn = None
         if self.gpu and fused_train and train_batch % 32 == 0:
             from ..ops.lstm_train import FusedLstmGrad
-            fg = FusedLstmGrad(train_batch, window, n_features, self.device)
-            grad_fn = fg.grads
+            self.fg = FusedLstmGrad(train_batch, window, n_features, self.device)
+            grad_fn = self.fg.grads
         self.fused_train = grad_fn is not None
         self.trainer = DPTrainer(self.model, lr=lr, grad_fn=grad_fn)
         self.fp8 = fp8
@@ -56,6 +56,7 @@ class LstmShard:
         self.app_stats = torch.zeros((max(n_apps, 1), 2), dtype=torch.int32, device=self.device)
         self.mean = torch.zeros(n_series, n_features, device=self.device)
         self.std = torch.ones(n_series, n_features, device=self.device)
+        self.rstd = torch.ones(n_series, n_features, device=self.device)
         self.mu, self.sigma = 0.0, 1.0
         self.ticks = 0
         self.gen = torch.Generator(device=self.device)
@@ -91,6 +92,7 @@ class LstmShard:
                 o = K.window_stats(ring.data, ring.head, ring.length, self._det, out=self._ws)
                 self.mean[:, f] = o["mean"]
                 self.std[:, f] = o["std"].clamp(min=1e-6)
+            torch.reciprocal(self.std, out=self.rstd)
             return
         for f, ring in enumerate(self.rings):
             yf = ring.logical().float()
@@ -121,6 +123,29 @@ class LstmShard:
         x = torch.stack(feats, 2)  # [B, T, F]
         return ((x - self.mean[series_idx][:, None, :]) / self.std[series_idx][:, None, :]).contiguous()
 
+    def _ring_src(self, win_series: Optional[torch.Tensor] = None, win_start: Optional[torch.Tensor] = None):
+        """Kernel-side input: the kernels read the bf16 rings directly and
+        z-score on the fly, so no ``[B, T, F]`` window tensor is materialised.
+        Without ``win_series`` row n scores its newest ``T`` samples."""
+        from ..ops.lstm import RingSource
+        r0 = self.rings[0]
+        return RingSource(rings=[r.data for r in self.rings], start_col=(r0.head + r0.length - self.T) % r0.R,
+                          mean=self.mean, rstd=self.rstd, win_series=win_series, win_start=win_start)
+
+    def _sample_ring(self, B: int):
+        """``B`` random history windows as ring coordinates (two RNG launches):
+        logical start in ``[1, L - T]`` → physical ``head + start`` (the kernel
+        reduces it mod R); same distribution as :meth:`_sample`."""
+        r0 = self.rings[0]
+        L = r0.length
+        si = torch.randint(0, self.n, (B,), generator=self.gen, device=self.device, dtype=torch.int32)
+        if L > self.T:
+            st = torch.randint(r0.head + 1, r0.head + L - self.T + 1, (B,), generator=self.gen,
+                               device=self.device, dtype=torch.int32)
+        else:  # too little history: every sample is the (NaN-padded) newest window
+            st = torch.full((B,), (r0.head + L - self.T) % r0.R, dtype=torch.int32, device=self.device)
+        return self._ring_src(si, st)
+
     # ------------------------------------------------------------------ train / score
     def _sample(self, B: int) -> torch.Tensor:
         L = self.rings[0].length
@@ -130,6 +155,8 @@ class LstmShard:
 
     def train_step(self) -> torch.Tensor:
         """One DP step on ``train_batch`` history windows of this shard."""
+        if self.fused_train:
+            return self.trainer.step(self._sample_ring(self.train_batch))
         return self.trainer.step(self._sample(self.train_batch))
 
     def calibrate(self, n: int = 4096) -> None:
@@ -153,44 +180,58 @@ class LstmShard:
         else:
             L.repack_into(self.packed, self.model)
 
-    def _score_packed(self, x: torch.Tensor) -> Dict[str, torch.Tensor]:
+    def _score_packed(self) -> Dict[str, torch.Tensor]:
         from ..ops import lstm as L
         self.app_stats.zero_()
-        self.out = L.lstm_score(self.packed, x, self.mu, self.sigma, thr_default=self.threshold,
-                                app_id=self.app_id, app_stats=self.app_stats, out=self.out)
+        self.out = L.lstm_score(self.packed, None, self.mu, self.sigma, thr_default=self.threshold,
+                                app_id=self.app_id, app_stats=self.app_stats, out=self.out,
+                                ring=self._ring_src(), T=self.T)
         return self.out
 
     def tick(self, newx: torch.Tensor, train: bool = True, overlap: bool = True) -> Dict[str, torch.Tensor]:
         """Ingest + (optional) DP training step + scoring of every series.
 
         On the GPU with ``overlap`` the training step runs on a side HIP stream
-        concurrently with scoring (the training kernel occupies B/32 SIMDs,
-        scoring fills the rest); scoring uses the weights from before this
-        tick's update (a one-step model lag) and the tick joins both streams."""
+        concurrently with scoring (the training kernel occupies B/32 SIMD
+        pairs, scoring fills the rest); it is enqueued first so that its waves
+        are resident before the scoring grid fills the GPU. The scoring weights
+        are repacked on the main stream before the side stream forks, so
+        scoring uses the weights from before this tick's update (a one-step
+        model lag) and never races the Adam step; the tick joins both streams."""
         self.ingest_tick(newx)
         if not (train and overlap and self.gpu):
             if train:
                 self.train_step()
             return self.score()
-        xs = self._gather(self._all, self._zero_off)
-        xt = self._sample(self.train_batch)
-        self._pack_scoring()
+        self._pack_scoring()  # before the wait: the side stream's Adam step must not race the repack
         main = torch.cuda.current_stream(self.device)
         if self._side is None:
-            self._side = torch.cuda.Stream(self.device)
+            # high-priority side stream: the long, latency-bound training kernel
+            # (B/32 wave pairs) must get its CU slots before the scoring grid
+            # (N/32 waves, enough to fill the GPU) takes them all
+            self._side = torch.cuda.Stream(self.device, priority=-1)
         self._side.wait_stream(main)
-        xt.record_stream(self._side)
-        with torch.cuda.stream(self._side):
-            self.trainer.step(xt)
-        out = self._score_packed(xs)
+        if self.fused_train:
+            # host order: training kernel, scoring kernel, then the training
+            # tail (GEMMs, grad scatter, all-reduce, Adam) whose host cost now
+            # overlaps both kernels instead of delaying the scoring launch
+            with torch.cuda.stream(self._side):
+                self.fg.launch(self.model, None, self._sample_ring(self.train_batch))
+            out = self._score_packed()
+            with torch.cuda.stream(self._side):
+                self.trainer.step(None, grad_fn=lambda m, _w: self.fg.finish(m))
+        else:
+            with torch.cuda.stream(self._side):
+                self.train_step()
+            out = self._score_packed()
         main.wait_stream(self._side)
         return out
 
     def score(self) -> Dict[str, torch.Tensor]:
-        x = self._gather(self._all, self._zero_off)
         if self.gpu:
             self._pack_scoring()
-            return self._score_packed(x)
+            return self._score_packed()
+        x = self._gather(self._all, self._zero_off)
         self.app_stats.zero_()
         with torch.no_grad():
             err = self.model.recon_error(x)

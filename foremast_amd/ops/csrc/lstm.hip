@@ -45,6 +45,8 @@ struct LstmArgs {
   float* recon;            // [N, T, F] or null
   const int* app_id;       // [N] or null
   int* app_stats;          // [A, 2] or null
+  const float* wmax;       // fp8: device absmax [enc, dec] of the packed weights (overrides scale_w_*) or null
+  LstmRingSrc src;         // ring-direct input (x == null)
 };
 
 extern __shared__ __attribute__((aligned(16))) char fm_lstm_smem[];
@@ -60,11 +62,11 @@ __device__ __forceinline__ void run_phase(const LstmArgs& a, const typename Frag
                                           const float* wout_lds, long long series, bool valid, int hh,
                                           float (&hreg)[32], float (&creg)[32], float& errsum) {
   using FT = typename Frag<FP8>::T;
-  const float sw = ENC ? a.scale_w_enc : a.scale_w_dec;
+  const float sw = a.wmax ? fp8_scale(a.wmax[ENC ? 0 : 1]) : (ENC ? a.scale_w_enc : a.scale_w_dec);
   const float sa = a.scale_act;
   const float deq = sw * sa;  // acc → real gates
   const int lane = lane_id();
-  const float* xrow = a.x + series * (long long)a.T * a.F;
+  const XPos xp = make_xpos(a.x, a.src, valid ? series : 0, a.T, a.F);  // tail lanes never index past N
   for (int t = 0; t < a.T; ++t) {
     // B fragments: h (4 k-steps) and the input/bias k-step
     FT hb[4];
@@ -82,7 +84,7 @@ __device__ __forceinline__ void run_phase(const LstmArgs& a, const typename Frag
         if (ENC && valid) {
 #pragma unroll
           for (int f = 0; f < 7; ++f)
-            if (f < a.F) v[f] = xrow[t * a.F + f] * (1.f / sa);
+            if (f < a.F) v[f] = load_x(a.src, xp, t, f, a.F) * (1.f / sa);
         }
         v[7] = 1.f / sa;
       }
@@ -134,7 +136,7 @@ __device__ __forceinline__ void run_phase(const LstmArgs& a, const typename Frag
         p += __shfl_xor(p, 32, FM_WAVE);
         const float y = p + a.b_out[f];
         if (valid && hh == 0) {
-          const float d = y - xrow[t * a.F + f];
+          const float d = y - load_x(a.src, xp, t, f, a.F);
           errsum += d * d;
           if (a.recon) a.recon[(series * a.T + t) * a.F + f] = y;
         }

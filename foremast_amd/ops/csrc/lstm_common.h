@@ -10,7 +10,56 @@
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// Optional direct read of the model input from the HBM history rings (no
+// materialised [N, T, F] window tensor): sample t of window w is ring column
+// (start + t) mod R of series row, z-scored with the series' mean / 1/std.
+struct LstmRingSrc {
+  const void* ring[7];     // per-feature [N, ld] rings (bf16 or fp32); ring[0] == null => dense x
+  long long ld;
+  int ring_len;
+  int bf16;
+  int start_col;           // physical column of t = 0 when win_start is null
+  int _pad;
+  const int* win_series;   // [B] ring row per window (training samples) or null (row = window)
+  const int* win_start;    // [B] start column per window (taken mod ring_len) or null
+  const float* mean;       // [N, F]
+  const float* rstd;       // [N, F]
+};
+
 namespace fm_lstm {
+
+// per-lane input cursor: dense row pointer, or (ring row, start column)
+struct XPos {
+  const float* xrow;
+  long long row;
+  int start;
+};
+
+__device__ __forceinline__ XPos make_xpos(const float* x, const LstmRingSrc& s, long long w, int T, int F) {
+  XPos p;
+  if (!s.ring[0]) {
+    p.xrow = x + w * (long long)T * F;
+    p.row = w;
+    p.start = 0;
+  } else {
+    p.xrow = nullptr;
+    p.row = s.win_series ? s.win_series[w] : w;
+    p.start = (s.win_start ? s.win_start[w] : s.start_col) % s.ring_len;  // any non-negative start
+  }
+  return p;
+}
+
+__device__ __forceinline__ float load_x(const LstmRingSrc& s, const XPos& p, int t, int f, int F) {
+  if (p.xrow) return p.xrow[t * F + f];
+  int c = p.start + t;
+  if (c >= s.ring_len) c -= s.ring_len;
+  const long long o = p.row * s.ld + c;
+  const float v = s.bf16 ? bf16_to_f32(((const bf16_t*)s.ring[f])[o]) : ((const float*)s.ring[f])[o];
+  return (v - s.mean[p.row * F + f]) * s.rstd[p.row * F + f];
+}
+// dequantisation scale of a pack.hip fp8 segment with absolute maximum m
+__device__ __forceinline__ float fp8_scale(float m) { return m > 0.f ? m * (1.f / 448.f) : 1.f; }
+
 constexpr int H = 64;
 constexpr int TILES = 8;
 constexpr int KSTEPS = 5;

@@ -55,6 +55,7 @@ struct LstmTrainArgs {
   float* err;            // [B]         per-window reconstruction MSE
   float loss_scale;      // 2 / (B*T*F)
   int variant;           // 0: one wave per 32 windows; 1: two waves (hidden units split, LDS exchange)
+  LstmRingSrc src;       // ring-direct input (x == null): sampled windows read from the history rings
 };
 
 extern __shared__ __attribute__((aligned(16))) char fm_lstm_train_smem[];
@@ -99,7 +100,7 @@ __device__ __forceinline__ void fwd_phase(const LstmTrainArgs& a, const uint4* w
                                           float4* scr, long long b, int hh, long long KB,
                                           float (&hreg)[32], float (&creg)[32], float& errsum) {
   const int lane = lane_id();
-  const float* xrow = a.x + b * (long long)a.T * a.F;
+  const XPos xp = make_xpos(a.x, a.src, b, a.T, a.F);
   bf16_t* hbuf = ENC ? a.h_enc : a.h_dec;
   const long long ldh = ENC ? KB : KB + a.B;
   for (int t = 0; t < a.T; ++t) {
@@ -128,7 +129,7 @@ __device__ __forceinline__ void fwd_phase(const LstmTrainArgs& a, const uint4* w
 #pragma unroll
           for (int f = 0; f < 7; ++f)
             if (f < a.F) {
-              v[f] = xrow[t * a.F + f];
+              v[f] = load_x(a.src, xp, t, f, a.F);
               a.h_enc[(long long)(64 + f) * KB + row] = f32_to_bf16(v[f]);
             }
         }
@@ -183,7 +184,7 @@ __device__ __forceinline__ void fwd_phase(const LstmTrainArgs& a, const uint4* w
 #pragma unroll
           for (int q = 0; q < 4; ++q) p += hreg[tt * 4 + q] * wout[f * H + unit_of(tt, hh, q)];
         p += __shfl_xor(p, 32, FM_WAVE);
-        const float d = p + a.b_out[f] - xrow[t * a.F + f];
+        const float d = p + a.b_out[f] - load_x(a.src, xp, t, f, a.F);
         if (hh == 0) {
           errsum += d * d;
           a.dy[(long long)f * KB + row] = d * a.loss_scale;
@@ -337,7 +338,7 @@ __device__ __forceinline__ void fwd_phase2(const LstmTrainArgs& a, const uint4* 
                                            float (&creg)[16], float& errsum, const Xch& x) {
   const int lane = lane_id();
   const int TB = 4 * w;
-  const float* xrow = a.x + b * (long long)a.T * a.F;
+  const XPos xp = make_xpos(a.x, a.src, b, a.T, a.F);
   bf16_t* hbuf = ENC ? a.h_enc : a.h_dec;
   const long long ldh = ENC ? KB : KB + a.B;
   // prologue: publish the initial h (zeros for the encoder, the encoder's final h for the decoder)
@@ -379,7 +380,7 @@ __device__ __forceinline__ void fwd_phase2(const LstmTrainArgs& a, const uint4* 
 #pragma unroll
           for (int f = 0; f < 7; ++f)
             if (f < a.F) {
-              v[f] = xrow[t * a.F + f];
+              v[f] = load_x(a.src, xp, t, f, a.F);
               if (w == 0) a.h_enc[(long long)(64 + f) * KB + row] = f32_to_bf16(v[f]);
             }
         }
@@ -447,7 +448,7 @@ __device__ __forceinline__ void fwd_phase2(const LstmTrainArgs& a, const uint4* 
       for (int f = 0; f < 7; ++f) {
         if (f >= a.F) break;
         const float y = py[f] + x.y[((buf * 2 + (1 - w)) * 8 + f) * 64 + lane] + a.b_out[f];
-        const float d = y - xrow[t * a.F + f];
+        const float d = y - load_x(a.src, xp, t, f, a.F);
         if (w == 0 && hh == 0) {
           errsum += d * d;
           a.dy[(long long)f * KB + row] = d * a.loss_scale;

@@ -5,7 +5,7 @@ from __future__ import annotations
 
 import ctypes as C
 from dataclasses import dataclass
-from typing import Dict, Optional
+from typing import Dict, List, Optional
 
 import torch
 
@@ -18,6 +18,50 @@ BIAS_K = 71  # bias column of the augmented weight (k-step 4, lane half 0, eleme
 FP8_MAX = 448.0
 
 
+class LstmRingSrc(C.Structure):
+    _fields_ = [("ring", C.c_void_p * 7), ("ld", C.c_longlong), ("ring_len", C.c_int), ("bf16", C.c_int),
+                ("start_col", C.c_int), ("_pad", C.c_int), ("win_series", C.c_void_p), ("win_start", C.c_void_p),
+                ("mean", C.c_void_p), ("rstd", C.c_void_p)]
+
+
+@dataclass
+class RingSource:
+    """Model input read by the kernels straight from the HBM history rings:
+    window w, sample t = ring column ``(start + t) mod R`` of row
+    ``win_series[w]`` (or w), z-scored with ``mean`` / ``rstd`` ``[N, F]``."""
+    rings: list                                  # F tensors [N, R] (bf16 or fp32, unit column stride)
+    start_col: int = 0
+    mean: Optional[torch.Tensor] = None          # float32 [N, F]
+    rstd: Optional[torch.Tensor] = None          # float32 [N, F]
+    win_series: Optional[torch.Tensor] = None    # int32 [B]
+    win_start: Optional[torch.Tensor] = None     # int32 [B]
+
+    def fill(self, src: "LstmRingSrc", n_windows: int, F: int) -> None:
+        r0 = self.rings[0]
+        _need(len(self.rings) == F and 1 <= F <= 7, "one ring per feature (1..7)")
+        _need(all(r.shape == r0.shape and r.stride() == r0.stride() and r.dtype == r0.dtype for r in self.rings),
+              "rings must share shape, strides and dtype")
+        _need(r0.dim() == 2 and r0.stride(1) == 1 and r0.dtype in (torch.bfloat16, torch.float32), "ring layout")
+        N, R = r0.shape
+        _need(self.mean is not None and self.mean.shape == (N, F) and self.mean.dtype == torch.float32
+              and self.mean.is_contiguous(), "mean must be float32 [N, F]")
+        _need(self.rstd is not None and self.rstd.shape == (N, F) and self.rstd.dtype == torch.float32
+              and self.rstd.is_contiguous(), "rstd must be float32 [N, F]")
+        if self.win_series is not None:
+            _need(self.win_series.shape == (n_windows,) and self.win_series.dtype == torch.int32, "win_series")
+            _need(self.win_start is not None and self.win_start.shape == (n_windows,)
+                  and self.win_start.dtype == torch.int32, "win_start")
+        else:
+            _need(n_windows == N, "without win_series every ring row is one window")
+        for f, r in enumerate(self.rings):
+            src.ring[f] = r.data_ptr()
+        src.ld, src.ring_len, src.bf16 = r0.stride(0), R, int(r0.dtype == torch.bfloat16)
+        src.start_col = int(self.start_col) % R
+        src.win_series = nat.ptr(self.win_series)
+        src.win_start = nat.ptr(self.win_start)
+        src.mean, src.rstd = self.mean.data_ptr(), self.rstd.data_ptr()
+
+
 class LstmArgs(C.Structure):
     _fields_ = [
         ("x", C.c_void_p), ("N", C.c_int), ("T", C.c_int), ("F", C.c_int), ("fp8", C.c_int),
@@ -25,7 +69,7 @@ class LstmArgs(C.Structure):
         ("scale_w_enc", C.c_float), ("scale_w_dec", C.c_float), ("scale_act", C.c_float),
         ("mu", C.c_float), ("sigma", C.c_float), ("threshold", C.c_void_p), ("thr_default", C.c_float),
         ("err", C.c_void_p), ("zscore", C.c_void_p), ("verdict", C.c_void_p), ("recon", C.c_void_p),
-        ("app_id", C.c_void_p), ("app_stats", C.c_void_p),
+        ("app_id", C.c_void_p), ("app_stats", C.c_void_p), ("wmax", C.c_void_p), ("src", LstmRingSrc),
     ]
 
 
@@ -101,9 +145,57 @@ def _augment_dev(w_hh, b, w_ih, F) -> torch.Tensor:
     return A
 
 
+# parameter order of the pack sources (csrc/pack.hip codes refer to these ids)
+LSTM_SRCS = ("enc_w_hh", "enc_w_ih", "enc_b", "dec_w_hh", "dec_b", "out_w", "out_b")
+
+
+def model_srcs(model) -> List[torch.Tensor]:
+    return [getattr(model, n).data for n in LSTM_SRCS]
+
+
+def augmented_codes(F: int, enc: bool) -> torch.Tensor:
+    """Pack codes of the A-fragment layout of ``[W_hh | W_ih | b]`` (the
+    ``_augment`` + ``pack_fragments`` reference, as a table)."""
+    from .pack import make_codes
+    idx = _frag_index("cpu")
+    r, k = idx // KAUG, idx % KAUG
+    is_h, is_b = k < H, k == BIAS_K
+    is_x = (k >= H) & (k < H + F) & torch.tensor(enc)
+    src = torch.where(is_h, LSTM_SRCS.index("enc_w_hh" if enc else "dec_w_hh"),
+                      torch.where(is_b, LSTM_SRCS.index("enc_b" if enc else "dec_b"), LSTM_SRCS.index("enc_w_ih")))
+    off = torch.where(is_h, r * H + k, torch.where(is_b, r, r * F + (k - H)))
+    return make_codes(src, off.clamp(min=0), valid=is_h | is_b | is_x)
+
+
+def identity_codes(name: str, n: int) -> torch.Tensor:
+    from .pack import make_codes
+    return make_codes(torch.full((n,), LSTM_SRCS.index(name)), torch.arange(n))
+
+
+def scoring_packer(p: "LstmPacked", model):
+    """Native packer refreshing ``p`` from ``model`` (one launch; two for fp8)."""
+    from .pack import KIND_BF16, KIND_F32, KIND_FP8, Packer
+    F = model.F
+    kind = KIND_FP8 if p.fp8 else KIND_BF16
+    pk = Packer(model_srcs(model))
+    pk.add(augmented_codes(F, True), p.w_enc.view(-1), kind)
+    pk.add(augmented_codes(F, False), p.w_dec.view(-1), kind)
+    pk.add(identity_codes("out_w", F * H), p.w_out.view(-1), KIND_F32)
+    pk.add(identity_codes("out_b", F), p.b_out.view(-1), KIND_F32)
+    return pk
+
+
 def repack_into(p: "LstmPacked", model) -> "LstmPacked":
-    """Refresh ``p`` in place from (device) model parameters: one gather per
-    matrix, no host round trip except the fp8 scale."""
+    """Refresh ``p`` in place from (device) model parameters.  With the native
+    library: one table-driven pack launch (fp8 scales stay on the device,
+    ``p.wmax``); otherwise one torch gather per matrix."""
+    if p.w_enc.is_cuda and nat.available():
+        if p.packer is None or p.packer_model is not model:
+            p.packer, p.packer_model = scoring_packer(p, model), model
+        p.packer.run()
+        if p.fp8:
+            p.wmax = p.packer.absmax
+        return p
     F = model.F
     idx = _frag_index(p.w_enc.device)
     Ae = _augment_dev(model.enc_w_hh, model.enc_b, model.enc_w_ih, F).flatten()[idx]
@@ -133,6 +225,9 @@ class LstmPacked:
     scale_w_enc: float = 1.0
     scale_w_dec: float = 1.0
     scale_act: float = 1.0
+    wmax: Optional[torch.Tensor] = None  # device absmax [enc, dec] of the fp8 weights (overrides scale_w_*)
+    packer: Optional[object] = None
+    packer_model: Optional[object] = None
 
 
 def pack(model, fp8: bool = False, device="cuda", act_scale: float = 1.0 / 32) -> LstmPacked:
@@ -158,16 +253,24 @@ def pack(model, fp8: bool = False, device="cuda", act_scale: float = 1.0 / 32) -
                       b_out=model.out_b.detach().float().contiguous().to(device))
 
 
-def lstm_score(p: LstmPacked, x: torch.Tensor, mu: float = 0.0, sigma: float = 1.0,
+def lstm_score(p: LstmPacked, x: Optional[torch.Tensor], mu: float = 0.0, sigma: float = 1.0,
                threshold: Optional[torch.Tensor] = None, thr_default: float = 3.0, want_recon: bool = False,
                app_id: Optional[torch.Tensor] = None, app_stats: Optional[torch.Tensor] = None,
-               out: Optional[Dict[str, torch.Tensor]] = None) -> Dict[str, torch.Tensor]:
+               out: Optional[Dict[str, torch.Tensor]] = None, ring: Optional[RingSource] = None,
+               T: Optional[int] = None) -> Dict[str, torch.Tensor]:
+    """Score windows ``x [N, T, F]`` — or, with ``ring`` (and ``T``), the last
+    ``T`` samples of every ring row read directly by the kernel."""
     lib = nat.require()
-    _need(x.is_cuda and x.dtype == torch.float32 and x.dim() == 3 and x.is_contiguous(),
-          "x must be a contiguous float32 [N, T, F] GPU tensor")
-    N, T, F = x.shape
+    if ring is None:
+        _need(x is not None and x.is_cuda and x.dtype == torch.float32 and x.dim() == 3 and x.is_contiguous(),
+              "x must be a contiguous float32 [N, T, F] GPU tensor")
+        N, T, F = x.shape
+        dev = x.device
+    else:
+        _need(T is not None and T >= 1, "ring scoring needs the window length T")
+        N, F = ring.rings[0].shape[0], len(ring.rings)
+        dev = ring.rings[0].device
     _need(F == p.F, f"feature mismatch {F} vs {p.F}")
-    dev = x.device
     if threshold is not None:
         _need(threshold.shape == (N,) and threshold.dtype == torch.float32 and threshold.is_contiguous()
               and threshold.device == dev, "threshold must be float32 [N]")
@@ -181,7 +284,9 @@ def lstm_score(p: LstmPacked, x: torch.Tensor, mu: float = 0.0, sigma: float = 1
     if want_recon:
         out.setdefault("recon", torch.empty((N, T, F), dtype=torch.float32, device=dev))
     a = LstmArgs()
-    a.x = x.data_ptr()
+    a.x = 0 if x is None else x.data_ptr()
+    if ring is not None:
+        ring.fill(a.src, N, F)
     a.N, a.T, a.F, a.fp8 = N, T, F, int(p.fp8)
     a.w_enc, a.w_dec = p.w_enc.data_ptr(), p.w_dec.data_ptr()
     a.w_out, a.b_out = p.w_out.data_ptr(), p.b_out.data_ptr()
@@ -192,6 +297,7 @@ def lstm_score(p: LstmPacked, x: torch.Tensor, mu: float = 0.0, sigma: float = 1
     a.err, a.zscore, a.verdict = nat.ptr(out["err"]), nat.ptr(out["zscore"]), nat.ptr(out["verdict"])
     a.recon = nat.ptr(out.get("recon")) if want_recon else 0
     a.app_id, a.app_stats = nat.ptr(app_id), nat.ptr(app_stats)
+    a.wmax = nat.ptr(p.wmax) if p.fp8 else 0
     nat.check(lib.fm_lstm_ae(C.byref(a), nat.stream_handle(dev)), "fm_lstm_ae")
     return out
 

@@ -19,7 +19,7 @@ import torch
 
 from . import _native as nat
 from .kernels import KernelShapeError, _need
-from .lstm import BIAS_K, H, KAUG, _augment_dev, _frag_index
+from .lstm import BIAS_K, H, KAUG, LstmRingSrc, RingSource, _augment_dev, _frag_index
 
 
 class LstmTrainArgs(C.Structure):
@@ -29,6 +29,7 @@ class LstmTrainArgs(C.Structure):
         ("w_out", C.c_void_p), ("b_out", C.c_void_p), ("scratch", C.c_void_p),
         ("g_enc", C.c_void_p), ("g_dec", C.c_void_p), ("h_enc", C.c_void_p), ("h_dec", C.c_void_p),
         ("dy", C.c_void_p), ("err", C.c_void_p), ("loss_scale", C.c_float), ("variant", C.c_int),
+        ("src", LstmRingSrc),
     ]
 
 
@@ -128,7 +129,54 @@ class FusedLstmGrad:
         self.wt_enc = torch.empty(2 * 16 * 64 * 8, dtype=torch.bfloat16, device=dev)
         self.wt_dec = torch.empty_like(self.wt_enc)
 
+    def _packer_for(self, model):
+        """Native packer: forward fragments of both phases + W_hhᵀ backward
+        fragments, one launch per step."""
+        from .lstm import LSTM_SRCS, augmented_codes, model_srcs
+        from .pack import KIND_BF16, Packer, make_codes
+        if getattr(self, "_pk_model", None) is not model:
+            tidx = _t_index("cpu")
+            pk = Packer(model_srcs(model))
+            pk.add(augmented_codes(self.F, True), self.w_enc, KIND_BF16)
+            pk.add(augmented_codes(self.F, False), self.w_dec, KIND_BF16)
+            pk.add(make_codes(torch.full_like(tidx, LSTM_SRCS.index("enc_w_hh")), tidx), self.wt_enc, KIND_BF16)
+            pk.add(make_codes(torch.full_like(tidx, LSTM_SRCS.index("dec_w_hh")), tidx), self.wt_dec, KIND_BF16)
+            self._pk, self._pk_model = pk, model
+        return self._pk
+
+    def _scatter_grads(self, model, dwe, dwd, dwo) -> None:
+        """GEMM results → ``p.grad`` (views of the DP buckets) in one pack
+        launch; the read-out bias gradient is a row sum written in place."""
+        from .pack import KIND_F32, Packer, make_codes
+        for p in model.parameters():
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        key = (model, tuple(p.grad.data_ptr() for p in model.parameters()))
+        if getattr(self, "_gs_key", None) != key:
+            F = self.F
+            r = torch.arange(4 * H)
+            k = torch.arange(H)
+            pk = Packer([dwe, dwd, dwo])
+            z = lambda n, v: torch.full((n,), v)  # noqa: E731
+            pk.add(make_codes(z(4 * H * H, 0), (r[:, None] * KAUG + k[None]).flatten()), model.enc_w_hh.grad.view(-1),
+                   KIND_F32)
+            pk.add(make_codes(z(4 * H * F, 0), (r[:, None] * KAUG + H + torch.arange(F)[None]).flatten()),
+                   model.enc_w_ih.grad.view(-1), KIND_F32)
+            pk.add(make_codes(z(4 * H, 0), r * KAUG + BIAS_K), model.enc_b.grad.view(-1), KIND_F32)
+            pk.add(make_codes(z(4 * H * H, 1), (r[:, None] * KAUG + k[None]).flatten()), model.dec_w_hh.grad.view(-1),
+                   KIND_F32)
+            pk.add(make_codes(z(4 * H, 1), r * KAUG + BIAS_K), model.dec_b.grad.view(-1), KIND_F32)
+            pk.add(make_codes(z(F * H, 2), torch.arange(F * H)), model.out_w.grad.view(-1), KIND_F32)
+            self._gs, self._gs_key = pk, key
+        for i, t in enumerate((dwe, dwd, dwo)):
+            self._gs.set_src(i, t.contiguous())
+        self._gs.run()
+        torch.sum(self.dy, 1, out=model.out_b.grad)
+
     def _pack(self, model) -> None:
+        if nat.available():
+            self._packer_for(model).run()
+            return
         F = self.F
         idx = _frag_index(self.device)
         self.w_enc.copy_(_augment_dev(model.enc_w_hh, model.enc_b, model.enc_w_ih, F).flatten()[idx])
@@ -140,17 +188,24 @@ class FusedLstmGrad:
     phases = 0  # profiling only: restrict the kernel to a subset of its four phases
     batched_gemm = True  # weight-grad reduction as a strided-batched GEMM over time slices
 
-    def launch(self, model, x: torch.Tensor) -> torch.Tensor:
-        """Run the fused forward+backward; returns per-window errors ``[B]``."""
+    def launch(self, model, x: Optional[torch.Tensor], ring: Optional[RingSource] = None) -> torch.Tensor:
+        """Run the fused forward+backward; returns per-window errors ``[B]``.
+        ``x [B, T, F]`` windows, or ``ring`` (windows sampled by
+        ``win_series``/``win_start``, read straight from the history rings)."""
         lib = nat.require()
-        _need(x.is_cuda and x.dtype == torch.float32 and x.is_contiguous()
-              and tuple(x.shape) == (self.B, self.T, self.F), "x must be contiguous float32 [B, T, F]")
+        if ring is None:
+            _need(x is not None and x.is_cuda and x.dtype == torch.float32 and x.is_contiguous()
+                  and tuple(x.shape) == (self.B, self.T, self.F), "x must be contiguous float32 [B, T, F]")
+        else:
+            _need(ring.win_series is not None, "ring training needs sampled windows (win_series/win_start)")
         _need(model.H == H and model.F == self.F, "model shape mismatch")
         self._pack(model)
         w_out = model.out_w.detach().contiguous()
         b_out = model.out_b.detach().contiguous()
         a = LstmTrainArgs()
-        a.x = x.data_ptr()
+        a.x = 0 if x is None else x.data_ptr()
+        if ring is not None:
+            ring.fill(a.src, self.B, self.F)
         a.B, a.T, a.F = self.B, self.T, self.F
         a.phases = int(self.phases)
         a.w_enc, a.w_dec = self.w_enc.data_ptr(), self.w_dec.data_ptr()
@@ -165,9 +220,20 @@ class FusedLstmGrad:
         nat.check(lib.fm_lstm_ae_train(C.byref(a), nat.stream_handle(self.device)), "fm_lstm_ae_train")
         return self.err
 
-    def grads(self, model, x: torch.Tensor) -> torch.Tensor:
-        """Fill ``p.grad`` of every model parameter (overwrite); returns the loss."""
-        err = self.launch(model, x)
+    def grads(self, model, x: Optional[torch.Tensor], ring: Optional[RingSource] = None) -> torch.Tensor:
+        """Fill ``p.grad`` of every model parameter (overwrite); returns the loss.
+        ``x`` may itself be a :class:`RingSource` (the DP trainer passes its
+        ``windows`` argument through unchanged)."""
+        if isinstance(x, RingSource):
+            x, ring = None, x
+        self.launch(model, x, ring)
+        return self.finish(model)
+
+    def finish(self, model) -> torch.Tensor:
+        """Second half of :meth:`grads` (after :meth:`launch`): weight-gradient
+        GEMMs + scatter into ``p.grad``.  Split so a caller can enqueue other
+        work (the scoring kernel) between the two halves."""
+        err = self.err
         F, KB, B, T = self.F, self.T * self.B, self.B, self.T
         if self.batched_gemm:
             dwe = _bmm_sum_f32(self.g_enc, self.h_enc.t(), T)           # [256, 80]
@@ -176,6 +242,9 @@ class FusedLstmGrad:
             dwe = _mm_f32(self.g_enc, self.h_enc.t())
             dwd = _mm_f32(self.g_dec, self.h_dec[:, :KB].t())
         dwo = _mm_f32(self.dy.to(torch.bfloat16), self.h_dec[:H, B:].t())  # [F, 64]
+        if nat.available():
+            self._scatter_grads(model, dwe, dwd, dwo)
+            return err.mean()
         grads = {
             "enc_w_hh": dwe[:, :H], "enc_w_ih": dwe[:, H:H + F], "enc_b": dwe[:, BIAS_K],
             "dec_w_hh": dwd[:, :H], "dec_b": dwd[:, BIAS_K],

@@ -1,0 +1,152 @@
+"""Table-driven weight packing for the LSTM kernels (``csrc/pack.hip``).
+
+Every training step changes the LSTM-AE parameters, and both MFMA kernels
+want them in their own fragment orders (scoring: augmented ``[W_hh | W_ih |
+b]`` A fragments in bf16 or fp8; training: the same plus ``W_hhᵀ`` backward
+fragments).  Doing that with torch index/convert ops costs ~15 launches per
+step, each longer on the host than on the GPU.  Here every output element is
+described by one int32 *code* (which parameter, which offset, which
+multiplier class) built once from the reference index maps, and one native
+launch (two for fp8: absmax, then quantise) produces every segment.
+
+:func:`reference_gather` evaluates the same codes with torch (CPU tests and
+the non-GPU path).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import torch
+
+from . import _native as nat
+
+SRC_BITS, CLS_BITS = 26, 24
+KIND_F32, KIND_BF16, KIND_FP8 = 0, 1, 2
+
+
+class PackSeg(C.Structure):
+    _fields_ = [("code", C.c_void_p), ("out", C.c_void_p), ("n", C.c_int), ("kind", C.c_int),
+                ("mul", C.c_float * 4)]
+
+
+class PackArgs(C.Structure):
+    _fields_ = [("src", C.c_void_p * 8), ("seg", PackSeg * 8), ("nseg", C.c_int), ("pass_", C.c_int),
+                ("absmax", C.c_void_p)]
+
+
+nat.register("fm_pack", [C.POINTER(PackArgs), C.c_void_p])
+nat.register("fm_pack_args_size", [], C.c_longlong)
+
+
+def make_codes(src: torch.Tensor, off: torch.Tensor, cls: Optional[torch.Tensor] = None,
+               valid: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Encode (source id, offset, multiplier class) per output element."""
+    off = off.long()
+    if off.numel() and int(off.max()) >= 1 << CLS_BITS:
+        raise ValueError("pack offset exceeds 24 bits")
+    c = (src.long() << SRC_BITS) | off
+    if cls is not None:
+        c = c | (cls.long() << CLS_BITS)
+    if valid is not None:
+        c = torch.where(valid, c, torch.full_like(c, -1))
+    return c.to(torch.int32)
+
+
+def reference_gather(code: torch.Tensor, srcs: Sequence[torch.Tensor], mul=(1.0, 1.0, 1.0, 1.0)) -> torch.Tensor:
+    """fp32 value of every coded element (the kernel before conversion)."""
+    c = code.long().cpu()
+    out = torch.zeros(c.numel(), dtype=torch.float32)
+    ok = c >= 0
+    sid = (c >> SRC_BITS) & 7
+    cls = (c >> CLS_BITS) & 3
+    off = c & ((1 << CLS_BITS) - 1)
+    m = torch.tensor(list(mul), dtype=torch.float32)
+    for s, t in enumerate(srcs):
+        sel = ok & (sid == s)
+        if sel.any():
+            out[sel] = t.detach().float().cpu().flatten()[off[sel]] * m[cls[sel]]
+    return out
+
+
+def fp8_scale(absmax: float) -> float:
+    """Dequantisation scale of an fp8 segment (the kernels use the same rule)."""
+    return absmax / 448.0 if absmax > 0 else 1.0
+
+
+@dataclass
+class _Seg:
+    code: torch.Tensor
+    out: torch.Tensor
+    kind: int
+    mul: tuple = (1.0, 1.0, 1.0, 1.0)
+
+
+@dataclass
+class Packer:
+    """A fixed set of segments over a fixed list of source tensors; the
+    ctypes argument block is built once, so :meth:`run` costs one C call."""
+    srcs: List[torch.Tensor]
+    segs: List[_Seg] = field(default_factory=list)
+    absmax: Optional[torch.Tensor] = None
+    _args: Optional[PackArgs] = None
+
+    def add(self, code: torch.Tensor, out: torch.Tensor, kind: int, mul=(1.0, 1.0, 1.0, 1.0)) -> "Packer":
+        if len(self.segs) == 8:
+            raise ValueError("at most 8 pack segments")
+        if out.numel() != code.numel() or not out.is_contiguous():
+            raise ValueError("pack output must be contiguous with one element per code")
+        want = {KIND_F32: torch.float32, KIND_BF16: torch.bfloat16, KIND_FP8: torch.uint8}[kind]
+        if out.dtype != want:
+            raise ValueError(f"pack kind {kind} writes {want}, got {out.dtype}")
+        self.segs.append(_Seg(code.to(out.device, torch.int32).contiguous(), out, kind, tuple(mul)))
+        self._args = None
+        return self
+
+    def set_src(self, i: int, t: torch.Tensor) -> None:
+        """Re-point source ``i`` (e.g. a freshly allocated GEMM output)."""
+        self.srcs[i] = t
+        if self._args is not None:
+            self._args.src[i] = t.data_ptr()
+
+    def _build(self) -> PackArgs:
+        a = PackArgs()
+        if len(self.srcs) > 8:
+            raise ValueError("at most 8 pack sources")
+        for i, t in enumerate(self.srcs):
+            if t.dtype != torch.float32 or not t.is_contiguous():
+                raise ValueError("pack sources must be contiguous float32")
+            a.src[i] = t.data_ptr()
+        for i, s in enumerate(self.segs):
+            a.seg[i].code, a.seg[i].out = s.code.data_ptr(), s.out.data_ptr()
+            a.seg[i].n, a.seg[i].kind = s.code.numel(), s.kind
+            for j in range(4):
+                a.seg[i].mul[j] = s.mul[j]
+        a.nseg = len(self.segs)
+        if any(s.kind == KIND_FP8 for s in self.segs):
+            if self.absmax is None:
+                self.absmax = torch.zeros(8, dtype=torch.float32, device=self.segs[0].out.device)
+            a.absmax = self.absmax.data_ptr()
+        return a
+
+    def run(self) -> None:
+        if self._args is None:
+            self._args = self._build()
+        nat.check(nat.require().fm_pack(C.byref(self._args), nat.stream_handle(self.segs[0].out.device)), "fm_pack")
+
+    def run_reference(self) -> None:
+        """Same outputs with torch ops (CPU / no native library)."""
+        for i, s in enumerate(self.segs):
+            v = reference_gather(s.code, self.srcs, s.mul).to(s.out.device)
+            if s.kind == KIND_F32:
+                s.out.copy_(v)
+            elif s.kind == KIND_BF16:
+                s.out.copy_(v.to(torch.bfloat16))
+            else:
+                m = float(v.abs().max()) if v.numel() else 0.0
+                if self.absmax is None:
+                    self.absmax = torch.zeros(8, dtype=torch.float32, device=s.out.device)
+                self.absmax[i] = m
+                s.out.copy_((v * (448.0 / m if m > 0 else 1.0)).to(torch.float8_e4m3fn).view(torch.uint8))

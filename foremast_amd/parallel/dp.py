@@ -110,10 +110,13 @@ class DPTrainer:
         self.opt = torch.optim.Adam(model.parameters(), lr=lr, fused=on_gpu or None)
         self.steps = 0
 
-    def step(self, windows: torch.Tensor) -> torch.Tensor:
+    def step(self, windows, grad_fn=None) -> torch.Tensor:
+        """``grad_fn`` overrides the constructor's for this step (e.g. the
+        second half of a split fused-kernel gradient)."""
         self.buckets.zero()
-        if self.grad_fn is not None:
-            loss = self.grad_fn(self.model, windows)
+        grad_fn = grad_fn or self.grad_fn
+        if grad_fn is not None:
+            loss = grad_fn(self.model, windows)
         else:
             loss = self.model.recon_error(windows).mean()
             loss.backward()

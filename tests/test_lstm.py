@@ -265,3 +265,96 @@ def test_fused_lstm_training_grads_match_autograd(F, variant):
         rel = (p.grad - g).norm() / g.norm().clamp(min=1e-12)
         assert cos > 0.99 and rel < 0.08, (name, float(cos), float(rel))
 
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 1])
+def test_fused_training_reads_rings_directly(variant):
+    """K7 with ring-direct input: sampled (series, start) windows read from the
+    bf16 rings (wrapping past column R-1) and z-scored in the kernel give the
+    same errors and gradients as the same windows gathered on the host."""
+    from foremast_amd.ops.lstm import RingSource
+    from foremast_amd.ops.lstm_train import FusedLstmGrad
+    torch.manual_seed(7)
+    dev = torch.device("cuda:0")
+    n, R, F, B, T = 200, 90, 2, 64, 16
+    m = lstm_ae.LSTMAutoencoder(F, 64).to(dev)
+    # row-padded [n, 96] storage viewed as [n, R], like HistoryRing
+    rings = [torch.randn(n, 96, device=dev).mul_(f + 1).add_(f).to(torch.bfloat16)[:, :R] for f in range(F)]
+    mean = torch.randn(n, F, device=dev) * 0.1
+    rstd = 1.0 / (0.5 + torch.rand(n, F, device=dev))
+    si = torch.randint(0, n, (B,), device=dev, dtype=torch.int32)
+    st = torch.randint(0, 3 * R, (B,), device=dev, dtype=torch.int32)  # kernel reduces mod R
+    st[:8] = R - 5  # windows that wrap
+    cols = (st.long()[:, None] + torch.arange(T, device=dev)[None]) % R
+    x = torch.stack([r[si.long()[:, None], cols].float() for r in rings], 2)
+    x = ((x - mean[si.long()][:, None]) * rstd[si.long()][:, None]).contiguous()
+    fg = FusedLstmGrad(B, T, F, dev, variant=variant)
+    loss_d = fg.grads(m, x)
+    err_d = fg.err.clone()
+    g_d = [p.grad.clone() for p in m.parameters()]
+    loss_r = fg.grads(m, RingSource(rings=rings, mean=mean, rstd=rstd, win_series=si, win_start=st))
+    torch.cuda.synchronize()
+    assert torch.allclose(fg.err, err_d, rtol=1e-5, atol=1e-6)
+    assert abs(float(loss_r) - float(loss_d)) <= 1e-5 * abs(float(loss_d))
+    for p, g in zip(m.parameters(), g_d):
+        assert torch.allclose(p.grad, g, rtol=1e-4, atol=1e-6)
+    # scoring the newest window of every row straight from the rings
+    p = L.pack(m, device=dev)
+    start = (R - T + 40) % R  # wraps
+    cols = (start + torch.arange(T, device=dev)) % R
+    xs = torch.stack([r[:, cols].float() for r in rings], 2)
+    xs = ((xs - mean[:, None]) * rstd[:, None]).contiguous()
+    ref = L.lstm_score(p, xs)["err"].clone()
+    got = L.lstm_score(p, None, ring=RingSource(rings=rings, start_col=start, mean=mean, rstd=rstd), T=T)["err"]
+    torch.cuda.synchronize()
+    assert torch.allclose(got, ref, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("F", [1, 3])
+def test_pack_codes_reproduce_reference_layouts(F):
+    """The table-driven packer's codes (evaluated with torch) equal the
+    reference fragment layouts: augmented forward fragments of both phases and
+    the transposed backward fragments."""
+    from foremast_amd.ops import lstm_train as LT
+    from foremast_amd.ops.pack import make_codes, reference_gather
+    torch.manual_seed(3)
+    m = lstm_ae.LSTMAutoencoder(F, 64)
+    srcs = L.model_srcs(m)
+    ref_e = L.pack_fragments(L._augment(m.enc_w_hh, m.enc_b, m.enc_w_ih, F)).flatten()
+    ref_d = L.pack_fragments(L._augment(m.dec_w_hh, m.dec_b, None, F)).flatten()
+    assert torch.equal(reference_gather(L.augmented_codes(F, True), srcs), ref_e)
+    assert torch.equal(reference_gather(L.augmented_codes(F, False), srcs), ref_d)
+    tidx = LT.transposed_frag_index()
+    got = reference_gather(make_codes(torch.full_like(tidx, L.LSTM_SRCS.index("dec_w_hh")), tidx), srcs)
+    assert torch.equal(got, m.dec_w_hh.detach().flatten()[tidx])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fp8", [False, True])
+def test_native_pack_matches_torch_repack(fp8):
+    """One pack launch (two for fp8) gives the same fragments as the torch
+    gather path; fp8 scales come from the device absmax."""
+    from foremast_amd.ops.pack import fp8_scale
+    torch.manual_seed(4)
+    dev = torch.device("cuda:0")
+    m = lstm_ae.LSTMAutoencoder(3, 64).to(dev)
+    ref = L.pack(m.cpu(), fp8=fp8, device=dev)
+    m = m.to(dev)
+    p = L.pack(m, fp8=fp8, device=dev)
+    with torch.no_grad():
+        for q in m.parameters():
+            q.mul_(1.5)
+    ref = L.pack(m, fp8=fp8, device=dev)
+    L.repack_into(p, m)
+    torch.cuda.synchronize()
+    if fp8:
+        se, sd = p.wmax.tolist()[:2]
+        assert fp8_scale(se) == pytest.approx(ref.scale_w_enc, rel=1e-6)
+        assert fp8_scale(sd) == pytest.approx(ref.scale_w_dec, rel=1e-6)
+        a = p.w_enc.view(torch.float8_e4m3fn).float()
+        b = ref.w_enc.view(torch.float8_e4m3fn).float()
+        assert (a != b).float().mean() < 1e-3  # reciprocal vs division rounding at ties
+    else:
+        assert torch.equal(p.w_enc, ref.w_enc) and torch.equal(p.w_dec, ref.w_dec)
+    assert torch.equal(p.w_out, ref.w_out) and torch.equal(p.b_out, ref.b_out)
