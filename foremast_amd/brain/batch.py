@@ -177,7 +177,8 @@ class BatchScorer:
         elif self.gpu:
             from ..ops import kernels as K
             spec = K.DetectSpec(horizons=t_hz, threshold=t_thr, bound=t_bnd, min_lower=t_low, cur=t_cur,
-                                differs=differs, pw_scale=cfg.pairwise_scale, min_valid=cfg.min_historical_points)
+                                differs=differs, pw_scale=cfg.pairwise_scale, min_valid=cfg.min_historical_points,
+                                max_horizon=int(hz.max()) if hz.size and hz.min() >= 1 else None)
             T = t_hist.shape[1]
             if mode is not None:
                 g = sm_ref.make_grid(mode, cfg.hw_alpha, cfg.hw_beta, cfg.hw_gamma).to(dev)

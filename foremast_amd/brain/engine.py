@@ -152,7 +152,7 @@ class StreamingShard:
                             min_lower=self.min_lower, cur=self.cur.data, differs=differs,
                             pw_scale=cfg.pairwise_scale, min_valid=cfg.min_historical_points,
                             want_band=self.spec.want_band, app_id=self.app_id, app_stats=self.app_stats,
-                            anomalies=self.anomalies)
+                            anomalies=self.anomalies, max_horizon=self.cur.W)
         if self.anomalies is not None:
             self.anomalies.reset()
         h = self.hist

@@ -207,9 +207,15 @@ struct PairTab {
 };
 
 __device__ __forceinline__ v2f ldv2(const float* p) { return *(const v2f*)p; }
+// constant address space: wave-uniform table reads become s_load (SGPR operands)
+typedef const __attribute__((address_space(4))) float* cfp;
+__device__ __forceinline__ v2f ldv2(cfp p) { return *(const __attribute__((address_space(4))) v2f*)p; }
 
 struct Mat2 { v2f a, b, c, d; };
 __device__ __forceinline__ Mat2 ldmat(const float* p) {
+  Mat2 m; m.a = ldv2(p); m.b = ldv2(p + 2); m.c = ldv2(p + 4); m.d = ldv2(p + 6); return m;
+}
+__device__ __forceinline__ Mat2 ldmat(cfp p) {
   Mat2 m; m.a = ldv2(p); m.b = ldv2(p + 2); m.c = ldv2(p + 4); m.d = ldv2(p + 6); return m;
 }
 __device__ __forceinline__ void matvec(const Mat2& m, v2f x1, v2f x2, v2f& y1, v2f& y2) {
@@ -286,7 +292,421 @@ __device__ __forceinline__ void pass2_tab(const Y& y, const Y& yn, v2f* s, v2f c
   }
 }
 
+// ---- variant 4 helpers: one series per 32-lane half-wave -----------------------------
+
+// bf16 values streamed from LDS 8 at a time (one ds_read_b128 per chunk), the next
+// chunk in flight while this one is consumed; the empty asm keeps the compiler from
+// hoisting every chunk (and its unpacked floats) to the top of the season.
+struct Chunk8 {
+  uint4 w;
+  __device__ __forceinline__ float get(int i) const {
+    const unsigned x = (i >> 1) == 0 ? w.x : (i >> 1) == 1 ? w.y : (i >> 1) == 2 ? w.z : w.w;
+    return __uint_as_float((i & 1) ? (x & 0xffff0000u) : (x << 16));
+  }
+};
+__device__ __forceinline__ void fence_sched() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);  // nor may the machine scheduler move ALU work across
+}
+// the pair table as a constant-address-space pointer (uniform: scalar loads)
+__device__ __forceinline__ cfp const_ptr(const float* p) {
+  return (cfp)(__builtin_amdgcn_readfirstlane((int)((unsigned long long)p)) & 0xffffffffull |
+               ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned long long)p >> 32)) << 32));
+}
+
+// fused: pass 2 of this season (true start state x) + table pass 1 of the next one.
+template <int K, bool MASK, bool FUSE>
+__device__ __forceinline__ void pass2_stream(const bf16_t* yc, const bf16_t* yn, v2f* s, v2f c1, v2f c2, v2f g1a,
+                                             cfp W, v2f& x1, v2f& x2, v2f& sse, v2f& p1, v2f& p2) {
+  constexpr int NCH = (K + 7) / 8;
+  const uint4* pc = (const uint4*)yc;
+  const uint4* pn = (const uint4*)yn;
+  if (FUSE) { p1 = splat2(0.f); p2 = splat2(0.f); }
+  fence_sched();  // the variants share loads: keep them from being merged above the branch
+  // y chunks (LDS) and pass-1 weights (scalar loads, 8 steps = 16 SGPR pairs) are
+  // fetched one chunk ahead, so no wait on lgkmcnt lands right after its load
+  Chunk8 cc, cn, nc, nn;
+  v2f wc[16], wn[16];
+  cn.w = pc[0];
+  if (FUSE) {
+    nn.w = pn[0];
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if (r < 2 * K) wn[r] = ldv2(W + 2 * r);
+  }
+#pragma unroll
+  for (int q = 0; q < NCH; ++q) {
+    cc = cn;
+    if (FUSE) {
+      nc = nn;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) wc[r] = wn[r];
+      // wait for this chunk's operands BEFORE the next chunk's loads are issued
+      // (scalar loads complete out of order: any use waits for lgkmcnt(0))
+      asm volatile("" ::"v"(cc.w.x), "v"(nc.w.x), "s"(wc[0].x));
+    }
+    if (q + 1 < NCH) {
+      cn.w = pc[q + 1];
+      if (FUSE) {
+        nn.w = pn[q + 1];
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (16 * (q + 1) + r < 2 * K) wn[r] = ldv2(W + 32 * (q + 1) + 2 * r);
+      }
+    }
+    fence_sched();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int i = 8 * q + r;
+      if (i < K) {
+        const v2f t = x1 + x2;
+        const float yi = cc.get(r);
+        v2f e = (splat2(yi) - s[i]) - x1;
+        if (MASK) e = (yi == yi) ? e : splat2(0.f);
+        x1 = t + c1 * e;
+        x2 = x2 + c2 * e;
+        s[i] = s[i] + g1a * e;
+        sse = sse + e * e;
+        if (FUSE) {
+          const v2f un = splat2(nc.get(r)) - s[i];
+          p1 = p1 + wc[2 * r] * un;
+          p2 = p2 + wc[2 * r + 1] * un;
+        }
+      }
+    }
+    fence_sched();
+  }
+}
+
+// table pass 1 (NaN-free season): v = sum_i W_i (y_i - s_i)
+template <int K>
+__device__ __forceinline__ void pass1_stream(const bf16_t* yc, const v2f* s, cfp W, v2f& p1, v2f& p2) {
+  constexpr int NCH = (K + 7) / 8;
+  const uint4* pc = (const uint4*)yc;
+  p1 = splat2(0.f);
+  p2 = splat2(0.f);
+  fence_sched();
+#pragma unroll
+  for (int q = 0; q < NCH; ++q) {
+    Chunk8 c;
+    c.w = pc[q];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int i = 8 * q + r;
+      if (i < K) {
+        const v2f un = splat2(c.get(r)) - s[i];
+        p1 = p1 + ldv2(W + 4 * i) * un;
+        p2 = p2 + ldv2(W + 4 * i + 2) * un;
+      }
+    }
+    fence_sched();
+  }
+}
+
+// value of lane 31 (half 0) / lane 63 (half 1): the end state of the half's season
+__device__ __forceinline__ v2f half_last(v2f x, int half) {
+  const v2f lo = rdlanev(x, 31), hi = rdlanev(x, 63);
+  return half ? hi : lo;
+}
+
+// Exclusive scan X_j = B X_{j-1} + v_j over the 32 lanes of each half (X_{-1} = x0
+// of that half); Bj = B^(lane & 15).  Four in-row DPP rounds, then rows 1 / 3 take
+// the row-0 / row-2 end state through row_bcast:15 — the halves never mix.
+__device__ __forceinline__ void half_uniform_scan(cfp tab_b, v2f v1, v2f v2, v2f x01, v2f x02,
+                                                  const Mat2& Bj, bool odd_row, v2f& s1, v2f& s2) {
+  const Mat2 B1 = ldmat(tab_b), B2 = ldmat(tab_b + 8), B4 = ldmat(tab_b + 16), B8 = ldmat(tab_b + 24),
+             B16 = ldmat(tab_b + 32);
+  v2f w1 = dpp2<0x111, 0xf>(0.f, v1);
+  v2f w2 = dpp2<0x111, 0xf>(0.f, v2);
+  row_round<0x111>(w1, w2, B1);
+  row_round<0x112>(w1, w2, B2);
+  row_round<0x114>(w1, w2, B4);
+  row_round<0x118>(w1, w2, B8);
+  v2f e1, e2;  // end state of each lane from zero; lanes 15 / 47 close rows 0 / 2
+  matvec(B1, w1, w2, e1, e2);
+  e1 = e1 + v1;
+  e2 = e2 + v2;
+  const v2f E1 = dpp2<0x142, 0xa>(0.f, e1), E2 = dpp2<0x142, 0xa>(0.f, e2);
+  v2f y1, y2;
+  matvec(B16, x01, x02, y1, y2);
+  y1 = odd_row ? y1 + E1 : x01;
+  y2 = odd_row ? y2 + E2 : x02;
+  matvec(Bj, y1, y2, s1, s2);
+  s1 = s1 + w1;
+  s2 = s2 + w2;
+}
+
+// General (per-lane matrix) exclusive affine scan within each 32-lane half.
+template <typename V>
+__device__ __forceinline__ void half_exclusive_scan(Aff<V>& a, int j) {
+  scan_round<0x111, 0xf>(a);  // row_shr:1
+  scan_round<0x112, 0xf>(a);  // row_shr:2
+  scan_round<0x114, 0xf>(a);  // row_shr:4
+  scan_round<0x118, 0xf>(a);  // row_shr:8
+  scan_round<0x142, 0xa>(a);  // row_bcast:15 → rows 1, 3
+  a.m11 = dppv<0x138, 0xf>(1.f, a.m11);  // wave_shr:1 (lane 32 is fixed below)
+  a.m12 = dppv<0x138, 0xf>(0.f, a.m12);
+  a.m21 = dppv<0x138, 0xf>(0.f, a.m21);
+  a.m22 = dppv<0x138, 0xf>(1.f, a.m22);
+  a.v1 = dppv<0x138, 0xf>(0.f, a.v1);
+  a.v2 = dppv<0x138, 0xf>(0.f, a.v2);
+  if (j == 0) {
+    const V one = splatv<V>(1.f), zero = splatv<V>(0.f);
+    a.m11 = one; a.m12 = zero; a.m21 = zero; a.m22 = one; a.v1 = zero; a.v2 = zero;
+  }
+}
+
 }  // namespace
+
+// ---- variant 4: two series per wave ----------------------------------------------------
+// For a season m = 32 K (daily 1440 = 32 x 45) each 32-lane half of a wave walks one
+// series: lane j owns phases [jK, (j+1)K).  Against variant 3 (one series per wave,
+// 60 lanes x 24 steps) the per-season scan is four in-row DPP rounds + one row_bcast
+// and is amortised over 45 steps instead of 24: ~12 VALU ops per step for two grid
+// points instead of ~17.5.  A workgroup (4 waves, 2 per SIMD) owns two series staged
+// once in LDS; every wave fits a quarter of the grid pairs for both.  Only the first
+// HALF_HB best seasonal phases are kept (enough for forecast horizons 1..hmax <= K), so
+// this variant does not produce season_out (the host falls back to variant 3 then).
+constexpr int HALF_HB = 64;
+
+template <int K>
+__global__ __launch_bounds__(256, 2) void hw_half_kernel(const SmoothArgs a, int hmax) {
+  using YR = YRegs<bf16_t, K>;
+  constexpr int KP = YR::KP;
+  constexpr int TS = PairTab<K>::SIZE;
+  const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+  const int half = lane >> 5, j = lane & 31;
+  const bool odd_row = ((lane >> 4) & 1) != 0;
+  const int nseg = a.Tp / a.seg, m = a.m;
+  const int n0 = blockIdx.x * 2;
+
+  // ---- LDS: ys[2][nseg][32][KP] | segnan[2][nseg] + nvs[2] | bests[4][2][HB] | wbest[4][2][4]
+  bf16_t* ys = (bf16_t*)fm_hw_smem;
+  size_t off = ((size_t)2 * nseg * 32 * KP * sizeof(bf16_t) + 15) & ~(size_t)15;
+  int* segnan = (int*)(fm_hw_smem + off);
+  float* nvs = (float*)(segnan + 2 * nseg);
+  off += ((size_t)(2 * nseg + 2) * 4 + 15) & ~(size_t)15;
+  float* bests = (float*)(fm_hw_smem + off);
+  off += (size_t)4 * 2 * HALF_HB * 4;
+  float* wbest = (float*)(fm_hw_smem + off);
+
+  for (int i = tid; i < 2 * nseg + 2; i += blockDim.x) segnan[i] = 0;  // also nvs = 0.f
+  __syncthreads();
+
+  // ---- stage both series: logical padded index p = pk*K + i, pk = sg*32 + lane -------
+  for (int r = 0; r < 2; ++r) {
+    const int n = n0 + r;
+    const bool real = n < a.N;
+    const bf16_t* row = (const bf16_t*)a.hist + (long long)(real ? n : 0) * a.ld;
+    float nv = 0.f;
+    for (int p = tid; p < a.Tp; p += blockDim.x) {
+      bf16_t v = 0;  // the padding series of an odd N is zeros (keeps the wave on the fast path)
+      if (real) {
+        v = 0x7fc0;
+        const int t = p - a.pad;
+        if (t >= 0) {
+          int c = a.head + t;
+          if (c >= a.ring_len) c -= a.ring_len;
+          v = row[c];
+        }
+      }
+      const int pk = p / K, i = p - pk * K;
+      ys[((size_t)r * nseg * 32 + pk) * KP + i] = v;
+      const float f = bf16_to_f32(v);
+      if (f != f) atomicOr(&segnan[r * nseg + (pk >> 5)], 1);
+      else if (p >= m) nv += 1.f;
+    }
+    nv = wave_sum(nv);
+    if (lane == 0) atomicAdd(&nvs[r], nv);
+  }
+  __syncthreads();
+
+  const bf16_t* myys = ys + ((size_t)half * nseg * 32 + j) * KP;
+  auto yseg = [&](int sg) { return myys + (size_t)sg * 32 * KP; };
+  auto seg_nan = [&](int sg) { return (segnan[sg] | segnan[nseg + sg]) != 0; };
+
+  // ---- initial state of my half's series (season means) ------------------------------
+  float l0, b0;
+  {
+    YR y0, y1;
+    y0.load(yseg(0));
+    y1.load(yseg(1));
+    float s0 = 0.f, q0 = 0.f, s1 = 0.f, q1 = 0.f;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      const float u = y0.get(i), v = y1.get(i);
+      if (u == u) { s0 += u; q0 += 1.f; }
+      if (v == v) { s1 += v; q1 += 1.f; }
+    }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+      s0 += __shfl_xor(s0, o, FM_WAVE);
+      q0 += __shfl_xor(q0, o, FM_WAVE);
+      s1 += __shfl_xor(s1, o, FM_WAVE);
+      q1 += __shfl_xor(q1, o, FM_WAVE);
+    }
+    l0 = q0 > 0.f ? s0 / q0 : 0.f;
+    b0 = ((q1 > 0.f ? s1 / q1 : 0.f) - l0) / (float)m;
+  }
+
+  float bestSSE = __builtin_huge_valf();
+  int bestIdx = 0x7fffffff;
+  float bestL = l0, bestB = b0;
+  float* mybest = bests + (w * 2 + half) * HALF_HB;
+  const int npairs = (a.G + 1) / 2;
+  const int nwaves = blockDim.x / FM_WAVE;
+
+  for (int pi = w; pi < npairs; pi += nwaves) {
+    const int c0 = 2 * pi;
+    const int c1i = (2 * pi + 1 < a.G) ? 2 * pi + 1 : c0;
+    const cfp tab = const_ptr(a.pair_tab + (size_t)pi * TS);
+    const v2f c1 = ldv2(tab), c2 = ldv2(tab + 2), g1a = ldv2(tab + 4);
+    const cfp W = tab + PairTab<K>::W0;
+    const cfp tb = tab + PairTab<K>::B0;
+    const v2f one = splat2(1.f), zero = splat2(0.f);
+    Mat2 Bj;  // B^(lane & 15)
+    Bj.a = one; Bj.b = zero; Bj.c = zero; Bj.d = one;
+#pragma unroll
+    for (int bit = 0; bit < 4; ++bit) {
+      const Mat2 Bb = ldmat(tb + 8 * bit);
+      const Mat2 r = matmul(Bj, Bb);
+      if ((lane >> bit) & 1) Bj = r;
+    }
+
+    v2f s[K];
+    {
+      YR y0;
+      y0.load(yseg(0));
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        const float y = y0.get(i);
+        s[i] = splat2(y == y ? y - l0 : 0.f);
+      }
+    }
+    v2f X1 = splat2(l0 + b0), X2 = splat2(b0), sse = zero;  // (f, b) at the season start
+
+    Aff<v2f> loc;
+    bool locfast = !seg_nan(1);
+    if (locfast) {
+      pass1_stream<K>(yseg(1), s, W, loc.v1, loc.v2);
+    } else {
+      YR y1;
+      y1.load(yseg(1));
+      pass1_slow<K>(y1, s, c1, c2, loc);
+    }
+
+    for (int sg = 1; sg < nseg; ++sg) {
+      v2f x1, x2;
+      if (locfast) {
+        half_uniform_scan(tb, loc.v1, loc.v2, X1, X2, Bj, odd_row, x1, x2);
+      } else {
+        half_exclusive_scan(loc, j);
+        x1 = loc.m11 * X1 + loc.m12 * X2 + loc.v1;
+        x2 = loc.m21 * X1 + loc.m22 * X2 + loc.v2;
+      }
+      const bool has_next = sg + 1 < nseg;
+      const bool mask = seg_nan(sg);
+      const bool next_fast = has_next && !seg_nan(sg + 1);
+      const bf16_t* yc = yseg(sg);
+      const bf16_t* yn = yseg(has_next ? sg + 1 : sg);
+      if (next_fast) {
+        if (mask) pass2_stream<K, true, true>(yc, yn, s, c1, c2, g1a, W, x1, x2, sse, loc.v1, loc.v2);
+        else pass2_stream<K, false, true>(yc, yn, s, c1, c2, g1a, W, x1, x2, sse, loc.v1, loc.v2);
+        locfast = true;
+      } else {
+        v2f d1, d2;
+        if (mask) pass2_stream<K, true, false>(yc, yn, s, c1, c2, g1a, W, x1, x2, sse, d1, d2);
+        else pass2_stream<K, false, false>(yc, yn, s, c1, c2, g1a, W, x1, x2, sse, d1, d2);
+        if (has_next) {
+          YR y1;
+          y1.load(yn);
+          pass1_slow<K>(y1, s, c1, c2, loc);
+        }
+        locfast = false;
+      }
+      X1 = half_last(x1, half);
+      X2 = half_last(x2, half);
+    }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+      sse.x += __shfl_xor(sse.x, o, FM_WAVE);
+      sse.y += __shfl_xor(sse.y, o, FM_WAVE);
+    }
+    const bool upd0 = (sse.x < bestSSE || (sse.x == bestSSE && c0 < bestIdx));
+    if (upd0) { bestSSE = sse.x; bestIdx = c0; bestL = X1.x - X2.x; bestB = X2.x; }
+    const bool upd1 = (c1i != c0) && (sse.y < bestSSE || (sse.y == bestSSE && c1i < bestIdx));
+    if (upd1) { bestSSE = sse.y; bestIdx = c1i; bestL = X1.y - X2.y; bestB = X2.y; }
+    if (j == 0 && (upd0 || upd1)) {
+#pragma unroll
+      for (int i = 0; i < K && i < HALF_HB; ++i)
+        if (i < hmax) mybest[i] = upd1 ? s[i].y : s[i].x;
+    }
+  }
+
+  // ---- arg-min across the 4 waves; wave r finishes series n0 + r ----------------------
+  if (j == 0) {
+    float* wb = wbest + (w * 2 + half) * 4;
+    wb[0] = bestSSE;
+    wb[1] = __int_as_float(bestIdx);
+    wb[2] = bestL;
+    wb[3] = bestB;
+  }
+  __syncthreads();
+  if (w >= 2) return;
+  const int r = w, n = n0 + r;
+  if (n >= a.N) return;
+  const int nw = blockDim.x / FM_WAVE;
+  int win = 0;
+  for (int q = 1; q < nw; ++q) {
+    const float sq = wbest[(q * 2 + r) * 4], sw = wbest[(win * 2 + r) * 4];
+    const int iq = __float_as_int(wbest[(q * 2 + r) * 4 + 1]), iw = __float_as_int(wbest[(win * 2 + r) * 4 + 1]);
+    if (sq < sw || (sq == sw && iq < iw)) win = q;
+  }
+  const float* wb = wbest + (win * 2 + r) * 4;
+  const float gSSE = wb[0], gL = wb[2], gB = wb[3];
+  const int gIdx = __float_as_int(wb[1]);
+  const float nvr = nvs[r];
+  const float sig = sqrtf(gSSE / fmaxf(nvr, 1.f));
+  if (lane == 0) {
+    a.level[n] = gL;
+    a.trend[n] = gB;
+    a.sigma[n] = sig;
+    a.best[n] = gIdx;
+  }
+  const float* sb = bests + (win * 2 + r) * HALF_HB;
+  const int Tp = a.Tp;
+  detect_epilogue_wave(a.det, n, sig, nvr, [&](int h) {
+    int ph = (Tp - 1 + h) % m;
+    if (ph < 0) ph += m;
+    ph = ph < HALF_HB ? ph : HALF_HB - 1;  // host guarantees ph < hmax; clamp keeps LDS reads in bounds
+    return gL + (float)h * gB + sb[ph];
+  });
+}
+
+extern "C" size_t fm_hw_half_lds_bytes(int Tp, int seg, int K) {
+  if (K != 45) return (size_t)-1;
+  constexpr int KP = 48;
+  const int nseg = Tp / seg;
+  size_t off = ((size_t)2 * nseg * 32 * KP * 2 + 15) & ~(size_t)15;
+  off += ((size_t)(2 * nseg + 2) * 4 + 15) & ~(size_t)15;
+  off += (size_t)4 * 2 * HALF_HB * 4;
+  off += (size_t)4 * 2 * 4 * 4;
+  return off;
+}
+
+// Variant 4 launcher: Holt-Winters, bf16 ring, season = seg = 32 K, pair table given,
+// forecast horizons within 1..hmax (hmax <= min(K, HALF_HB)), no season_out.
+extern "C" int fm_hw_half_fit(const SmoothArgs* a, int hmax, hipStream_t st) {
+  const int K = a->K;
+  if (K != 45 || a->seg != 32 * K || a->m != a->seg || a->Tp % a->seg != 0 || a->Tp / a->seg < 2 ||
+      !a->pair_tab || a->season_out || hmax < 1 || hmax > K || hmax > HALF_HB)
+    return (int)hipErrorNotSupported;
+  if (a->N <= 0) return 0;
+  const size_t lds = fm_hw_half_lds_bytes(a->Tp, a->seg, K);
+  if (lds > 64 * 1024) return (int)hipErrorNotSupported;
+  hipLaunchKernelGGL((hw_half_kernel<45>), dim3((a->N + 1) / 2), dim3(256), lds, st, *a, hmax);
+  return (int)hipGetLastError();
+}
 
 template <int K, int MODE, typename TIN, int NC, int MINW, bool TAB = false>
 __global__ __launch_bounds__(256, MINW) void hw_scan_kernel(const SmoothArgs a) {

@@ -63,6 +63,9 @@ class DetectSpec:
     app_id: Optional[torch.Tensor] = None   # int32 [N]
     app_stats: Optional[torch.Tensor] = None  # int32 [A, 2]
     anomalies: Optional["AnomalyBuffer"] = None  # K9 compaction of anomalous points
+    # host-known upper bound of ``horizons`` (all values in 1..max_horizon); lets the
+    # Holt-Winters kernel keep only the seasonal phases the forecast needs (variant 4)
+    max_horizon: Optional[int] = None
 
 
 class AnomalyBuffer:
@@ -166,6 +169,10 @@ def _hist_check(hist: torch.Tensor, head: int, length: int) -> None:
 
 
 UNIFORM_K = (8, 12, 16, 24, 32)
+HALF_K = (45,)        # variant 4 (two series per wave): season = 32 * K
+HALF_HB = 64          # seasonal phases kept per series by variant 4
+last_hw_variant: Optional[int] = None  # variant actually launched by the last smoothing_fit (tests/bench)
+DEFAULT_HW_VARIANT = 4
 
 
 def smoothing_geometry(mode: int, T: int, m: int, K: Optional[int] = None):
@@ -267,10 +274,19 @@ def smoothing_fit(hist: torch.Tensor, head: int, length: int, mode: int, m: int,
     Tp, pad, k, seg = smoothing_geometry(mode, length, mm, K)
     bf16 = hist.dtype == torch.bfloat16
     if variant is None:
-        variant = int(os.environ.get("FOREMAST_HW_VARIANT", "3"))
+        variant = int(os.environ.get("FOREMAST_HW_VARIANT", str(DEFAULT_HW_VARIANT)))
+    if variant == 4:
+        hmax = det.max_horizon
+        if (mode == MODE_HW and bf16 and mm % 32 == 0 and mm // 32 in HALF_K and not want_season
+                and hmax is not None and 1 <= hmax <= min(mm // 32, HALF_HB) and K is None
+                and lib.fm_hw_half_lds_bytes(Tp, mm, mm // 32) <= LDS_LIMIT):
+            return _hw_half_fit(lib, hist, head, length, mm, grid, det, Tp, pad, hmax, out)
+        variant = 3
     fast_lds = lib.fm_hw_scan_lds_bytes(Tp, seg, k, int(mode), int(bf16))
     if variant >= 0 and not (seg % k == 0 and seg // k <= 64 and fast_lds <= LDS_LIMIT):
         variant = -1
+    global last_hw_variant
+    last_hw_variant = variant
     if variant < 0:
         if mode == MODE_HW and k not in (8, 16, 24, 32):
             k = (mm + 63) // 64
@@ -307,6 +323,46 @@ def smoothing_fit(hist: torch.Tensor, head: int, length: int, mode: int, m: int,
     a.pair_tab = nat.ptr(pair_table(grid, k)) if variant == 3 else 0
     _fill_detect(a.det, det, N, dev, out)
     nat.check(lib.fm_smooth_fit(a, int(mode), int(bf16), int(variant), nat.stream_handle(dev)), "fm_smooth_fit")
+    return out
+
+
+def _hw_half_fit(lib, hist, head, length, m, grid, det, Tp, pad, hmax, out):
+    """Variant 4 of the Holt-Winters fit (hw_scan.hip ``hw_half_kernel``): two
+    series per wave, season = 32 lanes x K steps."""
+    dev = hist.device
+    N = hist.shape[0]
+    k = m // 32
+    out = {} if out is None else out
+    f32 = dict(dtype=torch.float32, device=dev)
+    for kname in ("level", "trend", "sigma"):
+        if kname not in out:
+            out[kname] = torch.empty(N, **f32)
+    if "best" not in out:
+        out["best"] = torch.empty(N, dtype=torch.int32, device=dev)
+    a = nat.SmoothArgs()
+    a.hist = nat.ptr(hist)
+    a.ld = hist.stride(0)
+    a.ring_len = hist.shape[1]
+    a.head = int(head)
+    a.T = int(length)
+    a.Tp = Tp
+    a.pad = pad
+    a.m = m
+    a.K = k
+    a.seg = m
+    a.grid = nat.ptr(grid)
+    a.G = grid.shape[0]
+    a.N = N
+    a.level = nat.ptr(out["level"])
+    a.trend = nat.ptr(out["trend"])
+    a.sigma = nat.ptr(out["sigma"])
+    a.best = nat.ptr(out["best"])
+    a.season_out = 0
+    a.pair_tab = nat.ptr(pair_table(grid, k))
+    _fill_detect(a.det, det, N, dev, out)
+    nat.check(lib.fm_hw_half_fit(a, int(hmax), nat.stream_handle(dev)), "fm_hw_half_fit")
+    global last_hw_variant
+    last_hw_variant = 4
     return out
 
 

@@ -245,3 +245,43 @@ def test_anomaly_compaction_matches_band_flags(K, which):
     assert (exp[:, 0] == s).all() and (exp[:, 1] == c).all()
     assert np.allclose(v, x.numpy()[s, c])
     assert (np.bincount(s, minlength=N) == out["count"].cpu().numpy()).all()
+
+
+@pytest.mark.parametrize("case", ["plain", "nan", "wrap_pad", "odd"])
+def test_hw_half_variant_matches_reference(K, case):
+    """Variant 4 (two series per wave, 1440 = 32 x 45): same fit as the fp64
+    reference and the same band/verdict semantics, on the flagship season."""
+    dev = torch.device("cuda:0")
+    m = 1440
+    N = 17 if case == "odd" else 16
+    T = 1440 * 4 + 300 if case == "wrap_pad" else 10080
+    R, head = (T + 97, 61) if case == "wrap_pad" else (T, 0)
+    y = _series(N, T, m, seed=11 + len(case), nan_frac=0.01 if case == "nan" else 0.0)
+    ring = torch.tensor(_ring(y, R, head), device=dev).to(torch.bfloat16)
+    yl = ring.float().cpu().numpy()[:, (head + np.arange(T)) % R]
+    grid = sm_ref.make_grid(sm_ref.MODE_HW, (0.1, 0.3, 0.5, 0.8), (0.0, 0.01, 0.05, 0.1), (0.05, 0.1, 0.3, 0.5))
+    C = 50
+    hz = torch.arange(1, 11, dtype=torch.int32).repeat(C // 10)
+    cur = torch.tensor(y[:, -C:] * 1.05, device=dev)
+    spec = K.DetectSpec(horizons=hz.to(dev), threshold=torch.full((N,), 2.0, device=dev),
+                        bound=torch.full((N,), 3, dtype=torch.int8, device=dev),
+                        min_lower=torch.full((N,), -1e30, device=dev), cur=cur, max_horizon=10)
+    out = K.smoothing_fit(ring, head, T, sm_ref.MODE_HW, m, grid.to(dev), spec, variant=4)
+    torch.cuda.synchronize()
+    assert K.last_hw_variant == 4
+    ref = sm_ref.fit_smoothing(torch.tensor(yl, dtype=torch.float64), sm_ref.MODE_HW, grid.double(), m=m)
+    kb = out["best"].cpu().long()
+    same = (kb == ref.best).numpy()
+    assert same.mean() >= 0.75
+    np.testing.assert_allclose(out["sigma"].cpu().numpy(), ref.sigma.numpy(), rtol=5e-3)
+    np.testing.assert_allclose(out["level"].cpu().numpy()[same], ref.level.numpy()[same], rtol=2e-3, atol=5e-3)
+    f_ref = sm_ref.forecast(ref, hz.long())
+    np.testing.assert_allclose(out["forecast"].cpu().numpy()[same], f_ref.numpy()[same], rtol=5e-3, atol=2e-2)
+    d = det_ref.detect(out["forecast"].cpu(), out["sigma"].cpu(), cur.cpu(), torch.full((N,), 2.0),
+                       torch.full((N,), 3, dtype=torch.int8), torch.full((N,), -1e30))
+    assert torch.equal(d.count, out["count"].cpu())
+    assert torch.equal(d.verdict, out["verdict"].cpu())
+    # variant 3 (one series per wave) on the same input agrees on the chosen grid point
+    out3 = K.smoothing_fit(ring, head, T, sm_ref.MODE_HW, m, grid.to(dev), spec, variant=3)
+    torch.cuda.synchronize()
+    assert (out3["best"].cpu() == out["best"].cpu()).float().mean() >= 0.9
