@@ -308,6 +308,13 @@ __device__ __forceinline__ void fence_sched() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);  // nor may the machine scheduler move ALU work across
 }
+// Constant-space loads are invariant, so LLVM hoists them out of every loop (and past
+// asm memory clobbers) — for a 180-float table that spills SGPRs.  Re-deriving the
+// pointer through an opaque asm per season / chunk keeps each load where it is used.
+__device__ __forceinline__ cfp launder(cfp p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
 // the pair table as a constant-address-space pointer (uniform: scalar loads)
 __device__ __forceinline__ cfp const_ptr(const float* p) {
   return (cfp)(__builtin_amdgcn_readfirstlane((int)((unsigned long long)p)) & 0xffffffffull |
@@ -348,6 +355,7 @@ __device__ __forceinline__ void pass2_stream(const bf16_t* yc, const bf16_t* yn,
     if (q + 1 < NCH) {
       cn.w = pc[q + 1];
       if (FUSE) {
+        W = launder(W);
         nn.w = pn[q + 1];
 #pragma unroll
         for (int r = 0; r < 16; ++r)
@@ -467,10 +475,14 @@ __device__ __forceinline__ void half_exclusive_scan(Aff<V>& a, int j) {
 // once in LDS; every wave fits a quarter of the grid pairs for both.  Only the first
 // HALF_HB best seasonal phases are kept (enough for forecast horizons 1..hmax <= K), so
 // this variant does not produce season_out (the host falls back to variant 3 then).
-constexpr int HALF_HB = 64;
+constexpr int HALF_HB = 16;
 
-template <int K>
-__global__ __launch_bounds__(256, 2) void hw_half_kernel(const SmoothArgs a, int hmax) {
+// One workgroup's work on the series pair (n0, n0 + 1).  GENERAL = false is the
+// straight-line NaN-free path: a pair with a gap in a fitted season is appended to
+// `deferred` and left to the GENERAL = true launch (per-lane affine scan, masked
+// steps), so the common path carries no NaN branches and no register copies at joins.
+template <int K, bool GENERAL>
+__device__ __forceinline__ void hw_half_block(const SmoothArgs& a, int hmax, int n0, int* deferred) {
   using YR = YRegs<bf16_t, K>;
   constexpr int KP = YR::KP;
   constexpr int TS = PairTab<K>::SIZE;
@@ -478,7 +490,6 @@ __global__ __launch_bounds__(256, 2) void hw_half_kernel(const SmoothArgs a, int
   const int half = lane >> 5, j = lane & 31;
   const bool odd_row = ((lane >> 4) & 1) != 0;
   const int nseg = a.Tp / a.seg, m = a.m;
-  const int n0 = blockIdx.x * 2;
 
   // ---- LDS: ys[2][nseg][32][KP] | segnan[2][nseg] + nvs[2] | bests[4][2][HB] | wbest[4][2][4]
   bf16_t* ys = (bf16_t*)fm_hw_smem;
@@ -494,27 +505,41 @@ __global__ __launch_bounds__(256, 2) void hw_half_kernel(const SmoothArgs a, int
   __syncthreads();
 
   // ---- stage both series: logical padded index p = pk*K + i, pk = sg*32 + lane -------
+  // 16 independent loads in flight per thread per batch (a dependent load per
+  // element would serialise ~80 HBM round trips per workgroup)
+  constexpr int U = 16;
   for (int r = 0; r < 2; ++r) {
     const int n = n0 + r;
     const bool real = n < a.N;
     const bf16_t* row = (const bf16_t*)a.hist + (long long)(real ? n : 0) * a.ld;
     float nv = 0.f;
-    for (int p = tid; p < a.Tp; p += blockDim.x) {
-      bf16_t v = 0;  // the padding series of an odd N is zeros (keeps the wave on the fast path)
-      if (real) {
-        v = 0x7fc0;
-        const int t = p - a.pad;
-        if (t >= 0) {
-          int c = a.head + t;
-          if (c >= a.ring_len) c -= a.ring_len;
-          v = row[c];
+    for (int p0 = tid; p0 < a.Tp; p0 += U * (int)blockDim.x) {
+      bf16_t v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int p = p0 + u * (int)blockDim.x;
+        v[u] = 0;  // the padding series of an odd N is zeros (keeps the wave on the fast path)
+        if (real && p < a.Tp) {
+          v[u] = 0x7fc0;
+          const int t = p - a.pad;
+          if (t >= 0) {
+            int c = a.head + t;
+            if (c >= a.ring_len) c -= a.ring_len;
+            v[u] = row[c];
+          }
         }
       }
-      const int pk = p / K, i = p - pk * K;
-      ys[((size_t)r * nseg * 32 + pk) * KP + i] = v;
-      const float f = bf16_to_f32(v);
-      if (f != f) atomicOr(&segnan[r * nseg + (pk >> 5)], 1);
-      else if (p >= m) nv += 1.f;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int p = p0 + u * (int)blockDim.x;
+        if (p < a.Tp) {
+          const int pk = p / K, i = p - pk * K;
+          ys[((size_t)r * nseg * 32 + pk) * KP + i] = v[u];
+          const float f = bf16_to_f32(v[u]);
+          if (f != f) atomicOr(&segnan[r * nseg + (pk >> 5)], 1);
+          else if (p >= m) nv += 1.f;
+        }
+      }
     }
     nv = wave_sum(nv);
     if (lane == 0) atomicAdd(&nvs[r], nv);
@@ -549,6 +574,12 @@ __global__ __launch_bounds__(256, 2) void hw_half_kernel(const SmoothArgs a, int
     b0 = ((q1 > 0.f ? s1 / q1 : 0.f) - l0) / (float)m;
   }
 
+  bool allfast = true;  // no NaN in the fitted seasons of either series
+  for (int sg = 1; sg < nseg; ++sg) allfast = allfast && !seg_nan(sg);
+  if (!GENERAL && !allfast) {
+    if (tid == 0) deferred[1 + atomicAdd(deferred, 1)] = n0;
+    return;
+  }
   float bestSSE = __builtin_huge_valf();
   int bestIdx = 0x7fffffff;
   float bestL = l0, bestB = b0;
@@ -586,46 +617,64 @@ __global__ __launch_bounds__(256, 2) void hw_half_kernel(const SmoothArgs a, int
     v2f X1 = splat2(l0 + b0), X2 = splat2(b0), sse = zero;  // (f, b) at the season start
 
     Aff<v2f> loc;
-    bool locfast = !seg_nan(1);
-    if (locfast) {
+    if constexpr (!GENERAL) {
+      // NaN-free seasons (the common case): one straight-line path, so the seasonal
+      // state keeps its registers across seasons (no phi copies at a join)
       pass1_stream<K>(yseg(1), s, W, loc.v1, loc.v2);
-    } else {
-      YR y1;
-      y1.load(yseg(1));
-      pass1_slow<K>(y1, s, c1, c2, loc);
-    }
-
-    for (int sg = 1; sg < nseg; ++sg) {
-      v2f x1, x2;
-      if (locfast) {
-        half_uniform_scan(tb, loc.v1, loc.v2, X1, X2, Bj, odd_row, x1, x2);
-      } else {
-        half_exclusive_scan(loc, j);
-        x1 = loc.m11 * X1 + loc.m12 * X2 + loc.v1;
-        x2 = loc.m21 * X1 + loc.m22 * X2 + loc.v2;
+      for (int sg = 1; sg < nseg - 1; ++sg) {
+        v2f x1, x2;
+        half_uniform_scan(launder(tb), loc.v1, loc.v2, X1, X2, Bj, odd_row, x1, x2);
+        pass2_stream<K, false, true>(yseg(sg), yseg(sg + 1), s, c1, c2, g1a, launder(W), x1, x2, sse, loc.v1,
+                                     loc.v2);
+        X1 = half_last(x1, half);
+        X2 = half_last(x2, half);
       }
-      const bool has_next = sg + 1 < nseg;
-      const bool mask = seg_nan(sg);
-      const bool next_fast = has_next && !seg_nan(sg + 1);
-      const bf16_t* yc = yseg(sg);
-      const bf16_t* yn = yseg(has_next ? sg + 1 : sg);
-      if (next_fast) {
-        if (mask) pass2_stream<K, true, true>(yc, yn, s, c1, c2, g1a, W, x1, x2, sse, loc.v1, loc.v2);
-        else pass2_stream<K, false, true>(yc, yn, s, c1, c2, g1a, W, x1, x2, sse, loc.v1, loc.v2);
-        locfast = true;
-      } else {
-        v2f d1, d2;
-        if (mask) pass2_stream<K, true, false>(yc, yn, s, c1, c2, g1a, W, x1, x2, sse, d1, d2);
-        else pass2_stream<K, false, false>(yc, yn, s, c1, c2, g1a, W, x1, x2, sse, d1, d2);
-        if (has_next) {
-          YR y1;
-          y1.load(yn);
-          pass1_slow<K>(y1, s, c1, c2, loc);
-        }
-        locfast = false;
-      }
+      v2f x1, x2, d1, d2;
+      half_uniform_scan(tb, loc.v1, loc.v2, X1, X2, Bj, odd_row, x1, x2);
+      pass2_stream<K, false, false>(yseg(nseg - 1), yseg(nseg - 1), s, c1, c2, g1a, W, x1, x2, sse, d1, d2);
       X1 = half_last(x1, half);
       X2 = half_last(x2, half);
+    } else {
+      bool locfast = !seg_nan(1);
+      if (locfast) {
+        pass1_stream<K>(yseg(1), s, W, loc.v1, loc.v2);
+      } else {
+        YR y1;
+        y1.load(yseg(1));
+        pass1_slow<K>(y1, s, c1, c2, loc);
+      }
+      for (int sg = 1; sg < nseg; ++sg) {
+        v2f x1, x2;
+        if (locfast) {
+          half_uniform_scan(tb, loc.v1, loc.v2, X1, X2, Bj, odd_row, x1, x2);
+        } else {
+          half_exclusive_scan(loc, j);
+          x1 = loc.m11 * X1 + loc.m12 * X2 + loc.v1;
+          x2 = loc.m21 * X1 + loc.m22 * X2 + loc.v2;
+        }
+        const bool has_next = sg + 1 < nseg;
+        const bool mask = seg_nan(sg);
+        const bool next_fast = has_next && !seg_nan(sg + 1);
+        const bf16_t* yc = yseg(sg);
+        const bf16_t* yn = yseg(has_next ? sg + 1 : sg);
+        if (next_fast) {
+          if (mask) pass2_stream<K, true, true>(yc, yn, s, c1, c2, g1a, W, x1, x2, sse, loc.v1, loc.v2);
+          else pass2_stream<K, false, true>(yc, yn, s, c1, c2, g1a, W, x1, x2, sse, loc.v1, loc.v2);
+          locfast = true;
+        } else {
+          v2f d1, d2;
+          if (mask) pass2_stream<K, true, false>(yc, yn, s, c1, c2, g1a, W, x1, x2, sse, d1, d2);
+          else pass2_stream<K, false, false>(yc, yn, s, c1, c2, g1a, W, x1, x2, sse, d1, d2);
+          if (has_next) {
+            YR y1;
+            y1.load(yn);
+            pass1_slow<K>(y1, s, c1, c2, loc);
+          }
+          locfast = false;
+        }
+        X1 = half_last(x1, half);
+        X2 = half_last(x2, half);
+      }
     }
 #pragma unroll
     for (int o = 16; o > 0; o >>= 1) {
@@ -683,6 +732,21 @@ __global__ __launch_bounds__(256, 2) void hw_half_kernel(const SmoothArgs a, int
   });
 }
 
+template <int K>
+__global__ __launch_bounds__(256, 2) void hw_half_kernel(const SmoothArgs a, int hmax, int* deferred) {
+  hw_half_block<K, false>(a, hmax, blockIdx.x * 2, deferred);
+}
+
+// persistent over the pairs deferred by hw_half_kernel (count in deferred[0])
+template <int K>
+__global__ __launch_bounds__(256, 2) void hw_half_general_kernel(const SmoothArgs a, int hmax, const int* deferred) {
+  const int cnt = deferred[0];
+  for (int q = blockIdx.x; q < cnt; q += gridDim.x) {
+    hw_half_block<K, true>(a, hmax, deferred[1 + q], nullptr);
+    __syncthreads();  // LDS is reused by the next pair
+  }
+}
+
 extern "C" size_t fm_hw_half_lds_bytes(int Tp, int seg, int K) {
   if (K != 45) return (size_t)-1;
   constexpr int KP = 48;
@@ -696,7 +760,8 @@ extern "C" size_t fm_hw_half_lds_bytes(int Tp, int seg, int K) {
 
 // Variant 4 launcher: Holt-Winters, bf16 ring, season = seg = 32 K, pair table given,
 // forecast horizons within 1..hmax (hmax <= min(K, HALF_HB)), no season_out.
-extern "C" int fm_hw_half_fit(const SmoothArgs* a, int hmax, hipStream_t st) {
+// `deferred`: device int32 workspace of 1 + ceil(N / 2) entries.
+extern "C" int fm_hw_half_fit(const SmoothArgs* a, int hmax, int* deferred, hipStream_t st) {
   const int K = a->K;
   if (K != 45 || a->seg != 32 * K || a->m != a->seg || a->Tp % a->seg != 0 || a->Tp / a->seg < 2 ||
       !a->pair_tab || a->season_out || hmax < 1 || hmax > K || hmax > HALF_HB)
@@ -704,7 +769,15 @@ extern "C" int fm_hw_half_fit(const SmoothArgs* a, int hmax, hipStream_t st) {
   if (a->N <= 0) return 0;
   const size_t lds = fm_hw_half_lds_bytes(a->Tp, a->seg, K);
   if (lds > 64 * 1024) return (int)hipErrorNotSupported;
-  hipLaunchKernelGGL((hw_half_kernel<45>), dim3((a->N + 1) / 2), dim3(256), lds, st, *a, hmax);
+  if (!deferred) return (int)hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(deferred, 0, sizeof(int), st);
+  if (e != hipSuccess) return (int)e;
+  const int pairs = (a->N + 1) / 2;
+  hipLaunchKernelGGL((hw_half_kernel<45>), dim3(pairs), dim3(256), lds, st, *a, hmax, deferred);
+  e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL((hw_half_general_kernel<45>), dim3(pairs < 512 ? pairs : 512), dim3(256), lds, st, *a, hmax,
+                     (const int*)deferred);
   return (int)hipGetLastError();
 }
 

@@ -170,7 +170,7 @@ def _hist_check(hist: torch.Tensor, head: int, length: int) -> None:
 
 UNIFORM_K = (8, 12, 16, 24, 32)
 HALF_K = (45,)        # variant 4 (two series per wave): season = 32 * K
-HALF_HB = 64          # seasonal phases kept per series by variant 4
+HALF_HB = 16          # seasonal phases kept per series by variant 4 (max forecast horizon)
 last_hw_variant: Optional[int] = None  # variant actually launched by the last smoothing_fit (tests/bench)
 DEFAULT_HW_VARIANT = 4
 
@@ -326,6 +326,20 @@ def smoothing_fit(hist: torch.Tensor, head: int, length: int, mode: int, m: int,
     return out
 
 
+_HALF_WS: Dict[tuple, torch.Tensor] = {}
+
+
+def _half_workspace(dev, N: int) -> torch.Tensor:
+    """Deferred-pair list of variant 4 (count + pair starts), reused across calls
+    so a captured tick allocates nothing."""
+    key = (dev.index, N)
+    ws = _HALF_WS.get(key)
+    if ws is None:
+        ws = torch.zeros(1 + (N + 1) // 2, dtype=torch.int32, device=dev)
+        _HALF_WS[key] = ws
+    return ws
+
+
 def _hw_half_fit(lib, hist, head, length, m, grid, det, Tp, pad, hmax, out):
     """Variant 4 of the Holt-Winters fit (hw_scan.hip ``hw_half_kernel``): two
     series per wave, season = 32 lanes x K steps."""
@@ -360,7 +374,8 @@ def _hw_half_fit(lib, hist, head, length, m, grid, det, Tp, pad, hmax, out):
     a.season_out = 0
     a.pair_tab = nat.ptr(pair_table(grid, k))
     _fill_detect(a.det, det, N, dev, out)
-    nat.check(lib.fm_hw_half_fit(a, int(hmax), nat.stream_handle(dev)), "fm_hw_half_fit")
+    ws = _half_workspace(dev, N)
+    nat.check(lib.fm_hw_half_fit(a, int(hmax), nat.ptr(ws), nat.stream_handle(dev)), "fm_hw_half_fit")
     global last_hw_variant
     last_hw_variant = 4
     return out

@@ -11,13 +11,14 @@ OUT="$PWD/gpurun_out/pmc_$TARGET"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 case $TARGET in
-  hw)   CMD=("$PWD/scripts/bench_kernels.py" --series 20000 --rounds 1 --only hw --variants=3) ;;
+  hw)   CMD=("$PWD/scripts/bench_kernels.py" --series 20000 --rounds 1 --only hw --variants=${VARIANTS:-3,4}) ;;
   dec)  CMD=("$PWD/scripts/bench_kernels.py" --series 20000 --rounds 1 --only decompose --variants=3) ;;
   lstm) CMD=("$PWD/scripts/bench_lstm_kernels.py") ;;
 esac
 SETS=("SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS"
       "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU"
-      "SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE")
+      "SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"
+      "SQ_WAIT_ANY SQ_INSTS_SMEM SQ_INSTS_SALU SQ_ACTIVE_INST_ANY")
 # (FETCH_SIZE / WRITE_SIZE need many replay passes: > 5 min for these workloads — not collected)
 for C in "${SETS[@]}"; do
   tag=$(echo $C | tr ' ' '_' | cut -c1-40)
