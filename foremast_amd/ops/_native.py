@@ -91,6 +91,10 @@ def _declare(lib: C.CDLL) -> None:
     lib.fm_hw_half_lds_bytes.restype = C.c_size_t
     lib.fm_hw_half_fit.argtypes = [C.POINTER(SmoothArgs), I, P, P]
     lib.fm_hw_half_fit.restype = I
+    lib.fm_hw_d_lds_bytes.argtypes = [I, I, I]
+    lib.fm_hw_d_lds_bytes.restype = C.c_size_t
+    lib.fm_hw_d_fit.argtypes = [C.POINTER(SmoothArgs), I, P, P]
+    lib.fm_hw_d_fit.restype = I
     lib.fm_rank_tests.argtypes = [C.POINTER(RankArgs), P]
     lib.fm_rank_tests.restype = I
     lib.fm_rank_lds_bytes.argtypes = [I, I]

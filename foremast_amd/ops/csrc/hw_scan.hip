@@ -444,6 +444,47 @@ __device__ __forceinline__ void half_uniform_scan(cfp tab_b, v2f v1, v2f v2, v2f
   s2 = s2 + w2;
 }
 
+// DPP move with BOUND_CTRL: lanes without a source read 0, so no zeroed "old" register
+// has to be materialised per move (variant 4 spends a v_mov per DPP on it)
+template <int CTRL, int RM>
+__device__ __forceinline__ v2f dppz2(v2f src) {
+  v2f r;
+  r.x = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(src.x), CTRL, RM, 0xf, true));
+  r.y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(src.y), CTRL, RM, 0xf, true));
+  return r;
+}
+template <int CTRL>
+__device__ __forceinline__ void row_round_z(v2f& w1, v2f& w2, const Mat2& Bd) {
+  const v2f q1 = dppz2<CTRL, 0xf>(w1);
+  const v2f q2 = dppz2<CTRL, 0xf>(w2);
+  w1 = w1 + Bd.a * q1 + Bd.b * q2;
+  w2 = w2 + Bd.c * q1 + Bd.d * q2;
+}
+// half_uniform_scan with BOUND_CTRL moves (rows 0 / 2 never read the row_bcast result)
+__device__ __forceinline__ void half_uniform_scan_z(cfp tab_b, v2f v1, v2f v2, v2f x01, v2f x02,
+                                                    const Mat2& Bj, bool odd_row, v2f& s1, v2f& s2) {
+  const Mat2 B1 = ldmat(tab_b), B2 = ldmat(tab_b + 8), B4 = ldmat(tab_b + 16), B8 = ldmat(tab_b + 24),
+             B16 = ldmat(tab_b + 32);
+  v2f w1 = dppz2<0x111, 0xf>(v1);
+  v2f w2 = dppz2<0x111, 0xf>(v2);
+  row_round_z<0x111>(w1, w2, B1);
+  row_round_z<0x112>(w1, w2, B2);
+  row_round_z<0x114>(w1, w2, B4);
+  row_round_z<0x118>(w1, w2, B8);
+  v2f e1, e2;
+  matvec(B1, w1, w2, e1, e2);
+  e1 = e1 + v1;
+  e2 = e2 + v2;
+  const v2f E1 = dppz2<0x142, 0xa>(e1), E2 = dppz2<0x142, 0xa>(e2);
+  v2f y1, y2;
+  matvec(B16, x01, x02, y1, y2);
+  y1 = odd_row ? y1 + E1 : x01;
+  y2 = odd_row ? y2 + E2 : x02;
+  matvec(Bj, y1, y2, s1, s2);
+  s1 = s1 + w1;
+  s2 = s2 + w2;
+}
+
 // General (per-lane matrix) exclusive affine scan within each 32-lane half.
 template <typename V>
 __device__ __forceinline__ void half_exclusive_scan(Aff<V>& a, int j) {
@@ -747,6 +788,347 @@ __global__ __launch_bounds__(256, 2) void hw_half_general_kernel(const SmoothArg
   }
 }
 
+// ---- variant 5: residual-state walk ------------------------------------------------------
+// Per phase i the walker keeps D_i = y_{k,i} - s_i, the observation of the season being
+// walked minus its seasonal state, instead of s_i.  Then
+//   e = D - f,   s' = s + g e   =>   D' = D + (y_{k+1,i} - y_{k,i}) - g e,
+// and D' is exactly the next season's pass-1 input u = y_{k+1} - s'.  The LDS image holds
+// D^(1) (season 1 minus the initial seasonal state) and the season-to-season differences
+// in fp32, so a step is 9 packed ops (e, f+b, f, b, sse, D+dy, D-ge, two pass-1 FMAs) with
+// no bf16 unpacking — variant 4 spends 12 (two unpacks, y-s, -f, un).  The image is twice
+// the bf16 one (fp32) but holds one season fewer: 2 series x 6 x 1440 x 4 B = 72 KiB per
+// workgroup, two workgroups per CU.  Series pairs with a NaN past season 0 are deferred
+// to hw_half_general_kernel exactly as in variant 4.
+template <int K>
+struct DLay {
+  static constexpr int NCH = (K + 7) / 8;
+  static constexpr int KP = NCH * 8;
+  static constexpr int SEASON = 32 * KP;  // floats per (series, season): [q][h][j][4]
+};
+// float offset of step i of lane j inside a season block: lanes are 16 B apart within a
+// half-chunk, so each ds_read_b128 lane group hits 16 distinct 16-B slots (no conflicts)
+__device__ __forceinline__ int dl_off(int i, int j) { return ((i >> 3) * 2 + ((i >> 2) & 1)) * 128 + j * 4 + (i & 3); }
+
+constexpr int D_MAXSEG = 7;  // seasons staged per series (LDS budget: 6 fp32 blocks)
+
+struct Chunk8f {
+  float4 lo, hi;
+  __device__ __forceinline__ float get(int r) const {
+    switch (r) {
+      case 0: return lo.x; case 1: return lo.y; case 2: return lo.z; case 3: return lo.w;
+      case 4: return hi.x; case 5: return hi.y; case 6: return hi.z; default: return hi.w;
+    }
+  }
+  __device__ __forceinline__ void load(const float* p) {  // p: chunk base + j*4
+    lo = *(const float4*)p;
+    hi = *(const float4*)(p + 128);
+  }
+};
+
+// pass 1 of season 1: D_i = splat(D1_i), v = sum_i W_i D1_i
+template <int K>
+__device__ __forceinline__ void d_pass1(const float* blk, cfp W, v2f* D, v2f& p1, v2f& p2) {
+  constexpr int NCH = (K + 7) / 8;
+  p1 = splat2(0.f);
+  p2 = splat2(0.f);
+#pragma unroll
+  for (int q = 0; q < NCH; ++q) {
+    Chunk8f c;
+    c.load(blk + q * 256);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int i = 8 * q + r;
+      if (i < K) {
+        const float d = c.get(r);
+        D[i] = splat2(d);
+        p1 = p1 + ldv2(W + 4 * i) * D[i];
+        p2 = p2 + ldv2(W + 4 * i + 2) * D[i];
+      }
+    }
+    fence_sched();
+  }
+}
+
+// pass 2 of a season from its true start state (x1, x2) = (f, b); FUSE: D advances to the
+// next season (dy block `blk`) and feeds that season's pass 1; !FUSE (last season): only
+// the first HALF_HB phases are advanced (they carry the forecast's seasonal terms).
+template <int K, bool FUSE>
+__device__ __forceinline__ void d_pass2(const float* blk, v2f* D, v2f c1, v2f c2, v2f g1a, cfp W, v2f& x1,
+                                        v2f& x2, v2f& sse, v2f& p1, v2f& p2) {
+  constexpr int NCH = (K + 7) / 8;
+  if (FUSE) { p1 = splat2(0.f); p2 = splat2(0.f); }
+  fence_sched();
+  Chunk8f cc, cn;
+  v2f wc[16], wn[16];
+  if (FUSE) {
+    cn.load(blk);
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if (r < 2 * K) wn[r] = ldv2(W + 2 * r);
+  }
+#pragma unroll
+  for (int q = 0; q < NCH; ++q) {
+    if (FUSE) {
+      cc = cn;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) wc[r] = wn[r];
+      asm volatile("" ::"v"(cc.lo.x), "v"(cc.hi.x), "s"(wc[0].x));
+      if (q + 1 < NCH) {
+        W = launder(W);
+        cn.load(blk + (q + 1) * 256);
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (16 * (q + 1) + r < 2 * K) wn[r] = ldv2(W + 32 * (q + 1) + 2 * r);
+      }
+    }
+    fence_sched();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int i = 8 * q + r;
+      if (i < K) {
+        const v2f e = D[i] - x1;
+        const v2f t = x1 + x2;
+        x1 = t + c1 * e;
+        x2 = x2 + c2 * e;
+        sse = sse + e * e;
+        if (FUSE) {
+          D[i] = (D[i] + splat2(cc.get(r))) - g1a * e;
+          p1 = p1 + wc[2 * r] * D[i];
+          p2 = p2 + wc[2 * r + 1] * D[i];
+        } else if (i < HALF_HB) {
+          D[i] = D[i] - g1a * e;
+        }
+      }
+    }
+    fence_sched();
+  }
+}
+
+template <int K>
+__device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0, int* deferred) {
+  constexpr int SEA = DLay<K>::SEASON;
+  constexpr int TS = PairTab<K>::SIZE;
+  constexpr int NMW = (32 * K + 31) / 32;  // season-0 validity bitmask words per series
+  const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+  const int half = lane >> 5, j = lane & 31;
+  const bool odd_row = ((lane >> 4) & 1) != 0;
+  const int nseg = a.Tp / a.seg, m = a.m, ns1 = nseg - 1;
+
+  // ---- LDS: dl[2][ns1][SEA] | vmask[2][NMW] | stat[2][4] | flag | ylast[2][HB] | bests[4][2][HB] | wbest[4][2][4]
+  float* dl = (float*)fm_hw_smem;
+  unsigned* vmask = (unsigned*)(dl + (size_t)2 * ns1 * SEA);
+  float* stat = (float*)(vmask + 2 * NMW);
+  int* flag = (int*)(stat + 8);
+  float* ylast = (float*)(flag + 4);
+  float* bests = ylast + 2 * HALF_HB;
+  float* wbest = bests + 4 * 2 * HALF_HB;
+
+  for (int i = tid; i < 2 * NMW + 8 + 4; i += blockDim.x) vmask[i] = 0u;  // vmask, stat, flag
+  __syncthreads();
+
+  // ---- stage: one thread per (series, 8 consecutive phases), all seasons of them in ------
+  // flight at once (up to 56 independent loads per thread: two round trips per workgroup)
+  {
+    constexpr int GRP = 8;
+    const int ngrp = (m + GRP - 1) / GRP;
+    float s0 = 0.f, c0 = 0.f, s1 = 0.f, c1 = 0.f, s0b = 0.f, c0b = 0.f, s1b = 0.f, c1b = 0.f;
+    int bad = 0;
+    for (int g = tid; g < 2 * ngrp; g += blockDim.x) {
+      const int r = g >= ngrp ? 1 : 0, o0 = (g - r * ngrp) * GRP;
+      const int n = n0 + r;
+      const bool real = n < a.N;
+      const bf16_t* row = (const bf16_t*)a.hist + (long long)(real ? n : 0) * a.ld;
+      float y[D_MAXSEG][GRP];
+#pragma unroll
+      for (int k = 0; k < D_MAXSEG; ++k) {
+#pragma unroll
+        for (int u = 0; u < GRP; ++u) {
+          // branch-free: every load is issued (clamped to a valid column) and the value
+          // selected afterwards, so all of them are in flight before the first wait
+          const bool ok = real && k < nseg && o0 + u < m;
+          const int t = k * m + o0 + u - a.pad;
+          const bool pos = t >= 0;
+          int c = a.head + ((ok && pos) ? t : 0);
+          c -= (c >= a.ring_len) ? a.ring_len : 0;
+          const float v = bf16_to_f32(row[c]);
+          // the padding series of an odd N is zeros (keeps the pair on the fast path)
+          y[k][u] = ok ? (pos ? v : fm_nan()) : 0.f;
+        }
+      }
+      unsigned vbits = 0u;
+#pragma unroll
+      for (int u = 0; u < GRP; ++u) {
+        const int o = o0 + u;
+        if (o < m) {
+          const int jj = o / K, i = o - jj * K;
+          const bool v0 = y[0][u] == y[0][u];
+          float* blk = dl + (size_t)r * ns1 * SEA + dl_off(i, jj);
+          blk[0] = v0 ? y[1][u] - y[0][u] : y[1][u];  // + l0 for valid y0 once the means are known
+          if (v0) vbits |= 1u << (o & 31);
+#pragma unroll
+          for (int k = 1; k < D_MAXSEG - 1; ++k)
+            if (k < ns1) blk[(size_t)k * SEA] = y[k + 1][u] - y[k][u];
+#pragma unroll
+          for (int k = 1; k < D_MAXSEG; ++k)
+            if (k < nseg && y[k][u] != y[k][u]) bad = 1;
+          if (o < HALF_HB) {
+            float yl = y[1][u];
+#pragma unroll
+            for (int k = 2; k < D_MAXSEG; ++k)
+              if (k == ns1) yl = y[k][u];
+            ylast[r * HALF_HB + o] = yl;
+          }
+          const bool v1 = y[1][u] == y[1][u];
+          const float y0v = v0 ? y[0][u] : 0.f, y0c = v0 ? 1.f : 0.f;
+          const float y1v = v1 ? y[1][u] : 0.f, y1c = v1 ? 1.f : 0.f;
+          if (r == 0) { s0 += y0v; c0 += y0c; s1 += y1v; c1 += y1c; }
+          else { s0b += y0v; c0b += y0c; s1b += y1v; c1b += y1c; }
+        }
+      }
+      if (vbits) atomicOr(&vmask[r * NMW + (o0 >> 5)], vbits);  // 8 | 32: never straddles a word
+    }
+    s0 = wave_sum(s0); c0 = wave_sum(c0); s1 = wave_sum(s1); c1 = wave_sum(c1);
+    s0b = wave_sum(s0b); c0b = wave_sum(c0b); s1b = wave_sum(s1b); c1b = wave_sum(c1b);
+    if (lane == 0) {
+      atomicAdd(&stat[0], s0); atomicAdd(&stat[1], c0); atomicAdd(&stat[2], s1); atomicAdd(&stat[3], c1);
+      atomicAdd(&stat[4], s0b); atomicAdd(&stat[5], c0b); atomicAdd(&stat[6], s1b); atomicAdd(&stat[7], c1b);
+    }
+    if (bad) atomicOr(flag, 1);
+  }
+  __syncthreads();
+  if (*flag) {  // block-uniform: a gap past season 0 — the general kernel takes the pair
+    if (tid == 0) deferred[1 + atomicAdd(deferred, 1)] = n0;
+    return;
+  }
+  float l0r[2], b0r[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const float* st = stat + 4 * r;
+    l0r[r] = st[1] > 0.f ? st[0] / st[1] : 0.f;
+    b0r[r] = ((st[3] > 0.f ? st[2] / st[3] : 0.f) - l0r[r]) / (float)m;
+  }
+  // D^(1) = y1 - s0 with s0 = y0 - l0 where y0 is valid (0 elsewhere)
+  for (int col = tid; col < 2 * m; col += blockDim.x) {
+    const int r = col >= m ? 1 : 0, o = col - r * m;
+    if ((vmask[r * NMW + (o >> 5)] >> (o & 31)) & 1u) {
+      const int jj = o / K, i = o - jj * K;
+      dl[(size_t)r * ns1 * SEA + dl_off(i, jj)] += l0r[r];
+    }
+  }
+  __syncthreads();
+
+  const float l0 = half ? l0r[1] : l0r[0], b0 = half ? b0r[1] : b0r[0];
+  const float* mydl = dl + (size_t)half * ns1 * SEA + j * 4;
+  float bestSSE = __builtin_huge_valf();
+  int bestIdx = 0x7fffffff;
+  float bestL = l0, bestB = b0;
+  float* mybest = bests + (w * 2 + half) * HALF_HB;
+  const int npairs = (a.G + 1) / 2;
+  const int nwaves = blockDim.x / FM_WAVE;
+
+  for (int pi = w; pi < npairs; pi += nwaves) {
+    const int c0 = 2 * pi;
+    const int c1i = (2 * pi + 1 < a.G) ? 2 * pi + 1 : c0;
+    const cfp tab = const_ptr(a.pair_tab + (size_t)pi * TS);
+    const v2f c1 = ldv2(tab), c2 = ldv2(tab + 2), g1a = ldv2(tab + 4);
+    const cfp W = tab + PairTab<K>::W0;
+    const cfp tb = tab + PairTab<K>::B0;
+    const v2f one = splat2(1.f), zero = splat2(0.f);
+    Mat2 Bj;  // B^(lane & 15)
+    Bj.a = one; Bj.b = zero; Bj.c = zero; Bj.d = one;
+#pragma unroll
+    for (int bit = 0; bit < 4; ++bit) {
+      const Mat2 Bb = ldmat(tb + 8 * bit);
+      const Mat2 r = matmul(Bj, Bb);
+      if ((lane >> bit) & 1) Bj = r;
+    }
+    v2f D[K];
+    v2f X1 = splat2(l0 + b0), X2 = splat2(b0), sse = zero;  // (f, b) at the season start
+    v2f p1, p2;
+    d_pass1<K>(mydl, W, D, p1, p2);
+    for (int sg = 1; sg < nseg - 1; ++sg) {
+      v2f x1, x2;
+      half_uniform_scan_z(launder(tb), p1, p2, X1, X2, Bj, odd_row, x1, x2);
+      d_pass2<K, true>(mydl + (size_t)sg * SEA, D, c1, c2, g1a, launder(W), x1, x2, sse, p1, p2);
+      X1 = half_last(x1, half);
+      X2 = half_last(x2, half);
+    }
+    {
+      v2f x1, x2, d1, d2;
+      half_uniform_scan_z(tb, p1, p2, X1, X2, Bj, odd_row, x1, x2);
+      d_pass2<K, false>(mydl, D, c1, c2, g1a, W, x1, x2, sse, d1, d2);
+      X1 = half_last(x1, half);
+      X2 = half_last(x2, half);
+    }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+      sse.x += __shfl_xor(sse.x, o, FM_WAVE);
+      sse.y += __shfl_xor(sse.y, o, FM_WAVE);
+    }
+    const bool upd0 = (sse.x < bestSSE || (sse.x == bestSSE && c0 < bestIdx));
+    if (upd0) { bestSSE = sse.x; bestIdx = c0; bestL = X1.x - X2.x; bestB = X2.x; }
+    const bool upd1 = (c1i != c0) && (sse.y < bestSSE || (sse.y == bestSSE && c1i < bestIdx));
+    if (upd1) { bestSSE = sse.y; bestIdx = c1i; bestL = X1.y - X2.y; bestB = X2.y; }
+    if (j == 0 && (upd0 || upd1)) {
+      const float* yl = ylast + half * HALF_HB;
+#pragma unroll
+      for (int i = 0; i < K && i < HALF_HB; ++i)
+        if (i < hmax) mybest[i] = yl[i] - (upd1 ? D[i].y : D[i].x);
+    }
+  }
+
+  // ---- arg-min across the 4 waves; wave r finishes series n0 + r ----------------------
+  if (j == 0) {
+    float* wb = wbest + (w * 2 + half) * 4;
+    wb[0] = bestSSE;
+    wb[1] = __int_as_float(bestIdx);
+    wb[2] = bestL;
+    wb[3] = bestB;
+  }
+  __syncthreads();
+  if (w >= 2) return;
+  const int r = w, n = n0 + r;
+  if (n >= a.N) return;
+  int win = 0;
+  for (int q = 1; q < nwaves; ++q) {
+    const float sq = wbest[(q * 2 + r) * 4], sw = wbest[(win * 2 + r) * 4];
+    const int iq = __float_as_int(wbest[(q * 2 + r) * 4 + 1]), iw = __float_as_int(wbest[(win * 2 + r) * 4 + 1]);
+    if (sq < sw || (sq == sw && iq < iw)) win = q;
+  }
+  const float* wb = wbest + (win * 2 + r) * 4;
+  const float gSSE = wb[0], gL = wb[2], gB = wb[3];
+  const int gIdx = __float_as_int(wb[1]);
+  const float nvr = (float)(ns1 * m);  // fast path: every sample past season 0 is valid
+  const float sig = sqrtf(gSSE / fmaxf(nvr, 1.f));
+  if (lane == 0) {
+    a.level[n] = gL;
+    a.trend[n] = gB;
+    a.sigma[n] = sig;
+    a.best[n] = gIdx;
+  }
+  const float* sb = bests + (win * 2 + r) * HALF_HB;
+  const int Tp = a.Tp;
+  detect_epilogue_wave(a.det, n, sig, nvr, [&](int h) {
+    int ph = (Tp - 1 + h) % m;
+    if (ph < 0) ph += m;
+    ph = ph < HALF_HB ? ph : HALF_HB - 1;  // host guarantees ph < hmax; clamp keeps LDS reads in bounds
+    return gL + (float)h * gB + sb[ph];
+  });
+}
+
+template <int K>
+__global__ __launch_bounds__(256, 2) void hw_d_kernel(const SmoothArgs a, int hmax, int* deferred) {
+  hw_d_block<K>(a, hmax, blockIdx.x * 2, deferred);
+}
+
+extern "C" size_t fm_hw_d_lds_bytes(int Tp, int seg, int K) {
+  if (K != 45 || seg <= 0) return (size_t)-1;
+  const int nseg = Tp / seg;
+  if (nseg < 2 || nseg > D_MAXSEG) return (size_t)-1;
+  const int NMW = (32 * K + 31) / 32;
+  return ((size_t)2 * (nseg - 1) * DLay<45>::SEASON + 2 * NMW + 8 + 4 + 2 * HALF_HB + 4 * 2 * HALF_HB + 4 * 2 * 4) * 4;
+}
+
 extern "C" size_t fm_hw_half_lds_bytes(int Tp, int seg, int K) {
   if (K != 45) return (size_t)-1;
   constexpr int KP = 48;
@@ -777,6 +1159,29 @@ extern "C" int fm_hw_half_fit(const SmoothArgs* a, int hmax, int* deferred, hipS
   e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL((hw_half_general_kernel<45>), dim3(pairs < 512 ? pairs : 512), dim3(256), lds, st, *a, hmax,
+                     (const int*)deferred);
+  return (int)hipGetLastError();
+}
+
+// Variant 5 launcher: same contract as fm_hw_half_fit (deferred pairs go to the
+// variant-4 general kernel), at most D_MAXSEG seasons.
+extern "C" int fm_hw_d_fit(const SmoothArgs* a, int hmax, int* deferred, hipStream_t st) {
+  const int K = a->K;
+  if (K != 45 || a->seg != 32 * K || a->m != a->seg || a->Tp % a->seg != 0 || a->Tp / a->seg < 2 ||
+      a->Tp / a->seg > D_MAXSEG || !a->pair_tab || a->season_out || hmax < 1 || hmax > K || hmax > HALF_HB)
+    return (int)hipErrorNotSupported;
+  if (a->N <= 0) return 0;
+  const size_t lds = fm_hw_d_lds_bytes(a->Tp, a->seg, K);
+  const size_t glds = fm_hw_half_lds_bytes(a->Tp, a->seg, K);
+  if (lds > 80 * 1024 || glds > 64 * 1024) return (int)hipErrorNotSupported;
+  if (!deferred) return (int)hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(deferred, 0, sizeof(int), st);
+  if (e != hipSuccess) return (int)e;
+  const int pairs = (a->N + 1) / 2;
+  hipLaunchKernelGGL((hw_d_kernel<45>), dim3(pairs), dim3(256), lds, st, *a, hmax, deferred);
+  e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL((hw_half_general_kernel<45>), dim3(pairs < 512 ? pairs : 512), dim3(256), glds, st, *a, hmax,
                      (const int*)deferred);
   return (int)hipGetLastError();
 }

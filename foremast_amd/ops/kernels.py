@@ -21,6 +21,7 @@ from . import _native as nat
 MODE_ES, MODE_DES, MODE_HW = 0, 1, 2
 DEFAULT_ES_K = 16  # steps per lane per segment for ES/DES (segment = 1024)
 LDS_LIMIT = 64 * 1024          # budget of the tiled kernels (keeps >= 2 workgroups per CU)
+D_LDS_LIMIT = 78 * 1024        # HW variant 5: two 4-wave workgroups per CU within 160 KiB
 LDS_MAX_WG = 160 * 1024        # gfx950: one workgroup may own the whole 160 KiB
 
 
@@ -172,7 +173,7 @@ UNIFORM_K = (8, 12, 16, 24, 32)
 HALF_K = (45,)        # variant 4 (two series per wave): season = 32 * K
 HALF_HB = 16          # seasonal phases kept per series by variant 4 (max forecast horizon)
 last_hw_variant: Optional[int] = None  # variant actually launched by the last smoothing_fit (tests/bench)
-DEFAULT_HW_VARIANT = 4
+DEFAULT_HW_VARIANT = 5
 
 
 def smoothing_geometry(mode: int, T: int, m: int, K: Optional[int] = None):
@@ -275,11 +276,13 @@ def smoothing_fit(hist: torch.Tensor, head: int, length: int, mode: int, m: int,
     bf16 = hist.dtype == torch.bfloat16
     if variant is None:
         variant = int(os.environ.get("FOREMAST_HW_VARIANT", str(DEFAULT_HW_VARIANT)))
-    if variant == 4:
+    if variant in (4, 5):
         hmax = det.max_horizon
         if (mode == MODE_HW and bf16 and mm % 32 == 0 and mm // 32 in HALF_K and not want_season
                 and hmax is not None and 1 <= hmax <= min(mm // 32, HALF_HB) and K is None
                 and lib.fm_hw_half_lds_bytes(Tp, mm, mm // 32) <= LDS_LIMIT):
+            if variant == 5 and lib.fm_hw_d_lds_bytes(Tp, mm, mm // 32) <= D_LDS_LIMIT:
+                return _hw_half_fit(lib, hist, head, length, mm, grid, det, Tp, pad, hmax, out, residual=True)
             return _hw_half_fit(lib, hist, head, length, mm, grid, det, Tp, pad, hmax, out)
         variant = 3
     fast_lds = lib.fm_hw_scan_lds_bytes(Tp, seg, k, int(mode), int(bf16))
@@ -340,9 +343,13 @@ def _half_workspace(dev, N: int) -> torch.Tensor:
     return ws
 
 
-def _hw_half_fit(lib, hist, head, length, m, grid, det, Tp, pad, hmax, out):
-    """Variant 4 of the Holt-Winters fit (hw_scan.hip ``hw_half_kernel``): two
-    series per wave, season = 32 lanes x K steps."""
+def _hw_half_fit(lib, hist, head, length, m, grid, det, Tp, pad, hmax, out, residual: bool = False):
+    """Variants 4/5 of the Holt-Winters fit: two series per wave, season = 32
+    lanes x K steps.  Variant 4 (hw_scan.hip ``hw_half_kernel``) walks the
+    seasonal state over a bf16 image; variant 5 (``residual``, ``hw_d_kernel``)
+    walks D = y - s over an fp32 image of season differences (fewer ops per
+    step, at most 7 seasons).  Pairs with gaps past season 0 go to the general
+    kernel in both."""
     dev = hist.device
     N = hist.shape[0]
     k = m // 32
@@ -375,8 +382,12 @@ def _hw_half_fit(lib, hist, head, length, m, grid, det, Tp, pad, hmax, out):
     a.pair_tab = nat.ptr(pair_table(grid, k))
     _fill_detect(a.det, det, N, dev, out)
     ws = _half_workspace(dev, N)
-    nat.check(lib.fm_hw_half_fit(a, int(hmax), nat.ptr(ws), nat.stream_handle(dev)), "fm_hw_half_fit")
     global last_hw_variant
+    if residual:
+        nat.check(lib.fm_hw_d_fit(a, int(hmax), nat.ptr(ws), nat.stream_handle(dev)), "fm_hw_d_fit")
+        last_hw_variant = 5
+        return out
+    nat.check(lib.fm_hw_half_fit(a, int(hmax), nat.ptr(ws), nat.stream_handle(dev)), "fm_hw_half_fit")
     last_hw_variant = 4
     return out
 

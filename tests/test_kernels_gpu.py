@@ -247,10 +247,12 @@ def test_anomaly_compaction_matches_band_flags(K, which):
     assert (np.bincount(s, minlength=N) == out["count"].cpu().numpy()).all()
 
 
+@pytest.mark.parametrize("variant", [4, 5])
 @pytest.mark.parametrize("case", ["plain", "nan", "wrap_pad", "odd"])
-def test_hw_half_variant_matches_reference(K, case):
-    """Variant 4 (two series per wave, 1440 = 32 x 45): same fit as the fp64
-    reference and the same band/verdict semantics, on the flagship season."""
+def test_hw_half_variant_matches_reference(K, case, variant):
+    """Variants 4/5 (two series per wave, 1440 = 32 x 45; 5 walks D = y - s over
+    fp32 season differences): same fit as the fp64 reference and the same
+    band/verdict semantics, on the flagship season."""
     dev = torch.device("cuda:0")
     m = 1440
     N = 17 if case == "odd" else 16
@@ -266,9 +268,9 @@ def test_hw_half_variant_matches_reference(K, case):
     spec = K.DetectSpec(horizons=hz.to(dev), threshold=torch.full((N,), 2.0, device=dev),
                         bound=torch.full((N,), 3, dtype=torch.int8, device=dev),
                         min_lower=torch.full((N,), -1e30, device=dev), cur=cur, max_horizon=10)
-    out = K.smoothing_fit(ring, head, T, sm_ref.MODE_HW, m, grid.to(dev), spec, variant=4)
+    out = K.smoothing_fit(ring, head, T, sm_ref.MODE_HW, m, grid.to(dev), spec, variant=variant)
     torch.cuda.synchronize()
-    assert K.last_hw_variant == 4
+    assert K.last_hw_variant == variant
     ref = sm_ref.fit_smoothing(torch.tensor(yl, dtype=torch.float64), sm_ref.MODE_HW, grid.double(), m=m)
     kb = out["best"].cpu().long()
     same = (kb == ref.best).numpy()
