@@ -139,12 +139,13 @@ class BatchScorer:
             if self.gpu:
                 from ..ops import kernels as K
                 o = K.rank_tests(t_base, t_cur, mode, cfg.pairwise_threshold, cfg.min_mann_white,
-                                 cfg.min_wilcoxon, cfg.min_kruskal)
+                                 cfg.min_wilcoxon, cfg.min_kruskal, pods=(1, 1), min_friedman=cfg.min_friedman)
                 differs, pvals = o["differs"], o["pvals"]
             else:
                 res = pw_ref.rank_tests(t_base, t_cur)
                 differs = pw_ref.pairwise_differs(res, mode, cfg.pairwise_threshold, cfg.min_mann_white,
-                                                  cfg.min_wilcoxon, cfg.min_kruskal).to(torch.uint8)
+                                                  cfg.min_wilcoxon, cfg.min_kruskal,
+                                                  cfg.min_friedman).to(torch.uint8)
                 pvals = torch.stack([res.p_mw, res.p_wilcoxon, res.p_kruskal], 1)
         has_base = torch.tensor([t.base_vals is not None for t in tasks], device=dev)
         if differs is not None:

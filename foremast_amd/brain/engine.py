@@ -146,7 +146,8 @@ class StreamingShard:
         if self.pw_mode != pw_ref.PW_NONE:
             self.pw_out = K.rank_tests(self.base, self.cur.data, self.pw_mode, cfg.pairwise_threshold,
                                        cfg.min_mann_white, cfg.min_wilcoxon, cfg.min_kruskal,
-                                       want_pvals=True, out=self.pw_out)
+                                       want_pvals=True, out=self.pw_out, pods=(self.cur.P, self.cur.P),
+                                       min_friedman=cfg.min_friedman)
             differs = self.pw_out["differs"]
         spec = K.DetectSpec(horizons=self.horizons, threshold=self.threshold, bound=self.bound,
                             min_lower=self.min_lower, cur=self.cur.data, differs=differs,
@@ -175,11 +176,12 @@ class StreamingShard:
         y = self.hist.logical().float()
         differs = None
         if self.pw_mode != pw_ref.PW_NONE:
-            res = pw_ref.rank_tests(self.base, self.cur.data)
+            res = pw_ref.rank_tests(self.base, self.cur.data, pods=(self.cur.P, self.cur.P))
             differs = pw_ref.pairwise_differs(res, self.pw_mode, cfg.pairwise_threshold, cfg.min_mann_white,
-                                              cfg.min_wilcoxon, cfg.min_kruskal)
+                                              cfg.min_wilcoxon, cfg.min_kruskal, cfg.min_friedman)
             self.pw_out = {"differs": differs.to(torch.uint8),
-                           "pvals": torch.stack([res.p_mw, res.p_wilcoxon, res.p_kruskal], 1).float()}
+                           "pvals": torch.stack([res.p_mw, res.p_wilcoxon, res.p_kruskal], 1).float(),
+                           "friedman": torch.stack([res.p_friedman, res.n_blocks], 1).float()}
         h = self.horizons.long()
         valid_hist = (~torch.isnan(y)).sum(1)
         if self.mode is not None:

@@ -15,7 +15,9 @@ padding.  Semantics match scipy's asymptotic forms (the oracle in
   method='approx')`` over the first ``k = min(nb, nc)`` aligned pairs where
   both are valid;
 * ``kruskal(b, c)`` — tie-corrected H, chi² with 1 dof;
-* ``friedmanchisquare`` over ``[N, n_blocks, k]`` groups.
+* ``friedmanchisquare`` over ``[N, n_blocks, k]`` groups (``friedman``), and
+  over time-slot blocks x pods of the canary windows (``friedman_pods``: the
+  design doc's "Friedman chi-square (special case)", ``design.md:92``).
 
 Degenerate inputs (all values tied, too few points) give ``p = 1``
 ("no evidence of a difference"); min-point gates are the
@@ -41,10 +43,11 @@ PW_ANY = 2
 PW_MANN_WHITE = 3
 PW_WILCOXON = 4
 PW_KRUSKAL = 5
+PW_FRIEDMAN = 6
 
 PW_BY_NAME = {"NONE": PW_NONE, "ALL": PW_ALL, "ANY": PW_ANY, "MANN_WHITE": PW_MANN_WHITE,
               "MANN_WHITNEY": PW_MANN_WHITE, "WILCOXON": PW_WILCOXON, "KRUSKAL": PW_KRUSKAL,
-              "FRIEDMAN": PW_KRUSKAL}
+              "FRIEDMAN": PW_FRIEDMAN}
 
 
 def norm_sf(z: torch.Tensor) -> torch.Tensor:
@@ -75,9 +78,49 @@ class PairwiseResult:
     n_base: torch.Tensor
     n_cur: torch.Tensor
     n_pairs: torch.Tensor
+    p_friedman: Optional[torch.Tensor] = None
+    n_blocks: Optional[torch.Tensor] = None
 
 
-def rank_tests(baseline: torch.Tensor, current: torch.Tensor) -> PairwiseResult:
+def friedman_pods(baseline: torch.Tensor, current: torch.Tensor, pods_b: int = 1, pods_c: int = 1):
+    """Friedman chi-square with time slots as blocks and pods as treatments.
+
+    ``baseline [N, pods_b * Wb]`` and ``current [N, pods_c * Wc]`` are pod-major
+    windows whose slot j is the same time in every pod (the streaming engine's
+    layout; the batch path pools pods, i.e. one pod per side).  Blocks are the
+    first ``min(Wb, Wc)`` slots that are valid in every pod; ranks within a
+    block, ties averaged, tie-corrected statistic, chi^2 with ``k - 1`` dof,
+    ``k = pods_b + pods_c`` (scipy's ``friedmanchisquare`` over the complete
+    blocks for k >= 3; k = 2 is the same statistic, which scipy refuses).
+    Returns ``(p [N], complete blocks [N])``; no complete block gives p = 1."""
+    dt = torch.promote_types(torch.promote_types(baseline.dtype, current.dtype), torch.float32)
+    b = baseline.to(dt)
+    c = current.to(dt)
+    N, nb = b.shape
+    nc = c.shape[1]
+    Wb, Wc = nb // pods_b, nc // pods_c
+    nbk = min(Wb, Wc)
+    k = pods_b + pods_c
+    g = torch.cat([b.reshape(N, pods_b, Wb)[:, :, :nbk], c.reshape(N, pods_c, Wc)[:, :, :nbk]], 1)
+    g = g.transpose(1, 2)  # [N, blocks, k]
+    ok = ~torch.isnan(g).any(2)
+    flat = torch.nan_to_num(g, nan=0.0).reshape(N * nbk, k)
+    r, tie = _ranks_with_ties(flat, torch.ones_like(flat, dtype=torch.bool))
+    r = r.to(dt).reshape(N, nbk, k) * ok[..., None]
+    tie = (tie.to(dt).reshape(N, nbk) * ok).sum(1)
+    nblk = ok.sum(1).to(dt)
+    Rj = r.sum(1)
+    chi = 12.0 / (nblk * k * (k + 1)).clamp(min=1e-30) * (Rj * Rj).sum(1) - 3 * nblk * (k + 1)
+    cc = 1 - tie / (nblk * k * (k * k - 1)).clamp(min=1e-30)
+    chi = chi / cc.clamp(min=1e-30)
+    p = torch.special.gammaincc(torch.full_like(chi, (k - 1) / 2.0), (chi / 2).clamp(min=0))
+    p = torch.where((nblk > 0) & (cc > 0), p, torch.ones_like(p))
+    return p, nblk
+
+
+def rank_tests(baseline: torch.Tensor, current: torch.Tensor, pods=None) -> PairwiseResult:
+    """All four tests; ``pods = (pods_b, pods_c)`` is the pod-major layout the
+    Friedman test blocks on (default: one pod per side)."""
     b = baseline.float()
     c = current.float()
     N, nb = b.shape
@@ -129,8 +172,10 @@ def rank_tests(baseline: torch.Tensor, current: torch.Tensor) -> PairwiseResult:
     wz = (Tw - wmu) / wsd.clamp(min=1e-30)
     p_w = (2 * norm_sf(wz.abs())).clamp(max=1.0)
     p_w = torch.where((wsd > 0) & (npairs > 0), p_w, one)
+    pb, pc = pods if pods is not None else (1, 1)
+    p_fr, nblk = friedman_pods(baseline, current, pb, pc)
     return PairwiseResult(p_mw=p_mw, p_wilcoxon=p_w, p_kruskal=p_kw, n_base=n1, n_cur=n2,
-                          n_pairs=npairs)
+                          n_pairs=npairs, p_friedman=p_fr, n_blocks=nblk)
 
 
 def friedman(groups: torch.Tensor) -> torch.Tensor:
@@ -152,7 +197,7 @@ def friedman(groups: torch.Tensor) -> torch.Tensor:
 
 
 def pairwise_differs(res: PairwiseResult, mode: int, alpha: float, min_mw: int = 20,
-                     min_wilcoxon: int = 20, min_kruskal: int = 5) -> torch.Tensor:
+                     min_wilcoxon: int = 20, min_kruskal: int = 5, min_friedman: int = 5) -> torch.Tensor:
     """Decision: do baseline and current differ?  A test whose min-point gate
     is not met abstains.  ALL = every non-abstaining test rejects (and at least
     one ran); ANY = some test rejects."""
@@ -171,6 +216,10 @@ def pairwise_differs(res: PairwiseResult, mode: int, alpha: float, min_mw: int =
         return rej_w
     if mode == PW_KRUSKAL:
         return rej_k
+    if mode == PW_FRIEDMAN:
+        if res.p_friedman is None:
+            raise ValueError("FRIEDMAN needs rank_tests(..., pods=...) results")
+        return (res.n_blocks >= min_friedman) & (res.p_friedman < alpha)
     if mode == PW_ANY:
         return rej_mw | rej_w | rej_k
     any_ran = ran_mw | ran_w | ran_k

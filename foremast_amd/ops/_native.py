@@ -57,6 +57,7 @@ class RankArgs(C.Structure):
         ("nb", I), ("nc", I), ("N", I), ("mode", I), ("alpha", F),
         ("min_mw", I), ("min_wilcoxon", I), ("min_kruskal", I),
         ("pvals", P), ("differs", P), ("counts", P),
+        ("pods_b", I), ("pods_c", I), ("min_friedman", I), ("p_friedman", P),
     ]
 
 

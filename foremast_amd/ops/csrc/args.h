@@ -67,7 +67,7 @@ struct RankArgs {
   int nb;
   int nc;
   int N;
-  int mode;       // 0 none, 1 ALL, 2 ANY, 3 MW, 4 WILCOXON, 5 KRUSKAL
+  int mode;       // 0 none, 1 ALL, 2 ANY, 3 MW, 4 WILCOXON, 5 KRUSKAL, 6 FRIEDMAN
   float alpha;
   int min_mw;
   int min_wilcoxon;
@@ -75,6 +75,12 @@ struct RankArgs {
   float* pvals;            // [N, 3] (mw, wilcoxon, kruskal) or null
   unsigned char* differs;  // [N]
   float* counts;           // [N, 3] (n_base, n_cur, n_pairs) or null
+  // Friedman chi-square over time blocks x pods: the windows are pod-major
+  // ([pods_b][nb / pods_b] and [pods_c][nc / pods_c], slot-aligned)
+  int pods_b;
+  int pods_c;
+  int min_friedman;        // complete blocks needed
+  float* p_friedman;       // [N, 2] (p, complete blocks) or null; computed when set or mode == 6
 };
 
 struct WindowArgs {

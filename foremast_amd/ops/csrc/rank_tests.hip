@@ -1,5 +1,6 @@
-// K5 + K11: batched Mann-Whitney U / Wilcoxon signed-rank / Kruskal-Wallis
-// and the pairwise "do baseline and current differ" decision.
+// K5 + K11: batched Mann-Whitney U / Wilcoxon signed-rank / Kruskal-Wallis /
+// Friedman chi-square and the pairwise "do baseline and current differ" decision
+// (docs/guides/design.md:89-92 of the reference lists the four tests).
 //
 // Semantics: foremast_amd/models/pairwise.py (scipy asymptotic forms).
 // One 64-lane wave per series; four series per 256-thread workgroup.  The
@@ -49,6 +50,79 @@ __device__ __forceinline__ void rank_sweep(const float* x, int n, GroupFn in_gro
   tie = wave_sum(tie);
 }
 
+// Upper tail of chi^2 with integer dof nu: Q(nu/2, x/2) by the finite series of the
+// regularised incomplete gamma at integer / half-integer order.
+__device__ __forceinline__ float chi2_sf(float x, int nu) {
+  if (!(x > 0.f)) return 1.f;
+  const float h = 0.5f * x;
+  float sum = 0.f;
+  if ((nu & 1) == 0) {
+    float term = 1.f;
+    for (int i = 0; i < nu / 2; ++i) {
+      sum += term;
+      term *= h / (float)(i + 1);
+    }
+    return fminf(expf(-h) * sum, 1.f);
+  }
+  float term = sqrtf(h) * 1.1283791670955126f;  // h^(1/2) / Gamma(3/2)
+  for (int i = 1; i <= (nu - 1) / 2; ++i) {
+    sum += term;
+    term *= h / ((float)i + 0.5f);
+  }
+  return fminf(erfcf(sqrtf(h)) + expf(-h) * sum, 1.f);
+}
+
+// Friedman chi-square over time blocks (window slots present in every pod) x
+// treatments (baseline pods, then canary pods): ranks within each complete
+// block (ties averaged), rank sums per treatment accumulated in LDS, tie-
+// corrected statistic, chi^2 with k - 1 dof.  One lane per block.
+__device__ __forceinline__ void friedman_wave(const RankArgs& a, const float* x, float* R, float& p_out,
+                                              float& nblk_out) {
+  const int lane = lane_id();
+  const int Pb = a.pods_b, Pc = a.pods_c, k = Pb + Pc;
+  const int Wb = a.nb / Pb, Wc = a.nc / Pc;
+  const int nbk = Wb < Wc ? Wb : Wc;
+  auto val = [&](int t, int j) { return t < Pb ? x[t * Wb + j] : x[a.nb + (t - Pb) * Wc + j]; };
+  if (lane < k) R[lane] = 0.f;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  float cnt = 0.f, tie = 0.f;
+  for (int j = lane; j < nbk; j += FM_WAVE) {
+    bool ok = true;
+    for (int t = 0; t < k; ++t) {
+      const float v = val(t, j);
+      ok = ok && (v == v);
+    }
+    if (!ok) continue;
+    cnt += 1.f;
+    for (int t = 0; t < k; ++t) {
+      const float vt = val(t, j);
+      float less = 0.f, eq = 0.f;
+      for (int u = 0; u < k; ++u) {
+        const float vu = val(u, j);
+        less += (vu < vt) ? 1.f : 0.f;
+        eq += (vu == vt) ? 1.f : 0.f;
+      }
+      atomicAdd(&R[t], less + (eq + 1.f) * 0.5f);
+      tie += eq * eq - 1.f;  // summed over a block's members = sum over tie groups of t^3 - t
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  const float r = lane < k ? R[lane] : 0.f;
+  const float ssq = wave_sum(r * r);
+  const float nb = wave_sum(cnt);
+  tie = wave_sum(tie);
+  nblk_out = nb;
+  p_out = 1.f;
+  if (nb > 0.f && k >= 2) {
+    const float fk = (float)k;
+    const float chi = 12.f / (nb * fk * (fk + 1.f)) * ssq - 3.f * nb * (fk + 1.f);
+    const float c = 1.f - tie / (nb * fk * (fk * fk - 1.f));
+    if (c > 0.f) p_out = chi2_sf(fmaxf(chi / c, 0.f), k - 1);
+  }
+}
+
 __global__ __launch_bounds__(256) void rank_tests_kernel(const RankArgs a) {
   const int w = wave_id(), lane = lane_id();
   const int n = blockIdx.x * (blockDim.x / FM_WAVE) + w;
@@ -56,8 +130,9 @@ __global__ __launch_bounds__(256) void rank_tests_kernel(const RankArgs a) {
   const int npool4 = (npool + 3) & ~3;
   const int k = a.nb < a.nc ? a.nb : a.nc;
   const int k4 = (k + 3) & ~3;
-  float* x = (float*)fm_rank_smem + (size_t)w * (npool4 + k4);
+  float* x = (float*)fm_rank_smem + (size_t)w * (npool4 + k4 + FM_WAVE);
   float* dabs = x + npool4;
+  float* Rf = dabs + k4;  // Friedman rank sums (<= 64 treatments)
   if (n >= a.N) return;  // wave-uniform; no block barrier below
 
   // stage pooled sample (NaN pads the vector tail) and |d| of aligned pairs
@@ -84,6 +159,10 @@ __global__ __launch_bounds__(256) void rank_tests_kernel(const RankArgs a) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   const float n1 = wave_sum(cnt_b), n2 = wave_sum(cnt_c), np = wave_sum(npairs);
   const float nn = n1 + n2;
+
+  // --- Friedman (time blocks x pods) on the staged windows
+  float p_fr = 1.f, nblk = 0.f;
+  if (a.mode == 6 || a.p_friedman != nullptr) friedman_wave(a, x, Rf, p_fr, nblk);
 
   // --- MW / Kruskal share the pooled ranks
   float R1, tie, R2;
@@ -135,9 +214,14 @@ __global__ __launch_bounds__(256) void rank_tests_kernel(const RankArgs a) {
     case 3: d = rej_mw; break;
     case 4: d = rej_w; break;
     case 5: d = rej_k; break;
+    case 6: d = nblk >= (float)a.min_friedman && p_fr < a.alpha; break;
     default: d = false;
   }
   a.differs[n] = d ? 1 : 0;
+  if (a.p_friedman) {
+    a.p_friedman[2 * (long long)n + 0] = p_fr;
+    a.p_friedman[2 * (long long)n + 1] = nblk;
+  }
   if (a.pvals) {
     a.pvals[3 * (long long)n + 0] = p_mw;
     a.pvals[3 * (long long)n + 1] = p_w;
@@ -154,13 +238,16 @@ extern "C" size_t fm_rank_lds_bytes(int nb, int nc) {
   const int npool4 = (nb + nc + 3) & ~3;
   const int k = nb < nc ? nb : nc;
   const int k4 = (k + 3) & ~3;
-  return (size_t)4 * (npool4 + k4) * 4;
+  return (size_t)4 * (npool4 + k4 + FM_WAVE) * 4;
 }
 
 extern "C" int fm_rank_tests(const RankArgs* a, hipStream_t st) {
   if (a->N <= 0) return 0;
   const size_t lds = fm_rank_lds_bytes(a->nb, a->nc);
   if (lds > 64 * 1024 || a->nb <= 0 || a->nc <= 0) return (int)hipErrorInvalidValue;
+  if ((a->mode == 6 || a->p_friedman) &&
+      (a->pods_b <= 0 || a->pods_c <= 0 || a->nb % a->pods_b || a->nc % a->pods_c || a->pods_b + a->pods_c > FM_WAVE))
+    return (int)hipErrorInvalidValue;
   dim3 grid((a->N + 3) / 4), block(256);
   hipLaunchKernelGGL(rank_tests_kernel, grid, block, lds, st, *a);
   return (int)hipGetLastError();

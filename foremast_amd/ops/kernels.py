@@ -12,7 +12,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 from dataclasses import dataclass
-from typing import Dict, Optional
+from typing import Tuple, Dict, Optional
 
 import torch
 
@@ -422,7 +422,12 @@ def window_stats(hist: torch.Tensor, head: int, length: int, det: DetectSpec,
 
 def rank_tests(base: torch.Tensor, cur: torch.Tensor, mode: int, alpha: float, min_mw: int = 20,
                min_wilcoxon: int = 20, min_kruskal: int = 5, want_pvals: bool = True,
-               out: Optional[Dict[str, torch.Tensor]] = None) -> Dict[str, torch.Tensor]:
+               out: Optional[Dict[str, torch.Tensor]] = None, pods: Optional[Tuple[int, int]] = None,
+               min_friedman: int = 5, want_friedman: bool = False) -> Dict[str, torch.Tensor]:
+    """K5/K11.  ``pods = (pods_b, pods_c)``: the pod-major window layout the
+    Friedman test blocks on (time slot x pod; default one pod per side).  The
+    Friedman statistic is computed for mode 6 (FRIEDMAN) or ``want_friedman``
+    (``out["friedman"]`` = [N, 2] p-value, complete blocks)."""
     lib = nat.require()
     _cuda(base, "base")
     _need(base.dim() == 2 and cur.dim() == 2 and base.shape[0] == cur.shape[0],
@@ -454,6 +459,15 @@ def rank_tests(base: torch.Tensor, cur: torch.Tensor, mode: int, alpha: float, m
     a.pvals = nat.ptr(out.get("pvals")) if want_pvals else 0
     a.counts = nat.ptr(out.get("counts")) if want_pvals else 0
     a.differs = nat.ptr(out["differs"])
+    pb, pc = pods if pods is not None else (1, 1)
+    fr = want_friedman or int(mode) == 6
+    if fr:
+        _need(pb >= 1 and pc >= 1 and nb % pb == 0 and nc % pc == 0 and pb + pc <= 64,
+              "Friedman needs pod-major windows (nb % pods_b == 0, nc % pods_c == 0, <= 64 pods)")
+        if "friedman" not in out:
+            out["friedman"] = torch.empty((N, 2), dtype=torch.float32, device=dev)
+    a.pods_b, a.pods_c, a.min_friedman = int(pb), int(pc), int(min_friedman)
+    a.p_friedman = nat.ptr(out["friedman"]) if fr else 0
     nat.check(lib.fm_rank_tests(a, nat.stream_handle(dev)), "fm_rank_tests")
     return out
 

@@ -56,6 +56,7 @@ class BrainConfig:
     min_mann_white: int = 20
     min_wilcoxon: int = 20
     min_kruskal: int = 5
+    min_friedman: int = 5  # complete time blocks (MIN_FRIEDMAN_DATA_POINTS; not in the reference env)
     max_stuck_seconds: float = 90.0
     pairwise_algorithm: str = "ALL"
     pairwise_threshold: float = 0.05
@@ -118,6 +119,7 @@ class BrainConfig:
         c.min_mann_white = int(f("MIN_MANN_WHITE_DATA_POINTS", c.min_mann_white, int))
         c.min_wilcoxon = int(f("MIN_WILCOXON_DATA_POINTS", c.min_wilcoxon, int))
         c.min_kruskal = int(f("MIN_KRUSKAL_DATA_POINTS", c.min_kruskal, int))
+        c.min_friedman = int(f("MIN_FRIEDMAN_DATA_POINTS", c.min_friedman, int))
         c.max_stuck_seconds = f("MAX_STUCK_IN_SECONDS", c.max_stuck_seconds)
         c.pairwise_algorithm = (e.get("ML_PAIRWISE_ALGORITHM") or c.pairwise_algorithm).upper()
         c.pairwise_threshold = f("ML_PAIRWISE_THRESHOLD", c.pairwise_threshold)

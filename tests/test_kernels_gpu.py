@@ -157,6 +157,37 @@ def test_rank_tests_kernel(K):
     assert agree > 0.99
 
 
+def test_rank_tests_kernel_friedman(K):
+    """Friedman mode (time slots x pods) against the reference, with ties,
+    incomplete blocks and a shifted canary."""
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(4)
+    N, P, W = 257, 5, 10
+    b = rng.normal(0, 1, (N, P * W)).astype(np.float32)
+    c = (rng.normal(0, 1, (N, P * W)) + rng.choice([0, 1.0], (N, 1))).astype(np.float32)
+    b[::5] = np.round(b[::5])
+    c[::5] = np.round(c[::5])
+    b[7, 3] = np.nan
+    c[11, 2 * W + 4] = np.nan
+    c[13, :] = np.nan
+    tb, tc = torch.tensor(b, device=dev), torch.tensor(c, device=dev)
+    out = K.rank_tests(tb, tc, pw_ref.PW_FRIEDMAN, 0.05, pods=(P, P), min_friedman=5)
+    torch.cuda.synchronize()
+    ref = pw_ref.rank_tests(torch.tensor(b, dtype=torch.float64), torch.tensor(c, dtype=torch.float64), pods=(P, P))
+    fr = out["friedman"].cpu().double()
+    np.testing.assert_array_equal(fr[:, 1].numpy(), ref.n_blocks.numpy())
+    np.testing.assert_allclose(fr[:, 0].numpy(), ref.p_friedman.numpy(), rtol=2e-3, atol=1e-5)
+    dref = pw_ref.pairwise_differs(ref, pw_ref.PW_FRIEDMAN, 0.05, min_friedman=5)
+    assert (out["differs"].cpu().bool() == dref).float().mean() > 0.99
+    assert 0 < int(dref.sum()) < N
+    # the other tests are unchanged when Friedman rides along
+    out2 = K.rank_tests(tb, tc, pw_ref.PW_ALL, 0.05, pods=(P, P), want_friedman=True)
+    out3 = K.rank_tests(tb, tc, pw_ref.PW_ALL, 0.05)
+    torch.cuda.synchronize()
+    assert torch.equal(out2["pvals"], out3["pvals"]) and torch.equal(out2["differs"], out3["differs"])
+    assert torch.equal(out2["friedman"], out["friedman"])
+
+
 def test_bivariate_kernel(K):
     dev = torch.device("cuda:0")
     rng = np.random.default_rng(4)

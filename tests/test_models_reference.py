@@ -116,6 +116,30 @@ def test_friedman_vs_scipy():
         assert p[i].item() == pytest.approx(exp, rel=1e-4)
 
 
+def test_friedman_pods_vs_scipy():
+    """Time slots x pods (2 baseline + 2 canary pods): scipy's friedmanchisquare
+    over the blocks valid in every pod."""
+    rng = np.random.default_rng(5)
+    N, Pb, Pc, W = 6, 2, 2, 12
+    b = rng.normal(0, 1, (N, Pb * W))
+    c = rng.normal(0.4, 1, (N, Pc * W))
+    b[1] = np.round(b[1])
+    c[1] = np.round(c[1])
+    b[2, 3] = np.nan      # slot 3 incomplete in series 2
+    c[3, W + 5] = np.nan  # slot 5 of canary pod 1 in series 3
+    p, nblk = pairwise.friedman_pods(torch.tensor(b), torch.tensor(c), Pb, Pc)
+    for i in range(N):
+        g = np.concatenate([b[i].reshape(Pb, W), c[i].reshape(Pc, W)], 0)  # [k, W]
+        ok = ~np.isnan(g).any(0)
+        exp = ss.friedmanchisquare(*[g[t, ok] for t in range(Pb + Pc)]).pvalue
+        assert int(nblk[i]) == int(ok.sum())
+        assert p[i].item() == pytest.approx(exp, rel=1e-5)
+    res = pairwise.rank_tests(torch.tensor(b), torch.tensor(c), pods=(Pb, Pc))
+    d = pairwise.pairwise_differs(res, pairwise.PW_FRIEDMAN, 0.05, min_friedman=5)
+    assert d.tolist() == ((p < 0.05) & (nblk >= 5)).tolist()
+    assert pairwise.PW_BY_NAME["FRIEDMAN"] == pairwise.PW_FRIEDMAN
+
+
 def test_pairwise_decision_modes():
     N = 4
     r = pairwise.PairwiseResult(

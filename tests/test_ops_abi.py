@@ -32,7 +32,7 @@ def test_struct_sizes(lib, name):
     ("SmoothArgs", "det"), ("SmoothArgs", "season_out"), ("SmoothArgs", "grid"),
     ("DetectArgs", "pw_scale"), ("DetectArgs", "app_stats"), ("DetectArgs", "ld_cur"),
     ("DetectArgs", "anom_count"), ("DetectArgs", "anom_cap"),
-    ("RankArgs", "pvals"), ("RankArgs", "alpha"), ("WindowArgs", "det"),
+    ("RankArgs", "pvals"), ("RankArgs", "alpha"), ("RankArgs", "p_friedman"), ("RankArgs", "pods_b"), ("WindowArgs", "det"),
     ("BivArgs", "eps"), ("BivArgs", "app_stats"),
 ])
 def test_struct_offsets(lib, name, field):
