@@ -2,7 +2,7 @@
 PY ?= python
 GPURUN ?= /usr/local/graft/bin/gpurun
 
-.PHONY: all build native test test-gpu bench deploy lint clean image
+.PHONY: all build native test test-gpu bench deploy lint clean image sanitize
 
 all: build test
 
@@ -16,6 +16,9 @@ test:             ## CPU suite (gloo for the multi-process paths)
 
 test-gpu:         ## GPU suite on an MI355X (run on the box)
 	$(PY) -m pytest tests -x -q -m gpu
+
+sanitize:         ## host parser under ASan + UBSan with the mutation harness (CPU)
+	$(PY) -m pytest tests/test_sanitizers.py -q
 
 bench:            ## headline benchmark, 1 GPU
 	$(PY) bench.py

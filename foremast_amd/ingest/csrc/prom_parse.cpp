@@ -43,7 +43,11 @@ bool skip_string(Cursor& c) {
   if (c.p >= c.e || *c.p != '"') return false;
   ++c.p;
   while (c.p < c.e) {
-    if (*c.p == '\\') { c.p += 2; continue; }
+    if (*c.p == '\\') {  // escape: the escaped byte must exist
+      if (c.e - c.p < 2) { c.p = c.e; return false; }
+      c.p += 2;
+      continue;
+    }
     if (*c.p == '"') { ++c.p; return true; }
     ++c.p;
   }
@@ -155,6 +159,7 @@ long long walk(const char* buf, long long len, OnSeries on_series, OnPoint on_po
             if (!c.eat(',')) return -10;
             c.ws();
             const char* v0 = c.p;
+            if (c.p >= c.e) return -11;
             if (*c.p == '"') { if (!skip_string(c)) return -11; } else { while (c.p < c.e && *c.p != ']') ++c.p; }
             double v;
             if (!parse_number(v0, c.p, v)) return -12;
