@@ -825,6 +825,35 @@ struct Chunk8f {
   }
 };
 
+// a + {pair[SEL], pair[SEL]}: VOP3P op_sel picks either 32-bit half of an aligned pair
+// for both lanes, so the odd elements of a float4 need no register copy (LLVM only
+// folds the even ones)
+template <int SEL>
+__device__ __forceinline__ v2f pk_add_bcast(v2f a, v2f pair) {
+  v2f r;
+  if (SEL == 0) asm("v_pk_add_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(r) : "v"(a), "v"(pair));
+  else asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(a), "v"(pair));
+  return r;
+}
+template <int R>
+__device__ __forceinline__ v2f chunk_pair(const Chunk8f& c) {
+  const float4 q = R < 4 ? c.lo : c.hi;
+  v2f p;
+  if ((R & 3) < 2) { p.x = q.x; p.y = q.y; } else { p.x = q.z; p.y = q.w; }
+  return p;
+}
+template <int R>
+__device__ __forceinline__ v2f add_dy(v2f d, const Chunk8f& c) { return pk_add_bcast<R & 1>(d, chunk_pair<R>(c)); }
+
+// end state of each half's season (lane 31 / lane 63) to every lane of the half:
+// one ds_bpermute per register (its latency hides under the next season's row rounds)
+__device__ __forceinline__ v2f half_last_bp(v2f x, int src_addr) {
+  v2f r;
+  r.x = __int_as_float(__builtin_amdgcn_ds_bpermute(src_addr, __float_as_int(x.x)));
+  r.y = __int_as_float(__builtin_amdgcn_ds_bpermute(src_addr, __float_as_int(x.y)));
+  return r;
+}
+
 // pass 1 of season 1: D_i = splat(D1_i), v = sum_i W_i D1_i
 template <int K>
 __device__ __forceinline__ void d_pass1(const float* blk, cfp W, v2f* D, v2f& p1, v2f& p2) {
@@ -846,6 +875,30 @@ __device__ __forceinline__ void d_pass1(const float* blk, cfp W, v2f* D, v2f& p1
       }
     }
     fence_sched();
+  }
+}
+
+// the 8 steps of chunk q (compile-time r: the Δ operand's register half is static)
+template <int K, bool FUSE, int R>
+__device__ __forceinline__ void d_steps(int q, const Chunk8f& cc, v2f* D, v2f c1, v2f c2, v2f g1a, const v2f* wc,
+                                        v2f& x1, v2f& x2, v2f& sse, v2f& p1, v2f& p2) {
+  if constexpr (R < 8) {
+    const int i = 8 * q + R;
+    if (i < K) {
+      const v2f e = D[i] - x1;
+      const v2f t = x1 + x2;
+      x1 = t + c1 * e;
+      x2 = x2 + c2 * e;
+      sse = sse + e * e;
+      if (FUSE) {
+        D[i] = add_dy<R>(D[i], cc) - g1a * e;
+        p1 = p1 + wc[2 * R] * D[i];
+        p2 = p2 + wc[2 * R + 1] * D[i];
+      } else if (i < HALF_HB) {
+        D[i] = D[i] - g1a * e;
+      }
+    }
+    d_steps<K, FUSE, R + 1>(q, cc, D, c1, c2, g1a, wc, x1, x2, sse, p1, p2);
   }
 }
 
@@ -882,24 +935,7 @@ __device__ __forceinline__ void d_pass2(const float* blk, v2f* D, v2f c1, v2f c2
       }
     }
     fence_sched();
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int i = 8 * q + r;
-      if (i < K) {
-        const v2f e = D[i] - x1;
-        const v2f t = x1 + x2;
-        x1 = t + c1 * e;
-        x2 = x2 + c2 * e;
-        sse = sse + e * e;
-        if (FUSE) {
-          D[i] = (D[i] + splat2(cc.get(r))) - g1a * e;
-          p1 = p1 + wc[2 * r] * D[i];
-          p2 = p2 + wc[2 * r + 1] * D[i];
-        } else if (i < HALF_HB) {
-          D[i] = D[i] - g1a * e;
-        }
-      }
-    }
+    d_steps<K, FUSE, 0>(q, cc, D, c1, c2, g1a, wc, x1, x2, sse, p1, p2);
     fence_sched();
   }
 }
@@ -1019,6 +1055,7 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
 
   const float l0 = half ? l0r[1] : l0r[0], b0 = half ? b0r[1] : b0r[0];
   const float* mydl = dl + (size_t)half * ns1 * SEA + j * 4;
+  const int last_addr = ((lane & 32) | 31) << 2;  // bpermute source: lane 31 / 63
   float bestSSE = __builtin_huge_valf();
   int bestIdx = 0x7fffffff;
   float bestL = l0, bestB = b0;
@@ -1050,15 +1087,15 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
       v2f x1, x2;
       half_uniform_scan_z(launder(tb), p1, p2, X1, X2, Bj, odd_row, x1, x2);
       d_pass2<K, true>(mydl + (size_t)sg * SEA, D, c1, c2, g1a, launder(W), x1, x2, sse, p1, p2);
-      X1 = half_last(x1, half);
-      X2 = half_last(x2, half);
+      X1 = half_last_bp(x1, last_addr);
+      X2 = half_last_bp(x2, last_addr);
     }
     {
       v2f x1, x2, d1, d2;
       half_uniform_scan_z(tb, p1, p2, X1, X2, Bj, odd_row, x1, x2);
       d_pass2<K, false>(mydl, D, c1, c2, g1a, W, x1, x2, sse, d1, d2);
-      X1 = half_last(x1, half);
-      X2 = half_last(x2, half);
+      X1 = half_last_bp(x1, last_addr);
+      X2 = half_last_bp(x2, last_addr);
     }
 #pragma unroll
     for (int o = 16; o > 0; o >>= 1) {
