@@ -485,6 +485,31 @@ __device__ __forceinline__ void half_uniform_scan_z(cfp tab_b, v2f v1, v2f v2, v
   s2 = s2 + w2;
 }
 
+// half_uniform_scan_z with B^1..B^8 already in registers (only B^16 is loaded here; it is
+// first used after the four row rounds)
+__device__ __forceinline__ void half_uniform_scan_pre(const Mat2* Bp, cfp tab_b, v2f v1, v2f v2, v2f x01, v2f x02,
+                                                      const Mat2& Bj, bool odd_row, v2f& s1, v2f& s2) {
+  const Mat2 B16 = ldmat(tab_b + 32);
+  v2f w1 = dppz2<0x111, 0xf>(v1);
+  v2f w2 = dppz2<0x111, 0xf>(v2);
+  row_round_z<0x111>(w1, w2, Bp[0]);
+  row_round_z<0x112>(w1, w2, Bp[1]);
+  row_round_z<0x114>(w1, w2, Bp[2]);
+  row_round_z<0x118>(w1, w2, Bp[3]);
+  v2f e1, e2;
+  matvec(Bp[0], w1, w2, e1, e2);
+  e1 = e1 + v1;
+  e2 = e2 + v2;
+  const v2f E1 = dppz2<0x142, 0xa>(e1), E2 = dppz2<0x142, 0xa>(e2);
+  v2f y1, y2;
+  matvec(B16, x01, x02, y1, y2);
+  y1 = odd_row ? y1 + E1 : x01;
+  y2 = odd_row ? y2 + E2 : x02;
+  matvec(Bj, y1, y2, s1, s2);
+  s1 = s1 + w1;
+  s2 = s2 + w2;
+}
+
 // General (per-lane matrix) exclusive affine scan within each 32-lane half.
 template <typename V>
 __device__ __forceinline__ void half_exclusive_scan(Aff<V>& a, int j) {
@@ -905,9 +930,13 @@ __device__ __forceinline__ void d_steps(int q, const Chunk8f& cc, v2f* D, v2f c1
 // pass 2 of a season from its true start state (x1, x2) = (f, b); FUSE: D advances to the
 // next season (dy block `blk`) and feeds that season's pass 1; !FUSE (last season): only
 // the first HALF_HB phases are advanced (they carry the forecast's seasonal terms).
+// FUSE also prefetches the next scan's B^1, B^2, B^4, B^8 (scalar loads) during the last
+// chunk, when the pass-1 weight registers of a next chunk are not needed: the scan then
+// starts without waiting on the scalar cache.
 template <int K, bool FUSE>
 __device__ __forceinline__ void d_pass2(const float* blk, v2f* D, v2f c1, v2f c2, v2f g1a, cfp W, v2f& x1,
-                                        v2f& x2, v2f& sse, v2f& p1, v2f& p2) {
+                                        v2f& x2, v2f& sse, v2f& p1, v2f& p2, cfp tb = nullptr,
+                                        Mat2* Bn = nullptr) {
   constexpr int NCH = (K + 7) / 8;
   if (FUSE) { p1 = splat2(0.f); p2 = splat2(0.f); }
   fence_sched();
@@ -932,10 +961,20 @@ __device__ __forceinline__ void d_pass2(const float* blk, v2f* D, v2f c1, v2f c2
 #pragma unroll
         for (int r = 0; r < 16; ++r)
           if (16 * (q + 1) + r < 2 * K) wn[r] = ldv2(W + 32 * (q + 1) + 2 * r);
+      } else if (Bn) {
+        tb = launder(tb);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) Bn[b] = ldmat(tb + 8 * b);
       }
     }
     fence_sched();
     d_steps<K, FUSE, 0>(q, cc, D, c1, c2, g1a, wc, x1, x2, sse, p1, p2);
+    fence_sched();
+  }
+  // retire the B prefetch here (it landed during the last chunk) so the wait the compiler
+  // needs for it is not placed after the caller's end-state ds_bpermutes
+  if (FUSE && Bn) {
+    asm volatile("" ::"s"(Bn[0].a.x), "s"(Bn[3].d.y));
     fence_sched();
   }
 }
@@ -1072,11 +1111,12 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
     const cfp tb = tab + PairTab<K>::B0;
     const v2f one = splat2(1.f), zero = splat2(0.f);
     Mat2 Bj;  // B^(lane & 15)
+    Mat2 Bp[4];  // B^1, B^2, B^4, B^8 of the next scan
     Bj.a = one; Bj.b = zero; Bj.c = zero; Bj.d = one;
 #pragma unroll
     for (int bit = 0; bit < 4; ++bit) {
-      const Mat2 Bb = ldmat(tb + 8 * bit);
-      const Mat2 r = matmul(Bj, Bb);
+      Bp[bit] = ldmat(tb + 8 * bit);
+      const Mat2 r = matmul(Bj, Bp[bit]);
       if ((lane >> bit) & 1) Bj = r;
     }
     v2f D[K];
@@ -1085,14 +1125,14 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
     d_pass1<K>(mydl, W, D, p1, p2);
     for (int sg = 1; sg < nseg - 1; ++sg) {
       v2f x1, x2;
-      half_uniform_scan_z(launder(tb), p1, p2, X1, X2, Bj, odd_row, x1, x2);
-      d_pass2<K, true>(mydl + (size_t)sg * SEA, D, c1, c2, g1a, launder(W), x1, x2, sse, p1, p2);
+      half_uniform_scan_pre(Bp, launder(tb), p1, p2, X1, X2, Bj, odd_row, x1, x2);
+      d_pass2<K, true>(mydl + (size_t)sg * SEA, D, c1, c2, g1a, launder(W), x1, x2, sse, p1, p2, tb, Bp);
       X1 = half_last_bp(x1, last_addr);
       X2 = half_last_bp(x2, last_addr);
     }
     {
       v2f x1, x2, d1, d2;
-      half_uniform_scan_z(tb, p1, p2, X1, X2, Bj, odd_row, x1, x2);
+      half_uniform_scan_pre(Bp, tb, p1, p2, X1, X2, Bj, odd_row, x1, x2);
       d_pass2<K, false>(mydl, D, c1, c2, g1a, W, x1, x2, sse, d1, d2);
       X1 = half_last_bp(x1, last_addr);
       X2 = half_last_bp(x2, last_addr);
