@@ -154,9 +154,18 @@ def setup_canary(args, world, rank, dev):
                      window=args.window, algorithm=args.algorithm, pairwise=args.pairwise,
                      dtype=dtype, n_apps=n_apps)
     app_id = (torch.arange(s, e, device=dev, dtype=torch.int64) // METRICS_PER_APP).to(torch.int32)
+    # shards are app-aligned, so each rank owns a disjoint slice of the app table: the
+    # health exchange is ONE all-gather of per-rank records the scorer writes in place
+    apps_per_rank = per // METRICS_PER_APP
+    agg = HealthAggregator(n_local, per, dev, apps_per_rank=apps_per_rank if world > 1 else None)
+    fused = {}
+    if agg.fused:
+        app_id = app_id - (s // METRICS_PER_APP)
+        spec.n_apps = apps_per_rank
+        fused = dict(app_stats=agg.app_stats_local, verdict_out=agg.verdict_local)
     shard = StreamingShard(spec, cfg, dev, app_id=app_id,
                            threshold=torch.full((n_local,), 4.0, device=dev),
-                           bound=torch.full((n_local,), 3, dtype=torch.int8, device=dev))
+                           bound=torch.full((n_local,), 3, dtype=torch.int8, device=dev), **fused)
     # --- synthetic data (outside the timed region) ---------------------------------
     params = synthetic_params(n_local, dev, seed=1234 + rank)
     hist = synthetic_eval(params, 0, args.ring, args.season, noise_seed=4321 + rank)
@@ -208,8 +217,9 @@ def setup_canary(args, world, rank, dev):
         if exch is not None:
             base_dev.copy_(base_host[k], non_blocking=pin)
             newb.index_copy_(0, local_rows, exch(base_dev))  # RC5: baseline windows to their owners
-    agg = HealthAggregator(n_local, per, dev)
-    health_host = torch.empty_like(shard.app_stats, device="cpu")
+    # host copy of the node health table (fused: the whole gathered record buffer)
+    health_src = agg.recv if agg.fused else shard.app_stats
+    health_host = torch.empty_like(health_src, device="cpu")
     if pin:
         health_host = health_host.pin_memory()
     # prefill the current window so every tick scores a full 10-minute window
@@ -222,7 +232,7 @@ def setup_canary(args, world, rank, dev):
         shard.ingest_tick(newv, newb)
         out = shard.score()
         stats, _ = agg.tick(shard.app_stats, out["verdict"])
-        health_host.copy_(stats, non_blocking=pin)
+        health_host.copy_(agg.recv if agg.fused else stats, non_blocking=pin)
         if dev.type == "cuda":
             torch.cuda.current_stream().synchronize()
         return out
@@ -236,7 +246,10 @@ def setup_canary(args, world, rank, dev):
         "current_window": W,
         "grid_points": int(shard.grid.shape[0]),
         "multi_cluster": bool(args.multi_cluster),
+        "health_collectives": "1 fused all_gather" if agg.fused else ("all_reduce + all_gather" if world > 1 else "none"),
     }
+    if agg.fused:
+        meta["_table"] = lambda h: HealthAggregator.host_app_table(h, world, apps_per_rank)
     dt = "bf16" if dtype == torch.bfloat16 else "fp32"
     meta["_agg"] = agg
     return tick, health_host, meta, dt, args.series
@@ -398,6 +411,7 @@ def main():
         tick, health_host, meta, dtype_name, n_series = setup_lstm(args, world, rank, dev, 2, True)
 
     agg = meta.pop("_agg", None)
+    table = meta.pop("_table", None)
     for k in range(args.warmup):
         tick(k)
     if agg is not None:
@@ -424,6 +438,8 @@ def main():
     elapsed = float(el.item())
     lat_ms = lat_t.cpu().numpy() * 1e3
     coll_ms = agg.flush_timings() if agg is not None else []
+    if table is not None:
+        health_host = table(health_host)
     anomalous_apps = int((health_host[:, 0] > 0).sum())
     scored = int(health_host[:, 1].sum())
     if rank == 0:
@@ -449,7 +465,8 @@ def main():
             "config": config,
             "p50_detect_latency_ms": round(float(np.percentile(lat_ms, 50)), 3),
             "p99_detect_latency_ms": round(float(np.percentile(lat_ms, 99)), 3),
-            # device time of the per-tick health collectives (RC2 all-reduce + RC1 all-gather), rank 0
+            # device time of the per-tick health collectives (fused all-gather, or RC2 all-reduce +
+            # RC1 all-gather), rank 0
             "collective_ms_p50": round(float(np.percentile(coll_ms, 50)), 4) if coll_ms else None,
             "health": {"apps": int(health_host.shape[0]), "anomalous_apps": anomalous_apps,
                        "series_scored_last_tick": scored},

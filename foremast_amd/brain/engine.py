@@ -54,7 +54,10 @@ class ShardSpec:
 class StreamingShard:
     def __init__(self, spec: ShardSpec, cfg: Optional[BrainConfig] = None, device="cpu",
                  app_id: Optional[torch.Tensor] = None, threshold: Optional[torch.Tensor] = None,
-                 bound: Optional[torch.Tensor] = None, min_lower: Optional[torch.Tensor] = None) -> None:
+                 bound: Optional[torch.Tensor] = None, min_lower: Optional[torch.Tensor] = None,
+                 app_stats: Optional[torch.Tensor] = None, verdict_out: Optional[torch.Tensor] = None) -> None:
+        """``app_stats`` / ``verdict_out``: optional caller-owned outputs (e.g. the
+        fused health record of :class:`HealthAggregator`) the tick writes in place."""
         self.spec = spec
         self.cfg = cfg or BrainConfig()
         self.device = torch.device(device)
@@ -70,7 +73,13 @@ class StreamingShard:
         self.min_lower = (min_lower if min_lower is not None
                           else torch.full((N,), self.cfg.min_lower_bound, dtype=torch.float32, **kw))
         self.app_id = app_id if app_id is not None else torch.zeros(N, dtype=torch.int32, **kw)
-        self.app_stats = torch.zeros((max(spec.n_apps, 1), 2), dtype=torch.int32, **kw)
+        if app_stats is not None:
+            if app_stats.dtype != torch.int32 or app_stats.dim() != 2 or app_stats.shape[1] != 2 \
+                    or not app_stats.is_contiguous() or app_stats.device != self.device:
+                raise ValueError("app_stats must be contiguous int32 [A, 2] on the shard's device")
+            self.app_stats = app_stats
+        else:
+            self.app_stats = torch.zeros((max(spec.n_apps, 1), 2), dtype=torch.int32, **kw)
         if N and app_id is not None:
             lo, hi = int(self.app_id.min()), int(self.app_id.max())  # one-time sync at setup
             if lo < 0 or hi >= self.app_stats.shape[0]:
@@ -86,6 +95,11 @@ class StreamingShard:
         if self.gpu:
             self._h_pinned = torch.empty(C, dtype=torch.int32).pin_memory()
         self.out: Dict[str, torch.Tensor] = {}
+        self._verdict_out = verdict_out
+        if verdict_out is not None:
+            if verdict_out.dtype != torch.int8 or verdict_out.shape != (N,) or verdict_out.device != self.device:
+                raise ValueError(f"verdict_out must be int8 [{N}] on the shard's device")
+            self.out["verdict"] = verdict_out
         self.pw_out: Dict[str, torch.Tensor] = {}
         # K9: compacted anomalous points of the current window (GPU), enabled via enable_anomaly_list()
         self.anomalies = None
@@ -204,8 +218,11 @@ class StreamingShard:
         self.app_stats.index_put_((self.app_id.long(), torch.zeros_like(v)), (v == 1).int(), accumulate=True)
         self.app_stats.index_put_((self.app_id.long(), torch.ones_like(v)), (v >= 0).int(), accumulate=True)
         del valid_hist
+        verdict = d.verdict
+        if self._verdict_out is not None:
+            verdict = self._verdict_out.copy_(d.verdict)
         self.out = dict(extra, forecast=f, upper=d.upper, lower=d.lower, count=d.count,
-                        verdict=d.verdict, score=d.score)
+                        verdict=verdict, score=d.score)
         return self.out
 
 

@@ -10,10 +10,17 @@ contributes:
   verdict table so any rank can answer a status lookup for any series.
 
 Both messages are < 1 MB even at 100k series, i.e. latency bound on xGMI
-(7 links x ~153 GB/s per GPU); they are issued back-to-back on the compute
-stream so RCCL pipelines them, and the whole tick is graph-capturable.
-With ``world_size == 1`` both are no-ops.  The ``gloo`` backend runs the same
-code on CPU for tests.
+(7 links x ~153 GB/s per GPU).  With ``world_size == 1`` both are no-ops.  The
+``gloo`` backend runs the same code on CPU for tests.
+
+Fused mode (``apps_per_rank``): when every app's series live on one rank
+(app-aligned contiguous shards, the streaming engine's layout) the per-app
+counters need no reduction — each rank owns a disjoint slice of the app table.
+Then RC1 + RC2 are ONE ``all_gather`` per tick of a per-rank record
+``[apps_per_rank x 2 int32 | verdict bytes]`` (~32 KB per rank at 100k series
+over 8 GPUs), and the scorer writes its counters and verdicts straight into the
+send record (``app_stats_local`` / ``verdict_local``), so the tick packs
+nothing.  The gathered buffer ``recv`` is the whole node's health table.
 """
 
 from __future__ import annotations
@@ -31,7 +38,7 @@ def _active() -> bool:
 
 class HealthAggregator:
     def __init__(self, n_series_local: int, n_series_padded: Optional[int] = None, device="cpu",
-                 group=None, metrics=None) -> None:
+                 group=None, metrics=None, apps_per_rank: Optional[int] = None) -> None:
         self.group = group
         self.metrics = metrics          # BrainMetrics: foremast_collective_seconds histogram
         self.timings_ms: List[float] = []  # per tick, resolved one tick late (no host sync)
@@ -41,6 +48,20 @@ class HealthAggregator:
         self.n_local = n_series_local
         self.n_pad = n_series_padded or n_series_local
         dev = torch.device(device)
+        self.fused = apps_per_rank is not None and self.world > 1
+        if self.fused:
+            self.apr = int(apps_per_rank)
+            vw = (self.n_pad + 3) // 4
+            self.chunk = 2 * self.apr + vw  # int32 words per rank record
+            self.send = torch.zeros(self.chunk, dtype=torch.int32, device=dev)
+            self.send[2 * self.apr:].view(torch.int8).fill_(-1)  # padded series: no verdict
+            self.recv = torch.zeros(self.world * self.chunk, dtype=torch.int32, device=dev)
+            self.app_stats_local = self.send[: 2 * self.apr].view(self.apr, 2)
+            self.verdict_local = self.send[2 * self.apr:].view(torch.int8)[: self.n_local]
+            rec = self.recv.view(self.world, self.chunk)
+            self.apps_all = rec[:, : 2 * self.apr].reshape(self.world, self.apr, 2)  # strided view
+            self.verdicts_all = rec[:, 2 * self.apr:].view(torch.int8)[:, : self.n_pad]
+            return
         self.verdict_pad = torch.full((self.n_pad,), -1, dtype=torch.int8, device=dev)
         self.verdict_all = torch.empty((self.n_pad * self.world,), dtype=torch.int8, device=dev)
 
@@ -80,10 +101,25 @@ class HealthAggregator:
         if self.metrics is not None:
             self.metrics.collective.observe(ms / 1e3)
 
+    def _gather_fused(self, app_stats: torch.Tensor, verdict: torch.Tensor):
+        if app_stats.data_ptr() != self.app_stats_local.data_ptr():
+            self.app_stats_local.copy_(app_stats)
+        if verdict.data_ptr() != self.verdict_local.data_ptr():
+            self.verdict_local.copy_(verdict)
+        dist.all_gather_into_tensor(self.recv, self.send, group=self.group)
+        return self.apps_all, self.verdicts_all
+
+    @staticmethod
+    def host_app_table(recv_host: torch.Tensor, world: int, apps_per_rank: int) -> torch.Tensor:
+        """``[world * apps_per_rank, 2]`` app table from a host copy of ``recv``."""
+        return recv_host.view(world, -1)[:, : 2 * apps_per_rank].reshape(-1, 2)
+
     def tick(self, app_stats: torch.Tensor, verdict: torch.Tensor):
-        """RC2 + RC1 for one scoring tick.  Their duration (device time between
-        events around the two collectives) is recorded without a host sync and
-        read back on the next tick (``timings_ms``, ``foremast_collective_seconds``)."""
+        """RC2 + RC1 for one scoring tick (one fused all-gather in fused mode:
+        returns the ``[world, apps_per_rank, 2]`` app table and ``[world, n_pad]``
+        verdict views of ``recv``).  Their duration (device time between events
+        around the collectives) is recorded without a host sync and read back on
+        the next tick (``timings_ms``, ``foremast_collective_seconds``)."""
         self._resolve()
         cuda = app_stats.is_cuda
         if cuda:
@@ -91,7 +127,10 @@ class HealthAggregator:
             ev0.record()
         else:
             t0 = time.perf_counter()
-        out = self.reduce_apps(app_stats), self.gather_verdicts(verdict)
+        if self.fused:
+            out = self._gather_fused(app_stats, verdict)
+        else:
+            out = self.reduce_apps(app_stats), self.gather_verdicts(verdict)
         if cuda:
             ev1.record()
             self._pending = (ev0, ev1)

@@ -73,6 +73,56 @@ def test_health_aggregation_gloo():
         assert len(valid) == 23
 
 
+def _fused_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n_total, mpa = 23, 5
+        s, e, per = shard_range(n_total, world, rank, align=mpa)
+        n = e - s
+        agg = HealthAggregator(n, per, "cpu", apps_per_rank=per // mpa)
+        assert agg.fused
+        # the scorer writes straight into the send record (local app ids)
+        app = torch.arange(s, e) // mpa - s // mpa
+        verdict = torch.tensor([1 if (i % 7 == 0) else 0 for i in range(s, e)], dtype=torch.int8)
+        agg.verdict_local.copy_(verdict)
+        for a, v in zip(app.tolist(), verdict.tolist()):
+            agg.app_stats_local[a, 0] += int(v == 1)
+            agg.app_stats_local[a, 1] += 1
+        apps, verd = agg.tick(agg.app_stats_local, agg.verdict_local)
+        table = HealthAggregator.host_app_table(agg.recv.clone(), world, per // mpa)
+        q.put((rank, apps.reshape(-1, 2).tolist(), table.tolist(), verd.tolist(), per))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_health_aggregation_fused_gloo():
+    """Fused mode: one all-gather of [app slice | verdict bytes] records gives the
+    same node table as all-reduce + all-gather."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fused_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    exp = [[0, 0] for _ in range(5)]
+    for i in range(23):
+        exp[i // 5][0] += int(i % 7 == 0)
+        exp[i // 5][1] += 1
+    for rank, apps, table, verd, per in res:
+        apr = per // 5
+        assert apps == table
+        assert table[:5] == exp and all(r == [0, 0] for r in table[5:])
+        assert len(table) == world * apr
+        got = [v for row in verd for v in row]
+        assert sorted(v for v in got if v != -1) == sorted(1 if i % 7 == 0 else 0 for i in range(23))
+
+
 def test_shard_range_alignment():
     world = 8
     spans = [shard_range(100_000, world, r, align=5) for r in range(world)]
