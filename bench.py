@@ -229,8 +229,11 @@ def setup_canary(args, world, rank, dev):
 
     def tick(k):
         load_tick(W + k)
-        shard.ingest_tick(newv, newb)
-        out = shard.score()
+        if args.graph:
+            out = shard.tick_graph(newv, newb)  # ingest + score as one HIP-graph replay
+        else:
+            shard.ingest_tick(newv, newb)
+            out = shard.score()
         stats, _ = agg.tick(shard.app_stats, out["verdict"])
         health_host.copy_(agg.recv if agg.fused else stats, non_blocking=pin)
         if dev.type == "cuda":
@@ -247,6 +250,7 @@ def setup_canary(args, world, rank, dev):
         "grid_points": int(shard.grid.shape[0]),
         "multi_cluster": bool(args.multi_cluster),
         "health_collectives": "1 fused all_gather" if agg.fused else ("all_reduce + all_gather" if world > 1 else "none"),
+        "hip_graph": bool(args.graph and dev.type == "cuda"),
     }
     if agg.fused:
         meta["_table"] = lambda h: HealthAggregator.host_app_table(h, world, apps_per_rank)

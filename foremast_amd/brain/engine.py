@@ -103,6 +103,12 @@ class StreamingShard:
         self.pw_out: Dict[str, torch.Tensor] = {}
         # K9: compacted anomalous points of the current window (GPU), enabled via enable_anomaly_list()
         self.anomalies = None
+        # HIP-graph tick (tick_graph): per-tick ring state lives in device memory
+        self._graph = None
+        self._graph_io = None
+        if self.gpu:
+            self._state_host = torch.zeros(8, dtype=torch.int32).pin_memory()
+            self._state_dev = torch.zeros(8, dtype=torch.int32, device=self.device)
 
     def enable_anomaly_list(self, cap: int) -> None:
         if self.gpu:
@@ -146,6 +152,52 @@ class StreamingShard:
             self.hist.advance(1)
         self._refresh_horizons()
 
+    # ------------------------------------------------------------------ graph tick
+    def graph_ready(self) -> bool:
+        """The steady state a captured tick assumes: GPU, full ring (head
+        advances by one per tick), warm window (every tick graduates), the
+        two-series-per-wave Holt-Winters path, no anomaly list."""
+        return (self.gpu and self.mode == sm_ref.MODE_HW and self.hist.length == self.hist.R
+                and self.cur.ticks >= self.cur.W and self.anomalies is None
+                and getattr(self, "_hw_variant", None) in (4, 5) and bool(self.out))
+
+    def tick_graph(self, newv: torch.Tensor, newb: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+        """``ingest_tick`` + ``score`` as ONE HIP-graph replay.
+
+        The graph (captured on the first steady-state call) holds the ingest
+        kernel, the app-counter reset, the rank tests and the Holt-Winters fit;
+        the ring head / hist column / window slot reach the kernels through a
+        device int32 record written from pinned memory before each replay, and
+        the horizons through their usual pinned copy.  Falls back to the eager
+        calls until :meth:`graph_ready`.  ``newv`` / ``newb`` must be the same
+        buffers on every call (their addresses are baked into the graph)."""
+        if not self.graph_ready():
+            self.ingest_tick(newv, newb)
+            return self.score()
+        from ..ops import kernels as K
+        io = (newv.data_ptr(), None if newb is None else newb.data_ptr())
+        if self._graph is not None and io != self._graph_io:
+            raise ValueError("tick_graph needs the same newv/newb buffers on every call")
+        st = self._state_host
+        st[0] = self.hist.next_col()
+        st[1] = self.cur.slot()
+        st[2] = 1
+        self.hist.advance(1)
+        self.cur.ticks += 1
+        st[3] = self.hist.head
+        self._state_dev.copy_(st, non_blocking=True)
+        self._refresh_horizons()
+        if self._graph is None:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                K.tick_ingest(self.hist.data, 0, self.cur.data, self.cur.P, self.cur.W, 0, newv,
+                              base=self.base if newb is not None else None, newb=newb, state=self._state_dev)
+                self.app_stats.zero_()
+                self._score_gpu(head_dev=self._state_dev[3:4])
+            self._graph, self._graph_io = g, io
+        self._graph.replay()
+        return self.out
+
     # ------------------------------------------------------------------ scoring
     def score(self) -> Dict[str, torch.Tensor]:
         self.app_stats.zero_()
@@ -153,7 +205,7 @@ class StreamingShard:
             return self._score_gpu()
         return self._score_cpu()
 
-    def _score_gpu(self) -> Dict[str, torch.Tensor]:
+    def _score_gpu(self, head_dev: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
         from ..ops import kernels as K
         cfg = self.cfg
         differs = None
@@ -173,7 +225,8 @@ class StreamingShard:
         h = self.hist
         if self.mode is not None:
             self.out = K.smoothing_fit(h.data, h.head, h.length, self.mode, self.spec.season, self.grid,
-                                       spec, out=self.out)
+                                       spec, out=self.out, head_dev=head_dev)
+            self._hw_variant = K.last_hw_variant
         elif self.algorithm in ("moving_average_all", "moving_average"):
             length = h.length
             head = h.head

@@ -47,7 +47,7 @@ class SmoothArgs(C.Structure):
         ("hist", P), ("ld", LL), ("ring_len", I), ("head", I), ("T", I), ("Tp", I),
         ("pad", I), ("m", I), ("K", I), ("seg", I), ("grid", P), ("G", I), ("N", I),
         ("level", P), ("trend", P), ("sigma", P), ("best", P), ("season_out", P),
-        ("pair_tab", P), ("det", DetectArgs),
+        ("pair_tab", P), ("det", DetectArgs), ("head_dev", P),
     ]
 
 
@@ -108,6 +108,8 @@ def _declare(lib: C.CDLL) -> None:
     lib.fm_ring_append.restype = I
     lib.fm_tick_ingest.argtypes = [P, LL, I, P, LL, I, I, I, P, LL, I, I, P, P, I, P]
     lib.fm_tick_ingest.restype = I
+    lib.fm_tick_ingest_dev.argtypes = [P, LL, P, LL, I, I, P, LL, I, P, P, I, P, P]
+    lib.fm_tick_ingest_dev.restype = I
     for name, args in _EXTRA.items():
         fn = getattr(lib, name, None)
         if fn is not None:

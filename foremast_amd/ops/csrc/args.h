@@ -57,6 +57,7 @@ struct SmoothArgs {
   float* season_out;    // [N, m] or null
   const float* pair_tab;  // per combo-pair precomputed table (hw_scan variant 3) or null
   DetectArgs det;
+  const int* head_dev;  // HW variants 4/5: if set, `head` is read from device memory (HIP-graph replays)
 };
 
 struct RankArgs {

@@ -568,6 +568,7 @@ __device__ __forceinline__ void hw_half_block(const SmoothArgs& a, int hmax, int
   float* wbest = (float*)(fm_hw_smem + off);
 
   for (int i = tid; i < 2 * nseg + 2; i += blockDim.x) segnan[i] = 0;  // also nvs = 0.f
+  const int head = a.head_dev ? *a.head_dev : a.head;
   __syncthreads();
 
   // ---- stage both series: logical padded index p = pk*K + i, pk = sg*32 + lane -------
@@ -589,7 +590,7 @@ __device__ __forceinline__ void hw_half_block(const SmoothArgs& a, int hmax, int
           v[u] = 0x7fc0;
           const int t = p - a.pad;
           if (t >= 0) {
-            int c = a.head + t;
+            int c = head + t;
             if (c >= a.ring_len) c -= a.ring_len;
             v[u] = row[c];
           }
@@ -999,6 +1000,7 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
   float* wbest = bests + 4 * 2 * HALF_HB;
 
   for (int i = tid; i < 2 * NMW + 8 + 4; i += blockDim.x) vmask[i] = 0u;  // vmask, stat, flag
+  const int head = a.head_dev ? *a.head_dev : a.head;
   __syncthreads();
 
   // ---- stage: one thread per (series, 8 consecutive phases), all seasons of them in ------
@@ -1023,7 +1025,7 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
           const bool ok = real && k < nseg && o0 + u < m;
           const int t = k * m + o0 + u - a.pad;
           const bool pos = t >= 0;
-          int c = a.head + ((ok && pos) ? t : 0);
+          int c = head + ((ok && pos) ? t : 0);
           c -= (c >= a.ring_len) ? a.ring_len : 0;
           const float v = bf16_to_f32(row[c]);
           // the padding series of an odd N is zeros (keeps the pair on the fast path)

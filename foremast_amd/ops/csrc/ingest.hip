@@ -17,9 +17,15 @@ __global__ __launch_bounds__(256) void tick_ingest_kernel(TH* __restrict__ hist,
                                                           float* __restrict__ cur, long long ld_c, int P, int W,
                                                           int slot, const float* __restrict__ newv,
                                                           long long ld_n, int N, int graduate,
-                                                          float* __restrict__ base, const float* __restrict__ newb) {
+                                                          float* __restrict__ base, const float* __restrict__ newb,
+                                                          const int* __restrict__ st) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
+  if (st) {  // per-tick ring state from device memory (HIP-graph replays): {hist_col, slot, graduate}
+    hist_col = st[0];
+    slot = st[1];
+    graduate = st[2];
+  }
   if (base) {
     float* brow = base + (long long)n * ld_c;
     const float* nb = newb + (long long)n * ld_n;
@@ -37,17 +43,33 @@ __global__ __launch_bounds__(256) void tick_ingest_kernel(TH* __restrict__ hist,
   if (graduate) hist[(long long)n * ld_h + hist_col] = from_f32<TH>(c > 0.f ? s / c : fm_nan());
 }
 
-extern "C" int fm_tick_ingest(void* hist, long long ld_h, int hist_col, float* cur, long long ld_c, int P,
+static int tick_ingest_launch(void* hist, long long ld_h, int hist_col, float* cur, long long ld_c, int P,
                               int W, int slot, const float* newv, long long ld_n, int N, int graduate,
-                              float* base, const float* newb, int bf16, hipStream_t st) {
+                              float* base, const float* newb, int bf16, const int* state, hipStream_t st) {
   if (N <= 0) return 0;
   if (P <= 0 || W <= 0 || slot < 0 || slot >= W || hist_col < 0) return (int)hipErrorInvalidValue;
   dim3 grid((N + 255) / 256), block(256);
   if (bf16)
     hipLaunchKernelGGL(tick_ingest_kernel<bf16_t>, grid, block, 0, st, (bf16_t*)hist, ld_h, hist_col, cur,
-                       ld_c, P, W, slot, newv, ld_n, N, graduate, base, newb);
+                       ld_c, P, W, slot, newv, ld_n, N, graduate, base, newb, state);
   else
     hipLaunchKernelGGL(tick_ingest_kernel<float>, grid, block, 0, st, (float*)hist, ld_h, hist_col, cur, ld_c,
-                       P, W, slot, newv, ld_n, N, graduate, base, newb);
+                       P, W, slot, newv, ld_n, N, graduate, base, newb, state);
   return (int)hipGetLastError();
+}
+
+extern "C" int fm_tick_ingest(void* hist, long long ld_h, int hist_col, float* cur, long long ld_c, int P,
+                              int W, int slot, const float* newv, long long ld_n, int N, int graduate,
+                              float* base, const float* newb, int bf16, hipStream_t st) {
+  return tick_ingest_launch(hist, ld_h, hist_col, cur, ld_c, P, W, slot, newv, ld_n, N, graduate, base, newb,
+                            bf16, nullptr, st);
+}
+
+// graph-replayable form: hist_col / slot / graduate are read from `state` (device int32
+// {hist_col, slot, graduate}, valid ranges are the caller's contract: hist_col < R, slot < W)
+extern "C" int fm_tick_ingest_dev(void* hist, long long ld_h, float* cur, long long ld_c, int P, int W,
+                                  const float* newv, long long ld_n, int N, float* base, const float* newb,
+                                  int bf16, const int* state, hipStream_t st) {
+  if (!state) return (int)hipErrorInvalidValue;
+  return tick_ingest_launch(hist, ld_h, 0, cur, ld_c, P, W, 0, newv, ld_n, N, 1, base, newb, bf16, state, st);
 }

@@ -262,7 +262,10 @@ def smoothing_supported(mode: int, T: int, m: int, bf16: bool) -> bool:
 def smoothing_fit(hist: torch.Tensor, head: int, length: int, mode: int, m: int,
                   grid: torch.Tensor, det: DetectSpec, K: Optional[int] = None,
                   want_season: bool = False, out: Optional[Dict[str, torch.Tensor]] = None,
-                  variant: Optional[int] = None) -> Dict[str, torch.Tensor]:
+                  variant: Optional[int] = None, head_dev: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+    """``head_dev`` (int32 device scalar): the ring head is read from device memory
+    at run time (HIP-graph replays); only the two-series-per-wave HW variants
+    (4/5) support it — other paths raise."""
     lib = nat.require()
     _hist_check(hist, head, length)
     dev = hist.device
@@ -282,9 +285,11 @@ def smoothing_fit(hist: torch.Tensor, head: int, length: int, mode: int, m: int,
                 and hmax is not None and 1 <= hmax <= min(mm // 32, HALF_HB) and K is None
                 and lib.fm_hw_half_lds_bytes(Tp, mm, mm // 32) <= LDS_LIMIT):
             if variant == 5 and lib.fm_hw_d_lds_bytes(Tp, mm, mm // 32) <= D_LDS_LIMIT:
-                return _hw_half_fit(lib, hist, head, length, mm, grid, det, Tp, pad, hmax, out, residual=True)
-            return _hw_half_fit(lib, hist, head, length, mm, grid, det, Tp, pad, hmax, out)
+                return _hw_half_fit(lib, hist, head, length, mm, grid, det, Tp, pad, hmax, out, residual=True,
+                                    head_dev=head_dev)
+            return _hw_half_fit(lib, hist, head, length, mm, grid, det, Tp, pad, hmax, out, head_dev=head_dev)
         variant = 3
+    _need(head_dev is None, "head_dev needs HW variant 4/5 geometry")
     fast_lds = lib.fm_hw_scan_lds_bytes(Tp, seg, k, int(mode), int(bf16))
     if variant >= 0 and not (seg % k == 0 and seg // k <= 64 and fast_lds <= LDS_LIMIT):
         variant = -1
@@ -343,7 +348,8 @@ def _half_workspace(dev, N: int) -> torch.Tensor:
     return ws
 
 
-def _hw_half_fit(lib, hist, head, length, m, grid, det, Tp, pad, hmax, out, residual: bool = False):
+def _hw_half_fit(lib, hist, head, length, m, grid, det, Tp, pad, hmax, out, residual: bool = False,
+                 head_dev: Optional[torch.Tensor] = None):
     """Variants 4/5 of the Holt-Winters fit: two series per wave, season = 32
     lanes x K steps.  Variant 4 (hw_scan.hip ``hw_half_kernel``) walks the
     seasonal state over a bf16 image; variant 5 (``residual``, ``hw_d_kernel``)
@@ -380,6 +386,10 @@ def _hw_half_fit(lib, hist, head, length, m, grid, det, Tp, pad, hmax, out, resi
     a.best = nat.ptr(out["best"])
     a.season_out = 0
     a.pair_tab = nat.ptr(pair_table(grid, k))
+    if head_dev is not None:
+        _need(head_dev.dtype == torch.int32 and head_dev.device == dev and head_dev.numel() >= 1,
+              "head_dev must be an int32 device scalar")
+        a.head_dev = nat.ptr(head_dev)
     _fill_detect(a.det, det, N, dev, out)
     ws = _half_workspace(dev, N)
     global last_hw_variant
@@ -533,9 +543,11 @@ def ring_append(dst: torch.Tensor, col0: int, src: torch.Tensor) -> None:
 
 def tick_ingest(hist: torch.Tensor, hist_col: int, cur: torch.Tensor, P: int, W: int, slot: int,
                 newv: torch.Tensor, graduate: bool = True, base: Optional[torch.Tensor] = None,
-                newb: Optional[torch.Tensor] = None) -> None:
+                newb: Optional[torch.Tensor] = None, state: Optional[torch.Tensor] = None) -> None:
     """Per-tick streaming ingest (see csrc/ingest.hip); ``newv``/``newb`` are
-    ``[N, P]`` (same row stride) current/baseline pod values."""
+    ``[N, P]`` (same row stride) current/baseline pod values.  ``state``: int32
+    device ``{hist_col, slot, graduate}`` read at run time instead of the scalar
+    arguments (HIP-graph replays; the caller keeps them in range)."""
     lib = nat.require()
     _cuda(hist, "hist")
     N = hist.shape[0]
@@ -552,6 +564,15 @@ def tick_ingest(hist: torch.Tensor, hist_col: int, cur: torch.Tensor, P: int, W:
               and base.dtype == torch.float32 and base.device == cur.device, "base must match cur")
         _need(newb.shape == newv.shape and newb.stride() == newv.stride() and newb.dtype == torch.float32
               and newb.device == newv.device, "newb must match newv")
+    if state is not None:
+        _need(state.dtype == torch.int32 and state.device == hist.device and state.numel() >= 3,
+              "state must be int32 {hist_col, slot, graduate} on the device")
+        nat.check(lib.fm_tick_ingest_dev(nat.ptr(hist), hist.stride(0), nat.ptr(cur), cur.stride(0), int(P), int(W),
+                                         nat.ptr(newv), newv.stride(0), N, nat.ptr(base),
+                                         nat.ptr(newb) if base is not None else 0,
+                                         int(hist.dtype == torch.bfloat16), nat.ptr(state),
+                                         nat.stream_handle(hist.device)), "fm_tick_ingest_dev")
+        return
     nat.check(lib.fm_tick_ingest(nat.ptr(hist), hist.stride(0), int(hist_col), nat.ptr(cur), cur.stride(0),
                                  int(P), int(W), int(slot), nat.ptr(newv), newv.stride(0), N, int(graduate),
                                  nat.ptr(base), nat.ptr(newb) if base is not None else 0,

@@ -89,3 +89,43 @@ def test_streaming_monitor_continuous_jobs(where, algorithm):
     text = metrics.registry and __import__("prometheus_client").generate_latest(metrics.registry).decode()
     assert "foremastbrain:namespace_app_per_pod:http_server_requests_error_5xx_upper" in text
     assert is_continuous({"strategy": "Continuous"})
+
+
+@pytest.mark.gpu
+def test_graph_tick_matches_eager():
+    """tick_graph (ingest + rank tests + HW fit as one HIP-graph replay, ring state
+    read from device memory) gives the same outputs as the eager calls, tick for
+    tick, through the ring wrap and the window slot cycle."""
+    from foremast_amd.brain.engine import ShardSpec, StreamingShard, synthetic_history
+    from foremast_amd.ops import _native
+    from foremast_amd.utils.config import BrainConfig
+    _native.require()
+    dev = torch.device("cuda:0")
+    n, R, m, P, W = 64, 2880, 1440, 3, 6
+    cfg = BrainConfig()
+    cfg.min_historical_points = 0
+    shards = []
+    hist = synthetic_history(n, R + 40, m, dev, seed=3)
+    for _ in range(2):
+        sh = StreamingShard(ShardSpec(n_series=n, ring_len=R, season=m, pods=P, window=W, n_apps=8), cfg, dev,
+                            app_id=(torch.arange(n, device=dev) % 8).int())
+        sh.load_history(hist[:, :R])
+        sh.set_baseline(hist[:, R - W:R].repeat(1, P).float())
+        shards.append(sh)
+    eager, graph = shards
+    newv = torch.empty((n, P), device=dev)
+    replays = 0
+    for k in range(30):
+        newv.copy_(hist[:, R + k:R + k + 1].repeat(1, P).float() * (1.0 + 0.3 * (k % 7 == 3)))
+        eager.ingest_tick(newv)
+        oe = {key: v.clone() for key, v in eager.score().items()}
+        se = eager.app_stats.clone()
+        replays += graph._graph is not None
+        og = graph.tick_graph(newv)
+        torch.cuda.synchronize()
+        for key in ("verdict", "sigma", "level", "trend", "best", "forecast", "count"):
+            assert torch.equal(oe[key], og[key]), (k, key)
+        assert torch.equal(se, graph.app_stats), k
+        assert eager.hist.head == graph.hist.head and eager.cur.ticks == graph.cur.ticks
+    assert graph._graph is not None and replays >= 20
+    assert torch.equal(eager.hist.data, graph.hist.data) and torch.equal(eager.cur.data, graph.cur.data)
