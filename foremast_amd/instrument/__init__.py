@@ -14,8 +14,11 @@ starter's behaviour:
   (``initializeForStatuses``);
 * a ``caller`` tag from the ``X-CALLER`` header (``CallerWebMvcTagsProvider``);
 * exposition at ``/actuator/prometheus`` (Spring path) and ``/metrics``;
-* optional ``whitelist``/``blacklist`` of metric name prefixes
-  (``CommonMetricsFilter``).
+* :class:`CommonMetricsFilter` — when enabled, every meter is hidden unless
+  an explicit enable override, the whitelist or a name prefix admits it, and
+  the blacklist hides; meters are toggled at run time through
+  ``/actuator/k8s-metrics/{enable,disable}/<metric>`` (``CommonMetricsFilter``,
+  ``K8sMetricsEndpoint``).
 """
 
 from __future__ import annotations
@@ -51,13 +54,113 @@ def parse_common_tags(spec: str, env: Optional[Dict[str, str]] = None) -> Dict[s
     return out
 
 
+_UNIT_SUFFIXES = ("_seconds_max", "_seconds_count", "_seconds_sum", "_seconds", "_bytes", "_total", "_max",
+                  "_count", "_sum")
+
+
+def meter_name(name: str) -> str:
+    """Micrometer meter name of a Prometheus family / meter name:
+    ``http_server_requests_seconds`` → ``http.server.requests``."""
+    for suf in _UNIT_SUFFIXES:
+        if name.endswith(suf) and len(name) > len(suf):
+            name = name[: -len(suf)]
+            break
+    return name.replace("_", ".")
+
+
+def _split(spec) -> list:
+    if not spec:
+        return []
+    if isinstance(spec, str):
+        spec = spec.split(",")
+    return [x.strip() for x in spec if x and x.strip()]
+
+
+class CommonMetricsFilter:
+    """The starter's meter filter (``CommonMetricsFilter.java:84-110``), applied to
+    exposition.  Disabled → everything is shown.  Enabled → per meter, in order:
+    an explicit enable override (``management.metrics.enable.<name>``: the
+    longest dotted prefix in ``enable_overrides``, falling back to ``all``),
+    the whitelist (shown), the blacklist (hidden), a name prefix (shown);
+    anything else is hidden.  Names are compared in Micrometer's dotted form
+    (``_`` → ``.``), prefixes against the dotted name as configured."""
+
+    def __init__(self, enabled: bool = False, whitelist=None, blacklist=None, prefixes=None,
+                 enable_overrides: Optional[Dict[str, bool]] = None) -> None:
+        self.enabled = enabled
+        self.whitelist = {meter_name(x) for x in _split(whitelist)}
+        self.blacklist = {meter_name(x) for x in _split(blacklist)}
+        self.prefixes = tuple(_split(prefixes))
+        self.enable_overrides = dict(enable_overrides or {})
+        self._lock = threading.Lock()
+
+    @classmethod
+    def from_env(cls, env: Optional[Dict[str, str]] = None) -> "CommonMetricsFilter":
+        """``K8S_METRICS_ENABLE_COMMON_METRICS_FILTER`` / ``..._WHITELIST`` /
+        ``..._BLACKLIST`` / ``..._PREFIX`` (the ``k8s.metrics.*`` properties)."""
+        e = os.environ if env is None else env
+        on = e.get("K8S_METRICS_ENABLE_COMMON_METRICS_FILTER", "false").strip().lower() in ("1", "true", "yes")
+        return cls(on, e.get("K8S_METRICS_COMMON_METRICS_WHITELIST"), e.get("K8S_METRICS_COMMON_METRICS_BLACKLIST"),
+                   e.get("K8S_METRICS_COMMON_METRICS_PREFIX"))
+
+    def _override(self, name: str) -> Optional[bool]:
+        if not self.enable_overrides:
+            return None
+        n = name
+        while n:
+            if n in self.enable_overrides:
+                return self.enable_overrides[n]
+            n = n.rpartition(".")[0]
+        return self.enable_overrides.get("all")
+
+    def accept(self, name: str) -> bool:
+        if not self.enabled:
+            return True
+        m = meter_name(name)
+        with self._lock:
+            o = self._override(m)
+            if o is not None:
+                return o
+            if m in self.whitelist:
+                return True
+            if m in self.blacklist:
+                return False
+            return any(m.startswith(p) for p in self.prefixes)
+
+    def enable_metric(self, name: str) -> None:
+        m = meter_name(name)
+        with self._lock:
+            self.blacklist.discard(m)
+            self.whitelist.add(m)
+
+    def disable_metric(self, name: str) -> None:
+        m = meter_name(name)
+        with self._lock:
+            self.whitelist.discard(m)
+            self.blacklist.add(m)
+
+
+class _Filtered:
+    def __init__(self, registry, flt: CommonMetricsFilter) -> None:
+        self.registry, self.flt = registry, flt
+
+    def collect(self):
+        for fam in self.registry.collect():
+            if self.flt.accept(fam.name):
+                yield fam
+
+
 class ForemastMetrics:
     def __init__(self, app, app_name: Optional[str] = None, registry: Optional[CollectorRegistry] = None,
                  common_tags: str = "app:ENV.APP_NAME|info.app.name",
                  initialize_for_statuses: Iterable[int] = (403, 404, 501, 502),
-                 caller_header: str = "X-CALLER", paths=("/actuator/prometheus", "/metrics")) -> None:
+                 caller_header: str = "X-CALLER", paths=("/actuator/prometheus", "/metrics"),
+                 metrics_filter: Optional[CommonMetricsFilter] = None,
+                 actuator_prefix: str = "/actuator/k8s-metrics/") -> None:
         self.app = app
         self.registry = registry or CollectorRegistry()
+        self.filter = metrics_filter if metrics_filter is not None else CommonMetricsFilter.from_env()
+        self.actuator_prefix = actuator_prefix
         tags = parse_common_tags(common_tags)
         if app_name:
             tags["app"] = app_name
@@ -96,12 +199,31 @@ class ForemastMetrics:
             return sum(v[0] for k, v in self._stats.items() if k[3] == str(status))
 
     def exposition(self) -> bytes:
-        return generate_latest(self.registry)
+        return generate_latest(_Filtered(self.registry, self.filter))
+
+    def actuator(self, path: str) -> Optional[bytes]:
+        """``/actuator/k8s-metrics/{enable,disable}/<metric>`` → ``OK``
+        (``K8sMetricsEndpoint.java:21-34``); None if the path is not one."""
+        if not path.startswith(self.actuator_prefix):
+            return None
+        action, _, metric = path[len(self.actuator_prefix):].partition("/")
+        if metric:
+            if action.lower() == "enable":
+                self.filter.enable_metric(metric)
+            elif action.lower() == "disable":
+                self.filter.disable_metric(metric)
+        return b"OK"
 
     async def __call__(self, scope, receive, send):
         if scope["type"] != "http":
             return await self.app(scope, receive, send)
         path = scope.get("path", "")
+        act = self.actuator(path)
+        if act is not None:
+            await send({"type": "http.response.start", "status": 200,
+                        "headers": [(b"content-type", b"text/plain; version=0.1.4; charset=utf-8")]})
+            await send({"type": "http.response.body", "body": act})
+            return
         if path in self.paths:
             body = self.exposition()
             await send({"type": "http.response.start", "status": 200,

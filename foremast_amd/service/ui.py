@@ -5,7 +5,9 @@ every 15 s it fetches the last 15 minutes at a 15 s step, through this
 service's query proxy, for four metric families and draws for each the
 observed series (``namespace_app_per_pod:<m>``), the brain's band
 (``foremastbrain:namespace_app_per_pod:<m>_{upper,lower}``, an area) and
-anomaly points (``..._anomaly``).  Unlike the reference (highcharts + React
+anomaly points (``..._anomaly``), plus the error-rate vs latency scatter
+(one point per step, coloured by time: the reference's 3-D time x 5xx x
+latency chart as a projection).  Unlike the reference (highcharts + React
 build, namespace/app hard-coded to foremast-examples/demo), this is one
 self-contained page with inline SVG — no external assets, so it works in
 air-gapped clusters — and namespace/app come from the URL.
@@ -24,6 +26,9 @@ PANELS: Dict[str, List] = {
     "cpu_usage_seconds_total": ["CPU", 1, "cores"],
     "memory_usage_bytes": ["Memory", 1.0 / (1 << 20), "MiB"],
 }
+
+# the reference's scatter: time x 5xx x latency (ScatterChart.js:144-173)
+SCATTER = ("http_server_requests_error_5xx", "http_server_requests_latency")
 
 REFRESH_S = 15
 WINDOW_S = 15 * 60
@@ -97,6 +102,26 @@ function draw(el, data, scale, unit) {
     '<text x="' + (W - P - 50) + '" y="' + (H - 6) + '" font-size="10" fill="#8a97a6">' + fmt(t1) + '</text></svg>' +
     '<div class="legend"><b style="background:#ffd54f"></b>observed (' + unit + ')<b style="background:#4fc3f7"></b>expected band<b style="background:#e57373"></b>anomaly</div>';
 }
+// error rate vs latency, one point per timestamp, colour = time (old → new): the
+// reference's 3-D time x 5xx x latency scatter (ScatterChart.js) as a projection
+function drawScatter(el, err, lat, latScale) {
+  const W = 600, H = 220, P = 40;
+  const lm = new Map(lat.map(p => [p[0], p[1] * latScale]));
+  const pts = err.filter(p => lm.has(p[0])).map(p => [p[0], lm.get(p[0]), p[1]]);
+  if (!pts.length) { el.innerHTML = '<div class="err">no data</div>'; return; }
+  const xs = pts.map(p => p[1]), ys = pts.map(p => p[2]), ts = pts.map(p => p[0]);
+  let x0 = Math.min(...xs), x1 = Math.max(...xs), y0 = Math.min(...ys), y1 = Math.max(...ys);
+  if (x1 === x0) { x1 += 1; x0 -= 1; } if (y1 === y0) { y1 += 1; y0 -= 1; }
+  const t0 = Math.min(...ts), t1 = Math.max(...ts);
+  const X = v => P + (W - 2 * P) * (v - x0) / (x1 - x0), Y = v => H - P + (2 * P - H) * (v - y0) / (y1 - y0);
+  const dots = pts.map(p => { const f = t1 > t0 ? (p[0] - t0) / (t1 - t0) : 1;
+    return '<circle cx="' + X(p[1]).toFixed(1) + '" cy="' + Y(p[2]).toFixed(1) + '" r="3.5" fill="hsl(' + (200 - 200 * f).toFixed(0) + ',80%,60%)"><title>' + fmt(p[0]) + '</title></circle>'; }).join("");
+  el.innerHTML = '<svg viewBox="0 0 ' + W + ' ' + H + '">' + dots +
+    '<text x="' + P + '" y="' + (H - 6) + '" font-size="10" fill="#8a97a6">latency ' + x0.toPrecision(3) + '…' + x1.toPrecision(3) + ' ms</text>' +
+    '<text x="2" y="14" font-size="10" fill="#8a97a6">5xx ' + y1.toPrecision(3) + '</text>' +
+    '<text x="2" y="' + (H - P) + '" font-size="10" fill="#8a97a6">' + y0.toPrecision(3) + '</text></svg>' +
+    '<div class="legend">one point per ' + CFG.step + ' s step; colour: ' + fmt(t0) + ' (blue) → ' + fmt(t1) + ' (red)</div>';
+}
 async function refresh() {
   const end = Math.floor(Date.now() / 1000), start = end - CFG.window;
   const panels = document.getElementById("panels");
@@ -109,6 +134,13 @@ async function refresh() {
       draw(el, data, scale, unit);
     } catch (e) { el.innerHTML = '<div class="err">' + e + '</div>'; }
   }
+  let sc = document.getElementById("scatter");
+  if (!sc) { const d = document.createElement("div"); d.className = "panel"; d.innerHTML = "<h2>5XX errors vs latency</h2><div id='scatter'></div>"; panels.appendChild(d); sc = document.getElementById("scatter"); }
+  try {
+    const err = await fetchSeries(CFG.queries[CFG.scatter[0]].base, start, end);
+    const lat = await fetchSeries(CFG.queries[CFG.scatter[1]].base, start, end);
+    drawScatter(sc, err, lat, CFG.panels[CFG.scatter[1]][1]);
+  } catch (e) { sc.innerHTML = '<div class="err">' + e + '</div>'; }
   document.getElementById("status").textContent = "updated " + new Date().toLocaleTimeString() + " · every " + CFG.refresh + " s";
 }
 refresh(); setInterval(refresh, CFG.refresh * 1000);
@@ -118,7 +150,7 @@ refresh(); setInterval(refresh, CFG.refresh * 1000);
 
 def page(namespace: str, app: str) -> str:
     cfg = {"panels": PANELS, "queries": queries(namespace, app), "refresh": REFRESH_S, "window": WINDOW_S,
-           "step": STEP_S}
+           "step": STEP_S, "scatter": list(SCATTER)}
     # </script> can't appear inside JSON from these inputs after escaping '<'
     blob = json.dumps(cfg).replace("<", "\\u003c")
     return _PAGE.replace("__CFG__", blob).replace("__TITLE__", html.escape(f"{namespace} : {app}"))
