@@ -34,6 +34,10 @@ def parse(argv=None):
                    help="serve continuous jobs from the resident streaming engine")
     p.add_argument("--model-cache", default=os.environ.get("FOREMAST_MODEL_CACHE"),
                    help="safetensors checkpoint of the LSTM model cache (loaded at start, saved at exit)")
+    p.add_argument("--snapshot", default=os.environ.get("FOREMAST_SNAPSHOT"),
+                   help="streaming-engine snapshot ({rank} expands): resume from it, re-save periodically and at exit")
+    p.add_argument("--snapshot-every", type=int, default=int(os.environ.get("FOREMAST_SNAPSHOT_EVERY", "60")),
+                   help="ticks between streaming snapshots")
     return p.parse_args(argv)
 
 
@@ -81,7 +85,8 @@ async def run(args) -> BrainWorker:
         from .streaming import StreamingMonitor
         mon = StreamingMonitor(store, cfg, device=worker.scorer.device, metrics=metrics,
                                worker_id=f"{worker.worker_id}-stream")
-        tasks.append(mon.run_forever(stop))
+        snap = args.snapshot.replace("{rank}", str(local)) if args.snapshot else None
+        tasks.append(mon.run_forever(stop, snapshot=snap, snapshot_every=args.snapshot_every))
     await asyncio.gather(*tasks)
     if cache_path and worker.lstm is not None:
         worker.lstm.cache.save(cache_path)

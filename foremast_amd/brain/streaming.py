@@ -270,15 +270,60 @@ class StreamingMonitor:
             written[jid] = status
         return written
 
-    async def run_forever(self, stop: Optional[asyncio.Event] = None, period: Optional[float] = None) -> None:
+    # ------------------------------------------------------------------ checkpoint / resume
+    def save_snapshot(self, path: str) -> bool:
+        """Checkpoint the resident shard (history ring, windows, last fit) with
+        the series keys it serves (``brain/checkpoint.py``)."""
+        if self.shard is None:
+            return False
+        from . import checkpoint as ck
+        ck.save_streaming_shard(self.shard, path, extra={"keys": [list(k) for k in self.keys],
+                                                         "t_last": float(self.t_last), "step": self.step})
+        return True
+
+    def restore_snapshot(self, path: str) -> bool:
+        """Adopt a snapshot instead of re-fetching a week of history per series:
+        only when it serves exactly the series of the leased jobs, with the same
+        geometry, and is younger than half the ring (the next tick then catches
+        up the missed points); otherwise the next tick rebuilds from Prometheus."""
+        import os
+        if not path or not os.path.exists(path):
+            return False
+        from . import checkpoint as ck
+        try:
+            shard = ck.load_streaming_shard(path, self.cfg, self.device)
+        except (ValueError, KeyError, OSError) as e:
+            log.warning("ignoring snapshot %s: %s", path, e)
+            return False
+        ex = shard.checkpoint_extra
+        keys = [tuple(k) for k in ex.get("keys", [])]
+        if (keys != self.keys or ex.get("step") != self.step or shard.spec.ring_len != self.R
+                or shard.spec.window != self.W or self.clock() - float(ex.get("t_last", 0)) > self.R * self.step / 2):
+            return False
+        shard.enable_anomaly_list(cap=max(1024, 4 * len(keys)))
+        self.shard, self.t_last, self.dirty = shard, float(ex["t_last"]), False
+        return True
+
+    async def run_forever(self, stop: Optional[asyncio.Event] = None, period: Optional[float] = None,
+                          snapshot: Optional[str] = None, snapshot_every: int = 60) -> None:
+        """Tick every ``period`` seconds; with ``snapshot``, resume from it on the
+        first tick and re-save it every ``snapshot_every`` ticks and at exit."""
         period = self.step if period is None else period
+        first = True
         while stop is None or not stop.is_set():
             try:
                 self.sync()
+                if first and snapshot and self.restore_snapshot(snapshot):
+                    log.info("resumed %d series from snapshot %s", len(self.keys), snapshot)
+                first = False
                 await self.tick()
+                if snapshot and snapshot_every > 0 and self.ticks % snapshot_every == 0:
+                    self.save_snapshot(snapshot)
             except Exception as e:  # noqa: BLE001 - keep monitoring
                 log.exception("streaming tick failed: %s", e)
             try:
                 await asyncio.wait_for(stop.wait(), timeout=period) if stop else await asyncio.sleep(period)
             except asyncio.TimeoutError:
                 pass
+        if snapshot:
+            self.save_snapshot(snapshot)

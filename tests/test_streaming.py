@@ -91,6 +91,52 @@ def test_streaming_monitor_continuous_jobs(where, algorithm):
     assert is_continuous({"strategy": "Continuous"})
 
 
+def test_streaming_monitor_resumes_from_snapshot(tmp_path):
+    """A restarted monitor adopts its snapshot (no week-long history refetch)
+    and scores exactly like the monitor that kept running."""
+    clock = Clock(T0)
+    prom = FakePrometheus(clock=clock)
+    for i, app in enumerate(("a", "b")):
+        prom.add(M, {"namespace": "ns", "app": app}, synth.error_rate(base=0.3 + 0.1 * i, spread=0.05, seed=i))
+    store = MemoryJobStore()
+    for app in ("a", "b"):
+        svc.register(store, _job(app))
+    cfg = BrainConfig.from_env(dict(reference_default_env(), MIN_HISTORICAL_DATA_POINT_TO_MEASURE="10", threshold0="8"))
+    transport = httpx.ASGITransport(app=prom.asgi_app())
+    snap = str(tmp_path / "stream.safetensors")
+
+    def monitor(worker):
+        return StreamingMonitor(store, cfg, prom=PromClient(transport=transport), device=torch.device("cpu"),
+                                worker_id=worker, ring_len=2880, window=5, clock=clock)
+
+    async def go():
+        m1 = monitor("w1")
+        m1.sync()
+        await m1.tick()
+        clock.t = T0 + 120
+        await m1.tick()
+        assert m1.save_snapshot(snap)
+        m2 = monitor("w1")          # restart of the same worker: re-leases its jobs
+        m2.jobs, m2.keys, m2.rows = m1.jobs, list(m1.keys), dict(m1.rows)
+        n_q = len(prom.queries)
+        assert m2.restore_snapshot(snap)
+        clock.t = T0 + 240
+        await m1.tick()
+        await m2.tick()
+        assert len(prom.queries) == n_q + 2      # one incremental query each, no history rebuild
+        for k in ("verdict", "std", "upper", "lower", "score"):
+            assert torch.equal(m1.shard.out[k], m2.shard.out[k]), k
+        m3 = monitor("w1")
+        m3.jobs, m3.keys, m3.rows = m1.jobs, list(m1.keys)[:1], {}
+        assert not m3.restore_snapshot(snap)      # different series set: rebuild instead
+        clock.t = T0 + 2 * 86400
+        m4 = monitor("w1")
+        m4.jobs, m4.keys, m4.rows = m1.jobs, list(m1.keys), dict(m1.rows)
+        assert not m4.restore_snapshot(snap)      # too old
+
+    asyncio.run(go())
+
+
 @pytest.mark.gpu
 def test_graph_tick_matches_eager():
     """tick_graph (ingest + rank tests + HW fit as one HIP-graph replay, ring state
