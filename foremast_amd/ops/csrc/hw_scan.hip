@@ -1004,44 +1004,78 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
   __syncthreads();
 
   // ---- stage: one thread per (series, 8 consecutive phases), all seasons of them in ------
-  // flight at once (up to 56 independent loads per thread: two round trips per workgroup)
+  // flight at once.  Aligned rings (R, m, ld multiples of 8, 16-B row base): the phase
+  // groups are shifted by phi = (pad - head) mod 8 so that each season's 8 columns are
+  // one aligned 16-byte chunk (one load per season, no per-element address math);
+  // otherwise one clamped 2-byte load per element.
   {
     constexpr int GRP = 8;
-    const int ngrp = (m + GRP - 1) / GRP;
+    const int R = a.ring_len;
+    const bool al = (R % GRP == 0) && (m % GRP == 0) && (a.ld % GRP == 0) &&
+                    ((((unsigned long long)a.hist) & 15ull) == 0);
+    const int phi = al ? (((a.pad - head) % GRP) + GRP) % GRP : 0;
+    const int ostart = phi ? phi - GRP : 0;
+    const int ngrp = (m - ostart + GRP - 1) / GRP;
     float s0 = 0.f, c0 = 0.f, s1 = 0.f, c1 = 0.f, s0b = 0.f, c0b = 0.f, s1b = 0.f, c1b = 0.f;
     int bad = 0;
     for (int g = tid; g < 2 * ngrp; g += blockDim.x) {
-      const int r = g >= ngrp ? 1 : 0, o0 = (g - r * ngrp) * GRP;
+      const int r = g >= ngrp ? 1 : 0, o0 = ostart + (g - r * ngrp) * GRP;
       const int n = n0 + r;
       const bool real = n < a.N;
       const bf16_t* row = (const bf16_t*)a.hist + (long long)(real ? n : 0) * a.ld;
       float y[D_MAXSEG][GRP];
+      if (al) {
 #pragma unroll
-      for (int k = 0; k < D_MAXSEG; ++k) {
+        for (int k = 0; k < D_MAXSEG; ++k) {
+          const int t0 = k * m + o0 - a.pad;  // logical index of element 0 (multiple-of-8 column)
+          int c = (head + t0) % R;
+          c += c < 0 ? R : 0;
+          uint4 w = make_uint4(0u, 0u, 0u, 0u);
+          if (k < nseg) w = *(const uint4*)(row + c);  // k < nseg is block-uniform
+          const unsigned ww[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-        for (int u = 0; u < GRP; ++u) {
-          // branch-free: every load is issued (clamped to a valid column) and the value
-          // selected afterwards, so all of them are in flight before the first wait
-          const bool ok = real && k < nseg && o0 + u < m;
-          const int t = k * m + o0 + u - a.pad;
-          const bool pos = t >= 0;
-          int c = head + ((ok && pos) ? t : 0);
-          c -= (c >= a.ring_len) ? a.ring_len : 0;
-          const float v = bf16_to_f32(row[c]);
-          // the padding series of an odd N is zeros (keeps the pair on the fast path)
-          y[k][u] = ok ? (pos ? v : fm_nan()) : 0.f;
+          for (int u = 0; u < GRP; ++u) {
+            const unsigned x = ww[u >> 1];
+            const float v = __uint_as_float((u & 1) ? (x & 0xffff0000u) : (x << 16));
+            const bool ok = real && k < nseg;
+            // the padding series of an odd N is zeros (keeps the pair on the fast path)
+            y[k][u] = ok ? (t0 + u >= 0 ? v : fm_nan()) : 0.f;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < D_MAXSEG; ++k) {
+#pragma unroll
+          for (int u = 0; u < GRP; ++u) {
+            // branch-free: every load is issued (clamped to a valid column) and the value
+            // selected afterwards, so all of them are in flight before the first wait
+            const bool ok = real && k < nseg && o0 + u < m;
+            const int t = k * m + o0 + u - a.pad;
+            const bool pos = t >= 0;
+            int c = head + ((ok && pos) ? t : 0);
+            c -= (c >= R) ? R : 0;
+            const float v = bf16_to_f32(row[c]);
+            y[k][u] = ok ? (pos ? v : fm_nan()) : 0.f;
+          }
         }
       }
-      unsigned vbits = 0u;
+      // (lane, step) of the group's first in-range phase; later phases step from it
+      const int ob = o0 > 0 ? o0 : 0;
+      const int jjb = ob / K, ib = ob - jjb * K;
+      unsigned vlo = 0u, vhi = 0u;  // season-0 validity bits for words o0 >> 5 and (o0 + 7) >> 5
 #pragma unroll
       for (int u = 0; u < GRP; ++u) {
         const int o = o0 + u;
-        if (o < m) {
-          const int jj = o / K, i = o - jj * K;
+        if (o >= 0 && o < m) {
+          int i = ib + (o - ob), jj = jjb;
+          if (i >= K) { i -= K; ++jj; }
           const bool v0 = y[0][u] == y[0][u];
           float* blk = dl + (size_t)r * ns1 * SEA + dl_off(i, jj);
           blk[0] = v0 ? y[1][u] - y[0][u] : y[1][u];  // + l0 for valid y0 once the means are known
-          if (v0) vbits |= 1u << (o & 31);
+          if (v0) {
+            if ((o >> 5) == ((o0 < 0 ? 0 : o0) >> 5)) vlo |= 1u << (o & 31);
+            else vhi |= 1u << (o & 31);
+          }
 #pragma unroll
           for (int k = 1; k < D_MAXSEG - 1; ++k)
             if (k < ns1) blk[(size_t)k * SEA] = y[k + 1][u] - y[k][u];
@@ -1062,7 +1096,9 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
           else { s0b += y0v; c0b += y0c; s1b += y1v; c1b += y1c; }
         }
       }
-      if (vbits) atomicOr(&vmask[r * NMW + (o0 >> 5)], vbits);  // 8 | 32: never straddles a word
+      const int wlo = (o0 < 0 ? 0 : o0) >> 5;
+      if (vlo) atomicOr(&vmask[r * NMW + wlo], vlo);
+      if (vhi) atomicOr(&vmask[r * NMW + wlo + 1], vhi);
     }
     s0 = wave_sum(s0); c0 = wave_sum(c0); s1 = wave_sum(s1); c1 = wave_sum(c1);
     s0b = wave_sum(s0b); c0b = wave_sum(c0b); s1b = wave_sum(s1b); c1b = wave_sum(c1b);

@@ -279,7 +279,7 @@ def test_anomaly_compaction_matches_band_flags(K, which):
 
 
 @pytest.mark.parametrize("variant", [4, 5])
-@pytest.mark.parametrize("case", ["plain", "nan", "wrap_pad", "odd"])
+@pytest.mark.parametrize("case", ["plain", "nan", "wrap_pad", "odd", "aligned_wrap_pad"])
 def test_hw_half_variant_matches_reference(K, case, variant):
     """Variants 4/5 (two series per wave, 1440 = 32 x 45; 5 walks D = y - s over
     fp32 season differences): same fit as the fp64 reference and the same
@@ -287,8 +287,14 @@ def test_hw_half_variant_matches_reference(K, case, variant):
     dev = torch.device("cuda:0")
     m = 1440
     N = 17 if case == "odd" else 16
-    T = 1440 * 4 + 300 if case == "wrap_pad" else 10080
-    R, head = (T + 97, 61) if case == "wrap_pad" else (T, 0)
+    T = 1440 * 4 + 300 if "wrap_pad" in case else 10080
+    R, head = (T, 0)
+    if case == "wrap_pad":
+        R, head = T + 97, 61           # ring length not a multiple of 8: per-element staging
+    elif case == "aligned_wrap_pad":
+        R, head = T + 100, 1061        # multiple of 8, head mid-ring: 16-byte chunk staging
+    if case == "plain":
+        head = 3                       # aligned ring, head not a multiple of 8
     y = _series(N, T, m, seed=11 + len(case), nan_frac=0.01 if case == "nan" else 0.0)
     ring = torch.tensor(_ring(y, R, head), device=dev).to(torch.bfloat16)
     yl = ring.float().cpu().numpy()[:, (head + np.arange(T)) % R]
