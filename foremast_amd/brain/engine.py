@@ -106,6 +106,8 @@ class StreamingShard:
         # HIP-graph tick (tick_graph): per-tick ring state lives in device memory
         self._graph = None
         self._graph_io = None
+        self._side = None                # side HIP stream for the rank tests (overlap_pairwise)
+        self.overlap_pairwise = self.gpu
         if self.gpu:
             self._state_host = torch.zeros(8, dtype=torch.int32).pin_memory()
             self._state_dev = torch.zeros(8, dtype=torch.int32, device=self.device)
@@ -209,11 +211,24 @@ class StreamingShard:
         from ..ops import kernels as K
         cfg = self.cfg
         differs = None
+        # Holt-Winters: the rank tests run on a side stream concurrently with the fit,
+        # whose band/verdict epilogue is deferred until both are done
+        overlap = self.pw_mode != pw_ref.PW_NONE and self.mode == sm_ref.MODE_HW and self.overlap_pairwise
+        main = torch.cuda.current_stream(self.device)
         if self.pw_mode != pw_ref.PW_NONE:
-            self.pw_out = K.rank_tests(self.base, self.cur.data, self.pw_mode, cfg.pairwise_threshold,
-                                       cfg.min_mann_white, cfg.min_wilcoxon, cfg.min_kruskal,
-                                       want_pvals=True, out=self.pw_out, pods=(self.cur.P, self.cur.P),
-                                       min_friedman=cfg.min_friedman)
+            def _rank():
+                return K.rank_tests(self.base, self.cur.data, self.pw_mode, cfg.pairwise_threshold,
+                                    cfg.min_mann_white, cfg.min_wilcoxon, cfg.min_kruskal,
+                                    want_pvals=True, out=self.pw_out, pods=(self.cur.P, self.cur.P),
+                                    min_friedman=cfg.min_friedman)
+            if overlap:
+                if self._side is None:
+                    self._side = torch.cuda.Stream(self.device)
+                self._side.wait_stream(main)  # after this tick's ingest
+                with torch.cuda.stream(self._side):
+                    self.pw_out = _rank()
+            else:
+                self.pw_out = _rank()
             differs = self.pw_out["differs"]
         spec = K.DetectSpec(horizons=self.horizons, threshold=self.threshold, bound=self.bound,
                             min_lower=self.min_lower, cur=self.cur.data, differs=differs,
@@ -225,8 +240,13 @@ class StreamingShard:
         h = self.hist
         if self.mode is not None:
             self.out = K.smoothing_fit(h.data, h.head, h.length, self.mode, self.spec.season, self.grid,
-                                       spec, out=self.out, head_dev=head_dev)
+                                       spec, out=self.out, head_dev=head_dev, defer_detect=overlap,
+                                       detect_after=self._side if overlap else None)
             self._hw_variant = K.last_hw_variant
+            if overlap and K.last_detect_deferred:
+                main.wait_stream(self._side)
+                Tp = K.smoothing_geometry(self.mode, h.length, self.spec.season)[0]
+                K.hw_detect_deferred(self.out, spec, Tp, self.spec.season)
         elif self.algorithm in ("moving_average_all", "moving_average"):
             length = h.length
             head = h.head

@@ -47,7 +47,7 @@ class SmoothArgs(C.Structure):
         ("hist", P), ("ld", LL), ("ring_len", I), ("head", I), ("T", I), ("Tp", I),
         ("pad", I), ("m", I), ("K", I), ("seg", I), ("grid", P), ("G", I), ("N", I),
         ("level", P), ("trend", P), ("sigma", P), ("best", P), ("season_out", P),
-        ("pair_tab", P), ("det", DetectArgs), ("head_dev", P),
+        ("pair_tab", P), ("det", DetectArgs), ("head_dev", P), ("season_hb", P), ("nvalid_out", P),
     ]
 
 
@@ -96,6 +96,8 @@ def _declare(lib: C.CDLL) -> None:
     lib.fm_hw_d_lds_bytes.restype = C.c_size_t
     lib.fm_hw_d_fit.argtypes = [C.POINTER(SmoothArgs), I, P, P]
     lib.fm_hw_d_fit.restype = I
+    lib.fm_hw_detect_params.argtypes = [C.POINTER(SmoothArgs), P]
+    lib.fm_hw_detect_params.restype = I
     lib.fm_rank_tests.argtypes = [C.POINTER(RankArgs), P]
     lib.fm_rank_tests.restype = I
     lib.fm_rank_lds_bytes.argtypes = [I, I]

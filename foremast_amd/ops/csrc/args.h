@@ -58,6 +58,12 @@ struct SmoothArgs {
   const float* pair_tab;  // per combo-pair precomputed table (hw_scan variant 3) or null
   DetectArgs det;
   const int* head_dev;  // HW variants 4/5: if set, `head` is read from device memory (HIP-graph replays)
+  // HW variants 4/5, deferred detection (det.C = 0 at fit time): the fit writes the
+  // seasonal terms of the first HALF_HB forecast phases and the valid-sample count, and
+  // fm_hw_detect_params runs the band/verdict epilogue later (after the rank tests,
+  // which then overlap the fit on another stream)
+  float* season_hb;     // [N, 16] or null
+  float* nvalid_out;    // [N] or null
 };
 
 struct RankArgs {

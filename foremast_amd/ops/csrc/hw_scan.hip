@@ -791,6 +791,8 @@ __device__ __forceinline__ void hw_half_block(const SmoothArgs& a, int hmax, int
   }
   const float* sb = bests + (win * 2 + r) * HALF_HB;
   const int Tp = a.Tp;
+  if (a.season_hb && lane < hmax) a.season_hb[(long long)n * HALF_HB + lane] = sb[lane];
+  if (a.nvalid_out && lane == 0) a.nvalid_out[n] = nvr;
   detect_epilogue_wave(a.det, n, sig, nvr, [&](int h) {
     int ph = (Tp - 1 + h) % m;
     if (ph < 0) ph += m;
@@ -1223,6 +1225,8 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
   }
   const float* sb = bests + (win * 2 + r) * HALF_HB;
   const int Tp = a.Tp;
+  if (a.season_hb && lane < hmax) a.season_hb[(long long)n * HALF_HB + lane] = sb[lane];
+  if (a.nvalid_out && lane == 0) a.nvalid_out[n] = nvr;
   detect_epilogue_wave(a.det, n, sig, nvr, [&](int h) {
     int ph = (Tp - 1 + h) % m;
     if (ph < 0) ph += m;
@@ -1242,6 +1246,31 @@ extern "C" size_t fm_hw_d_lds_bytes(int Tp, int seg, int K) {
   if (nseg < 2 || nseg > D_MAXSEG) return (size_t)-1;
   const int NMW = (32 * K + 31) / 32;
   return ((size_t)2 * (nseg - 1) * DLay<45>::SEASON + 2 * NMW + 8 + 4 + 2 * HALF_HB + 4 * 2 * HALF_HB + 4 * 2 * 4) * 4;
+}
+
+// Deferred detection for HW variants 4/5: band, verdict, per-app counters and the K9
+// anomaly list from the fitted parameters (one wave per series), with the same
+// forecast as the fused epilogue: level + h * trend + season[(Tp - 1 + h) mod m].
+__global__ __launch_bounds__(256) void hw_detect_params_kernel(const SmoothArgs a) {
+  const int n = blockIdx.x * (blockDim.x / FM_WAVE) + wave_id();
+  if (n >= a.N) return;  // wave-uniform
+  const float gL = a.level[n], gB = a.trend[n], sig = a.sigma[n], nvr = a.nvalid_out[n];
+  const float* sb = a.season_hb + (long long)n * HALF_HB;
+  const int Tp = a.Tp, m = a.m;
+  detect_epilogue_wave(a.det, n, sig, nvr, [&](int h) {
+    int ph = (Tp - 1 + h) % m;
+    if (ph < 0) ph += m;
+    ph = ph < HALF_HB ? ph : HALF_HB - 1;
+    return gL + (float)h * gB + sb[ph];
+  });
+}
+
+extern "C" int fm_hw_detect_params(const SmoothArgs* a, hipStream_t st) {
+  if (a->N <= 0 || a->det.C <= 0) return 0;
+  if (!a->season_hb || !a->nvalid_out || !a->level || !a->trend || !a->sigma || a->m <= 0)
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(hw_detect_params_kernel, dim3((a->N + 3) / 4), dim3(256), 0, st, *a);
+  return (int)hipGetLastError();
 }
 
 extern "C" size_t fm_hw_half_lds_bytes(int Tp, int seg, int K) {

@@ -174,6 +174,7 @@ HALF_K = (45,)        # variant 4 (two series per wave): season = 32 * K
 HALF_HB = 16          # seasonal phases kept per series by variant 4 (max forecast horizon)
 last_hw_variant: Optional[int] = None  # variant actually launched by the last smoothing_fit (tests/bench)
 DEFAULT_HW_VARIANT = 5
+last_detect_deferred = False
 
 
 def smoothing_geometry(mode: int, T: int, m: int, K: Optional[int] = None):
@@ -262,10 +263,21 @@ def smoothing_supported(mode: int, T: int, m: int, bf16: bool) -> bool:
 def smoothing_fit(hist: torch.Tensor, head: int, length: int, mode: int, m: int,
                   grid: torch.Tensor, det: DetectSpec, K: Optional[int] = None,
                   want_season: bool = False, out: Optional[Dict[str, torch.Tensor]] = None,
-                  variant: Optional[int] = None, head_dev: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+                  variant: Optional[int] = None, head_dev: Optional[torch.Tensor] = None,
+                  defer_detect: bool = False, detect_after=None) -> Dict[str, torch.Tensor]:
     """``head_dev`` (int32 device scalar): the ring head is read from device memory
     at run time (HIP-graph replays); only the two-series-per-wave HW variants
-    (4/5) support it — other paths raise."""
+    (4/5) support it — other paths raise.
+
+    ``defer_detect``: on the variant 4/5 path the fit skips the band/verdict
+    epilogue and stores what it needs (``season_hb``, ``nvalid``); call
+    :func:`hw_detect_deferred` afterwards (``det.differs`` is read only then, so
+    the rank tests can run concurrently with the fit).  ``last_detect_deferred``
+    says whether the request was honoured; when it is not, the fit detects inline
+    and, if ``detect_after`` (a stream producing ``det.differs``) is given, the
+    current stream first waits for it."""
+    global last_detect_deferred
+    last_detect_deferred = False
     lib = nat.require()
     _hist_check(hist, head, length)
     dev = hist.device
@@ -286,9 +298,12 @@ def smoothing_fit(hist: torch.Tensor, head: int, length: int, mode: int, m: int,
                 and lib.fm_hw_half_lds_bytes(Tp, mm, mm // 32) <= LDS_LIMIT):
             if variant == 5 and lib.fm_hw_d_lds_bytes(Tp, mm, mm // 32) <= D_LDS_LIMIT:
                 return _hw_half_fit(lib, hist, head, length, mm, grid, det, Tp, pad, hmax, out, residual=True,
-                                    head_dev=head_dev)
-            return _hw_half_fit(lib, hist, head, length, mm, grid, det, Tp, pad, hmax, out, head_dev=head_dev)
+                                    head_dev=head_dev, defer=defer_detect)
+            return _hw_half_fit(lib, hist, head, length, mm, grid, det, Tp, pad, hmax, out, head_dev=head_dev,
+                                defer=defer_detect)
         variant = 3
+    if detect_after is not None:
+        torch.cuda.current_stream(dev).wait_stream(detect_after)
     _need(head_dev is None, "head_dev needs HW variant 4/5 geometry")
     fast_lds = lib.fm_hw_scan_lds_bytes(Tp, seg, k, int(mode), int(bf16))
     if variant >= 0 and not (seg % k == 0 and seg // k <= 64 and fast_lds <= LDS_LIMIT):
@@ -349,7 +364,7 @@ def _half_workspace(dev, N: int) -> torch.Tensor:
 
 
 def _hw_half_fit(lib, hist, head, length, m, grid, det, Tp, pad, hmax, out, residual: bool = False,
-                 head_dev: Optional[torch.Tensor] = None):
+                 head_dev: Optional[torch.Tensor] = None, defer: bool = False):
     """Variants 4/5 of the Holt-Winters fit: two series per wave, season = 32
     lanes x K steps.  Variant 4 (hw_scan.hip ``hw_half_kernel``) walks the
     seasonal state over a bf16 image; variant 5 (``residual``, ``hw_d_kernel``)
@@ -391,14 +406,39 @@ def _hw_half_fit(lib, hist, head, length, m, grid, det, Tp, pad, hmax, out, resi
               "head_dev must be an int32 device scalar")
         a.head_dev = nat.ptr(head_dev)
     _fill_detect(a.det, det, N, dev, out)
+    if defer:
+        for kname, shape in (("season_hb", (N, HALF_HB)), ("nvalid", (N,))):
+            if kname not in out:
+                out[kname] = torch.empty(shape, **f32)
+        a.season_hb = nat.ptr(out["season_hb"])
+        a.nvalid_out = nat.ptr(out["nvalid"])
+        a.det.C = 0  # no epilogue in the fit
     ws = _half_workspace(dev, N)
-    global last_hw_variant
+    global last_hw_variant, last_detect_deferred
+    last_detect_deferred = defer
     if residual:
         nat.check(lib.fm_hw_d_fit(a, int(hmax), nat.ptr(ws), nat.stream_handle(dev)), "fm_hw_d_fit")
         last_hw_variant = 5
         return out
     nat.check(lib.fm_hw_half_fit(a, int(hmax), nat.ptr(ws), nat.stream_handle(dev)), "fm_hw_half_fit")
     last_hw_variant = 4
+    return out
+
+
+def hw_detect_deferred(out: Dict[str, torch.Tensor], det: DetectSpec, Tp: int, m: int) -> Dict[str, torch.Tensor]:
+    """Band / verdict / per-app counters / K9 list for a fit run with
+    ``smoothing_fit(..., defer_detect=True)`` (hw_scan.hip ``hw_detect_params_kernel``)."""
+    lib = nat.require()
+    for kname in ("level", "trend", "sigma", "season_hb", "nvalid"):
+        _need(kname in out, f"deferred detection needs out[{kname!r}] from the fit")
+    dev = out["level"].device
+    N = out["level"].shape[0]
+    a = nat.SmoothArgs()
+    a.N, a.Tp, a.m = N, int(Tp), int(m)
+    a.level, a.trend, a.sigma = nat.ptr(out["level"]), nat.ptr(out["trend"]), nat.ptr(out["sigma"])
+    a.season_hb, a.nvalid_out = nat.ptr(out["season_hb"]), nat.ptr(out["nvalid"])
+    _fill_detect(a.det, det, N, dev, out)
+    nat.check(lib.fm_hw_detect_params(a, nat.stream_handle(dev)), "fm_hw_detect_params")
     return out
 
 

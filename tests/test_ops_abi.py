@@ -29,7 +29,7 @@ def test_struct_sizes(lib, name):
 
 
 @pytest.mark.parametrize("name,field", [
-    ("SmoothArgs", "det"), ("SmoothArgs", "season_out"), ("SmoothArgs", "grid"), ("SmoothArgs", "head_dev"),
+    ("SmoothArgs", "det"), ("SmoothArgs", "season_out"), ("SmoothArgs", "grid"), ("SmoothArgs", "head_dev"), ("SmoothArgs", "season_hb"), ("SmoothArgs", "nvalid_out"),
     ("DetectArgs", "pw_scale"), ("DetectArgs", "app_stats"), ("DetectArgs", "ld_cur"),
     ("DetectArgs", "anom_count"), ("DetectArgs", "anom_cap"),
     ("RankArgs", "pvals"), ("RankArgs", "alpha"), ("RankArgs", "p_friedman"), ("RankArgs", "pods_b"), ("WindowArgs", "det"),

@@ -175,3 +175,47 @@ def test_graph_tick_matches_eager():
         assert eager.hist.head == graph.hist.head and eager.cur.ticks == graph.cur.ticks
     assert graph._graph is not None and replays >= 20
     assert torch.equal(eager.hist.data, graph.hist.data) and torch.equal(eager.cur.data, graph.cur.data)
+
+
+@pytest.mark.gpu
+def test_overlapped_rank_tests_match_inline_detection():
+    """Rank tests on a side stream concurrently with the Holt-Winters fit, band and
+    verdict from the deferred-detection kernel: identical to the fused epilogue
+    (pairwise-scaled thresholds, verdicts, app counters, K9 anomaly list)."""
+    from foremast_amd.brain.engine import ShardSpec, StreamingShard, synthetic_history
+    from foremast_amd.ops import _native
+    from foremast_amd.utils.config import BrainConfig
+    _native.require()
+    dev = torch.device("cuda:0")
+    n, R, m, P, W = 96, 4320, 1440, 5, 10
+    cfg = BrainConfig()
+    cfg.min_historical_points = 0
+    hist = synthetic_history(n, R + 30, m, dev, seed=9)
+    shards = []
+    for overlap in (False, True):
+        sh = StreamingShard(ShardSpec(n_series=n, ring_len=R, season=m, pods=P, window=W, n_apps=12), cfg, dev,
+                            app_id=(torch.arange(n, device=dev) % 12).int(),
+                            threshold=torch.full((n,), 3.0, device=dev))
+        sh.overlap_pairwise = overlap
+        sh.load_history(hist[:, :R])
+        sh.set_baseline(hist[:, R - W:R].repeat(1, P))
+        sh.enable_anomaly_list(4096)
+        shards.append(sh)
+    g = torch.Generator(device=dev).manual_seed(1)
+    for k in range(W + 4):
+        newv = hist[:, R + k:R + k + 1].repeat(1, P) + torch.randn(n, P, device=dev, generator=g)
+        newv[::7] *= 2.5  # a shifted canary on some series: pairwise tests fire, thresholds drop
+        outs = []
+        for sh in shards:
+            sh.ingest_tick(newv.contiguous())
+            outs.append({key: v.clone() for key, v in sh.score().items() if torch.is_tensor(v)})
+        torch.cuda.synchronize()
+        for key in ("verdict", "count", "score", "forecast", "upper", "lower", "sigma", "level", "best"):
+            assert torch.equal(outs[0][key], outs[1][key]), (k, key)
+        assert torch.equal(shards[0].app_stats, shards[1].app_stats)
+        assert torch.equal(shards[0].pw_out["differs"], shards[1].pw_out["differs"])
+        a0 = sorted(zip(*[x.tolist() for x in shards[0].anomalies.fetch()[:2]]))
+        a1 = sorted(zip(*[x.tolist() for x in shards[1].anomalies.fetch()[:2]]))
+        assert a0 == a1
+    from foremast_amd.ops import kernels as K
+    assert K.last_detect_deferred and int(shards[1].pw_out["differs"].sum()) > 0
