@@ -982,8 +982,14 @@ __device__ __forceinline__ void d_pass2(const float* blk, v2f* D, v2f c1, v2f c2
   }
 }
 
+// Split tail (see fm_hw_d_fit): a workgroup may fit only the grid pairs [pi_lo, pi_hi)
+// of its series pair; its per-series best then goes to slot `slot` of `cand` (half
+// `hid`), and whichever half arrives second merges the two and finishes the series.
+constexpr int CAND_FLOATS = 4 + HALF_HB;  // SSE, index bits, level, trend, seasonal phases
+
 template <int K>
-__device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0, int* deferred) {
+__device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0, int* deferred, int pi_lo,
+                                           int pi_hi, int slot, int hid, int* cnt, float* cand) {
   constexpr int SEA = DLay<K>::SEASON;
   constexpr int TS = PairTab<K>::SIZE;
   constexpr int NMW = (32 * K + 31) / 32;  // season-0 validity bitmask words per series
@@ -1112,7 +1118,7 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
   }
   __syncthreads();
   if (*flag) {  // block-uniform: a gap past season 0 — the general kernel takes the pair
-    if (tid == 0) deferred[1 + atomicAdd(deferred, 1)] = n0;
+    if (tid == 0 && hid == 0) deferred[1 + atomicAdd(deferred, 1)] = n0;
     return;
   }
   float l0r[2], b0r[2];
@@ -1142,7 +1148,8 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
   const int npairs = (a.G + 1) / 2;
   const int nwaves = blockDim.x / FM_WAVE;
 
-  for (int pi = w; pi < npairs; pi += nwaves) {
+  (void)npairs;
+  for (int pi = pi_lo + w; pi < pi_hi; pi += nwaves) {
     const int c0 = 2 * pi;
     const int c1i = (2 * pi + 1 < a.G) ? 2 * pi + 1 : c0;
     const cfp tab = const_ptr(a.pair_tab + (size_t)pi * TS);
@@ -1213,8 +1220,38 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
     if (sq < sw || (sq == sw && iq < iw)) win = q;
   }
   const float* wb = wbest + (win * 2 + r) * 4;
-  const float gSSE = wb[0], gL = wb[2], gB = wb[3];
-  const int gIdx = __float_as_int(wb[1]);
+  float gSSE = wb[0], gL = wb[2], gB = wb[3];
+  int gIdx = __float_as_int(wb[1]);
+  float* sb = bests + (win * 2 + r) * HALF_HB;
+  if (slot >= 0) {
+    // publish this half's best: write-through (sc1) stores drained before the device-scope
+    // arrival count, so the second arriver's sc1 loads see them from any XCD
+    float* mine = cand + (((size_t)slot * 2 + hid) * 2 + r) * CAND_FLOATS;
+    if (lane < HALF_HB) __hip_atomic_store(&mine[4 + lane], sb[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) {
+      __hip_atomic_store(&mine[0], gSSE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&mine[1], __int_as_float(gIdx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&mine[2], gL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&mine[3], gB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int prev = 0;
+    if (lane == 0) prev = __hip_atomic_fetch_add(&cnt[slot * 2 + r], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    prev = __shfl(prev, 0, FM_WAVE);
+    if (prev == 0) return;  // first half in: the other one finishes this series
+    const float* oth = cand + (((size_t)slot * 2 + (1 - hid)) * 2 + r) * CAND_FLOATS;
+    const float oSSE = __hip_atomic_load(&oth[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int oIdx = __float_as_int(__hip_atomic_load(&oth[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (oSSE < gSSE || (oSSE == gSSE && oIdx < gIdx)) {  // same tie rule as the in-block argmin
+      gSSE = oSSE;
+      gIdx = oIdx;
+      gL = __hip_atomic_load(&oth[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      gB = __hip_atomic_load(&oth[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane < HALF_HB) sb[lane] = __hip_atomic_load(&oth[4 + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    }
+  }
   const float nvr = (float)(ns1 * m);  // fast path: every sample past season 0 is valid
   const float sig = sqrtf(gSSE / fmaxf(nvr, 1.f));
   if (lane == 0) {
@@ -1223,7 +1260,6 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
     a.sigma[n] = sig;
     a.best[n] = gIdx;
   }
-  const float* sb = bests + (win * 2 + r) * HALF_HB;
   const int Tp = a.Tp;
   if (a.season_hb && lane < hmax) a.season_hb[(long long)n * HALF_HB + lane] = sb[lane];
   if (a.nvalid_out && lane == 0) a.nvalid_out[n] = nvr;
@@ -1235,9 +1271,19 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
   });
 }
 
+// Workgroups [0, n_full) fit whole series pairs 0..n_full-1; the rest are split-tail
+// halves: workgroup n_full + 2 s + h fits half h of the grid of pair n_full + s.
 template <int K>
-__global__ __launch_bounds__(256, 2) void hw_d_kernel(const SmoothArgs a, int hmax, int* deferred) {
-  hw_d_block<K>(a, hmax, blockIdx.x * 2, deferred);
+__global__ __launch_bounds__(256, 2) void hw_d_kernel(const SmoothArgs a, int hmax, int* deferred, int n_full,
+                                                     int* cnt, float* cand) {
+  const int b = blockIdx.x;
+  const int npairs = (a.G + 1) / 2;
+  if (b < n_full) {
+    hw_d_block<K>(a, hmax, 2 * b, deferred, 0, npairs, -1, 0, cnt, cand);
+    return;
+  }
+  const int item = b - n_full, slot = item >> 1, h = item & 1, mid = npairs / 2;
+  hw_d_block<K>(a, hmax, 2 * (n_full + slot), deferred, h ? mid : 0, h ? npairs : mid, slot, h, cnt, cand);
 }
 
 extern "C" size_t fm_hw_d_lds_bytes(int Tp, int seg, int K) {
@@ -1307,9 +1353,41 @@ extern "C" int fm_hw_half_fit(const SmoothArgs* a, int hmax, int* deferred, hipS
   return (int)hipGetLastError();
 }
 
+// Split-tail plan: with P series pairs and `slots` resident workgroups, whole pairs run in
+// ceil(P / slots) rounds and the last one can be nearly empty (12.5k series per GPU:
+// 6250 pairs on 512 slots = 12.2 rounds).  Splitting the grid of the last S pairs in two
+// halves (each a workgroup, merged by the second arriver) evens the tail; S is the
+// candidate with the smallest modelled makespan (a half costs ~half a pair plus its
+// staging).  Returns S (0 = no split).
+extern "C" int fm_hw_d_split_plan(int pairs, int slots, int max_split) {
+  if (pairs <= 0 || slots <= 0) return 0;
+  auto cost = [&](int S) {
+    const int full = pairs - S;
+    return 2.0 * ((full + slots - 1) / slots) + 1.1 * ((2 * S + slots - 1) / slots);
+  };
+  int best = 0;
+  double bc = cost(0);
+  const int cands[3] = {pairs % slots, pairs % slots + slots, pairs};
+  for (int S : cands) {
+    if (S <= 0 || S > pairs || S > max_split) continue;
+    const double c = cost(S);
+    if (c < bc - 1e-9) { bc = c; best = S; }
+  }
+  return best;
+}
+
 // Variant 5 launcher: same contract as fm_hw_half_fit (deferred pairs go to the
-// variant-4 general kernel), at most D_MAXSEG seasons.
+// variant-4 general kernel), at most D_MAXSEG seasons.  `split_ws` (optional):
+// int32 [2 * max_split] arrival counters followed by float [max_split * 2 * 2 *
+// CAND_FLOATS] candidates; the counters are zeroed here.
+extern "C" int fm_hw_d_fit_split(const SmoothArgs* a, int hmax, int* deferred, int* split_ws, int max_split,
+                                 int slots, hipStream_t st);
 extern "C" int fm_hw_d_fit(const SmoothArgs* a, int hmax, int* deferred, hipStream_t st) {
+  return fm_hw_d_fit_split(a, hmax, deferred, nullptr, 0, 0, st);
+}
+
+extern "C" int fm_hw_d_fit_split(const SmoothArgs* a, int hmax, int* deferred, int* split_ws, int max_split,
+                                 int slots, hipStream_t st) {
   const int K = a->K;
   if (K != 45 || a->seg != 32 * K || a->m != a->seg || a->Tp % a->seg != 0 || a->Tp / a->seg < 2 ||
       a->Tp / a->seg > D_MAXSEG || !a->pair_tab || a->season_out || hmax < 1 || hmax > K || hmax > HALF_HB)
@@ -1322,7 +1400,15 @@ extern "C" int fm_hw_d_fit(const SmoothArgs* a, int hmax, int* deferred, hipStre
   hipError_t e = hipMemsetAsync(deferred, 0, sizeof(int), st);
   if (e != hipSuccess) return (int)e;
   const int pairs = (a->N + 1) / 2;
-  hipLaunchKernelGGL((hw_d_kernel<45>), dim3(pairs), dim3(256), lds, st, *a, hmax, deferred);
+  const int S = (split_ws && max_split > 0 && a->G >= 2) ? fm_hw_d_split_plan(pairs, slots, max_split) : 0;
+  int* cnt = split_ws;
+  float* cand = split_ws ? (float*)(split_ws + 2 * max_split) : nullptr;
+  if (S > 0) {
+    e = hipMemsetAsync(cnt, 0, sizeof(int) * 2 * (size_t)S, st);
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL((hw_d_kernel<45>), dim3(pairs - S + 2 * S), dim3(256), lds, st, *a, hmax, deferred, pairs - S,
+                     cnt, cand);
   e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL((hw_half_general_kernel<45>), dim3(pairs < 512 ? pairs : 512), dim3(256), glds, st, *a, hmax,

@@ -363,6 +363,24 @@ def _half_workspace(dev, N: int) -> torch.Tensor:
     return ws
 
 
+SPLIT_MAX = 4096       # HW variant 5 split tail: at most this many series pairs split in two halves
+_SPLIT_WS: Dict[int, tuple] = {}
+
+
+def _split_workspace(dev) -> tuple:
+    """Split-tail workspace of variant 5 (hw_scan.hip ``fm_hw_d_fit_split``): int32
+    arrival counters [2 * SPLIT_MAX] followed by the halves' candidates (float
+    [SPLIT_MAX * 4 * (4 + HALF_HB)]), plus the number of resident workgroup slots
+    (two 4-wave workgroups per CU)."""
+    hit = _SPLIT_WS.get(dev.index)
+    if hit is None:
+        words = 2 * SPLIT_MAX + SPLIT_MAX * 4 * (4 + HALF_HB)
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        hit = (torch.zeros(words, dtype=torch.int32, device=dev), 2 * cus)
+        _SPLIT_WS[dev.index] = hit
+    return hit
+
+
 def _hw_half_fit(lib, hist, head, length, m, grid, det, Tp, pad, hmax, out, residual: bool = False,
                  head_dev: Optional[torch.Tensor] = None, defer: bool = False):
     """Variants 4/5 of the Holt-Winters fit: two series per wave, season = 32
@@ -417,7 +435,11 @@ def _hw_half_fit(lib, hist, head, length, m, grid, det, Tp, pad, hmax, out, resi
     global last_hw_variant, last_detect_deferred
     last_detect_deferred = defer
     if residual:
-        nat.check(lib.fm_hw_d_fit(a, int(hmax), nat.ptr(ws), nat.stream_handle(dev)), "fm_hw_d_fit")
+        sws, slots = _split_workspace(dev)
+        if os.environ.get("FOREMAST_HW_SPLIT", "1") == "0":
+            slots = 0  # whole pairs only
+        nat.check(lib.fm_hw_d_fit_split(a, int(hmax), nat.ptr(ws), nat.ptr(sws), SPLIT_MAX, slots,
+                                        nat.stream_handle(dev)), "fm_hw_d_fit_split")
         last_hw_variant = 5
         return out
     nat.check(lib.fm_hw_half_fit(a, int(hmax), nat.ptr(ws), nat.stream_handle(dev)), "fm_hw_half_fit")

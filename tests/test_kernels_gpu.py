@@ -324,3 +324,42 @@ def test_hw_half_variant_matches_reference(K, case, variant):
     out3 = K.smoothing_fit(ring, head, T, sm_ref.MODE_HW, m, grid.to(dev), spec, variant=3)
     torch.cuda.synchronize()
     assert (out3["best"].cpu() == out["best"].cpu()).float().mean() >= 0.9
+
+
+@pytest.mark.parametrize("N", [40, 1030])
+def test_hw_split_tail_matches_whole_pairs(K, N, monkeypatch):
+    """Variant 5's split tail (the grid of a series pair fitted by two workgroups,
+    merged by the second arriver through device-scope sc1 stores / loads) gives
+    exactly the whole-pair result."""
+    dev = torch.device("cuda:0")
+    m, T = 1440, 4320
+    y = _series(N, T, m, seed=21, nan_frac=0.0)
+    y[3, 2000] = np.nan  # one gapped pair goes to the general kernel in both runs
+    ring = torch.tensor(y, device=dev).to(torch.bfloat16)
+    grid = sm_ref.make_grid(sm_ref.MODE_HW, (0.1, 0.3, 0.5, 0.8), (0.0, 0.01, 0.05, 0.1), (0.05, 0.1, 0.3, 0.5))
+    hz = torch.arange(1, 11, dtype=torch.int32).repeat(2)
+    cur = torch.tensor(y[:, -20:] * 1.04, device=dev)
+    spec = K.DetectSpec(horizons=hz.to(dev), threshold=torch.full((N,), 2.0, device=dev),
+                        bound=torch.full((N,), 3, dtype=torch.int8, device=dev),
+                        min_lower=torch.full((N,), -1e30, device=dev), cur=cur, max_horizon=10)
+    lib = K.nat.require()
+    slots = K._split_workspace(dev)[1]
+    S = lib.fm_hw_d_split_plan((N + 1) // 2, slots, K.SPLIT_MAX)
+    assert S > 0
+    outs = []
+    for split in ("1", "0"):
+        monkeypatch.setenv("FOREMAST_HW_SPLIT", split)
+        outs.append({k: v.clone() for k, v in
+                     K.smoothing_fit(ring, 0, T, sm_ref.MODE_HW, m, grid.to(dev), spec, variant=5).items()})
+        torch.cuda.synchronize()
+    for key in ("best", "level", "trend", "sigma", "verdict", "count", "forecast", "upper", "lower"):
+        assert torch.equal(outs[0][key], outs[1][key]), key
+
+
+def test_hw_split_plan():
+    from foremast_amd.ops import _native as nat
+    lib = nat.require()
+    assert lib.fm_hw_d_split_plan(6250, 512, 4096) == 106   # 12.5k series/GPU: split the last partial round
+    assert lib.fm_hw_d_split_plan(50000, 512, 4096) == 0    # 100k: the tail is already negligible
+    assert lib.fm_hw_d_split_plan(20, 512, 4096) == 20      # tiny batches: every pair in two halves
+    assert lib.fm_hw_d_split_plan(20, 0, 4096) == 0
