@@ -100,6 +100,10 @@ def _declare(lib: C.CDLL) -> None:
     lib.fm_hw_d_fit_split.restype = I
     lib.fm_hw_d_split_plan.argtypes = [I, I, I]
     lib.fm_hw_d_split_plan.restype = I
+    lib.fm_es_seq_fit.argtypes = [C.POINTER(SmoothArgs), I, I, P]
+    lib.fm_es_seq_fit.restype = I
+    lib.fm_es_seq_tpc.argtypes = [I]
+    lib.fm_es_seq_tpc.restype = I
     lib.fm_hw_detect_params.argtypes = [C.POINTER(SmoothArgs), P]
     lib.fm_hw_detect_params.restype = I
     lib.fm_rank_tests.argtypes = [C.POINTER(RankArgs), P]

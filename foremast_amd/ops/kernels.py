@@ -291,6 +291,8 @@ def smoothing_fit(hist: torch.Tensor, head: int, length: int, mode: int, m: int,
     bf16 = hist.dtype == torch.bfloat16
     if variant is None:
         variant = int(os.environ.get("FOREMAST_HW_VARIANT", str(DEFAULT_HW_VARIANT)))
+    if mode in (MODE_ES, MODE_DES) and variant in (4, 5) and K is None and G <= 64:
+        return _es_seq_fit(lib, hist, head, length, mode, grid, det, out, head_dev=head_dev, defer=defer_detect)
     if variant in (4, 5):
         hmax = det.max_horizon
         if (mode == MODE_HW and bf16 and mm % 32 == 0 and mm // 32 in HALF_K and not want_season
@@ -444,6 +446,50 @@ def _hw_half_fit(lib, hist, head, length, m, grid, det, Tp, pad, hmax, out, resi
         return out
     nat.check(lib.fm_hw_half_fit(a, int(hmax), nat.ptr(ws), nat.stream_handle(dev)), "fm_hw_half_fit")
     last_hw_variant = 4
+    return out
+
+
+def _es_seq_fit(lib, hist, head, length, mode, grid, det, out, head_dev=None, defer: bool = False):
+    """K2 sequential ES / DES grid fit (csrc/es_seq.hip): one thread per series and
+    pair of grid points, LDS-staged 64-step chunks; band / verdict by the
+    per-series detection kernel (no seasonal term)."""
+    _need(head_dev is None, "head_dev needs HW variant 4/5 geometry")
+    dev = hist.device
+    N = hist.shape[0]
+    out = {} if out is None else out
+    f32 = dict(dtype=torch.float32, device=dev)
+    for kname in ("level", "trend", "sigma", "nvalid"):
+        if kname not in out:
+            out[kname] = torch.empty(N, **f32)
+    if "best" not in out:
+        out["best"] = torch.empty(N, dtype=torch.int32, device=dev)
+    if "season_hb" not in out:
+        out["season_hb"] = torch.zeros((N, HALF_HB), **f32)  # ES / DES forecasts carry no seasonal term
+    a = nat.SmoothArgs()
+    a.hist = nat.ptr(hist)
+    a.ld = hist.stride(0)
+    a.ring_len = hist.shape[1]
+    a.head = int(head)
+    a.T = int(length)
+    a.Tp = int(length)
+    a.m = 1
+    a.K = 1
+    a.seg = 1
+    a.grid = nat.ptr(grid)
+    a.G = grid.shape[0]
+    a.N = N
+    a.level, a.trend, a.sigma = nat.ptr(out["level"]), nat.ptr(out["trend"]), nat.ptr(out["sigma"])
+    a.best = nat.ptr(out["best"])
+    a.nvalid_out = nat.ptr(out["nvalid"])
+    a.season_hb = nat.ptr(out["season_hb"])
+    _fill_detect(a.det, det, N, dev, out)
+    if defer:
+        a.det.C = 0
+    global last_hw_variant, last_detect_deferred
+    nat.check(lib.fm_es_seq_fit(a, int(mode), int(hist.dtype == torch.bfloat16), nat.stream_handle(dev)),
+              "fm_es_seq_fit")
+    last_hw_variant = 5
+    last_detect_deferred = defer
     return out
 
 

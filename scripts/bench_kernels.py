@@ -68,9 +68,17 @@ def main():
     if not args.only or "hw" in args.only:
         for v in variants:
             jobs[f"holt_winters_v{v}"] = (lambda v=v: run_hw(v))
+    es_grid = sm.make_grid(sm.MODE_ES, (0.1, 0.3, 0.6, 0.9), (0.0,), (0.0,)).to(dev)
+    des_grid = sm.make_grid(sm.MODE_DES, (0.1, 0.3, 0.6, 0.9), (0.0, 0.05, 0.1, 0.2), (0.0,)).to(dev)
+
+    def run_es(v, mode):
+        g = es_grid if mode == sm.MODE_ES else des_grid
+        outs[(v, mode)] = K.smoothing_fit(hist, 0, R, mode, 1, g, spec, out=outs.get((v, mode)), variant=v)
+
     if not args.only or "es" in args.only:
-        for v in (-1, 0):
-            jobs[f"exp_smoothing_v{v}"] = (lambda v=v: run_hw(v, sm.MODE_ES))
+        for v in (-1, 0, 5):  # 5 = sequential K2 (csrc/es_seq.hip); -1 / 0 = time-parallel scan
+            jobs[f"exp_smoothing_v{v}"] = (lambda v=v: run_es(v, sm.MODE_ES))
+            jobs[f"double_exp_smoothing_v{v}"] = (lambda v=v: run_es(v, sm.MODE_DES))
     base = cur[:, :50].contiguous()
     rk = {}
     jobs["rank_tests"] = lambda: rk.update(K.rank_tests(base, cur + 0.1, 1, 0.05, out=rk))

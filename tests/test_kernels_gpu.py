@@ -96,6 +96,45 @@ def test_smoothing_kernel_matches_reference(K, mode, m, T, nan, dtype, variant):
     assert torch.equal(d.verdict, out["verdict"].cpu())
 
 
+@pytest.mark.parametrize("mode,T,nan,lead", [
+    (sm_ref.MODE_ES, 3000, 0.0, 0),
+    (sm_ref.MODE_DES, 2500, 0.01, 0),
+    (sm_ref.MODE_ES, 777, 0.05, 150),    # first chunks all missing for some series
+    (sm_ref.MODE_DES, 10080, 0.0, 0),
+])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_es_sequential_kernel_matches_reference(K, mode, T, nan, lead, dtype):
+    """K2 sequential ES / DES (csrc/es_seq.hip): same argmin, sigma, level/trend,
+    forecast and verdicts as the fp64 reference, through leading gaps and a ring
+    that wraps."""
+    dev = torch.device("cuda:0")
+    N, C = 300, 12
+    y = _series(N, T, 24, seed=T + 7 * mode, nan_frac=nan)
+    if lead:
+        y[::3, :lead] = np.nan
+    R, head = T + 37, 29
+    ring = torch.tensor(_ring(y, R, head), device=dev).to(dtype)
+    yl = ring.float().cpu().numpy()[:, (head + np.arange(T)) % R]
+    grid = sm_ref.make_grid(mode, (0.1, 0.3, 0.6, 0.9), (0.0, 0.05, 0.1, 0.2), (0.0,))
+    cur = torch.tensor(y[:, -C:] * 1.05, device=dev)
+    spec = _det_spec(K, N, C, dev, cur=cur)
+    out = K.smoothing_fit(ring, head, T, mode, 1, grid.to(dev), spec, variant=5)
+    torch.cuda.synchronize()
+    ref = sm_ref.fit_smoothing(torch.tensor(yl, dtype=torch.float64), mode, grid.double())
+    kb = out["best"].cpu().long()
+    same = (kb == ref.best).numpy()
+    assert same.mean() > 0.97
+    np.testing.assert_allclose(out["sigma"].cpu().numpy()[same], ref.sigma.numpy()[same], rtol=2e-3, atol=1e-4)
+    np.testing.assert_allclose(out["level"].cpu().numpy()[same], ref.level.numpy()[same], rtol=1e-3, atol=2e-3)
+    np.testing.assert_allclose(out["trend"].cpu().numpy()[same], ref.trend.numpy()[same], rtol=1e-2, atol=1e-4)
+    np.testing.assert_allclose(out["nvalid"].cpu().numpy(), ref.n_valid.numpy())
+    f_ref = sm_ref.forecast(ref, torch.arange(1, C + 1))
+    np.testing.assert_allclose(out["forecast"].cpu().numpy()[same], f_ref.numpy()[same], rtol=2e-3, atol=5e-3)
+    d = det_ref.detect(out["forecast"].cpu(), out["sigma"].cpu(), cur.cpu(),
+                       torch.full((N,), 2.0), torch.full((N,), 3, dtype=torch.int8), torch.full((N,), -1e30))
+    assert torch.equal(d.count, out["count"].cpu()) and torch.equal(d.verdict, out["verdict"].cpu())
+
+
 @pytest.mark.parametrize("variant", [-1, 0, 1, 2, 3])
 def test_smoothing_kernel_flagship_shape(K, variant):
     """T = 10080 (7 days at 60 s), season 1440 (daily), bf16 ring."""
