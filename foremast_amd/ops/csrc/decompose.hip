@@ -5,17 +5,19 @@
 // trend, centred per-phase means of the detrended series, residual).
 //
 // Schedule (512 threads, the series read from HBM exactly once):
-//  0. coalesced staging of the ring window into LDS as fp32 (+ block mean of
+//  0. coalesced staging of the ring window (all of a thread's loads in flight
+//     at once, samples kept in registers) into LDS as fp32 (+ block mean of
 //     the valid values: the offset that keeps the fp32 prefix sums small —
 //     the MA is a difference of two prefix sums);
-//  1. exclusive prefix sums of valid*(y - mean) and of the valid count, in
-//     LDS: per-thread contiguous chunks + one shuffle scan + one LDS round;
+//  1. exclusive prefix sums of valid*(y - mean) (in place over the staged
+//     copy) and of the valid count (uint16), per-thread contiguous chunks +
+//     one shuffle scan + one LDS round;
 //  2. trend per sample from the prefix sums (O(1) each), kept in registers;
 //     the detrended series overwrites the prefix array;
 //  3. per phase p (strided over threads): mean over periods of y - trend;
 //  4. one coalesced output pass: trend, seasonal = phase_mean[t mod m],
-//     resid.  LDS: 3 x (T+1) + m floats (127 KiB at T = 10080, m = 1440 —
-//     gfx950 lets one workgroup own up to 160 KiB).
+//     resid.  LDS: 6 (T+1) + 4 m bytes (66 KiB at T = 10080, m = 1440), so
+//     two workgroups share a CU.
 #include "common.h"
 
 struct DecompArgs {
@@ -87,39 +89,49 @@ __global__ __launch_bounds__(BLOCK) void decompose_kernel(const DecompArgs a) {
   const int n = blockIdx.x;
   const TIN* row = (const TIN*)a.hist + (long long)n * a.ld;
   const int T = a.T, m = a.m, tid = threadIdx.x;
-  float* Y = (float*)fm_dec_smem;    // [T+1] staged series (NaN = missing)
-  float* S = Y + (T + 1);            // [T+1] prefix of valid*(y - ybar)
-  float* Cn = S + (T + 1);           // [T+1] prefix of valid
-  float* pm = Cn + (T + 1);          // [m]
+  float* S = (float*)fm_dec_smem;    // [T+1] staged series, then (in place) prefix of valid*(y - ybar)
+  float* pm = S + (T + 1);           // [m]
   float* red = pm + m;               // [2 * waves]
+  unsigned short* Cn = (unsigned short*)(red + 2 * (BLOCK / FM_WAVE));  // [T+1] prefix of valid (exact: T < 2^16)
 
-  // 0. stage (coalesced) + mean of valid values
+  // 0. stage (coalesced) + mean of valid values.  All loads of a thread are issued back
+  //    to back (clamped index, no per-element branch) and the samples stay in registers
+  //    for the detrended series.
+  float yr[MAX_ITEMS];
+#pragma unroll
+  for (int k = 0; k < MAX_ITEMS; ++k)
+    if (k * BLOCK < T) yr[k] = load_y<TIN>(a, row, min(tid + k * BLOCK, T - 1));
   float sv = 0.f, cv = 0.f;
-  for (int i = tid; i < T; i += BLOCK) {
-    const float y = load_y<TIN>(a, row, i);
-    Y[i] = y;
-    if (y == y) { sv += y; cv += 1.f; }
+#pragma unroll
+  for (int k = 0; k < MAX_ITEMS; ++k) {
+    const int t = tid + k * BLOCK;
+    if (t < T) {
+      const float y = yr[k];
+      S[t] = y;
+      if (y == y) { sv += y; cv += 1.f; }
+    }
   }
   const float ssum = block_sum(sv, red);
   const float csum = block_sum(cv, red);
   const float ybar = csum > 0.f ? ssum / csum : 0.f;
 
-  // 1. prefix sums, contiguous chunk per thread (reads the staged copy)
+  // 1. prefix sums, contiguous chunk per thread (reads the staged copy and overwrites it
+  //    with the prefix: every thread only touches its own chunk)
   const int chunk = (T + BLOCK - 1) / BLOCK;
   const int i0 = min(T, tid * chunk), i1 = min(T, i0 + chunk);
   v2f loc = {0.f, 0.f};
   for (int i = i0; i < i1; ++i) {
-    const float y = Y[i];
+    const float y = S[i];
     if (y == y) { loc.x += y - ybar; loc.y += 1.f; }
   }
   v2f run = block_exscan2(loc, red);
   for (int i = i0; i < i1; ++i) {
+    const float y = S[i];
     S[i] = run.x;
-    Cn[i] = run.y;
-    const float y = Y[i];
+    Cn[i] = (unsigned short)run.y;
     if (y == y) { run.x += y - ybar; run.y += 1.f; }
   }
-  if (i1 == T && i0 < i1) { S[T] = run.x; Cn[T] = run.y; }
+  if (i1 == T && i0 < i1) { S[T] = run.x; Cn[T] = (unsigned short)run.y; }
   __syncthreads();
 
   const int h = m / 2;
@@ -129,15 +141,16 @@ __global__ __launch_bounds__(BLOCK) void decompose_kernel(const DecompArgs a) {
   auto trend_at = [&](int t) -> float {
     if (t < h || t + h > T - 1) return fm_nan();
     float num, den;
+    auto cn = [&](int i) { return (float)Cn[i]; };
     if (even) {
       num = (S[t + h] - S[t - h + 1]);
-      den = (Cn[t + h] - Cn[t - h + 1]);
-      const float ca = Cn[t - h + 1] - Cn[t - h], cb = Cn[t + h + 1] - Cn[t + h];
+      den = (cn(t + h) - cn(t - h + 1));
+      const float ca = cn(t - h + 1) - cn(t - h), cb = cn(t + h + 1) - cn(t + h);
       num += 0.5f * ((S[t - h + 1] - S[t - h]) + (S[t + h + 1] - S[t + h]));
       den += 0.5f * (ca + cb);
     } else {
       num = S[t + h + 1] - S[t - h];
-      den = Cn[t + h + 1] - Cn[t - h];
+      den = cn(t + h + 1) - cn(t - h);
     }
     num *= inv_m;
     den *= inv_m;
@@ -157,7 +170,7 @@ __global__ __launch_bounds__(BLOCK) void decompose_kernel(const DecompArgs a) {
 #pragma unroll
   for (int k = 0; k < MAX_ITEMS; ++k) {
     const int t = tid + k * BLOCK;
-    if (t < T) D[t] = Y[t] - tr_r[k];
+    if (t < T) D[t] = yr[k] - tr_r[k];
   }
   __syncthreads();
 
@@ -197,7 +210,7 @@ __global__ __launch_bounds__(BLOCK) void decompose_kernel(const DecompArgs a) {
 }  // namespace
 
 extern "C" size_t fm_decompose_lds_bytes(int T, int m) {
-  return (size_t)(3 * (T + 1) + m + 2 * (BLOCK / FM_WAVE)) * sizeof(float);
+  return (size_t)((T + 1) + m + 2 * (BLOCK / FM_WAVE)) * sizeof(float) + (((size_t)(T + 1) * 2 + 3) & ~(size_t)3);
 }
 
 extern "C" long long fm_decompose_args_size() { return (long long)sizeof(DecompArgs); }

@@ -8,14 +8,18 @@
 //
 // Why not the time-parallel scan of hw_scan.hip: ES / DES carry a 1- or 2-float state,
 // so N x G independent chains (100k series x 4..16 grid points) already fill the chip;
-// walking them sequentially costs 3 (ES) or 6 (DES) packed FP32 ops per step for two
+// walking them sequentially costs 3 (ES) or 5 (DES) packed FP32 ops per step for two
 // grid points, against a scan's per-segment composition and carry passes.  The work
 // is staged through LDS: a workgroup owns 256 / tpc series (tpc = threads per series),
 // loads 64-step chunks of all its rows with coalesced 128-byte row segments into a
-// double-buffered [series][65] fp32 tile (row stride 65: the series of a wave hit
-// distinct banks), and every thread walks its row from LDS while the next chunk's loads
-// are in flight.  Chunks with a missing point take a masked walk; the rest are
-// straight-line.  The band / verdict epilogue is fm_hw_detect_params with m = 1.
+// [series][65] fp32 tile (row stride 65: the series of a wave hit distinct banks), and
+// every thread walks its row from LDS while the next two chunks load into registers
+// (loads are issued unconditionally, clamped to the last chunk, so the wait before a
+// store covers only the older chunk).  The tile is single-buffered so that four
+// 128-series workgroups fit a CU: the 100k-series ES grid is one round of workgroups.
+// A chunk's missing points are counted with one ballot per row; chunks with a missing
+// point take a masked walk, the rest are straight-line.  The
+// band / verdict epilogue is fm_hw_detect_params with m = 1.
 #include "common.h"
 #include "args.h"
 
@@ -27,7 +31,21 @@ namespace {
 
 constexpr int ES_TC = 64;
 constexpr int ES_LD = ES_TC + 1;
+static_assert(ES_TC == FM_WAVE, "one wave-wide load is one row's chunk (missing counts by ballot)");
 enum { MODE_ES = 0, MODE_DES = 1 };
+constexpr int FM_BUF_DW3 = 0x00020000;  // buffer resource word 3 (raw dword access) on gfx950
+
+// raw bits of one element (bf16: zero-extended 16 bits); converted when stored to LDS so
+// that nothing waits on the load before then
+template <typename TIN>
+__device__ __forceinline__ unsigned buf_load(__amdgpu_buffer_rsrc_t r, unsigned off, unsigned soff) {
+  if (sizeof(TIN) == 2) return (unsigned)__builtin_amdgcn_raw_buffer_load_b16(r, off, soff, 0);
+  return __builtin_amdgcn_raw_buffer_load_b32(r, off, soff, 0);
+}
+template <typename TIN>
+__device__ __forceinline__ float bits_f32(unsigned u) {
+  return __uint_as_float(sizeof(TIN) == 2 ? u << 16 : u);
+}
 
 template <int MODE, bool SAFE>
 __device__ __forceinline__ void es_walk(const float* row, int nt, v2f al, v2f c2, v2f& l, v2f& b, v2f& sse,
@@ -35,24 +53,23 @@ __device__ __forceinline__ void es_walk(const float* row, int nt, v2f al, v2f c2
 #pragma unroll 8
   for (int t = 0; t < nt; ++t) {
     const float y = row[t];
-    v2f e;
+    v2f e, f;
+    if (MODE == MODE_DES) f = l + b;  // one-step forecast
     if (SAFE) {
       const bool ok = y == y;
       if (ok && !started) {  // first valid point: l0 = y (e = 0 there)
         l = splat2(y);
+        if (MODE == MODE_DES) f = l + b;
         started = true;
       }
-      e = splat2(ok ? y : 0.f) - l;
-      if (MODE == MODE_DES) e = e - b;
+      e = splat2(ok ? y : 0.f) - (MODE == MODE_DES ? f : l);
       e = ok ? e : splat2(0.f);
     } else {
-      e = splat2(y) - l;
-      if (MODE == MODE_DES) e = e - b;
+      e = splat2(y) - (MODE == MODE_DES ? f : l);
     }
     if (MODE == MODE_ES) {
       l = l + al * e;
     } else {
-      const v2f f = l + b;
       l = f + al * e;
       b = b + c2 * e;
     }
@@ -60,16 +77,19 @@ __device__ __forceinline__ void es_walk(const float* row, int nt, v2f al, v2f c2
   }
 }
 
-template <int MODE, typename TIN, int TPC>
+// PARTIAL: N < SW (one workgroup with rows past N).  Otherwise every workgroup owns SW
+// valid rows: the last one is shifted back to N - SW and recomputes (bit-identically)
+// some series of its neighbour.
+template <int MODE, typename TIN, int TPC, bool PARTIAL>
 __global__ __launch_bounds__(256) void es_seq_kernel(const SmoothArgs a) {
   constexpr int SW = 256 / TPC;             // series per workgroup
   constexpr int PER = SW * ES_TC / 256;     // staged elements per thread per chunk
   const int tid = threadIdx.x;
   const int s = tid / TPC, gp = tid - s * TPC;
-  const int n0 = blockIdx.x * SW;
+  const int n0 = PARTIAL ? 0 : min((int)blockIdx.x * SW, a.N - SW);
   const int n = n0 + s;
-  float* tile = (float*)fm_es_smem;               // [2][SW][ES_LD]
-  int* nanc = (int*)(tile + 2 * SW * ES_LD);      // [2][SW]  missing points per chunk
+  float* tile = (float*)fm_es_smem;               // [SW][ES_LD]  the chunk being walked
+  int* nanc = (int*)(tile + SW * ES_LD);          // [SW]         missing points of the chunk
   const int T = a.T, R = a.ring_len;
   const int nch = (T + ES_TC - 1) / ES_TC;
   const TIN* base = (const TIN*)a.hist;
@@ -80,47 +100,62 @@ __global__ __launch_bounds__(256) void es_seq_kernel(const SmoothArgs a) {
   be.x = a.grid[3 * c0 + 1]; be.y = a.grid[3 * c1 + 1];
   const v2f c2 = al * be;
 
-  float v[PER];
-  // loads of chunk ch into registers: element e = tid + 256 k -> (row e / 64, step e % 64),
-  // so a wave reads one 128-byte row segment per load; rows / steps out of range read a
-  // clamped valid column and become 0 (not NaN: they are never walked nor counted)
-  auto load_chunk = [&](int ch) {
+  // loads of chunk ch (clamped to the last one) into registers: element e = tid + 256 k
+  // -> (row e / 64, step e % 64), so a wave reads one 128-byte row segment per load.
+  // A raw buffer over this workgroup's rows gives one 32-bit lane offset per element
+  // (no 64-bit address per element), and rows past N read 0 through the hardware range
+  // check; steps past T read a valid column
+  const int nrow = min(SW, a.N - n0);
+  const __amdgpu_buffer_rsrc_t rows = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(base + (long long)n0 * a.ld), (short)0, (int)(nrow * a.ld * (long long)sizeof(TIN)), FM_BUF_DW3);
+  const unsigned row_step = (unsigned)(256 / ES_TC) * (unsigned)a.ld * (unsigned)sizeof(TIN);
+  auto load_chunk = [&](int ch, unsigned (&v)[PER]) {
+    ch = min(ch, nch - 1);
+    const int t = ch * ES_TC + (tid % ES_TC);  // the same step for every k (256 % ES_TC == 0)
+    int c = a.head + (t < T ? t : 0);
+    c -= (c >= R) ? R : 0;
+    const unsigned vo = (unsigned)((tid / ES_TC) * (int)a.ld + c) * (unsigned)sizeof(TIN);
+    if (!PARTIAL) {  // every row in range: the per-row step rides in the scalar offset
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int e = tid + 256 * k, se = e / ES_TC, t = ch * ES_TC + (e % ES_TC);
-      const bool ok = (n0 + se < a.N) && (t < T);
-      int c = a.head + (ok ? t : 0);
-      c -= (c >= R) ? R : 0;
-      const float x = to_f32<TIN>(base[(long long)(ok ? n0 + se : 0) * a.ld + c]);
-      v[k] = ok ? x : 0.f;
+      for (int k = 0; k < PER; ++k) {
+        v[k] = buf_load<TIN>(rows, vo, (unsigned)k * row_step);
+      }
+    } else {         // N < SW: rows past N read 0 through the range-checked lane offset
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        v[k] = buf_load<TIN>(rows, vo + (unsigned)k * row_step, 0u);
+      }
     }
   };
-  auto store_chunk = [&](int buf) {
+  // chunk ch into the tile; steps past T become 0 (not NaN: never walked or counted)
+  auto store_chunk = [&](int ch, const unsigned (&v)[PER]) {
+    const int t = tid % ES_TC;
+    const bool okt = ch * ES_TC + t < T;
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-      const int e = tid + 256 * k, se = e / ES_TC, t = e % ES_TC;
-      tile[(buf * SW + se) * ES_LD + t] = v[k];
-      if (v[k] != v[k]) atomicAdd(&nanc[buf * SW + se], 1);
+      const int se = tid / ES_TC + k * (256 / ES_TC);
+      const float x = okt ? bits_f32<TIN>(v[k]) : 0.f;
+      tile[se * ES_LD + t] = x;
+      const unsigned long long nb = __ballot(x != x);  // this wave's load k is row se's whole chunk
+      if (t == 0) nanc[se] = __popcll(nb);
     }
   };
 
-  for (int i = tid; i < 2 * SW; i += blockDim.x) nanc[i] = 0;
-  __syncthreads();
-  load_chunk(0);
-  store_chunk(0);
+  unsigned va[PER], vb[PER];
+  load_chunk(0, va);
+  store_chunk(0, va);
+  load_chunk(1, va);
   __syncthreads();
 
   v2f l = splat2(0.f), b = splat2(0.f), sse = splat2(0.f);
   bool started = false;
   int nv = 0;
-  for (int ch = 0; ch < nch; ++ch) {
-    const int buf = ch & 1;
-    const bool more = ch + 1 < nch;
-    if (more) load_chunk(ch + 1);                   // in flight during the walk
-    if (more && tid < SW) nanc[(buf ^ 1) * SW + tid] = 0;
+  const float* row = tile + s * ES_LD;
+  // walk chunk ch from the tile while nx (chunk ch + 1) and pf (chunk ch + 2) load
+  auto body = [&](int ch, unsigned (&nx)[PER], unsigned (&pf)[PER]) {
+    load_chunk(ch + 2, pf);
     const int nt = min(ES_TC, T - ch * ES_TC);
-    const float* row = tile + (buf * SW + s) * ES_LD;
-    const int miss = nanc[buf * SW + s];
+    const int miss = nanc[s];
     nv += nt - miss;
     if (miss == 0 && !started) {
       l = splat2(row[0]);
@@ -128,9 +163,13 @@ __global__ __launch_bounds__(256) void es_seq_kernel(const SmoothArgs a) {
     }
     if (__all(miss == 0)) es_walk<MODE, false>(row, nt, al, c2, l, b, sse, started);
     else es_walk<MODE, true>(row, nt, al, c2, l, b, sse, started);
-    __syncthreads();                                // buf^1 free, its counters zeroed
-    if (more) store_chunk(buf ^ 1);
+    __syncthreads();                                // tile and counts free
+    if (ch + 1 < nch) store_chunk(ch + 1, nx);
     __syncthreads();
+  };
+  for (int ch = 0; ch < nch; ch += 2) {
+    body(ch, va, vb);
+    if (ch + 1 < nch) body(ch + 1, vb, va);
   }
 
   // argmin over this thread's two grid points, then over the TPC threads of the series
@@ -155,15 +194,26 @@ __global__ __launch_bounds__(256) void es_seq_kernel(const SmoothArgs a) {
 template <int MODE, typename TIN>
 hipError_t launch_es(const SmoothArgs& a, int tpc, hipStream_t st) {
   const int sw = 256 / tpc;
-  const size_t lds = (size_t)2 * sw * ES_LD * 4 + (size_t)2 * sw * 4;
+  const size_t lds = (size_t)sw * ES_LD * 4 + (size_t)sw * 4;
   const dim3 grid((a.N + sw - 1) / sw), block(256);
+  if (a.N < sw) {
+    switch (tpc) {
+      case 1: hipLaunchKernelGGL((es_seq_kernel<MODE, TIN, 1, true>), grid, block, lds, st, a); break;
+      case 2: hipLaunchKernelGGL((es_seq_kernel<MODE, TIN, 2, true>), grid, block, lds, st, a); break;
+      case 4: hipLaunchKernelGGL((es_seq_kernel<MODE, TIN, 4, true>), grid, block, lds, st, a); break;
+      case 8: hipLaunchKernelGGL((es_seq_kernel<MODE, TIN, 8, true>), grid, block, lds, st, a); break;
+      case 16: hipLaunchKernelGGL((es_seq_kernel<MODE, TIN, 16, true>), grid, block, lds, st, a); break;
+      default: hipLaunchKernelGGL((es_seq_kernel<MODE, TIN, 32, true>), grid, block, lds, st, a); break;
+    }
+    return hipGetLastError();
+  }
   switch (tpc) {
-    case 1: hipLaunchKernelGGL((es_seq_kernel<MODE, TIN, 1>), grid, block, lds, st, a); break;
-    case 2: hipLaunchKernelGGL((es_seq_kernel<MODE, TIN, 2>), grid, block, lds, st, a); break;
-    case 4: hipLaunchKernelGGL((es_seq_kernel<MODE, TIN, 4>), grid, block, lds, st, a); break;
-    case 8: hipLaunchKernelGGL((es_seq_kernel<MODE, TIN, 8>), grid, block, lds, st, a); break;
-    case 16: hipLaunchKernelGGL((es_seq_kernel<MODE, TIN, 16>), grid, block, lds, st, a); break;
-    default: hipLaunchKernelGGL((es_seq_kernel<MODE, TIN, 32>), grid, block, lds, st, a); break;
+    case 1: hipLaunchKernelGGL((es_seq_kernel<MODE, TIN, 1, false>), grid, block, lds, st, a); break;
+    case 2: hipLaunchKernelGGL((es_seq_kernel<MODE, TIN, 2, false>), grid, block, lds, st, a); break;
+    case 4: hipLaunchKernelGGL((es_seq_kernel<MODE, TIN, 4, false>), grid, block, lds, st, a); break;
+    case 8: hipLaunchKernelGGL((es_seq_kernel<MODE, TIN, 8, false>), grid, block, lds, st, a); break;
+    case 16: hipLaunchKernelGGL((es_seq_kernel<MODE, TIN, 16, false>), grid, block, lds, st, a); break;
+    default: hipLaunchKernelGGL((es_seq_kernel<MODE, TIN, 32, false>), grid, block, lds, st, a); break;
   }
   return hipGetLastError();
 }
@@ -182,7 +232,7 @@ extern "C" int fm_es_seq_tpc(int G) {
 extern "C" int fm_es_seq_fit(const SmoothArgs* a, int mode, int bf16, hipStream_t st) {
   if (a->N <= 0) return 0;
   if ((mode != MODE_ES && mode != MODE_DES) || a->G < 1 || a->G > 64 || a->T < 1 || a->T > a->ring_len ||
-      a->head < 0 || a->head >= a->ring_len || !a->nvalid_out || !a->level || !a->trend || !a->sigma || !a->best)
+      a->head < 0 || a->head >= a->ring_len || a->ld < a->ring_len || a->ld > (1 << 20) || !a->nvalid_out || !a->level || !a->trend || !a->sigma || !a->best)
     return (int)hipErrorInvalidValue;
   const int tpc = fm_es_seq_tpc(a->G);
   hipError_t e;

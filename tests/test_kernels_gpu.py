@@ -96,19 +96,20 @@ def test_smoothing_kernel_matches_reference(K, mode, m, T, nan, dtype, variant):
     assert torch.equal(d.verdict, out["verdict"].cpu())
 
 
-@pytest.mark.parametrize("mode,T,nan,lead", [
-    (sm_ref.MODE_ES, 3000, 0.0, 0),
-    (sm_ref.MODE_DES, 2500, 0.01, 0),
-    (sm_ref.MODE_ES, 777, 0.05, 150),    # first chunks all missing for some series
-    (sm_ref.MODE_DES, 10080, 0.0, 0),
+@pytest.mark.parametrize("mode,T,nan,lead,N", [
+    (sm_ref.MODE_ES, 3000, 0.0, 0, 300),     # last workgroup shifted back (300 % 128 != 0)
+    (sm_ref.MODE_DES, 2500, 0.01, 0, 300),
+    (sm_ref.MODE_ES, 777, 0.05, 150, 300),   # first chunks all missing for some series
+    (sm_ref.MODE_DES, 10080, 0.0, 0, 300),
+    (sm_ref.MODE_ES, 500, 0.02, 0, 50),      # N < series per workgroup: range-checked rows
 ])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_es_sequential_kernel_matches_reference(K, mode, T, nan, lead, dtype):
+def test_es_sequential_kernel_matches_reference(K, mode, T, nan, lead, N, dtype):
     """K2 sequential ES / DES (csrc/es_seq.hip): same argmin, sigma, level/trend,
     forecast and verdicts as the fp64 reference, through leading gaps and a ring
     that wraps."""
     dev = torch.device("cuda:0")
-    N, C = 300, 12
+    C = 12
     y = _series(N, T, 24, seed=T + 7 * mode, nan_frac=nan)
     if lead:
         y[::3, :lead] = np.nan
