@@ -66,18 +66,27 @@ __device__ __forceinline__ void acc_range(const TIN* row, int p0, int p1, float&
   if (a0 > p1) a0 = p1;
   for (int i = p0 + tid; i < a0; i += nt) add(to_f32<TIN>(row[i]));
   const int nvec = (p1 - a0) / VEC;
-  for (int v = tid; v < nvec; v += nt) {
-    const uint4 q = *(const uint4*)(row + a0 + v * VEC);
-    if (sizeof(TIN) == 2) {
-      const unsigned w[4] = {q.x, q.y, q.z, q.w};
+  // UNR 16-byte loads of a thread in flight at once (clamped index, no branch before the
+  // loads), then the accumulation: one memory latency per UNR vectors instead of one each
+  constexpr int UNR = 6;
+  for (int v0 = tid; v0 < nvec; v0 += nt * UNR) {
+    uint4 q[UNR];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        add(__uint_as_float(w[k] << 16));
-        add(__uint_as_float(w[k] & 0xffff0000u));
+    for (int u = 0; u < UNR; ++u) q[u] = *(const uint4*)(row + a0 + min(v0 + u * nt, nvec - 1) * VEC);
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      if (v0 + u * nt >= nvec) break;
+      if (sizeof(TIN) == 2) {
+        const unsigned w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          add(__uint_as_float(w[k] << 16));
+          add(__uint_as_float(w[k] & 0xffff0000u));
+        }
+      } else {
+        add(__uint_as_float(q[u].x)); add(__uint_as_float(q[u].y));
+        add(__uint_as_float(q[u].z)); add(__uint_as_float(q[u].w));
       }
-    } else {
-      add(__uint_as_float(q.x)); add(__uint_as_float(q.y));
-      add(__uint_as_float(q.z)); add(__uint_as_float(q.w));
     }
   }
   for (int i = a0 + nvec * VEC + tid; i < p1; i += nt) add(to_f32<TIN>(row[i]));
