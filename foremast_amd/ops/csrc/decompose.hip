@@ -15,8 +15,8 @@
 //  2. trend per sample from the prefix sums (O(1) each), kept in registers;
 //     the detrended series overwrites the prefix array;
 //  3. per phase p (strided over threads): mean over periods of y - trend;
-//  4. one coalesced output pass: trend, seasonal = phase_mean[t mod m],
-//     resid.  LDS: 6 (T+1) + 4 m bytes (66 KiB at T = 10080, m = 1440), so
+//  4. one coalesced output pass: seasonal = phase_mean[t mod m], resid (the
+//     trend is stored in pass 2).  LDS: 6 (T+1) + 4 m bytes (66 KiB at T = 10080, m = 1440), so
 //     two workgroups share a CU.
 #include "common.h"
 
@@ -154,16 +154,20 @@ __global__ __launch_bounds__(BLOCK) void decompose_kernel(const DecompArgs a) {
     }
     num *= inv_m;
     den *= inv_m;
-    return den >= 0.5f ? ybar + num / den : fm_nan();
+    return den >= 0.5f ? ybar + num * __builtin_amdgcn_rcpf(den) : fm_nan();  // den >= 0.5: rcp is 1 ulp
   };
 
   // 2. trend once per sample into registers (t = tid + k*BLOCK); after a
   //    barrier S is free and becomes the detrended series D
+  //    (the trend output is stored here, so its 4 bytes per sample leave while the
+  //    workgroup still has the phase-mean pass to do)
+  const long long base = (long long)n * T;
   float tr_r[MAX_ITEMS];
 #pragma unroll
   for (int k = 0; k < MAX_ITEMS; ++k) {
     const int t = tid + k * BLOCK;
     tr_r[k] = t < T ? trend_at(t) : 0.f;
+    if (t < T && a.trend) a.trend[base + t] = tr_r[k];
   }
   __syncthreads();
   float* D = S;
@@ -194,13 +198,17 @@ __global__ __launch_bounds__(BLOCK) void decompose_kernel(const DecompArgs a) {
   __syncthreads();
 
   // 4. outputs (coalesced)
-  const long long base = (long long)n * T;
+  const int pstep = BLOCK % m;  // phase of t = tid + k*BLOCK, advanced without an integer division per sample
+  int ph = tid % m;
 #pragma unroll
   for (int k = 0; k < MAX_ITEMS; ++k) {
     const int t = tid + k * BLOCK;
+    if (k > 0) {
+      ph += pstep;
+      ph -= (ph >= m) ? m : 0;
+    }
     if (t < T) {
-      const float se = pm[t % m];
-      if (a.trend) a.trend[base + t] = tr_r[k];
+      const float se = pm[ph];
       if (a.seasonal) a.seasonal[base + t] = se;
       if (a.resid) a.resid[base + t] = D[t] - se;
     }
