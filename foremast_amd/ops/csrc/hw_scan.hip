@@ -1224,15 +1224,17 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
   int gIdx = __float_as_int(wb[1]);
   float* sb = bests + (win * 2 + r) * HALF_HB;
   if (slot >= 0) {
-    // publish this half's best: write-through (sc1) stores drained before the device-scope
-    // arrival count, so the second arriver's sc1 loads see them from any XCD
+    // publish this half's best: system-scope (sc0 sc1) stores, which write through every
+    // cache level, drained before the device-scope arrival count; the second arriver reads
+    // them with system-scope loads, which bypass its XCD's L2 (an agent-scope sc1 load
+    // could hit a line left there by an earlier call: the L2 is per XCD)
     float* mine = cand + (((size_t)slot * 2 + hid) * 2 + r) * CAND_FLOATS;
-    if (lane < HALF_HB) __hip_atomic_store(&mine[4 + lane], sb[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane < HALF_HB) __hip_atomic_store(&mine[4 + lane], sb[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (lane == 0) {
-      __hip_atomic_store(&mine[0], gSSE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&mine[1], __int_as_float(gIdx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&mine[2], gL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&mine[3], gB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&mine[0], gSSE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&mine[1], __int_as_float(gIdx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&mine[2], gL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&mine[3], gB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int prev = 0;
@@ -1240,14 +1242,14 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
     prev = __shfl(prev, 0, FM_WAVE);
     if (prev == 0) return;  // first half in: the other one finishes this series
     const float* oth = cand + (((size_t)slot * 2 + (1 - hid)) * 2 + r) * CAND_FLOATS;
-    const float oSSE = __hip_atomic_load(&oth[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const float oSSE = __hip_atomic_load(&oth[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const int oIdx = __float_as_int(__hip_atomic_load(&oth[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     if (oSSE < gSSE || (oSSE == gSSE && oIdx < gIdx)) {  // same tie rule as the in-block argmin
       gSSE = oSSE;
       gIdx = oIdx;
-      gL = __hip_atomic_load(&oth[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      gB = __hip_atomic_load(&oth[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (lane < HALF_HB) sb[lane] = __hip_atomic_load(&oth[4 + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      gL = __hip_atomic_load(&oth[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      gB = __hip_atomic_load(&oth[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (lane < HALF_HB) sb[lane] = __hip_atomic_load(&oth[4 + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     }
