@@ -42,19 +42,17 @@ extern "C" int fm_ring_append(void* dst, long long ld_dst, int R, int col0, int 
 }
 
 // ---------------------------------------------------------------------------------
-// window statistics + detection (one 256-thread workgroup per series)
+// window statistics + detection (one wave per series)
 // ---------------------------------------------------------------------------------
 
 
-extern __shared__ __attribute__((aligned(16))) char fm_win_smem[];
 
 // Accumulate shifted sums over physical range [p0, p1) of a row; vector body
 // of 16-byte loads, scalar head/tail.
-template <typename TIN>
+template <typename TIN, int UNR = 6>
 __device__ __forceinline__ void acc_range(const TIN* row, int p0, int p1, float& shift, bool& has_shift,
-                                          float& n, float& s1, float& s2) {
+                                          float& n, float& s1, float& s2, int tid, int nt) {
   constexpr int VEC = 16 / sizeof(TIN);
-  const int tid = threadIdx.x, nt = blockDim.x;
   auto add = [&](float v) {
     if (v == v) {
       if (!has_shift) { shift = v; has_shift = true; }
@@ -68,7 +66,6 @@ __device__ __forceinline__ void acc_range(const TIN* row, int p0, int p1, float&
   const int nvec = (p1 - a0) / VEC;
   // UNR 16-byte loads of a thread in flight at once (clamped index, no branch before the
   // loads), then the accumulation: one memory latency per UNR vectors instead of one each
-  constexpr int UNR = 6;
   for (int v0 = tid; v0 < nvec; v0 += nt * UNR) {
     uint4 q[UNR];
 #pragma unroll
@@ -92,42 +89,40 @@ __device__ __forceinline__ void acc_range(const TIN* row, int p0, int p1, float&
   for (int i = a0 + nvec * VEC + tid; i < p1; i += nt) add(to_f32<TIN>(row[i]));
 }
 
+// One wave per series (four per workgroup): the same statistics with wave reductions
+// only, no workgroup barriers, and ~20 16-byte loads of a lane in flight in two batches.
 template <typename TIN>
-__global__ __launch_bounds__(256) void window_stats_kernel(const WindowArgs a) {
-  const int n = blockIdx.x;
-  float* red = (float*)fm_win_smem;
+__global__ __launch_bounds__(256) void window_stats_wave_kernel(const WindowArgs a) {
+  const int n = blockIdx.x * (256 / FM_WAVE) + wave_id();
+  if (n >= a.N) return;  // wave-uniform
+  const int lane = lane_id();
   const TIN* row = (const TIN*)a.hist + (long long)n * a.ld;
   float shift = 0.f, cnt = 0.f, s1 = 0.f, s2 = 0.f;
   bool has = false;
-  int p0 = a.head, p1 = a.head + a.len;
+  const int p0 = a.head, p1 = a.head + a.len;
   if (p1 <= a.ring_len) {
-    acc_range<TIN>(row, p0, p1, shift, has, cnt, s1, s2);
+    acc_range<TIN, 10>(row, p0, p1, shift, has, cnt, s1, s2, lane, FM_WAVE);
   } else {
-    acc_range<TIN>(row, p0, a.ring_len, shift, has, cnt, s1, s2);
-    acc_range<TIN>(row, 0, p1 - a.ring_len, shift, has, cnt, s1, s2);
+    acc_range<TIN, 10>(row, p0, a.ring_len, shift, has, cnt, s1, s2, lane, FM_WAVE);
+    acc_range<TIN, 10>(row, 0, p1 - a.ring_len, shift, has, cnt, s1, s2, lane, FM_WAVE);
   }
-  // per-thread (n, mean, M2) → Chan merge via block sums of shifted moments
-  // relative to a common reference (the block's first thread with data).
-  float mean_t = cnt > 0.f ? shift + s1 / cnt : 0.f;
-  float m2_t = cnt > 0.f ? fmaxf(s2 - s1 * s1 / cnt, 0.f) : 0.f;
-  const float N = blk_sum(cnt, red);
-  float ref = 0.f;
-  {
-    // pick a common reference: mean over threads of their means (weighted)
-    const float sm = blk_sum(cnt * mean_t, red);
-    ref = N > 0.f ? sm / N : 0.f;
-  }
+  // per-lane (n, mean, M2) -> Chan merge about the count-weighted mean of the lane means
+  const float mean_t = cnt > 0.f ? shift + s1 / cnt : 0.f;
+  const float m2_t = cnt > 0.f ? fmaxf(s2 - s1 * s1 / cnt, 0.f) : 0.f;
+  const float N = wave_sum(cnt);
+  const float sm = wave_sum(cnt * mean_t);
+  const float ref = N > 0.f ? sm / N : 0.f;
   const float dm = mean_t - ref;
-  const float M2 = blk_sum(m2_t + cnt * dm * dm, red);
+  const float M2 = wave_sum(m2_t + cnt * dm * dm);
   const float mean = ref;
   const float var = N > 0.f ? M2 / N : 0.f;
   const float sd = N > 0.f ? sqrtf(fmaxf(var, 0.f)) : fm_nan();
-  if (threadIdx.x == 0) {
+  if (lane == 0) {
     a.mean[n] = N > 0.f ? mean : fm_nan();
     a.stdv[n] = sd;
     a.count[n] = N;
   }
-  detect_epilogue(a.det, n, sd, N, [mean](int) { return mean; }, red);
+  detect_epilogue_wave(a.det, n, sd, N, [mean](int) { return mean; });
 }
 
 extern "C" int fm_window_stats(const WindowArgs* a, int bf16, hipStream_t st) {
@@ -136,9 +131,10 @@ extern "C" int fm_window_stats(const WindowArgs* a, int bf16, hipStream_t st) {
     return (int)hipErrorInvalidValue;
   if (bf16 && (a->ld % 8) != 0) return (int)hipErrorInvalidValue;
   if (!bf16 && (a->ld % 4) != 0) return (int)hipErrorInvalidValue;
+  const dim3 wgrid((a->N + 3) / 4);
   if (bf16)
-    hipLaunchKernelGGL(window_stats_kernel<bf16_t>, dim3(a->N), dim3(256), 256, st, *a);
+    hipLaunchKernelGGL(window_stats_wave_kernel<bf16_t>, wgrid, dim3(256), 0, st, *a);
   else
-    hipLaunchKernelGGL(window_stats_kernel<float>, dim3(a->N), dim3(256), 256, st, *a);
+    hipLaunchKernelGGL(window_stats_wave_kernel<float>, wgrid, dim3(256), 0, st, *a);
   return (int)hipGetLastError();
 }
