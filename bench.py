@@ -30,8 +30,10 @@ Other BASELINE configs (same metric/JSON contract, ``--config``):
 * ``multivariate`` (config 5): 50k entities x (latency, error-rate) = 100k
   metric-series, LSTM-AE scored with fp8 e4m3 MFMA.
 
-Usage: ``python bench.py --gpus N --steps K --warmup W`` (N > 1 under
-``torch.distributed.run``; rank 0 prints ONE JSON line).
+Usage: ``python bench.py --gpus N --steps K --warmup W``.  With N > 1 and no
+launcher the script starts its own ``torch.distributed.run`` group of N ranks
+(one per GPU, RCCL); under a launcher it checks WORLD_SIZE == N.  Rank 0 prints
+ONE JSON line.
 """
 
 from __future__ import annotations
@@ -93,8 +95,33 @@ def parse():
     return p.parse_args()
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def self_launch(args, argv) -> int:
+    """``--gpus N`` without a launcher: start N ranks (one per GPU) as ONE child
+    ``torch.distributed.run`` process group and forward its exit code.
+
+    Runs before this process touches the GPU (no HIP call, no
+    ``torch.cuda.is_available()``): the parent only waits; rank 0's JSON line
+    reaches stdout through the inherited file descriptors."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL on this host driver
+    env.setdefault("OMP_NUM_THREADS", "4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd, env=env)
+
+
 def init_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU is required")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_gpu = torch.cuda.is_available() and not args.cpu
@@ -400,6 +427,8 @@ def setup_single(args, world, rank, dev):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args, sys.argv[1:]))
     if args.config == "hw10k":
         args.series = 10_000  # BASELINE config 2: same pipeline as the headline at 10k series
         args.config = "canary"

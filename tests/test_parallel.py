@@ -133,14 +133,19 @@ def test_shard_range_alignment():
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("config", ["canary", "lstm", "multicluster"])
+@pytest.mark.parametrize("config", ["canary", "lstm", "multicluster", "selflaunch"])
 def test_bench_distributed_cpu(config):
+    """Under torchrun, and (``selflaunch``) as the driver may call it: a plain
+    ``python bench.py --gpus 2`` that must start its own 2-rank group."""
     extra = ["--multi-cluster"] if config == "multicluster" else []
-    config = "canary" if config == "multicluster" else config
+    launcher = config != "selflaunch"
+    config = "canary" if config in ("multicluster", "selflaunch") else config
     port = _free_port()
     env = dict(os.environ, OMP_NUM_THREADS="2")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
+    env.pop("WORLD_SIZE", None)
+    pre = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}"] if launcher else [sys.executable]
+    cmd = pre + [os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "2", "--warmup", "1", "--cpu", "--series", "200", "--ring", "480",
            "--season", "48", "--config", config, "--lstm-train-batch", "32", "--lstm-pretrain", "2"] + extra
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
