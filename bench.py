@@ -75,6 +75,8 @@ def parse():
     p.add_argument("--algorithm", default="holt_winters")
     p.add_argument("--pairwise", default="ALL")
     p.add_argument("--anomaly-frac", type=float, default=0.01)
+    p.add_argument("--anomaly-kind", default="scale3", choices=["scale3", "shift3sigma"],
+                   help="injected canary regression: values x3, or a level shift of +3 noise sigma")
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--graph", action="store_true", help="capture the GPU part of a tick in a HIP graph")
     p.add_argument("--cpu", action="store_true", help="force CPU (reference path; tiny sizes only)")
@@ -149,21 +151,45 @@ def barrier(dev):
             dist.barrier()
 
 
-def make_ticks(params, pods, nticks, season, t0, seed, anomaly_frac):
+NOISE = 0.03  # synthetic noise sigma as a fraction of the level (engine.synthetic_eval default)
+
+
+def make_ticks(params, pods, nticks, season, t0, seed, anomaly_frac, kind="scale3", want_bad=False):
     """Per-tick per-pod values ``[nticks, n, pods]`` continuing each series'
     synthetic model past the history (same noise level as the history), with a
-    fraction of series turned anomalous (canary regression: values x3)."""
+    fraction of series turned anomalous: ``scale3`` (canary regression, values
+    x3) or ``shift3sigma`` (level shift of +3 noise sigma).  ``want_bad``: also
+    return the regressed series' indices (detection-quality ground truth)."""
     lvl = params["lvl"]
     n, dev = lvl.shape[0], lvl.device
     g = torch.Generator(device=dev)
     g.manual_seed(seed + 17)
     vals = synthetic_eval(params, t0, nticks, season, None).T.contiguous()  # [nticks, n]
-    out = vals[..., None] + torch.randn((nticks, n, pods), generator=g, device=dev) * (0.03 * lvl[:, 0])[None, :, None]
+    out = vals[..., None] + torch.randn((nticks, n, pods), generator=g, device=dev) * (NOISE * lvl[:, 0])[None, :, None]
     n_bad = int(n * anomaly_frac)
+    bad = torch.zeros(0, dtype=torch.int64, device=dev)
     if n_bad:
         bad = torch.randperm(n, generator=g, device=dev)[:n_bad]
-        out[:, bad, :] *= 3.0
-    return out.float()
+        if kind == "scale3":
+            out[:, bad, :] *= 3.0
+        else:
+            out[:, bad, :] += (3 * NOISE * lvl[bad, 0])[None, :, None]
+    return (out.float(), bad) if want_bad else out.float()
+
+
+def detection_report(table: torch.Tensor, truth_apps, n_apps: int) -> dict:
+    """Per-app detection quality of the last tick against the injected ground
+    truth: an app is flagged when any of its series is anomalous."""
+    flagged = (table[:n_apps, 0] > 0).numpy()
+    truth = np.zeros(n_apps, dtype=bool)
+    truth[np.asarray(sorted(truth_apps), dtype=np.int64)] = True
+    tp = int((flagged & truth).sum())
+    fp = int((flagged & ~truth).sum())
+    fn = int((~flagged & truth).sum())
+    healthy = int((~truth).sum())
+    return {"apps": n_apps, "injected_apps": int(truth.sum()), "tp": tp, "fp": fp, "fn": fn,
+            "precision": round(tp / max(tp + fp, 1), 4), "recall": round(tp / max(tp + fn, 1), 4) if truth.any() else None,
+            "false_positive_rate": round(fp / max(healthy, 1), 5)}
 
 
 def setup_canary(args, world, rank, dev):
@@ -202,7 +228,9 @@ def setup_canary(args, world, rank, dev):
     total_ticks = args.warmup + args.steps
     # per tick: P canary-pod values (a fraction of series regressed) and P
     # baseline-pod values (healthy, same times) -> [ticks, N, 2P]
-    cur_t = make_ticks(params, P, total_ticks + W, args.season, args.ring, 99 + rank, args.anomaly_frac)
+    cur_t, bad = make_ticks(params, P, total_ticks + W, args.season, args.ring, 99 + rank, args.anomaly_frac,
+                            args.anomaly_kind, want_bad=True)
+    truth_apps = sorted(set(((bad.cpu() + s) // METRICS_PER_APP).tolist()))
     exch = None
     if args.multi_cluster:
         # this rank scrapes the baseline pods of the neighbour's shard
@@ -283,6 +311,7 @@ def setup_canary(args, world, rank, dev):
         meta["_table"] = lambda h: HealthAggregator.host_app_table(h, world, apps_per_rank)
     dt = "bf16" if dtype == torch.bfloat16 else "fp32"
     meta["_agg"] = agg
+    meta["_truth"] = (truth_apps, n_apps)
     return tick, health_host, meta, dt, args.series
 
 
@@ -311,8 +340,11 @@ def setup_lstm(args, world, rank, dev, n_features, fp8):
                         for f, p in enumerate(params)])
     total = args.warmup + args.steps
     # the same entities regress on every metric (seed shared across features)
-    ticks = torch.stack([make_ticks(p, 1, total, args.season, args.ring, 99 + rank, args.anomaly_frac)[..., 0]
-                         for p in params], 2)  # [ticks, n, F]
+    tk = [make_ticks(p, 1, total, args.season, args.ring, 99 + rank, args.anomaly_frac, args.anomaly_kind,
+                     want_bad=True) for p in params]
+    ticks = torch.stack([t[..., 0] for t, _ in tk], 2)  # [ticks, n, F]
+    truth_apps = sorted(set(((tk[0][1].cpu() + s) // ent_per_app).tolist()))
+    del tk
     pin = dev.type == "cuda"
     host_ticks = ticks.cpu()
     if pin:
@@ -352,6 +384,7 @@ def setup_lstm(args, world, rank, dev, n_features, fp8):
     }
     dt = "bf16"  # training fp32 master / bf16 MFMA scoring (fp8 weights+activations for config 5)
     meta["_agg"] = agg
+    meta["_truth"] = (truth_apps, n_apps)
     return tick, health_host, meta, dt, n_ent * F
 
 
@@ -445,6 +478,11 @@ def main():
 
     agg = meta.pop("_agg", None)
     table = meta.pop("_table", None)
+    truth = meta.pop("_truth", None)
+    if truth is not None and world > 1:
+        parts = [None] * world
+        dist.all_gather_object(parts, truth[0])
+        truth = (sorted(set().union(*parts)), truth[1])
     for k in range(args.warmup):
         tick(k)
     if agg is not None:
@@ -504,6 +542,9 @@ def main():
             "health": {"apps": int(health_host.shape[0]), "anomalous_apps": anomalous_apps,
                        "series_scored_last_tick": scored},
         }
+        if truth is not None:
+            res["detection"] = dict(detection_report(health_host, truth[0], truth[1]),
+                                    injected=f"{args.anomaly_kind} on {args.anomaly_frac:g} of series")
         print(json.dumps(res), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()

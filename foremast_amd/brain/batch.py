@@ -150,8 +150,13 @@ class BatchScorer:
         has_base = torch.tensor([t.base_vals is not None for t in tasks], device=dev)
         if differs is not None:
             differs = torch.where(has_base, differs, torch.zeros_like(differs)).contiguous()
-        t_thr = torch.from_numpy(thr).to(dev)
         t_bnd = torch.from_numpy(bnd).to(dev)
+        # per-point thresholds of the full and the lowered band for each task's window
+        n_pts = torch.tensor([max(1, len(t.cur_vals)) for t in tasks], dtype=torch.float64)
+        thr_f, thr_l = det_ref.effective_thresholds(torch.from_numpy(thr), torch.from_numpy(bnd), n_pts,
+                                                    cfg.pairwise_scale, cfg.window_correction)
+        t_thr, t_thr_low = thr_f.to(dev).contiguous(), thr_l.to(dev).contiguous()
+        dkw = dict(threshold_low=t_thr_low, pw_min_points=cfg.pairwise_min_points)
         t_low = torch.from_numpy(low).to(dev)
         t_hz = torch.from_numpy(hz).to(dev)
         t_hist = torch.from_numpy(hist).to(dev)
@@ -173,13 +178,14 @@ class BatchScorer:
             f = pl_ref.forecast(fit, torch.from_numpy(cts).to(dev))
             d = det_ref.detect(f, fit.sigma.float(), t_cur, t_thr, t_bnd, t_low, differs=differs,
                                pairwise_scale=cfg.pairwise_scale,
-                               model_ok=fit.n_valid >= cfg.min_historical_points)
+                               model_ok=fit.n_valid >= cfg.min_historical_points, **dkw)
             upper, lower, verdict, anom = d.upper, d.lower, d.verdict, d.anomaly
         elif self.gpu:
             from ..ops import kernels as K
             spec = K.DetectSpec(horizons=t_hz, threshold=t_thr, bound=t_bnd, min_lower=t_low, cur=t_cur,
                                 differs=differs, pw_scale=cfg.pairwise_scale, min_valid=cfg.min_historical_points,
-                                max_horizon=int(hz.max()) if hz.size and hz.min() >= 1 else None)
+                                max_horizon=int(hz.max()) if hz.size and hz.min() >= 1 else None,
+                                horizon_variance=cfg.horizon_variance, **dkw)
             T = t_hist.shape[1]
             if mode is not None:
                 g = sm_ref.make_grid(mode, cfg.hw_alpha, cfg.hw_beta, cfg.hw_gamma).to(dev)
@@ -195,16 +201,19 @@ class BatchScorer:
             anom = None
         else:
             if mode is not None:
-                fit = sm_ref.fit_smoothing(t_hist, mode, sm_ref.make_grid(mode, cfg.hw_alpha, cfg.hw_beta,
-                                                                          cfg.hw_gamma), m=max(m, 1))
+                grid = sm_ref.make_grid(mode, cfg.hw_alpha, cfg.hw_beta, cfg.hw_gamma)
+                fit = sm_ref.fit_smoothing(t_hist, mode, grid, m=max(m, 1))
                 f = sm_ref.forecast(fit, t_hz)
                 sigma, n_valid = fit.sigma, fit.n_valid
+                if cfg.horizon_variance:
+                    sigma = sigma[:, None] * det_ref.horizon_sigma_factor(grid[fit.best.long()], mode, max(m, 1), t_hz)
             else:
                 st = ma_ref.window_stats(t_hist, cfg.ma_window if algo == "moving_average" else None)
                 f = st.mean[:, None].expand(B, t_cur.shape[1])
                 sigma, n_valid = st.std, st.count
             d = det_ref.detect(f, sigma, t_cur, t_thr, t_bnd, t_low, differs=differs,
-                               pairwise_scale=cfg.pairwise_scale, model_ok=n_valid >= cfg.min_historical_points)
+                               pairwise_scale=cfg.pairwise_scale, model_ok=n_valid >= cfg.min_historical_points,
+                               **dkw)
             upper, lower, verdict, anom = d.upper, d.lower, d.verdict, d.anomaly
         upper_np = upper.float().cpu().numpy()
         lower_np = lower.float().cpu().numpy()

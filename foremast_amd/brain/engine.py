@@ -73,6 +73,7 @@ class StreamingShard:
         self.min_lower = (min_lower if min_lower is not None
                           else torch.full((N,), self.cfg.min_lower_bound, dtype=torch.float32, **kw))
         self.app_id = app_id if app_id is not None else torch.zeros(N, dtype=torch.int32, **kw)
+        self.refresh_thresholds()
         if app_stats is not None:
             if app_stats.dtype != torch.int32 or app_stats.dim() != 2 or app_stats.shape[1] != 2 \
                     or not app_stats.is_contiguous() or app_stats.device != self.device:
@@ -112,6 +113,16 @@ class StreamingShard:
             self._state_host = torch.zeros(8, dtype=torch.int32).pin_memory()
             self._state_dev = torch.zeros(8, dtype=torch.int32, device=self.device)
 
+    def refresh_thresholds(self) -> None:
+        """Per-point thresholds of the full and the lowered (pairwise) band for the
+        window of P*W points (models/detect.py effective_thresholds); call again
+        after changing ``threshold`` / ``bound``."""
+        C = self.spec.pods * self.spec.window
+        self.thr_full, self.thr_low = det_ref.effective_thresholds(
+            self.threshold, self.bound, C, self.cfg.pairwise_scale, self.cfg.window_correction)
+        self.thr_full = self.thr_full.to(self.device).contiguous()
+        self.thr_low = self.thr_low.to(self.device).contiguous()
+
     def enable_anomaly_list(self, cap: int) -> None:
         if self.gpu:
             from ..ops import kernels as K
@@ -135,7 +146,10 @@ class StreamingShard:
     def ingest_tick(self, newv: torch.Tensor, newb: Optional[torch.Tensor] = None) -> None:
         """``newv``: ``[N, P]`` float32 current-pod values on the shard's device;
         ``newb`` (optional, same shape): baseline-pod values streamed into the
-        baseline window at the same slot (continuous canary)."""
+        baseline window at the same slot (continuous canary).  The evicted
+        slot's pod-mean graduates into the history: the baseline pods' when a
+        baseline stream is given (the model tracks the stable version, never
+        the canary it judges), else the current pods'."""
         graduate = self.cur.ticks >= self.cur.W
         if self.gpu:
             from ..ops import kernels as K
@@ -144,10 +158,18 @@ class StreamingShard:
                           base=self.base if newb is not None else None, newb=newb)
             self.cur.ticks += 1
         else:
+            old_b = None
             if newb is not None:
                 cols = torch.arange(self.cur.P, device=self.device) * self.cur.W + self.cur.slot()
+                ob = self.base[:, cols]
+                ok = ~torch.isnan(ob)
+                cnt = ok.sum(1)
+                old_b = torch.where(cnt > 0, torch.where(ok, ob, torch.zeros_like(ob)).sum(1) / cnt.clamp(min=1),
+                                    torch.full_like(cnt, float("nan"), dtype=torch.float32))
                 self.base[:, cols] = newb.float()
             old = self.cur.push_(newv)
+            if old_b is not None:
+                old = old_b  # canary: the baseline (stable-version) pods graduate into the history
             if graduate:
                 self.hist.data[:, self.hist.next_col()] = old.to(self.hist.data.dtype)
         if graduate:
@@ -230,11 +252,12 @@ class StreamingShard:
             else:
                 self.pw_out = _rank()
             differs = self.pw_out["differs"]
-        spec = K.DetectSpec(horizons=self.horizons, threshold=self.threshold, bound=self.bound,
+        spec = K.DetectSpec(horizons=self.horizons, threshold=self.thr_full, bound=self.bound,
                             min_lower=self.min_lower, cur=self.cur.data, differs=differs,
                             pw_scale=cfg.pairwise_scale, min_valid=cfg.min_historical_points,
                             want_band=self.spec.want_band, app_id=self.app_id, app_stats=self.app_stats,
-                            anomalies=self.anomalies, max_horizon=self.cur.W)
+                            anomalies=self.anomalies, max_horizon=self.cur.W, threshold_low=self.thr_low,
+                            pw_min_points=cfg.pairwise_min_points, horizon_variance=cfg.horizon_variance)
         if self.anomalies is not None:
             self.anomalies.reset()
         h = self.hist
@@ -246,7 +269,7 @@ class StreamingShard:
             if overlap and K.last_detect_deferred:
                 main.wait_stream(self._side)
                 Tp = K.smoothing_geometry(self.mode, h.length, self.spec.season)[0]
-                K.hw_detect_deferred(self.out, spec, Tp, self.spec.season)
+                K.hw_detect_deferred(self.out, spec, Tp, self.spec.season, grid=self.grid)
         elif self.algorithm in ("moving_average_all", "moving_average"):
             length = h.length
             head = h.head
@@ -274,9 +297,12 @@ class StreamingShard:
         if self.mode is not None:
             fit = sm_ref.fit_smoothing(y, self.mode, self.grid.cpu(), m=self.spec.season)
             f = sm_ref.forecast(fit, h)
-            sigma = fit.sigma
             n_valid = fit.n_valid
-            extra = {"level": fit.level, "trend": fit.trend, "sigma": sigma, "best": fit.best.int()}
+            extra = {"level": fit.level, "trend": fit.trend, "sigma": fit.sigma, "best": fit.best.int()}
+            sigma = fit.sigma
+            if cfg.horizon_variance:
+                params = self.grid.cpu()[fit.best.long()]
+                sigma = fit.sigma[:, None] * det_ref.horizon_sigma_factor(params, self.mode, self.spec.season, h)
         else:
             win = cfg.ma_window if self.algorithm == "moving_average" else None
             st = ma_ref.window_stats(y, win)
@@ -285,8 +311,9 @@ class StreamingShard:
             n_valid = st.count
             extra = {"mean": st.mean, "std": st.std}
         ok = n_valid >= cfg.min_historical_points
-        d = det_ref.detect(f, sigma, self.cur.data, self.threshold, self.bound, self.min_lower,
-                           differs=differs, pairwise_scale=cfg.pairwise_scale, model_ok=ok)
+        d = det_ref.detect(f, sigma, self.cur.data, self.thr_full, self.bound, self.min_lower,
+                           differs=differs, pairwise_scale=cfg.pairwise_scale, model_ok=ok,
+                           threshold_low=self.thr_low, pw_min_points=cfg.pairwise_min_points)
         v = d.verdict.long()
         self.app_stats.index_put_((self.app_id.long(), torch.zeros_like(v)), (v == 1).int(), accumulate=True)
         self.app_stats.index_put_((self.app_id.long(), torch.ones_like(v)), (v >= 0).int(), accumulate=True)

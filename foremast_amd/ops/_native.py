@@ -35,7 +35,8 @@ class DetectArgs(C.Structure):
         ("horizons", P), ("h_ld", LL), ("C", I), ("min_valid", I),
         ("cur", P), ("ld_cur", LL),
         ("threshold", P), ("bound", P), ("min_lower", P), ("differs", P),
-        ("pw_scale", F), ("_pad0", I),
+        ("pw_scale", F), ("pw_min_points", I), ("threshold_low", P),
+        ("hv_grid", P), ("hv_mode", I), ("hv_m", I),
         ("forecast", P), ("upper", P), ("lower", P), ("count", P), ("verdict", P),
         ("score", P), ("app_id", P), ("app_stats", P),
         ("anom_count", P), ("anom_series", P), ("anom_col", P), ("anom_val", P), ("anom_cap", I), ("_pad1", I),

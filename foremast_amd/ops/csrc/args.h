@@ -16,8 +16,14 @@ struct DetectArgs {
   const signed char* bound;     // [N]
   const float* min_lower;       // [N]
   const unsigned char* differs; // [N] or null
-  float pw_scale;
-  int _pad0;
+  float pw_scale;               // lowered threshold = threshold * pw_scale (when threshold_low is null)
+  int pw_min_points;            // the lowered band applies only with >= this many points beyond it
+  const float* threshold_low;   // [N] lowered (pairwise) threshold, or null
+  // h-step forecast variance of the fitted smoothing model (null grid: sigma is used
+  // unchanged for every horizon).  hv_mode 1 ES, 2 DES, 3 HW (season hv_m)
+  const float* hv_grid;         // [G, 3] (alpha, beta, gamma)
+  int hv_mode;
+  int hv_m;
   float* forecast;              // [N, C] or null
   float* upper;                 // [N, C] or null
   float* lower;                 // [N, C] or null

@@ -798,7 +798,7 @@ __device__ __forceinline__ void hw_half_block(const SmoothArgs& a, int hmax, int
     if (ph < 0) ph += m;
     ph = ph < HALF_HB ? ph : HALF_HB - 1;  // host guarantees ph < hmax; clamp keeps LDS reads in bounds
     return gL + (float)h * gB + sb[ph];
-  });
+  }, gIdx);
 }
 
 template <int K>
@@ -1270,7 +1270,7 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
     if (ph < 0) ph += m;
     ph = ph < HALF_HB ? ph : HALF_HB - 1;  // host guarantees ph < hmax; clamp keeps LDS reads in bounds
     return gL + (float)h * gB + sb[ph];
-  });
+  }, gIdx);
 }
 
 // Workgroups [0, n_full) fit whole series pairs 0..n_full-1; the rest are split-tail
@@ -1310,7 +1310,7 @@ __global__ __launch_bounds__(256) void hw_detect_params_kernel(const SmoothArgs 
     if (ph < 0) ph += m;
     ph = ph < HALF_HB ? ph : HALF_HB - 1;
     return gL + (float)h * gB + sb[ph];
-  });
+  }, a.best ? a.best[n] : -1);
 }
 
 extern "C" int fm_hw_detect_params(const SmoothArgs* a, hipStream_t st) {
@@ -1672,7 +1672,7 @@ __global__ __launch_bounds__(256, MINW) void hw_scan_kernel(const SmoothArgs a) 
                     }
                     return f;
                   },
-                  red);
+                  red, gIdx);
 }
 
 template <int K>

@@ -4,12 +4,15 @@
 //   hist [N, R]      7-day history ring (bf16 or f32), one point per minute;
 //   cur  [N, P*W]    current window, P pods x W slots (slot = tick mod W);
 //   newv [N, P]      this tick's per-pod values (from the host ingest, H2D);
-//   base [N, P*W]    optional baseline (old-pod) window, streamed the same way
-//   newb [N, P]      (no graduation: the model history is the app aggregate).
-// Per series: the slot being overwritten holds the oldest current points
-// (age W); their pod-mean graduates into history at column hist_col, then
-// the new per-pod values take the slot.  One thread per series; everything
-// the tick needs is touched once.
+//   base [N, P*W]    optional baseline (old-pod) window, streamed the same way;
+//   newb [N, P]
+// Per series: the slot being overwritten holds the oldest points (age W); their
+// pod-mean graduates into history at column hist_col, then the new per-pod
+// values take the slot.  With a baseline stream (canary) it is the BASELINE
+// pods' mean that graduates: the model history follows the stable version and
+// the canary is never fitted into the model it is judged against.  Without one
+// (continuous monitoring) the current pods' mean graduates.  One thread per
+// series; everything the tick needs is touched once.
 #include "common.h"
 
 template <typename TH>
@@ -26,18 +29,23 @@ __global__ __launch_bounds__(256) void tick_ingest_kernel(TH* __restrict__ hist,
     slot = st[1];
     graduate = st[2];
   }
+  float s = 0.f, c = 0.f;
   if (base) {
     float* brow = base + (long long)n * ld_c;
     const float* nb = newb + (long long)n * ld_n;
-    for (int p = 0; p < P; ++p) brow[p * W + slot] = nb[p];
+    for (int p = 0; p < P; ++p) {
+      const int col = p * W + slot;
+      const float old = brow[col];
+      if (old == old) { s += old; c += 1.f; }
+      brow[col] = nb[p];
+    }
   }
-  float s = 0.f, c = 0.f;
   float* row = cur + (long long)n * ld_c;
   const float* nv = newv + (long long)n * ld_n;
   for (int p = 0; p < P; ++p) {
     const int col = p * W + slot;
     const float old = row[col];
-    if (old == old) { s += old; c += 1.f; }
+    if (!base && old == old) { s += old; c += 1.f; }
     row[col] = nv[p];
   }
   if (graduate) hist[(long long)n * ld_h + hist_col] = from_f32<TH>(c > 0.f ? s / c : fm_nan());

@@ -296,7 +296,7 @@ __global__ __launch_bounds__(256) void smooth_fit_kernel(const SmoothArgs a) {
                     }
                     return f;
                   },
-                  red);
+                  red, gIdx);
 }
 
 template <int KMAX, int MODE>

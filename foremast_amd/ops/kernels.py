@@ -67,6 +67,12 @@ class DetectSpec:
     # host-known upper bound of ``horizons`` (all values in 1..max_horizon); lets the
     # Holt-Winters kernel keep only the seasonal phases the forecast needs (variant 4)
     max_horizon: Optional[int] = None
+    # lowered (pairwise) threshold per series (models/detect.py effective_thresholds);
+    # None: threshold * pw_scale.  The lowered band needs >= pw_min_points points.
+    threshold_low: Optional[torch.Tensor] = None
+    pw_min_points: int = 1
+    # scale sigma by the h-step forecast-error factor of the fitted smoothing model
+    horizon_variance: bool = True
 
 
 class AnomalyBuffer:
@@ -110,6 +116,7 @@ def _fill_detect(d: nat.DetectArgs, spec: DetectSpec, N: int, device, out: Dict[
     _vec(spec.bound, N, torch.int8, "bound", device)
     _vec(spec.min_lower, N, torch.float32, "min_lower", device)
     _vec(spec.differs, N, torch.uint8, "differs", device)
+    _vec(spec.threshold_low, N, torch.float32, "threshold_low", device)
     if spec.cur is not None:
         c = spec.cur
         _need(c.dim() == 2 and c.shape[0] == N and c.shape[1] == C,
@@ -149,6 +156,9 @@ def _fill_detect(d: nat.DetectArgs, spec: DetectSpec, N: int, device, out: Dict[
     d.min_lower = nat.ptr(spec.min_lower)
     d.differs = nat.ptr(spec.differs)
     d.pw_scale = float(spec.pw_scale)
+    d.pw_min_points = int(spec.pw_min_points)
+    d.threshold_low = nat.ptr(spec.threshold_low)
+    d.hv_grid, d.hv_mode, d.hv_m = None, 0, 0
     d.forecast = nat.ptr(out.get("forecast"))
     d.upper = nat.ptr(out.get("upper"))
     d.lower = nat.ptr(out.get("lower"))
@@ -157,6 +167,15 @@ def _fill_detect(d: nat.DetectArgs, spec: DetectSpec, N: int, device, out: Dict[
     d.score = nat.ptr(out["score"])
     d.app_id = nat.ptr(spec.app_id)
     d.app_stats = nat.ptr(spec.app_stats)
+
+
+def _set_hvar(d: nat.DetectArgs, spec: DetectSpec, grid: torch.Tensor, mode: int, m: int) -> None:
+    """h-step forecast-error scaling of sigma from the fitted grid point (detect.h
+    ``hstep_factor``); call after :func:`_fill_detect`."""
+    if spec.horizon_variance:
+        d.hv_grid = nat.ptr(grid)
+        d.hv_mode = {MODE_ES: 1, MODE_DES: 2, MODE_HW: 3}[int(mode)]
+        d.hv_m = int(m) if mode == MODE_HW else 0
 
 
 def _hist_check(hist: torch.Tensor, head: int, length: int) -> None:
@@ -347,6 +366,7 @@ def smoothing_fit(hist: torch.Tensor, head: int, length: int, mode: int, m: int,
     a.season_out = nat.ptr(out.get("season")) if (want_season and mode == MODE_HW) else 0
     a.pair_tab = nat.ptr(pair_table(grid, k)) if variant == 3 else 0
     _fill_detect(a.det, det, N, dev, out)
+    _set_hvar(a.det, det, grid, mode, mm)
     nat.check(lib.fm_smooth_fit(a, int(mode), int(bf16), int(variant), nat.stream_handle(dev)), "fm_smooth_fit")
     return out
 
@@ -426,6 +446,7 @@ def _hw_half_fit(lib, hist, head, length, m, grid, det, Tp, pad, hmax, out, resi
               "head_dev must be an int32 device scalar")
         a.head_dev = nat.ptr(head_dev)
     _fill_detect(a.det, det, N, dev, out)
+    _set_hvar(a.det, det, grid, MODE_HW, m)
     if defer:
         for kname, shape in (("season_hb", (N, HALF_HB)), ("nvalid", (N,))):
             if kname not in out:
@@ -483,6 +504,7 @@ def _es_seq_fit(lib, hist, head, length, mode, grid, det, out, head_dev=None, de
     a.nvalid_out = nat.ptr(out["nvalid"])
     a.season_hb = nat.ptr(out["season_hb"])
     _fill_detect(a.det, det, N, dev, out)
+    _set_hvar(a.det, det, grid, mode, 1)
     if defer:
         a.det.C = 0
     global last_hw_variant, last_detect_deferred
@@ -493,7 +515,8 @@ def _es_seq_fit(lib, hist, head, length, mode, grid, det, out, head_dev=None, de
     return out
 
 
-def hw_detect_deferred(out: Dict[str, torch.Tensor], det: DetectSpec, Tp: int, m: int) -> Dict[str, torch.Tensor]:
+def hw_detect_deferred(out: Dict[str, torch.Tensor], det: DetectSpec, Tp: int, m: int,
+                       grid: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
     """Band / verdict / per-app counters / K9 list for a fit run with
     ``smoothing_fit(..., defer_detect=True)`` (hw_scan.hip ``hw_detect_params_kernel``)."""
     lib = nat.require()
@@ -505,7 +528,13 @@ def hw_detect_deferred(out: Dict[str, torch.Tensor], det: DetectSpec, Tp: int, m
     a.N, a.Tp, a.m = N, int(Tp), int(m)
     a.level, a.trend, a.sigma = nat.ptr(out["level"]), nat.ptr(out["trend"]), nat.ptr(out["sigma"])
     a.season_hb, a.nvalid_out = nat.ptr(out["season_hb"]), nat.ptr(out["nvalid"])
+    a.best = nat.ptr(out.get("best"))
     _fill_detect(a.det, det, N, dev, out)
+    if grid is not None:
+        _need("best" in out, "horizon variance needs out['best'] from the fit")
+        _need(grid.dim() == 2 and grid.shape[1] == 3 and grid.dtype == torch.float32 and grid.is_contiguous()
+              and grid.device == dev, "grid must be contiguous float32 [G, 3] on device")
+        _set_hvar(a.det, det, grid, MODE_HW, m)
     nat.check(lib.fm_hw_detect_params(a, nat.stream_handle(dev)), "fm_hw_detect_params")
     return out
 

@@ -70,6 +70,14 @@ class BrainConfig:
     season: int = 1440
     ma_window: int = 60
     pairwise_scale: float = 0.5
+    # detection semantics (docs/SCORING.md "Band, bound and verdict"): the lowered
+    # pairwise band needs this many points outside it (ML_PAIRWISE_MIN_ANOMALIES);
+    # per-point thresholds are Sidak-corrected for the window size
+    # (FOREMAST_WINDOW_CORRECTION = sidak | none); sigma is scaled to the forecast
+    # horizon (FOREMAST_HORIZON_VARIANCE = 1 | 0)
+    pairwise_min_points: int = 3
+    window_correction: str = "sidak"
+    horizon_variance: bool = True
     poll_seconds: float = 5.0
     hw_alpha: tuple = (0.1, 0.3, 0.5, 0.8)
     hw_beta: tuple = (0.0, 0.01, 0.05, 0.1)
@@ -134,6 +142,9 @@ class BrainConfig:
         c.ma_window = int(f("FOREMAST_MA_WINDOW", c.ma_window, int))
         c.pairwise_scale = f("FOREMAST_PAIRWISE_SCALE", c.pairwise_scale)
         c.poll_seconds = f("FOREMAST_POLL_SECONDS", c.poll_seconds)
+        c.pairwise_min_points = int(f("ML_PAIRWISE_MIN_ANOMALIES", c.pairwise_min_points, int))
+        c.window_correction = (e.get("FOREMAST_WINDOW_CORRECTION") or c.window_correction).strip().lower()
+        c.horizon_variance = e.get("FOREMAST_HORIZON_VARIANCE", "1").strip().lower() not in ("0", "false", "no")
         c.lstm_hidden = int(f("FOREMAST_LSTM_HIDDEN", c.lstm_hidden, int))
         c.lstm_window = int(f("FOREMAST_LSTM_WINDOW", c.lstm_window, int))
         c.metrics_port = int(f("FOREMAST_METRICS_PORT", c.metrics_port, int))

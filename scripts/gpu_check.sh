@@ -17,9 +17,14 @@ run() {
 STEPS=${STEPS:-"tests smoke bench prof"}
 for s in $STEPS; do
   case $s in
-    tests) run gpu_tests 900 python -m pytest tests -m gpu -x -q ;;
+    tests) run gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    kgpu) run kernel_tests 600 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
+    bench0) run bench_frac0 600 python bench.py --steps 20 --warmup 5 --anomaly-frac 0 ;;
+    benchshift) run bench_shift 600 python bench.py --steps 20 --warmup 5 --anomaly-kind shift3sigma ;;
+    hw10k) run bench_hw10k 600 python bench.py --config hw10k --steps 20 --warmup 5 ;;
+    graph) run bench_graph 600 python bench.py --steps 20 --warmup 5 --graph ;;
     kbench) run kbench 600 python scripts/bench_kernels.py ;;
     lstm) run bench_lstm 600 python bench.py --config lstm --steps 20 --warmup 5 ;;
     mv) run bench_mv 600 python bench.py --config multivariate --steps 20 --warmup 5 ;;

@@ -50,6 +50,29 @@ def _det_spec(K, N, C, dev, cur=None, thr=2.0, bound=3):
         min_lower=torch.full((N,), -1e30, device=dev), cur=cur)
 
 
+def _ref_detect(out, grid, mode, m, hz, cur, thr=2.0, bound=3, differs=None, thr_low=None, pw_min=1):
+    """Reference verdicts for a kernel fit: the kernel's own forecast and grid
+    choice, sigma scaled to each horizon (models/detect.py horizon_sigma_factor)."""
+    N = cur.shape[0]
+    params = grid.cpu().float()[out["best"].cpu().long()]
+    sig = out["sigma"].cpu()[:, None] * det_ref.horizon_sigma_factor(params, mode, m, hz.cpu())
+    return det_ref.detect(out["forecast"].cpu(), sig, cur.cpu(), torch.full((N,), thr),
+                          torch.full((N,), bound, dtype=torch.int8), torch.full((N,), -1e30),
+                          differs=None if differs is None else differs.cpu(), threshold_low=thr_low,
+                          pw_min_points=pw_min)
+
+
+def _assert_near_optimal(yl, grid, mode, m, best, rel=1e-3):
+    """The kernel's grid point must be within ``rel`` of the best fp64 SSE (bf16 /
+    fp32 summation order may flip near-ties, but never pick a clearly worse fit)."""
+    y64 = torch.tensor(yl, dtype=torch.float64)
+    sse = torch.stack([sm_ref.fit_smoothing(y64, mode, grid[g:g + 1].double(), m=m).sse
+                       for g in range(grid.shape[0])], 1)
+    chosen = sse.gather(1, best.cpu().long()[:, None]).squeeze(1)
+    opt = sse.min(1).values
+    assert torch.all(chosen <= opt * (1 + rel) + 1e-6), (chosen / opt).max()
+
+
 @pytest.mark.parametrize("mode,m,T,nan", [
     (sm_ref.MODE_HW, 24, 24 * 5 + 7, 0.0),
     (sm_ref.MODE_HW, 24, 24 * 6, 0.02),
@@ -90,8 +113,7 @@ def test_smoothing_kernel_matches_reference(K, mode, m, T, nan, dtype, variant):
     f_ref = sm_ref.forecast(ref, torch.arange(1, C + 1))
     np.testing.assert_allclose(out["forecast"].cpu().numpy()[same.numpy()], f_ref.numpy()[same.numpy()],
                                rtol=2e-3, atol=5e-3)
-    d = det_ref.detect(torch.tensor(out["forecast"].cpu()), out["sigma"].cpu(), cur.cpu(),
-                       torch.full((N,), 2.0), torch.full((N,), 3, dtype=torch.int8), torch.full((N,), -1e30))
+    d = _ref_detect(out, grid, mode, m, torch.arange(1, C + 1), cur)
     assert torch.equal(d.count, out["count"].cpu())
     assert torch.equal(d.verdict, out["verdict"].cpu())
 
@@ -131,8 +153,7 @@ def test_es_sequential_kernel_matches_reference(K, mode, T, nan, lead, N, dtype)
     np.testing.assert_allclose(out["nvalid"].cpu().numpy(), ref.n_valid.numpy())
     f_ref = sm_ref.forecast(ref, torch.arange(1, C + 1))
     np.testing.assert_allclose(out["forecast"].cpu().numpy()[same], f_ref.numpy()[same], rtol=2e-3, atol=5e-3)
-    d = det_ref.detect(out["forecast"].cpu(), out["sigma"].cpu(), cur.cpu(),
-                       torch.full((N,), 2.0), torch.full((N,), 3, dtype=torch.int8), torch.full((N,), -1e30))
+    d = _ref_detect(out, grid, mode, 1, torch.arange(1, C + 1), cur)
     assert torch.equal(d.count, out["count"].cpu()) and torch.equal(d.verdict, out["verdict"].cpu())
 
 
@@ -150,6 +171,7 @@ def test_smoothing_kernel_flagship_shape(K, variant):
     ref = sm_ref.fit_smoothing(ring.float().cpu(), sm_ref.MODE_HW, grid, m=m)
     same = (out["best"].cpu().long() == ref.best)
     assert same.float().mean() >= 0.75
+    _assert_near_optimal(ring.float().cpu().numpy(), grid, sm_ref.MODE_HW, m, out["best"])
     np.testing.assert_allclose(out["sigma"].cpu().numpy(), ref.sigma.numpy(), rtol=5e-3)
     sm_ = same.numpy()
     np.testing.assert_allclose(out["season"].cpu().numpy()[sm_], ref.season.numpy()[sm_], rtol=2e-2, atol=2e-2)
@@ -352,12 +374,12 @@ def test_hw_half_variant_matches_reference(K, case, variant):
     kb = out["best"].cpu().long()
     same = (kb == ref.best).numpy()
     assert same.mean() >= 0.75
+    _assert_near_optimal(yl, grid, sm_ref.MODE_HW, m, kb)
     np.testing.assert_allclose(out["sigma"].cpu().numpy(), ref.sigma.numpy(), rtol=5e-3)
     np.testing.assert_allclose(out["level"].cpu().numpy()[same], ref.level.numpy()[same], rtol=2e-3, atol=5e-3)
     f_ref = sm_ref.forecast(ref, hz.long())
     np.testing.assert_allclose(out["forecast"].cpu().numpy()[same], f_ref.numpy()[same], rtol=5e-3, atol=2e-2)
-    d = det_ref.detect(out["forecast"].cpu(), out["sigma"].cpu(), cur.cpu(), torch.full((N,), 2.0),
-                       torch.full((N,), 3, dtype=torch.int8), torch.full((N,), -1e30))
+    d = _ref_detect(out, grid, sm_ref.MODE_HW, m, hz, cur)
     assert torch.equal(d.count, out["count"].cpu())
     assert torch.equal(d.verdict, out["verdict"].cpu())
     # variant 3 (one series per wave) on the same input agrees on the chosen grid point
@@ -403,3 +425,55 @@ def test_hw_split_plan():
     assert lib.fm_hw_d_split_plan(50000, 512, 4096) == 0    # 100k: the tail is already negligible
     assert lib.fm_hw_d_split_plan(20, 512, 4096) == 20      # tiny batches: every pair in two halves
     assert lib.fm_hw_d_split_plan(20, 0, 4096) == 0
+
+
+@pytest.mark.parametrize("which", ["window_stats", "holt_winters", "hw_deferred"])
+def test_two_rule_detection_matches_reference(K, which):
+    """Full band + lowered pairwise band that needs >= pw_min_points points
+    (detect.h det_decide): kernel verdicts, counts, bands and the K9 list equal
+    the reference on series built to sit on each side of both rules."""
+    from foremast_amd.brain.engine import synthetic_history
+    dev = torch.device("cuda:0")
+    N, T, m, C = 2000, 2 * 1440, 1440, 10
+    hist = synthetic_history(N, T, m, dev, seed=5).to(torch.bfloat16)
+    g = torch.Generator(device=dev).manual_seed(3)
+    hf = hist.float()
+    # noise on the scale of each model's sigma, so both rules fire on some series and not others
+    scale = hf.std(1, keepdim=True) if which == "window_stats" else (hf[:, 1:] - hf[:, :-1]).std(1, keepdim=True)
+    cur = (hf[:, -C:] + torch.randn((N, C), generator=g, device=dev) * scale).contiguous()
+    differs = (torch.arange(N, device=dev) % 2).to(torch.uint8)
+    thr = torch.full((N,), 3.0, device=dev)
+    bound = torch.tensor([1, 2, 3, 3], dtype=torch.int8, device=dev).repeat(N // 4)
+    full, low = det_ref.effective_thresholds(thr.cpu(), bound.cpu(), C, 0.5, "sidak")
+    spec = K.DetectSpec(horizons=torch.arange(1, C + 1, dtype=torch.int32, device=dev), threshold=full.to(dev),
+                        bound=bound, min_lower=torch.full((N,), -1e9, device=dev), cur=cur, differs=differs,
+                        threshold_low=low.to(dev), pw_min_points=3, anomalies=K.AnomalyBuffer(N * C, dev),
+                        max_horizon=C)
+    spec.anomalies.reset()
+    grid = sm_ref.make_grid(sm_ref.MODE_HW, (0.1, 0.5), (0.0, 0.1), (0.1, 0.5)).to(dev)
+    if which == "window_stats":
+        out = K.window_stats(hist, 0, T, spec)
+        sig = out["std"].cpu()
+    else:
+        if which == "hw_deferred":
+            out = K.smoothing_fit(hist, 0, T, sm_ref.MODE_HW, m, grid, spec, defer_detect=True, variant=5)
+            if K.last_detect_deferred:
+                Tp = K.smoothing_geometry(sm_ref.MODE_HW, T, m)[0]
+                K.hw_detect_deferred(out, spec, Tp, m, grid=grid)
+        else:
+            out = K.smoothing_fit(hist, 0, T, sm_ref.MODE_HW, m, grid, spec)
+        params = grid.cpu()[out["best"].cpu().long()]
+        sig = out["sigma"].cpu()[:, None] * det_ref.horizon_sigma_factor(params, sm_ref.MODE_HW, m,
+                                                                        torch.arange(1, C + 1))
+    torch.cuda.synchronize()
+    d = det_ref.detect(out["forecast"].cpu(), sig, cur.cpu(), full, bound.cpu(), torch.full((N,), -1e9),
+                       differs=differs.cpu(), threshold_low=low, pw_min_points=3)
+    assert torch.equal(d.verdict, out["verdict"].cpu())
+    assert torch.equal(d.count, out["count"].cpu())
+    low_fired = (differs.cpu().bool() & (d.count > 0))
+    assert int(low_fired.sum()) > 0 and int((d.verdict == 0).sum()) > 0  # both sides exercised
+    np.testing.assert_allclose(out["upper"].cpu().numpy(), d.upper.numpy(), rtol=1e-4, atol=1e-3)
+    s_, c_, v_, overflow = spec.anomalies.fetch()
+    assert not overflow
+    exp = d.anomaly.nonzero().numpy()
+    assert len(exp) == len(s_) and (exp[:, 0] == s_).all() and (exp[:, 1] == c_).all()

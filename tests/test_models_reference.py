@@ -230,3 +230,61 @@ def test_seasonal_decompose_reference():
     y2[:, 50:55] = float("nan")
     d2 = seasonal_decompose(y2, m)
     assert torch.isfinite(d2.trend[:, 52]).all() and torch.allclose(d2.seasonal, d.seasonal, atol=0.05)
+
+
+def test_horizon_sigma_factor_matches_direct_sum():
+    """Closed form of the h-step forecast-error factor equals the direct sum of
+    c_j^2 (c_j = a (1 + j b) + g (1 - a) [j mod m == 0]) for ES / DES / HW."""
+    rng = np.random.default_rng(7)
+    params = torch.tensor(rng.uniform(0.05, 0.9, (5, 3)), dtype=torch.float32)
+    h = torch.arange(1, 40)
+    for mode, m in ((0, 0), (1, 0), (2, 7), (2, 1)):
+        got = detect.horizon_sigma_factor(params, mode, m, h).double().numpy()
+        for i in range(5):
+            a, b, g = params[i].double().tolist()
+            b = b if mode >= 1 else 0.0
+            for k, hh in enumerate(h.tolist()):
+                v = 1.0
+                for j in range(1, hh):
+                    c = a * (1 + j * b) + (g * (1 - a) if mode == 2 and m > 0 and j % m == 0 else 0.0)
+                    v += c * c
+                assert got[i, k] == pytest.approx(np.sqrt(v), rel=1e-5)
+
+
+def test_window_threshold_sidak():
+    """P(any of C points outside the corrected band) equals P(one point outside
+    the uncorrected band), on the sides the bound enables."""
+    from scipy import stats
+    thr = torch.tensor([2.0, 3.0, 4.0, 2.0])
+    bound = torch.tensor([1, 2, 3, 3], dtype=torch.int8)
+    for C in (1, 10, 50):
+        z = detect.window_threshold(thr, bound, C).double().numpy()
+        for i in range(4):
+            sides = 2 if int(bound[i]) == 3 else 1
+            p1 = sides * stats.norm.sf(float(thr[i]))
+            pc = sides * stats.norm.sf(z[i])
+            assert 1 - (1 - pc) ** C == pytest.approx(p1, rel=1e-4)
+    assert torch.equal(detect.window_threshold(thr, bound, 50, "none"), thr)
+
+
+def test_pairwise_lowered_band_needs_min_points():
+    """The lowered band applies only when differs AND >= pw_min_points points
+    fall outside it; one point outside the full band always flags."""
+    f = torch.zeros(4, 10)
+    sig = torch.ones(4)
+    x = torch.zeros(4, 10)
+    x[0, :2] = 2.5      # 2 points between the lowered (2) and full (4) bands
+    x[1, :3] = 2.5      # 3 such points
+    x[2, 0] = 5.0       # one spike beyond the full band
+    x[3, :3] = 2.5      # 3 points, but baseline and current do not differ
+    thr = torch.full((4,), 4.0)
+    low = torch.full((4,), 2.0)
+    differs = torch.tensor([1, 1, 0, 0], dtype=torch.uint8)
+    d = detect.detect(f, sig, x, thr, torch.full((4,), 3, dtype=torch.int8), torch.full((4,), -1e9),
+                      differs=differs, threshold_low=low, pw_min_points=3)
+    assert d.verdict.tolist() == [0, 1, 1, 0]
+    assert d.count.tolist() == [0, 3, 1, 0]
+    assert float(d.upper[1, 0]) == 2.0 and float(d.upper[0, 0]) == 4.0  # band of the rule in force
+    d1 = detect.detect(f, sig, x, thr, torch.full((4,), 3, dtype=torch.int8), torch.full((4,), -1e9),
+                       differs=differs, threshold_low=low, pw_min_points=1)
+    assert d1.verdict.tolist() == [1, 1, 1, 0]
