@@ -132,6 +132,29 @@ class StreamingShard:
     def load_history(self, values: torch.Tensor) -> None:
         self.hist.load(values.to(self.device))
 
+    def load_rows(self, rows: torch.Tensor, values: torch.Tensor) -> None:
+        """Write the full history AND current window of some rows (a series
+        joining a running shard): ``values`` ``[k, length + W]`` oldest first,
+        the last W points go to the window (every pod); the ring rotation is
+        resolved with two column-slice copies, no ``[k, length]`` index tensor."""
+        dev = self.device
+        rows = rows.to(dev, torch.long)
+        v = values.to(dev, torch.float32)
+        L, R, W, P = self.hist.length, self.hist.R, self.cur.W, self.cur.P
+        if v.dim() != 2 or v.shape[0] != rows.numel() or v.shape[1] != L + W:
+            raise ValueError(f"values must be [{rows.numel()}, {L + W}]")
+        hv = v[:, :L].to(self.hist.data.dtype)
+        head = self.hist.head
+        n1 = min(L, R - head)
+        self.hist.data[:, head:head + n1].index_copy_(0, rows, hv[:, :n1])
+        if L > n1:
+            self.hist.data[:, :L - n1].index_copy_(0, rows, hv[:, n1:])
+        for a in range(W):  # age a (0 = newest) sits in slot (ticks - 1 - a) mod W
+            slot = (self.cur.ticks - 1 - a) % W
+            col = v[:, L + W - 1 - a:L + W - a]
+            for p in range(P):
+                self.cur.data[:, p * W + slot:p * W + slot + 1].index_copy_(0, rows, col)
+
     def set_baseline(self, values: torch.Tensor) -> None:
         self.base.copy_(values.to(self.device, torch.float32))
 

@@ -7,17 +7,25 @@ the job runs.  Instead of refetching and refitting each job independently
 canary/rollout jobs), the :class:`StreamingMonitor` keeps every continuous
 series resident in one :class:`~foremast_amd.brain.engine.StreamingShard`:
 
-* history: 7 days at the query step in the HBM bf16 ring, loaded once per
-  membership change with ONE range query per metric family (the bare
-  recorded series name returns every app's series; the response is parsed by
-  the native C++ matrix parser and scattered by ``(namespace, app)``);
-* every tick: one short range query per metric family for the newest point
-  of all series → tick ingest kernel → one fused scoring launch for all
-  series → per-job verdicts;
-* jobs: leased from the job store with a strategy filter (the one-shot
-  worker skips them), lease renewed each tick; any anomalous series finishes
-  its job ``completed_unhealth`` with the anomalous point; past ``endTime``
-  a job finishes ``completed_health``; band gauges are exported for the UI.
+* rows: one per (endpoint, metric, namespace, app) series.  Rows are stable
+  while a series is live; a new job's series take free rows (the shard grows
+  by doubling when full) and only THEIR history is fetched, a finished job's
+  rows are cleared and freed — no full rebuild on membership changes;
+* history: 7 days at the query step, fetched in chunks that stay far below
+  Prometheus' ``--query.max-samples`` (≤ ``history_chunk_points`` per query in
+  time and ≤ ``apps_per_query`` apps per selector, ``app=~"a|b|…"``), decoded
+  by the native keyed parser straight into a pinned staging block (each series
+  lands in its row, no per-series Python) and copied H2D in one transfer;
+* every tick: one short range query per metric family for the newest points of
+  all series → keyed decode into a pinned ``[rows, k]`` block → H2D → tick
+  ingest kernel per point → one fused scoring launch for all series → per-job
+  verdicts;
+* jobs: leased from the job store with a strategy filter (the one-shot worker
+  skips them) and an optional ownership filter (``owns``: the node brain
+  shards apps over GPU ranks, ``brain/node.py``); any anomalous series
+  finishes its job ``completed_unhealth`` with the anomalous points; past
+  ``endTime`` a job finishes ``completed_health``; band gauges are exported
+  for the UI; per-app counters feed the node health table.
 """
 
 from __future__ import annotations
@@ -25,15 +33,17 @@ from __future__ import annotations
 import asyncio
 import json
 import logging
+import re
 import time
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Tuple
+from typing import Callable, Dict, List, Optional, Set, Tuple
 from urllib.parse import quote
 
 import numpy as np
 import torch
 
 from ..api import rest as r
+from ..ingest import native
 from ..promql.client import PromClient
 from ..promql.selector import SelectorError, parse_selector
 from ..service import urls
@@ -46,23 +56,58 @@ from .engine import ShardSpec, StreamingShard
 log = logging.getLogger("foremast.streaming")
 
 STRATEGY_CONTINUOUS = "continuous"
+Key = Tuple[str, str, str, str]  # (endpoint, metric, namespace, app)
 
 
 def is_continuous(doc) -> bool:
     return (doc.get("strategy") or "").lower() == STRATEGY_CONTINUOUS
 
 
+def series_of(doc) -> Dict[str, Key]:
+    """alias → series key of a job's historical queries."""
+    out = {}
+    for alias, url in urls.parse_config(doc.get("historicalConfig", "")).items():
+        try:
+            p = urls.parse_prometheus_url(url)
+            sel = parse_selector(str(p["query"]))
+        except (urls.ConfigError, SelectorError):
+            continue
+        lab = {k: v for k, op, v in sel.matchers if op == "="}
+        endpoint = url.split("query_range?")[0]
+        out[alias] = (endpoint, sel.name, lab.get("namespace", ""), lab.get("app", ""))
+    return out
+
+
+def app_of(doc) -> Tuple[str, str]:
+    """(namespace, app) a job monitors: the first historical selector's labels,
+    else the job's appName."""
+    for key in series_of(doc).values():
+        if key[3]:
+            return key[2], key[3]
+    return "", doc.get("appName", "")
+
+
+_RE2_SPECIAL = re.compile(r"([\\.^$|?*+()\[\]{}])")
+
+
+def _re_alt(values) -> str:
+    """RE2 alternation of literal label values, escaped for a PromQL string."""
+    return "|".join(_RE2_SPECIAL.sub(r"\\\\\1", v) for v in sorted(values))
+
+
 @dataclass
 class StreamJob:
     doc: Dict
     end_ts: float
-    series: Dict[str, int] = field(default_factory=dict)  # alias -> row
+    series: Dict[str, Key] = field(default_factory=dict)  # alias -> series key
 
 
 class StreamingMonitor:
     def __init__(self, store: JobStore, cfg: Optional[BrainConfig] = None, prom: Optional[PromClient] = None,
                  device=None, worker_id: str = "stream-0", metrics: Optional[BrainMetrics] = None,
-                 ring_len: int = 10080, step: float = 60.0, window: int = 10, clock=time.time) -> None:
+                 ring_len: int = 10080, step: float = 60.0, window: int = 10, clock=time.time,
+                 owns: Optional[Callable[[Dict], bool]] = None, history_chunk_points: int = 1440,
+                 apps_per_query: int = 256, min_capacity: int = 64) -> None:
         self.store = store
         self.cfg = cfg or BrainConfig.from_env()
         self.prom = prom or PromClient()
@@ -72,151 +117,275 @@ class StreamingMonitor:
         self.metrics = metrics or BrainMetrics()
         self.R, self.step, self.W = ring_len, step, window
         self.clock = clock
+        self.owns = owns
+        self.chunk_pts = max(1, int(history_chunk_points))
+        self.apps_per_query = max(1, int(apps_per_query))
+        self.min_capacity = min_capacity
         self.jobs: Dict[str, StreamJob] = {}
-        self.keys: List[Tuple[str, str, str, str]] = []  # (endpoint, metric, namespace, app)
-        self.rows: Dict[Tuple[str, str, str, str], int] = {}
+        self.keys: List[Optional[Key]] = []          # row -> key (None: free row)
+        self.rows: Dict[Key, int] = {}
+        self.pending: Set[Key] = set()               # live keys whose history is not loaded yet
+        self.apps: Dict[Tuple[str, str], int] = {}   # (namespace, app) -> app index (node health table)
+        self.roster_version = 0
         self.shard: Optional[StreamingShard] = None
-        self.dirty = False
+        self.t_last: float = 0.0
         self.ticks = 0
+        self.history_queries = 0
+        self._table: Optional[Dict[Tuple[str, str], native.KeyTable]] = None
 
     # ------------------------------------------------------------------ membership
-    def _series_of(self, doc) -> Dict[str, Tuple[str, str, str, str]]:
-        out = {}
-        for alias, url in urls.parse_config(doc.get("historicalConfig", "")).items():
-            try:
-                p = urls.parse_prometheus_url(url)
-                sel = parse_selector(str(p["query"]))
-            except (urls.ConfigError, SelectorError):
-                continue
-            lab = {k: v for k, op, v in sel.matchers if op == "="}
-            endpoint = url.split("query_range?")[0]
-            out[alias] = (endpoint, sel.name, lab.get("namespace", ""), lab.get("app", ""))
-        return out
-
-    def sync(self) -> int:
-        """Lease new continuous jobs; returns how many were added."""
+    def sync(self, steal_from=None) -> int:
+        """Lease new continuous jobs (that this rank owns); returns how many were added."""
         now = self.clock()
+
+        def only(d):
+            return is_continuous(d) and (self.owns is None or self.owns(d))
         docs = self.store.claim(self.worker_id, now=now, max_stuck_s=self.cfg.max_stuck_seconds, limit=10_000,
-                                only=is_continuous)
+                                only=only, steal_from=steal_from)
         for d in docs:
             try:
                 end_ts = parse_rfc3339(d.get("endTime", "")).timestamp()
             except TimeFormatError:
                 end_ts = float("inf")
-            job = StreamJob(doc=d, end_ts=end_ts)
-            for alias, key in self._series_of(d).items():
+            job = StreamJob(doc=d, end_ts=end_ts, series=series_of(d))
+            for key in job.series.values():
                 if key not in self.rows:
-                    self.rows[key] = len(self.keys)
-                    self.keys.append(key)
-                    self.dirty = True
-                job.series[alias] = self.rows[key]
+                    self.pending.add(key)
             self.jobs[d["id"]] = job
         return len(docs)
 
-    def _compact(self) -> None:
-        """Drop series no job uses any more (after jobs finish)."""
-        used = {row for j in self.jobs.values() for row in j.series.values()}
-        if len(used) == len(self.keys):
-            return
-        keep = [k for k in self.keys if self.rows[k] in used]
-        remap = {self.rows[k]: i for i, k in enumerate(keep)}
-        self.keys = keep
-        self.rows = {k: i for i, k in enumerate(keep)}
-        for j in self.jobs.values():
-            j.series = {a: remap[row] for a, row in j.series.items()}
-        self.dirty = True
+    def release(self, pred: Callable[[Dict], bool]) -> int:
+        """Hand back the leases of jobs matching ``pred`` (re-sharding: another
+        rank owns their app now); their series are freed at the next tick."""
+        n = 0
+        for jid, job in list(self.jobs.items()):
+            if pred(job.doc):
+                self.store.update(jid, {"status": r.ST_REPROGRESS, "claimed_by": "", "not_before": 0.0},
+                                  expect_claimed_by=self.worker_id)
+                del self.jobs[jid]
+                n += 1
+        return n
 
-    # ------------------------------------------------------------------ data
-    def _families(self) -> Dict[Tuple[str, str], List[int]]:
-        fam: Dict[Tuple[str, str], List[int]] = {}
-        for i, (ep, metric, _ns, _app) in enumerate(self.keys):
-            fam.setdefault((ep, metric), []).append(i)
-        return fam
+    def live_keys(self) -> Set[Key]:
+        return {k for j in self.jobs.values() for k in j.series.values()}
 
-    async def _fetch_grid(self, start: float, n: int) -> np.ndarray:
-        """``[N, n]`` values on the grid ``start + k*step`` (NaN where missing):
-        one range query per (endpoint, metric family)."""
-        N = len(self.keys)
-        out = np.full((N, n), np.nan, dtype=np.float32)
-        fams = self._families()
-        end = start + (n - 1) * self.step
-        req = [f"{ep}query_range?query={quote(metric, safe='')}&start={int(start)}&end={int(end)}"
-               f"&step={int(self.step)}" for (ep, metric) in fams]
-        res = await self.prom.fetch_many(req)
-        for (ep, metric), series in zip(fams, res):
-            if isinstance(series, Exception):
-                log.warning("fetch %s failed: %s", metric, series)
-                continue
-            for s in series:
-                row = self.rows.get((ep, metric, s.labels.get("namespace", ""), s.labels.get("app", "")))
-                if row is None:
-                    continue
-                idx = np.rint((s.ts - start) / self.step).astype(np.int64)
-                ok = (idx >= 0) & (idx < n)
-                out[row, idx[ok]] = s.values[ok]
-        return out
+    @property
+    def n_live(self) -> int:
+        return len(self.rows)
 
-    async def rebuild(self) -> None:
-        """(Re)load every live series' history and prefill the current window."""
-        self._compact()
-        N = len(self.keys)
-        self.dirty = False
-        if N == 0:
-            self.shard = None
-            return
-        now = self.clock()
-        t_last = np.floor(now / self.step) * self.step
-        first = t_last - (self.R + self.W - 1) * self.step
-        grid = await self._fetch_grid(first, self.R + self.W)
+    # ------------------------------------------------------------------ rows
+    def _new_shard(self, capacity: int) -> StreamingShard:
         season = max(2, int(round(86400.0 / self.step)))
         algo = self.cfg.algorithm if self.cfg.algorithm in ("holt_winters", "exponential_smoothing",
                                                             "double_exponential_smoothing", "moving_average",
                                                             "moving_average_all") else "moving_average_all"
         if algo == "holt_winters" and self.R < 2 * season:
             algo = "double_exponential_smoothing"
-        aliases = [""] * N
-        for j in self.jobs.values():
-            for a, row in j.series.items():
-                aliases[row] = a
-        th = [self.cfg.for_metric(aliases[i], self.keys[i][1]) for i in range(N)]
         dev = self.device
-        spec = ShardSpec(n_series=N, ring_len=self.R, season=season, pods=1, window=self.W, algorithm=algo,
-                         pairwise="NONE", dtype=torch.bfloat16 if dev.type == "cuda" else torch.float32)
-        self.shard = StreamingShard(
-            spec, self.cfg, dev,
-            threshold=torch.tensor([t.threshold for t in th], dtype=torch.float32, device=dev),
-            bound=torch.tensor([t.bound for t in th], dtype=torch.int8, device=dev),
-            min_lower=torch.tensor([t.min_lower_bound for t in th], dtype=torch.float32, device=dev))
-        self.shard.enable_anomaly_list(cap=max(1024, 4 * N))
-        self.shard.load_history(torch.from_numpy(np.ascontiguousarray(grid[:, :self.R])))
-        for k in range(self.W):
-            self.shard.ingest_tick(torch.from_numpy(np.ascontiguousarray(grid[:, self.R + k:self.R + k + 1])).to(dev))
-        self.t_last = t_last
+        spec = ShardSpec(n_series=capacity, ring_len=self.R, season=season, pods=1, window=self.W, algorithm=algo,
+                         pairwise="NONE", dtype=torch.bfloat16 if dev.type == "cuda" else torch.float32,
+                         n_apps=max(1, len(self.apps)))
+        sh = StreamingShard(spec, self.cfg, dev)
+        sh.hist.state.head, sh.hist.state.length = 0, self.R   # rows start all-NaN (free)
+        sh.cur.ticks = self.W                                   # a full window: every tick graduates
+        sh._refresh_horizons()
+        sh.enable_anomaly_list(cap=max(1024, 4 * capacity))
+        return sh
+
+    def _grow(self, capacity: int) -> None:
+        old = self.shard
+        new = self._new_shard(capacity)
+        if old is not None:
+            n = old.spec.n_series
+            new.hist._store[:n].copy_(old.hist._store)
+            new.hist.state.head, new.hist.state.length = old.hist.head, old.hist.length
+            new.cur.data[:n].copy_(old.cur.data)
+            new.cur.ticks = old.cur.ticks
+            for name in ("threshold", "bound", "min_lower", "app_id"):
+                getattr(new, name)[:n].copy_(getattr(old, name))
+            new._refresh_horizons()
+        self.keys.extend([None] * (capacity - len(self.keys)))
+        self.shard = new
+
+    def _clear_rows(self, rows: List[int]) -> None:
+        if not rows:
+            return
+        idx = torch.tensor(rows, dtype=torch.long, device=self.device)
+        self.shard.hist._store.index_fill_(0, idx, float("nan"))
+        self.shard.cur.data.index_fill_(0, idx, float("nan"))
+
+    def _assign_rows(self) -> List[Tuple[Key, int]]:
+        """Free the rows of dead series, give pending series rows; returns the
+        (key, row) pairs whose history must be loaded."""
+        live = self.live_keys()
+        dead = [k for k in self.rows if k not in live]
+        freed = [self.rows.pop(k) for k in dead]
+        for row in freed:
+            self.keys[row] = None
+        self.pending &= live
+        new = sorted(self.pending)
+        need = len(self.rows) + len(new)
+        if self.shard is None or need > self.shard.spec.n_series:
+            cap = max(self.min_capacity, self.shard.spec.n_series if self.shard is not None else 1)
+            while cap < need:
+                cap *= 2
+            self._grow(cap)
+        if freed:
+            self._clear_rows(freed)
+        free = [i for i, k in enumerate(self.keys) if k is None]
+        out = []
+        for key, row in zip(new, free):
+            self.keys[row] = key
+            self.rows[key] = row
+            out.append((key, row))
+        if dead or new:
+            self._table = None
+            self._refresh_apps()
+        return out
+
+    def _refresh_apps(self) -> None:
+        """App roster of the live series (index = row of the per-app counters)."""
+        names = sorted({(k[2], k[3]) for k in self.rows})
+        if list(self.apps) != names:
+            self.apps = {a: i for i, a in enumerate(names)}
+            self.roster_version += 1
+        sh = self.shard
+        if sh.app_stats.shape[0] < max(1, len(self.apps)):
+            cap = sh.app_stats.shape[0]
+            while cap < len(self.apps):
+                cap *= 2
+            sh.app_stats = torch.zeros((cap, 2), dtype=torch.int32, device=self.device)
+        ids = np.zeros(sh.spec.n_series, dtype=np.int32)
+        for k, row in self.rows.items():
+            ids[row] = self.apps[(k[2], k[3])]
+        sh.app_id.copy_(torch.from_numpy(ids))
+
+    def _set_thresholds(self, assigned: List[Tuple[Key, int]]) -> None:
+        aliases: Dict[Key, str] = {}
+        for j in self.jobs.values():
+            for a, k in j.series.items():
+                aliases.setdefault(k, a)
+        rows = torch.tensor([row for _, row in assigned], dtype=torch.long, device=self.device)
+        th = [self.cfg.for_metric(aliases.get(k, ""), k[1]) for k, _ in assigned]
+        sh = self.shard
+        sh.threshold[rows] = torch.tensor([t.threshold for t in th], dtype=torch.float32, device=self.device)
+        sh.bound[rows] = torch.tensor([t.bound for t in th], dtype=torch.int8, device=self.device)
+        sh.min_lower[rows] = torch.tensor([t.min_lower_bound for t in th], dtype=torch.float32, device=self.device)
+        sh.refresh_thresholds()
+
+    def _key_tables(self) -> Dict[Tuple[str, str], native.KeyTable]:
+        """Per metric family (endpoint, metric): (namespace, app) → row."""
+        if self._table is None:
+            fams: Dict[Tuple[str, str], List] = {}
+            for k, row in self.rows.items():
+                fams.setdefault((k[0], k[1]), []).append(((k[2], k[3]), row))
+            self._table = {fam: native.KeyTable(v) for fam, v in fams.items()}
+        return self._table
+
+    def _staging(self, rows: int, cols: int) -> Tuple[torch.Tensor, np.ndarray]:
+        """NaN-filled host staging block (pinned for the GPU: one async H2D)."""
+        t = torch.full((rows, cols), float("nan"), dtype=torch.float32)
+        if self.device.type == "cuda":
+            t = t.pin_memory()
+        return t, t.numpy()
+
+    # ------------------------------------------------------------------ data
+    async def _fetch_into(self, reqs: List[Tuple[str, float, int, int]], out: np.ndarray,
+                          tables: Dict[Tuple[str, str], native.KeyTable], fams: List[Tuple[str, str]]) -> None:
+        """``reqs``: (url, start, n_points, col0) per query, ``fams`` the family of
+        each; every response is decoded by the keyed native scatter into ``out``."""
+        bodies = await self.prom.fetch_raw_many([u for u, *_ in reqs])
+        for (url, start, n, col0), fam, body in zip(reqs, fams, bodies):
+            if isinstance(body, Exception):
+                log.warning("fetch %s failed: %s", url.split("?")[0], body)
+                continue
+            try:
+                native.parse_dense_keyed(body, start, self.step, n, out, tables[fam], col0=col0)
+            except native.ParseError as e:
+                log.warning("bad response for %s: %s", fam[1], e)
+
+    async def _load_history(self, assigned: List[Tuple[Key, int]]) -> None:
+        """Fetch R + W points ending at ``t_last`` for the given series only, in
+        (time chunk x app group) queries, into a pinned block; one H2D."""
+        if not assigned:
+            return
+        n_pts = self.R + self.W
+        first = self.t_last - (n_pts - 1) * self.step
+        by_fam: Dict[Tuple[str, str], List[Tuple[Key, int]]] = {}
+        for i, (key, _row) in enumerate(assigned):
+            by_fam.setdefault((key[0], key[1]), []).append((key, i))
+        block_t, block = self._staging(len(assigned), n_pts)
+        reqs, fams, tables = [], [], {}
+        for fam, items in by_fam.items():
+            tables[fam] = native.KeyTable([((k[2], k[3]), i) for k, i in items])
+            for g in range(0, len(items), self.apps_per_query):
+                grp = items[g:g + self.apps_per_query]
+                sel = (f'{fam[1]}{{namespace=~"{_re_alt({k[2] for k, _ in grp})}",'
+                       f'app=~"{_re_alt({k[3] for k, _ in grp})}"}}')
+                for c0 in range(0, n_pts, self.chunk_pts):
+                    n = min(self.chunk_pts, n_pts - c0)
+                    s = first + c0 * self.step
+                    url = (f"{fam[0]}query_range?query={quote(sel, safe='')}&start={int(s)}"
+                           f"&end={int(s + (n - 1) * self.step)}&step={int(self.step)}")
+                    reqs.append((url, s, n, c0))
+                    fams.append(fam)
+        self.history_queries += len(reqs)
+        await self._fetch_into(reqs, block, tables, fams)
+        self.shard.load_rows(torch.tensor([row for _, row in assigned], dtype=torch.long),
+                             block_t.to(self.device, non_blocking=True))
+        self._set_thresholds(assigned)
+
+    async def _apply_changes(self) -> None:
+        assigned = self._assign_rows()
+        if self.shard is not None and self.t_last == 0.0:
+            self.t_last = float(np.floor(self.clock() / self.step) * self.step)
+        if assigned:
+            await self._load_history(assigned)
+            self.pending -= {k for k, _ in assigned}
+
+    async def _ingest_new(self, now: float) -> None:
+        t_new = float(np.floor(now / self.step) * self.step)
+        n_new = int(round((t_new - self.t_last) / self.step))
+        if n_new <= 0 or not self.rows:
+            return
+        if n_new > self.R:  # down for more than the whole history: reload every row
+            self.t_last = t_new
+            assigned = sorted(self.rows.items(), key=lambda kv: kv[1])
+            await self._load_history(assigned)
+            return
+        tables = self._key_tables()
+        block_t, block = self._staging(self.shard.spec.n_series, n_new)
+        s = self.t_last + self.step
+        reqs, fams = [], []
+        for fam in tables:
+            url = (f"{fam[0]}query_range?query={quote(fam[1], safe='')}&start={int(s)}"
+                   f"&end={int(s + (n_new - 1) * self.step)}&step={int(self.step)}")
+            reqs.append((url, s, n_new, 0))
+            fams.append(fam)
+        await self._fetch_into(reqs, block, tables, fams)
+        dev_block = block_t.to(self.device, non_blocking=True)
+        for k in range(n_new):
+            self.shard.ingest_tick(dev_block[:, k:k + 1].contiguous())
+        self.t_last = t_new
 
     # ------------------------------------------------------------------ tick
     async def tick(self) -> Dict[str, str]:
         """One scoring tick over every continuous series; returns job → status written."""
-        if self.dirty or self.shard is None:
-            await self.rebuild()
+        await self._apply_changes()
         written: Dict[str, str] = {}
-        if self.shard is None:
+        if self.shard is None or not self.rows:
+            if self.shard is not None:
+                self.shard.app_stats.zero_()
             return written
         t0 = time.perf_counter()
         now = self.clock()
-        t_new = np.floor(now / self.step) * self.step
-        n_new = int(round((t_new - self.t_last) / self.step))
-        if n_new > 0:
-            grid = await self._fetch_grid(self.t_last + self.step, min(n_new, self.W))
-            for k in range(grid.shape[1]):
-                self.shard.ingest_tick(torch.from_numpy(np.ascontiguousarray(grid[:, k:k + 1])).to(self.device))
-            self.t_last = t_new
+        await self._ingest_new(now)
         out = self.shard.score()
         C = self.W
         col = (self.shard.cur.ticks - 1) % C
         verdict = out["verdict"].cpu().numpy()
         upper = out["upper"][:, col].float().cpu().numpy() if "upper" in out else None
         lower = out["lower"][:, col].float().cpu().numpy() if "lower" in out else None
-        # anomalous points of the current window per series: (timestamp, value) pairs
         points: Dict[int, List[Tuple[float, float]]] = {}
         ab = self.shard.anomalies
         overflow = False
@@ -236,11 +405,14 @@ class StreamingMonitor:
             points.setdefault(rr, []).append((self.t_last - age * self.step, vv))
         self.ticks += 1
         self.metrics.tick.observe(time.perf_counter() - t0)
-        self.metrics.series_scored.inc(len(self.keys))
+        self.metrics.series_scored.inc(len(self.rows))
         for jid, job in list(self.jobs.items()):
             anomaly = {}
-            for alias, row in job.series.items():
-                ep, metric, ns, app = self.keys[row]
+            for alias, key in job.series.items():
+                row = self.rows.get(key)
+                if row is None:
+                    continue
+                ep, metric, ns, app = key
                 if upper is not None and ns:
                     self.metrics.export_band(metric, ns, app, float(upper[row]), float(lower[row]),
                                              self.t_last if verdict[row] == 1 else None)
@@ -264,28 +436,35 @@ class StreamingMonitor:
             ok = self.store.update(jid, fields, expect_claimed_by=self.worker_id)
             if not ok or status in r.TERMINAL_STATUSES:
                 del self.jobs[jid]  # finished, or another worker took the lease
-                self.dirty = True
                 if ok:
                     self.metrics.jobs.labels(status=status).inc()
             written[jid] = status
         return written
 
+    def app_table(self) -> Tuple[List[Tuple[str, str]], torch.Tensor]:
+        """(app roster, ``[A, 2]`` int32 device counters of the last tick:
+        anomalous series, scored series)."""
+        names = list(self.apps)
+        if self.shard is None:
+            return names, torch.zeros((len(names), 2), dtype=torch.int32, device=self.device)
+        return names, self.shard.app_stats[:len(names)]
+
     # ------------------------------------------------------------------ checkpoint / resume
     def save_snapshot(self, path: str) -> bool:
         """Checkpoint the resident shard (history ring, windows, last fit) with
-        the series keys it serves (``brain/checkpoint.py``)."""
-        if self.shard is None:
+        the series key of every row (``brain/checkpoint.py``)."""
+        if self.shard is None or self.pending:
             return False
         from . import checkpoint as ck
-        ck.save_streaming_shard(self.shard, path, extra={"keys": [list(k) for k in self.keys],
+        ck.save_streaming_shard(self.shard, path, extra={"keys": [list(k) if k else None for k in self.keys],
                                                          "t_last": float(self.t_last), "step": self.step})
         return True
 
     def restore_snapshot(self, path: str) -> bool:
         """Adopt a snapshot instead of re-fetching a week of history per series:
-        only when it serves exactly the series of the leased jobs, with the same
+        only when it holds every series of the leased jobs, with the same
         geometry, and is younger than half the ring (the next tick then catches
-        up the missed points); otherwise the next tick rebuilds from Prometheus."""
+        up the missed points); otherwise rows are loaded from Prometheus."""
         import os
         if not path or not os.path.exists(path):
             return False
@@ -296,12 +475,16 @@ class StreamingMonitor:
             log.warning("ignoring snapshot %s: %s", path, e)
             return False
         ex = shard.checkpoint_extra
-        keys = [tuple(k) for k in ex.get("keys", [])]
-        if (keys != self.keys or ex.get("step") != self.step or shard.spec.ring_len != self.R
+        keys = [tuple(k) if k else None for k in ex.get("keys", [])]
+        snap_rows = {k: i for i, k in enumerate(keys) if k is not None}
+        if (set(snap_rows) != self.live_keys() or ex.get("step") != self.step or shard.spec.ring_len != self.R
                 or shard.spec.window != self.W or self.clock() - float(ex.get("t_last", 0)) > self.R * self.step / 2):
             return False
         shard.enable_anomaly_list(cap=max(1024, 4 * len(keys)))
-        self.shard, self.t_last, self.dirty = shard, float(ex["t_last"]), False
+        self.shard, self.t_last = shard, float(ex["t_last"])
+        self.keys, self.rows, self.pending = keys, snap_rows, set()
+        self._table = None
+        self._refresh_apps()
         return True
 
     async def run_forever(self, stop: Optional[asyncio.Event] = None, period: Optional[float] = None,
@@ -314,7 +497,7 @@ class StreamingMonitor:
             try:
                 self.sync()
                 if first and snapshot and self.restore_snapshot(snapshot):
-                    log.info("resumed %d series from snapshot %s", len(self.keys), snapshot)
+                    log.info("resumed %d series from snapshot %s", len(self.rows), snapshot)
                 first = False
                 await self.tick()
                 if snapshot and snapshot_every > 0 and self.ticks % snapshot_every == 0:

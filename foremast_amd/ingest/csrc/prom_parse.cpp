@@ -12,7 +12,12 @@
 //  * fm_prom_dense  — scatters values straight into a NaN-initialised dense
 //                     [S, T] float32 matrix on the (start, step) grid, which
 //                     is what the GPU ring buffer ingests (pinned host memory
-//                     → one H2D copy).
+//                     → one H2D copy);
+//  * fm_prom_dense_keyed — the same scatter, but each series goes to the row
+//                     its (label_a, label_b) values map to (FNV-1a 64 key,
+//                     binary search in the caller's sorted key table), so a
+//                     response for any subset of a shard's series lands in
+//                     place in one pass with no per-series Python work.
 //
 // Numbers are decoded with std::from_chars (locale independent).  Special
 // values "NaN", "+Inf", "-Inf" are accepted.  Returns < 0 on malformed input.
@@ -187,6 +192,40 @@ long long walk(const char* buf, long long len, OnSeries on_series, OnPoint on_po
   return nseries;
 }
 
+// FNV-1a 64 over a + 0x1f + b (foremast_amd/ingest/native.py key_hash must agree)
+uint64_t fnv_key(const char* a0, const char* a1, const char* b0, const char* b1) {
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&h](unsigned char ch) { h ^= ch; h *= 1099511628211ull; };
+  for (const char* q = a0; q < a1; ++q) mix((unsigned char)*q);
+  mix(0x1f);
+  for (const char* q = b0; q < b1; ++q) mix((unsigned char)*q);
+  return h;
+}
+
+// raw bytes of the string value of `key` inside the metric object [m0, m1)
+// (label values are plain DNS-style names; a value with escapes keeps them raw)
+bool label_value(const char* m0, const char* m1, const char* key, const char*& v0, const char*& v1) {
+  if (!m0) return false;
+  Cursor c{m0, m1};
+  if (!c.eat('{')) return false;
+  c.ws();
+  if (c.eat('}')) return false;
+  while (true) {
+    const char *k0, *k1;
+    if (!read_key(c, k0, k1)) return false;
+    c.ws();
+    if (c.p < c.e && *c.p == '"') {
+      const char* s0 = c.p + 1;
+      if (!skip_string(c)) return false;
+      if (key_is(k0, k1, key)) { v0 = s0; v1 = c.p - 1; return true; }
+    } else if (!skip_value(c)) {
+      return false;
+    }
+    if (c.eat(',')) continue;
+    return false;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -239,6 +278,40 @@ long long fm_prom_dense(const char* buf, long long len, double start, double ste
         out[row * ld + i] = (float)v;
       });
   if (dropped) *dropped = drop;
+  return r;
+}
+
+// Keyed dense scatter: series s goes to row key_rows[j] where key_hash[j] is the
+// FNV key of its (label_a, label_b) values (key_hash sorted ascending, n_keys
+// entries); unmatched series are skipped and counted in *unmatched.
+long long fm_prom_dense_keyed(const char* buf, long long len, double start, double step, long long T, float* out,
+                              long long ld, long long max_rows, const char* label_a, const char* label_b,
+                              const uint64_t* key_hash, const long long* key_rows, long long n_keys,
+                              long long* dropped, long long* unmatched) {
+  long long drop = 0, miss = 0, row = -1;
+  const long long r = walk(
+      buf, len,
+      [&](long long, const char* m0, const char* m1) {
+        const char *a0 = "", *a1 = a0, *b0 = a0, *b1 = a0;
+        label_value(m0, m1, label_a, a0, a1);
+        label_value(m0, m1, label_b, b0, b1);
+        const uint64_t h = fnv_key(a0, a1, b0, b1);
+        long long lo = 0, hi = n_keys;
+        while (lo < hi) {
+          const long long mid = (lo + hi) >> 1;
+          if (key_hash[mid] < h) lo = mid + 1; else hi = mid;
+        }
+        row = (lo < n_keys && key_hash[lo] == h) ? key_rows[lo] : -1;
+        if (row < 0 || row >= max_rows) { row = -1; ++miss; }
+      },
+      [&](long long, double t, double v) {
+        const double fi = (t - start) / step;
+        const long long i = (long long)llround(fi);
+        if (row < 0 || i < 0 || i >= T || std::fabs(fi - (double)i) > 1e-6) { ++drop; return; }
+        out[row * ld + i] = (float)v;
+      });
+  if (dropped) *dropped = drop;
+  if (unmatched) *unmatched = miss;
   return r;
 }
 

@@ -2,7 +2,9 @@
 
 ``parse_matrix(body)`` → list of ``(labels, ts, values)``;
 ``parse_dense(body, start, step, T, out, row0)`` scatters straight into a
-dense float32 matrix (e.g. a pinned host staging buffer for the GPU ring).
+dense float32 matrix (e.g. a pinned host staging buffer for the GPU ring);
+``parse_dense_keyed(body, start, step, T, out, table)`` puts each series in
+the row of its (namespace, app) key.
 Falls back to ``json`` when the native library cannot be built (no g++).
 """
 
@@ -65,6 +67,9 @@ def _load() -> Optional[C.CDLL]:
         lib.fm_prom_fill.restype = LL
         lib.fm_prom_dense.argtypes = [C.c_char_p, LL, C.c_double, C.c_double, LL, P, LL, LL, LL, P]
         lib.fm_prom_dense.restype = LL
+        lib.fm_prom_dense_keyed.argtypes = [C.c_char_p, LL, C.c_double, C.c_double, LL, P, LL, LL, C.c_char_p,
+                                            C.c_char_p, P, P, LL, P, P]
+        lib.fm_prom_dense_keyed.restype = LL
         _lib = lib
         return lib
 
@@ -141,6 +146,71 @@ def parse_dense(body: bytes, start: float, step: float, T: int, out: np.ndarray,
     if n < 0:
         raise ParseError(f"malformed query_range body (code {n})")
     return int(n), int(dropped.value)
+
+
+def key_hash(a: str, b: str) -> int:
+    """FNV-1a 64 of ``a + 0x1f + b`` (UTF-8) — the row key of a series in
+    :func:`parse_dense_keyed` (``prom_parse.cpp fnv_key``)."""
+    h = 1469598103934665603
+    for ch in a.encode() + b"\x1f" + b.encode():
+        h = ((h ^ ch) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+class KeyTable:
+    """Sorted (hash → row) table of a shard's series keys for the keyed scatter."""
+
+    def __init__(self, keys_rows, label_a: str = "namespace", label_b: str = "app") -> None:
+        pairs = sorted((key_hash(a, b), int(r)) for (a, b), r in keys_rows)
+        hs = [h for h, _ in pairs]
+        if len(set(hs)) != len(hs):
+            raise ValueError("series key hash collision")
+        self.hash = np.array(hs, dtype=np.uint64)
+        self.rows = np.array([r for _, r in pairs], dtype=np.int64)
+        self.label_a, self.label_b = label_a.encode(), label_b.encode()
+
+    def __len__(self) -> int:
+        return len(self.rows)
+
+
+def parse_dense_keyed(body: bytes, start: float, step: float, T: int, out: np.ndarray, table: KeyTable,
+                      col0: int = 0) -> Tuple[int, int, int]:
+    """Scatter each series into ``out[row, col0 + (t - start)/step]`` where
+    ``row`` is its (namespace, app) key's row in ``table`` (``out`` float32,
+    pre-filled with NaN, unit column stride).  Returns (n_series,
+    n_dropped_points, n_unmatched_series)."""
+    if isinstance(body, str):
+        body = body.encode()
+    _check_status(body)
+    if out.dtype != np.float32 or out.ndim != 2 or out.shape[1] < col0 + T or out.strides[1] != 4:
+        raise ValueError("out must be float32 [rows, >= col0 + T] with unit column stride")
+    lib = _load()
+    if lib is None:
+        lookup = dict(zip(table.hash.tolist(), table.rows.tolist()))
+        dropped = unmatched = 0
+        series = _parse_py(body)
+        la, lb = table.label_a.decode(), table.label_b.decode()
+        for labels, ts, v in series:
+            row = lookup.get(key_hash(labels.get(la, ""), labels.get(lb, "")), -1)
+            if row < 0 or row >= out.shape[0]:
+                unmatched += 1
+                dropped += len(ts)
+                continue
+            fi = (ts - start) / step
+            i = np.rint(fi).astype(np.int64)
+            ok = (i >= 0) & (i < T) & (np.abs(fi - i) < 1e-6)
+            out[row, col0 + i[ok]] = v[ok]
+            dropped += int((~ok).sum())
+        return len(series), dropped, unmatched
+    dropped, unmatched = C.c_longlong(0), C.c_longlong(0)
+    ld = out.strides[0] // 4
+    base = out.ctypes.data + 4 * col0
+    n = lib.fm_prom_dense_keyed(body, len(body), float(start), float(step), int(T), base, ld, out.shape[0],
+                                table.label_a, table.label_b, table.hash.ctypes.data, table.rows.ctypes.data,
+                                len(table), C.byref(dropped), C.byref(unmatched))
+    if n < 0:
+        raise ParseError(f"malformed query_range body (code {n})")
+    return int(n), int(dropped.value), int(unmatched.value)
 
 
 def _parse_py(body: bytes):

@@ -64,6 +64,25 @@ class PromClient:
             raise FetchError(f"GET {url}: {e}") from e
         return [Series(labels=l, ts=t, values=v) for l, t, v in parsed]
 
+    async def fetch_raw(self, url: str, client: httpx.AsyncClient) -> bytes:
+        """Body of one query_range call (decoded by the caller, e.g. the keyed
+        native scatter straight into a staging block)."""
+        async with self._sem:
+            try:
+                resp = await client.get(url)
+            except httpx.HTTPError as e:
+                raise FetchError(f"GET {url}: {e}") from e
+        self.requests += 1
+        self.bytes_fetched += len(resp.content)
+        if resp.status_code != 200:
+            raise FetchError(f"GET {url}: HTTP {resp.status_code}")
+        return resp.content
+
+    async def fetch_raw_many(self, urls: Sequence[str]) -> List[Any]:
+        """Bodies (or the exception) of concurrent query_range calls."""
+        async with self._client() as c:
+            return await asyncio.gather(*(self.fetch_raw(u, c) for u in urls), return_exceptions=True)
+
     async def fetch_many(self, urls: Sequence[str]) -> List[Any]:
         """Fetch concurrently; each result is a list of Series or the exception."""
         async with self._client() as c:

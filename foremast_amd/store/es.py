@@ -34,6 +34,7 @@ from .jobstore import JobStore, is_claimable
 
 INDEX = "documents"
 DOC_TYPE = "document"
+META_INDEX = "foremast-engine"
 
 
 class ElasticJobStore(JobStore):
@@ -118,13 +119,13 @@ class ElasticJobStore(JobStore):
         hits = resp.json().get("hits", {}).get("hits", [])
         return [(h["_source"], int(h.get("_version", 1))) for h in hits]
 
-    def claim(self, worker, now=None, max_stuck_s=90.0, limit=64, only=None):
+    def claim(self, worker, now=None, max_stuck_s=90.0, limit=64, only=None, steal_from=None):
         now = time.time() if now is None else now
         out = []
         for d, ver in self._search(r.OPEN_STATUSES + r.INPROGRESS_STATUSES):
             if len(out) >= limit:
                 break
-            if not is_claimable(d, now, max_stuck_s) or (only is not None and not only(d)):
+            if not is_claimable(d, now, max_stuck_s, steal_from) or (only is not None and not only(d)):
                 continue
             d.update(status=r.ST_PREPROCESS_INPROGRESS, claimed_by=worker, claimed_at=now,
                      modified_ts=now, modified_at=format_rfc3339_nano(now))
@@ -140,6 +141,24 @@ class ElasticJobStore(JobStore):
             return []
         resp.raise_for_status()
         return [h["_source"] for h in resp.json().get("hits", {}).get("hits", [])]
+
+    # engine records live in their own index so the reference service's
+    # ``documents`` searches never see them
+    def _meta_url(self, key: str) -> str:
+        return f"{self.base}/{META_INDEX}/{self.doc_type}/{key}"
+
+    def put_meta(self, key, value):
+        resp = self.http.put(self._meta_url(key), params={"refresh": self.refresh},
+                             content=json.dumps({"value": value}), headers={"Content-Type": "application/json"})
+        resp.raise_for_status()
+
+    def get_meta(self, key):
+        resp = self.http.get(self._meta_url(key))
+        if resp.status_code == 404:
+            return None
+        resp.raise_for_status()
+        body = resp.json()
+        return body["_source"].get("value") if body.get("found", False) else None
 
     def close(self):
         self.http.close()

@@ -78,11 +78,16 @@ def new_document(req: r.DocumentRequest, job_id: str, now: Optional[float] = Non
     }
 
 
-def is_claimable(doc: Dict[str, Any], now: float, max_stuck_s: float) -> bool:
+def is_claimable(doc: Dict[str, Any], now: float, max_stuck_s: float, steal_from=None) -> bool:
+    """Open (and due), stuck for longer than ``max_stuck_s``, or leased by a
+    worker in ``steal_from`` (a brain rank the node has declared dead: its jobs
+    move at once instead of after the stuck-job timeout)."""
     st = doc.get("status")
     if st in r.OPEN_STATUSES:
         return float(doc.get("not_before", 0.0) or 0.0) <= now
     if st in r.INPROGRESS_STATUSES:
+        if steal_from and doc.get("claimed_by") in steal_from:
+            return True
         return now - float(doc.get("modified_ts", 0.0) or 0.0) > max_stuck_s
     return False
 
@@ -104,12 +109,21 @@ class JobStore(abc.ABC):
 
     @abc.abstractmethod
     def claim(self, worker: str, now: Optional[float] = None, max_stuck_s: float = 90.0,
-              limit: int = 64, only=None) -> List[Dict[str, Any]]:
+              limit: int = 64, only=None, steal_from=None) -> List[Dict[str, Any]]:
         """Lease up to ``limit`` claimable documents (``only(doc)`` filters,
-        e.g. by strategy: the streaming monitor takes continuous jobs)."""
+        e.g. by strategy: the streaming monitor takes continuous jobs;
+        ``steal_from``: worker ids whose leases are void, see is_claimable)."""
 
     @abc.abstractmethod
     def all(self) -> List[Dict[str, Any]]: ...
+
+    # small engine-side records next to the job table (e.g. the node health table
+    # rank 0 publishes for GET /v1/healthcheck/cluster)
+    @abc.abstractmethod
+    def put_meta(self, key: str, value: Dict[str, Any]) -> None: ...
+
+    @abc.abstractmethod
+    def get_meta(self, key: str) -> Optional[Dict[str, Any]]: ...
 
     def create(self, req: r.DocumentRequest, now: Optional[float] = None) -> str:
         job_id = job_id_for(req)
@@ -128,6 +142,7 @@ class JobStore(abc.ABC):
 class MemoryJobStore(JobStore):
     def __init__(self) -> None:
         self._docs: Dict[str, Dict[str, Any]] = {}
+        self._meta: Dict[str, Dict[str, Any]] = {}
         self._lock = threading.RLock()
 
     def get(self, job_id):
@@ -155,14 +170,14 @@ class MemoryJobStore(JobStore):
             d["modified_at"] = format_rfc3339_nano(d["modified_ts"])
             return True
 
-    def claim(self, worker, now=None, max_stuck_s=90.0, limit=64, only=None):
+    def claim(self, worker, now=None, max_stuck_s=90.0, limit=64, only=None, steal_from=None):
         now = time.time() if now is None else now
         out = []
         with self._lock:
             for d in sorted(self._docs.values(), key=lambda x: x.get("modified_ts", 0.0)):
                 if len(out) >= limit:
                     break
-                if is_claimable(d, now, max_stuck_s) and (only is None or only(d)):
+                if is_claimable(d, now, max_stuck_s, steal_from) and (only is None or only(d)):
                     d["status"] = r.ST_PREPROCESS_INPROGRESS
                     d["claimed_by"] = worker
                     d["claimed_at"] = now
@@ -174,6 +189,15 @@ class MemoryJobStore(JobStore):
     def all(self):
         with self._lock:
             return [copy.deepcopy(d) for d in self._docs.values()]
+
+    def put_meta(self, key, value):
+        with self._lock:
+            self._meta[key] = copy.deepcopy(value)
+
+    def get_meta(self, key):
+        with self._lock:
+            v = self._meta.get(key)
+            return copy.deepcopy(v) if v is not None else None
 
 
 class SqliteJobStore(JobStore):
@@ -189,6 +213,7 @@ class SqliteJobStore(JobStore):
             c.execute("CREATE TABLE IF NOT EXISTS documents ("
                       "id TEXT PRIMARY KEY, status TEXT, modified_ts REAL, doc TEXT)")
             c.execute("CREATE INDEX IF NOT EXISTS documents_status ON documents(status)")
+            c.execute("CREATE TABLE IF NOT EXISTS meta (key TEXT PRIMARY KEY, value TEXT)")
 
     def _conn(self) -> sqlite3.Connection:
         c = getattr(self._local, "conn", None)
@@ -230,7 +255,7 @@ class SqliteJobStore(JobStore):
             c.execute("ROLLBACK")
             raise
 
-    def claim(self, worker, now=None, max_stuck_s=90.0, limit=64, only=None):
+    def claim(self, worker, now=None, max_stuck_s=90.0, limit=64, only=None, steal_from=None):
         now = time.time() if now is None else now
         c = self._conn()
         c.execute("BEGIN IMMEDIATE")
@@ -243,7 +268,7 @@ class SqliteJobStore(JobStore):
                 if len(out) >= limit:
                     break
                 d = json.loads(raw)
-                if not is_claimable(d, now, max_stuck_s) or (only is not None and not only(d)):
+                if not is_claimable(d, now, max_stuck_s, steal_from) or (only is not None and not only(d)):
                     continue
                 d.update(status=r.ST_PREPROCESS_INPROGRESS, claimed_by=worker, claimed_at=now,
                          modified_ts=now, modified_at=format_rfc3339_nano(now))
@@ -258,6 +283,13 @@ class SqliteJobStore(JobStore):
 
     def all(self):
         return [json.loads(x[0]) for x in self._conn().execute("SELECT doc FROM documents")]
+
+    def put_meta(self, key, value):
+        self._conn().execute("INSERT OR REPLACE INTO meta(key, value) VALUES (?, ?)", (key, json.dumps(value)))
+
+    def get_meta(self, key):
+        row = self._conn().execute("SELECT value FROM meta WHERE key=?", (key,)).fetchone()
+        return json.loads(row[0]) if row else None
 
     def close(self):
         c = getattr(self._local, "conn", None)

@@ -71,7 +71,9 @@ def test_streaming_monitor_continuous_jobs(where, algorithm):
         assert mon.sync() == 3                       # only the continuous jobs
         assert store.get(oneshot)["status"] == "initial"
         w = await mon.tick()
-        assert set(w.values()) == {"preprocess_inprogress"} and len(mon.keys) == 3
+        assert set(w.values()) == {"preprocess_inprogress"} and mon.n_live == 3
+        # 2 days of history + window in <= 1-day chunks: 3 queries, one app group
+        assert mon.history_queries == 3
         n_queries = len(prom.queries)
         clock.t = T0 + 300
         w = await mon.tick()
@@ -81,8 +83,8 @@ def test_streaming_monitor_continuous_jobs(where, algorithm):
         info = json.loads(doc["anomalyInfo"])
         assert info["error5xx"]["values"][1] > 30
         clock.t = T0 + 1900                          # past endTime
-        w = await mon.tick()                         # rebuild without b's series, then finish
-        assert len(mon.keys) == 2
+        w = await mon.tick()                         # b's row freed in place (no rebuild), then finish
+        assert mon.n_live == 2 and mon.history_queries == 3
         assert w[ids["a"]] == "completed_health" and w[ids["c"]] == "completed_health"
 
     asyncio.run(go())
@@ -117,7 +119,7 @@ def test_streaming_monitor_resumes_from_snapshot(tmp_path):
         await m1.tick()
         assert m1.save_snapshot(snap)
         m2 = monitor("w1")          # restart of the same worker: re-leases its jobs
-        m2.jobs, m2.keys, m2.rows = m1.jobs, list(m1.keys), dict(m1.rows)
+        m2.jobs = dict(m1.jobs)
         n_q = len(prom.queries)
         assert m2.restore_snapshot(snap)
         clock.t = T0 + 240
@@ -125,13 +127,14 @@ def test_streaming_monitor_resumes_from_snapshot(tmp_path):
         await m2.tick()
         assert len(prom.queries) == n_q + 2      # one incremental query each, no history rebuild
         for k in ("verdict", "std", "upper", "lower", "score"):
-            assert torch.equal(m1.shard.out[k], m2.shard.out[k]), k
+            torch.testing.assert_close(m1.shard.out[k], m2.shard.out[k], rtol=0, atol=0, equal_nan=True,
+                                       msg=k)  # free rows are NaN in both
         m3 = monitor("w1")
-        m3.jobs, m3.keys, m3.rows = m1.jobs, list(m1.keys)[:1], {}
-        assert not m3.restore_snapshot(snap)      # different series set: rebuild instead
+        m3.jobs = dict(list(m1.jobs.items())[:1])
+        assert not m3.restore_snapshot(snap)      # different series set: load rows from Prometheus instead
         clock.t = T0 + 2 * 86400
         m4 = monitor("w1")
-        m4.jobs, m4.keys, m4.rows = m1.jobs, list(m1.keys), dict(m1.rows)
+        m4.jobs = dict(m1.jobs)
         assert not m4.restore_snapshot(snap)      # too old
 
     asyncio.run(go())
@@ -219,3 +222,56 @@ def test_overlapped_rank_tests_match_inline_detection():
         assert a0 == a1
     from foremast_amd.ops import kernels as K
     assert K.last_detect_deferred and int(shards[1].pw_out["differs"].sum()) > 0
+
+
+def test_streaming_rows_grow_incrementally_with_chunked_history():
+    """New jobs join a running shard without a rebuild: only their series'
+    history is fetched (1-day x 2-app chunks, regex app selectors), the shard
+    grows by doubling, rows of live series keep their state, and the result
+    equals a monitor that loaded everything at once."""
+    clock = Clock(T0)
+    prom = FakePrometheus(clock=clock)
+    apps = ["a", "b.v2", "c", "d", "e"]
+    for i, app in enumerate(apps):
+        prom.add(M, {"namespace": "ns", "app": app}, synth.error_rate(base=0.3 + 0.05 * i, spread=0.05, seed=i))
+    prom.add(M, {"namespace": "ns", "app": "bXv2"}, synth.error_rate(base=9.0, spread=0.05, seed=99))  # regex decoy
+    store = MemoryJobStore()
+    ids = {app: svc.register(store, _job(app))[1]["jobId"] for app in apps}
+    cfg = BrainConfig.from_env(dict(reference_default_env(), MIN_HISTORICAL_DATA_POINT_TO_MEASURE="10"))
+    transport = httpx.ASGITransport(app=prom.asgi_app())
+
+    def monitor(worker, owns=None):
+        return StreamingMonitor(store, cfg, prom=PromClient(transport=transport), device=torch.device("cpu"),
+                                worker_id=worker, ring_len=2880, window=5, clock=clock, min_capacity=2,
+                                apps_per_query=2, owns=owns)
+
+    first = {ids["a"], ids["b.v2"]}
+
+    async def go():
+        inc = monitor("inc", owns=lambda d: d["id"] in first)
+        assert inc.sync() == 2
+        await inc.tick()
+        assert inc.shard.spec.n_series == 2 and inc.history_queries == 3   # 1 app group x 3 day chunks
+        inc.owns = None
+        assert inc.sync() == 3
+        clock.t = T0 + 60
+        await inc.tick()
+        assert inc.shard.spec.n_series == 8 and inc.n_live == 5
+        assert inc.history_queries == 3 + 2 * 3                            # only the 3 new series: 2 groups
+        assert inc.roster_version == 2 and len(inc.apps) == 5
+        # a fresh monitor over the same jobs, everything loaded at once
+        for jid in ids.values():
+            store.update(jid, {"claimed_by": "", "status": "reprogress"})
+        ref = monitor("ref")
+        assert ref.sync() == 5
+        await ref.tick()
+        for key, row in inc.rows.items():
+            r2 = ref.rows[key]
+            assert torch.equal(inc.shard.hist.logical()[row], ref.shard.hist.logical()[r2]), key
+            assert torch.equal(inc.shard.out["verdict"][row], ref.shard.out["verdict"][r2])
+            torch.testing.assert_close(inc.shard.out["upper"][row], ref.shard.out["upper"][r2], rtol=0, atol=0)
+        # the decoy app never leaks into b.v2's row
+        row = inc.rows[[k for k in inc.rows if k[3] == "b.v2"][0]]
+        assert float(inc.shard.hist.logical()[row].nanmean()) < 5.0
+
+    asyncio.run(go())
