@@ -7,6 +7,12 @@ same environment variables (``ES_ENDPOINT``, ``ML_ALGORITHM``, ``threshold``,
 on :8000 (``foremastbrain:<metric>_{upper,lower,anomaly}`` plus engine
 metrics).  ``FOREMAST_JOB_STORE`` (``sqlite:///…`` / ``memory://``) overrides
 ``ES_ENDPOINT``.  Several processes can share one store: claims are leases.
+
+Node mode (``--streaming`` with ``--nproc N``, or under torchrun): one rank per
+GPU, continuous jobs sharded by app over the ranks, ONE all-gather of per-app
+counters per tick (RCCL), rank 0 publishes the node health table that
+``GET /v1/healthcheck/cluster`` serves; a dead rank's apps move to the
+survivors (``brain/node.py``).
 """
 
 from __future__ import annotations
@@ -38,12 +44,17 @@ def parse(argv=None):
                    help="streaming-engine snapshot ({rank} expands): resume from it, re-save periodically and at exit")
     p.add_argument("--snapshot-every", type=int, default=int(os.environ.get("FOREMAST_SNAPSHOT_EVERY", "60")),
                    help="ticks between streaming snapshots")
+    p.add_argument("--nproc", type=int, default=int(os.environ.get("FOREMAST_NPROC", "1")),
+                   help="node mode: start this many brain ranks (one per GPU) around a node key-value store")
+    p.add_argument("--tick-seconds", type=float, default=None,
+                   help="streaming tick period (default: the query step)")
+    p.add_argument("--step", type=float, default=float(os.environ.get("FOREMAST_STEP_SECONDS", "60")))
+    p.add_argument("--window", type=int, default=int(os.environ.get("FOREMAST_WINDOW", "10")))
     return p.parse_args(argv)
 
 
 def _bind_gpu() -> int:
-    """One scorer process per GPU under torchrun: bind LOCAL_RANK's device.
-    Ranks share nothing but the job store (lease-based claims)."""
+    """One scorer process per GPU (launch_node or torchrun): bind LOCAL_RANK's device."""
     local = int(os.environ.get("LOCAL_RANK", "0"))
     try:
         import torch
@@ -82,11 +93,20 @@ async def run(args) -> BrainWorker:
         loop.call_later(args.run_seconds, stop.set)
     tasks = [worker.run_forever(stop)]
     if args.streaming:
+        from .node import NodeBrain, elastic_world_from_env, worker_id_of
         from .streaming import StreamingMonitor
-        mon = StreamingMonitor(store, cfg, device=worker.scorer.device, metrics=metrics,
-                               worker_id=f"{worker.worker_id}-stream")
-        snap = args.snapshot.replace("{rank}", str(local)) if args.snapshot else None
-        tasks.append(mon.run_forever(stop, snapshot=snap, snapshot_every=args.snapshot_every))
+        dev = worker.scorer.device
+        world = elastic_world_from_env(dev)
+        member = world.id if world is not None else f"{worker.worker_id}-stream"
+        mon = StreamingMonitor(store, cfg, device=dev, metrics=metrics, ring_len=cfg.ring_len, step=args.step,
+                               window=args.window, worker_id=worker_id_of(member) if world else member)
+        period = args.tick_seconds if args.tick_seconds else args.step
+        if world is None and args.snapshot:
+            snap = args.snapshot.replace("{rank}", str(local))
+            tasks.append(mon.run_forever(stop, period=period, snapshot=snap, snapshot_every=args.snapshot_every))
+        else:
+            # node brain (also for one rank: it publishes the health table)
+            tasks.append(NodeBrain(mon, world, store, dev).run_forever(stop, period))
     await asyncio.gather(*tasks)
     if cache_path and worker.lstm is not None:
         worker.lstm.cache.save(cache_path)
@@ -95,9 +115,26 @@ async def run(args) -> BrainWorker:
 
 
 def main(argv=None) -> None:
+    import sys
     logging.basicConfig(level=os.environ.get("FOREMAST_LOG_LEVEL", "INFO"),
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")
-    asyncio.run(run(parse(argv)))
+    args = parse(argv)
+    if args.nproc > 1 and not os.environ.get("FOREMAST_NODE_STORE") and "WORLD_SIZE" not in os.environ:
+        from .node import launch_node
+        raw = list(sys.argv[1:] if argv is None else argv)
+        rest, skip = [], False
+        for a in raw:  # the ranks get the same arguments minus --nproc
+            if skip:
+                skip = False
+                continue
+            if a == "--nproc":
+                skip = True
+                continue
+            if a.startswith("--nproc="):
+                continue
+            rest.append(a)
+        raise SystemExit(launch_node(args.nproc, rest))
+    asyncio.run(run(args))
 
 
 if __name__ == "__main__":

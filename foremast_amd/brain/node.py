@@ -1,0 +1,197 @@
+"""The node brain: one scorer process per GPU, sharded by app, joined by RCCL.
+
+The reference scales its brain as shared-nothing replicas that only meet in
+the ES job table (``docs/guides/design.md:37-41``) and promises "aggregate
+service health check across multiple K8s clusters" (``README.md:27``).  Here
+the brains of one node form a process group (``nccl`` = RCCL over xGMI on the
+GPU, ``gloo`` on CPU):
+
+* ownership: continuous jobs are sharded by a stable hash of (namespace, app)
+  over the current members, so every app's series live on one rank and the
+  per-app counters need no reduction (:func:`owner_of`);
+* each tick every rank scores its own :class:`StreamingMonitor` shard, then the
+  ranks exchange their per-app counters in ONE all-gather
+  (:class:`~foremast_amd.parallel.cluster.ClusterHealth`); rank 0 publishes
+  the node health table into the job store (``put_meta("cluster_health")``),
+  which ``GET /v1/healthcheck/cluster`` serves;
+* failure detection / elastic recovery: members heartbeat into
+  the node's key-value store; when one goes silent (or a collective fails)
+  the survivors agree on a new member list, re-form the process group
+  (:class:`~foremast_amd.parallel.elastic.ElasticWorld`), hand back the
+  leases of apps that moved to another rank, and take over the dead rank's
+  jobs at once (``steal_from``) instead of after the 90 s stuck-job timeout.
+
+:func:`launch_node` is the launcher (``python -m foremast_amd.brain
+--streaming --nproc N``): it hosts the key-value store itself, so the store
+outlives any rank, starts N rank processes and never touches the GPU.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import datetime
+import logging
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+import zlib
+from typing import Dict, List, Optional, Set
+
+import torch
+import torch.distributed as dist
+
+from ..parallel.cluster import ClusterHealth
+from ..parallel.elastic import ElasticWorld
+from .streaming import StreamingMonitor, app_of
+
+log = logging.getLogger("foremast.node")
+
+META_KEY = "cluster_health"
+
+
+def owner_of(namespace: str, app: str, world: int) -> int:
+    """Rank index that owns an app (stable across processes and restarts)."""
+    return zlib.crc32(f"{namespace}/{app}".encode()) % max(world, 1)
+
+
+def worker_id_of(member: str) -> str:
+    return f"node-{member}"
+
+
+class NodeBrain:
+    def __init__(self, mon: StreamingMonitor, world: Optional[ElasticWorld], store, device,
+                 publish: bool = True) -> None:
+        self.mon = mon
+        self.world = world
+        self.store = store
+        self.device = torch.device(device)
+        self.health = ClusterHealth(self.device)
+        self.publish = publish
+        self.dead: Set[str] = set()
+        self.table: Dict = {}
+        self.ticks = 0
+        mon.owns = self.owns
+
+    @property
+    def rank(self) -> int:
+        return self.world.rank if self.world is not None else 0
+
+    @property
+    def size(self) -> int:
+        return self.world.world if self.world is not None else 1
+
+    def owns(self, doc) -> bool:
+        ns, app = app_of(doc)
+        return owner_of(ns, app, self.size) == self.rank
+
+    def _after_reform(self, before: List[str]) -> None:
+        gone = set(before) - set(self.world.members)
+        self.dead |= {worker_id_of(m) for m in gone}
+        moved = self.mon.release(lambda d: not self.owns(d))
+        self.health.reset()
+        log.warning("node re-formed: generation %d, members %s (lost %s); released %d moved jobs",
+                    self.world.generation, self.world.members, sorted(gone), moved)
+
+    def _exchange(self) -> Dict:
+        names, counts = self.mon.app_table()
+        info = {"member": self.world.id if self.world else "m0", "pid": os.getpid()}
+        return self.health.exchange(names, counts, self.mon.roster_version, self.mon.n_live, info)
+
+    async def tick(self) -> Dict:
+        self.mon.sync(steal_from=self.dead or None)
+        try:
+            await self.mon.tick()
+        except Exception as e:  # noqa: BLE001 - a scoring failure must not desynchronise the collectives
+            log.exception("streaming tick failed: %s", e)
+        if self.world is None:
+            table = self._exchange()
+        else:
+            before, gen = list(self.world.members), self.world.generation
+            table = self.world.run_tick(self._exchange)
+            if self.world.generation != gen:
+                self._after_reform(before)
+        table["generation"] = self.world.generation if self.world else 0
+        self.table = table
+        self.ticks += 1
+        if self.publish and self.rank == 0:
+            try:
+                self.store.put_meta(META_KEY, table)
+            except Exception as e:  # noqa: BLE001 - the store may be briefly unavailable
+                log.warning("publishing the node health table failed: %s", e)
+        return table
+
+    async def run_forever(self, stop: asyncio.Event, period: float) -> None:
+        if self.world is not None and not dist.is_initialized():
+            self.world.form()
+            self.world.start_heartbeat()
+        try:
+            while not stop.is_set():
+                t0 = time.monotonic()
+                await self.tick()
+                try:
+                    await asyncio.wait_for(stop.wait(), timeout=max(0.0, period - (time.monotonic() - t0)))
+                except asyncio.TimeoutError:
+                    pass
+        finally:
+            if self.world is not None:
+                self.world.stop_heartbeat()
+
+
+def elastic_world_from_env(device: torch.device) -> Optional[ElasticWorld]:
+    """The rank's ElasticWorld: under :func:`launch_node` (``FOREMAST_NODE_STORE``)
+    or under torchrun (``WORLD_SIZE`` > 1: the agent's store at MASTER_ADDR:PORT);
+    None for a single brain process."""
+    hb = float(os.environ.get("FOREMAST_HEARTBEAT_S", "5"))
+    coll = float(os.environ.get("FOREMAST_COLLECTIVE_TIMEOUT_S", "60"))
+    if os.environ.get("FOREMAST_NODE_STORE"):
+        host, port = os.environ["FOREMAST_NODE_STORE"].rsplit(":", 1)
+        n = int(os.environ["FOREMAST_NODE_MEMBERS"])
+        me = int(os.environ["FOREMAST_NODE_MEMBER"])
+    elif int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        host, port = os.environ.get("MASTER_ADDR", "127.0.0.1"), os.environ["MASTER_PORT"]
+        n, me = int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"])
+    else:
+        return None
+    kv = dist.TCPStore(host, int(port), is_master=False, timeout=datetime.timedelta(seconds=60))
+    backend = os.environ.get("FOREMAST_DIST_BACKEND", "nccl" if device.type == "cuda" else "gloo")
+    return ElasticWorld(kv, f"m{me}", [f"m{i}" for i in range(n)], backend=backend, heartbeat_timeout_s=hb,
+                        collective_timeout_s=coll, device_id=device if backend == "nccl" else None)
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_node(nproc: int, argv: List[str]) -> int:
+    """Start ``nproc`` brain ranks (``python -m foremast_amd.brain <argv>``) around a
+    key-value store this process hosts.  A rank that dies is not restarted: the
+    survivors re-shard its apps.  Returns when every rank has exited (SIGTERM /
+    SIGINT are forwarded); the exit code is 0 if any rank exited cleanly."""
+    port = _free_port()
+    kv = dist.TCPStore("127.0.0.1", port, is_master=True, wait_for_workers=False,
+                       timeout=datetime.timedelta(seconds=60))
+    procs = []
+    for i in range(nproc):
+        env = dict(os.environ, FOREMAST_NODE_STORE=f"127.0.0.1:{port}", FOREMAST_NODE_MEMBERS=str(nproc),
+                   FOREMAST_NODE_MEMBER=str(i), LOCAL_RANK=str(i), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        env.pop("WORLD_SIZE", None)
+        procs.append(subprocess.Popen([sys.executable, "-m", "foremast_amd.brain"] + argv, env=env))
+    kv.set("launcher/pids", ",".join(str(p.pid) for p in procs))
+
+    def forward(sig, _frame):
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(sig)
+    old = {s: signal.signal(s, forward) for s in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        codes = [p.wait() for p in procs]
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+    del kv
+    return 0 if any(c == 0 for c in codes) else (codes[0] or 1)

@@ -15,7 +15,8 @@ Routes and behaviour follow ``foremast-service/cmd/manager/main.go:130-276``:
 
 Extensions (not in the reference): ``GET /healthz`` and
 ``GET /v1/healthcheck/cluster`` (the node-level health table aggregated over
-the GPU ranks, when a brain publishes one into the service).
+the GPU ranks: rank 0 of the node brain publishes it into the job store,
+``brain/node.py``).
 """
 
 from __future__ import annotations
@@ -141,9 +142,14 @@ def create_app(store: Optional[JobStore] = None, query_endpoint: Optional[str] =
 
     @app.get("/v1/healthcheck/cluster")
     async def cluster():
-        if cluster_health is None:
-            return JSONResponse(content={"ranks": 0, "apps": {}})
-        return JSONResponse(content=cluster_health())
+        if cluster_health is not None:
+            return JSONResponse(content=cluster_health())
+        table = None
+        try:
+            table = store.get_meta("cluster_health")  # published by the node brain's rank 0
+        except Exception as e:  # noqa: BLE001 - store down: report "no table"
+            log.warning("cluster health lookup failed: %s", e)
+        return JSONResponse(content=table or {"ranks": 0, "apps": {}})
 
     @app.get("/healthz")
     async def healthz():
