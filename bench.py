@@ -79,6 +79,12 @@ def parse():
                    help="injected canary regression: values x3, or a level shift of +3 noise sigma")
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--graph", action="store_true", help="capture the GPU part of a tick in a HIP graph")
+    p.add_argument("--ingest", default="pinned", choices=["pinned", "prom"],
+                   help="pinned: a tick's points arrive decoded in pinned memory; prom: they arrive as "
+                        "Prometheus query_range JSON bodies (one per metric family and canary/baseline pod "
+                        "set), decoded in the timed tick by the native keyed parser on a thread pool, "
+                        "double-buffered so tick k+1 decodes while the GPU scores tick k")
+    p.add_argument("--decode-threads", type=int, default=8)
     p.add_argument("--cpu", action="store_true", help="force CPU (reference path; tiny sizes only)")
     p.add_argument("--config", default="canary", choices=["canary", "single", "hw10k", "lstm", "multivariate"],
                    help="canary = headline (BASELINE configs 2/4 at 100k); single = config 1 (one latency "
@@ -267,7 +273,23 @@ def setup_canary(args, world, rank, dev):
         newvb = torch.empty((n_local, P), dtype=torch.float32, device=dev)
         newv, newb = newvb, torch.empty((n_local, P), dtype=torch.float32, device=dev)
 
+    decoder = None
+    if args.ingest == "prom":
+        if exch is not None:
+            raise SystemExit("--ingest prom covers the single-cluster canary layout")
+        decoder, bodies = prom_bodies(host_ticks, s, P, args.ring, args.decode_threads, pin)
+        del host_ticks
+        pending = {}
+
     def load_tick(k):
+        if decoder is not None:
+            fut = pending.pop(k, None) or decoder.submit(bodies[k], T_STEP * (args.ring + k), T_STEP)
+            LAT_START[k - W] = fut.t_submit  # detect latency includes this tick's decode
+            block, _ = fut.result()
+            newvb.copy_(block.view(n_local, 2 * P), non_blocking=pin)
+            if k + 1 < len(bodies):  # decode the next tick while the GPU scores this one
+                pending[k + 1] = decoder.submit(bodies[k + 1], T_STEP * (args.ring + k + 1), T_STEP)
+            return
         newvb.copy_(host_ticks[k], non_blocking=pin)
         if exch is not None:
             base_dev.copy_(base_host[k], non_blocking=pin)
@@ -306,13 +328,51 @@ def setup_canary(args, world, rank, dev):
         "multi_cluster": bool(args.multi_cluster),
         "health_collectives": "1 fused all_gather" if agg.fused else ("all_reduce + all_gather" if world > 1 else "none"),
         "hip_graph": bool(args.graph and dev.type == "cuda"),
+        "ingest": args.ingest,
     }
+    if decoder is not None:
+        meta["ingest_bytes_per_tick"] = int(sum(len(b) for b in bodies[0]))
+        meta["_decoder"] = decoder
     if agg.fused:
         meta["_table"] = lambda h: HealthAggregator.host_app_table(h, world, apps_per_rank)
     dt = "bf16" if dtype == torch.bfloat16 else "fp32"
     meta["_agg"] = agg
     meta["_truth"] = (truth_apps, n_apps)
     return tick, health_host, meta, dt, args.series
+
+
+T_STEP = 60.0  # query step (metricsquery.go:43)
+LAT_START = {}  # timed tick -> perf_counter time its data arrived (set by the prom ingest path)
+
+
+def prom_bodies(host_ticks, s, P, ring, threads, pin):
+    """Render every tick's points as Prometheus ``query_range`` bodies (untimed
+    setup): per metric family one body for the canary pods and one for the
+    baseline pods, one series per (app, pod) — the shape the brain gets from
+    ``namespace_pod:<metric>{...}`` at a 60 s step.  Returns the decoder (key
+    tables from the bodies' own label order) and ``bodies[tick][family*2+kind]``."""
+    from foremast_amd.ingest import native
+    from foremast_amd.ingest.tickdecode import TickDecoder, pod_matrix_body
+    nt, n, twoP = host_ticks.shape
+    gid = np.arange(n) + s                     # global series id: app = gid // 5, family = gid % 5
+    labels, rows, sel = [], [], []
+    for m in range(METRICS_PER_APP):
+        ids = np.nonzero(gid % METRICS_PER_APP == m)[0]
+        for kind, tag in enumerate(("c", "b")):
+            labels.append([f'"namespace":"ns{a % 200}","app":"app{a}","pod":"app{a}-{tag}{p}-7d9f8b6c5d"'
+                           for a in (gid[ids] // METRICS_PER_APP).tolist() for p in range(P)])
+            rows.append((ids[:, None] * twoP + kind * P + np.arange(P)[None, :]).reshape(-1))
+            sel.append((ids, kind))
+    vals = host_ticks.numpy()
+    bodies = []
+    for k in range(nt):
+        ts = T_STEP * (ring + k)
+        bodies.append([pod_matrix_body(f"namespace_pod:metric{j // 2}", labels[j], ts,
+                                       vals[k, ids, kind * P:(kind + 1) * P].reshape(-1))
+                       for j, (ids, kind) in enumerate(sel)])
+    tables = [native.KeyTable.from_hashes(native.series_keys(b, "app", "pod"), r, "app", "pod")
+              for b, r in zip(bodies[0], rows)]
+    return TickDecoder(tables, n * twoP, 1, pinned=pin, threads=threads), bodies
 
 
 def setup_lstm(args, world, rank, dev, n_features, fp8):
@@ -478,6 +538,7 @@ def main():
 
     agg = meta.pop("_agg", None)
     table = meta.pop("_table", None)
+    decoder = meta.pop("_decoder", None)
     truth = meta.pop("_truth", None)
     if truth is not None and world > 1:
         parts = [None] * world
@@ -496,7 +557,7 @@ def main():
     for k in range(args.steps):
         ts = time.perf_counter()
         tick(args.warmup + k)
-        lat.append(time.perf_counter() - ts)
+        lat.append(time.perf_counter() - LAT_START.pop(args.warmup + k, ts))
     if dev.type == "cuda":
         torch.cuda.synchronize()
     barrier(dev)
@@ -542,6 +603,8 @@ def main():
             "health": {"apps": int(health_host.shape[0]), "anomalous_apps": anomalous_apps,
                        "series_scored_last_tick": scored},
         }
+        if decoder is not None:
+            res["decode_ms_last_tick"] = round(decoder.last_decode_ms, 3)
         if truth is not None:
             res["detection"] = dict(detection_report(health_host, truth[0], truth[1]),
                                     injected=f"{args.anomaly_kind} on {args.anomaly_frac:g} of series")

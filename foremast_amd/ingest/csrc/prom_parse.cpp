@@ -281,6 +281,21 @@ long long fm_prom_dense(const char* buf, long long len, double start, double ste
   return r;
 }
 
+// Key of every series in response order (FNV of its label_a / label_b values):
+// builds the KeyTable of a known response layout without per-series Python.
+long long fm_prom_keys(const char* buf, long long len, long long max_series, const char* label_a,
+                       const char* label_b, uint64_t* out) {
+  return walk(
+      buf, len,
+      [&](long long s, const char* m0, const char* m1) {
+        const char *a0 = "", *a1 = a0, *b0 = a0, *b1 = a0;
+        label_value(m0, m1, label_a, a0, a1);
+        label_value(m0, m1, label_b, b0, b1);
+        if (s < max_series) out[s] = fnv_key(a0, a1, b0, b1);
+      },
+      [&](long long, double, double) {});
+}
+
 // Keyed dense scatter: series s goes to row key_rows[j] where key_hash[j] is the
 // FNV key of its (label_a, label_b) values (key_hash sorted ascending, n_keys
 // entries); unmatched series are skipped and counted in *unmatched.

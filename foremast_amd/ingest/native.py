@@ -70,6 +70,8 @@ def _load() -> Optional[C.CDLL]:
         lib.fm_prom_dense_keyed.argtypes = [C.c_char_p, LL, C.c_double, C.c_double, LL, P, LL, LL, C.c_char_p,
                                             C.c_char_p, P, P, LL, P, P]
         lib.fm_prom_dense_keyed.restype = LL
+        lib.fm_prom_keys.argtypes = [C.c_char_p, LL, LL, C.c_char_p, C.c_char_p, P]
+        lib.fm_prom_keys.restype = LL
         _lib = lib
         return lib
 
@@ -169,8 +171,35 @@ class KeyTable:
         self.rows = np.array([r for _, r in pairs], dtype=np.int64)
         self.label_a, self.label_b = label_a.encode(), label_b.encode()
 
+    @classmethod
+    def from_hashes(cls, hashes: np.ndarray, rows: np.ndarray, label_a: str = "namespace",
+                    label_b: str = "app") -> "KeyTable":
+        t = cls([], label_a, label_b)
+        order = np.argsort(hashes, kind="stable")
+        t.hash = np.ascontiguousarray(hashes[order], dtype=np.uint64)
+        t.rows = np.ascontiguousarray(np.asarray(rows, dtype=np.int64)[order])
+        if len(t.hash) > 1 and bool((t.hash[1:] == t.hash[:-1]).any()):
+            raise ValueError("series key hash collision")
+        return t
+
     def __len__(self) -> int:
         return len(self.rows)
+
+
+def series_keys(body: bytes, label_a: str = "namespace", label_b: str = "app") -> np.ndarray:
+    """FNV key of every series of a response, in response order (uint64)."""
+    if isinstance(body, str):
+        body = body.encode()
+    lib = _load()
+    if lib is None:
+        return np.array([key_hash(l.get(label_a, ""), l.get(label_b, "")) for l, _, _ in _parse_py(body)],
+                        dtype=np.uint64)
+    n = lib.fm_prom_scan(body, len(body), 0, None, None, None, None)
+    if n < 0:
+        raise ParseError(f"malformed query_range body (code {n})")
+    out = np.zeros(n, dtype=np.uint64)
+    lib.fm_prom_keys(body, len(body), n, label_a.encode(), label_b.encode(), out.ctypes.data)
+    return out
 
 
 def parse_dense_keyed(body: bytes, start: float, step: float, T: int, out: np.ndarray, table: KeyTable,

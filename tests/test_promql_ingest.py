@@ -82,3 +82,49 @@ def test_error_rate_spikes():
     v = f(np.arange(0, 3600, 60.0))
     assert v[10] > 30 and v[30] > 30
     assert np.all(v[[0, 5, 20, 40]] < 2)
+
+
+def test_tick_decoder_round_trips_pod_bodies():
+    """Bodies rendered per (app, pod) decode, in parallel and double-buffered,
+    into exactly the float32 block they were rendered from."""
+    import torch
+    from foremast_amd.ingest import native
+    from foremast_amd.ingest.tickdecode import TickDecoder, pod_matrix_body
+    rng = np.random.default_rng(0)
+    n_app, P = 300, 4
+    vals = rng.normal(50, 10, (2, n_app, 2 * P)).astype(np.float32)
+    vals[0, 7, 3] = np.nan
+    labels, rows = [], []
+    for kind in range(2):
+        labels.append([f'"app":"a{a}","pod":"a{a}-{kind}{p}"' for a in range(n_app) for p in range(P)])
+        rows.append((np.arange(n_app)[:, None] * 2 * P + kind * P + np.arange(P)[None, :]).reshape(-1))
+    bodies = [[pod_matrix_body("m", labels[kind], 600 * (k + 1), vals[k, :, kind * P:(kind + 1) * P].reshape(-1))
+               for kind in range(2)] for k in range(2)]
+    tables = [native.KeyTable.from_hashes(native.series_keys(b, "app", "pod"), r, "app", "pod")
+              for b, r in zip(bodies[0], rows)]
+    dec = TickDecoder(tables, n_app * 2 * P, 1, pinned=False, threads=2)
+    futs = [dec.submit(bodies[k], 600 * (k + 1), 60.0) for k in range(2)]
+    for k, f in enumerate(futs):
+        block, stats = f.result()
+        assert [s[2] for s in stats] == [0, 0]  # every series matched a row
+        np.testing.assert_array_equal(block.view(n_app, 2 * P).numpy(), vals[k])
+    dec.close()
+
+
+def test_bench_prom_ingest_matches_pinned_ingest():
+    """bench --ingest prom (JSON bodies decoded inside the tick) scores exactly
+    what the pinned-arrival path scores."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = []
+    for mode in ("pinned", "prom"):
+        out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--cpu", "--steps", "2", "--warmup",
+                              "1", "--ingest", mode, "--anomaly-frac", "0.05"], capture_output=True, text=True,
+                             timeout=600, env=dict(os.environ, OMP_NUM_THREADS="2"))
+        assert out.returncode == 0, out.stderr[-2000:]
+        res.append(json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0]))
+    assert res[0]["health"] == res[1]["health"] and res[0]["detection"] == res[1]["detection"]
+    assert res[1]["config"]["ingest"] == "prom" and res[1]["config"]["ingest_bytes_per_tick"] > 0
