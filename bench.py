@@ -58,7 +58,11 @@ from foremast_amd.parallel.health import HealthAggregator, shard_range  # noqa: 
 from foremast_amd.utils.config import BrainConfig  # noqa: E402
 
 METRIC = "metric-series scored/sec (whole node) + p50 detect latency, 100k-series canary"
-BASELINE_VALUE = None  # the reference publishes no number (BASELINE.json "published": {})
+# The reference publishes no number (BASELINE.json "published": {}).  vs_baseline is
+# measured against this repo's CPU re-creation of the reference brain's design: the
+# same scorer as a per-series numpy/scipy loop on ONE core (bench.py --config
+# cpu_baseline, models/cpu_baseline.py; BASELINE.md "CPU per-series baseline").
+CPU_BASELINE_SERIES_PER_S = {"canary": 16.08, "hw10k": 16.08, "lstm": 256.4, "multivariate": 418.6}
 METRICS_PER_APP = 5
 
 
@@ -86,7 +90,12 @@ def parse():
                         "double-buffered so tick k+1 decodes while the GPU scores tick k")
     p.add_argument("--decode-threads", type=int, default=8)
     p.add_argument("--cpu", action="store_true", help="force CPU (reference path; tiny sizes only)")
-    p.add_argument("--config", default="canary", choices=["canary", "single", "hw10k", "lstm", "multivariate"],
+    p.add_argument("--baseline-sample", type=int, default=48,
+                   help="cpu_baseline: series scored by the per-series CPU loop (the rate is per core)")
+    p.add_argument("--baseline-model", default="canary", choices=["canary", "lstm", "multivariate"],
+                   help="cpu_baseline: which GPU config's scorer the per-series CPU loop re-creates")
+    p.add_argument("--config", default="canary",
+                   choices=["canary", "single", "hw10k", "lstm", "multivariate", "cpu_baseline"],
                    help="canary = headline (BASELINE configs 2/4 at 100k); single = config 1 (one latency "
                         "series, moving average, CPU brain plumbing end to end); hw10k = config 2 (10k series); "
                         "lstm = config 3; multivariate = config 5 (fp8 LSTM, latency + error-rate)")
@@ -518,8 +527,88 @@ def setup_single(args, world, rank, dev):
     return tick_and_health, health, meta, "fp32", world
 
 
+def run_cpu_baseline_lstm(args, F: int) -> None:
+    """Comparator of configs 3 / 5: one entity at a time on ONE core — z-score
+    its F histories, run the LSTM autoencoder (H=64) over its latest window,
+    compare the reconstruction error — scoring only (no training, which only
+    favours the baseline)."""
+    from foremast_amd.models.lstm_ae import LSTMAutoencoder
+    torch.set_num_threads(1)
+    dev = torch.device("cpu")
+    n, T = args.baseline_sample, args.lstm_window
+    torch.manual_seed(0)
+    model = LSTMAutoencoder(F, 64).eval()
+    params = [synthetic_params(n, dev, seed=1234 + 7 * f) for f in range(F)]
+    hist = np.stack([synthetic_eval(p, 0, args.ring, args.season, noise_seed=555 + f).numpy()
+                     for f, p in enumerate(params)], 2)  # [n, R, F]
+    t0 = time.perf_counter()
+    flagged = 0
+    with torch.no_grad():
+        for i in range(n):
+            h = hist[i]
+            mu, sd = h.mean(0), np.maximum(h.std(0), 1e-6)
+            x = torch.from_numpy(((h[-T:] - mu) / sd).astype(np.float32))[None]
+            err = float(model.recon_error(x))
+            flagged += int(err > 1.0 + 4.0 * 0.5)
+    dt = time.perf_counter() - t0
+    rate = n * F / dt
+    print(json.dumps({
+        "metric": METRIC, "value": round(rate, 3), "unit": "series/s", "n_gpus": 0, "steps": 1, "warmup": 0,
+        "ms_per_entity": round(dt / n * 1e3, 3), "higher_is_better": True, "scaling": "none", "vs_baseline": 1.0,
+        "dtype": "fp32", "data": "synthetic (same generator as the lstm bench); random-init weights",
+        "config": {"model": f"LSTM autoencoder (F={F}, H=64, window {T}) scoring, per entity",
+                   "bench_config": "cpu_baseline", "baseline_model": args.baseline_model, "global_batch": n,
+                   "seq_len": T, "history": args.ring, "device": "cpu, 1 core (torch CPU, batch 1)",
+                   "reference_budget_100m_cpu_series_per_s": round(rate * 0.1, 4)}}), flush=True)
+
+
+def run_cpu_baseline(args) -> None:
+    """The comparator: the headline canary scorer as a per-series numpy/scipy
+    loop on ONE CPU core (models/cpu_baseline.py) over a sample of the same
+    synthetic series, windows and injected regressions."""
+    if args.baseline_model != "canary":
+        return run_cpu_baseline_lstm(args, 1 if args.baseline_model == "lstm" else 2)
+    from foremast_amd.models import cpu_baseline as cb
+    from foremast_amd.models import smoothing as sm
+    torch.set_num_threads(1)
+    dev = torch.device("cpu")
+    n, P, W = args.baseline_sample, args.pods, args.window
+    cfg = BrainConfig()
+    grid = sm.make_grid(sm.MODE_HW, cfg.hw_alpha, cfg.hw_beta, cfg.hw_gamma).numpy()
+    params = synthetic_params(n, dev, seed=1234)
+    hist = synthetic_eval(params, 0, args.ring, args.season, noise_seed=4321).numpy()
+    cur, bad = make_ticks(params, P, W, args.season, args.ring, 99, max(args.anomaly_frac, 1.0 / n),
+                          args.anomaly_kind, want_bad=True)
+    base = make_ticks(params, P, W, args.season, args.ring, 7, 0.0)
+    cur = cur.permute(1, 2, 0).reshape(n, P * W).numpy()    # pod-major windows, as the engine's
+    base = base.permute(1, 2, 0).reshape(n, P * W).numpy()
+    hz = np.tile(np.arange(1, W + 1), P)
+    t0 = time.perf_counter()
+    verdicts = [cb.score_series(hist[i], cur[i], base[i], hz, args.season, grid, threshold=4.0, bound=3,
+                                alpha=cfg.pairwise_threshold, pairwise_scale=cfg.pairwise_scale,
+                                pw_min_points=cfg.pairwise_min_points).verdict for i in range(n)]
+    dt = time.perf_counter() - t0
+    truth = set(bad.tolist())
+    flagged = {i for i, v in enumerate(verdicts) if v == 1}
+    rate = n / dt
+    print(json.dumps({
+        "metric": METRIC, "value": round(rate, 3), "unit": "series/s", "n_gpus": 0, "steps": 1, "warmup": 0,
+        "ms_per_series": round(dt / n * 1e3, 2), "higher_is_better": True, "scaling": "none", "vs_baseline": 1.0,
+        "dtype": "fp64", "data": "synthetic (same generator and seeds as the canary bench)",
+        "config": {"model": "holt_winters (64-point grid) + scipy mannwhitneyu/wilcoxon/kruskal, per series",
+                   "bench_config": "cpu_baseline", "baseline_model": "canary", "global_batch": n,
+                   "seq_len": args.ring, "season": args.season,
+                   "pods": P, "current_window": W, "device": "cpu, 1 core (numpy/scipy loop)",
+                   "reference_budget_100m_cpu_series_per_s": round(rate * 0.1, 4)},
+        "detection": {"injected": len(truth), "tp": len(truth & flagged), "fp": len(flagged - truth)},
+    }), flush=True)
+
+
 def main():
     args = parse()
+    if args.config == "cpu_baseline":
+        run_cpu_baseline(args)
+        return
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(self_launch(args, sys.argv[1:]))
     if args.config == "hw10k":
@@ -576,6 +665,7 @@ def main():
     scored = int(health_host[:, 1].sum())
     if rank == 0:
         value = n_series * args.steps / elapsed
+        cfg_name = getattr(args, "config_name", args.config)
         config = {"model": meta.pop("model"), "global_batch": meta.pop("global_batch"),
                   "seq_len": meta.pop("seq_len"), "parallelism": f"dp{world}",
                   "bench_config": getattr(args, "config_name", args.config)}
@@ -591,7 +681,8 @@ def main():
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
             "scaling": "strong",
-            "vs_baseline": None if BASELINE_VALUE is None else round(value / BASELINE_VALUE, 3),
+            "vs_baseline": (round(value / CPU_BASELINE_SERIES_PER_S[cfg_name], 1)
+                            if cfg_name in CPU_BASELINE_SERIES_PER_S else None),
             "dtype": dtype_name,
             "data": "synthetic (seasonal Prometheus-like range-vectors, random per-series params; random-init weights)",
             "config": config,
