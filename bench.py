@@ -105,7 +105,8 @@ def parse():
     p.add_argument("--lstm-window", type=int, default=32)
     p.add_argument("--lstm-train-batch", type=int, default=4096)
     p.add_argument("--lstm-train-every", type=int, default=1)
-    p.add_argument("--lstm-pretrain", type=int, default=10)
+    p.add_argument("--lstm-pretrain", type=int, default=200,
+                   help="DP training steps of model initialisation before the timed ticks (untimed)")
     p.add_argument("--lstm-autograd", action="store_true", help="train with autograd instead of the fused K7 kernel")
     p.add_argument("--lstm-no-overlap", action="store_true",
                    help="run the training step and scoring back to back instead of on two HIP streams")

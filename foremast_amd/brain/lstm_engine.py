@@ -162,9 +162,20 @@ class LstmShard:
     def calibrate(self, n: int = 4096) -> None:
         """Reconstruction-error mean/std over ``n`` history windows per rank,
         combined across ranks (one 3-float all-reduce) so every rank applies
-        the same threshold."""
-        with torch.no_grad():
-            e = self.model.recon_error(self._sample(n)).double()
+        the same threshold.  On the GPU the windows are scored by the SAME
+        fused kernel (and precision: bf16, or fp8 e4m3) that scores the ticks,
+        so the z-score of a healthy window is calibrated for the scoring
+        path's quantisation noise, not for the fp32 training model."""
+        if self.gpu:
+            from ..ops import lstm as L
+            self._pack_scoring()
+            o = L.lstm_score(self.packed, None, 0.0, 1.0, thr_default=float("inf"), ring=self._sample_ring(n),
+                             T=self.T)
+            e = o["err"].double()
+            e = e[torch.isfinite(e)]
+        else:
+            with torch.no_grad():
+                e = self.model.recon_error(self._sample(n)).double()
         mom = torch.stack([e.sum(), (e * e).sum(), torch.tensor(float(e.numel()), dtype=torch.float64,
                                                                 device=e.device)])
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
