@@ -83,6 +83,9 @@ def parse():
                    help="injected canary regression: values x3, or a level shift of +3 noise sigma")
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--graph", action="store_true", help="capture the GPU part of a tick in a HIP graph")
+    p.add_argument("--refit-every", type=int, default=1,
+                   help="Holt-Winters model cache: full 64-point grid refit every K ticks, O(1) state update + "
+                        "detect in between (1 = refit every tick: the headline)")
     p.add_argument("--ingest", default="pinned", choices=["pinned", "prom"],
                    help="pinned: a tick's points arrive decoded in pinned memory; prom: they arrive as "
                         "Prometheus query_range JSON bodies (one per metric family and canary/baseline pod "
@@ -221,7 +224,7 @@ def setup_canary(args, world, rank, dev):
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     spec = ShardSpec(n_series=n_local, ring_len=args.ring, season=args.season, pods=args.pods,
                      window=args.window, algorithm=args.algorithm, pairwise=args.pairwise,
-                     dtype=dtype, n_apps=n_apps)
+                     dtype=dtype, n_apps=n_apps, refit_every=args.refit_every)
     app_id = (torch.arange(s, e, device=dev, dtype=torch.int64) // METRICS_PER_APP).to(torch.int32)
     # shards are app-aligned, so each rank owns a disjoint slice of the app table: the
     # health exchange is ONE all-gather of per-rank records the scorer writes in place
@@ -325,6 +328,7 @@ def setup_canary(args, world, rank, dev):
         health_host.copy_(agg.recv if agg.fused else stats, non_blocking=pin)
         if dev.type == "cuda":
             torch.cuda.current_stream().synchronize()
+        REFIT_FLAGS[k] = shard.last_refit
         return out
 
     meta = {
@@ -339,6 +343,8 @@ def setup_canary(args, world, rank, dev):
         "health_collectives": "1 fused all_gather" if agg.fused else ("all_reduce + all_gather" if world > 1 else "none"),
         "hip_graph": bool(args.graph and dev.type == "cuda"),
         "ingest": args.ingest,
+        "model_cache": ("none: every tick refits every series" if args.refit_every <= 1 else
+                        f"refit every {args.refit_every} ticks, O(1) Holt-Winters state update + detect in between"),
     }
     if decoder is not None:
         meta["ingest_bytes_per_tick"] = int(sum(len(b) for b in bodies[0]))
@@ -353,6 +359,7 @@ def setup_canary(args, world, rank, dev):
 
 T_STEP = 60.0  # query step (metricsquery.go:43)
 LAT_START = {}  # timed tick -> perf_counter time its data arrived (set by the prom ingest path)
+REFIT_FLAGS = {}  # tick -> whether it refit the model (canary --refit-every)
 
 
 def prom_bodies(host_ticks, s, P, ring, threads, pin):
@@ -697,6 +704,12 @@ def main():
         }
         if decoder is not None:
             res["decode_ms_last_tick"] = round(decoder.last_decode_ms, 3)
+        if args.config == "canary" and args.refit_every > 1:
+            flags = np.array([REFIT_FLAGS.get(args.warmup + k, True) for k in range(args.steps)])
+            res["refit_ticks_timed"] = int(flags.sum())
+            for name, sel in (("refit", flags), ("cached", ~flags)):
+                if sel.any():
+                    res[f"p50_{name}_tick_ms"] = round(float(np.percentile(lat_ms[sel], 50)), 3)
         if truth is not None:
             res["detection"] = dict(detection_report(health_host, truth[0], truth[1]),
                                     injected=f"{args.anomaly_kind} on {args.anomaly_frac:g} of series")

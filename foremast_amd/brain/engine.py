@@ -48,6 +48,10 @@ class ShardSpec:
     dtype: torch.dtype = torch.bfloat16
     n_apps: int = 1
     want_band: bool = True
+    # Holt-Winters model cache: refit (64-point grid over the whole window) every
+    # ``refit_every`` ticks; in between the fitted state is advanced by the graduated
+    # point and the window scored from it in O(1) per series (1 = refit every tick)
+    refit_every: int = 1
     extra: Dict = field(default_factory=dict)
 
 
@@ -112,6 +116,11 @@ class StreamingShard:
         if self.gpu:
             self._state_host = torch.zeros(8, dtype=torch.int32).pin_memory()
             self._state_dev = torch.zeros(8, dtype=torch.int32, device=self.device)
+        # cached Holt-Winters model (refit_every > 1): state after the last refit / update
+        self.refit_every = max(1, int(spec.refit_every))
+        self._cache: Optional[Dict] = None
+        self._new_pts = 0          # points graduated into the history since the state was advanced
+        self.last_refit = True     # whether the last score() refit the model
 
     def refresh_thresholds(self) -> None:
         """Per-point thresholds of the full and the lowered (pairwise) band for the
@@ -131,6 +140,7 @@ class StreamingShard:
     # ------------------------------------------------------------------ data in
     def load_history(self, values: torch.Tensor) -> None:
         self.hist.load(values.to(self.device))
+        self._cache = None
 
     def load_rows(self, rows: torch.Tensor, values: torch.Tensor) -> None:
         """Write the full history AND current window of some rows (a series
@@ -144,6 +154,7 @@ class StreamingShard:
         if v.dim() != 2 or v.shape[0] != rows.numel() or v.shape[1] != L + W:
             raise ValueError(f"values must be [{rows.numel()}, {L + W}]")
         hv = v[:, :L].to(self.hist.data.dtype)
+        self._cache = None  # the new rows need a fitted state: refit on the next tick
         head = self.hist.head
         n1 = min(L, R - head)
         self.hist.data[:, head:head + n1].index_copy_(0, rows, hv[:, :n1])
@@ -196,6 +207,10 @@ class StreamingShard:
             if graduate:
                 self.hist.data[:, self.hist.next_col()] = old.to(self.hist.data.dtype)
         if graduate:
+            if self.hist.length == self.hist.R:
+                self._new_pts += 1   # the window slides: the cached state can absorb the point
+            else:
+                self._cache = None   # the window grows (padding / phases change): refit
             self.hist.advance(1)
         self._refresh_horizons()
 
@@ -204,7 +219,8 @@ class StreamingShard:
         """The steady state a captured tick assumes: GPU, full ring (head
         advances by one per tick), warm window (every tick graduates), the
         two-series-per-wave Holt-Winters path, no anomaly list."""
-        return (self.gpu and self.mode == sm_ref.MODE_HW and self.hist.length == self.hist.R
+        return (self.gpu and self.mode == sm_ref.MODE_HW and self.refit_every == 1
+                and self.hist.length == self.hist.R
                 and self.cur.ticks >= self.cur.W and self.anomalies is None
                 and getattr(self, "_hw_variant", None) in (4, 5) and bool(self.out))
 
@@ -248,9 +264,76 @@ class StreamingShard:
     # ------------------------------------------------------------------ scoring
     def score(self) -> Dict[str, torch.Tensor]:
         self.app_stats.zero_()
+        cached = self._use_cache()
+        self.last_refit = not cached
         if self.gpu:
-            return self._score_gpu()
-        return self._score_cpu()
+            out = self._score_cached_gpu() if cached else self._score_gpu()
+        else:
+            out = self._score_cpu(cached)
+        if self._cache is not None:
+            self._cache["since"] = 0 if not cached else self._cache["since"] + 1
+        return out
+
+    # ------------------------------------------------------------------ model cache
+    def cache_supported(self) -> bool:
+        from ..ops import kernels as K
+        return (self.refit_every > 1 and self.mode == sm_ref.MODE_HW
+                and (not self.gpu or self.spec.season >= K.HW_STATE_MIN_M))
+
+    def _use_cache(self) -> bool:
+        c = self._cache
+        return (c is not None and self.cache_supported() and c["since"] + 1 < self.refit_every
+                and self.hist.length == self.hist.R and self._new_pts <= self.hist.R)
+
+    def _rank_tests_main(self):
+        """Pairwise tests on the current stream (cached ticks: nothing to overlap)."""
+        from ..ops import kernels as K
+        cfg = self.cfg
+        if self.pw_mode == pw_ref.PW_NONE:
+            return None
+        self.pw_out = K.rank_tests(self.base, self.cur.data, self.pw_mode, cfg.pairwise_threshold,
+                                   cfg.min_mann_white, cfg.min_wilcoxon, cfg.min_kruskal,
+                                   want_pvals=True, out=self.pw_out, pods=(self.cur.P, self.cur.P),
+                                   min_friedman=cfg.min_friedman)
+        return self.pw_out["differs"]
+
+    def _detect_spec(self, differs):
+        from ..ops import kernels as K
+        cfg = self.cfg
+        return K.DetectSpec(horizons=self.horizons, threshold=self.thr_full, bound=self.bound,
+                            min_lower=self.min_lower, cur=self.cur.data, differs=differs,
+                            pw_scale=cfg.pairwise_scale, min_valid=cfg.min_historical_points,
+                            want_band=self.spec.want_band, app_id=self.app_id, app_stats=self.app_stats,
+                            anomalies=self.anomalies, max_horizon=self.cur.W, threshold_low=self.thr_low,
+                            pw_min_points=cfg.pairwise_min_points, horizon_variance=cfg.horizon_variance)
+
+    def _refresh_cache_gpu(self) -> None:
+        """After a refit: the full state of the fitted model (hw_state.hip)."""
+        from ..ops import kernels as K
+        if not self.cache_supported() or self.hist.length != self.hist.R:
+            self._cache = None
+            return
+        h = self.hist
+        prev = self._cache["state"] if self._cache is not None else None
+        st = K.hw_state(h.data, h.head, h.length, self.spec.season, self.grid, self.out["best"], state=prev)
+        self._cache = {"state": st, "t_last": st["Tp"] - 1, "since": 0,
+                       "sigma": self.out["sigma"], "best": self.out["best"]}
+        self._new_pts = 0
+
+    def _score_cached_gpu(self) -> Dict[str, torch.Tensor]:
+        from ..ops import kernels as K
+        c, h = self._cache, self.hist
+        differs = self._rank_tests_main()
+        spec = self._detect_spec(differs)
+        if self.anomalies is not None:
+            self.anomalies.reset()
+        npts = self._new_pts
+        col0 = (h.head + h.length - npts) % h.R
+        self.out = K.hw_update_detect(h.data, col0, npts, c["t_last"], self.spec.season, self.grid, c["best"],
+                                      c["state"], c["sigma"], c["state"]["nvalid"], spec, out=self.out)
+        c["t_last"] += npts
+        self._new_pts = 0
+        return self.out
 
     def _score_gpu(self, head_dev: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
         from ..ops import kernels as K
@@ -293,6 +376,8 @@ class StreamingShard:
                 main.wait_stream(self._side)
                 Tp = K.smoothing_geometry(self.mode, h.length, self.spec.season)[0]
                 K.hw_detect_deferred(self.out, spec, Tp, self.spec.season, grid=self.grid)
+            if self.refit_every > 1 and head_dev is None:
+                self._refresh_cache_gpu()
         elif self.algorithm in ("moving_average_all", "moving_average"):
             length = h.length
             head = h.head
@@ -304,7 +389,7 @@ class StreamingShard:
             raise ValueError(f"algorithm {self.algorithm!r} is not a streaming univariate scorer")
         return self.out
 
-    def _score_cpu(self) -> Dict[str, torch.Tensor]:
+    def _score_cpu(self, cached: bool = False) -> Dict[str, torch.Tensor]:
         cfg = self.cfg
         y = self.hist.logical().float()
         differs = None
@@ -317,7 +402,20 @@ class StreamingShard:
                            "friedman": torch.stack([res.p_friedman, res.n_blocks], 1).float()}
         h = self.horizons.long()
         valid_hist = (~torch.isnan(y)).sum(1)
-        if self.mode is not None:
+        if cached:
+            c = self._cache
+            params = self.grid.cpu()[c["best"].long()]
+            st = c["state"]
+            if self._new_pts:
+                sm_ref.hw_update(st, y[:, y.shape[1] - self._new_pts:], params)
+            self._new_pts = 0
+            f = sm_ref.hw_state_forecast(st, h)
+            n_valid = c["n_valid"]
+            extra = {"level": st.level, "trend": st.trend, "sigma": c["sigma"], "best": c["best"]}
+            sigma = c["sigma"]
+            if cfg.horizon_variance:
+                sigma = c["sigma"][:, None] * det_ref.horizon_sigma_factor(params, self.mode, self.spec.season, h)
+        elif self.mode is not None:
             fit = sm_ref.fit_smoothing(y, self.mode, self.grid.cpu(), m=self.spec.season)
             f = sm_ref.forecast(fit, h)
             n_valid = fit.n_valid
@@ -326,6 +424,14 @@ class StreamingShard:
             if cfg.horizon_variance:
                 params = self.grid.cpu()[fit.best.long()]
                 sigma = fit.sigma[:, None] * det_ref.horizon_sigma_factor(params, self.mode, self.spec.season, h)
+            if self.cache_supported() and self.hist.length == self.hist.R:
+                self._cache = {"state": sm_ref.HwState(level=fit.level.clone(), trend=fit.trend.clone(),
+                                                       season=fit.season.clone(), t_last=fit.t_len - 1,
+                                                       m=self.spec.season),
+                               "since": 0, "sigma": fit.sigma, "best": fit.best.int(), "n_valid": fit.n_valid}
+                self._new_pts = 0
+            else:
+                self._cache = None
         else:
             win = cfg.ma_window if self.algorithm == "moving_average" else None
             st = ma_ref.window_stats(y, win)

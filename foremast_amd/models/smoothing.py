@@ -169,3 +169,70 @@ def forecast(fit: SmoothingFit, horizons: torch.Tensor) -> torch.Tensor:
         ph = (fit.t_len - 1 + h.long()) % fit.m
         f = f + fit.season.gather(1, ph)
     return f
+
+
+# ---------------------------------------------------------------------------------
+# Cached model (streaming engine ``refit_every > 1``; ops/csrc/hw_state.hip)
+# ---------------------------------------------------------------------------------
+
+@dataclass
+class HwState:
+    """State of a fitted Holt-Winters model after the point at padded time
+    ``t_last``: forecast for horizon h is ``level + h trend + season[(t_last + h) mod m]``."""
+    level: torch.Tensor   # [N]
+    trend: torch.Tensor   # [N]
+    season: torch.Tensor  # [N, m] (padded-time phase)
+    t_last: int
+    m: int
+
+
+def hw_run(y: torch.Tensor, params: torch.Tensor, m: int, pad_to: Optional[int] = None) -> HwState:
+    """The Holt-Winters recursion of :func:`fit_smoothing` with ONE parameter
+    row per series (``params [N, 3]`` = alpha, beta, gamma; e.g. the fitted grid
+    points), same initialisation and padding; returns the end state."""
+    y = y.float()
+    N, T = y.shape
+    Tp = pad_to or padded_length(MODE_HW, T, m)
+    pad = Tp - T
+    if pad:
+        y = torch.cat([torch.full((N, pad), float("nan"), device=y.device), y], dim=1)
+    al, be, ga = (params[:, i].to(y.device).float() for i in range(3))
+    ab, g1a = al * be, ga * (1.0 - al)
+    s0 = y[:, :m]
+    l0 = _nanmean(s0, 1)
+    lvl = l0.clone()
+    trd = (_nanmean(y[:, m:2 * m], 1) - l0) / m
+    season = torch.where(torch.isnan(s0), torch.zeros_like(s0), s0 - l0[:, None])
+    for t in range(m, Tp):
+        p = t % m
+        yt = y[:, t]
+        e = torch.where(torch.isnan(yt), torch.zeros_like(yt), yt - season[:, p] - lvl - trd)
+        lvl = lvl + trd + al * e
+        trd = trd + ab * e
+        season[:, p] = season[:, p] + g1a * e
+    return HwState(level=lvl, trend=trd, season=season, t_last=Tp - 1, m=m)
+
+
+def hw_update(st: HwState, y: torch.Tensor, params: torch.Tensor) -> HwState:
+    """Advance the state by new points ``y [N, k]`` (oldest first; NaN = missing,
+    imputed by the forecast) in place."""
+    al, be, ga = (params[:, i].to(y.device).float() for i in range(3))
+    ab, g1a = al * be, ga * (1.0 - al)
+    for j in range(y.shape[1]):
+        st.t_last += 1
+        p = st.t_last % st.m
+        yt = y[:, j].float()
+        e = torch.where(torch.isnan(yt), torch.zeros_like(yt), yt - st.season[:, p] - st.level - st.trend)
+        st.level = st.level + st.trend + al * e
+        st.trend = st.trend + ab * e
+        st.season[:, p] = st.season[:, p] + g1a * e
+    return st
+
+
+def hw_state_forecast(st: HwState, horizons: torch.Tensor) -> torch.Tensor:
+    """``horizons [C]`` or ``[N, C]`` (>= 1) → ``[N, C]`` forecasts from the state."""
+    h = horizons.to(st.level.device)
+    if h.dim() == 1:
+        h = h[None, :].expand(st.level.shape[0], -1)
+    ph = (st.t_last + h.long()) % st.m
+    return st.level[:, None] + h.float() * st.trend[:, None] + st.season.gather(1, ph)

@@ -760,3 +760,99 @@ def seasonal_decompose(hist: torch.Tensor, head: int, length: int, m: int, want=
     a.phase_means = nat.ptr(out["phase_means"])
     nat.check(lib.fm_seasonal_decompose(C.byref(a), nat.stream_handle(dev)), "fm_seasonal_decompose")
     return out
+
+
+# ---------------------------------------------------------------------------------
+# K3 cached model: Holt-Winters state extraction + O(1) update/detect (hw_state.hip)
+# ---------------------------------------------------------------------------------
+
+class HwStateArgs(C.Structure):
+    _fields_ = [("hist", C.c_void_p), ("ld", C.c_longlong), ("ring_len", C.c_int), ("head", C.c_int),
+                ("T", C.c_int), ("Tp", C.c_int), ("m", C.c_int), ("N", C.c_int), ("bf16", C.c_int),
+                ("_pad0", C.c_int), ("grid", C.c_void_p), ("best", C.c_void_p), ("level", C.c_void_p),
+                ("trend", C.c_void_p), ("season", C.c_void_p), ("nvalid", C.c_void_p)]
+
+
+class HwUpdateArgs(C.Structure):
+    _fields_ = [("hist", C.c_void_p), ("ld", C.c_longlong), ("ring_len", C.c_int), ("col0", C.c_int),
+                ("npts", C.c_int), ("t_last", C.c_int), ("m", C.c_int), ("N", C.c_int), ("bf16", C.c_int),
+                ("_pad0", C.c_int), ("grid", C.c_void_p), ("best", C.c_void_p), ("level", C.c_void_p),
+                ("trend", C.c_void_p), ("season", C.c_void_p), ("sigma", C.c_void_p), ("nvalid", C.c_void_p),
+                ("det", nat.DetectArgs)]
+
+
+nat.register("fm_hw_state", [C.POINTER(HwStateArgs), C.c_void_p])
+nat.register("fm_hw_update_detect", [C.POINTER(HwUpdateArgs), C.c_void_p])
+nat.register("fm_hw_state_args_size", [], C.c_longlong)
+nat.register("fm_hw_update_args_size", [], C.c_longlong)
+
+HW_STATE_MIN_M = 128  # two consecutive 64-step chunks never share a phase (season prefetch)
+
+
+def hw_state(hist: torch.Tensor, head: int, length: int, m: int, grid: torch.Tensor, best: torch.Tensor,
+             state: Optional[Dict[str, torch.Tensor]] = None) -> Dict[str, torch.Tensor]:
+    """Full state of the fitted Holt-Winters model at the end of the window
+    (models/smoothing.py ``hw_run`` with each series' fitted grid point):
+    ``level``/``trend`` ``[N]`` and ``season`` ``[m, N]`` (phase-major, padded-time
+    phase), ``nvalid [N]`` (valid points of the fitted steps) and ``Tp`` (padded
+    length; the last point has padded time Tp - 1)."""
+    lib = nat.require()
+    _hist_check(hist, head, length)
+    dev, N = hist.device, hist.shape[0]
+    _need(m >= HW_STATE_MIN_M, f"cached Holt-Winters needs a season >= {HW_STATE_MIN_M} (got {m})")
+    Tp, pad, _, _ = smoothing_geometry(MODE_HW, length, m)
+    _need(Tp // m >= 2, "holt_winters needs >= 2 seasons")
+    _need(grid.dim() == 2 and grid.shape[1] == 3 and grid.dtype == torch.float32 and grid.is_contiguous()
+          and grid.device == dev, "grid must be contiguous float32 [G, 3] on device")
+    _vec(best, N, torch.int32, "best", dev)
+    state = {} if state is None else state
+    f32 = dict(dtype=torch.float32, device=dev)
+    for k in ("level", "trend", "nvalid"):
+        if k not in state or state[k].shape != (N,):
+            state[k] = torch.empty(N, **f32)
+    if "season" not in state or state["season"].shape != (m, N):
+        state["season"] = torch.empty((m, N), **f32)
+    a = HwStateArgs()
+    a.hist, a.ld, a.ring_len, a.head = nat.ptr(hist), hist.stride(0), hist.shape[1], int(head)
+    a.T, a.Tp, a.m, a.N, a.bf16 = int(length), int(Tp), int(m), N, int(hist.dtype == torch.bfloat16)
+    a.grid, a.best = nat.ptr(grid), nat.ptr(best)
+    a.level, a.trend, a.season = nat.ptr(state["level"]), nat.ptr(state["trend"]), nat.ptr(state["season"])
+    a.nvalid = nat.ptr(state["nvalid"])
+    nat.check(lib.fm_hw_state(C.byref(a), nat.stream_handle(dev)), "fm_hw_state")
+    state["Tp"] = Tp
+    return state
+
+
+def hw_update_detect(hist: torch.Tensor, col0: int, npts: int, t_last: int, m: int, grid: torch.Tensor,
+                     best: torch.Tensor, state: Dict[str, torch.Tensor], sigma: torch.Tensor,
+                     nvalid: torch.Tensor, det: DetectSpec,
+                     out: Optional[Dict[str, torch.Tensor]] = None) -> Dict[str, torch.Tensor]:
+    """Advance the cached state by the ``npts`` points at ring columns ``col0 ..``
+    (mod R), the first at padded time ``t_last + 1``, then forecast the current
+    window and run the band / verdict epilogue with the refit's ``sigma`` /
+    ``nvalid`` / ``best`` (h-step variance of that grid point)."""
+    lib = nat.require()
+    _cuda(hist, "hist")
+    _need(hist.dim() == 2 and hist.stride(1) == 1 and hist.dtype in (torch.float32, torch.bfloat16),
+          "hist must be [N, R] row-contiguous float32/bf16")
+    dev, N, R = hist.device, hist.shape[0], hist.shape[1]
+    _need(0 <= col0 < R and 0 <= npts <= R and t_last >= 0, "col0/npts/t_last out of range")
+    _need(state["season"].shape == (m, N) and state["season"].is_contiguous(), "season must be [m, N]")
+    for k in ("level", "trend"):
+        _vec(state[k], N, torch.float32, k, dev)
+    _vec(best, N, torch.int32, "best", dev)
+    _vec(sigma, N, torch.float32, "sigma", dev)
+    _vec(nvalid, N, torch.float32, "nvalid", dev)
+    _need(grid.dim() == 2 and grid.shape[1] == 3 and grid.dtype == torch.float32 and grid.is_contiguous()
+          and grid.device == dev, "grid must be contiguous float32 [G, 3] on device")
+    out = {} if out is None else out
+    a = HwUpdateArgs()
+    a.hist, a.ld, a.ring_len, a.col0, a.npts = nat.ptr(hist), hist.stride(0), R, int(col0), int(npts)
+    a.t_last, a.m, a.N, a.bf16 = int(t_last), int(m), N, int(hist.dtype == torch.bfloat16)
+    a.grid, a.best = nat.ptr(grid), nat.ptr(best)
+    a.level, a.trend, a.season = nat.ptr(state["level"]), nat.ptr(state["trend"]), nat.ptr(state["season"])
+    a.sigma, a.nvalid = nat.ptr(sigma), nat.ptr(nvalid)
+    _fill_detect(a.det, det, N, dev, out)
+    _set_hvar(a.det, det, grid, MODE_HW, m)
+    nat.check(lib.fm_hw_update_detect(C.byref(a), nat.stream_handle(dev)), "fm_hw_update_detect")
+    return out
