@@ -457,6 +457,9 @@ def setup_lstm(args, world, rank, dev, n_features, fp8):
         "train_batch_per_rank": args.lstm_train_batch,
         "scoring_dtype": "fp8_e4m3" if fp8 else "bf16",
         "training": "fused K7 kernel + hipBLASLt weight-grad GEMMs" if shard.fused_train else "autograd",
+        "entity": ("one (app, caller) pair: the latency + error-rate series of the requests a calling service "
+                   "sends to a deployed app (downstream impact, metricType: downstream)" if F == 2 else
+                   "one univariate metric-series"),
         "train_score_overlap": not args.lstm_no_overlap,
     }
     dt = "bf16"  # training fp32 master / bf16 MFMA scoring (fp8 weights+activations for config 5)

@@ -51,6 +51,8 @@ class MetricTask:
     threshold: float = 2.0
     bound: int = 1
     min_lower: float = 0.0
+    caller: str = ""            # downstream impact: the calling service this series is split by
+    base_alias: str = ""        # the job's metric alias (alias = "<base_alias>[caller=<caller>]")
 
 
 @dataclass

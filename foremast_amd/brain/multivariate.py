@@ -135,13 +135,14 @@ def _ffill(a: np.ndarray) -> np.ndarray:
 class LstmJobScorer:
     def __init__(self, device=None, cache: Optional[ModelCache] = None, hidden: int = 64,
                  train_steps: int = 80, train_batch: int = 256, lr: float = 1e-2, threshold: float = 4.0,
-                 max_age_s: float = 24 * 3600.0, seed: int = 0) -> None:
+                 max_age_s: float = 24 * 3600.0, seed: int = 0, fp8: bool = False) -> None:
         self.device = torch.device(device) if device is not None else (
             torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
         self.gpu = self.device.type == "cuda"
         self.cache = cache if cache is not None else ModelCache()
         self.hidden, self.train_steps, self.train_batch, self.lr = hidden, train_steps, train_batch, lr
         self.threshold, self.max_age_s, self.seed = threshold, max_age_s, seed
+        self.fp8 = fp8  # score with fp8 e4m3 weights/activations on MFMA (GPU)
         self.trained = 0
 
     # ------------------------------------------------------------------ fit
@@ -207,7 +208,7 @@ class LstmJobScorer:
         x = torch.from_numpy(win).to(self.device)
         if self.gpu and m.model.H == 64:
             from ..ops import lstm as L
-            p = L.pack(m.model, fp8=False, device=self.device)
+            p = L.pack(m.model, fp8=self.fp8, device=self.device)
             err = L.lstm_score(p, x.contiguous(), m.mu, m.sigma)["err"]
         else:
             with torch.no_grad():

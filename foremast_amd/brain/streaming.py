@@ -63,6 +63,16 @@ def is_continuous(doc) -> bool:
     return (doc.get("strategy") or "").lower() == STRATEGY_CONTINUOUS
 
 
+CALLER_SPLIT = ("namespace_pod_caller:", "namespace_app_caller:", "namespace_app_caller_per_pod:")
+
+
+def is_streamable(doc) -> bool:
+    """Continuous jobs whose series are one per (namespace, app): the resident
+    GPU shard's keying.  Downstream (per-caller) metrics split an app into one
+    series per caller, so such jobs stay with the batch worker (brain/worker.py)."""
+    return is_continuous(doc) and not any(k[1].startswith(CALLER_SPLIT) for k in series_of(doc).values())
+
+
 def series_of(doc) -> Dict[str, Key]:
     """alias → series key of a job's historical queries."""
     out = {}
@@ -139,7 +149,7 @@ class StreamingMonitor:
         now = self.clock()
 
         def only(d):
-            return is_continuous(d) and (self.owns is None or self.owns(d))
+            return is_streamable(d) and (self.owns is None or self.owns(d))
         docs = self.store.claim(self.worker_id, now=now, max_stuck_s=self.cfg.max_stuck_seconds, limit=10_000,
                                 only=only, steal_from=steal_from)
         for d in docs:

@@ -41,6 +41,9 @@ from ..utils.metrics import BrainMetrics
 from ..utils.timeutil import TimeFormatError, parse_rfc3339
 from .batch import BatchScorer, MetricTask, TaskResult
 
+# recorded per-caller families (deploy/rules.py CALLER_PREFIX)
+CALLER_PREFIXES = ("namespace_pod_caller:", "namespace_app_caller:", "namespace_app_caller_per_pod:")
+
 log = logging.getLogger("foremast.brain")
 
 
@@ -86,6 +89,16 @@ class BrainWorker:
         # strategies another component owns (the streaming monitor takes "continuous")
         self.exclude = {x.lower() for x in exclude_strategies}
         self.lstm = None  # LstmJobScorer, created on first multivariate LSTM job
+        self.downstream = None  # per-caller joint LstmJobScorer (fp8), created on first downstream job
+
+    def _claimable(self, d: Dict[str, Any]) -> bool:
+        """Strategies another component owns are skipped — except continuous jobs
+        the streaming shard cannot hold (per-caller series)."""
+        s = (d.get("strategy") or "").lower()
+        if s not in self.exclude:
+            return True
+        from .streaming import is_streamable
+        return s == "continuous" and not is_streamable(d)
 
     # ------------------------------------------------------------------ planning
     def plan(self, doc: Dict[str, Any]) -> JobPlan:
@@ -112,7 +125,7 @@ class BrainWorker:
     async def cycle(self) -> int:
         t0 = time.perf_counter()
         now = self.clock()
-        only = (lambda d: (d.get("strategy") or "").lower() not in self.exclude) if self.exclude else None
+        only = self._claimable if self.exclude else None
         docs = self.store.claim(self.worker_id, now=now, max_stuck_s=self.cfg.max_stuck_seconds,
                                 limit=self.batch_limit, only=only)
         if not docs:
@@ -137,8 +150,7 @@ class BrainWorker:
             if p.error:
                 continue
             for alias in sorted(p.current):
-                task = self._build_task(i, p, alias, data, fetch_errors)
-                if task is not None:
+                for task in self._build_tasks(i, p, alias, data, fetch_errors):
                     tasks.append(task)
                     owners.append(i)
         results: List[TaskResult] = self.scorer.score(tasks) if tasks else []
@@ -152,7 +164,9 @@ class BrainWorker:
         self.metrics.series_scored.inc(len(tasks))
         return len(docs)
 
-    def _build_task(self, i: int, p: JobPlan, alias: str, data, errors) -> Optional[MetricTask]:
+    def _build_tasks(self, i: int, p: JobPlan, alias: str, data, errors) -> List[MetricTask]:
+        """One task per metric alias — or, for a downstream (per-caller) alias, one
+        per calling service found in the history or the current window."""
         cur = data.get((i, "current", alias))
         hist = data.get((i, "historical", alias))
         base = data.get((i, "baseline", alias))
@@ -161,9 +175,27 @@ class BrainWorker:
             cur = []
         if isinstance(hist, Exception) or hist is None:
             errors.setdefault(i, []).append(f"{alias}: historical fetch failed")
-            return None
+            return []
+        if base is not None and isinstance(base, Exception):
+            base = None
         hurl = p.historical.get(alias, "")
         metric, ns, app = _selector_info(hurl)
+        if not metric.startswith(CALLER_PREFIXES):
+            return [self._task(p, alias, metric, ns, app, hurl, hist, cur or [], base)]
+        callers = sorted({s.labels.get("caller", "") for s in list(hist) + list(cur or [])})
+
+        def of(series, c):
+            return [s for s in series if s.labels.get("caller", "") == c]
+        out = []
+        for c in callers:
+            t = self._task(p, f"{alias}[caller={c}]", metric, ns, app, hurl, of(hist, c), of(cur or [], c),
+                           of(base, c) if base is not None else None)
+            t.caller, t.base_alias = c, alias
+            out.append(t)
+        return out
+
+    def _task(self, p: JobPlan, alias: str, metric: str, ns: str, app: str, hurl: str, hist, cur,
+              base) -> MetricTask:
         start, end, step = _grid(hurl)
         T = int(round((end - start) / step)) + 1
         sums = np.zeros(T)
@@ -175,29 +207,32 @@ class BrainWorker:
             np.add.at(sums, idx[ok], s.values[ok].astype(np.float64))
         h = np.where(cnt > 0, sums / np.maximum(cnt, 1), np.nan).astype(np.float32)
         cts, cvs, tags = [], [], []
-        for s in cur or []:
+        for s in cur:
             cts.append(s.ts)
             cvs.append(s.values)
             tags += [s.labels.get("pod", s.labels.get("app", ""))] * len(s.ts)
         cur_ts = np.concatenate(cts) if cts else np.zeros(0)
         cur_vals = np.concatenate(cvs).astype(np.float32) if cvs else np.zeros(0, dtype=np.float32)
         base_vals = None
-        if base is not None and not isinstance(base, Exception) and base:
+        if base:
             base_vals = np.concatenate([s.values for s in base]).astype(np.float32)
         th = self.cfg.for_metric(alias, metric)
         return MetricTask(job_id=p.doc["id"], alias=alias, metric=metric or alias, namespace=ns, app=app,
                           step=step, hist=h, hist_end=start + (T - 1) * step, cur_ts=cur_ts, cur_vals=cur_vals,
                           cur_tags=tags, base_vals=base_vals, threshold=th.threshold, bound=th.bound,
-                          min_lower=th.min_lower_bound)
+                          min_lower=th.min_lower_bound, base_alias=alias)
 
     def _multivariate(self, plans: List[JobPlan], per_job) -> None:
         """Joint models on top of the per-metric verdicts: ``bivariate_normal``
         (>= 2 metrics, first two aliases), ``lstm`` (>= 2 metrics), or
         ``auto`` = the design doc's dispatch (2 metrics → bivariate normal,
         3+ → LSTM autoencoder; ``docs/guides/design.md:76-84``)."""
+        self._downstream(per_job)
         algo = self.cfg.algorithm
         if algo not in ("bivariate_normal", "lstm", "auto"):
             return
+        # per-caller (downstream) tasks are scored jointly per caller by _downstream
+        per_job = {i: [(t, r_) for t, r_ in items if not t.caller] for i, items in per_job.items()}
         lstm_jobs = [i for i, items in per_job.items()
                      if (algo == "lstm" and len(items) >= 2) or (algo == "auto" and len(items) >= 3)]
         if lstm_jobs:
@@ -218,6 +253,44 @@ class BrainWorker:
                 ra.anomalies = [(float(ta.cur_ts[j]), float(ta.cur_vals[j]),
                                  ta.cur_tags[j] if j < len(ta.cur_tags) else "") for j in idx]
                 ra.model = rb.model = "bivariate_normal"
+
+    def _downstream(self, per_job) -> None:
+        """Downstream impact: for every caller of the deployed app with >= 2
+        monitored metrics (e.g. latency + error rate), the caller's metrics are
+        scored JOINTLY by an LSTM autoencoder (fp8 e4m3 MFMA scoring on the GPU),
+        keyed per (namespace, app, caller) in the model cache; a joint anomaly
+        marks each of the caller's metrics anomalous at the flagged timestamps.
+        ``ML_DOWNSTREAM_ALGORITHM=none`` keeps only the per-metric verdicts."""
+        if self.cfg.downstream_algorithm == "none":
+            return
+        from .multivariate import LstmJobScorer, ModelCache, align_job
+        for i, items in per_job.items():
+            by_caller: Dict[str, List[Tuple[MetricTask, TaskResult]]] = {}
+            for t, res in items:
+                if t.caller:
+                    by_caller.setdefault(t.caller, []).append((t, res))
+            for caller, group in sorted(by_caller.items()):
+                group = sorted(group, key=lambda tr: tr[0].base_alias)
+                if len(group) < 2:
+                    continue
+                tasks = [t for t, _ in group]
+                hist, cts, cur = align_job(tasks)
+                if not len(cts):
+                    continue
+                if self.downstream is None:
+                    self.downstream = LstmJobScorer(device=self.scorer.device,
+                                                    cache=ModelCache(self.cfg.max_cache_size),
+                                                    threshold=self.cfg.lstm_threshold, fp8=True)
+                key = self.downstream.cache.key(tasks[0].namespace, tasks[0].app + "@" + caller,
+                                                [t.base_alias for t in tasks])
+                verdict, bad, _z = self.downstream.score_job(key, hist, cts, cur, now=self.clock())
+                for f, (t, res) in enumerate(group):
+                    if verdict == 1:
+                        res.verdict = 1
+                        seen = {(ts, tag) for ts, _, tag in res.anomalies}
+                        res.anomalies = res.anomalies + [(float(cts[j]), float(cur[j, f]), "joint")
+                                                         for j in bad if (float(cts[j]), "joint") not in seen]
+                        res.model = (res.model + "+lstm_fp8") if "lstm" not in res.model else res.model
 
     def _score_lstm(self, per_job, jobs: List[int]) -> None:
         from .multivariate import LstmJobScorer, ModelCache, align_job
@@ -253,7 +326,10 @@ class BrainWorker:
                 vals: List[float] = []
                 for ts, v, _ in sorted(res.anomalies):
                     vals += [ts, v]
-                tags = ",".join(sorted({tag for _, _, tag in res.anomalies if tag}))
+                tags = sorted({tag for _, _, tag in res.anomalies if tag})
+                if t.caller:  # downstream impact: name the calling service
+                    tags = [f"caller={t.caller}"] + [x for x in tags if x != "joint"]
+                tags = ",".join(tags)
                 anomaly[t.alias] = {"tags": tags, "values": vals}
         if anomaly:
             self._write(doc_id, r.ST_COMPLETED_UNHEALTH,

@@ -10,6 +10,12 @@ with identical PromQL strings and time windows:
 * baseline = ``[floor((now-W min)/60)*60, nowUnix]`` over the old pods
   (only when there are old pods and the strategy is not rollingUpdate);
 * historical = 7 days of ``namespace_app_per_pod:<m>``.
+
+Extension — downstream impact (reference ``README.md:24``): a monitoring entry
+with ``metricType: downstream`` reads the per-caller recordings instead
+(``namespace_pod_caller:<m>`` / ``namespace_app_caller_per_pod:<m>``, one series
+per calling service, ``deploy/rules.py``); the brain scores every caller of the
+deployed app separately and names the impacted one in the verdict.
 """
 
 from __future__ import annotations
@@ -22,21 +28,22 @@ from ..api import rest as r
 
 STEP = 60
 HISTORICAL_DAYS = 7
+METRIC_TYPE_DOWNSTREAM = "downstream"
 
 
 class QueryError(ValueError):
     pass
 
 
-def _pod_selector(namespace: str, metric: str, pods: Sequence[str]) -> str:
+def _pod_selector(namespace: str, metric: str, pods: Sequence[str], prefix: str = "namespace_pod:") -> str:
     if len(pods) > 1:
-        return ('namespace_pod:' + metric + '{namespace="' + namespace + '",pod=~"'
+        return (prefix + metric + '{namespace="' + namespace + '",pod=~"'
                 + "|".join(pods) + '"}')
-    return 'namespace_pod:' + metric + '{namespace="' + namespace + '",pod="' + pods[0] + '"}'
+    return prefix + metric + '{namespace="' + namespace + '",pod="' + pods[0] + '"}'
 
 
-def _app_selector(namespace: str, metric: str, app: str) -> str:
-    return 'namespace_app_per_pod:' + metric + '{namespace="' + namespace + '",app="' + app + '"}'
+def _app_selector(namespace: str, metric: str, app: str, prefix: str = "namespace_app_per_pod:") -> str:
+    return prefix + metric + '{namespace="' + namespace + '",app="' + app + '"}'
 
 
 def create_map(namespace: str, app_name: str, pod_names: Sequence[str], metrics: crd.Metrics,
@@ -45,6 +52,9 @@ def create_map(namespace: str, app_name: str, pod_names: Sequence[str], metrics:
     now = time.time() if now is None else now
     out: Dict[str, r.MetricQuery] = {}
     for mon in metrics.monitoring:
+        down = (mon.metric_type or "").lower() == METRIC_TYPE_DOWNSTREAM
+        pod_pfx = "namespace_pod_caller:" if down else "namespace_pod:"
+        app_pfx = "namespace_app_caller_per_pod:" if down else "namespace_app_per_pod:"
         now_unix = (int(now) // STEP) * STEP
         before = (int(now - time_window_min * 60) // STEP) * STEP
         p: Dict[str, object] = {"endpoint": metrics.endpoint, "step": STEP}
@@ -52,22 +62,22 @@ def create_map(namespace: str, app_name: str, pod_names: Sequence[str], metrics:
             p["start"] = now_unix + STEP
             p["end"] = (int(now + (time_window_min + 1) * 60) // STEP) * STEP
             if strategy == r.STRATEGY_CONTINUOUS:
-                p["query"] = _app_selector(namespace, mon.metric_name, app_name)
+                p["query"] = _app_selector(namespace, mon.metric_name, app_name, app_pfx)
             else:
                 if not pod_names:
                     raise QueryError("No valid pod names")
-                p["query"] = _pod_selector(namespace, mon.metric_name, pod_names)
+                p["query"] = _pod_selector(namespace, mon.metric_name, pod_names, pod_pfx)
         elif category == r.CATEGORY_BASELINE:
             if not pod_names:
                 raise QueryError("No valid pod names")
             p["start"] = before
             p["end"] = now_unix
-            p["query"] = _pod_selector(namespace, mon.metric_name, pod_names)
+            p["query"] = _pod_selector(namespace, mon.metric_name, pod_names, pod_pfx)
         elif category == r.CATEGORY_HISTORICAL:
             t = now - HISTORICAL_DAYS * 24 * 3600
             p["start"] = (int(t) // STEP) * STEP
             p["end"] = now_unix
-            p["query"] = _app_selector(namespace, mon.metric_name, app_name)
+            p["query"] = _app_selector(namespace, mon.metric_name, app_name, app_pfx)
         out[mon.metric_alias] = r.MetricQuery(data_source_type=metrics.data_source_type,
                                               parameters=p)
     return out

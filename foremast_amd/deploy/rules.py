@@ -34,6 +34,14 @@ RESOURCE_FAMILIES: Dict[str, str] = {
     "memory_usage_bytes": 'container_memory_usage_bytes{job="kubelet", image!="", container!=""}',
 }
 
+# Downstream impact (reference README.md:24, CallerWebMvcTagsProvider.java:22-25): the
+# metrics starter tags every request with the calling service (``caller``, from the
+# X-CALLER header), so each HTTP family is also recorded per caller — the query builder
+# reads these for ``metricType: downstream`` and the brain scores each caller of the
+# deployed app (controller/queries.py, brain/worker.py).
+CALLER_PREFIX = {"pod": "namespace_pod_caller:", "app": "namespace_app_caller:",
+                 "app_per_pod": "namespace_app_caller_per_pod:"}
+
 POD_COUNT = "namespace_app:pod_count"
 APP_LABEL = 'label_replace({inner}, "app", "$1", "label_app", "(.*)")'
 
@@ -62,6 +70,12 @@ def rules() -> List[Dict[str, str]]:
         # apps expose the `app` tag themselves (metrics starter, C27)
         out.append({"record": f"namespace_app:{fam}", "expr": _http_expr(sel, kind, "namespace, app")})
         out.append({"record": f"namespace_app_per_pod:{fam}", "expr": f"namespace_app:{fam} / on (namespace, app) {POD_COUNT}"})
+    for fam, (sel, kind) in HTTP_FAMILIES.items():
+        cp = CALLER_PREFIX
+        out.append({"record": cp["pod"] + fam, "expr": _http_expr(sel, kind, "namespace, pod, caller")})
+        out.append({"record": cp["app"] + fam, "expr": _http_expr(sel, kind, "namespace, app, caller")})
+        out.append({"record": cp["app_per_pod"] + fam,
+                    "expr": f"{cp['app']}{fam} / on (namespace, app) group_left {POD_COUNT}"})
     for fam, inner in RESOURCE_FAMILIES.items():
         by_pod = f"sum by (namespace, pod) ({inner})"
         out.append({"record": f"namespace_pod:{fam}", "expr": by_pod})
