@@ -117,9 +117,11 @@ class BatchScorer:
             m = self._season_points(t.step)
             if algo == "holt_winters" and np.count_nonzero(~np.isnan(t.hist)) and len(t.hist) < 2 * m:
                 algo = "double_exponential_smoothing"
+            if algo == "seasonal_decompose" and len(t.hist) < 2 * m + 1:
+                algo = "moving_average_all"  # needs more than two seasons of history
             if algo in ("bivariate_normal", "lstm", "auto"):
                 algo = "moving_average_all"  # per-metric part; the joint model runs in the worker
-            groups.setdefault((algo, m if algo == "holt_winters" else 0), []).append(i)
+            groups.setdefault((algo, m if algo in ("holt_winters", "seasonal_decompose") else 0), []).append(i)
         for (algo, m), idx in groups.items():
             sub = [tasks[i] for i in idx]
             for i, r in zip(idx, self._score_group(sub, algo, m)):
@@ -189,7 +191,9 @@ class BatchScorer:
                                 max_horizon=int(hz.max()) if hz.size and hz.min() >= 1 else None,
                                 horizon_variance=cfg.horizon_variance, **dkw)
             T = t_hist.shape[1]
-            if mode is not None:
+            if algo == "seasonal_decompose":
+                out = K.decompose_score(t_hist, 0, T, m, spec)
+            elif mode is not None:
                 g = sm_ref.make_grid(mode, cfg.hw_alpha, cfg.hw_beta, cfg.hw_gamma).to(dev)
                 out = K.smoothing_fit(t_hist, 0, T, mode, m if mode == sm_ref.MODE_HW else 1, g, spec)
             else:
@@ -202,7 +206,12 @@ class BatchScorer:
             verdict = out["verdict"]
             anom = None
         else:
-            if mode is not None:
+            if algo == "seasonal_decompose":
+                from ..models import decompose as dec_ref
+                fc = dec_ref.decompose_forecast(t_hist, m)
+                f = dec_ref.forecast_decomposition(fc, t_hz)
+                sigma, n_valid = fc.sigma, fc.n_valid
+            elif mode is not None:
                 grid = sm_ref.make_grid(mode, cfg.hw_alpha, cfg.hw_beta, cfg.hw_gamma)
                 fit = sm_ref.fit_smoothing(t_hist, mode, grid, m=max(m, 1))
                 f = sm_ref.forecast(fit, t_hz)

@@ -385,6 +385,8 @@ class StreamingShard:
                 head = (h.head + length - cfg.ma_window) % h.R
                 length = cfg.ma_window
             self.out = K.window_stats(h.data, head, length, spec, out=self.out)
+        elif self.algorithm == "seasonal_decompose":
+            self.out = K.decompose_score(h.data, h.head, h.length, self.spec.season, spec, out=self.out)
         else:
             raise ValueError(f"algorithm {self.algorithm!r} is not a streaming univariate scorer")
         return self.out
@@ -415,6 +417,12 @@ class StreamingShard:
             sigma = c["sigma"]
             if cfg.horizon_variance:
                 sigma = c["sigma"][:, None] * det_ref.horizon_sigma_factor(params, self.mode, self.spec.season, h)
+        elif self.algorithm == "seasonal_decompose":
+            from ..models import decompose as dec_ref
+            fc = dec_ref.decompose_forecast(y, self.spec.season)
+            f = dec_ref.forecast_decomposition(fc, h)
+            sigma, n_valid = fc.sigma, fc.n_valid
+            extra = {"level": fc.level, "slope": fc.slope, "sigma": fc.sigma}
         elif self.mode is not None:
             fit = sm_ref.fit_smoothing(y, self.mode, self.grid.cpu(), m=self.spec.season)
             f = sm_ref.forecast(fit, h)

@@ -188,9 +188,12 @@ class StreamingMonitor:
         season = max(2, int(round(86400.0 / self.step)))
         algo = self.cfg.algorithm if self.cfg.algorithm in ("holt_winters", "exponential_smoothing",
                                                             "double_exponential_smoothing", "moving_average",
-                                                            "moving_average_all") else "moving_average_all"
+                                                            "moving_average_all", "seasonal_decompose") \
+            else "moving_average_all"
         if algo == "holt_winters" and self.R < 2 * season:
             algo = "double_exponential_smoothing"
+        if algo == "seasonal_decompose" and self.R < 2 * season + 1:
+            algo = "moving_average_all"
         dev = self.device
         spec = ShardSpec(n_series=capacity, ring_len=self.R, season=season, pods=1, window=self.W, algorithm=algo,
                          pairwise="NONE", dtype=torch.bfloat16 if dev.type == "cuda" else torch.float32,

@@ -12,8 +12,11 @@ implements), made NaN-aware for scraped metrics with gaps:
   defined, centred so the m phase means sum to zero, tiled over time;
 * resid: ``y - trend - seasonal``.
 
-Used for Holt-Winters seasonal initialisation, and exposed for dashboards
-("seasonality decomposition" in BASELINE.json).
+Scoring (``ML_ALGORITHM=seasonal_decompose``, :func:`decompose_forecast`): the
+forecast continues the trend from its last defined value ``t_e = T-1-m//2`` with
+the slope over the last season of trend, plus the phase mean; sigma is the RMS
+of the residuals.  The K4 kernel's scoring mode (``ops.decompose_score``) fuses
+this with the band / verdict epilogue.
 """
 
 from __future__ import annotations
@@ -67,3 +70,44 @@ def seasonal_decompose(y: torch.Tensor, m: int) -> Decomposition:
     resid = yd - trend - seasonal
     f = y.dtype if y.dtype.is_floating_point and y.dtype != torch.bfloat16 else torch.float32
     return Decomposition(trend.to(f), seasonal.to(f), resid.to(f), pm.to(f))
+
+
+@dataclass
+class DecompForecast:
+    level: torch.Tensor    # [N] trend at t_e (series mean when undefined)
+    slope: torch.Tensor    # [N] per step
+    t_e: int
+    sigma: torch.Tensor    # [N] residual RMS
+    n_valid: torch.Tensor  # [N]
+    phase_means: torch.Tensor
+    T: int
+    m: int
+
+
+def decompose_forecast(y: torch.Tensor, m: int) -> DecompForecast:
+    """Forecast model of the seasonal-decomposition scorer over ``y [N, T]``."""
+    N, T = y.shape
+    d = seasonal_decompose(y, m)
+    te = T - 1 - m // 2
+    tr = d.trend.double()
+    tr_e = tr[:, te]
+    tr_p = tr[:, te - m] if te - m >= 0 else torch.full_like(tr_e, float("nan"))
+    yd = y.double()
+    ok = ~torch.isnan(yd)
+    ybar = torch.where(ok, yd, torch.zeros_like(yd)).sum(1) / ok.sum(1).clamp(min=1)
+    level = torch.where(torch.isnan(tr_e), ybar, tr_e)
+    slope = torch.where(torch.isnan(tr_e) | torch.isnan(tr_p), torch.zeros_like(tr_e), (tr_e - tr_p) / m)
+    r = d.resid.double()
+    rok = ~torch.isnan(r)
+    sigma = torch.sqrt(torch.where(rok, r * r, torch.zeros_like(r)).sum(1) / rok.sum(1).clamp(min=1))
+    return DecompForecast(level=level.float(), slope=slope.float(), t_e=te, sigma=sigma.float(),
+                          n_valid=ok.sum(1).float(), phase_means=d.phase_means.float(), T=T, m=m)
+
+
+def forecast_decomposition(fc: DecompForecast, horizons: torch.Tensor) -> torch.Tensor:
+    """``horizons [C]`` or ``[N, C]`` (>= 1) → ``[N, C]``."""
+    h = horizons.to(fc.level.device).long()
+    if h.dim() == 1:
+        h = h[None, :].expand(fc.level.shape[0], -1)
+    t = fc.T - 1 + h
+    return fc.level[:, None] + fc.slope[:, None] * (t - fc.t_e).float() + fc.phase_means.gather(1, t % fc.m)

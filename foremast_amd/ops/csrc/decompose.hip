@@ -18,7 +18,15 @@
 //  4. one coalesced output pass: seasonal = phase_mean[t mod m], resid (the
 //     trend is stored in pass 2).  LDS: 6 (T+1) + 4 m bytes (66 KiB at T = 10080, m = 1440), so
 //     two workgroups share a CU.
+//
+// Scoring mode (det.C > 0, the ML_ALGORITHM=seasonal_decompose scorer): the residual RMS
+// is reduced in pass 4 and the forecast f(h) = trend_e + slope (T - 1 + h - t_e) +
+// seasonal[(T - 1 + h) mod m] (t_e: the last sample with a centred-MA trend, slope over
+// the last season of trend) runs through the shared band / verdict epilogue (detect.h);
+// with the full outputs null, a series costs one HBM read and no [N, T] writes.
 #include "common.h"
+#include "args.h"
+#include "detect.h"
 
 struct DecompArgs {
   const void* hist;   // [N, ld] ring (bf16 or fp32)
@@ -33,6 +41,12 @@ struct DecompArgs {
   float* seasonal;    // [N, T] or null
   float* resid;       // [N, T] or null
   float* phase_means; // [N, m] or null
+  // scoring mode (det.C > 0): forecast parameters, residual RMS, valid count
+  float* fc_level;    // [N] trend at t_e (NaN: no trend defined) or null
+  float* fc_slope;    // [N] trend slope per step or null
+  float* sigma;       // [N] residual RMS or null
+  float* nvalid;      // [N] valid samples or null
+  DetectArgs det;
 };
 
 extern __shared__ __attribute__((aligned(16))) char fm_dec_smem[];
@@ -169,6 +183,10 @@ __global__ __launch_bounds__(BLOCK) void decompose_kernel(const DecompArgs a) {
     tr_r[k] = t < T ? trend_at(t) : 0.f;
     if (t < T && a.trend) a.trend[base + t] = tr_r[k];
   }
+  // scoring mode: the last defined trend and the one a season earlier (every thread, from
+  // the prefix sums, before they are overwritten)
+  const int te = T - 1 - h;
+  const float tr_e = trend_at(te), tr_p = te - m >= 0 ? trend_at(te - m) : fm_nan();
   __syncthreads();
   float* D = S;
 #pragma unroll
@@ -197,9 +215,10 @@ __global__ __launch_bounds__(BLOCK) void decompose_kernel(const DecompArgs a) {
   }
   __syncthreads();
 
-  // 4. outputs (coalesced)
+  // 4. outputs (coalesced) and the residual sum of squares
   const int pstep = BLOCK % m;  // phase of t = tid + k*BLOCK, advanced without an integer division per sample
   int ph = tid % m;
+  float r2 = 0.f, rc = 0.f;
 #pragma unroll
   for (int k = 0; k < MAX_ITEMS; ++k) {
     const int t = tid + k * BLOCK;
@@ -209,10 +228,30 @@ __global__ __launch_bounds__(BLOCK) void decompose_kernel(const DecompArgs a) {
     }
     if (t < T) {
       const float se = pm[ph];
+      const float r = D[t] - se;
       if (a.seasonal) a.seasonal[base + t] = se;
-      if (a.resid) a.resid[base + t] = D[t] - se;
+      if (a.resid) a.resid[base + t] = r;
+      if (r == r) { r2 += r * r; rc += 1.f; }
     }
   }
+  if (a.det.C <= 0 && !a.sigma) return;
+
+  // 5. scoring: trend extrapolated from its last defined value over the last season
+  const float rss = block_sum(r2, red), rcnt = block_sum(rc, red);
+  const float sig = sqrtf(rss / fmaxf(rcnt, 1.f));
+  const float lvl = tr_e == tr_e ? tr_e : ybar;
+  const float slope = (tr_e == tr_e && tr_p == tr_p) ? (tr_e - tr_p) / (float)m : 0.f;
+  if (tid == 0) {
+    if (a.fc_level) a.fc_level[n] = lvl;
+    if (a.fc_slope) a.fc_slope[n] = slope;
+    if (a.sigma) a.sigma[n] = sig;
+    if (a.nvalid) a.nvalid[n] = csum;
+  }
+  const int tlast = T - 1;
+  detect_epilogue(a.det, n, sig, csum, [&](int hz) {
+    const int p = (tlast + hz) % m;
+    return lvl + slope * (float)(tlast + hz - te) + pm[p < 0 ? p + m : p];
+  }, red);
 }
 
 }  // namespace

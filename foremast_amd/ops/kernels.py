@@ -725,7 +725,8 @@ class DecompArgs(C.Structure):
     _fields_ = [("hist", C.c_void_p), ("ld", C.c_longlong), ("ring_len", C.c_int), ("head", C.c_int),
                 ("T", C.c_int), ("N", C.c_int), ("m", C.c_int), ("bf16", C.c_int),
                 ("trend", C.c_void_p), ("seasonal", C.c_void_p), ("resid", C.c_void_p),
-                ("phase_means", C.c_void_p)]
+                ("phase_means", C.c_void_p), ("fc_level", C.c_void_p), ("fc_slope", C.c_void_p),
+                ("sigma", C.c_void_p), ("nvalid", C.c_void_p), ("det", nat.DetectArgs)]
 
 
 nat.register("fm_seasonal_decompose", [C.POINTER(DecompArgs), C.c_void_p])
@@ -758,6 +759,36 @@ def seasonal_decompose(hist: torch.Tensor, head: int, length: int, m: int, want=
     a.seasonal = nat.ptr(out.get("seasonal"))
     a.resid = nat.ptr(out.get("resid"))
     a.phase_means = nat.ptr(out["phase_means"])
+    nat.check(lib.fm_seasonal_decompose(C.byref(a), nat.stream_handle(dev)), "fm_seasonal_decompose")
+    return out
+
+
+def decompose_score(hist: torch.Tensor, head: int, length: int, m: int, det: DetectSpec,
+                    out: Optional[Dict[str, torch.Tensor]] = None) -> Dict[str, torch.Tensor]:
+    """Seasonal-decomposition scorer (``ML_ALGORITHM=seasonal_decompose``): K4 over
+    the ring window without the ``[N, T]`` outputs, forecast = extrapolated trend +
+    phase mean, sigma = residual RMS, then the fused band / verdict epilogue
+    (models/decompose.py ``decompose_forecast``)."""
+    lib = nat.require()
+    _hist_check(hist, head, length)
+    _need(2 <= m and 2 * m + 1 <= length, f"period {m} needs more than two seasons of history")
+    _need(lib.fm_decompose_lds_bytes(length, m) <= LDS_MAX_WG, "window too long for the decomposition kernel")
+    N, dev = hist.shape[0], hist.device
+    out = {} if out is None else out
+    f32 = dict(dtype=torch.float32, device=dev)
+    for k in ("level", "slope", "sigma", "nvalid"):
+        if k not in out:
+            out[k] = torch.empty(N, **f32)
+    if "phase_means" not in out:
+        out["phase_means"] = torch.empty((N, m), **f32)
+    a = DecompArgs()
+    a.hist, a.ld, a.ring_len, a.head, a.T, a.N, a.m = nat.ptr(hist), hist.stride(0), hist.shape[1], int(head), \
+        int(length), N, int(m)
+    a.bf16 = int(hist.dtype == torch.bfloat16)
+    a.phase_means = nat.ptr(out["phase_means"])
+    a.fc_level, a.fc_slope = nat.ptr(out["level"]), nat.ptr(out["slope"])
+    a.sigma, a.nvalid = nat.ptr(out["sigma"]), nat.ptr(out["nvalid"])
+    _fill_detect(a.det, det, N, dev, out)
     nat.check(lib.fm_seasonal_decompose(C.byref(a), nat.stream_handle(dev)), "fm_seasonal_decompose")
     return out
 

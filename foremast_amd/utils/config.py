@@ -31,7 +31,7 @@ BOUND_BOTH = 3
 
 ALGORITHMS = (
     "moving_average", "moving_average_all", "exponential_smoothing",
-    "double_exponential_smoothing", "holt_winters", "prophet",
+    "double_exponential_smoothing", "holt_winters", "prophet", "seasonal_decompose",
     "bivariate_normal", "lstm",
 )
 

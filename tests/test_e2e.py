@@ -116,11 +116,12 @@ async def _drive_rollout(world):
 
 
 @pytest.mark.parametrize("algorithm,device", [
-    ("moving_average_all", "cpu"), ("holt_winters", "cpu"), ("prophet", "cpu"),
+    ("moving_average_all", "cpu"), ("holt_winters", "cpu"), ("prophet", "cpu"), ("seasonal_decompose", "cpu"),
     # the same scenario through the HIP kernels (rank tests, window stats / HW scan, fused epilogue)
     pytest.param("moving_average_all", "cuda", marks=pytest.mark.gpu),
     pytest.param("holt_winters", "cuda", marks=pytest.mark.gpu),
     pytest.param("prophet", "cuda", marks=pytest.mark.gpu),
+    pytest.param("seasonal_decompose", "cuda", marks=pytest.mark.gpu),
 ])
 def test_rollout_spike_rolls_back(algorithm, device):
     world = build_world(algorithm, device=device)

@@ -304,6 +304,40 @@ def test_seasonal_decompose_kernel_matches_reference(K, dtype, m, T):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dtype,m,T", [(torch.float32, 24, 24 * 9 + 5), (torch.float32, 25, 25 * 6),
+                                       (torch.bfloat16, 1440, 10080)])
+def test_decompose_scorer_matches_reference(K, dtype, m, T):
+    """ML_ALGORITHM=seasonal_decompose: K4's scoring mode (no [N, T] outputs) —
+    trend extrapolation, phase means, residual RMS, band and verdicts — against
+    models/decompose.py decompose_forecast + models/detect.py."""
+    from foremast_amd.models import decompose as dec
+    from foremast_amd.brain.engine import synthetic_history
+    dev = torch.device("cuda:0")
+    N, R, C = 64, T + 37, 20
+    y = synthetic_history(N, T + C, m, dev, seed=6)
+    y[3, 100:140] = float("nan")
+    ring = torch.full((N, R), float("nan"), device=dev, dtype=dtype)
+    head = 29
+    cols = (head + torch.arange(T, device=dev)) % R
+    ring[:, cols] = y[:, :T].to(dtype)
+    cur = y[:, T:].float().contiguous()
+    cur[::5, 7] *= 1.5
+    spec = _det_spec(K, N, C, dev, cur=cur, thr=3.0)
+    out = K.decompose_score(ring, head, T, m, spec)
+    torch.cuda.synchronize()
+    fc = dec.decompose_forecast(ring[:, cols].float().cpu(), m)
+    scale = float(torch.nan_to_num(y.float()).abs().max())
+    f_ref = dec.forecast_decomposition(fc, torch.arange(1, C + 1))
+    assert float((out["forecast"].cpu() - f_ref).abs().max()) < 5e-4 * scale
+    torch.testing.assert_close(out["sigma"].cpu(), fc.sigma, rtol=2e-3, atol=1e-4 * scale)
+    assert torch.equal(out["nvalid"].cpu(), fc.n_valid)
+    d = det_ref.detect(out["forecast"].cpu(), out["sigma"].cpu(), cur.cpu(), torch.full((N,), 3.0),
+                       torch.full((N,), 3, dtype=torch.int8), torch.full((N,), -1e30))
+    assert torch.equal(d.verdict, out["verdict"].cpu()) and torch.equal(d.count, out["count"].cpu())
+    assert int((out["verdict"] == 1).sum()) >= N // 5 - 2
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("which", ["window_stats", "holt_winters"])
 def test_anomaly_compaction_matches_band_flags(K, which):
     """K9: the compacted (series, col, value) list equals the points outside

@@ -288,3 +288,17 @@ def test_pairwise_lowered_band_needs_min_points():
     d1 = detect.detect(f, sig, x, thr, torch.full((4,), 3, dtype=torch.int8), torch.full((4,), -1e9),
                        differs=differs, threshold_low=low, pw_min_points=1)
     assert d1.verdict.tolist() == [1, 1, 1, 0]
+
+
+def test_decompose_forecast_continues_trend_and_season():
+    """Decomposition scorer reference: on a noiseless linear trend + sinusoid the
+    forecast matches the generating function and the residual RMS is ~0."""
+    import math
+    from foremast_amd.models import decompose as dec
+    m, T = 24, 24 * 6
+    t = torch.arange(T + 10, dtype=torch.float64)
+    y = (5.0 + 0.01 * t + torch.sin(2 * math.pi * t / m)).float()[None].repeat(3, 1)
+    fc = dec.decompose_forecast(y[:, :T], m)
+    f = dec.forecast_decomposition(fc, torch.arange(1, 11))
+    torch.testing.assert_close(f, y[:, T:], rtol=0, atol=2e-3)
+    assert float(fc.sigma.max()) < 1e-3 and int(fc.n_valid[0]) == T
