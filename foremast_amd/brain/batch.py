@@ -51,8 +51,9 @@ class MetricTask:
     threshold: float = 2.0
     bound: int = 1
     min_lower: float = 0.0
-    caller: str = ""            # downstream impact: the calling service this series is split by
-    base_alias: str = ""        # the job's metric alias (alias = "<base_alias>[caller=<caller>]")
+    caller: str = ""            # split value: the calling service (downstream) or request path (api)
+    base_alias: str = ""        # the job's metric alias (alias = "<base_alias>[<split_label>=<caller>]")
+    split_label: str = ""       # "caller" | "uri" | "" (not split)
 
 
 @dataclass

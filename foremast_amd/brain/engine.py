@@ -97,8 +97,10 @@ class StreamingShard:
         self.grid = g.to(self.device)
         C = P * W
         self.horizons = torch.tensor(self.cur.horizons(), dtype=torch.int32, device=self.device)
-        if self.gpu:
-            self._h_pinned = torch.empty(C, dtype=torch.int32).pin_memory()
+        self._h_slots = None  # pinned horizon rows per window slot (see _refresh_horizons)
+        self._h_dev = None    # the same rows on the device: eager ticks point at a row, no copy
+        self._h_buf = self.horizons
+        self._stats_zeroed = False
         self.out: Dict[str, torch.Tensor] = {}
         self._verdict_out = verdict_out
         if verdict_out is not None:
@@ -114,7 +116,10 @@ class StreamingShard:
         self._side = None                # side HIP stream for the rank tests (overlap_pairwise)
         self.overlap_pairwise = self.gpu
         if self.gpu:
-            self._state_host = torch.zeros(8, dtype=torch.int32).pin_memory()
+            # graph-tick ring state: a ring of pinned sources, so a copy still in flight
+            # (pipelined ticks, at most two ahead) never sees the next tick's values
+            self._state_ring = torch.zeros((4, 8), dtype=torch.int32).pin_memory()
+            self._state_k = 0
             self._state_dev = torch.zeros(8, dtype=torch.int32, device=self.device)
         # cached Holt-Winters model (refit_every > 1): state after the last refit / update
         self.refit_every = max(1, int(spec.refit_every))
@@ -169,11 +174,32 @@ class StreamingShard:
     def set_baseline(self, values: torch.Tensor) -> None:
         self.base.copy_(values.to(self.device, torch.float32))
 
-    def _refresh_horizons(self) -> None:
+    def _refresh_horizons(self, stable: bool = False) -> None:
         h = self.cur.horizons()
         if self.gpu:
-            self._h_pinned.copy_(torch.from_numpy(h))
-            self.horizons.copy_(self._h_pinned, non_blocking=True)
+            # The H2D copy runs when the stream reaches it, possibly after the host has moved
+            # on to the next tick (pipelined ticks): its pinned source must not be rewritten
+            # with other values while in flight.  Once the window is full the horizons only
+            # depend on the slot, so each slot has its own pinned source (same bytes every
+            # time); warm-up ticks copy from a fresh pinned buffer.
+            # Eager ticks (not `stable`) in that steady state point `horizons` at the slot's
+            # row of a device table instead: no per-tick copy at all.  A HIP-graph tick
+            # (`stable`) needs the one buffer its capture baked in.
+            W = self.cur.W
+            if self.cur.ticks >= W:
+                if self._h_slots is None:
+                    self._h_slots = torch.empty((W, h.shape[0]), dtype=torch.int32).pin_memory()
+                    for s in range(W):
+                        self._h_slots[s].copy_(torch.from_numpy(self.cur.horizons(W + s)))
+                    self._h_dev = self._h_slots.to(self.device)
+                if not stable:
+                    self.horizons = self._h_dev[self.cur.ticks % W]
+                    return
+                src = self._h_slots[self.cur.ticks % W]
+            else:
+                src = torch.from_numpy(h).pin_memory()
+            self._h_buf.copy_(src, non_blocking=True)
+            self.horizons = self._h_buf
         else:
             self.horizons.copy_(torch.from_numpy(h))
 
@@ -189,7 +215,9 @@ class StreamingShard:
             from ..ops import kernels as K
             K.tick_ingest(self.hist.data, self.hist.next_col(), self.cur.data, self.cur.P, self.cur.W,
                           self.cur.slot(), newv, graduate=graduate,
-                          base=self.base if newb is not None else None, newb=newb)
+                          base=self.base if newb is not None else None, newb=newb,
+                          zero=self.app_stats.view(-1))
+            self._stats_zeroed = True  # the tick's per-app counters were cleared by the same launch
             self.cur.ticks += 1
         else:
             old_b = None
@@ -241,7 +269,8 @@ class StreamingShard:
         io = (newv.data_ptr(), None if newb is None else newb.data_ptr())
         if self._graph is not None and io != self._graph_io:
             raise ValueError("tick_graph needs the same newv/newb buffers on every call")
-        st = self._state_host
+        st = self._state_ring[self._state_k % 4]
+        self._state_k += 1
         st[0] = self.hist.next_col()
         st[1] = self.cur.slot()
         st[2] = 1
@@ -249,13 +278,13 @@ class StreamingShard:
         self.cur.ticks += 1
         st[3] = self.hist.head
         self._state_dev.copy_(st, non_blocking=True)
-        self._refresh_horizons()
+        self._refresh_horizons(stable=True)
         if self._graph is None:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 K.tick_ingest(self.hist.data, 0, self.cur.data, self.cur.P, self.cur.W, 0, newv,
-                              base=self.base if newb is not None else None, newb=newb, state=self._state_dev)
-                self.app_stats.zero_()
+                              base=self.base if newb is not None else None, newb=newb, state=self._state_dev,
+                              zero=self.app_stats.view(-1))
                 self._score_gpu(head_dev=self._state_dev[3:4])
             self._graph, self._graph_io = g, io
         self._graph.replay()
@@ -263,7 +292,9 @@ class StreamingShard:
 
     # ------------------------------------------------------------------ scoring
     def score(self) -> Dict[str, torch.Tensor]:
-        self.app_stats.zero_()
+        if not self._stats_zeroed:
+            self.app_stats.zero_()
+        self._stats_zeroed = False
         cached = self._use_cache()
         self.last_refit = not cached
         if self.gpu:

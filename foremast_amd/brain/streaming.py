@@ -63,13 +63,15 @@ def is_continuous(doc) -> bool:
     return (doc.get("strategy") or "").lower() == STRATEGY_CONTINUOUS
 
 
-CALLER_SPLIT = ("namespace_pod_caller:", "namespace_app_caller:", "namespace_app_caller_per_pod:")
+CALLER_SPLIT = ("namespace_pod_caller:", "namespace_app_caller:", "namespace_app_caller_per_pod:",
+                "namespace_pod_uri:", "namespace_app_uri:", "namespace_app_uri_per_pod:")
 
 
 def is_streamable(doc) -> bool:
     """Continuous jobs whose series are one per (namespace, app): the resident
-    GPU shard's keying.  Downstream (per-caller) metrics split an app into one
-    series per caller, so such jobs stay with the batch worker (brain/worker.py)."""
+    GPU shard's keying.  Downstream (per-caller) and API-level (per-uri) metrics
+    split an app into one series per caller / path, so such jobs stay with the
+    batch worker (brain/worker.py)."""
     return is_continuous(doc) and not any(k[1].startswith(CALLER_SPLIT) for k in series_of(doc).values())
 
 

@@ -41,8 +41,17 @@ from ..utils.metrics import BrainMetrics
 from ..utils.timeutil import TimeFormatError, parse_rfc3339
 from .batch import BatchScorer, MetricTask, TaskResult
 
-# recorded per-caller families (deploy/rules.py CALLER_PREFIX)
-CALLER_PREFIXES = ("namespace_pod_caller:", "namespace_app_caller:", "namespace_app_caller_per_pod:")
+# recorded split families (deploy/rules.py SPLIT_PREFIXES): selector prefix -> split label
+SPLIT_PREFIXES = {"namespace_pod_caller:": "caller", "namespace_app_caller:": "caller",
+                  "namespace_app_caller_per_pod:": "caller", "namespace_pod_uri:": "uri",
+                  "namespace_app_uri:": "uri", "namespace_app_uri_per_pod:": "uri"}
+
+
+def split_label_of(metric: str) -> str:
+    for pfx, label in SPLIT_PREFIXES.items():
+        if metric.startswith(pfx):
+            return label
+    return ""
 
 log = logging.getLogger("foremast.brain")
 
@@ -165,8 +174,9 @@ class BrainWorker:
         return len(docs)
 
     def _build_tasks(self, i: int, p: JobPlan, alias: str, data, errors) -> List[MetricTask]:
-        """One task per metric alias — or, for a downstream (per-caller) alias, one
-        per calling service found in the history or the current window."""
+        """One task per metric alias — or, for a split alias (``metricType:
+        downstream`` / ``api``), one per calling service / request path found in
+        the history or the current window."""
         cur = data.get((i, "current", alias))
         hist = data.get((i, "historical", alias))
         base = data.get((i, "baseline", alias))
@@ -180,17 +190,18 @@ class BrainWorker:
             base = None
         hurl = p.historical.get(alias, "")
         metric, ns, app = _selector_info(hurl)
-        if not metric.startswith(CALLER_PREFIXES):
+        label = split_label_of(metric)
+        if not label:
             return [self._task(p, alias, metric, ns, app, hurl, hist, cur or [], base)]
-        callers = sorted({s.labels.get("caller", "") for s in list(hist) + list(cur or [])})
+        groups = sorted({s.labels.get(label, "") for s in list(hist) + list(cur or [])})
 
         def of(series, c):
-            return [s for s in series if s.labels.get("caller", "") == c]
+            return [s for s in series if s.labels.get(label, "") == c]
         out = []
-        for c in callers:
-            t = self._task(p, f"{alias}[caller={c}]", metric, ns, app, hurl, of(hist, c), of(cur or [], c),
+        for c in groups:
+            t = self._task(p, f"{alias}[{label}={c}]", metric, ns, app, hurl, of(hist, c), of(cur or [], c),
                            of(base, c) if base is not None else None)
-            t.caller, t.base_alias = c, alias
+            t.caller, t.base_alias, t.split_label = c, alias, label
             out.append(t)
         return out
 
@@ -232,7 +243,7 @@ class BrainWorker:
         if algo not in ("bivariate_normal", "lstm", "auto"):
             return
         # per-caller (downstream) tasks are scored jointly per caller by _downstream
-        per_job = {i: [(t, r_) for t, r_ in items if not t.caller] for i, items in per_job.items()}
+        per_job = {i: [(t, r_) for t, r_ in items if not t.split_label] for i, items in per_job.items()}
         lstm_jobs = [i for i, items in per_job.items()
                      if (algo == "lstm" and len(items) >= 2) or (algo == "auto" and len(items) >= 3)]
         if lstm_jobs:
@@ -255,8 +266,8 @@ class BrainWorker:
                 ra.model = rb.model = "bivariate_normal"
 
     def _downstream(self, per_job) -> None:
-        """Downstream impact: for every caller of the deployed app with >= 2
-        monitored metrics (e.g. latency + error rate), the caller's metrics are
+        """Downstream impact / API level: for every caller (or request path) of the
+        deployed app with >= 2 monitored metrics (e.g. latency + error rate), its metrics are
         scored JOINTLY by an LSTM autoencoder (fp8 e4m3 MFMA scoring on the GPU),
         keyed per (namespace, app, caller) in the model cache; a joint anomaly
         marks each of the caller's metrics anomalous at the flagged timestamps.
@@ -265,11 +276,11 @@ class BrainWorker:
             return
         from .multivariate import LstmJobScorer, ModelCache, align_job
         for i, items in per_job.items():
-            by_caller: Dict[str, List[Tuple[MetricTask, TaskResult]]] = {}
+            by_caller: Dict[Tuple[str, str], List[Tuple[MetricTask, TaskResult]]] = {}
             for t, res in items:
-                if t.caller:
-                    by_caller.setdefault(t.caller, []).append((t, res))
-            for caller, group in sorted(by_caller.items()):
+                if t.split_label:
+                    by_caller.setdefault((t.split_label, t.caller), []).append((t, res))
+            for (label, caller), group in sorted(by_caller.items()):
                 group = sorted(group, key=lambda tr: tr[0].base_alias)
                 if len(group) < 2:
                     continue
@@ -281,7 +292,7 @@ class BrainWorker:
                     self.downstream = LstmJobScorer(device=self.scorer.device,
                                                     cache=ModelCache(self.cfg.max_cache_size),
                                                     threshold=self.cfg.lstm_threshold, fp8=True)
-                key = self.downstream.cache.key(tasks[0].namespace, tasks[0].app + "@" + caller,
+                key = self.downstream.cache.key(tasks[0].namespace, f"{tasks[0].app}@{label}={caller}",
                                                 [t.base_alias for t in tasks])
                 verdict, bad, _z = self.downstream.score_job(key, hist, cts, cur, now=self.clock())
                 for f, (t, res) in enumerate(group):
@@ -327,8 +338,8 @@ class BrainWorker:
                 for ts, v, _ in sorted(res.anomalies):
                     vals += [ts, v]
                 tags = sorted({tag for _, _, tag in res.anomalies if tag})
-                if t.caller:  # downstream impact: name the calling service
-                    tags = [f"caller={t.caller}"] + [x for x in tags if x != "joint"]
+                if t.split_label:  # downstream / API level: name the caller or the request path
+                    tags = [f"{t.split_label}={t.caller}"] + [x for x in tags if x != "joint"]
                 tags = ",".join(tags)
                 anomaly[t.alias] = {"tags": tags, "values": vals}
         if anomaly:

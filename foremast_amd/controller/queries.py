@@ -16,6 +16,8 @@ with ``metricType: downstream`` reads the per-caller recordings instead
 (``namespace_pod_caller:<m>`` / ``namespace_app_caller_per_pod:<m>``, one series
 per calling service, ``deploy/rules.py``); the brain scores every caller of the
 deployed app separately and names the impacted one in the verdict.
+``metricType: api`` does the same per request path (``uri``): anomalies
+aggregated at API level (reference ``README.md:26``).
 """
 
 from __future__ import annotations
@@ -29,6 +31,10 @@ from ..api import rest as r
 STEP = 60
 HISTORICAL_DAYS = 7
 METRIC_TYPE_DOWNSTREAM = "downstream"
+METRIC_TYPE_API = "api"
+# metricType -> (per-pod prefix, per-app-per-pod prefix) of the split recordings (deploy/rules.py)
+_SPLIT = {METRIC_TYPE_DOWNSTREAM: ("namespace_pod_caller:", "namespace_app_caller_per_pod:"),
+          METRIC_TYPE_API: ("namespace_pod_uri:", "namespace_app_uri_per_pod:")}
 
 
 class QueryError(ValueError):
@@ -52,9 +58,7 @@ def create_map(namespace: str, app_name: str, pod_names: Sequence[str], metrics:
     now = time.time() if now is None else now
     out: Dict[str, r.MetricQuery] = {}
     for mon in metrics.monitoring:
-        down = (mon.metric_type or "").lower() == METRIC_TYPE_DOWNSTREAM
-        pod_pfx = "namespace_pod_caller:" if down else "namespace_pod:"
-        app_pfx = "namespace_app_caller_per_pod:" if down else "namespace_app_per_pod:"
+        pod_pfx, app_pfx = _SPLIT.get((mon.metric_type or "").lower(), ("namespace_pod:", "namespace_app_per_pod:"))
         now_unix = (int(now) // STEP) * STEP
         before = (int(now - time_window_min * 60) // STEP) * STEP
         p: Dict[str, object] = {"endpoint": metrics.endpoint, "step": STEP}

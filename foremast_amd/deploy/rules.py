@@ -41,6 +41,13 @@ RESOURCE_FAMILIES: Dict[str, str] = {
 # deployed app (controller/queries.py, brain/worker.py).
 CALLER_PREFIX = {"pod": "namespace_pod_caller:", "app": "namespace_app_caller:",
                  "app_per_pod": "namespace_app_caller_per_pod:"}
+# API level (reference README.md:26, "metrics anomaly aggregated at service or API
+# level"): the same families recorded per request path (Micrometer's ``uri`` tag),
+# read for ``metricType: api``
+URI_PREFIX = {"pod": "namespace_pod_uri:", "app": "namespace_app_uri:",
+              "app_per_pod": "namespace_app_uri_per_pod:"}
+# split label -> recorded prefixes
+SPLIT_PREFIXES = {"caller": CALLER_PREFIX, "uri": URI_PREFIX}
 
 POD_COUNT = "namespace_app:pod_count"
 APP_LABEL = 'label_replace({inner}, "app", "$1", "label_app", "(.*)")'
@@ -70,12 +77,12 @@ def rules() -> List[Dict[str, str]]:
         # apps expose the `app` tag themselves (metrics starter, C27)
         out.append({"record": f"namespace_app:{fam}", "expr": _http_expr(sel, kind, "namespace, app")})
         out.append({"record": f"namespace_app_per_pod:{fam}", "expr": f"namespace_app:{fam} / on (namespace, app) {POD_COUNT}"})
-    for fam, (sel, kind) in HTTP_FAMILIES.items():
-        cp = CALLER_PREFIX
-        out.append({"record": cp["pod"] + fam, "expr": _http_expr(sel, kind, "namespace, pod, caller")})
-        out.append({"record": cp["app"] + fam, "expr": _http_expr(sel, kind, "namespace, app, caller")})
-        out.append({"record": cp["app_per_pod"] + fam,
-                    "expr": f"{cp['app']}{fam} / on (namespace, app) group_left {POD_COUNT}"})
+    for label, cp in SPLIT_PREFIXES.items():
+        for fam, (sel, kind) in HTTP_FAMILIES.items():
+            out.append({"record": cp["pod"] + fam, "expr": _http_expr(sel, kind, f"namespace, pod, {label}")})
+            out.append({"record": cp["app"] + fam, "expr": _http_expr(sel, kind, f"namespace, app, {label}")})
+            out.append({"record": cp["app_per_pod"] + fam,
+                        "expr": f"{cp['app']}{fam} / on (namespace, app) group_left {POD_COUNT}"})
     for fam, inner in RESOURCE_FAMILIES.items():
         by_pod = f"sum by (namespace, pod) ({inner})"
         out.append({"record": f"namespace_pod:{fam}", "expr": by_pod})

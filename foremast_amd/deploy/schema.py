@@ -60,7 +60,8 @@ def schema_of(cls) -> Dict[str, Any]:
     return out
 
 
-def crd_manifest(kind: str, plural: str, spec_cls, status_cls, short_names=(), printer_columns=()) -> Dict[str, Any]:
+def crd_manifest(kind: str, plural: str, spec_cls, status_cls, short_names=(), printer_columns=(),
+                 selectable=()) -> Dict[str, Any]:
     group, version = crd.API_VERSION.split("/")
     return {
         "apiVersion": "apiextensions.k8s.io/v1",
@@ -75,6 +76,7 @@ def crd_manifest(kind: str, plural: str, spec_cls, status_cls, short_names=(), p
                 "name": version, "served": True, "storage": True,
                 "subresources": {"status": {}},
                 "additionalPrinterColumns": list(printer_columns),
+                **({"selectableFields": [{"jsonPath": p} for p in selectable]} if selectable else {}),
                 "schema": {"openAPIV3Schema": {
                     "type": "object",
                     "properties": {
@@ -99,7 +101,9 @@ def crds():
                          {"name": "Phase", "type": "string", "jsonPath": ".status.phase"},
                          {"name": "Job", "type": "string", "jsonPath": ".status.jobId"},
                          {"name": "Remediated", "type": "boolean", "jsonPath": ".status.remediationTaken"},
-                     ]),
+                     ],
+                     # the reference's field labels (v1alpha1/register.go:38-53)
+                     selectable=(".status.jobId", ".status.phase")),
     ]
 
 

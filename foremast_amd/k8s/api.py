@@ -12,7 +12,7 @@ generated fake clientset the reference ships but never uses,
 
 from __future__ import annotations
 
-from typing import Any, AsyncIterator, Dict, List, Optional, Protocol
+from typing import Any, AsyncIterator, Dict, List, Optional, Protocol, Tuple
 
 Obj = Dict[str, Any]
 
@@ -55,7 +55,7 @@ class KubeAPI(Protocol):
     async def get(self, kind: str, namespace: str, name: str) -> Obj: ...
 
     async def list(self, kind: str, namespace: Optional[str] = None,
-                   label_selector: Optional[str] = None) -> List[Obj]: ...
+                   label_selector: Optional[str] = None, field_selector: Optional[str] = None) -> List[Obj]: ...
 
     async def create(self, kind: str, obj: Obj) -> Obj: ...
 
@@ -133,6 +133,66 @@ def matches(labels: Optional[Dict[str, str]], sel: Optional[str]) -> bool:
         if op == "notin" and have in v:
             return False
         if op == "exists" and k not in labels:
+            return False
+    return True
+
+
+# ---------------------------------------------------------------------------------
+# field selectors: metadata.name / metadata.namespace for every kind, plus the
+# DeploymentMonitor status fields the reference registers as field labels
+# (v1alpha1/register.go:38-53: status.jobId, status.phase); the generated CRD declares
+# them as selectableFields so a real API server filters on them too (deploy/schema.py)
+# ---------------------------------------------------------------------------------
+
+FIELD_LABELS: Dict[str, Tuple[str, ...]] = {
+    "deploymentmonitors": ("metadata.name", "metadata.namespace", "status.jobId", "status.phase"),
+}
+DEFAULT_FIELD_LABELS = ("metadata.name", "metadata.namespace")
+
+
+class BadRequest(ApiError):
+    def __init__(self, message: str = "") -> None:
+        super().__init__(400, "BadRequest", message)
+
+
+def parse_field_selector(kind: str, sel: Optional[str]) -> List[Tuple[str, str, str]]:
+    """``a=b`` / ``a==b`` / ``a!=b`` terms joined by commas (ANDed); an unsupported
+    field label is a 400, like the API server's."""
+    out = []
+    allowed = FIELD_LABELS.get(kind, DEFAULT_FIELD_LABELS)
+    for term in (sel or "").split(","):
+        term = term.strip()
+        if not term:
+            continue
+        if "!=" in term:
+            k, v = term.split("!=", 1)
+            op = "!="
+        elif "==" in term:
+            k, v = term.split("==", 1)
+            op = "="
+        elif "=" in term:
+            k, v = term.split("=", 1)
+            op = "="
+        else:
+            raise BadRequest(f"invalid field selector term {term!r}")
+        k = k.strip()
+        if k not in allowed:
+            raise BadRequest(f'field label not supported: "{k}"')
+        out.append((k, op, v.strip()))
+    return out
+
+
+def field_value(obj: Obj, path: str) -> str:
+    cur: Any = obj
+    for part in path.split("."):
+        cur = cur.get(part) if isinstance(cur, dict) else None
+    return "" if cur is None else str(cur)
+
+
+def field_matches(obj: Obj, terms: List[Tuple[str, str, str]]) -> bool:
+    for k, op, v in terms:
+        have = field_value(obj, k)
+        if (op == "=" and have != v) or (op == "!=" and have == v):
             return False
     return True
 

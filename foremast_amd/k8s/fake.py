@@ -30,7 +30,7 @@ import uuid
 from typing import Any, AsyncIterator, Dict, List, Optional, Tuple
 
 from .api import (API_VERSION_OF, CLUSTER_SCOPED, KIND_OF, AlreadyExists, Conflict, NotFound, Obj,
-                  matches, revision_of)
+                  field_matches, matches, parse_field_selector, revision_of)
 
 REV = "deployment.kubernetes.io/revision"
 
@@ -81,7 +81,8 @@ class FakeCluster:
         return copy.deepcopy(o)
 
     def list_sync(self, kind: str, namespace: Optional[str] = None,
-                  label_selector: Optional[str] = None) -> List[Obj]:
+                  label_selector: Optional[str] = None, field_selector: Optional[str] = None) -> List[Obj]:
+        fields = parse_field_selector(kind, field_selector)
         out = []
         for (k, ns, _), o in sorted(self._objs.items()):
             if k != kind:
@@ -89,6 +90,8 @@ class FakeCluster:
             if namespace and kind not in CLUSTER_SCOPED and ns != namespace:
                 continue
             if label_selector and not matches((o.get("metadata") or {}).get("labels"), label_selector):
+                continue
+            if fields and not field_matches(o, fields):
                 continue
             out.append(copy.deepcopy(o))
         return out
@@ -149,8 +152,8 @@ class FakeCluster:
     async def get(self, kind, namespace, name):
         return self.get_sync(kind, namespace, name)
 
-    async def list(self, kind, namespace=None, label_selector=None):
-        return self.list_sync(kind, namespace, label_selector)
+    async def list(self, kind, namespace=None, label_selector=None, field_selector=None):
+        return self.list_sync(kind, namespace, label_selector, field_selector)
 
     async def create(self, kind, obj):
         return self.create_sync(kind, obj)

@@ -50,7 +50,8 @@ def create_apiserver(cluster: FakeCluster, min_watch_rv: int = 0) -> FastAPI:
                                              "message": "too old resource version"}, status_code=410)
                     return StreamingResponse(_watch(kind, namespace, rv), media_type="application/json")
                 if m == "GET":
-                    items = cluster.list_sync(kind, namespace, request.query_params.get("labelSelector"))
+                    items = cluster.list_sync(kind, namespace, request.query_params.get("labelSelector"),
+                                              request.query_params.get("fieldSelector"))
                     return JSONResponse({"kind": KIND_OF[kind] + "List", "items": items,
                                          "metadata": {"resourceVersion": current_rv()}})
                 if m == "POST":

@@ -153,15 +153,16 @@ class HttpKube:
         _raise_for(resp)
         return resp.json()
 
-    async def _list_raw(self, kind: str, namespace: Optional[str], label_selector: Optional[str] = None):
-        params = {"labelSelector": label_selector} if label_selector else None
-        resp = await self.http.get(resource_path(kind, namespace), params=params)
+    async def _list_raw(self, kind: str, namespace: Optional[str], label_selector: Optional[str] = None,
+                        field_selector: Optional[str] = None):
+        params = {k: v for k, v in (("labelSelector", label_selector), ("fieldSelector", field_selector)) if v}
+        resp = await self.http.get(resource_path(kind, namespace), params=params or None)
         _raise_for(resp)
         return resp.json()
 
     async def list(self, kind: str, namespace: Optional[str] = None,
-                   label_selector: Optional[str] = None) -> List[Obj]:
-        return list((await self._list_raw(kind, namespace, label_selector)).get("items") or [])
+                   label_selector: Optional[str] = None, field_selector: Optional[str] = None) -> List[Obj]:
+        return list((await self._list_raw(kind, namespace, label_selector, field_selector)).get("items") or [])
 
     async def create(self, kind: str, obj: Obj) -> Obj:
         ns = (obj.get("metadata") or {}).get("namespace")

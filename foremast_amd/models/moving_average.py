@@ -9,8 +9,14 @@ applied by :mod:`foremast_amd.models.detect`).
 * ``moving_average_all`` — statistics over the whole history;
 * ``moving_average``     — statistics over the last ``window`` positions.
 
-NaNs are ignored.  Accumulation is fp32 with a per-series shift (the first
-valid value) to avoid catastrophic cancellation in ``E[x²] − E[x]²``.
+NaNs are ignored.  This reference accumulates in fp32 with ONE per-series shift
+(the first valid value) to avoid catastrophic cancellation in ``E[x²] − E[x]²``.
+The K1 kernel (``ops/csrc/window.hip``, one wave per series) computes the same
+statistics with a different rounding order: every lane keeps shifted sums about
+its own first valid value, and the 64 per-lane ``(n, mean, M2)`` triples are
+merged Chan-style about their count-weighted mean — algebraically identical,
+equal to the reference within fp32 rounding (GPU test with a large offset and a
+small variance, ``tests/test_kernels_gpu.py::test_window_stats_kernel``).
 """
 
 from __future__ import annotations

@@ -806,13 +806,25 @@ __global__ __launch_bounds__(256, 2) void hw_half_kernel(const SmoothArgs a, int
   hw_half_block<K, false>(a, hmax, blockIdx.x * 2, deferred);
 }
 
-// persistent over the pairs deferred by hw_half_kernel (count in deferred[0])
+// persistent over the pairs deferred by hw_half_kernel (count in deferred[0]).
+// Self-cleaning: the workspace is int32 [2 + ceil(N / 2)] = {count, pairs..., done};
+// every workgroup counts itself in `done` after it has read the count, and the last
+// one resets count and done to 0, so the next fit needs no memset launch (the host
+// allocates the workspace zeroed).
 template <int K>
-__global__ __launch_bounds__(256, 2) void hw_half_general_kernel(const SmoothArgs a, int hmax, const int* deferred) {
+__global__ __launch_bounds__(256, 2) void hw_half_general_kernel(const SmoothArgs a, int hmax, int* deferred) {
   const int cnt = deferred[0];
   for (int q = blockIdx.x; q < cnt; q += gridDim.x) {
     hw_half_block<K, true>(a, hmax, deferred[1 + q], nullptr);
     __syncthreads();  // LDS is reused by the next pair
+  }
+  __syncthreads();  // every thread of this workgroup has read the count
+  if (threadIdx.x == 0) {
+    int* done = deferred + 1 + (a.N + 1) / 2;
+    if (atomicAdd(done, 1) == (int)gridDim.x - 1) {
+      *done = 0;
+      deferred[0] = 0;
+    }
   }
 }
 
@@ -1241,6 +1253,8 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
     if (lane == 0) prev = __hip_atomic_fetch_add(&cnt[slot * 2 + r], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     prev = __shfl(prev, 0, FM_WAVE);
     if (prev == 0) return;  // first half in: the other one finishes this series
+    // second arriver: the last user of this counter in the launch resets it for the next one
+    if (lane == 0) __hip_atomic_store(&cnt[slot * 2 + r], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const float* oth = cand + (((size_t)slot * 2 + (1 - hid)) * 2 + r) * CAND_FLOATS;
     const float oSSE = __hip_atomic_load(&oth[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const int oIdx = __float_as_int(__hip_atomic_load(&oth[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -1334,7 +1348,8 @@ extern "C" size_t fm_hw_half_lds_bytes(int Tp, int seg, int K) {
 
 // Variant 4 launcher: Holt-Winters, bf16 ring, season = seg = 32 K, pair table given,
 // forecast horizons within 1..hmax (hmax <= min(K, HALF_HB)), no season_out.
-// `deferred`: device int32 workspace of 1 + ceil(N / 2) entries.
+// `deferred`: device int32 workspace of 2 + ceil(N / 2) entries, zero on entry (kept zero
+// between launches by the general kernel).
 extern "C" int fm_hw_half_fit(const SmoothArgs* a, int hmax, int* deferred, hipStream_t st) {
   const int K = a->K;
   if (K != 45 || a->seg != 32 * K || a->m != a->seg || a->Tp % a->seg != 0 || a->Tp / a->seg < 2 ||
@@ -1344,14 +1359,12 @@ extern "C" int fm_hw_half_fit(const SmoothArgs* a, int hmax, int* deferred, hipS
   const size_t lds = fm_hw_half_lds_bytes(a->Tp, a->seg, K);
   if (lds > 64 * 1024) return (int)hipErrorNotSupported;
   if (!deferred) return (int)hipErrorInvalidValue;
-  hipError_t e = hipMemsetAsync(deferred, 0, sizeof(int), st);
-  if (e != hipSuccess) return (int)e;
   const int pairs = (a->N + 1) / 2;
   hipLaunchKernelGGL((hw_half_kernel<45>), dim3(pairs), dim3(256), lds, st, *a, hmax, deferred);
-  e = hipGetLastError();
+  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL((hw_half_general_kernel<45>), dim3(pairs < 512 ? pairs : 512), dim3(256), lds, st, *a, hmax,
-                     (const int*)deferred);
+                     deferred);
   return (int)hipGetLastError();
 }
 
@@ -1381,7 +1394,7 @@ extern "C" int fm_hw_d_split_plan(int pairs, int slots, int max_split) {
 // Variant 5 launcher: same contract as fm_hw_half_fit (deferred pairs go to the
 // variant-4 general kernel), at most D_MAXSEG seasons.  `split_ws` (optional):
 // int32 [2 * max_split] arrival counters followed by float [max_split * 2 * 2 *
-// CAND_FLOATS] candidates; the counters are zeroed here.
+// CAND_FLOATS] candidates; the counters must be zero on entry (they are left zero).
 extern "C" int fm_hw_d_fit_split(const SmoothArgs* a, int hmax, int* deferred, int* split_ws, int max_split,
                                  int slots, hipStream_t st);
 extern "C" int fm_hw_d_fit(const SmoothArgs* a, int hmax, int* deferred, hipStream_t st) {
@@ -1399,22 +1412,18 @@ extern "C" int fm_hw_d_fit_split(const SmoothArgs* a, int hmax, int* deferred, i
   const size_t glds = fm_hw_half_lds_bytes(a->Tp, a->seg, K);
   if (lds > 80 * 1024 || glds > 64 * 1024) return (int)hipErrorNotSupported;
   if (!deferred) return (int)hipErrorInvalidValue;
-  hipError_t e = hipMemsetAsync(deferred, 0, sizeof(int), st);
-  if (e != hipSuccess) return (int)e;
   const int pairs = (a->N + 1) / 2;
   const int S = (split_ws && max_split > 0 && a->G >= 2) ? fm_hw_d_split_plan(pairs, slots, max_split) : 0;
+  // arrival counters are zero between launches: allocated zeroed, and the second arriver
+  // of each (slot, row) resets its counter
   int* cnt = split_ws;
   float* cand = split_ws ? (float*)(split_ws + 2 * max_split) : nullptr;
-  if (S > 0) {
-    e = hipMemsetAsync(cnt, 0, sizeof(int) * 2 * (size_t)S, st);
-    if (e != hipSuccess) return (int)e;
-  }
   hipLaunchKernelGGL((hw_d_kernel<45>), dim3(pairs - S + 2 * S), dim3(256), lds, st, *a, hmax, deferred, pairs - S,
                      cnt, cand);
-  e = hipGetLastError();
+  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL((hw_half_general_kernel<45>), dim3(pairs < 512 ? pairs : 512), dim3(256), glds, st, *a, hmax,
-                     (const int*)deferred);
+                     deferred);
   return (int)hipGetLastError();
 }
 

@@ -12,7 +12,9 @@
 // pods' mean that graduates: the model history follows the stable version and
 // the canary is never fitted into the model it is judged against.  Without one
 // (continuous monitoring) the current pods' mean graduates.  One thread per
-// series; everything the tick needs is touched once.
+// series; everything the tick needs is touched once.  `zero` (optional, nzero int32
+// words): per-tick counters the scoring kernels accumulate into (per-app health
+// counters) are cleared here, in the tick's first launch, instead of by a fill.
 #include "common.h"
 
 template <typename TH>
@@ -21,8 +23,10 @@ __global__ __launch_bounds__(256) void tick_ingest_kernel(TH* __restrict__ hist,
                                                           int slot, const float* __restrict__ newv,
                                                           long long ld_n, int N, int graduate,
                                                           float* __restrict__ base, const float* __restrict__ newb,
-                                                          const int* __restrict__ st) {
+                                                          const int* __restrict__ st, int* __restrict__ zero,
+                                                          int nzero) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  for (int i = n; i < nzero; i += gridDim.x * blockDim.x) zero[i] = 0;
   if (n >= N) return;
   if (st) {  // per-tick ring state from device memory (HIP-graph replays): {hist_col, slot, graduate}
     hist_col = st[0];
@@ -53,31 +57,35 @@ __global__ __launch_bounds__(256) void tick_ingest_kernel(TH* __restrict__ hist,
 
 static int tick_ingest_launch(void* hist, long long ld_h, int hist_col, float* cur, long long ld_c, int P,
                               int W, int slot, const float* newv, long long ld_n, int N, int graduate,
-                              float* base, const float* newb, int bf16, const int* state, hipStream_t st) {
-  if (N <= 0) return 0;
-  if (P <= 0 || W <= 0 || slot < 0 || slot >= W || hist_col < 0) return (int)hipErrorInvalidValue;
-  dim3 grid((N + 255) / 256), block(256);
+                              float* base, const float* newb, int bf16, const int* state, int* zero, int nzero,
+                              hipStream_t st) {
+  if (N <= 0 && nzero <= 0) return 0;
+  if (P <= 0 || W <= 0 || slot < 0 || slot >= W || hist_col < 0 || nzero < 0 || (nzero > 0 && !zero))
+    return (int)hipErrorInvalidValue;
+  const int work = N > nzero ? N : nzero;
+  dim3 grid((work + 255) / 256), block(256);
   if (bf16)
     hipLaunchKernelGGL(tick_ingest_kernel<bf16_t>, grid, block, 0, st, (bf16_t*)hist, ld_h, hist_col, cur,
-                       ld_c, P, W, slot, newv, ld_n, N, graduate, base, newb, state);
+                       ld_c, P, W, slot, newv, ld_n, N, graduate, base, newb, state, zero, nzero);
   else
     hipLaunchKernelGGL(tick_ingest_kernel<float>, grid, block, 0, st, (float*)hist, ld_h, hist_col, cur, ld_c,
-                       P, W, slot, newv, ld_n, N, graduate, base, newb, state);
+                       P, W, slot, newv, ld_n, N, graduate, base, newb, state, zero, nzero);
   return (int)hipGetLastError();
 }
 
 extern "C" int fm_tick_ingest(void* hist, long long ld_h, int hist_col, float* cur, long long ld_c, int P,
                               int W, int slot, const float* newv, long long ld_n, int N, int graduate,
-                              float* base, const float* newb, int bf16, hipStream_t st) {
+                              float* base, const float* newb, int bf16, int* zero, int nzero, hipStream_t st) {
   return tick_ingest_launch(hist, ld_h, hist_col, cur, ld_c, P, W, slot, newv, ld_n, N, graduate, base, newb,
-                            bf16, nullptr, st);
+                            bf16, nullptr, zero, nzero, st);
 }
 
 // graph-replayable form: hist_col / slot / graduate are read from `state` (device int32
 // {hist_col, slot, graduate}, valid ranges are the caller's contract: hist_col < R, slot < W)
 extern "C" int fm_tick_ingest_dev(void* hist, long long ld_h, float* cur, long long ld_c, int P, int W,
                                   const float* newv, long long ld_n, int N, float* base, const float* newb,
-                                  int bf16, const int* state, hipStream_t st) {
+                                  int bf16, const int* state, int* zero, int nzero, hipStream_t st) {
   if (!state) return (int)hipErrorInvalidValue;
-  return tick_ingest_launch(hist, ld_h, 0, cur, ld_c, P, W, 0, newv, ld_n, N, 1, base, newb, bf16, state, st);
+  return tick_ingest_launch(hist, ld_h, 0, cur, ld_c, P, W, 0, newv, ld_n, N, 1, base, newb, bf16, state, zero,
+                            nzero, st);
 }

@@ -89,11 +89,15 @@ __device__ __forceinline__ void acc_range(const TIN* row, int p0, int p1, float&
   for (int i = a0 + nvec * VEC + tid; i < p1; i += nt) add(to_f32<TIN>(row[i]));
 }
 
-// One wave per series (four per workgroup): the same statistics with wave reductions
-// only, no workgroup barriers, and ~20 16-byte loads of a lane in flight in two batches.
+// One wave per series (kSeriesPerWG per workgroup): the same statistics with wave
+// reductions only, no workgroup barriers, and ~20 16-byte loads of a lane in flight in
+// two batches.
+constexpr int kWindowBlock = 256;
+constexpr int kSeriesPerWG = kWindowBlock / FM_WAVE;
+
 template <typename TIN>
-__global__ __launch_bounds__(256) void window_stats_wave_kernel(const WindowArgs a) {
-  const int n = blockIdx.x * (256 / FM_WAVE) + wave_id();
+__global__ __launch_bounds__(kWindowBlock) void window_stats_wave_kernel(const WindowArgs a) {
+  const int n = blockIdx.x * kSeriesPerWG + wave_id();
   if (n >= a.N) return;  // wave-uniform
   const int lane = lane_id();
   const TIN* row = (const TIN*)a.hist + (long long)n * a.ld;
@@ -131,10 +135,10 @@ extern "C" int fm_window_stats(const WindowArgs* a, int bf16, hipStream_t st) {
     return (int)hipErrorInvalidValue;
   if (bf16 && (a->ld % 8) != 0) return (int)hipErrorInvalidValue;
   if (!bf16 && (a->ld % 4) != 0) return (int)hipErrorInvalidValue;
-  const dim3 wgrid((a->N + 3) / 4);
+  const dim3 wgrid((a->N + kSeriesPerWG - 1) / kSeriesPerWG);
   if (bf16)
-    hipLaunchKernelGGL(window_stats_wave_kernel<bf16_t>, wgrid, dim3(256), 0, st, *a);
+    hipLaunchKernelGGL(window_stats_wave_kernel<bf16_t>, wgrid, dim3(kWindowBlock), 0, st, *a);
   else
-    hipLaunchKernelGGL(window_stats_wave_kernel<float>, wgrid, dim3(256), 0, st, *a);
+    hipLaunchKernelGGL(window_stats_wave_kernel<float>, wgrid, dim3(kWindowBlock), 0, st, *a);
   return (int)hipGetLastError();
 }

@@ -375,12 +375,13 @@ _HALF_WS: Dict[tuple, torch.Tensor] = {}
 
 
 def _half_workspace(dev, N: int) -> torch.Tensor:
-    """Deferred-pair list of variant 4 (count + pair starts), reused across calls
-    so a captured tick allocates nothing."""
+    """Deferred-pair list of variants 4/5 (count, pair starts, done counter),
+    reused across calls so a captured tick allocates nothing; allocated zeroed and
+    left zeroed by the general kernel (no per-call memset)."""
     key = (dev.index, N)
     ws = _HALF_WS.get(key)
     if ws is None:
-        ws = torch.zeros(1 + (N + 1) // 2, dtype=torch.int32, device=dev)
+        ws = torch.zeros(2 + (N + 1) // 2, dtype=torch.int32, device=dev)  # {count, pairs..., done}
         _HALF_WS[key] = ws
     return ws
 
@@ -680,11 +681,13 @@ def ring_append(dst: torch.Tensor, col0: int, src: torch.Tensor) -> None:
 
 def tick_ingest(hist: torch.Tensor, hist_col: int, cur: torch.Tensor, P: int, W: int, slot: int,
                 newv: torch.Tensor, graduate: bool = True, base: Optional[torch.Tensor] = None,
-                newb: Optional[torch.Tensor] = None, state: Optional[torch.Tensor] = None) -> None:
+                newb: Optional[torch.Tensor] = None, state: Optional[torch.Tensor] = None,
+                zero: Optional[torch.Tensor] = None) -> None:
     """Per-tick streaming ingest (see csrc/ingest.hip); ``newv``/``newb`` are
     ``[N, P]`` (same row stride) current/baseline pod values.  ``state``: int32
     device ``{hist_col, slot, graduate}`` read at run time instead of the scalar
-    arguments (HIP-graph replays; the caller keeps them in range)."""
+    arguments (HIP-graph replays; the caller keeps them in range).  ``zero``: a
+    contiguous int32 tensor (e.g. the per-app counters) cleared by the same launch."""
     lib = nat.require()
     _cuda(hist, "hist")
     N = hist.shape[0]
@@ -701,19 +704,25 @@ def tick_ingest(hist: torch.Tensor, hist_col: int, cur: torch.Tensor, P: int, W:
               and base.dtype == torch.float32 and base.device == cur.device, "base must match cur")
         _need(newb.shape == newv.shape and newb.stride() == newv.stride() and newb.dtype == torch.float32
               and newb.device == newv.device, "newb must match newv")
+    nz = 0
+    if zero is not None:
+        _need(zero.dtype == torch.int32 and zero.is_contiguous() and zero.device == hist.device,
+              "zero must be a contiguous int32 tensor on the device")
+        nz = int(zero.numel())
     if state is not None:
         _need(state.dtype == torch.int32 and state.device == hist.device and state.numel() >= 3,
               "state must be int32 {hist_col, slot, graduate} on the device")
         nat.check(lib.fm_tick_ingest_dev(nat.ptr(hist), hist.stride(0), nat.ptr(cur), cur.stride(0), int(P), int(W),
                                          nat.ptr(newv), newv.stride(0), N, nat.ptr(base),
                                          nat.ptr(newb) if base is not None else 0,
-                                         int(hist.dtype == torch.bfloat16), nat.ptr(state),
+                                         int(hist.dtype == torch.bfloat16), nat.ptr(state), nat.ptr(zero), nz,
                                          nat.stream_handle(hist.device)), "fm_tick_ingest_dev")
         return
     nat.check(lib.fm_tick_ingest(nat.ptr(hist), hist.stride(0), int(hist_col), nat.ptr(cur), cur.stride(0),
                                  int(P), int(W), int(slot), nat.ptr(newv), newv.stride(0), N, int(graduate),
                                  nat.ptr(base), nat.ptr(newb) if base is not None else 0,
-                                 int(hist.dtype == torch.bfloat16), nat.stream_handle(hist.device)),
+                                 int(hist.dtype == torch.bfloat16), nat.ptr(zero), nz,
+                                 nat.stream_handle(hist.device)),
               "fm_tick_ingest")
 
 

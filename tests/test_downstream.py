@@ -157,3 +157,57 @@ def test_per_caller_continuous_jobs_stay_with_the_batch_worker():
     assert is_streamable(store.get(a)) and not is_streamable(store.get(b))
     w = BrainWorker(store, BrainConfig(), exclude_strategies=("continuous",))
     assert [d["id"] for d in store.claim("w", now=T0, max_stuck_s=90, only=w._claimable)] == [b]
+
+
+def test_api_level_rollup_names_the_request_path():
+    """``metricType: api`` (reference README.md:26, anomalies aggregated at service
+    or API level): the same families per request path (``uri``); a v2 that fails
+    one endpoint is reported on that path only."""
+    import torch
+    clock = Clock(T0)
+    kube = FakeCluster()
+    for ns in (NS, "foremast"):
+        kube.add_namespace(ns)
+    md = _metadata()
+    md["spec"]["metrics"]["monitoring"] = [{"metricName": ERR, "metricType": "api", "metricAlias": "errors"}]
+    kube.create_sync("deploymentmetadatas", md)
+    prom = FakePrometheus(clock=clock)
+    paths = ("/orders", "/cart")
+    for i, u in enumerate(paths):
+        prom.add("namespace_app_uri_per_pod:" + ERR, {"namespace": NS, "app": "cart", "uri": u},
+                 synth.error_rate(base=0.3, spread=0.1, seed=40 + i))
+    store = MemoryJobStore()
+    svc_transport = httpx.ASGITransport(app=create_app(store, query_endpoint="http://prometheus:9090/"))
+    barrel = Barrelman(kube, namespace="foremast", clock=clock, poll_seconds=0, pod_retry_sleep=0,
+                       analyst_factory=lambda ep: AnalystClient(ep, transport=svc_transport))
+    env = reference_default_env()
+    env.update(ML_ALGORITHM="moving_average_all", MIN_HISTORICAL_DATA_POINT_TO_MEASURE="10")
+    cfg = BrainConfig.from_env(env)
+    brain = BrainWorker(store, cfg, prom=PromClient(transport=httpx.ASGITransport(app=prom.asgi_app())),
+                        scorer=BatchScorer(cfg, device=torch.device("cpu")), worker_id="brain-0", clock=clock)
+
+    async def go():
+        v1 = kube.apply_deployment(NS, "cart", "cart", "shop/cart:v1", replicas=1, labels={"appType": "spring-boot"})
+        await barrel.on_deployment_added(v1)
+        old_hash = kube.list_sync("replicasets", NS)[0]["metadata"]["labels"]["pod-template-hash"]
+        v1 = kube.get_sync("deployments", NS, "cart")
+        v2 = kube.apply_deployment(NS, "cart", "cart", "shop/cart:v2", replicas=1, labels={"appType": "spring-boot"})
+        for j, p in enumerate(kube.list_sync("pods", NS)):
+            new = p["metadata"]["labels"]["pod-template-hash"] != old_hash
+            for i, u in enumerate(paths):
+                gen = synth.error_rate(base=0.3, spread=0.1, seed=60 + 3 * j + i)
+                if new and u == "/orders":
+                    gen = synth.step_change(gen, at=T0 + 120, factor=0.0, add=25.0)
+                prom.add("namespace_pod_uri:" + ERR, {"namespace": NS, "pod": p["metadata"]["name"], "uri": u}, gen)
+        await barrel.on_deployment_updated(v1, v2)
+        await barrel.drain()
+        mon = crd.DeploymentMonitor.from_dict(kube.get_sync("deploymentmonitors", NS, "cart"))
+        assert "namespace_pod_uri%3A" + ERR in store.get(mon.status.job_id)["currentConfig"]
+        clock.t = T0 + 300
+        assert await brain.cycle() == 1
+        doc = store.get(mon.status.job_id)
+        assert doc["status"] == "completed_unhealth"
+        info = json.loads(doc["anomalyInfo"])
+        assert list(info) == ["errors[uri=/orders]"] and info["errors[uri=/orders]"]["tags"].startswith("uri=/orders")
+
+    asyncio.run(go())

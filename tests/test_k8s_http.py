@@ -145,3 +145,40 @@ def test_watch_relists_after_gone(apiserver):
             await kube.aclose()
 
     asyncio.run(run())
+
+
+def test_field_selectors_status_job_id_and_phase():
+    """The reference's DeploymentMonitor field labels (v1alpha1/register.go:38-53):
+    status.jobId / status.phase filter lists on the fake cluster and through the
+    REST client + fake API server; other fields are a 400; the generated CRD
+    declares them as selectableFields."""
+    import asyncio
+    import httpx
+    from foremast_amd.deploy import schema
+    from foremast_amd.k8s.api import ApiError
+    from foremast_amd.k8s.fake import FakeCluster
+    from foremast_amd.k8s.fake_apiserver import create_apiserver as apiserver
+    from foremast_amd.k8s.http import HttpKube
+    kube = FakeCluster()
+    kube.add_namespace("a")
+    for i, phase in enumerate(("Running", "Healthy", "Running")):
+        kube.create_sync("deploymentmonitors", {"metadata": {"name": f"m{i}", "namespace": "a"},
+                                                "status": {"jobId": f"j{i}", "phase": phase}})
+    names = lambda objs: [o["metadata"]["name"] for o in objs]  # noqa: E731
+    assert names(kube.list_sync("deploymentmonitors", field_selector="status.phase=Running")) == ["m0", "m2"]
+    assert names(kube.list_sync("deploymentmonitors", field_selector="status.phase!=Running")) == ["m1"]
+    assert names(kube.list_sync("deploymentmonitors", field_selector="status.jobId==j2,status.phase=Running")) == ["m2"]
+    with pytest.raises(ApiError) as e:
+        kube.list_sync("deploymentmonitors", field_selector="spec.continuous=true")
+    assert e.value.code == 400
+
+    async def go():
+        client = HttpKube(base_url="http://k8s", transport=httpx.ASGITransport(app=apiserver(kube)))
+        got = await client.list("deploymentmonitors", "a", field_selector="status.jobId=j1")
+        assert names(got) == ["m1"]
+        with pytest.raises(ApiError):
+            await client.list("deploymentmonitors", "a", field_selector="status.bogus=1")
+    asyncio.run(go())
+    dm = [c for c in schema.crds() if c["spec"]["names"]["kind"] == "DeploymentMonitor"][0]
+    assert dm["spec"]["versions"][0]["selectableFields"] == [{"jsonPath": ".status.jobId"},
+                                                             {"jsonPath": ".status.phase"}]

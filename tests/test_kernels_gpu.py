@@ -177,9 +177,10 @@ def test_smoothing_kernel_flagship_shape(K, variant):
     np.testing.assert_allclose(out["season"].cpu().numpy()[sm_], ref.season.numpy()[sm_], rtol=2e-2, atol=2e-2)
 
 
-def test_window_stats_kernel(K):
+@pytest.mark.parametrize("N", [40, 41, 43])  # a partial last workgroup (4 series per workgroup)
+def test_window_stats_kernel(K, N):
     dev = torch.device("cuda:0")
-    N, T, C = 40, 1000, 8
+    T, C = 1000, 8
     y = _series(N, T, 24, seed=11, nan_frac=0.05)
     for dtype in (torch.float32, torch.bfloat16):
         R, head = 1024, 1000  # wraps
@@ -195,6 +196,38 @@ def test_window_stats_kernel(K):
         d = det_ref.detect(st.mean[:, None].expand(N, C), st.std, cur.cpu(), torch.full((N,), 2.0),
                            torch.full((N,), 3, dtype=torch.int8), torch.full((N,), -1e30))
         assert torch.equal(d.verdict, out["verdict"].cpu())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_window_stats_short_window_odd_head_and_offset(K, dtype):
+    """A window shorter than the 64-lane wave starting at an unaligned head that wraps
+    (the scalar head/tail path of the staged loads), and a large offset with a small
+    variance (1e4 + N(0, 1e-2): cancellation in the per-lane shifted sums + Chan merge)."""
+    dev = torch.device("cuda:0")
+    N, R, L, head, C = 41, 1024, 60, 1001, 6
+    rng = np.random.default_rng(3)
+    y = (1e4 + rng.normal(0, 1e-2, (N, L))).astype(np.float32)
+    y[::5, 7] = np.nan
+    ring = torch.tensor(_ring(y, R, head), device=dev).to(dtype)
+    yl = ring.float().cpu()[:, (head + np.arange(L)) % R]
+    cur = torch.tensor(y[:, :C], device=dev)
+    cur[::3, 2] += 1.0
+    spec = _det_spec(K, N, C, dev, cur=cur, thr=3.0)
+    out = K.window_stats(ring, head, L, spec)
+    torch.cuda.synchronize()
+    ref = torch.tensor(yl.numpy().astype(np.float64))
+    ok = ~torch.isnan(ref)
+    cnt = ok.sum(1)
+    mean = torch.where(ok, ref, torch.zeros_like(ref)).sum(1) / cnt
+    var = (torch.where(ok, ref - mean[:, None], torch.zeros_like(ref)) ** 2).sum(1) / cnt
+    np.testing.assert_allclose(out["mean"].cpu().numpy(), mean.numpy(), rtol=1e-7, atol=2e-3)
+    if dtype == torch.float32:  # bf16 quantises 1e4 + 1e-2 noise to a few levels: variance checked in fp32
+        np.testing.assert_allclose(out["std"].cpu().numpy(), var.sqrt().numpy(), rtol=5e-2, atol=2e-3)
+    assert torch.equal(out["count_hist"].cpu(), cnt.float())
+    d = det_ref.detect(out["mean"].cpu()[:, None].expand(N, C), out["std"].cpu(), cur.cpu(), torch.full((N,), 3.0),
+                       torch.full((N,), 3, dtype=torch.int8), torch.full((N,), -1e30))
+    assert torch.equal(d.verdict, out["verdict"].cpu()) and torch.equal(d.count, out["count"].cpu())
+    np.testing.assert_allclose(out["score"].cpu().numpy(), d.score.numpy(), rtol=1e-4)
 
 
 def test_rank_tests_kernel(K):
