@@ -122,16 +122,18 @@ def test_hw_state_kernel_matches_reference(dtype, pad):
 
 
 @pytest.mark.gpu
-def test_cached_engine_gpu_matches_cpu():
-    """StreamingShard with refit_every=3 at m = 1440 on the GPU (variant-5 fit,
-    state kernel, update/detect kernel) against the CPU engine on the same data:
-    refit schedule, verdicts, counts, forecasts and bands."""
+@pytest.mark.parametrize("refit_every", [1, 3])
+def test_cached_engine_gpu_matches_cpu(refit_every):
+    """GPU StreamingShard vs the CPU StreamingShard on the same data at m = 1440,
+    P = 5, W = 10, pairwise ALL: refit every tick (variant-5 fit, side-stream rank
+    tests, deferred band/verdict) or every 3 ticks (+ state kernel, update/detect
+    kernel): refit schedule, verdicts, forecasts, app counters."""
     from foremast_amd.ops import _native
     _native.require()
     n, m, P, W = 64, 1440, 5, 10
     R = 3 * m
-    cpu, hist = _shard(torch.device("cpu"), 3, n=n, R=R, m=m, P=P, W=W, seed=21)
-    gpu, _ = _shard(torch.device("cuda:0"), 3, n=n, R=R, m=m, P=P, W=W, seed=21, dtype=torch.bfloat16)
+    cpu, hist = _shard(torch.device("cpu"), refit_every, n=n, R=R, m=m, P=P, W=W, seed=21)
+    gpu, _ = _shard(torch.device("cuda:0"), refit_every, n=n, R=R, m=m, P=P, W=W, seed=21, dtype=torch.bfloat16)
     g = torch.Generator().manual_seed(7)
     for k in range(W + 7):
         newv = hist[:, R + k:R + k + 1].repeat(1, P).float() + 0.5 * torch.randn(n, P, generator=g)
@@ -149,4 +151,6 @@ def test_cached_engine_gpu_matches_cpu():
         torch.testing.assert_close(o_g["forecast"], o_c["forecast"], rtol=2e-3, atol=2e-2, msg=f"tick {k}")
         agree = (o_g["verdict"] == o_c["verdict"]).float().mean().item()
         assert agree >= 0.97, (k, agree)
-    assert gpu._cache is not None
+        if agree == 1.0:
+            assert torch.equal(cpu.app_stats, gpu.app_stats.cpu()), k
+    assert (gpu._cache is not None) == (refit_every > 1)
