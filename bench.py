@@ -442,6 +442,7 @@ def setup_lstm(args, world, rank, dev, n_features, fp8):
                      want_bad=True) for p in params]
     ticks = torch.stack([t[..., 0] for t, _ in tk], 2)  # [ticks, n, F]
     truth_apps = sorted(set(((tk[0][1].cpu() + s) // ent_per_app).tolist()))
+    bad_local = tk[0][1].cpu()
     del tk
     pin = dev.type == "cuda"
     host_ticks = ticks.cpu()
@@ -486,6 +487,7 @@ def setup_lstm(args, world, rank, dev, n_features, fp8):
     dt = "bf16"  # training fp32 master / bf16 MFMA scoring (fp8 weights+activations for config 5)
     meta["_agg"] = agg
     meta["_truth"] = (truth_apps, n_apps)
+    meta["_shard"], meta["_bad"] = shard, bad_local
     return tick, health_host, meta, dt, n_ent * F
 
 
@@ -661,6 +663,8 @@ def main():
     table = meta.pop("_table", None)
     decoder = meta.pop("_decoder", None)
     truth = meta.pop("_truth", None)
+    for k in [k for k in meta if k.startswith("_")]:
+        meta.pop(k)
     if truth is not None and world > 1:
         parts = [None] * world
         dist.all_gather_object(parts, truth[0])

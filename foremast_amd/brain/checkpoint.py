@@ -126,15 +126,18 @@ def save_lstm_shard(shard, path: str, extra: Optional[Dict[str, Any]] = None) ->
     for k in ("mean", "std", "rstd", "app_id"):
         tensors[k] = getattr(shard, k)
     tensors["gen_state"] = shard.gen.get_state()
+    if shard.cal is not None:
+        tensors["cal"] = shard.cal
     hidden = int(shard.model.H)
     meta = {"format": FORMAT, "kind": "lstm_shard",
             "args": {"n_series": shard.n, "ring_len": shard.R, "n_features": shard.F, "window": shard.T,
                      "hidden": hidden, "fp8": bool(shard.fp8), "n_apps": int(shard.app_stats.shape[0]),
                      "threshold": float(shard.threshold), "train_batch": int(shard.train_batch),
                      "restat_every": int(shard.restat_every), "fused_train": bool(shard.fused_train),
-                     "dtype": _dtype_name(shard.rings[0].data.dtype)},
+                     "dtype": _dtype_name(shard.rings[0].data.dtype), "cal_windows": int(shard.cal_windows),
+                     "cal_ewma": float(shard.cal_ewma)},
             "param_groups": opt["param_groups"], "trainer_steps": int(shard.trainer.steps),
-            "mu": float(shard.mu), "sigma": float(shard.sigma), "ticks": int(shard.ticks),
+            "mu": float(shard.mu), "sigma": float(shard.sigma), "rho": float(shard.rho), "ticks": int(shard.ticks),
             "rings": [[r.head, r.length] for r in shard.rings], "extra": extra or {}}
     _atomic_save(tensors, meta, path)
 
@@ -151,7 +154,8 @@ def load_lstm_shard(path: str, device="cpu"):
     shard = LstmShard(a["n_series"], a["ring_len"], a["n_features"], window=a["window"], hidden=hidden,
                       fp8=a["fp8"], device=device, app_id=t["app_id"].to(torch.int32), n_apps=a["n_apps"],
                       threshold=a["threshold"], train_batch=a["train_batch"], lr=lr,
-                      restat_every=a["restat_every"], dtype=dtype, fused_train=a["fused_train"])
+                      restat_every=a["restat_every"], dtype=dtype, fused_train=a["fused_train"],
+                      cal_windows=int(a.get("cal_windows", 0)), cal_ewma=float(a.get("cal_ewma", 0.0)))
     for f, ring in enumerate(shard.rings):
         ring._store.copy_(t[f"ring{f}"])
         ring.state = RingState(head=int(meta["rings"][f][0]), length=int(meta["rings"][f][1]))
@@ -167,6 +171,8 @@ def load_lstm_shard(path: str, device="cpu"):
         getattr(shard, k).copy_(t[k])
     shard.gen.set_state(t["gen_state"].cpu())
     shard.mu, shard.sigma = float(meta["mu"]), float(meta["sigma"])
+    shard.rho = float(meta.get("rho", 1.0))
+    shard.cal = t["cal"].float().contiguous() if "cal" in t else None
     shard.ticks = int(meta["ticks"])
     shard.packed = None  # repacked for the fused scorer on the next score
     shard.checkpoint_extra = meta.get("extra", {})

@@ -47,6 +47,8 @@ struct LstmArgs {
   int* app_stats;          // [A, 2] or null
   const float* wmax;       // fp8: device absmax [enc, dec] of the packed weights (overrides scale_w_*) or null
   LstmRingSrc src;         // ring-direct input (x == null)
+  float* cal;              // [N, 2] per-series (mu, 1/sigma) of the reconstruction error, or null (global only)
+  float cal_ewma;          // > 0: mu_i tracks healthy errors, mu_i += cal_ewma * (err - mu_i) when verdict 0
 };
 
 extern __shared__ __attribute__((aligned(16))) char fm_lstm_smem[];
@@ -84,7 +86,7 @@ __device__ __forceinline__ void run_phase(const LstmArgs& a, const typename Frag
         if (ENC && valid) {
 #pragma unroll
           for (int f = 0; f < 7; ++f)
-            if (f < a.F) v[f] = load_x(a.src, xp, t, f, a.F) * (1.f / sa);
+            if (f < a.F) v[f] = sat_input<FP8>(load_x(a.src, xp, t, f, a.F) * (1.f / sa));
         }
         v[7] = 1.f / sa;
       }
@@ -181,11 +183,26 @@ __global__ __launch_bounds__(256, 2) void lstm_ae_kernel(const LstmArgs a) {
   if (valid && hh == 0) {
     const float err = errsum / (float)(a.T * a.F);
     a.err[series] = err;
-    const float z = (err - a.mu) / fmaxf(a.sigma, 1e-12f);
+    // global z (error in series-std units vs the pooled healthy level), and
+    // with a calibration the smaller of it and the series' own z: a window is
+    // anomalous only when it is unusual for its series AND in absolute terms
+    float z = (err - a.mu) / fmaxf(a.sigma, 1e-12f);
+    if (a.cal) {
+      const float2 c = ((const float2*)a.cal)[series];
+      z = fminf(z, (err - c.x) * c.y);
+    }
     if (a.zscore) a.zscore[series] = z;
     const float thr = a.threshold ? a.threshold[series] : a.thr_default;
     const int v = z > thr ? 1 : 0;
     if (a.verdict) a.verdict[series] = (signed char)v;
+    // healthy windows keep the per-series error level current as the shared
+    // model keeps training (NaN errors — missing samples — never update it)
+    if (a.cal && a.cal_ewma > 0.f && !v && err == err) {
+      const float mu = a.cal[2 * series];
+      const float nmu = mu + a.cal_ewma * (err - mu);
+      a.cal[2 * series] = nmu;
+      a.cal[2 * series + 1] *= mu / nmu;  // the dispersion is relative to the level
+    }
     if (a.app_id) {
       const int app = a.app_id[series];
       if (v) atomicAdd(&a.app_stats[2 * app], 1);

@@ -109,6 +109,15 @@ __device__ __forceinline__ f32x16 mfma(const typename Frag<FP8>::T& a, const typ
   }
 }
 
+// Model inputs enter the fp8 B operand saturated to the e4m3 range (±448):
+// the conversion would turn an out-of-range z-score — a regressed series,
+// the very thing being detected — into NaN.  bf16 covers the fp32 range.
+template <bool FP8>
+__device__ __forceinline__ float sat_input(float v) {
+  if constexpr (FP8) return fminf(fmaxf(v, -448.f), 448.f);
+  return v;
+}
+
 // Build the B fragment for a k-step from 8 fp32 values (already scaled).
 template <bool FP8>
 __device__ __forceinline__ typename Frag<FP8>::T make_b(const float (&v)[8]) {

@@ -70,6 +70,7 @@ class LstmArgs(C.Structure):
         ("mu", C.c_float), ("sigma", C.c_float), ("threshold", C.c_void_p), ("thr_default", C.c_float),
         ("err", C.c_void_p), ("zscore", C.c_void_p), ("verdict", C.c_void_p), ("recon", C.c_void_p),
         ("app_id", C.c_void_p), ("app_stats", C.c_void_p), ("wmax", C.c_void_p), ("src", LstmRingSrc),
+        ("cal", C.c_void_p), ("cal_ewma", C.c_float),
     ]
 
 
@@ -257,9 +258,17 @@ def lstm_score(p: LstmPacked, x: Optional[torch.Tensor], mu: float = 0.0, sigma:
                threshold: Optional[torch.Tensor] = None, thr_default: float = 3.0, want_recon: bool = False,
                app_id: Optional[torch.Tensor] = None, app_stats: Optional[torch.Tensor] = None,
                out: Optional[Dict[str, torch.Tensor]] = None, ring: Optional[RingSource] = None,
-               T: Optional[int] = None) -> Dict[str, torch.Tensor]:
+               T: Optional[int] = None, cal: Optional[torch.Tensor] = None,
+               cal_ewma: float = 0.0) -> Dict[str, torch.Tensor]:
     """Score windows ``x [N, T, F]`` — or, with ``ring`` (and ``T``), the last
-    ``T`` samples of every ring row read directly by the kernel."""
+    ``T`` samples of every ring row (or the ``ring.win_series`` / ``win_start``
+    windows) read directly by the kernel.
+
+    ``cal`` ``[N, 2]`` float32 (per-window ``mu``, ``1/sigma``): the z-score is
+    the smaller of the global one (``mu``/``sigma``) and the window's own
+    series' one, so a window must be unusual for its series AND in absolute
+    terms; with ``cal_ewma > 0`` the kernel moves ``mu`` toward every
+    non-anomalous error (relative dispersion kept)."""
     lib = nat.require()
     if ring is None:
         _need(x is not None and x.is_cuda and x.dtype == torch.float32 and x.dim() == 3 and x.is_contiguous(),
@@ -268,7 +277,8 @@ def lstm_score(p: LstmPacked, x: Optional[torch.Tensor], mu: float = 0.0, sigma:
         dev = x.device
     else:
         _need(T is not None and T >= 1, "ring scoring needs the window length T")
-        N, F = ring.rings[0].shape[0], len(ring.rings)
+        F = len(ring.rings)
+        N = ring.win_series.shape[0] if ring.win_series is not None else ring.rings[0].shape[0]
         dev = ring.rings[0].device
     _need(F == p.F, f"feature mismatch {F} vs {p.F}")
     if threshold is not None:
@@ -277,6 +287,9 @@ def lstm_score(p: LstmPacked, x: Optional[torch.Tensor], mu: float = 0.0, sigma:
     if app_id is not None:
         _need(app_id.shape == (N,) and app_id.dtype == torch.int32 and app_stats is not None
               and app_stats.dtype == torch.int32 and app_stats.is_contiguous(), "app_id/app_stats")
+    if cal is not None:
+        _need(cal.shape == (N, 2) and cal.dtype == torch.float32 and cal.is_contiguous() and cal.device == dev,
+              "cal must be float32 [N, 2] (mu, 1/sigma)")
     out = {} if out is None else out
     out.setdefault("err", torch.empty(N, dtype=torch.float32, device=dev))
     out.setdefault("zscore", torch.empty(N, dtype=torch.float32, device=dev))
@@ -298,6 +311,7 @@ def lstm_score(p: LstmPacked, x: Optional[torch.Tensor], mu: float = 0.0, sigma:
     a.recon = nat.ptr(out.get("recon")) if want_recon else 0
     a.app_id, a.app_stats = nat.ptr(app_id), nat.ptr(app_stats)
     a.wmax = nat.ptr(p.wmax) if p.fp8 else 0
+    a.cal, a.cal_ewma = nat.ptr(cal), float(cal_ewma)
     nat.check(lib.fm_lstm_ae(C.byref(a), nat.stream_handle(dev)), "fm_lstm_ae")
     return out
 

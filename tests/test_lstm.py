@@ -142,6 +142,26 @@ def test_fused_lstm_kernel_matches_reference(fp8):
 
 
 @pytest.mark.gpu
+def test_fp8_scoring_saturates_out_of_range_inputs():
+    """A regressed window's z-scored inputs can exceed the fp8 e4m3 range
+    (|x / act_scale| > 448): the kernel saturates them, so the error stays
+    finite and large instead of becoming NaN (which would read as healthy)."""
+    torch.manual_seed(4)
+    dev = torch.device("cuda:0")
+    N, T, F = 64, 16, 2
+    m = lstm_ae.LSTMAutoencoder(F, 64)
+    x = torch.randn(N, T, F) * 0.5
+    x[:8, 4:] += 60.0  # x3 regression of a calm series, in z units
+    p = L.pack(m, fp8=True, device=dev)
+    out = L.lstm_score(p, x.to(dev).contiguous(), mu=1.0, sigma=1.0, thr_default=4.0)
+    torch.cuda.synchronize()
+    err = out["err"].cpu()
+    assert torch.isfinite(err).all()
+    assert float(err[:8].min()) > 10 * float(err[8:].max())
+    assert out["verdict"][:8].cpu().eq(1).all()
+
+
+@pytest.mark.gpu
 def test_device_fp8_matches_torch_ocp():
     dev = torch.device("cuda:0")
     v = torch.tensor([0.0, 1.0, -1.5, 0.3, 447.0, -240.0, 1e-3, 3.14159], device=dev)
@@ -174,6 +194,39 @@ def test_lstm_shard_cpu_streaming():
     assert out["verdict"].shape == (n,) and int(sh.app_stats[:, 1].sum()) == n
 
 
+def test_lstm_per_series_calibration_cpu():
+    """One shared model, series of very different noise: the per-series
+    calibration learns each series' own healthy error level, so a x3
+    regression of a calm series is flagged while no healthy series — noisy
+    ones included — crosses the threshold."""
+    from foremast_amd.brain.lstm_engine import LstmShard
+    n, R, T = 64, 240, 12
+    g = torch.Generator().manual_seed(7)
+    t = torch.arange(R, dtype=torch.float32)
+    noise = torch.where(torch.arange(n) % 2 == 0, 0.05, 1.5)[:, None]  # calm / noisy alternate
+    ph = torch.rand(n, 1, generator=g) * 6.28
+    hist = 10 + 3 * torch.sin(2 * np.pi * t / 48 + ph) + noise * torch.randn(n, R, generator=g)
+    torch.manual_seed(0)
+    sh = LstmShard(n, R, 1, window=T, device="cpu", app_id=torch.arange(n).int(), n_apps=n,
+                   train_batch=64, lr=1e-2, cal_windows=8)
+    sh.load_history([hist])
+    for _ in range(60):
+        sh.train_step()
+    sh.calibrate(256)
+    mu = sh.cal[:, 0]
+    assert float(mu[1::2].median()) > 3 * float(mu[0::2].median())  # noisy series reconstruct worse
+    bad = torch.tensor([0, 2, 4])
+    for k in range(8):
+        tk = torch.tensor([float(R + k)])
+        v = 10 + 3 * torch.sin(2 * np.pi * tk / 48 + ph) + noise * torch.randn(n, 1, generator=g)
+        v[bad] *= 3.0
+        sh.ingest_tick(v)
+    out = sh.score()
+    flagged = set(torch.nonzero(out["verdict"]).flatten().tolist())
+    assert set(bad.tolist()) <= flagged
+    assert len(flagged - set(bad.tolist())) <= 1
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("fp8", [False, True])
 def test_lstm_shard_gpu_matches_model(fp8):
@@ -191,9 +244,19 @@ def test_lstm_shard_gpu_matches_model(fp8):
     for k in range(5):
         sh.ingest_tick(torch.full((n, F), 10.0, device=dev))
         sh.train_step()
-    sh.calibrate(512)
+    sh.calibrate(1000)  # sampled window count != series count
+    assert sh.cal is not None and sh.cal.shape == (n, 2) and bool((sh.cal[:, 0] > 0).all())
+    cal0 = sh.cal.clone()
     out = sh.score()
     torch.cuda.synchronize()
+    # per-series z-score from the calibration in force at scoring time; the
+    # epilogue then moved mu_i of the non-flagged series toward their error
+    z_ref = torch.minimum((out["err"] - sh.mu) / sh.sigma, (out["err"] - cal0[:, 0]) * cal0[:, 1])
+    assert torch.allclose(out["zscore"], z_ref, rtol=1e-5, atol=1e-5)
+    upd = out["verdict"] == 0
+    mu_ref = torch.where(upd, cal0[:, 0] + sh.cal_ewma * (out["err"] - cal0[:, 0]), cal0[:, 0])
+    assert torch.allclose(sh.cal[:, 0], mu_ref, rtol=1e-5, atol=1e-7)
+    assert torch.allclose(sh.cal[:, 0] * sh.cal[:, 1], cal0[:, 0] * cal0[:, 1], rtol=1e-5)
     x = sh._gather(sh._all, sh._zero_off)
     with torch.no_grad():
         ref = sh.model.recon_error(x)
