@@ -14,18 +14,35 @@
 //                     is what the GPU ring buffer ingests (pinned host memory
 //                     → one H2D copy);
 //  * fm_prom_dense_keyed — the same scatter, but each series goes to the row
-//                     its (label_a, label_b) values map to (FNV-1a 64 key,
+//                     its (label_a, label_b) values map to (64-bit key,
 //                     binary search in the caller's sorted key table), so a
 //                     response for any subset of a shard's series lands in
 //                     place in one pass with no per-series Python work.
 //
-// Numbers are decoded with std::from_chars (locale independent).  Special
-// values "NaN", "+Inf", "-Inf" are accepted.  Returns < 0 on malformed input.
+//  * fm_prom_decode_tick — a whole tick: many bodies, each split at series
+//                     boundaries into chunks that a pool of native threads
+//                     decode in parallel (keyed scatter through open-addressing
+//                     key indexes, fm_keyindex_new), after a parallel NaN fill.
+//
+// Hot-path details: strings are skipped 16 bytes at a time (SSE2 compare for
+// '"' / '\\'), a series' label object is walked once for both key labels, and
+// plain decimals (<= 19 digits, no exponent — every Prometheus sample value
+// and timestamp in practice) take an exact fast path: an integer mantissa
+// below 2^53 divided by an exact power of ten is one correctly rounded IEEE
+// operation, i.e. the same double std::from_chars returns.  Anything else
+// goes through std::from_chars (locale independent).  Special values "NaN",
+// "+Inf", "-Inf" are accepted.  Returns < 0 on malformed input.
+#include <emmintrin.h>
+
+#include <algorithm>
+#include <atomic>
 #include <charconv>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <limits>
+#include <thread>
+#include <vector>
 
 namespace {
 
@@ -43,20 +60,30 @@ struct Cursor {
   }
 };
 
+// first '"' or '\\' in [p, e) (e if none), 16 bytes per step
+inline const char* find_quote_or_bs(const char* p, const char* e) {
+  const __m128i q = _mm_set1_epi8('"'), bs = _mm_set1_epi8('\\');
+  while (e - p >= 16) {
+    const __m128i v = _mm_loadu_si128((const __m128i*)p);
+    const int m = _mm_movemask_epi8(_mm_or_si128(_mm_cmpeq_epi8(v, q), _mm_cmpeq_epi8(v, bs)));
+    if (m) return p + __builtin_ctz((unsigned)m);
+    p += 16;
+  }
+  while (p < e && *p != '"' && *p != '\\') ++p;
+  return p;
+}
+
 // skip a JSON string (cursor at opening quote); returns false on error
 bool skip_string(Cursor& c) {
   if (c.p >= c.e || *c.p != '"') return false;
   ++c.p;
-  while (c.p < c.e) {
-    if (*c.p == '\\') {  // escape: the escaped byte must exist
-      if (c.e - c.p < 2) { c.p = c.e; return false; }
-      c.p += 2;
-      continue;
-    }
+  while (true) {
+    c.p = find_quote_or_bs(c.p, c.e);
+    if (c.p >= c.e) return false;
     if (*c.p == '"') { ++c.p; return true; }
-    ++c.p;
+    if (c.e - c.p < 2) { c.p = c.e; return false; }  // escape: the escaped byte must exist
+    c.p += 2;
   }
-  return false;
 }
 
 bool skip_value(Cursor& c);
@@ -102,6 +129,36 @@ bool key_is(const char* k0, const char* k1, const char* lit) {
   return (size_t)(k1 - k0) == n && memcmp(k0, lit, n) == 0;
 }
 
+constexpr double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                               1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+
+// [-]digits[.digits], at most 19 digits, mantissa <= 2^53, <= 22 fraction digits:
+// exact (see the header); false = use the general parser
+inline bool fast_decimal(const char* p, const char* b, double& out) {
+  bool neg = false;
+  if (p < b && *p == '-') { neg = true; ++p; }
+  uint64_t m = 0;
+  int nd = 0, frac = 0;
+  bool dot = false;
+  for (; p < b; ++p) {
+    const unsigned d = (unsigned)(*p - '0');
+    if (d < 10) {
+      if (++nd > 19) return false;
+      m = m * 10 + d;
+      frac += dot;
+    } else if (*p == '.' && !dot) {
+      dot = true;
+    } else {
+      return false;
+    }
+  }
+  if (nd == 0 || m > (1ull << 53) || frac > 22) return false;
+  double v = (double)m;
+  if (frac) v /= kPow10[frac];
+  out = neg ? -v : v;
+  return true;
+}
+
 bool parse_number(const char* a, const char* b, double& out) {
   while (a < b && (*a == ' ' || *a == '"')) ++a;
   while (b > a && (b[-1] == ' ' || b[-1] == '"')) --b;
@@ -113,6 +170,7 @@ bool parse_number(const char* a, const char* b, double& out) {
   }
   if (n == 4 && memcmp(a, "-Inf", 4) == 0) { out = -std::numeric_limits<double>::infinity(); return true; }
   if (*a == '+') ++a;
+  if (fast_decimal(a, b, out)) return true;
   auto r = std::from_chars(a, b, out);
   return r.ec == std::errc() && r.ptr == b;
 }
@@ -192,14 +250,35 @@ long long walk(const char* buf, long long len, OnSeries on_series, OnPoint on_po
   return nseries;
 }
 
-// FNV-1a 64 over a + 0x1f + b (foremast_amd/ingest/native.py key_hash must agree)
-uint64_t fnv_key(const char* a0, const char* a1, const char* b0, const char* b1) {
-  uint64_t h = 1469598103934665603ull;
-  auto mix = [&h](unsigned char ch) { h ^= ch; h *= 1099511628211ull; };
-  for (const char* q = a0; q < a1; ++q) mix((unsigned char)*q);
-  mix(0x1f);
-  for (const char* q = b0; q < b1; ++q) mix((unsigned char)*q);
-  return h;
+// Series key: a 64-bit word-at-a-time hash of the bytes a + 0x1f + b
+// (little-endian 8-byte words, the last one zero-padded; multiply/xorshift
+// rounds and a final avalanche).  foremast_amd/ingest/native.py key_hash must
+// agree bit for bit.  ~4 multiply rounds for a typical (app, pod) key instead
+// of FNV-1a's one serial multiply per byte.
+constexpr uint64_t kKeyMul = 0x9E3779B97F4A7C15ull;
+inline uint64_t key_round(uint64_t h, uint64_t w) {
+  h = (h ^ w) * kKeyMul;
+  return h ^ (h >> 29);
+}
+uint64_t series_key(const char* a0, const char* a1, const char* b0, const char* b1) {
+  const size_t na = (size_t)(a1 - a0), nb = (size_t)(b1 - b0), n = na + 1 + nb;
+  uint64_t h = 0x243F6A8885A308D3ull ^ (uint64_t)n;
+  unsigned char tmp[256];
+  std::vector<unsigned char> big;
+  unsigned char* buf = tmp;
+  if (n + 8 > sizeof(tmp)) { big.resize(n + 8); buf = big.data(); }
+  memcpy(buf, a0, na);
+  buf[na] = 0x1f;
+  memcpy(buf + na + 1, b0, nb);
+  memset(buf + n, 0, 8);
+  for (size_t i = 0; i < n; i += 8) {
+    uint64_t w;
+    memcpy(&w, buf + i, 8);
+    h = key_round(h, w);
+  }
+  h ^= h >> 32;
+  h *= 0xD6E8FEB86659FD93ull;
+  return h ^ (h >> 32);
 }
 
 // raw bytes of the string value of `key` inside the metric object [m0, m1)
@@ -224,6 +303,236 @@ bool label_value(const char* m0, const char* m1, const char* key, const char*& v
     if (c.eat(',')) continue;
     return false;
   }
+}
+
+// ---- keyed fast path ---------------------------------------------------------------
+
+// Open-addressing (hash -> row) index of a shard's series keys: one probe per
+// series in the common case, instead of a binary search over the sorted table.
+struct KeyIndex {
+  struct Slot { uint64_t h; long long row; };  // row < 0: empty
+  std::vector<Slot> slots;
+  uint64_t mask = 0;
+  static uint64_t mix(uint64_t h) { h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33; return h; }
+  bool build(const uint64_t* hash, const long long* rows, long long n) {
+    uint64_t cap = 16;
+    while (cap < (uint64_t)(2 * n)) cap <<= 1;
+    slots.assign(cap, Slot{0, -1});
+    mask = cap - 1;
+    for (long long j = 0; j < n; ++j) {
+      if (rows[j] < 0) return false;
+      uint64_t i = mix(hash[j]) & mask;
+      while (slots[i].row >= 0) {
+        if (slots[i].h == hash[j]) return false;  // duplicate key
+        i = (i + 1) & mask;
+      }
+      slots[i] = Slot{hash[j], rows[j]};
+    }
+    return true;
+  }
+  void prefetch(uint64_t h) const { __builtin_prefetch(&slots[mix(h) & mask]); }
+  long long find(uint64_t h) const {
+    uint64_t i = mix(h) & mask;
+    while (true) {
+      const Slot& sl = slots[i];
+      if (sl.row < 0) return -1;
+      if (sl.h == h) return sl.row;
+      i = (i + 1) & mask;
+    }
+  }
+};
+
+struct Label {
+  const char* k;
+  size_t n;
+};
+
+// Walk a flat label object {"k":"v",...} once (cursor at '{'), taking the raw
+// value spans of labels `la` and `lb` (empty when absent).  False for anything
+// else (a non-string value, malformed input): strings are skipped exactly as
+// skip_container skips them and a flat object has no brace outside them, so
+// when this succeeds it ends where brace matching would.
+bool scan_labels(Cursor& c, const Label& la, const Label& lb, const char*& a0, const char*& a1, const char*& b0,
+                 const char*& b1) {
+  a0 = a1 = b0 = b1 = "";
+  bool fa = false, fb = false;
+  if (!c.eat('{')) return false;
+  c.ws();
+  if (c.p < c.e && *c.p == '}') { ++c.p; return true; }
+  while (true) {
+    const char *k0, *k1;
+    if (!read_key(c, k0, k1)) return false;
+    c.ws();
+    if (c.p < c.e && *c.p == '"') {
+      const char* v0 = c.p + 1;
+      if (!skip_string(c)) return false;
+      const size_t kn = (size_t)(k1 - k0);
+      // first occurrence wins (as in label_value)
+      if (!fa && kn == la.n && memcmp(k0, la.k, kn) == 0) { a0 = v0; a1 = c.p - 1; fa = true; }
+      else if (!fb && kn == lb.n && memcmp(k0, lb.k, kn) == 0) { b0 = v0; b1 = c.p - 1; fb = true; }
+    } else {
+      return false;  // not a flat label object: the caller takes the general path
+    }
+    if (c.eat(',')) continue;
+    if (c.eat('}')) return true;
+    return false;
+  }
+}
+
+struct KeyedOut {
+  double start, step;
+  long long T;
+  float* out;
+  long long ld, max_rows;
+  Label la, lb;
+};
+
+struct KeyedCounts {
+  long long series = 0, dropped = 0, unmatched = 0;
+};
+
+// Decode result-array elements starting at c.p (an element's '{') into the
+// keyed dense matrix; stops after the element that ends the range (the next
+// one would start at or past `stop`) or at the array's ']'.  < 0 on error.
+// The label key's index slot is prefetched as soon as the key is hashed and
+// probed only when the first sample is stored, so the (L3 / DRAM) miss
+// overlaps the sample parsing.
+long long keyed_elements(Cursor& c, const char* stop, const KeyedOut& o, const KeyIndex& ix, KeyedCounts& k) {
+  while (true) {
+    if (!c.eat('{')) return -4;
+    long long row = -1;
+    bool have_labels = false, resolved = false;
+    uint64_t key = 0;
+    auto resolve = [&]() {
+      if (resolved) return;
+      resolved = true;
+      row = ix.find(key);
+      if (row >= o.max_rows) row = -1;
+      if (row < 0) ++k.unmatched;
+    };
+    while (true) {
+      const char *k0, *k1;
+      if (!read_key(c, k0, k1)) return -5;
+      c.ws();
+      const size_t kn = (size_t)(k1 - k0);
+      if (kn == 6 && memcmp(k0, "metric", 6) == 0 && !have_labels) {
+        const char *a0, *a1, *b0, *b1;
+        const char* m0 = c.p;
+        if (!scan_labels(c, o.la, o.lb, a0, a1, b0, b1)) {
+          // not flat: brace matching for the extent, then the lenient lookup
+          // of fm_prom_dense_keyed, so both decoders agree on any input
+          c.p = m0;
+          if (!skip_container(c, '{', '}')) return -6;
+          a0 = a1 = b0 = b1 = "";
+          label_value(m0, c.p, o.la.k, a0, a1);
+          label_value(m0, c.p, o.lb.k, b0, b1);
+        }
+        key = series_key(a0, a1, b0, b1);
+        ix.prefetch(key);
+        have_labels = true;
+      } else if ((kn == 6 && memcmp(k0, "values", 6) == 0) || (kn == 5 && memcmp(k0, "value", 5) == 0)) {
+        const bool many = kn == 6;
+        if (!have_labels) {  // values before the label object: key of an empty label set
+          key = series_key("", "", "", "");
+          have_labels = true;
+        }
+        if (many && !c.eat('[')) return -7;
+        c.ws();
+        if (!(many && c.eat(']'))) {
+          while (true) {
+            if (!c.eat('[')) return -8;
+            c.ws();
+            const char* a = c.p;
+            while (c.p < c.e && *c.p != ',') ++c.p;
+            double ts;
+            if (!parse_number(a, c.p, ts)) return -9;
+            if (!c.eat(',')) return -10;
+            c.ws();
+            const char* v0 = c.p;
+            if (c.p >= c.e) return -11;
+            if (*c.p == '"') { if (!skip_string(c)) return -11; } else { while (c.p < c.e && *c.p != ']') ++c.p; }
+            double v;
+            if (!parse_number(v0, c.p, v)) return -12;
+            if (!c.eat(']')) return -13;
+            resolve();
+            const double fi = (ts - o.start) / o.step;
+            const long long i = (long long)llround(fi);
+            if (row < 0 || i < 0 || i >= o.T || std::fabs(fi - (double)i) > 1e-6) ++k.dropped;
+            else o.out[row * o.ld + i] = (float)v;
+            if (!many) break;
+            if (c.eat(',')) continue;
+            if (c.eat(']')) break;
+            return -14;
+          }
+        }
+      } else if (!skip_value(c)) {
+        return -15;
+      }
+      if (c.eat(',')) continue;
+      if (c.eat('}')) break;
+      return -16;
+    }
+    if (!have_labels) key = series_key("", "", "", "");
+    resolve();
+    ++k.series;
+    if (c.eat(',')) {
+      c.ws();
+      if (c.p >= stop) return k.series;
+      continue;
+    }
+    if (c.eat(']')) return k.series;
+    return -17;
+  }
+}
+
+// Position just after `"result":[` (ws allowed), or null.
+const char* result_array(const char* buf, long long len) {
+  const char* end = buf + len;
+  for (const char* q = buf; q + 9 <= end; ++q) {
+    q = (const char*)memchr(q, '"', (size_t)(end - q));
+    if (!q || q + 9 > end) return nullptr;
+    if (memcmp(q, "\"result\"", 8) == 0) {
+      Cursor c{q + 8, end};
+      if (!c.eat(':') || !c.eat('[')) return nullptr;
+      return c.p;
+    }
+  }
+  return nullptr;
+}
+
+// Up to `parts` series-aligned chunk starts of a body's result array (cut[0] =
+// the first element); returns the count (0: empty array, < 0: malformed).  A
+// later cut is the first `{"metric"` at or after an even byte split whose
+// preceding non-space byte is ',' — a quote inside a JSON string is always
+// escaped, so that byte sequence cannot occur inside a label value.
+long long split_elements(const char* buf, long long len, int parts, const char** cut) {
+  const char* p = result_array(buf, len);
+  if (!p) return -1;
+  const char* end = buf + len;
+  Cursor c{p, end};
+  c.ws();
+  if (c.p >= end) return -3;
+  if (*c.p == ']') return 0;
+  cut[0] = c.p;
+  long long n = 1;
+  static const char pat[] = "{\"metric\"";
+  for (int k = 1; k < parts; ++k) {
+    const char* q = cut[0] + (end - cut[0]) * (long long)k / parts;
+    if (q <= cut[n - 1]) q = cut[n - 1] + 1;
+    while (q + 9 <= end) {
+      q = (const char*)memchr(q, '{', (size_t)(end - q));
+      if (!q || q + 9 > end) { q = end; break; }
+      if (memcmp(q, pat, 9) == 0) {
+        const char* b = q - 1;
+        while (b > cut[0] && (*b == ' ' || *b == '\n' || *b == '\r' || *b == '\t')) --b;
+        if (*b == ',') break;
+      }
+      ++q;
+    }
+    if (q + 9 > end) break;
+    cut[n++] = q;
+  }
+  return n;
 }
 
 }  // namespace
@@ -281,7 +590,7 @@ long long fm_prom_dense(const char* buf, long long len, double start, double ste
   return r;
 }
 
-// Key of every series in response order (FNV of its label_a / label_b values):
+// Key of every series in response order (series_key of its label_a / label_b values):
 // builds the KeyTable of a known response layout without per-series Python.
 long long fm_prom_keys(const char* buf, long long len, long long max_series, const char* label_a,
                        const char* label_b, uint64_t* out) {
@@ -291,13 +600,13 @@ long long fm_prom_keys(const char* buf, long long len, long long max_series, con
         const char *a0 = "", *a1 = a0, *b0 = a0, *b1 = a0;
         label_value(m0, m1, label_a, a0, a1);
         label_value(m0, m1, label_b, b0, b1);
-        if (s < max_series) out[s] = fnv_key(a0, a1, b0, b1);
+        if (s < max_series) out[s] = series_key(a0, a1, b0, b1);
       },
       [&](long long, double, double) {});
 }
 
 // Keyed dense scatter: series s goes to row key_rows[j] where key_hash[j] is the
-// FNV key of its (label_a, label_b) values (key_hash sorted ascending, n_keys
+// series_key of its (label_a, label_b) values (key_hash sorted ascending, n_keys
 // entries); unmatched series are skipped and counted in *unmatched.
 long long fm_prom_dense_keyed(const char* buf, long long len, double start, double step, long long T, float* out,
                               long long ld, long long max_rows, const char* label_a, const char* label_b,
@@ -310,7 +619,7 @@ long long fm_prom_dense_keyed(const char* buf, long long len, double start, doub
         const char *a0 = "", *a1 = a0, *b0 = a0, *b1 = a0;
         label_value(m0, m1, label_a, a0, a1);
         label_value(m0, m1, label_b, b0, b1);
-        const uint64_t h = fnv_key(a0, a1, b0, b1);
+        const uint64_t h = series_key(a0, a1, b0, b1);
         long long lo = 0, hi = n_keys;
         while (lo < hi) {
           const long long mid = (lo + hi) >> 1;
@@ -328,6 +637,145 @@ long long fm_prom_dense_keyed(const char* buf, long long len, double start, doub
   if (dropped) *dropped = drop;
   if (unmatched) *unmatched = miss;
   return r;
+}
+
+// ---- key index + parallel tick decode -----------------------------------------------
+
+void* fm_keyindex_new(const uint64_t* key_hash, const long long* key_rows, long long n_keys) {
+  KeyIndex* ix = new KeyIndex();
+  if (!ix->build(key_hash, key_rows, n_keys)) { delete ix; return nullptr; }
+  return ix;
+}
+
+void fm_keyindex_free(void* ix) { delete (KeyIndex*)ix; }
+
+// Keyed dense scatter of one body through a KeyIndex (same outputs as
+// fm_prom_dense_keyed).
+long long fm_prom_dense_indexed(const char* buf, long long len, double start, double step, long long T, float* out,
+                                long long ld, long long max_rows, const char* label_a, const char* label_b,
+                                const void* index, long long* dropped, long long* unmatched) {
+  const KeyIndex* ix = (const KeyIndex*)index;
+  const char* p = result_array(buf, len);
+  if (!p || !ix) return -1;
+  Cursor c{p, buf + len};
+  c.ws();
+  KeyedCounts k;
+  long long r = 0;
+  if (c.eat(']')) {
+    r = 0;
+  } else {
+    const KeyedOut o{start, step, T, out, ld, max_rows, {label_a, strlen(label_a)}, {label_b, strlen(label_b)}};
+    r = keyed_elements(c, buf + len + 1, o, *ix, k);
+  }
+  if (dropped) *dropped = k.dropped;
+  if (unmatched) *unmatched = k.unmatched;
+  return r;
+}
+
+// One tick: `nb` bodies (body j keyed by index[j]) scattered into `out`
+// ([max_rows, ld] float32, columns [0, T) on the (start, step) grid) by
+// `threads` native threads.  With fill_nan the rows are first set to NaN (in
+// parallel); otherwise the caller pre-fills them.  Each body is split at series boundaries into chunks sized so
+// the pool stays balanced; stats[3j..3j+2] = (series, dropped points,
+// unmatched series) of body j, or stats[3j] < 0 when body j is malformed.
+// Returns 0, or the first negative code.
+long long fm_prom_decode_tick(int nb, const char* const* bufs, const long long* lens, const void* const* index,
+                              const char* label_a, const char* label_b, double start, double step, long long T,
+                              float* out, long long ld, long long max_rows, int threads, int fill_nan,
+                              long long* stats) {
+  if (nb < 0 || threads < 1) return -1;
+  threads = std::min(threads, 256);
+  struct Task { int body; const char* p; const char* stop; const char* end = nullptr; };
+  std::vector<Task> tasks;
+  long long total = 0;
+  for (int j = 0; j < nb; ++j) total += std::max(0ll, lens[j]);
+  const long long target = std::max(1ll, total / (4ll * threads));  // ~4 chunks per thread
+  std::vector<long long> code(nb, 0);
+  for (int j = 0; j < nb; ++j) {
+    if (!index[j]) { code[j] = -1; continue; }
+    const int parts = (int)std::min<long long>(4096, std::max(1ll, lens[j] / target));
+    std::vector<const char*> cut(parts + 1);
+    const long long n = split_elements(bufs[j], lens[j], parts, cut.data());
+    if (n < 0) { code[j] = n; continue; }
+    for (long long i = 0; i < n; ++i)
+      tasks.push_back(Task{j, cut[i], i + 1 < n ? cut[i + 1] : bufs[j] + lens[j] + 1});
+  }
+  const Label la{label_a, strlen(label_a)}, lb{label_b, strlen(label_b)};
+  std::vector<std::atomic<long long>> acc(3 * (size_t)std::max(nb, 1));
+  for (auto& a : acc) a.store(0);
+  std::vector<std::atomic<long long>> err(std::max(nb, 1));
+  for (auto& a : err) a.store(0);
+  std::atomic<long long> next{0};
+  std::atomic<long long> fill_next{0};
+  const long long rows_per = 4096;
+  auto work = [&]() {
+    if (fill_nan) {
+      const float nan = std::numeric_limits<float>::quiet_NaN();
+      while (true) {
+        const long long r0 = fill_next.fetch_add(rows_per);
+        if (r0 >= max_rows) break;
+        const long long r1 = std::min(max_rows, r0 + rows_per);
+        for (long long r = r0; r < r1; ++r) std::fill(out + r * ld, out + r * ld + T, nan);
+      }
+    }
+  };
+  auto parse = [&]() {
+    while (true) {
+      const long long t = next.fetch_add(1);
+      if (t >= (long long)tasks.size()) break;
+      Task& tk = tasks[t];
+      const int j = tk.body;
+      const KeyIndex* ix = (const KeyIndex*)index[j];
+      Cursor c{tk.p, bufs[j] + lens[j]};
+      KeyedCounts k;
+      const KeyedOut o{start, step, T, out, ld, max_rows, la, lb};
+      const long long r = keyed_elements(c, tk.stop, o, *ix, k);
+      if (r < 0) { err[j].store(1); continue; }
+      tk.end = c.p;
+      acc[3 * j].fetch_add(k.series);
+      acc[3 * j + 1].fetch_add(k.dropped);
+      acc[3 * j + 2].fetch_add(k.unmatched);
+    }
+  };
+  auto run = [&](auto fn) {
+    std::vector<std::thread> pool;
+    pool.reserve(threads - 1);
+    for (int i = 1; i < threads; ++i) pool.emplace_back(fn);
+    fn();
+    for (auto& th : pool) th.join();
+  };
+  if (fill_nan) run(work);
+  if (!tasks.empty()) run(parse);
+  // Every chunk but a body's last must have stopped exactly at the next cut.
+  // A failed chunk, or one that did not (a cut that was not an element of the
+  // result array — impossible in a Prometheus body, possible in malformed or
+  // foreign JSON), makes the body's result that of a sequential decode, after
+  // its rows (every row its key index maps to, the only rows a chunk can
+  // write) are reset to NaN.
+  for (size_t t = 0; t + 1 < tasks.size(); ++t) {
+    const int j = tasks[t].body;
+    if (tasks[t + 1].body == j && tasks[t].end != tasks[t + 1].p) err[j].store(1);
+  }
+  const float nanf = std::numeric_limits<float>::quiet_NaN();
+  for (int j = 0; j < nb; ++j) {
+    if (err[j].load() != 1) continue;
+    for (const auto& sl : ((const KeyIndex*)index[j])->slots)
+      if (sl.row >= 0 && sl.row < max_rows) std::fill(out + sl.row * ld, out + sl.row * ld + T, nanf);
+    long long dr = 0, um = 0;
+    const long long r = fm_prom_dense_indexed(bufs[j], lens[j], start, step, T, out, ld, max_rows, label_a, label_b,
+                                              index[j], &dr, &um);
+    err[j].store(r < 0 ? r : 0);
+    acc[3 * j].store(r < 0 ? 0 : r);
+    acc[3 * j + 1].store(dr);
+    acc[3 * j + 2].store(um);
+  }
+  long long rc = 0;
+  for (int j = 0; j < nb; ++j) {
+    const long long s0 = code[j] < 0 ? code[j] : (err[j].load() < 0 ? err[j].load() : acc[3 * j].load());
+    if (stats) { stats[3 * j] = s0; stats[3 * j + 1] = acc[3 * j + 1].load(); stats[3 * j + 2] = acc[3 * j + 2].load(); }
+    if (s0 < 0 && rc == 0) rc = s0;
+  }
+  return rc;
 }
 
 }  // extern "C"

@@ -9,7 +9,9 @@
 // per-series outputs, fill, dense scatter into a guarded matrix.  Each input
 // is copied into an exactly-sized heap buffer so any read past `len` is an
 // ASan report.  Exit status 0 = no sanitizer finding and consistent counts.
+#include <algorithm>
 #include <cstdio>
+#include <limits>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -68,6 +70,63 @@ void run_one(const std::string& body, long long& checks) {
     fm_prom_dense(buf, len, 1700000000.0, 60.0, T, dense.data() + ld, ld, 0, rows, &dropped);
     for (long long j = 0; j < ld; ++j)
       if (dense[j] != -7.f || dense[(rows + 1) * ld + j] != -7.f) { std::fprintf(stderr, "dense guard hit\n"); std::exit(3); }
+    // keyed paths: binary-search table, key index, threaded tick decode (the body
+    // twice, so it is split into chunks) must agree on a guarded matrix
+    if (n > 0) {
+      std::vector<uint64_t> keys(n);
+      fm_prom_keys(buf, len, n, "__name__", "pod", keys.data());
+      std::vector<uint64_t> hs;
+      std::vector<long long> rws;
+      for (long long i = 0; i < n; ++i)
+        if (std::find(hs.begin(), hs.end(), keys[i]) == hs.end()) { hs.push_back(keys[i]); rws.push_back((long long)hs.size() - 1); }
+      std::vector<size_t> ord(hs.size());
+      for (size_t i = 0; i < ord.size(); ++i) ord[i] = i;
+      std::sort(ord.begin(), ord.end(), [&](size_t x, size_t y) { return hs[x] < hs[y]; });
+      std::vector<uint64_t> sh;
+      std::vector<long long> sr;
+      for (size_t i : ord) { sh.push_back(hs[i]); sr.push_back(rws[i]); }
+      const long long kr = (long long)hs.size();
+      void* ix = fm_keyindex_new(sh.data(), sr.data(), kr);
+      if (!ix) { std::fprintf(stderr, "key index build failed\n"); std::exit(3); }
+      // guard rows -7, body rows NaN (the tick decoder resets a re-decoded body's rows to NaN)
+      std::vector<float> m1((kr + 2) * ld, -7.f), m2((kr + 2) * ld, -7.f), m3((kr + 2) * ld, -7.f);
+      for (long long q = ld; q < (kr + 1) * ld; ++q) m1[q] = m2[q] = m3[q] = std::numeric_limits<float>::quiet_NaN();
+      long long d1 = 0, u1 = 0, d2 = 0, u2 = 0;
+      const long long r1 = fm_prom_dense_keyed(buf, len, 1700000000.0, 60.0, T, m1.data() + ld, ld, kr, "__name__",
+                                               "pod", sh.data(), sr.data(), kr, &d1, &u1);
+      const long long r2 = fm_prom_dense_indexed(buf, len, 1700000000.0, 60.0, T, m2.data() + ld, ld, kr, "__name__",
+                                                 "pod", ix, &d2, &u2);
+      // the body twice, keyed to disjoint row blocks [0, kr) and [kr, 2kr)
+      std::vector<long long> sr2(sr);
+      for (auto& x : sr2) x += kr;
+      void* ix2 = fm_keyindex_new(sh.data(), sr2.data(), kr);
+      m3.assign((2 * kr + 2) * ld, std::numeric_limits<float>::quiet_NaN());
+      for (long long j = 0; j < ld; ++j) m3[j] = m3[(2 * kr + 1) * ld + j] = -7.f;
+      const char* bufs[2] = {buf, buf};
+      const long long lens[2] = {len, len};
+      const void* ixs[2] = {ix, ix2};
+      long long st[6];
+      fm_prom_decode_tick(2, bufs, lens, ixs, "__name__", "pod", 1700000000.0, 60.0, T, m3.data() + ld, ld, 2 * kr, 3,
+                          0, st);
+      for (long long j = 0; j < ld; ++j)
+        if (m2[j] != -7.f || m2[(kr + 1) * ld + j] != -7.f || m3[j] != -7.f || m3[(2 * kr + 1) * ld + j] != -7.f) {
+          std::fprintf(stderr, "keyed guard hit\n"); std::exit(3);
+        }
+      // a key that occurs twice in one body may land in two chunks: which of its
+      // values survives is then unspecified, so bodies with repeated keys only
+      // get the guard and error-code checks
+      const bool unique = kr == n;
+      if (r1 >= 0 && (r2 != r1 || d2 != d1 || u2 != u1 || std::memcmp(m1.data(), m2.data(), m1.size() * 4) != 0)) {
+        std::fprintf(stderr, "indexed decode disagrees with the table decode\n"); std::exit(3);
+      }
+      if (r2 >= 0 && (st[0] != r2 || st[3] != r2 || st[1] != d2 || st[2] != u2 ||
+                      (unique && (std::memcmp(m2.data() + ld, m3.data() + ld, kr * ld * 4) != 0 ||
+                                  std::memcmp(m2.data() + ld, m3.data() + (kr + 1) * ld, kr * ld * 4) != 0)))) {
+        std::fprintf(stderr, "tick decode disagrees with the indexed decode\n"); std::exit(3);
+      }
+      fm_keyindex_free(ix);
+      fm_keyindex_free(ix2);
+    }
     ++checks;
   }
   std::free(buf);
@@ -96,9 +155,19 @@ int main(int argc, char** argv) {
   const long long iters = argc > 1 ? std::atoll(argv[1]) : 20000;
   Rng r{0x9E3779B97F4A7C15ull};
   long long checks = 0;
-  for (const char* s : kSeeds) run_one(s, checks);
-  const int nseeds = (int)(sizeof(kSeeds) / sizeof(kSeeds[0]));
-  for (long long it = 0; it < iters; ++it) run_one(mutate(kSeeds[r.below(nseeds)], r), checks);
-  std::printf("fuzz OK: %lld inputs, %lld parsed\n", iters + nseeds, checks);
+  std::vector<std::string> seeds(kSeeds, kSeeds + sizeof(kSeeds) / sizeof(kSeeds[0]));
+  // a body with enough series that the tick decoder splits it into chunks
+  std::string many = R"({"status":"success","data":{"resultType":"matrix","result":[)";
+  for (int i = 0; i < 24; ++i) {
+    if (i) many += (i % 5 == 0) ? ",\n " : ",";
+    many += R"({"metric":{"__name__":"m","pod":"p-)" + std::to_string(i) + R"("},"values":[[1700000000,")" +
+            std::to_string(i) + R"(.25"],[1700000060,")" + std::to_string(2 * i) + R"("]]})";
+  }
+  many += "]}}";
+  seeds.push_back(many);
+  for (const auto& s : seeds) run_one(s, checks);
+  const unsigned nseeds = (unsigned)seeds.size();
+  for (long long it = 0; it < iters; ++it) run_one(mutate(seeds[r.below(nseeds)], r), checks);
+  std::printf("fuzz OK: %lld inputs, %lld parsed\n", iters + (long long)nseeds, checks);
   return 0;
 }

@@ -72,6 +72,16 @@ def _load() -> Optional[C.CDLL]:
         lib.fm_prom_dense_keyed.restype = LL
         lib.fm_prom_keys.argtypes = [C.c_char_p, LL, LL, C.c_char_p, C.c_char_p, P]
         lib.fm_prom_keys.restype = LL
+        lib.fm_keyindex_new.argtypes = [P, P, LL]
+        lib.fm_keyindex_new.restype = P
+        lib.fm_keyindex_free.argtypes = [P]
+        lib.fm_keyindex_free.restype = None
+        lib.fm_prom_dense_indexed.argtypes = [C.c_char_p, LL, C.c_double, C.c_double, LL, P, LL, LL, C.c_char_p,
+                                              C.c_char_p, P, P, P]
+        lib.fm_prom_dense_indexed.restype = LL
+        lib.fm_prom_decode_tick.argtypes = [C.c_int, P, P, P, C.c_char_p, C.c_char_p, C.c_double, C.c_double, LL,
+                                            P, LL, LL, C.c_int, C.c_int, P]
+        lib.fm_prom_decode_tick.restype = LL
         _lib = lib
         return lib
 
@@ -150,13 +160,22 @@ def parse_dense(body: bytes, start: float, step: float, T: int, out: np.ndarray,
     return int(n), int(dropped.value)
 
 
+_M64 = 0xFFFFFFFFFFFFFFFF
+
+
 def key_hash(a: str, b: str) -> int:
-    """FNV-1a 64 of ``a + 0x1f + b`` (UTF-8) — the row key of a series in
-    :func:`parse_dense_keyed` (``prom_parse.cpp fnv_key``)."""
-    h = 1469598103934665603
-    for ch in a.encode() + b"\x1f" + b.encode():
-        h = ((h ^ ch) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
-    return h
+    """64-bit key of ``a + 0x1f + b`` (UTF-8) — the row key of a series in
+    :func:`parse_dense_keyed`; bit-identical to ``prom_parse.cpp series_key``
+    (8-byte little-endian words, multiply/xorshift rounds, final avalanche)."""
+    data = a.encode() + b"\x1f" + b.encode()
+    h = 0x243F6A8885A308D3 ^ len(data)
+    pad = data + b"\0" * (-len(data) % 8)
+    for i in range(0, len(pad), 8):
+        h = ((h ^ int.from_bytes(pad[i:i + 8], "little")) * 0x9E3779B97F4A7C15) & _M64
+        h ^= h >> 29
+    h ^= h >> 32
+    h = (h * 0xD6E8FEB86659FD93) & _M64
+    return h ^ (h >> 32)
 
 
 class KeyTable:
@@ -185,9 +204,31 @@ class KeyTable:
     def __len__(self) -> int:
         return len(self.rows)
 
+    @property
+    def index(self) -> int:
+        """Native open-addressing (hash → row) index of this table (built on
+        first use; one probe per series instead of a binary search)."""
+        ix = getattr(self, "_index", None)
+        if ix is None:
+            lib = _load()
+            if lib is None:
+                raise RuntimeError("native ingest library unavailable")
+            ix = lib.fm_keyindex_new(self.hash.ctypes.data, self.rows.ctypes.data, len(self.rows))
+            if not ix:
+                raise ValueError("series key hash collision or negative row")
+            self._index = ix
+            self._lib = lib
+        return ix
+
+    def __del__(self) -> None:
+        ix = getattr(self, "_index", None)
+        if ix:
+            self._lib.fm_keyindex_free(ix)
+            self._index = None
+
 
 def series_keys(body: bytes, label_a: str = "namespace", label_b: str = "app") -> np.ndarray:
-    """FNV key of every series of a response, in response order (uint64)."""
+    """Key (:func:`key_hash`) of every series of a response, in response order (uint64)."""
     if isinstance(body, str):
         body = body.encode()
     lib = _load()
@@ -234,12 +275,46 @@ def parse_dense_keyed(body: bytes, start: float, step: float, T: int, out: np.nd
     dropped, unmatched = C.c_longlong(0), C.c_longlong(0)
     ld = out.strides[0] // 4
     base = out.ctypes.data + 4 * col0
-    n = lib.fm_prom_dense_keyed(body, len(body), float(start), float(step), int(T), base, ld, out.shape[0],
-                                table.label_a, table.label_b, table.hash.ctypes.data, table.rows.ctypes.data,
-                                len(table), C.byref(dropped), C.byref(unmatched))
+    n = lib.fm_prom_dense_indexed(body, len(body), float(start), float(step), int(T), base, ld, out.shape[0],
+                                  table.label_a, table.label_b, table.index, C.byref(dropped), C.byref(unmatched))
     if n < 0:
         raise ParseError(f"malformed query_range body (code {n})")
     return int(n), int(dropped.value), int(unmatched.value)
+
+
+def decode_tick(bodies, tables, start: float, step: float, T: int, out: np.ndarray, threads: int = 8,
+                fill_nan: bool = True) -> List[Tuple[int, int, int]]:
+    """Keyed scatter of a whole tick (body j through ``tables[j]``) into
+    ``out`` (float32 ``[rows, >= T]``, unit column stride) by ``threads``
+    native threads — each body split at series boundaries so the pool stays
+    balanced — after a parallel NaN fill of the ``T`` columns.  One call,
+    GIL released throughout.  Returns ``(series, dropped, unmatched)`` per body."""
+    if len(bodies) != len(tables):
+        raise ValueError(f"{len(bodies)} bodies for {len(tables)} key tables")
+    if out.dtype != np.float32 or out.ndim != 2 or out.shape[1] < T or out.strides[1] != 4:
+        raise ValueError("out must be float32 [rows, >= T] with unit column stride")
+    bodies = [b.encode() if isinstance(b, str) else b for b in bodies]
+    for b in bodies:
+        _check_status(b)
+    lib = _load()
+    labels = {(t.label_a, t.label_b) for t in tables}
+    if lib is None or len(labels) > 1:
+        if fill_nan:
+            out[:, :T] = np.nan
+        return [parse_dense_keyed(b, start, step, T, out, t) for b, t in zip(bodies, tables)]
+    nb = len(bodies)
+    bufs = (C.c_char_p * nb)(*bodies)
+    lens = (C.c_longlong * nb)(*[len(b) for b in bodies])
+    idx = (C.c_void_p * nb)(*[t.index for t in tables])
+    stats = np.zeros(3 * max(nb, 1), dtype=np.int64)
+    la, lb = next(iter(labels)) if labels else (b"", b"")
+    rc = lib.fm_prom_decode_tick(nb, C.cast(bufs, C.c_void_p), C.cast(lens, C.c_void_p), C.cast(idx, C.c_void_p),
+                                 la, lb, float(start), float(step), int(T), out.ctypes.data, out.strides[0] // 4,
+                                 out.shape[0], int(max(1, threads)), int(fill_nan), stats.ctypes.data)
+    if rc < 0:
+        bad = [j for j in range(nb) if stats[3 * j] < 0]
+        raise ParseError(f"malformed query_range body {bad[:1]} (code {rc})")
+    return [(int(stats[3 * j]), int(stats[3 * j + 1]), int(stats[3 * j + 2])) for j in range(nb)]
 
 
 def _parse_py(body: bytes):

@@ -5,10 +5,12 @@ A 100k-series canary tick at one point per pod and minute is ~1M series in
 set; ~140 MB of JSON).  :class:`TickDecoder` turns them into the ``[rows,
 cols]`` float32 block the tick-ingest kernel reads:
 
-* every body is decoded by the native keyed scatter
-  (:func:`~foremast_amd.ingest.native.parse_dense_keyed`) straight into its
-  rows of a pinned staging block — the ctypes call releases the GIL, so the
-  bodies decode on a thread pool in parallel;
+* the whole tick is ONE native call
+  (:func:`~foremast_amd.ingest.native.decode_tick`): a pool of C++ threads
+  NaN-fills the pinned staging block, then decodes every body — split at
+  series boundaries into ~4 chunks per thread, so one large body does not
+  serialise the tick — scattering each series into its row through an
+  open-addressing key index (the ctypes call releases the GIL);
 * two staging blocks alternate: tick k+1 decodes on the CPU while the GPU
   scores tick k (the caller submits k+1 right after enqueueing tick k's H2D
   copy; block k is reused by tick k+2, after tick k's copy has completed).
@@ -36,7 +38,7 @@ class TickDecoder:
             t = torch.empty((rows, cols), dtype=torch.float32)
             self.bufs.append(t.pin_memory() if pinned else t)
         self.views = [b.numpy() for b in self.bufs]
-        self.pool = ThreadPoolExecutor(max_workers=max(1, threads), thread_name_prefix="tick-decode")
+        self.threads = max(1, threads)
         self.coord = ThreadPoolExecutor(max_workers=1, thread_name_prefix="tick-decode-coord")
         self.i = 0
         self.last_decode_ms = 0.0
@@ -44,10 +46,7 @@ class TickDecoder:
     def _decode(self, slot: int, bodies: Sequence[bytes], start: float, step: float):
         out = self.views[slot]
         t0 = time.perf_counter()
-        out.fill(np.nan)
-        futs = [self.pool.submit(native.parse_dense_keyed, b, start, step, self.cols, out, t)
-                for b, t in zip(bodies, self.tables)]
-        stats = [f.result() for f in futs]
+        stats = native.decode_tick(bodies, self.tables, start, step, self.cols, out, threads=self.threads)
         self.last_decode_ms = (time.perf_counter() - t0) * 1e3
         return self.bufs[slot], stats
 
@@ -66,7 +65,6 @@ class TickDecoder:
 
     def close(self) -> None:
         self.coord.shutdown(wait=True)
-        self.pool.shutdown(wait=True)
 
 
 def pod_matrix_body(metric: str, labels: Sequence[str], ts: float, values: np.ndarray) -> bytes:
