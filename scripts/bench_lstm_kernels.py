@@ -33,7 +33,7 @@ def main():
     B, T, F = int(os.environ.get("B", 4096)), int(os.environ.get("T", 32)), int(os.environ.get("F", 1))
     m = LSTMAutoencoder(F, 64).to(dev)
     x = torch.randn(B, T, F, device=dev)
-    for variant in (0, 1):
+    for variant in (() if os.environ.get("SKIP_TRAIN") else (0, 1)):
         fg = FusedLstmGrad(B, T, F, dev, variant=variant)
         for ph, name in [(15, "all"), (1, "enc_fwd"), (2, "dec_fwd"), (3, "fwd"), (4, "dec_bwd"), (8, "enc_bwd")]:
             fg.phases = ph
@@ -44,13 +44,13 @@ def main():
             fg.batched_gemm = bg
             print(json.dumps({"kernel": "lstm_train+gemms", "variant": variant, "batched_gemm": bg, "B": B, "T": T,
                               "ms": round(timeit(lambda: fg.grads(m, x)), 4)}))
-    N = int(os.environ.get("N", 100000))
-    xs = torch.randn(N, T, F, device=dev)
-    for fp8 in (False, True):
-        p = L.pack(m, fp8=fp8, device=dev)
-        out = {}
-        ms = timeit(lambda: L.lstm_score(p, xs, out=out))
-        print(json.dumps({"kernel": "lstm_score", "fp8": fp8, "N": N, "T": T, "ms": round(ms, 4)}))
+    for N in [int(v) for v in os.environ.get("N", "100000").split(",")]:  # N=a,b,c: a scoring-size sweep
+        xs = torch.randn(N, T, F, device=dev)
+        for fp8 in (False, True):
+            p = L.pack(m, fp8=fp8, device=dev)
+            out = {}
+            ms = timeit(lambda: L.lstm_score(p, xs, out=out))
+            print(json.dumps({"kernel": "lstm_score", "fp8": fp8, "N": N, "T": T, "ms": round(ms, 4)}))
 
 
 if __name__ == "__main__":
