@@ -309,38 +309,106 @@ bool label_value(const char* m0, const char* m1, const char* key, const char*& v
 
 // Open-addressing (hash -> row) index of a shard's series keys: one probe per
 // series in the common case, instead of a binary search over the sorted table.
+//
+// It also learns the response LAYOUT: a Prometheus response lists the same
+// series in the same (label-sorted) order tick after tick, so for every key
+// the index remembers the label object that FOLLOWED it last time (its length,
+// a 64-bit hash of its bytes and its slot).  When the next element's label
+// bytes hash to the remembered value, its row is known without parsing the
+// labels, hashing the key or probing the table.  The remembered record is
+// self-checking (the tag folds in the slot and length), so a record torn by a
+// concurrent writer (possible only for a key repeated within one body) fails
+// the check and falls back to the full path.
 struct KeyIndex {
-  struct Slot { uint64_t h; long long row; };  // row < 0: empty
+  // one 32-byte slot per key: the key, its row and what followed it last time
+  // (`nx_*`: the next element's label-object length, its row, its slot, and
+  // the self-checking tag) — the prediction for the next element sits in the
+  // cache line the current element already brought in
+  struct Slot {
+    uint64_t h;
+    uint64_t nx_tag;
+    int32_t row;     // < 0: empty
+    int32_t nx_slot;
+    int32_t nx_row;
+    uint32_t nx_len; // 0: nothing learned
+  };
   std::vector<Slot> slots;
   uint64_t mask = 0;
   static uint64_t mix(uint64_t h) { h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33; return h; }
   bool build(const uint64_t* hash, const long long* rows, long long n) {
     uint64_t cap = 16;
     while (cap < (uint64_t)(2 * n)) cap <<= 1;
-    slots.assign(cap, Slot{0, -1});
+    slots.assign(cap, Slot{0, 0, -1, -1, -1, 0});
     mask = cap - 1;
     for (long long j = 0; j < n; ++j) {
-      if (rows[j] < 0) return false;
+      if (rows[j] < 0 || rows[j] > 0x7fffffffll) return false;
       uint64_t i = mix(hash[j]) & mask;
       while (slots[i].row >= 0) {
         if (slots[i].h == hash[j]) return false;  // duplicate key
         i = (i + 1) & mask;
       }
-      slots[i] = Slot{hash[j], rows[j]};
+      slots[i] = Slot{hash[j], 0, (int32_t)rows[j], -1, -1, 0};
     }
     return true;
   }
   void prefetch(uint64_t h) const { __builtin_prefetch(&slots[mix(h) & mask]); }
-  long long find(uint64_t h) const {
+  void prefetch_slot(long long i) const { __builtin_prefetch(&slots[i]); }
+  long long find_slot(uint64_t h) const {
     uint64_t i = mix(h) & mask;
     while (true) {
       const Slot& sl = slots[i];
       if (sl.row < 0) return -1;
-      if (sl.h == h) return sl.row;
+      if (sl.h == h) return (long long)i;
       i = (i + 1) & mask;
     }
   }
+  long long find(uint64_t h) const {
+    const long long i = find_slot(h);
+    return i < 0 ? -1 : slots[i].row;
+  }
+  static uint64_t tag_of(uint64_t bytes_hash, uint32_t len, int32_t slot, int32_t row) {
+    return bytes_hash ^ mix(((uint64_t)len << 32) ^ (uint32_t)slot ^ ((uint64_t)(uint32_t)row << 20) ^ 0x5bd1e995ull);
+  }
+  // record / predict the element that follows the key in slot `prev`
+  void learn(long long prev, uint64_t bytes_hash, uint32_t len, int32_t slot) {
+    Slot& n = slots[prev];
+    const int32_t row = slots[slot].row;
+    __atomic_store_n(&n.nx_slot, slot, __ATOMIC_RELAXED);
+    __atomic_store_n(&n.nx_row, row, __ATOMIC_RELAXED);
+    __atomic_store_n(&n.nx_len, len, __ATOMIC_RELAXED);
+    __atomic_store_n(&n.nx_tag, tag_of(bytes_hash, len, slot, row), __ATOMIC_RELAXED);
+  }
+  bool predict(long long prev, uint32_t& len, int32_t& slot, int32_t& row, uint64_t& tag) const {
+    const Slot& n = slots[prev];
+    tag = __atomic_load_n(&n.nx_tag, __ATOMIC_RELAXED);
+    len = __atomic_load_n(&n.nx_len, __ATOMIC_RELAXED);
+    slot = __atomic_load_n(&n.nx_slot, __ATOMIC_RELAXED);
+    row = __atomic_load_n(&n.nx_row, __ATOMIC_RELAXED);
+    return len > 0 && slot >= 0 && (uint64_t)slot <= mask && row >= 0;
+  }
 };
+
+// 64-bit hash of a byte span (two independent multiply lanes, 16 bytes per round)
+inline uint64_t bytes_hash(const char* p, size_t n) {
+  uint64_t a = 0x9E3779B97F4A7C15ull ^ n, b = 0xC2B2AE3D27D4EB4Full;
+  size_t i = 0;
+  for (; i + 16 <= n; i += 16) {
+    uint64_t w0, w1;
+    memcpy(&w0, p + i, 8);
+    memcpy(&w1, p + i + 8, 8);
+    a = (a ^ w0) * 0x9E3779B97F4A7C15ull;
+    b = (b ^ w1) * 0xC2B2AE3D27D4EB4Full;
+    a ^= a >> 29;
+    b ^= b >> 31;
+  }
+  if (i < n) {
+    uint64_t w[2] = {0, 0};
+    memcpy(w, p + i, n - i);
+    a = (a ^ w[0]) * 0x9E3779B97F4A7C15ull;
+    b = (b ^ w[1]) * 0xC2B2AE3D27D4EB4Full;
+  }
+  return KeyIndex::mix(a ^ ((b << 17) | (b >> 47)));
+}
 
 struct Label {
   const char* k;
@@ -397,18 +465,23 @@ struct KeyedCounts {
 // The label key's index slot is prefetched as soon as the key is hashed and
 // probed only when the first sample is stored, so the (L3 / DRAM) miss
 // overlaps the sample parsing.
-long long keyed_elements(Cursor& c, const char* stop, const KeyedOut& o, const KeyIndex& ix, KeyedCounts& k) {
+long long keyed_elements(Cursor& c, const char* stop, const KeyedOut& o, KeyIndex& ix, KeyedCounts& k) {
+  long long prev_slot = -1;  // slot of the previous element of this chunk (-1: unknown / not flat)
   while (true) {
     if (!c.eat('{')) return -4;
-    long long row = -1;
-    bool have_labels = false, resolved = false;
+    long long row = -1, cur_slot = -1;
+    bool have_labels = false, resolved = false, flat = false;
     uint64_t key = 0;
+    const char* lab0 = nullptr;
+    uint32_t lab_len = 0;
     auto resolve = [&]() {
       if (resolved) return;
       resolved = true;
-      row = ix.find(key);
+      cur_slot = ix.find_slot(key);
+      row = cur_slot < 0 ? -1 : ix.slots[cur_slot].row;
       if (row >= o.max_rows) row = -1;
-      if (row < 0) ++k.unmatched;
+      if (row < 0) { ++k.unmatched; cur_slot = -1; return; }
+      if (flat && prev_slot >= 0) ix.learn(prev_slot, bytes_hash(lab0, lab_len), lab_len, (int32_t)cur_slot);
     };
     while (true) {
       const char *k0, *k1;
@@ -418,18 +491,37 @@ long long keyed_elements(Cursor& c, const char* stop, const KeyedOut& o, const K
       if (kn == 6 && memcmp(k0, "metric", 6) == 0 && !have_labels) {
         const char *a0, *a1, *b0, *b1;
         const char* m0 = c.p;
-        if (!scan_labels(c, o.la, o.lb, a0, a1, b0, b1)) {
-          // not flat: brace matching for the extent, then the lenient lookup
-          // of fm_prom_dense_keyed, so both decoders agree on any input
-          c.p = m0;
-          if (!skip_container(c, '{', '}')) return -6;
-          a0 = a1 = b0 = b1 = "";
-          label_value(m0, c.p, o.la.k, a0, a1);
-          label_value(m0, c.p, o.lb.k, b0, b1);
-        }
-        key = series_key(a0, a1, b0, b1);
-        ix.prefetch(key);
         have_labels = true;
+        // layout prediction: the label object that followed the previous key last time
+        uint32_t plen;
+        int32_t pslot, prow;
+        uint64_t ptag;
+        if (prev_slot >= 0 && ix.predict(prev_slot, plen, pslot, prow, ptag) && (size_t)(c.e - m0) >= plen &&
+            m0[plen - 1] == '}' && KeyIndex::tag_of(bytes_hash(m0, plen), plen, pslot, prow) == ptag) {
+          c.p = m0 + plen;
+          cur_slot = pslot;
+          ix.prefetch_slot(pslot);  // the next element's prediction, needed after the samples
+          row = prow;
+          if (row >= o.max_rows) { row = -1; ++k.unmatched; cur_slot = -1; }
+          resolved = true;
+          flat = true;
+        } else {
+          if (scan_labels(c, o.la, o.lb, a0, a1, b0, b1)) {
+            flat = true;  // learnable: the next tick can predict this label object
+            lab0 = m0;
+            lab_len = (uint32_t)(c.p - m0);
+          } else {
+            // not flat: brace matching for the extent, then the lenient lookup
+            // of fm_prom_dense_keyed, so both decoders agree on any input
+            c.p = m0;
+            if (!skip_container(c, '{', '}')) return -6;
+            a0 = a1 = b0 = b1 = "";
+            label_value(m0, c.p, o.la.k, a0, a1);
+            label_value(m0, c.p, o.lb.k, b0, b1);
+          }
+          key = series_key(a0, a1, b0, b1);
+          ix.prefetch(key);
+        }
       } else if ((kn == 6 && memcmp(k0, "values", 6) == 0) || (kn == 5 && memcmp(k0, "value", 5) == 0)) {
         const bool many = kn == 6;
         if (!have_labels) {  // values before the label object: key of an empty label set
@@ -474,6 +566,7 @@ long long keyed_elements(Cursor& c, const char* stop, const KeyedOut& o, const K
     }
     if (!have_labels) key = series_key("", "", "", "");
     resolve();
+    prev_slot = flat ? cur_slot : -1;
     ++k.series;
     if (c.eat(',')) {
       c.ws();
@@ -653,8 +746,8 @@ void fm_keyindex_free(void* ix) { delete (KeyIndex*)ix; }
 // fm_prom_dense_keyed).
 long long fm_prom_dense_indexed(const char* buf, long long len, double start, double step, long long T, float* out,
                                 long long ld, long long max_rows, const char* label_a, const char* label_b,
-                                const void* index, long long* dropped, long long* unmatched) {
-  const KeyIndex* ix = (const KeyIndex*)index;
+                                void* index, long long* dropped, long long* unmatched) {
+  KeyIndex* ix = (KeyIndex*)index;
   const char* p = result_array(buf, len);
   if (!p || !ix) return -1;
   Cursor c{p, buf + len};
@@ -679,7 +772,7 @@ long long fm_prom_dense_indexed(const char* buf, long long len, double start, do
 // the pool stays balanced; stats[3j..3j+2] = (series, dropped points,
 // unmatched series) of body j, or stats[3j] < 0 when body j is malformed.
 // Returns 0, or the first negative code.
-long long fm_prom_decode_tick(int nb, const char* const* bufs, const long long* lens, const void* const* index,
+long long fm_prom_decode_tick(int nb, const char* const* bufs, const long long* lens, void* const* index,
                               const char* label_a, const char* label_b, double start, double step, long long T,
                               float* out, long long ld, long long max_rows, int threads, int fill_nan,
                               long long* stats) {
@@ -725,7 +818,7 @@ long long fm_prom_decode_tick(int nb, const char* const* bufs, const long long* 
       if (t >= (long long)tasks.size()) break;
       Task& tk = tasks[t];
       const int j = tk.body;
-      const KeyIndex* ix = (const KeyIndex*)index[j];
+      KeyIndex* ix = (KeyIndex*)index[j];
       Cursor c{tk.p, bufs[j] + lens[j]};
       KeyedCounts k;
       const KeyedOut o{start, step, T, out, ld, max_rows, la, lb};

@@ -104,10 +104,12 @@ void run_one(const std::string& body, long long& checks) {
       for (long long j = 0; j < ld; ++j) m3[j] = m3[(2 * kr + 1) * ld + j] = -7.f;
       const char* bufs[2] = {buf, buf};
       const long long lens[2] = {len, len};
-      const void* ixs[2] = {ix, ix2};
+      void* ixs[2] = {ix, ix2};
       long long st[6];
-      fm_prom_decode_tick(2, bufs, lens, ixs, "__name__", "pod", 1700000000.0, 60.0, T, m3.data() + ld, ld, 2 * kr, 3,
-                          0, st);
+      // twice: the second decode runs on the layout the first one taught the indexes
+      for (int pass = 0; pass < 2; ++pass)
+        fm_prom_decode_tick(2, bufs, lens, ixs, "__name__", "pod", 1700000000.0, 60.0, T, m3.data() + ld, ld, 2 * kr,
+                            3, 0, st);
       for (long long j = 0; j < ld; ++j)
         if (m2[j] != -7.f || m2[(kr + 1) * ld + j] != -7.f || m3[j] != -7.f || m3[(2 * kr + 1) * ld + j] != -7.f) {
           std::fprintf(stderr, "keyed guard hit\n"); std::exit(3);

@@ -10,7 +10,9 @@ cols]`` float32 block the tick-ingest kernel reads:
   NaN-fills the pinned staging block, then decodes every body — split at
   series boundaries into ~4 chunks per thread, so one large body does not
   serialise the tick — scattering each series into its row through an
-  open-addressing key index (the ctypes call releases the GIL);
+  open-addressing key index that also learns the response layout (the label
+  object that followed each key last tick: a matching byte hash gives the
+  next row without parsing the labels); the ctypes call releases the GIL;
 * two staging blocks alternate: tick k+1 decodes on the CPU while the GPU
   scores tick k (the caller submits k+1 right after enqueueing tick k's H2D
   copy; block k is reused by tick k+2, after tick k's copy has completed).
