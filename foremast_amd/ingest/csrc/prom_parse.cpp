@@ -467,6 +467,9 @@ struct KeyedCounts {
 // overlaps the sample parsing.
 long long keyed_elements(Cursor& c, const char* stop, const KeyedOut& o, KeyIndex& ix, KeyedCounts& k) {
   long long prev_slot = -1;  // slot of the previous element of this chunk (-1: unknown / not flat)
+  const char* ts_txt = nullptr;  // last parsed timestamp text and its grid column
+  long long ts_len = 0, ts_col = 0;
+  bool ts_ok = false;
   while (true) {
     if (!c.eat('{')) return -4;
     long long row = -1, cur_slot = -1;
@@ -485,7 +488,15 @@ long long keyed_elements(Cursor& c, const char* stop, const KeyedOut& o, KeyInde
     };
     while (true) {
       const char *k0, *k1;
-      if (!read_key(c, k0, k1)) return -5;
+      // the two keys of every element, byte-exact and unspaced: no string scan
+      if (c.e - c.p >= 9 && c.p[0] == '"' && c.p[7] == '"' && c.p[8] == ':' &&
+          (memcmp(c.p + 1, "metric", 6) == 0 || memcmp(c.p + 1, "values", 6) == 0)) {
+        k0 = c.p + 1;
+        k1 = c.p + 7;
+        c.p += 9;
+      } else if (!read_key(c, k0, k1)) {
+        return -5;
+      }
       c.ws();
       const size_t kn = (size_t)(k1 - k0);
       if (kn == 6 && memcmp(k0, "metric", 6) == 0 && !have_labels) {
@@ -536,8 +547,21 @@ long long keyed_elements(Cursor& c, const char* stop, const KeyedOut& o, KeyInde
             c.ws();
             const char* a = c.p;
             while (c.p < c.e && *c.p != ',') ++c.p;
-            double ts;
-            if (!parse_number(a, c.p, ts)) return -9;
+            // every series of a tick carries the same timestamps: reuse the grid
+            // column of the last timestamp text when the bytes repeat
+            long long gi;
+            bool on_grid;
+            if (ts_len > 0 && c.p - a == ts_len && memcmp(a, ts_txt, (size_t)ts_len) == 0) {
+              gi = ts_col;
+              on_grid = ts_ok;
+            } else {
+              double ts;
+              if (!parse_number(a, c.p, ts)) return -9;
+              const double fi = (ts - o.start) / o.step;
+              gi = (long long)llround(fi);
+              on_grid = !(gi < 0 || gi >= o.T || std::fabs(fi - (double)gi) > 1e-6);
+              if (c.p - a <= 32) { ts_txt = a; ts_len = c.p - a; ts_col = gi; ts_ok = on_grid; }
+            }
             if (!c.eat(',')) return -10;
             c.ws();
             const char* v0 = c.p;
@@ -547,10 +571,8 @@ long long keyed_elements(Cursor& c, const char* stop, const KeyedOut& o, KeyInde
             if (!parse_number(v0, c.p, v)) return -12;
             if (!c.eat(']')) return -13;
             resolve();
-            const double fi = (ts - o.start) / o.step;
-            const long long i = (long long)llround(fi);
-            if (row < 0 || i < 0 || i >= o.T || std::fabs(fi - (double)i) > 1e-6) ++k.dropped;
-            else o.out[row * o.ld + i] = (float)v;
+            if (row < 0 || !on_grid) ++k.dropped;
+            else o.out[row * o.ld + gi] = (float)v;
             if (!many) break;
             if (c.eat(',')) continue;
             if (c.eat(']')) break;
