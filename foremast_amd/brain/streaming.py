@@ -119,7 +119,7 @@ class StreamingMonitor:
                  device=None, worker_id: str = "stream-0", metrics: Optional[BrainMetrics] = None,
                  ring_len: int = 10080, step: float = 60.0, window: int = 10, clock=time.time,
                  owns: Optional[Callable[[Dict], bool]] = None, history_chunk_points: int = 1440,
-                 apps_per_query: int = 256, min_capacity: int = 64) -> None:
+                 apps_per_query: int = 256, min_capacity: int = 64, decode_threads: int = 8) -> None:
         self.store = store
         self.cfg = cfg or BrainConfig.from_env()
         self.prom = prom or PromClient()
@@ -132,6 +132,7 @@ class StreamingMonitor:
         self.owns = owns
         self.chunk_pts = max(1, int(history_chunk_points))
         self.apps_per_query = max(1, int(apps_per_query))
+        self.decode_threads = max(1, int(decode_threads))  # native threads decoding the responses
         self.min_capacity = min_capacity
         self.jobs: Dict[str, StreamJob] = {}
         self.keys: List[Optional[Key]] = []          # row -> key (None: free row)
@@ -310,14 +311,22 @@ class StreamingMonitor:
         """``reqs``: (url, start, n_points, col0) per query, ``fams`` the family of
         each; every response is decoded by the keyed native scatter into ``out``."""
         bodies = await self.prom.fetch_raw_many([u for u, *_ in reqs])
+        good = []
         for (url, start, n, col0), fam, body in zip(reqs, fams, bodies):
             if isinstance(body, Exception):
                 log.warning("fetch %s failed: %s", url.split("?")[0], body)
                 continue
-            try:
-                native.parse_dense_keyed(body, start, self.step, n, out, tables[fam], col0=col0)
-            except native.ParseError as e:
-                log.warning("bad response for %s: %s", fam[1], e)
+            good.append((body, tables[fam], start, n, col0, fam))
+        if not good:
+            return
+        # every response in ONE native call on a thread pool (GIL released), off the event loop
+        b, t, st, ns, c0, fm = zip(*good)
+        stats = await asyncio.get_running_loop().run_in_executor(
+            None, lambda: native.decode_bodies(list(b), list(t), list(st), self.step, list(ns), list(c0), out,
+                                               threads=self.decode_threads))
+        for (series, _dropped, _unmatched), fam in zip(stats, fm):
+            if series < 0:
+                log.warning("bad response for %s (code %d)", fam[1], series)
 
     async def _load_history(self, assigned: List[Tuple[Key, int]]) -> None:
         """Fetch R + W points ending at ``t_last`` for the given series only, in

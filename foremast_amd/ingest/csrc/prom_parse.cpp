@@ -617,9 +617,9 @@ const char* result_array(const char* buf, long long len) {
 
 // Up to `parts` series-aligned chunk starts of a body's result array (cut[0] =
 // the first element); returns the count (0: empty array, < 0: malformed).  A
-// later cut is the first `{"metric"` at or after an even byte split whose
-// preceding non-space byte is ',' — a quote inside a JSON string is always
-// escaped, so that byte sequence cannot occur inside a label value.
+// later cut is the first `{"metric"` at or after an even byte split preceded
+// (spaces aside) by `},` — a quote inside a JSON string is always escaped, so
+// that byte sequence cannot occur inside a label value.
 long long split_elements(const char* buf, long long len, int parts, const char** cut) {
   const char* p = result_array(buf, len);
   if (!p) return -1;
@@ -640,7 +640,11 @@ long long split_elements(const char* buf, long long len, int parts, const char**
       if (memcmp(q, pat, 9) == 0) {
         const char* b = q - 1;
         while (b > cut[0] && (*b == ' ' || *b == '\n' || *b == '\r' || *b == '\t')) --b;
-        if (*b == ',') break;
+        if (*b == ',' && b > cut[0]) {
+          const char* b2 = b - 1;  // the previous element's closing brace
+          while (b2 > cut[0] && (*b2 == ' ' || *b2 == '\n' || *b2 == '\r' || *b2 == '\t')) --b2;
+          if (*b2 == '}') break;
+        }
       }
       ++q;
     }
@@ -787,19 +791,26 @@ long long fm_prom_dense_indexed(const char* buf, long long len, double start, do
   return r;
 }
 
-// One tick: `nb` bodies (body j keyed by index[j]) scattered into `out`
-// ([max_rows, ld] float32, columns [0, T) on the (start, step) grid) by
-// `threads` native threads.  With fill_nan the rows are first set to NaN (in
-// parallel); otherwise the caller pre-fills them.  Each body is split at series boundaries into chunks sized so
-// the pool stays balanced; stats[3j..3j+2] = (series, dropped points,
-// unmatched series) of body j, or stats[3j] < 0 when body j is malformed.
-// Returns 0, or the first negative code.
-long long fm_prom_decode_tick(int nb, const char* const* bufs, const long long* lens, void* const* index,
-                              const char* label_a, const char* label_b, double start, double step, long long T,
-                              float* out, long long ld, long long max_rows, int threads, int fill_nan,
-                              long long* stats) {
+// Many bodies at once: body j (keyed by index[j]) is scattered into columns
+// [col0s[j], col0s[j] + Ts[j]) of `out` ([max_rows, ld] float32) on the
+// (starts[j], step) grid (null arrays: start / T / column 0 for every body) by
+// `threads` native threads.  With fill_nan those columns of every row are
+// first set to NaN (in parallel); otherwise the caller pre-fills them.  Each
+// body is split at series boundaries into chunks sized so the pool stays
+// balanced; stats[3j..3j+2] = (series, dropped points, unmatched series) of
+// body j, or stats[3j] < 0 when body j is malformed.  Returns 0, or the first
+// negative code.
+long long fm_prom_decode_bodies(int nb, const char* const* bufs, const long long* lens, void* const* index,
+                                const char* label_a, const char* label_b, const double* starts, double start,
+                                double step, const long long* Ts, long long T, const long long* col0s, float* out,
+                                long long ld, long long max_rows, int threads, int fill_nan, long long* stats) {
   if (nb < 0 || threads < 1) return -1;
   threads = std::min(threads, 256);
+  auto st_of = [&](int j) { return starts ? starts[j] : start; };
+  auto T_of = [&](int j) { return Ts ? Ts[j] : T; };
+  auto c0_of = [&](int j) { return col0s ? col0s[j] : 0ll; };
+  for (int j = 0; j < nb; ++j)
+    if (T_of(j) < 0 || c0_of(j) < 0 || c0_of(j) + T_of(j) > ld) return -1;
   struct Task { int body; const char* p; const char* stop; const char* end = nullptr; };
   std::vector<Task> tasks;
   long long total = 0;
@@ -823,15 +834,16 @@ long long fm_prom_decode_tick(int nb, const char* const* bufs, const long long* 
   std::atomic<long long> next{0};
   std::atomic<long long> fill_next{0};
   const long long rows_per = 4096;
+  // the column span every body covers (fill_nan)
+  long long fc0 = ld, fc1 = 0;
+  for (int j = 0; j < nb; ++j) { fc0 = std::min(fc0, c0_of(j)); fc1 = std::max(fc1, c0_of(j) + T_of(j)); }
   auto work = [&]() {
-    if (fill_nan) {
-      const float nan = std::numeric_limits<float>::quiet_NaN();
-      while (true) {
-        const long long r0 = fill_next.fetch_add(rows_per);
-        if (r0 >= max_rows) break;
-        const long long r1 = std::min(max_rows, r0 + rows_per);
-        for (long long r = r0; r < r1; ++r) std::fill(out + r * ld, out + r * ld + T, nan);
-      }
+    const float nan = std::numeric_limits<float>::quiet_NaN();
+    while (true) {
+      const long long r0 = fill_next.fetch_add(rows_per);
+      if (r0 >= max_rows) break;
+      const long long r1 = std::min(max_rows, r0 + rows_per);
+      for (long long r = r0; r < r1; ++r) std::fill(out + r * ld + fc0, out + r * ld + fc1, nan);
     }
   };
   auto parse = [&]() {
@@ -843,7 +855,7 @@ long long fm_prom_decode_tick(int nb, const char* const* bufs, const long long* 
       KeyIndex* ix = (KeyIndex*)index[j];
       Cursor c{tk.p, bufs[j] + lens[j]};
       KeyedCounts k;
-      const KeyedOut o{start, step, T, out, ld, max_rows, la, lb};
+      const KeyedOut o{st_of(j), step, T_of(j), out + c0_of(j), ld, max_rows, la, lb};
       const long long r = keyed_elements(c, tk.stop, o, *ix, k);
       if (r < 0) { err[j].store(1); continue; }
       tk.end = c.p;
@@ -859,14 +871,15 @@ long long fm_prom_decode_tick(int nb, const char* const* bufs, const long long* 
     fn();
     for (auto& th : pool) th.join();
   };
-  if (fill_nan) run(work);
+  if (fill_nan && fc1 > fc0) run(work);
   if (!tasks.empty()) run(parse);
   // Every chunk but a body's last must have stopped exactly at the next cut.
   // A failed chunk, or one that did not (a cut that was not an element of the
   // result array — impossible in a Prometheus body, possible in malformed or
   // foreign JSON), makes the body's result that of a sequential decode, after
-  // its rows (every row its key index maps to, the only rows a chunk can
-  // write) are reset to NaN.
+  // its cells (its column range of every row its key index maps to: the only
+  // cells a chunk can write) are reset to NaN — unless another body of this
+  // call shares the index (its rows may hold that body's data).
   for (size_t t = 0; t + 1 < tasks.size(); ++t) {
     const int j = tasks[t].body;
     if (tasks[t + 1].body == j && tasks[t].end != tasks[t + 1].p) err[j].store(1);
@@ -874,11 +887,15 @@ long long fm_prom_decode_tick(int nb, const char* const* bufs, const long long* 
   const float nanf = std::numeric_limits<float>::quiet_NaN();
   for (int j = 0; j < nb; ++j) {
     if (err[j].load() != 1) continue;
-    for (const auto& sl : ((const KeyIndex*)index[j])->slots)
-      if (sl.row >= 0 && sl.row < max_rows) std::fill(out + sl.row * ld, out + sl.row * ld + T, nanf);
+    bool shared = false;
+    for (int q = 0; q < nb; ++q) shared |= (q != j && index[q] == index[j]);
+    if (!shared)
+      for (const auto& sl : ((const KeyIndex*)index[j])->slots)
+        if (sl.row >= 0 && sl.row < max_rows)
+          std::fill(out + sl.row * ld + c0_of(j), out + sl.row * ld + c0_of(j) + T_of(j), nanf);
     long long dr = 0, um = 0;
-    const long long r = fm_prom_dense_indexed(bufs[j], lens[j], start, step, T, out, ld, max_rows, label_a, label_b,
-                                              index[j], &dr, &um);
+    const long long r = fm_prom_dense_indexed(bufs[j], lens[j], st_of(j), step, T_of(j), out + c0_of(j), ld,
+                                              max_rows, label_a, label_b, index[j], &dr, &um);
     err[j].store(r < 0 ? r : 0);
     acc[3 * j].store(r < 0 ? 0 : r);
     acc[3 * j + 1].store(dr);
@@ -891,6 +908,15 @@ long long fm_prom_decode_tick(int nb, const char* const* bufs, const long long* 
     if (s0 < 0 && rc == 0) rc = s0;
   }
   return rc;
+}
+
+// One tick: every body on the same (start, step) grid, columns [0, T).
+long long fm_prom_decode_tick(int nb, const char* const* bufs, const long long* lens, void* const* index,
+                              const char* label_a, const char* label_b, double start, double step, long long T,
+                              float* out, long long ld, long long max_rows, int threads, int fill_nan,
+                              long long* stats) {
+  return fm_prom_decode_bodies(nb, bufs, lens, index, label_a, label_b, nullptr, start, step, nullptr, T, nullptr,
+                               out, ld, max_rows, threads, fill_nan, stats);
 }
 
 }  // extern "C"

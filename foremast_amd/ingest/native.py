@@ -82,6 +82,9 @@ def _load() -> Optional[C.CDLL]:
         lib.fm_prom_decode_tick.argtypes = [C.c_int, P, P, P, C.c_char_p, C.c_char_p, C.c_double, C.c_double, LL,
                                             P, LL, LL, C.c_int, C.c_int, P]
         lib.fm_prom_decode_tick.restype = LL
+        lib.fm_prom_decode_bodies.argtypes = [C.c_int, P, P, P, C.c_char_p, C.c_char_p, P, C.c_double, C.c_double, P,
+                                              LL, P, P, LL, LL, C.c_int, C.c_int, P]
+        lib.fm_prom_decode_bodies.restype = LL
         _lib = lib
         return lib
 
@@ -315,6 +318,60 @@ def decode_tick(bodies, tables, start: float, step: float, T: int, out: np.ndarr
         bad = [j for j in range(nb) if stats[3 * j] < 0]
         raise ParseError(f"malformed query_range body {bad[:1]} (code {rc})")
     return [(int(stats[3 * j]), int(stats[3 * j + 1]), int(stats[3 * j + 2])) for j in range(nb)]
+
+
+def decode_bodies(bodies, tables, starts, step: float, Ts, col0s, out: np.ndarray, threads: int = 8,
+                  fill_nan: bool = False) -> List[Tuple[int, int, int]]:
+    """Keyed scatter of many bodies in ONE native call on ``threads`` threads:
+    body j through ``tables[j]`` into columns ``[col0s[j], col0s[j] + Ts[j])``
+    of ``out`` on the ``(starts[j], step)`` grid (e.g. a history load: one
+    body per (time chunk, app group) query).  Returns ``(series, dropped,
+    unmatched)`` per body, ``series < 0`` marking a malformed body (the others
+    are still decoded)."""
+    n = len(bodies)
+    if not (len(tables) == len(starts) == len(Ts) == len(col0s) == n):
+        raise ValueError("one table, start, T and col0 per body")
+    if out.dtype != np.float32 or out.ndim != 2 or out.strides[1] != 4:
+        raise ValueError("out must be float32 [rows, cols] with unit column stride")
+    if n and max(int(c) + int(t) for c, t in zip(col0s, Ts)) > out.shape[1]:
+        raise ValueError("a body's column range exceeds out")
+    bodies = [b.encode() if isinstance(b, str) else b for b in bodies]
+    lib = _load()
+    labels = {(t.label_a, t.label_b) for t in tables}
+    res: List[Tuple[int, int, int]] = []
+    if lib is None or len(labels) > 1:
+        if fill_nan:
+            out[:] = np.nan
+        for b, t, st, T, c0 in zip(bodies, tables, starts, Ts, col0s):
+            try:
+                _check_status(b)
+                res.append(parse_dense_keyed(b, st, step, int(T), out, t, col0=int(c0)))
+            except ParseError:
+                res.append((-1, 0, 0))
+        return res
+    ok = []
+    for j, b in enumerate(bodies):
+        try:
+            _check_status(b)
+            ok.append(j)
+        except ParseError:
+            pass
+    m = len(ok)
+    stats = np.zeros(3 * max(m, 1), dtype=np.int64)
+    if m:
+        bufs = (C.c_char_p * m)(*[bodies[j] for j in ok])
+        lens = (C.c_longlong * m)(*[len(bodies[j]) for j in ok])
+        idx = (C.c_void_p * m)(*[tables[j].index for j in ok])
+        st = np.ascontiguousarray([float(starts[j]) for j in ok], dtype=np.float64)
+        tt = np.ascontiguousarray([int(Ts[j]) for j in ok], dtype=np.int64)
+        cc = np.ascontiguousarray([int(col0s[j]) for j in ok], dtype=np.int64)
+        la, lb = next(iter(labels))
+        lib.fm_prom_decode_bodies(m, C.cast(bufs, C.c_void_p), C.cast(lens, C.c_void_p), C.cast(idx, C.c_void_p),
+                                  la, lb, st.ctypes.data, 0.0, float(step), tt.ctypes.data, 0, cc.ctypes.data,
+                                  out.ctypes.data, out.strides[0] // 4, out.shape[0], int(max(1, threads)),
+                                  int(fill_nan), stats.ctypes.data)
+    by_j = {j: (int(stats[3 * i]), int(stats[3 * i + 1]), int(stats[3 * i + 2])) for i, j in enumerate(ok)}
+    return [by_j.get(j, (-1, 0, 0)) for j in range(n)]
 
 
 def _parse_py(body: bytes):

@@ -128,3 +128,52 @@ def test_bench_prom_ingest_matches_pinned_ingest():
         res.append(json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0]))
     assert res[0]["health"] == res[1]["health"] and res[0]["detection"] == res[1]["detection"]
     assert res[1]["config"]["ingest"] == "prom" and res[1]["config"]["ingest_bytes_per_tick"] > 0
+
+
+def test_decode_bodies_matches_per_body_decode_and_learns_layout():
+    """A history load's bodies (time chunks x app groups, each with its own grid
+    start and column offset, one key table per family) decode in ONE threaded
+    native call into exactly what per-body keyed decodes produce — including a
+    malformed body in the middle (reported; its complete series and all other
+    bodies still decoded) and a
+    second pass over the same bodies, which runs on the learned layout."""
+    from foremast_amd.ingest import native
+    rng = np.random.default_rng(3)
+    n_app, chunk, n_chunk, step = 120, 30, 4, 60.0
+    t0 = 1_700_000_000.0
+    vals = rng.normal(20, 5, (n_app, chunk * n_chunk)).astype(np.float32)
+    vals[5, 17] = np.nan
+    keys = [(f"ns{a % 3}", f"app{a}") for a in range(n_app)]
+    table = native.KeyTable([(k, i) for i, k in enumerate(keys)])
+
+    def body(apps, c):
+        items = []
+        for a in apps:
+            pts = ",".join(f'[{int(t0 + (c * chunk + i) * step)},"{float(vals[a, c * chunk + i]):.9g}"]'
+                           for i in range(chunk))
+            items.append(f'{{"metric":{{"__name__":"m","namespace":"{keys[a][0]}","app":"{keys[a][1]}"}},'
+                         f'"values":[{pts}]}}')
+        return ('{"status":"success","data":{"resultType":"matrix","result":[' + ",".join(items) + "]}}").encode()
+
+    groups = [range(0, 50), range(50, 120)]
+    bodies, starts, cols = [], [], []
+    for c in range(n_chunk):
+        for g in groups:
+            bodies.append(body(g, c))
+            starts.append(t0 + c * chunk * step)
+            cols.append(c * chunk)
+    bad = len(bodies) // 2
+    bodies[bad] = bodies[bad][: len(bodies[bad]) // 2]  # truncated response
+    ref = np.full((n_app, chunk * n_chunk), np.nan, dtype=np.float32)
+    for j, (b, st, c0) in enumerate(zip(bodies, starts, cols)):
+        try:  # the truncated body writes its complete series, then fails (both decoders)
+            native.parse_dense_keyed(b, st, step, chunk, ref, table, col0=c0)
+        except native.ParseError:
+            assert j == bad
+    for _ in range(2):
+        out = np.full_like(ref, np.nan)
+        stats = native.decode_bodies(bodies, [table] * len(bodies), starts, step, [chunk] * len(bodies), cols, out,
+                                     threads=3)
+        assert stats[bad][0] < 0
+        assert all(s[0] == len(groups[j % 2]) and s[2] == 0 for j, s in enumerate(stats) if j != bad)
+        np.testing.assert_array_equal(out, ref)
