@@ -55,6 +55,7 @@ if ROOT not in sys.path:
 
 from foremast_amd.brain.engine import (ShardSpec, StreamingShard, synthetic_eval,  # noqa: E402
                                        synthetic_history, synthetic_params)
+from foremast_amd.parallel import comm  # noqa: E402
 from foremast_amd.parallel.health import HealthAggregator, shard_range  # noqa: E402
 from foremast_amd.utils.config import BrainConfig  # noqa: E402
 
@@ -164,7 +165,9 @@ def init_dist(args):
         dev = torch.device("cuda", local)
     else:
         dev = torch.device("cpu")
-    if world > 1:
+    # FOREMAST_FORCE_COLLECTIVES=1 (tests/test_rccl_gpu.py): a 1-rank group that still runs
+    # every collective, so one GPU exercises the RCCL path of the N-GPU tick
+    if world > 1 or comm.force_collectives():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         backend = os.environ.get("FOREMAST_DIST_BACKEND", "nccl" if use_gpu else "gloo")
         if backend == "nccl":
@@ -241,7 +244,7 @@ def setup_canary(args, world, rank, dev):
     # shards are app-aligned, so each rank owns a disjoint slice of the app table: the
     # health exchange is ONE all-gather of per-rank records the scorer writes in place
     apps_per_rank = per // METRICS_PER_APP
-    agg = HealthAggregator(n_local, per, dev, apps_per_rank=apps_per_rank if world > 1 else None)
+    agg = HealthAggregator(n_local, per, dev, apps_per_rank=apps_per_rank if comm.active() else None)
     fused = {}
     if agg.fused:
         app_id = app_id - (s // METRICS_PER_APP)
@@ -405,7 +408,7 @@ def setup_canary(args, world, rank, dev):
         "current_window": W,
         "grid_points": int(shard.grid.shape[0]),
         "multi_cluster": bool(args.multi_cluster),
-        "health_collectives": "1 fused all_gather" if agg.fused else ("all_reduce + all_gather" if world > 1 else "none"),
+        "health_collectives": "1 fused all_gather" if agg.fused else ("all_reduce + all_gather" if agg.active else "none"),
         "hip_graph": bool(args.graph and dev.type == "cuda"),
         "ingest": args.ingest,
         "pipelined_ticks": pipelined,

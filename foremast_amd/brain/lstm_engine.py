@@ -41,6 +41,7 @@ import torch.distributed as dist
 
 from ..ingest.ringbuffer import HistoryRing
 from ..models.lstm_ae import LSTMAutoencoder
+from ..parallel import comm
 from ..parallel.dp import DPTrainer
 
 
@@ -246,7 +247,7 @@ class LstmShard:
 
     @staticmethod
     def _all_reduce(t: torch.Tensor) -> None:
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        if comm.active():
             dist.all_reduce(t)
 
     def _pack_scoring(self) -> None:

@@ -23,6 +23,8 @@ from typing import Tuple
 import torch
 import torch.distributed as dist
 
+from . import comm
+
 
 def _world(group=None) -> int:
     return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
@@ -33,7 +35,7 @@ def exchange_windows(ids: torch.Tensor, values: torch.Tensor, owner: torch.Tenso
     """Send row ``i`` (``ids[i]``, ``values[i, :]``) to rank ``owner[i]``.
     Returns the rows this rank received (ids, values), grouped by source rank."""
     world = _world(group)
-    if world == 1:
+    if not comm.active(group):
         return ids, values
     dev = values.device
     W = values.shape[1]
@@ -88,10 +90,11 @@ class WindowExchanger:
     def __init__(self, ids: torch.Tensor, owner: torch.Tensor, width: int, group=None) -> None:
         self.group = group
         self.world = _world(group)
+        self.active = comm.active(group)
         self.width = width
         self.order = torch.argsort(owner, stable=True)
         dev = ids.device
-        if self.world == 1:
+        if not self.active:
             self.recv_ids = ids
             return
         send_counts = torch.bincount(owner.long(), minlength=self.world).to(torch.int64)
@@ -104,7 +107,7 @@ class WindowExchanger:
         self.recv = torch.empty((int(sum(self.rc)), width), dtype=torch.float32, device=dev)
 
     def __call__(self, values: torch.Tensor) -> torch.Tensor:
-        if self.world == 1:
+        if not self.active:
             return values
         send = values[self.order].contiguous()
         W = self.width

@@ -18,6 +18,8 @@ from typing import Dict, List, Optional
 import torch
 import torch.distributed as dist
 
+from . import comm
+
 
 def _world(group=None) -> int:
     return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
@@ -28,6 +30,7 @@ class GradBuckets:
                  overlap: bool = True) -> None:
         self.group = group
         self.world = _world(group)
+        self.active = comm.active(group)
         self.params = [p for p in params if p.requires_grad]
         self.buckets: List[Dict] = []
         cur: List[torch.nn.Parameter] = []
@@ -41,7 +44,7 @@ class GradBuckets:
                 cur, size = [], 0
         if cur:
             self._make(cur)
-        self.overlap = overlap and self.world > 1
+        self.overlap = overlap and self.active
         self._handles: List = []
         if self.overlap:
             for bi, b in enumerate(self.buckets):
@@ -77,7 +80,7 @@ class GradBuckets:
         """Complete the reduction (average over ranks).  Buckets whose hooks
         did not fire (gradients written directly, e.g. by the fused LSTM
         training kernel) are all-reduced here."""
-        if self.world > 1:
+        if self.active:
             for b in self.buckets:
                 if not self.overlap or b["ready"] < len(b["params"]):
                     self._handles.append(dist.all_reduce(b["flat"], group=self.group, async_op=True))
@@ -89,7 +92,7 @@ class GradBuckets:
 
 
 def broadcast_params(module: torch.nn.Module, src: int = 0, group=None) -> None:
-    if _world(group) > 1:
+    if comm.active(group):
         for p in module.parameters():
             dist.broadcast(p.data, src=src, group=group)
 

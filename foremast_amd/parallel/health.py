@@ -31,9 +31,11 @@ from typing import List, Optional
 import torch
 import torch.distributed as dist
 
+from . import comm
 
-def _active() -> bool:
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+def _active(group=None) -> bool:
+    return comm.active(group)
 
 
 class HealthAggregator:
@@ -43,12 +45,13 @@ class HealthAggregator:
         self.metrics = metrics          # BrainMetrics: foremast_collective_seconds histogram
         self.timings_ms: List[float] = []  # per tick, resolved one tick late (no host sync)
         self._pending = None
-        self.world = dist.get_world_size(group) if _active() else 1
-        self.rank = dist.get_rank(group) if _active() else 0
+        self.active = _active(group)      # issue the collectives (N > 1 ranks, or forced)
+        self.world = dist.get_world_size(group) if self.active else 1
+        self.rank = dist.get_rank(group) if self.active else 0
         self.n_local = n_series_local
         self.n_pad = n_series_padded or n_series_local
         dev = torch.device(device)
-        self.fused = apps_per_rank is not None and self.world > 1
+        self.fused = apps_per_rank is not None and self.active
         if self.fused:
             self.apr = int(apps_per_rank)
             vw = (self.n_pad + 3) // 4
@@ -66,12 +69,12 @@ class HealthAggregator:
         self.verdict_all = torch.empty((self.n_pad * self.world,), dtype=torch.int8, device=dev)
 
     def reduce_apps(self, app_stats: torch.Tensor) -> torch.Tensor:
-        if self.world > 1:
+        if self.active:
             dist.all_reduce(app_stats, op=dist.ReduceOp.SUM, group=self.group)
         return app_stats
 
     def gather_verdicts(self, verdict: torch.Tensor) -> torch.Tensor:
-        if self.world == 1:
+        if not self.active:
             return verdict
         v = verdict
         if v.shape[0] != self.n_pad:

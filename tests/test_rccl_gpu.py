@@ -1,0 +1,87 @@
+"""The RCCL path on one GPU.
+
+The driver's scaling run launches ``bench.py --gpus N`` on an 8-GPU node, one
+rank per GPU over RCCL (``nccl``).  One GPU cannot host two RCCL ranks, so
+these tests run the SAME code in a 1-rank ``nccl`` group with
+``FOREMAST_FORCE_COLLECTIVES=1``: every per-tick collective is issued exactly
+as with N ranks — the canary tick's fused health all-gather (int32 records
+the scoring kernel wrote in place), the multi-cluster baseline all-to-all
+(int64 counts, ids, float32 windows with split sizes), the LSTM trainer's
+gradient all-reduce and parameter broadcast, and the per-app all-reduce +
+int8 verdict all-gather of the non-fused aggregator — and the results must
+equal the collective-free run.  The same on CPU with gloo keeps the forced
+mode itself covered in the CPU suite.
+"""
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _bench(args, force: bool, launcher: bool, cpu: bool):
+    env = dict(os.environ, OMP_NUM_THREADS="4", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.pop("WORLD_SIZE", None)
+    if force:
+        env["FOREMAST_FORCE_COLLECTIVES"] = "1"
+    else:
+        env.pop("FOREMAST_FORCE_COLLECTIVES", None)
+    pre = ([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+            "--master-addr=127.0.0.1", f"--master-port={_port()}"] if launcher else [sys.executable])
+    cmd = pre + [os.path.join(ROOT, "bench.py"), "--gpus", "1"] + args + (["--cpu"] if cpu else [])
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert out.returncode == 0, (out.stdout[-1000:] + out.stderr[-3000:])
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+CANARY = ["--steps", "3", "--warmup", "2", "--series", "5000", "--ring", "2880", "--anomaly-frac", "0.02"]
+CASES = {
+    "canary": (CANARY, "1 fused all_gather"),
+    "multicluster": (CANARY + ["--multi-cluster"], "1 fused all_gather"),
+    "lstm": (["--config", "lstm", "--steps", "3", "--warmup", "2", "--series", "4096", "--ring", "2880",
+              "--lstm-train-batch", "256", "--lstm-pretrain", "5", "--lstm-train-every", "1"],
+             "all_reduce + all_gather"),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_rccl_one_rank_collectives_match_local_tick(case):
+    args, coll = CASES[case]
+    ref = _bench(args, force=False, launcher=False, cpu=False)
+    got = _bench(args, force=True, launcher=True, cpu=False)
+    assert got["n_gpus"] == 1 and got["config"]["parallelism"] == "dp1"
+    if case != "lstm":
+        assert ref["config"]["health_collectives"] == "none"
+        assert got["config"]["health_collectives"] == coll
+        assert got["config"]["multi_cluster"] == (case == "multicluster")
+        assert got["health"] == ref["health"] and got["detection"] == ref["detection"]
+    else:
+        # training is stochastic across processes only through the all-reduce's
+        # arithmetic (a 1-rank sum is exact), so the verdict counts agree too
+        assert got["health"]["series_scored_last_tick"] == ref["health"]["series_scored_last_tick"]
+        assert got["detection"]["recall"] == ref["detection"]["recall"]
+    assert got["collective_ms_p50"] is not None and got["collective_ms_p50"] > 0
+
+
+def test_forced_collectives_gloo_one_rank_cpu():
+    """The forced mode on CPU (gloo, 1 rank): same health table as the plain run."""
+    args = ["--steps", "2", "--warmup", "1", "--series", "200", "--ring", "480", "--season", "48",
+            "--anomaly-frac", "0.05"]
+    ref = _bench(args, force=False, launcher=False, cpu=True)
+    got = _bench(args, force=True, launcher=True, cpu=True)
+    assert got["config"]["health_collectives"] == "1 fused all_gather"
+    assert got["health"] == ref["health"] and got["detection"] == ref["detection"]
