@@ -121,6 +121,8 @@ def _declare(lib: C.CDLL) -> None:
     lib.fm_tick_ingest.restype = I
     lib.fm_tick_ingest_dev.argtypes = [P, LL, P, LL, I, I, P, LL, I, P, P, I, P, P, I, P]
     lib.fm_tick_ingest_dev.restype = I
+    lib.fm_copy_to_host_i32.argtypes = [P, P, LL, P]
+    lib.fm_copy_to_host_i32.restype = I
     for name, args in _EXTRA.items():
         fn = getattr(lib, name, None)
         if fn is not None:

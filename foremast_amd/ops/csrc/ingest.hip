@@ -89,3 +89,24 @@ extern "C" int fm_tick_ingest_dev(void* hist, long long ld_h, float* cur, long l
   return tick_ingest_launch(hist, ld_h, 0, cur, ld_c, P, W, 0, newv, ld_n, N, 1, base, newb, bf16, state, zero,
                             nzero, st);
 }
+
+// Tick health table to the host without a DMA round trip: the table (a few
+// KB of int32 app counters) is written straight into pinned host memory by a
+// kernel queued behind the scoring kernels, with system-scope stores so the
+// host sees it once the stream is synchronised.  A hipMemcpyAsync D2H here is
+// a separate copy engine / blit operation with its own ~20 us queue turnaround
+// per tick (profiles/canary_12k5_r2.md).
+__global__ __launch_bounds__(256) void copy_to_host_kernel(int* __restrict__ dst, const int* __restrict__ src,
+                                                            long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+extern "C" int fm_copy_to_host_i32(int* dst_host, const int* src, long long n, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (!dst_host || !src) return (int)hipErrorInvalidValue;
+  long long blocks = (n + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(copy_to_host_kernel, dim3((unsigned)blocks), dim3(256), 0, st, dst_host, src, n);
+  return (int)hipGetLastError();
+}

@@ -679,6 +679,19 @@ def ring_append(dst: torch.Tensor, col0: int, src: torch.Tensor) -> None:
               "fm_ring_append")
 
 
+def copy_to_host(dst: torch.Tensor, src: torch.Tensor) -> None:
+    """Write a small int32 device tensor into a pinned host tensor with a kernel on
+    the current stream (system-scope stores; visible to the host after a stream
+    sync) instead of a D2H memcpy (csrc/ingest.hip copy_to_host_kernel)."""
+    lib = nat.require()
+    _cuda(src, "src")
+    _need(src.dtype == torch.int32 and src.is_contiguous(), "src must be a contiguous int32 device tensor")
+    _need(dst.device.type == "cpu" and dst.is_pinned() and dst.dtype == torch.int32 and dst.is_contiguous()
+          and dst.numel() == src.numel(), "dst must be a pinned contiguous int32 host tensor like src")
+    nat.check(lib.fm_copy_to_host_i32(dst.data_ptr(), src.data_ptr(), src.numel(), nat.stream_handle(src.device)),
+              "fm_copy_to_host_i32")
+
+
 def tick_ingest(hist: torch.Tensor, hist_col: int, cur: torch.Tensor, P: int, W: int, slot: int,
                 newv: torch.Tensor, graduate: bool = True, base: Optional[torch.Tensor] = None,
                 newb: Optional[torch.Tensor] = None, state: Optional[torch.Tensor] = None,
@@ -697,13 +710,17 @@ def tick_ingest(hist: torch.Tensor, hist_col: int, cur: torch.Tensor, P: int, W:
           and cur.dtype == torch.float32, f"cur must be float32 [N, {P * W}]")
     _need(newv.dim() == 2 and newv.shape[0] == N and newv.shape[1] == P and newv.stride(1) == 1
           and newv.dtype == torch.float32, f"newv must be float32 [N, {P}]")
-    _need(cur.device == hist.device and newv.device == hist.device, "device mismatch")
+    # newv / newb may live in pinned host memory: the kernel reads them over the fabric
+    # (zero-copy ingest, no separate H2D copy in the tick)
+    _need(cur.device == hist.device and (newv.device == hist.device or (newv.device.type == "cpu" and newv.is_pinned())),
+          "newv must be on the device or in pinned host memory")
     _need(0 <= slot < W and 0 <= hist_col < hist.shape[1], "slot/hist_col out of range")
     if base is not None:
         _need(newb is not None and base.shape == cur.shape and base.stride() == cur.stride()
               and base.dtype == torch.float32 and base.device == cur.device, "base must match cur")
         _need(newb.shape == newv.shape and newb.stride() == newv.stride() and newb.dtype == torch.float32
-              and newb.device == newv.device, "newb must match newv")
+              and newb.device == newv.device and (newb.device.type != "cpu" or newb.is_pinned()),
+              "newb must match newv")
     nz = 0
     if zero is not None:
         _need(zero.dtype == torch.int32 and zero.is_contiguous() and zero.device == hist.device,

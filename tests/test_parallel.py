@@ -223,7 +223,9 @@ def _elastic_worker(mid, members, port, q, die_after):
     from torch.distributed import TCPStore
     from foremast_amd.parallel.elastic import ElasticWorld
     store = TCPStore("127.0.0.1", port, is_master=False, timeout=_dt.timedelta(seconds=60))
-    ew = ElasticWorld(store, mid, members, backend="gloo", heartbeat_timeout_s=1.0, collective_timeout_s=5)
+    # generous liveness margins: a live rank of a loaded CI box (parallel test
+    # workers) must not miss heartbeats for 3 s; the killed one stops for good
+    ew = ElasticWorld(store, mid, members, backend="gloo", heartbeat_timeout_s=3.0, collective_timeout_s=10)
     ew.start_heartbeat(0.2)
     ew.form()
     n_total = 1000
