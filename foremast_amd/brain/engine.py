@@ -121,6 +121,7 @@ class StreamingShard:
             self._state_ring = torch.zeros((4, 8), dtype=torch.int32).pin_memory()
             self._state_k = 0
             self._state_dev = torch.zeros(8, dtype=torch.int32, device=self.device)
+        self._state_synced = False  # the device tick record matches the host ring (graph ticks)
         # cached Holt-Winters model (refit_every > 1): state after the last refit / update
         self.refit_every = max(1, int(spec.refit_every))
         self._cache: Optional[Dict] = None
@@ -204,6 +205,10 @@ class StreamingShard:
             self.horizons.copy_(torch.from_numpy(h))
 
     def ingest_tick(self, newv: torch.Tensor, newb: Optional[torch.Tensor] = None) -> None:
+        self._state_synced = False  # an eager tick moves the ring behind the device record's back
+        self._ingest_tick(newv, newb)
+
+    def _ingest_tick(self, newv: torch.Tensor, newb: Optional[torch.Tensor] = None) -> None:
         """``newv``: ``[N, P]`` float32 current-pod values on the shard's device;
         ``newb`` (optional, same shape): baseline-pod values streamed into the
         baseline window at the same slot (continuous canary).  The evicted
@@ -253,15 +258,19 @@ class StreamingShard:
                 and getattr(self, "_hw_variant", None) in (4, 5) and bool(self.out))
 
     def tick_graph(self, newv: torch.Tensor, newb: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
-        """``ingest_tick`` + ``score`` as ONE HIP-graph replay.
+        """``ingest_tick`` + ``score`` as ONE HIP-graph replay with no host-to-device copy.
 
-        The graph (captured on the first steady-state call) holds the ingest
-        kernel, the app-counter reset, the rank tests and the Holt-Winters fit;
-        the ring head / hist column / window slot reach the kernels through a
-        device int32 record written from pinned memory before each replay, and
-        the horizons through their usual pinned copy.  Falls back to the eager
-        calls until :meth:`graph_ready`.  ``newv`` / ``newb`` must be the same
-        buffers on every call (their addresses are baked into the graph)."""
+        The graph (captured on the first steady-state call) holds a tick-advance
+        kernel, the ingest kernel (which also clears the app counters), the rank
+        tests and the Holt-Winters fit + deferred detection.  The ring state
+        (hist column, window slot, head) lives in a device int32 record that the
+        advance kernel steps by one tick at the start of every replay, and the
+        forecast horizons of the new slot are copied from a device table by the
+        same kernel; the host only mirrors the ring bookkeeping.  The record is
+        written from the host once, when the graph path (re)starts after eager
+        ticks.  Falls back to the eager calls until :meth:`graph_ready`.
+        ``newv`` / ``newb`` must be the same buffers on every call (their
+        addresses are baked into the graph)."""
         if not self.graph_ready():
             self.ingest_tick(newv, newb)
             return self.score()
@@ -269,25 +278,36 @@ class StreamingShard:
         io = (newv.data_ptr(), None if newb is None else newb.data_ptr())
         if self._graph is not None and io != self._graph_io:
             raise ValueError("tick_graph needs the same newv/newb buffers on every call")
-        st = self._state_ring[self._state_k % 4]
-        self._state_k += 1
-        st[0] = self.hist.next_col()
-        st[1] = self.cur.slot()
-        st[2] = 1
+        W, R = self.cur.W, self.hist.R
+        if self._h_slots is None:
+            self._refresh_horizons()  # builds the per-slot horizon table (host + device)
+        if not self._state_synced:
+            # the record of the PREVIOUS tick, so that the replay's advance kernel yields this one
+            st = self._state_ring[self._state_k % 4]
+            self._state_k += 1
+            st.zero_()
+            st[1] = (self.cur.slot() - 1) % W
+            st[2] = 1
+            st[3] = self.hist.next_col()
+            self._state_dev.copy_(st, non_blocking=True)
+            self._state_synced = True
+        # host mirror of the ring bookkeeping (same as ingest_tick's steady state)
         self.hist.advance(1)
         self.cur.ticks += 1
-        st[3] = self.hist.head
-        self._state_dev.copy_(st, non_blocking=True)
-        self._refresh_horizons(stable=True)
+        self._new_pts += 1
+        self.horizons = self._h_buf
         if self._graph is None:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
+                K.tick_advance(self._state_dev, R, W, self._h_dev, self._h_buf)
                 K.tick_ingest(self.hist.data, 0, self.cur.data, self.cur.P, self.cur.W, 0, newv,
                               base=self.base if newb is not None else None, newb=newb, state=self._state_dev,
                               zero=self.app_stats.view(-1))
                 self._score_gpu(head_dev=self._state_dev[3:4])
             self._graph, self._graph_io = g, io
         self._graph.replay()
+        self._stats_zeroed = False
+        self.last_refit = True
         return self.out
 
     # ------------------------------------------------------------------ scoring

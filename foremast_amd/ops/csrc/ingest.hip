@@ -110,3 +110,33 @@ extern "C" int fm_copy_to_host_i32(int* dst_host, const int* src, long long n, h
   hipLaunchKernelGGL(copy_to_host_kernel, dim3((unsigned)blocks), dim3(256), 0, st, dst_host, src, n);
   return (int)hipGetLastError();
 }
+
+// Device-resident ring state for HIP-graph ticks: the first node of a replay
+// advances the steady-state tick record {hist_col, slot, graduate, head} held
+// in device memory (full ring: the graduating point overwrites the column at
+// `head`, which then moves by one; the window slot cycles mod W) and copies
+// the forecast horizons of the new slot from a device table, so a replay needs
+// no host-to-device copy at all.
+__global__ __launch_bounds__(256) void tick_advance_kernel(int* __restrict__ st, int R, int W,
+                                                           const int* __restrict__ h_table, int nh,
+                                                           int* __restrict__ h_buf) {
+  const int head = st[3], slot = st[1];
+  __syncthreads();  // every thread has the previous record before thread 0 rewrites it
+  const int nslot = slot + 1 < W ? slot + 1 : 0;
+  if (threadIdx.x == 0) {
+    st[0] = head;                      // hist_col: the oldest column is overwritten
+    st[1] = nslot;                     // this tick's window slot
+    st[2] = 1;                         // graduate
+    st[3] = head + 1 < R ? head + 1 : 0;
+  }
+  if (h_table) {
+    const int hs = nslot + 1 < W ? nslot + 1 : 0;  // horizons after the tick (ticks + 1) mod W
+    for (int i = threadIdx.x; i < nh; i += blockDim.x) h_buf[i] = h_table[(long long)hs * nh + i];
+  }
+}
+
+extern "C" int fm_tick_advance(int* state, int R, int W, const int* h_table, int nh, int* h_buf, hipStream_t st) {
+  if (!state || R <= 0 || W <= 0 || (h_table && (!h_buf || nh <= 0))) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(tick_advance_kernel, dim3(1), dim3(256), 0, st, state, R, W, h_table, nh, h_buf);
+  return (int)hipGetLastError();
+}

@@ -679,6 +679,25 @@ def ring_append(dst: torch.Tensor, col0: int, src: torch.Tensor) -> None:
               "fm_ring_append")
 
 
+def tick_advance(state: torch.Tensor, R: int, W: int, h_table: Optional[torch.Tensor] = None,
+                 h_buf: Optional[torch.Tensor] = None) -> None:
+    """Advance the device tick record ``state`` (int32 ``{hist_col, slot,
+    graduate, head}``) by one steady-state tick and copy row ``(slot + 1) mod W``
+    of ``h_table`` (int32 ``[W, nh]``) into ``h_buf`` (csrc/ingest.hip)."""
+    lib = nat.require()
+    _cuda(state, "state")
+    _need(state.dtype == torch.int32 and state.numel() >= 4 and state.is_contiguous(), "state must be int32 [>=4]")
+    nh = 0
+    if h_table is not None:
+        _need(h_buf is not None and h_table.dtype == torch.int32 and h_buf.dtype == torch.int32
+              and h_table.dim() == 2 and h_table.shape[0] == W and h_table.is_contiguous() and h_buf.is_contiguous()
+              and h_buf.numel() == h_table.shape[1] and h_table.device == state.device
+              and h_buf.device == state.device, "h_table must be int32 [W, nh] and h_buf int32 [nh]")
+        nh = int(h_table.shape[1])
+    nat.check(lib.fm_tick_advance(nat.ptr(state), int(R), int(W), nat.ptr(h_table), nh, nat.ptr(h_buf),
+                                  nat.stream_handle(state.device)), "fm_tick_advance")
+
+
 def copy_to_host(dst: torch.Tensor, src: torch.Tensor) -> None:
     """Write a small int32 device tensor into a pinned host tensor with a kernel on
     the current stream (system-scope stores; visible to the host after a stream

@@ -144,8 +144,10 @@ def test_streaming_monitor_resumes_from_snapshot(tmp_path):
 def test_graph_tick_matches_eager():
     """tick_graph (ingest + rank tests + HW fit as one HIP-graph replay, ring state
     read from device memory) gives the same outputs as the eager calls, tick for
-    tick, through the ring wrap and the window slot cycle."""
+    tick, through the ring wrap, the window slot cycle and eager ticks in between
+    (the device tick record resyncs)."""
     from foremast_amd.brain.engine import ShardSpec, StreamingShard, synthetic_history
+    from foremast_amd.ingest.ringbuffer import RingState
     from foremast_amd.ops import _native
     from foremast_amd.utils.config import BrainConfig
     _native.require()
@@ -159,6 +161,8 @@ def test_graph_tick_matches_eager():
         sh = StreamingShard(ShardSpec(n_series=n, ring_len=R, season=m, pods=P, window=W, n_apps=8), cfg, dev,
                             app_id=(torch.arange(n, device=dev) % 8).int())
         sh.load_history(hist[:, :R])
+        # start near the end of the ring so the head wraps during the run (same data in both)
+        sh.hist.state = RingState(head=R - 12, length=R)
         sh.set_baseline(hist[:, R - W:R].repeat(1, P).float())
         shards.append(sh)
     eager, graph = shards
@@ -170,7 +174,11 @@ def test_graph_tick_matches_eager():
         oe = {key: v.clone() for key, v in eager.score().items()}
         se = eager.app_stats.clone()
         replays += graph._graph is not None
-        og = graph.tick_graph(newv)
+        if k in (17, 18):  # eager ticks in between: the device tick record must resync
+            graph.ingest_tick(newv)
+            og = graph.score()
+        else:
+            og = graph.tick_graph(newv)
         torch.cuda.synchronize()
         for key in ("verdict", "sigma", "level", "trend", "best", "forecast", "count"):
             assert torch.equal(oe[key], og[key]), (k, key)
