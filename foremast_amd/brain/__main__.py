@@ -119,7 +119,11 @@ def main(argv=None) -> None:
     logging.basicConfig(level=os.environ.get("FOREMAST_LOG_LEVEL", "INFO"),
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")
     args = parse(argv)
-    if args.nproc > 1 and not os.environ.get("FOREMAST_NODE_STORE") and "WORLD_SIZE" not in os.environ:
+    from ..parallel import comm
+    # --nproc N: one launcher hosting the node store + N ranks; with forced collectives
+    # (FOREMAST_FORCE_COLLECTIVES=1) also for one rank, so it runs the N-rank code path
+    multi = args.nproc > 1 or (args.streaming and comm.force_collectives())
+    if multi and not os.environ.get("FOREMAST_NODE_STORE") and "WORLD_SIZE" not in os.environ:
         from .node import launch_node
         raw = list(sys.argv[1:] if argv is None else argv)
         rest, skip = [], False

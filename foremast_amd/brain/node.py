@@ -44,6 +44,7 @@ import torch
 import torch.distributed as dist
 
 from ..parallel.cluster import ClusterHealth
+from ..parallel import comm
 from ..parallel.elastic import ElasticWorld
 from .streaming import StreamingMonitor, app_of
 
@@ -114,6 +115,8 @@ class NodeBrain:
             if self.world.generation != gen:
                 self._after_reform(before)
         table["generation"] = self.world.generation if self.world else 0
+        table["backend"] = dist.get_backend() if dist.is_available() and dist.is_initialized() else "none"
+        table["collectives"] = comm.active()
         self.table = table
         self.ticks += 1
         if self.publish and self.rank == 0:

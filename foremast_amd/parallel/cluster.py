@@ -28,6 +28,8 @@ from typing import Any, Dict, List, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
+from . import comm
+
 HDR = 4
 
 
@@ -68,7 +70,7 @@ class ClusterHealth:
         send[:HDR].copy_(hdr.to(self.device, non_blocking=True))
         if k:
             send[HDR:HDR + 2 * k].copy_(counts[:k].reshape(-1))
-        if world > 1:
+        if comm.active(self.group):
             recv = torch.empty(world * chunk, dtype=torch.int32, device=self.device)
             dist.all_gather_into_tensor(recv, send, group=self.group)
         else:
@@ -77,7 +79,7 @@ class ClusterHealth:
         versions = host[:, 0].tolist()
         if versions != self._versions or len(self._rosters) != world:
             mine = dict(info or {}, names=[list(n) for n in names], version=roster_version)
-            if world > 1:
+            if comm.active(self.group):
                 rosters: List[Any] = [None] * world
                 dist.all_gather_object(rosters, mine, group=self.group)
             else:

@@ -149,3 +149,57 @@ def test_node_brain_two_ranks_cluster_table_and_rank_kill(tmp_path):
         except subprocess.TimeoutExpired:
             os.killpg(launcher.pid, signal.SIGKILL)
         server.should_exit = True
+
+
+@pytest.mark.gpu
+def test_node_brain_gpu_rccl_one_rank(tmp_path):
+    """The production node brain on the GPU: one rank launched by
+    ``--nproc 1``, its ElasticWorld formed over RCCL (``nccl``), collectives
+    forced in the 1-rank group (``FOREMAST_FORCE_COLLECTIVES=1``: the per-tick
+    counter all-gather and roster exchange run as with 8 ranks); the node table
+    is published and the injected app's job ends unhealthy."""
+    prom = FakePrometheus()
+    apps = [f"app{i}" for i in range(6)]
+    for i, app in enumerate(apps):
+        gen = synth.error_rate(base=0.3 + 0.02 * i, spread=0.05, seed=i)
+        if app == "app3":
+            gen = synth.step_change(gen, at=time.time() - 150, factor=0.0, add=40.0)
+        prom.add(M, {"namespace": "ns", "app": app}, gen)
+    port = _free_port()
+    server = _serve(prom.asgi_app(), port)
+    db = str(tmp_path / "jobs.db")
+    store = SqliteJobStore(db)
+    now = time.time()
+    ids = {app: svc.register(store, _job(app, f"http://127.0.0.1:{port}/api/v1/", now))[1]["jobId"] for app in apps}
+    env = dict(os.environ, FOREMAST_RING_LEN="240", FOREMAST_HEARTBEAT_S="5", FOREMAST_COLLECTIVE_TIMEOUT_S="30",
+               MIN_HISTORICAL_DATA_POINT_TO_MEASURE="10", ML_ALGORITHM="moving_average_all", OMP_NUM_THREADS="2",
+               FOREMAST_FORCE_COLLECTIVES="1", metric_type_threshold_count="1", metric_type0="error5xx",
+               threshold0="6", bound0="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for k in ("WORLD_SIZE", "FOREMAST_DEVICE", "FOREMAST_DIST_BACKEND", "CUDA_VISIBLE_DEVICES"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "foremast_amd.brain", "--streaming", "--nproc", "1", "--store", f"sqlite://{db}",
+           "--metrics-port", "0", "--tick-seconds", "1", "--window", "5"]
+    log_path = tmp_path / "node.log"
+    launcher = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=open(log_path, "w"), stderr=subprocess.STDOUT,
+                                start_new_session=True)
+    try:
+        t_end = time.time() + 90
+        t = {}
+        while time.time() < t_end and launcher.poll() is None:
+            t = store.get_meta("cluster_health") or {}
+            live = [a for a in apps if a != "app3"]  # app3's job completes unhealthy and leaves the table
+            if t.get("ranks") == 1 and all(f"ns/{a}" in t.get("apps", {}) for a in live) and \
+                    store.get(ids["app3"])["status"] == "completed_unhealth":
+                break
+            time.sleep(0.5)
+        log = log_path.read_text()
+        assert t.get("ranks") == 1 and all(f"ns/{a}" in t.get("apps", {}) for a in live), log[-3000:]
+        assert store.get(ids["app3"])["status"] == "completed_unhealth", log[-3000:]
+        assert t.get("backend") == "nccl" and t.get("collectives") is True, t
+    finally:
+        os.killpg(launcher.pid, signal.SIGTERM)
+        try:
+            launcher.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            os.killpg(launcher.pid, signal.SIGKILL)
+        server.should_exit = True
