@@ -320,45 +320,54 @@ bool label_value(const char* m0, const char* m1, const char* key, const char*& v
 // concurrent writer (possible only for a key repeated within one body) fails
 // the check and falls back to the full path.
 struct KeyIndex {
-  // one 32-byte slot per key: the key, its row and what followed it last time
-  // (`nx_*`: the next element's label-object length, its row, its slot, and
-  // the self-checking tag) — the prediction for the next element sits in the
-  // cache line the current element already brought in
+  // one 32-byte entry per key, stored in the order the keys were given (for a
+  // table built from a response, the response order): the key, its row and
+  // what followed it last time (`nx_*`: the next element's label-object
+  // length, its row, its entry, and the self-checking tag).  A repeated
+  // response therefore walks the entries sequentially — the prediction for the
+  // next element is in the next cache line, which the hardware prefetcher has
+  // already fetched — instead of chasing hash-ordered slots through DRAM.  The
+  // open-addressing table maps key hash -> entry (int32, 4 bytes a slot: it
+  // stays cache-resident) for chunk starts and mispredictions.
   struct Slot {
     uint64_t h;
     uint64_t nx_tag;
-    int32_t row;     // < 0: empty
+    int32_t row;
     int32_t nx_slot;
     int32_t nx_row;
     uint32_t nx_len; // 0: nothing learned
   };
-  std::vector<Slot> slots;
+  std::vector<Slot> slots;       // entries, build order
+  std::vector<int32_t> table;    // hash slot -> entry (-1: empty)
   uint64_t mask = 0;
   static uint64_t mix(uint64_t h) { h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33; return h; }
   bool build(const uint64_t* hash, const long long* rows, long long n) {
+    if (n > 0x3fffffffll) return false;
     uint64_t cap = 16;
     while (cap < (uint64_t)(2 * n)) cap <<= 1;
-    slots.assign(cap, Slot{0, 0, -1, -1, -1, 0});
+    table.assign(cap, -1);
+    slots.resize((size_t)n);
     mask = cap - 1;
     for (long long j = 0; j < n; ++j) {
       if (rows[j] < 0 || rows[j] > 0x7fffffffll) return false;
       uint64_t i = mix(hash[j]) & mask;
-      while (slots[i].row >= 0) {
-        if (slots[i].h == hash[j]) return false;  // duplicate key
+      while (table[i] >= 0) {
+        if (slots[table[i]].h == hash[j]) return false;  // duplicate key
         i = (i + 1) & mask;
       }
-      slots[i] = Slot{hash[j], 0, (int32_t)rows[j], -1, -1, 0};
+      table[i] = (int32_t)j;
+      slots[j] = Slot{hash[j], 0, (int32_t)rows[j], -1, -1, 0};
     }
     return true;
   }
-  void prefetch(uint64_t h) const { __builtin_prefetch(&slots[mix(h) & mask]); }
+  void prefetch(uint64_t h) const { __builtin_prefetch(&table[mix(h) & mask]); }
   void prefetch_slot(long long i) const { __builtin_prefetch(&slots[i]); }
   long long find_slot(uint64_t h) const {
     uint64_t i = mix(h) & mask;
     while (true) {
-      const Slot& sl = slots[i];
-      if (sl.row < 0) return -1;
-      if (sl.h == h) return (long long)i;
+      const int32_t e = table[i];
+      if (e < 0) return -1;
+      if (slots[e].h == h) return e;
       i = (i + 1) & mask;
     }
   }
@@ -384,7 +393,7 @@ struct KeyIndex {
     len = __atomic_load_n(&n.nx_len, __ATOMIC_RELAXED);
     slot = __atomic_load_n(&n.nx_slot, __ATOMIC_RELAXED);
     row = __atomic_load_n(&n.nx_row, __ATOMIC_RELAXED);
-    return len > 0 && slot >= 0 && (uint64_t)slot <= mask && row >= 0;
+    return len > 0 && slot >= 0 && (size_t)slot < slots.size() && row >= 0;
   }
 };
 

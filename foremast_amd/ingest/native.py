@@ -185,12 +185,17 @@ class KeyTable:
     """Sorted (hash → row) table of a shard's series keys for the keyed scatter."""
 
     def __init__(self, keys_rows, label_a: str = "namespace", label_b: str = "app") -> None:
-        pairs = sorted((key_hash(a, b), int(r)) for (a, b), r in keys_rows)
+        given = [(key_hash(a, b), int(r)) for (a, b), r in keys_rows]
+        pairs = sorted(given)
         hs = [h for h, _ in pairs]
         if len(set(hs)) != len(hs):
             raise ValueError("series key hash collision")
         self.hash = np.array(hs, dtype=np.uint64)
         self.rows = np.array([r for _, r in pairs], dtype=np.int64)
+        # the native index keeps the keys in the GIVEN order (ideally the order the
+        # responses list them): a repeated response then walks it sequentially
+        self._ix_hash = np.array([h for h, _ in given], dtype=np.uint64)
+        self._ix_rows = np.array([r for _, r in given], dtype=np.int64)
         self.label_a, self.label_b = label_a.encode(), label_b.encode()
 
     @classmethod
@@ -200,6 +205,8 @@ class KeyTable:
         order = np.argsort(hashes, kind="stable")
         t.hash = np.ascontiguousarray(hashes[order], dtype=np.uint64)
         t.rows = np.ascontiguousarray(np.asarray(rows, dtype=np.int64)[order])
+        t._ix_hash = np.ascontiguousarray(hashes, dtype=np.uint64)
+        t._ix_rows = np.ascontiguousarray(np.asarray(rows, dtype=np.int64))
         if len(t.hash) > 1 and bool((t.hash[1:] == t.hash[:-1]).any()):
             raise ValueError("series key hash collision")
         return t
@@ -216,7 +223,7 @@ class KeyTable:
             lib = _load()
             if lib is None:
                 raise RuntimeError("native ingest library unavailable")
-            ix = lib.fm_keyindex_new(self.hash.ctypes.data, self.rows.ctypes.data, len(self.rows))
+            ix = lib.fm_keyindex_new(self._ix_hash.ctypes.data, self._ix_rows.ctypes.data, len(self._ix_rows))
             if not ix:
                 raise ValueError("series key hash collision or negative row")
             self._index = ix
