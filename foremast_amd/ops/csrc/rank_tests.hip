@@ -27,23 +27,24 @@ __device__ __forceinline__ void rank_sweep(const float* x, int n, GroupFn in_gro
   for (int i = lane; i < n; i += FM_WAVE) {
     const float xi = x[i];
     if (xi != xi) continue;
-    float less = 0.f, eq = 0.f;
+    // integer counters: each comparison is one v_cmp into VCC plus one add-with-carry
+    int less = 0, eq = 0;
     int j = 0;
     for (; j + 4 <= n; j += 4) {
       const v4f q = *(const v4f*)(x + j);
-      less += (q.x < xi) ? 1.f : 0.f; eq += (q.x == xi) ? 1.f : 0.f;
-      less += (q.y < xi) ? 1.f : 0.f; eq += (q.y == xi) ? 1.f : 0.f;
-      less += (q.z < xi) ? 1.f : 0.f; eq += (q.z == xi) ? 1.f : 0.f;
-      less += (q.w < xi) ? 1.f : 0.f; eq += (q.w == xi) ? 1.f : 0.f;
+      less += (q.x < xi); eq += (q.x == xi);
+      less += (q.y < xi); eq += (q.y == xi);
+      less += (q.z < xi); eq += (q.z == xi);
+      less += (q.w < xi); eq += (q.w == xi);
     }
     for (; j < n; ++j) {
       const float q = x[j];
-      less += (q < xi) ? 1.f : 0.f;
-      eq += (q == xi) ? 1.f : 0.f;
+      less += (q < xi);
+      eq += (q == xi);
     }
-    const float r = less + (eq + 1.f) * 0.5f;
+    const float r = (float)less + ((float)eq + 1.f) * 0.5f;
     if (in_group(i)) rsum_g += r; else rsum_o += r;
-    tie += eq * eq - 1.f;
+    tie += (float)(eq * eq - 1);
   }
   rsum_g = wave_sum(rsum_g);
   rsum_o = wave_sum(rsum_o);
