@@ -65,8 +65,9 @@ __device__ __forceinline__ void run_phase(const LstmArgs& a, const typename Frag
                                           float (&hreg)[32], float (&creg)[32], float& errsum) {
   using FT = typename Frag<FP8>::T;
   const float sw = a.wmax ? fp8_scale(a.wmax[ENC ? 0 : 1]) : (ENC ? a.scale_w_enc : a.scale_w_dec);
-  const float sa = a.scale_act;
-  const float deq = sw * sa;  // acc → real gates
+  // bf16: unit scales by construction (ops/lstm.py pack), so the compiler drops the multiplies
+  const float sa = FP8 ? a.scale_act : 1.f;
+  const float deq = FP8 ? sw * sa : 1.f;  // acc → real gates
   const int lane = lane_id();
   const XPos xp = make_xpos(a.x, a.src, valid ? series : 0, a.T, a.F);  // tail lanes never index past N
   for (int t = 0; t < a.T; ++t) {

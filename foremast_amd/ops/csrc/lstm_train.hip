@@ -111,7 +111,7 @@ __device__ __forceinline__ void fwd_phase(const LstmTrainArgs& a, const uint4* w
       for (int tt = 0; tt < TILES; ++tt)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          hbuf[(long long)unit_of(tt, hh, q) * ldh + row] = f32_to_bf16(hreg[4 * tt + q]);
+          hbuf[(long long)unit_of(tt, hh, q) * ldh + row] = bf16_hw(hreg[4 * tt + q]);
     }
     uint4 hb[4];
 #pragma unroll
@@ -130,7 +130,7 @@ __device__ __forceinline__ void fwd_phase(const LstmTrainArgs& a, const uint4* w
           for (int f = 0; f < 7; ++f)
             if (f < a.F) {
               v[f] = load_x(a.src, xp, t, f, a.F);
-              a.h_enc[(long long)(64 + f) * KB + row] = f32_to_bf16(v[f]);
+              a.h_enc[(long long)(64 + f) * KB + row] = bf16_hw(v[f]);
             }
         }
         v[7] = 1.f;
@@ -174,7 +174,7 @@ __device__ __forceinline__ void fwd_phase(const LstmTrainArgs& a, const uint4* w
       for (int tt = 0; tt < TILES; ++tt)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          a.h_dec[(long long)unit_of(tt, hh, q) * ldh + row1] = f32_to_bf16(hreg[4 * tt + q]);
+          a.h_dec[(long long)unit_of(tt, hh, q) * ldh + row1] = bf16_hw(hreg[4 * tt + q]);
 #pragma unroll
       for (int f = 0; f < 7; ++f) {
         if (f >= a.F) break;
@@ -245,7 +245,7 @@ __device__ __forceinline__ void bwd_phase(const LstmTrainArgs& a, const uint4* w
       // dgates → HBM (PyTorch gate-row order: gate*64 + unit)
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        gbuf[(long long)((r >> 2) * H + unit_of(tt, hh, r & 3)) * KB + row] = f32_to_bf16(dg[r]);
+        gbuf[(long long)((r >> 2) * H + unit_of(tt, hh, r & 3)) * KB + row] = bf16_hw(dg[r]);
       // dh_{t-1} += W_hh^T[:, rows of this tile] · dgates (2 k-steps x 2 M-tiles)
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -370,7 +370,7 @@ __device__ __forceinline__ void fwd_phase2(const LstmTrainArgs& a, const uint4* 
       for (int tl = 0; tl < 4; ++tl)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          hbuf[(long long)unit_of(TB + tl, hh, q) * ldh + row] = f32_to_bf16(hreg[4 * tl + q]);
+          hbuf[(long long)unit_of(TB + tl, hh, q) * ldh + row] = bf16_hw(hreg[4 * tl + q]);
     }
     uint4 xb;
     {
@@ -381,7 +381,7 @@ __device__ __forceinline__ void fwd_phase2(const LstmTrainArgs& a, const uint4* 
           for (int f = 0; f < 7; ++f)
             if (f < a.F) {
               v[f] = load_x(a.src, xp, t, f, a.F);
-              if (w == 0) a.h_enc[(long long)(64 + f) * KB + row] = f32_to_bf16(v[f]);
+              if (w == 0) a.h_enc[(long long)(64 + f) * KB + row] = bf16_hw(v[f]);
             }
         }
         v[7] = 1.f;
@@ -425,7 +425,7 @@ __device__ __forceinline__ void fwd_phase2(const LstmTrainArgs& a, const uint4* 
       for (int tl = 0; tl < 4; ++tl)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          a.h_dec[(long long)unit_of(TB + tl, hh, q) * ldh + row1] = f32_to_bf16(hreg[4 * tl + q]);
+          a.h_dec[(long long)unit_of(TB + tl, hh, q) * ldh + row1] = bf16_hw(hreg[4 * tl + q]);
 #pragma unroll
       for (int f = 0; f < 7; ++f) {
         py[f] = 0.f;
@@ -508,7 +508,7 @@ __device__ __forceinline__ void bwd_phase2(const LstmTrainArgs& a, const uint4* 
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        gbuf[(long long)((r >> 2) * H + unit_of(tt, hh, r & 3)) * KB + row] = f32_to_bf16(dg[r]);
+        gbuf[(long long)((r >> 2) * H + unit_of(tt, hh, r & 3)) * KB + row] = bf16_hw(dg[r]);
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         float v[8];
