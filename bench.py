@@ -128,6 +128,8 @@ def parse():
     p.add_argument("--lstm-train-every", type=int, default=1)
     p.add_argument("--lstm-pretrain", type=int, default=200,
                    help="DP training steps of model initialisation before the timed ticks (untimed)")
+    p.add_argument("--lstm-restat-every", type=int, default=16,
+                   help="ticks between refreshes of the per-series normalisation statistics (window_stats over the ring)")
     p.add_argument("--lstm-autograd", action="store_true", help="train with autograd instead of the fused K7 kernel")
     p.add_argument("--lstm-no-overlap", action="store_true",
                    help="run the training step and scoring back to back instead of on two HIP streams")
@@ -501,7 +503,7 @@ def setup_lstm(args, world, rank, dev, n_features, fp8):
     app_id = (torch.arange(s, e, device=dev, dtype=torch.int64) // ent_per_app).to(torch.int32)
     shard = LstmShard(n_local, args.ring, F, window=args.lstm_window, hidden=64, fp8=fp8, device=dev,
                       app_id=app_id, n_apps=n_apps, threshold=4.0, train_batch=args.lstm_train_batch,
-                      lr=1e-3, seed=0, fused_train=not args.lstm_autograd)
+                      lr=1e-3, seed=0, fused_train=not args.lstm_autograd, restat_every=args.lstm_restat_every)
     params = [synthetic_params(n_local, dev, seed=1234 + 7 * f + 101 * rank) for f in range(F)]
     shard.load_history([synthetic_eval(p, 0, args.ring, args.season, noise_seed=555 + f + 101 * rank)
                         for f, p in enumerate(params)])
@@ -556,7 +558,7 @@ def setup_lstm(args, world, rank, dev, n_features, fp8):
     dt = "bf16"  # training fp32 master / bf16 MFMA scoring (fp8 weights+activations for config 5)
     meta["_agg"] = agg
     meta["_truth"] = (truth_apps, n_apps)
-    meta["_shard"], meta["_bad"] = shard, bad_local
+    meta["_shard"], meta["_bad"], meta["_ticks"], meta["_params"] = shard, bad_local, host_ticks, params
     return tick, health_host, meta, dt, n_ent * F
 
 

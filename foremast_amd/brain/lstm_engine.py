@@ -28,8 +28,9 @@ series-std units): a window is anomalous only when it is unusual for its
 series AND in absolute terms.  Measured on 20k healthy + 200 x3-regressed
 multivariate entities (fp8), thr 4: per-series alone flags 605 healthy
 entities, global alone 263, both 27, every regression caught by each.  Each
-tick the kernel's epilogue moves ``mu_i`` toward the series' non-anomalous
-errors (``cal_ewma``), tracking the continuously trained model.
+tick the kernel's epilogue moves ``mu_i`` toward the series' errors that lie
+within ``CAL_GATE`` of its level (``cal_ewma``), tracking the continuously
+trained model without absorbing a regression that builds up over ticks.
 """
 
 from __future__ import annotations
@@ -43,6 +44,9 @@ from ..ingest.ringbuffer import HistoryRing
 from ..models.lstm_ae import LSTMAutoencoder
 from ..parallel import comm
 from ..parallel.dp import DPTrainer
+
+
+CAL_GATE = 2.0  # csrc/lstm.hip: errors above 2 series-sigma do not refresh the calibration
 
 
 class LstmShard:
@@ -313,11 +317,13 @@ class LstmShard:
         with torch.no_grad():
             err = self.model.recon_error(x)
         z = (err - self.mu) / max(self.sigma, 1e-12)
+        zs = None
         if self.cal is not None:
-            z = torch.minimum(z, (err - self.cal[:, 0]) * self.cal[:, 1])
+            zs = (err - self.cal[:, 0]) * self.cal[:, 1]
+            z = torch.minimum(z, zs)
         v = (z > self.threshold).to(torch.int8)
-        if self.cal is not None and self.cal_ewma > 0:  # same update as the kernel epilogue
-            upd = (v == 0) & torch.isfinite(err)
+        if self.cal is not None and self.cal_ewma > 0:  # same update (and gate) as the kernel epilogue
+            upd = (v == 0) & torch.isfinite(err) & (zs <= CAL_GATE)
             nmu = self.cal[:, 0] + self.cal_ewma * (err - self.cal[:, 0])
             nmu = torch.where(upd, nmu, self.cal[:, 0])
             self.cal[:, 1] *= self.cal[:, 0] / nmu

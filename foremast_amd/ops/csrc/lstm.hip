@@ -53,6 +53,8 @@ struct LstmArgs {
 
 extern __shared__ __attribute__((aligned(16))) char fm_lstm_smem[];
 
+constexpr float CAL_GATE = 2.f;  // per-series z above which an error does not refresh the calibration
+
 namespace {
 
 using namespace fm_lstm;
@@ -112,14 +114,19 @@ __device__ __forceinline__ void run_phase(const LstmArgs& a, const typename Frag
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const f32x16& acc = e ? acc1 : acc0;
+        // two units per step of the loop: packed-FP32 activation arithmetic
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float gi = acc[q] * deq, gf = acc[4 + q] * deq;
-          const float gg = acc[8 + q] * deq, go = acc[12 + q] * deq;
+        for (int q = 0; q < 4; q += 2) {
+          const f32x2_t gi = (f32x2_t){acc[q], acc[q + 1]} * deq, gf = (f32x2_t){acc[4 + q], acc[5 + q]} * deq;
+          const f32x2_t gg = (f32x2_t){acc[8 + q], acc[9 + q]} * deq;
+          const f32x2_t go = (f32x2_t){acc[12 + q], acc[13 + q]} * deq;
           const int u = (tp + e) * 4 + q;
-          const float c = sigm(gf) * creg[u] + sigm(gi) * tanh_f(gg);
-          creg[u] = c;
-          hreg[u] = sigm(go) * tanh_f(c);
+          const f32x2_t c = sigm2(gf) * (f32x2_t){creg[u], creg[u + 1]} + sigm2(gi) * tanh2(gg);
+          creg[u] = c.x;
+          creg[u + 1] = c.y;
+          const f32x2_t h = sigm2(go) * tanh2(c);
+          hreg[u] = h.x;
+          hreg[u + 1] = h.y;
         }
       }
     }
@@ -188,17 +195,22 @@ __global__ __launch_bounds__(256, 2) void lstm_ae_kernel(const LstmArgs a) {
     // with a calibration the smaller of it and the series' own z: a window is
     // anomalous only when it is unusual for its series AND in absolute terms
     float z = (err - a.mu) / fmaxf(a.sigma, 1e-12f);
+    float zs = 0.f;  // the series' own z
     if (a.cal) {
       const float2 c = ((const float2*)a.cal)[series];
-      z = fminf(z, (err - c.x) * c.y);
+      zs = (err - c.x) * c.y;
+      z = fminf(z, zs);
     }
     if (a.zscore) a.zscore[series] = z;
     const float thr = a.threshold ? a.threshold[series] : a.thr_default;
     const int v = z > thr ? 1 : 0;
     if (a.verdict) a.verdict[series] = (signed char)v;
     // healthy windows keep the per-series error level current as the shared
-    // model keeps training (NaN errors — missing samples — never update it)
-    if (a.cal && a.cal_ewma > 0.f && !v && err == err) {
+    // model keeps training.  Only windows within CAL_GATE of the series' own
+    // level update it: a regression that builds up over several ticks (its
+    // first windows still below the verdict threshold) must not be absorbed
+    // into the baseline it is judged against.  NaN errors never update it.
+    if (a.cal && a.cal_ewma > 0.f && !v && err == err && zs <= CAL_GATE) {
       const float mu = a.cal[2 * series];
       const float nmu = mu + a.cal_ewma * (err - mu);
       a.cal[2 * series] = nmu;

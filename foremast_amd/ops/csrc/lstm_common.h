@@ -88,6 +88,21 @@ __device__ __forceinline__ bf16_t bf16_hw(float f) {  // one fp32 -> bf16 (RNE),
   __builtin_memcpy(&r, &b, 2);
   return r;
 }
+// the same activations for two units at once: the multiplies / adds become
+// packed-FP32 VOP3P ops (v_pk_mul_f32, v_pk_add_f32, v_pk_fma_f32), only the two
+// transcendentals per value stay scalar
+__device__ __forceinline__ f32x2_t sigm2(f32x2_t v) {
+  const f32x2_t t = v * (-LOG2E);
+  const f32x2_t d = (f32x2_t){__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + 1.f;
+  return (f32x2_t){__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
+__device__ __forceinline__ f32x2_t tanh2(f32x2_t v) {
+  const f32x2_t t = v * (-2.f * LOG2E);
+  const f32x2_t d = (f32x2_t){__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + 1.f;
+  const f32x2_t r = (f32x2_t){__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  return r * 2.f - 1.f;
+}
+
 __device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
   const bf16x2_t b = __builtin_convertvector((f32x2_t){lo, hi}, bf16x2_t);
   unsigned r;

@@ -154,15 +154,21 @@ __device__ __forceinline__ void fwd_phase(const LstmTrainArgs& a, const uint4* w
         const f32x16& acc = e ? acc1 : acc0;
         float4 cv;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float gi = sigm(acc[q]), gf = sigm(acc[4 + q]);
-          const float gg = tanh_f(acc[8 + q]), go = sigm(acc[12 + q]);
+        for (int q = 0; q < 4; q += 2) {  // two units at a time: packed-FP32 activation arithmetic
+          const f32x2_t gi = sigm2((f32x2_t){acc[q], acc[q + 1]}), gf = sigm2((f32x2_t){acc[4 + q], acc[5 + q]});
+          const f32x2_t gg = tanh2((f32x2_t){acc[8 + q], acc[9 + q]});
+          const f32x2_t go = sigm2((f32x2_t){acc[12 + q], acc[13 + q]});
           const int u = (tp + e) * 4 + q;
-          const float c = gf * creg[u] + gi * gg;
-          creg[u] = c;
-          hreg[u] = go * tanh_f(c);
-          srow[u * 64] = make_float4(gi, gf, gg, go);
-          (&cv.x)[q] = c;
+          const f32x2_t c = gf * (f32x2_t){creg[u], creg[u + 1]} + gi * gg;
+          const f32x2_t h = go * tanh2(c);
+          creg[u] = c.x;
+          creg[u + 1] = c.y;
+          hreg[u] = h.x;
+          hreg[u + 1] = h.y;
+          srow[u * 64] = make_float4(gi.x, gf.x, gg.x, go.x);
+          srow[(u + 1) * 64] = make_float4(gi.y, gf.y, gg.y, go.y);
+          (&cv.x)[q] = c.x;
+          (&cv.x)[q + 1] = c.y;
         }
         srow[(32 + tp + e) * 64] = cv;
       }
@@ -405,15 +411,21 @@ __device__ __forceinline__ void fwd_phase2(const LstmTrainArgs& a, const uint4* 
         const f32x16& acc = e ? acc1 : acc0;
         float4 cv;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float gi = sigm(acc[q]), gf = sigm(acc[4 + q]);
-          const float gg = tanh_f(acc[8 + q]), go = sigm(acc[12 + q]);
+        for (int q = 0; q < 4; q += 2) {  // two units at a time: packed-FP32 activation arithmetic
+          const f32x2_t gi = sigm2((f32x2_t){acc[q], acc[q + 1]}), gf = sigm2((f32x2_t){acc[4 + q], acc[5 + q]});
+          const f32x2_t gg = tanh2((f32x2_t){acc[8 + q], acc[9 + q]});
+          const f32x2_t go = sigm2((f32x2_t){acc[12 + q], acc[13 + q]});
           const int u = (tp + e) * 4 + q;
-          const float c = gf * creg[u] + gi * gg;
-          creg[u] = c;
-          hreg[u] = go * tanh_f(c);
-          srow[u * 64] = make_float4(gi, gf, gg, go);
-          (&cv.x)[q] = c;
+          const f32x2_t c = gf * (f32x2_t){creg[u], creg[u + 1]} + gi * gg;
+          const f32x2_t h = go * tanh2(c);
+          creg[u] = c.x;
+          creg[u + 1] = c.y;
+          hreg[u] = h.x;
+          hreg[u + 1] = h.y;
+          srow[u * 64] = make_float4(gi.x, gf.x, gg.x, go.x);
+          srow[(u + 1) * 64] = make_float4(gi.y, gf.y, gg.y, go.y);
+          (&cv.x)[q] = c.x;
+          (&cv.x)[q + 1] = c.y;
         }
         srow[(16 + tp + e) * 64] = cv;
       }

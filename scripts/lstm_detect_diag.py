@@ -48,6 +48,27 @@ def main():
                 print(f"  >thr {thr}: per-series {int((zz[fin] > thr).sum())} global {int((zg[m][fin] > thr).sum())}"
                       f" both {int(((zz[fin] > thr) & (zg[m][fin] > thr)).sum())}")
     print(bench.detection_report(health_host, truth_apps, n_apps))
+    tk_last = meta["_ticks"][-1, :, 0].float()
+    lvl = meta["_params"][0]["lvl"][:, 0].float().cpu()
+    bb = meta["_bad"].long()
+    print("bad series with last tick > 2 x level:", int((tk_last[bb] > 2 * lvl[bb]).sum()), "of", len(bb),
+          "| all ticks of bad > 2x:", int((meta["_ticks"][:, bb, 0] > 2 * lvl[bb][None]).all(0).sum()))
+    # the injected series the detector missed: their scored window vs the fp32 model
+    miss = np.nonzero(bad & (v == 0))[0][:6]
+    if len(miss):
+        idx = torch.as_tensor(miss, device=sh.device)
+        x = sh._gather(idx, torch.zeros_like(idx))
+        with torch.no_grad():
+            ref = sh.model.recon_error(x).cpu().numpy()
+            y = sh.model(x)
+        for j, i in enumerate(miss.tolist()):
+            xi = x[j, :, 0].cpu().numpy()
+            print(f"miss {i}: kernel err {err[i]:.4g} fp32 err {ref[j]:.4g} mean {float(sh.mean[i, 0]):.4g} "
+                  f"std {float(sh.std[i, 0]):.4g} x[0] {xi[0]:.3g} x[-1] {xi[-1]:.3g} y[-1] {float(y[j, -1, 0]):.3g}")
+            ring = sh.rings[0]
+            last = ring.logical()[i, -3:].float().cpu().numpy()
+            tk = meta["_ticks"][-3:, i, 0].numpy()
+            print(f"   lvl {float(meta['_params'][0]['lvl'][i]):.4g} ring last {np.round(last, 2)} ticks last {np.round(tk, 2)}")
 
 
 if __name__ == "__main__":
