@@ -87,6 +87,8 @@ def main():
     dc = {}
     if not args.only or "decompose" in args.only:
         jobs["seasonal_decompose"] = lambda: dc.update(K.seasonal_decompose(hist, 0, R, m, out=dc))
+        ds = {}
+        jobs["decompose_score"] = lambda: ds.update(K.decompose_score(hist, 0, R, m, spec, out=ds))
     for name, fn in jobs.items():  # warm-up / compile
         fn()
     torch.cuda.synchronize()
