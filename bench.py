@@ -83,6 +83,9 @@ def parse():
     p.add_argument("--anomaly-frac", type=float, default=0.01)
     p.add_argument("--anomaly-kind", default="scale3", choices=["scale3", "shift3sigma"],
                    help="injected canary regression: values x3, or a level shift of +3 noise sigma")
+    p.add_argument("--gap-frac", type=float, default=0.0,
+                   help="canary: fraction of series whose 7-day history has a 30-minute scrape outage (NaN run) "
+                        "after the first season (production-like gaps; those series take the masked kernels)")
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--graph", action="store_true", help="capture the GPU part of a tick in a HIP graph")
     p.add_argument("--pipeline", action="store_true",
@@ -265,6 +268,12 @@ def setup_canary(args, world, rank, dev):
     # --- synthetic data (outside the timed region) ---------------------------------
     params = synthetic_params(n_local, dev, seed=1234 + rank)
     hist = synthetic_eval(params, 0, args.ring, args.season, noise_seed=4321 + rank)
+    if args.gap_frac > 0:
+        g = torch.Generator().manual_seed(77 + rank)
+        rows = torch.randperm(n_local, generator=g)[: int(round(args.gap_frac * n_local))]
+        starts = torch.randint(args.season, args.ring - 30, (rows.numel(),), generator=g)
+        cols = (starts[:, None] + torch.arange(30)[None, :]).reshape(-1)
+        hist[rows.repeat_interleave(30).to(hist.device), cols.to(hist.device)] = float("nan")
     shard.load_history(hist)
     del hist
     W, P = args.window, args.pods
@@ -423,6 +432,7 @@ def setup_canary(args, world, rank, dev):
         "current_window": W,
         "grid_points": int(shard.grid.shape[0]),
         "multi_cluster": bool(args.multi_cluster),
+        "gap_frac": args.gap_frac,
         "health_collectives": "1 fused all_gather" if agg.fused else ("all_reduce + all_gather" if agg.active else "none"),
         "hip_graph": bool(args.graph and dev.type == "cuda"),
         "ingest": args.ingest,
