@@ -133,13 +133,15 @@ def test_shard_range_alignment():
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("config", ["canary", "lstm", "multicluster", "selflaunch"])
+@pytest.mark.parametrize("config", ["canary", "lstm", "multicluster", "selflaunch", "gaps"])
 def test_bench_distributed_cpu(config):
     """Under torchrun, and (``selflaunch``) as the driver may call it: a plain
-    ``python bench.py --gpus 2`` that must start its own 2-rank group."""
-    extra = ["--multi-cluster"] if config == "multicluster" else []
+    ``python bench.py --gpus 2`` that must start its own 2-rank group.  ``gaps``:
+    a fifth of the histories have a 30-minute outage (masked fit path)."""
+    variant = config
+    extra = {"multicluster": ["--multi-cluster"], "gaps": ["--gap-frac", "0.2"]}.get(config, [])
     launcher = config != "selflaunch"
-    config = "canary" if config in ("multicluster", "selflaunch") else config
+    config = "canary" if config in ("multicluster", "selflaunch", "gaps") else config
     port = _free_port()
     env = dict(os.environ, OMP_NUM_THREADS="2")
     env.pop("WORLD_SIZE", None)
@@ -156,8 +158,10 @@ def test_bench_distributed_cpu(config):
     assert d["n_gpus"] == 2 and d["steps"] == 2 and d["config"]["parallelism"] == "dp2"
     assert d["config"]["bench_config"] == config
     assert d["health"]["series_scored_last_tick"] == 200
-    if extra:
+    if variant == "multicluster":
         assert d["config"]["multi_cluster"] is True
+    if variant == "gaps":
+        assert d["config"]["gap_frac"] == 0.2 and d["detection"]["recall"] == 1.0
     for k in ("metric", "value", "unit", "ms_per_step", "higher_is_better", "scaling", "vs_baseline", "dtype",
               "data", "config"):
         assert k in d
