@@ -814,6 +814,9 @@ __global__ __launch_bounds__(256, 2) void hw_half_kernel(const SmoothArgs a, int
 template <int K>
 __global__ __launch_bounds__(256, 2) void hw_half_general_kernel(const SmoothArgs a, int hmax, int* deferred) {
   const int cnt = deferred[0];
+  // nothing deferred (gap-free shard, the common case): count and done are already 0, so
+  // no workgroup needs to count itself — skip the 512 same-address atomics
+  if (cnt == 0) return;
   for (int q = blockIdx.x; q < cnt; q += gridDim.x) {
     hw_half_block<K, true>(a, hmax, deferred[1 + q], nullptr);
     __syncthreads();  // LDS is reused by the next pair
