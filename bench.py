@@ -81,8 +81,11 @@ def parse():
     p.add_argument("--algorithm", default="holt_winters")
     p.add_argument("--pairwise", default="ALL")
     p.add_argument("--anomaly-frac", type=float, default=0.01)
-    p.add_argument("--anomaly-kind", default="scale3", choices=["scale3", "shift3sigma"],
-                   help="injected canary regression: values x3, or a level shift of +3 noise sigma")
+    p.add_argument("--anomaly-kind", default="scale3", choices=["scale3", "shift3sigma", "scale", "shift"],
+                   help="injected canary regression: values x3, or a level shift of +3 noise sigma; "
+                        "scale / shift take their size from --anomaly-size")
+    p.add_argument("--anomaly-size", type=float, default=3.0,
+                   help="scale: values multiplied by this; shift: level shift in noise sigmas")
     p.add_argument("--gap-frac", type=float, default=0.0,
                    help="canary: fraction of series whose 7-day history has a 30-minute scrape outage (NaN run) "
                         "after the first season (production-like gaps; those series take the masked kernels)")
@@ -198,11 +201,12 @@ def barrier(dev):
 NOISE = 0.03  # synthetic noise sigma as a fraction of the level (engine.synthetic_eval default)
 
 
-def make_ticks(params, pods, nticks, season, t0, seed, anomaly_frac, kind="scale3", want_bad=False):
+def make_ticks(params, pods, nticks, season, t0, seed, anomaly_frac, kind="scale3", want_bad=False, size=3.0):
     """Per-tick per-pod values ``[nticks, n, pods]`` continuing each series'
     synthetic model past the history (same noise level as the history), with a
     fraction of series turned anomalous: ``scale3`` (canary regression, values
-    x3) or ``shift3sigma`` (level shift of +3 noise sigma).  ``want_bad``: also
+    x3) or ``shift3sigma`` (level shift of +3 noise sigma); ``scale`` / ``shift``
+    use ``size`` instead of 3.  ``want_bad``: also
     return the regressed series' indices (detection-quality ground truth)."""
     lvl = params["lvl"]
     n, dev = lvl.shape[0], lvl.device
@@ -214,10 +218,11 @@ def make_ticks(params, pods, nticks, season, t0, seed, anomaly_frac, kind="scale
     bad = torch.zeros(0, dtype=torch.int64, device=dev)
     if n_bad:
         bad = torch.randperm(n, generator=g, device=dev)[:n_bad]
-        if kind == "scale3":
-            out[:, bad, :] *= 3.0
+        k = 3.0 if kind in ("scale3", "shift3sigma") else float(size)
+        if kind.startswith("scale"):
+            out[:, bad, :] *= k
         else:
-            out[:, bad, :] += (3 * NOISE * lvl[bad, 0])[None, :, None]
+            out[:, bad, :] += (k * NOISE * lvl[bad, 0])[None, :, None]
     return (out.float(), bad) if want_bad else out.float()
 
 
@@ -281,7 +286,7 @@ def setup_canary(args, world, rank, dev):
     # per tick: P canary-pod values (a fraction of series regressed) and P
     # baseline-pod values (healthy, same times) -> [ticks, N, 2P]
     cur_t, bad = make_ticks(params, P, total_ticks + W, args.season, args.ring, 99 + rank, args.anomaly_frac,
-                            args.anomaly_kind, want_bad=True)
+                            args.anomaly_kind, want_bad=True, size=args.anomaly_size)
     truth_apps = sorted(set(((bad.cpu() + s) // METRICS_PER_APP).tolist()))
     exch = None
     if args.multi_cluster:
@@ -520,7 +525,7 @@ def setup_lstm(args, world, rank, dev, n_features, fp8):
     total = args.warmup + args.steps
     # the same entities regress on every metric (seed shared across features)
     tk = [make_ticks(p, 1, total, args.season, args.ring, 99 + rank, args.anomaly_frac, args.anomaly_kind,
-                     want_bad=True) for p in params]
+                     want_bad=True, size=args.anomaly_size) for p in params]
     ticks = torch.stack([t[..., 0] for t, _ in tk], 2)  # [ticks, n, F]
     truth_apps = sorted(set(((tk[0][1].cpu() + s) // ent_per_app).tolist()))
     bad_local = tk[0][1].cpu()
@@ -693,7 +698,7 @@ def run_cpu_baseline(args) -> None:
     params = synthetic_params(n, dev, seed=1234)
     hist = synthetic_eval(params, 0, args.ring, args.season, noise_seed=4321).numpy()
     cur, bad = make_ticks(params, P, W, args.season, args.ring, 99, max(args.anomaly_frac, 1.0 / n),
-                          args.anomaly_kind, want_bad=True)
+                          args.anomaly_kind, want_bad=True, size=args.anomaly_size)
     base = make_ticks(params, P, W, args.season, args.ring, 7, 0.0)
     cur = cur.permute(1, 2, 0).reshape(n, P * W).numpy()    # pod-major windows, as the engine's
     base = base.permute(1, 2, 0).reshape(n, P * W).numpy()
@@ -850,8 +855,9 @@ def main():
                 if sel.any():
                     res[f"p50_{name}_tick_ms"] = round(float(np.percentile(lat_ms[sel], 50)), 3)
         if truth is not None:
+            size = f" {args.anomaly_size:g}" if args.anomaly_kind in ("scale", "shift") else ""
             res["detection"] = dict(detection_report(health_host, truth[0], truth[1]),
-                                    injected=f"{args.anomaly_kind} on {args.anomaly_frac:g} of series")
+                                    injected=f"{args.anomaly_kind}{size} on {args.anomaly_frac:g} of series")
         print(json.dumps(res), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
