@@ -348,7 +348,10 @@ __global__ __launch_bounds__(BLOCK, KT <= kItemsWeek ? 8 : 4) void decompose_ker
   // 5. scoring: trend extrapolated from its last defined value over the last season
   const v2f rr = block_sum2(v2f{r2, rc}, red);
   const float rss = rr.x, rcnt = rr.y;
-  const float sig = sqrtf(rss / fmaxf(rcnt, 1.f));
+  // residual RMS -> prediction spread of the phase-mean model (models/decompose.py
+  // prediction_factor): sqrt((K+1)/(K-1)), K = seasons with a centred trend
+  const float Ks = fmaxf((float)(T - 2 * h) / (float)m, 1.5f);
+  const float sig = sqrtf(rss / fmaxf(rcnt, 1.f)) * sqrtf((Ks + 1.f) / (Ks - 1.f));
   const float lvl = tr_e == tr_e ? tr_e : ybar;
   const float slope = (tr_e == tr_e && tr_p == tr_p) ? (tr_e - tr_p) / (float)m : 0.f;
   if (tid == 0) {
