@@ -48,6 +48,10 @@ def parse(argv=None):
                    help="node mode: start this many brain ranks (one per GPU) around a node key-value store")
     p.add_argument("--tick-seconds", type=float, default=None,
                    help="streaming tick period (default: the query step)")
+    p.add_argument("--rollout", type=int, default=int(os.environ.get("FOREMAST_ROLLOUT", "1")),
+                   help="with --streaming: serve canary / rollingUpdate jobs from the resident rollout engine")
+    p.add_argument("--pods", type=int, default=int(os.environ.get("FOREMAST_CANARY_PODS", "5")),
+                   help="rollout engine: pods per side kept per (job, metric) window")
     p.add_argument("--step", type=float, default=float(os.environ.get("FOREMAST_STEP_SECONDS", "60")))
     p.add_argument("--window", type=int, default=int(os.environ.get("FOREMAST_WINDOW", "10")))
     return p.parse_args(argv)
@@ -73,8 +77,11 @@ async def run(args) -> BrainWorker:
     if args.metrics_port:
         from prometheus_client import start_http_server
         start_http_server(args.metrics_port + local, registry=metrics.registry)
+    # --streaming: continuous jobs go to the streaming monitor and keyable canary /
+    # rollingUpdate jobs to the rollout monitor; the worker keeps what they cannot key
     worker = BrainWorker(store, cfg, worker_id=args.worker_id, metrics=metrics,
-                         exclude_strategies=("continuous",) if args.streaming else ())
+                         exclude_strategies=(("continuous", "canary", "rollingupdate") if args.streaming and
+                                             args.rollout else ("continuous",) if args.streaming else ()))
     cache_path = None
     if args.model_cache:
         from .multivariate import LstmJobScorer, ModelCache
@@ -101,12 +108,18 @@ async def run(args) -> BrainWorker:
         mon = StreamingMonitor(store, cfg, device=dev, metrics=metrics, ring_len=cfg.ring_len, step=args.step,
                                window=args.window, worker_id=worker_id_of(member) if world else member)
         period = args.tick_seconds if args.tick_seconds else args.step
-        if world is None and args.snapshot:
+        rollout = None
+        if args.rollout:
+            from .rollout import RolloutMonitor
+            rollout = RolloutMonitor(store, cfg, device=dev, metrics=metrics, step=args.step, window=args.window,
+                                     pods=args.pods, worker_id=(worker_id_of(member) if world else member) + "-rollout",
+                                     ring_len=cfg.ring_len)
+        if world is None and args.snapshot and rollout is None:
             snap = args.snapshot.replace("{rank}", str(local))
             tasks.append(mon.run_forever(stop, period=period, snapshot=snap, snapshot_every=args.snapshot_every))
         else:
             # node brain (also for one rank: it publishes the health table)
-            tasks.append(NodeBrain(mon, world, store, dev).run_forever(stop, period))
+            tasks.append(NodeBrain(mon, world, store, dev, extra=(rollout,)).run_forever(stop, period))
     await asyncio.gather(*tasks)
     if cache_path and worker.lstm is not None:
         worker.lstm.cache.save(cache_path)

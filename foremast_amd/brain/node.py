@@ -63,9 +63,15 @@ def worker_id_of(member: str) -> str:
 
 
 class NodeBrain:
+    """``mon``: the continuous-job monitor; ``extra``: further resident engines
+    on the same rank (the rollout monitor for canary / rollingUpdate jobs),
+    all sharded by app with the same ownership function and merged into one
+    per-app record for the exchange."""
+
     def __init__(self, mon: StreamingMonitor, world: Optional[ElasticWorld], store, device,
-                 publish: bool = True) -> None:
+                 publish: bool = True, extra=()) -> None:
         self.mon = mon
+        self.monitors = [mon] + [m for m in extra if m is not None]
         self.world = world
         self.store = store
         self.device = torch.device(device)
@@ -74,7 +80,8 @@ class NodeBrain:
         self.dead: Set[str] = set()
         self.table: Dict = {}
         self.ticks = 0
-        mon.owns = self.owns
+        for m in self.monitors:
+            m.owns = self.owns
 
     @property
     def rank(self) -> int:
@@ -91,22 +98,40 @@ class NodeBrain:
     def _after_reform(self, before: List[str]) -> None:
         gone = set(before) - set(self.world.members)
         self.dead |= {worker_id_of(m) for m in gone}
-        moved = self.mon.release(lambda d: not self.owns(d))
+        moved = sum(m.release(lambda d: not self.owns(d)) for m in self.monitors)
         self.health.reset()
         log.warning("node re-formed: generation %d, members %s (lost %s); released %d moved jobs",
                     self.world.generation, self.world.members, sorted(gone), moved)
 
+    def app_table(self):
+        """(app roster, ``[A, 2]`` device counters, roster version, live series)
+        of every monitor of this rank, merged per app."""
+        if len(self.monitors) == 1:
+            names, counts = self.mon.app_table()
+            return names, counts, self.mon.roster_version, self.mon.n_live
+        tables = [m.app_table() for m in self.monitors]
+        names = sorted({n for ns, _ in tables for n in ns})
+        idx = {n: i for i, n in enumerate(names)}
+        counts = torch.zeros((len(names), 2), dtype=torch.int32, device=self.device)
+        for ns, c in tables:
+            if ns:
+                at = torch.tensor([idx[n] for n in ns], dtype=torch.long, device=self.device)
+                counts.index_add_(0, at, c[:len(ns)].to(self.device))
+        return (names, counts, sum(m.roster_version for m in self.monitors),
+                sum(m.n_live for m in self.monitors))
+
     def _exchange(self) -> Dict:
-        names, counts = self.mon.app_table()
+        names, counts, version, n_live = self.app_table()
         info = {"member": self.world.id if self.world else "m0", "pid": os.getpid()}
-        return self.health.exchange(names, counts, self.mon.roster_version, self.mon.n_live, info)
+        return self.health.exchange(names, counts, version, n_live, info)
 
     async def tick(self) -> Dict:
-        self.mon.sync(steal_from=self.dead or None)
-        try:
-            await self.mon.tick()
-        except Exception as e:  # noqa: BLE001 - a scoring failure must not desynchronise the collectives
-            log.exception("streaming tick failed: %s", e)
+        for m in self.monitors:
+            m.sync(steal_from=self.dead or None)
+            try:
+                await m.tick()
+            except Exception as e:  # noqa: BLE001 - a scoring failure must not desynchronise the collectives
+                log.exception("%s tick failed: %s", type(m).__name__, e)
         if self.world is None:
             table = self._exchange()
         else:

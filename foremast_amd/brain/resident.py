@@ -1,0 +1,318 @@
+"""The node's resident 7-day history, keyed by series.
+
+A one-shot canary / rollingUpdate job asks for the 7-day history of every
+metric it watches (``namespace_app_per_pod:<m>{namespace, app}`` over
+``[start - 7d, start]``, ``metricsquery.go:73-79``).  The reference brain
+re-fetches that week of points per job and cycle.  Here the week of every
+series a job has used stays in HBM (100k series x 10,080 points x 2 B = 2 GB
+bf16 of the 288 GB) and is kept current with ONE short range query per metric
+family per tick, so a job on an app seen before (re-deploys, canaries of a
+continuously watched app) starts scoring without any history fetch:
+
+* rows: one per (endpoint, metric, namespace, app); a row is referenced by
+  the jobs that use it (:meth:`want` / :meth:`unwant`) and retained for
+  ``retain_s`` after its last job (``FOREMAST_HISTORY_RETAIN_S``), then
+  freed in place; the table grows by doubling;
+* columns: one shared time axis at the query step, newest point at
+  ``t_last`` (a full ring: unknown points are NaN, the kernels skip them);
+* loads: a new series' week arrives in (time chunk x app group) queries that
+  stay below Prometheus' ``--query.max-samples``, decoded by the native keyed
+  parser into one pinned block and copied H2D once; a key whose load had a
+  failed query stays pending and is retried next sync;
+* advance: the tick's newest points of every resident row (one query per
+  family, split into time chunks after an outage); if any of them fails the
+  ring does not move, so the next sync fetches the same minutes again
+  instead of leaving NaN holes; behind by more than the ring, every row is
+  reloaded.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import logging
+import re
+import time
+from typing import Dict, Iterable, List, Optional, Sequence, Set, Tuple
+from urllib.parse import quote
+
+import numpy as np
+import torch
+
+from ..ingest import native
+from ..ingest.ringbuffer import HistoryRing
+
+log = logging.getLogger("foremast.resident")
+
+Key = Tuple[str, str, str, str]  # (endpoint, metric, namespace, app)
+
+_RE2_SPECIAL = re.compile(r"([\\.^$|?*+()\[\]{}])")
+
+
+def re_alt(values: Iterable[str]) -> str:
+    """RE2 alternation of literal label values, escaped for a PromQL string."""
+    return "|".join(_RE2_SPECIAL.sub(r"\\\\\1", v) for v in sorted(values))
+
+
+def range_url(endpoint: str, selector: str, start: float, n: int, step: float) -> str:
+    return (f"{endpoint}query_range?query={quote(selector, safe='')}&start={int(start)}"
+            f"&end={int(start + (n - 1) * step)}&step={int(step)}")
+
+
+async def fetch_decode(prom, reqs: Sequence[Tuple[str, float, int, int]], tables: Sequence[native.KeyTable],
+                       out: np.ndarray, step: float, threads: int) -> List[bool]:
+    """Fetch ``reqs`` = (url, start, n_points, col0) and scatter every body through
+    its key table into ``out`` (one native call on a thread pool, off the event
+    loop).  Returns per request whether it was fetched and decoded."""
+    bodies = await prom.fetch_raw_many([u for u, *_ in reqs])
+    ok = [not isinstance(b, Exception) for b in bodies]
+    for (url, *_), b in zip(reqs, bodies):
+        if isinstance(b, Exception):
+            log.warning("fetch %s failed: %s", url.split("?")[0], b)
+    good = [j for j in range(len(reqs)) if ok[j]]
+    if not good:
+        return ok
+    args = ([bodies[j] for j in good], [tables[j] for j in good], [reqs[j][1] for j in good],
+            [reqs[j][2] for j in good], [reqs[j][3] for j in good])
+    stats = await asyncio.get_running_loop().run_in_executor(
+        None, lambda: native.decode_bodies(args[0], args[1], args[2], step, args[3], args[4], out, threads=threads))
+    for j, (series, _dropped, _unmatched) in zip(good, stats):
+        if series < 0:
+            log.warning("malformed response for %s", reqs[j][0].split("?")[0])
+            ok[j] = False
+    return ok
+
+
+class ResidentHistory:
+    def __init__(self, prom, device, ring_len: int = 10080, step: float = 60.0, clock=time.time,
+                 chunk_points: int = 1440, apps_per_query: int = 256, decode_threads: int = 8,
+                 min_capacity: int = 64, retain_s: float = 86400.0, dtype: Optional[torch.dtype] = None) -> None:
+        self.prom = prom
+        self.device = torch.device(device)
+        self.R, self.step, self.clock = int(ring_len), float(step), clock
+        self.chunk_pts = max(1, int(chunk_points))
+        self.apps_per_query = max(1, int(apps_per_query))
+        self.decode_threads = max(1, int(decode_threads))
+        self.min_capacity = max(1, int(min_capacity))
+        self.retain_s = float(retain_s)
+        self.dtype = dtype or (torch.bfloat16 if self.device.type == "cuda" else torch.float32)
+        self.ring: Optional[HistoryRing] = None
+        self.t_last = 0.0
+        self.rows: Dict[Key, int] = {}
+        self.keys: List[Optional[Key]] = []
+        self.refs: Dict[Key, int] = {}
+        self.last_used: Dict[Key, float] = {}
+        self.pending: Set[Key] = set()
+        self._tables: Optional[Dict[Tuple[str, str], native.KeyTable]] = None
+        self.history_queries = 0
+        self.tick_queries = 0
+        self.failed_queries = 0
+        self.reloads = 0
+
+    # ------------------------------------------------------------------ references
+    def want(self, keys: Iterable[Key], now: float) -> None:
+        for k in keys:
+            self.refs[k] = self.refs.get(k, 0) + 1
+            self.last_used[k] = now
+            if k not in self.rows:
+                self.pending.add(k)
+
+    def unwant(self, keys: Iterable[Key], now: float) -> None:
+        for k in keys:
+            n = self.refs.get(k, 0) - 1
+            if n > 0:
+                self.refs[k] = n
+            else:
+                self.refs.pop(k, None)
+            self.last_used[k] = now
+
+    def ready(self, key: Key) -> bool:
+        return key in self.rows and key not in self.pending
+
+    @property
+    def n_rows(self) -> int:
+        return len(self.rows)
+
+    # ------------------------------------------------------------------ storage
+    def _grow(self, capacity: int) -> None:
+        new = HistoryRing(capacity, self.R, self.dtype, self.device)
+        new.state.head, new.state.length = 0, self.R
+        if self.ring is not None:
+            n = self.ring.n
+            new._store[:n].copy_(self.ring._store)
+            new.state.head = self.ring.head
+        self.keys.extend([None] * (capacity - len(self.keys)))
+        self.ring = new
+
+    def _assign(self, now: float) -> List[Tuple[Key, int]]:
+        """Free expired rows, give pending keys rows; returns the (key, row)
+        pairs whose history must be (re)loaded."""
+        expired = [k for k in self.rows if k not in self.refs and now - self.last_used.get(k, 0.0) > self.retain_s]
+        freed = [self.rows.pop(k) for k in expired]
+        for k in expired:
+            self.last_used.pop(k, None)
+            self.pending.discard(k)
+        for row in freed:
+            self.keys[row] = None
+        self.pending = {k for k in self.pending if k in self.refs or k in self.rows}
+        new = sorted(k for k in self.pending if k not in self.rows)
+        need = len(self.rows) + len(new)
+        if self.ring is None or need > self.ring.n:
+            cap = max(self.min_capacity, self.ring.n if self.ring is not None else 1)
+            while cap < need:
+                cap *= 2
+            self._grow(cap)
+        if freed:
+            idx = torch.tensor(freed, dtype=torch.long, device=self.device)
+            self.ring._store.index_fill_(0, idx, float("nan"))
+        free = iter(i for i, k in enumerate(self.keys) if k is None)
+        for key in new:
+            row = next(free)
+            self.keys[row] = key
+            self.rows[key] = row
+        if expired or new:
+            self._tables = None
+        return sorted(((k, self.rows[k]) for k in self.pending), key=lambda kr: kr[1])
+
+    def _key_tables(self) -> Dict[Tuple[str, str], native.KeyTable]:
+        """Per metric family (endpoint, metric): (namespace, app) -> row."""
+        if self._tables is None:
+            fams: Dict[Tuple[str, str], List] = {}
+            for k, row in self.rows.items():
+                fams.setdefault((k[0], k[1]), []).append(((k[2], k[3]), row))
+            self._tables = {fam: native.KeyTable(v) for fam, v in fams.items()}
+        return self._tables
+
+    def _staging(self, rows: int, cols: int) -> Tuple[torch.Tensor, np.ndarray]:
+        t = torch.full((rows, cols), float("nan"), dtype=torch.float32)
+        if self.device.type == "cuda":
+            t = t.pin_memory()
+        return t, t.numpy()
+
+    # ------------------------------------------------------------------ sync
+    async def sync(self, now: Optional[float] = None) -> None:
+        """Advance the ring to ``now``, free expired rows, load pending keys."""
+        now = self.clock() if now is None else now
+        t_new = float(np.floor(now / self.step) * self.step)
+        if self.t_last == 0.0:
+            self.t_last = t_new
+        elif self.rows:
+            await self._advance(t_new)
+        else:
+            self.t_last = max(self.t_last, t_new)
+        todo = self._assign(now)
+        if todo:
+            await self._load(todo)
+
+    async def _advance(self, t_new: float) -> None:
+        n_new = int(round((t_new - self.t_last) / self.step))
+        if n_new <= 0:
+            return
+        if n_new >= self.R:  # down for longer than the ring: reload every row
+            self.t_last = t_new
+            self.ring.state.head = 0
+            self.ring._store.fill_(float("nan"))
+            self.pending |= set(self.rows)
+            self.reloads += 1
+            return
+        tables = self._key_tables()
+        block_t, block = self._staging(self.ring.n, n_new)
+        reqs, tabs = [], []
+        s = self.t_last + self.step
+        for fam, table in tables.items():
+            for c0 in range(0, n_new, self.chunk_pts):  # catch-up after an outage: time chunks
+                n = min(self.chunk_pts, n_new - c0)
+                reqs.append((range_url(fam[0], fam[1], s + c0 * self.step, n, self.step), s + c0 * self.step, n, c0))
+                tabs.append(table)
+        self.tick_queries += len(reqs)
+        ok = await fetch_decode(self.prom, reqs, tabs, block, self.step, self.decode_threads)
+        if not all(ok):
+            self.failed_queries += ok.count(False)
+            return  # all or nothing: the next sync fetches these minutes again
+        self._append(block_t, n_new)
+        self.t_last = t_new
+
+    def _append(self, block_t: torch.Tensor, n: int) -> None:
+        ring = self.ring
+        col = ring.head  # full ring: the oldest column is overwritten
+        if self.device.type == "cuda":
+            from ..ops import kernels as K
+            K.ring_append(ring.data, col, block_t.to(self.device, non_blocking=True))
+            ring.state.head = (ring.head + n) % self.R
+        else:
+            ring.append_(block_t)
+
+    async def _load(self, todo: List[Tuple[Key, int]]) -> None:
+        """The R points ending at ``t_last`` of the given rows, in (time chunk x
+        app group) queries, into one pinned block; one H2D and row scatter."""
+        R = self.R
+        first = self.t_last - (R - 1) * self.step
+        by_fam: Dict[Tuple[str, str], List[Tuple[Key, int]]] = {}
+        for i, (key, _row) in enumerate(todo):
+            by_fam.setdefault((key[0], key[1]), []).append((key, i))
+        block_t, block = self._staging(len(todo), R)
+        reqs, tabs, groups = [], [], []
+        for fam, items in by_fam.items():
+            for g in range(0, len(items), self.apps_per_query):
+                grp = items[g:g + self.apps_per_query]
+                table = native.KeyTable([((k[2], k[3]), i) for k, i in grp])
+                sel = (f'{fam[1]}{{namespace=~"{re_alt({k[2] for k, _ in grp})}",'
+                       f'app=~"{re_alt({k[3] for k, _ in grp})}"}}')
+                for c0 in range(0, R, self.chunk_pts):
+                    n = min(self.chunk_pts, R - c0)
+                    reqs.append((range_url(fam[0], sel, first + c0 * self.step, n, self.step),
+                                 first + c0 * self.step, n, c0))
+                    tabs.append(table)
+                    groups.append([k for k, _ in grp])
+        self.history_queries += len(reqs)
+        ok = await fetch_decode(self.prom, reqs, tabs, block, self.step, self.decode_threads)
+        failed: Set[Key] = set()
+        for good, keys in zip(ok, groups):
+            if not good:
+                failed.update(keys)
+        self.failed_queries += ok.count(False)
+        rows = torch.tensor([row for _, row in todo], dtype=torch.long)
+        self._write_rows(rows, block_t)
+        self.pending = {k for k in self.pending if k in failed}
+
+    def _write_rows(self, rows: torch.Tensor, values: torch.Tensor) -> None:
+        """``values [k, R]`` oldest first into the rotated ring (two column slices)."""
+        ring = self.ring
+        dev = self.device
+        rows = rows.to(dev)
+        v = values.to(dev, non_blocking=True).to(ring.data.dtype)
+        head, R = ring.head, self.R
+        n1 = R - head
+        ring.data[:, head:].index_copy_(0, rows, v[:, :n1])
+        if head:
+            ring.data[:, :head].index_copy_(0, rows, v[:, n1:])
+
+    def load_rows(self, keys: Sequence[Key], values: torch.Tensor) -> None:
+        """Adopt known histories (``values [k, R]`` oldest first, ending at
+        ``t_last``) for keys that already have rows — e.g. a warm node restored
+        from a snapshot, or a benchmark's synthetic week — without a fetch."""
+        rows = torch.tensor([self.rows[k] for k in keys], dtype=torch.long)
+        self._write_rows(rows, values)
+        self.pending -= set(keys)
+
+    async def assign_only(self, now: Optional[float] = None) -> None:
+        """Give pending keys rows without loading them (then :meth:`load_rows`)."""
+        now = self.clock() if now is None else now
+        if self.t_last == 0.0:
+            self.t_last = float(np.floor(now / self.step) * self.step)
+        self._assign(now)
+
+    # ------------------------------------------------------------------ reads
+    def gather(self, rows: Sequence[int], drop_newest: int = 0) -> Tuple[torch.Tensor, int, int]:
+        """Rows' histories for a batched fit: ``(hist [k, R] view of a 16-byte
+        aligned block, head, length)`` where the logical window is the ring's
+        minus its ``drop_newest`` newest points (a job's history ends at its
+        start time, ``metricsquery.go:73-79``)."""
+        ring = self.ring
+        idx = torch.as_tensor(list(rows), dtype=torch.long, device=self.device)
+        buf = torch.index_select(ring._store, 0, idx)
+        length = max(1, self.R - max(0, int(drop_newest)))
+        return buf[:, :self.R], ring.head, length
+
+    def column_time(self) -> float:
+        """Time of the newest column."""
+        return self.t_last

@@ -101,13 +101,19 @@ class BrainWorker:
         self.downstream = None  # per-caller joint LstmJobScorer (fp8), created on first downstream job
 
     def _claimable(self, d: Dict[str, Any]) -> bool:
-        """Strategies another component owns are skipped — except continuous jobs
-        the streaming shard cannot hold (per-caller series)."""
+        """Strategies a resident engine owns are skipped — except the jobs that
+        engine cannot key: continuous jobs with per-caller series
+        (streaming.is_streamable) and rollout jobs outside the rollout table
+        (rollout.is_rollout_keyable: other data sources, split families,
+        multi-metric algorithms)."""
         s = (d.get("strategy") or "").lower()
         if s not in self.exclude:
             return True
-        from .streaming import is_streamable
-        return s == "continuous" and not is_streamable(d)
+        if s == "continuous":
+            from .streaming import is_streamable
+            return not is_streamable(d)
+        from .rollout import STRATEGIES, is_rollout_keyable
+        return s in STRATEGIES and not is_rollout_keyable(d, self.cfg)
 
     # ------------------------------------------------------------------ planning
     def plan(self, doc: Dict[str, Any]) -> JobPlan:

@@ -932,3 +932,27 @@ def hw_update_detect(hist: torch.Tensor, col0: int, npts: int, t_last: int, m: i
     _set_hvar(a.det, det, grid, MODE_HW, m)
     nat.check(lib.fm_hw_update_detect(C.byref(a), nat.stream_handle(dev)), "fm_hw_update_detect")
     return out
+
+
+# ---------------------------------------------------------------------------------
+# one-shot job windows (brain/rollout.py)
+# ---------------------------------------------------------------------------------
+
+nat.register("fm_rollout_scatter", [C.c_void_p, C.c_longlong, C.c_int, C.c_int, C.c_void_p, C.c_longlong, C.c_int,
+                                    C.c_void_p, C.c_int, C.c_void_p])
+
+
+def rollout_scatter(win: torch.Tensor, P: int, Wc: int, src: torch.Tensor, col0: torch.Tensor) -> None:
+    """``win[n, p*Wc + col0[n] + j] = src[n*P + p, j]`` for the columns inside
+    ``[0, Wc)`` and non-NaN values (csrc/ingest.hip ``rollout_scatter_kernel``)."""
+    lib = nat.require()
+    _cuda(win, "win")
+    N = win.shape[0]
+    _need(win.dim() == 2 and win.dtype == torch.float32 and win.stride(1) == 1 and win.shape[1] == P * Wc,
+          f"win must be float32 [N, {P * Wc}] with unit inner stride")
+    _need(src.dim() == 2 and src.dtype == torch.float32 and src.stride(1) == 1 and src.shape[0] == N * P
+          and src.device == win.device, f"src must be float32 [{N * P}, k] on the device")
+    _vec(col0, N, torch.int32, "col0", win.device)
+    nat.check(lib.fm_rollout_scatter(nat.ptr(win), win.stride(0), int(P), int(Wc), nat.ptr(src), src.stride(0),
+                                     int(src.shape[1]), nat.ptr(col0), N, nat.stream_handle(win.device)),
+              "fm_rollout_scatter")

@@ -35,6 +35,7 @@ from .jobstore import JobStore, is_claimable
 INDEX = "documents"
 DOC_TYPE = "document"
 META_INDEX = "foremast-engine"
+BEAT_TYPE = "worker"  # worker heartbeats (lease renewal), next to the engine records
 
 
 class ElasticJobStore(JobStore):
@@ -108,24 +109,52 @@ class ElasticJobStore(JobStore):
                 return True
         return False
 
-    def _search(self, statuses, size: int = 1000) -> List[Tuple[Dict[str, Any], int]]:
-        body = {"query": {"bool": {"filter": [{"terms": {"status": list(statuses)}}]}},
+    def _search(self, statuses, size: int = 1000, extra=(), must_not=(), index: Optional[str] = None,
+                doc_type: Optional[str] = None) -> List[Tuple[Dict[str, Any], int]]:
+        filt = ([{"terms": {"status": list(statuses)}}] if statuses else []) + list(extra)
+        body = {"query": {"bool": {"filter": filt, "must_not": list(must_not)}},
                 "size": size, "version": True, "sort": [{"modified_ts": {"order": "asc"}}]}
-        resp = self.http.post(f"{self.base}/{self.index}/{self.doc_type}/_search", content=json.dumps(body),
-                              headers={"Content-Type": "application/json"})
+        resp = self.http.post(f"{self.base}/{index or self.index}/{doc_type or self.doc_type}/_search",
+                              content=json.dumps(body), headers={"Content-Type": "application/json"})
         if resp.status_code == 404:  # index not created yet
             return []
         resp.raise_for_status()
         hits = resp.json().get("hits", {}).get("hits", [])
         return [(h["_source"], int(h.get("_version", 1))) for h in hits]
 
+    def heartbeat(self, worker, now=None):
+        now = time.time() if now is None else float(now)
+        resp = self.http.put(f"{self.base}/{META_INDEX}/{BEAT_TYPE}/{worker}", params={"refresh": self.refresh},
+                             content=json.dumps({"worker": worker, "beat": now, "modified_ts": now}),
+                             headers={"Content-Type": "application/json"})
+        resp.raise_for_status()
+
+    def _beats(self, since: float) -> Dict[str, float]:
+        hits = self._search((), size=10000, extra=[{"range": {"beat": {"gte": since}}}], index=META_INDEX,
+                            doc_type=BEAT_TYPE)
+        return {d["worker"]: float(d["beat"]) for d, _ in hits if "worker" in d}
+
     def claim(self, worker, now=None, max_stuck_s=90.0, limit=64, only=None, steal_from=None):
+        """Two searches, so open jobs are never hidden behind thousands of live
+        leases: due open documents, then in-progress ones whose lease is stale
+        (not modified within ``max_stuck_s`` and the holder has no fresh
+        heartbeat) or held by a worker in ``steal_from``."""
         now = time.time() if now is None else now
-        out = []
-        for d, ver in self._search(r.OPEN_STATUSES + r.INPROGRESS_STATUSES):
+        cutoff = now - max_stuck_s
+        beats = self._beats(cutoff)
+        cand = self._search(r.OPEN_STATUSES)  # not_before is checked below (docs of other writers lack it)
+        cand += self._search(r.INPROGRESS_STATUSES, extra=[{"range": {"modified_ts": {"lt": cutoff}}}],
+                             must_not=[{"terms": {"claimed_by": sorted(beats)}}] if beats else [])
+        if steal_from:
+            cand += self._search(r.INPROGRESS_STATUSES, extra=[{"terms": {"claimed_by": sorted(steal_from)}}])
+        seen, out = set(), []
+        for d, ver in sorted(cand, key=lambda dv: dv[0].get("modified_ts", 0.0)):
             if len(out) >= limit:
                 break
-            if not is_claimable(d, now, max_stuck_s, steal_from) or (only is not None and not only(d)):
+            if d["id"] in seen:
+                continue
+            seen.add(d["id"])
+            if not is_claimable(d, now, max_stuck_s, steal_from, beats) or (only is not None and not only(d)):
                 continue
             d.update(status=r.ST_PREPROCESS_INPROGRESS, claimed_by=worker, claimed_at=now,
                      modified_ts=now, modified_at=format_rfc3339_nano(now))

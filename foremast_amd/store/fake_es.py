@@ -5,7 +5,7 @@ WSGI server for local runs).
 Supported: ``GET /``, ``GET|PUT /<index>/<type>/<id>`` (``?version=`` for
 optimistic concurrency → 409 on mismatch), ``PUT .../<id>/_create`` (409 if
 present), ``POST /<index>/<type>/_search`` with ``match_all`` or a
-``bool.filter[terms.status]`` query, ``size``, ``version`` and a single-key
+``bool.filter`` / ``bool.must_not`` of ``terms`` / ``term`` / ``range`` queries, ``size``, ``version`` and a single-key
 ``sort``.  Documents are versioned per id exactly like ES internal versions.
 """
 
@@ -91,12 +91,22 @@ class FakeElasticsearch:
         if not any(True for (i, _d) in self.docs if i == idx):
             return 404, {"error": {"type": "index_not_found_exception"}}
         q = body.get("query", {"match_all": {}})
-        statuses = None
-        for f in q.get("bool", {}).get("filter", []):
-            if "terms" in f and "status" in f["terms"]:
-                statuses = set(f["terms"]["status"])
-        if statuses is not None:
-            items = [x for x in items if x[1].get("status") in statuses]
+        b = q.get("bool", {})
+
+        def hit(doc, f) -> bool:
+            if "terms" in f:
+                (key, vals), = f["terms"].items()
+                return doc.get(key) in set(vals)
+            if "term" in f:
+                (key, val), = f["term"].items()
+                return doc.get(key) == val
+            if "range" in f:
+                (key, ops), = f["range"].items()
+                v = doc.get(key, 0)
+                return all({"lt": v < x, "lte": v <= x, "gt": v > x, "gte": v >= x}[op] for op, x in ops.items())
+            return True
+        items = [x for x in items if all(hit(x[1], f) for f in b.get("filter", []))
+                 and not any(hit(x[1], f) for f in b.get("must_not", []))]
         for s in body.get("sort", []):
             (key, spec), = s.items()
             items.sort(key=lambda x: x[1].get(key, 0), reverse=spec.get("order") == "desc")

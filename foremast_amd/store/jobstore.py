@@ -78,17 +78,27 @@ def new_document(req: r.DocumentRequest, job_id: str, now: Optional[float] = Non
     }
 
 
-def is_claimable(doc: Dict[str, Any], now: float, max_stuck_s: float, steal_from=None) -> bool:
+def is_claimable(doc: Dict[str, Any], now: float, max_stuck_s: float, steal_from=None,
+                 beats: Optional[Dict[str, float]] = None) -> bool:
     """Open (and due), stuck for longer than ``max_stuck_s``, or leased by a
     worker in ``steal_from`` (a brain rank the node has declared dead: its jobs
-    move at once instead of after the stuck-job timeout)."""
+    move at once instead of after the stuck-job timeout).
+
+    A lease is alive while the document was modified, or its holder sent a
+    worker heartbeat (``beats``: worker -> last :meth:`JobStore.heartbeat`),
+    within ``max_stuck_s``: a resident engine holding 100k series renews all of
+    its leases with one heartbeat per tick instead of one write per job."""
     st = doc.get("status")
     if st in r.OPEN_STATUSES:
         return float(doc.get("not_before", 0.0) or 0.0) <= now
     if st in r.INPROGRESS_STATUSES:
-        if steal_from and doc.get("claimed_by") in steal_from:
+        holder = doc.get("claimed_by")
+        if steal_from and holder in steal_from:
             return True
-        return now - float(doc.get("modified_ts", 0.0) or 0.0) > max_stuck_s
+        alive = float(doc.get("modified_ts", 0.0) or 0.0)
+        if beats and holder:
+            alive = max(alive, float(beats.get(holder, 0.0)))
+        return now - alive > max_stuck_s
     return False
 
 
@@ -107,12 +117,21 @@ class JobStore(abc.ABC):
         """Patch a document; with ``expect_claimed_by`` the write only lands if
         the caller still holds the lease (lost-update protection)."""
 
+    def update_many(self, items: List[tuple], expect_claimed_by: Optional[str] = None) -> List[bool]:
+        """``update`` for many ``(job_id, fields)`` (one transaction / lock where
+        the backend has one); returns which writes landed."""
+        return [self.update(j, f, expect_claimed_by=expect_claimed_by) for j, f in items]
+
     @abc.abstractmethod
     def claim(self, worker: str, now: Optional[float] = None, max_stuck_s: float = 90.0,
               limit: int = 64, only=None, steal_from=None) -> List[Dict[str, Any]]:
         """Lease up to ``limit`` claimable documents (``only(doc)`` filters,
         e.g. by strategy: the streaming monitor takes continuous jobs;
         ``steal_from``: worker ids whose leases are void, see is_claimable)."""
+
+    @abc.abstractmethod
+    def heartbeat(self, worker: str, now: Optional[float] = None) -> None:
+        """Renew every lease ``worker`` holds (see :func:`is_claimable`)."""
 
     @abc.abstractmethod
     def all(self) -> List[Dict[str, Any]]: ...
@@ -139,11 +158,45 @@ class JobStore(abc.ABC):
         pass
 
 
+def _stamp(d: Dict[str, Any], fields: Dict[str, Any]) -> None:
+    d.update(fields)
+    d["modified_ts"] = fields.get("modified_ts", time.time())
+    d["modified_at"] = format_rfc3339_nano(d["modified_ts"])
+
+
 class MemoryJobStore(JobStore):
+    """In-process table with claim indexes: open documents and in-progress
+    documents per lease holder, so a claim touches only the open jobs and the
+    leases of workers whose heartbeat is stale — not every document ever
+    created (a node holds tens of thousands of running jobs)."""
+
     def __init__(self) -> None:
         self._docs: Dict[str, Dict[str, Any]] = {}
         self._meta: Dict[str, Dict[str, Any]] = {}
+        self._open: Dict[str, Dict[str, Any]] = {}
+        self._held: Dict[str, Dict[str, Dict[str, Any]]] = {}   # holder -> in-progress docs
+        self._beats: Dict[str, float] = {}
         self._lock = threading.RLock()
+
+    def _index(self, d: Dict[str, Any], before: Optional[tuple] = None) -> None:
+        """Move ``d`` between the claim indexes after a status / holder change
+        (``before``: its (status, claimed_by) prior to the change)."""
+        jid = d["id"]
+        if before is not None:
+            st, holder = before
+            if st in r.OPEN_STATUSES:
+                self._open.pop(jid, None)
+            elif st in r.INPROGRESS_STATUSES:
+                h = self._held.get(holder or "")
+                if h is not None:
+                    h.pop(jid, None)
+                    if not h:
+                        del self._held[holder or ""]
+        st = d.get("status")
+        if st in r.OPEN_STATUSES:
+            self._open[jid] = d
+        elif st in r.INPROGRESS_STATUSES:
+            self._held.setdefault(d.get("claimed_by") or "", {})[jid] = d
 
     def get(self, job_id):
         with self._lock:
@@ -154,35 +207,56 @@ class MemoryJobStore(JobStore):
         with self._lock:
             if doc["id"] in self._docs:
                 return False
-            self._docs[doc["id"]] = copy.deepcopy(doc)
+            d = copy.deepcopy(doc)
+            self._docs[doc["id"]] = d
+            self._index(d)
             return True
+
+    def _update_locked(self, job_id, fields, expect_claimed_by):
+        d = self._docs.get(job_id)
+        if d is None:
+            return False
+        if expect_claimed_by is not None and d.get("claimed_by") != expect_claimed_by:
+            return False
+        before = (d.get("status"), d.get("claimed_by"))
+        _stamp(d, copy.deepcopy(fields))
+        self._index(d, before)
+        return True
 
     def update(self, job_id, fields, expect_claimed_by=None):
         with self._lock:
-            d = self._docs.get(job_id)
-            if d is None:
-                return False
-            if expect_claimed_by is not None and d.get("claimed_by") != expect_claimed_by:
-                return False
-            d.update(copy.deepcopy(fields))
-            now = time.time()
-            d["modified_ts"] = fields.get("modified_ts", now)
-            d["modified_at"] = format_rfc3339_nano(d["modified_ts"])
-            return True
+            return self._update_locked(job_id, fields, expect_claimed_by)
+
+    def update_many(self, items, expect_claimed_by=None):
+        with self._lock:
+            return [self._update_locked(j, f, expect_claimed_by) for j, f in items]
+
+    def heartbeat(self, worker, now=None):
+        with self._lock:
+            self._beats[worker] = time.time() if now is None else float(now)
 
     def claim(self, worker, now=None, max_stuck_s=90.0, limit=64, only=None, steal_from=None):
         now = time.time() if now is None else now
         out = []
         with self._lock:
-            for d in sorted(self._docs.values(), key=lambda x: x.get("modified_ts", 0.0)):
+            cand = list(self._open.values())
+            for holder, docs in self._held.items():
+                if steal_from and holder in steal_from:
+                    cand.extend(docs.values())
+                elif now - self._beats.get(holder, 0.0) > max_stuck_s:
+                    cand.extend(d for d in docs.values() if now - float(d.get("modified_ts", 0.0) or 0.0) > max_stuck_s)
+            cand.sort(key=lambda x: x.get("modified_ts", 0.0))
+            for d in cand:
                 if len(out) >= limit:
                     break
-                if is_claimable(d, now, max_stuck_s, steal_from) and (only is None or only(d)):
+                if is_claimable(d, now, max_stuck_s, steal_from, self._beats) and (only is None or only(d)):
+                    before = (d.get("status"), d.get("claimed_by"))
                     d["status"] = r.ST_PREPROCESS_INPROGRESS
                     d["claimed_by"] = worker
                     d["claimed_at"] = now
                     d["modified_ts"] = now
                     d["modified_at"] = format_rfc3339_nano(now)
+                    self._index(d, before)
                     out.append(copy.deepcopy(d))
         return out
 
@@ -201,7 +275,9 @@ class MemoryJobStore(JobStore):
 
 
 class SqliteJobStore(JobStore):
-    """Durable store; safe across processes (``BEGIN IMMEDIATE`` claims)."""
+    """Durable store; safe across processes (``BEGIN IMMEDIATE`` claims).  The
+    claim query selects only due open documents and in-progress documents whose
+    lease (document write and holder heartbeat) is stale, through indexed columns."""
 
     def __init__(self, path: str) -> None:
         self.path = path
@@ -212,8 +288,13 @@ class SqliteJobStore(JobStore):
             c.execute("PRAGMA journal_mode=WAL")
             c.execute("CREATE TABLE IF NOT EXISTS documents ("
                       "id TEXT PRIMARY KEY, status TEXT, modified_ts REAL, doc TEXT)")
-            c.execute("CREATE INDEX IF NOT EXISTS documents_status ON documents(status)")
+            cols = {row[1] for row in c.execute("PRAGMA table_info(documents)")}
+            for col, decl in (("claimed_by", "TEXT DEFAULT ''"), ("not_before", "REAL DEFAULT 0")):
+                if col not in cols:  # stores written by an older version
+                    c.execute(f"ALTER TABLE documents ADD COLUMN {col} {decl}")
+            c.execute("CREATE INDEX IF NOT EXISTS documents_status ON documents(status, modified_ts)")
             c.execute("CREATE TABLE IF NOT EXISTS meta (key TEXT PRIMARY KEY, value TEXT)")
+            c.execute("CREATE TABLE IF NOT EXISTS workers (worker TEXT PRIMARY KEY, beat REAL)")
 
     def _conn(self) -> sqlite3.Connection:
         c = getattr(self._local, "conn", None)
@@ -228,41 +309,61 @@ class SqliteJobStore(JobStore):
 
     def _insert_if_absent(self, doc):
         cur = self._conn().execute(
-            "INSERT OR IGNORE INTO documents(id, status, modified_ts, doc) VALUES (?,?,?,?)",
-            (doc["id"], doc["status"], doc["modified_ts"], json.dumps(doc)))
+            "INSERT OR IGNORE INTO documents(id, status, modified_ts, doc, claimed_by, not_before) "
+            "VALUES (?,?,?,?,?,?)",
+            (doc["id"], doc["status"], doc["modified_ts"], json.dumps(doc), doc.get("claimed_by", ""),
+             float(doc.get("not_before", 0.0) or 0.0)))
         return cur.rowcount == 1
 
+    def _write(self, c, d):
+        c.execute("UPDATE documents SET status=?, modified_ts=?, doc=?, claimed_by=?, not_before=? WHERE id=?",
+                  (d["status"], d["modified_ts"], json.dumps(d), d.get("claimed_by", "") or "",
+                   float(d.get("not_before", 0.0) or 0.0), d["id"]))
+
+    def _update_in(self, c, job_id, fields, expect_claimed_by):
+        row = c.execute("SELECT doc FROM documents WHERE id=?", (job_id,)).fetchone()
+        if row is None:
+            return False
+        d = json.loads(row[0])
+        if expect_claimed_by is not None and d.get("claimed_by") != expect_claimed_by:
+            return False
+        _stamp(d, fields)
+        self._write(c, d)
+        return True
+
     def update(self, job_id, fields, expect_claimed_by=None):
+        return self.update_many([(job_id, fields)], expect_claimed_by)[0]
+
+    def update_many(self, items, expect_claimed_by=None):
         c = self._conn()
         c.execute("BEGIN IMMEDIATE")
         try:
-            row = c.execute("SELECT doc FROM documents WHERE id=?", (job_id,)).fetchone()
-            if row is None:
-                c.execute("ROLLBACK")
-                return False
-            d = json.loads(row[0])
-            if expect_claimed_by is not None and d.get("claimed_by") != expect_claimed_by:
-                c.execute("ROLLBACK")
-                return False
-            d.update(fields)
-            d["modified_ts"] = fields.get("modified_ts", time.time())
-            d["modified_at"] = format_rfc3339_nano(d["modified_ts"])
-            c.execute("UPDATE documents SET status=?, modified_ts=?, doc=? WHERE id=?",
-                      (d["status"], d["modified_ts"], json.dumps(d), job_id))
+            res = [self._update_in(c, j, f, expect_claimed_by) for j, f in items]
             c.execute("COMMIT")
-            return True
+            return res
         except Exception:
             c.execute("ROLLBACK")
             raise
 
+    def heartbeat(self, worker, now=None):
+        self._conn().execute("INSERT OR REPLACE INTO workers(worker, beat) VALUES (?, ?)",
+                             (worker, time.time() if now is None else float(now)))
+
     def claim(self, worker, now=None, max_stuck_s=90.0, limit=64, only=None, steal_from=None):
         now = time.time() if now is None else now
+        cutoff = now - max_stuck_s
+        steal = sorted(steal_from or ())
         c = self._conn()
         c.execute("BEGIN IMMEDIATE")
         try:
+            q_open = ",".join("?" * len(r.OPEN_STATUSES))
+            q_prog = ",".join("?" * len(r.INPROGRESS_STATUSES))
+            q_steal = ("OR claimed_by IN (" + ",".join("?" * len(steal)) + ")") if steal else ""
             rows = c.execute(
-                "SELECT doc FROM documents WHERE status IN (?,?,?,?,?) ORDER BY modified_ts",
-                r.OPEN_STATUSES + r.INPROGRESS_STATUSES).fetchall()
+                f"SELECT doc FROM documents WHERE (status IN ({q_open}) AND not_before <= ?) OR "
+                f"(status IN ({q_prog}) AND ((modified_ts < ? AND COALESCE((SELECT beat FROM workers w "
+                f"WHERE w.worker = documents.claimed_by), 0) < ?) {q_steal})) ORDER BY modified_ts",
+                r.OPEN_STATUSES + (now,) + r.INPROGRESS_STATUSES + (cutoff, cutoff) + tuple(steal)).fetchall()
             out = []
             for (raw,) in rows:
                 if len(out) >= limit:
@@ -272,8 +373,7 @@ class SqliteJobStore(JobStore):
                     continue
                 d.update(status=r.ST_PREPROCESS_INPROGRESS, claimed_by=worker, claimed_at=now,
                          modified_ts=now, modified_at=format_rfc3339_nano(now))
-                c.execute("UPDATE documents SET status=?, modified_ts=?, doc=? WHERE id=?",
-                          (d["status"], now, json.dumps(d), d["id"]))
+                self._write(c, d)
                 out.append(d)
             c.execute("COMMIT")
             return out
