@@ -253,6 +253,7 @@ class RolloutMonitor:
         self.timings: Dict[str, float] = {}
         self._bands: Tuple[np.ndarray, np.ndarray, np.ndarray] = (np.zeros(0), np.zeros(0), np.zeros(0))
         self._last_anom: Dict[int, float] = {}
+        self._ids_dirty = False
         self._build_grid()
         self.anomalies = None
         self.metrics.add_band_source(f"rollout:{worker_id}", self._band_rows)
@@ -375,11 +376,14 @@ class RolloutMonitor:
         self.history.unwant([s.hkey for s in p.series], now)
         self._free_rows(p.rows)
         p.rows = []
-        self._refresh_apps()
 
     def _refresh_apps(self) -> None:
+        """App roster of the admitted jobs (index = row of the per-app counters).
+        Called only before scoring, so the roster :meth:`app_table` reports is
+        the one the last tick's counters were accumulated under."""
         names = sorted({p.app for p in self.jobs.values()})
-        if list(self.apps) != names:
+        changed = list(self.apps) != names
+        if changed:
             self.apps = {a: i for i, a in enumerate(names)}
             self.roster_version += 1
             if self.cap and self.app_stats.shape[0] < max(1, len(names)):
@@ -387,11 +391,12 @@ class RolloutMonitor:
                 while cap < len(names):
                     cap *= 2
                 self.app_stats = torch.zeros((cap, 2), dtype=torch.int32, device=self.device)
-            if self.cap:
-                ids = np.zeros(self.cap, dtype=np.int32)
-                for jid, p in self.jobs.items():
-                    ids[p.rows] = self.apps[p.app]
-                self.app_id.copy_(torch.from_numpy(ids))
+        if self.cap and (changed or self._ids_dirty):
+            ids = np.zeros(self.cap, dtype=np.int32)
+            for p in self.jobs.values():
+                ids[p.rows] = self.apps[p.app]
+            self.app_id.copy_(torch.from_numpy(ids))
+        self._ids_dirty = False
 
     # ------------------------------------------------------------------ admission
     async def _admit(self, now: float) -> int:
@@ -414,9 +419,9 @@ class RolloutMonitor:
         self._set_row_params(items)
         self._fit(items)
         await self._load_windows(items)
-        self._refresh_apps()
         self._tables = None
         self.admitted += len(ready)
+        self._ids_dirty = True
         self.timings["admit_ms"] = (time.perf_counter() - t0) * 1e3
         return len(ready)
 
@@ -707,6 +712,7 @@ class RolloutMonitor:
         await self.history.sync(now)
         self.timings["history_ms"] = (time.perf_counter() - t0) * 1e3
         await self._admit(now)
+        self._refresh_apps()
         written: Dict[str, str] = {}
         if not self.jobs:
             self.t_cur = max(self.t_cur, t_new)
@@ -820,7 +826,6 @@ class RolloutMonitor:
                 self._free_rows(p.rows)
                 for row in p.rows:
                     self._last_anom.pop(row, None)
-        self._refresh_apps()
         return written
 
     # ------------------------------------------------------------------ node integration

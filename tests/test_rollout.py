@@ -204,3 +204,45 @@ def test_rollout_release_and_failed_fetch_retry():
         n = mon.release(lambda d: d["appName"] == "b")
         assert n == 1 and store.get(ids["b"])["status"] == r.ST_REPROGRESS and ids["b"] not in mon.jobs
     asyncio.run(go())
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_node_brain_serves_rollout_jobs(device):
+    """Canary jobs through the production node brain (streaming + rollout
+    monitors on one rank): the GPU run writes the same verdicts and anomalous
+    points as the CPU reference run, and the node health table names the app."""
+    from foremast_amd.brain.node import NodeBrain
+    from foremast_amd.brain.streaming import StreamingMonitor
+
+    def run(dev):
+        clock, prom, store, ids = world()
+        cfg = config("holt_winters")
+        client = PromClient(transport=httpx.ASGITransport(app=prom.asgi_app()))
+        stream = StreamingMonitor(store, cfg, prom=client, device=torch.device(dev), ring_len=2880, window=10,
+                                  clock=clock)
+        roll = monitor(store, prom, clock, dev, cfg)
+        node = NodeBrain(stream, None, store, torch.device(dev), extra=(roll,))
+        tables = []
+
+        async def go():
+            for t in (T0, T0 + 60, T0 + 120, T0 + 180, T0 + 660):
+                clock.t = t
+                tables.append(await node.tick())
+        asyncio.run(go())
+        return {app: store.get(j) for app, j in ids.items()}, tables, node
+
+    docs, tables, node = run(device)
+    assert tables[2]["anomalous_apps"] == ["ns/a"] and tables[1]["anomalous_apps"] == []
+    assert store_status(docs) == {"a": r.ST_COMPLETED_UNHEALTH, "b": r.ST_COMPLETED_HEALTH,
+                                  "c": r.ST_COMPLETED_HEALTH}
+    if device != "cpu":
+        ref, _, _ = run("cpu")
+        assert store_status(ref) == store_status(docs)
+        got = json.loads(docs["a"]["anomalyInfo"])["error5xx"]["values"]
+        want = json.loads(ref["a"]["anomalyInfo"])["error5xx"]["values"]
+        assert got[0::2] == want[0::2]
+        np.testing.assert_allclose(got[1::2], want[1::2], rtol=1e-6)
+
+
+def store_status(docs):
+    return {app: d["status"] for app, d in docs.items()}
