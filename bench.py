@@ -71,8 +71,8 @@ METRICS_PER_APP = 5
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=None, help="timed ticks (default 20; node: 8)")
+    p.add_argument("--warmup", type=int, default=None, help="untimed ticks (default 5; node: 1)")
     p.add_argument("--series", type=int, default=100_000)
     p.add_argument("--ring", type=int, default=10080)
     p.add_argument("--season", type=int, default=1440)
@@ -122,10 +122,12 @@ def parse():
     p.add_argument("--baseline-model", default="canary", choices=["canary", "lstm", "multivariate"],
                    help="cpu_baseline: which GPU config's scorer the per-series CPU loop re-creates")
     p.add_argument("--config", default="canary",
-                   choices=["canary", "single", "hw10k", "lstm", "multivariate", "cpu_baseline"],
+                   choices=["canary", "single", "hw10k", "lstm", "multivariate", "cpu_baseline", "node"],
                    help="canary = headline (BASELINE configs 2/4 at 100k); single = config 1 (one latency "
                         "series, moving average, CPU brain plumbing end to end); hw10k = config 2 (10k series); "
-                        "lstm = config 3; multivariate = config 5 (fp8 LSTM, latency + error-rate)")
+                        "lstm = config 3; multivariate = config 5 (fp8 LSTM, latency + error-rate); node = the product "
+                        "path: canary jobs registered through the service and scored by the production node brain "
+                        "from Prometheus JSON (foremast_amd/benchmarks/node.py)")
     p.add_argument("--multi-cluster", action="store_true",
                    help="config 4 layout: each rank scrapes the baseline cluster of its neighbour's shard; "
                         "baseline windows reach their owner through one RCCL all-to-all per tick")
@@ -139,7 +141,12 @@ def parse():
     p.add_argument("--lstm-autograd", action="store_true", help="train with autograd instead of the fused K7 kernel")
     p.add_argument("--lstm-no-overlap", action="store_true",
                    help="run the training step and scoring back to back instead of on two HIP streams")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.steps is None:
+        a.steps = 8 if a.config == "node" else 20
+    if a.warmup is None:
+        a.warmup = 1 if a.config == "node" else 5
+    return a
 
 
 def _free_port() -> int:
@@ -740,6 +747,9 @@ def main():
         tick, health_host, meta, dtype_name, n_series = setup_single(args, world, rank, dev)
     elif args.config == "canary":
         tick, health_host, meta, dtype_name, n_series = setup_canary(args, world, rank, dev)
+    elif args.config == "node":
+        from foremast_amd.benchmarks.node import setup_node
+        tick, health_host, meta, dtype_name, n_series = setup_node(args, world, rank, dev)
     elif args.config == "lstm":
         tick, health_host, meta, dtype_name, n_series = setup_lstm(args, world, rank, dev, 1, False)
     else:
@@ -749,6 +759,9 @@ def main():
     table = meta.pop("_table", None)
     decoder = meta.pop("_decoder", None)
     truth = meta.pop("_truth", None)
+    scored_rows = meta.pop("_scored_rows", None)   # node: rows actually scored per tick
+    node_finish = meta.pop("_finish", None)
+    node_roll = meta.pop("_roll", None)
     for k in [k for k in meta if k.startswith("_")]:
         meta.pop(k)
     if truth is not None and world > 1:
@@ -810,13 +823,21 @@ def main():
         dist.all_reduce(lat_t, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
     lat_ms = lat_t.cpu().numpy() * 1e3
+    timed_rows = None
+    if scored_rows is not None:
+        rows_t = torch.tensor([float(sum(scored_rows[args.warmup:]))], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(rows_t)
+        timed_rows = float(rows_t.item())
+        tick_breakdown = {k: round(v, 3) for k, v in node_roll.timings.items()}
+        fin_s, statuses = node_finish()
     coll_ms = agg.flush_timings() if agg is not None else []
     if table is not None:
         health_host = table(health_host)
     anomalous_apps = int((health_host[:, 0] > 0).sum())
     scored = int(health_host[:, 1].sum())
     if rank == 0:
-        value = n_series * args.steps / elapsed
+        value = (timed_rows if timed_rows is not None else n_series * args.steps) / elapsed
         cfg_name = getattr(args, "config_name", args.config)
         config = {"model": meta.pop("model"), "global_batch": meta.pop("global_batch"),
                   "seq_len": meta.pop("seq_len"), "parallelism": f"dp{world}",
@@ -848,6 +869,9 @@ def main():
         }
         if decoder is not None:
             res["decode_ms_last_tick"] = round(decoder.last_decode_ms, 3)
+        if timed_rows is not None:
+            res["node"] = {"series_scored_timed": int(timed_rows), "tick_breakdown_ms_last": tick_breakdown,
+                           "completion_tick_s": round(fin_s, 3), "job_statuses_rank0": statuses}
         if args.config == "canary" and args.refit_every > 1:
             flags = np.array([REFIT_FLAGS.get(args.warmup + k, True) for k in range(args.steps)])
             res["refit_ticks_timed"] = int(flags.sum())

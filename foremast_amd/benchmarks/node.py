@@ -1,0 +1,302 @@
+"""``bench.py --config node``: the product path at node scale.
+
+The kernel headline (``--config canary``) times a ``StreamingShard`` the bench
+assembles itself.  This config times what production runs: N canary jobs x 5
+metrics registered through the service's create handler (the barrelman
+request, ``controller/queries.py`` = ``metricsquery.go``), claimed and scored by
+the production :class:`~foremast_amd.brain.node.NodeBrain` (streaming monitor
++ rollout monitor, ``brain/rollout.py``), with every datum arriving as
+Prometheus ``query_range`` JSON:
+
+* setup (untimed): synthetic Prometheus bodies for every query the brain will
+  issue are rendered in advance (an in-process server answers by URL — the
+  time of rendering JSON is Prometheus', not the brain's); the node is *warm*:
+  the resident 7-day history of every (app, metric) is in HBM, as after
+  earlier deployments or a snapshot restore (``brain/resident.py``);
+* register: every job goes through ``service.register`` (timed, reported);
+* intake tick (timed, reported separately): claim + plan of every job,
+  admission — the Holt-Winters grid fit of each (job, metric) on its history
+  ending at the job start (100k fits), baseline-pod windows fetched as JSON and
+  decoded;
+* scoring ticks (the timed steps; ``value``): from "this minute's bodies are
+  available" to "verdicts written to the job store": heartbeat, history
+  advance (one ``namespace_app_per_pod`` body per metric family), pod windows
+  (one ``namespace_pod`` body per family: every new pod's newest point),
+  native keyed decode, H2D, scatter, rank tests, band / verdict / per-app
+  counters, D2H, fail-fast writes of anomalous jobs, node health exchange;
+* completion tick (reported): every job reaches ``endTime`` and is written
+  ``completed_health`` (or stays unhealthy).
+
+Detection quality comes from the job statuses the brain wrote (x3 regressions
+on ``--anomaly-frac`` of the (job, metric) series, in the new pods only).
+"""
+
+from __future__ import annotations
+
+import asyncio
+import time
+from typing import Dict, List, Tuple
+from urllib.parse import parse_qs, unquote, urlsplit
+
+import numpy as np
+import torch
+
+T0 = 1_700_000_040.0     # deployment time of every job (aligned to the minute)
+STEP = 60.0
+METRICS = ("http_server_requests_error_5xx", "http_server_requests_latency", "http_server_requests_count",
+           "process_cpu_usage", "jvm_memory_used_bytes")
+ENDPOINT = "http://prometheus:9090/api/v1/"
+
+
+def _fmt(v: np.ndarray) -> List[str]:
+    return np.char.mod("%.9g", np.asarray(v, dtype=np.float64)).tolist()
+
+
+def _body(items: List[str]) -> bytes:
+    return ('{"status":"success","data":{"resultType":"matrix","result":[' + ",".join(items) + "]}}").encode()
+
+
+def _series(metric: str, labels: str, ts: np.ndarray, vals: List[str]) -> str:
+    pts = ",".join(f'[{int(t)},"{v}"]' for t, v in zip(ts.tolist(), vals))
+    return f'{{"metric":{{"__name__":"{metric}",{labels}}},"values":[{pts}]}}'
+
+
+class BodyServer:
+    """In-process Prometheus stand-in for the bench: ``fetch_raw_many`` returns
+    pre-rendered ``query_range`` bodies — per tick one body per family of every
+    app's (``namespace_app_per_pod``) or every new pod's (``namespace_pod``)
+    newest point; per family the baseline window of each old pod as a fragment,
+    joined for the pods a query's ``pod=~`` matcher names."""
+
+    def __init__(self) -> None:
+        self.tick_bodies: Dict[Tuple[str, float], bytes] = {}
+        self.fragments: Dict[Tuple[str, float], Dict[str, str]] = {}
+        self.requests = 0
+        self.bytes_served = 0
+
+    async def fetch_raw_many(self, urls) -> List[object]:
+        return [self._one(u) for u in urls]
+
+    def _one(self, url: str):
+        self.requests += 1
+        q = parse_qs(urlsplit(url).query)
+        query, start, end = unquote(q["query"][0]), float(q["start"][0]), float(q["end"][0])
+        if "{" not in query:
+            body = self.tick_bodies.get((query, end), _body([]))
+        else:
+            name = query.split("{", 1)[0]
+            frags = self.fragments.get((name, start), {})
+            pods = query.split('pod=~"', 1)[1].rsplit('"', 1)[0].split("|") if 'pod=~"' in query else []
+            body = _body([frags[p] for p in pods if p in frags])
+        self.bytes_served += len(body)
+        return body
+
+
+def setup_node(args, world, rank, dev):
+    from ..brain.node import NodeBrain, owner_of
+    from ..brain.rollout import RolloutMonitor
+    from ..brain.streaming import StreamingMonitor
+    from ..brain.engine import synthetic_eval, synthetic_params
+    from ..api import crd
+    from ..api import rest as r
+    from ..controller import queries
+    from ..service import app as svc
+    from ..store import MemoryJobStore
+    from ..utils.config import BrainConfig, reference_default_env
+    from ..utils.timeutil import format_rfc3339
+
+    if dev.type == "cpu" and args.series > 5000:
+        args.series, args.ring = 500, 2880
+    M = len(METRICS)
+    n_apps = args.series // M
+    P = args.pods
+    W = args.window
+    R, season = args.ring, args.season
+    ticks = args.warmup + args.steps + 1
+    if ticks > W:
+        raise SystemExit(f"--config node: warmup + steps + 1 = {ticks} ticks must fit in the {W}-minute watch window "
+                         f"(jobs finish at endTime); raise --window or lower --steps")
+    # this rank's apps: the node brain's ownership function (the shared store sees all jobs;
+    # each rank keeps its share, so a rank-local store holds exactly what that rank claims)
+    mine = [a for a in range(n_apps) if owner_of(f"ns{a % 200}", f"app{a}", world) == rank]
+    na = len(mine)
+    t_setup = time.perf_counter()
+    clock = {"t": T0}
+    server = BodyServer()
+    env = reference_default_env()
+    env.update(ML_ALGORITHM=args.algorithm, ML_PAIRWISE_ALGORITHM=args.pairwise,
+               MIN_HISTORICAL_DATA_POINT_TO_MEASURE="0", threshold="4", bound="3")
+    for i in range(5):  # every metric type: the headline's threshold 4, both bounds
+        env[f"threshold{i}"], env[f"bound{i}"] = "4", "3"
+    cfg = BrainConfig.from_env(env)
+    cfg.ring_len = R
+    cfg.season = season
+    store = MemoryJobStore()
+
+    # --- synthetic series: one seasonal model per (app, metric) ------------------------------
+    g = torch.Generator().manual_seed(1234)
+    gid = torch.tensor([a * M + j for a in mine for j in range(M)], dtype=torch.int64)  # global series id
+    params = synthetic_params(args.series, torch.device("cpu"), seed=1234)
+    params = {k: v[gid] for k, v in params.items()}
+    n_bad = int(round(args.anomaly_frac * args.series))
+    bad_global = set(torch.randperm(args.series, generator=g)[:n_bad].tolist())
+    bad = np.array([int(x) in bad_global for x in gid.tolist()])                   # [na * M]
+    truth_apps = sorted({mine[i // M] for i in np.nonzero(bad)[0].tolist()})
+    noise = 0.03 * params["lvl"][:, 0].numpy()
+    rng = np.random.default_rng(99 + rank)
+    ns = [f"ns{a % 200}" for a in mine]
+    app = [f"app{a}" for a in mine]
+
+    # --- history: resident (warm node), generated in chunks on the device ----------------------
+    roll = RolloutMonitor(store, cfg, prom=server, device=dev, worker_id=f"node-m{rank}-rollout", step=STEP,
+                          window=W, pods=P, clock=lambda: clock["t"], ring_len=R, min_capacity=na * M,
+                          decode_threads=args.decode_threads, apps_per_query=256)
+    keys = [(ENDPOINT, "namespace_app_per_pod:" + m, ns[i], app[i]) for i in range(na) for m in METRICS]
+    hist = roll.history
+    hist.clock = lambda: clock["t"]
+    hist.want(keys, T0)
+    asyncio.run(hist.assign_only(T0))
+    dparams = {k: v.to(dev) for k, v in params.items()}
+    for c0 in range(0, len(keys), 16384):
+        c1 = min(len(keys), c0 + 16384)
+        sub = {k: v[c0:c1] for k, v in dparams.items()}
+        hist.load_rows(keys[c0:c1], synthetic_eval(sub, 0, R, season, noise_seed=4321 + c0))
+    hist.unwant(keys, T0)  # retained for retain_s after their last job: the jobs re-reference them
+
+    # --- Prometheus bodies -------------------------------------------------------------------
+    # the newest point of minute T0 + 60 k is model time R - 1 + k; the job's baseline window
+    # [T0 - W min, T0] is model time R - 1 - W .. R - 1
+    new_pods = [[f"{app[i]}-v2-{p}-7d9f8b6c5d" for p in range(P)] for i in range(na)]
+    old_pods = [[f"{app[i]}-v1-{p}-5b6c7d8e9f" for p in range(P)] for i in range(na)]
+    app_lab = [f'"namespace":"{ns[i]}","app":"{app[i]}"' for i in range(na)]
+    newp_lab = [f'"namespace":"{ns[i]}","pod":"{pod}"' for i in range(na) for pod in new_pods[i]]
+    model = synthetic_eval(params, R - 1 - W, W + 1 + ticks + 1, season, None).numpy()   # [na*M, T] no noise
+    t_axis = T0 + STEP * (np.arange(model.shape[1]) - W)                                   # time of each column
+    col = {float(t): i for i, t in enumerate(t_axis.tolist())}
+    bad_m = bad.reshape(na, M)
+    for j, m in enumerate(METRICS):
+        rows = np.arange(na) * M + j
+        for k in range(ticks + 1):
+            ts = T0 + STEP * k
+            c = col[ts]
+            vals = model[rows, c] + rng.standard_normal(na) * noise[rows]
+            server.tick_bodies[("namespace_app_per_pod:" + m, ts)] = _body(
+                [f'{{"metric":{{"__name__":"namespace_app_per_pod:{m}",{lab}}},"values":[[{int(ts)},"{v}"]]}}'
+                 for lab, v in zip(app_lab, _fmt(vals))])
+            pv = (model[rows, c][:, None] + rng.standard_normal((na, P)) * noise[rows][:, None])
+            pv = np.where(bad_m[:, j][:, None], pv * 3.0, pv)    # the regressed deployments' new pods
+            server.tick_bodies[("namespace_pod:" + m, ts)] = _body(
+                [f'{{"metric":{{"__name__":"namespace_pod:{m}",{lab}}},"values":[[{int(ts)},"{v}"]]}}'
+                 for lab, v in zip(newp_lab, _fmt(pv.reshape(-1)))])
+        # baseline windows of the old pods: [T0 - W min, T0]
+        bt = t_axis[:W + 1]
+        base = model[rows, :W + 1][:, None, :] + rng.standard_normal((na, P, W + 1)) * noise[rows][:, None, None]
+        frags = {}
+        for i in range(na):
+            for p, pod in enumerate(old_pods[i]):
+                frags[pod] = _series("namespace_pod:" + m, f'"namespace":"{ns[i]}","pod":"{pod}"', bt,
+                                     _fmt(base[i, p]))
+        server.fragments[("namespace_pod:" + m, float(bt[0]))] = frags
+    del model
+
+    # --- jobs: the barrelman request of a canary rollout per app, through the service ---------
+    mets = crd.Metrics(data_source_type="prometheus", endpoint=ENDPOINT,
+                       monitoring=[crd.Monitoring(metric_name=m, metric_alias=f"m{j}") for j, m in enumerate(METRICS)])
+    reqs = []
+    for i in range(na):
+        info = queries.create_metrics_info(ns[i], app[i], [new_pods[i], old_pods[i]], mets, W, "canary", now=T0)
+        reqs.append(r.ApplicationHealthAnalyzeRequest(app_name=app[i], start_time=format_rfc3339(T0),
+                                                      end_time=format_rfc3339(T0 + W * STEP), metrics=info,
+                                                      strategy="canary").to_dict())
+    setup_s = time.perf_counter() - t_setup
+    t0 = time.perf_counter()
+    job_of = {}
+    for i, body in enumerate(reqs):
+        code, resp = svc.register(store, body)
+        assert code == 200, resp
+        job_of[resp["jobId"]] = mine[i]
+    register_s = time.perf_counter() - t0
+    del reqs
+
+    stream = StreamingMonitor(store, cfg, prom=server, device=dev, worker_id=f"node-m{rank}", ring_len=R,
+                              window=W, clock=lambda: clock["t"])
+    node = NodeBrain(stream, None, store, dev, publish=False, extra=(roll,))
+    node.owns = lambda d: True  # the rank-local store holds exactly this rank's share
+    for mon in node.monitors:
+        mon.owns = None
+    loop = asyncio.new_event_loop()
+    flagged = set()
+
+    def run_tick():
+        table = loop.run_until_complete(node.tick())
+        return table
+
+    # --- intake tick: claim + admission of every job --------------------------------------------
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run_tick()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    intake_s = time.perf_counter() - t0
+    assert len(roll.jobs) == na, f"admitted {len(roll.jobs)} of {na} jobs"
+    intake_timings = dict(roll.timings)
+
+    health = torch.zeros((n_apps, 2), dtype=torch.int32)
+    health[mine, 1] = 1
+    scored: List[int] = []
+
+    def tick(k):
+        clock["t"] = T0 + STEP * (k + 1)
+        n_rows = roll.n_live
+        table = run_tick()
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        scored.append(n_rows)
+        for a, v in table["apps"].items():
+            if v["anomalous"] > 0:
+                flagged.add(int(a.split("/app")[1]))
+        return table
+
+    def finish():
+        """The completion tick (every job past endTime) and the verdicts written."""
+        clock["t"] = T0 + STEP * W
+        t0 = time.perf_counter()
+        run_tick()
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        fin = time.perf_counter() - t0
+        st: Dict[str, int] = {}
+        for d in store.all():
+            st[d["status"]] = st.get(d["status"], 0) + 1
+            if d["status"] == r.ST_COMPLETED_UNHEALTH:
+                health[job_of[d["id"]], 0] = 1
+        return fin, st
+
+    meta = {
+        "model": f"{args.algorithm} + pairwise {args.pairwise} canary jobs on the production node brain "
+                 f"(rollout engine: model fitted at admission, per-tick pod windows)",
+        "global_batch": args.series,
+        "seq_len": R,
+        "season": season,
+        "jobs": n_apps,
+        "metrics_per_job": M,
+        "pods_new_old": [P, P],
+        "watch_window_min": W,
+        "path": "service.register -> store claim -> plan -> resident history -> fit at admission -> per tick: "
+                "history advance + pod windows as query_range JSON -> native decode -> H2D -> scatter -> rank tests "
+                "-> cached-state band/verdict -> D2H -> fail-fast writes -> node health exchange",
+        "warm_node": "resident 7-day history of every (app, metric) in HBM before the jobs arrive",
+        "setup_s": round(setup_s, 2),
+        "register_s": round(register_s, 3),
+        "register_jobs_per_s": round(na / max(register_s, 1e-9), 1),
+        "intake_s": round(intake_s, 3),
+        "intake_breakdown_ms": {k: round(v, 2) for k, v in intake_timings.items()},
+        "_scored_rows": scored,
+        "_finish": finish,
+        "_roll": roll,
+        "_server": server,
+        "_flagged": flagged,
+        "_truth": (truth_apps, n_apps),
+    }
+    return tick, health, meta, "bf16" if dev.type == "cuda" else "fp32", na * M

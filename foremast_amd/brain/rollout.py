@@ -49,6 +49,7 @@ import time
 from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Set, Tuple
+from urllib.parse import unquote
 
 import numpy as np
 import torch
@@ -124,10 +125,59 @@ def _pods_of(sel) -> Optional[Tuple[str, Tuple[str, ...]]]:
     return ns, tuple(sorted(set(pods)))
 
 
+_SIMPLE_SEL = re.compile(r'^([a-zA-Z_:][a-zA-Z0-9_:]*)\{((?:[a-zA-Z_][a-zA-Z0-9_]*(?:=~|=)"[^"\\]*",?)*)\}$')
+
+
+class _Sel:
+    __slots__ = ("name", "matchers")
+
+    def __init__(self, name, matchers):
+        self.name, self.matchers = name, matchers
+
+
+def _selector(q: str):
+    """The plain selectors barrelman writes (``name{l="v",l=~"a|b"}``, no
+    escapes) split without the general PromQL matcher regex; anything else
+    goes through :func:`parse_selector`."""
+    m = _SIMPLE_SEL.match(q)
+    if m is None:
+        return parse_selector(q)
+    out = []
+    for part in m.group(2).split('",'):
+        if not part:
+            continue
+        label, _, rest = part.partition("=")
+        op = "=~" if rest.startswith("~") else "="
+        out.append((label, op, rest[2 if op == "=~" else 1:].rstrip('"')))
+    return _Sel(m.group(1), tuple(out))
+
+
 def _grid(url: str) -> Tuple[str, object, float, float, float]:
-    p = urls.parse_prometheus_url(url)
-    return url.split("query_range?")[0], parse_selector(str(p["query"])), float(p["start"]), float(p["end"]), \
-        float(p["step"])
+    """(endpoint, selector, start, end, step) of a flattened Prometheus
+    ``query_range`` URL (``prometheushelper.go:12-27`` shape: four parameters,
+    only the query percent-encoded); other shapes take the general parser."""
+    ep, sep, qs = url.partition("query_range?")
+    fields = dict(kv.partition("=")[::2] for kv in qs.split("&")) if sep else {}
+    if set(fields) != {"query", "start", "end", "step"}:
+        p = urls.parse_prometheus_url(url)
+        return ep, parse_selector(str(p["query"])), float(p["start"]), float(p["end"]), float(p["step"])
+    return (ep, _selector(_unquote(fields["query"])), float(fields["start"]), float(fields["end"]),
+            float(fields["step"]))
+
+
+_ESC = (("%3A", ":"), ("%7B", "{"), ("%7D", "}"), ("%3D", "="), ("%22", '"'), ("%2C", ","), ("%7C", "|"),
+        ("%7E", "~"), ("%2F", "/"))
+
+
+def _unquote(q: str) -> str:
+    """Percent-decoding of a selector: the escapes a PromQL selector of k8s
+    names produces are replaced directly (C string ops); any other escape
+    takes ``urllib.parse.unquote``."""
+    if "%" not in q:
+        return q
+    for a, b in _ESC:
+        q = q.replace(a, b)
+    return unquote(q) if "%" in q else q
 
 
 _PLANS: "OrderedDict[Tuple[str, str], Optional[RolloutPlan]]" = OrderedDict()
@@ -210,6 +260,58 @@ def is_rollout_keyable(doc: Dict, cfg: BrainConfig) -> bool:
     return plan_rollout(doc, cfg) is not None
 
 
+class PodSlots:
+    """``(namespace, pod)`` -> slot: the row of a pod in each metric family's part
+    of the per-tick decode block.  Slots are reference counted by the jobs
+    watching the pod (two jobs on one pod share it); key hashes are computed
+    once per pod, so the per-family native key indexes are rebuilt from arrays
+    when the pod set changes, without touching Python strings."""
+
+    def __init__(self, cap: int = 1024) -> None:
+        self.index: Dict[Tuple[str, str], int] = {}
+        self.cap = int(cap)
+        self.refs = np.zeros(self.cap, dtype=np.int32)
+        self.hash = np.zeros(self.cap, dtype=np.uint64)
+        self.free: List[int] = list(range(self.cap - 1, -1, -1))
+        self.version = 0   # bumps when the pod set changes (key indexes rebuild)
+        self.grown = 0     # bumps when cap grows (every src row moves)
+
+    def acquire(self, keys: List[Tuple[str, str]]) -> np.ndarray:
+        new = list(dict.fromkeys(k for k in keys if k not in self.index))
+        if new:
+            while len(self.free) < len(new):
+                old = self.cap
+                self.cap *= 2
+                self.refs = np.concatenate([self.refs, np.zeros(old, dtype=np.int32)])
+                self.hash = np.concatenate([self.hash, np.zeros(old, dtype=np.uint64)])
+                self.free = list(range(self.cap - 1, old - 1, -1)) + self.free
+                self.grown += 1
+            hs = native.key_hashes([k[0] for k in new], [k[1] for k in new])
+            for k, h in zip(new, hs):
+                slot = self.free.pop()
+                self.index[k] = slot
+                self.hash[slot] = h
+            self.version += 1
+        slots = np.fromiter((self.index[k] for k in keys), dtype=np.int64, count=len(keys))
+        np.add.at(self.refs, slots, 1)
+        return slots
+
+    def release(self, keys: List[Tuple[str, str]]) -> None:
+        for k in keys:
+            slot = self.index.get(k)
+            if slot is None:
+                continue
+            self.refs[slot] -= 1
+            if self.refs[slot] <= 0:
+                self.refs[slot] = 0
+                del self.index[k]
+                self.free.append(slot)
+                self.version += 1
+
+    def live(self) -> np.ndarray:
+        return np.fromiter(self.index.values(), dtype=np.int64, count=len(self.index))
+
+
 class RolloutMonitor:
     def __init__(self, store: JobStore, cfg: Optional[BrainConfig] = None, prom=None, device=None,
                  worker_id: str = "rollout-0", metrics: Optional[BrainMetrics] = None, step: float = 60.0,
@@ -249,11 +351,16 @@ class RolloutMonitor:
         self.tick_queries = 0
         self.admitted = 0
         self.cap = 0
-        self._tables = None
+        self.slots = PodSlots()
+        self.fams: Dict[Tuple[str, str], int] = {}     # pod metric family -> index in the decode block
+        self._tables = None                            # (slots.version, cap, fam tables)
+        self._srcmap_dirty = True
         self.timings: Dict[str, float] = {}
         self._bands: Tuple[np.ndarray, np.ndarray, np.ndarray] = (np.zeros(0), np.zeros(0), np.zeros(0))
         self._last_anom: Dict[int, float] = {}
         self._ids_dirty = False
+        self._apps_dirty = False
+        self._n_live = 0
         self._build_grid()
         self.anomalies = None
         self.metrics.add_band_source(f"rollout:{worker_id}", self._band_rows)
@@ -306,6 +413,10 @@ class RolloutMonitor:
         self.app_stats = torch.zeros((max(1, len(self.apps)), 2), dtype=torch.int32, device=dev)
         self.row_plan.extend([None] * (cap - len(self.row_plan)))
         self.model_ok = np.concatenate([getattr(self, "model_ok", np.zeros(0, bool)), np.zeros(cap - n, bool)])
+        self.row_fam = np.concatenate([getattr(self, "row_fam", np.zeros(0, np.int64)), np.full(cap - n, -1)])
+        self.row_slot = np.concatenate([getattr(self, "row_slot", np.zeros((0, self.P), np.int64)),
+                                        np.full((cap - n, self.P), -1)])
+        self._srcmap_dirty = True
         self.cap = cap
         if self.gpu:
             from ..ops import kernels as K
@@ -321,7 +432,10 @@ class RolloutMonitor:
         for row in rows:
             self.row_plan[row] = None
             self.model_ok[row] = False
-        self._tables = None
+        self.row_fam[rows] = -1
+        self.row_slot[rows] = -1
+        self._n_live -= len(rows)
+        self._srcmap_dirty = True
 
     def _take_rows(self, n: int) -> List[int]:
         free = [i for i, p in enumerate(self.row_plan) if p is None]
@@ -336,7 +450,7 @@ class RolloutMonitor:
 
     @property
     def n_live(self) -> int:
-        return sum(len(p.series) for p in self.jobs.values())
+        return self._n_live
 
     # ------------------------------------------------------------------ membership
     def _claimable(self, d) -> bool:
@@ -375,12 +489,17 @@ class RolloutMonitor:
             return
         self.history.unwant([s.hkey for s in p.series], now)
         self._free_rows(p.rows)
+        self._apps_dirty = True
+        if p.rows:
+            self.slots.release(self._job_pods(p))
         p.rows = []
 
     def _refresh_apps(self) -> None:
         """App roster of the admitted jobs (index = row of the per-app counters).
         Called only before scoring, so the roster :meth:`app_table` reports is
         the one the last tick's counters were accumulated under."""
+        if not (self._apps_dirty or self._ids_dirty):
+            return
         names = sorted({p.app for p in self.jobs.values()})
         changed = list(self.apps) != names
         if changed:
@@ -396,7 +515,7 @@ class RolloutMonitor:
             for p in self.jobs.values():
                 ids[p.rows] = self.apps[p.app]
             self.app_id.copy_(torch.from_numpy(ids))
-        self._ids_dirty = False
+        self._ids_dirty = self._apps_dirty = False
 
     # ------------------------------------------------------------------ admission
     async def _admit(self, now: float) -> int:
@@ -415,11 +534,12 @@ class RolloutMonitor:
                 self.row_plan[row] = (p.doc_id, k)
                 items.append((row, s))
             self.jobs[p.doc_id] = p
+            self._n_live += len(p.series)
             heapq.heappush(self._ends, (p.end_ts, p.doc_id))
         self._set_row_params(items)
+        self._assign_slots(ready)
         self._fit(items)
         await self._load_windows(items)
-        self._tables = None
         self.admitted += len(ready)
         self._ids_dirty = True
         self.timings["admit_ms"] = (time.perf_counter() - t0) * 1e3
@@ -537,72 +657,100 @@ class RolloutMonitor:
         return {"level": ws.mean, "trend": torch.zeros(k), "sigma": ws.std, "nvalid": ws.count.float(),
                 "season_hb": torch.zeros((k, HB)), "best": torch.full((k,), -1, dtype=torch.int32)}
 
+    @staticmethod
+    def _job_pods(p: RolloutPlan) -> List[Tuple[str, str]]:
+        """The (namespace, pod) keys a job holds slots for (current pods, once per job)."""
+        return list(dict.fromkeys((s.namespace, pod) for s in p.series for pod in s.cur_pods))
+
+    def _fam(self, fam: Tuple[str, str]) -> int:
+        fi = self.fams.get(fam)
+        if fi is None:
+            fi = self.fams[fam] = len(self.fams)
+            self._tables = None
+        return fi
+
+    def _assign_slots(self, plans: List[RolloutPlan]) -> None:
+        P = self.P
+        for p in plans:
+            keys = self._job_pods(p)
+            slots = dict(zip(keys, self.slots.acquire(keys).tolist()))
+            for row, s in zip(p.rows, p.series):
+                self.row_fam[row] = self._fam(s.fam)
+                pods = s.cur_pods[:P]
+                self.row_slot[row, :len(pods)] = [slots[(s.namespace, pod)] for pod in pods]
+                self.row_slot[row, len(pods):] = -1
+        self._srcmap_dirty = True
+
+    def _srcmap(self) -> torch.Tensor:
+        """Device ``[cap * P]`` src row of every (row, pod): family x slot cap + slot."""
+        if self._srcmap_dirty or getattr(self, "_srcmap_grown", -1) != self.slots.grown:
+            fam = self.row_fam[:, None]
+            m = np.where((self.row_slot >= 0) & (fam >= 0), fam * self.slots.cap + self.row_slot, -1)
+            self._srcmap_t = torch.from_numpy(m.astype(np.int32).reshape(-1)).to(self.device)
+            self._srcmap_dirty = False
+            self._srcmap_grown = self.slots.grown
+        return self._srcmap_t
+
+    def _key_tables(self) -> Dict[Tuple[str, str], native.KeyTable]:
+        """Per pod family: native (namespace, pod) -> src row index over the live slots."""
+        key = (self.slots.version, self.slots.cap, len(self.fams))
+        if self._tables is None or self._tables[0] != key:
+            live = self.slots.live()
+            h = self.slots.hash[live]
+            used = {f for f in self.row_fam.tolist() if f >= 0}
+            tabs = {fam: native.KeyTable.indexed(h, fi * self.slots.cap + live, "namespace", "pod")
+                    for fam, fi in self.fams.items() if fi in used}
+            self._tables = (key, tabs)
+        return self._tables[1]
+
     async def _load_windows(self, items: List[Tuple[int, RolloutSeries]]) -> None:
         """Baseline windows (fixed: ``[start - W, start]``) and any current points
-        that already exist (a job claimed late), batched per pod family and
-        window start."""
+        that already exist (a job claimed late), per (kind, window start): one
+        query per pod family and group of jobs, every body decoded through one
+        key index over the group's pods, then gathered into the rows."""
         t_last = self.history.t_last
-        jobs = []
+        groups: Dict[Tuple[str, float, int], List[Tuple[int, RolloutSeries, Tuple[str, ...]]]] = {}
         for row, s in items:
             if s.base_pods and s.base_n > 0:
-                jobs.append(("base", row, s, s.base_pods, s.base_start, s.base_n))
+                groups.setdefault(("base", s.base_start, s.base_n), []).append((row, s, s.base_pods))
             if s.cur_n > 0 and s.cur_start <= t_last:
                 n = min(s.cur_n, int(round((t_last - s.cur_start) / self.step)) + 1)
-                jobs.append(("win", row, s, s.cur_pods, s.cur_start, n))
-        if not jobs:
-            return
-        groups: Dict[Tuple, List] = {}
-        for j in jobs:
-            groups.setdefault((j[0], j[2].fam, j[4], j[5]), []).append(j)
+                groups.setdefault(("win", s.cur_start, n), []).append((row, s, s.cur_pods))
         P, Wc = self.P, self.Wc
-        for (dst, fam, start, n), grp in groups.items():
-            for g in range(0, len(grp), self.apps_per_query):
-                part = grp[g:g + self.apps_per_query]
-                block_t = torch.full((len(part) * P, Wc), float("nan"), dtype=torch.float32)
-                if self.gpu:
-                    block_t = block_t.pin_memory()
-                pairs, dup = {}, []
-                for i, (_, _row, s, pods, _, _) in enumerate(part):
-                    for p, pod in enumerate(pods[:P]):
-                        key = (s.namespace, pod)
-                        if key in pairs:
-                            dup.append((i * P + p, pairs[key]))
-                        else:
-                            pairs[key] = i * P + p
-                table = native.KeyTable(list(pairs.items()), "namespace", "pod")
-                sel = (f'{fam[1]}{{namespace=~"{re_alt({k[0] for k in pairs})}",'
-                       f'pod=~"{re_alt({k[1] for k in pairs})}"}}')
-                ok = await fetch_decode(self.prom, [(range_url(fam[0], sel, start, n, self.step), start, n, 0)],
-                                        [table], block_t.numpy(), self.step, self.decode_threads)
-                if not ok[0]:
-                    log.warning("window fetch failed for %d rows of %s", len(part), fam[1])
-                b = block_t.numpy()
-                for d, src in dup:
-                    b[d] = b[src]
-                rows = torch.tensor([j[1] for j in part], dtype=torch.long, device=self.device)
-                vals = block_t.to(self.device, non_blocking=True).view(len(part), P * Wc)
-                tgt = self.base if dst == "base" else self.win
-                tgt.index_copy_(0, rows, vals)
-
-    # ------------------------------------------------------------------ tick
-    def _key_tables(self):
-        """Per pod family: (namespace, pod) -> flat row*P + pod, plus duplicate
-        (pod watched by two rows) copies."""
-        if self._tables is None:
-            fams: Dict[Tuple[str, str], Dict] = {}
-            dups: List[Tuple[int, int]] = []
-            for jid, p in self.jobs.items():
-                for row, s in zip(p.rows, p.series):
-                    d = fams.setdefault(s.fam, {})
-                    for k, pod in enumerate(s.cur_pods[:self.P]):
-                        key = (s.namespace, pod)
-                        if key in d:
-                            dups.append((row * self.P + k, d[key]))
-                        else:
-                            d[key] = row * self.P + k
-            self._tables = ({fam: native.KeyTable(list(d.items()), "namespace", "pod") for fam, d in fams.items()},
-                            np.array([a for a, _ in dups], dtype=np.int64), np.array([b for _, b in dups], dtype=np.int64))
-        return self._tables
+        for (dst, start, n), grp in groups.items():
+            pods = list(dict.fromkeys((s.namespace, pod) for _, s, ps in grp for pod in ps[:P]))
+            local = {k: i for i, k in enumerate(pods)}
+            fams = list(dict.fromkeys(s.fam for _, s, _ in grp))
+            fidx = {f: i for i, f in enumerate(fams)}
+            nl = len(pods)
+            hs = native.key_hashes([k[0] for k in pods], [k[1] for k in pods])
+            block_t = torch.full((len(fams) * nl, Wc), float("nan"), dtype=torch.float32)
+            if self.gpu:
+                block_t = block_t.pin_memory()
+            tables = {f: native.KeyTable.indexed(hs, fidx[f] * nl + np.arange(nl), "namespace", "pod") for f in fams}
+            reqs, tabs = [], []
+            for f in fams:
+                rows_f = [(s, ps) for _, s, ps in grp if s.fam == f]
+                for g in range(0, len(rows_f), self.apps_per_query):
+                    part = rows_f[g:g + self.apps_per_query]
+                    sel = (f'{f[1]}{{namespace=~"{re_alt({s.namespace for s, _ in part})}",'
+                           f'pod=~"{re_alt({pod for _, ps in part for pod in ps[:P]})}"}}')
+                    reqs.append((range_url(f[0], sel, start, n, self.step), start, n, 0))
+                    tabs.append(tables[f])
+            ok = await fetch_decode(self.prom, reqs, tabs, block_t.numpy(), self.step, self.decode_threads)
+            if not all(ok):
+                log.warning("%d of %d window queries failed (%s from %d)", ok.count(False), len(ok), dst, start)
+            gidx = np.full((len(grp), P), -1, dtype=np.int64)
+            for i, (_, s, ps) in enumerate(grp):
+                fo = fidx[s.fam] * nl
+                for p, pod in enumerate(ps[:P]):
+                    gidx[i, p] = fo + local[(s.namespace, pod)]
+            blk = block_t.to(self.device, non_blocking=True)
+            gi = torch.from_numpy(gidx).to(self.device)
+            vals = blk[gi.clamp(min=0)]                       # [k, P, Wc]
+            vals = torch.where((gi >= 0)[:, :, None], vals, torch.full_like(vals, float("nan")))
+            rows = torch.tensor([row for row, _, _ in grp], dtype=torch.long, device=self.device)
+            (self.base if dst == "base" else self.win).index_copy_(0, rows, vals.reshape(len(grp), P * Wc))
 
     async def _ingest(self, t_new: float) -> None:
         if self.t_cur == 0.0:
@@ -613,39 +761,37 @@ class RolloutMonitor:
             return
         k = min(k, 4 * self.Wc)  # behind by more than any window: only the recent minutes matter
         first = t_new - (k - 1) * self.step
-        tables, dst, src = self._key_tables()
+        tables = self._key_tables()
         P = self.P
-        block_t = torch.full((self.cap * P, k), float("nan"), dtype=torch.float32)
+        S = len(self.fams) * self.slots.cap
+        block_t = torch.empty((S, k), dtype=torch.float32)
         if self.gpu:
             block_t = block_t.pin_memory()
+        block = block_t.numpy()
+        block.fill(np.nan)
         reqs = [(range_url(fam[0], fam[1], first, k, self.step), first, k, 0) for fam in tables]
         self.tick_queries += len(reqs)
         t0 = time.perf_counter()
-        ok = await fetch_decode(self.prom, reqs, list(tables.values()), block_t.numpy(), self.step,
-                                self.decode_threads)
+        ok = await fetch_decode(self.prom, reqs, list(tables.values()), block, self.step, self.decode_threads)
         self.timings["decode_ms"] = (time.perf_counter() - t0) * 1e3
         if not all(ok):
             return  # t_cur stays: the next tick fetches these minutes again
-        if len(dst):
-            b = block_t.numpy()
-            b[dst] = b[src]
-        col0 = (int(round(first / self.step)) - self.start_min).to(torch.int32)
+        col0 = (int(round(first / self.step)) - self.start_min).to(torch.int32).contiguous()
+        srcmap = self._srcmap()
         if self.gpu:
             from ..ops import kernels as K
-            K.rollout_scatter(self.win, P, self.Wc, block_t.to(self.device, non_blocking=True), col0.contiguous())
+            K.rollout_scatter(self.win, P, self.Wc, block_t.to(self.device, non_blocking=True), col0, srcmap)
         else:
             win = self.win.view(self.cap, P, self.Wc)
-            src_v = block_t.view(self.cap, P, k)
-            pods = torch.arange(P)
+            sm = srcmap.view(self.cap, P).long()
+            src = block_t
             for j in range(k):
                 c = (col0 + j).long()
-                rr = torch.nonzero((c >= 0) & (c < self.Wc)).flatten()
-                if rr.numel() == 0:
-                    continue
-                vals = src_v[rr, :, j]
-                keep = ~torch.isnan(vals)
-                r2 = rr[:, None].expand(-1, P)[keep]
-                win[r2, pods[None, :].expand(rr.numel(), -1)[keep], c[r2]] = vals[keep]
+                ok_r = ((c >= 0) & (c < self.Wc))[:, None] & (sm >= 0)
+                vals = torch.where(ok_r, src[sm.clamp(min=0), j], torch.full(sm.shape, float("nan")))
+                keep = ok_r & ~torch.isnan(vals)
+                rr, pp = torch.nonzero(keep, as_tuple=True)
+                win[rr, pp, c[rr]] = vals[rr, pp]
         self.t_cur = t_new
 
     def _score(self) -> Dict[str, torch.Tensor]:
@@ -824,6 +970,8 @@ class RolloutMonitor:
                                                  self._last_anom.get(row))
                 self.history.unwant([s.hkey for s in p.series], now)
                 self._free_rows(p.rows)
+                self.slots.release(self._job_pods(p))
+                self._apps_dirty = True
                 for row in p.rows:
                     self._last_anom.pop(row, None)
         return written

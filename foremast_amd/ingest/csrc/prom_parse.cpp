@@ -929,3 +929,17 @@ long long fm_prom_decode_tick(int nb, const char* const* bufs, const long long* 
 }
 
 }  // extern "C"
+
+// Batch form of series_key for host-side tables: key i hashes a[i] + 0x1f + b[i]
+// where a[i] is A[a_off[i] .. a_off[i] + a_len[i]) (same for b): the rollout
+// engine keys tens of thousands of (namespace, pod) pairs per admission batch.
+extern "C" long long fm_key_hashes(const char* A, const long long* a_off, const long long* a_len, const char* B,
+                                   const long long* b_off, const long long* b_len, long long n, uint64_t* out) {
+  if (n < 0 || (n > 0 && (!A || !B || !a_off || !a_len || !b_off || !b_len || !out))) return -1;
+  for (long long i = 0; i < n; ++i) {
+    const char* a = A + a_off[i];
+    const char* b = B + b_off[i];
+    out[i] = series_key(a, a + a_len[i], b, b + b_len[i]);
+  }
+  return n;
+}

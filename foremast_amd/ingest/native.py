@@ -85,6 +85,8 @@ def _load() -> Optional[C.CDLL]:
         lib.fm_prom_decode_bodies.argtypes = [C.c_int, P, P, P, C.c_char_p, C.c_char_p, P, C.c_double, C.c_double, P,
                                               LL, P, P, LL, LL, C.c_int, C.c_int, P]
         lib.fm_prom_decode_bodies.restype = LL
+        lib.fm_key_hashes.argtypes = [C.c_char_p, P, P, C.c_char_p, P, P, LL, P]
+        lib.fm_key_hashes.restype = LL
         _lib = lib
         return lib
 
@@ -181,11 +183,37 @@ def key_hash(a: str, b: str) -> int:
     return h ^ (h >> 32)
 
 
+def key_hashes(a_list, b_list) -> np.ndarray:
+    """:func:`key_hash` of many ``(a[i], b[i])`` pairs (uint64), in one native call."""
+    n = len(a_list)
+    if len(b_list) != n:
+        raise ValueError("a_list and b_list differ in length")
+    lib = _load()
+    if lib is None or n == 0:
+        return np.array([key_hash(a, b) for a, b in zip(a_list, b_list)], dtype=np.uint64)
+    ea = [x.encode() for x in a_list]
+    eb = [x.encode() for x in b_list]
+    la = np.fromiter((len(x) for x in ea), dtype=np.int64, count=n)
+    lb = np.fromiter((len(x) for x in eb), dtype=np.int64, count=n)
+    oa = np.zeros(n, dtype=np.int64)
+    ob = np.zeros(n, dtype=np.int64)
+    np.cumsum(la[:-1], out=oa[1:])
+    np.cumsum(lb[:-1], out=ob[1:])
+    out = np.empty(n, dtype=np.uint64)
+    A, B = b"".join(ea) or b"\0", b"".join(eb) or b"\0"
+    if lib.fm_key_hashes(A, oa.ctypes.data, la.ctypes.data, B, ob.ctypes.data, lb.ctypes.data, n,
+                         out.ctypes.data) != n:
+        raise RuntimeError("fm_key_hashes failed")
+    return out
+
+
 class KeyTable:
     """Sorted (hash → row) table of a shard's series keys for the keyed scatter."""
 
     def __init__(self, keys_rows, label_a: str = "namespace", label_b: str = "app") -> None:
-        given = [(key_hash(a, b), int(r)) for (a, b), r in keys_rows]
+        keys_rows = list(keys_rows)
+        hs = key_hashes([a for (a, _), _ in keys_rows], [b for (_, b), _ in keys_rows]).tolist() if keys_rows else []
+        given = [(h, int(r)) for h, (_, r) in zip(hs, keys_rows)]
         pairs = sorted(given)
         hs = [h for h, _ in pairs]
         if len(set(hs)) != len(hs):
@@ -197,6 +225,17 @@ class KeyTable:
         self._ix_hash = np.array([h for h, _ in given], dtype=np.uint64)
         self._ix_rows = np.array([r for _, r in given], dtype=np.int64)
         self.label_a, self.label_b = label_a.encode(), label_b.encode()
+
+    @classmethod
+    def indexed(cls, hashes: np.ndarray, rows: np.ndarray, label_a: str = "namespace",
+                label_b: str = "app") -> "KeyTable":
+        """A table for the native index only (no sorted copy): duplicate keys are
+        reported when the index is built."""
+        t = cls([], label_a, label_b)
+        t._ix_hash = np.ascontiguousarray(hashes, dtype=np.uint64)
+        t._ix_rows = np.ascontiguousarray(rows, dtype=np.int64)
+        t.hash, t.rows = t._ix_hash, t._ix_rows
+        return t
 
     @classmethod
     def from_hashes(cls, hashes: np.ndarray, rows: np.ndarray, label_a: str = "namespace",

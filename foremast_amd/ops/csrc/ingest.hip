@@ -145,13 +145,15 @@ extern "C" int fm_tick_advance(int* state, int R, int W, const int* h_table, int
 // one (job, metric) of a job that started at its own minute, laid out pod-major
 // as P pods x Wc minutes of the job's current window (column c = minute c + 1
 // after the job's start, so every row forecasts the same horizons).  A tick's
-// decoded points arrive as src [N*P, k] (row n*P + p = pod p of row n, k
-// consecutive minutes starting at the tick's first new minute); col0[n] is the
-// window column of that first minute for row n (negative / >= Wc: outside the
-// job's window, dropped).  Missing points (NaN) never overwrite a value.  One
-// thread per (row, pod, minute).
+// decoded points arrive as src [S, k] (one row per (metric family, pod) the
+// node watches, k consecutive minutes starting at the tick's first new minute);
+// srcmap[n*P + p] is the src row of pod p of row n (-1: no such pod) and
+// col0[n] the window column of the first minute for row n (negative / >= Wc:
+// outside the job's window, dropped).  Missing points (NaN) never overwrite a
+// value.  One thread per (row, pod, minute).
 __global__ __launch_bounds__(256) void rollout_scatter_kernel(float* __restrict__ win, long long ld_w, int P, int Wc,
                                                               const float* __restrict__ src, long long ld_s, int k,
+                                                              long long S, const int* __restrict__ srcmap,
                                                               const int* __restrict__ col0, int N) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long total = (long long)N * P * k;
@@ -161,17 +163,20 @@ __global__ __launch_bounds__(256) void rollout_scatter_kernel(float* __restrict_
   const int n = (int)(np / P), p = (int)(np % P);
   const int c = col0[n] + j;
   if (c < 0 || c >= Wc) return;
-  const float v = src[np * ld_s + j];
+  const long long sr = srcmap ? (long long)srcmap[np] : np;
+  if (sr < 0 || sr >= S) return;
+  const float v = src[sr * ld_s + j];
   if (v == v) win[(long long)n * ld_w + p * Wc + c] = v;
 }
 
 extern "C" int fm_rollout_scatter(float* win, long long ld_w, int P, int Wc, const float* src, long long ld_s, int k,
-                                  const int* col0, int N, hipStream_t st) {
+                                  long long S, const int* srcmap, const int* col0, int N, hipStream_t st) {
   if (N <= 0 || k <= 0) return 0;
-  if (!win || !src || !col0 || P <= 0 || Wc <= 0 || ld_w < (long long)P * Wc || ld_s < k)
+  if (!win || !src || !col0 || P <= 0 || Wc <= 0 || ld_w < (long long)P * Wc || ld_s < k || S < 0 ||
+      (!srcmap && S < (long long)N * P))
     return (int)hipErrorInvalidValue;
   const long long total = (long long)N * P * k;
   hipLaunchKernelGGL(rollout_scatter_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, win, ld_w, P,
-                     Wc, src, ld_s, k, col0, N);
+                     Wc, src, ld_s, k, S, srcmap, col0, N);
   return (int)hipGetLastError();
 }

@@ -939,20 +939,26 @@ def hw_update_detect(hist: torch.Tensor, col0: int, npts: int, t_last: int, m: i
 # ---------------------------------------------------------------------------------
 
 nat.register("fm_rollout_scatter", [C.c_void_p, C.c_longlong, C.c_int, C.c_int, C.c_void_p, C.c_longlong, C.c_int,
-                                    C.c_void_p, C.c_int, C.c_void_p])
+                                    C.c_longlong, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p])
 
 
-def rollout_scatter(win: torch.Tensor, P: int, Wc: int, src: torch.Tensor, col0: torch.Tensor) -> None:
-    """``win[n, p*Wc + col0[n] + j] = src[n*P + p, j]`` for the columns inside
-    ``[0, Wc)`` and non-NaN values (csrc/ingest.hip ``rollout_scatter_kernel``)."""
+def rollout_scatter(win: torch.Tensor, P: int, Wc: int, src: torch.Tensor, col0: torch.Tensor,
+                    srcmap: Optional[torch.Tensor] = None) -> None:
+    """``win[n, p*Wc + col0[n] + j] = src[srcmap[n*P + p], j]`` (``srcmap`` None:
+    row ``n*P + p``) for the columns inside ``[0, Wc)``, mapped pods and non-NaN
+    values (csrc/ingest.hip ``rollout_scatter_kernel``)."""
     lib = nat.require()
     _cuda(win, "win")
     N = win.shape[0]
     _need(win.dim() == 2 and win.dtype == torch.float32 and win.stride(1) == 1 and win.shape[1] == P * Wc,
           f"win must be float32 [N, {P * Wc}] with unit inner stride")
-    _need(src.dim() == 2 and src.dtype == torch.float32 and src.stride(1) == 1 and src.shape[0] == N * P
-          and src.device == win.device, f"src must be float32 [{N * P}, k] on the device")
+    _need(src.dim() == 2 and src.dtype == torch.float32 and src.stride(1) == 1 and src.device == win.device,
+          "src must be float32 [S, k] on the device")
+    if srcmap is None:
+        _need(src.shape[0] >= N * P, f"src must have >= {N * P} rows without a srcmap")
+    else:
+        _vec(srcmap, N * P, torch.int32, "srcmap", win.device)
     _vec(col0, N, torch.int32, "col0", win.device)
     nat.check(lib.fm_rollout_scatter(nat.ptr(win), win.stride(0), int(P), int(Wc), nat.ptr(src), src.stride(0),
-                                     int(src.shape[1]), nat.ptr(col0), N, nat.stream_handle(win.device)),
-              "fm_rollout_scatter")
+                                     int(src.shape[1]), int(src.shape[0]), nat.ptr(srcmap), nat.ptr(col0), N,
+                                     nat.stream_handle(win.device)), "fm_rollout_scatter")
