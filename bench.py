@@ -53,7 +53,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-from foremast_amd.brain.engine import (ShardSpec, StreamingShard, synthetic_eval,  # noqa: E402
+from foremast_amd.brain.engine import (ShardSpec, StreamingShard, global_randn, synthetic_eval,  # noqa: E402
                                        synthetic_history, synthetic_params)
 from foremast_amd.parallel import comm  # noqa: E402
 from foremast_amd.parallel.health import HealthAggregator, shard_range  # noqa: E402
@@ -208,23 +208,28 @@ def barrier(dev):
 NOISE = 0.03  # synthetic noise sigma as a fraction of the level (engine.synthetic_eval default)
 
 
-def make_ticks(params, pods, nticks, season, t0, seed, anomaly_frac, kind="scale3", want_bad=False, size=3.0):
+def make_ticks(params, pods, nticks, season, t0, seed, anomaly_frac, kind="scale3", want_bad=False, size=3.0,
+               row0=0, n_global=None):
     """Per-tick per-pod values ``[nticks, n, pods]`` continuing each series'
     synthetic model past the history (same noise level as the history), with a
     fraction of series turned anomalous: ``scale3`` (canary regression, values
     x3) or ``shift3sigma`` (level shift of +3 noise sigma); ``scale`` / ``shift``
-    use ``size`` instead of 3.  ``want_bad``: also
-    return the regressed series' indices (detection-quality ground truth)."""
+    use ``size`` instead of 3.  ``want_bad``: also return the regressed series'
+    LOCAL indices (detection-quality ground truth).  ``row0`` / ``n_global``: the
+    local series are global ``row0 ..`` of ``n_global``; noise and the regressed
+    set are functions of the global index, so every sharding scores the same data."""
     lvl = params["lvl"]
     n, dev = lvl.shape[0], lvl.device
-    g = torch.Generator(device=dev)
-    g.manual_seed(seed + 17)
+    n_global = n if n_global is None else n_global
     vals = synthetic_eval(params, t0, nticks, season, None).T.contiguous()  # [nticks, n]
-    out = vals[..., None] + torch.randn((nticks, n, pods), generator=g, device=dev) * (NOISE * lvl[:, 0])[None, :, None]
-    n_bad = int(n * anomaly_frac)
+    eps = global_randn(lambda r: (nticks, r, pods), n, row0, seed + 17, dev, dim=1)
+    out = vals[..., None] + eps * (NOISE * lvl[:, 0])[None, :, None]
+    n_bad = int(n_global * anomaly_frac)
     bad = torch.zeros(0, dtype=torch.int64, device=dev)
     if n_bad:
-        bad = torch.randperm(n, generator=g, device=dev)[:n_bad]
+        g = torch.Generator().manual_seed(seed + 17)
+        gbad = torch.randperm(n_global, generator=g)[:n_bad]
+        bad = (gbad[(gbad >= row0) & (gbad < row0 + n)] - row0).to(dev)
         k = 3.0 if kind in ("scale3", "shift3sigma") else float(size)
         if kind.startswith("scale"):
             out[:, bad, :] *= k
@@ -278,12 +283,16 @@ def setup_canary(args, world, rank, dev):
     if args.serial_pairwise:
         shard.overlap_pairwise = False
     # --- synthetic data (outside the timed region) ---------------------------------
-    params = synthetic_params(n_local, dev, seed=1234 + rank)
-    hist = synthetic_eval(params, 0, args.ring, args.season, noise_seed=4321 + rank)
+    # every datum is a function of the GLOBAL series index: N ranks score exactly the
+    # series the one-rank run scores (tests/test_parallel.py::test_bench_n_rank_equals_one_rank)
+    params = synthetic_params(args.series, dev, seed=1234, rows=(s, e))
+    hist = synthetic_eval(params, 0, args.ring, args.season, noise_seed=4321, row0=s)
     if args.gap_frac > 0:
-        g = torch.Generator().manual_seed(77 + rank)
-        rows = torch.randperm(n_local, generator=g)[: int(round(args.gap_frac * n_local))]
-        starts = torch.randint(args.season, args.ring - 30, (rows.numel(),), generator=g)
+        g = torch.Generator().manual_seed(77)
+        grows = torch.randperm(args.series, generator=g)[: int(round(args.gap_frac * args.series))]
+        gstarts = torch.randint(args.season, args.ring - 30, (grows.numel(),), generator=g)
+        mine = (grows >= s) & (grows < e)
+        rows, starts = grows[mine] - s, gstarts[mine]
         cols = (starts[:, None] + torch.arange(30)[None, :]).reshape(-1)
         hist[rows.repeat_interleave(30).to(hist.device), cols.to(hist.device)] = float("nan")
     shard.load_history(hist)
@@ -292,17 +301,18 @@ def setup_canary(args, world, rank, dev):
     total_ticks = args.warmup + args.steps
     # per tick: P canary-pod values (a fraction of series regressed) and P
     # baseline-pod values (healthy, same times) -> [ticks, N, 2P]
-    cur_t, bad = make_ticks(params, P, total_ticks + W, args.season, args.ring, 99 + rank, args.anomaly_frac,
-                            args.anomaly_kind, want_bad=True, size=args.anomaly_size)
+    cur_t, bad = make_ticks(params, P, total_ticks + W, args.season, args.ring, 99, args.anomaly_frac,
+                            args.anomaly_kind, want_bad=True, size=args.anomaly_size, row0=s, n_global=args.series)
     truth_apps = sorted(set(((bad.cpu() + s) // METRICS_PER_APP).tolist()))
     exch = None
     if args.multi_cluster:
         # this rank scrapes the baseline pods of the neighbour's shard
         from foremast_amd.parallel import canary
         r_ids = canary.remote_baseline_ids(args.series, world, rank, align=METRICS_PER_APP).to(dev)
-        r_rank = (rank + 1) % world
-        r_params = synthetic_params(int(r_ids.numel()), dev, seed=1234 + r_rank)
-        base_t = make_ticks(r_params, P, total_ticks + W, args.season, args.ring, 7 + r_rank, 0.0)
+        r0 = int(r_ids[0]) if r_ids.numel() else 0
+        r_params = synthetic_params(args.series, dev, seed=1234, rows=(r0, r0 + int(r_ids.numel())))
+        base_t = make_ticks(r_params, P, total_ticks + W, args.season, args.ring, 7, 0.0, row0=r0,
+                            n_global=args.series)
         owner = canary.owner_of(r_ids, canary.shard_starts(args.series, world, METRICS_PER_APP, dev))
         exch = canary.WindowExchanger(r_ids, owner, P)
         local_rows = (exch.recv_ids - s).long()
@@ -315,7 +325,7 @@ def setup_canary(args, world, rank, dev):
         base_dev = torch.empty((base_t.shape[1], P), dtype=torch.float32, device=dev)
         del base_t
     else:
-        base_t = make_ticks(params, P, total_ticks + W, args.season, args.ring, 7 + rank, 0.0)
+        base_t = make_ticks(params, P, total_ticks + W, args.season, args.ring, 7, 0.0, row0=s, n_global=args.series)
         ticks = torch.cat([cur_t, base_t], 2)
         del base_t
     del cur_t
@@ -526,13 +536,13 @@ def setup_lstm(args, world, rank, dev, n_features, fp8):
     shard = LstmShard(n_local, args.ring, F, window=args.lstm_window, hidden=64, fp8=fp8, device=dev,
                       app_id=app_id, n_apps=n_apps, threshold=4.0, train_batch=args.lstm_train_batch,
                       lr=1e-3, seed=0, fused_train=not args.lstm_autograd, restat_every=args.lstm_restat_every)
-    params = [synthetic_params(n_local, dev, seed=1234 + 7 * f + 101 * rank) for f in range(F)]
-    shard.load_history([synthetic_eval(p, 0, args.ring, args.season, noise_seed=555 + f + 101 * rank)
+    params = [synthetic_params(n_ent, dev, seed=1234 + 7 * f, rows=(s, e)) for f in range(F)]
+    shard.load_history([synthetic_eval(p, 0, args.ring, args.season, noise_seed=555 + f, row0=s)
                         for f, p in enumerate(params)])
     total = args.warmup + args.steps
     # the same entities regress on every metric (seed shared across features)
-    tk = [make_ticks(p, 1, total, args.season, args.ring, 99 + rank, args.anomaly_frac, args.anomaly_kind,
-                     want_bad=True, size=args.anomaly_size) for p in params]
+    tk = [make_ticks(p, 1, total, args.season, args.ring, 99, args.anomaly_frac, args.anomaly_kind,
+                     want_bad=True, size=args.anomaly_size, row0=s, n_global=n_ent) for p in params]
     ticks = torch.stack([t[..., 0] for t, _ in tk], 2)  # [ticks, n, F]
     truth_apps = sorted(set(((tk[0][1].cpu() + s) // ent_per_app).tolist()))
     bad_local = tk[0][1].cpu()

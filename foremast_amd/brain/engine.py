@@ -20,7 +20,7 @@ On CPU (tests, no GPU) the same API runs the PyTorch reference scorers.
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Dict, Optional
+from typing import Dict, Optional, Tuple
 
 import numpy as np
 import torch
@@ -514,41 +514,66 @@ class StreamingShard:
         return self.out
 
 
-def synthetic_params(N: int, device, seed: int = 0) -> Dict[str, torch.Tensor]:
+def synthetic_params(N: int, device, seed: int = 0, rows: Optional[Tuple[int, int]] = None) -> Dict[str, torch.Tensor]:
     """Per-series parameters of the synthetic seasonal model: level, daily
-    amplitude, phase, linear trend (each ``[N, 1]``)."""
+    amplitude, phase, linear trend (each ``[N, 1]``).  ``rows = (s, e)``: only
+    global series ``s .. e-1`` of the ``N`` (a rank's shard gets exactly the
+    parameters the one-rank run gives those series)."""
     g = torch.Generator(device=device)
     g.manual_seed(seed)
     lvl = torch.rand((N, 1), generator=g, device=device) * 95 + 5
     amp = (torch.rand((N, 1), generator=g, device=device) * 0.25 + 0.05) * lvl
     ph = torch.rand((N, 1), generator=g, device=device) * 6.283
     tr = (torch.rand((N, 1), generator=g, device=device) - 0.5) * 1e-4 * lvl
-    return {"lvl": lvl, "amp": amp, "ph": ph, "tr": tr}
+    out = {"lvl": lvl, "amp": amp, "ph": ph, "tr": tr}
+    if rows is not None:
+        out = {k: v[rows[0]:rows[1]].contiguous() for k, v in out.items()}
+    return out
+
+
+NOISE_CHUNK = 8192  # synthetic noise is drawn per block of this many GLOBAL series
+
+
+def global_randn(shape_fn, n: int, row0: int, seed: int, device, dim: int = 0) -> torch.Tensor:
+    """Standard normal draws for global series ``row0 .. row0+n-1`` along ``dim``:
+    block ``c`` of :data:`NOISE_CHUNK` global series comes from its own generator
+    (``seed`` + c), so any shard of the series sees the draws the whole set
+    sees.  ``shape_fn(rows)`` gives the block shape for ``rows`` series."""
+    parts = []
+    c0, c1 = row0 // NOISE_CHUNK, (row0 + n - 1) // NOISE_CHUNK if n else row0 // NOISE_CHUNK - 1
+    for c in range(c0, c1 + 1):
+        g = torch.Generator(device=device)
+        g.manual_seed(seed * 1_000_003 + c)
+        blk = torch.randn(shape_fn(NOISE_CHUNK), generator=g, device=device)
+        lo = max(row0, c * NOISE_CHUNK) - c * NOISE_CHUNK
+        hi = min(row0 + n, (c + 1) * NOISE_CHUNK) - c * NOISE_CHUNK
+        parts.append(blk.narrow(dim, lo, hi - lo))
+    if not parts:
+        return torch.empty(shape_fn(0), device=device)
+    return torch.cat(parts, dim) if len(parts) > 1 else parts[0].contiguous()
 
 
 def synthetic_eval(params: Dict[str, torch.Tensor], t0: int, T: int, season: int, noise_seed: Optional[int],
-                   dtype=torch.float32, chunk: int = 8192, noise: float = 0.03) -> torch.Tensor:
+                   dtype=torch.float32, chunk: int = NOISE_CHUNK, noise: float = 0.03, row0: int = 0) -> torch.Tensor:
     """Values of the synthetic model at times ``t0 .. t0+T-1`` → ``[N, T]``;
-    i.i.d. Gaussian noise of ``noise * level`` unless ``noise_seed`` is None."""
+    i.i.d. Gaussian noise of ``noise * level`` unless ``noise_seed`` is None.
+    ``row0``: global index of the first series (noise is a function of the
+    global series index, see :func:`global_randn`)."""
     lvl = params["lvl"]
     N, dev = lvl.shape[0], lvl.device
     out = torch.empty((N, T), dtype=dtype, device=dev)
-    gn = None
-    if noise_seed is not None:
-        gn = torch.Generator(device=dev)
-        gn.manual_seed(noise_seed)
     t = torch.arange(t0, t0 + T, device=dev, dtype=torch.float32)
     for s in range(0, N, chunk):
         e = min(N, s + chunk)
         y = lvl[s:e] + params["tr"][s:e] * t + params["amp"][s:e] * torch.sin(2 * np.pi * t / season + params["ph"][s:e])
-        if gn is not None:
-            y = y + torch.randn((e - s, T), generator=gn, device=dev) * (noise * lvl[s:e])
+        if noise_seed is not None:
+            y = y + global_randn(lambda r: (r, T), e - s, row0 + s, noise_seed, dev) * (noise * lvl[s:e])
         out[s:e] = y.to(dtype)
     return out
 
 
 def synthetic_history(N: int, T: int, season: int, device, seed: int = 0, dtype=torch.float32,
-                      chunk: int = 8192) -> torch.Tensor:
+                      chunk: int = NOISE_CHUNK) -> torch.Tensor:
     """Seasonal synthetic series (level, daily seasonality, slight trend, noise)
     generated on ``device`` in chunks; returns ``[N, T]`` in ``dtype``.
     Continue a series with ``synthetic_eval(synthetic_params(N, dev, seed), T, ...)``."""

@@ -313,3 +313,31 @@ def test_canary_cross_shard_exchange():
             assert row[:4] == exp[:4], (rank, sid, row)  # (col 4 is NaN for some rows by construction)
             covered += 1
     assert covered == 37
+
+
+def _bench_line(n, extra=()):
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", "2", "--warmup", "1", "--cpu",
+           "--series", "400", "--ring", "480", "--season", "48", "--anomaly-frac", "0.05"] + list(extra)
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("extra", [(), ("--gap-frac", "0.2")], ids=["canary", "gaps"])
+def test_bench_n_rank_equals_one_rank(extra):
+    """Every datum of the bench is a function of the GLOBAL series index, so the
+    1, 2, 4 and 8-rank runs (self-launched gloo groups, one all-gather per tick)
+    score the same 400 series and must report the same node health table and the
+    same detection against the same injected regressions."""
+    ref = _bench_line(1, extra)
+    assert ref["detection"]["injected_apps"] > 0 and ref["health"]["series_scored_last_tick"] == 400
+    for n in (2, 4, 8):
+        d = _bench_line(n, extra)
+        assert d["n_gpus"] == n and d["config"]["parallelism"] == f"dp{n}"
+        assert d["health"] == ref["health"], n
+        assert d["detection"] == ref["detection"], n
