@@ -99,7 +99,7 @@ class NodeBrain:
         gone = set(before) - set(self.world.members)
         self.dead |= {worker_id_of(m) for m in gone}
         moved = sum(m.release(lambda d: not self.owns(d)) for m in self.monitors)
-        self.health.reset()
+        self.health.reset(kv=self.world.pstore)
         log.warning("node re-formed: generation %d, members %s (lost %s); released %d moved jobs",
                     self.world.generation, self.world.members, sorted(gone), moved)
 
@@ -154,6 +154,7 @@ class NodeBrain:
     async def run_forever(self, stop: asyncio.Event, period: float) -> None:
         if self.world is not None and not dist.is_initialized():
             self.world.form()
+            self.health.reset(kv=self.world.pstore)
             self.world.start_heartbeat()
         try:
             while not stop.is_set():
@@ -173,7 +174,10 @@ def elastic_world_from_env(device: torch.device) -> Optional[ElasticWorld]:
     or under torchrun (``WORLD_SIZE`` > 1: the agent's store at MASTER_ADDR:PORT);
     None for a single brain process."""
     hb = float(os.environ.get("FOREMAST_HEARTBEAT_S", "5"))
-    coll = float(os.environ.get("FOREMAST_COLLECTIVE_TIMEOUT_S", "60"))
+    backend = os.environ.get("FOREMAST_DIST_BACKEND", "nccl" if device.type == "cuda" else "gloo")
+    # RCCL aborts a wedged communicator at once (ncclCommAbort); gloo's teardown waits for
+    # in-flight work until the group timeout, so a gloo node bounds it near the heartbeat
+    coll = float(os.environ.get("FOREMAST_COLLECTIVE_TIMEOUT_S", "60" if backend == "nccl" else str(2 * hb)))
     if os.environ.get("FOREMAST_NODE_STORE"):
         host, port = os.environ["FOREMAST_NODE_STORE"].rsplit(":", 1)
         n = int(os.environ["FOREMAST_NODE_MEMBERS"])
@@ -184,7 +188,6 @@ def elastic_world_from_env(device: torch.device) -> Optional[ElasticWorld]:
     else:
         return None
     kv = dist.TCPStore(host, int(port), is_master=False, timeout=datetime.timedelta(seconds=60))
-    backend = os.environ.get("FOREMAST_DIST_BACKEND", "nccl" if device.type == "cuda" else "gloo")
     return ElasticWorld(kv, f"m{me}", [f"m{i}" for i in range(n)], backend=backend, heartbeat_timeout_s=hb,
                         collective_timeout_s=coll, device_id=device if backend == "nccl" else None)
 

@@ -16,12 +16,22 @@ all take that branch together and the collective sequence stays matched.
 When a rank needs more rows than the record holds it asks for a larger
 ``cap`` in its header; every rank adopts the maximum on the next tick.
 
+Failure handling: the all-gather is issued ``async_op=True`` and waited for
+on the host with a deadline (:func:`~foremast_amd.parallel.comm.wait_bounded`),
+so a dead or SIGSTOPped peer raises :class:`~foremast_amd.parallel.comm.CollectiveTimeout`
+instead of wedging the rank in a D2H copy until the RCCL watchdog kills it;
+with a key-value store (``kv``: the generation's prefix store of the elastic
+world) the app rosters travel through the store, read with the same deadline,
+instead of an object collective.
+
 At 100k series over 8 ranks (~2.5k apps per rank) the record is ~20 KB, so the
 exchange is latency bound (one collective, tens of microseconds on xGMI).
 """
 
 from __future__ import annotations
 
+import datetime
+import json
 import time
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
@@ -40,19 +50,34 @@ def _world(group=None) -> Tuple[int, int]:
 
 
 class ClusterHealth:
-    def __init__(self, device, cap: int = 256, group=None) -> None:
+    def __init__(self, device, cap: int = 256, group=None, kv=None, timeout_s: Optional[float] = None) -> None:
         self.device = torch.device(device)
         self.cap = max(1, int(cap))
         self.group = group
+        self.kv = kv                       # roster store (None: all_gather_object)
+        self.timeout_s = comm.exchange_timeout_s() if timeout_s is None else float(timeout_s)
         self._versions: Optional[List[int]] = None
         self._rosters: List[Dict[str, Any]] = []
+        self._published: Optional[int] = None
         self.roster_exchanges = 0
         self.last_ms = 0.0
 
-    def reset(self) -> None:
-        """Forget the peers' rosters (after the process group was re-formed)."""
+    def reset(self, kv=None) -> None:
+        """Forget the peers' rosters (after the process group was re-formed);
+        ``kv``: the new generation's roster store."""
         self._versions = None
         self._rosters = []
+        self._published = None
+        if kv is not None:
+            self.kv = kv
+
+    def _read_roster(self, r: int, version: int) -> Dict[str, Any]:
+        key = f"roster/{r}/{version}"
+        try:
+            self.kv.wait([key], datetime.timedelta(seconds=self.timeout_s))
+            return json.loads(self.kv.get(key))
+        except Exception as e:  # noqa: BLE001 - store timeout: the peer is gone
+            raise comm.CollectiveTimeout(f"roster of rank {r} (version {version}) not published: {e}") from e
 
     def exchange(self, names: Sequence[Tuple[str, str]], counts: torch.Tensor, roster_version: int,
                  n_series: int, info: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
@@ -70,20 +95,33 @@ class ClusterHealth:
         send[:HDR].copy_(hdr.to(self.device, non_blocking=True))
         if k:
             send[HDR:HDR + 2 * k].copy_(counts[:k].reshape(-1))
+        mine = dict(info or {}, names=[list(n) for n in names], version=roster_version)
+        if self.kv is not None and comm.active(self.group) and self._published != roster_version:
+            # publish before the gather that announces the version: a peer that sees it can read it
+            self.kv.set(f"roster/{rank}/{roster_version}", json.dumps(mine))
+            if self._published is not None:
+                try:
+                    self.kv.delete_key(f"roster/{rank}/{self._published}")
+                except Exception:  # noqa: BLE001 - best effort cleanup
+                    pass
+            self._published = roster_version
         if comm.active(self.group):
             recv = torch.empty(world * chunk, dtype=torch.int32, device=self.device)
-            dist.all_gather_into_tensor(recv, send, group=self.group)
+            work = dist.all_gather_into_tensor(recv, send, group=self.group, async_op=True)
+            comm.fault_point("exchange")
+            comm.wait_bounded(work, self.timeout_s, "health all-gather")
         else:
             recv = send
         host = recv.cpu().view(world, chunk)
         versions = host[:, 0].tolist()
         if versions != self._versions or len(self._rosters) != world:
-            mine = dict(info or {}, names=[list(n) for n in names], version=roster_version)
-            if comm.active(self.group):
-                rosters: List[Any] = [None] * world
-                dist.all_gather_object(rosters, mine, group=self.group)
+            if not comm.active(self.group):
+                rosters: List[Any] = [mine]
+            elif self.kv is not None:
+                rosters = [mine if r == rank else self._read_roster(r, int(versions[r])) for r in range(world)]
             else:
-                rosters = [mine]
+                rosters = [None] * world
+                dist.all_gather_object(rosters, mine, group=self.group)
             self._rosters, self._versions = rosters, versions
             self.roster_exchanges += 1
         self.cap = max(self.cap, int(host[:, 2].max()))  # every rank adopts the same cap next tick

@@ -11,9 +11,15 @@ the node's scoring down (SURVEY §5.3 "New build"):
   check heartbeat freshness;
 * on a membership change the survivors agree on ONE new member list: the
   first ``compare_set`` on the generation's key wins, everyone adopts it;
-* the process group is destroyed and re-created over the survivors under a
-  generation-prefixed store (the ``ncclCommAbort`` + re-init analogue), and
-  the caller re-shards its series with the new (rank, world).
+* the process group's communicators are ABORTED (``ncclCommAbort`` through
+  ``_abort_process_group``: a wedged RCCL communicator cannot hang the
+  teardown), destroyed and re-created over the survivors under a
+  generation-prefixed store, and the caller re-shards its series with the new
+  (rank, world);
+* under RCCL the watchdog is told to abort communicators without killing the
+  process (``TORCH_NCCL_ASYNC_ERROR_HANDLING=2``, CleanUpOnly) and the per-tick
+  exchange waits on the host with a deadline (``comm.wait_bounded``), so a peer
+  that dies or stops mid-collective surfaces as an exception in the survivors.
 
 Works with ``gloo`` (CPU tests) and ``nccl`` (= RCCL on ROCm).
 """
@@ -22,6 +28,7 @@ from __future__ import annotations
 
 import datetime
 import json
+import os
 import threading
 import time
 from typing import Callable, List, Optional, Sequence
@@ -48,6 +55,7 @@ class ElasticWorld:
         self.coll_timeout = datetime.timedelta(seconds=collective_timeout_s)
         self.device_id = device_id
         self.generation = 0
+        self.pstore = None
         self.rank = -1
         self.world = 0
         self.reforms = 0
@@ -112,9 +120,12 @@ class ElasticWorld:
         self.rank = members.index(self.id)
         self.world = len(members)
         pstore = dist.PrefixStore(f"pg/{self.generation}", self.store)
+        self.pstore = dist.PrefixStore(f"kv/{self.generation}", self.store)  # per-generation records (rosters)
         kw = {}
         if self.device_id is not None:
             kw["device_id"] = self.device_id
+        if self.backend == "nccl":
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")  # abort comms, keep the process
         dist.init_process_group(self.backend, store=pstore, rank=self.rank, world_size=self.world,
                                 timeout=self.coll_timeout, **kw)
 
@@ -125,10 +136,16 @@ class ElasticWorld:
     def reform(self, settle_s: float = 0.0) -> None:
         """Tear the group down and re-form it over the live members."""
         if dist.is_initialized():
-            try:
-                dist.destroy_process_group()
-            except Exception:  # noqa: BLE001 - a broken communicator may fail to close cleanly
+            try:  # abort first: destroying a communicator with a collective in flight can block
+                from torch.distributed.distributed_c10d import _abort_process_group
+                _abort_process_group()
+            except Exception:  # noqa: BLE001 - backends without abort (gloo) fall through to destroy
                 pass
+            if dist.is_initialized():
+                try:
+                    dist.destroy_process_group()
+                except Exception:  # noqa: BLE001 - a broken communicator may fail to close cleanly
+                    pass
         if settle_s:
             time.sleep(settle_s)
         self.beat()

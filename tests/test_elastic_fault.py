@@ -1,0 +1,66 @@
+"""A rank frozen INSIDE the per-tick health exchange (SIGSTOP right after its
+all-gather was issued, ``FOREMAST_FAULT=exchange:3``), then killed: the
+survivors' host-side deadline fires, they agree on the live members, abort and
+re-form the group, and own all of the victim's apps within ~2 x heartbeat."""
+
+import datetime
+import json
+import os
+import signal
+import subprocess
+import sys
+import time
+
+import pytest
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HELPER = os.path.join(ROOT, "tests", "helpers", "elastic_rank.py")
+
+
+@pytest.mark.slow
+def test_rank_stopped_inside_exchange_survivors_reform(tmp_path):
+    hb, n, ticks = 2.0, 3, 25
+    kv = dist.TCPStore("127.0.0.1", 0, is_master=True, wait_for_workers=False,
+                       timeout=datetime.timedelta(seconds=60))
+    port = kv.port
+    procs, outs = [], []
+    for i in range(n):
+        out = tmp_path / f"rank{i}.jsonl"
+        env = dict(os.environ, OMP_NUM_THREADS="1", CUDA_VISIBLE_DEVICES="")
+        if i == 2:
+            env["FOREMAST_FAULT"] = "exchange:3"
+        procs.append(subprocess.Popen([sys.executable, HELPER, str(port), str(i), str(n), str(hb), str(ticks),
+                                       str(out)], env=env, cwd=ROOT))
+        outs.append(out)
+    try:
+        # wait until the victim froze itself inside its 3rd exchange
+        victim = procs[2]
+        t_end = time.time() + 90
+        stopped_at = None
+        while time.time() < t_end:
+            with open(f"/proc/{victim.pid}/stat") as f:
+                if f.read().split(") ", 1)[1].split()[0] == "T":
+                    stopped_at = time.time()
+                    break
+            time.sleep(0.05)
+        assert stopped_at is not None, "victim never reached the fault point"
+        for p in procs[:2]:
+            assert p.wait(timeout=120) == 0
+        victim.send_signal(signal.SIGKILL)
+        for i in range(2):
+            lines = [json.loads(x) for x in outs[i].read_text().splitlines()]
+            assert len(lines) == ticks
+            first3 = [x for x in lines if x["ranks"] == 3]
+            assert first3 and len(first3[0]["apps"]) == 24
+            after = [x for x in lines if x["generation"] >= 1]
+            assert after, lines[-1]
+            reform = after[0]
+            assert reform["ranks"] == 2 and reform["members"] == ["m0", "m1"]
+            assert len(reform["apps"]) == 24                 # the victim's apps are owned by the survivors
+            assert reform["time"] - stopped_at <= 2 * hb + 2.0, reform["time"] - stopped_at
+            assert all(x["ranks"] == 2 and len(x["apps"]) == 24 for x in after)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
