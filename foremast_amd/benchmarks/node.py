@@ -105,7 +105,7 @@ def setup_node(args, world, rank, dev):
     from ..utils.config import BrainConfig, reference_default_env
     from ..utils.timeutil import format_rfc3339
 
-    if dev.type == "cpu" and args.series > 5000:
+    if dev.type == "cpu" and args.series > 20000:
         args.series, args.ring = 500, 2880
     M = len(METRICS)
     n_apps = args.series // M
@@ -253,9 +253,8 @@ def setup_node(args, world, rank, dev):
         if dev.type == "cuda":
             torch.cuda.synchronize()
         scored.append(n_rows)
-        for a, v in table["apps"].items():
-            if v["anomalous"] > 0:
-                flagged.add(int(a.split("/app")[1]))
+        for a in table["anomalous_apps"]:
+            flagged.add(int(a.split("/app")[1]))
         return table
 
     def finish():

@@ -80,6 +80,11 @@ class NodeBrain:
         self.dead: Set[str] = set()
         self.table: Dict = {}
         self.ticks = 0
+        # the full per-app table goes to the store at most every publish_every_s (and at once
+        # when the anomalous set changes): GET /v1/healthcheck/cluster is polled like barrelman's 10 s
+        self.publish_every_s = float(os.environ.get("FOREMAST_PUBLISH_EVERY_S", "10"))
+        self._published = -1e18
+        self._last_anomalous = None
         for m in self.monitors:
             m.owns = self.owns
 
@@ -106,10 +111,12 @@ class NodeBrain:
     def app_table(self):
         """(app roster, ``[A, 2]`` device counters, roster version, live series)
         of every monitor of this rank, merged per app."""
-        if len(self.monitors) == 1:
-            names, counts = self.mon.app_table()
-            return names, counts, self.mon.roster_version, self.mon.n_live
         tables = [m.app_table() for m in self.monitors]
+        used = [i for i, (ns, _) in enumerate(tables) if ns]
+        if len(used) <= 1:  # one engine holds every app of this rank: no merge
+            names, counts = tables[used[0]] if used else tables[0]
+            return (names, counts, sum(m.roster_version for m in self.monitors) + 1_000_000 * (used[0] if used else 0),
+                    sum(m.n_live for m in self.monitors))
         names = sorted({n for ns, _ in tables for n in ns})
         idx = {n: i for i, n in enumerate(names)}
         counts = torch.zeros((len(names), 2), dtype=torch.int32, device=self.device)
@@ -144,9 +151,13 @@ class NodeBrain:
         table["collectives"] = comm.active()
         self.table = table
         self.ticks += 1
-        if self.publish and self.rank == 0:
+        now = time.monotonic()
+        shape = (table["ranks"], table["generation"], table["anomalous_apps"])
+        if self.publish and self.rank == 0 and (now - self._published >= self.publish_every_s
+                                                 or shape != self._last_anomalous):
             try:
-                self.store.put_meta(META_KEY, table)
+                self.store.put_meta(META_KEY, table.full() if hasattr(table, "full") else table)
+                self._published, self._last_anomalous = now, shape
             except Exception as e:  # noqa: BLE001 - the store may be briefly unavailable
                 log.warning("publishing the node health table failed: %s", e)
         return table

@@ -29,6 +29,7 @@ continuously watched app) starts scoring without any history fetch:
 from __future__ import annotations
 
 import asyncio
+import collections
 import logging
 import re
 import time
@@ -102,6 +103,9 @@ class ResidentHistory:
         self.refs: Dict[Key, int] = {}
         self.last_used: Dict[Key, float] = {}
         self.pending: Set[Key] = set()
+        self._idle: "collections.deque[Tuple[float, Key]]" = collections.deque()  # (last use, key) of unreferenced rows
+        self._stage: Dict[Tuple[int, int], List[torch.Tensor]] = {}
+        self._stage_i = 0
         self._tables: Optional[Dict[Tuple[str, str], native.KeyTable]] = None
         self.history_queries = 0
         self.tick_queries = 0
@@ -123,6 +127,7 @@ class ResidentHistory:
                 self.refs[k] = n
             else:
                 self.refs.pop(k, None)
+                self._idle.append((now, k))  # expiry candidate (checked in time order)
             self.last_used[k] = now
 
     def ready(self, key: Key) -> bool:
@@ -146,13 +151,20 @@ class ResidentHistory:
     def _assign(self, now: float) -> List[Tuple[Key, int]]:
         """Free expired rows, give pending keys rows; returns the (key, row)
         pairs whose history must be (re)loaded."""
-        expired = [k for k in self.rows if k not in self.refs and now - self.last_used.get(k, 0.0) > self.retain_s]
+        expired = []
+        while self._idle and now - self._idle[0][0] > self.retain_s:
+            t, k = self._idle.popleft()
+            # still unreferenced and not used again since it went idle
+            if k in self.rows and k not in self.refs and self.last_used.get(k, 0.0) <= t:
+                expired.append(k)
         freed = [self.rows.pop(k) for k in expired]
         for k in expired:
             self.last_used.pop(k, None)
             self.pending.discard(k)
         for row in freed:
             self.keys[row] = None
+        if not self.pending and not expired:
+            return []
         self.pending = {k for k in self.pending if k in self.refs or k in self.rows}
         new = sorted(k for k in self.pending if k not in self.rows)
         need = len(self.rows) + len(new)
@@ -182,7 +194,22 @@ class ResidentHistory:
             self._tables = {fam: native.KeyTable(v) for fam, v in fams.items()}
         return self._tables
 
-    def _staging(self, rows: int, cols: int) -> Tuple[torch.Tensor, np.ndarray]:
+    def _staging(self, rows: int, cols: int, reuse: bool = False) -> Tuple[torch.Tensor, np.ndarray]:
+        """NaN-filled host block (pinned for the GPU).  ``reuse``: one of two
+        per-shape buffers kept across ticks (a tick's H2D has completed before
+        the buffer comes round again: every tick ends with a D2H sync)."""
+        if reuse:
+            bufs = self._stage.get((rows, cols))
+            if bufs is None:
+                bufs = [torch.empty((rows, cols), dtype=torch.float32) for _ in range(2)]
+                if self.device.type == "cuda":
+                    bufs = [b.pin_memory() for b in bufs]
+                self._stage = {(rows, cols): bufs}  # one live shape: the ring's capacity
+            self._stage_i ^= 1
+            t = bufs[self._stage_i]
+            a = t.numpy()
+            a.fill(np.nan)
+            return t, a
         t = torch.full((rows, cols), float("nan"), dtype=torch.float32)
         if self.device.type == "cuda":
             t = t.pin_memory()
@@ -215,7 +242,7 @@ class ResidentHistory:
             self.reloads += 1
             return
         tables = self._key_tables()
-        block_t, block = self._staging(self.ring.n, n_new)
+        block_t, block = self._staging(self.ring.n, n_new, reuse=True)
         reqs, tabs = [], []
         s = self.t_last + self.step
         for fam, table in tables.items():

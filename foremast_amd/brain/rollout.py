@@ -355,6 +355,8 @@ class RolloutMonitor:
         self.fams: Dict[Tuple[str, str], int] = {}     # pod metric family -> index in the decode block
         self._tables = None                            # (slots.version, cap, fam tables)
         self._srcmap_dirty = True
+        self._blocks: Dict[Tuple[int, int], List[torch.Tensor]] = {}
+        self._block_i = 0
         self.timings: Dict[str, float] = {}
         self._bands: Tuple[np.ndarray, np.ndarray, np.ndarray] = (np.zeros(0), np.zeros(0), np.zeros(0))
         self._last_anom: Dict[int, float] = {}
@@ -752,6 +754,20 @@ class RolloutMonitor:
             rows = torch.tensor([row for row, _, _ in grp], dtype=torch.long, device=self.device)
             (self.base if dst == "base" else self.win).index_copy_(0, rows, vals.reshape(len(grp), P * Wc))
 
+    def _tick_block(self, S: int, k: int):
+        """NaN-filled pinned decode block of the tick, one of two kept across ticks."""
+        bufs = self._blocks.get((S, k))
+        if bufs is None:
+            bufs = [torch.empty((S, k), dtype=torch.float32) for _ in range(2)]
+            if self.gpu:
+                bufs = [b.pin_memory() for b in bufs]
+            self._blocks = {(S, k): bufs}
+        self._block_i ^= 1
+        t = bufs[self._block_i]
+        a = t.numpy()
+        a.fill(np.nan)
+        return t, a
+
     async def _ingest(self, t_new: float) -> None:
         if self.t_cur == 0.0:
             self.t_cur = t_new - self.step  # the first tick fetches the current minute
@@ -764,11 +780,7 @@ class RolloutMonitor:
         tables = self._key_tables()
         P = self.P
         S = len(self.fams) * self.slots.cap
-        block_t = torch.empty((S, k), dtype=torch.float32)
-        if self.gpu:
-            block_t = block_t.pin_memory()
-        block = block_t.numpy()
-        block.fill(np.nan)
+        block_t, block = self._tick_block(S, k)
         reqs = [(range_url(fam[0], fam[1], first, k, self.step), first, k, 0) for fam in tables]
         self.tick_queries += len(reqs)
         t0 = time.perf_counter()

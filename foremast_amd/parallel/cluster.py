@@ -126,16 +126,42 @@ class ClusterHealth:
             self.roster_exchanges += 1
         self.cap = max(self.cap, int(host[:, 2].max()))  # every rank adopts the same cap next tick
         self.last_ms = (time.perf_counter() - t0) * 1e3
-        apps: Dict[str, Dict[str, int]] = {}
-        members = []
+        members, anomalous = [], []
         for r in range(world):
             ro = self._rosters[r]
             n = min(int(host[r, 1]), (chunk - HDR) // 2, len(ro["names"]))
-            cnt = host[r, HDR:HDR + 2 * n].view(n, 2).tolist()
-            for (ns, app), (an, sc) in zip(ro["names"][:n], cnt):
-                apps[f"{ns}/{app}"] = {"anomalous": an, "scored": sc, "rank": r}
+            bad = torch.nonzero(host[r, HDR:HDR + 2 * n:2] > 0).flatten().tolist()
+            anomalous += [f"{ro['names'][i][0]}/{ro['names'][i][1]}" for i in bad]
             members.append({k: v for k, v in ro.items() if k not in ("names", "version")}
                            | {"rank": r, "apps": int(host[r, 1]), "series": int(host[r, 3])})
-        return {"ranks": world, "members": members, "apps": apps,
-                "anomalous_apps": sorted(a for a, v in apps.items() if v["anomalous"] > 0),
-                "collective_ms": round(self.last_ms, 3), "updated": time.time()}
+        return NodeTable({"ranks": world, "members": members, "anomalous_apps": sorted(anomalous),
+                          "collective_ms": round(self.last_ms, 3), "updated": time.time()},
+                         host, self._rosters, chunk)
+
+
+class NodeTable(dict):
+    """The node health table of one tick.  ``table["apps"]`` — one entry per app
+    of the node (``{"ns/app": {anomalous, scored, rank}}``) — is built from the
+    gathered counters on first access only: at 20k apps building it costs tens
+    of milliseconds of Python, and the tick itself needs just the anomalous
+    apps (computed vectorised)."""
+
+    def __init__(self, base: Dict[str, Any], host: torch.Tensor, rosters: List[Dict[str, Any]], chunk: int) -> None:
+        super().__init__(base)
+        self._host, self._rosters, self._chunk = host, rosters, chunk
+
+    def __missing__(self, key):
+        if key != "apps":
+            raise KeyError(key)
+        apps: Dict[str, Dict[str, int]] = {}
+        for r, ro in enumerate(self._rosters):
+            n = min(int(self._host[r, 1]), (self._chunk - HDR) // 2, len(ro["names"]))
+            cnt = self._host[r, HDR:HDR + 2 * n].view(n, 2).tolist()
+            for (ns, app), (an, sc) in zip(ro["names"][:n], cnt):
+                apps[f"{ns}/{app}"] = {"anomalous": an, "scored": sc, "rank": r}
+        self["apps"] = apps
+        return apps
+
+    def full(self) -> Dict[str, Any]:
+        """Plain dict with every key (for publishing / JSON)."""
+        return dict(self, apps=self["apps"])

@@ -51,8 +51,10 @@ def wait_bounded(work, timeout_s: float, what: str = "collective") -> None:
         if now > t_end:
             raise CollectiveTimeout(f"{what} did not complete within {timeout_s:.1f} s")
         time.sleep(0 if now < spin_until else 0.0005)
-    if hasattr(work, "is_success") and not work.is_success():
-        raise CollectiveTimeout(f"{what} failed: {work.exception()}")
+    try:
+        work.wait()  # completed: returns at once, or raises the backend's error
+    except Exception as e:  # noqa: BLE001 - the peer's death surfaces as a backend error
+        raise CollectiveTimeout(f"{what} failed: {e}") from e
 
 
 def exchange_timeout_s() -> float:
