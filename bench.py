@@ -881,6 +881,7 @@ def main():
             res["decode_ms_last_tick"] = round(decoder.last_decode_ms, 3)
         if timed_rows is not None:
             res["node"] = {"series_scored_timed": int(timed_rows), "tick_breakdown_ms_last": tick_breakdown,
+                           "tick_ms": [round(float(x), 2) for x in lat_ms.tolist()],
                            "completion_tick_s": round(fin_s, 3), "job_statuses_rank0": statuses}
         if args.config == "canary" and args.refit_every > 1:
             flags = np.array([REFIT_FLAGS.get(args.warmup + k, True) for k in range(args.steps)])

@@ -112,18 +112,20 @@ class NodeBrain:
         """(app roster, ``[A, 2]`` device counters, roster version, live series)
         of every monitor of this rank, merged per app."""
         tables = [m.app_table() for m in self.monitors]
-        used = [i for i, (ns, _) in enumerate(tables) if ns]
+        used = [i for i, (ns, _) in enumerate(tables) if any(ns)]
         if len(used) <= 1:  # one engine holds every app of this rank: no merge
             names, counts = tables[used[0]] if used else tables[0]
             return (names, counts, sum(m.roster_version for m in self.monitors) + 1_000_000 * (used[0] if used else 0),
                     sum(m.n_live for m in self.monitors))
-        names = sorted({n for ns, _ in tables for n in ns})
+        names = sorted({n for ns, _ in tables for n in ns if n})
         idx = {n: i for i, n in enumerate(names)}
         counts = torch.zeros((len(names), 2), dtype=torch.int32, device=self.device)
         for ns, c in tables:
-            if ns:
-                at = torch.tensor([idx[n] for n in ns], dtype=torch.long, device=self.device)
-                counts.index_add_(0, at, c[:len(ns)].to(self.device))
+            keep = [i for i, n in enumerate(ns) if n]
+            if keep:
+                at = torch.tensor([idx[ns[i]] for i in keep], dtype=torch.long, device=self.device)
+                sel = torch.tensor(keep, dtype=torch.long, device=self.device)
+                counts.index_add_(0, at, c.index_select(0, sel).to(self.device))
         return (names, counts, sum(m.roster_version for m in self.monitors),
                 sum(m.n_live for m in self.monitors))
 

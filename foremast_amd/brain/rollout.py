@@ -360,8 +360,12 @@ class RolloutMonitor:
         self.timings: Dict[str, float] = {}
         self._bands: Tuple[np.ndarray, np.ndarray, np.ndarray] = (np.zeros(0), np.zeros(0), np.zeros(0))
         self._last_anom: Dict[int, float] = {}
-        self._ids_dirty = False
         self._apps_dirty = False
+        self._app_refs: Dict[Tuple[str, str], int] = {}
+        self._app_names: List[Optional[Tuple[str, str]]] = []   # app index -> name (None: free index)
+        self._app_free: List[int] = []
+        self._app_new: List[Tuple[Tuple[str, str], List[int]]] = []
+        self._app_gone: List[Tuple[str, str]] = []
         self._n_live = 0
         self._build_grid()
         self.anomalies = None
@@ -389,6 +393,7 @@ class RolloutMonitor:
         f32 = dict(dtype=torch.float32, device=dev)
         old = getattr(self, "win", None)
         n = self.cap
+        old_app_id = getattr(self, "app_id", None)
         new = {
             "win": torch.full((cap, C), float("nan"), **f32),
             "base": torch.full((cap, C), float("nan"), **f32),
@@ -412,7 +417,9 @@ class RolloutMonitor:
         self.state = st
         self.out: Dict[str, torch.Tensor] = {}
         self.pw_out: Dict[str, torch.Tensor] = {}
-        self.app_stats = torch.zeros((max(1, len(self.apps)), 2), dtype=torch.int32, device=dev)
+        self.app_stats = torch.zeros((max(1, len(self._app_names)), 2), dtype=torch.int32, device=dev)
+        if n:  # rows keep their app index across growth
+            self.app_id[:n].copy_(old_app_id)
         self.row_plan.extend([None] * (cap - len(self.row_plan)))
         self.model_ok = np.concatenate([getattr(self, "model_ok", np.zeros(0, bool)), np.zeros(cap - n, bool)])
         self.row_fam = np.concatenate([getattr(self, "row_fam", np.zeros(0, np.int64)), np.full(cap - n, -1)])
@@ -491,33 +498,54 @@ class RolloutMonitor:
             return
         self.history.unwant([s.hkey for s in p.series], now)
         self._free_rows(p.rows)
-        self._apps_dirty = True
         if p.rows:
+            self._app_ref(p, -1)
             self.slots.release(self._job_pods(p))
         p.rows = []
 
     def _refresh_apps(self) -> None:
-        """App roster of the admitted jobs (index = row of the per-app counters).
-        Called only before scoring, so the roster :meth:`app_table` reports is
-        the one the last tick's counters were accumulated under."""
-        if not (self._apps_dirty or self._ids_dirty):
+        """Apply the app-roster changes of the last admissions / verdicts.  App
+        indices are stable (a freed index is reused by a later app), so a job
+        finishing never renumbers the other rows; called only before scoring,
+        so the roster :meth:`app_table` reports is the one the last tick's
+        counters were accumulated under."""
+        if not self._apps_dirty:
             return
-        names = sorted({p.app for p in self.jobs.values()})
-        changed = list(self.apps) != names
-        if changed:
-            self.apps = {a: i for i, a in enumerate(names)}
-            self.roster_version += 1
-            if self.cap and self.app_stats.shape[0] < max(1, len(names)):
-                cap = self.app_stats.shape[0]
-                while cap < len(names):
-                    cap *= 2
-                self.app_stats = torch.zeros((cap, 2), dtype=torch.int32, device=self.device)
-        if self.cap and (changed or self._ids_dirty):
-            ids = np.zeros(self.cap, dtype=np.int32)
-            for p in self.jobs.values():
-                ids[p.rows] = self.apps[p.app]
-            self.app_id.copy_(torch.from_numpy(ids))
-        self._ids_dirty = self._apps_dirty = False
+        for a in self._app_gone:
+            if self._app_refs.get(a, 0) <= 0 and a in self.apps:
+                i = self.apps.pop(a)
+                self._app_names[i] = None
+                self._app_free.append(i)
+        self._app_gone = []
+        for a, rows in self._app_new:
+            i = self.apps.get(a)
+            if i is None:
+                i = self._app_free.pop() if self._app_free else len(self._app_names)
+                if i == len(self._app_names):
+                    self._app_names.append(a)
+                else:
+                    self._app_names[i] = a
+                self.apps[a] = i
+            if rows:
+                self.app_id[torch.tensor(rows, dtype=torch.long, device=self.device)] = i
+        self._app_new = []
+        if self.cap and self.app_stats.shape[0] < max(1, len(self._app_names)):
+            cap = self.app_stats.shape[0]
+            while cap < len(self._app_names):
+                cap *= 2
+            self.app_stats = torch.zeros((cap, 2), dtype=torch.int32, device=self.device)
+        self.roster_version += 1
+        self._apps_dirty = False
+
+    def _app_ref(self, p: RolloutPlan, delta: int) -> None:
+        n = self._app_refs.get(p.app, 0) + delta
+        self._app_refs[p.app] = n
+        if delta > 0:
+            self._app_new.append((p.app, list(p.rows)))
+        elif n <= 0:
+            self._app_refs.pop(p.app, None)
+            self._app_gone.append(p.app)
+        self._apps_dirty = True
 
     # ------------------------------------------------------------------ admission
     async def _admit(self, now: float) -> int:
@@ -543,7 +571,8 @@ class RolloutMonitor:
         self._fit(items)
         await self._load_windows(items)
         self.admitted += len(ready)
-        self._ids_dirty = True
+        for p in ready:
+            self._app_ref(p, +1)
         self.timings["admit_ms"] = (time.perf_counter() - t0) * 1e3
         return len(ready)
 
@@ -983,14 +1012,16 @@ class RolloutMonitor:
                 self.history.unwant([s.hkey for s in p.series], now)
                 self._free_rows(p.rows)
                 self.slots.release(self._job_pods(p))
-                self._apps_dirty = True
+                self._app_ref(p, -1)
                 for row in p.rows:
                     self._last_anom.pop(row, None)
         return written
 
     # ------------------------------------------------------------------ node integration
-    def app_table(self) -> Tuple[List[Tuple[str, str]], torch.Tensor]:
-        names = list(self.apps)
+    def app_table(self) -> Tuple[List[Optional[Tuple[str, str]]], torch.Tensor]:
+        """(app index -> name, None for a free index; ``[A, 2]`` device counters
+        of the last tick: anomalous series, scored series)."""
+        names = list(self._app_names)
         if not self.cap:
             return names, torch.zeros((len(names), 2), dtype=torch.int32, device=self.device)
         return names, self.app_stats[:len(names)]

@@ -95,7 +95,7 @@ class ClusterHealth:
         send[:HDR].copy_(hdr.to(self.device, non_blocking=True))
         if k:
             send[HDR:HDR + 2 * k].copy_(counts[:k].reshape(-1))
-        mine = dict(info or {}, names=[list(n) for n in names], version=roster_version)
+        mine = dict(info or {}, names=[list(n) if n else None for n in names], version=roster_version)
         if self.kv is not None and comm.active(self.group) and self._published != roster_version:
             # publish before the gather that announces the version: a peer that sees it can read it
             self.kv.set(f"roster/{rank}/{roster_version}", json.dumps(mine))
@@ -131,7 +131,7 @@ class ClusterHealth:
             ro = self._rosters[r]
             n = min(int(host[r, 1]), (chunk - HDR) // 2, len(ro["names"]))
             bad = torch.nonzero(host[r, HDR:HDR + 2 * n:2] > 0).flatten().tolist()
-            anomalous += [f"{ro['names'][i][0]}/{ro['names'][i][1]}" for i in bad]
+            anomalous += [f"{ro['names'][i][0]}/{ro['names'][i][1]}" for i in bad if ro["names"][i]]
             members.append({k: v for k, v in ro.items() if k not in ("names", "version")}
                            | {"rank": r, "apps": int(host[r, 1]), "series": int(host[r, 3])})
         return NodeTable({"ranks": world, "members": members, "anomalous_apps": sorted(anomalous),
@@ -157,8 +157,9 @@ class NodeTable(dict):
         for r, ro in enumerate(self._rosters):
             n = min(int(self._host[r, 1]), (self._chunk - HDR) // 2, len(ro["names"]))
             cnt = self._host[r, HDR:HDR + 2 * n].view(n, 2).tolist()
-            for (ns, app), (an, sc) in zip(ro["names"][:n], cnt):
-                apps[f"{ns}/{app}"] = {"anomalous": an, "scored": sc, "rank": r}
+            for name, (an, sc) in zip(ro["names"][:n], cnt):
+                if name:  # None: a free index of the rank's stable app table
+                    apps[f"{name[0]}/{name[1]}"] = {"anomalous": an, "scored": sc, "rank": r}
         self["apps"] = apps
         return apps
 
