@@ -52,6 +52,7 @@ from ..utils.config import BrainConfig
 from ..utils.metrics import BrainMetrics
 from ..utils.timeutil import TimeFormatError, parse_rfc3339
 from .engine import ShardSpec, StreamingShard
+from .resident import fetch_decode
 
 log = logging.getLogger("foremast.streaming")
 
@@ -239,7 +240,7 @@ class StreamingMonitor:
         for row in freed:
             self.keys[row] = None
         self.pending &= live
-        new = sorted(self.pending)
+        new = sorted(k for k in self.pending if k not in self.rows)
         need = len(self.rows) + len(new)
         if self.shard is None or need > self.shard.spec.n_series:
             cap = max(self.min_capacity, self.shard.spec.n_series if self.shard is not None else 1)
@@ -307,39 +308,26 @@ class StreamingMonitor:
 
     # ------------------------------------------------------------------ data
     async def _fetch_into(self, reqs: List[Tuple[str, float, int, int]], out: np.ndarray,
-                          tables: Dict[Tuple[str, str], native.KeyTable], fams: List[Tuple[str, str]]) -> None:
+                          tables: Dict[Tuple[str, str], native.KeyTable], fams: List[Tuple[str, str]]) -> List[bool]:
         """``reqs``: (url, start, n_points, col0) per query, ``fams`` the family of
-        each; every response is decoded by the keyed native scatter into ``out``."""
-        bodies = await self.prom.fetch_raw_many([u for u, *_ in reqs])
-        good = []
-        for (url, start, n, col0), fam, body in zip(reqs, fams, bodies):
-            if isinstance(body, Exception):
-                log.warning("fetch %s failed: %s", url.split("?")[0], body)
-                continue
-            good.append((body, tables[fam], start, n, col0, fam))
-        if not good:
-            return
-        # every response in ONE native call on a thread pool (GIL released), off the event loop
-        b, t, st, ns, c0, fm = zip(*good)
-        stats = await asyncio.get_running_loop().run_in_executor(
-            None, lambda: native.decode_bodies(list(b), list(t), list(st), self.step, list(ns), list(c0), out,
-                                               threads=self.decode_threads))
-        for (series, _dropped, _unmatched), fam in zip(stats, fm):
-            if series < 0:
-                log.warning("bad response for %s (code %d)", fam[1], series)
+        each; every response is decoded by the keyed native scatter into ``out``.
+        Returns per request whether it was fetched and decoded."""
+        return await fetch_decode(self.prom, reqs, [tables[f] for f in fams], out, self.step, self.decode_threads)
 
-    async def _load_history(self, assigned: List[Tuple[Key, int]]) -> None:
+    async def _load_history(self, assigned: List[Tuple[Key, int]]) -> Set[Key]:
         """Fetch R + W points ending at ``t_last`` for the given series only, in
-        (time chunk x app group) queries, into a pinned block; one H2D."""
+        (time chunk x app group) queries, into a pinned block; one H2D.  Returns
+        the keys whose load had a failed query (they stay pending: retried next
+        tick instead of keeping a NaN week)."""
         if not assigned:
-            return
+            return set()
         n_pts = self.R + self.W
         first = self.t_last - (n_pts - 1) * self.step
         by_fam: Dict[Tuple[str, str], List[Tuple[Key, int]]] = {}
         for i, (key, _row) in enumerate(assigned):
             by_fam.setdefault((key[0], key[1]), []).append((key, i))
         block_t, block = self._staging(len(assigned), n_pts)
-        reqs, fams, tables = [], [], {}
+        reqs, fams, tables, groups = [], [], {}, []
         for fam, items in by_fam.items():
             tables[fam] = native.KeyTable([((k[2], k[3]), i) for k, i in items])
             for g in range(0, len(items), self.apps_per_query):
@@ -353,19 +341,24 @@ class StreamingMonitor:
                            f"&end={int(s + (n - 1) * self.step)}&step={int(self.step)}")
                     reqs.append((url, s, n, c0))
                     fams.append(fam)
+                    groups.append([k for k, _ in grp])
         self.history_queries += len(reqs)
-        await self._fetch_into(reqs, block, tables, fams)
+        ok = await self._fetch_into(reqs, block, tables, fams)
         self.shard.load_rows(torch.tensor([row for _, row in assigned], dtype=torch.long),
                              block_t.to(self.device, non_blocking=True))
         self._set_thresholds(assigned)
+        return {k for good, keys in zip(ok, groups) if not good for k in keys}
 
     async def _apply_changes(self) -> None:
         assigned = self._assign_rows()
         if self.shard is not None and self.t_last == 0.0:
             self.t_last = float(np.floor(self.clock() / self.step) * self.step)
+        # rows whose history load failed earlier are still pending: load them again
+        assigned = assigned + [(k, self.rows[k]) for k in sorted(self.pending)
+                               if k in self.rows and k not in {a for a, _ in assigned}]
         if assigned:
-            await self._load_history(assigned)
-            self.pending -= {k for k, _ in assigned}
+            failed = await self._load_history(assigned)
+            self.pending -= {k for k, _ in assigned if k not in failed}
 
     async def _ingest_new(self, now: float) -> None:
         t_new = float(np.floor(now / self.step) * self.step)
@@ -375,18 +368,26 @@ class StreamingMonitor:
         if n_new > self.R:  # down for more than the whole history: reload every row
             self.t_last = t_new
             assigned = sorted(self.rows.items(), key=lambda kv: kv[1])
-            await self._load_history(assigned)
+            failed = await self._load_history(assigned)
+            self.pending |= failed
             return
         tables = self._key_tables()
         block_t, block = self._staging(self.shard.spec.n_series, n_new)
         s = self.t_last + self.step
         reqs, fams = [], []
         for fam in tables:
-            url = (f"{fam[0]}query_range?query={quote(fam[1], safe='')}&start={int(s)}"
-                   f"&end={int(s + (n_new - 1) * self.step)}&step={int(self.step)}")
-            reqs.append((url, s, n_new, 0))
-            fams.append(fam)
-        await self._fetch_into(reqs, block, tables, fams)
+            for c0 in range(0, n_new, self.chunk_pts):  # catch-up after an outage: time chunks
+                n = min(self.chunk_pts, n_new - c0)
+                st = s + c0 * self.step
+                url = (f"{fam[0]}query_range?query={quote(fam[1], safe='')}&start={int(st)}"
+                       f"&end={int(st + (n - 1) * self.step)}&step={int(self.step)}")
+                reqs.append((url, st, n, c0))
+                fams.append(fam)
+        ok = await self._fetch_into(reqs, block, tables, fams)
+        if not all(ok):
+            log.warning("%d of %d tick queries failed: the ring stays at %d, the next tick refetches",
+                        ok.count(False), len(ok), int(self.t_last))
+            return
         dev_block = block_t.to(self.device, non_blocking=True)
         for k in range(n_new):
             self.shard.ingest_tick(dev_block[:, k:k + 1].contiguous())

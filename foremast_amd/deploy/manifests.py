@@ -118,7 +118,12 @@ def service() -> List[Dict[str, Any]]:
 def brain(gpus: int = 8) -> List[Dict[str, Any]]:
     env = [{"name": k, "value": v} for k, v in reference_default_env().items()]
     env += [{"name": "ES_ENDPOINT", "value": ES_URL}, {"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"},
-            {"name": "FOREMAST_DTYPE", "value": "bf16"}]
+            {"name": "FOREMAST_DTYPE", "value": "bf16"},
+            # resident engines: continuous (streaming) + canary / rollingUpdate (rollout) jobs on the GPUs
+            {"name": "FOREMAST_STREAMING", "value": "1"}, {"name": "FOREMAST_ROLLOUT", "value": "1"},
+            # "reference": the reference brain's per-point thresholds (no window correction, one point
+            # outside the lowered band fires, one-step sigma); "engine" (default): docs/SCORING.md
+            {"name": "FOREMAST_DETECTION_PRESET", "value": "engine"}]
     c = {"name": "foremast-brain", "image": IMAGE,
          "command": ["python", "-m", "torch.distributed.run", "--standalone", f"--nproc-per-node={gpus}",
                      "-m", "foremast_amd.brain"],
@@ -146,4 +151,6 @@ def bundle() -> Dict[str, List[Dict[str, Any]]]:
         "3_brain/elasticsearch.yaml": elasticsearch(),
         "3_brain/foremast-service.yaml": service(),
         "3_brain/foremast-brain.yaml": brain(),
+        # opt-in, Kubernetes >= 1.31: field selectors on status.jobId / status.phase
+        "../optional/crds-selectable.yaml": schema.crds(selectable=True),
     }

@@ -91,7 +91,12 @@ def crd_manifest(kind: str, plural: str, spec_cls, status_cls, short_names=(), p
     }
 
 
-def crds():
+def crds(selectable: bool = False):
+    """The two CRDs.  ``selectable``: declare the reference's field labels
+    (``status.jobId``, ``status.phase``) as ``selectableFields`` — needs
+    Kubernetes >= 1.31 (1.30 behind the CustomResourceFieldSelectors gate);
+    older API servers reject the unknown field under strict validation, so the
+    default bundle leaves it out (``deploy/optional/crds-selectable.yaml`` has it)."""
     return [
         crd_manifest("DeploymentMetadata", "deploymentmetadatas", crd.DeploymentMetadataSpec,
                      crd.DeploymentMetadataStatus, short_names=("dmd",)),
@@ -103,7 +108,7 @@ def crds():
                          {"name": "Remediated", "type": "boolean", "jsonPath": ".status.remediationTaken"},
                      ],
                      # the reference's field labels (v1alpha1/register.go:38-53)
-                     selectable=(".status.jobId", ".status.phase")),
+                     selectable=(".status.jobId", ".status.phase") if selectable else ()),
     ]
 
 

@@ -644,7 +644,10 @@ __device__ __forceinline__ void hw_half_block(const SmoothArgs& a, int hmax, int
   bool allfast = true;  // no NaN in the fitted seasons of either series
   for (int sg = 1; sg < nseg; ++sg) allfast = allfast && !seg_nan(sg);
   if (!GENERAL && !allfast) {
-    if (tid == 0) deferred[1 + atomicAdd(deferred, 1)] = n0;
+    if (tid == 0) {
+      const int q = atomicAdd(deferred, 1);
+      if (q < (a.N + 1) / 2) deferred[1 + q] = n0;  // a stale count can never write past the pair list
+    }
     return;
   }
   float bestSSE = __builtin_huge_valf();
@@ -813,7 +816,7 @@ __global__ __launch_bounds__(256, 2) void hw_half_kernel(const SmoothArgs a, int
 // allocates the workspace zeroed).
 template <int K>
 __global__ __launch_bounds__(256, 2) void hw_half_general_kernel(const SmoothArgs a, int hmax, int* deferred) {
-  const int cnt = deferred[0];
+  const int cnt = min(deferred[0], (a.N + 1) / 2);
   // nothing deferred (gap-free shard, the common case): count and done are already 0, so
   // no workgroup needs to count itself — skip the 512 same-address atomics
   if (cnt == 0) return;
@@ -1133,7 +1136,10 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
   }
   __syncthreads();
   if (*flag) {  // block-uniform: a gap past season 0 — the general kernel takes the pair
-    if (tid == 0 && hid == 0) deferred[1 + atomicAdd(deferred, 1)] = n0;
+    if (tid == 0 && hid == 0) {
+      const int q = atomicAdd(deferred, 1);
+      if (q < (a.N + 1) / 2) deferred[1 + q] = n0;  // a stale count can never write past the pair list
+    }
     return;
   }
   float l0r[2], b0r[2];

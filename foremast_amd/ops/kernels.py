@@ -377,8 +377,11 @@ _HALF_WS: Dict[tuple, torch.Tensor] = {}
 def _half_workspace(dev, N: int) -> torch.Tensor:
     """Deferred-pair list of variants 4/5 (count, pair starts, done counter),
     reused across calls so a captured tick allocates nothing; allocated zeroed and
-    left zeroed by the general kernel (no per-call memset)."""
-    key = (dev.index, N)
+    left zeroed by the general kernel (no per-call memset).  One workspace per
+    (device, N, stream): fits on two streams never share a count; the kernels
+    bound every append by the pair list and the caller zeroes the workspace when a
+    launch on this path fails (``_hw_half_fit``)."""
+    key = (dev.index, N, nat.stream_handle(dev))
     ws = _HALF_WS.get(key)
     if ws is None:
         ws = torch.zeros(2 + (N + 1) // 2, dtype=torch.int32, device=dev)  # {count, pairs..., done}
@@ -462,11 +465,17 @@ def _hw_half_fit(lib, hist, head, length, m, grid, det, Tp, pad, hmax, out, resi
         sws, slots = _split_workspace(dev)
         if os.environ.get("FOREMAST_HW_SPLIT", "1") == "0":
             slots = 0  # whole pairs only
-        nat.check(lib.fm_hw_d_fit_split(a, int(hmax), nat.ptr(ws), nat.ptr(sws), SPLIT_MAX, slots,
-                                        nat.stream_handle(dev)), "fm_hw_d_fit_split")
+        rc = lib.fm_hw_d_fit_split(a, int(hmax), nat.ptr(ws), nat.ptr(sws), SPLIT_MAX, slots,
+                                   nat.stream_handle(dev))
+        if rc != 0:
+            ws.zero_()  # the general kernel did not run: its self-cleaning reset did not happen
+        nat.check(rc, "fm_hw_d_fit_split")
         last_hw_variant = 5
         return out
-    nat.check(lib.fm_hw_half_fit(a, int(hmax), nat.ptr(ws), nat.stream_handle(dev)), "fm_hw_half_fit")
+    rc = lib.fm_hw_half_fit(a, int(hmax), nat.ptr(ws), nat.stream_handle(dev))
+    if rc != 0:
+        ws.zero_()
+    nat.check(rc, "fm_hw_half_fit")
     last_hw_variant = 4
     return out
 

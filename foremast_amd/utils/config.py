@@ -148,6 +148,14 @@ class BrainConfig:
         c.pairwise_min_points = int(f("ML_PAIRWISE_MIN_ANOMALIES", c.pairwise_min_points, int))
         c.window_correction = (e.get("FOREMAST_WINDOW_CORRECTION") or c.window_correction).strip().lower()
         c.horizon_variance = e.get("FOREMAST_HORIZON_VARIANCE", "1").strip().lower() not in ("0", "false", "no")
+        # FOREMAST_DETECTION_PRESET=reference: the reference brain's documented per-point
+        # semantics (foremast-brain/README.md:22-38): threshold applied to each point as is (no
+        # window correction), a single point outside the lowered band fires, one-step sigma at
+        # every horizon.  Explicit variables still override the preset.
+        if (e.get("FOREMAST_DETECTION_PRESET") or "").strip().lower() == "reference":
+            c.window_correction = (e.get("FOREMAST_WINDOW_CORRECTION") or "none").strip().lower()
+            c.pairwise_min_points = int(f("ML_PAIRWISE_MIN_ANOMALIES", 1, int))
+            c.horizon_variance = e.get("FOREMAST_HORIZON_VARIANCE", "0").strip().lower() not in ("0", "false", "no")
         c.lstm_hidden = int(f("FOREMAST_LSTM_HIDDEN", c.lstm_hidden, int))
         c.lstm_window = int(f("FOREMAST_LSTM_WINDOW", c.lstm_window, int))
         c.metrics_port = int(f("FOREMAST_METRICS_PORT", c.metrics_port, int))

@@ -283,3 +283,43 @@ def test_streaming_rows_grow_incrementally_with_chunked_history():
         assert float(inc.shard.hist.logical()[row].nanmean()) < 5.0
 
     asyncio.run(go())
+
+
+def test_streaming_failed_fetches_are_retried_not_nan_filled():
+    """a failed history load keeps its series pending (reloaded next
+    tick); a failed tick query leaves the ring where it was (the next tick
+    refetches those minutes) instead of ingesting NaN."""
+    clock = Clock(T0)
+    prom = FakePrometheus(clock=clock)
+    prom.add(M, {"namespace": "ns", "app": "a"}, synth.error_rate(base=0.3, spread=0.05, seed=1))
+    store = MemoryJobStore()
+    svc.register(store, _job("a"))
+    env = reference_default_env()
+    env.update(MIN_HISTORICAL_DATA_POINT_TO_MEASURE="10", ML_ALGORITHM="moving_average_all")
+    mon = StreamingMonitor(store, BrainConfig.from_env(env),
+                           prom=PromClient(transport=httpx.ASGITransport(app=prom.asgi_app())),
+                           device=torch.device("cpu"), ring_len=480, window=5, clock=clock)
+
+    async def go():
+        mon.sync()
+        prom.faults.error_rate = 1.0
+        await mon.tick()
+        assert mon.pending, "a failed history load must stay pending"
+        prom.faults.error_rate = 0.0
+        clock.t = T0 + 60
+        await mon.tick()
+        assert not mon.pending
+        hist = mon.shard.hist.logical()[0]
+        assert torch.isnan(hist).float().mean() < 0.05          # the week arrived on the retry
+        t_before = mon.t_last
+        prom.faults.error_rate = 1.0
+        clock.t = T0 + 180
+        await mon.tick()
+        assert mon.t_last == t_before                            # ring not advanced over the outage
+        prom.faults.error_rate = 0.0
+        clock.t = T0 + 240
+        await mon.tick()
+        assert mon.t_last == (T0 + 240) // 60 * 60
+        newest = mon.shard.hist.logical()[0][-8:]                # graduated window points, no NaN hole
+        assert not torch.isnan(newest).any(), newest
+    asyncio.run(go())
