@@ -50,6 +50,10 @@ def parse(argv=None):
                    help="streaming tick period (default: the query step)")
     p.add_argument("--rollout", type=int, default=int(os.environ.get("FOREMAST_ROLLOUT", "1")),
                    help="with --streaming: serve canary / rollingUpdate jobs from the resident rollout engine")
+    p.add_argument("--lstm", type=int, default=(int(os.environ["FOREMAST_LSTM"]) if os.environ.get("FOREMAST_LSTM")
+                                                 else None),
+                   help="with --streaming: serve continuous multi-metric jobs from the resident DP LSTM engine "
+                        "(default: when ML_ALGORITHM is lstm or auto)")
     p.add_argument("--pods", type=int, default=int(os.environ.get("FOREMAST_CANARY_PODS", "5")),
                    help="rollout engine: pods per side kept per (job, metric) window")
     p.add_argument("--step", type=float, default=float(os.environ.get("FOREMAST_STEP_SECONDS", "60")))
@@ -114,12 +118,20 @@ async def run(args) -> BrainWorker:
             rollout = RolloutMonitor(store, cfg, device=dev, metrics=metrics, step=args.step, window=args.window,
                                      pods=args.pods, worker_id=(worker_id_of(member) if world else member) + "-rollout",
                                      ring_len=cfg.ring_len)
-        if world is None and args.snapshot and rollout is None:
+        lstm = None
+        if args.lstm is None:
+            args.lstm = cfg.algorithm in ("lstm", "auto")
+        if args.lstm:
+            from .lstm_monitor import LstmMonitor
+            lstm = LstmMonitor(store, cfg, device=dev, metrics=metrics, step=args.step, ring_len=cfg.ring_len,
+                               worker_id=(worker_id_of(member) if world else member) + "-lstm")
+            mon.exclude = lstm.is_mine
+        if world is None and args.snapshot and rollout is None and lstm is None:
             snap = args.snapshot.replace("{rank}", str(local))
             tasks.append(mon.run_forever(stop, period=period, snapshot=snap, snapshot_every=args.snapshot_every))
         else:
             # node brain (also for one rank: it publishes the health table)
-            tasks.append(NodeBrain(mon, world, store, dev, extra=(rollout,)).run_forever(stop, period))
+            tasks.append(NodeBrain(mon, world, store, dev, extra=(rollout, lstm)).run_forever(stop, period))
     await asyncio.gather(*tasks)
     if cache_path and worker.lstm is not None:
         worker.lstm.cache.save(cache_path)

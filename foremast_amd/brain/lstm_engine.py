@@ -54,7 +54,7 @@ class LstmShard:
                  fp8: bool = False, device="cuda", app_id: Optional[torch.Tensor] = None, n_apps: int = 1,
                  threshold: float = 4.0, train_batch: int = 4096, lr: float = 1e-3, restat_every: int = 16,
                  seed: int = 0, dtype=torch.bfloat16, fused_train: bool = True, cal_windows: int = 16,
-                 cal_ewma: float = 1.0 / 32) -> None:
+                 cal_ewma: float = 1.0 / 32, dp_overlap: bool = True) -> None:
         self.n, self.R, self.F, self.T = n_series, ring_len, n_features, window
         self.device = torch.device(device)
         self.gpu = self.device.type == "cuda"
@@ -68,7 +68,11 @@ class LstmShard:
             self.fg = FusedLstmGrad(train_batch, window, n_features, self.device)
             grad_fn = self.fg.grads
         self.fused_train = grad_fn is not None
-        self.trainer = DPTrainer(self.model, lr=lr, grad_fn=grad_fn)
+        self.trainer = DPTrainer(self.model, lr=lr, grad_fn=grad_fn, overlap=dp_overlap)
+        self.dtype = dtype
+        # rows training samples are drawn from (None: every row); the resident monitor
+        # (brain/lstm_monitor.py) keeps free rows out of training
+        self.live: Optional[torch.Tensor] = None
         self.fp8 = fp8
         self.train_batch = train_batch
         self.threshold = threshold
@@ -94,6 +98,52 @@ class LstmShard:
         self._ws: Dict[str, torch.Tensor] = {}
         self._all = torch.arange(n_series, device=self.device)
         self._zero_off = torch.zeros(n_series, dtype=torch.long, device=self.device)
+
+    # ------------------------------------------------------------------ rows (resident monitor)
+    def grow(self, capacity: int) -> None:
+        """Re-allocate for ``capacity`` rows, keeping every row's ring, statistics
+        and calibration (the model and optimizer are untouched)."""
+        n, dev = self.n, self.device
+        if capacity <= n:
+            return
+        for f, ring in enumerate(self.rings):
+            new = HistoryRing(capacity, self.R, self.dtype, dev)
+            new._store[:n].copy_(ring._store)
+            new.state.head, new.state.length = ring.head, ring.length
+            self.rings[f] = new
+
+        def ext(t, fill):
+            out = torch.full((capacity,) + tuple(t.shape[1:]), fill, dtype=t.dtype, device=dev)
+            out[:n].copy_(t)
+            return out
+        self.mean, self.std, self.rstd = ext(self.mean, 0.0), ext(self.std, 1.0), ext(self.rstd, 1.0)
+        self.app_id = ext(self.app_id, 0)
+        if self.cal is not None:
+            self.cal = ext(self.cal, 1.0).contiguous()
+        self.n = capacity
+        self._all = torch.arange(capacity, device=dev)
+        self._zero_off = torch.zeros(capacity, dtype=torch.long, device=dev)
+        self.out = {}
+
+    def write_rows(self, rows: torch.Tensor, values) -> None:
+        """History of some rows: ``values`` F tensors ``[k, length]`` in time order,
+        ending at the rings' newest sample (the ring rotation is resolved with
+        two column-slice copies)."""
+        rows = rows.to(self.device, torch.long)
+        for f, ring in enumerate(self.rings):
+            v = values[f].to(self.device, ring.data.dtype)
+            L, R, head = ring.length, ring.R, ring.head
+            v = v[:, -L:]
+            n1 = min(L, R - head)
+            ring.data[:, head:head + n1].index_copy_(0, rows, v[:, :n1])
+            if L > n1:
+                ring.data[:, :L - n1].index_copy_(0, rows, v[:, n1:])
+
+    def _draw_rows(self, B: int, dtype) -> torch.Tensor:
+        if self.live is None:
+            return torch.randint(0, self.n, (B,), generator=self.gen, device=self.device, dtype=dtype)
+        k = torch.randint(0, max(1, self.live.numel()), (B,), generator=self.gen, device=self.device)
+        return self.live[k].to(dtype)
 
     # ------------------------------------------------------------------ data
     def load_history(self, values) -> None:
@@ -163,7 +213,7 @@ class LstmShard:
         reduces it mod R); same distribution as :meth:`_sample`."""
         r0 = self.rings[0]
         L = r0.length
-        si = torch.randint(0, self.n, (B,), generator=self.gen, device=self.device, dtype=torch.int32)
+        si = self._draw_rows(B, torch.int32)
         if L > self.T:
             st = torch.randint(r0.head + 1, r0.head + L - self.T + 1, (B,), generator=self.gen,
                                device=self.device, dtype=torch.int32)
@@ -174,17 +224,23 @@ class LstmShard:
     # ------------------------------------------------------------------ train / score
     def _sample(self, B: int) -> torch.Tensor:
         L = self.rings[0].length
-        si = torch.randint(0, self.n, (B,), generator=self.gen, device=self.device)
+        si = self._draw_rows(B, torch.int64)
         off = torch.randint(0, max(1, L - self.T), (B,), generator=self.gen, device=self.device)
         return self._gather(si, off)
 
-    def train_step(self) -> torch.Tensor:
-        """One DP step on ``train_batch`` history windows of this shard."""
+    def train_step(self, weight: Optional[float] = None, flags: Optional[torch.Tensor] = None,
+                   timeout_s: Optional[float] = None) -> torch.Tensor:
+        """One DP step on ``train_batch`` history windows of this shard.
+        ``weight`` 0: no live rows — join the gradient reduction with nothing
+        (see :meth:`DPTrainer.step`); ``flags``: summed in the same collective."""
+        kw = dict(weight=weight, flags=flags, timeout_s=timeout_s)
+        if weight is not None and weight == 0:
+            return self.trainer.step(None, grad_fn=lambda m, _w: torch.zeros((), device=self.device), **kw)
         if self.fused_train:
-            return self.trainer.step(self._sample_ring(self.train_batch))
-        return self.trainer.step(self._sample(self.train_batch))
+            return self.trainer.step(self._sample_ring(self.train_batch), **kw)
+        return self.trainer.step(self._sample(self.train_batch), **kw)
 
-    def calibrate(self, n: int = 4096) -> None:
+    def calibrate(self, n: int = 4096, rows: Optional[torch.Tensor] = None) -> None:
         """Calibrate the verdict threshold on healthy history (untimed, once and
         then on a slow cadence).
 
@@ -195,30 +251,40 @@ class LstmShard:
         unusual day does not inflate it) and the pooled relative spread
         ``rho``.  On the GPU the windows are scored by the SAME fused kernel
         (and precision: bf16, or fp8 e4m3) that scores the ticks, so the
-        calibration includes the scoring path's quantisation noise."""
-        e = self._calib_errors(self._sample_ring(n) if self.gpu else None, n)
+        calibration includes the scoring path's quantisation noise.
+
+        ``rows``: calibrate only these rows' ``mu_i`` (series that joined a
+        running monitor); the global level and ``rho`` are still re-estimated
+        over the live rows with the same collectives on every rank."""
+        if self.live is not None and self.live.numel() == 0:  # nothing live here: join the reductions
+            e = torch.zeros(0, dtype=torch.float64, device=self.device)
+        else:
+            e = self._calib_errors(self._sample_ring(n) if self.gpu else None, n)
         e = e[torch.isfinite(e)]
         mom = torch.stack([e.sum(), (e * e).sum(), torch.tensor(float(e.numel()), dtype=torch.float64,
                                                                 device=e.device)])
         self._all_reduce(mom)
         s1, s2, cnt = mom.tolist()
-        self.mu = s1 / cnt
-        self.sigma = max(s2 / cnt - self.mu * self.mu, 0.0) ** 0.5 + 1e-12
+        if cnt > 0:
+            self.mu = s1 / cnt
+            self.sigma = max(s2 / cnt - self.mu * self.mu, 0.0) ** 0.5 + 1e-12
         if self.cal_windows <= 0:
             self.cal = None
             return
         K, L, R = self.cal_windows, self.rings[0].length, self.rings[0].R
         span = max(L - self.T, 1)
         offs = [(k * span) // K for k in range(K)]  # logical window starts, oldest first
+        sel = self._all if rows is None else rows.to(self.device, torch.long)
+        nr = int(sel.numel())
         if self.gpu:
             head = self.rings[0].head
-            si = self._all.to(torch.int32).repeat(K)
+            si = sel.to(torch.int32).repeat(K)
             st = torch.tensor([(head + o) % R for o in offs], dtype=torch.int32,
-                              device=self.device).repeat_interleave(self.n)
-            ek = self._calib_errors(self._ring_src(si, st), K * self.n).view(K, self.n)
+                              device=self.device).repeat_interleave(nr)
+            ek = self._calib_errors(self._ring_src(si, st), K * nr).view(K, nr)
         else:
-            ek = torch.stack([self._calib_errors(self._gather(self._all, torch.full_like(
-                self._zero_off, L - self.T - o)), self.n) for o in offs])
+            ek = torch.stack([self._calib_errors(self._gather(sel, torch.full_like(
+                sel, L - self.T - o)), nr) for o in offs])
         ek = torch.where(torch.isfinite(ek), ek, torch.nan)
         srt = ek.sort(0).values  # NaN last
         ok = torch.isfinite(srt)
@@ -234,8 +300,15 @@ class LstmShard:
         self._all_reduce(mom)
         r1, r2, rc = mom.tolist()
         m1 = r1 / max(rc, 1.0)
-        self.rho = max((max(r2 / max(rc, 1.0) - m1 * m1, 0.0)) ** 0.5, 1e-6)
-        self.cal = torch.stack([mu_i, 1.0 / (self.rho * mu_i)], 1).float().contiguous()
+        if rc > 0:
+            self.rho = max((max(r2 / max(rc, 1.0) - m1 * m1, 0.0)) ** 0.5, 1e-6)
+        new = torch.stack([mu_i, 1.0 / (self.rho * mu_i)], 1).float()
+        if rows is None or self.cal is None:
+            full = torch.ones((self.n, 2), dtype=torch.float32, device=self.device)
+            full[sel] = new
+            self.cal = full.contiguous()
+        else:
+            self.cal[sel] = new
 
     def _calib_errors(self, src, n: int) -> torch.Tensor:
         """Reconstruction errors (float64) of ``src``'s windows: a kernel

@@ -1,0 +1,351 @@
+"""Continuous multi-metric jobs on the resident LSTM-autoencoder engine.
+
+The reference brain scores a job with 3+ metrics with an LSTM model
+(``docs/guides/design.md:84``; ``ML_ALGORITHM=lstm`` for 2+).  The per-job
+path (:mod:`.multivariate`) trains one small model per job.  On a GPU node
+the continuous LSTM jobs of every rank are served by ONE shared
+LSTM-autoencoder per node, trained data-parallel across the ranks
+(BASELINE configs 3 / 5 in the product, not only in the bench):
+
+* entity = a continuous job; its metrics (sorted aliases, at most ``F``,
+  absent ones zero-padded) are the features of one row of an
+  :class:`~.lstm_engine.LstmShard`; the 7-day history of each metric comes
+  from the node's resident keyed history (:mod:`.resident`: one query per
+  metric family per tick, week-long loads only for new series) and is copied
+  into the shard's per-feature rings when the job joins;
+* every tick, on every rank in lockstep: the new minute of every entity is
+  appended, ONE data-parallel Adam step runs on windows sampled from this
+  rank's live entities (RC3: bucketed gradient all-reduce over RCCL, the
+  rank's weight — 0 when it holds no LSTM job — and an "admitted entities"
+  flag in the same collective), every rank's replica applies the same
+  averaged step, so the replicas stay bit-identical; when any rank admitted
+  entities, every rank joins a calibration pass (new rows' error levels,
+  pooled spread); after a node re-formation the weights and Adam state are
+  broadcast from rank 0 (RC4);
+* the fused MFMA kernel scores every entity's newest window (bf16; fp8 e4m3
+  with ``FOREMAST_LSTM_FP8=1``) → per-entity z-score against its calibrated
+  error level → verdict; an anomalous entity finishes its job
+  ``completed_unhealth`` naming every metric with its newest point, past
+  ``endTime`` the job finishes ``completed_health``.
+"""
+
+from __future__ import annotations
+
+import json
+import logging
+import os
+import time
+from dataclasses import dataclass
+from typing import Callable, Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..api import rest as r
+from ..parallel import comm
+from ..store.jobstore import JobStore
+from ..utils.config import BrainConfig
+from ..utils.metrics import BrainMetrics
+from ..utils.timeutil import TimeFormatError, parse_rfc3339
+from .lstm_engine import LstmShard
+from .resident import Key, ResidentHistory
+from .streaming import CALLER_SPLIT, is_continuous, series_of
+
+log = logging.getLogger("foremast.lstm_monitor")
+
+
+def lstm_features(doc, cfg: BrainConfig) -> Optional[List[Tuple[str, Key]]]:
+    """(alias, series key) features of a continuous job the LSTM engine scores
+    (``ML_ALGORITHM=lstm`` with 2+ metrics, ``auto`` with 3+), else None."""
+    if not is_continuous(doc) or cfg.algorithm not in ("lstm", "auto"):
+        return None
+    feats = sorted(series_of(doc).items())
+    if any(k[1].startswith(CALLER_SPLIT) or not k[3] for _, k in feats):
+        return None
+    need = 2 if cfg.algorithm == "lstm" else 3
+    return feats if len(feats) >= need else None
+
+
+@dataclass
+class Entity:
+    doc: Dict
+    end_ts: float
+    feats: List[Tuple[str, Key]]
+    row: int = -1
+
+
+class LstmMonitor:
+    def __init__(self, store: JobStore, cfg: Optional[BrainConfig] = None, prom=None, device=None,
+                 worker_id: str = "lstm-0", metrics: Optional[BrainMetrics] = None, step: float = 60.0,
+                 clock=time.time, owns: Optional[Callable[[Dict], bool]] = None, ring_len: Optional[int] = None,
+                 features: int = 5, window: Optional[int] = None, hidden: Optional[int] = None,
+                 fp8: Optional[bool] = None, train_batch: int = 4096, min_capacity: int = 64, seed: int = 0,
+                 history: Optional[ResidentHistory] = None, decode_threads: int = 8) -> None:
+        from ..promql.client import PromClient
+        self.store = store
+        self.cfg = cfg or BrainConfig.from_env()
+        self.prom = prom or PromClient()
+        self.device = torch.device(device) if device is not None else (
+            torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
+        self.gpu = self.device.type == "cuda"
+        self.worker_id, self.step, self.clock, self.owns = worker_id, float(step), clock, owns
+        self.metrics = metrics or BrainMetrics()
+        self.F = int(features)
+        R = ring_len or self.cfg.ring_len
+        self.history = history or ResidentHistory(self.prom, self.device, R, self.step, clock=clock,
+                                                  decode_threads=decode_threads)
+        if fp8 is None:
+            fp8 = os.environ.get("FOREMAST_LSTM_FP8", "0") not in ("0", "", "false")
+        tb = train_batch if self.gpu else min(train_batch, 64)
+        self.shard = LstmShard(max(1, min_capacity), R, self.F, window=window or self.cfg.lstm_window,
+                               hidden=hidden or self.cfg.lstm_hidden, fp8=bool(fp8) and self.gpu,
+                               device=self.device, threshold=self.cfg.lstm_threshold, train_batch=tb, seed=seed,
+                               dtype=torch.bfloat16 if self.gpu else torch.float32, dp_overlap=False,
+                               restat_every=1 << 30)
+        for ring in self.shard.rings:
+            ring.state.head, ring.state.length = 0, R
+        self.shard.live = torch.zeros(0, dtype=torch.int64, device=self.device)
+        self.jobs: Dict[str, Entity] = {}
+        self.waiting: Dict[str, Entity] = {}
+        self.row_job: List[Optional[str]] = [None] * self.shard.n
+        self.feat_rows = torch.full((self.shard.n, self.F), -1, dtype=torch.int64, device=self.device)
+        self.padded = torch.zeros((self.shard.n, self.F), dtype=torch.bool, device=self.device)
+        self.apps: Dict[Tuple[str, str], int] = {}
+        self._app_names: List[Optional[Tuple[str, str]]] = [None]  # app 0: free rows (never reported)
+        self.roster_version = 0
+        self.t_cur = 0.0
+        self.ticks = 0
+        self.exchange_timeout = comm.exchange_timeout_s()
+        # DP steps before the first calibration of a fresh node's model (FOREMAST_LSTM_PRETRAIN)
+        self.pretrain_steps = int(os.environ.get("FOREMAST_LSTM_PRETRAIN", "200" if self.gpu else "20"))
+        self.timings: Dict[str, float] = {}
+
+    # ------------------------------------------------------------------ membership
+    def is_mine(self, d) -> bool:
+        return lstm_features(d, self.cfg) is not None and (self.owns is None or self.owns(d))
+
+    def sync(self, steal_from=None) -> int:
+        now = self.clock()
+        docs = self.store.claim(self.worker_id, now=now, max_stuck_s=self.cfg.max_stuck_seconds, limit=10_000,
+                                only=self.is_mine, steal_from=steal_from)
+        for d in docs:
+            if d["id"] in self.jobs or d["id"] in self.waiting:
+                continue
+            try:
+                end_ts = parse_rfc3339(d.get("endTime", "")).timestamp()
+            except TimeFormatError:
+                end_ts = float("inf")
+            feats = lstm_features(d, self.cfg)[:self.F]
+            self.waiting[d["id"]] = Entity(doc=d, end_ts=end_ts, feats=feats)
+            self.history.want([k for _, k in feats], now)
+        return len(docs)
+
+    def release(self, pred: Callable[[Dict], bool]) -> int:
+        now, back = self.clock(), []
+        for jid, e in list(self.jobs.items()) + list(self.waiting.items()):
+            if pred(e.doc):
+                back.append((jid, {"status": r.ST_REPROGRESS, "claimed_by": "", "not_before": 0.0}))
+                self._drop(jid, now)
+        if back:
+            self.store.update_many(back, expect_claimed_by=self.worker_id)
+        return len(back)
+
+    def after_reform(self) -> None:
+        """RC4: every rank adopts rank 0's weights and optimizer state after the
+        node re-formed (a step may have been applied on some ranks only)."""
+        if comm.active():
+            for p in self.shard.model.parameters():
+                dist.broadcast(p.data, src=0)
+            for st in self.shard.trainer.opt.state.values():
+                for v in st.values():
+                    if torch.is_tensor(v):
+                        dist.broadcast(v.data if v.device == self.device else v, src=0)
+            self.shard.packed = None
+
+    def _drop(self, jid: str, now: float) -> None:
+        e = self.jobs.pop(jid, None) or self.waiting.pop(jid, None)
+        if e is None:
+            return
+        self.history.unwant([k for _, k in e.feats], now)
+        if e.row >= 0:
+            self._free_row(e.row)
+
+    @property
+    def n_live(self) -> int:
+        return len(self.jobs)
+
+    # ------------------------------------------------------------------ rows
+    def _grow(self, cap: int) -> None:
+        n = self.shard.n
+        self.shard.grow(cap)
+        self.row_job.extend([None] * (cap - n))
+        fr = torch.full((cap, self.F), -1, dtype=torch.int64, device=self.device)
+        fr[:n] = self.feat_rows
+        pd = torch.zeros((cap, self.F), dtype=torch.bool, device=self.device)
+        pd[:n] = self.padded
+        self.feat_rows, self.padded = fr, pd
+
+    def _free_row(self, row: int) -> None:
+        self.row_job[row] = None
+        self.feat_rows[row] = -1
+        self.padded[row] = False
+        self.shard.app_id[row] = 0
+        for ring in self.shard.rings:
+            ring.data[row].fill_(float("nan"))
+        self._live_dirty = True
+
+    def _app_index(self, app: Tuple[str, str]) -> int:
+        i = self.apps.get(app)
+        if i is None:
+            i = self.apps[app] = len(self._app_names)
+            self._app_names.append(app)
+            self.roster_version += 1
+            if self.shard.app_stats.shape[0] < len(self._app_names):
+                cap = self.shard.app_stats.shape[0]
+                while cap < len(self._app_names):
+                    cap *= 2
+                self.shard.app_stats = torch.zeros((cap, 2), dtype=torch.int32, device=self.device)
+        return i
+
+    def _admit(self) -> List[int]:
+        hist = self.history
+        ready = [e for e in self.waiting.values() if all(hist.ready(k) for _, k in e.feats)]
+        if not ready:
+            return []
+        free = [i for i, j in enumerate(self.row_job) if j is None]
+        if len(free) < len(ready):
+            cap = self.shard.n
+            while cap - (self.shard.n - len(free)) < len(ready):
+                cap *= 2
+            self._grow(cap)
+            free = [i for i, j in enumerate(self.row_job) if j is None]
+        rows = []
+        fr = np.full((len(ready), self.F), -1, dtype=np.int64)
+        for i, (e, row) in enumerate(zip(ready, free)):
+            del self.waiting[e.doc["id"]]
+            e.row = row
+            self.jobs[e.doc["id"]] = e
+            self.row_job[row] = e.doc["id"]
+            rows.append(row)
+            for f, (_, k) in enumerate(e.feats):
+                fr[i, f] = hist.rows[k]
+            ns, app = e.feats[0][1][2], e.feats[0][1][3]
+            self.shard.app_id[row] = self._app_index((ns, app))
+        idx = torch.tensor(rows, dtype=torch.long, device=self.device)
+        fr_t = torch.from_numpy(fr).to(self.device)
+        self.feat_rows[idx] = fr_t
+        self.padded[idx] = fr_t < 0
+        # the week of each feature, from the resident ring (logical order, ending at t_last)
+        ring = hist.ring
+        cols = (torch.arange(hist.R, device=self.device) + ring.head) % hist.R
+        vals = []
+        for f in range(self.F):
+            src = fr_t[:, f].clamp(min=0)
+            v = ring.data.index_select(0, src).index_select(1, cols).float()
+            vals.append(torch.where((fr_t[:, f] >= 0)[:, None], v, torch.zeros_like(v)))
+        self.shard.write_rows(idx, vals)
+        self._live_dirty = True
+        return rows
+
+    def _ingest(self) -> None:
+        """Append the minutes the resident history gained since the last tick to
+        every row (free rows get NaN, zero-padded features 0)."""
+        hist = self.history
+        if self.t_cur == 0.0:
+            self.t_cur = hist.t_last
+            return
+        n_new = int(round((hist.t_last - self.t_cur) / self.step))
+        if n_new <= 0:
+            return
+        R = hist.R
+        for j in range(min(n_new, R)):
+            age = min(n_new, R) - 1 - j                   # oldest new minute first
+            col = (hist.ring.head + R - 1 - age) % R
+            v = hist.ring.data[:, col].float()
+            x = v[self.feat_rows.clamp(min=0)]
+            x = torch.where(self.padded, torch.zeros_like(x), x)
+            x = torch.where((self.feat_rows >= 0) | self.padded, x, torch.full_like(x, float("nan")))
+            self.shard.ingest_tick(x.contiguous())
+        self.t_cur = hist.t_last
+
+    # ------------------------------------------------------------------ tick
+    async def tick(self) -> Dict[str, str]:
+        """One lockstep tick (every rank runs it: the DP step is a collective)."""
+        t0 = time.perf_counter()
+        now = self.clock()
+        admitted: List[int] = []
+        try:
+            self.store.heartbeat(self.worker_id, now)
+            await self.history.sync(now)
+            self._ingest()
+            admitted = self._admit()
+            if admitted:
+                self.shard.refresh_stats()
+        except Exception as e:  # noqa: BLE001 - the collectives below must still run on this rank
+            log.exception("lstm data step failed: %s", e)
+        if getattr(self, "_live_dirty", True):
+            live = [i for i, j in enumerate(self.row_job) if j is not None]
+            self.shard.live = torch.tensor(live, dtype=torch.int64, device=self.device)
+            self._live_dirty = False
+        has = int(self.shard.live.numel() > 0)
+        flags = torch.tensor([float(len(admitted))], device=self.device)
+        self.shard.train_step(weight=float(has), flags=flags,
+                              timeout_s=self.exchange_timeout if comm.active() else None)
+        red = self.shard.trainer.last_flags
+        if red is not None and float(red[0]) > 0:  # some rank admitted entities (every rank sees it)
+            # a fresh model first gets its initial training (same step count on every rank:
+            # the trainers advance in lockstep), then the new rows are calibrated (collective)
+            while self.shard.trainer.steps < self.pretrain_steps:
+                self.shard.train_step(weight=float(has), timeout_s=self.exchange_timeout if comm.active() else None)
+            self.shard.calibrate(min(self.shard.train_batch, 4096),
+                                 rows=torch.tensor(admitted, dtype=torch.long, device=self.device))
+        self.timings["train_ms"] = (time.perf_counter() - t0) * 1e3
+        written: Dict[str, str] = {}
+        if not self.jobs:
+            self.shard.app_stats.zero_()
+            return written
+        out = self.shard.score()
+        v = out["verdict"].cpu().numpy()
+        newest = self._newest()
+        items = []
+        for jid, e in list(self.jobs.items()):
+            if v[e.row] == 1:
+                anomaly = {}
+                for f, (alias, _k) in enumerate(e.feats):
+                    anomaly[alias] = {"tags": "lstm", "values": [self.history.t_last, float(newest[e.row, f])]}
+                items.append((jid, {"status": r.ST_COMPLETED_UNHEALTH, "claimed_by": "", "modified_ts": now,
+                                    "reason": "anomaly detected in " + ",".join(sorted(anomaly)) + " (lstm)",
+                                    "anomalyInfo": json.dumps(anomaly),
+                                    "processingContent": f"scored by {self.worker_id} (resident lstm)"}))
+            elif now >= e.end_ts:
+                items.append((jid, {"status": r.ST_COMPLETED_HEALTH, "claimed_by": "", "reason": "",
+                                    "modified_ts": now,
+                                    "processingContent": f"scored by {self.worker_id} (resident lstm)"}))
+        if items:
+            for (jid, fields), ok in zip(items, self.store.update_many(items, expect_claimed_by=self.worker_id)):
+                if ok:
+                    written[jid] = fields["status"]
+                    self.metrics.jobs.labels(status=fields["status"]).inc()
+                self._drop(jid, now)
+        self.ticks += 1
+        self.metrics.series_scored.inc(sum(len(e.feats) for e in self.jobs.values()))
+        self.timings["tick_ms"] = (time.perf_counter() - t0) * 1e3
+        return written
+
+    def _newest(self) -> np.ndarray:
+        R = self.history.R
+        col = (self.shard.rings[0].head + R - 1) % R
+        return torch.stack([ring.data[:, col].float() for ring in self.shard.rings], 1).cpu().numpy()
+
+    def model_digest(self) -> str:
+        """CRC of the replica's weights (the node table shows every rank's: equal = in sync)."""
+        import zlib
+        crc = 0
+        for p in self.shard.model.parameters():
+            crc = zlib.crc32(p.detach().float().cpu().numpy().tobytes(), crc)
+        return f"{crc:08x}"
+
+    def app_table(self):
+        names = list(self._app_names)
+        return names, self.shard.app_stats[:len(names)]

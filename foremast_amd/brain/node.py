@@ -104,6 +104,9 @@ class NodeBrain:
         gone = set(before) - set(self.world.members)
         self.dead |= {worker_id_of(m) for m in gone}
         moved = sum(m.release(lambda d: not self.owns(d)) for m in self.monitors)
+        for m in self.monitors:
+            if hasattr(m, "after_reform"):
+                m.after_reform()
         self.health.reset(kv=self.world.pstore)
         log.warning("node re-formed: generation %d, members %s (lost %s); released %d moved jobs",
                     self.world.generation, self.world.members, sorted(gone), moved)
@@ -132,6 +135,9 @@ class NodeBrain:
     def _exchange(self) -> Dict:
         names, counts, version, n_live = self.app_table()
         info = {"member": self.world.id if self.world else "m0", "pid": os.getpid()}
+        for m in self.monitors:
+            if hasattr(m, "model_digest"):
+                info["lstm_model"] = m.model_digest()
         return self.health.exchange(names, counts, version, n_live, info)
 
     async def tick(self) -> Dict:

@@ -131,6 +131,7 @@ class StreamingMonitor:
         self.R, self.step, self.W = ring_len, step, window
         self.clock = clock
         self.owns = owns
+        self.exclude: Optional[Callable[[Dict], bool]] = None  # jobs another resident engine serves (LSTM)
         self.chunk_pts = max(1, int(history_chunk_points))
         self.apps_per_query = max(1, int(apps_per_query))
         self.decode_threads = max(1, int(decode_threads))  # native threads decoding the responses
@@ -153,7 +154,8 @@ class StreamingMonitor:
         now = self.clock()
 
         def only(d):
-            return is_streamable(d) and (self.owns is None or self.owns(d))
+            return (is_streamable(d) and (self.owns is None or self.owns(d))
+                    and (self.exclude is None or not self.exclude(d)))
         docs = self.store.claim(self.worker_id, now=now, max_stuck_s=self.cfg.max_stuck_seconds, limit=10_000,
                                 only=only, steal_from=steal_from)
         for d in docs:

@@ -76,19 +76,74 @@ class GradBuckets:
             b["flat"].zero_()
             b["ready"] = 0
 
-    def finish(self) -> None:
+    def finish(self, weight: Optional[float] = None, flags: Optional[torch.Tensor] = None,
+               timeout_s: Optional[float] = None) -> Optional[torch.Tensor]:
         """Complete the reduction (average over ranks).  Buckets whose hooks
         did not fire (gradients written directly, e.g. by the fused LSTM
-        training kernel) are all-reduced here."""
-        if self.active:
+        training kernel) are all-reduced here.
+
+        ``weight``: this rank's share of the step (e.g. 0 for a rank with no
+        series: it still joins the collective, with a zero gradient); the
+        average is then weighted, the weights travelling in the same
+        all-reduce as an extra element.  ``flags``: small float tensor of
+        per-rank values summed in that same collective (returned reduced) —
+        e.g. "some rank admitted series and needs a calibration pass".
+        ``timeout_s``: host-side deadline on the reduction
+        (:func:`~foremast_amd.parallel.comm.wait_bounded`)."""
+        extra = None
+        if weight is not None and self.overlap and any(b["ready"] for b in self.buckets):
+            raise ValueError("weighted steps need GradBuckets(overlap=False): hooks reduce before the weight applies")
+        if weight is not None or flags is not None:
+            parts = [torch.tensor([1.0 if weight is None else float(weight)], device=self.buckets[-1]["flat"].device)]
+            if flags is not None:
+                parts.append(flags.to(parts[0].device, torch.float32).reshape(-1))
+            extra = torch.cat(parts)
+            if weight is not None and weight != 1.0:
+                for b in self.buckets:
+                    b["flat"].mul_(float(weight))
+        active = comm.active(self.group)
+        if active:
+            world = dist.get_world_size(self.group)
             for b in self.buckets:
                 if not self.overlap or b["ready"] < len(b["params"]):
-                    self._handles.append(dist.all_reduce(b["flat"], group=self.group, async_op=True))
+                    if extra is not None and b is self.buckets[-1]:
+                        # one collective: the last bucket carries the weights / flags
+                        cat = torch.cat([b["flat"], extra.to(b["flat"].dtype)])
+                        self._handles.append((dist.all_reduce(cat, group=self.group, async_op=True), cat, b))
+                    else:
+                        self._handles.append((dist.all_reduce(b["flat"], group=self.group, async_op=True), None, b))
             for h in self._handles:
-                h.wait()
+                if isinstance(h, tuple):
+                    work, cat, b = h
+                    if timeout_s is not None:
+                        comm.wait_bounded(work, timeout_s, "gradient all-reduce")
+                    else:
+                        work.wait()
+                    if cat is not None:
+                        n = b["flat"].numel()
+                        b["flat"].copy_(cat[:n])
+                        extra = cat[n:].to(torch.float32)
+                else:
+                    h.wait()
             self._handles.clear()
+        else:
+            world = 1
+        if extra is not None:
+            if active and self.overlap and all(b["ready"] == len(b["params"]) for b in self.buckets):
+                # hooks reduced every bucket already: reduce the extras on their own
+                if timeout_s is not None:
+                    w = dist.all_reduce(extra, group=self.group, async_op=True)
+                    comm.wait_bounded(w, timeout_s, "gradient weights")
+                else:
+                    dist.all_reduce(extra, group=self.group)
+            total = float(extra[0])
             for b in self.buckets:
-                b["flat"].div_(self.world)
+                b["flat"].div_(max(total, 1e-12))
+            return extra[1:]
+        if active:
+            for b in self.buckets:
+                b["flat"].div_(world)
+        return None
 
 
 def broadcast_params(module: torch.nn.Module, src: int = 0, group=None) -> None:
@@ -113,17 +168,24 @@ class DPTrainer:
         self.opt = torch.optim.Adam(model.parameters(), lr=lr, fused=on_gpu or None)
         self.steps = 0
 
-    def step(self, windows, grad_fn=None) -> torch.Tensor:
+    def step(self, windows, grad_fn=None, weight: Optional[float] = None, flags: Optional[torch.Tensor] = None,
+             timeout_s: Optional[float] = None) -> torch.Tensor:
         """``grad_fn`` overrides the constructor's for this step (e.g. the
-        second half of a split fused-kernel gradient)."""
+        second half of a split fused-kernel gradient).  ``windows`` None with
+        ``weight`` 0: this rank has no data and joins the reduction with a zero
+        gradient (every rank's Adam then applies the same averaged step, so the
+        replicas stay identical).  ``flags`` / ``timeout_s``: see
+        :meth:`GradBuckets.finish`; the reduced flags are kept in ``last_flags``."""
         self.buckets.zero()
         grad_fn = grad_fn or self.grad_fn
-        if grad_fn is not None:
+        if windows is None and grad_fn is None:
+            loss = torch.zeros((), device=self.buckets.buckets[0]["flat"].device)
+        elif grad_fn is not None:
             loss = grad_fn(self.model, windows)
         else:
             loss = self.model.recon_error(windows).mean()
             loss.backward()
-        self.buckets.finish()
+        self.last_flags = self.buckets.finish(weight, flags, timeout_s)
         self.opt.step()
         self.steps += 1
         return loss.detach()
