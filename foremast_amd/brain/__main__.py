@@ -118,6 +118,10 @@ async def run(args) -> BrainWorker:
             rollout = RolloutMonitor(store, cfg, device=dev, metrics=metrics, step=args.step, window=args.window,
                                      pods=args.pods, worker_id=(worker_id_of(member) if world else member) + "-rollout",
                                      ring_len=cfg.ring_len)
+            if os.environ.get("FOREMAST_CLUSTER_AFFINE", "0") not in ("0", "", "false") and world is not None:
+                # each rank scrapes its own clusters; cross-cluster windows cross ranks (RC5)
+                from ..parallel.affine import ClusterRouter, affinity_from_env
+                rollout.router = ClusterRouter(affinity_from_env(), dev)
         lstm = None
         if args.lstm is None:
             args.lstm = cfg.algorithm in ("lstm", "auto")

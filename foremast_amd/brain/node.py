@@ -86,7 +86,7 @@ class NodeBrain:
         self._published = -1e18
         self._last_anomalous = None
         for m in self.monitors:
-            m.owns = self.owns
+            m.owns = self._owns_for(m)
 
     @property
     def rank(self) -> int:
@@ -100,10 +100,15 @@ class NodeBrain:
         ns, app = app_of(doc)
         return owner_of(ns, app, self.size) == self.rank
 
+    def _owns_for(self, m):
+        """Ownership a monitor claims by: by app, or — a rollout monitor in
+        cluster-affine mode — by the cluster of the job's new pods."""
+        return m.owns_affine if getattr(m, "router", None) is not None else self.owns
+
     def _after_reform(self, before: List[str]) -> None:
         gone = set(before) - set(self.world.members)
         self.dead |= {worker_id_of(m) for m in gone}
-        moved = sum(m.release(lambda d: not self.owns(d)) for m in self.monitors)
+        moved = sum(m.release(lambda d, o=self._owns_for(m): not o(d)) for m in self.monitors)
         for m in self.monitors:
             if hasattr(m, "after_reform"):
                 m.after_reform()

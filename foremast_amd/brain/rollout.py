@@ -85,7 +85,7 @@ class RolloutSeries:
     """One (job, metric alias): a row of the rollout table."""
     alias: str
     hkey: Key                       # 7-day history series (endpoint, metric, namespace, app)
-    fam: Tuple[str, str]            # (endpoint, pod metric) of the current / baseline windows
+    fam: Tuple[str, str]            # (endpoint, pod metric) of the current window
     namespace: str
     cur_pods: Tuple[str, ...]
     base_pods: Tuple[str, ...]
@@ -94,6 +94,7 @@ class RolloutSeries:
     base_start: float
     base_n: int
     hist_end: float
+    base_fam: Tuple[str, str] = ("", "")  # (endpoint, pod metric) of the baseline window (may be another cluster)
 
 
 @dataclass
@@ -242,7 +243,8 @@ def _plan(doc, step, window_cols) -> Optional[RolloutPlan]:
             except (urls.ConfigError, SelectorError, KeyError, ValueError):
                 return None
             pb = _pods_of(sel_b)
-            if pb is None or sel_b.name != sel_c.name or ep_b != ep_c or b_step != step or pb[0] != pc[0]:
+            # the baseline may live in another cluster (its own Prometheus): multi-cluster canary
+            if pb is None or sel_b.name != sel_c.name or b_step != step or pb[0] != pc[0]:
                 return None
             b_pods, b_n = pb[1], min(window_cols, int(round((b_end - b_start) / step)) + 1)
             if b_n > 0 and int(round((b_end - b_start) / step)) + 1 > window_cols:
@@ -252,7 +254,8 @@ def _plan(doc, step, window_cols) -> Optional[RolloutPlan]:
             alias=alias, hkey=(ep_h, sel_h.name, lab["namespace"], lab["app"]), fam=(ep_c, sel_c.name),
             namespace=pc[0], cur_pods=pc[1], base_pods=b_pods, cur_start=c_start,
             cur_n=max(0, min(window_cols, int(round((c_end - c_start) / step)) + 1)),
-            base_start=b_start, base_n=b_n, hist_end=h_end))
+            base_start=b_start, base_n=b_n, hist_end=h_end,
+            base_fam=(ep_b, sel_b.name) if alias in base else ("", "")))
     return RolloutPlan(doc_id=doc["id"], app=app, end_ts=end_ts, series=out, doc=doc)
 
 
@@ -357,6 +360,10 @@ class RolloutMonitor:
         self._srcmap_dirty = True
         self._blocks: Dict[Tuple[int, int], List[torch.Tensor]] = {}
         self._block_i = 0
+        # cluster-affine ingest (parallel/affine.py): windows of another rank's clusters are
+        # requested at admission and delivered by that rank in the tick's lockstep exchange
+        self.router = None
+        self._remote: List[Tuple[str, Tuple[str, str], float, int, List]] = []
         self.timings: Dict[str, float] = {}
         self._bands: Tuple[np.ndarray, np.ndarray, np.ndarray] = (np.zeros(0), np.zeros(0), np.zeros(0))
         self._last_anom: Dict[int, float] = {}
@@ -462,6 +469,12 @@ class RolloutMonitor:
         return self._n_live
 
     # ------------------------------------------------------------------ membership
+    def owns_affine(self, d) -> bool:
+        """Cluster-affine mode: a job belongs to the rank that scrapes the cluster
+        of its new pods (its history and current windows are then local)."""
+        p = plan_rollout(d, self.cfg, self.step, self.Wc)
+        return p is not None and self.router.local(p.series[0].fam[0])
+
     def _claimable(self, d) -> bool:
         return plan_rollout(d, self.cfg, self.step, self.Wc) is not None and (self.owns is None or self.owns(d))
 
@@ -740,18 +753,30 @@ class RolloutMonitor:
         query per pod family and group of jobs, every body decoded through one
         key index over the group's pods, then gathered into the rows."""
         t_last = self.history.t_last
-        groups: Dict[Tuple[str, float, int], List[Tuple[int, RolloutSeries, Tuple[str, ...]]]] = {}
+        # (kind, window start, points) -> [(row, series, pods, family)]
+        groups: Dict[Tuple[str, float, int], List[Tuple[int, RolloutSeries, Tuple[str, ...], Tuple[str, str]]]] = {}
         for row, s in items:
             if s.base_pods and s.base_n > 0:
-                groups.setdefault(("base", s.base_start, s.base_n), []).append((row, s, s.base_pods))
+                groups.setdefault(("base", s.base_start, s.base_n), []).append((row, s, s.base_pods, s.base_fam))
             if s.cur_n > 0 and s.cur_start <= t_last:
                 n = min(s.cur_n, int(round((t_last - s.cur_start) / self.step)) + 1)
-                groups.setdefault(("win", s.cur_start, n), []).append((row, s, s.cur_pods))
+                groups.setdefault(("win", s.cur_start, n), []).append((row, s, s.cur_pods, s.fam))
         P, Wc = self.P, self.Wc
+        if self.router is not None:  # windows of other ranks' clusters: requested, not fetched
+            for (dst, start, n), grp in list(groups.items()):
+                remote = [g for g in grp if not self.router.local(g[3][0])]
+                if not remote:
+                    continue
+                groups[(dst, start, n)] = [g for g in grp if self.router.local(g[3][0])]
+                for f in dict.fromkeys(g[3] for g in remote):
+                    part = [(row, s, ps) for row, s, ps, fam in remote if fam == f]
+                    pods = list(dict.fromkeys((s.namespace, pod) for _, s, ps in part for pod in ps[:P]))
+                    self._remote.append((dst, f, start, n, part, pods))
+            groups = {k: v for k, v in groups.items() if v}
         for (dst, start, n), grp in groups.items():
-            pods = list(dict.fromkeys((s.namespace, pod) for _, s, ps in grp for pod in ps[:P]))
+            pods = list(dict.fromkeys((s.namespace, pod) for _, s, ps, _f in grp for pod in ps[:P]))
             local = {k: i for i, k in enumerate(pods)}
-            fams = list(dict.fromkeys(s.fam for _, s, _ in grp))
+            fams = list(dict.fromkeys(f for _, _, _, f in grp))
             fidx = {f: i for i, f in enumerate(fams)}
             nl = len(pods)
             hs = native.key_hashes([k[0] for k in pods], [k[1] for k in pods])
@@ -761,7 +786,7 @@ class RolloutMonitor:
             tables = {f: native.KeyTable.indexed(hs, fidx[f] * nl + np.arange(nl), "namespace", "pod") for f in fams}
             reqs, tabs = [], []
             for f in fams:
-                rows_f = [(s, ps) for _, s, ps in grp if s.fam == f]
+                rows_f = [(s, ps) for _, s, ps, ff in grp if ff == f]
                 for g in range(0, len(rows_f), self.apps_per_query):
                     part = rows_f[g:g + self.apps_per_query]
                     sel = (f'{f[1]}{{namespace=~"{re_alt({s.namespace for s, _ in part})}",'
@@ -772,16 +797,52 @@ class RolloutMonitor:
             if not all(ok):
                 log.warning("%d of %d window queries failed (%s from %d)", ok.count(False), len(ok), dst, start)
             gidx = np.full((len(grp), P), -1, dtype=np.int64)
-            for i, (_, s, ps) in enumerate(grp):
-                fo = fidx[s.fam] * nl
+            for i, (_, s, ps, f) in enumerate(grp):
+                fo = fidx[f] * nl
                 for p, pod in enumerate(ps[:P]):
                     gidx[i, p] = fo + local[(s.namespace, pod)]
             blk = block_t.to(self.device, non_blocking=True)
             gi = torch.from_numpy(gidx).to(self.device)
             vals = blk[gi.clamp(min=0)]                       # [k, P, Wc]
             vals = torch.where((gi >= 0)[:, :, None], vals, torch.full_like(vals, float("nan")))
-            rows = torch.tensor([row for row, _, _ in grp], dtype=torch.long, device=self.device)
+            rows = torch.tensor([row for row, _, _, _ in grp], dtype=torch.long, device=self.device)
             (self.base if dst == "base" else self.win).index_copy_(0, rows, vals.reshape(len(grp), P * Wc))
+
+    async def _serve_windows(self, requests) -> List[np.ndarray]:
+        """Fetch + decode window requests of this rank's clusters (cluster-affine mode)."""
+        out = []
+        for fam, start, n, pods in requests:
+            hs = native.key_hashes([k[0] for k in pods], [k[1] for k in pods])
+            table = native.KeyTable.indexed(hs, np.arange(len(pods)), "namespace", "pod")
+            buf = np.full((len(pods), n), np.nan, dtype=np.float32)
+            reqs = []
+            for g in range(0, len(pods), self.apps_per_query * self.P):
+                part = pods[g:g + self.apps_per_query * self.P]
+                sel = (f'{fam[1]}{{namespace=~"{re_alt({k[0] for k in part})}",'
+                       f'pod=~"{re_alt({k[1] for k in part})}"}}')
+                reqs.append((range_url(fam[0], sel, start, n, self.step), start, n, 0))
+            ok = await fetch_decode(self.prom, reqs, [table] * len(reqs), buf, self.step, self.decode_threads)
+            if not all(ok):
+                log.warning("served window request %s from %d: %d queries failed", fam[1], start, ok.count(False))
+            out.append(buf)
+        return out
+
+    async def _route(self) -> None:
+        """Cluster-affine lockstep exchange of this tick's remote window requests."""
+        mine, self._remote = self._remote, []
+        vals = await self.router.exchange([(f, st, n, pods) for _dst, f, st, n, _part, pods in mine],
+                                          self._serve_windows)
+        P, Wc = self.P, self.Wc
+        for (dst, f, st, n, part, pods), v in zip(mine, vals):
+            local = {k: i for i, k in enumerate(pods)}
+            block = np.full((len(part), P, Wc), np.nan, dtype=np.float32)
+            for i, (_row, s, ps) in enumerate(part):
+                for p, pod in enumerate(ps[:P]):
+                    block[i, p, :n] = v[local[(s.namespace, pod)]]
+            rows = torch.tensor([row for row, _, _ in part], dtype=torch.long, device=self.device)
+            tgt = self.base if dst == "base" else self.win
+            if all(0 <= row < len(self.row_plan) and self.row_plan[row] is not None for row in rows.tolist()):
+                tgt.index_copy_(0, rows, torch.from_numpy(block.reshape(len(part), P * Wc)).to(self.device))
 
     def _tick_block(self, S: int, k: int):
         """NaN-filled pinned decode block of the tick, one of two kept across ticks."""
@@ -896,9 +957,16 @@ class RolloutMonitor:
         self.store.heartbeat(self.worker_id, now)
         t_new = float(np.floor(now / self.step) * self.step)
         t0 = time.perf_counter()
-        await self.history.sync(now)
-        self.timings["history_ms"] = (time.perf_counter() - t0) * 1e3
-        await self._admit(now)
+        try:
+            await self.history.sync(now)
+            self.timings["history_ms"] = (time.perf_counter() - t0) * 1e3
+            await self._admit(now)
+        except Exception:  # noqa: BLE001
+            if self.router is None:
+                raise
+            log.exception("rollout data step failed (the affine exchange still runs)")
+        if self.router is not None:
+            await self._route()  # every rank, every tick (collectives)
         self._refresh_apps()
         written: Dict[str, str] = {}
         if not self.jobs:

@@ -1,0 +1,124 @@
+"""Cluster-affine ingest (RC5 in the product): each rank scrapes only its own
+clusters' Prometheus, and the windows a job needs from another cluster cross
+ranks over the node's process group.
+
+The reference serves many clusters from one brain: every cluster runs a
+barrelman pointing at the same service (``docs/guides/design.md:21``;
+"aggregate service health check across multiple K8s clusters",
+``README.md:27``).  On a GPU node the scrape of a cluster's Prometheus is
+bound to ONE rank (network locality: each rank holds the connections and the
+decode work of its clusters), a job is owned by the rank of the cluster its
+new pods run in (history and current windows are then local), and the
+windows that live in another cluster — the baseline pods of a cross-cluster
+canary — are fetched and decoded by that cluster's rank and delivered to the
+owner in the node's lockstep tick:
+
+1. one ``all_gather`` of per-rank request counts (an int per rank, every tick);
+2. when any rank has requests: ``all_gather_object`` of the requests
+   ``(family, start, n_points, [(namespace, pod), ...])``, every rank fetches
+   and decodes the requests of its own clusters, and ONE ``all_to_all_single``
+   (RCCL over xGMI on the GPU) returns the ``[pods, n_points]`` values to the
+   requesters, in an order every rank derives from the gathered requests.
+
+Affinity: ``FOREMAST_CLUSTER_AFFINITY="<endpoint>=<rank>,..."`` or a stable
+hash of the endpoint over the ranks.
+"""
+
+from __future__ import annotations
+
+import os
+import zlib
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import comm
+
+Request = Tuple[Tuple[str, str], float, int, List[Tuple[str, str]]]  # (family, start, n, pods)
+
+
+def affinity_from_env() -> Callable[[str, int], int]:
+    spec = os.environ.get("FOREMAST_CLUSTER_AFFINITY", "")
+    table: Dict[str, int] = {}
+    for part in spec.split(","):
+        if "=" in part:
+            ep, r = part.rsplit("=", 1)
+            table[ep.strip()] = int(r)
+
+    def rank_of(endpoint: str, world: int) -> int:
+        if endpoint in table:
+            return table[endpoint] % max(world, 1)  # a mapped rank that left: the survivors share it
+        return zlib.crc32(endpoint.encode()) % max(world, 1)
+    return rank_of
+
+
+class ClusterRouter:
+    def __init__(self, rank_of: Callable[[str, int], int], device, group=None,
+                 timeout_s: Optional[float] = None) -> None:
+        self.rank_of = rank_of
+        self.device = torch.device(device)
+        self.group = group
+        self.timeout_s = comm.exchange_timeout_s() if timeout_s is None else float(timeout_s)
+        self.exchanges = 0
+        self.values_moved = 0
+
+    @property
+    def rank(self) -> int:
+        return dist.get_rank(self.group) if comm.active(self.group) else 0
+
+    @property
+    def world(self) -> int:
+        return dist.get_world_size(self.group) if comm.active(self.group) else 1
+
+    def local(self, endpoint: str) -> bool:
+        return self.rank_of(endpoint, self.world) == self.rank
+
+    async def exchange(self, mine: Sequence[Request], serve) -> List[np.ndarray]:
+        """Lockstep (every rank calls it once per tick).  ``mine``: this rank's
+        requests for windows of other ranks' clusters; ``serve(requests) ->
+        [values [pods, n]]`` fetches and decodes requests of this rank's own
+        clusters (awaitable).  Returns the values of ``mine``, in order."""
+        world, rank = self.world, self.rank
+        if world <= 1:
+            return list(await serve(list(mine))) if mine else []
+        cnt = torch.tensor([len(mine)], dtype=torch.int64, device=self.device)
+        counts = torch.empty(world, dtype=torch.int64, device=self.device)
+        work = dist.all_gather_into_tensor(counts, cnt, group=self.group, async_op=True)
+        comm.wait_bounded(work, self.timeout_s, "affine request counts")
+        if int(counts.sum()) == 0:
+            return []
+        gathered: List[Optional[List[Request]]] = [None] * world
+        dist.all_gather_object(gathered, list(mine), group=self.group)
+        self.exchanges += 1
+        # every rank derives the same order: requester q's requests by index, routed to the
+        # rank whose cluster serves the family
+        served_by = [[self.rank_of(req[0][0], world) for req in (gathered[q] or [])] for q in range(world)]
+        to_serve = [(q, i, req) for q in range(world) for i, req in enumerate(gathered[q] or [])
+                    if served_by[q][i] == rank]
+        values = await serve([req for _, _, req in to_serve]) if to_serve else []
+        send_parts: List[List[np.ndarray]] = [[] for _ in range(world)]
+        for (q, _i, req), v in zip(to_serve, values):
+            send_parts[q].append(np.asarray(v, dtype=np.float32).reshape(len(req[3]), req[2]))
+        send_sizes = [sum(p.size for p in parts) for parts in send_parts]
+        recv_sizes = [sum(len(req[3]) * req[2] for i, req in enumerate(mine) if served_by[rank][i] == a)
+                      for a in range(world)]
+        send = np.concatenate([p.reshape(-1) for parts in send_parts for p in parts]) if sum(send_sizes) else \
+            np.zeros(0, dtype=np.float32)
+        send_t = torch.from_numpy(send).to(self.device)
+        recv_t = torch.empty(sum(recv_sizes), dtype=torch.float32, device=self.device)
+        work = dist.all_to_all_single(recv_t, send_t, output_split_sizes=recv_sizes, input_split_sizes=send_sizes,
+                                      group=self.group, async_op=True)
+        comm.wait_bounded(work, self.timeout_s, "affine window all-to-all")
+        self.values_moved += int(recv_t.numel())
+        recv = recv_t.cpu().numpy()
+        offs = np.concatenate([[0], np.cumsum(recv_sizes)])
+        out: List[Optional[np.ndarray]] = [None] * len(mine)
+        pos = {a: int(offs[a]) for a in range(world)}
+        for i, req in enumerate(mine):  # rank a's part holds my requests to a, in index order
+            a = served_by[rank][i]
+            sz = len(req[3]) * req[2]
+            out[i] = recv[pos[a]:pos[a] + sz].reshape(len(req[3]), req[2])
+            pos[a] += sz
+        return out  # type: ignore[return-value]
