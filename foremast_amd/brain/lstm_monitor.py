@@ -98,6 +98,12 @@ class LstmMonitor:
         if fp8 is None:
             fp8 = os.environ.get("FOREMAST_LSTM_FP8", "0") not in ("0", "", "false")
         tb = train_batch if self.gpu else min(train_batch, 64)
+        if self.gpu:  # the fused MFMA kernels are built for one hidden size
+            from ..ops.lstm import H as KERNEL_H
+            if (hidden or self.cfg.lstm_hidden) != KERNEL_H:
+                log.warning("LSTM hidden size %s -> %d (the fused GPU kernels' size)", hidden or self.cfg.lstm_hidden,
+                            KERNEL_H)
+            hidden = KERNEL_H
         self.shard = LstmShard(max(1, min_capacity), R, self.F, window=window or self.cfg.lstm_window,
                                hidden=hidden or self.cfg.lstm_hidden, fp8=bool(fp8) and self.gpu,
                                device=self.device, threshold=self.cfg.lstm_threshold, train_batch=tb, seed=seed,

@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import asyncio
 import datetime
+import gc
 import logging
 import os
 import signal
@@ -85,6 +86,8 @@ class NodeBrain:
         self.publish_every_s = float(os.environ.get("FOREMAST_PUBLISH_EVERY_S", "10"))
         self._published = -1e18
         self._last_anomalous = None
+        self.gc_freeze_min = int(os.environ.get("FOREMAST_GC_FREEZE_MIN", "256"))
+        self._frozen_at = 0
         for m in self.monitors:
             m.owns = self._owns_for(m)
 
@@ -145,6 +148,20 @@ class NodeBrain:
                 info["lstm_model"] = m.model_digest()
         return self.health.exchange(names, counts, version, n_live, info)
 
+    def _freeze_admitted(self) -> None:
+        """Admission builds long-lived per-job state (plans, slot maps, entities):
+        after a large intake, one full collection, then ``gc.freeze()`` moves
+        everything alive into the permanent generation, so the periodic gen-2
+        collections of the steady ticks no longer walk the admitted jobs' objects
+        (a 100+ ms pause in a ~9 ms tick at 10k jobs otherwise)."""
+        n = sum(len(getattr(m, "jobs", ())) for m in self.monitors)
+        if n - self._frozen_at >= self.gc_freeze_min:
+            gc.collect()
+            gc.freeze()
+            self._frozen_at = n
+        elif n < self._frozen_at:
+            self._frozen_at = n  # jobs finished: the next intake of the same size freezes again
+
     async def tick(self) -> Dict:
         for m in self.monitors:
             m.sync(steal_from=self.dead or None)
@@ -152,6 +169,7 @@ class NodeBrain:
                 await m.tick()
             except Exception as e:  # noqa: BLE001 - a scoring failure must not desynchronise the collectives
                 log.exception("%s tick failed: %s", type(m).__name__, e)
+        self._freeze_admitted()
         if self.world is None:
             table = self._exchange()
         else:

@@ -141,8 +141,8 @@ def _node(tmp_path, nproc, extra_env, apps, bad):
            for a in apps}
     env = dict(os.environ, FOREMAST_RING_LEN="2880", FOREMAST_HEARTBEAT_S="5", OMP_NUM_THREADS="1",
                ML_ALGORITHM="lstm", ML_LSTM_THRESHOLD="4", FOREMAST_LSTM_WINDOW="16", FOREMAST_LSTM_HIDDEN="16",
-               FOREMAST_LSTM_PRETRAIN="20", FOREMAST_PUBLISH_EVERY_S="0", HSA_ENABLE_IPC_MODE_LEGACY="0",
-               **extra_env)
+               FOREMAST_LSTM_PRETRAIN="20", FOREMAST_PUBLISH_EVERY_S="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.update(extra_env)
     env.pop("WORLD_SIZE", None)
     cmd = [sys.executable, "-m", "foremast_amd.brain", "--streaming", "--nproc", str(nproc), "--store",
            f"sqlite://{db}", "--metrics-port", "0", "--tick-seconds", "1", "--window", "5"]
@@ -200,7 +200,9 @@ def test_lstm_node_gpu_forced_collectives(tmp_path):
     """The same path on the GPU: one rank, RCCL group, collectives forced
     (gradient all-reduce + node exchange as with 8 ranks)."""
     apps = [f"app{i}" for i in range(6)]
-    store, ids, proc, server, log_path = _node(tmp_path, 1, {"FOREMAST_FORCE_COLLECTIVES": "1"}, apps, bad="app3")
+    store, ids, proc, server, log_path = _node(tmp_path, 1, {"FOREMAST_FORCE_COLLECTIVES": "1",
+                                                            "FOREMAST_LSTM_WINDOW": "32", "FOREMAST_LSTM_HIDDEN": "64"},
+                                               apps, bad="app3")
     try:
         t_end = time.time() + 150
         t = {}
