@@ -772,6 +772,7 @@ def main():
     scored_rows = meta.pop("_scored_rows", None)   # node: rows actually scored per tick
     node_finish = meta.pop("_finish", None)
     node_roll = meta.pop("_roll", None)
+    node_breakdowns = meta.pop("_breakdowns", None)
     for k in [k for k in meta if k.startswith("_")]:
         meta.pop(k)
     if truth is not None and world > 1:
@@ -881,6 +882,7 @@ def main():
             res["decode_ms_last_tick"] = round(decoder.last_decode_ms, 3)
         if timed_rows is not None:
             res["node"] = {"series_scored_timed": int(timed_rows), "tick_breakdown_ms_last": tick_breakdown,
+                           "tick_breakdown_ms": (node_breakdowns or [])[-args.steps:],
                            "tick_ms": [round(float(x), 2) for x in lat_ms.tolist()],
                            "completion_tick_s": round(fin_s, 3), "job_statuses_rank0": statuses}
         if args.config == "canary" and args.refit_every > 1:

@@ -245,6 +245,7 @@ def setup_node(args, world, rank, dev):
     health = torch.zeros((n_apps, 2), dtype=torch.int32)
     health[mine, 1] = 1
     scored: List[int] = []
+    breakdowns: List[Dict[str, float]] = []
 
     def tick(k):
         clock["t"] = T0 + STEP * (k + 1)
@@ -253,6 +254,7 @@ def setup_node(args, world, rank, dev):
         if dev.type == "cuda":
             torch.cuda.synchronize()
         scored.append(n_rows)
+        breakdowns.append({k: round(v, 2) for k, v in roll.timings.items() if k != "admit_ms"})
         for a in table["anomalous_apps"]:
             flagged.add(int(a.split("/app")[1]))
         return table
@@ -292,6 +294,7 @@ def setup_node(args, world, rank, dev):
         "intake_s": round(intake_s, 3),
         "intake_breakdown_ms": {k: round(v, 2) for k, v in intake_timings.items()},
         "_scored_rows": scored,
+        "_breakdowns": breakdowns,
         "_finish": finish,
         "_roll": roll,
         "_server": server,

@@ -57,6 +57,10 @@ struct DecompArgs {
   float* sigma;       // [N] residual RMS or null
   float* nvalid;      // [N] valid samples or null
   DetectArgs det;
+  int* defer;         // scoring fast path: [1 + N] count + series the general kernel finishes, or null
+  float* sfc;         // fast path, split epilogue: [N, hmax] seasonal term of horizons 1..hmax, or null
+  int hmax;           // (sfc) every horizon is in 1..hmax <= 64
+  int _pad;
 };
 
 extern __shared__ __attribute__((aligned(16))) char fm_dec_smem[];
@@ -116,8 +120,7 @@ __host__ __device__ __forceinline__ int dec_blocks(int T) { return ((T + BLOCK -
 // EXACT: the launch guarantees ceil(T / BLOCK) == KT, so every item but the last is
 // in range at compile time (fewer per-item scalar guards and SGPR pairs live)
 template <typename TIN, int KT, bool EXACT>
-__global__ __launch_bounds__(BLOCK, KT <= kItemsWeek ? 8 : 4) void decompose_kernel(const DecompArgs a) {
-  const int n = blockIdx.x;
+__device__ __forceinline__ void decompose_series(const DecompArgs& a, const int n) {
   const TIN* row = (const TIN*)a.hist + (long long)n * a.ld;
   const int T = a.T, m = a.m, tid = threadIdx.x, lane = lane_id(), w = wave_id();
   const int NB = dec_blocks(T);
@@ -370,7 +373,370 @@ __global__ __launch_bounds__(BLOCK, KT <= kItemsWeek ? 8 : 4) void decompose_ker
   });
 }
 
+template <typename TIN, int KT, bool EXACT>
+__global__ __launch_bounds__(BLOCK, KT <= kItemsWeek ? 8 : 4) void decompose_kernel(const DecompArgs a) {
+  decompose_series<TIN, KT, EXACT>(a, blockIdx.x);
+}
+
+// out of line: inlined into the loop below, LLVM hoists every per-item invariant out of it
+// and spills hundreds of registers
+template <typename TIN, int KT, bool EXACT>
+__device__ __attribute__((noinline)) void decompose_series_call(const DecompArgs& a, int n) {
+  decompose_series<TIN, KT, EXACT>(a, n);
+}
+
+// the series the scoring fast path deferred (a gap or a non-finite value in the window):
+// a grid-stride loop over the device-side list (the count is only known on the device).
+// Every wave runs every iteration (the early returns above are per call), and nothing in a
+// call writes LDS before its first workgroup barrier, so calls follow each other safely.
+template <typename TIN, int KT, bool EXACT>
+__global__ __launch_bounds__(BLOCK, 4) void decompose_deferred_kernel(const DecompArgs a) {
+  const int cnt = min(a.defer[0], a.N);
+  for (int q = blockIdx.x; q < cnt; q += gridDim.x) {
+    decompose_series_call<TIN, KT, EXACT>(a, a.defer[1 + q]);
+    __syncthreads();
+  }
+}
+
+// ---- scoring fast path: one streaming pass ------------------------------------------
+// ML_ALGORITHM=seasonal_decompose scores with the forecast, the residual RMS and the band;
+// none of the [N, T] outputs.  For a gap-free window with an even period (m % 16 == 0) the
+// whole decomposition collapses to:
+//  * P = inclusive prefix of y - y0 (8 consecutive samples per lane from one 16-byte load,
+//    in-lane prefix, one DPP wave scan per 8 samples, block offsets), written once to LDS;
+//  * D_t = y_t - trend_t = (P[t] - P[t-1]) - (d[t-1] + d[t]) / 2m with d[j] = P[j+h] - P[j-h]
+//    (the 2 x m centred window as two prefix differences), 8 samples of a lane at once:
+//    D_i = g_i - e_{i-1} with g = P - d/2m, e = P + d/2m (packed FP32; e_{-1} is the
+//    neighbour lane's e_7, one DPP move — no strided LDS reads);
+//  * per phase p (consecutive lanes, conflict-free): the mean pm_p of D over the periods with
+//    a centred trend and W_p = sum (D - pm_p)^2.  With the seasonal s_p = pm_p - pmean the
+//    residual sum of squares is sum_p W_p + pmean^2 * count (the cross term vanishes), so no
+//    residual pass and no cancellation.  The 7-day / daily geometry (T = 7 m, m = 1440) is
+//    compiled with its period: every phase has exactly 6 centred periods at immediate offsets.
+// Persistent workgroups (3 per CU, the LDS bound) walk the series with a stride of the grid
+// and issue the next series' loads before working on the current one, so HBM latency hides
+// under the LDS passes.  With a host-known horizon bound the band / verdict runs in its own
+// kernel (decompose_detect_kernel) from the seasonal terms left here, off this loop's
+// critical path.  A window with a NaN/Inf has a non-finite prefix total: its series is
+// appended to `defer` and the general kernel above finishes it (identical semantics, gaps
+// included).  The ring head moves one column per tick: t' = t + (head mod 8) keeps every
+// 8-group of samples one aligned vector load (the columns outside the window are zeros).
+constexpr int SB = 448;             // threads per workgroup (7 waves: 3 x 3,584 samples cover 7 days)
+constexpr int SNW = SB / FM_WAVE;
+constexpr int SE = 8;               // consecutive samples per lane and item
+constexpr int S_MAX_ITEMS = 5;      // T + 14 <= 17,920
+constexpr int S_WG_PER_CU = 3;      // 49 KiB of LDS per workgroup at T = 10,080
+
+struct v8f { v4f lo, hi; };
+
+template <typename TIN> struct Raw8;  // the raw bits of 8 consecutive samples
+template <> struct Raw8<bf16_t> {
+  uint4 u;
+  __device__ __forceinline__ void load(const bf16_t* p) { u = *(const uint4*)p; }
+  __device__ __forceinline__ void zero() { u = make_uint4(0u, 0u, 0u, 0u); }
+  __device__ __forceinline__ v8f get() const {
+    v8f r;
+    r.lo = v4f{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+               __uint_as_float(u.y & 0xffff0000u)};
+    r.hi = v4f{__uint_as_float(u.z << 16), __uint_as_float(u.z & 0xffff0000u), __uint_as_float(u.w << 16),
+               __uint_as_float(u.w & 0xffff0000u)};
+    return r;
+  }
+};
+template <> struct Raw8<float> {
+  v4f a, b;
+  __device__ __forceinline__ void load(const float* p) { a = *(const v4f*)p; b = *(const v4f*)(p + 4); }
+  __device__ __forceinline__ void zero() { a = b = v4f{0.f, 0.f, 0.f, 0.f}; }
+  __device__ __forceinline__ v8f get() const { return v8f{a, b}; }
+};
+
+// items per thread of the instantiated kernel (1..5) for a window of T samples
+__host__ __device__ __forceinline__ int score_items(int T) { return (T + 14 + SB * SE - 1) / (SB * SE); }
+
+// the kernel arguments in the constant address space: reads are scalar loads (a generic
+// pointer would turn them into flat loads whose waits also drain the prefetched samples)
+typedef const __attribute__((address_space(4))) DecompArgs* KArgs;
+
+// the detection arguments as a register value (word-wise scalar loads from the kernarg segment)
+__device__ __forceinline__ DetectArgs kdet(KArgs a) {
+  static_assert(sizeof(DetectArgs) % 4 == 0, "word copy");
+  DetectArgs d;
+  const __attribute__((address_space(4))) int* src = (const __attribute__((address_space(4))) int*)&a->det;
+  int* dst = (int*)&d;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(DetectArgs) / 4); ++i) dst[i] = src[i];
+  return d;
+}
+
+// y0: the raw first sample, converted only when the series is worked on (converting it here
+// would wait for the load, and with it for every prefetched sample)
+template <typename TIN, int KT>
+__device__ __forceinline__ void score_issue(KArgs a, int n, Raw8<TIN>* raw, TIN& y0) {
+  const TIN* row = (const TIN*)a->hist + (long long)n * a->ld;
+  const int head = a->head, phi = head & 7, TP = a->T + phi, col0 = head - phi, R = a->ring_len;
+  y0 = row[head];
+#pragma unroll
+  for (int k = 0; k < KT; ++k) {
+    const int tg = (threadIdx.x + k * SB) * SE;
+    raw[k].zero();
+    if (tg < TP) {
+      int c = col0 + tg;
+      c -= (c >= R) ? R : 0;
+      raw[k].load(row + c);
+    }
+  }
+}
+
+__device__ __forceinline__ float wave_shr1(float old, float v) {  // lane l <- lane l-1 (lane 0: old)
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+
+// M > 0: the compiled geometry T = 7 M (host-checked); M = 0: any period with m % 16 == 0
+// (the general-period variants need more registers: two workgroups per CU)
+template <typename TIN, int KT, int M>
+__global__ __launch_bounds__(SB, M > 0 ? 6 : 4) void decompose_score_kernel(const DecompArgs a0) {
+  const KArgs a0p = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
+  const int T = a0.T, m = M > 0 ? M : a0.m, h = m >> 1;
+  const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+  const int phi = a0.head & 7, TP = T + phi;
+  float* P = (float*)fm_dec_smem + 4;  // [-4, KT SB SE): inclusive prefix of y - y0, then D
+  float* pmv = P + KT * SB * SE;       // [m] phase means
+  float* red = pmv + m;                // [4 SNW] reductions, [4 SNW] prefix total
+  float* bsum = red + 8 * SNW;         // [KT SNW] wave totals, then their exclusive offsets
+  const float cm = 0.5f / (float)m;
+  const int te = T - 1 - h;
+  const int lo = h, hi = (te + phi) & ~7;
+  if (tid < 4) P[tid - 4] = 0.f;
+
+  Raw8<TIN> nxt[KT];
+  TIN y0n = 0;
+  int n = blockIdx.x;
+  if (n < a0.N) score_issue<TIN, KT>(a0p, n, nxt, y0n);
+  for (; n < a0.N; n += gridDim.x) {
+    // the arguments are re-read from the kernarg segment where they are used (scalar loads):
+    // hoisted out of the loop they hold ~100 SGPRs live across it and spill
+    KArgs a = a0p;
+    asm volatile("" : "+s"(a));
+    // lane-derived addresses are recomputed per series (hoisted, ~20 VGPRs live across the
+    // loop spill, and a spill reload's wait drains the prefetched samples)
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    Raw8<TIN> raw[KT];
+#pragma unroll
+    for (int k = 0; k < KT; ++k) raw[k] = nxt[k];
+    const float y0 = to_f32<TIN>(y0n);
+    if (n + (int)gridDim.x < a->N) score_issue<TIN, KT>(a, n + gridDim.x, nxt, y0n);  // block-uniform
+
+    // 1. prefix: in-lane inclusive over 8 samples, DPP wave scan of the lane totals, written
+    //    to LDS at once (the wave offsets are added in place after the block scan)
+#pragma unroll
+    for (int k = 0; k < KT; ++k) {
+      const int tg = (tid + k * SB) * SE;
+      v8f q = raw[k].get();
+      q.lo -= y0;
+      q.hi -= y0;
+      if (tg < phi || tg + SE > TP) {  // the window's edge groups: columns outside it are 0
+        float e[8] = {q.lo.x, q.lo.y, q.lo.z, q.lo.w, q.hi.x, q.hi.y, q.hi.z, q.hi.w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) e[i] = (tg + i >= phi && tg + i < TP) ? e[i] : 0.f;
+        q.lo = v4f{e[0], e[1], e[2], e[3]};
+        q.hi = v4f{e[4], e[5], e[6], e[7]};
+      }
+      q.lo.y += q.lo.x;
+      q.lo.z += q.lo.y;
+      q.lo.w += q.lo.z;
+      q.hi.x += q.lo.w;
+      q.hi.y += q.hi.x;
+      q.hi.z += q.hi.y;
+      q.hi.w += q.hi.z;
+      const float inc = wave_inclusive_scan(q.hi.w);
+      const float ex = inc - q.hi.w;
+      *(v4f*)(P + tg) = q.lo + ex;
+      *(v4f*)(P + tg + 4) = q.hi + ex;
+      if (lane == FM_WAVE - 1) bsum[k * SNW + w] = inc;
+    }
+    __syncthreads();
+    if (w == 0) {
+      const float b = lane < KT * SNW ? bsum[lane] : 0.f;
+      const float inc = wave_inclusive_scan(b);
+      if (lane < KT * SNW) bsum[lane] = inc - b;
+      if (lane == KT * SNW - 1) red[4 * SNW] = inc;
+    }
+    __syncthreads();
+    const float total = red[4 * SNW];
+    if (!__builtin_isfinite(total)) {  // block-uniform: a gap or a non-finite sample
+      if (tid == 0) {
+        const int q = atomicAdd(a->defer, 1);
+        if (q < a->N) a->defer[1 + q] = n;
+        if (a->sfc) a->sfc[(long long)n * a->hmax] = fm_nan();  // the detect kernel skips it
+      }
+      continue;
+    }
+#pragma unroll
+    for (int k = 0; k < KT; ++k) {
+      const int tg = (tid + k * SB) * SE;
+      const float o = bsum[k * SNW + w];
+      *(v4f*)(P + tg) += o;
+      *(v4f*)(P + tg + 4) += o;
+    }
+    __syncthreads();
+
+    // 2. detrended samples in registers; the groups without a centred trend read a clamped
+    //    (in-range) position and are never used.  D_i = (P_i - P_{i-1}) - (d_i + d_{i-1}) / 2m:
+    //    P_{-1} and d_{-1} come from the previous lane (its group is the adjacent one) except
+    //    in lane 0 and at the lower clamp, which read them.
+    v8f D[KT];
+#pragma unroll
+    for (int k = 0; k < KT; ++k) {
+      const int tg = (tid + k * SB) * SE;
+      const int tc = min(max(tg, lo), hi);
+      const v4f y0v = *(const v4f*)(P + tg), y1v = *(const v4f*)(P + tg + 4);
+      v4f d0 = *(const v4f*)(P + tc + h), d1 = *(const v4f*)(P + tc + h + 4);
+      d0 -= *(const v4f*)(P + tc - h);
+      d1 -= *(const v4f*)(P + tc - h + 4);
+      const bool own = lane == 0 || tg <= lo;
+      float ym = 0.f, dm = 0.f;
+      if (own) {
+        ym = P[tg - 1];
+        dm = P[tc + h - 1] - P[tc - h - 1];
+      }
+      const float ysh = wave_shr1(ym, y1v.w), dsh = wave_shr1(dm, d1.w);
+      ym = own ? ym : ysh;
+      dm = own ? dm : dsh;
+      D[k].lo = (y0v - v4f{ym, y0v.x, y0v.y, y0v.z}) - cm * (d0 + v4f{dm, d0.x, d0.y, d0.z});
+      D[k].hi = (y1v - v4f{y0v.w, y1v.x, y1v.y, y1v.z}) - cm * (d1 + v4f{d0.w, d1.x, d1.y, d1.z});
+      // the item is finished before the next one's LDS reads issue (all in flight: spills)
+      asm volatile("" : "+v"(D[k].lo), "+v"(D[k].hi)::"memory");
+    }
+    // the forecast's trend anchors: the last centred trend and the one a season earlier
+    float tr_e = 0.f, tr_p = 0.f;
+    if (w == 0) {
+      auto trend_at = [&](int t) {
+        const int u = t + phi;
+        return y0 + cm * ((P[u + h - 1] + P[u + h]) - (P[u - h - 1] + P[u - h]));
+      };
+      tr_e = trend_at(te);
+      tr_p = trend_at(te - m);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < KT; ++k) {
+      const int tg = (tid + k * SB) * SE;
+      if (tg < TP) {
+        *(v4f*)(P + tg) = D[k].lo;
+        *(v4f*)(P + tg + 4) = D[k].hi;
+      }
+    }
+    __syncthreads();
+
+    // 3. per phase: mean over the periods with a centred trend, squared deviations from it
+    float spm = 0.f, sw = 0.f, sc = 0.f;
+    if constexpr (M > 0) {  // T = 7 M: periods 1..6 for p < h, 0..5 otherwise — 6 at immediate offsets
+      constexpr float inv6 = 1.f / 6.f;
+      constexpr int NP = M > 0 ? (M + SB - 1) / SB : 1;
+#pragma unroll
+      for (int j = 0; j < NP; ++j) {
+        const int p = tid + j * SB;
+        if (j * SB + SB <= M || p < M) {
+          const float* d = P + p + phi + (p < h ? M : 0);
+          float v6[6];
+#pragma unroll
+          for (int k = 0; k < 6; ++k) v6[k] = d[k * M];
+          const float pm = (((v6[0] + v6[1]) + (v6[2] + v6[3])) + (v6[4] + v6[5])) * inv6;
+          float ww = 0.f;
+#pragma unroll
+          for (int k = 0; k < 6; ++k) {
+            const float e = v6[k] - pm;
+            ww += e * e;
+          }
+          pmv[p] = pm;
+          spm += pm;
+          sw += ww;
+        }
+      }
+      sc = (float)(6 * (M / SB) + (tid < M % SB ? 6 : 0));
+    } else {
+      for (int p = tid; p < m; p += SB) {
+        const int k0 = p < h ? 1 : 0, k1 = (te - p) / m;
+        const float* d = P + p + phi;
+        float s = 0.f;
+        for (int k = k0; k <= k1; ++k) s += d[k * m];
+        const float cnt = (float)(k1 - k0 + 1);
+        const float pm = s * __builtin_amdgcn_rcpf(cnt);
+        float ww = 0.f;
+        for (int k = k0; k <= k1; ++k) {
+          const float e = d[k * m] - pm;
+          ww += e * e;
+        }
+        pmv[p] = pm;
+        spm += pm;
+        sw += ww;
+        sc += cnt;
+      }
+    }
+    spm = wave_sum(spm);
+    sw = wave_sum(sw);
+    sc = wave_sum(sc);
+    if (lane == 0) { red[w] = spm; red[SNW + w] = sw; red[2 * SNW + w] = sc; }
+    __syncthreads();
+    float tpm = 0.f, tw = 0.f, tcnt = 0.f;
+#pragma unroll
+    for (int i = 0; i < SNW; ++i) { tpm += red[i]; tw += red[SNW + i]; tcnt += red[2 * SNW + i]; }
+    const float pmean = tpm / (float)m;
+    const float rss = tw + pmean * pmean * tcnt;
+    if (a->phase_means)
+      for (int p = tid; p < m; p += SB) a->phase_means[(long long)n * m + p] = pmv[p] - pmean;
+
+    // 4. forecast parameters, spread, band / verdict (wave 0; the other waves go on to the
+    //    next series, whose first LDS writes cannot touch pmv before wave 0 has joined them).
+    //    Split epilogue (sfc): only the seasonal terms of horizons 1..hmax leave here.
+    if (w == 0) {
+      const float Ks = fmaxf((float)(T - 2 * h) / (float)m, 1.5f);
+      const float sig = sqrtf(rss / fmaxf(tcnt, 1.f)) * sqrtf((Ks + 1.f) / (Ks - 1.f));
+      const float slope = (tr_e - tr_p) / (float)m;
+      if (lane == 0) {
+        if (a->fc_level) a->fc_level[n] = tr_e;
+        if (a->fc_slope) a->fc_slope[n] = slope;
+        if (a->sigma) a->sigma[n] = sig;
+        if (a->nvalid) a->nvalid[n] = (float)T;
+      }
+      const int tlast = T - 1;
+      if (a->sfc) {
+        if (lane < a->hmax) a->sfc[(long long)n * a->hmax + lane] = pmv[(tlast + 1 + lane) % m] - pmean;
+        continue;
+      }
+      const DetectArgs det = kdet(a);
+      detect_epilogue_wave(det, n, sig, (float)T, [&](int hz) {
+        int p = (tlast + hz) % m;
+        p += p < 0 ? m : 0;
+        return tr_e + slope * (float)(tlast + hz - te) + (pmv[p] - pmean);
+      });
+    }
+  }
+}
+
+// split epilogue of the fast path: one wave per series, the band / verdict from the forecast
+// parameters and the seasonal terms the score kernel left (deferred series: NaN marker,
+// the general kernel has done their epilogue)
+__global__ __launch_bounds__(256) void decompose_detect_kernel(const DecompArgs a) {
+  const int n = blockIdx.x * (blockDim.x / FM_WAVE) + wave_id();
+  if (n >= a.N) return;  // wave-uniform
+  const float* sf = a.sfc + (long long)n * a.hmax;
+  const float s0 = sf[0];
+  if (s0 != s0) return;
+  const float lvl = a.fc_level[n], slope = a.fc_slope[n], sig = a.sigma[n], nv = a.nvalid[n];
+  const int h = a.m >> 1, hm = a.hmax;
+  detect_epilogue_wave(a.det, n, sig, nv, [&](int hz) {
+    const int i = min(max(hz, 1), hm) - 1;  // the host guarantees 1 <= hz <= hmax
+    return lvl + slope * (float)(h + hz) + sf[i];
+  });
+}
+
 }  // namespace
+
+extern "C" size_t fm_decompose_score_lds_bytes(int T, int m) {
+  return ((size_t)4 + (size_t)score_items(T) * SB * SE + m + 8 * SNW + (size_t)score_items(T) * SNW) * sizeof(float);
+}
 
 extern "C" size_t fm_decompose_lds_bytes(int T, int m) {
   const size_t nb = (size_t)dec_blocks(T);
@@ -386,11 +752,48 @@ extern "C" int fm_seasonal_decompose(const DecompArgs* a, hipStream_t st) {
     return (int)hipErrorInvalidValue;
   const size_t lds = fm_decompose_lds_bytes(a->T, a->m);
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  const int ks = score_items(a->T);
+  const bool fast = a->defer && !a->trend && !a->seasonal && !a->resid && a->m % 16 == 0 && a->T >= 2 * a->m + 1 &&
+                    a->ring_len % 8 == 0 && a->ld % 8 == 0 && (((unsigned long long)a->hist) & 15ull) == 0 &&
+                    ks <= S_MAX_ITEMS && fm_decompose_score_lds_bytes(a->T, a->m) <= 160 * 1024 &&
+                    (!a->sfc || (a->hmax >= 1 && a->hmax <= FM_WAVE));
+  if (fast) {
+    hipError_t e = hipMemsetAsync(a->defer, 0, sizeof(int), st);
+    if (e != hipSuccess) return (int)e;
+    const size_t slds = fm_decompose_score_lds_bytes(a->T, a->m);
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
+    }
+    const bool day7 = a->m == 1440 && a->T == 7 * 1440;
+    const int wgs = cus * (day7 ? S_WG_PER_CU : 2);
+    const int sgrid = a->N < wgs ? a->N : wgs;
+#define FM_DEC_SCORE(TIN, KT, M) \
+    hipLaunchKernelGGL((decompose_score_kernel<TIN, KT, M>), dim3(sgrid), dim3(SB), slds, st, *a)
+#define FM_DEC_SCORE_T(TIN)                                                                       \
+    if (day7) FM_DEC_SCORE(TIN, 3, 1440);                                                         \
+    else switch (ks) { case 1: FM_DEC_SCORE(TIN, 1, 0); break; case 2: FM_DEC_SCORE(TIN, 2, 0); break; \
+                       case 3: FM_DEC_SCORE(TIN, 3, 0); break; case 4: FM_DEC_SCORE(TIN, 4, 0); break; \
+                       default: FM_DEC_SCORE(TIN, 5, 0); break; }
+    if (a->bf16) { FM_DEC_SCORE_T(bf16_t) } else { FM_DEC_SCORE_T(float) }
+#undef FM_DEC_SCORE_T
+#undef FM_DEC_SCORE
+    e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
   // register-resident items: 20 per thread covers a 7-day window of 60 s points (10,080)
   const int kt = (a->T + BLOCK - 1) / BLOCK;
   const bool small = kt <= kItemsWeek;
-#define FM_DEC_LAUNCH(TIN, KT, EX) \
-  hipLaunchKernelGGL((decompose_kernel<TIN, KT, EX>), dim3(a->N), dim3(BLOCK), lds, st, *a)
+  // fast path: the general kernel only finishes the deferred series (grid-stride over the list)
+  const int grid = fast ? (a->N < 256 ? a->N : 256) : a->N;
+#define FM_DEC_LAUNCH(TIN, KT, EX)                                                                          \
+  do {                                                                                                      \
+    if (fast) hipLaunchKernelGGL((decompose_deferred_kernel<TIN, KT, EX>), dim3(grid), dim3(BLOCK), lds, st, *a); \
+    else hipLaunchKernelGGL((decompose_kernel<TIN, KT, EX>), dim3(grid), dim3(BLOCK), lds, st, *a);         \
+  } while (0)
   if (a->bf16) {
     if (kt == kItemsWeek) FM_DEC_LAUNCH(bf16_t, kItemsWeek, true);
     else if (small) FM_DEC_LAUNCH(bf16_t, kItemsWeek, false);
@@ -401,5 +804,10 @@ extern "C" int fm_seasonal_decompose(const DecompArgs* a, hipStream_t st) {
     else FM_DEC_LAUNCH(float, MAX_ITEMS, false);
   }
 #undef FM_DEC_LAUNCH
+  if (fast && a->sfc && a->det.C > 0) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(decompose_detect_kernel, dim3((a->N + 3) / 4), dim3(256), 0, st, *a);
+  }
   return (int)hipGetLastError();
 }

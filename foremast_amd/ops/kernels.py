@@ -780,7 +780,8 @@ class DecompArgs(C.Structure):
                 ("T", C.c_int), ("N", C.c_int), ("m", C.c_int), ("bf16", C.c_int),
                 ("trend", C.c_void_p), ("seasonal", C.c_void_p), ("resid", C.c_void_p),
                 ("phase_means", C.c_void_p), ("fc_level", C.c_void_p), ("fc_slope", C.c_void_p),
-                ("sigma", C.c_void_p), ("nvalid", C.c_void_p), ("det", nat.DetectArgs)]
+                ("sigma", C.c_void_p), ("nvalid", C.c_void_p), ("det", nat.DetectArgs), ("defer", C.c_void_p),
+                ("sfc", C.c_void_p), ("hmax", C.c_int), ("_pad", C.c_int)]
 
 
 nat.register("fm_seasonal_decompose", [C.POINTER(DecompArgs), C.c_void_p])
@@ -818,11 +819,16 @@ def seasonal_decompose(hist: torch.Tensor, head: int, length: int, m: int, want=
 
 
 def decompose_score(hist: torch.Tensor, head: int, length: int, m: int, det: DetectSpec,
-                    out: Optional[Dict[str, torch.Tensor]] = None) -> Dict[str, torch.Tensor]:
+                    out: Optional[Dict[str, torch.Tensor]] = None,
+                    phase_means: bool = False) -> Dict[str, torch.Tensor]:
     """Seasonal-decomposition scorer (``ML_ALGORITHM=seasonal_decompose``): K4 over
     the ring window without the ``[N, T]`` outputs, forecast = extrapolated trend +
     phase mean, sigma = residual RMS, then the fused band / verdict epilogue
-    (models/decompose.py ``decompose_forecast``)."""
+    (models/decompose.py ``decompose_forecast``).  An even period (``m % 8 == 0``) on an
+    aligned ring takes the single-pass kernel (gap-free series; a series with a gap
+    is finished by the general kernel from a device-side list).  ``phase_means``:
+    also write the centred ``[N, m]`` phase means (576 MB at 100k x 1440 — off for
+    scoring)."""
     lib = nat.require()
     _hist_check(hist, head, length)
     _need(2 <= m and 2 * m + 1 <= length, f"period {m} needs more than two seasons of history")
@@ -833,13 +839,23 @@ def decompose_score(hist: torch.Tensor, head: int, length: int, m: int, det: Det
     for k in ("level", "slope", "sigma", "nvalid"):
         if k not in out:
             out[k] = torch.empty(N, **f32)
-    if "phase_means" not in out:
+    if phase_means and "phase_means" not in out:
         out["phase_means"] = torch.empty((N, m), **f32)
+    if "_defer" not in out or out["_defer"].numel() < N + 1:
+        out["_defer"] = torch.zeros(N + 1, dtype=torch.int32, device=dev)
     a = DecompArgs()
     a.hist, a.ld, a.ring_len, a.head, a.T, a.N, a.m = nat.ptr(hist), hist.stride(0), hist.shape[1], int(head), \
         int(length), N, int(m)
     a.bf16 = int(hist.dtype == torch.bfloat16)
-    a.phase_means = nat.ptr(out["phase_means"])
+    a.phase_means = nat.ptr(out["phase_means"]) if phase_means else 0
+    a.defer = nat.ptr(out["_defer"])
+    hmax = det.max_horizon
+    if hmax is not None and 1 <= hmax <= 64 and det.horizons is not None:
+        # split epilogue: the band / verdict runs in its own kernel from the seasonal terms of
+        # horizons 1..hmax (the host-known bound of every horizon)
+        if "_sfc" not in out or out["_sfc"].shape != (N, hmax):
+            out["_sfc"] = torch.empty((N, hmax), **f32)
+        a.sfc, a.hmax = nat.ptr(out["_sfc"]), int(hmax)
     a.fc_level, a.fc_slope = nat.ptr(out["level"]), nat.ptr(out["slope"])
     a.sigma, a.nvalid = nat.ptr(out["sigma"]), nat.ptr(out["nvalid"])
     _fill_detect(a.det, det, N, dev, out)

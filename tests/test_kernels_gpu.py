@@ -337,27 +337,37 @@ def test_seasonal_decompose_kernel_matches_reference(K, dtype, m, T):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dtype,m,T", [(torch.float32, 24, 24 * 9 + 5), (torch.float32, 25, 25 * 6),
-                                       (torch.bfloat16, 1440, 10080)])
-def test_decompose_scorer_matches_reference(K, dtype, m, T):
+@pytest.mark.parametrize("dtype,m,T,aligned,head,split", [
+    (torch.float32, 24, 24 * 9 + 5, False, 29, False), (torch.float32, 25, 25 * 6, False, 29, False),
+    (torch.bfloat16, 1440, 10080, False, 29, False),
+    # single-pass kernel (ring length a multiple of 8, m % 16 == 0): head phases, inline and
+    # split (own-kernel) band / verdict, gapped series finished by the general kernel
+    (torch.float32, 32, 32 * 9 + 5, True, 24, False), (torch.float32, 32, 32 * 9 + 5, True, 31, True),
+    (torch.bfloat16, 1440, 10080, True, 29, False), (torch.bfloat16, 1440, 10080, True, 30, True),
+    (torch.bfloat16, 1440, 10080, True, 35, True), (torch.float32, 1440, 10080, True, 32, True)])
+def test_decompose_scorer_matches_reference(K, dtype, m, T, aligned, head, split):
     """ML_ALGORITHM=seasonal_decompose: K4's scoring mode (no [N, T] outputs) —
     trend extrapolation, phase means, residual RMS, band and verdicts — against
     models/decompose.py decompose_forecast + models/detect.py."""
     from foremast_amd.models import decompose as dec
     from foremast_amd.brain.engine import synthetic_history
     dev = torch.device("cuda:0")
-    N, R, C = 64, T + 37, 20
+    N, C = 64, 20
+    R = (T + 40) // 8 * 8 if aligned else T + 37
     y = synthetic_history(N, T + C, m, dev, seed=6)
     y[3, 100:140] = float("nan")
+    y[40, T - 1] = float("nan")
     ring = torch.full((N, R), float("nan"), device=dev, dtype=dtype)
-    head = 29
     cols = (head + torch.arange(T, device=dev)) % R
     ring[:, cols] = y[:, :T].to(dtype)
     cur = y[:, T:].float().contiguous()
     cur[::5, 7] *= 1.5
     spec = _det_spec(K, N, C, dev, cur=cur, thr=3.0)
+    if split:
+        spec.max_horizon = C
     out = K.decompose_score(ring, head, T, m, spec)
     torch.cuda.synchronize()
+    assert ("_sfc" in out) == split
     fc = dec.decompose_forecast(ring[:, cols].float().cpu(), m)
     scale = float(torch.nan_to_num(y.float()).abs().max())
     f_ref = dec.forecast_decomposition(fc, torch.arange(1, C + 1))
@@ -368,6 +378,35 @@ def test_decompose_scorer_matches_reference(K, dtype, m, T):
                        torch.full((N,), 3, dtype=torch.int8), torch.full((N,), -1e30))
     assert torch.equal(d.verdict, out["verdict"].cpu()) and torch.equal(d.count, out["count"].cpu())
     assert int((out["verdict"] == 1).sum()) >= N // 5 - 2
+    if aligned and m % 16 == 0:
+        assert int(out["_defer"][0]) == 2  # the two gapped series took the general kernel
+
+
+@pytest.mark.gpu
+def test_decompose_scorer_many_deferred(K):
+    """More gapped series than the deferred launch has workgroups (256): the
+    grid-stride loop finishes every one of them, gap-free ones stay on the fast path."""
+    from foremast_amd.models import decompose as dec
+    from foremast_amd.brain.engine import synthetic_history
+    dev = torch.device("cuda:0")
+    N, m, T, C = 2600, 32, 32 * 9, 8
+    y = synthetic_history(N, T + C, m, dev, seed=8)
+    y[::2, 50] = float("nan")  # 1300 gapped series
+    ring = y[:, :T].contiguous()
+    cur = y[:, T:].contiguous()
+    spec = _det_spec(K, N, C, dev, cur=cur, thr=3.0)
+    spec.max_horizon = C
+    out = K.decompose_score(ring, 0, T, m, spec)
+    torch.cuda.synchronize()
+    assert int(out["_defer"][0]) == N // 2
+    fc = dec.decompose_forecast(ring.cpu(), m)
+    scale = float(torch.nan_to_num(y).abs().max())
+    f_ref = dec.forecast_decomposition(fc, torch.arange(1, C + 1))
+    assert float((out["forecast"].cpu() - f_ref).abs().max()) < 5e-4 * scale
+    torch.testing.assert_close(out["sigma"].cpu(), fc.sigma, rtol=2e-3, atol=1e-4 * scale)
+    d = det_ref.detect(out["forecast"].cpu(), out["sigma"].cpu(), cur.cpu(), torch.full((N,), 3.0),
+                       torch.full((N,), 3, dtype=torch.int8), torch.full((N,), -1e30))
+    assert torch.equal(d.verdict, out["verdict"].cpu()) and torch.equal(d.count, out["count"].cpu())
 
 
 @pytest.mark.gpu
