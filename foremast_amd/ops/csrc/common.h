@@ -67,6 +67,32 @@ __device__ __forceinline__ v2f wave_sum2(v2f v) {
   return v;
 }
 
+// All-lane reductions with DPP row scans + row broadcasts (no LDS permute round trips);
+// the result is read from lane 63 as a wave-uniform value.  Every lane must be active.
+template <int CTRL, int RM, bool BC>
+__device__ __forceinline__ float dpp_f(float old, float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL, RM, 0xf, BC));
+}
+__device__ __forceinline__ float wave_allsum(float v) {
+  v += dpp_f<0x111, 0xf, false>(0.f, v);  // row_shr:1..8 (lanes without a source add 0)
+  v += dpp_f<0x112, 0xf, false>(0.f, v);
+  v += dpp_f<0x114, 0xf, false>(0.f, v);
+  v += dpp_f<0x118, 0xf, false>(0.f, v);
+  v += dpp_f<0x142, 0xa, false>(0.f, v);  // row_bcast:15 -> rows 1, 3
+  v += dpp_f<0x143, 0xc, false>(0.f, v);  // row_bcast:31 -> rows 2, 3
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), FM_WAVE - 1));
+}
+__device__ __forceinline__ float wave_allmax(float v) {
+  const float lo = -__builtin_huge_valf();
+  v = fmaxf(v, dpp_f<0x111, 0xf, false>(lo, v));
+  v = fmaxf(v, dpp_f<0x112, 0xf, false>(lo, v));
+  v = fmaxf(v, dpp_f<0x114, 0xf, false>(lo, v));
+  v = fmaxf(v, dpp_f<0x118, 0xf, false>(lo, v));
+  v = fmaxf(v, dpp_f<0x142, 0xa, false>(lo, v));
+  v = fmaxf(v, dpp_f<0x143, 0xc, false>(lo, v));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), FM_WAVE - 1));
+}
+
 __device__ __forceinline__ v2f shfl_up2(v2f v, int d) {
   v2f r;
   r.x = __shfl_up(v.x, d, FM_WAVE);

@@ -57,7 +57,8 @@ struct DecompArgs {
   float* sigma;       // [N] residual RMS or null
   float* nvalid;      // [N] valid samples or null
   DetectArgs det;
-  int* defer;         // scoring fast path: [1 + N] count + series the general kernel finishes, or null
+  int* defer;         // scoring fast path: [N + 2] count, series the general kernel finishes, finished
+                      // workgroups of that launch (both counts zero between launches); or null
   float* sfc;         // fast path, split epilogue: [N, hmax] seasonal term of horizons 1..hmax, or null
   int hmax;           // (sfc) every horizon is in 1..hmax <= 64
   int _pad;
@@ -396,6 +397,15 @@ __global__ __launch_bounds__(BLOCK, 4) void decompose_deferred_kernel(const Deco
     decompose_series_call<TIN, KT, EXACT>(a, a.defer[1 + q]);
     __syncthreads();
   }
+  // the last workgroup out resets the count for the next launch (every workgroup has read
+  // it by then): no memset launch per call.  defer[N + 1] counts the finished workgroups.
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(&a.defer[a.N + 1], 1) == (int)gridDim.x - 1) {
+      atomicExch(&a.defer[0], 0);
+      atomicExch(&a.defer[a.N + 1], 0);
+    }
+  }
 }
 
 // ---- scoring fast path: one streaming pass ------------------------------------------
@@ -527,8 +537,12 @@ __global__ __launch_bounds__(SB, M > 0 ? 6 : 4) void decompose_score_kernel(cons
     const float y0 = to_f32<TIN>(y0n);
     if (n + (int)gridDim.x < a->N) score_issue<TIN, KT>(a, n + gridDim.x, nxt, y0n);  // block-uniform
 
-    // 1. prefix: in-lane inclusive over 8 samples, DPP wave scan of the lane totals, written
-    //    to LDS at once (the wave offsets are added in place after the block scan)
+    // 1. prefix: in-lane inclusive over 8 samples, DPP wave scan of the lane totals; the
+    //    samples (y - y0, masked) stay in registers through the block scan and the prefix is
+    //    written once, offsets included (recomputing the 7 in-lane adds is cheaper than an
+    //    LDS read-modify-write pass)
+    v8f v[KT];
+    float ex[KT];
 #pragma unroll
     for (int k = 0; k < KT; ++k) {
       const int tg = (tid + k * SB) * SE;
@@ -542,17 +556,10 @@ __global__ __launch_bounds__(SB, M > 0 ? 6 : 4) void decompose_score_kernel(cons
         q.lo = v4f{e[0], e[1], e[2], e[3]};
         q.hi = v4f{e[4], e[5], e[6], e[7]};
       }
-      q.lo.y += q.lo.x;
-      q.lo.z += q.lo.y;
-      q.lo.w += q.lo.z;
-      q.hi.x += q.lo.w;
-      q.hi.y += q.hi.x;
-      q.hi.z += q.hi.y;
-      q.hi.w += q.hi.z;
-      const float inc = wave_inclusive_scan(q.hi.w);
-      const float ex = inc - q.hi.w;
-      *(v4f*)(P + tg) = q.lo + ex;
-      *(v4f*)(P + tg + 4) = q.hi + ex;
+      v[k] = q;
+      const float tot = ((q.lo.x + q.lo.y) + (q.lo.z + q.lo.w)) + ((q.hi.x + q.hi.y) + (q.hi.z + q.hi.w));
+      const float inc = wave_inclusive_scan(tot);
+      ex[k] = inc - tot;
       if (lane == FM_WAVE - 1) bsum[k * SNW + w] = inc;
     }
     __syncthreads();
@@ -575,38 +582,40 @@ __global__ __launch_bounds__(SB, M > 0 ? 6 : 4) void decompose_score_kernel(cons
 #pragma unroll
     for (int k = 0; k < KT; ++k) {
       const int tg = (tid + k * SB) * SE;
-      const float o = bsum[k * SNW + w];
-      *(v4f*)(P + tg) += o;
-      *(v4f*)(P + tg + 4) += o;
+      v8f q = v[k];
+      q.lo.x += ex[k] + bsum[k * SNW + w];
+      q.lo.y += q.lo.x;
+      q.lo.z += q.lo.y;
+      q.lo.w += q.lo.z;
+      q.hi.x += q.lo.w;
+      q.hi.y += q.hi.x;
+      q.hi.z += q.hi.y;
+      q.hi.w += q.hi.z;
+      *(v4f*)(P + tg) = q.lo;
+      *(v4f*)(P + tg + 4) = q.hi;
     }
     __syncthreads();
 
-    // 2. detrended samples in registers; the groups without a centred trend read a clamped
-    //    (in-range) position and are never used.  D_i = (P_i - P_{i-1}) - (d_i + d_{i-1}) / 2m:
-    //    P_{-1} and d_{-1} come from the previous lane (its group is the adjacent one) except
-    //    in lane 0 and at the lower clamp, which read them.
-    v8f D[KT];
+    // 2. detrended samples, in place of the samples: D_i = v_i - (d_i + d_{i-1}) / 2m with
+    //    d_j = P[j+h] - P[j-h] (the groups without a centred trend read a clamped, in-range
+    //    position and are never used); d_{-1} comes from the previous lane (its group is the
+    //    adjacent one) except in lane 0 and at the lower clamp, which read it
 #pragma unroll
     for (int k = 0; k < KT; ++k) {
       const int tg = (tid + k * SB) * SE;
       const int tc = min(max(tg, lo), hi);
-      const v4f y0v = *(const v4f*)(P + tg), y1v = *(const v4f*)(P + tg + 4);
       v4f d0 = *(const v4f*)(P + tc + h), d1 = *(const v4f*)(P + tc + h + 4);
       d0 -= *(const v4f*)(P + tc - h);
       d1 -= *(const v4f*)(P + tc - h + 4);
       const bool own = lane == 0 || tg <= lo;
-      float ym = 0.f, dm = 0.f;
-      if (own) {
-        ym = P[tg - 1];
-        dm = P[tc + h - 1] - P[tc - h - 1];
-      }
-      const float ysh = wave_shr1(ym, y1v.w), dsh = wave_shr1(dm, d1.w);
-      ym = own ? ym : ysh;
+      float dm = 0.f;
+      if (own) dm = P[tc + h - 1] - P[tc - h - 1];
+      const float dsh = wave_shr1(dm, d1.w);
       dm = own ? dm : dsh;
-      D[k].lo = (y0v - v4f{ym, y0v.x, y0v.y, y0v.z}) - cm * (d0 + v4f{dm, d0.x, d0.y, d0.z});
-      D[k].hi = (y1v - v4f{y0v.w, y1v.x, y1v.y, y1v.z}) - cm * (d1 + v4f{d0.w, d1.x, d1.y, d1.z});
+      v[k].lo -= cm * (d0 + v4f{dm, d0.x, d0.y, d0.z});
+      v[k].hi -= cm * (d1 + v4f{d0.w, d1.x, d1.y, d1.z});
       // the item is finished before the next one's LDS reads issue (all in flight: spills)
-      asm volatile("" : "+v"(D[k].lo), "+v"(D[k].hi)::"memory");
+      asm volatile("" : "+v"(v[k].lo), "+v"(v[k].hi)::"memory");
     }
     // the forecast's trend anchors: the last centred trend and the one a season earlier
     float tr_e = 0.f, tr_p = 0.f;
@@ -623,8 +632,8 @@ __global__ __launch_bounds__(SB, M > 0 ? 6 : 4) void decompose_score_kernel(cons
     for (int k = 0; k < KT; ++k) {
       const int tg = (tid + k * SB) * SE;
       if (tg < TP) {
-        *(v4f*)(P + tg) = D[k].lo;
-        *(v4f*)(P + tg + 4) = D[k].hi;
+        *(v4f*)(P + tg) = v[k].lo;
+        *(v4f*)(P + tg + 4) = v[k].hi;
       }
     }
     __syncthreads();
@@ -674,9 +683,9 @@ __global__ __launch_bounds__(SB, M > 0 ? 6 : 4) void decompose_score_kernel(cons
         sc += cnt;
       }
     }
-    spm = wave_sum(spm);
-    sw = wave_sum(sw);
-    sc = wave_sum(sc);
+    spm = wave_allsum(spm);
+    sw = wave_allsum(sw);
+    sc = wave_allsum(sc);
     if (lane == 0) { red[w] = spm; red[SNW + w] = sw; red[2 * SNW + w] = sc; }
     __syncthreads();
     float tpm = 0.f, tw = 0.f, tcnt = 0.f;
@@ -758,8 +767,7 @@ extern "C" int fm_seasonal_decompose(const DecompArgs* a, hipStream_t st) {
                     ks <= S_MAX_ITEMS && fm_decompose_score_lds_bytes(a->T, a->m) <= 160 * 1024 &&
                     (!a->sfc || (a->hmax >= 1 && a->hmax <= FM_WAVE));
   if (fast) {
-    hipError_t e = hipMemsetAsync(a->defer, 0, sizeof(int), st);
-    if (e != hipSuccess) return (int)e;
+    hipError_t e;
     const size_t slds = fm_decompose_score_lds_bytes(a->T, a->m);
     static int cus = 0;
     if (!cus) {

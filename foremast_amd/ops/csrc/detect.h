@@ -158,10 +158,10 @@ __device__ __forceinline__ void detect_epilogue_wave(const DetectArgs& d, int n,
     float cnt_f = 0.f, cnt_l = 0.f;
     for (int c = lane; c < d.C; c += FM_WAVE)
       det_count_col(d, n, c, t, sig, gidx, bnd, mlow, model_ok, fcast, cnt_f, cnt_l, anyv, sc);
-    cnt_f = wave_sum(cnt_f);
-    cnt_l = t.differs ? wave_sum(cnt_l) : 0.f;  // t.differs is wave-uniform (one series per wave)
-    anyv = wave_max(anyv);
-    sc = wave_max(sc);
+    cnt_f = wave_allsum(cnt_f);
+    cnt_l = t.differs ? wave_allsum(cnt_l) : 0.f;  // t.differs is wave-uniform (one series per wave)
+    anyv = wave_allmax(anyv);
+    sc = wave_allmax(sc);
     thr = det_decide(d, t, cnt_f, cnt_l, &ic);
   }
   const bool emit = d.anom_count && ic > 0;

@@ -841,8 +841,9 @@ def decompose_score(hist: torch.Tensor, head: int, length: int, m: int, det: Det
             out[k] = torch.empty(N, **f32)
     if phase_means and "phase_means" not in out:
         out["phase_means"] = torch.empty((N, m), **f32)
-    if "_defer" not in out or out["_defer"].numel() < N + 1:
-        out["_defer"] = torch.zeros(N + 1, dtype=torch.int32, device=dev)
+    if "_defer" not in out or out["_defer"].numel() != N + 2:
+        # [count, series..., finished workgroups]: the kernels keep both counts zero between calls
+        out["_defer"] = torch.zeros(N + 2, dtype=torch.int32, device=dev)
     a = DecompArgs()
     a.hist, a.ld, a.ring_len, a.head, a.T, a.N, a.m = nat.ptr(hist), hist.stride(0), hist.shape[1], int(head), \
         int(length), N, int(m)
