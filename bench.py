@@ -535,7 +535,8 @@ def setup_lstm(args, world, rank, dev, n_features, fp8):
     app_id = (torch.arange(s, e, device=dev, dtype=torch.int64) // ent_per_app).to(torch.int32)
     shard = LstmShard(n_local, args.ring, F, window=args.lstm_window, hidden=64, fp8=fp8, device=dev,
                       app_id=app_id, n_apps=n_apps, threshold=4.0, train_batch=args.lstm_train_batch,
-                      lr=1e-3, seed=0, fused_train=not args.lstm_autograd, restat_every=args.lstm_restat_every)
+                      lr=1e-3, seed=0, fused_train=not args.lstm_autograd, restat_every=args.lstm_restat_every,
+                      season=args.season)
     params = [synthetic_params(n_ent, dev, seed=1234 + 7 * f, rows=(s, e)) for f in range(F)]
     shard.load_history([synthetic_eval(p, 0, args.ring, args.season, noise_seed=555 + f, row0=s)
                         for f, p in enumerate(params)])

@@ -34,6 +34,7 @@ on ``--anomaly-frac`` of the (job, metric) series, in the new pods only).
 from __future__ import annotations
 
 import asyncio
+import gc
 import time
 from typing import Dict, List, Tuple
 from urllib.parse import parse_qs, unquote, urlsplit
@@ -247,14 +248,30 @@ def setup_node(args, world, rank, dev):
     scored: List[int] = []
     breakdowns: List[Dict[str, float]] = []
 
+    gc_pause = {"t": 0.0, "t0": 0.0, "n": 0}
+
+    def _gc_cb(phase, info):  # cyclic-GC pauses inside the timed ticks (reported per tick)
+        if phase == "start":
+            gc_pause["t0"] = time.perf_counter()
+        else:
+            gc_pause["t"] += time.perf_counter() - gc_pause["t0"]
+            gc_pause["n"] += 1
+
     def tick(k):
         clock["t"] = T0 + STEP * (k + 1)
         n_rows = roll.n_live
-        table = run_tick()
+        gc_pause["t"], gc_pause["n"] = 0.0, 0
+        gc.callbacks.append(_gc_cb)
+        try:
+            table = run_tick()
+        finally:
+            gc.callbacks.remove(_gc_cb)
         if dev.type == "cuda":
             torch.cuda.synchronize()
         scored.append(n_rows)
-        breakdowns.append({k: round(v, 2) for k, v in roll.timings.items() if k != "admit_ms"})
+        bd = {k: round(v, 2) for k, v in roll.timings.items() if k != "admit_ms"}
+        bd["gc_ms"], bd["gc_runs"] = round(gc_pause["t"] * 1e3, 2), gc_pause["n"]
+        breakdowns.append(bd)
         for a in table["anomalous_apps"]:
             flagged.add(int(a.split("/app")[1]))
         return table

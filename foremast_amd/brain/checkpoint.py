@@ -128,6 +128,8 @@ def save_lstm_shard(shard, path: str, extra: Optional[Dict[str, Any]] = None) ->
     tensors["gen_state"] = shard.gen.get_state()
     if shard.cal is not None:
         tensors["cal"] = shard.cal
+    if shard.lvl_sig is not None:
+        tensors["lvl_sig"] = shard.lvl_sig
     hidden = int(shard.model.H)
     meta = {"format": FORMAT, "kind": "lstm_shard",
             "args": {"n_series": shard.n, "ring_len": shard.R, "n_features": shard.F, "window": shard.T,
@@ -135,7 +137,9 @@ def save_lstm_shard(shard, path: str, extra: Optional[Dict[str, Any]] = None) ->
                      "threshold": float(shard.threshold), "train_batch": int(shard.train_batch),
                      "restat_every": int(shard.restat_every), "fused_train": bool(shard.fused_train),
                      "dtype": _dtype_name(shard.rings[0].data.dtype), "cal_windows": int(shard.cal_windows),
-                     "cal_ewma": float(shard.cal_ewma)},
+                     "cal_ewma": float(shard.cal_ewma), "season": int(shard.season),
+                     "level_points": int(shard.level_points), "level_cal": int(shard.level_cal),
+                     "level_threshold": shard.level_threshold},
             "param_groups": opt["param_groups"], "trainer_steps": int(shard.trainer.steps),
             "mu": float(shard.mu), "sigma": float(shard.sigma), "rho": float(shard.rho), "ticks": int(shard.ticks),
             "rings": [[r.head, r.length] for r in shard.rings], "extra": extra or {}}
@@ -155,7 +159,9 @@ def load_lstm_shard(path: str, device="cpu"):
                       fp8=a["fp8"], device=device, app_id=t["app_id"].to(torch.int32), n_apps=a["n_apps"],
                       threshold=a["threshold"], train_batch=a["train_batch"], lr=lr,
                       restat_every=a["restat_every"], dtype=dtype, fused_train=a["fused_train"],
-                      cal_windows=int(a.get("cal_windows", 0)), cal_ewma=float(a.get("cal_ewma", 0.0)))
+                      cal_windows=int(a.get("cal_windows", 0)), cal_ewma=float(a.get("cal_ewma", 0.0)),
+                      season=int(a.get("season", 1440)), level_points=int(a.get("level_points", 8)),
+                      level_cal=int(a.get("level_cal", 64)), level_threshold=a.get("level_threshold", None))
     for f, ring in enumerate(shard.rings):
         ring._store.copy_(t[f"ring{f}"])
         ring.state = RingState(head=int(meta["rings"][f][0]), length=int(meta["rings"][f][1]))
@@ -173,6 +179,7 @@ def load_lstm_shard(path: str, device="cpu"):
     shard.mu, shard.sigma = float(meta["mu"]), float(meta["sigma"])
     shard.rho = float(meta.get("rho", 1.0))
     shard.cal = t["cal"].float().contiguous() if "cal" in t else None
+    shard.lvl_sig = t["lvl_sig"].float().contiguous() if "lvl_sig" in t else None
     shard.ticks = int(meta["ticks"])
     shard.packed = None  # repacked for the fused scorer on the next score
     shard.checkpoint_extra = meta.get("extra", {})

@@ -31,6 +31,17 @@ entities, global alone 263, both 27, every regression caught by each.  Each
 tick the kernel's epilogue moves ``mu_i`` toward the series' errors that lie
 within ``CAL_GATE`` of its level (``cal_ewma``), tracking the continuously
 trained model without absorbing a regression that builds up over ticks.
+
+Level term: the autoencoder scores the *shape* of a z-scored 32-point window,
+so a level shift of a few noise sigmas inside the daily swing is weak evidence
+for it (round-2 sweep: +3 sigma recall 0.24).  Each tick ``lstm_level``
+(csrc/lstm.hip) computes, per (series, feature), the mean over the newest
+``level_points`` samples of x_t minus the same minutes' mean over the previous
+days the ring holds (<= 7), divided by that statistic's own spread — calibrated
+on the series' history as the RMS of the statistic at ``level_cal`` earlier
+offsets (:meth:`calibrate`).  A window is anomalous when the AE z-score OR any
+feature's ``|level z|`` exceeds its threshold (``level_threshold``; the
+epilogue also keeps such windows out of the calibration refresh).
 """
 
 from __future__ import annotations
@@ -54,7 +65,8 @@ class LstmShard:
                  fp8: bool = False, device="cuda", app_id: Optional[torch.Tensor] = None, n_apps: int = 1,
                  threshold: float = 4.0, train_batch: int = 4096, lr: float = 1e-3, restat_every: int = 16,
                  seed: int = 0, dtype=torch.bfloat16, fused_train: bool = True, cal_windows: int = 16,
-                 cal_ewma: float = 1.0 / 32, dp_overlap: bool = True) -> None:
+                 cal_ewma: float = 1.0 / 32, dp_overlap: bool = True, season: int = 1440,
+                 level_points: int = 8, level_threshold: Optional[float] = 5.5, level_cal: int = 64) -> None:
         self.n, self.R, self.F, self.T = n_series, ring_len, n_features, window
         self.device = torch.device(device)
         self.gpu = self.device.type == "cuda"
@@ -87,6 +99,10 @@ class LstmShard:
         self.cal_windows, self.cal_ewma = cal_windows, cal_ewma
         self.cal: Optional[torch.Tensor] = None  # [n, 2] (mu_i, 1 / (rho * mu_i)) after calibrate()
         self.rho = 1.0
+        self.season, self.level_points, self.level_cal = int(season), int(level_points), int(level_cal)
+        self.level_threshold = level_threshold
+        self.lvl_sig: Optional[torch.Tensor] = None  # [n, F] spread of the level statistic after calibrate()
+        self._zl: Optional[torch.Tensor] = None
         self.ticks = 0
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed + 1)
@@ -120,6 +136,8 @@ class LstmShard:
         self.app_id = ext(self.app_id, 0)
         if self.cal is not None:
             self.cal = ext(self.cal, 1.0).contiguous()
+        if self.lvl_sig is not None:  # rows not calibrated yet carry no level term (z = 0)
+            self.lvl_sig = ext(self.lvl_sig, float("inf")).contiguous()
         self.n = capacity
         self._all = torch.arange(capacity, device=dev)
         self._zero_off = torch.zeros(capacity, dtype=torch.long, device=dev)
@@ -309,6 +327,83 @@ class LstmShard:
             self.cal = full.contiguous()
         else:
             self.cal[sel] = new
+        self.calibrate_level(rows)
+
+    # ------------------------------------------------------------------ level term
+    def _level_geometry(self):
+        r0 = self.rings[0]
+        L, m, avail = self.level_points, self.season, r0.length
+        back_max = avail - L - m  # offsets keep at least one earlier day behind them
+        if self.level_threshold is None or back_max < L:
+            return None
+        step = max(L, min(back_max, m) // max(self.level_cal, 1))
+        K = max(1, min(self.level_cal, back_max // step))
+        return (r0.head + avail - 1) % r0.R, avail, K, step
+
+    def _level_stat_cpu(self, back: int) -> torch.Tensor:
+        """The level statistic ``[n, F]`` ending ``back`` samples before the newest
+        (same definition as ``lstm_level_kernel``)."""
+        r0 = self.rings[0]
+        L, m, avail = self.level_points, self.season, r0.length
+        D = min(7, (avail - back - L) // m)
+        out = torch.full((self.n, self.F), float("nan"), device=self.device)
+        if D < 1:
+            return out
+        i = torch.arange(L, device=self.device)
+        d = torch.arange(D + 1, device=self.device)
+        logical = avail - 1 - back - (L - 1 - i)[None, :] - d[:, None] * m  # [D+1, L]
+        cols = (r0.head + logical) % r0.R
+        for f, ring in enumerate(self.rings):
+            x = ring.data[:, cols.reshape(-1)].float().view(self.n, D + 1, L)
+            base = torch.nanmean(x[:, 1:], 1)
+            r = x[:, 0] - base
+            out[:, f] = torch.nanmean(r, 1)
+        return out
+
+    def calibrate_level(self, rows: Optional[torch.Tensor] = None) -> None:
+        """Spread of the level statistic per (series, feature): the RMS of the
+        statistic at ``level_cal`` offsets over the last day (each with at least
+        one earlier day behind it), floored at 1e-6 of the series' std."""
+        geo = self._level_geometry()
+        if geo is None:
+            self.lvl_sig = None
+            return
+        newest, avail, K, step = geo
+        if self.gpu:
+            from ..ops import lstm as L
+            st = L.lstm_level([r.data for r in self.rings], newest, avail, self.season, self.level_points,
+                              K=K, back_step=step)
+        else:
+            st = torch.stack([self._level_stat_cpu((k + 1) * step) for k in range(K)])
+        ok = torch.isfinite(st)
+        cnt = ok.sum(0)
+        ms = torch.where(ok, st * st, 0.0).sum(0) / cnt.clamp(min=1)
+        sig = ms.sqrt().clamp(min=1e-12)
+        sig = torch.maximum(sig, self.std * 1e-6)
+        sig = torch.where(cnt >= 4, sig, torch.full_like(sig, float("inf")))  # too little history: no level term
+        if rows is None or self.lvl_sig is None:
+            full = torch.full((self.n, self.F), float("inf"), device=self.device)
+            sel = self._all if rows is None else rows.to(self.device, torch.long)
+            full[sel] = sig[sel]
+            self.lvl_sig = full.contiguous()
+        else:
+            sel = rows.to(self.device, torch.long)
+            self.lvl_sig[sel] = sig[sel]
+
+    def level_z(self) -> Optional[torch.Tensor]:
+        """``[n, F]`` level z of every series' newest points (None: no level term)."""
+        if self.lvl_sig is None or self.level_threshold is None:
+            return None
+        r0 = self.rings[0]
+        if r0.length < self.level_points + self.season:
+            return None
+        if self.gpu:
+            from ..ops import lstm as L
+            self._zl = L.lstm_level([r.data for r in self.rings], (r0.head + r0.length - 1) % r0.R, r0.length,
+                                    self.season, self.level_points, sig=self.lvl_sig, out=self._zl)
+            return self._zl
+        st = self._level_stat_cpu(0)
+        return torch.where(torch.isfinite(st) & (self.lvl_sig > 0), st / self.lvl_sig, 0.0)
 
     def _calib_errors(self, src, n: int) -> torch.Tensor:
         """Reconstruction errors (float64) of ``src``'s windows: a kernel
@@ -337,9 +432,11 @@ class LstmShard:
     def _score_packed(self) -> Dict[str, torch.Tensor]:
         from ..ops import lstm as L
         self.app_stats.zero_()
+        zl = self.level_z()
         self.out = L.lstm_score(self.packed, None, self.mu, self.sigma, thr_default=self.threshold,
                                 app_id=self.app_id, app_stats=self.app_stats, out=self.out,
-                                ring=self._ring_src(), T=self.T, cal=self.cal, cal_ewma=self.cal_ewma)
+                                ring=self._ring_src(), T=self.T, cal=self.cal, cal_ewma=self.cal_ewma,
+                                zlvl=zl, thr_level=float(self.level_threshold or float("inf")))
         return self.out
 
     def tick(self, newx: torch.Tensor, train: bool = True, overlap: bool = True) -> Dict[str, torch.Tensor]:
@@ -394,7 +491,11 @@ class LstmShard:
         if self.cal is not None:
             zs = (err - self.cal[:, 0]) * self.cal[:, 1]
             z = torch.minimum(z, zs)
-        v = (z > self.threshold).to(torch.int8)
+        v = z > self.threshold
+        zl = self.level_z()
+        if zl is not None:  # same level term as the kernel epilogue
+            v = v | (zl.abs().amax(1) > float(self.level_threshold))
+        v = v.to(torch.int8)
         if self.cal is not None and self.cal_ewma > 0:  # same update (and gate) as the kernel epilogue
             upd = (v == 0) & torch.isfinite(err) & (zs <= CAL_GATE)
             nmu = self.cal[:, 0] + self.cal_ewma * (err - self.cal[:, 0])

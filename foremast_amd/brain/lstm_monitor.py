@@ -108,7 +108,7 @@ class LstmMonitor:
                                hidden=hidden or self.cfg.lstm_hidden, fp8=bool(fp8) and self.gpu,
                                device=self.device, threshold=self.cfg.lstm_threshold, train_batch=tb, seed=seed,
                                dtype=torch.bfloat16 if self.gpu else torch.float32, dp_overlap=False,
-                               restat_every=1 << 30)
+                               restat_every=1 << 30, season=self.cfg.season)
         for ring in self.shard.rings:
             ring.state.head, ring.state.length = 0, R
         self.shard.live = torch.zeros(0, dtype=torch.int64, device=self.device)

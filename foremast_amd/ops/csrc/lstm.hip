@@ -49,6 +49,31 @@ struct LstmArgs {
   LstmRingSrc src;         // ring-direct input (x == null)
   float* cal;              // [N, 2] per-series (mu, 1/sigma) of the reconstruction error, or null (global only)
   float cal_ewma;          // > 0: mu_i tracks healthy errors, mu_i += cal_ewma * (err - mu_i) when verdict 0
+  const float* zlvl;       // [N, F] level z-scores (lstm_level_kernel) or null
+  float thr_level;         // a window is also anomalous when any |zlvl| exceeds this
+  int _pad2;
+};
+
+// Level term of the LSTM-AE verdict (lstm_level_kernel): the autoencoder scores the SHAPE
+// of a z-scored window, so a level shift of a few noise sigmas inside the daily swing is
+// weak evidence for it.  The level statistic of (series, feature) is the mean over the
+// newest L points of x_t - mean_{d=1..D} x_{t - d m} (the same minutes of the D previous
+// days, D <= 7 as the ring allows): ~N(0, sigma^2 (1 + 1/D) / L) on a healthy series with
+// a stable daily profile, so a +3 sigma shift reaches ~7 of its own spreads after 8 points.
+// Its spread per (series, feature) is calibrated on the series' own history: the RMS of the
+// statistic at K earlier offsets (calibration mode writes the raw statistics).
+struct LevelArgs {
+  LstmRingSrc src;   // rings, ld, ring_len, bf16 (start_col / windows unused)
+  int N;
+  int F;
+  int newest;        // physical column of the newest sample
+  int avail;         // valid samples in the rings
+  int m;             // samples per day
+  int L;             // points averaged, 1..8
+  int K;             // calibration: number of offsets (grid.y); 0: scoring
+  int back_step;     // calibration: offset k ends (k + 1) * back_step samples before the newest
+  const float* sig;  // scoring: [N, F] spread of the statistic
+  float* out;        // scoring: [N, F] z; calibration: [K, N, F] raw statistic (NaN: not enough data)
 };
 
 extern __shared__ __attribute__((aligned(16))) char fm_lstm_smem[];
@@ -203,7 +228,10 @@ __global__ __launch_bounds__(256, 2) void lstm_ae_kernel(const LstmArgs a) {
     }
     if (a.zscore) a.zscore[series] = z;
     const float thr = a.threshold ? a.threshold[series] : a.thr_default;
-    const int v = z > thr ? 1 : 0;
+    float zl = 0.f;  // level term: the largest |z| of the series' features
+    if (a.zlvl)
+      for (int f = 0; f < a.F; ++f) zl = fmaxf(zl, fabsf(a.zlvl[series * a.F + f]));
+    const int v = (z > thr || zl > a.thr_level) ? 1 : 0;
     if (a.verdict) a.verdict[series] = (signed char)v;
     // healthy windows keep the per-series error level current as the shared
     // model keeps training.  Only windows within CAL_GATE of the series' own
@@ -224,7 +252,62 @@ __global__ __launch_bounds__(256, 2) void lstm_ae_kernel(const LstmArgs a) {
   }
 }
 
+// one wave per (series, feature): lane = 8 d + i holds x at point i of day d back
+__global__ __launch_bounds__(256) void lstm_level_kernel(const LevelArgs a) {
+  const long long gw = (long long)blockIdx.x * (blockDim.x / FM_WAVE) + wave_id();
+  if (gw >= (long long)a.N * a.F) return;  // wave-uniform
+  const int n = (int)(gw / a.F), f = (int)(gw - (long long)n * a.F);
+  const int lane = lane_id(), d = lane >> 3, i = lane & 7;
+  const int back = a.K > 0 ? ((int)blockIdx.y + 1) * a.back_step : 0;
+  const int D = min(7, (a.avail - back - a.L) / a.m);
+  const int R = a.src.ring_len;
+  float x = 0.f;
+  bool ok = false;
+  if (D >= 1 && d <= D && i < a.L) {
+    int c = (a.newest - back - (a.L - 1 - i) - d * a.m) % R;
+    c += c < 0 ? R : 0;
+    const long long o = (long long)n * a.src.ld + c;
+    x = a.src.bf16 ? bf16_to_f32(((const bf16_t*)a.src.ring[f])[o]) : ((const float*)a.src.ring[f])[o];
+    ok = x == x;
+  }
+  // the D earlier days' mean at each point i (lanes i, i + 8, ..., i + 56)
+  float bs = (d >= 1 && ok) ? x : 0.f, bc = (d >= 1 && ok) ? 1.f : 0.f;
+#pragma unroll
+  for (int o = 8; o < FM_WAVE; o <<= 1) {
+    bs += __shfl_xor(bs, o, FM_WAVE);
+    bc += __shfl_xor(bc, o, FM_WAVE);
+  }
+  const bool use = d == 0 && ok && bc > 0.f;
+  float r = use ? x - bs / bc : 0.f, rc = use ? 1.f : 0.f;
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) {
+    r += __shfl_xor(r, o, FM_WAVE);
+    rc += __shfl_xor(rc, o, FM_WAVE);
+  }
+  if (lane != 0) return;
+  const float st = rc > 0.f ? r / rc : fm_nan();
+  if (a.K > 0) {
+    a.out[((long long)blockIdx.y * a.N + n) * a.F + f] = st;
+  } else {
+    const float sg = a.sig[(long long)n * a.F + f];
+    a.out[(long long)n * a.F + f] = (st == st && sg > 0.f) ? st / sg : 0.f;
+  }
+}
+
 }  // namespace
+
+extern "C" int fm_lstm_level(const LevelArgs* a, hipStream_t st) {
+  if (a->N <= 0 || a->F <= 0) return 0;
+  if (a->F > 7 || a->L < 1 || a->L > 8 || a->m < 1 || a->K < 0 || a->K > 65535 || (a->K == 0 && !a->sig) ||
+      (a->K > 0 && a->back_step < 1) || a->src.ring_len < 1 || a->newest < 0 || a->newest >= a->src.ring_len)
+    return (int)hipErrorInvalidValue;
+  const long long waves = (long long)a->N * a->F;
+  dim3 grid((unsigned)((waves + 3) / 4), (unsigned)(a->K > 0 ? a->K : 1));
+  hipLaunchKernelGGL(lstm_level_kernel, grid, dim3(256), 0, st, *a);
+  return (int)hipGetLastError();
+}
+
+extern "C" long long fm_lstm_level_args_size() { return (long long)sizeof(LevelArgs); }
 
 extern "C" size_t fm_lstm_lds_bytes(int F, int fp8) {
   return (size_t)(fp8 ? FRAG_BYTES_FP8 : FRAG_BYTES_BF16) + (size_t)F * H * 4;

@@ -70,10 +70,19 @@ class LstmArgs(C.Structure):
         ("mu", C.c_float), ("sigma", C.c_float), ("threshold", C.c_void_p), ("thr_default", C.c_float),
         ("err", C.c_void_p), ("zscore", C.c_void_p), ("verdict", C.c_void_p), ("recon", C.c_void_p),
         ("app_id", C.c_void_p), ("app_stats", C.c_void_p), ("wmax", C.c_void_p), ("src", LstmRingSrc),
-        ("cal", C.c_void_p), ("cal_ewma", C.c_float),
+        ("cal", C.c_void_p), ("cal_ewma", C.c_float), ("zlvl", C.c_void_p), ("thr_level", C.c_float),
+        ("_pad2", C.c_int),
     ]
 
 
+class LevelArgs(C.Structure):
+    _fields_ = [("src", LstmRingSrc), ("N", C.c_int), ("F", C.c_int), ("newest", C.c_int), ("avail", C.c_int),
+                ("m", C.c_int), ("L", C.c_int), ("K", C.c_int), ("back_step", C.c_int), ("sig", C.c_void_p),
+                ("out", C.c_void_p)]
+
+
+nat.register("fm_lstm_level", [C.POINTER(LevelArgs), C.c_void_p])
+nat.register("fm_lstm_level_args_size", [], C.c_longlong)
 nat.register("fm_lstm_ae", [C.POINTER(LstmArgs), C.c_void_p])
 nat.register("fm_lstm_lds_bytes", [C.c_int, C.c_int], C.c_size_t)
 nat.register("fm_lstm_args_size", [], C.c_longlong)
@@ -259,7 +268,8 @@ def lstm_score(p: LstmPacked, x: Optional[torch.Tensor], mu: float = 0.0, sigma:
                app_id: Optional[torch.Tensor] = None, app_stats: Optional[torch.Tensor] = None,
                out: Optional[Dict[str, torch.Tensor]] = None, ring: Optional[RingSource] = None,
                T: Optional[int] = None, cal: Optional[torch.Tensor] = None,
-               cal_ewma: float = 0.0) -> Dict[str, torch.Tensor]:
+               cal_ewma: float = 0.0, zlvl: Optional[torch.Tensor] = None,
+               thr_level: float = float("inf")) -> Dict[str, torch.Tensor]:
     """Score windows ``x [N, T, F]`` — or, with ``ring`` (and ``T``), the last
     ``T`` samples of every ring row (or the ``ring.win_series`` / ``win_start``
     windows) read directly by the kernel.
@@ -268,7 +278,9 @@ def lstm_score(p: LstmPacked, x: Optional[torch.Tensor], mu: float = 0.0, sigma:
     the smaller of the global one (``mu``/``sigma``) and the window's own
     series' one, so a window must be unusual for its series AND in absolute
     terms; with ``cal_ewma > 0`` the kernel moves ``mu`` toward every
-    non-anomalous error (relative dispersion kept)."""
+    non-anomalous error (relative dispersion kept).  ``zlvl`` ``[N, F]`` (from
+    :func:`lstm_level`): a window is also anomalous when any ``|zlvl|`` exceeds
+    ``thr_level``."""
     lib = nat.require()
     if ring is None:
         _need(x is not None and x.is_cuda and x.dtype == torch.float32 and x.dim() == 3 and x.is_contiguous(),
@@ -312,7 +324,48 @@ def lstm_score(p: LstmPacked, x: Optional[torch.Tensor], mu: float = 0.0, sigma:
     a.app_id, a.app_stats = nat.ptr(app_id), nat.ptr(app_stats)
     a.wmax = nat.ptr(p.wmax) if p.fp8 else 0
     a.cal, a.cal_ewma = nat.ptr(cal), float(cal_ewma)
+    if zlvl is not None:
+        _need(zlvl.shape == (N, F) and zlvl.dtype == torch.float32 and zlvl.is_contiguous() and zlvl.device == dev,
+              "zlvl must be float32 [N, F]")
+    a.zlvl, a.thr_level = nat.ptr(zlvl), float(thr_level)
     nat.check(lib.fm_lstm_ae(C.byref(a), nat.stream_handle(dev)), "fm_lstm_ae")
+    return out
+
+
+def lstm_level(rings: List[torch.Tensor], newest: int, avail: int, m: int, L: int = 8,
+               sig: Optional[torch.Tensor] = None, K: int = 0, back_step: int = 0,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Level statistic of every (row, feature) (see ``LevelArgs`` in csrc/lstm.hip):
+    the mean over the newest ``L`` samples of x_t minus the same minutes' mean over
+    up to 7 earlier days.  Scoring (``K == 0``): ``[N, F]`` statistic / ``sig``.
+    Calibration: the raw statistic ``[K, N, F]`` at offsets ending ``(k+1) *
+    back_step`` samples before the newest (NaN where a window has no data)."""
+    lib = nat.require()
+    F = len(rings)
+    r0 = rings[0]
+    _need(1 <= F <= 7 and all(r.shape == r0.shape and r.stride() == r0.stride() and r.dtype == r0.dtype
+                              for r in rings), "one ring per feature, same layout")
+    _need(r0.dim() == 2 and r0.stride(1) == 1 and r0.dtype in (torch.bfloat16, torch.float32), "ring layout")
+    N, R = r0.shape
+    _need(0 <= newest < R and 1 <= L <= 8 and m >= 1, "level geometry")
+    dev = r0.device
+    if K == 0:
+        _need(sig is not None and sig.shape == (N, F) and sig.dtype == torch.float32 and sig.is_contiguous(),
+              "sig must be float32 [N, F]")
+        shape = (N, F)
+    else:
+        _need(back_step >= 1 and K <= 65535, "calibration offsets")
+        shape = (K, N, F)
+    if out is None or out.shape != shape:
+        out = torch.empty(shape, dtype=torch.float32, device=dev)
+    a = LevelArgs()
+    for f, r in enumerate(rings):
+        a.src.ring[f] = r.data_ptr()
+    a.src.ld, a.src.ring_len, a.src.bf16 = r0.stride(0), R, int(r0.dtype == torch.bfloat16)
+    a.N, a.F, a.newest, a.avail, a.m, a.L, a.K, a.back_step = N, F, int(newest), int(avail), int(m), int(L), \
+        int(K), int(back_step)
+    a.sig, a.out = nat.ptr(sig), out.data_ptr()
+    nat.check(lib.fm_lstm_level(C.byref(a), nat.stream_handle(dev)), "fm_lstm_level")
     return out
 
 

@@ -422,3 +422,69 @@ def test_native_pack_matches_torch_repack(fp8):
     else:
         assert torch.equal(p.w_enc, ref.w_enc) and torch.equal(p.w_dec, ref.w_dec)
     assert torch.equal(p.w_out, ref.w_out) and torch.equal(p.b_out, ref.b_out)
+
+
+def _level_shard(device, dtype, n=64, m=96, days=4, F=2, seed=3):
+    from foremast_amd.brain.lstm_engine import LstmShard
+    R = m * days
+    g = torch.Generator().manual_seed(seed)
+    t = torch.arange(R, dtype=torch.float32)
+    hist = [100.0 + 20.0 * torch.sin(2 * np.pi * t / m)[None, :] + torch.randn(n, R, generator=g)
+            for _ in range(F)]
+    shard = LstmShard(n, R, F, window=16, hidden=64 if device == "cuda" else 16, device=device, dtype=dtype,
+                      fused_train=False,
+                      cal_windows=4, train_batch=64, season=m, level_points=8, level_threshold=5.5)
+    shard.load_history([h.to(device) for h in hist])
+    return shard, g, m
+
+
+def _level_ticks(shard, g, m, shifted, k=8, size=4.0):
+    n, F = shard.n, shard.F
+    for j in range(k):
+        tt = float(shard.rings[0].length + shard.ticks)
+        v = 100.0 + 20.0 * np.sin(2 * np.pi * tt / m) + torch.randn(n, F, generator=g)
+        v[shifted] += size
+        shard.ingest_tick(v.to(shard.device))
+
+
+def test_lstm_level_term_flags_small_shift_cpu():
+    """The level term (mean of the newest 8 points minus the same minutes of the earlier
+    days, over its calibrated spread) flags a +4 sigma shift the shape-scoring AE cannot
+    see, and stays quiet on the healthy series."""
+    shard, g, m = _level_shard("cpu", torch.float32)
+    shard.calibrate(256)
+    assert shard.lvl_sig is not None and torch.isfinite(shard.lvl_sig).all()
+    # the spread of an 8-point mean against 3 earlier days: sigma * sqrt((1 + 1/3) / 8) ~ 0.41
+    assert 0.25 < float(shard.lvl_sig.median()) < 0.6
+    shifted = torch.arange(8)
+    _level_ticks(shard, g, m, shifted)
+    zl = shard.level_z()
+    z = zl.abs().amax(1)
+    assert bool((z[shifted] > 5.5).all()), z[shifted]
+    assert int((z[8:] > 5.5).sum()) == 0
+    shard.threshold = 1e9  # AE term off: the verdict is the level term alone
+    out = shard.score()
+    assert out["verdict"][:8].all() and int(out["verdict"][8:].sum()) == 0
+
+
+@pytest.mark.gpu
+def test_lstm_level_kernel_matches_cpu():
+    """lstm_level (GPU, bf16 rings) == the torch definition, calibration and scoring."""
+    shard, g, m = _level_shard("cuda", torch.bfloat16, n=300, F=3)
+    shifted = torch.arange(0, 300, 7)
+    _level_ticks(shard, g, m, shifted, k=5)
+    r0 = shard.rings[0]
+    newest, avail = (r0.head + r0.length - 1) % r0.R, r0.length
+    st = L.lstm_level([r.data for r in shard.rings], newest, avail, m, 8, K=20, back_step=9)
+    torch.cuda.synchronize()
+    shard.gpu = False
+    ref = torch.stack([shard._level_stat_cpu((k + 1) * 9) for k in range(20)])
+    shard.gpu = True
+    torch.testing.assert_close(st.cpu(), ref.cpu(), rtol=1e-5, atol=1e-4, equal_nan=True)
+    shard.calibrate(256)
+    zl = shard.level_z()
+    shard.gpu = False
+    zref = shard.level_z()
+    shard.gpu = True
+    torch.testing.assert_close(zl.cpu(), zref.cpu(), rtol=1e-4, atol=1e-4)
+    assert bool((zl.abs().amax(1)[shifted] > 5.5).all())

@@ -44,7 +44,7 @@ def test_module_local_struct_sizes(lib):
     """Structs declared next to their kernels (lstm / lstm_train / decompose)."""
     from foremast_amd.ops import kernels, lstm, lstm_train, pack
     for sym, cls in (("fm_lstm_args_size", lstm.LstmArgs), ("fm_lstm_train_args_size", lstm_train.LstmTrainArgs),
-                     ("fm_decompose_args_size", kernels.DecompArgs),
+                     ("fm_decompose_args_size", kernels.DecompArgs), ("fm_lstm_level_args_size", lstm.LevelArgs),
                      ("fm_hw_state_args_size", kernels.HwStateArgs),
                      ("fm_hw_update_args_size", kernels.HwUpdateArgs), ("fm_pack_args_size", pack.PackArgs)):
         f = getattr(lib, sym)
