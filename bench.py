@@ -139,6 +139,9 @@ def parse():
     p.add_argument("--lstm-restat-every", type=int, default=16,
                    help="ticks between refreshes of the per-series normalisation statistics (window_stats over the ring)")
     p.add_argument("--lstm-autograd", action="store_true", help="train with autograd instead of the fused K7 kernel")
+    p.add_argument("--lstm-threshold", type=float, default=4.0, help="AE reconstruction z threshold")
+    p.add_argument("--lstm-level-threshold", type=float, default=5.5,
+                   help="level-term |z| threshold (<= 0: no level term)")
     p.add_argument("--lstm-no-overlap", action="store_true",
                    help="run the training step and scoring back to back instead of on two HIP streams")
     a = p.parse_args()
@@ -534,9 +537,10 @@ def setup_lstm(args, world, rank, dev, n_features, fp8):
     n_apps = (n_ent + ent_per_app - 1) // ent_per_app
     app_id = (torch.arange(s, e, device=dev, dtype=torch.int64) // ent_per_app).to(torch.int32)
     shard = LstmShard(n_local, args.ring, F, window=args.lstm_window, hidden=64, fp8=fp8, device=dev,
-                      app_id=app_id, n_apps=n_apps, threshold=4.0, train_batch=args.lstm_train_batch,
-                      lr=1e-3, seed=0, fused_train=not args.lstm_autograd, restat_every=args.lstm_restat_every,
-                      season=args.season)
+                      app_id=app_id, n_apps=n_apps, threshold=args.lstm_threshold,
+                      train_batch=args.lstm_train_batch, lr=1e-3, seed=0, fused_train=not args.lstm_autograd,
+                      restat_every=args.lstm_restat_every, season=args.season,
+                      level_threshold=args.lstm_level_threshold if args.lstm_level_threshold > 0 else None)
     params = [synthetic_params(n_ent, dev, seed=1234 + 7 * f, rows=(s, e)) for f in range(F)]
     shard.load_history([synthetic_eval(p, 0, args.ring, args.season, noise_seed=555 + f, row0=s)
                         for f, p in enumerate(params)])

@@ -35,11 +35,12 @@ trained model without absorbing a regression that builds up over ticks.
 Level term: the autoencoder scores the *shape* of a z-scored 32-point window,
 so a level shift of a few noise sigmas inside the daily swing is weak evidence
 for it (round-2 sweep: +3 sigma recall 0.24).  Each tick ``lstm_level``
-(csrc/lstm.hip) computes, per (series, feature), the mean over the newest
-``level_points`` samples of x_t minus the same minutes' mean over the previous
-days the ring holds (<= 7), divided by that statistic's own spread — calibrated
-on the series' history as the RMS of the statistic at ``level_cal`` earlier
-offsets (:meth:`calibrate`).  A window is anomalous when the AE z-score OR any
+(csrc/lstm.hip) computes, per (series, feature), the mean of the newest 8
+samples minus its forecast from the earlier days the ring holds (<= 7): the
+centred (up to) 32-point mean around the same minutes of each day, extrapolated to
+today by least squares over the days (a linear trend across days cancels),
+divided by that statistic's own spread — calibrated on the series' history as
+the RMS of the statistic at ``level_cal`` earlier offsets (:meth:`calibrate`).  A window is anomalous when the AE z-score OR any
 feature's ``|level z|`` exceeds its threshold (``level_threshold``; the
 epilogue also keeps such windows out of the calibration refresh).
 """
@@ -99,6 +100,8 @@ class LstmShard:
         self.cal_windows, self.cal_ewma = cal_windows, cal_ewma
         self.cal: Optional[torch.Tensor] = None  # [n, 2] (mu_i, 1 / (rho * mu_i)) after calibrate()
         self.rho = 1.0
+        if level_points != 8:
+            raise ValueError("level_points: the level kernel averages the newest 8 points")
         self.season, self.level_points, self.level_cal = int(season), int(level_points), int(level_cal)
         self.level_threshold = level_threshold
         self.lvl_sig: Optional[torch.Tensor] = None  # [n, F] spread of the level statistic after calibrate()
@@ -330,10 +333,15 @@ class LstmShard:
         self.calibrate_level(rows)
 
     # ------------------------------------------------------------------ level term
+    @property
+    def LVL_E(self) -> int:  # extra minutes each side of the earlier days' windows (ops/lstm.py)
+        from ..ops.lstm import level_extension
+        return level_extension(self.season)
+
     def _level_geometry(self):
         r0 = self.rings[0]
         L, m, avail = self.level_points, self.season, r0.length
-        back_max = avail - L - m  # offsets keep at least one earlier day behind them
+        back_max = avail - (L + self.LVL_E) - m  # offsets keep at least one earlier day behind them
         if self.level_threshold is None or back_max < L:
             return None
         step = max(L, min(back_max, m) // max(self.level_cal, 1))
@@ -342,22 +350,38 @@ class LstmShard:
 
     def _level_stat_cpu(self, back: int) -> torch.Tensor:
         """The level statistic ``[n, F]`` ending ``back`` samples before the newest
-        (same definition as ``lstm_level_kernel``)."""
+        (same definition as ``lstm_level_kernel``): the newest ``L`` points' mean minus
+        its least-squares extrapolation over the earlier days' centred 32-point means."""
         r0 = self.rings[0]
-        L, m, avail = self.level_points, self.season, r0.length
-        D = min(7, (avail - back - L) // m)
+        L, E, m, avail = self.level_points, self.LVL_E, self.season, r0.length
+        W = L + 2 * E
+        D = min(7, (avail - back - (L + E)) // m)
         out = torch.full((self.n, self.F), float("nan"), device=self.device)
         if D < 1:
             return out
-        i = torch.arange(L, device=self.device)
+        p = torch.arange(W, device=self.device)
         d = torch.arange(D + 1, device=self.device)
-        logical = avail - 1 - back - (L - 1 - i)[None, :] - d[:, None] * m  # [D+1, L]
+        logical = avail - 1 - back - (L + E - 1) + p[None, :] - d[:, None] * m  # [D+1, W]
         cols = (r0.head + logical) % r0.R
+        fd = d[1:].to(torch.float32)
         for f, ring in enumerate(self.rings):
-            x = ring.data[:, cols.reshape(-1)].float().view(self.n, D + 1, L)
-            base = torch.nanmean(x[:, 1:], 1)
-            r = x[:, 0] - base
-            out[:, f] = torch.nanmean(r, 1)
+            x = ring.data[:, cols.reshape(-1)].float().view(self.n, D + 1, W)
+            today = torch.nanmean(x[:, 0, E:E + L], 1)
+            b = torch.nanmean(x[:, 1:], 2)  # [n, D]
+            ok = torch.isfinite(b)
+            w = ok.float()
+            s0 = w.sum(1)
+            s1 = (w * fd).sum(1)
+            s2 = (w * fd * fd).sum(1)
+            bz = torch.where(ok, b, 0.0)
+            sb = bz.sum(1)
+            sdb = (bz * fd).sum(1)
+            dbar = s1 / s0.clamp(min=1)
+            bbar = sb / s0.clamp(min=1)
+            sdd = s2 - s1 * dbar
+            slope = torch.where(sdd > 1e-6, (sdb - s1 * bbar) / sdd.clamp(min=1e-6), 0.0)
+            st = today - (bbar - slope * dbar)
+            out[:, f] = torch.where((s0 > 0) & torch.isfinite(today), st, float("nan"))
         return out
 
     def calibrate_level(self, rows: Optional[torch.Tensor] = None) -> None:
@@ -395,7 +419,7 @@ class LstmShard:
         if self.lvl_sig is None or self.level_threshold is None:
             return None
         r0 = self.rings[0]
-        if r0.length < self.level_points + self.season:
+        if r0.length < self.level_points + self.LVL_E + self.season:
             return None
         if self.gpu:
             from ..ops import lstm as L

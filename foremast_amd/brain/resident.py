@@ -60,11 +60,15 @@ def range_url(endpoint: str, selector: str, start: float, n: int, step: float) -
 
 
 async def fetch_decode(prom, reqs: Sequence[Tuple[str, float, int, int]], tables: Sequence[native.KeyTable],
-                       out: np.ndarray, step: float, threads: int) -> List[bool]:
+                       out: np.ndarray, step: float, threads: int,
+                       timings: Optional[Dict[str, float]] = None) -> List[bool]:
     """Fetch ``reqs`` = (url, start, n_points, col0) and scatter every body through
     its key table into ``out`` (one native call on a thread pool, off the event
-    loop).  Returns per request whether it was fetched and decoded."""
+    loop).  Returns per request whether it was fetched and decoded; ``timings``
+    receives ``fetch_ms`` / ``native_ms`` / ``resume_ms`` (executor hand-back)."""
+    t0 = time.perf_counter()
     bodies = await prom.fetch_raw_many([u for u, *_ in reqs])
+    t1 = time.perf_counter()
     ok = [not isinstance(b, Exception) for b in bodies]
     for (url, *_), b in zip(reqs, bodies):
         if isinstance(b, Exception):
@@ -74,8 +78,19 @@ async def fetch_decode(prom, reqs: Sequence[Tuple[str, float, int, int]], tables
         return ok
     args = ([bodies[j] for j in good], [tables[j] for j in good], [reqs[j][1] for j in good],
             [reqs[j][2] for j in good], [reqs[j][3] for j in good])
-    stats = await asyncio.get_running_loop().run_in_executor(
-        None, lambda: native.decode_bodies(args[0], args[1], args[2], step, args[3], args[4], out, threads=threads))
+    span = [0.0, 0.0]
+
+    def run():
+        span[0] = time.perf_counter()
+        r = native.decode_bodies(args[0], args[1], args[2], step, args[3], args[4], out, threads=threads)
+        span[1] = time.perf_counter()
+        return r
+    stats = await asyncio.get_running_loop().run_in_executor(None, run)
+    if timings is not None:
+        t2 = time.perf_counter()
+        timings["fetch_ms"] = (t1 - t0) * 1e3
+        timings["native_ms"] = (span[1] - span[0]) * 1e3
+        timings["resume_ms"] = ((span[0] - t1) + (t2 - span[1])) * 1e3
     for j, (series, _dropped, _unmatched) in zip(good, stats):
         if series < 0:
             log.warning("malformed response for %s", reqs[j][0].split("?")[0])

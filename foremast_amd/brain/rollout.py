@@ -874,7 +874,8 @@ class RolloutMonitor:
         reqs = [(range_url(fam[0], fam[1], first, k, self.step), first, k, 0) for fam in tables]
         self.tick_queries += len(reqs)
         t0 = time.perf_counter()
-        ok = await fetch_decode(self.prom, reqs, list(tables.values()), block, self.step, self.decode_threads)
+        ok = await fetch_decode(self.prom, reqs, list(tables.values()), block, self.step, self.decode_threads,
+                                timings=self.timings)
         self.timings["decode_ms"] = (time.perf_counter() - t0) * 1e3
         if not all(ok):
             return  # t_cur stays: the next tick fetches these minutes again

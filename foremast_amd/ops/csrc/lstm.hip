@@ -56,12 +56,17 @@ struct LstmArgs {
 
 // Level term of the LSTM-AE verdict (lstm_level_kernel): the autoencoder scores the SHAPE
 // of a z-scored window, so a level shift of a few noise sigmas inside the daily swing is
-// weak evidence for it.  The level statistic of (series, feature) is the mean over the
-// newest L points of x_t - mean_{d=1..D} x_{t - d m} (the same minutes of the D previous
-// days, D <= 7 as the ring allows): ~N(0, sigma^2 (1 + 1/D) / L) on a healthy series with
-// a stable daily profile, so a +3 sigma shift reaches ~7 of its own spreads after 8 points.
-// Its spread per (series, feature) is calibrated on the series' own history: the RMS of the
-// statistic at K earlier offsets (calibration mode writes the raw statistics).
+// weak evidence for it.  The level statistic of (series, feature): the mean of the newest 8
+// points minus its forecast from the earlier days — for each day d = 1..D (D <= 7 as the ring
+// allows) the mean of the 32 points centred on the same minutes (b_d: 4x the points, and the
+// daily profile's slope cancels in a centred window; E = 12 extra minutes each side for a
+// 1440-minute day, fewer for short seasons where the profile's curvature would bias it), extrapolated to d = 0 by least squares
+// over d (a linear trend across days cancels too; D = 1: b_1).  On a healthy series that is
+// ~N(0, sigma^2 (1/8 + ~0.9/32)), so a +3 sigma shift of the newest 7 points is ~6.7 of its own
+// spreads.  The spread per (series, feature) is calibrated on the series' own history: the
+// RMS of the statistic at K earlier offsets (calibration mode writes the raw statistics).
+constexpr int LVL_L = 8;      // newest points averaged
+constexpr int LVL_EMAX = 12;  // extra minutes each side of the earlier days' windows (<= 32 points)
 struct LevelArgs {
   LstmRingSrc src;   // rings, ld, ring_len, bf16 (start_col / windows unused)
   int N;
@@ -69,7 +74,8 @@ struct LevelArgs {
   int newest;        // physical column of the newest sample
   int avail;         // valid samples in the rings
   int m;             // samples per day
-  int L;             // points averaged, 1..8
+  int L;             // points averaged: LVL_L (checked)
+  int E;             // extra points each side of the earlier days' windows, 0..LVL_EMAX
   int K;             // calibration: number of offsets (grid.y); 0: scoring
   int back_step;     // calibration: offset k ends (k + 1) * back_step samples before the newest
   const float* sig;  // scoring: [N, F] spread of the statistic
@@ -252,40 +258,57 @@ __global__ __launch_bounds__(256, 2) void lstm_ae_kernel(const LstmArgs a) {
   }
 }
 
-// one wave per (series, feature): lane = 8 d + i holds x at point i of day d back
+// one wave per (series, feature): lane = 8 d + q holds points 4q .. 4q+3 of day d's 32-point
+// window (today: only the newest 8 of them)
 __global__ __launch_bounds__(256) void lstm_level_kernel(const LevelArgs a) {
   const long long gw = (long long)blockIdx.x * (blockDim.x / FM_WAVE) + wave_id();
   if (gw >= (long long)a.N * a.F) return;  // wave-uniform
   const int n = (int)(gw / a.F), f = (int)(gw - (long long)n * a.F);
-  const int lane = lane_id(), d = lane >> 3, i = lane & 7;
+  const int lane = lane_id(), d = lane >> 3, q = lane & 7;
   const int back = a.K > 0 ? ((int)blockIdx.y + 1) * a.back_step : 0;
-  const int D = min(7, (a.avail - back - a.L) / a.m);
+  const int E = a.E, W = LVL_L + 2 * E;
+  const int D = min(7, (a.avail - back - (LVL_L + E)) / a.m);
   const int R = a.src.ring_len;
-  float x = 0.f;
-  bool ok = false;
-  if (D >= 1 && d <= D && i < a.L) {
-    int c = (a.newest - back - (a.L - 1 - i) - d * a.m) % R;
-    c += c < 0 ? R : 0;
-    const long long o = (long long)n * a.src.ld + c;
-    x = a.src.bf16 ? bf16_to_f32(((const bf16_t*)a.src.ring[f])[o]) : ((const float*)a.src.ring[f])[o];
-    ok = x == x;
+  // window of day d: points p = 0..W-1 at newest - back - (L + E - 1) + p - d m; today p in [E, E + 8)
+  float s = 0.f, c = 0.f;
+  if (D >= 1 && d <= D) {
+    const long long row = (long long)n * a.src.ld;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int p = 4 * q + j;
+      if (p >= W || (d == 0 && (p < E || p >= E + LVL_L))) continue;
+      int col = (a.newest - back - (LVL_L + E - 1) + p - d * a.m) % R;
+      col += col < 0 ? R : 0;
+      const float x = a.src.bf16 ? bf16_to_f32(((const bf16_t*)a.src.ring[f])[row + col])
+                                 : ((const float*)a.src.ring[f])[row + col];
+      if (x == x) { s += x; c += 1.f; }
+    }
   }
-  // the D earlier days' mean at each point i (lanes i, i + 8, ..., i + 56)
-  float bs = (d >= 1 && ok) ? x : 0.f, bc = (d >= 1 && ok) ? 1.f : 0.f;
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) {  // per day
+    s += __shfl_xor(s, o, FM_WAVE);
+    c += __shfl_xor(c, o, FM_WAVE);
+  }
+  const float today = __shfl(c > 0.f ? s / c : fm_nan(), 0, FM_WAVE);
+  // least squares of the day means b_d over d = 1..D (lanes 8d), extrapolated to d = 0
+  const bool use = q == 0 && d >= 1 && d <= D && c > 0.f;
+  const float b = use ? s / c : 0.f, fd = (float)d;
+  float s0 = use ? 1.f : 0.f, s1 = use ? fd : 0.f, s2 = use ? fd * fd : 0.f, sb = b, sdb = use ? fd * b : 0.f;
 #pragma unroll
   for (int o = 8; o < FM_WAVE; o <<= 1) {
-    bs += __shfl_xor(bs, o, FM_WAVE);
-    bc += __shfl_xor(bc, o, FM_WAVE);
-  }
-  const bool use = d == 0 && ok && bc > 0.f;
-  float r = use ? x - bs / bc : 0.f, rc = use ? 1.f : 0.f;
-#pragma unroll
-  for (int o = 1; o < 8; o <<= 1) {
-    r += __shfl_xor(r, o, FM_WAVE);
-    rc += __shfl_xor(rc, o, FM_WAVE);
+    s0 += __shfl_xor(s0, o, FM_WAVE);
+    s1 += __shfl_xor(s1, o, FM_WAVE);
+    s2 += __shfl_xor(s2, o, FM_WAVE);
+    sb += __shfl_xor(sb, o, FM_WAVE);
+    sdb += __shfl_xor(sdb, o, FM_WAVE);
   }
   if (lane != 0) return;
-  const float st = rc > 0.f ? r / rc : fm_nan();
+  float st = fm_nan();
+  if (s0 > 0.f && today == today) {
+    const float dbar = s1 / s0, bbar = sb / s0, sdd = s2 - s1 * dbar;
+    const float slope = sdd > 1e-6f ? (sdb - s1 * bbar) / sdd : 0.f;
+    st = today - (bbar - slope * dbar);
+  }
   if (a.K > 0) {
     a.out[((long long)blockIdx.y * a.N + n) * a.F + f] = st;
   } else {
@@ -298,7 +321,7 @@ __global__ __launch_bounds__(256) void lstm_level_kernel(const LevelArgs a) {
 
 extern "C" int fm_lstm_level(const LevelArgs* a, hipStream_t st) {
   if (a->N <= 0 || a->F <= 0) return 0;
-  if (a->F > 7 || a->L < 1 || a->L > 8 || a->m < 1 || a->K < 0 || a->K > 65535 || (a->K == 0 && !a->sig) ||
+  if (a->F > 7 || a->L != LVL_L || a->E < 0 || a->E > LVL_EMAX || a->m < LVL_L + 2 * a->E || a->K < 0 || a->K > 65535 || (a->K == 0 && !a->sig) ||
       (a->K > 0 && a->back_step < 1) || a->src.ring_len < 1 || a->newest < 0 || a->newest >= a->src.ring_len)
     return (int)hipErrorInvalidValue;
   const long long waves = (long long)a->N * a->F;

@@ -77,7 +77,8 @@ class LstmArgs(C.Structure):
 
 class LevelArgs(C.Structure):
     _fields_ = [("src", LstmRingSrc), ("N", C.c_int), ("F", C.c_int), ("newest", C.c_int), ("avail", C.c_int),
-                ("m", C.c_int), ("L", C.c_int), ("K", C.c_int), ("back_step", C.c_int), ("sig", C.c_void_p),
+                ("m", C.c_int), ("L", C.c_int), ("E", C.c_int), ("K", C.c_int), ("back_step", C.c_int),
+                ("sig", C.c_void_p),
                 ("out", C.c_void_p)]
 
 
@@ -332,9 +333,16 @@ def lstm_score(p: LstmPacked, x: Optional[torch.Tensor], mu: float = 0.0, sigma:
     return out
 
 
+def level_extension(m: int) -> int:
+    """Extra minutes each side of the earlier days' windows for a season of ``m``
+    samples: 12 for a day of minutes, fewer when the profile's curvature over the
+    window would bias the centred mean."""
+    return max(0, min(12, int(round(m / 120))))
+
+
 def lstm_level(rings: List[torch.Tensor], newest: int, avail: int, m: int, L: int = 8,
                sig: Optional[torch.Tensor] = None, K: int = 0, back_step: int = 0,
-               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+               out: Optional[torch.Tensor] = None, E: Optional[int] = None) -> torch.Tensor:
     """Level statistic of every (row, feature) (see ``LevelArgs`` in csrc/lstm.hip):
     the mean over the newest ``L`` samples of x_t minus the same minutes' mean over
     up to 7 earlier days.  Scoring (``K == 0``): ``[N, F]`` statistic / ``sig``.
@@ -347,7 +355,8 @@ def lstm_level(rings: List[torch.Tensor], newest: int, avail: int, m: int, L: in
                               for r in rings), "one ring per feature, same layout")
     _need(r0.dim() == 2 and r0.stride(1) == 1 and r0.dtype in (torch.bfloat16, torch.float32), "ring layout")
     N, R = r0.shape
-    _need(0 <= newest < R and 1 <= L <= 8 and m >= 1, "level geometry")
+    E = level_extension(m) if E is None else int(E)
+    _need(0 <= newest < R and L == 8 and 0 <= E <= 12 and m >= L + 2 * E, "level geometry")
     dev = r0.device
     if K == 0:
         _need(sig is not None and sig.shape == (N, F) and sig.dtype == torch.float32 and sig.is_contiguous(),
@@ -362,8 +371,8 @@ def lstm_level(rings: List[torch.Tensor], newest: int, avail: int, m: int, L: in
     for f, r in enumerate(rings):
         a.src.ring[f] = r.data_ptr()
     a.src.ld, a.src.ring_len, a.src.bf16 = r0.stride(0), R, int(r0.dtype == torch.bfloat16)
-    a.N, a.F, a.newest, a.avail, a.m, a.L, a.K, a.back_step = N, F, int(newest), int(avail), int(m), int(L), \
-        int(K), int(back_step)
+    a.N, a.F, a.newest, a.avail, a.m, a.L, a.E, a.K, a.back_step = N, F, int(newest), int(avail), int(m), int(L), \
+        E, int(K), int(back_step)
     a.sig, a.out = nat.ptr(sig), out.data_ptr()
     nat.check(lib.fm_lstm_level(C.byref(a), nat.stream_handle(dev)), "fm_lstm_level")
     return out

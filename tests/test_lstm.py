@@ -424,17 +424,26 @@ def test_native_pack_matches_torch_repack(fp8):
     assert torch.equal(p.w_out, ref.w_out) and torch.equal(p.b_out, ref.b_out)
 
 
-def _level_shard(device, dtype, n=64, m=96, days=4, F=2, seed=3):
+def _level_shard(device, dtype, n=64, m=480, days=4, F=2, seed=3):
+    """Seasonal series with noise sigma 1 and, on half of them, a trend of ~5 sigma a day
+    (a naive same-minutes-of-earlier-days baseline would flag every trending series)."""
     from foremast_amd.brain.lstm_engine import LstmShard
     R = m * days
     g = torch.Generator().manual_seed(seed)
-    t = torch.arange(R, dtype=torch.float32)
-    hist = [100.0 + 20.0 * torch.sin(2 * np.pi * t / m)[None, :] + torch.randn(n, R, generator=g)
-            for _ in range(F)]
+    slope = torch.zeros(n, 1)
+    slope[::2] = 5.0 / m
+
+    def values(t, noise):
+        t = torch.as_tensor(t, dtype=torch.float32)
+        return 100.0 + 20.0 * torch.sin(2 * np.pi * t / m) + slope * t + noise
+
+    t = torch.arange(R, dtype=torch.float32)[None, :]
+    hist = [values(t, torch.randn(n, R, generator=g)) for _ in range(F)]
     shard = LstmShard(n, R, F, window=16, hidden=64 if device == "cuda" else 16, device=device, dtype=dtype,
-                      fused_train=False,
-                      cal_windows=4, train_batch=64, season=m, level_points=8, level_threshold=5.5)
+                      fused_train=False, cal_windows=4, train_batch=64, season=m, level_points=8,
+                      level_threshold=5.5)
     shard.load_history([h.to(device) for h in hist])
+    shard._test_values = values
     return shard, g, m
 
 
@@ -442,7 +451,7 @@ def _level_ticks(shard, g, m, shifted, k=8, size=4.0):
     n, F = shard.n, shard.F
     for j in range(k):
         tt = float(shard.rings[0].length + shard.ticks)
-        v = 100.0 + 20.0 * np.sin(2 * np.pi * tt / m) + torch.randn(n, F, generator=g)
+        v = torch.stack([shard._test_values(tt, torch.randn(n, generator=g)[:, None])[:, 0] for _ in range(F)], 1)
         v[shifted] += size
         shard.ingest_tick(v.to(shard.device))
 
@@ -454,8 +463,11 @@ def test_lstm_level_term_flags_small_shift_cpu():
     shard, g, m = _level_shard("cpu", torch.float32)
     shard.calibrate(256)
     assert shard.lvl_sig is not None and torch.isfinite(shard.lvl_sig).all()
-    # the spread of an 8-point mean against 3 earlier days: sigma * sqrt((1 + 1/3) / 8) ~ 0.41
-    assert 0.25 < float(shard.lvl_sig.median()) < 0.6
+    # the spread of an 8-point mean against the 3 earlier days' 16-point means (E = 4 at
+    # m = 480) extrapolated over the days: sigma * sqrt(1/8 + (21/9)/16) ~ 0.52, trending
+    # series included
+    assert 0.35 < float(shard.lvl_sig.median()) < 0.7
+    assert float(shard.lvl_sig[::2].median()) < 1.3 * float(shard.lvl_sig[1::2].median())
     shifted = torch.arange(8)
     _level_ticks(shard, g, m, shifted)
     zl = shard.level_z()
@@ -472,7 +484,7 @@ def test_lstm_level_kernel_matches_cpu():
     """lstm_level (GPU, bf16 rings) == the torch definition, calibration and scoring."""
     shard, g, m = _level_shard("cuda", torch.bfloat16, n=300, F=3)
     shifted = torch.arange(0, 300, 7)
-    _level_ticks(shard, g, m, shifted, k=5)
+    _level_ticks(shard, g, m, shifted, k=8)
     r0 = shard.rings[0]
     newest, avail = (r0.head + r0.length - 1) % r0.R, r0.length
     st = L.lstm_level([r.data for r in shard.rings], newest, avail, m, 8, K=20, back_step=9)
