@@ -140,6 +140,9 @@ def parse():
                    help="ticks between refreshes of the per-series normalisation statistics (window_stats over the ring)")
     p.add_argument("--lstm-autograd", action="store_true", help="train with autograd instead of the fused K7 kernel")
     p.add_argument("--lstm-threshold", type=float, default=4.0, help="AE reconstruction z threshold")
+    p.add_argument("--mv-bf16", action="store_true", help="multivariate config: bf16 scoring instead of fp8")
+    p.add_argument("--lstm-cal-ewma", type=float, default=1.0 / 32,
+                   help="per-series calibration refresh rate of healthy windows")
     p.add_argument("--lstm-level-threshold", type=float, default=5.5,
                    help="level-term |z| threshold (<= 0: no level term)")
     p.add_argument("--lstm-no-overlap", action="store_true",
@@ -539,7 +542,7 @@ def setup_lstm(args, world, rank, dev, n_features, fp8):
     shard = LstmShard(n_local, args.ring, F, window=args.lstm_window, hidden=64, fp8=fp8, device=dev,
                       app_id=app_id, n_apps=n_apps, threshold=args.lstm_threshold,
                       train_batch=args.lstm_train_batch, lr=1e-3, seed=0, fused_train=not args.lstm_autograd,
-                      restat_every=args.lstm_restat_every, season=args.season,
+                      restat_every=args.lstm_restat_every, season=args.season, cal_ewma=args.lstm_cal_ewma,
                       level_threshold=args.lstm_level_threshold if args.lstm_level_threshold > 0 else None)
     params = [synthetic_params(n_ent, dev, seed=1234 + 7 * f, rows=(s, e)) for f in range(F)]
     shard.load_history([synthetic_eval(p, 0, args.ring, args.season, noise_seed=555 + f, row0=s)
@@ -768,7 +771,7 @@ def main():
     elif args.config == "lstm":
         tick, health_host, meta, dtype_name, n_series = setup_lstm(args, world, rank, dev, 1, False)
     else:
-        tick, health_host, meta, dtype_name, n_series = setup_lstm(args, world, rank, dev, 2, True)
+        tick, health_host, meta, dtype_name, n_series = setup_lstm(args, world, rank, dev, 2, not args.mv_bf16)
 
     agg = meta.pop("_agg", None)
     table = meta.pop("_table", None)

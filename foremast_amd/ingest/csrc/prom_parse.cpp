@@ -41,8 +41,13 @@
 #include <cstdint>
 #include <cstring>
 #include <limits>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
+
+#include <unistd.h>
 
 namespace {
 
@@ -800,6 +805,78 @@ long long fm_prom_dense_indexed(const char* buf, long long len, double start, do
   return r;
 }
 
+// Persistent decode workers.  A tick's bodies decode in ~2 ms on 16 threads; creating and
+// joining 15 std::threads per call (stacks mapped and unmapped every time) cost a 10-15 ms
+// stall every few ticks on the GPU hosts.  run() executes fn on n threads (the caller and
+// n - 1 workers) and returns when every one has finished; calls are serialised.  The pool is
+// rebuilt in a forked child (its workers do not exist there) and never joined (process exit).
+namespace {
+class DecodePool {
+ public:
+  void run(int n, const std::function<void()>& fn) {
+    std::lock_guard<std::mutex> call(call_mu_);
+    if (n <= 1) {
+      fn();
+      return;
+    }
+    ensure(n - 1);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = &fn;
+      want_ = n - 1;
+      started_ = 0;
+      done_ = 0;
+      ++gen_;
+    }
+    cv_.notify_all();
+    fn();
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return done_ == want_; });
+    job_ = nullptr;
+  }
+
+ private:
+  void ensure(int k) {
+    std::lock_guard<std::mutex> lk(mu_);
+    // a new worker joins from the NEXT call: it starts from the generation current now (read
+    // at its own start, a call issued meanwhile would be missed and never completed)
+    while ((int)workers_.size() < k) workers_.emplace_back([this, g = gen_] { loop(g); });
+  }
+  void loop(unsigned long long seen) {
+    std::unique_lock<std::mutex> lk(mu_);
+    while (true) {
+      cv_.wait(lk, [&] { return gen_ != seen; });
+      seen = gen_;
+      if (started_ >= want_) continue;  // this call needs fewer workers than the pool has
+      ++started_;
+      const std::function<void()>* f = job_;
+      lk.unlock();
+      (*f)();
+      lk.lock();
+      if (++done_ == want_) done_cv_.notify_one();
+    }
+  }
+  std::mutex call_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<std::thread> workers_;
+  const std::function<void()>* job_ = nullptr;
+  int want_ = 0, started_ = 0, done_ = 0;
+  unsigned long long gen_ = 0;
+};
+
+DecodePool& decode_pool() {
+  static std::mutex mu;
+  static DecodePool* pool = nullptr;
+  static pid_t owner = 0;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!pool || owner != getpid()) {  // first use, or a forked child: a fresh pool (the old one leaks)
+    pool = new DecodePool();
+    owner = getpid();
+  }
+  return *pool;
+}
+}  // namespace
+
 // Many bodies at once: body j (keyed by index[j]) is scattered into columns
 // [col0s[j], col0s[j] + Ts[j]) of `out` ([max_rows, ld] float32) on the
 // (starts[j], step) grid (null arrays: start / T / column 0 for every body) by
@@ -874,11 +951,8 @@ long long fm_prom_decode_bodies(int nb, const char* const* bufs, const long long
     }
   };
   auto run = [&](auto fn) {
-    std::vector<std::thread> pool;
-    pool.reserve(threads - 1);
-    for (int i = 1; i < threads; ++i) pool.emplace_back(fn);
-    fn();
-    for (auto& th : pool) th.join();
+    const std::function<void()> f = fn;
+    decode_pool().run(threads, f);
   };
   if (fill_nan && fc1 > fc0) run(work);
   if (!tasks.empty()) run(parse);
