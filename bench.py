@@ -134,12 +134,13 @@ def parse():
     p.add_argument("--lstm-window", type=int, default=32)
     p.add_argument("--lstm-train-batch", type=int, default=4096)
     p.add_argument("--lstm-train-every", type=int, default=1)
-    p.add_argument("--lstm-pretrain", type=int, default=200,
+    p.add_argument("--lstm-pretrain", type=int, default=800,
                    help="DP training steps of model initialisation before the timed ticks (untimed)")
     p.add_argument("--lstm-restat-every", type=int, default=16,
                    help="ticks between refreshes of the per-series normalisation statistics (window_stats over the ring)")
     p.add_argument("--lstm-autograd", action="store_true", help="train with autograd instead of the fused K7 kernel")
-    p.add_argument("--lstm-threshold", type=float, default=4.0, help="AE reconstruction z threshold")
+    p.add_argument("--lstm-threshold", type=float, default=5.0,
+                   help="AE reconstruction z threshold (5: the level term carries the small shifts)")
     p.add_argument("--mv-bf16", action="store_true", help="multivariate config: bf16 scoring instead of fp8")
     p.add_argument("--lstm-cal-ewma", type=float, default=1.0 / 32,
                    help="per-series calibration refresh rate of healthy windows")

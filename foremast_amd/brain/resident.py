@@ -91,6 +91,7 @@ async def fetch_decode(prom, reqs: Sequence[Tuple[str, float, int, int]], tables
         timings["fetch_ms"] = (t1 - t0) * 1e3
         timings["native_ms"] = (span[1] - span[0]) * 1e3
         timings["resume_ms"] = ((span[0] - t1) + (t2 - span[1])) * 1e3
+        timings["body_mb"] = sum(len(b) for b in args[0]) / 1e6
     for j, (series, _dropped, _unmatched) in zip(good, stats):
         if series < 0:
             log.warning("malformed response for %s", reqs[j][0].split("?")[0])

@@ -871,6 +871,7 @@ class RolloutMonitor:
         P = self.P
         S = len(self.fams) * self.slots.cap
         block_t, block = self._tick_block(S, k)
+        self.timings["points"] = k
         reqs = [(range_url(fam[0], fam[1], first, k, self.step), first, k, 0) for fam in tables]
         self.tick_queries += len(reqs)
         t0 = time.perf_counter()

@@ -8,3 +8,4 @@ run thr4_pre800 $C --lstm-pretrain 800
 run thr5_pre800 $C --lstm-threshold 5 --lstm-pretrain 800
 run thr6 $C --lstm-threshold 6
 run thr5_bf16 --config multivariate --steps 5 --warmup 2 --anomaly-frac 0 --lstm-threshold 5 --mv-bf16
+timeout -k 10 400 python -u bench.py --config node > gpurun_out/node8.json 2> gpurun_out/node8.err || exit 1
