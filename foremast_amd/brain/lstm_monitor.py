@@ -108,7 +108,9 @@ class LstmMonitor:
                                hidden=hidden or self.cfg.lstm_hidden, fp8=bool(fp8) and self.gpu,
                                device=self.device, threshold=self.cfg.lstm_threshold, train_batch=tb, seed=seed,
                                dtype=torch.bfloat16 if self.gpu else torch.float32, dp_overlap=False,
-                               restat_every=1 << 30, season=self.cfg.season)
+                               restat_every=1 << 30, season=self.cfg.season,
+                               level_threshold=(self.cfg.lstm_level_threshold
+                                                if self.cfg.lstm_level_threshold > 0 else None))
         for ring in self.shard.rings:
             ring.state.head, ring.state.length = 0, R
         self.shard.live = torch.zeros(0, dtype=torch.int64, device=self.device)
@@ -124,7 +126,9 @@ class LstmMonitor:
         self.ticks = 0
         self.exchange_timeout = comm.exchange_timeout_s()
         # DP steps before the first calibration of a fresh node's model (FOREMAST_LSTM_PRETRAIN)
-        self.pretrain_steps = int(os.environ.get("FOREMAST_LSTM_PRETRAIN", "200" if self.gpu else "20"))
+        # (800 on the GPU: a model calibrated after 200 steps keeps drifting under the per-tick
+        # training, and its first ticks flag healthy series — profiles/lstm_detection_r3.md)
+        self.pretrain_steps = int(os.environ.get("FOREMAST_LSTM_PRETRAIN", "800" if self.gpu else "20"))
         self.timings: Dict[str, float] = {}
 
     # ------------------------------------------------------------------ membership

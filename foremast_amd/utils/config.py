@@ -63,6 +63,9 @@ class BrainConfig:
     min_historical_points: int = 60
     max_cache_size: int = 1000
     lstm_threshold: float = 4.0  # z-score of the joint reconstruction error (ML_LSTM_THRESHOLD)
+    # resident LSTM engine: |z| of the level term (newest points vs their forecast from the
+    # earlier days); <= 0 turns it off (FOREMAST_LSTM_LEVEL_THRESHOLD)
+    lstm_level_threshold: float = 5.5
     # downstream impact: joint model over each caller's metrics (ML_DOWNSTREAM_ALGORITHM lstm | none)
     downstream_algorithm: str = "lstm"
     # --- MI355X engine knobs -------------------------------------------------------
@@ -137,6 +140,7 @@ class BrainConfig:
                                         c.min_historical_points, int))
         c.max_cache_size = int(f("MAX_CACHE_SIZE", c.max_cache_size, int))
         c.lstm_threshold = f("ML_LSTM_THRESHOLD", c.lstm_threshold)
+        c.lstm_level_threshold = f("FOREMAST_LSTM_LEVEL_THRESHOLD", c.lstm_level_threshold)
         c.downstream_algorithm = (e.get("ML_DOWNSTREAM_ALGORITHM") or c.downstream_algorithm).strip().lower()
         c.dtype = e.get("FOREMAST_DTYPE", c.dtype)
         c.device = e.get("FOREMAST_DEVICE", c.device)
