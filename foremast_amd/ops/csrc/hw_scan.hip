@@ -845,16 +845,24 @@ __global__ __launch_bounds__(256, 2) void hw_half_general_kernel(const SmoothArg
 // the bf16 one (fp32) but holds one season fewer: 2 series x 6 x 1440 x 4 B = 72 KiB per
 // workgroup, two workgroups per CU.  Series pairs with a NaN past season 0 are deferred
 // to hw_half_general_kernel exactly as in variant 4.
+constexpr int D_CHUNK = 260;  // floats per 8-step chunk: 256 + 4 pad (see dl_off)
 template <int K>
 struct DLay {
   static constexpr int NCH = (K + 7) / 8;
   static constexpr int KP = NCH * 8;
-  static constexpr int SEASON = 32 * KP;  // floats per (series, season): [q][h][j][4]
+  static constexpr int SEASON = D_CHUNK * NCH;  // floats per (series, season): [q][h][j][4] + pad
 };
 // float offset of step i of lane j inside a season block: lanes are 16 B apart within a
-// half-chunk, so each ds_read_b128 lane group hits 16 distinct 16-B slots (no conflicts)
-__device__ __forceinline__ int dl_off(int i, int j) { return ((i >> 3) * 2 + ((i >> 2) & 1)) * 128 + j * 4 + (i & 3); }
+// half-chunk, so each ds_read_b128 lane group hits 16 distinct 16-B slots (no conflicts).
+// Chunk q starts 4 floats further than 256 q: the stage phase writes, per instruction, the
+// ~6 steps i = i0 + 8k of one lane from 6 threads, which without the pad all hit bank
+// 4 j + (i & 3); with it they land 4 banks apart (at most 2-way, lanes 4 apart with
+// chunks 4 apart).
+__device__ __forceinline__ int dl_off(int i, int j) {
+  return (i >> 3) * D_CHUNK + ((i >> 2) & 1) * 128 + j * 4 + (i & 3);
+}
 
+constexpr int D_WAVES = 4;   // waves per hw_d workgroup (launched with 256 threads)
 constexpr int D_MAXSEG = 7;  // seasons staged per series (LDS budget: 6 fp32 blocks)
 
 struct Chunk8f {
@@ -909,7 +917,7 @@ __device__ __forceinline__ void d_pass1(const float* blk, cfp W, v2f* D, v2f& p1
 #pragma unroll
   for (int q = 0; q < NCH; ++q) {
     Chunk8f c;
-    c.load(blk + q * 256);
+    c.load(blk + q * D_CHUNK);
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const int i = 8 * q + r;
@@ -978,7 +986,7 @@ __device__ __forceinline__ void d_pass2(const float* blk, v2f* D, v2f c1, v2f c2
       asm volatile("" ::"v"(cc.lo.x), "v"(cc.hi.x), "s"(wc[0].x));
       if (q + 1 < NCH) {
         W = launder(W);
-        cn.load(blk + (q + 1) * 256);
+        cn.load(blk + (q + 1) * D_CHUNK);
 #pragma unroll
         for (int r = 0; r < 16; ++r)
           if (16 * (q + 1) + r < 2 * K) wn[r] = ldv2(W + 32 * (q + 1) + 2 * r);
@@ -1016,16 +1024,16 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
   const bool odd_row = ((lane >> 4) & 1) != 0;
   const int nseg = a.Tp / a.seg, m = a.m, ns1 = nseg - 1;
 
-  // ---- LDS: dl[2][ns1][SEA] | vmask[2][NMW] | stat[2][4] | flag | ylast[2][HB] | bests[4][2][HB] | wbest[4][2][4]
+  // ---- LDS: dl[2][ns1][SEA] | vmask[2][NMW] | stat[4 waves][2][4] | flag | ylast[2][HB] | bests[4][2][HB] | wbest[4][2][4]
   float* dl = (float*)fm_hw_smem;
   unsigned* vmask = (unsigned*)(dl + (size_t)2 * ns1 * SEA);
   float* stat = (float*)(vmask + 2 * NMW);
-  int* flag = (int*)(stat + 8);
+  int* flag = (int*)(stat + 8 * D_WAVES);
   float* ylast = (float*)(flag + 4);
   float* bests = ylast + 2 * HALF_HB;
   float* wbest = bests + 4 * 2 * HALF_HB;
 
-  for (int i = tid; i < 2 * NMW + 8 + 4; i += blockDim.x) vmask[i] = 0u;  // vmask, stat, flag
+  for (int i = tid; i < 2 * NMW + 8 * D_WAVES + 4; i += blockDim.x) vmask[i] = 0u;  // vmask, stat, flag
   const int head = a.head_dev ? *a.head_dev : a.head;
   __syncthreads();
 
@@ -1128,9 +1136,12 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
     }
     s0 = wave_sum(s0); c0 = wave_sum(c0); s1 = wave_sum(s1); c1 = wave_sum(c1);
     s0b = wave_sum(s0b); c0b = wave_sum(c0b); s1b = wave_sum(s1b); c1b = wave_sum(c1b);
+    // per-wave slots summed in wave order below: a float atomicAdd's order would make l0 / b0
+    // (and a beta = 0 fit's trend) differ in the last bit from run to run
     if (lane == 0) {
-      atomicAdd(&stat[0], s0); atomicAdd(&stat[1], c0); atomicAdd(&stat[2], s1); atomicAdd(&stat[3], c1);
-      atomicAdd(&stat[4], s0b); atomicAdd(&stat[5], c0b); atomicAdd(&stat[6], s1b); atomicAdd(&stat[7], c1b);
+      float* sw = stat + 8 * w;
+      sw[0] = s0; sw[1] = c0; sw[2] = s1; sw[3] = c1;
+      sw[4] = s0b; sw[5] = c0b; sw[6] = s1b; sw[7] = c1b;
     }
     if (bad) atomicOr(flag, 1);
   }
@@ -1145,7 +1156,11 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
   float l0r[2], b0r[2];
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
-    const float* st = stat + 4 * r;
+    float st[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int v = 0; v < D_WAVES; ++v)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) st[u] += stat[8 * v + 4 * r + u];
     l0r[r] = st[1] > 0.f ? st[0] / st[1] : 0.f;
     b0r[r] = ((st[3] > 0.f ? st[2] / st[3] : 0.f) - l0r[r]) / (float)m;
   }
@@ -1316,7 +1331,7 @@ extern "C" size_t fm_hw_d_lds_bytes(int Tp, int seg, int K) {
   const int nseg = Tp / seg;
   if (nseg < 2 || nseg > D_MAXSEG) return (size_t)-1;
   const int NMW = (32 * K + 31) / 32;
-  return ((size_t)2 * (nseg - 1) * DLay<45>::SEASON + 2 * NMW + 8 + 4 + 2 * HALF_HB + 4 * 2 * HALF_HB + 4 * 2 * 4) * 4;
+  return ((size_t)2 * (nseg - 1) * DLay<45>::SEASON + 2 * NMW + 8 * D_WAVES + 4 + 2 * HALF_HB + 4 * 2 * HALF_HB + 4 * 2 * 4) * 4;
 }
 
 // Deferred detection for HW variants 4/5: band, verdict, per-app counters and the K9
