@@ -21,6 +21,7 @@
 #include "detect.h"
 #include "args.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 extern __shared__ __attribute__((aligned(16))) char fm_hw_smem[];
@@ -908,6 +909,34 @@ __device__ __forceinline__ v2f half_last_bp(v2f x, int src_addr) {
   return r;
 }
 
+// sum over each 32-lane half, valid in lanes 31 and 63 only: DPP row scans (row_shr
+// 1/2/4/8) then row_bcast:15 into rows 1 / 3.  One fixed tree of adds, so a sum of
+// larger operands is never smaller (the grid branch and bound relies on it).
+__device__ __forceinline__ v2f half_sum_last(v2f v) {
+  // v_add_f32 with a DPP source (LLVM would re-pack separate adds into v_pk_add_f32,
+  // which takes no DPP operand); s_nop 1 covers the VALU-write -> DPP-read hazard.
+  // row_bcast:15 writes rows 1 / 3 only: rows 0 / 2 keep their value.
+  asm volatile(
+      "s_nop 1\n"
+      "v_add_f32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "v_add_f32_dpp %1, %1, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "s_nop 1\n"
+      "v_add_f32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "v_add_f32_dpp %1, %1, %1 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "s_nop 1\n"
+      "v_add_f32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "v_add_f32_dpp %1, %1, %1 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "s_nop 1\n"
+      "v_add_f32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "v_add_f32_dpp %1, %1, %1 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "s_nop 1\n"
+      "v_add_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
+      "v_add_f32_dpp %1, %1, %1 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
+      "s_nop 1"
+      : "+v"(v.x), "+v"(v.y));
+  return v;
+}
+
 // pass 1 of season 1: D_i = splat(D1_i), v = sum_i W_i D1_i
 template <int K>
 __device__ __forceinline__ void d_pass1(const float* blk, cfp W, v2f* D, v2f& p1, v2f& p2) {
@@ -965,7 +994,8 @@ __device__ __forceinline__ void d_steps(int q, const Chunk8f& cc, v2f* D, v2f c1
 template <int K, bool FUSE>
 __device__ __forceinline__ void d_pass2(const float* blk, v2f* D, v2f c1, v2f c2, v2f g1a, cfp W, v2f& x1,
                                         v2f& x2, v2f& sse, v2f& p1, v2f& p2, cfp tb = nullptr,
-                                        Mat2* Bn = nullptr) {
+                                        Mat2* Bn = nullptr, bool chk = false, const unsigned* ubp = nullptr,
+                                        int* alive = nullptr) {
   constexpr int NCH = (K + 7) / 8;
   if (FUSE) { p1 = splat2(0.f); p2 = splat2(0.f); }
   fence_sched();
@@ -979,6 +1009,18 @@ __device__ __forceinline__ void d_pass2(const float* blk, v2f* D, v2f c1, v2f c2
   }
 #pragma unroll
   for (int q = 0; q < NCH; ++q) {
+    if (FUSE && q + 1 == NCH && chk) {
+      // grid branch and bound (hw_d_block): the SSE before the season's last chunk is a
+      // lower bound of the pair's final SSE.  Checked here, before the B prefetch, where
+      // the scalar registers of the next chunk's weights are free.
+      // Only lanes 31 / 63 hold their half's sum and vote; the wave keeps the pair while
+      // either of them does (the caller's __any).
+      const v2f s = half_sum_last(sse);  // the same sum as the final SSE
+      const float U = __uint_as_float(__hip_atomic_load(ubp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+      int v = ((lane_id() & 31) == 31 && !(s.x > U && s.y > U)) ? 1 : 0;
+      asm volatile("" : "+v"(v));  // the flag lives in a VGPR: no scalar register across the loop
+      *alive = v;
+    }
     if (FUSE) {
       cc = cn;
 #pragma unroll
@@ -1013,7 +1055,7 @@ __device__ __forceinline__ void d_pass2(const float* blk, v2f* D, v2f c1, v2f c2
 // `hid`), and whichever half arrives second merges the two and finishes the series.
 constexpr int CAND_FLOATS = 4 + HALF_HB;  // SSE, index bits, level, trend, seasonal phases
 
-template <int K>
+template <int K, bool PRUNE>
 __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0, int* deferred, int pi_lo,
                                            int pi_hi, int slot, int hid, int* cnt, float* cand) {
   constexpr int SEA = DLay<K>::SEASON;
@@ -1025,6 +1067,7 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
   const int nseg = a.Tp / a.seg, m = a.m, ns1 = nseg - 1;
 
   // ---- LDS: dl[2][ns1][SEA] | vmask[2][NMW] | stat[4 waves][2][4] | flag | ylast[2][HB] | bests[4][2][HB] | wbest[4][2][4]
+  //          | ubound[4]
   float* dl = (float*)fm_hw_smem;
   unsigned* vmask = (unsigned*)(dl + (size_t)2 * ns1 * SEA);
   float* stat = (float*)(vmask + 2 * NMW);
@@ -1032,8 +1075,10 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
   float* ylast = (float*)(flag + 4);
   float* bests = ylast + 2 * HALF_HB;
   float* wbest = bests + 4 * 2 * HALF_HB;
+  unsigned* ubound = (unsigned*)(wbest + 4 * 2 * 4);  // [2] per-series SSE bound, [2] pair queue
 
   for (int i = tid; i < 2 * NMW + 8 * D_WAVES + 4; i += blockDim.x) vmask[i] = 0u;  // vmask, stat, flag
+  if (tid < 4) ubound[tid] = tid < 2 ? 0x7f800000u : 0u;  // +inf, +inf, queue 0
   const int head = a.head_dev ? *a.head_dev : a.head;
   __syncthreads();
 
@@ -1181,11 +1226,15 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
   int bestIdx = 0x7fffffff;
   float bestL = l0, bestB = b0;
   float* mybest = bests + (w * 2 + half) * HALF_HB;
-  const int npairs = (a.G + 1) / 2;
   const int nwaves = blockDim.x / FM_WAVE;
+  // Exact branch and bound over the grid (PRUNE): ubound[half] is the smallest
+  // complete SSE any wave of this block has found for that series.  A per-lane SSE only
+  // grows (fl(s + e*e) >= s) and the butterfly sum is monotone in its operands, so a
+  // pair whose partial sum after season sg already exceeds the bound (strictly, for both
+  // series and both grid points) ends above it and can never be the argmin or tie it:
+  // the wave drops it and takes the next pair from the block's queue.
 
-  (void)npairs;
-  for (int pi = pi_lo + w; pi < pi_hi; pi += nwaves) {
+  for (int pi = pi_lo + w; pi < pi_hi;) {
     const int c0 = 2 * pi;
     const int c1i = (2 * pi + 1 < a.G) ? 2 * pi + 1 : c0;
     const cfp tab = const_ptr(a.pair_tab + (size_t)pi * TS);
@@ -1206,35 +1255,45 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
     v2f X1 = splat2(l0 + b0), X2 = splat2(b0), sse = zero;  // (f, b) at the season start
     v2f p1, p2;
     d_pass1<K>(mydl, W, D, p1, p2);
+    int alive = 1;  // per lane: 0 once this lane's partial SSEs exceed the bound (read wave-wide)
     for (int sg = 1; sg < nseg - 1; ++sg) {
       v2f x1, x2;
       half_uniform_scan_pre(Bp, launder(tb), p1, p2, X1, X2, Bj, odd_row, x1, x2);
-      d_pass2<K, true>(mydl + (size_t)sg * SEA, D, c1, c2, g1a, launder(W), x1, x2, sse, p1, p2, tb, Bp);
+      // checked in seasons max(2, nseg - 4) .. nseg - 2
+      d_pass2<K, true>(mydl + (size_t)sg * SEA, D, c1, c2, g1a, launder(W), x1, x2, sse, p1, p2, tb, Bp,
+                       PRUNE, ubound + half, &alive);
       X1 = half_last_bp(x1, last_addr);
       X2 = half_last_bp(x2, last_addr);
+      if (PRUNE && !__any(alive)) break;
     }
-    {
+    if (!PRUNE || __any(alive)) {
       v2f x1, x2, d1, d2;
       half_uniform_scan_pre(Bp, tb, p1, p2, X1, X2, Bj, odd_row, x1, x2);
       d_pass2<K, false>(mydl, D, c1, c2, g1a, W, x1, x2, sse, d1, d2);
       X1 = half_last_bp(x1, last_addr);
       X2 = half_last_bp(x2, last_addr);
-    }
+      sse = half_sum_last(sse);
+      sse = half_last_bp(sse, last_addr);  // lane 31 / 63 -> the whole half
+      const bool upd0 = (sse.x < bestSSE || (sse.x == bestSSE && c0 < bestIdx));
+      if (upd0) { bestSSE = sse.x; bestIdx = c0; bestL = X1.x - X2.x; bestB = X2.x; }
+      const bool upd1 = (c1i != c0) && (sse.y < bestSSE || (sse.y == bestSSE && c1i < bestIdx));
+      if (upd1) { bestSSE = sse.y; bestIdx = c1i; bestL = X1.y - X2.y; bestB = X2.y; }
+      if (j == 0 && (upd0 || upd1)) {
+        const float* yl = ylast + half * HALF_HB;
 #pragma unroll
-    for (int o = 16; o > 0; o >>= 1) {
-      sse.x += __shfl_xor(sse.x, o, FM_WAVE);
-      sse.y += __shfl_xor(sse.y, o, FM_WAVE);
+        for (int i = 0; i < K && i < HALF_HB; ++i)
+          if (i < hmax) mybest[i] = yl[i] - (upd1 ? D[i].y : D[i].x);
+      }
+      // publish the bound (SSE >= 0: float order is unsigned-int order; a NaN never lowers it)
+      if (PRUNE && j == 0 && (upd0 || upd1))
+        __hip_atomic_fetch_min(ubound + half, __float_as_uint(bestSSE), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    const bool upd0 = (sse.x < bestSSE || (sse.x == bestSSE && c0 < bestIdx));
-    if (upd0) { bestSSE = sse.x; bestIdx = c0; bestL = X1.x - X2.x; bestB = X2.x; }
-    const bool upd1 = (c1i != c0) && (sse.y < bestSSE || (sse.y == bestSSE && c1i < bestIdx));
-    if (upd1) { bestSSE = sse.y; bestIdx = c1i; bestL = X1.y - X2.y; bestB = X2.y; }
-    if (j == 0 && (upd0 || upd1)) {
-      const float* yl = ylast + half * HALF_HB;
-#pragma unroll
-      for (int i = 0; i < K && i < HALF_HB; ++i)
-        if (i < hmax) mybest[i] = yl[i] - (upd1 ? D[i].y : D[i].x);
-    }
+    // next pair: the first round is static (pi_lo + w), later ones come from the queue
+    int k = 0;
+    if (lane == 0)
+      k = __hip_atomic_fetch_add(ubound + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    pi = pi_lo + nwaves + __builtin_amdgcn_readfirstlane(k);
   }
 
   // ---- arg-min across the 4 waves; wave r finishes series n0 + r ----------------------
@@ -1313,17 +1372,17 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
 
 // Workgroups [0, n_full) fit whole series pairs 0..n_full-1; the rest are split-tail
 // halves: workgroup n_full + 2 s + h fits half h of the grid of pair n_full + s.
-template <int K>
+template <int K, bool PRUNE>
 __global__ __launch_bounds__(256, 2) void hw_d_kernel(const SmoothArgs a, int hmax, int* deferred, int n_full,
                                                      int* cnt, float* cand) {
   const int b = blockIdx.x;
   const int npairs = (a.G + 1) / 2;
   if (b < n_full) {
-    hw_d_block<K>(a, hmax, 2 * b, deferred, 0, npairs, -1, 0, cnt, cand);
+    hw_d_block<K, PRUNE>(a, hmax, 2 * b, deferred, 0, npairs, -1, 0, cnt, cand);
     return;
   }
   const int item = b - n_full, slot = item >> 1, h = item & 1, mid = npairs / 2;
-  hw_d_block<K>(a, hmax, 2 * (n_full + slot), deferred, h ? mid : 0, h ? npairs : mid, slot, h, cnt, cand);
+  hw_d_block<K, PRUNE>(a, hmax, 2 * (n_full + slot), deferred, h ? mid : 0, h ? npairs : mid, slot, h, cnt, cand);
 }
 
 extern "C" size_t fm_hw_d_lds_bytes(int Tp, int seg, int K) {
@@ -1331,7 +1390,8 @@ extern "C" size_t fm_hw_d_lds_bytes(int Tp, int seg, int K) {
   const int nseg = Tp / seg;
   if (nseg < 2 || nseg > D_MAXSEG) return (size_t)-1;
   const int NMW = (32 * K + 31) / 32;
-  return ((size_t)2 * (nseg - 1) * DLay<45>::SEASON + 2 * NMW + 8 * D_WAVES + 4 + 2 * HALF_HB + 4 * 2 * HALF_HB + 4 * 2 * 4) * 4;
+  return ((size_t)2 * (nseg - 1) * DLay<45>::SEASON + 2 * NMW + 8 * D_WAVES + 4 + 2 * HALF_HB + 4 * 2 * HALF_HB + 4 * 2 * 4 +
+          4) * 4;
 }
 
 // Deferred detection for HW variants 4/5: band, verdict, per-app counters and the K9
@@ -1442,8 +1502,15 @@ extern "C" int fm_hw_d_fit_split(const SmoothArgs* a, int hmax, int* deferred, i
   // of each (slot, row) resets its counter
   int* cnt = split_ws;
   float* cand = split_ws ? (float*)(split_ws + 2 * max_split) : nullptr;
-  hipLaunchKernelGGL((hw_d_kernel<45>), dim3(pairs - S + 2 * S), dim3(256), lds, st, *a, hmax, deferred, pairs - S,
-                     cnt, cand);
+  // FOREMAST_HW_PRUNE=0 turns the exact grid branch and bound off (A/B runs)
+  const char* pe = getenv("FOREMAST_HW_PRUNE");
+  const bool prune = !(pe && pe[0] == '0');
+  if (prune)
+    hipLaunchKernelGGL((hw_d_kernel<45, true>), dim3(pairs - S + 2 * S), dim3(256), lds, st, *a, hmax, deferred,
+                       pairs - S, cnt, cand);
+  else
+    hipLaunchKernelGGL((hw_d_kernel<45, false>), dim3(pairs - S + 2 * S), dim3(256), lds, st, *a, hmax, deferred,
+                       pairs - S, cnt, cand);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL((hw_half_general_kernel<45>), dim3(pairs < 512 ? pairs : 512), dim3(256), glds, st, *a, hmax,

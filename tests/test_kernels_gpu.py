@@ -526,6 +526,40 @@ def test_hw_split_tail_matches_whole_pairs(K, N, monkeypatch):
         assert torch.equal(outs[0][key], outs[1][key]), key
 
 
+@pytest.mark.parametrize("N,split", [(64, "0"), (1030, "1"), (4096, "0")])
+def test_hw_grid_pruning_is_exact(K, N, split, monkeypatch):
+    """Variant 5's grid branch and bound (a wave drops a grid pair once its partial SSE
+    exceeds the best complete SSE of the block) returns exactly the exhaustive fit:
+    every output bit for bit, on series whose grid SSEs are close (low noise), spread
+    (level shifts, spikes) and tied (constant series)."""
+    dev = torch.device("cuda:0")
+    m, T = 1440, 10080
+    y = _series(N, T, m, seed=31, nan_frac=0.0)
+    rng = np.random.default_rng(5)
+    y[1::7] += rng.normal(0.0, 5.0, size=y[1::7].shape)            # noisy: every pair close
+    y[2::7, 6000:] += 40.0                                          # level shift: alpha matters
+    y[3::7, rng.integers(1440, T, 50)] += 300.0                     # spikes
+    y[4::7] = 7.0                                                   # constant: every SSE ties at 0
+    y[5::7] *= np.linspace(1.0, 3.0, T)                             # growing amplitude
+    ring = torch.tensor(y, device=dev).to(torch.bfloat16)
+    grid = sm_ref.make_grid(sm_ref.MODE_HW, (0.1, 0.3, 0.5, 0.8), (0.0, 0.01, 0.05, 0.1), (0.05, 0.1, 0.3, 0.5))
+    hz = torch.arange(1, 11, dtype=torch.int32).repeat(5)
+    cur = torch.tensor(y[:, -50:] * 1.04, device=dev)
+    spec = K.DetectSpec(horizons=hz.to(dev), threshold=torch.full((N,), 2.0, device=dev),
+                        bound=torch.full((N,), 3, dtype=torch.int8, device=dev),
+                        min_lower=torch.full((N,), -1e30, device=dev), cur=cur, max_horizon=10)
+    monkeypatch.setenv("FOREMAST_HW_SPLIT", split)
+    outs = []
+    for prune in ("1", "0", "1"):
+        monkeypatch.setenv("FOREMAST_HW_PRUNE", prune)
+        outs.append({k: v.clone() for k, v in
+                     K.smoothing_fit(ring, 0, T, sm_ref.MODE_HW, m, grid.to(dev), spec, variant=5).items()})
+        torch.cuda.synchronize()
+    for o in (outs[0], outs[2]):
+        for key in ("best", "level", "trend", "sigma", "verdict", "count", "forecast", "upper", "lower"):
+            assert torch.equal(o[key], outs[1][key]), key
+
+
 def test_hw_split_plan():
     from foremast_amd.ops import _native as nat
     lib = nat.require()
