@@ -90,7 +90,12 @@ def parse():
                    help="canary: fraction of series whose 7-day history has a 30-minute scrape outage (NaN run) "
                         "after the first season (production-like gaps; those series take the masked kernels)")
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    p.add_argument("--graph", action="store_true", help="capture the GPU part of a tick in a HIP graph")
+    p.add_argument("--graph", dest="graph", action="store_true", default=True,
+                   help="(default) canary: the GPU part of a steady-state tick (ring advance, ingest, rank tests, "
+                        "fit, deferred detect) is one HIP-graph replay; the host only copies the health table "
+                        "back and waits. Falls back to eager launches where the shard cannot be captured")
+    p.add_argument("--eager", dest="graph", action="store_false",
+                   help="canary: launch every kernel of a tick from Python (no HIP graph)")
     p.add_argument("--pipeline", action="store_true",
                    help="canary: enqueue tick k+1 before waiting for tick k's health table (the GPU never idles on "
                         "the host; detect latency then includes the queueing behind the previous tick). Measured "
@@ -479,6 +484,7 @@ def setup_canary(args, world, rank, dev):
     dt = "bf16" if dtype == torch.bfloat16 else "fp32"
     meta["_agg"] = agg
     meta["_truth"] = (truth_apps, n_apps)
+    meta["_graph_used"] = lambda: shard._graph is not None  # captured (vs eager fallback)
     return tick, health_host, meta, dt, args.series
 
 
@@ -782,6 +788,7 @@ def main():
     node_finish = meta.pop("_finish", None)
     node_roll = meta.pop("_roll", None)
     node_breakdowns = meta.pop("_breakdowns", None)
+    graph_used = meta.pop("_graph_used", None)
     for k in [k for k in meta if k.startswith("_")]:
         meta.pop(k)
     if truth is not None and world > 1:
@@ -836,6 +843,8 @@ def main():
         torch.cuda.synchronize()
     barrier(dev)
     elapsed = time.perf_counter() - t0
+    if graph_used is not None:
+        meta["hip_graph"] = bool(graph_used())
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     lat_t = torch.tensor(lat, dtype=torch.float64, device=dev)
     if world > 1:
