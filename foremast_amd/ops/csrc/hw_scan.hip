@@ -1050,6 +1050,19 @@ __device__ __forceinline__ void d_pass2(const float* blk, v2f* D, v2f c1, v2f c2
   }
 }
 
+// k-th grid pair of a block's queue: the (at most two, distinct) hint pairs packed in hp
+// first, then [lo, ...) in order without them
+__device__ __forceinline__ int hint_pair_at(int k, int lo, unsigned hp) {
+  const int h0 = (int)(hp & 0xffffu), h1 = (int)(hp >> 16);
+  const int nh = (h0 != 0xffff) + (h1 != 0xffff);
+  if (k < nh) return (k == 0 && h0 != 0xffff) ? h0 : h1;
+  int r = lo + k - nh;
+  const int a0 = h0 < h1 ? h0 : h1, a1 = h0 < h1 ? h1 : h0;  // 0xffff sorts last, past every pair
+  r += r >= a0 ? 1 : 0;
+  r += r >= a1 ? 1 : 0;
+  return r;
+}
+
 // Split tail (see fm_hw_d_fit): a workgroup may fit only the grid pairs [pi_lo, pi_hi)
 // of its series pair; its per-series best then goes to slot `slot` of `cand` (half
 // `hid`), and whichever half arrives second merges the two and finishes the series.
@@ -1057,7 +1070,7 @@ constexpr int CAND_FLOATS = 4 + HALF_HB;  // SSE, index bits, level, trend, seas
 
 template <int K, bool PRUNE>
 __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0, int* deferred, int pi_lo,
-                                           int pi_hi, int slot, int hid, int* cnt, float* cand) {
+                                           int pi_hi, int slot, int hid, int* cnt, float* cand, int hints) {
   constexpr int SEA = DLay<K>::SEASON;
   constexpr int TS = PairTab<K>::SIZE;
   constexpr int NMW = (32 * K + 31) / 32;  // season-0 validity bitmask words per series
@@ -1075,10 +1088,24 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
   float* ylast = (float*)(flag + 4);
   float* bests = ylast + 2 * HALF_HB;
   float* wbest = bests + 4 * 2 * HALF_HB;
-  unsigned* ubound = (unsigned*)(wbest + 4 * 2 * 4);  // [2] per-series SSE bound, [2] pair queue
+  // [0..1] per-series SSE bound, [2] pair queue, [3] hint pairs (lo16 | hi16, 0xffff = none)
+  unsigned* ubound = (unsigned*)(wbest + 4 * 2 * 4);
 
   for (int i = tid; i < 2 * NMW + 8 * D_WAVES + 4; i += blockDim.x) vmask[i] = 0u;  // vmask, stat, flag
-  if (tid < 4) ubound[tid] = tid < 2 ? 0x7f800000u : 0u;  // +inf, +inf, queue 0
+  if (tid < 3) ubound[tid] = tid < 2 ? 0x7f800000u : 0u;  // +inf, +inf, queue 0
+  if (tid == 3) {
+    // hints: the grid pairs that won the previous fit of these series (a.best still holds it: only
+    // this block -- or, split, the second arriver of its two halves -- rewrites it, at the
+    // end) go first, so the branch and bound starts from a near-optimal bound
+    unsigned hp[2] = {0xffffu, 0xffffu};
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int b = (hints && n0 + r < a.N) ? a.best[n0 + r] : -1;
+      const int q = (b >= 0 && b < a.G) ? b / 2 : -1;
+      if (q >= pi_lo && q < pi_hi && (r == 0 || (unsigned)q != hp[0])) hp[r] = (unsigned)q;
+    }
+    ubound[3] = hp[0] | (hp[1] << 16);
+  }
   const int head = a.head_dev ? *a.head_dev : a.head;
   __syncthreads();
 
@@ -1229,12 +1256,14 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
   const int nwaves = blockDim.x / FM_WAVE;
   // Exact branch and bound over the grid (PRUNE): ubound[half] is the smallest
   // complete SSE any wave of this block has found for that series.  A per-lane SSE only
-  // grows (fl(s + e*e) >= s) and the butterfly sum is monotone in its operands, so a
-  // pair whose partial sum after season sg already exceeds the bound (strictly, for both
-  // series and both grid points) ends above it and can never be the argmin or tie it:
-  // the wave drops it and takes the next pair from the block's queue.
-
-  for (int pi = pi_lo + w; pi < pi_hi;) {
+  // grows (fl(s + e*e) >= s) and the DPP half sum is one fixed tree of adds, monotone in
+  // its operands, so a pair whose partial sum in season sg already exceeds the bound
+  // (strictly, for both series and both grid points) ends above it and can never be the
+  // argmin or tie it: the wave drops it and takes the next pair from the block's queue.
+  // Queue order: the hint pairs (previous winners), then the rest in grid order.
+  const int npb = pi_hi - pi_lo;
+  for (int k = w; k < npb;) {
+    const int pi = hint_pair_at(k, pi_lo, ubound[3]);
     const int c0 = 2 * pi;
     const int c1i = (2 * pi + 1 < a.G) ? 2 * pi + 1 : c0;
     const cfp tab = const_ptr(a.pair_tab + (size_t)pi * TS);
@@ -1290,10 +1319,10 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
                                __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     // next pair: the first round is static (pi_lo + w), later ones come from the queue
-    int k = 0;
+    int q = 0;
     if (lane == 0)
-      k = __hip_atomic_fetch_add(ubound + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    pi = pi_lo + nwaves + __builtin_amdgcn_readfirstlane(k);
+      q = __hip_atomic_fetch_add(ubound + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    k = nwaves + __builtin_amdgcn_readfirstlane(q);
   }
 
   // ---- arg-min across the 4 waves; wave r finishes series n0 + r ----------------------
@@ -1374,15 +1403,16 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
 // halves: workgroup n_full + 2 s + h fits half h of the grid of pair n_full + s.
 template <int K, bool PRUNE>
 __global__ __launch_bounds__(256, 2) void hw_d_kernel(const SmoothArgs a, int hmax, int* deferred, int n_full,
-                                                     int* cnt, float* cand) {
+                                                     int* cnt, float* cand, int hints) {
   const int b = blockIdx.x;
   const int npairs = (a.G + 1) / 2;
   if (b < n_full) {
-    hw_d_block<K, PRUNE>(a, hmax, 2 * b, deferred, 0, npairs, -1, 0, cnt, cand);
+    hw_d_block<K, PRUNE>(a, hmax, 2 * b, deferred, 0, npairs, -1, 0, cnt, cand, hints);
     return;
   }
   const int item = b - n_full, slot = item >> 1, h = item & 1, mid = npairs / 2;
-  hw_d_block<K, PRUNE>(a, hmax, 2 * (n_full + slot), deferred, h ? mid : 0, h ? npairs : mid, slot, h, cnt, cand);
+  hw_d_block<K, PRUNE>(a, hmax, 2 * (n_full + slot), deferred, h ? mid : 0, h ? npairs : mid, slot, h, cnt, cand,
+                       hints);
 }
 
 extern "C" size_t fm_hw_d_lds_bytes(int Tp, int seg, int K) {
@@ -1505,12 +1535,14 @@ extern "C" int fm_hw_d_fit_split(const SmoothArgs* a, int hmax, int* deferred, i
   // FOREMAST_HW_PRUNE=0 turns the exact grid branch and bound off (A/B runs)
   const char* pe = getenv("FOREMAST_HW_PRUNE");
   const bool prune = !(pe && pe[0] == '0');
+  const char* he = getenv("FOREMAST_HW_HINTS");  // previous winners first (=0: grid order)
+  const int hints = (prune && !(he && he[0] == '0')) ? 1 : 0;
   if (prune)
     hipLaunchKernelGGL((hw_d_kernel<45, true>), dim3(pairs - S + 2 * S), dim3(256), lds, st, *a, hmax, deferred,
-                       pairs - S, cnt, cand);
+                       pairs - S, cnt, cand, hints);
   else
     hipLaunchKernelGGL((hw_d_kernel<45, false>), dim3(pairs - S + 2 * S), dim3(256), lds, st, *a, hmax, deferred,
-                       pairs - S, cnt, cand);
+                       pairs - S, cnt, cand, hints);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL((hw_half_general_kernel<45>), dim3(pairs < 512 ? pairs : 512), dim3(256), glds, st, *a, hmax,

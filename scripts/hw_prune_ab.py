@@ -1,6 +1,7 @@
-"""A/B of the Holt-Winters fit (variant 5) with and without the exact grid branch and
-bound (FOREMAST_HW_PRUNE=0|1, read by the launcher on every launch): kernel time by
-HIP events, outputs compared bit for bit."""
+"""A/B of the Holt-Winters fit (variant 5): exhaustive grid, exact grid branch and bound
+in grid order, and with the previous winners first (FOREMAST_HW_PRUNE / FOREMAST_HW_HINTS,
+read by the launcher on every launch): kernel time by HIP events, outputs compared bit
+for bit."""
 import argparse
 import json
 import os
@@ -20,21 +21,31 @@ def main():
     p.add_argument("--ring", type=int, default=10080)
     p.add_argument("--season", type=int, default=1440)
     p.add_argument("--iters", type=int, default=10)
-    p.add_argument("--noise", type=float, default=0.03)
+    p.add_argument("--mix", action="store_true",
+                   help="vary the winning grid point: noisy / level-shifted / spiky / growing series mixed in")
     args = p.parse_args()
     dev = torch.device("cuda:0")
     N, R, m, C = args.series, args.ring, args.season, 50
-    hist = synthetic_history(N, R, m, dev, seed=3).to(torch.bfloat16)
+    hist = synthetic_history(N, R, m, dev, seed=3)
+    if args.mix:
+        g = torch.Generator(device=dev).manual_seed(5)
+        lvl = hist.mean(1, keepdim=True)
+        hist[1::7] += torch.randn(hist[1::7].shape, generator=g, device=dev) * 0.2 * lvl[1::7]
+        hist[2::7, R // 2:] += 0.5 * lvl[2::7]
+        hist[3::7, 2000::97] += 3.0 * lvl[3::7]
+        hist[5::7] *= torch.linspace(1.0, 3.0, R, device=dev)
+    hist = hist.to(torch.bfloat16)
     grid = sm.make_grid(sm.MODE_HW, (0.1, 0.3, 0.5, 0.8), (0.0, 0.01, 0.05, 0.1), (0.05, 0.1, 0.3, 0.5)).to(dev)
     cur = hist[:, -C:].float().contiguous()
     spec = K.DetectSpec(horizons=torch.arange(1, 11, dtype=torch.int32, device=dev).repeat(C // 10), max_horizon=10,
                         threshold=torch.full((N,), 3.0, device=dev), bound=torch.full((N,), 3, dtype=torch.int8, device=dev),
                         min_lower=torch.zeros(N, device=dev), cur=cur)
     res, outs = {}, {}
-    for mode in ("0", "1", "0", "1"):
-        os.environ["FOREMAST_HW_PRUNE"] = mode
-        o = None
+    modes = {"noprune": ("0", "1"), "prune_gridorder": ("1", "0"), "prune_hints": ("1", "1")}
+    for name in list(modes) * 2:
+        os.environ["FOREMAST_HW_PRUNE"], os.environ["FOREMAST_HW_HINTS"] = modes[name]
         o = K.smoothing_fit(hist, 0, R, sm.MODE_HW, m, grid, spec, variant=5)
+        o = K.smoothing_fit(hist, 0, R, sm.MODE_HW, m, grid, spec, out=o, variant=5)  # hints: this fit's winners
         torch.cuda.synchronize()
         ts = []
         for _ in range(args.iters):
@@ -45,12 +56,14 @@ def main():
             torch.cuda.synchronize()
             ts.append(a.elapsed_time(b))
         ts.sort()
-        res.setdefault(mode, []).append(ts[len(ts) // 2])
-        outs[mode] = {k: v.clone() for k, v in o.items() if torch.is_tensor(v)}
-    same = {k: bool(torch.equal(outs["0"][k], outs["1"][k])) for k in outs["0"]}
-    print(json.dumps({"series": N, "median_ms_noprune": res["0"], "median_ms_prune": res["1"],
-                      "speedup": min(res["0"]) / min(res["1"]), "identical": same}), flush=True)
-
+        res.setdefault(name, []).append(round(ts[len(ts) // 2], 3))
+        outs[name] = {k: v.clone() for k, v in o.items() if torch.is_tensor(v)}
+    same = all(torch.equal(outs["noprune"][k], outs[n][k]) for n in modes for k in outs["noprune"])
+    wins = torch.bincount(outs["noprune"]["best"].long(), minlength=grid.shape[0])
+    print(json.dumps({"series": N, "mix": args.mix, "median_ms": res,
+                      "speedup_hints": min(res["noprune"]) / min(res["prune_hints"]),
+                      "speedup_gridorder": min(res["noprune"]) / min(res["prune_gridorder"]),
+                      "identical": same, "distinct_winners": int((wins > 0).sum())}), flush=True)
 
 if __name__ == "__main__":
     main()

@@ -549,15 +549,22 @@ def test_hw_grid_pruning_is_exact(K, N, split, monkeypatch):
                         bound=torch.full((N,), 3, dtype=torch.int8, device=dev),
                         min_lower=torch.full((N,), -1e30, device=dev), cur=cur, max_horizon=10)
     monkeypatch.setenv("FOREMAST_HW_SPLIT", split)
-    outs = []
-    for prune in ("1", "0", "1"):
+
+    def fit(prune, out=None):
         monkeypatch.setenv("FOREMAST_HW_PRUNE", prune)
-        outs.append({k: v.clone() for k, v in
-                     K.smoothing_fit(ring, 0, T, sm_ref.MODE_HW, m, grid.to(dev), spec, variant=5).items()})
+        o = K.smoothing_fit(ring, 0, T, sm_ref.MODE_HW, m, grid.to(dev), spec, variant=5, out=out)
         torch.cuda.synchronize()
-    for o in (outs[0], outs[2]):
+        return o
+
+    ref = {k: v.clone() for k, v in fit("0").items()}
+    reused = fit("1")                                      # out["best"] is uninitialised: arbitrary hints
+    runs = [{k: v.clone() for k, v in reused.items()}]
+    runs.append({k: v.clone() for k, v in fit("1", reused).items()})  # hints = the previous winners
+    reused["best"].copy_(torch.randint(-3, 70, (N,), dtype=torch.int32, device=dev))  # wrong / out-of-range hints
+    runs.append({k: v.clone() for k, v in fit("1", reused).items()})
+    for o in runs:
         for key in ("best", "level", "trend", "sigma", "verdict", "count", "forecast", "upper", "lower"):
-            assert torch.equal(o[key], outs[1][key]), key
+            assert torch.equal(o[key], ref[key]), key
 
 
 def test_hw_split_plan():
