@@ -80,6 +80,9 @@ def parse():
     p.add_argument("--window", type=int, default=10)
     p.add_argument("--algorithm", default="holt_winters")
     p.add_argument("--pairwise", default="ALL")
+    p.add_argument("--pairwise-shift", type=float, default=None,
+                   help="canary: mean-shift rule threshold in sigmas (ML_PAIRWISE_SHIFT; 0 = off; "
+                        "default: the BrainConfig default)")
     p.add_argument("--anomaly-frac", type=float, default=0.01)
     p.add_argument("--anomaly-kind", default="scale3", choices=["scale3", "shift3sigma", "scale", "shift"],
                    help="injected canary regression: values x3, or a level shift of +3 noise sigma; "
@@ -272,6 +275,8 @@ def setup_canary(args, world, rank, dev):
         args.series, args.ring, args.season = 256, 480, 48
     cfg = BrainConfig()
     cfg.min_historical_points = 0
+    if args.pairwise_shift is not None:
+        cfg.pairwise_shift = args.pairwise_shift
     s, e, per = shard_range(args.series, world, rank, align=METRICS_PER_APP)
     n_local = e - s
     n_apps = (args.series + METRICS_PER_APP - 1) // METRICS_PER_APP
@@ -467,6 +472,7 @@ def setup_canary(args, world, rank, dev):
         "grid_points": int(shard.grid.shape[0]),
         "multi_cluster": bool(args.multi_cluster),
         "gap_frac": args.gap_frac,
+        "pairwise_shift_sigma": cfg.pairwise_shift,
         "health_collectives": "1 fused all_gather" if agg.fused else ("all_reduce + all_gather" if agg.active else "none"),
         "hip_graph": bool(args.graph and dev.type == "cuda"),
         "ingest": args.ingest,
@@ -738,7 +744,8 @@ def run_cpu_baseline(args) -> None:
     t0 = time.perf_counter()
     verdicts = [cb.score_series(hist[i], cur[i], base[i], hz, args.season, grid, threshold=4.0, bound=3,
                                 alpha=cfg.pairwise_threshold, pairwise_scale=cfg.pairwise_scale,
-                                pw_min_points=cfg.pairwise_min_points).verdict for i in range(n)]
+                                pw_min_points=cfg.pairwise_min_points,
+                                shift_threshold=cfg.pairwise_shift).verdict for i in range(n)]
     dt = time.perf_counter() - t0
     truth = set(bad.tolist())
     flagged = {i for i, v in enumerate(verdicts) if v == 1}

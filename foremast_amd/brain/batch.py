@@ -161,7 +161,8 @@ class BatchScorer:
         thr_f, thr_l = det_ref.effective_thresholds(torch.from_numpy(thr), torch.from_numpy(bnd), n_pts,
                                                     cfg.pairwise_scale, cfg.window_correction)
         t_thr, t_thr_low = thr_f.to(dev).contiguous(), thr_l.to(dev).contiguous()
-        dkw = dict(threshold_low=t_thr_low, pw_min_points=cfg.pairwise_min_points)
+        dkw = dict(threshold_low=t_thr_low, pw_min_points=cfg.pairwise_min_points,
+                   shift_threshold=cfg.pairwise_shift)
         t_low = torch.from_numpy(low).to(dev)
         t_hz = torch.from_numpy(hz).to(dev)
         t_hist = torch.from_numpy(hist).to(dev)

@@ -356,7 +356,8 @@ class StreamingShard:
                             pw_scale=cfg.pairwise_scale, min_valid=cfg.min_historical_points,
                             want_band=self.spec.want_band, app_id=self.app_id, app_stats=self.app_stats,
                             anomalies=self.anomalies, max_horizon=self.cur.W, threshold_low=self.thr_low,
-                            pw_min_points=cfg.pairwise_min_points, horizon_variance=cfg.horizon_variance)
+                            pw_min_points=cfg.pairwise_min_points,
+                            shift_threshold=cfg.pairwise_shift, horizon_variance=cfg.horizon_variance)
 
     def _refresh_cache_gpu(self) -> None:
         """After a refit: the full state of the fitted model (hw_state.hip)."""
@@ -414,7 +415,8 @@ class StreamingShard:
                             pw_scale=cfg.pairwise_scale, min_valid=cfg.min_historical_points,
                             want_band=self.spec.want_band, app_id=self.app_id, app_stats=self.app_stats,
                             anomalies=self.anomalies, max_horizon=self.cur.W, threshold_low=self.thr_low,
-                            pw_min_points=cfg.pairwise_min_points, horizon_variance=cfg.horizon_variance)
+                            pw_min_points=cfg.pairwise_min_points,
+                            shift_threshold=cfg.pairwise_shift, horizon_variance=cfg.horizon_variance)
         if self.anomalies is not None:
             self.anomalies.reset()
         h = self.hist
@@ -501,7 +503,8 @@ class StreamingShard:
         ok = n_valid >= cfg.min_historical_points
         d = det_ref.detect(f, sigma, self.cur.data, self.thr_full, self.bound, self.min_lower,
                            differs=differs, pairwise_scale=cfg.pairwise_scale, model_ok=ok,
-                           threshold_low=self.thr_low, pw_min_points=cfg.pairwise_min_points)
+                           threshold_low=self.thr_low, pw_min_points=cfg.pairwise_min_points,
+                           shift_threshold=cfg.pairwise_shift)
         v = d.verdict.long()
         self.app_stats.index_put_((self.app_id.long(), torch.zeros_like(v)), (v == 1).int(), accumulate=True)
         self.app_stats.index_put_((self.app_id.long(), torch.ones_like(v)), (v >= 0).int(), accumulate=True)

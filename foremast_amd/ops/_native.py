@@ -39,7 +39,7 @@ class DetectArgs(C.Structure):
         ("hv_grid", P), ("hv_mode", I), ("hv_m", I),
         ("forecast", P), ("upper", P), ("lower", P), ("count", P), ("verdict", P),
         ("score", P), ("app_id", P), ("app_stats", P),
-        ("anom_count", P), ("anom_series", P), ("anom_col", P), ("anom_val", P), ("anom_cap", I), ("_pad1", I),
+        ("anom_count", P), ("anom_series", P), ("anom_col", P), ("anom_val", P), ("anom_cap", I), ("shift_thr", F),
     ]
 
 

@@ -39,7 +39,7 @@ struct DetectArgs {
   int* anom_col;                // [anom_cap]
   float* anom_val;              // [anom_cap]
   int anom_cap;
-  int _pad1;
+  float shift_thr;              // > 0: mean-shift rule when differs (window mean of (x - f) / s beyond it)
 };
 
 struct SmoothArgs {

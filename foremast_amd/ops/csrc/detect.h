@@ -53,21 +53,30 @@ __device__ __forceinline__ float hstep_factor(const DetectArgs& d, int gidx, int
   return sqrtf(v);
 }
 
-// Per-series thresholds of the two detection rules (models/detect.py detect):
-// full band (threshold) and, when the canary test says baseline and current
-// differ, the lowered band (threshold_low, or threshold * pw_scale) — which only
-// counts when at least pw_min_points points fall outside it.
+// Per-series thresholds of the detection rules (models/detect.py detect): full
+// band (threshold) and, when the canary test says baseline and current differ,
+// the lowered band (threshold_low, or threshold * pw_scale) — which only counts
+// when at least pw_min_points points fall outside it — and the mean-shift rule
+// (shift_thr > 0): the window's mean standardised deviation beyond shift_thr on
+// an enabled side.
 struct DetThr {
-  float full, low;
-  bool differs;
+  float full, low, shift;
+  bool differs, shift_on;
 };
 __device__ __forceinline__ DetThr det_thresholds(const DetectArgs& d, int n) {
   DetThr t;
   t.full = d.threshold[n];
   t.differs = d.differs && d.differs[n];
   t.low = d.threshold_low ? d.threshold_low[n] : t.full * d.pw_scale;
+  t.shift = d.shift_thr;
+  t.shift_on = t.differs && d.shift_thr > 0.f;
   return t;
 }
+
+// Pass-1 sums of a series (reduced by the caller)
+struct DetSums {
+  float cnt_f = 0.f, cnt_l = 0.f, cnt_s = 0.f, zsum = 0.f, nz = 0.f, anyv = 0.f, sc = 0.f;
+};
 
 __device__ __forceinline__ bool det_outside(float x, float f, float thr, float s, float mlow, int bnd) {
   return ((bnd & 1) && x > f + thr * s) || ((bnd & 2) && x < fmaxf(f - thr * s, mlow));
@@ -76,19 +85,24 @@ __device__ __forceinline__ bool det_outside(float x, float f, float thr, float s
 // Pass 1 of a column: counts against both bands (the caller reduces them).
 template <typename ForecastFn>
 __device__ __forceinline__ void det_count_col(const DetectArgs& d, int n, int c, const DetThr& t, float sig, int gidx,
-                                              int bnd, float mlow, bool model_ok, ForecastFn& fcast, float& cnt_f,
-                                              float& cnt_l, float& anyv, float& sc) {
+                                              int bnd, float mlow, bool model_ok, ForecastFn& fcast, DetSums& u) {
   const float x = d.cur[(long long)n * d.ld_cur + c];
   if (!(x == x)) return;
-  anyv = 1.f;
+  u.anyv = 1.f;
   const int h = d.horizons[d.h_ld * n + c];
   const float f = fcast(h);
   const float s = sig * hstep_factor(d, gidx, h);
+  const float z = (x - f) / fmaxf(s, 1e-12f);
   if (model_ok) {
-    cnt_f += det_outside(x, f, t.full, s, mlow, bnd) ? 1.f : 0.f;
-    if (t.differs) cnt_l += det_outside(x, f, t.low, s, mlow, bnd) ? 1.f : 0.f;
+    u.cnt_f += det_outside(x, f, t.full, s, mlow, bnd) ? 1.f : 0.f;
+    if (t.differs) u.cnt_l += det_outside(x, f, t.low, s, mlow, bnd) ? 1.f : 0.f;
+    if (t.shift_on) {
+      u.cnt_s += det_outside(x, f, t.shift, s, mlow, bnd) ? 1.f : 0.f;
+      u.zsum += z;
+      u.nz += 1.f;
+    }
   }
-  sc = fmaxf(sc, fabsf(x - f) / fmaxf(s, 1e-12f));
+  u.sc = fmaxf(u.sc, fabsf(z));
 }
 
 // Pass 2 of a column: band of the rule in force, and the K9 list (rare: one atomic
@@ -118,12 +132,24 @@ __device__ __forceinline__ void det_emit_col(const DetectArgs& d, int n, int c, 
   }
 }
 
-// Verdict from the reduced counts; returns the threshold of the rule in force and
-// sets *count (anomalous points under that rule).
-__device__ __forceinline__ float det_decide(const DetectArgs& d, const DetThr& t, float cnt_f, float cnt_l, int* count) {
-  const bool low_rule = t.differs && cnt_l >= (float)max(d.pw_min_points, 1);
-  *count = (int)(low_rule ? cnt_l : cnt_f);
-  return low_rule ? t.low : t.full;
+// Verdict from the reduced sums; returns the threshold of the rule in force and
+// sets *count (anomalous points under that rule).  Precedence: lowered band, full
+// band, mean shift (whose band is f +- shift_thr * s).
+__device__ __forceinline__ float det_decide(const DetectArgs& d, const DetThr& t, const DetSums& u, int bnd,
+                                            int* count) {
+  if (t.differs && u.cnt_l >= (float)max(d.pw_min_points, 1)) {
+    *count = (int)u.cnt_l;
+    return t.low;
+  }
+  if (u.cnt_f <= 0.f && t.shift_on && u.nz >= (float)max(d.pw_min_points, 1)) {
+    const float mz = u.zsum / u.nz;
+    if (((bnd & 1) && mz > t.shift) || ((bnd & 2) && mz < -t.shift)) {
+      *count = (int)u.cnt_s;
+      return t.shift;
+    }
+  }
+  *count = (int)u.cnt_f;
+  return t.full;
 }
 
 __device__ __forceinline__ void det_write(const DetectArgs& d, int n, int ic, float anyv, bool model_ok, float sc) {
@@ -153,17 +179,21 @@ __device__ __forceinline__ void detect_epilogue_wave(const DetectArgs& d, int n,
   const bool model_ok = n_valid >= (float)d.min_valid;
   float thr = t.full;
   int ic = 0;
-  float anyv = 0.f, sc = 0.f;
+  DetSums u;
   if (d.cur) {
-    float cnt_f = 0.f, cnt_l = 0.f;
-    for (int c = lane; c < d.C; c += FM_WAVE)
-      det_count_col(d, n, c, t, sig, gidx, bnd, mlow, model_ok, fcast, cnt_f, cnt_l, anyv, sc);
-    cnt_f = wave_allsum(cnt_f);
-    cnt_l = t.differs ? wave_allsum(cnt_l) : 0.f;  // t.differs is wave-uniform (one series per wave)
-    anyv = wave_allmax(anyv);
-    sc = wave_allmax(sc);
-    thr = det_decide(d, t, cnt_f, cnt_l, &ic);
+    for (int c = lane; c < d.C; c += FM_WAVE) det_count_col(d, n, c, t, sig, gidx, bnd, mlow, model_ok, fcast, u);
+    u.cnt_f = wave_allsum(u.cnt_f);
+    if (t.differs) u.cnt_l = wave_allsum(u.cnt_l);  // t.differs is wave-uniform (one series per wave)
+    if (t.shift_on) {
+      u.cnt_s = wave_allsum(u.cnt_s);
+      u.zsum = wave_allsum(u.zsum);
+      u.nz = wave_allsum(u.nz);
+    }
+    u.anyv = wave_allmax(u.anyv);
+    u.sc = wave_allmax(u.sc);
+    thr = det_decide(d, t, u, bnd, &ic);
   }
+  const float anyv = u.anyv, sc = u.sc;
   const bool emit = d.anom_count && ic > 0;
   if (d.forecast || d.upper || d.lower || emit)
     for (int c = lane; c < d.C; c += FM_WAVE) det_emit_col(d, n, c, thr, sig, gidx, bnd, mlow, emit, fcast);
@@ -182,17 +212,21 @@ __device__ __forceinline__ void detect_epilogue(const DetectArgs& d, int n, floa
   const bool model_ok = n_valid >= (float)d.min_valid;
   float thr = t.full;
   int ic = 0;
-  float anyv = 0.f, sc = 0.f;
+  DetSums u;
   if (d.cur) {
-    float cnt_f = 0.f, cnt_l = 0.f;
-    for (int c = tid; c < d.C; c += blockDim.x)
-      det_count_col(d, n, c, t, sig, gidx, bnd, mlow, model_ok, fcast, cnt_f, cnt_l, anyv, sc);
-    cnt_f = blk_sum(cnt_f, red);
-    cnt_l = blk_sum(cnt_l, red);
-    anyv = blk_max(anyv, red);
-    sc = blk_max(sc, red);
-    thr = det_decide(d, t, cnt_f, cnt_l, &ic);
+    for (int c = tid; c < d.C; c += blockDim.x) det_count_col(d, n, c, t, sig, gidx, bnd, mlow, model_ok, fcast, u);
+    u.cnt_f = blk_sum(u.cnt_f, red);
+    if (t.differs) u.cnt_l = blk_sum(u.cnt_l, red);  // block-uniform: one series per workgroup
+    if (t.shift_on) {
+      u.cnt_s = blk_sum(u.cnt_s, red);
+      u.zsum = blk_sum(u.zsum, red);
+      u.nz = blk_sum(u.nz, red);
+    }
+    u.anyv = blk_max(u.anyv, red);
+    u.sc = blk_max(u.sc, red);
+    thr = det_decide(d, t, u, bnd, &ic);
   }
+  const float anyv = u.anyv, sc = u.sc;
   const bool emit = d.anom_count && ic > 0;
   if (d.forecast || d.upper || d.lower || emit)
     for (int c = tid; c < d.C; c += blockDim.x) det_emit_col(d, n, c, thr, sig, gidx, bnd, mlow, emit, fcast);

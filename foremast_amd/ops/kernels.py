@@ -73,6 +73,8 @@ class DetectSpec:
     pw_min_points: int = 1
     # scale sigma by the h-step forecast-error factor of the fitted smoothing model
     horizon_variance: bool = True
+    # > 0: mean-shift rule when ``differs`` (models/detect.py ``shift_threshold``)
+    shift_threshold: float = 0.0
 
 
 class AnomalyBuffer:
@@ -157,6 +159,7 @@ def _fill_detect(d: nat.DetectArgs, spec: DetectSpec, N: int, device, out: Dict[
     d.differs = nat.ptr(spec.differs)
     d.pw_scale = float(spec.pw_scale)
     d.pw_min_points = int(spec.pw_min_points)
+    d.shift_thr = float(spec.shift_threshold)
     d.threshold_low = nat.ptr(spec.threshold_low)
     d.hv_grid, d.hv_mode, d.hv_m = None, 0, 0
     d.forecast = nat.ptr(out.get("forecast"))

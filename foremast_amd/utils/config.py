@@ -81,6 +81,10 @@ class BrainConfig:
     # (FOREMAST_WINDOW_CORRECTION = sidak | none); sigma is scaled to the forecast
     # horizon (FOREMAST_HORIZON_VARIANCE = 1 | 0)
     pairwise_min_points: int = 3
+    # mean-shift rule (ML_PAIRWISE_SHIFT, 0 = off): when the rank tests say the pods
+    # differ, a window whose mean deviation from the forecast is beyond this many sigmas
+    # is anomalous even if few of its points leave the window-corrected band
+    pairwise_shift: float = 1.5
     window_correction: str = "sidak"
     horizon_variance: bool = True
     poll_seconds: float = 5.0
@@ -150,6 +154,7 @@ class BrainConfig:
         c.pairwise_scale = f("FOREMAST_PAIRWISE_SCALE", c.pairwise_scale)
         c.poll_seconds = f("FOREMAST_POLL_SECONDS", c.poll_seconds)
         c.pairwise_min_points = int(f("ML_PAIRWISE_MIN_ANOMALIES", c.pairwise_min_points, int))
+        c.pairwise_shift = f("ML_PAIRWISE_SHIFT", c.pairwise_shift)
         c.window_correction = (e.get("FOREMAST_WINDOW_CORRECTION") or c.window_correction).strip().lower()
         c.horizon_variance = e.get("FOREMAST_HORIZON_VARIANCE", "1").strip().lower() not in ("0", "false", "no")
         # FOREMAST_DETECTION_PRESET=reference: the reference brain's documented per-point
@@ -160,6 +165,7 @@ class BrainConfig:
             c.window_correction = (e.get("FOREMAST_WINDOW_CORRECTION") or "none").strip().lower()
             c.pairwise_min_points = int(f("ML_PAIRWISE_MIN_ANOMALIES", 1, int))
             c.horizon_variance = e.get("FOREMAST_HORIZON_VARIANCE", "0").strip().lower() not in ("0", "false", "no")
+            c.pairwise_shift = f("ML_PAIRWISE_SHIFT", 0.0)
         c.lstm_hidden = int(f("FOREMAST_LSTM_HIDDEN", c.lstm_hidden, int))
         c.lstm_window = int(f("FOREMAST_LSTM_WINDOW", c.lstm_window, int))
         c.metrics_port = int(f("FOREMAST_METRICS_PORT", c.metrics_port, int))

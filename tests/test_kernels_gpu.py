@@ -576,11 +576,13 @@ def test_hw_split_plan():
     assert lib.fm_hw_d_split_plan(20, 0, 4096) == 0
 
 
+@pytest.mark.parametrize("shift", [0.0, 1.0])
 @pytest.mark.parametrize("which", ["window_stats", "holt_winters", "hw_deferred"])
-def test_two_rule_detection_matches_reference(K, which):
-    """Full band + lowered pairwise band that needs >= pw_min_points points
-    (detect.h det_decide): kernel verdicts, counts, bands and the K9 list equal
-    the reference on series built to sit on each side of both rules."""
+def test_two_rule_detection_matches_reference(K, which, shift):
+    """Full band + lowered pairwise band that needs >= pw_min_points points, and
+    (shift > 0) the mean-shift rule (detect.h det_decide): kernel verdicts, counts,
+    bands and the K9 list equal the reference on series built to sit on each side
+    of every rule."""
     from foremast_amd.brain.engine import synthetic_history
     dev = torch.device("cuda:0")
     N, T, m, C = 2000, 2 * 1440, 1440, 10
@@ -590,6 +592,10 @@ def test_two_rule_detection_matches_reference(K, which):
     # noise on the scale of each model's sigma, so both rules fire on some series and not others
     scale = hf.std(1, keepdim=True) if which == "window_stats" else (hf[:, 1:] - hf[:, :-1]).std(1, keepdim=True)
     cur = (hf[:, -C:] + torch.randn((N, C), generator=g, device=dev) * scale).contiguous()
+    if shift:  # sustained level shifts around the mean-shift threshold on a quarter of the series
+        sgn = torch.where(torch.arange(N, device=dev) % 16 < 8, 1.0, -1.0)[:, None]
+        lift = (torch.arange(N, device=dev) % 8 >= 6).float()[:, None]
+        cur = (cur + lift * sgn * 1.3 * shift * scale).contiguous()
     differs = (torch.arange(N, device=dev) % 2).to(torch.uint8)
     thr = torch.full((N,), 3.0, device=dev)
     bound = torch.tensor([1, 2, 3, 3], dtype=torch.int8, device=dev).repeat(N // 4)
@@ -597,7 +603,7 @@ def test_two_rule_detection_matches_reference(K, which):
     spec = K.DetectSpec(horizons=torch.arange(1, C + 1, dtype=torch.int32, device=dev), threshold=full.to(dev),
                         bound=bound, min_lower=torch.full((N,), -1e9, device=dev), cur=cur, differs=differs,
                         threshold_low=low.to(dev), pw_min_points=3, anomalies=K.AnomalyBuffer(N * C, dev),
-                        max_horizon=C)
+                        max_horizon=C, shift_threshold=shift)
     spec.anomalies.reset()
     grid = sm_ref.make_grid(sm_ref.MODE_HW, (0.1, 0.5), (0.0, 0.1), (0.1, 0.5)).to(dev)
     if which == "window_stats":
@@ -616,11 +622,16 @@ def test_two_rule_detection_matches_reference(K, which):
                                                                         torch.arange(1, C + 1))
     torch.cuda.synchronize()
     d = det_ref.detect(out["forecast"].cpu(), sig, cur.cpu(), full, bound.cpu(), torch.full((N,), -1e9),
-                       differs=differs.cpu(), threshold_low=low, pw_min_points=3)
+                       differs=differs.cpu(), threshold_low=low, pw_min_points=3, shift_threshold=shift)
     assert torch.equal(d.verdict, out["verdict"].cpu())
     assert torch.equal(d.count, out["count"].cpu())
     low_fired = (differs.cpu().bool() & (d.count > 0))
     assert int(low_fired.sum()) > 0 and int((d.verdict == 0).sum()) > 0  # both sides exercised
+    if shift:
+        d0 = det_ref.detect(out["forecast"].cpu(), sig, cur.cpu(), full, bound.cpu(), torch.full((N,), -1e9),
+                            differs=differs.cpu(), threshold_low=low, pw_min_points=3)
+        by_shift = (d.verdict == 1) & (d0.verdict == 0)
+        assert int(by_shift.sum()) > 0 and not bool((by_shift & ~differs.cpu().bool()).any())
     np.testing.assert_allclose(out["upper"].cpu().numpy(), d.upper.numpy(), rtol=1e-4, atol=1e-3)
     s_, c_, v_, overflow = spec.anomalies.fetch()
     assert not overflow
