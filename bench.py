@@ -161,6 +161,8 @@ def parse():
         a.steps = 8 if a.config == "node" else 20
     if a.warmup is None:
         a.warmup = 1 if a.config == "node" else 5
+    if a.zero_copy or a.prefetch:
+        a.graph = False  # these modes stage the tick's I/O from the host: eager launches
     return a
 
 
