@@ -747,7 +747,8 @@ def run_cpu_baseline(args) -> None:
     verdicts = [cb.score_series(hist[i], cur[i], base[i], hz, args.season, grid, threshold=4.0, bound=3,
                                 alpha=cfg.pairwise_threshold, pairwise_scale=cfg.pairwise_scale,
                                 pw_min_points=cfg.pairwise_min_points,
-                                shift_threshold=cfg.pairwise_shift).verdict for i in range(n)]
+                                shift_threshold=cfg.pairwise_shift,
+                                shift_min_points=cfg.pairwise_shift_min_points).verdict for i in range(n)]
     dt = time.perf_counter() - t0
     truth = set(bad.tolist())
     flagged = {i for i, v in enumerate(verdicts) if v == 1}

@@ -138,9 +138,11 @@ class BatchScorer:
         t_cur = torch.from_numpy(cur).to(dev)
         differs = None
         pvals = None
+        bmean = None  # the baseline window means (mean-shift rule)
         if base is not None and cfg.pairwise_algorithm.upper() != "NONE":
             mode = pw_ref.PW_BY_NAME.get(cfg.pairwise_algorithm.upper(), pw_ref.PW_ALL)
             t_base = torch.from_numpy(base).to(dev)
+            bmean = torch.nanmean(t_base.float(), 1).contiguous()
             if self.gpu:
                 from ..ops import kernels as K
                 o = K.rank_tests(t_base, t_cur, mode, cfg.pairwise_threshold, cfg.min_mann_white,
@@ -162,7 +164,7 @@ class BatchScorer:
                                                     cfg.pairwise_scale, cfg.window_correction)
         t_thr, t_thr_low = thr_f.to(dev).contiguous(), thr_l.to(dev).contiguous()
         dkw = dict(threshold_low=t_thr_low, pw_min_points=cfg.pairwise_min_points,
-                   shift_threshold=cfg.pairwise_shift)
+                   shift_threshold=cfg.pairwise_shift, shift_min_points=cfg.pairwise_shift_min_points, base_mean=bmean)
         t_low = torch.from_numpy(low).to(dev)
         t_hz = torch.from_numpy(hz).to(dev)
         t_hist = torch.from_numpy(hist).to(dev)

@@ -357,7 +357,9 @@ class StreamingShard:
                             want_band=self.spec.want_band, app_id=self.app_id, app_stats=self.app_stats,
                             anomalies=self.anomalies, max_horizon=self.cur.W, threshold_low=self.thr_low,
                             pw_min_points=cfg.pairwise_min_points,
-                            shift_threshold=cfg.pairwise_shift, horizon_variance=cfg.horizon_variance)
+                            shift_threshold=cfg.pairwise_shift, shift_min_points=cfg.pairwise_shift_min_points,
+                            base_mean=self.pw_out["base_mean"] if differs is not None else None,
+                            horizon_variance=cfg.horizon_variance)
 
     def _refresh_cache_gpu(self) -> None:
         """After a refit: the full state of the fitted model (hw_state.hip)."""
@@ -416,7 +418,9 @@ class StreamingShard:
                             want_band=self.spec.want_band, app_id=self.app_id, app_stats=self.app_stats,
                             anomalies=self.anomalies, max_horizon=self.cur.W, threshold_low=self.thr_low,
                             pw_min_points=cfg.pairwise_min_points,
-                            shift_threshold=cfg.pairwise_shift, horizon_variance=cfg.horizon_variance)
+                            shift_threshold=cfg.pairwise_shift, shift_min_points=cfg.pairwise_shift_min_points,
+                            base_mean=self.pw_out["base_mean"] if differs is not None else None,
+                            horizon_variance=cfg.horizon_variance)
         if self.anomalies is not None:
             self.anomalies.reset()
         h = self.hist
@@ -504,7 +508,8 @@ class StreamingShard:
         d = det_ref.detect(f, sigma, self.cur.data, self.thr_full, self.bound, self.min_lower,
                            differs=differs, pairwise_scale=cfg.pairwise_scale, model_ok=ok,
                            threshold_low=self.thr_low, pw_min_points=cfg.pairwise_min_points,
-                           shift_threshold=cfg.pairwise_shift)
+                           shift_threshold=cfg.pairwise_shift, shift_min_points=cfg.pairwise_shift_min_points,
+                           base_mean=torch.nanmean(self.base.float(), 1) if differs is not None else None)
         v = d.verdict.long()
         self.app_stats.index_put_((self.app_id.long(), torch.zeros_like(v)), (v == 1).int(), accumulate=True)
         self.app_stats.index_put_((self.app_id.long(), torch.ones_like(v)), (v >= 0).int(), accumulate=True)

@@ -921,7 +921,9 @@ class RolloutMonitor:
                                 min_valid=cfg.min_historical_points, want_band=True, app_id=self.app_id,
                                 app_stats=self.app_stats, anomalies=self.anomalies, threshold_low=thr_l,
                                 pw_min_points=cfg.pairwise_min_points,
-                                shift_threshold=cfg.pairwise_shift, horizon_variance=cfg.horizon_variance)
+                                shift_threshold=cfg.pairwise_shift, shift_min_points=cfg.pairwise_shift_min_points,
+                                base_mean=self.pw_out["base_mean"] if differs is not None else None,
+                                horizon_variance=cfg.horizon_variance)
             st = dict(self.state)
             st.update(self.out)
             out = K.hw_detect_deferred(st, spec, self.m_detect, self.m_detect,
@@ -944,7 +946,8 @@ class RolloutMonitor:
             d = det_ref.detect(f, sigma, self.win, thr_f, self.bound, self.min_lower, differs=differs,
                                pairwise_scale=cfg.pairwise_scale, model_ok=s["nvalid"] >= cfg.min_historical_points,
                                threshold_low=thr_l, pw_min_points=cfg.pairwise_min_points,
-                               shift_threshold=cfg.pairwise_shift)
+                               shift_threshold=cfg.pairwise_shift, shift_min_points=cfg.pairwise_shift_min_points,
+                               base_mean=torch.nanmean(self.base.float(), 1) if differs is not None else None)
             v = d.verdict.long()
             self.app_stats.index_put_((self.app_id.long(), torch.zeros_like(v)), (v == 1).int(), accumulate=True)
             self.app_stats.index_put_((self.app_id.long(), torch.ones_like(v)), (v >= 0).int(), accumulate=True)

@@ -21,15 +21,16 @@ window points ``x [N, C]``:
   but only when at least ``pw_min_points`` points fall outside it
   (``ML_PAIRWISE_MIN_ANOMALIES``); a single point outside the full band is
   always an anomaly (fail fast on spikes);
-* mean-shift rule (``shift_threshold`` > 0, ``ML_PAIRWISE_SHIFT``): when the
-  canary test says the pods differ and neither band fired, the series is
-  anomalous if the window's mean standardised deviation ``mean((x - f) / s)``
-  (at least ``pw_min_points`` points) is beyond ``shift_threshold`` on a side
+* mean-shift rule (``shift_threshold`` > 0, ``ML_PAIRWISE_SHIFT``, needs
+  ``base_mean``, the baseline pods' window mean): when the canary test says the
+  pods differ and neither band fired, the series is anomalous if the canary
+  window's mean deviation from the baseline mean, ``mean((x - base_mean) / s)``
+  (at least ``shift_min_points`` points), is beyond ``shift_threshold`` on a side
   enabled by ``bound`` -- the rank tests' evidence of a level shift, sized
-  against the model's spread; its band is ``f +- shift_threshold * s`` and its
-  count the points outside it.  A sustained shift of ~2 sigma leaves few points
-  outside a window-corrected band, but its mean is far outside the noise of a
-  50-point mean;
+  against the model's spread.  Its band is ``base_mean +- shift_threshold * s``
+  and its count the points outside it.  Measured against the baseline pods (not
+  the forecast), it is immune to forecast bias: healthy canaries sit on their
+  baseline whatever the model's error;
 * verdict per series: ``1`` anomalous, ``0`` healthy, ``-1`` unknown (no
   current point, or no model).  ``upper``/``lower`` are the band of the rule
   in force (lowered band only when it fired).
@@ -121,7 +122,8 @@ def detect(forecast: torch.Tensor, sigma: torch.Tensor, x: torch.Tensor,
            threshold: torch.Tensor, bound: torch.Tensor, min_lower: torch.Tensor,
            differs: Optional[torch.Tensor] = None, pairwise_scale: float = 0.5,
            model_ok: Optional[torch.Tensor] = None, threshold_low: Optional[torch.Tensor] = None,
-           pw_min_points: int = 1, shift_threshold: float = 0.0) -> Detection:
+           pw_min_points: int = 1, shift_threshold: float = 0.0,
+           base_mean: Optional[torch.Tensor] = None, shift_min_points: int = 1) -> Detection:
     """``sigma``: ``[N]`` or per point ``[N, C]`` (horizon-scaled).  ``threshold``
     / ``threshold_low`` are per-point levels (already window-corrected, see
     :func:`effective_thresholds`); ``threshold_low`` defaults to
@@ -150,21 +152,26 @@ def detect(forecast: torch.Tensor, sigma: torch.Tensor, x: torch.Tensor,
     cnt_l = an_l.sum(1)
     dif = torch.zeros(N, dtype=torch.bool, device=f.device) if differs is None else differs.bool()
     low_rule = dif & (cnt_l >= max(int(pw_min_points), 1))
-    zs = torch.where(valid, (xv - f) / sig.clamp(min=1e-12), torch.zeros_like(xv))
     shift_rule = torch.zeros_like(low_rule)
-    if shift_threshold > 0:
-        st = torch.full((N,), float(shift_threshold), device=f.device)
-        up_s, lo_s, an_s = outside(st)
+    use_shift = shift_threshold > 0 and base_mean is not None
+    if use_shift:
+        bm = base_mean.float().to(f.device).view(-1, 1)
+        st = float(shift_threshold)
+        up_s = bm + st * sig
+        lo_s = torch.maximum(bm - st * sig, mlow)
+        an_s = (((xv > up_s) & ((bnd & 1) != 0)) | ((xv < lo_s) & ((bnd & 2) != 0))) & valid & ok[:, None]
+        zb = torch.where(valid & ok[:, None], (xv - bm) / sig.clamp(min=1e-12), torch.zeros_like(xv))
         nz = (valid & ok[:, None]).sum(1)
-        mz = torch.where(ok[:, None], zs, torch.zeros_like(zs)).sum(1) / nz.clamp(min=1)
-        side = (((bnd[:, 0] & 1) != 0) & (mz > shift_threshold)) | (((bnd[:, 0] & 2) != 0) & (mz < -shift_threshold))
-        shift_rule = dif & ~low_rule & (cnt_f == 0) & (nz >= max(int(pw_min_points), 1)) & side
+        mz = zb.sum(1) / nz.clamp(min=1)
+        side = (((bnd[:, 0] & 1) != 0) & (mz > st)) | (((bnd[:, 0] & 2) != 0) & (mz < -st))
+        shift_rule = (dif & ~torch.isnan(bm[:, 0]) & ~low_rule & (cnt_f == 0)
+                      & (nz >= max(int(shift_min_points), 1)) & side)
     lr, sr = low_rule[:, None], shift_rule[:, None]
     upper = torch.where(lr, up_l, up_f)
     lower = torch.where(lr, lo_l, lo_f)
     anom = torch.where(lr, an_l, an_f)
     count = torch.where(low_rule, cnt_l, cnt_f)
-    if shift_threshold > 0:
+    if use_shift:
         upper, lower = torch.where(sr, up_s, upper), torch.where(sr, lo_s, lower)
         anom = torch.where(sr, an_s, anom)
         count = torch.where(shift_rule, an_s.sum(1), count)
@@ -172,6 +179,6 @@ def detect(forecast: torch.Tensor, sigma: torch.Tensor, x: torch.Tensor,
     has = valid.any(1) & ok
     verdict = torch.where(count > 0, torch.ones_like(count),
                           torch.where(has, torch.zeros_like(count), torch.full_like(count, -1)))
-    z = zs.abs()
+    z = torch.where(valid, (xv - f).abs() / sig.clamp(min=1e-12), torch.zeros_like(xv))
     return Detection(upper=upper, lower=lower, anomaly=anom, count=count,
                      verdict=verdict.to(torch.int8), score=z.amax(1))

@@ -39,7 +39,8 @@ class DetectArgs(C.Structure):
         ("hv_grid", P), ("hv_mode", I), ("hv_m", I),
         ("forecast", P), ("upper", P), ("lower", P), ("count", P), ("verdict", P),
         ("score", P), ("app_id", P), ("app_stats", P),
-        ("anom_count", P), ("anom_series", P), ("anom_col", P), ("anom_val", P), ("anom_cap", I), ("shift_thr", F),
+        ("anom_count", P), ("anom_series", P), ("anom_col", P), ("anom_val", P), ("anom_cap", I), ("shift_thr", F), ("base_mean", P),
+        ("shift_min_points", I), ("_pad1", I),
     ]
 
 
@@ -58,7 +59,7 @@ class RankArgs(C.Structure):
         ("nb", I), ("nc", I), ("N", I), ("mode", I), ("alpha", F),
         ("min_mw", I), ("min_wilcoxon", I), ("min_kruskal", I),
         ("pvals", P), ("differs", P), ("counts", P),
-        ("pods_b", I), ("pods_c", I), ("min_friedman", I), ("p_friedman", P),
+        ("pods_b", I), ("pods_c", I), ("min_friedman", I), ("p_friedman", P), ("base_mean", P),
     ]
 
 

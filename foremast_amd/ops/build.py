@@ -47,7 +47,8 @@ def headers() -> List[str]:
 
 
 def lib_path() -> str:
-    return os.path.join(LIBDIR, LIBNAME)
+    # FOREMAST_HIP_LIB: load another build of the library (same-box A/B of a kernel change)
+    return os.environ.get("FOREMAST_HIP_LIB") or os.path.join(LIBDIR, LIBNAME)
 
 
 def _needs(obj: str, deps: List[str]) -> bool:

@@ -39,7 +39,12 @@ struct DetectArgs {
   int* anom_col;                // [anom_cap]
   float* anom_val;              // [anom_cap]
   int anom_cap;
-  float shift_thr;              // > 0: mean-shift rule when differs (window mean of (x - f) / s beyond it)
+  // > 0: mean-shift rule when differs -- the window's mean of (x - base_mean) / s (canary
+  // points against the baseline pods' mean) beyond shift_thr; needs base_mean
+  float shift_thr;
+  const float* base_mean;       // [N] mean of the baseline pods' window (NaN: none) or null
+  int shift_min_points;         // the mean-shift rule needs this many valid canary points
+  int _pad1;
 };
 
 struct SmoothArgs {
@@ -94,6 +99,7 @@ struct RankArgs {
   int pods_c;
   int min_friedman;        // complete blocks needed
   float* p_friedman;       // [N, 2] (p, complete blocks) or null; computed when set or mode == 6
+  float* base_mean;        // [N] mean of the valid baseline values (NaN if none) or null
 };
 
 struct WindowArgs {

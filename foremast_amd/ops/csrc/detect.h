@@ -57,10 +57,10 @@ __device__ __forceinline__ float hstep_factor(const DetectArgs& d, int gidx, int
 // band (threshold) and, when the canary test says baseline and current differ,
 // the lowered band (threshold_low, or threshold * pw_scale) — which only counts
 // when at least pw_min_points points fall outside it — and the mean-shift rule
-// (shift_thr > 0): the window's mean standardised deviation beyond shift_thr on
-// an enabled side.
+// (shift_thr > 0): the window's mean deviation from the baseline pods' mean, in
+// units of the spread s, beyond shift_thr on an enabled side.
 struct DetThr {
-  float full, low, shift;
+  float full, low, shift, bm;
   bool differs, shift_on;
 };
 __device__ __forceinline__ DetThr det_thresholds(const DetectArgs& d, int n) {
@@ -69,7 +69,8 @@ __device__ __forceinline__ DetThr det_thresholds(const DetectArgs& d, int n) {
   t.differs = d.differs && d.differs[n];
   t.low = d.threshold_low ? d.threshold_low[n] : t.full * d.pw_scale;
   t.shift = d.shift_thr;
-  t.shift_on = t.differs && d.shift_thr > 0.f;
+  t.bm = (d.base_mean && t.differs) ? d.base_mean[n] : fm_nan();
+  t.shift_on = t.differs && d.shift_thr > 0.f && t.bm == t.bm;
   return t;
 }
 
@@ -92,29 +93,30 @@ __device__ __forceinline__ void det_count_col(const DetectArgs& d, int n, int c,
   const int h = d.horizons[d.h_ld * n + c];
   const float f = fcast(h);
   const float s = sig * hstep_factor(d, gidx, h);
-  const float z = (x - f) / fmaxf(s, 1e-12f);
   if (model_ok) {
     u.cnt_f += det_outside(x, f, t.full, s, mlow, bnd) ? 1.f : 0.f;
     if (t.differs) u.cnt_l += det_outside(x, f, t.low, s, mlow, bnd) ? 1.f : 0.f;
     if (t.shift_on) {
-      u.cnt_s += det_outside(x, f, t.shift, s, mlow, bnd) ? 1.f : 0.f;
-      u.zsum += z;
+      u.cnt_s += det_outside(x, t.bm, t.shift, s, mlow, bnd) ? 1.f : 0.f;
+      u.zsum += (x - t.bm) / fmaxf(s, 1e-12f);
       u.nz += 1.f;
     }
   }
-  u.sc = fmaxf(u.sc, fabsf(z));
+  u.sc = fmaxf(u.sc, fabsf(x - f) / fmaxf(s, 1e-12f));
 }
 
-// Pass 2 of a column: band of the rule in force, and the K9 list (rare: one atomic
+// Pass 2 of a column: band of the rule in force (centred on the forecast, or on the
+// baseline mean `center` for the mean-shift rule), and the K9 list (rare: one atomic
 // per anomalous point of an anomalous series).
 template <typename ForecastFn>
 __device__ __forceinline__ void det_emit_col(const DetectArgs& d, int n, int c, float thr, float sig, int gidx, int bnd,
-                                             float mlow, bool emit, ForecastFn& fcast) {
+                                             float mlow, bool emit, ForecastFn& fcast, float center) {
   const int h = d.horizons[d.h_ld * n + c];
   const float f = fcast(h);
   const float s = sig * hstep_factor(d, gidx, h);
-  const float up = f + thr * s;
-  const float lo = fmaxf(f - thr * s, mlow);
+  const float fc = center == center ? center : f;
+  const float up = fc + thr * s;
+  const float lo = fmaxf(fc - thr * s, mlow);
   const long long o = (long long)n * d.C + c;
   if (d.forecast) d.forecast[o] = f;
   if (d.upper) d.upper[o] = up;
@@ -133,18 +135,21 @@ __device__ __forceinline__ void det_emit_col(const DetectArgs& d, int n, int c, 
 }
 
 // Verdict from the reduced sums; returns the threshold of the rule in force and
-// sets *count (anomalous points under that rule).  Precedence: lowered band, full
-// band, mean shift (whose band is f +- shift_thr * s).
+// sets *count (anomalous points under that rule) and *center (NaN: the band is
+// centred on the forecast).  Precedence: lowered band, full band, mean shift (whose
+// band is base_mean +- shift_thr * s).
 __device__ __forceinline__ float det_decide(const DetectArgs& d, const DetThr& t, const DetSums& u, int bnd,
-                                            int* count) {
+                                            int* count, float* center) {
+  *center = fm_nan();
   if (t.differs && u.cnt_l >= (float)max(d.pw_min_points, 1)) {
     *count = (int)u.cnt_l;
     return t.low;
   }
-  if (u.cnt_f <= 0.f && t.shift_on && u.nz >= (float)max(d.pw_min_points, 1)) {
+  if (u.cnt_f <= 0.f && t.shift_on && u.nz >= (float)max(d.shift_min_points, 1)) {
     const float mz = u.zsum / u.nz;
     if (((bnd & 1) && mz > t.shift) || ((bnd & 2) && mz < -t.shift)) {
       *count = (int)u.cnt_s;
+      *center = t.bm;
       return t.shift;
     }
   }
@@ -177,7 +182,7 @@ __device__ __forceinline__ void detect_epilogue_wave(const DetectArgs& d, int n,
   const int bnd = d.bound[n];
   const float mlow = d.min_lower[n];
   const bool model_ok = n_valid >= (float)d.min_valid;
-  float thr = t.full;
+  float thr = t.full, center = fm_nan();
   int ic = 0;
   DetSums u;
   if (d.cur) {
@@ -191,12 +196,12 @@ __device__ __forceinline__ void detect_epilogue_wave(const DetectArgs& d, int n,
     }
     u.anyv = wave_allmax(u.anyv);
     u.sc = wave_allmax(u.sc);
-    thr = det_decide(d, t, u, bnd, &ic);
+    thr = det_decide(d, t, u, bnd, &ic, &center);
   }
   const float anyv = u.anyv, sc = u.sc;
   const bool emit = d.anom_count && ic > 0;
   if (d.forecast || d.upper || d.lower || emit)
-    for (int c = lane; c < d.C; c += FM_WAVE) det_emit_col(d, n, c, thr, sig, gidx, bnd, mlow, emit, fcast);
+    for (int c = lane; c < d.C; c += FM_WAVE) det_emit_col(d, n, c, thr, sig, gidx, bnd, mlow, emit, fcast, center);
   if (d.cur && lane == 0) det_write(d, n, ic, anyv, model_ok, sc);
 }
 
@@ -210,7 +215,7 @@ __device__ __forceinline__ void detect_epilogue(const DetectArgs& d, int n, floa
   const int bnd = d.bound[n];
   const float mlow = d.min_lower[n];
   const bool model_ok = n_valid >= (float)d.min_valid;
-  float thr = t.full;
+  float thr = t.full, center = fm_nan();
   int ic = 0;
   DetSums u;
   if (d.cur) {
@@ -224,11 +229,11 @@ __device__ __forceinline__ void detect_epilogue(const DetectArgs& d, int n, floa
     }
     u.anyv = blk_max(u.anyv, red);
     u.sc = blk_max(u.sc, red);
-    thr = det_decide(d, t, u, bnd, &ic);
+    thr = det_decide(d, t, u, bnd, &ic, &center);
   }
   const float anyv = u.anyv, sc = u.sc;
   const bool emit = d.anom_count && ic > 0;
   if (d.forecast || d.upper || d.lower || emit)
-    for (int c = tid; c < d.C; c += blockDim.x) det_emit_col(d, n, c, thr, sig, gidx, bnd, mlow, emit, fcast);
+    for (int c = tid; c < d.C; c += blockDim.x) det_emit_col(d, n, c, thr, sig, gidx, bnd, mlow, emit, fcast, center);
   if (d.cur && tid == 0) det_write(d, n, ic, anyv, model_ok, sc);
 }

@@ -953,6 +953,9 @@ __device__ __forceinline__ void d_pass1(const float* blk, cfp W, v2f* D, v2f& p1
       if (i < K) {
         const float d = c.get(r);
         D[i] = splat2(d);
+        // a 64-bit register pair from the start: left as one 32-bit value used twice, the
+        // season loop's D registers were re-paired by 48 copies on every iteration
+        asm volatile("" : "+v"(D[i]));
         p1 = p1 + ldv2(W + 4 * i) * D[i];
         p2 = p2 + ldv2(W + 4 * i + 2) * D[i];
       }

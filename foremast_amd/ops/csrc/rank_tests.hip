@@ -139,13 +139,16 @@ __global__ __launch_bounds__(256) void rank_tests_kernel(const RankArgs a) {
   // stage pooled sample (NaN pads the vector tail) and |d| of aligned pairs
   const float* b = a.base + (long long)n * a.ld_base;
   const float* c = a.cur + (long long)n * a.ld_cur;
-  float cnt_b = 0.f, cnt_c = 0.f;
+  float cnt_b = 0.f, cnt_c = 0.f, sum_b = 0.f;
   for (int i = lane; i < npool4; i += FM_WAVE) {
     float v = fm_nan();
     if (i < a.nb) v = b[i];
     else if (i < npool) v = c[i - a.nb];
     x[i] = v;
-    if (v == v) { if (i < a.nb) cnt_b += 1.f; else cnt_c += 1.f; }
+    if (v == v) {
+      if (i < a.nb) { cnt_b += 1.f; sum_b += v; }
+      else cnt_c += 1.f;
+    }
   }
   float npairs = 0.f;
   for (int i = lane; i < k4; i += FM_WAVE) {
@@ -159,6 +162,7 @@ __global__ __launch_bounds__(256) void rank_tests_kernel(const RankArgs a) {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   const float n1 = wave_sum(cnt_b), n2 = wave_sum(cnt_c), np = wave_sum(npairs);
+  const float sb = a.base_mean ? wave_sum(sum_b) : 0.f;
   const float nn = n1 + n2;
 
   // --- Friedman (time blocks x pods) on the staged windows
@@ -219,6 +223,7 @@ __global__ __launch_bounds__(256) void rank_tests_kernel(const RankArgs a) {
     default: d = false;
   }
   a.differs[n] = d ? 1 : 0;
+  if (a.base_mean) a.base_mean[n] = n1 > 0.f ? sb / n1 : fm_nan();
   if (a.p_friedman) {
     a.p_friedman[2 * (long long)n + 0] = p_fr;
     a.p_friedman[2 * (long long)n + 1] = nblk;

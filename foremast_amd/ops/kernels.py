@@ -73,8 +73,11 @@ class DetectSpec:
     pw_min_points: int = 1
     # scale sigma by the h-step forecast-error factor of the fitted smoothing model
     horizon_variance: bool = True
-    # > 0: mean-shift rule when ``differs`` (models/detect.py ``shift_threshold``)
+    # > 0: mean-shift rule when ``differs`` (models/detect.py ``shift_threshold``), against
+    # ``base_mean`` (float32 [N], the baseline pods' window mean: rank_tests out["base_mean"])
     shift_threshold: float = 0.0
+    base_mean: Optional[torch.Tensor] = None
+    shift_min_points: int = 1
 
 
 class AnomalyBuffer:
@@ -160,6 +163,8 @@ def _fill_detect(d: nat.DetectArgs, spec: DetectSpec, N: int, device, out: Dict[
     d.pw_scale = float(spec.pw_scale)
     d.pw_min_points = int(spec.pw_min_points)
     d.shift_thr = float(spec.shift_threshold)
+    d.base_mean = nat.ptr(spec.base_mean)
+    d.shift_min_points = int(spec.shift_min_points)
     d.threshold_low = nat.ptr(spec.threshold_low)
     d.hv_grid, d.hv_mode, d.hv_m = None, 0, 0
     d.forecast = nat.ptr(out.get("forecast"))
@@ -603,6 +608,8 @@ def rank_tests(base: torch.Tensor, cur: torch.Tensor, mode: int, alpha: float, m
     out = {} if out is None else out
     if "differs" not in out:
         out["differs"] = torch.empty(N, dtype=torch.uint8, device=dev)
+    if "base_mean" not in out:  # the mean-shift rule's centre (DetectSpec.base_mean)
+        out["base_mean"] = torch.empty(N, dtype=torch.float32, device=dev)
     if want_pvals:
         if "pvals" not in out:
             out["pvals"] = torch.empty((N, 3), dtype=torch.float32, device=dev)
@@ -619,6 +626,7 @@ def rank_tests(base: torch.Tensor, cur: torch.Tensor, mode: int, alpha: float, m
     a.pvals = nat.ptr(out.get("pvals")) if want_pvals else 0
     a.counts = nat.ptr(out.get("counts")) if want_pvals else 0
     a.differs = nat.ptr(out["differs"])
+    a.base_mean = nat.ptr(out["base_mean"])
     pb, pc = pods if pods is not None else (1, 1)
     fr = want_friedman or int(mode) == 6
     if fr:

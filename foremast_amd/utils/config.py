@@ -85,6 +85,7 @@ class BrainConfig:
     # differ, a window whose mean deviation from the forecast is beyond this many sigmas
     # is anomalous even if few of its points leave the window-corrected band
     pairwise_shift: float = 1.5
+    pairwise_shift_min_points: int = 20  # ML_PAIRWISE_SHIFT_MIN_POINTS (as MIN_MANN_WHITE_DATA_POINTS)
     window_correction: str = "sidak"
     horizon_variance: bool = True
     poll_seconds: float = 5.0
@@ -155,6 +156,7 @@ class BrainConfig:
         c.poll_seconds = f("FOREMAST_POLL_SECONDS", c.poll_seconds)
         c.pairwise_min_points = int(f("ML_PAIRWISE_MIN_ANOMALIES", c.pairwise_min_points, int))
         c.pairwise_shift = f("ML_PAIRWISE_SHIFT", c.pairwise_shift)
+        c.pairwise_shift_min_points = int(f("ML_PAIRWISE_SHIFT_MIN_POINTS", c.pairwise_shift_min_points, int))
         c.window_correction = (e.get("FOREMAST_WINDOW_CORRECTION") or c.window_correction).strip().lower()
         c.horizon_variance = e.get("FOREMAST_HORIZON_VARIANCE", "1").strip().lower() not in ("0", "false", "no")
         # FOREMAST_DETECTION_PRESET=reference: the reference brain's documented per-point

@@ -27,7 +27,9 @@ def test_rank_stopped_inside_exchange_survivors_reform(tmp_path):
     procs, outs = [], []
     for i in range(n):
         out = tmp_path / f"rank{i}.jsonl"
-        env = dict(os.environ, OMP_NUM_THREADS="1", CUDA_VISIBLE_DEVICES="")
+        # gloo pairs over loopback: resolving the container hostname can hand out interfaces
+        # whose connects time out under load (then the first exchange misses its deadline)
+        env = dict(os.environ, OMP_NUM_THREADS="1", CUDA_VISIBLE_DEVICES="", GLOO_SOCKET_IFNAME="lo")
         if i == 2:
             env["FOREMAST_FAULT"] = "exchange:3"
         procs.append(subprocess.Popen([sys.executable, HELPER, str(port), str(i), str(n), str(hb), str(ticks),

@@ -250,6 +250,8 @@ def test_rank_tests_kernel(K):
     dref = pw_ref.pairwise_differs(ref, pw_ref.PW_ALL, 0.05)
     agree = (out["differs"].cpu().bool() == dref).float().mean()
     assert agree > 0.99
+    # the baseline window means (the mean-shift rule's centre)
+    np.testing.assert_allclose(out["base_mean"].cpu().numpy(), np.nanmean(b, 1), rtol=1e-5, atol=1e-6)
 
 
 def test_rank_tests_kernel_friedman(K):
@@ -597,13 +599,16 @@ def test_two_rule_detection_matches_reference(K, which, shift):
         lift = (torch.arange(N, device=dev) % 8 >= 6).float()[:, None]
         cur = (cur + lift * sgn * 1.3 * shift * scale).contiguous()
     differs = (torch.arange(N, device=dev) % 2).to(torch.uint8)
+    # baseline pods: on the history's level (+ noise), none for every 32nd series
+    bmean = (hf[:, -C:].mean(1) + torch.randn((N,), generator=g, device=dev) * scale[:, 0] * 0.2).contiguous()
+    bmean[::32] = float("nan")
     thr = torch.full((N,), 3.0, device=dev)
     bound = torch.tensor([1, 2, 3, 3], dtype=torch.int8, device=dev).repeat(N // 4)
     full, low = det_ref.effective_thresholds(thr.cpu(), bound.cpu(), C, 0.5, "sidak")
     spec = K.DetectSpec(horizons=torch.arange(1, C + 1, dtype=torch.int32, device=dev), threshold=full.to(dev),
                         bound=bound, min_lower=torch.full((N,), -1e9, device=dev), cur=cur, differs=differs,
                         threshold_low=low.to(dev), pw_min_points=3, anomalies=K.AnomalyBuffer(N * C, dev),
-                        max_horizon=C, shift_threshold=shift)
+                        max_horizon=C, shift_threshold=shift, base_mean=bmean, shift_min_points=5)
     spec.anomalies.reset()
     grid = sm_ref.make_grid(sm_ref.MODE_HW, (0.1, 0.5), (0.0, 0.1), (0.1, 0.5)).to(dev)
     if which == "window_stats":
@@ -622,7 +627,8 @@ def test_two_rule_detection_matches_reference(K, which, shift):
                                                                         torch.arange(1, C + 1))
     torch.cuda.synchronize()
     d = det_ref.detect(out["forecast"].cpu(), sig, cur.cpu(), full, bound.cpu(), torch.full((N,), -1e9),
-                       differs=differs.cpu(), threshold_low=low, pw_min_points=3, shift_threshold=shift)
+                       differs=differs.cpu(), threshold_low=low, pw_min_points=3, shift_threshold=shift,
+                       base_mean=bmean.cpu(), shift_min_points=5)
     assert torch.equal(d.verdict, out["verdict"].cpu())
     assert torch.equal(d.count, out["count"].cpu())
     low_fired = (differs.cpu().bool() & (d.count > 0))

@@ -291,29 +291,38 @@ def test_pairwise_lowered_band_needs_min_points():
 
 
 def test_pairwise_mean_shift_rule():
-    """With differs and no band fired, a window whose mean standardised deviation is
-    beyond shift_threshold (on a side bound enables) is anomalous; its band is
-    f +- shift * s and its count the points outside it."""
-    f = torch.zeros(5, 10)
-    sig = torch.ones(5)
-    x = torch.full((5, 10), 1.6)    # every point 1.6 sigma up: inside both bands
+    """With differs and no band fired, a canary window whose mean deviation from the
+    baseline pods' mean is beyond shift_threshold sigmas (on a side bound enables) is
+    anomalous; its band is base_mean +- shift * s and its count the points outside it.
+    A forecast error does not trigger it: only the distance to the baseline counts."""
+    f = torch.zeros(6, 10)
+    sig = torch.ones(6)
+    x = torch.full((6, 10), 1.6)    # every point 1.6 sigma above the baseline: inside both bands
     x[1] = -1.6                      # down, upper-only bound below
     x[2, :5] = 0.0                   # mean 0.8: below the shift threshold
     x[4, 0] = float("nan")           # missing points do not count
-    thr, low = torch.full((5,), 4.0), torch.full((5,), 2.0)
-    bound = torch.tensor([3, 1, 3, 3, 2], dtype=torch.int8)
-    differs = torch.tensor([1, 1, 1, 0, 1], dtype=torch.uint8)
-    kw = dict(differs=differs, threshold_low=low, pw_min_points=3)
-    d0 = detect.detect(f, sig, x, thr, bound, torch.full((5,), -1e9), **kw)
-    assert d0.verdict.tolist() == [0, 0, 0, 0, 0]
-    d = detect.detect(f, sig, x, thr, bound, torch.full((5,), -1e9), shift_threshold=1.5, **kw)
-    assert d.verdict.tolist() == [1, 0, 0, 0, 0]  # row 4: upward shift, lower-only bound
-    assert d.count.tolist() == [10, 0, 0, 0, 0]
+    bm = torch.zeros(6)
+    bm[5] = 1.6                      # canary on its baseline, 1.6 sigma off the forecast: healthy
+    thr, low = torch.full((6,), 4.0), torch.full((6,), 2.0)
+    bound = torch.tensor([3, 1, 3, 3, 2, 3], dtype=torch.int8)
+    differs = torch.tensor([1, 1, 1, 0, 1, 1], dtype=torch.uint8)
+    kw = dict(differs=differs, threshold_low=low, pw_min_points=3, shift_min_points=9)
+    d0 = detect.detect(f, sig, x, thr, bound, torch.full((6,), -1e9), **kw)
+    assert d0.verdict.tolist() == [0] * 6
+    d = detect.detect(f, sig, x, thr, bound, torch.full((6,), -1e9), shift_threshold=1.5, base_mean=bm, **kw)
+    assert d.verdict.tolist() == [1, 0, 0, 0, 0, 0]  # row 4: upward shift, lower-only bound
+    assert d.count.tolist() == [10, 0, 0, 0, 0, 0]
     assert float(d.upper[0, 0]) == 1.5 and float(d.upper[2, 0]) == 4.0
     x[4] = -1.6
     x[4, 0] = float("nan")
-    d = detect.detect(f, sig, x, thr, bound, torch.full((5,), -1e9), shift_threshold=1.5, **kw)
-    assert d.verdict.tolist() == [1, 0, 0, 0, 1] and d.count.tolist()[4] == 9
+    d = detect.detect(f, sig, x, thr, bound, torch.full((6,), -1e9), shift_threshold=1.5, base_mean=bm, **kw)
+    assert d.verdict.tolist() == [1, 0, 0, 0, 1, 0] and d.count.tolist()[4] == 9
+    d = detect.detect(f, sig, x, thr, bound, torch.full((6,), -1e9), shift_threshold=1.5, base_mean=bm,
+                      **{**kw, "shift_min_points": 10})
+    assert d.verdict.tolist() == [1, 0, 0, 0, 0, 0]  # row 4 has 9 valid points: too few
+    bm[0] = float("nan")             # no baseline values: no mean-shift rule
+    d = detect.detect(f, sig, x, thr, bound, torch.full((6,), -1e9), shift_threshold=1.5, base_mean=bm, **kw)
+    assert d.verdict.tolist()[0] == 0
 
 
 def test_decompose_forecast_continues_trend_and_season():
