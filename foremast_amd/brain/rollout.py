@@ -1083,6 +1083,7 @@ class RolloutMonitor:
             items.append((jid, fields))
         res = self.store.update_many(items, expect_claimed_by=self.worker_id)
         written = {}
+        freed: List[int] = []  # every finished job's rows, released in ONE batch of device fills
         for (jid, fields), ok in zip(items, res):
             if ok:
                 self.metrics.jobs.labels(status=fields["status"]).inc()
@@ -1095,11 +1096,12 @@ class RolloutMonitor:
                         self.metrics.export_band(s.hkey[1], s.hkey[2], s.hkey[3], float(up[row]), float(lo[row]),
                                                  self._last_anom.get(row))
                 self.history.unwant([s.hkey for s in p.series], now)
-                self._free_rows(p.rows)
+                freed += p.rows
                 self.slots.release(self._job_pods(p))
                 self._app_ref(p, -1)
                 for row in p.rows:
                     self._last_anom.pop(row, None)
+        self._free_rows(freed)
         return written
 
     # ------------------------------------------------------------------ node integration
