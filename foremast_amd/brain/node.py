@@ -115,6 +115,8 @@ class NodeBrain:
         for m in self.monitors:
             if hasattr(m, "after_reform"):
                 m.after_reform()
+            if getattr(m, "router", None) is not None:
+                m.router.reset(kv=dist.PrefixStore("affine", self.world.pstore))
         self.health.reset(kv=self.world.pstore)
         log.warning("node re-formed: generation %d, members %s (lost %s); released %d moved jobs",
                     self.world.generation, self.world.members, sorted(gone), moved)
@@ -197,6 +199,9 @@ class NodeBrain:
         if self.world is not None and not dist.is_initialized():
             self.world.form()
             self.health.reset(kv=self.world.pstore)
+            for m in self.monitors:
+                if getattr(m, "router", None) is not None:
+                    m.router.reset(kv=dist.PrefixStore("affine", self.world.pstore))
             self.world.start_heartbeat()
         try:
             while not stop.is_set():

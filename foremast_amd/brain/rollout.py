@@ -971,10 +971,12 @@ class RolloutMonitor:
         verdicts; returns job -> status written."""
         t_tick = time.perf_counter()
         now = self.clock()
-        self.store.heartbeat(self.worker_id, now)
         t_new = float(np.floor(now / self.step) * self.step)
         t0 = time.perf_counter()
         try:
+            # inside the guard: a store error on this rank must not skip the lockstep
+            # exchange below, or its peers' all_to_all would pair with another collective
+            self.store.heartbeat(self.worker_id, now)
             await self.history.sync(now)
             self.timings["history_ms"] = (time.perf_counter() - t0) * 1e3
             await self._admit(now)

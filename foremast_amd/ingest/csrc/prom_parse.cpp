@@ -44,6 +44,7 @@
 #include <condition_variable>
 #include <functional>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -1016,4 +1017,47 @@ extern "C" long long fm_key_hashes(const char* A, const long long* a_off, const 
     out[i] = series_key(a, a + a_len[i], b, b + b_len[i]);
   }
   return n;
+}
+
+// Encoder of the same wire format (the Prometheus side of the node benchmarks and
+// tests): series s is {"metric":{<labels[lab_off[s] .. lab_off[s + 1])>},"values":[[t,"v"],...]}
+// with T points at ts0 + j * step; NaN values are omitted (Prometheus returns no
+// sample for a missing scrape).  Values print as the shortest decimal that reads back
+// as the same float (std::to_chars).  Returns the bytes written, or -(bytes needed)
+// when `cap` is too small.
+extern "C" long long fm_prom_render(const char* labels, const long long* lab_off, long long S, const float* vals,
+                                    long long T, double ts0, double step, char* out, long long cap) {
+  if (S < 0 || T < 0) return 0;
+  static const char head[] = "{\"status\":\"success\",\"data\":{\"resultType\":\"matrix\",\"result\":[";
+  static const char tail[] = "]}}";
+  std::string buf;
+  buf.reserve((size_t)(S * (64 + 28 * T)) + 128);
+  buf.append(head);
+  char num[64];
+  for (long long s = 0; s < S; ++s) {
+    if (s) buf.push_back(',');
+    buf.append("{\"metric\":{");
+    buf.append(labels + lab_off[s], (size_t)(lab_off[s + 1] - lab_off[s]));
+    buf.append("},\"values\":[");
+    bool first = true;
+    for (long long j = 0; j < T; ++j) {
+      const float v = vals[s * T + j];
+      if (std::isnan(v)) continue;
+      if (!first) buf.push_back(',');
+      first = false;
+      buf.push_back('[');
+      const double t = ts0 + (double)j * step;
+      auto r = std::to_chars(num, num + sizeof(num), (long long)std::llround(t));
+      buf.append(num, r.ptr);
+      buf.append(",\"");
+      r = std::to_chars(num, num + sizeof(num), v);
+      buf.append(num, r.ptr);
+      buf.append("\"]");
+    }
+    buf.append("]}");
+  }
+  buf.append(tail);
+  if ((long long)buf.size() > cap) return -(long long)buf.size();
+  std::memcpy(out, buf.data(), buf.size());
+  return (long long)buf.size();
 }

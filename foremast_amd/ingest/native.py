@@ -72,6 +72,8 @@ def _load() -> Optional[C.CDLL]:
         lib.fm_prom_dense_keyed.restype = LL
         lib.fm_prom_keys.argtypes = [C.c_char_p, LL, LL, C.c_char_p, C.c_char_p, P]
         lib.fm_prom_keys.restype = LL
+        lib.fm_prom_render.argtypes = [C.c_char_p, P, LL, P, LL, C.c_double, C.c_double, P, LL]
+        lib.fm_prom_render.restype = LL
         lib.fm_keyindex_new.argtypes = [P, P, LL]
         lib.fm_keyindex_new.restype = P
         lib.fm_keyindex_free.argtypes = [P]
@@ -431,3 +433,33 @@ def _parse_py(body: bytes):
         vals = np.array([float(p[1]) for p in pts], dtype=np.float32)
         out.append((r.get("metric", {}), ts, vals))
     return out
+
+
+def label_blob(labels: List[str]) -> Tuple[bytes, np.ndarray]:
+    """Label objects (the text between the braces of ``"metric":{...}``) packed for
+    :func:`render_matrix`: one blob and ``S + 1`` byte offsets."""
+    enc = [x.encode() for x in labels]
+    off = np.zeros(len(enc) + 1, dtype=np.int64)
+    np.cumsum([len(e) for e in enc], out=off[1:])
+    return b"".join(enc), off
+
+
+def render_matrix(blob: Tuple[bytes, np.ndarray], vals: np.ndarray, ts0: float, step: float) -> bytes:
+    """A ``query_range`` matrix body for S series x T points (``vals`` [S, T] float32,
+    NaN = no sample) at ``ts0 + j * step`` — the encoder the benchmarks' Prometheus
+    stand-in uses (native, ~20x a Python f-string renderer)."""
+    lib = _load()
+    if lib is None:
+        raise RuntimeError("native ingest library unavailable")
+    labels, off = blob
+    v = np.ascontiguousarray(vals, dtype=np.float32)
+    S, T = (v.shape[0], v.shape[1]) if v.ndim == 2 else (v.shape[0], 1)
+    assert off.shape[0] == S + 1, "one label object per series"
+    cap = int(S * (40 + 32 * T) + off[-1] + 256)
+    while True:
+        out = np.empty(cap, dtype=np.uint8)
+        n = lib.fm_prom_render(labels, off.ctypes.data, S, v.ctypes.data, T, float(ts0), float(step),
+                               out.ctypes.data, cap)
+        if n >= 0:
+            return out[:n].tobytes()
+        cap = -n

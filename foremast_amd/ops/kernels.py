@@ -835,7 +835,7 @@ def decompose_score(hist: torch.Tensor, head: int, length: int, m: int, det: Det
     """Seasonal-decomposition scorer (``ML_ALGORITHM=seasonal_decompose``): K4 over
     the ring window without the ``[N, T]`` outputs, forecast = extrapolated trend +
     phase mean, sigma = residual RMS, then the fused band / verdict epilogue
-    (models/decompose.py ``decompose_forecast``).  An even period (``m % 8 == 0``) on an
+    (models/decompose.py ``decompose_forecast``).  A period with ``m % 16 == 0`` on an
     aligned ring takes the single-pass kernel (gap-free series; a series with a gap
     is finished by the general kernel from a device-side list).  ``phase_means``:
     also write the centred ``[N, m]`` phase means (576 MB at 100k x 1440 — off for

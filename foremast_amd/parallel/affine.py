@@ -14,10 +14,13 @@ canary — are fetched and decoded by that cluster's rank and delivered to the
 owner in the node's lockstep tick:
 
 1. one ``all_gather`` of per-rank request counts (an int per rank, every tick);
-2. when any rank has requests: ``all_gather_object`` of the requests
-   ``(family, start, n_points, [(namespace, pod), ...])``, every rank fetches
-   and decodes the requests of its own clusters, and ONE ``all_to_all_single``
-   (RCCL over xGMI on the GPU) returns the ``[pods, n_points]`` values to the
+2. when any rank has requests: every rank publishes its requests
+   ``(family, start, n_points, [(namespace, pod), ...])`` in the node's key-value
+   store and reads its peers' with a deadline (no object collective: a dead peer
+   raises :class:`~foremast_amd.parallel.comm.CollectiveTimeout` instead of
+   wedging the rank), every rank fetches and decodes the requests of its own
+   clusters, and ONE ``all_to_all_single`` (RCCL over xGMI on the GPU, waited for
+   with the same deadline) returns the ``[pods, n_points]`` values to the
    requesters, in an order every rank derives from the gathered requests.
 
 Affinity: ``FOREMAST_CLUSTER_AFFINITY="<endpoint>=<rank>,..."`` or a stable
@@ -26,6 +29,8 @@ hash of the endpoint over the ranks.
 
 from __future__ import annotations
 
+import datetime
+import json
 import os
 import zlib
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
@@ -56,13 +61,41 @@ def affinity_from_env() -> Callable[[str, int], int]:
 
 class ClusterRouter:
     def __init__(self, rank_of: Callable[[str, int], int], device, group=None,
-                 timeout_s: Optional[float] = None) -> None:
+                 timeout_s: Optional[float] = None, kv=None) -> None:
         self.rank_of = rank_of
         self.device = torch.device(device)
         self.group = group
         self.timeout_s = comm.exchange_timeout_s() if timeout_s is None else float(timeout_s)
+        self.kv = kv        # request store (None: the default process group's store)
+        self.seq = 0        # exchanges with requests so far (lockstep: equal on every rank)
         self.exchanges = 0
         self.values_moved = 0
+
+    def reset(self, kv=None) -> None:
+        """After a re-formation: the new generation's store, sequence from zero."""
+        self.kv, self.seq = kv, 0
+
+    def _store(self):
+        if self.kv is None:
+            self.kv = dist.PrefixStore("affine", dist.distributed_c10d._get_default_store())
+        return self.kv
+
+    def _gather_requests(self, mine: Sequence[Request], world: int, rank: int) -> List[List[Request]]:
+        kv, seq = self._store(), self.seq
+        kv.set(f"req/{seq}/{rank}", json.dumps([[list(q[0]), q[1], q[2], [list(p) for p in q[3]]] for q in mine]))
+        out: List[List[Request]] = []
+        for r in range(world):
+            if r == rank:
+                out.append(list(mine))
+                continue
+            key = f"req/{seq}/{r}"
+            try:
+                kv.wait([key], datetime.timedelta(seconds=self.timeout_s))
+                raw = json.loads(kv.get(key))
+            except Exception as e:  # noqa: BLE001 - store timeout: the peer is gone
+                raise comm.CollectiveTimeout(f"affine requests of rank {r} (exchange {seq}) not published: {e}") from e
+            out.append([(tuple(q[0]), float(q[1]), int(q[2]), [tuple(p) for p in q[3]]) for q in raw])
+        return out
 
     @property
     def rank(self) -> int:
@@ -89,8 +122,7 @@ class ClusterRouter:
         comm.wait_bounded(work, self.timeout_s, "affine request counts")
         if int(counts.sum()) == 0:
             return []
-        gathered: List[Optional[List[Request]]] = [None] * world
-        dist.all_gather_object(gathered, list(mine), group=self.group)
+        gathered = self._gather_requests(mine, world, rank)
         self.exchanges += 1
         # every rank derives the same order: requester q's requests by index, routed to the
         # rank whose cluster serves the family
@@ -111,6 +143,12 @@ class ClusterRouter:
         work = dist.all_to_all_single(recv_t, send_t, output_split_sizes=recv_sizes, input_split_sizes=send_sizes,
                                       group=self.group, async_op=True)
         comm.wait_bounded(work, self.timeout_s, "affine window all-to-all")
+        # every peer entered the all-to-all, so every peer has read this exchange's requests
+        try:
+            self._store().delete_key(f"req/{self.seq}/{rank}")
+        except Exception:  # noqa: BLE001 - best-effort cleanup
+            pass
+        self.seq += 1
         self.values_moved += int(recv_t.numel())
         recv = recv_t.cpu().numpy()
         offs = np.concatenate([[0], np.cumsum(recv_sizes)])

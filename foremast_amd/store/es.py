@@ -35,7 +35,19 @@ from .jobstore import JobStore, is_claimable
 INDEX = "documents"
 DOC_TYPE = "document"
 META_INDEX = "foremast-engine"
-BEAT_TYPE = "worker"  # worker heartbeats (lease renewal), next to the engine records
+# Worker heartbeats (lease renewal) get an index of their own: ES 6.x allows one mapping
+# type per index, so they cannot share META_INDEX (type ``document``) under another type.
+BEAT_INDEX = "foremast-workers"
+PAGE = 1000  # hits per search page
+
+
+def _kw(field: str) -> str:
+    """Exact-match name of a string field.  Under ES dynamic mapping (how the reference
+    service creates ``documents``: ``elasticsearchstore.go:54-59`` indexes without a
+    mapping) a string is analysed ``text`` — ``node-m0-rollout`` is stored as the tokens
+    ``node`` / ``m0`` / ``rollout`` — with an exact ``.keyword`` sub-field; ``terms``
+    filters must use the latter."""
+    return field + ".keyword"
 
 
 class ElasticJobStore(JobStore):
@@ -109,10 +121,10 @@ class ElasticJobStore(JobStore):
                 return True
         return False
 
-    def _search(self, statuses, size: int = 1000, extra=(), must_not=(), index: Optional[str] = None,
-                doc_type: Optional[str] = None) -> List[Tuple[Dict[str, Any], int]]:
-        filt = ([{"terms": {"status": list(statuses)}}] if statuses else []) + list(extra)
-        body = {"query": {"bool": {"filter": filt, "must_not": list(must_not)}},
+    def _search(self, statuses, size: int = PAGE, extra=(), must_not=(), index: Optional[str] = None,
+                doc_type: Optional[str] = None, offset: int = 0) -> List[Tuple[Dict[str, Any], int]]:
+        filt = ([{"terms": {_kw("status"): list(statuses)}}] if statuses else []) + list(extra)
+        body = {"query": {"bool": {"filter": filt, "must_not": list(must_not)}}, "from": offset,
                 "size": size, "version": True, "sort": [{"modified_ts": {"order": "asc"}}]}
         resp = self.http.post(f"{self.base}/{index or self.index}/{doc_type or self.doc_type}/_search",
                               content=json.dumps(body), headers={"Content-Type": "application/json"})
@@ -122,16 +134,25 @@ class ElasticJobStore(JobStore):
         hits = resp.json().get("hits", {}).get("hits", [])
         return [(h["_source"], int(h.get("_version", 1))) for h in hits]
 
+    def _search_pages(self, statuses, want: int, max_pages: int = 10, **kw) -> List[Tuple[Dict[str, Any], int]]:
+        """Oldest-first pages until ``want`` hits or the result is exhausted."""
+        out: List[Tuple[Dict[str, Any], int]] = []
+        for p in range(max_pages):
+            page = self._search(statuses, offset=p * PAGE, **kw)
+            out += page
+            if len(page) < PAGE or len(out) >= want:
+                break
+        return out
+
     def heartbeat(self, worker, now=None):
         now = time.time() if now is None else float(now)
-        resp = self.http.put(f"{self.base}/{META_INDEX}/{BEAT_TYPE}/{worker}", params={"refresh": self.refresh},
+        resp = self.http.put(f"{self.base}/{BEAT_INDEX}/{self.doc_type}/{worker}", params={"refresh": self.refresh},
                              content=json.dumps({"worker": worker, "beat": now, "modified_ts": now}),
                              headers={"Content-Type": "application/json"})
         resp.raise_for_status()
 
     def _beats(self, since: float) -> Dict[str, float]:
-        hits = self._search((), size=10000, extra=[{"range": {"beat": {"gte": since}}}], index=META_INDEX,
-                            doc_type=BEAT_TYPE)
+        hits = self._search((), size=10000, extra=[{"range": {"beat": {"gte": since}}}], index=BEAT_INDEX)
         return {d["worker"]: float(d["beat"]) for d, _ in hits if "worker" in d}
 
     def claim(self, worker, now=None, max_stuck_s=90.0, limit=64, only=None, steal_from=None):
@@ -142,11 +163,17 @@ class ElasticJobStore(JobStore):
         now = time.time() if now is None else now
         cutoff = now - max_stuck_s
         beats = self._beats(cutoff)
-        cand = self._search(r.OPEN_STATUSES)  # not_before is checked below (docs of other writers lack it)
-        cand += self._search(r.INPROGRESS_STATUSES, extra=[{"range": {"modified_ts": {"lt": cutoff}}}],
-                             must_not=[{"terms": {"claimed_by": sorted(beats)}}] if beats else [])
+        # not_before is checked below (docs of other writers lack it)
+        cand = self._search_pages(r.OPEN_STATUSES, 4 * PAGE)
+        # stale leases: live workers' leases are filtered out in the query (they are renewed by
+        # heartbeat, so their modified_ts is old) and the rest is paged, so stuck jobs are never
+        # crowded out of the oldest-first window
+        cand += self._search_pages(r.INPROGRESS_STATUSES, 4 * PAGE,
+                                   extra=[{"range": {"modified_ts": {"lt": cutoff}}}],
+                                   must_not=[{"terms": {_kw("claimed_by"): sorted(beats)}}] if beats else [])
         if steal_from:
-            cand += self._search(r.INPROGRESS_STATUSES, extra=[{"terms": {"claimed_by": sorted(steal_from)}}])
+            cand += self._search_pages(r.INPROGRESS_STATUSES, 4 * PAGE,
+                                       extra=[{"terms": {_kw("claimed_by"): sorted(steal_from)}}])
         seen, out = set(), []
         for d, ver in sorted(cand, key=lambda dv: dv[0].get("modified_ts", 0.0)):
             if len(out) >= limit:

@@ -7,11 +7,21 @@ optimistic concurrency → 409 on mismatch), ``PUT .../<id>/_create`` (409 if
 present), ``POST /<index>/<type>/_search`` with ``match_all`` or a
 ``bool.filter`` / ``bool.must_not`` of ``terms`` / ``term`` / ``range`` queries, ``size``, ``version`` and a single-key
 ``sort``.  Documents are versioned per id exactly like ES internal versions.
+
+Two ES 6.x rules the real cluster enforces are modelled, so tests catch code that
+only works against a lenient fake:
+
+* one mapping type per index: a write under a second type is rejected with 400
+  (``illegal_argument_exception``, "Rejecting mapping update ... more than 1 type");
+* dynamic mapping of strings: a string field is analysed ``text`` (lower-cased,
+  split on anything but letters, digits and ``_``) with an exact ``<field>.keyword``
+  sub-field, so ``term`` / ``terms`` on the bare field match single tokens only.
 """
 
 from __future__ import annotations
 
 import json
+import re
 import threading
 from typing import Any, Dict, List, Tuple
 from urllib.parse import parse_qs
@@ -20,6 +30,7 @@ from urllib.parse import parse_qs
 class FakeElasticsearch:
     def __init__(self) -> None:
         self.docs: Dict[Tuple[str, str], Tuple[Dict[str, Any], int]] = {}
+        self.types: Dict[str, str] = {}  # index -> its one mapping type
         self.lock = threading.Lock()
         self.requests: List[str] = []
         self.fail_next = 0  # fault injection: return 503 for the next N requests
@@ -58,7 +69,7 @@ class FakeElasticsearch:
         if len(parts) == 3 and parts[2] == "_search" and method in ("GET", "POST"):
             return self._search(parts[0], body or {})
         if len(parts) == 4 and parts[3] == "_create" and method in ("PUT", "POST"):
-            return self._put(parts[0], parts[2], body, create=True, version=None)
+            return self._put(parts[0], parts[2], body, create=True, version=None, typ=parts[1])
         if len(parts) == 3:
             idx, _typ, did = parts
             if method == "GET":
@@ -70,11 +81,15 @@ class FakeElasticsearch:
                              "_source": cur[0]}
             if method in ("PUT", "POST"):
                 ver = int(qs["version"]) if "version" in qs else None
-                return self._put(idx, did, body, create=False, version=ver)
+                return self._put(idx, did, body, create=False, version=ver, typ=_typ)
         return 400, {"error": f"unsupported {method} {path}"}
 
-    def _put(self, idx: str, did: str, doc: Any, create: bool, version):
+    def _put(self, idx: str, did: str, doc: Any, create: bool, version, typ: str):
         with self.lock:
+            if self.types.setdefault(idx, typ) != typ:
+                return 400, {"error": {"type": "illegal_argument_exception",
+                                       "reason": f"Rejecting mapping update to [{idx}] as the final mapping "
+                                                 f"would have more than 1 type: [{self.types[idx]}, {typ}]"}}
             cur = self.docs.get((idx, did))
             if create and cur is not None:
                 return 409, {"error": {"type": "version_conflict_engine_exception"}}
@@ -96,10 +111,10 @@ class FakeElasticsearch:
         def hit(doc, f) -> bool:
             if "terms" in f:
                 (key, vals), = f["terms"].items()
-                return doc.get(key) in set(vals)
+                return any(_matches(doc, key, v) for v in vals)
             if "term" in f:
                 (key, val), = f["term"].items()
-                return doc.get(key) == val
+                return _matches(doc, key, val)
             if "range" in f:
                 (key, ops), = f["range"].items()
                 v = doc.get(key, 0)
@@ -110,7 +125,8 @@ class FakeElasticsearch:
         for s in body.get("sort", []):
             (key, spec), = s.items()
             items.sort(key=lambda x: x[1].get(key, 0), reverse=spec.get("order") == "desc")
-        items = items[: int(body.get("size", 10))]
+        start = int(body.get("from", 0))
+        items = items[start:start + int(body.get("size", 10))]
         hits = []
         for did, d, v in items:
             h = {"_index": idx, "_id": did, "_source": json.loads(json.dumps(d))}
@@ -118,3 +134,18 @@ class FakeElasticsearch:
                 h["_version"] = v
             hits.append(h)
         return 200, {"hits": {"total": len(hits), "hits": hits}}
+
+
+_TOKEN = re.compile(r"[0-9A-Za-z_]+")
+
+
+def _matches(doc: Dict[str, Any], key: str, want: Any) -> bool:
+    """ES term-level match under dynamic mapping: ``x.keyword`` is exact; a bare string
+    field holds analysed tokens (a term query is not analysed, so it must equal one)."""
+    if key.endswith(".keyword"):
+        v = doc.get(key[: -len(".keyword")])
+        return isinstance(v, str) and v == want
+    v = doc.get(key)
+    if isinstance(v, str):
+        return isinstance(want, str) and want in {t.lower() for t in _TOKEN.findall(v)}
+    return v == want

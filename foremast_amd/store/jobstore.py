@@ -289,9 +289,14 @@ class SqliteJobStore(JobStore):
             c.execute("CREATE TABLE IF NOT EXISTS documents ("
                       "id TEXT PRIMARY KEY, status TEXT, modified_ts REAL, doc TEXT)")
             cols = {row[1] for row in c.execute("PRAGMA table_info(documents)")}
+            added = False
             for col, decl in (("claimed_by", "TEXT DEFAULT ''"), ("not_before", "REAL DEFAULT 0")):
                 if col not in cols:  # stores written by an older version
                     c.execute(f"ALTER TABLE documents ADD COLUMN {col} {decl}")
+                    added = True
+            if added:  # the new columns index what the JSON documents already say
+                c.execute("UPDATE documents SET claimed_by=COALESCE(json_extract(doc,'$.claimed_by'),''), "
+                          "not_before=COALESCE(json_extract(doc,'$.not_before'),0)")
             c.execute("CREATE INDEX IF NOT EXISTS documents_status ON documents(status, modified_ts)")
             c.execute("CREATE TABLE IF NOT EXISTS meta (key TEXT PRIMARY KEY, value TEXT)")
             c.execute("CREATE TABLE IF NOT EXISTS workers (worker TEXT PRIMARY KEY, beat REAL)")

@@ -81,9 +81,11 @@ class BrainConfig:
     # (FOREMAST_WINDOW_CORRECTION = sidak | none); sigma is scaled to the forecast
     # horizon (FOREMAST_HORIZON_VARIANCE = 1 | 0)
     pairwise_min_points: int = 3
-    # mean-shift rule (ML_PAIRWISE_SHIFT, 0 = off): when the rank tests say the pods
-    # differ, a window whose mean deviation from the forecast is beyond this many sigmas
-    # is anomalous even if few of its points leave the window-corrected band
+    # mean-shift rule (ML_PAIRWISE_SHIFT, 0 = off; ON by default): when the rank tests say
+    # the pods differ, a canary window whose mean lies beyond this many sigmas of the
+    # BASELINE pods' mean (not of the forecast) is anomalous even if few of its points
+    # leave the window-corrected band.  A departure from the reference brain's per-point
+    # band semantics (docs/SCORING.md); set ML_PAIRWISE_SHIFT=0 for the per-point rule only
     pairwise_shift: float = 1.5
     pairwise_shift_min_points: int = 20  # ML_PAIRWISE_SHIFT_MIN_POINTS (as MIN_MANN_WHITE_DATA_POINTS)
     window_correction: str = "sidak"

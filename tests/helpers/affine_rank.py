@@ -62,6 +62,16 @@ def main():
     env.update(MIN_HISTORICAL_DATA_POINT_TO_MEASURE="10", threshold0="4")
     cfg = BrainConfig.from_env(env)
     store = SqliteJobStore(db)
+    if os.environ.get("AFFINE_FAIL_BEAT") == str(rank):  # a transient store error on this rank
+        beat, calls = store.heartbeat, []
+
+        def flaky(worker, now=None):
+            if worker.endswith("-rollout"):
+                calls.append(now)
+                if len(calls) in (3, 4):
+                    raise OSError("injected heartbeat failure")
+            return beat(worker, now)
+        store.heartbeat = flaky
     roll = RolloutMonitor(store, cfg, prom=client, device=torch.device("cpu"), window=10, pods=5, clock=clock,
                           ring_len=2880, worker_id=f"rank{rank}-rollout", min_capacity=4)
     roll.router = ClusterRouter(affinity_from_env(), torch.device("cpu"), timeout_s=30)

@@ -61,7 +61,11 @@ def request(app):
 
 
 @pytest.mark.slow
-def test_multi_cluster_canary_crosses_ranks(tmp_path):
+@pytest.mark.parametrize("fail_beat", [None, "1"])
+def test_multi_cluster_canary_crosses_ranks(tmp_path, fail_beat):
+    """``fail_beat``: rank 1's store heartbeat raises on two ticks; the lockstep exchange
+    must still run on that rank (else the peers' collectives desynchronise) and the
+    verdicts must not change."""
     import torch.distributed as dist
     from foremast_amd.service import app as svc
     from foremast_amd.store.jobstore import SqliteJobStore
@@ -71,6 +75,8 @@ def test_multi_cluster_canary_crosses_ranks(tmp_path):
     kv = dist.TCPStore("127.0.0.1", 0, is_master=True, wait_for_workers=False, timeout=datetime.timedelta(seconds=60))
     env = dict(os.environ, OMP_NUM_THREADS="1", CUDA_VISIBLE_DEVICES="",
                FOREMAST_CLUSTER_AFFINITY=f"{ENDPOINTS['prom-a']}=0,{ENDPOINTS['prom-b']}=1")
+    if fail_beat is not None:
+        env["AFFINE_FAIL_BEAT"] = fail_beat
     outs = [tmp_path / f"rank{i}.jsonl" for i in range(2)]
     procs = [subprocess.Popen([sys.executable, HELPER, str(kv.port), str(i), db, str(outs[i])], env=env, cwd=ROOT,
                               stderr=subprocess.PIPE, text=True) for i in range(2)]
@@ -82,6 +88,7 @@ def test_multi_cluster_canary_crosses_ranks(tmp_path):
     # the baseline (3 pods x 11 points) came from the other rank's cluster
     assert first[1]["base_valid"] == {"cart": 33, "shop": 33} and first[0]["base_valid"] == {"inv": 33}
     assert all(ls[-1]["values_moved"] > 0 for ls in lines)
+    assert lines[0][-1]["exchanges"] == lines[1][-1]["exchanges"] > 0  # the ranks stayed in lockstep
     assert first[0]["scrapes"]["prom-b"] == 0 and first[1]["scrapes"]["prom-a"] == 0  # cluster-affine scraping
     st = {a: store.get(j) for a, j in ids.items()}
     assert st["shop"]["status"] == r.ST_COMPLETED_UNHEALTH, st["shop"]

@@ -67,3 +67,49 @@ def test_memory_claim_does_not_scan_live_leases():
     st.create(_req(99999), now=1500.0)
     got = st.claim("w", now=1500.0, only=lambda d: calls.append(d["id"]) or True)
     assert len(got) == 1 and len(calls) == 1
+
+
+@pytest.mark.parametrize("kind", ["memory", "sqlite", "es"])
+def test_hyphenated_worker_ids(kind, tmp_path):
+    """Worker ids like ``node-m0-rollout``: ES dynamic mapping analyses them into tokens,
+    so lease filters must match the exact keyword (the fake analyses strings as ES does)."""
+    st = _store(kind, tmp_path)
+    ids = [st.create(_req(i), now=1000.0) for i in range(4)]
+    a = st.claim("node-m0-rollout", now=1000.0, limit=2)
+    st.claim("node-m1-rollout", now=1000.0, limit=2)
+    st.heartbeat("node-m0-rollout", now=1100.0)
+    # m1 is dead (no heartbeat): its leases are stale at +120 s, m0's are live
+    got = st.claim("node-m2-rollout", now=1120.0, max_stuck_s=90.0)
+    assert sorted(d["id"] for d in got) == sorted(set(ids) - {d["id"] for d in a})
+    # steal_from moves the live holder's leases at once
+    st.heartbeat("node-m2-rollout", now=1121.0)
+    moved = st.claim("node-m3-rollout", now=1122.0, steal_from={"node-m0-rollout"})
+    assert sorted(d["id"] for d in moved) == sorted(d["id"] for d in a)
+
+
+def test_es_stale_leases_not_crowded_out():
+    """More than a search page of live (heartbeat-renewed, so old modified_ts) leases
+    must not hide a dead worker's stuck job."""
+    st = ElasticJobStore("http://es:9200", transport=httpx.WSGITransport(app=FakeElasticsearch()))
+    for i in range(1100):
+        st.create(_req(i), now=1000.0)
+    st.claim("node-live", now=1000.0, limit=10_000)
+    dead = st.create(_req(5000), now=1001.0)
+    assert [d["id"] for d in st.claim("node-dead", now=1001.0)] == [dead]
+    st.heartbeat("node-live", now=1150.0)
+    got = st.claim("node-new", now=1150.0, max_stuck_s=90.0)
+    assert [d["id"] for d in got] == [dead]
+
+
+def test_fake_es_one_mapping_type_per_index():
+    es = FakeElasticsearch()
+    assert es.handle("PUT", "/idx/document/a", {}, {"x": 1})[0] == 201
+    status, body = es.handle("PUT", "/idx/worker/b", {}, {"x": 2})
+    assert status == 400 and "more than 1 type" in body["error"]["reason"]
+    # the store keeps heartbeats, engine records and jobs each under one type per index
+    st = ElasticJobStore("http://es:9200", transport=httpx.WSGITransport(app=es))
+    st.create(_req(1), now=1000.0)
+    st.heartbeat("node-m0", now=1000.0)
+    st.put_meta("cluster_health", {"ok": 1})
+    assert st.get_meta("cluster_health") == {"ok": 1}
+    assert len(st.claim("node-m0", now=1000.0)) == 1
