@@ -136,6 +136,10 @@ def parse():
                         "lstm = config 3; multivariate = config 5 (fp8 LSTM, latency + error-rate); node = the product "
                         "path: canary jobs registered through the service and scored by the production node brain "
                         "from Prometheus JSON (foremast_amd/benchmarks/node.py)")
+    p.add_argument("--arrival-per-tick", type=int, default=0,
+                   help="node config: steady arrivals -- this many canary rollouts start every minute and finish at "
+                        "endTime (--window minutes later); ~J x window jobs live at steady state "
+                        "(foremast_amd/benchmarks/node.py setup_arrival)")
     p.add_argument("--multi-cluster", action="store_true",
                    help="config 4 layout: each rank scrapes the baseline cluster of its neighbour's shard; "
                         "baseline windows reach their owner through one RCCL all-to-all per tick")
@@ -158,9 +162,9 @@ def parse():
                    help="run the training step and scoring back to back instead of on two HIP streams")
     a = p.parse_args()
     if a.steps is None:
-        a.steps = 8 if a.config == "node" else 20
+        a.steps = (60 if a.arrival_per_tick else 8) if a.config == "node" else 20
     if a.warmup is None:
-        a.warmup = 1 if a.config == "node" else 5
+        a.warmup = (a.window + 1 if a.arrival_per_tick else 1) if a.config == "node" else 5
     if a.zero_copy or a.prefetch:
         a.graph = False  # these modes stage the tick's I/O from the host: eager launches
     return a
@@ -782,6 +786,9 @@ def main():
         tick, health_host, meta, dtype_name, n_series = setup_single(args, world, rank, dev)
     elif args.config == "canary":
         tick, health_host, meta, dtype_name, n_series = setup_canary(args, world, rank, dev)
+    elif args.config == "node" and args.arrival_per_tick > 0:
+        from foremast_amd.benchmarks.node import setup_arrival
+        tick, health_host, meta, dtype_name, n_series = setup_arrival(args, world, rank, dev)
     elif args.config == "node":
         from foremast_amd.benchmarks.node import setup_node
         tick, health_host, meta, dtype_name, n_series = setup_node(args, world, rank, dev)
@@ -796,6 +803,7 @@ def main():
     truth = meta.pop("_truth", None)
     scored_rows = meta.pop("_scored_rows", None)   # node: rows actually scored per tick
     node_finish = meta.pop("_finish", None)
+    arrival_finish = meta.pop("_arrival_finish", None)
     node_roll = meta.pop("_roll", None)
     node_breakdowns = meta.pop("_breakdowns", None)
     graph_used = meta.pop("_graph_used", None)
@@ -869,7 +877,10 @@ def main():
             dist.all_reduce(rows_t)
         timed_rows = float(rows_t.item())
         tick_breakdown = {k: round(v, 3) for k, v in node_roll.timings.items()}
-        fin_s, statuses = node_finish()
+        if arrival_finish is not None:
+            fin_s, statuses, arrival_det = arrival_finish()
+        else:
+            fin_s, statuses = node_finish()
     coll_ms = agg.flush_timings() if agg is not None else []
     if table is not None:
         health_host = table(health_host)
@@ -908,7 +919,31 @@ def main():
         }
         if decoder is not None:
             res["decode_ms_last_tick"] = round(decoder.last_decode_ms, 3)
-        if timed_rows is not None:
+        if timed_rows is not None and arrival_finish is not None:
+            bds = (node_breakdowns or [])[-args.steps:]
+
+            def pct(key, q):
+                xs = [b[key] for b in bds if key in b]
+                return round(float(np.percentile(xs, q)), 3) if xs else None
+            adm = [b for b in bds if b.get("admitted")]
+            res["p50_detect_latency_ms"] = pct("detect_ms", 50)
+            res["p99_detect_latency_ms"] = pct("detect_ms", 99)
+            res["node"] = {
+                "series_scored_timed": int(timed_rows),
+                "detect_ms_p50_p99_max": [pct("detect_ms", 50), pct("detect_ms", 99), pct("detect_ms", 100)],
+                "tick_total_ms_p50_p99_max": [pct("tick_total_ms", 50), pct("tick_total_ms", 99),
+                                              pct("tick_total_ms", 100)],
+                "intake_ms_p50_p99_max": [pct("intake_ms", 50), pct("intake_ms", 99), pct("intake_ms", 100)],
+                "admitted_per_tick_mean": round(float(np.mean([b.get("admitted", 0) for b in bds])), 1) if bds else 0,
+                "admission_ms_p50": {k: (round(float(np.percentile([b.get(k, 0.0) for b in adm], 50)), 3)
+                                         if adm else None)
+                                     for k in ("claim_ms", "plan_ms", "admit_ms", "admit_rows_ms", "admit_fit_ms",
+                                               "admit_windows_ms")},
+                "live_rows_mean": round(float(np.mean([b.get("live_rows", 0) for b in bds])), 1) if bds else 0,
+                "tick_breakdown_ms": bds,
+                "completion_ticks_s": round(fin_s, 3), "job_statuses_rank0": statuses}
+            res["detection"] = arrival_det
+        elif timed_rows is not None:
             res["node"] = {"series_scored_timed": int(timed_rows), "tick_breakdown_ms_last": tick_breakdown,
                            "tick_breakdown_ms": (node_breakdowns or [])[-args.steps:],
                            "tick_ms": [round(float(x), 2) for x in lat_ms.tolist()],

@@ -319,3 +319,290 @@ def setup_node(args, world, rank, dev):
         "_truth": (truth_apps, n_apps),
     }
     return tick, health, meta, "bf16" if dev.type == "cuda" else "fp32", na * M
+
+
+# --------------------------------------------------------------------------- steady arrivals
+class ArrivalServer:
+    """Prometheus stand-in of the steady-arrival bench: per tick one pre-rendered
+    body per family (every app's newest point; every live new pod's newest point),
+    and baseline windows rendered on request for the pods a query names (native
+    encoder, so the stand-in's own time stays small next to the brain's)."""
+
+    def __init__(self) -> None:
+        self.tick_bodies: Dict[Tuple[str, float], bytes] = {}
+        # (family, window start) -> (pod -> row, label objects, values [pods, W + 1])
+        self.windows: Dict[Tuple[str, float], Tuple[Dict[str, int], List[str], np.ndarray]] = {}
+        self.requests = 0
+        self.bytes_served = 0
+        self.serve_s = 0.0
+
+    async def fetch_raw_many(self, urls) -> List[object]:
+        t0 = time.perf_counter()
+        out = [self._one(u) for u in urls]
+        self.serve_s += time.perf_counter() - t0
+        return out
+
+    def _one(self, url: str):
+        from ..ingest import native
+        self.requests += 1
+        q = parse_qs(urlsplit(url).query)
+        query, start, end = unquote(q["query"][0]), float(q["start"][0]), float(q["end"][0])
+        if "{" not in query:
+            body = self.tick_bodies.get((query, end), _body([]))
+        else:
+            name = query.split("{", 1)[0]
+            win = self.windows.get((name, start))
+            pods = query.split('pod=~"', 1)[1].rsplit('"', 1)[0].split("|") if 'pod=~"' in query else []
+            if win is None:
+                body = _body([])
+            else:
+                idx, labels, vals = win
+                rows = [idx[p] for p in pods if p in idx]
+                body = native.render_matrix(native.label_blob([labels[i] for i in rows]), vals[rows], start, STEP)
+        self.bytes_served += len(body)
+        return body
+
+
+def setup_arrival(args, world, rank, dev):
+    """``--config node --arrival-per-tick J``: the product path under a steady
+    deployment stream.  Every tick J canary rollouts start (one job per app, 5
+    metrics, P new + P old pods: the barrelman request of ``Barrelman.go:783-899``
+    with the 10-minute watch of ``:52``), each finishes at its endTime; at steady
+    state the node holds ~J x W jobs (2,000 x 10 = 20,000 jobs = 100k live rows by
+    default).  Arrivals are registered by the service's create handler at setup
+    (the service's work, not the brain's) and enter the job store at their start
+    minute.  Each timed tick is NodeBrain.tick: scoring of the running jobs, the
+    node health exchange (detect latency ends here), then the claim and admission
+    of that minute's arrivals (decode, rows, slots, Holt-Winters fit of 5 J
+    histories, baseline windows).  The node is warm: the 7-day history of every
+    (app, metric) is resident (``brain/resident.py``)."""
+    from ..api import crd
+    from ..api import rest as r
+    from ..brain.engine import synthetic_eval, synthetic_params
+    from ..brain.node import NodeBrain, owner_of
+    from ..brain.rollout import RolloutMonitor
+    from ..brain.streaming import StreamingMonitor
+    from ..controller import queries
+    from ..ingest import native
+    from ..service import app as svc
+    from ..store import MemoryJobStore
+    from ..utils.config import BrainConfig, reference_default_env
+    from ..utils.timeutil import format_rfc3339
+
+    M, P, W = len(METRICS), args.pods, args.window
+    R, season = args.ring, args.season
+    J = int(args.arrival_per_tick)
+    if dev.type == "cpu":
+        J, R = min(J, 40), min(R, 2880)
+    ticks = args.warmup + args.steps + 1
+    A_all = J * (W + 1)                       # app pool: an app redeploys once its last job ended
+    mine = [a for a in range(A_all) if owner_of(f"ns{a % 200}", f"app{a}", world) == rank]
+    local = {a: i for i, a in enumerate(mine)}
+    na = len(mine)
+    t_setup = time.perf_counter()
+    clock = {"t": T0}
+    server = ArrivalServer()
+    env = reference_default_env()
+    env.update(ML_ALGORITHM=args.algorithm, ML_PAIRWISE_ALGORITHM=args.pairwise,
+               MIN_HISTORICAL_DATA_POINT_TO_MEASURE="0", threshold="4", bound="3")
+    for i in range(5):
+        env[f"threshold{i}"], env[f"bound{i}"] = "4", "3"
+    cfg = BrainConfig.from_env(env)
+    cfg.ring_len, cfg.season = R, season
+    store = MemoryJobStore()
+    ns = [f"ns{a % 200}" for a in mine]
+    app = [f"app{a}" for a in mine]
+    gid = torch.tensor([a * M + j for a in mine for j in range(M)], dtype=torch.int64)
+    params = {k: v[gid] for k, v in synthetic_params(A_all * M, torch.device("cpu"), seed=1234).items()}
+    noise = 0.03 * params["lvl"][:, 0].numpy()
+    rng = np.random.default_rng(99 + rank)
+
+    # --- resident history (warm node) ---------------------------------------------------------
+    roll = RolloutMonitor(store, cfg, prom=server, device=dev, worker_id=f"node-m{rank}-rollout", step=STEP,
+                          window=W, pods=P, clock=lambda: clock["t"], ring_len=R, min_capacity=max(64, J * W * M),
+                          decode_threads=args.decode_threads, apps_per_query=256)
+    keys = [(ENDPOINT, "namespace_app_per_pod:" + m, ns[i], app[i]) for i in range(na) for m in METRICS]
+    hist = roll.history
+    hist.clock = lambda: clock["t"]
+    hist.want(keys, T0)
+    asyncio.run(hist.assign_only(T0))
+    dparams = {k: v.to(dev) for k, v in params.items()}
+    for c0 in range(0, len(keys), 16384):
+        c1 = min(len(keys), c0 + 16384)
+        hist.load_rows(keys[c0:c1], synthetic_eval({k: v[c0:c1] for k, v in dparams.items()}, 0, R, season,
+                                                   noise_seed=4321 + c0))
+    hist.unwant(keys, T0)
+
+    # --- the deployment schedule: tick k deploys apps (k J .. k J + J) mod A (revision k // (W + 1))
+    deploys: List[List[int]] = []    # per tick: local app indices deploying
+    for k in range(ticks):
+        deploys.append([local[a % A_all] for a in range(k * J, k * J + J) if a % A_all in local])
+    rev = lambda k: k // (W + 1) + 1                                              # noqa: E731
+    new_pods = lambda i, k: [f"{app[i]}-v{rev(k) + 1}-{p}-7d9f8b6c5d" for p in range(P)]  # noqa: E731
+    old_pods = lambda i, k: [f"{app[i]}-v{rev(k)}-{p}-5b6c7d8e9f" for p in range(P)]      # noqa: E731
+    n_bad = int(round(args.anomaly_frac * M * sum(len(d) for d in deploys)))
+    bad_set = set(rng.choice(sum(len(d) for d in deploys) * M, size=n_bad, replace=False).tolist()) if n_bad else set()
+    model = synthetic_eval(params, R - 1 - W, W + 1 + ticks + W + 1, season, None).numpy()  # [na*M, T] no noise
+    col = lambda t: int(round((t - T0) / STEP)) + W                                # noqa: E731
+
+    # --- jobs: the barrelman request of each rollout, through the service (staged) ------------
+    mets = crd.Metrics(data_source_type="prometheus", endpoint=ENDPOINT,
+                       monitoring=[crd.Monitoring(metric_name=m, metric_alias=f"m{j}") for j, m in enumerate(METRICS)])
+    staging = MemoryJobStore()
+    arrivals: List[List[Dict]] = []
+    truth: Dict[str, bool] = {}
+    job_bad: List[List[np.ndarray]] = []   # per tick, per deploying app: [M] injected flags
+    t_reg = time.perf_counter()
+    seq = 0
+    for k in range(ticks):
+        tk = T0 + STEP * k
+        docs, flags = [], []
+        for i in deploys[k]:
+            info = queries.create_metrics_info(ns[i], app[i], [new_pods(i, k), old_pods(i, k)], mets, W, "canary",
+                                               now=tk)
+            req = r.ApplicationHealthAnalyzeRequest(app_name=app[i], start_time=format_rfc3339(tk),
+                                                    end_time=format_rfc3339(tk + W * STEP), metrics=info,
+                                                    strategy="canary").to_dict()
+            code, resp = svc.register(staging, req)
+            assert code == 200, resp
+            f = np.array([(seq * M + j) in bad_set for j in range(M)])
+            seq += 1
+            flags.append(f)
+            d = staging._docs[resp["jobId"]]
+            truth[d["id"]] = bool(f.any())
+            docs.append(d)
+        arrivals.append(docs)
+        job_bad.append(flags)
+    register_s = time.perf_counter() - t_reg
+
+    # --- Prometheus bodies (native encoder) ---------------------------------------------------
+    app_lab = {m: native.label_blob([f'"__name__":"namespace_app_per_pod:{m}","namespace":"{ns[i]}","app":"{app[i]}"'
+                                     for i in range(na)]) for m in METRICS}
+    for k in range(ticks + W + 1):
+        tk = T0 + STEP * k
+        c = col(tk)
+        live = [(kk, i, n) for kk in range(max(0, k - W), min(k + 1, ticks)) for n, i in enumerate(deploys[kk])]
+        for j, m in enumerate(METRICS):
+            rows = np.arange(na) * M + j
+            vals = (model[rows, c] + rng.standard_normal(na) * noise[rows]).astype(np.float32)
+            server.tick_bodies[("namespace_app_per_pod:" + m, tk)] = native.render_matrix(app_lab[m], vals[:, None],
+                                                                                          tk, STEP)
+            if live:
+                li = np.array([i for _, i, _ in live])
+                lv = model[li * M + j, c][:, None] + rng.standard_normal((len(live), P)) * noise[li * M + j][:, None]
+                badf = np.array([job_bad[kk][n][j] for kk, _, n in live])
+                lv = np.where(badf[:, None], lv * 3.0, lv).astype(np.float32).reshape(-1)
+                labels = [f'"__name__":"namespace_pod:{m}","namespace":"{ns[i]}","pod":"{pod}"'
+                          for kk, i, _ in live for pod in new_pods(i, kk)]
+                server.tick_bodies[("namespace_pod:" + m, tk)] = native.render_matrix(
+                    native.label_blob(labels), lv[:, None], tk, STEP)
+        if k < ticks and deploys[k]:  # baseline windows [tk - W, tk] of this tick's old pods
+            bt0 = tk - W * STEP
+            for j, m in enumerate(METRICS):
+                pods = [(i, pod) for i in deploys[k] for pod in old_pods(i, k)]
+                rows = np.array([i * M + j for i, _ in pods])
+                base = model[rows, c - W:c + 1] + rng.standard_normal((len(pods), W + 1)) * noise[rows][:, None]
+                server.windows[("namespace_pod:" + m, bt0)] = (
+                    {pod: n for n, (_, pod) in enumerate(pods)},
+                    [f'"__name__":"namespace_pod:{m}","namespace":"{ns[i]}","pod":"{pod}"' for i, pod in pods],
+                    base.astype(np.float32))
+    del model
+    setup_s = time.perf_counter() - t_setup
+
+    stream = StreamingMonitor(store, cfg, prom=server, device=dev, worker_id=f"node-m{rank}", ring_len=R,
+                              window=W, clock=lambda: clock["t"])
+    node = NodeBrain(stream, None, store, dev, publish=False, extra=(roll,))
+    node.owns = lambda d: True  # the rank-local store holds exactly this rank's share
+    for mon in node.monitors:
+        mon.owns = None
+    loop = asyncio.new_event_loop()
+    flagged: set = set()
+    scored: List[int] = []
+    breakdowns: List[Dict[str, float]] = []
+    gc_pause = {"t": 0.0, "t0": 0.0, "n": 0}
+
+    def _gc_cb(phase, info):
+        if phase == "start":
+            gc_pause["t0"] = time.perf_counter()
+        else:
+            gc_pause["t"] += time.perf_counter() - gc_pause["t0"]
+            gc_pause["n"] += 1
+
+    def arrive(k):
+        """This minute's rollout requests reach the job store (the service wrote them)."""
+        for d in arrivals[k]:
+            store._docs[d["id"]] = d
+            store._index(d)
+
+    def tick(k):
+        clock["t"] = T0 + STEP * k
+        arrive(k)
+        n_rows = roll.n_live
+        gc_pause["t"], gc_pause["n"] = 0.0, 0
+        gc.callbacks.append(_gc_cb)
+        t0 = time.perf_counter()
+        try:
+            table = loop.run_until_complete(node.tick())
+        finally:
+            gc.callbacks.remove(_gc_cb)
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        scored.append(n_rows)
+        bd = {kk: round(v, 3) for kk, v in roll.timings.items()}
+        bd.update({kk: round(v, 3) for kk, v in node.timings.items()})
+        bd["tick_total_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
+        bd["live_rows"] = roll.n_live
+        bd["gc_ms"], bd["gc_runs"] = round(gc_pause["t"] * 1e3, 2), gc_pause["n"]
+        breakdowns.append(bd)
+        for a in table["anomalous_apps"]:
+            flagged.add(a)
+        return table
+
+    def finish():
+        """Completion ticks (every job past endTime), then detection over every job."""
+        t0 = time.perf_counter()
+        for k in range(ticks, ticks + W + 1):
+            clock["t"] = T0 + STEP * k
+            loop.run_until_complete(node.tick())
+        fin = time.perf_counter() - t0
+        st: Dict[str, int] = {}
+        tp = fp = fn = 0
+        for jid, bad in truth.items():
+            d = store._docs.get(jid)
+            s = d["status"] if d is not None else "never-arrived"
+            st[s] = st.get(s, 0) + 1
+            hit = s == r.ST_COMPLETED_UNHEALTH
+            tp += bad and hit
+            fp += (not bad) and hit
+            fn += bad and not hit
+        return fin, st, {"jobs": len(truth), "injected_jobs": sum(truth.values()), "tp": tp, "fp": fp, "fn": fn,
+                         "recall": round(tp / max(1, tp + fn), 4), "false_positive_rate":
+                         round(fp / max(1, len(truth) - sum(truth.values())), 6)}
+
+    health = torch.zeros((1, 2), dtype=torch.int32)
+    meta = {
+        "model": f"{args.algorithm} + pairwise {args.pairwise} canary jobs on the production node brain, steady "
+                 f"arrivals ({J} rollouts per minute, {W}-minute watch)",
+        "global_batch": J * W * M * world,
+        "seq_len": R,
+        "season": season,
+        "arrivals_per_tick": J,
+        "watch_window_min": W,
+        "metrics_per_job": M,
+        "pods_new_old": [P, P],
+        "app_pool": A_all,
+        "path": "per tick: score running jobs (history advance + pod windows as query_range JSON -> native decode "
+                "-> H2D -> scatter -> rank tests -> cached-state band/verdict -> D2H -> fail-fast / endTime writes) "
+                "-> node health exchange [detect latency] -> claim + native job decode + admission (rows, slots, "
+                "HW fit of the new rows, baseline windows) of this minute's arrivals",
+        "warm_node": "resident 7-day history of every (app, metric) in HBM",
+        "setup_s": round(setup_s, 2),
+        "register_s": round(register_s, 3),
+        "register_jobs_per_s": round(sum(len(a) for a in arrivals) / max(register_s, 1e-9), 1),
+        "_scored_rows": scored,
+        "_breakdowns": breakdowns,
+        "_arrival_finish": finish,
+        "_roll": roll,
+        "_server": server,
+    }
+    return tick, health, meta, "bf16" if dev.type == "cuda" else "fp32", J * W * M

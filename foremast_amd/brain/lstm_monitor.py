@@ -239,7 +239,7 @@ class LstmMonitor:
             self.row_job[row] = e.doc["id"]
             rows.append(row)
             for f, (_, k) in enumerate(e.feats):
-                fr[i, f] = hist.rows[k]
+                fr[i, f] = hist.row_of(k)
             ns, app = e.feats[0][1][2], e.feats[0][1][3]
             self.shard.app_id[row] = self._app_index((ns, app))
         idx = torch.tensor(rows, dtype=torch.long, device=self.device)

@@ -87,6 +87,7 @@ class NodeBrain:
         self._published = -1e18
         self._last_anomalous = None
         self.gc_freeze_min = int(os.environ.get("FOREMAST_GC_FREEZE_MIN", "256"))
+        self.timings: Dict[str, float] = {}
         self._frozen_at = 0
         for m in self.monitors:
             m.owns = self._owns_for(m)
@@ -165,13 +166,23 @@ class NodeBrain:
             self._frozen_at = n  # jobs finished: the next intake of the same size freezes again
 
     async def tick(self) -> Dict:
+        """One node tick: every monitor scores its running jobs, the ranks exchange
+        the node health table — the verdicts are out (``timings["detect_ms"]``) —
+        then the monitors that split their tick (:meth:`RolloutMonitor.intake`)
+        claim and admit new jobs (``timings["intake_ms"]``): a deploy burst never
+        delays the verdicts of the jobs already running."""
+        t0 = time.perf_counter()
+        split = []
         for m in self.monitors:
-            m.sync(steal_from=self.dead or None)
             try:
-                await m.tick()
+                if hasattr(m, "intake"):
+                    split.append(m)
+                    await m.score_tick()
+                else:
+                    m.sync(steal_from=self.dead or None)
+                    await m.tick()
             except Exception as e:  # noqa: BLE001 - a scoring failure must not desynchronise the collectives
                 log.exception("%s tick failed: %s", type(m).__name__, e)
-        self._freeze_admitted()
         if self.world is None:
             table = self._exchange()
         else:
@@ -179,6 +190,15 @@ class NodeBrain:
             table = self.world.run_tick(self._exchange)
             if self.world.generation != gen:
                 self._after_reform(before)
+        t1 = time.perf_counter()
+        for m in split:
+            try:
+                m.sync(steal_from=self.dead or None)
+            except Exception as e:  # noqa: BLE001 - the store may be briefly unavailable
+                log.exception("%s claim failed: %s", type(m).__name__, e)
+            await m.intake()  # every rank, every tick: it may run the lockstep window exchange
+        self._freeze_admitted()
+        self.timings = {"detect_ms": (t1 - t0) * 1e3, "intake_ms": (time.perf_counter() - t1) * 1e3}
         table["generation"] = self.world.generation if self.world else 0
         table["backend"] = dist.get_backend() if dist.is_available() and dist.is_initialized() else "none"
         table["collectives"] = comm.active()

@@ -99,7 +99,18 @@ async def fetch_decode(prom, reqs: Sequence[Tuple[str, float, int, int]], tables
     return ok
 
 
+def history_key_hash(k: Key) -> int:
+    """64-bit key of a history series: series_key of "endpoint\x1fmetric" and
+    "namespace\x1fapp" (the key ``ingest/csrc/job_plan.cpp`` emits per series)."""
+    return native.key_hash(k[0] + "\x1f" + k[1], k[2] + "\x1f" + k[3])
+
+
 class ResidentHistory:
+    """Rows are indexed by the 64-bit history key (:func:`history_key_hash`), so a
+    batch of admitted jobs finds its rows with integer dict lookups; the key tuple
+    of a row is kept for its queries.  The tuple API (:meth:`want`, :meth:`ready`,
+    :meth:`row_of`) hashes once per distinct key."""
+
     def __init__(self, prom, device, ring_len: int = 10080, step: float = 60.0, clock=time.time,
                  chunk_points: int = 1440, apps_per_query: int = 256, decode_threads: int = 8,
                  min_capacity: int = 64, retain_s: float = 86400.0, dtype: Optional[torch.dtype] = None) -> None:
@@ -114,40 +125,73 @@ class ResidentHistory:
         self.dtype = dtype or (torch.bfloat16 if self.device.type == "cuda" else torch.float32)
         self.ring: Optional[HistoryRing] = None
         self.t_last = 0.0
-        self.rows: Dict[Key, int] = {}
-        self.keys: List[Optional[Key]] = []
-        self.refs: Dict[Key, int] = {}
-        self.last_used: Dict[Key, float] = {}
-        self.pending: Set[Key] = set()
-        self._idle: "collections.deque[Tuple[float, Key]]" = collections.deque()  # (last use, key) of unreferenced rows
+        self.rows: Dict[int, int] = {}                 # history key -> row
+        self.keys: List[Optional[Key]] = []            # row -> key tuple (None: free)
+        self.refs: Dict[int, int] = {}
+        self.last_used: Dict[int, float] = {}
+        self.pending: Set[int] = set()
+        self._tuples: Dict[int, Key] = {}              # key tuples of wanted keys without a row yet
+        self._hash: Dict[Key, int] = {}                # tuple -> key (tuple API)
+        self._idle: "collections.deque[Tuple[float, int]]" = collections.deque()  # (last use, key) of unreferenced rows
         self._stage: Dict[Tuple[int, int], List[torch.Tensor]] = {}
         self._stage_i = 0
         self._tables: Optional[Dict[Tuple[str, str], native.KeyTable]] = None
+        self._fam_ids: Dict[Tuple[str, str], int] = {}
+        self._row_fam = np.zeros(0, dtype=np.int64)   # row -> family id (-1: free)
+        self._row_app = np.zeros(0, dtype=np.uint64)  # row -> (namespace, app) decode key
+        self._free_rows: List[int] = []
         self.history_queries = 0
         self.tick_queries = 0
         self.failed_queries = 0
         self.reloads = 0
 
     # ------------------------------------------------------------------ references
+    def key_hash(self, k: Key) -> int:
+        h = self._hash.get(k)
+        if h is None:
+            if len(self._hash) > 1 << 20:
+                self._hash.clear()
+            h = self._hash[k] = history_key_hash(k)
+        return h
+
     def want(self, keys: Iterable[Key], now: float) -> None:
-        for k in keys:
-            self.refs[k] = self.refs.get(k, 0) + 1
-            self.last_used[k] = now
-            if k not in self.rows:
-                self.pending.add(k)
+        keys = list(keys)
+        self.want_h([self.key_hash(k) for k in keys], now, keys.__getitem__)
+
+    def want_h(self, hashes: Sequence[int], now: float, key_of) -> None:
+        """Reference history keys; ``key_of(i)`` gives the tuple of ``hashes[i]``
+        (asked only for keys without a row)."""
+        refs, last, rows = self.refs, self.last_used, self.rows
+        for i, h in enumerate(hashes):
+            refs[h] = refs.get(h, 0) + 1
+            last[h] = now
+            if h not in rows:
+                self.pending.add(h)
+                if h not in self._tuples:
+                    self._tuples[h] = key_of(i)
 
     def unwant(self, keys: Iterable[Key], now: float) -> None:
-        for k in keys:
-            n = self.refs.get(k, 0) - 1
+        self.unwant_h([self.key_hash(k) for k in keys], now)
+
+    def unwant_h(self, hashes: Iterable[int], now: float) -> None:
+        refs, last = self.refs, self.last_used
+        for h in hashes:
+            n = refs.get(h, 0) - 1
             if n > 0:
-                self.refs[k] = n
+                refs[h] = n
             else:
-                self.refs.pop(k, None)
-                self._idle.append((now, k))  # expiry candidate (checked in time order)
-            self.last_used[k] = now
+                refs.pop(h, None)
+                self._idle.append((now, h))  # expiry candidate (checked in time order)
+            last[h] = now
 
     def ready(self, key: Key) -> bool:
-        return key in self.rows and key not in self.pending
+        return self.ready_h(self.key_hash(key))
+
+    def ready_h(self, h: int) -> bool:
+        return h in self.rows and h not in self.pending
+
+    def row_of(self, key: Key) -> int:
+        return self.rows[self.key_hash(key)]
 
     @property
     def n_rows(self) -> int:
@@ -161,7 +205,11 @@ class ResidentHistory:
             n = self.ring.n
             new._store[:n].copy_(self.ring._store)
             new.state.head = self.ring.head
-        self.keys.extend([None] * (capacity - len(self.keys)))
+        old = len(self.keys)
+        self.keys.extend([None] * (capacity - old))
+        self._row_fam = np.concatenate([self._row_fam, np.full(capacity - old, -1, dtype=np.int64)])
+        self._row_app = np.concatenate([self._row_app, np.zeros(capacity - old, dtype=np.uint64)])
+        self._free_rows += list(range(capacity - 1, old - 1, -1))
         self.ring = new
 
     def _assign(self, now: float) -> List[Tuple[Key, int]]:
@@ -169,20 +217,23 @@ class ResidentHistory:
         pairs whose history must be (re)loaded."""
         expired = []
         while self._idle and now - self._idle[0][0] > self.retain_s:
-            t, k = self._idle.popleft()
+            t, h = self._idle.popleft()
             # still unreferenced and not used again since it went idle
-            if k in self.rows and k not in self.refs and self.last_used.get(k, 0.0) <= t:
-                expired.append(k)
-        freed = [self.rows.pop(k) for k in expired]
-        for k in expired:
-            self.last_used.pop(k, None)
-            self.pending.discard(k)
+            if h in self.rows and h not in self.refs and self.last_used.get(h, 0.0) <= t:
+                expired.append(h)
+        freed = [self.rows.pop(h) for h in expired]
+        for h in expired:
+            self.last_used.pop(h, None)
+            self.pending.discard(h)
         for row in freed:
             self.keys[row] = None
+            self._free_rows.append(row)
+        if freed:
+            self._row_fam[freed] = -1
         if not self.pending and not expired:
             return []
-        self.pending = {k for k in self.pending if k in self.refs or k in self.rows}
-        new = sorted(k for k in self.pending if k not in self.rows)
+        self.pending = {h for h in self.pending if h in self.refs or h in self.rows}
+        new = sorted((h for h in self.pending if h not in self.rows), key=lambda h: self._tuples[h])
         need = len(self.rows) + len(new)
         if self.ring is None or need > self.ring.n:
             cap = max(self.min_capacity, self.ring.n if self.ring is not None else 1)
@@ -192,22 +243,31 @@ class ResidentHistory:
         if freed:
             idx = torch.tensor(freed, dtype=torch.long, device=self.device)
             self.ring._store.index_fill_(0, idx, float("nan"))
-        free = iter(i for i, k in enumerate(self.keys) if k is None)
-        for key in new:
-            row = next(free)
-            self.keys[row] = key
-            self.rows[key] = row
+        if new:
+            self._free_rows.sort(reverse=True)  # lowest rows first (pop from the end)
+            keys = [self._tuples.pop(h) for h in new]
+            rows = [self._free_rows.pop() for _ in new]
+            for h, k, row in zip(new, keys, rows):
+                self.keys[row] = k
+                self.rows[h] = row
+            fam = [self._fam_ids.setdefault((k[0], k[1]), len(self._fam_ids)) for k in keys]
+            self._row_fam[rows] = fam
+            self._row_app[rows] = native.key_hashes([k[2] for k in keys], [k[3] for k in keys])
+        for h in [h for h in self._tuples if h not in self.refs]:
+            self._tuples.pop(h)  # wanted and released before they got a row
         if expired or new:
             self._tables = None
-        return sorted(((k, self.rows[k]) for k in self.pending), key=lambda kr: kr[1])
+        return sorted(((self.keys[self.rows[h]], self.rows[h]) for h in self.pending), key=lambda kr: kr[1])
 
     def _key_tables(self) -> Dict[Tuple[str, str], native.KeyTable]:
         """Per metric family (endpoint, metric): (namespace, app) -> row."""
         if self._tables is None:
-            fams: Dict[Tuple[str, str], List] = {}
-            for k, row in self.rows.items():
-                fams.setdefault((k[0], k[1]), []).append(((k[2], k[3]), row))
-            self._tables = {fam: native.KeyTable(v) for fam, v in fams.items()}
+            tabs = {}
+            for fam, fid in self._fam_ids.items():
+                rows = np.nonzero(self._row_fam == fid)[0]
+                if len(rows):
+                    tabs[fam] = native.KeyTable.indexed(self._row_app[rows], rows.astype(np.int64), "namespace", "app")
+            self._tables = tabs
         return self._tables
 
     def _staging(self, rows: int, cols: int, reuse: bool = False) -> Tuple[torch.Tensor, np.ndarray]:
@@ -232,8 +292,9 @@ class ResidentHistory:
         return t, t.numpy()
 
     # ------------------------------------------------------------------ sync
-    async def sync(self, now: Optional[float] = None) -> None:
-        """Advance the ring to ``now``, free expired rows, load pending keys."""
+    async def sync(self, now: Optional[float] = None, load: bool = True) -> None:
+        """Advance the ring to ``now``; with ``load``, free expired rows and load
+        pending keys too (:meth:`load_pending`)."""
         now = self.clock() if now is None else now
         t_new = float(np.floor(now / self.step) * self.step)
         if self.t_last == 0.0:
@@ -242,6 +303,14 @@ class ResidentHistory:
             await self._advance(t_new)
         else:
             self.t_last = max(self.t_last, t_new)
+        if load:
+            await self.load_pending(now)
+
+    async def load_pending(self, now: Optional[float] = None) -> None:
+        """Free expired rows, give pending keys rows and load their week."""
+        now = self.clock() if now is None else now
+        if self.t_last == 0.0:
+            self.t_last = float(np.floor(now / self.step) * self.step)
         todo = self._assign(now)
         if todo:
             await self._load(todo)
@@ -315,7 +384,8 @@ class ResidentHistory:
         self.failed_queries += ok.count(False)
         rows = torch.tensor([row for _, row in todo], dtype=torch.long)
         self._write_rows(rows, block_t)
-        self.pending = {k for k in self.pending if k in failed}
+        failed_rows = {row for k, row in todo if k in failed}
+        self.pending = {h for h in self.pending if self.rows.get(h) in failed_rows}
 
     def _write_rows(self, rows: torch.Tensor, values: torch.Tensor) -> None:
         """``values [k, R]`` oldest first into the rotated ring (two column slices)."""
@@ -333,9 +403,10 @@ class ResidentHistory:
         """Adopt known histories (``values [k, R]`` oldest first, ending at
         ``t_last``) for keys that already have rows — e.g. a warm node restored
         from a snapshot, or a benchmark's synthetic week — without a fetch."""
-        rows = torch.tensor([self.rows[k] for k in keys], dtype=torch.long)
+        hs = [self.key_hash(k) for k in keys]
+        rows = torch.tensor([self.rows[h] for h in hs], dtype=torch.long)
         self._write_rows(rows, values)
-        self.pending -= set(keys)
+        self.pending -= set(hs)
 
     async def assign_only(self, now: Optional[float] = None) -> None:
         """Give pending keys rows without loading them (then :meth:`load_rows`)."""

@@ -8,7 +8,8 @@ model, run the pairwise test, lower the threshold if baseline and current
 differ, detect.  :class:`RolloutMonitor` serves the same jobs from resident
 state instead:
 
-* admission (once per job, batched over every job claimed in a tick): the
+* admission (once per job, batched over every job claimed in a tick): job
+  documents are decoded in one native batch (:mod:`.plans`) into columns; the
   history comes from the node's resident ring (:mod:`.resident`; fetched only
   for series the node has never held), the model is fitted ONCE on the
   history ending at the job's start — the reference job's historical window is
@@ -16,21 +17,32 @@ state instead:
   model — and reduced to a forecast state per (job, metric) row: level,
   trend, the 16 forecast offsets of the current window's horizons, sigma,
   fitted grid point (h-step variance) and valid points.  The baseline pods'
-  window ``[start - W, start]`` is fetched once, batched by pod family;
+  window ``[start - W, start]`` is fetched once, batched by pod family.  Rows,
+  thresholds, pod slots and window maps are set with array operations over the
+  admitted batch (no per-row Python objects);
 * every tick: ONE range query per pod metric family for the newest minute of
-  every pod of every running job → native keyed decode (``(namespace, pod)`` →
-  row x pod) → one H2D → scatter kernel into each row's window at its own
-  job-minute column → rank tests (MW-U / Wilcoxon / Kruskal, pods pooled) of
-  baseline vs current → band / verdict / per-app counters / compacted anomaly
-  list from the cached state (one launch, ``hw_detect_params_kernel``) → D2H;
+  every pod of every running job → native keyed decode through ONE live pod
+  index (``(namespace, pod)`` → slot; the tick block is ``[slot, family x
+  minute]``, a family's body lands at its column offset) → one H2D → scatter
+  kernel into each row's window at its own job-minute column → rank tests
+  (MW-U / Wilcoxon / Kruskal, pods pooled) of baseline vs current → band /
+  verdict / per-app counters / compacted anomaly list from the cached state
+  (one launch, ``hw_detect_params_kernel``) → D2H;
 * verdicts follow the reference state machine: an anomalous metric finishes
   the job ``completed_unhealth`` with its points and pod tags (fail fast);
   past ``endTime`` it finishes ``completed_health`` (current data seen) or
   ``completed_unknown``; in between the job stays leased — the engine renews
   all of its leases with one store heartbeat per tick instead of a write per
   job — and nothing is written;
-* rows are freed when their job finishes; band gauges are read from the last
-  tick's host arrays at scrape time.
+* a tick is split in two (:meth:`score_tick`, then :meth:`intake`): verdicts
+  of the running jobs first, then the claim and admission of new jobs — a new
+  job's first current point is one step after its start (``metricsquery.go:52``),
+  so admitting it after this tick's scoring delays nothing, and a deploy burst
+  never delays the verdicts of the jobs already running;
+* every per-tick host step is O(changed jobs): slots, the decode index, the
+  window map and the app roster are updated in place for the admitted and
+  finished jobs; band gauges are read from the last tick's host arrays at
+  scrape time.
 
 Jobs the resident engine cannot key (non-Prometheus sources, per-caller /
 per-uri families, selectors that are not plain pod lists, multi-metric
@@ -43,13 +55,8 @@ from __future__ import annotations
 import heapq
 import json
 import logging
-import math
-import re
 import time
-from collections import OrderedDict
-from dataclasses import dataclass, field
-from typing import Callable, Dict, List, Optional, Set, Tuple
-from urllib.parse import unquote
+from typing import Callable, Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -61,202 +68,22 @@ from ..models import detect as det_ref
 from ..models import moving_average as ma_ref
 from ..models import pairwise as pw_ref
 from ..models import smoothing as sm_ref
-from ..promql.selector import SelectorError, parse_selector
-from ..service import urls
 from ..store.jobstore import JobStore
 from ..utils.config import BrainConfig
 from ..utils.metrics import BrainMetrics
-from ..utils.timeutil import TimeFormatError, parse_rfc3339
+from . import plans as pl
+from .plans import ALGORITHMS, STRATEGIES, PlanCols, RolloutPlan, RolloutSeries  # noqa: F401 (re-exported)
 from .resident import Key, ResidentHistory, fetch_decode, range_url, re_alt
 
 log = logging.getLogger("foremast.rollout")
 
-STRATEGIES = ("canary", "rollingupdate")
-ALGORITHMS = ("holt_winters", "exponential_smoothing", "double_exponential_smoothing", "moving_average",
-              "moving_average_all", "seasonal_decompose")
 HB = 16  # forecast offsets kept per row (kernels.HALF_HB): horizons 1..16 of the current window
-_SPLIT = ("namespace_pod_caller:", "namespace_app_caller:", "namespace_app_caller_per_pod:",
-          "namespace_pod_uri:", "namespace_app_uri:", "namespace_app_uri_per_pod:")
-_REGEX_META = re.compile(r"[*+?()\[\]{}^$\\]")
-
-
-@dataclass
-class RolloutSeries:
-    """One (job, metric alias): a row of the rollout table."""
-    alias: str
-    hkey: Key                       # 7-day history series (endpoint, metric, namespace, app)
-    fam: Tuple[str, str]            # (endpoint, pod metric) of the current window
-    namespace: str
-    cur_pods: Tuple[str, ...]
-    base_pods: Tuple[str, ...]
-    cur_start: float
-    cur_n: int
-    base_start: float
-    base_n: int
-    hist_end: float
-    base_fam: Tuple[str, str] = ("", "")  # (endpoint, pod metric) of the baseline window (may be another cluster)
-
-
-@dataclass
-class RolloutPlan:
-    doc_id: str
-    app: Tuple[str, str]
-    end_ts: float
-    series: List[RolloutSeries]
-    doc: Dict = field(default_factory=dict)
-    rows: List[int] = field(default_factory=list)
-
-
-def _pods_of(sel) -> Optional[Tuple[str, Tuple[str, ...]]]:
-    """(namespace, pods) of ``<m>{namespace="ns", pod="a"}`` / ``pod=~"a|b"``."""
-    ns, pods = None, None
-    for label, op, val in sel.matchers:
-        if label == "namespace" and op == "=":
-            ns = val
-        elif label == "pod" and op == "=":
-            pods = (val,)
-        elif label == "pod" and op == "=~":
-            if _REGEX_META.search(val):
-                return None
-            pods = tuple(p for p in val.split("|") if p)
-        else:
-            return None
-    if ns is None or not pods:
-        return None
-    return ns, tuple(sorted(set(pods)))
-
-
-_SIMPLE_SEL = re.compile(r'^([a-zA-Z_:][a-zA-Z0-9_:]*)\{((?:[a-zA-Z_][a-zA-Z0-9_]*(?:=~|=)"[^"\\]*",?)*)\}$')
-
-
-class _Sel:
-    __slots__ = ("name", "matchers")
-
-    def __init__(self, name, matchers):
-        self.name, self.matchers = name, matchers
-
-
-def _selector(q: str):
-    """The plain selectors barrelman writes (``name{l="v",l=~"a|b"}``, no
-    escapes) split without the general PromQL matcher regex; anything else
-    goes through :func:`parse_selector`."""
-    m = _SIMPLE_SEL.match(q)
-    if m is None:
-        return parse_selector(q)
-    out = []
-    for part in m.group(2).split('",'):
-        if not part:
-            continue
-        label, _, rest = part.partition("=")
-        op = "=~" if rest.startswith("~") else "="
-        out.append((label, op, rest[2 if op == "=~" else 1:].rstrip('"')))
-    return _Sel(m.group(1), tuple(out))
-
-
-def _grid(url: str) -> Tuple[str, object, float, float, float]:
-    """(endpoint, selector, start, end, step) of a flattened Prometheus
-    ``query_range`` URL (``prometheushelper.go:12-27`` shape: four parameters,
-    only the query percent-encoded); other shapes take the general parser."""
-    ep, sep, qs = url.partition("query_range?")
-    fields = dict(kv.partition("=")[::2] for kv in qs.split("&")) if sep else {}
-    if set(fields) != {"query", "start", "end", "step"}:
-        p = urls.parse_prometheus_url(url)
-        return ep, parse_selector(str(p["query"])), float(p["start"]), float(p["end"]), float(p["step"])
-    return (ep, _selector(_unquote(fields["query"])), float(fields["start"]), float(fields["end"]),
-            float(fields["step"]))
-
-
-_ESC = (("%3A", ":"), ("%7B", "{"), ("%7D", "}"), ("%3D", "="), ("%22", '"'), ("%2C", ","), ("%7C", "|"),
-        ("%7E", "~"), ("%2F", "/"))
-
-
-def _unquote(q: str) -> str:
-    """Percent-decoding of a selector: the escapes a PromQL selector of k8s
-    names produces are replaced directly (C string ops); any other escape
-    takes ``urllib.parse.unquote``."""
-    if "%" not in q:
-        return q
-    for a, b in _ESC:
-        q = q.replace(a, b)
-    return unquote(q) if "%" in q else q
-
-
-_PLANS: "OrderedDict[Tuple[str, str], Optional[RolloutPlan]]" = OrderedDict()
 
 
 def plan_rollout(doc: Dict, cfg: BrainConfig, step: float = 60.0, window_cols: int = 11) -> Optional[RolloutPlan]:
     """The rollout-table plan of a job, or None when the resident engine cannot
-    key it.  Memoised per job id (content-addressed: the request, hence the
-    plan, never changes), because the claim filters of several engines ask
-    for the same documents."""
-    if cfg.algorithm not in ALGORITHMS:
-        return None
-    ck = (doc.get("id", ""), step, window_cols)
-    if ck in _PLANS:
-        _PLANS.move_to_end(ck)
-        return _PLANS[ck]
-    plan = _plan(doc, step, window_cols)
-    _PLANS[ck] = plan
-    if len(_PLANS) > 65536:
-        _PLANS.popitem(last=False)
-    return plan
-
-
-def _plan(doc, step, window_cols) -> Optional[RolloutPlan]:
-    if (doc.get("strategy") or "").lower() not in STRATEGIES:
-        return None
-    try:
-        cur = urls.parse_config(doc.get("currentConfig", ""))
-        base = urls.parse_config(doc.get("baselineConfig", ""))
-        hist = urls.parse_config(doc.get("historicalConfig", ""))
-        stores = [v for k in ("currentMetricStore", "baselineMetricStore", "historicalMetricStore")
-                  for v in urls.parse_config(doc.get(k, "")).values()]
-    except urls.ConfigError:
-        return None
-    if not cur or any(s and s != r.DATASOURCE_PROMETHEUS for s in stores):
-        return None
-    try:
-        end_ts = parse_rfc3339(doc.get("endTime", "")).timestamp()
-    except TimeFormatError:
-        return None
-    out, app = [], None
-    for alias in sorted(cur):
-        if alias not in hist:
-            return None
-        try:
-            ep_h, sel_h, _hs, h_end, h_step = _grid(hist[alias])
-            ep_c, sel_c, c_start, c_end, c_step = _grid(cur[alias])
-        except (urls.ConfigError, SelectorError, KeyError, ValueError):
-            return None
-        lab = {k: v for k, op, v in sel_h.matchers if op == "="}
-        if (len(sel_h.matchers) != 2 or set(lab) != {"namespace", "app"} or not sel_h.name or not sel_c.name
-                or sel_h.name.startswith(_SPLIT) or sel_c.name.startswith(_SPLIT)
-                or h_step != step or c_step != step or ep_c != ep_h):
-            return None
-        pc = _pods_of(sel_c)
-        if pc is None or pc[0] != lab["namespace"]:
-            return None
-        b_pods, b_start, b_n = (), 0.0, 0
-        if alias in base:
-            try:
-                ep_b, sel_b, b_start, b_end, b_step = _grid(base[alias])
-            except (urls.ConfigError, SelectorError, KeyError, ValueError):
-                return None
-            pb = _pods_of(sel_b)
-            # the baseline may live in another cluster (its own Prometheus): multi-cluster canary
-            if pb is None or sel_b.name != sel_c.name or b_step != step or pb[0] != pc[0]:
-                return None
-            b_pods, b_n = pb[1], min(window_cols, int(round((b_end - b_start) / step)) + 1)
-            if b_n > 0 and int(round((b_end - b_start) / step)) + 1 > window_cols:
-                b_start = b_end - (window_cols - 1) * step  # the newest window_cols points
-        app = app or (lab["namespace"], lab["app"])
-        out.append(RolloutSeries(
-            alias=alias, hkey=(ep_h, sel_h.name, lab["namespace"], lab["app"]), fam=(ep_c, sel_c.name),
-            namespace=pc[0], cur_pods=pc[1], base_pods=b_pods, cur_start=c_start,
-            cur_n=max(0, min(window_cols, int(round((c_end - c_start) / step)) + 1)),
-            base_start=b_start, base_n=b_n, hist_end=h_end,
-            base_fam=(ep_b, sel_b.name) if alias in base else ("", "")))
-    return RolloutPlan(doc_id=doc["id"], app=app, end_ts=end_ts, series=out, doc=doc)
+    key it (memoised per job id, see :func:`plans.plan_many`)."""
+    return pl.plan_rollout(doc, cfg.algorithm, step, window_cols)
 
 
 def is_rollout_keyable(doc: Dict, cfg: BrainConfig) -> bool:
@@ -264,25 +91,35 @@ def is_rollout_keyable(doc: Dict, cfg: BrainConfig) -> bool:
 
 
 class PodSlots:
-    """``(namespace, pod)`` -> slot: the row of a pod in each metric family's part
-    of the per-tick decode block.  Slots are reference counted by the jobs
-    watching the pod (two jobs on one pod share it); key hashes are computed
-    once per pod, so the per-family native key indexes are rebuilt from arrays
-    when the pod set changes, without touching Python strings."""
+    """``(namespace, pod)`` key -> slot: a pod's row in the per-tick decode block
+    (``[slot, family x minute]``: one slot serves every metric family).  Slots are
+    reference counted by the jobs watching the pod (two jobs on one pod share it).
+    Keys are the 64-bit pod keys of the job decoder, and the native decode index
+    is updated in place when pods come and go (a released pod's key is retired, so
+    a pod that keeps reporting after its job can never land in a reused slot)."""
 
     def __init__(self, cap: int = 1024) -> None:
-        self.index: Dict[Tuple[str, str], int] = {}
+        self.index: Dict[int, int] = {}
         self.cap = int(cap)
         self.refs = np.zeros(self.cap, dtype=np.int32)
         self.hash = np.zeros(self.cap, dtype=np.uint64)
         self.free: List[int] = list(range(self.cap - 1, -1, -1))
-        self.version = 0   # bumps when the pod set changes
-        self.added = 0     # bumps when a pod gets a slot (key indexes rebuild)
-        self.grown = 0     # bumps when cap grows (every src row moves)
+        self.grown = 0     # bumps when cap grows
+        self.live = native.LiveKeyIndex("namespace", "pod") if native.available() else None
 
-    def acquire(self, keys: List[Tuple[str, str]]) -> np.ndarray:
-        new = list(dict.fromkeys(k for k in keys if k not in self.index))
-        if new:
+    def __len__(self) -> int:
+        return len(self.index)
+
+    def acquire(self, hashes: np.ndarray) -> np.ndarray:
+        """One reference per occurrence of each key; returns the slot of each."""
+        if not len(hashes):
+            return np.zeros(0, dtype=np.int64)
+        u, inv, cnt = np.unique(np.asarray(hashes, dtype=np.uint64), return_inverse=True, return_counts=True)
+        ul = u.tolist()
+        idx = self.index
+        slots = np.fromiter((idx.get(h, -1) for h in ul), dtype=np.int64, count=len(ul))
+        new = np.nonzero(slots < 0)[0]
+        if len(new):
             while len(self.free) < len(new):
                 old = self.cap
                 self.cap *= 2
@@ -290,31 +127,39 @@ class PodSlots:
                 self.hash = np.concatenate([self.hash, np.zeros(old, dtype=np.uint64)])
                 self.free = list(range(self.cap - 1, old - 1, -1)) + self.free
                 self.grown += 1
-            hs = native.key_hashes([k[0] for k in new], [k[1] for k in new])
-            for k, h in zip(new, hs):
-                slot = self.free.pop()
-                self.index[k] = slot
-                self.hash[slot] = h
-            self.version += 1
-            self.added += 1
-        slots = np.fromiter((self.index[k] for k in keys), dtype=np.int64, count=len(keys))
-        np.add.at(self.refs, slots, 1)
-        return slots
+            got = [self.free.pop() for _ in range(len(new))]
+            slots[new] = got
+            for k, s in zip(new.tolist(), got):
+                idx[ul[k]] = s
+            self.hash[got] = u[new]
+            if self.live is not None:
+                self.live.set(u[new], np.asarray(got, dtype=np.int64))
+        np.add.at(self.refs, slots, cnt.astype(np.int32))
+        return slots[inv]
 
-    def release(self, keys: List[Tuple[str, str]]) -> None:
-        for k in keys:
-            slot = self.index.get(k)
-            if slot is None:
-                continue
-            self.refs[slot] -= 1
-            if self.refs[slot] <= 0:
-                self.refs[slot] = 0
-                del self.index[k]
-                self.free.append(slot)
-                self.version += 1
+    def release(self, hashes: np.ndarray) -> None:
+        if not len(hashes):
+            return
+        u, cnt = np.unique(np.asarray(hashes, dtype=np.uint64), return_counts=True)
+        idx = self.index
+        ul = u.tolist()
+        slots = np.fromiter((idx.get(h, -1) for h in ul), dtype=np.int64, count=len(ul))
+        ok = slots >= 0
+        slots, cnt, u = slots[ok], cnt[ok], u[ok]
+        self.refs[slots] -= cnt.astype(np.int32)
+        gone = np.nonzero(self.refs[slots] <= 0)[0]
+        if len(gone):
+            gs = slots[gone]
+            self.refs[gs] = 0
+            for h in u[gone].tolist():
+                del idx[h]
+            self.free.extend(gs.tolist())
+            if self.live is not None:
+                self.live.retire(u[gone])
 
-    def live(self) -> np.ndarray:
-        return np.fromiter(self.index.values(), dtype=np.int64, count=len(self.index))
+    def table(self, fams: int):
+        """The decode index (native): key -> slot."""
+        return self.live
 
 
 class RolloutMonitor:
@@ -356,18 +201,22 @@ class RolloutMonitor:
         self.tick_queries = 0
         self.admitted = 0
         self.cap = 0
+        self._free: List[int] = []                     # free rows (stack)
         self.slots = PodSlots()
         self.fams: Dict[Tuple[str, str], int] = {}     # pod metric family -> index in the decode block
-        self._tables = None                            # (slots.version, cap, fam tables)
-        self._srcmap_dirty = True
+        self._fam_of_key: Dict[int, int] = {}          # family key (job decoder) -> index
         self._blocks: Dict[Tuple[int, int], List[torch.Tensor]] = {}
         self._block_i = 0
+        self._srcmap_t: Optional[torch.Tensor] = None
+        self._srcmap_geom = None                       # (slots cap, families, rows cap) it was built for
+        self._srcmap_dirty: List[np.ndarray] = []      # rows changed since the device map was synced
         # cluster-affine ingest (parallel/affine.py): windows of another rank's clusters are
         # requested at admission and delivered by that rank in the tick's lockstep exchange
         self.router = None
         self._remote: List[Tuple[str, Tuple[str, str], float, int, List]] = []
         self.timings: Dict[str, float] = {}
         self._bands: Tuple[np.ndarray, np.ndarray, np.ndarray] = (np.zeros(0), np.zeros(0), np.zeros(0))
+        self._done_bands: Dict[int, Tuple[PlanCols, int, float, float, Optional[float]]] = {}
         self._last_anom: Dict[int, float] = {}
         self._apps_dirty = False
         self._app_refs: Dict[Tuple[str, str], int] = {}
@@ -375,6 +224,7 @@ class RolloutMonitor:
         self._app_free: List[int] = []
         self._app_new: List[Tuple[Tuple[str, str], List[int]]] = []
         self._app_gone: List[Tuple[str, str]] = []
+        self._thr_cache: Dict[Tuple[str, str], Tuple[float, int, float]] = {}
         self._n_live = 0
         self._build_grid()
         self.anomalies = None
@@ -430,11 +280,19 @@ class RolloutMonitor:
         if n:  # rows keep their app index across growth
             self.app_id[:n].copy_(old_app_id)
         self.row_plan.extend([None] * (cap - len(self.row_plan)))
-        self.model_ok = np.concatenate([getattr(self, "model_ok", np.zeros(0, bool)), np.zeros(cap - n, bool)])
-        self.row_fam = np.concatenate([getattr(self, "row_fam", np.zeros(0, np.int64)), np.full(cap - n, -1)])
-        self.row_slot = np.concatenate([getattr(self, "row_slot", np.zeros((0, self.P), np.int64)),
-                                        np.full((cap - n, self.P), -1)])
-        self._srcmap_dirty = True
+        grow = cap - n
+
+        def ext(name, fill, dtype, shape=()):
+            setattr(self, name, np.concatenate([getattr(self, name, np.zeros((0,) + shape, dtype)),
+                                                np.full((grow,) + shape, fill, dtype=dtype)]))
+        ext("model_ok", False, bool)
+        ext("row_fam", -1, np.int64)
+        ext("row_slot", -1, np.int64, (self.P,))
+        ext("row_cs", 0.0, np.float64)      # cur_start of the row (anomaly timestamps)
+        ext("row_s", -1, np.int64)          # series index in its PlanCols
+        self.row_cols: List[Optional[PlanCols]] = getattr(self, "row_cols", []) + [None] * grow
+        self._free = list(range(cap - 1, n - 1, -1)) + self._free
+        self._srcmap_geom = None
         self.cap = cap
         if self.gpu:
             from ..ops import kernels as K
@@ -447,24 +305,29 @@ class RolloutMonitor:
         self.win.index_fill_(0, idx, float("nan"))
         self.base.index_fill_(0, idx, float("nan"))
         self.app_id.index_fill_(0, idx, 0)
+        ra = np.asarray(rows, dtype=np.int64)
         for row in rows:
             self.row_plan[row] = None
-            self.model_ok[row] = False
-        self.row_fam[rows] = -1
-        self.row_slot[rows] = -1
+            self.row_cols[row] = None
+        self.model_ok[ra] = False
+        self.row_fam[ra] = -1
+        self.row_slot[ra] = -1
+        self.row_s[ra] = -1
+        self._srcmap_dirty.append(ra)
+        self._free.extend(rows)
         self._n_live -= len(rows)
-        self._srcmap_dirty = True
 
-    def _take_rows(self, n: int) -> List[int]:
-        free = [i for i, p in enumerate(self.row_plan) if p is None]
-        if len(free) < n:
-            used = self.cap - len(free)
+    def _take_rows(self, n: int) -> np.ndarray:
+        if len(self._free) < n:
+            used = self.cap - len(self._free)
             cap = max(self.min_capacity, self.cap or 1)
             while cap < used + n:
                 cap *= 2
             self._alloc(cap)
-            free = [i for i, p in enumerate(self.row_plan) if p is None]
-        return free[:n]
+        self._free.sort(reverse=True)
+        out = self._free[-n:][::-1] if n else []
+        del self._free[len(self._free) - n:]
+        return np.asarray(out, dtype=np.int64)
 
     @property
     def n_live(self) -> int:
@@ -475,23 +338,41 @@ class RolloutMonitor:
         """Cluster-affine mode: a job belongs to the rank that scrapes the cluster
         of its new pods (its history and current windows are then local)."""
         p = plan_rollout(d, self.cfg, self.step, self.Wc)
-        return p is not None and self.router.local(p.series[0].fam[0])
+        return p is not None and self.router.local(p.first_fam[0])
 
     def _claimable(self, d) -> bool:
-        return plan_rollout(d, self.cfg, self.step, self.Wc) is not None and (self.owns is None or self.owns(d))
+        return self._claimable_many([d])[0]
+
+    def _claimable_many(self, docs) -> List[bool]:
+        """Claim filter over a batch: one native decode for every unseen document."""
+        plans = pl.plan_many(docs, self.cfg.algorithm, self.step, self.Wc)
+        if self.owns is None:
+            return [p is not None for p in plans]
+        if self.router is not None and self.owns == self.owns_affine:
+            return [p is not None and self.router.local(p.first_fam[0]) for p in plans]
+        return [p is not None and self.owns(d) for p, d in zip(plans, docs)]
 
     def sync(self, steal_from=None) -> int:
         """Lease new keyable rollout jobs (that this rank owns)."""
         now = self.clock()
+        t0 = time.perf_counter()
         docs = self.store.claim(self.worker_id, now=now, max_stuck_s=self.cfg.max_stuck_seconds,
-                                limit=self.claim_limit, only=self._claimable, steal_from=steal_from)
-        for d in docs:
-            p = plan_rollout(d, self.cfg, self.step, self.Wc)
+                                limit=self.claim_limit, only_batch=self._claimable_many, steal_from=steal_from)
+        t1 = time.perf_counter()
+        plans = pl.plan_many(docs, self.cfg.algorithm, self.step, self.Wc)
+        hist = self.history
+        n = 0
+        for d, p in zip(docs, plans):
             if p is None or d["id"] in self.jobs or d["id"] in self.waiting:
                 continue
             p.doc = d
             self.waiting[d["id"]] = p
-            self.history.want([s.hkey for s in p.series], now)
+            c, s0 = p.cols, p.s0
+            hist.want_h(c.u64[s0:s0 + p.n, 0].tolist(), now, lambda i, c=c, s0=s0: c.hkey_at(s0 + i))
+            n += 1
+        self.timings["claim_ms"] = (t1 - t0) * 1e3
+        self.timings["plan_ms"] = (time.perf_counter() - t1) * 1e3
+        self.timings["claimed"] = n
         return len(docs)
 
     def release(self, pred: Callable[[Dict], bool]) -> int:
@@ -511,11 +392,11 @@ class RolloutMonitor:
         p = self.jobs.pop(jid, None) or self.waiting.pop(jid, None)
         if p is None:
             return
-        self.history.unwant([s.hkey for s in p.series], now)
+        self.history.unwant_h(p.cols.u64[p.s0:p.s0 + p.n, 0].tolist(), now)
         self._free_rows(p.rows)
         if p.rows:
             self._app_ref(p, -1)
-            self.slots.release(self._job_pods(p))
+            self.slots.release(p.pod_keys)
         p.rows = []
 
     def _refresh_apps(self) -> None:
@@ -532,6 +413,7 @@ class RolloutMonitor:
                 self._app_names[i] = None
                 self._app_free.append(i)
         self._app_gone = []
+        rows_all, ids_all = [], []
         for a, rows in self._app_new:
             i = self.apps.get(a)
             if i is None:
@@ -541,8 +423,12 @@ class RolloutMonitor:
                 else:
                     self._app_names[i] = a
                 self.apps[a] = i
-            if rows:
-                self.app_id[torch.tensor(rows, dtype=torch.long, device=self.device)] = i
+            if len(rows):
+                rows_all.append(np.asarray(rows, dtype=np.int64))
+                ids_all.append(np.full(len(rows), i, dtype=np.int32))
+        if rows_all:  # one device scatter for every admitted row
+            rr = torch.from_numpy(np.concatenate(rows_all)).to(self.device)
+            self.app_id[rr] = torch.from_numpy(np.concatenate(ids_all)).to(self.device)
         self._app_new = []
         if self.cap and self.app_stats.shape[0] < max(1, len(self._app_names)):
             cap = self.app_stats.shape[0]
@@ -556,7 +442,7 @@ class RolloutMonitor:
         n = self._app_refs.get(p.app, 0) + delta
         self._app_refs[p.app] = n
         if delta > 0:
-            self._app_new.append((p.app, list(p.rows)))
+            self._app_new.append((p.app, p.rows))
         elif n <= 0:
             self._app_refs.pop(p.app, None)
             self._app_gone.append(p.app)
@@ -564,70 +450,88 @@ class RolloutMonitor:
 
     # ------------------------------------------------------------------ admission
     async def _admit(self, now: float) -> int:
-        ready = [p for p in self.waiting.values() if all(self.history.ready(s.hkey) for s in p.series)]
+        hist = self.history
+        ready = []
+        for p in self.waiting.values():
+            ks = p.cols.u64[p.s0:p.s0 + p.n, 0].tolist()
+            if all(hist.ready_h(h) for h in ks):
+                ready.append(p)
         if not ready:
             return 0
         t0 = time.perf_counter()
-        n_rows = sum(len(p.series) for p in ready)
-        rows = self._take_rows(n_rows)
-        it = iter(rows)
-        items: List[Tuple[int, RolloutSeries]] = []
-        for p in ready:
+        b = _Batch(ready, self.P)
+        rows = self._take_rows(b.n)
+        b.rows = rows
+        off = 0
+        for p in b.plans:
             del self.waiting[p.doc_id]
-            p.rows = [next(it) for _ in p.series]
-            for k, (row, s) in enumerate(zip(p.rows, p.series)):
+            p.rows = rows[off:off + p.n].tolist()
+            for k, row in enumerate(p.rows):
                 self.row_plan[row] = (p.doc_id, k)
-                items.append((row, s))
+            off += p.n
             self.jobs[p.doc_id] = p
-            self._n_live += len(p.series)
             heapq.heappush(self._ends, (p.end_ts, p.doc_id))
-        self._set_row_params(items)
-        self._assign_slots(ready)
-        self._fit(items)
-        await self._load_windows(items)
-        self.admitted += len(ready)
-        for p in ready:
+        self._n_live += b.n
+        for cols, lo, hi in b.parts:
+            rr = rows[lo:hi]
+            for row in rr.tolist():
+                self.row_cols[row] = cols
+        self.row_s[rows] = b.s
+        self.row_cs[rows] = b.f64[:, 0]
+        t1 = time.perf_counter()
+        self._set_row_params(b)
+        self._assign_slots(b)
+        t2 = time.perf_counter()
+        self._fit(b)
+        t3 = time.perf_counter()
+        await self._load_windows(b)
+        t4 = time.perf_counter()
+        self.admitted += len(b.plans)
+        for p in b.plans:
             self._app_ref(p, +1)
-        self.timings["admit_ms"] = (time.perf_counter() - t0) * 1e3
-        return len(ready)
+        self.timings.update(admit_ms=(time.perf_counter() - t0) * 1e3, admit_rows_ms=(t2 - t0) * 1e3,
+                            admit_fit_ms=(t3 - t2) * 1e3, admit_windows_ms=(t4 - t3) * 1e3,
+                            admitted=len(b.plans), admit_bookkeeping_ms=(t1 - t0) * 1e3)
+        return len(b.plans)
 
-    def _set_row_params(self, items: List[Tuple[int, RolloutSeries]]) -> None:
+    def _set_row_params(self, b: "_Batch") -> None:
         dev = self.device
-        rows = torch.tensor([row for row, _ in items], dtype=torch.long, device=dev)
-        f = lambda xs, dt: torch.tensor(xs, dtype=dt, device=dev)  # noqa: E731
-        th = {}
-        for _, s in items:
-            if (s.alias, s.hkey[1]) not in th:
-                th[(s.alias, s.hkey[1])] = self.cfg.for_metric(s.alias, s.hkey[1])
-        ths = [th[(s.alias, s.hkey[1])] for _, s in items]
-        self.threshold[rows] = f([t.threshold for t in ths], torch.float32)
-        self.bound[rows] = f([t.bound for t in ths], torch.int8)
-        self.min_lower[rows] = f([t.min_lower_bound for t in ths], torch.float32)
-        self.start_min[rows] = f([int(round(s.cur_start / self.step)) for _, s in items], torch.int32)
+        thr = np.empty((b.n, 3), dtype=np.float64)
+        cache = self._thr_cache
+        for i, (al, met) in enumerate(b.alias_metric()):
+            t = cache.get((al, met))
+            if t is None:
+                c = self.cfg.for_metric(al, met)
+                t = cache[(al, met)] = (c.threshold, c.bound, c.min_lower_bound)
+            thr[i] = t
+        rows = torch.from_numpy(b.rows).to(dev)
+        self.threshold[rows] = torch.from_numpy(thr[:, 0].astype(np.float32)).to(dev)
+        self.bound[rows] = torch.from_numpy(thr[:, 1].astype(np.int8)).to(dev)
+        self.min_lower[rows] = torch.from_numpy(thr[:, 2].astype(np.float32)).to(dev)
+        self.start_min[rows] = torch.from_numpy(np.round(b.f64[:, 0] / self.step).astype(np.int32)).to(dev)
         self.win[rows] = float("nan")
         self.base[rows] = float("nan")
 
-    def _fit(self, items: List[Tuple[int, RolloutSeries]]) -> None:
+    def _fit(self, b: "_Batch") -> None:
         """Fit every admitted row's model on its history ending at the job's
         start (grouped by how many of the ring's newest points that drops) and
         store the forecast state + per-column horizons."""
         hist = self.history
-        groups: Dict[int, List[Tuple[int, RolloutSeries]]] = {}
-        for row, s in items:
-            drop = int(round((hist.t_last - s.hist_end) / self.step))
-            groups.setdefault(max(0, drop), []).append((row, s))
+        drop = np.maximum(0, np.round((hist.t_last - b.f64[:, 2]) / self.step).astype(np.int64))
+        hrows = np.fromiter((hist.rows[h] for h in b.u64[:, 0].tolist()), dtype=np.int64, count=b.n)
         Wc = self.Wc
-        for drop, grp in groups.items():
-            t_fit = hist.t_last - drop * self.step
-            rows = [row for row, _ in grp]
-            data, head, length = hist.gather([hist.rows[s.hkey] for _, s in grp], drop)
+        tiles = np.tile(np.arange(Wc), self.P)[None, :]
+        for dv in np.unique(drop).tolist():
+            sel = np.nonzero(drop == dv)[0]
+            t_fit = hist.t_last - dv * self.step
+            data, head, length = hist.gather(hrows[sel].tolist(), dv)
             st = self._fit_state(data, head, length)
-            idx = torch.tensor(rows, dtype=torch.long, device=self.device)
+            idx = torch.from_numpy(b.rows[sel]).to(self.device)
             for k, v in st.items():
                 self.state[k][idx] = v.to(self.state[k].dtype)
-            self.model_ok[rows] = (st["nvalid"] >= self.cfg.min_historical_points).cpu().numpy()
-            off = np.array([int(round((s.cur_start - t_fit) / self.step)) for _, s in grp], dtype=np.int64)
-            hz = off[:, None] + np.tile(np.arange(Wc), self.P)[None, :]
+            self.model_ok[b.rows[sel]] = (st["nvalid"] >= self.cfg.min_historical_points).cpu().numpy()
+            off = np.round((b.f64[sel, 0] - t_fit) / self.step).astype(np.int64)
+            hz = off[:, None] + tiles
             self.hz[idx] = torch.from_numpy(np.clip(hz, 1, 1 << 20).astype(np.int32)).to(self.device)
 
     def _algo_for(self, length: int) -> str:
@@ -703,119 +607,149 @@ class RolloutMonitor:
         return {"level": ws.mean, "trend": torch.zeros(k), "sigma": ws.std, "nvalid": ws.count.float(),
                 "season_hb": torch.zeros((k, HB)), "best": torch.full((k,), -1, dtype=torch.int32)}
 
-    @staticmethod
-    def _job_pods(p: RolloutPlan) -> List[Tuple[str, str]]:
-        """The (namespace, pod) keys a job holds slots for (current pods, once per job)."""
-        return list(dict.fromkeys((s.namespace, pod) for s in p.series for pod in s.cur_pods))
+    def _fam_index(self, fkeys: np.ndarray, cols_of, s_of) -> np.ndarray:
+        """Family index of each row (by the decoder's family key; names interned once)."""
+        out = np.empty(len(fkeys), dtype=np.int64)
+        for i, k in enumerate(fkeys.tolist()):
+            fi = self._fam_of_key.get(k)
+            if fi is None:
+                fam = cols_of(i).fam[s_of(i)]
+                fi = self.fams.get(fam)
+                if fi is None:
+                    fi = self.fams[fam] = len(self.fams)
+                self._fam_of_key[k] = fi
+            out[i] = fi
+        return out
 
-    def _fam(self, fam: Tuple[str, str]) -> int:
-        fi = self.fams.get(fam)
-        if fi is None:
-            fi = self.fams[fam] = len(self.fams)
-            self._tables = None
-        return fi
-
-    def _assign_slots(self, plans: List[RolloutPlan]) -> None:
+    def _assign_slots(self, b: "_Batch") -> None:
+        """Pod slots of the admitted rows: the first P current pods of each row; a
+        job holds one reference per distinct pod (released when it finishes)."""
         P = self.P
-        for p in plans:
-            keys = self._job_pods(p)
-            slots = dict(zip(keys, self.slots.acquire(keys).tolist()))
-            for row, s in zip(p.rows, p.series):
-                self.row_fam[row] = self._fam(s.fam)
-                pods = s.cur_pods[:P]
-                self.row_slot[row, :len(pods)] = [slots[(s.namespace, pod)] for pod in pods]
-                self.row_slot[row, len(pods):] = -1
-        self._srcmap_dirty = True
+        H, valid = b.cur_pod_keys()                           # [n, P] pod keys, mask
+        job = np.repeat(np.arange(len(b.plans)), b.lens)      # plan index of each row
+        jk = np.repeat(job, P)[valid.reshape(-1)]
+        hk = H.reshape(-1)[valid.reshape(-1)]
+        # distinct (job, pod): one reference each
+        pair = np.unique(np.stack([jk.astype(np.uint64), hk]), axis=1) if len(hk) else np.zeros((2, 0), np.uint64)
+        self.slots.acquire(pair[1])
+        starts = np.searchsorted(pair[0], np.arange(len(b.plans) + 1).astype(np.uint64))
+        for i, p in enumerate(b.plans):
+            p.pod_keys = pair[1, starts[i]:starts[i + 1]]
+        # slot of every (row, pod): the keys are all live now
+        u = np.asarray(sorted(set(hk.tolist())), dtype=np.uint64) if len(hk) else np.zeros(0, np.uint64)
+        us = np.fromiter((self.slots.index[h] for h in u.tolist()), dtype=np.int64, count=len(u))
+        pos = np.searchsorted(u, H.reshape(-1)).clip(0, max(len(u) - 1, 0))
+        sl = np.where(valid.reshape(-1), us[pos] if len(u) else -1, -1).reshape(b.n, P)
+        self.row_slot[b.rows] = sl
+        self.row_fam[b.rows] = self._fam_index(b.u64[:, 1], b.cols_of, b.s_of)
+        self._srcmap_dirty.append(b.rows)
 
     def _srcmap(self) -> torch.Tensor:
-        """Device ``[cap * P]`` src row of every (row, pod): family x slot cap + slot."""
-        if self._srcmap_dirty or getattr(self, "_srcmap_grown", -1) != self.slots.grown:
-            fam = self.row_fam[:, None]
-            m = np.where((self.row_slot >= 0) & (fam >= 0), fam * self.slots.cap + self.row_slot, -1)
-            self._srcmap_t = torch.from_numpy(m.astype(np.int32).reshape(-1)).to(self.device)
-            self._srcmap_dirty = False
-            self._srcmap_grown = self.slots.grown
+        """Device ``[cap * P]`` src row of every (row, pod) in the tick block viewed as
+        ``[slots * F, k]``: slot x F + family (-1: no pod).  Rebuilt when the slot
+        capacity, the family count or the row capacity changes; otherwise only the
+        rows admitted / freed since the last tick are written."""
+        F = max(1, len(self.fams))
+        geom = (self.slots.cap, F, self.cap)
+        fam = self.row_fam[:, None]
+
+        def rows_map(sel):
+            s = self.row_slot[sel]
+            f = fam[sel]
+            return np.where((s >= 0) & (f >= 0), s * F + f, -1).astype(np.int32)
+        if self._srcmap_t is None or self._srcmap_geom != geom:
+            self._srcmap_t = torch.from_numpy(rows_map(slice(None)).reshape(-1)).to(self.device)
+            self._srcmap_geom = geom
+            self._srcmap_dirty = []
+        elif self._srcmap_dirty:
+            rows = np.unique(np.concatenate(self._srcmap_dirty))
+            self._srcmap_dirty = []
+            vals = torch.from_numpy(rows_map(rows)).to(self.device)
+            self._srcmap_t.view(self.cap, self.P)[torch.from_numpy(rows).to(self.device)] = vals
         return self._srcmap_t
 
-    def _key_tables(self) -> Dict[Tuple[str, str], native.KeyTable]:
-        """Per pod family: native (namespace, pod) -> src row index over the live slots.
-
-        Rebuilt only when a pod gets a slot (or the slots grow), not when pods leave: a
-        released pod's key still maps to its old slot until that slot is reused, and the
-        points decoded there are never scattered (no live series reads a free slot).  So
-        the ticks on which jobs finish do not pay an index rebuild (~10 ms at 100k keys) in
-        their decode."""
-        key = (self.slots.added, self.slots.cap, len(self.fams))
-        if self._tables is None or self._tables[0] != key:
-            live = self.slots.live()
-            h = self.slots.hash[live]
-            used = {f for f in self.row_fam.tolist() if f >= 0}
-            tabs = {fam: native.KeyTable.indexed(h, fi * self.slots.cap + live, "namespace", "pod")
-                    for fam, fi in self.fams.items() if fi in used}
-            for t in tabs.values():
-                t.index  # build the native index now, not inside the first decode
-            self._tables = (key, tabs)
-        return self._tables[1]
-
-    async def _load_windows(self, items: List[Tuple[int, RolloutSeries]]) -> None:
+    async def _load_windows(self, b: "_Batch") -> None:
         """Baseline windows (fixed: ``[start - W, start]``) and any current points
         that already exist (a job claimed late), per (kind, window start): one
         query per pod family and group of jobs, every body decoded through one
         key index over the group's pods, then gathered into the rows."""
         t_last = self.history.t_last
-        # (kind, window start, points) -> [(row, series, pods, family)]
-        groups: Dict[Tuple[str, float, int], List[Tuple[int, RolloutSeries, Tuple[str, ...], Tuple[str, str]]]] = {}
-        for row, s in items:
-            if s.base_pods and s.base_n > 0:
-                groups.setdefault(("base", s.base_start, s.base_n), []).append((row, s, s.base_pods, s.base_fam))
-            if s.cur_n > 0 and s.cur_start <= t_last:
-                n = min(s.cur_n, int(round((t_last - s.cur_start) / self.step)) + 1)
-                groups.setdefault(("win", s.cur_start, n), []).append((row, s, s.cur_pods, s.fam))
         P, Wc = self.P, self.Wc
+        # (kind, window start, points) -> batch row indices
+        groups: Dict[Tuple[str, float, int], List[int]] = {}
+        base_n = b.i32[:, 1]
+        has_b = (b.i32[:, 6] > 0) & (b.i32[:, 5] > 0) & (base_n > 0)
+        for i in np.nonzero(has_b)[0].tolist():
+            groups.setdefault(("base", float(b.f64[i, 1]), int(base_n[i])), []).append(i)
+        cur_n = b.i32[:, 0]
+        late = np.nonzero((cur_n > 0) & (b.f64[:, 0] <= t_last))[0]
+        for i in late.tolist():
+            n = min(int(cur_n[i]), int(round((t_last - b.f64[i, 0]) / self.step)) + 1)
+            groups.setdefault(("win", float(b.f64[i, 0]), n), []).append(i)
+        if not groups:
+            return
+
+        def fam_of(i, dst):
+            c, s = b.cols_of(i), b.s_of(i)
+            return c.base_fam[s] if dst == "base" else c.fam[s]
+
+        def pods_of(i, dst):
+            c, s = b.cols_of(i), b.s_of(i)
+            return (c.base_pods(s) if dst == "base" else c.cur_pods(s))[:P]
+
+        def pod_keys(i, dst):
+            c, s = b.cols_of(i), b.s_of(i)
+            q0, nq = (int(c.i32[s, 4]), int(c.i32[s, 5])) if dst == "base" else (int(c.i32[s, 2]), int(c.i32[s, 3]))
+            return c.pod_u64[q0:q0 + min(nq, P)]
         if self.router is not None:  # windows of other ranks' clusters: requested, not fetched
-            for (dst, start, n), grp in list(groups.items()):
-                remote = [g for g in grp if not self.router.local(g[3][0])]
+            for key, grp in list(groups.items()):
+                dst, start, n = key
+                remote = [i for i in grp if not self.router.local(fam_of(i, dst)[0])]
                 if not remote:
                     continue
-                groups[(dst, start, n)] = [g for g in grp if self.router.local(g[3][0])]
-                for f in dict.fromkeys(g[3] for g in remote):
-                    part = [(row, s, ps) for row, s, ps, fam in remote if fam == f]
-                    pods = list(dict.fromkeys((s.namespace, pod) for _, s, ps in part for pod in ps[:P]))
+                groups[key] = [i for i in grp if self.router.local(fam_of(i, dst)[0])]
+                for f in dict.fromkeys(fam_of(i, dst) for i in remote):
+                    part = [(int(b.rows[i]), b.ns_of(i), pods_of(i, dst)) for i in remote if fam_of(i, dst) == f]
+                    pods = list(dict.fromkeys((ns, pod) for _, ns, ps in part for pod in ps))
                     self._remote.append((dst, f, start, n, part, pods))
             groups = {k: v for k, v in groups.items() if v}
         for (dst, start, n), grp in groups.items():
-            pods = list(dict.fromkeys((s.namespace, pod) for _, s, ps, _f in grp for pod in ps[:P]))
-            local = {k: i for i, k in enumerate(pods)}
-            fams = list(dict.fromkeys(f for _, _, _, f in grp))
-            fidx = {f: i for i, f in enumerate(fams)}
-            nl = len(pods)
-            hs = native.key_hashes([k[0] for k in pods], [k[1] for k in pods])
+            # every (row, pod) of the group: keys, then one index over the group's distinct pods
+            keys = [pod_keys(i, dst) for i in grp]
+            allk = np.concatenate(keys) if keys else np.zeros(0, np.uint64)
+            uk, inv = np.unique(allk, return_inverse=True)
+            nl = len(uk)
+            fams = list(dict.fromkeys(fam_of(i, dst) for i in grp))
+            fidx = {f: j for j, f in enumerate(fams)}
+            rowfam = np.array([fidx[fam_of(i, dst)] for i in grp], dtype=np.int64)
             block_t = torch.full((len(fams) * nl, Wc), float("nan"), dtype=torch.float32)
             if self.gpu:
                 block_t = block_t.pin_memory()
-            tables = {f: native.KeyTable.indexed(hs, fidx[f] * nl + np.arange(nl), "namespace", "pod") for f in fams}
+            tables = {f: native.KeyTable.indexed(uk, j * nl + np.arange(nl), "namespace", "pod")
+                      for f, j in fidx.items()}
             reqs, tabs = [], []
             for f in fams:
-                rows_f = [(s, ps) for _, s, ps, ff in grp if ff == f]
-                for g in range(0, len(rows_f), self.apps_per_query):
-                    part = rows_f[g:g + self.apps_per_query]
-                    sel = (f'{f[1]}{{namespace=~"{re_alt({s.namespace for s, _ in part})}",'
-                           f'pod=~"{re_alt({pod for _, ps in part for pod in ps[:P]})}"}}')
+                mine = [i for i in grp if fam_of(i, dst) == f]
+                for g in range(0, len(mine), self.apps_per_query):
+                    part = mine[g:g + self.apps_per_query]
+                    sel = (f'{f[1]}{{namespace=~"{re_alt({b.ns_of(i) for i in part})}",'
+                           f'pod=~"{re_alt({pod for i in part for pod in pods_of(i, dst)})}"}}')
                     reqs.append((range_url(f[0], sel, start, n, self.step), start, n, 0))
                     tabs.append(tables[f])
             ok = await fetch_decode(self.prom, reqs, tabs, block_t.numpy(), self.step, self.decode_threads)
             if not all(ok):
                 log.warning("%d of %d window queries failed (%s from %d)", ok.count(False), len(ok), dst, start)
+            # gather map: (group row, pod) -> block row
+            lens = np.array([len(k) for k in keys], dtype=np.int64)
             gidx = np.full((len(grp), P), -1, dtype=np.int64)
-            for i, (_, s, ps, f) in enumerate(grp):
-                fo = fidx[f] * nl
-                for p, pod in enumerate(ps[:P]):
-                    gidx[i, p] = fo + local[(s.namespace, pod)]
+            rr = np.repeat(np.arange(len(grp)), lens)
+            cc = np.arange(len(allk)) - np.repeat(np.cumsum(lens) - lens, lens)
+            gidx[rr, cc] = rowfam[rr] * nl + inv
             blk = block_t.to(self.device, non_blocking=True)
             gi = torch.from_numpy(gidx).to(self.device)
             vals = blk[gi.clamp(min=0)]                       # [k, P, Wc]
             vals = torch.where((gi >= 0)[:, :, None], vals, torch.full_like(vals, float("nan")))
-            rows = torch.tensor([row for row, _, _, _ in grp], dtype=torch.long, device=self.device)
+            rows = torch.from_numpy(b.rows[np.asarray(grp, dtype=np.int64)]).to(self.device)
             (self.base if dst == "base" else self.win).index_copy_(0, rows, vals.reshape(len(grp), P * Wc))
 
     async def _serve_windows(self, requests) -> List[np.ndarray]:
@@ -846,9 +780,9 @@ class RolloutMonitor:
         for (dst, f, st, n, part, pods), v in zip(mine, vals):
             local = {k: i for i, k in enumerate(pods)}
             block = np.full((len(part), P, Wc), np.nan, dtype=np.float32)
-            for i, (_row, s, ps) in enumerate(part):
+            for i, (_row, ns, ps) in enumerate(part):
                 for p, pod in enumerate(ps[:P]):
-                    block[i, p, :n] = v[local[(s.namespace, pod)]]
+                    block[i, p, :n] = v[local[(ns, pod)]]
             rows = torch.tensor([row for row, _, _ in part], dtype=torch.long, device=self.device)
             tgt = self.base if dst == "base" else self.win
             if all(0 <= row < len(self.row_plan) and self.row_plan[row] is not None for row in rows.tolist()):
@@ -877,28 +811,32 @@ class RolloutMonitor:
             return
         k = min(k, 4 * self.Wc)  # behind by more than any window: only the recent minutes matter
         first = t_new - (k - 1) * self.step
-        tables = self._key_tables()
         P = self.P
-        S = len(self.fams) * self.slots.cap
-        block_t, block = self._tick_block(S, k)
+        F = max(1, len(self.fams))
+        S = self.slots.cap
+        srcmap = self._srcmap()
+        # the tick block is [slot, family x minute]: ONE pod index serves every family's body
+        block_t, block = self._tick_block(S, F * k)
         self.timings["points"] = k
-        reqs = [(range_url(fam[0], fam[1], first, k, self.step), first, k, 0) for fam in tables]
+        index = self.slots.table(F)
+        used = {int(f) for f in np.unique(self.row_fam[self.row_fam >= 0]).tolist()}
+        fams = [(fam, fi) for fam, fi in self.fams.items() if fi in used]
+        reqs = [(range_url(fam[0], fam[1], first, k, self.step), first, k, fi * k) for fam, fi in fams]
         self.tick_queries += len(reqs)
         t0 = time.perf_counter()
-        ok = await fetch_decode(self.prom, reqs, list(tables.values()), block, self.step, self.decode_threads,
+        ok = await fetch_decode(self.prom, reqs, [index] * len(reqs), block, self.step, self.decode_threads,
                                 timings=self.timings)
         self.timings["decode_ms"] = (time.perf_counter() - t0) * 1e3
         if not all(ok):
             return  # t_cur stays: the next tick fetches these minutes again
         col0 = (int(round(first / self.step)) - self.start_min).to(torch.int32).contiguous()
-        srcmap = self._srcmap()
+        src = block_t.view(S * F, k)
         if self.gpu:
             from ..ops import kernels as K
-            K.rollout_scatter(self.win, P, self.Wc, block_t.to(self.device, non_blocking=True), col0, srcmap)
+            K.rollout_scatter(self.win, P, self.Wc, src.to(self.device, non_blocking=True), col0, srcmap)
         else:
             win = self.win.view(self.cap, P, self.Wc)
             sm = srcmap.view(self.cap, P).long()
-            src = block_t
             for j in range(k):
                 c = (col0 + j).long()
                 ok_r = ((c >= 0) & (c < self.Wc))[:, None] & (sm >= 0)
@@ -966,26 +904,25 @@ class RolloutMonitor:
         self.out["npts"] = npts
         return self.out
 
-    async def tick(self) -> Dict[str, str]:
-        """One tick: heartbeat, history sync, admissions, window ingest, scoring,
-        verdicts; returns job -> status written."""
+    # ------------------------------------------------------------------ ticks
+    async def score_tick(self) -> Dict[str, str]:
+        """The scoring half of a tick: heartbeat, history advance, window ingest,
+        scoring, verdicts of the running jobs; returns job -> status written."""
         t_tick = time.perf_counter()
         now = self.clock()
         t_new = float(np.floor(now / self.step) * self.step)
         t0 = time.perf_counter()
         try:
             # inside the guard: a store error on this rank must not skip the lockstep
-            # exchange below, or its peers' all_to_all would pair with another collective
+            # exchange of the intake half, or its peers' all_to_all would pair with another
+            # collective
             self.store.heartbeat(self.worker_id, now)
-            await self.history.sync(now)
-            self.timings["history_ms"] = (time.perf_counter() - t0) * 1e3
-            await self._admit(now)
+            await self.history.sync(now, load=False)
         except Exception:  # noqa: BLE001
             if self.router is None:
                 raise
-            log.exception("rollout data step failed (the affine exchange still runs)")
-        if self.router is not None:
-            await self._route()  # every rank, every tick (collectives)
+            log.exception("rollout history step failed (the affine exchange still runs)")
+        self.timings["history_ms"] = (time.perf_counter() - t0) * 1e3
         self._refresh_apps()
         written: Dict[str, str] = {}
         if not self.jobs:
@@ -1021,6 +958,32 @@ class RolloutMonitor:
         self.timings["tick_ms"] = (time.perf_counter() - t_tick) * 1e3
         return written
 
+    async def intake(self) -> int:
+        """The intake half of a tick: history of newly claimed jobs, admission, and
+        (cluster-affine mode) the lockstep exchange of remote windows.  Returns the
+        jobs admitted."""
+        t0 = time.perf_counter()
+        now = self.clock()
+        n = 0
+        try:
+            await self.history.load_pending(now)
+            n = await self._admit(now)
+        except Exception:  # noqa: BLE001
+            if self.router is None:
+                raise
+            log.exception("rollout admission failed (the affine exchange still runs)")
+        if self.router is not None:
+            await self._route()  # every rank, every tick (collectives)
+        self.timings["intake_ms"] = (time.perf_counter() - t0) * 1e3
+        return n
+
+    async def tick(self) -> Dict[str, str]:
+        """One standalone tick: verdicts of the running jobs, then the admission of
+        the jobs claimed by :meth:`sync`."""
+        written = await self.score_tick()
+        await self.intake()
+        return written
+
     def _anomalies_from_band(self, verdict):
         x = self.win.cpu().numpy()
         up, lo = self.out["upper"].cpu().numpy(), self.out["lower"].cpu().numpy()
@@ -1033,17 +996,17 @@ class RolloutMonitor:
     def _verdicts(self, now: float, verdict: np.ndarray, npts: np.ndarray, a_rows, a_cols, a_vals) -> Dict[str, str]:
         """Jobs with an anomalous metric (fail fast) and jobs past endTime finish;
         the others stay leased and untouched."""
-        P, Wc = self.P, self.Wc
+        Wc = self.Wc
         bad_rows = np.nonzero(verdict == 1)[0]
         points: Dict[int, List[Tuple[float, float, str]]] = {}
         for rr, cc, vv in zip(np.asarray(a_rows).tolist(), np.asarray(a_cols).tolist(), np.asarray(a_vals).tolist()):
-            plan_ref = self.row_plan[rr]
-            if plan_ref is None:
+            if self.row_plan[rr] is None:
                 continue
-            s = self.jobs[plan_ref[0]].series[plan_ref[1]]
+            cols, s = self.row_cols[rr], int(self.row_s[rr])
             p, c = divmod(int(cc), Wc)
-            points.setdefault(rr, []).append((s.cur_start + c * self.step, float(vv),
-                                              s.cur_pods[p] if p < len(s.cur_pods) else ""))
+            pods = cols.cur_pods(s)
+            points.setdefault(rr, []).append((float(self.row_cs[rr]) + c * self.step, float(vv),
+                                              pods[p] if p < len(pods) else ""))
         finish: Dict[str, Tuple[str, str, Optional[Dict]]] = {}
         for rr in bad_rows.tolist():
             plan_ref = self.row_plan[rr]
@@ -1052,14 +1015,15 @@ class RolloutMonitor:
             jid = plan_ref[0]
             p = self.jobs[jid]
             anomaly = {}
-            for row, s in zip(p.rows, p.series):
+            for k, row in enumerate(p.rows):
                 if verdict[row] != 1:
                     continue
                 pts = sorted(points.get(row, []))
                 vals: List[float] = []
                 for ts, v, _ in pts:
                     vals += [ts, v]
-                anomaly[s.alias] = {"tags": ",".join(sorted({t for _, _, t in pts if t})), "values": vals}
+                anomaly[p.cols.alias[p.s0 + k]] = {"tags": ",".join(sorted({t for _, _, t in pts if t})),
+                                                   "values": vals}
                 self._last_anom[row] = pts[-1][0] if pts else now
             finish[jid] = (r.ST_COMPLETED_UNHEALTH, "anomaly detected in " + ",".join(sorted(anomaly)), anomaly)
         while self._ends and self._ends[0][0] <= now:
@@ -1068,7 +1032,7 @@ class RolloutMonitor:
             if p is None or jid in finish:
                 continue
             seen = bool(npts[p.rows].sum() > 0)
-            if seen and any(self.model_ok[row] for row in p.rows):
+            if seen and bool(self.model_ok[p.rows].any()):
                 finish[jid] = (r.ST_COMPLETED_HEALTH, "", None)
             elif seen:
                 finish[jid] = (r.ST_COMPLETED_UNKNOWN, "missing historical data", None)
@@ -1077,32 +1041,36 @@ class RolloutMonitor:
         if not finish:
             return {}
         items = []
+        content = f"scored by {self.worker_id} (resident engine)"
         for jid, (status, reason, anomaly) in finish.items():
             fields = {"status": status, "reason": reason, "claimed_by": "", "modified_ts": now,
-                      "processingContent": f"scored by {self.worker_id} (resident engine)"}
+                      "processingContent": content}
             if anomaly:
                 fields["anomalyInfo"] = json.dumps(anomaly)
             items.append((jid, fields))
         res = self.store.update_many(items, expect_claimed_by=self.worker_id)
         written = {}
         freed: List[int] = []  # every finished job's rows, released in ONE batch of device fills
+        gone_keys: List[np.ndarray] = []
+        up, lo, _ = self._bands
+        done = self._done_bands
         for (jid, fields), ok in zip(items, res):
             if ok:
                 self.metrics.jobs.labels(status=fields["status"]).inc()
                 written[jid] = fields["status"]
             p = self.jobs.pop(jid, None)
-            if p is not None:
-                up, lo, _ = self._bands
-                for row, s in zip(p.rows, p.series):  # the finished job's last band stays exported
-                    if row < len(up) and not math.isnan(up[row]):
-                        self.metrics.export_band(s.hkey[1], s.hkey[2], s.hkey[3], float(up[row]), float(lo[row]),
-                                                 self._last_anom.get(row))
-                self.history.unwant([s.hkey for s in p.series], now)
-                freed += p.rows
-                self.slots.release(self._job_pods(p))
-                self._app_ref(p, -1)
-                for row in p.rows:
-                    self._last_anom.pop(row, None)
+            if p is None:
+                continue
+            hk = p.cols.u64[p.s0:p.s0 + p.n, 0].tolist()
+            for k, (row, h) in enumerate(zip(p.rows, hk)):  # the finished job's last band stays exported
+                if row < len(up) and up[row] == up[row]:
+                    done[h] = (p.cols, p.s0 + k, float(up[row]), float(lo[row]), self._last_anom.pop(row, None))
+            self.history.unwant_h(hk, now)
+            freed += p.rows
+            gone_keys.append(p.pod_keys)
+            self._app_ref(p, -1)
+        if gone_keys:
+            self.slots.release(np.concatenate(gone_keys))
         self._free_rows(freed)
         return written
 
@@ -1117,7 +1085,80 @@ class RolloutMonitor:
 
     def _band_rows(self):
         up, lo, verdict = self._bands
+        live = set()
         for jid, p in list(self.jobs.items()):
-            for row, s in zip(p.rows, p.series):
-                if row < len(up) and not math.isnan(up[row]):
-                    yield (s.hkey[1], s.hkey[2], s.hkey[3], float(up[row]), float(lo[row]), self._last_anom.get(row))
+            hk = p.cols.u64[p.s0:p.s0 + p.n, 0].tolist()
+            for k, row in enumerate(p.rows):
+                if row < len(up) and up[row] == up[row]:
+                    live.add(hk[k])
+                    key = p.cols.hkey_at(p.s0 + k)
+                    yield (key[1], key[2], key[3], float(up[row]), float(lo[row]), self._last_anom.get(row))
+        for h, (cols, s, u, l_, an) in list(self._done_bands.items()):
+            if h not in live:
+                key = cols.hkey_at(s)
+                yield (key[1], key[2], key[3], u, l_, an)
+
+
+class _Batch:
+    """The rows of one admission batch, gathered from the plans' columns (grouped
+    by the PlanCols they came from)."""
+
+    def __init__(self, plans: List[RolloutPlan], P: int) -> None:
+        groups: Dict[int, Tuple[PlanCols, List[RolloutPlan]]] = {}
+        for p in plans:
+            groups.setdefault(id(p.cols), (p.cols, []))[1].append(p)
+        self.plans: List[RolloutPlan] = []
+        self.parts: List[Tuple[PlanCols, int, int]] = []   # (cols, first batch row, end)
+        sidx, f64, i32, u64 = [], [], [], []
+        n = 0
+        for cols, ps in groups.values():
+            s0 = np.fromiter((p.s0 for p in ps), dtype=np.int64, count=len(ps))
+            ln = np.fromiter((p.n for p in ps), dtype=np.int64, count=len(ps))
+            tot = int(ln.sum())
+            s = np.repeat(s0 - (np.cumsum(ln) - ln), ln) + np.arange(tot)
+            sidx.append(s)
+            f64.append(cols.f64[s])
+            i32.append(cols.i32[s])
+            u64.append(cols.u64[s])
+            self.parts.append((cols, n, n + tot))
+            self.plans += ps
+            n += tot
+        self.n = n
+        self.P = P
+        self.s = np.concatenate(sidx) if sidx else np.zeros(0, np.int64)
+        self.f64 = np.concatenate(f64) if f64 else np.zeros((0, 3))
+        self.i32 = np.concatenate(i32) if i32 else np.zeros((0, 7), np.int32)
+        self.u64 = np.concatenate(u64) if u64 else np.zeros((0, 6), np.uint64)
+        self.lens = np.fromiter((p.n for p in self.plans), dtype=np.int64, count=len(self.plans))
+        self._part_of = np.concatenate([np.full(hi - lo, k, dtype=np.int64) for k, (_, lo, hi) in
+                                        enumerate(self.parts)]) if self.parts else np.zeros(0, np.int64)
+        self.rows = np.zeros(0, np.int64)
+
+    def cols_of(self, i: int) -> PlanCols:
+        return self.parts[int(self._part_of[i])][0]
+
+    def s_of(self, i: int) -> int:
+        return int(self.s[i])
+
+    def ns_of(self, i: int) -> str:
+        return self.cols_of(i).ns_at(self.s_of(i))
+
+    def alias_metric(self):
+        for cols, lo, hi in self.parts:
+            for s in self.s[lo:hi].tolist():
+                yield cols.alias[s], cols.hfam[s][1]
+
+    def cur_pod_keys(self) -> Tuple[np.ndarray, np.ndarray]:
+        """``[n, P]`` keys of each row's first P current pods and the valid mask."""
+        P = self.P
+        H = np.zeros((self.n, P), dtype=np.uint64)
+        valid = np.zeros((self.n, P), dtype=bool)
+        K = np.arange(P)[None, :]
+        for cols, lo, hi in self.parts:
+            q0 = self.i32[lo:hi, 2].astype(np.int64)[:, None]
+            nq = np.minimum(self.i32[lo:hi, 3], P)[:, None]
+            v = K < nq
+            idx = np.where(v, q0 + K, 0)
+            H[lo:hi] = np.where(v, cols.pod_u64[idx] if len(cols.pod_u64) else 0, 0)
+            valid[lo:hi] = v
+        return H, valid

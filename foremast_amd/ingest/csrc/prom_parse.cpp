@@ -366,6 +366,60 @@ struct KeyIndex {
     }
     return true;
   }
+  // ---- live updates (single-threaded, between decodes) -----------------------------
+  // A key's row can change or be retired (row -1: lookups miss, so a retired pod that
+  // still reports is counted unmatched instead of landing in its reused slot).  The
+  // predictions of `learn` carry entry indices, and a prediction is used only while
+  // its entry still holds the predicted row (see keyed_elements), so updates need no
+  // prediction reset; a compaction renumbers entries and forgets them all.
+  long long dead = 0;
+  void rehash(uint64_t cap) {
+    table.assign(cap, -1);
+    mask = cap - 1;
+    for (size_t e = 0; e < slots.size(); ++e) {
+      uint64_t i = mix(slots[e].h) & mask;
+      while (table[i] >= 0) i = (i + 1) & mask;
+      table[i] = (int32_t)e;
+    }
+  }
+  bool upsert(uint64_t h, long long row) {
+    if (row < 0 || row > 0x7fffffffll) return false;
+    const long long e = find_slot(h);
+    if (e >= 0) {
+      if (slots[e].row < 0) --dead;
+      __atomic_store_n(&slots[e].row, (int32_t)row, __ATOMIC_RELAXED);
+      return true;
+    }
+    if (slots.size() >= 0x3fffffff) return false;
+    slots.push_back(Slot{h, 0, (int32_t)row, -1, -1, 0});
+    if (2 * slots.size() > table.size()) {
+      rehash(table.size() * 2);
+    } else {
+      uint64_t i = mix(h) & mask;
+      while (table[i] >= 0) i = (i + 1) & mask;
+      table[i] = (int32_t)(slots.size() - 1);
+    }
+    return true;
+  }
+  void retire(uint64_t h) {
+    const long long e = find_slot(h);
+    if (e >= 0 && slots[e].row >= 0) {
+      __atomic_store_n(&slots[e].row, (int32_t)-1, __ATOMIC_RELAXED);
+      ++dead;
+    }
+  }
+  void compact() {  // drop retired entries once they are half the index
+    if (dead * 2 <= (long long)slots.size()) return;
+    std::vector<Slot> keep;
+    keep.reserve(slots.size() - (size_t)dead);
+    for (const Slot& sl : slots)
+      if (sl.row >= 0) keep.push_back(Slot{sl.h, 0, sl.row, -1, -1, 0});
+    slots.swap(keep);
+    dead = 0;
+    uint64_t cap = 16;
+    while (cap < 2 * slots.size()) cap <<= 1;
+    rehash(cap);
+  }
   void prefetch(uint64_t h) const { __builtin_prefetch(&table[mix(h) & mask]); }
   void prefetch_slot(long long i) const { __builtin_prefetch(&slots[i]); }
   long long find_slot(uint64_t h) const {
@@ -523,7 +577,8 @@ long long keyed_elements(Cursor& c, const char* stop, const KeyedOut& o, KeyInde
         int32_t pslot, prow;
         uint64_t ptag;
         if (prev_slot >= 0 && ix.predict(prev_slot, plen, pslot, prow, ptag) && (size_t)(c.e - m0) >= plen &&
-            m0[plen - 1] == '}' && KeyIndex::tag_of(bytes_hash(m0, plen), plen, pslot, prow) == ptag) {
+            m0[plen - 1] == '}' && __atomic_load_n(&ix.slots[pslot].row, __ATOMIC_RELAXED) == prow &&
+            KeyIndex::tag_of(bytes_hash(m0, plen), plen, pslot, prow) == ptag) {
           c.p = m0 + plen;
           cur_slot = pslot;
           ix.prefetch_slot(pslot);  // the next element's prediction, needed after the samples
@@ -782,6 +837,31 @@ void* fm_keyindex_new(const uint64_t* key_hash, const long long* key_rows, long 
 }
 
 void fm_keyindex_free(void* ix) { delete (KeyIndex*)ix; }
+
+// Live index updates: set (insert or re-row) / retire keys; returns n or -1.
+long long fm_keyindex_upsert(void* index, const uint64_t* key_hash, const long long* key_rows, long long n) {
+  KeyIndex* ix = (KeyIndex*)index;
+  if (!ix || n < 0) return -1;
+  for (long long j = 0; j < n; ++j)
+    if (!ix->upsert(key_hash[j], key_rows[j])) return -1;
+  return n;
+}
+
+long long fm_keyindex_retire(void* index, const uint64_t* key_hash, long long n) {
+  KeyIndex* ix = (KeyIndex*)index;
+  if (!ix || n < 0) return -1;
+  for (long long j = 0; j < n; ++j) ix->retire(key_hash[j]);
+  ix->compact();
+  return n;
+}
+
+// rows of keys (-1: absent or retired)
+long long fm_keyindex_lookup(void* index, const uint64_t* key_hash, long long n, long long* rows) {
+  KeyIndex* ix = (KeyIndex*)index;
+  if (!ix || n < 0) return -1;
+  for (long long j = 0; j < n; ++j) rows[j] = ix->find(key_hash[j]);
+  return n;
+}
 
 // Keyed dense scatter of one body through a KeyIndex (same outputs as
 // fm_prom_dense_keyed).
@@ -1060,4 +1140,9 @@ extern "C" long long fm_prom_render(const char* labels, const long long* lab_off
   if ((long long)buf.size() > cap) return -(long long)buf.size();
   std::memcpy(out, buf.data(), buf.size());
   return (long long)buf.size();
+}
+
+// series_key for the other translation units of this library (job_plan.cpp)
+extern "C" uint64_t fm_series_key(const char* a0, const char* a1, const char* b0, const char* b1) {
+  return series_key(a0, a1, b0, b1);
 }

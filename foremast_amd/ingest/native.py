@@ -22,6 +22,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "prom_parse.cpp")
+SRCS = [SRC, os.path.join(HERE, "csrc", "job_plan.cpp")]
 LIBDIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(LIBDIR, "libforemast_ingest.so")
 
@@ -35,12 +36,12 @@ class ParseError(ValueError):
 
 def build(verbose: bool = False) -> str:
     os.makedirs(LIBDIR, exist_ok=True)
-    if os.path.exists(LIB) and os.path.getmtime(LIB) >= os.path.getmtime(SRC):
+    if os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(x) for x in SRCS):
         return LIB
     cxx = os.environ.get("CXX") or shutil.which("g++") or shutil.which("clang++")
     if not cxx:
         raise RuntimeError("no C++ compiler for the ingest parser")
-    cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-o", LIB + ".tmp", SRC]
+    cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-o", LIB + ".tmp", *SRCS]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -74,6 +75,15 @@ def _load() -> Optional[C.CDLL]:
         lib.fm_prom_keys.restype = LL
         lib.fm_prom_render.argtypes = [C.c_char_p, P, LL, P, LL, C.c_double, C.c_double, P, LL]
         lib.fm_prom_render.restype = LL
+        lib.fm_plan_rollout.argtypes = [C.c_char_p, P, LL, C.c_double, LL, P, P, P, P, P, P, P, LL, P, P, LL,
+                                         P, LL]
+        lib.fm_plan_rollout.restype = LL
+        lib.fm_keyindex_upsert.argtypes = [P, P, P, LL]
+        lib.fm_keyindex_upsert.restype = LL
+        lib.fm_keyindex_retire.argtypes = [P, P, LL]
+        lib.fm_keyindex_retire.restype = LL
+        lib.fm_keyindex_lookup.argtypes = [P, P, LL, P]
+        lib.fm_keyindex_lookup.restype = LL
         lib.fm_keyindex_new.argtypes = [P, P, LL]
         lib.fm_keyindex_new.restype = P
         lib.fm_keyindex_free.argtypes = [P]
@@ -270,6 +280,52 @@ class KeyTable:
             self._index = ix
             self._lib = lib
         return ix
+
+    def __del__(self) -> None:
+        ix = getattr(self, "_index", None)
+        if ix:
+            self._lib.fm_keyindex_free(ix)
+            self._index = None
+
+
+class LiveKeyIndex:
+    """A native (hash -> row) index that is updated in place: keys are set or
+    retired between decodes (a retired key is unmatched).  Usable wherever a
+    :class:`KeyTable` is (``index``, ``label_a`` / ``label_b``), e.g. one pod index
+    shared by every metric family's body of a tick."""
+
+    def __init__(self, label_a: str = "namespace", label_b: str = "pod") -> None:
+        self.label_a, self.label_b = label_a.encode(), label_b.encode()
+        lib = _load()
+        if lib is None:
+            raise RuntimeError("native ingest library unavailable")
+        self._lib = lib
+        empty = np.zeros(1, dtype=np.uint64)
+        self._index = lib.fm_keyindex_new(empty.ctypes.data, np.zeros(1, np.int64).ctypes.data, 0)
+        if not self._index:
+            raise RuntimeError("fm_keyindex_new failed")
+
+    @property
+    def index(self) -> int:
+        return self._index
+
+    def set(self, hashes: np.ndarray, rows: np.ndarray) -> None:
+        h = np.ascontiguousarray(hashes, dtype=np.uint64)
+        r = np.ascontiguousarray(rows, dtype=np.int64)
+        if len(h) and self._lib.fm_keyindex_upsert(self._index, h.ctypes.data, r.ctypes.data, len(h)) != len(h):
+            raise ValueError("key index update failed (negative row)")
+
+    def retire(self, hashes: np.ndarray) -> None:
+        h = np.ascontiguousarray(hashes, dtype=np.uint64)
+        if len(h):
+            self._lib.fm_keyindex_retire(self._index, h.ctypes.data, len(h))
+
+    def lookup(self, hashes: np.ndarray) -> np.ndarray:
+        h = np.ascontiguousarray(hashes, dtype=np.uint64)
+        out = np.empty(len(h), dtype=np.int64)
+        if len(h):
+            self._lib.fm_keyindex_lookup(self._index, h.ctypes.data, len(h), out.ctypes.data)
+        return out
 
     def __del__(self) -> None:
         ix = getattr(self, "_index", None)

@@ -30,7 +30,7 @@ import httpx
 
 from ..api import rest as r
 from ..utils.timeutil import format_rfc3339_nano
-from .jobstore import JobStore, is_claimable
+from .jobstore import JobStore, _filter, is_claimable
 
 INDEX = "documents"
 DOC_TYPE = "document"
@@ -155,7 +155,7 @@ class ElasticJobStore(JobStore):
         hits = self._search((), size=10000, extra=[{"range": {"beat": {"gte": since}}}], index=BEAT_INDEX)
         return {d["worker"]: float(d["beat"]) for d, _ in hits if "worker" in d}
 
-    def claim(self, worker, now=None, max_stuck_s=90.0, limit=64, only=None, steal_from=None):
+    def claim(self, worker, now=None, max_stuck_s=90.0, limit=64, only=None, steal_from=None, only_batch=None):
         """Two searches, so open jobs are never hidden behind thousands of live
         leases: due open documents, then in-progress ones whose lease is stale
         (not modified within ``max_stuck_s`` and the holder has no fresh
@@ -174,18 +174,22 @@ class ElasticJobStore(JobStore):
         if steal_from:
             cand += self._search_pages(r.INPROGRESS_STATUSES, 4 * PAGE,
                                        extra=[{"terms": {_kw("claimed_by"): sorted(steal_from)}}])
-        seen, out = set(), []
+        seen, keep = set(), []
         for d, ver in sorted(cand, key=lambda dv: dv[0].get("modified_ts", 0.0)):
-            if len(out) >= limit:
-                break
             if d["id"] in seen:
                 continue
             seen.add(d["id"])
-            if not is_claimable(d, now, max_stuck_s, steal_from, beats) or (only is not None and not only(d)):
-                continue
+            if is_claimable(d, now, max_stuck_s, steal_from, beats):
+                keep.append((d, ver))
+        vers = {id(d): ver for d, ver in keep}
+        out = []
+        stamp = format_rfc3339_nano(now)
+        for d in _filter([d for d, _ in keep], only, only_batch):
+            if len(out) >= limit:
+                break
             d.update(status=r.ST_PREPROCESS_INPROGRESS, claimed_by=worker, claimed_at=now,
-                     modified_ts=now, modified_at=format_rfc3339_nano(now))
-            if self._put_versioned(d, ver):  # lost races simply drop out
+                     modified_ts=now, modified_at=stamp)
+            if self._put_versioned(d, vers[id(d)]):  # lost races simply drop out
                 out.append(d)
         return out
 

@@ -124,9 +124,11 @@ class JobStore(abc.ABC):
 
     @abc.abstractmethod
     def claim(self, worker: str, now: Optional[float] = None, max_stuck_s: float = 90.0,
-              limit: int = 64, only=None, steal_from=None) -> List[Dict[str, Any]]:
+              limit: int = 64, only=None, steal_from=None, only_batch=None) -> List[Dict[str, Any]]:
         """Lease up to ``limit`` claimable documents (``only(doc)`` filters,
         e.g. by strategy: the streaming monitor takes continuous jobs;
+        ``only_batch(docs) -> [bool]`` is the same filter over every candidate at
+        once (the rollout engine decodes a deploy burst in one native batch);
         ``steal_from``: worker ids whose leases are void, see is_claimable)."""
 
     @abc.abstractmethod
@@ -156,6 +158,15 @@ class JobStore(abc.ABC):
 
     def close(self) -> None:
         pass
+
+
+def _filter(cand: List[Dict[str, Any]], only, only_batch) -> List[Dict[str, Any]]:
+    """Candidates passing ``only`` / ``only_batch`` (in order)."""
+    if only_batch is not None and cand:
+        cand = [d for d, ok in zip(cand, only_batch(cand)) if ok]
+    if only is not None:
+        cand = [d for d in cand if only(d)]
+    return cand
 
 
 def _stamp(d: Dict[str, Any], fields: Dict[str, Any]) -> None:
@@ -235,9 +246,10 @@ class MemoryJobStore(JobStore):
         with self._lock:
             self._beats[worker] = time.time() if now is None else float(now)
 
-    def claim(self, worker, now=None, max_stuck_s=90.0, limit=64, only=None, steal_from=None):
+    def claim(self, worker, now=None, max_stuck_s=90.0, limit=64, only=None, steal_from=None, only_batch=None):
         now = time.time() if now is None else now
         out = []
+        stamp = format_rfc3339_nano(now)
         with self._lock:
             cand = list(self._open.values())
             for holder, docs in self._held.items():
@@ -246,18 +258,16 @@ class MemoryJobStore(JobStore):
                 elif now - self._beats.get(holder, 0.0) > max_stuck_s:
                     cand.extend(d for d in docs.values() if now - float(d.get("modified_ts", 0.0) or 0.0) > max_stuck_s)
             cand.sort(key=lambda x: x.get("modified_ts", 0.0))
-            for d in cand:
-                if len(out) >= limit:
-                    break
-                if is_claimable(d, now, max_stuck_s, steal_from, self._beats) and (only is None or only(d)):
-                    before = (d.get("status"), d.get("claimed_by"))
-                    d["status"] = r.ST_PREPROCESS_INPROGRESS
-                    d["claimed_by"] = worker
-                    d["claimed_at"] = now
-                    d["modified_ts"] = now
-                    d["modified_at"] = format_rfc3339_nano(now)
-                    self._index(d, before)
-                    out.append(copy.deepcopy(d))
+            cand = [d for d in cand if is_claimable(d, now, max_stuck_s, steal_from, self._beats)]
+            for d in _filter(cand, only, only_batch)[:limit]:
+                before = (d.get("status"), d.get("claimed_by"))
+                d["status"] = r.ST_PREPROCESS_INPROGRESS
+                d["claimed_by"] = worker
+                d["claimed_at"] = now
+                d["modified_ts"] = now
+                d["modified_at"] = stamp
+                self._index(d, before)
+                out.append(dict(d))  # documents are flat (str / number values): a shallow copy is a copy
         return out
 
     def all(self):
@@ -354,7 +364,7 @@ class SqliteJobStore(JobStore):
         self._conn().execute("INSERT OR REPLACE INTO workers(worker, beat) VALUES (?, ?)",
                              (worker, time.time() if now is None else float(now)))
 
-    def claim(self, worker, now=None, max_stuck_s=90.0, limit=64, only=None, steal_from=None):
+    def claim(self, worker, now=None, max_stuck_s=90.0, limit=64, only=None, steal_from=None, only_batch=None):
         now = time.time() if now is None else now
         cutoff = now - max_stuck_s
         steal = sorted(steal_from or ())
@@ -370,14 +380,11 @@ class SqliteJobStore(JobStore):
                 f"WHERE w.worker = documents.claimed_by), 0) < ?) {q_steal})) ORDER BY modified_ts",
                 r.OPEN_STATUSES + (now,) + r.INPROGRESS_STATUSES + (cutoff, cutoff) + tuple(steal)).fetchall()
             out = []
-            for (raw,) in rows:
-                if len(out) >= limit:
-                    break
-                d = json.loads(raw)
-                if not is_claimable(d, now, max_stuck_s, steal_from) or (only is not None and not only(d)):
-                    continue
+            cand = [d for d in (json.loads(raw) for (raw,) in rows) if is_claimable(d, now, max_stuck_s, steal_from)]
+            stamp = format_rfc3339_nano(now)
+            for d in _filter(cand, only, only_batch)[:limit]:
                 d.update(status=r.ST_PREPROCESS_INPROGRESS, claimed_by=worker, claimed_at=now,
-                         modified_ts=now, modified_at=format_rfc3339_nano(now))
+                         modified_ts=now, modified_at=stamp)
                 self._write(c, d)
                 out.append(d)
             c.execute("COMMIT")
