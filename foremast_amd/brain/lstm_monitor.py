@@ -129,6 +129,18 @@ class LstmMonitor:
         # (800 on the GPU: a model calibrated after 200 steps keeps drifting under the per-tick
         # training, and its first ticks flag healthy series — profiles/lstm_detection_r3.md)
         self.pretrain_steps = int(os.environ.get("FOREMAST_LSTM_PRETRAIN", "800" if self.gpu else "20"))
+        # the fresh model's initial training is spread over ticks (this many extra DP steps per
+        # tick, every rank in lockstep) instead of stalling one lockstep tick for all of it;
+        # entities admitted meanwhile are scored once it is done and they are calibrated
+        self.pretrain_per_tick = int(os.environ.get("FOREMAST_LSTM_PRETRAIN_PER_TICK", "100" if self.gpu else "20"))
+        self._uncalibrated: List[int] = []
+        self._pending_cal = False   # some rank admitted entities while the model was pretraining
+        self._pretraining = False
+        self._calibrated = np.zeros(self.shard.n, dtype=bool)
+        # the weights' CRC in the node table: every digest_every ticks and after a re-formation
+        self.digest_every = int(os.environ.get("FOREMAST_LSTM_DIGEST_EVERY", "60"))
+        self._digest: Optional[str] = None
+        self._digest_tick = -1
         self.timings: Dict[str, float] = {}
 
     # ------------------------------------------------------------------ membership
@@ -172,6 +184,7 @@ class LstmMonitor:
                     if torch.is_tensor(v):
                         dist.broadcast(v.data if v.device == self.device else v, src=0)
             self.shard.packed = None
+        self._digest = None
 
     def _drop(self, jid: str, now: float) -> None:
         e = self.jobs.pop(jid, None) or self.waiting.pop(jid, None)
@@ -195,9 +208,11 @@ class LstmMonitor:
         pd = torch.zeros((cap, self.F), dtype=torch.bool, device=self.device)
         pd[:n] = self.padded
         self.feat_rows, self.padded = fr, pd
+        self._calibrated = np.concatenate([self._calibrated, np.zeros(cap - n, dtype=bool)])
 
     def _free_row(self, row: int) -> None:
         self.row_job[row] = None
+        self._calibrated[row] = False
         self.feat_rows[row] = -1
         self.padded[row] = False
         self.shard.app_id[row] = 0
@@ -303,13 +318,25 @@ class LstmMonitor:
         self.shard.train_step(weight=float(has), flags=flags,
                               timeout_s=self.exchange_timeout if comm.active() else None)
         red = self.shard.trainer.last_flags
-        if red is not None and float(red[0]) > 0:  # some rank admitted entities (every rank sees it)
-            # a fresh model first gets its initial training (same step count on every rank:
-            # the trainers advance in lockstep), then the new rows are calibrated (collective)
-            while self.shard.trainer.steps < self.pretrain_steps:
+        self._uncalibrated += admitted
+        # a fresh model's initial training, at most pretrain_per_tick extra steps per tick (the
+        # step counts are equal on every rank: the trainers advance in lockstep)
+        if red is not None and float(red[0]) > 0:
+            self._pretraining = True  # the first entities anywhere start the initial training
+        if self._pretraining and self.shard.trainer.steps < self.pretrain_steps:
+            for _ in range(min(self.pretrain_per_tick, self.pretrain_steps - self.shard.trainer.steps)):
                 self.shard.train_step(weight=float(has), timeout_s=self.exchange_timeout if comm.active() else None)
+            self.timings["pretrain_steps"] = self.shard.trainer.steps
+        pre_done = self.shard.trainer.steps >= self.pretrain_steps
+        if pre_done and (self._pending_cal or (red is not None and float(red[0]) > 0)):
+            # new rows (any rank) are calibrated together: a collective every rank joins
             self.shard.calibrate(min(self.shard.train_batch, 4096),
-                                 rows=torch.tensor(admitted, dtype=torch.long, device=self.device))
+                                 rows=torch.tensor(self._uncalibrated, dtype=torch.long, device=self.device))
+            self._calibrated[self._uncalibrated] = True
+            self._uncalibrated = []
+            self._pending_cal = False
+        elif not pre_done and red is not None and float(red[0]) > 0:
+            self._pending_cal = True
         self.timings["train_ms"] = (time.perf_counter() - t0) * 1e3
         written: Dict[str, str] = {}
         if not self.jobs:
@@ -320,6 +347,8 @@ class LstmMonitor:
         newest = self._newest()
         items = []
         for jid, e in list(self.jobs.items()):
+            if not self._calibrated[e.row]:
+                continue  # admitted while the model was pretraining: scored once calibrated
             if v[e.row] == 1:
                 anomaly = {}
                 for f, (alias, _k) in enumerate(e.feats):
@@ -349,12 +378,17 @@ class LstmMonitor:
         return torch.stack([ring.data[:, col].float() for ring in self.shard.rings], 1).cpu().numpy()
 
     def model_digest(self) -> str:
-        """CRC of the replica's weights (the node table shows every rank's: equal = in sync)."""
+        """CRC of the replica's weights (the node table shows every rank's: equal = in
+        sync).  Recomputed every ``digest_every`` ticks and after a re-formation (it
+        copies every weight to the host), the cached value otherwise."""
+        if self._digest is not None and self.ticks - self._digest_tick < self.digest_every:
+            return self._digest
         import zlib
         crc = 0
         for p in self.shard.model.parameters():
             crc = zlib.crc32(p.detach().float().cpu().numpy().tobytes(), crc)
-        return f"{crc:08x}"
+        self._digest, self._digest_tick = f"{crc:08x}", self.ticks
+        return self._digest
 
     def app_table(self):
         names = list(self._app_names)

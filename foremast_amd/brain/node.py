@@ -87,6 +87,15 @@ class NodeBrain:
         self._published = -1e18
         self._last_anomalous = None
         self.gc_freeze_min = int(os.environ.get("FOREMAST_GC_FREEZE_MIN", "256"))
+        self.gc_full_every_s = float(os.environ.get("FOREMAST_GC_FULL_EVERY_S", "600"))
+        self._full_gc_at = time.monotonic()
+        self._admitted_since = 0
+        # young-generation threshold: a tick allocates ~10^5 short-lived objects (decoded
+        # rows, query strings); the default 700 runs ~150 young collections per tick
+        t0 = int(os.environ.get("FOREMAST_GC_THRESHOLD0", "50000"))
+        if t0 > 0:
+            th = gc.get_threshold()
+            gc.set_threshold(max(th[0], t0), th[1], th[2])
         self.timings: Dict[str, float] = {}
         self._frozen_at = 0
         for m in self.monitors:
@@ -152,16 +161,27 @@ class NodeBrain:
         return self.health.exchange(names, counts, version, n_live, info)
 
     def _freeze_admitted(self) -> None:
-        """Admission builds long-lived per-job state (plans, slot maps, entities):
-        after a large intake, one full collection, then ``gc.freeze()`` moves
-        everything alive into the permanent generation, so the periodic gen-2
-        collections of the steady ticks no longer walk the admitted jobs' objects
-        (a 100+ ms pause in a ~9 ms tick at 10k jobs otherwise)."""
+        """Admission builds long-lived per-job state (plans, slot maps, documents):
+        after an intake of ``gc_freeze_min`` jobs, ``gc.freeze()`` moves everything
+        alive into the permanent generation (O(1)), so the generational collections
+        of the following ticks no longer walk the admitted jobs' objects (a 100+ ms
+        gen-2 pause in a ~9 ms tick at 10k jobs otherwise).  Frozen objects are
+        still freed by reference counting when their jobs finish; what only the
+        cycle collector could reclaim is reclaimed by a full collection every
+        ``gc_full_every_s`` (default 10 min), off the steady ticks' path."""
+        self._admitted_since += sum(getattr(m, "timings", {}).get("admitted", 0) or 0 for m in self.monitors
+                                    if hasattr(m, "intake"))
         n = sum(len(getattr(m, "jobs", ())) for m in self.monitors)
-        if n - self._frozen_at >= self.gc_freeze_min:
+        now = time.monotonic()
+        if now - self._full_gc_at >= self.gc_full_every_s:
+            gc.unfreeze()
             gc.collect()
             gc.freeze()
-            self._frozen_at = n
+            self._full_gc_at = now
+            self._frozen_at, self._admitted_since = n, 0
+        elif n - self._frozen_at >= self.gc_freeze_min or self._admitted_since >= self.gc_freeze_min:
+            gc.freeze()
+            self._frozen_at, self._admitted_since = n, 0
         elif n < self._frozen_at:
             self._frozen_at = n  # jobs finished: the next intake of the same size freezes again
 

@@ -24,6 +24,7 @@ decoder accepts.
 
 from __future__ import annotations
 
+import os
 import re
 from collections import OrderedDict
 from dataclasses import dataclass, field
@@ -71,8 +72,9 @@ class PlanCols:
     """Columnar plans of a batch of jobs: series rows ``[S]`` and pods ``[Q]``.
 
     ``f64 [S, 3]`` cur_start, base_start, hist_end; ``i32 [S, 7]`` cur_n, base_n,
-    cur pod0, cur npod, base pod0, base npod, has_base; ``u64 [S, 5]`` history key,
-    family key, baseline family key, history family key, (namespace, app) key;
+    cur pod0, cur npod, base pod0, base npod, has_base; ``u64 [S, 6]`` history key,
+    family key, baseline family key, history family key, (namespace, app) key,
+    (alias, history metric) key;
     ``pod_u64 [Q]`` (namespace, pod) keys.  The few distinct strings (alias,
     families) are interned per row at construction; a row's history key tuple,
     namespace and pod names are decoded on demand from ``text`` (``span``)."""
@@ -119,6 +121,15 @@ class PlanCols:
             self._pods[(p0, n)] = got
         return got
 
+    def pods_alt(self, s: int, base: bool) -> bytes:
+        """The row's current (or baseline) pods as the RE2 alternation ``a|b|c``
+        (sorted, distinct; empty for rows of the Python parser: use :meth:`pods`)."""
+        if self.span is None:
+            return b""
+        a = self.span[s]
+        k = 18 if base else 16
+        return self.text[a[k]:a[k] + a[k + 1]]
+
     def cur_pods(self, s: int) -> Tuple[str, ...]:
         return self.pods(int(self.i32[s, 2]), int(self.i32[s, 3]))
 
@@ -139,7 +150,7 @@ class PlanCols:
         f64 = np.array([[s.cur_start, s.base_start, s.hist_end] for s in series], dtype=np.float64).reshape(S, 3)
         pods: List[Tuple[str, str]] = []
         i32 = np.zeros((S, 7), dtype=np.int32)
-        u64 = np.zeros((S, 5), dtype=np.uint64)
+        u64 = np.zeros((S, 6), dtype=np.uint64)
         for k, s in enumerate(series):
             i32[k, 0], i32[k, 1] = s.cur_n, s.base_n
             i32[k, 2], i32[k, 3] = len(pods), len(s.cur_pods)
@@ -152,6 +163,7 @@ class PlanCols:
             u64[k, 2] = native.key_hash(*s.base_fam) if i32[k, 6] else 0
             u64[k, 3] = native.key_hash(s.hkey[0], s.hkey[1])
             u64[k, 4] = native.key_hash(s.hkey[2], s.hkey[3])
+            u64[k, 5] = native.key_hash(s.alias, s.hkey[1])
         text = "".join(p for _, p in pods).encode()
         lens = np.array([len(p.encode()) for _, p in pods], dtype=np.int64)
         span = np.zeros((len(pods), 2), dtype=np.int64)
@@ -347,9 +359,29 @@ def _plan(doc, step, window_cols) -> Optional[RolloutPlan]:
 
 # ---------------------------------------------------------------------- native batches
 # interned strings of the few distinct aliases / families (keyed by bytes or 64-bit key)
-_INTERN_A: Dict[bytes, str] = {}
+_INTERN_A: Dict[int, str] = {}
 _INTERN_H: Dict[int, Tuple[str, str]] = {}
 _INTERN_F: Dict[int, Tuple[str, str]] = {}
+
+
+def _native_call(lib, blob, off, N, step, window_cols, ser_cap, pod_cap, text_cap):
+    job_i32 = np.zeros((N, 3), dtype=np.int32)
+    job_f64 = np.zeros(N, dtype=np.float64)
+    job_span = np.zeros((N, 4), dtype=np.int64)
+    f64 = np.empty((ser_cap, 3), dtype=np.float64)
+    i32 = np.empty((ser_cap, 7), dtype=np.int32)
+    span = np.empty((ser_cap, 20), dtype=np.int64)
+    u64 = np.empty((ser_cap, 6), dtype=np.uint64)
+    pod_span = np.empty((pod_cap, 2), dtype=np.int64)
+    pod_u64 = np.empty(pod_cap, dtype=np.uint64)
+    text = np.empty(text_cap, dtype=np.uint8)
+    S = lib.fm_plan_rollout(blob, off.ctypes.data, N, float(step), int(window_cols), job_i32.ctypes.data,
+                            job_f64.ctypes.data, job_span.ctypes.data, f64.ctypes.data, i32.ctypes.data,
+                            span.ctypes.data, u64.ctypes.data, ser_cap, pod_span.ctypes.data, pod_u64.ctypes.data,
+                            pod_cap, text.ctypes.data, text_cap)
+    if S < 0:
+        return None
+    return S, job_i32, job_f64, job_span, f64, i32, span, u64, pod_span, pod_u64, text
 
 
 def _native_batch(docs: Sequence[Dict], step: float, window_cols: int) -> Optional[Tuple[np.ndarray, List]]:
@@ -357,65 +389,94 @@ def _native_batch(docs: Sequence[Dict], step: float, window_cols: int) -> Option
     lib = native._load()
     if lib is None or not docs:
         return None
-    parts = [(d.get(k) or "").encode() if isinstance(d.get(k) or "", str) else b"" for d in docs for k in DOC_FIELDS]
-    lens = np.fromiter((len(x) for x in parts), dtype=np.int64, count=len(parts))
-    off = np.zeros(len(parts) + 1, dtype=np.int64)
+    fields = [d.get(k) for d in docs for k in DOC_FIELDS]
+    fields = [f if isinstance(f, str) else "" for f in fields]
+    joined = "".join(fields)
+    if joined.isascii():  # one encode; byte offsets = character offsets
+        lens = np.fromiter(map(len, fields), dtype=np.int64, count=len(fields))
+        blob = joined.encode("ascii") or b"\0"
+    else:
+        parts = [f.encode() for f in fields]
+        lens = np.fromiter(map(len, parts), dtype=np.int64, count=len(parts))
+        blob = b"".join(parts) or b"\0"
+    off = np.zeros(len(fields) + 1, dtype=np.int64)
     np.cumsum(lens, out=off[1:])
-    blob = b"".join(parts) or b"\0"
     N = len(docs)
-    # capacities: series <= aliases in the current configs, pods <= bytes / 2
-    ser_cap = max(16, sum(d.get("currentConfig", "").count("== ") for d in docs if isinstance(d.get("currentConfig"), str)))
-    pod_cap = max(64, int(off[-1]) // 2)
-    text_cap = int(off[-1]) + 1024
-    job_i32 = np.zeros((N, 3), dtype=np.int32)
-    job_f64 = np.zeros(N, dtype=np.float64)
-    job_span = np.zeros((N, 4), dtype=np.int64)
-    f64 = np.zeros((ser_cap, 3), dtype=np.float64)
-    i32 = np.zeros((ser_cap, 7), dtype=np.int32)
-    span = np.zeros((ser_cap, 16), dtype=np.int64)
-    u64 = np.zeros((ser_cap, 5), dtype=np.uint64)
-    pod_span = np.zeros((pod_cap, 2), dtype=np.int64)
-    pod_u64 = np.zeros(pod_cap, dtype=np.uint64)
-    text = np.zeros(text_cap, dtype=np.uint8)
-    S = lib.fm_plan_rollout(blob, off.ctypes.data, N, float(step), int(window_cols), job_i32.ctypes.data,
-                            job_f64.ctypes.data, job_span.ctypes.data, f64.ctypes.data, i32.ctypes.data,
-                            span.ctypes.data, u64.ctypes.data, ser_cap, pod_span.ctypes.data, pod_u64.ctypes.data,
-                            pod_cap, text.ctypes.data, text_cap)
-    if S < 0:
+    nchunk = max(1, min(_THREADS, N // 256))
+    bounds = [N * c // nchunk for c in range(nchunk + 1)]
+
+    def run(c):
+        d0, d1 = bounds[c], bounds[c + 1]
+        o = off[8 * d0:8 * d1 + 1]
+        piece = joined[off[8 * d0]:off[8 * d1]] if nchunk > 1 else joined
+        # capacities (grown and retried if short): series <= entries of the configs, pods <=
+        # escaped pod separators + one per series and kind
+        ser_cap = max(16, piece.count("== "))
+        pod_cap = max(64, piece.count("%7C") + piece.count("|") + 2 * ser_cap)
+        text_cap = int(o[-1] - o[0]) + 1024
+        for _ in range(4):
+            got = _native_call(lib, blob, o, d1 - d0, step, window_cols, ser_cap, pod_cap, text_cap)
+            if got is not None:
+                return got
+            ser_cap, pod_cap, text_cap = 2 * ser_cap, 2 * pod_cap, 2 * text_cap
         return None
+    # the decoder releases the GIL: a deploy burst is decoded on several cores
+    outs = list(_pool().map(run, range(nchunk))) if nchunk > 1 else [run(0)]
+    if any(o is None for o in outs):
+        return None
+    oks, plans = [], []
+    for c, got in enumerate(outs):
+        ok, pl_ = _columns(got, docs[bounds[c]:bounds[c + 1]])
+        oks.append(ok)
+        plans += pl_
+    return np.concatenate(oks), plans
+
+
+_THREADS = max(1, min(8, (os.cpu_count() or 1)))
+_POOL = None
+
+
+def _pool():
+    global _POOL
+    if _POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _POOL = ThreadPoolExecutor(_THREADS, thread_name_prefix="plan")
+    return _POOL
+
+
+def _columns(got, docs: Sequence[Dict]) -> Tuple[np.ndarray, List]:
+    """PlanCols and plans of one decoded chunk."""
+    S, job_i32, job_f64, job_span, f64, i32, span, u64, pod_span, pod_u64, text = got
     tb = text.tobytes()
-    alias, fam, bfam, hfam = [], [], [], []
-    ia, ih, iff = _INTERN_A, _INTERN_H, _INTERN_F
-    ukeys = u64[:S].tolist()
-    has_b = i32[:S, 6].tolist()
-    for a, k, hb in zip(span[:S].tolist(), ukeys, has_b):
-        key = tb[a[0]:a[0] + a[1]]
-        al = ia.get(key)
-        if al is None:
-            al = ia[key] = key.decode()
-        alias.append(al)
-        hf = ih.get(k[3])
-        if hf is None:
-            hf = ih[k[3]] = (tb[a[2]:a[2] + a[3]].decode(), tb[a[4]:a[4] + a[5]].decode())
-        hfam.append(hf)
-        f = iff.get(k[1])
-        if f is None:
-            f = iff[k[1]] = (tb[a[2]:a[2] + a[3]].decode(), tb[a[10]:a[10] + a[11]].decode())
-        fam.append(f)
-        if hb:
-            b = iff.get(k[2])
-            if b is None:
-                b = iff[k[2]] = (tb[a[12]:a[12] + a[13]].decode(), tb[a[14]:a[14] + a[15]].decode())
-            bfam.append(b)
-        else:
-            bfam.append(("", ""))
-    for d in (ia, ih, iff):
+    sp = span[:S]
+
+    def interned(col: int, table: Dict, make) -> List:
+        """Per row, the interned value of its key column (one decode per distinct key)."""
+        u, first, inv = np.unique(u64[:S, col], return_index=True, return_inverse=True)
+        vals = []
+        for k, r0 in zip(u.tolist(), first.tolist()):
+            v = table.get(k)
+            if v is None:
+                v = table[k] = make(sp[r0].tolist())
+            vals.append(v)
+        return [vals[i] for i in inv.tolist()]
+
+    def st(a, k):
+        return tb[a[2 * k]:a[2 * k] + a[2 * k + 1]].decode()
+    alias = interned(5, _INTERN_A, lambda a: st(a, 0))
+    hfam = interned(3, _INTERN_H, lambda a: (st(a, 1), st(a, 2)))
+    fam = interned(1, _INTERN_F, lambda a: (st(a, 1), st(a, 5)))
+    has_b = i32[:S, 6] > 0
+    bfam = interned(2, _INTERN_F, lambda a: (st(a, 6), st(a, 7)) if a[13] or a[15] else ("", ""))
+    if not has_b.all():
+        bfam = [x if h else ("", "") for x, h in zip(bfam, has_b.tolist())]
+    for d in (_INTERN_A, _INTERN_H, _INTERN_F):
         if len(d) > 1 << 16:
             d.clear()
     Q = int(i32[S - 1, 4] + i32[S - 1, 5]) if S else 0
     cols = PlanCols(tb, f64[:S].copy(), i32[:S].copy(), u64[:S].copy(), span[:S].copy(), pod_span[:Q].copy(),
                     pod_u64[:Q].copy(), alias, fam, bfam, hfam)
-    plans: List[Optional[RolloutPlan]] = [None] * N
+    plans: List[Optional[RolloutPlan]] = [None] * len(docs)
     ok = job_i32[:, 0] == 1
     ji, jf, js = job_i32.tolist(), job_f64.tolist(), job_span.tolist()
     for d in np.nonzero(ok)[0].tolist():

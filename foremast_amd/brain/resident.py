@@ -49,13 +49,32 @@ Key = Tuple[str, str, str, str]  # (endpoint, metric, namespace, app)
 _RE2_SPECIAL = re.compile(r"([\\.^$|?*+()\[\]{}])")
 
 
+_RE2_SPECIAL_NOBAR = re.compile(r"[\\.^$?*+()\[\]{}]")
+
+
 def re_alt(values: Iterable[str]) -> str:
-    """RE2 alternation of literal label values, escaped for a PromQL string."""
-    return "|".join(_RE2_SPECIAL.sub(r"\\\\\1", v) for v in sorted(values))
+    """RE2 alternation of literal label values, escaped for a PromQL string (values
+    without RE2 metacharacters -- every k8s pod / app name without a dot -- are
+    joined as they are: one scan of the joined string instead of one per value)."""
+    vals = sorted(values)
+    joined = "|".join(vals)
+    if "|" not in "".join(vals) and _RE2_SPECIAL_NOBAR.search(joined) is None:
+        return joined
+    return "|".join(_RE2_SPECIAL.sub(r"\\\\\1", v) for v in vals)
+
+
+# urllib.parse.quote(s, safe="") as one str.translate for ASCII selectors (quote builds a
+# list of per-character strings: milliseconds for the 30 KB pod alternations of a window query)
+_QUOTE = {c: f"%{c:02X}" for c in range(128)
+          if not (chr(c).isascii() and (chr(c).isalnum() or chr(c) in "_.-~"))}
+
+
+def _quote(s: str) -> str:
+    return s.translate(_QUOTE) if s.isascii() else quote(s, safe="")
 
 
 def range_url(endpoint: str, selector: str, start: float, n: int, step: float) -> str:
-    return (f"{endpoint}query_range?query={quote(selector, safe='')}&start={int(start)}"
+    return (f"{endpoint}query_range?query={_quote(selector)}&start={int(start)}"
             f"&end={int(start + (n - 1) * step)}&step={int(step)}")
 
 

@@ -114,11 +114,16 @@ class PodSlots:
         """One reference per occurrence of each key; returns the slot of each."""
         if not len(hashes):
             return np.zeros(0, dtype=np.int64)
-        u, inv, cnt = np.unique(np.asarray(hashes, dtype=np.uint64), return_inverse=True, return_counts=True)
+        u, first, inv, cnt = np.unique(np.asarray(hashes, dtype=np.uint64), return_index=True, return_inverse=True,
+                                       return_counts=True)
         ul = u.tolist()
         idx = self.index
         slots = np.fromiter((idx.get(h, -1) for h in ul), dtype=np.int64, count=len(ul))
         new = np.nonzero(slots < 0)[0]
+        # new keys in the order they were given (jobs in admission order, pods in row order:
+        # the order the tick's bodies list them), so the native index's entries -- and its
+        # next-element predictions -- are walked sequentially by the decode
+        new = new[np.argsort(first[new], kind="stable")]
         if len(new):
             while len(self.free) < len(new):
                 old = self.cap
@@ -205,6 +210,7 @@ class RolloutMonitor:
         self.slots = PodSlots()
         self.fams: Dict[Tuple[str, str], int] = {}     # pod metric family -> index in the decode block
         self._fam_of_key: Dict[int, int] = {}          # family key (job decoder) -> index
+        self._fam_rows = np.zeros(0, dtype=np.int64)   # live rows per family
         self._blocks: Dict[Tuple[int, int], List[torch.Tensor]] = {}
         self._block_i = 0
         self._srcmap_t: Optional[torch.Tensor] = None
@@ -224,7 +230,7 @@ class RolloutMonitor:
         self._app_free: List[int] = []
         self._app_new: List[Tuple[Tuple[str, str], List[int]]] = []
         self._app_gone: List[Tuple[str, str]] = []
-        self._thr_cache: Dict[Tuple[str, str], Tuple[float, int, float]] = {}
+        self._thr_cache: Dict[int, Tuple[float, int, float]] = {}   # (alias, metric) key -> threshold
         self._n_live = 0
         self._build_grid()
         self.anomalies = None
@@ -310,6 +316,7 @@ class RolloutMonitor:
             self.row_plan[row] = None
             self.row_cols[row] = None
         self.model_ok[ra] = False
+        self._fam_count(self.row_fam[ra], -1)
         self.row_fam[ra] = -1
         self.row_slot[ra] = -1
         self.row_s[ra] = -1
@@ -496,14 +503,18 @@ class RolloutMonitor:
 
     def _set_row_params(self, b: "_Batch") -> None:
         dev = self.device
-        thr = np.empty((b.n, 3), dtype=np.float64)
+        # thresholds per (alias, metric) class: one lookup per distinct class of the batch
+        u, first, inv = np.unique(b.u64[:, 5], return_index=True, return_inverse=True)
         cache = self._thr_cache
-        for i, (al, met) in enumerate(b.alias_metric()):
-            t = cache.get((al, met))
+        tab = np.empty((len(u), 3), dtype=np.float64)
+        for k, (key, i) in enumerate(zip(u.tolist(), first.tolist())):
+            t = cache.get(key)
             if t is None:
-                c = self.cfg.for_metric(al, met)
-                t = cache[(al, met)] = (c.threshold, c.bound, c.min_lower_bound)
-            thr[i] = t
+                c, s_ = b.cols_of(i), b.s_of(i)
+                m = self.cfg.for_metric(c.alias[s_], c.hfam[s_][1])
+                t = cache[key] = (m.threshold, m.bound, m.min_lower_bound)
+            tab[k] = t
+        thr = tab[inv]
         rows = torch.from_numpy(b.rows).to(dev)
         self.threshold[rows] = torch.from_numpy(thr[:, 0].astype(np.float32)).to(dev)
         self.bound[rows] = torch.from_numpy(thr[:, 1].astype(np.int8)).to(dev)
@@ -629,20 +640,36 @@ class RolloutMonitor:
         job = np.repeat(np.arange(len(b.plans)), b.lens)      # plan index of each row
         jk = np.repeat(job, P)[valid.reshape(-1)]
         hk = H.reshape(-1)[valid.reshape(-1)]
-        # distinct (job, pod): one reference each
-        pair = np.unique(np.stack([jk.astype(np.uint64), hk]), axis=1) if len(hk) else np.zeros((2, 0), np.uint64)
-        self.slots.acquire(pair[1])
-        starts = np.searchsorted(pair[0], np.arange(len(b.plans) + 1).astype(np.uint64))
+        # distinct (job, pod): one reference each (sort by job then key, drop repeats)
+        order = np.lexsort((hk, jk))
+        jk, hk = jk[order], hk[order]
+        keep = np.ones(len(hk), dtype=bool)
+        keep[1:] = (jk[1:] != jk[:-1]) | (hk[1:] != hk[:-1])
+        jk, hk_u = jk[keep], hk[keep]
+        self.slots.acquire(hk_u)
+        starts = np.searchsorted(jk, np.arange(len(b.plans) + 1))
         for i, p in enumerate(b.plans):
-            p.pod_keys = pair[1, starts[i]:starts[i + 1]]
+            p.pod_keys = hk_u[starts[i]:starts[i + 1]]
         # slot of every (row, pod): the keys are all live now
-        u = np.asarray(sorted(set(hk.tolist())), dtype=np.uint64) if len(hk) else np.zeros(0, np.uint64)
+        u = np.unique(hk_u)
         us = np.fromiter((self.slots.index[h] for h in u.tolist()), dtype=np.int64, count=len(u))
         pos = np.searchsorted(u, H.reshape(-1)).clip(0, max(len(u) - 1, 0))
         sl = np.where(valid.reshape(-1), us[pos] if len(u) else -1, -1).reshape(b.n, P)
         self.row_slot[b.rows] = sl
-        self.row_fam[b.rows] = self._fam_index(b.u64[:, 1], b.cols_of, b.s_of)
+        fi = self._fam_index(b.u64[:, 1], b.cols_of, b.s_of)
+        self.row_fam[b.rows] = fi
+        self._fam_count(fi, +1)
         self._srcmap_dirty.append(b.rows)
+
+    def _fam_count(self, fi: np.ndarray, sign: int) -> None:
+        """Live rows per pod family (the tick queries only families with rows)."""
+        fi = fi[fi >= 0]
+        if not len(fi):
+            return
+        c = np.bincount(fi, minlength=len(self.fams))
+        if len(self._fam_rows) < len(c):
+            self._fam_rows = np.concatenate([self._fam_rows, np.zeros(len(c) - len(self._fam_rows), np.int64)])
+        self._fam_rows[:len(c)] += sign * c
 
     def _srcmap(self) -> torch.Tensor:
         """Device ``[cap * P]`` src row of every (row, pod) in the tick block viewed as
@@ -670,87 +697,100 @@ class RolloutMonitor:
 
     async def _load_windows(self, b: "_Batch") -> None:
         """Baseline windows (fixed: ``[start - W, start]``) and any current points
-        that already exist (a job claimed late), per (kind, window start): one
-        query per pod family and group of jobs, every body decoded through one
-        key index over the group's pods, then gathered into the rows."""
+        that already exist (a job claimed late), per (kind, window start, points):
+        one query per pod family and group of jobs, every body of the group decoded
+        through ONE key index over the group's pods (a family's body at its column
+        offset), then gathered into the rows.  Rows are grouped with array ops."""
         t_last = self.history.t_last
         P, Wc = self.P, self.Wc
-        # (kind, window start, points) -> batch row indices
-        groups: Dict[Tuple[str, float, int], List[int]] = {}
-        base_n = b.i32[:, 1]
-        has_b = (b.i32[:, 6] > 0) & (b.i32[:, 5] > 0) & (base_n > 0)
-        for i in np.nonzero(has_b)[0].tolist():
-            groups.setdefault(("base", float(b.f64[i, 1]), int(base_n[i])), []).append(i)
-        cur_n = b.i32[:, 0]
+        specs = []  # (dst, batch rows, start per row, n per row, family key per row, pod column)
+        hb = np.nonzero((b.i32[:, 6] > 0) & (b.i32[:, 5] > 0) & (b.i32[:, 1] > 0))[0]
+        if len(hb):
+            specs.append(("base", hb, b.f64[hb, 1], b.i32[hb, 1].astype(np.int64), b.u64[hb, 2], 4))
+        cur_n = b.i32[:, 0].astype(np.int64)
         late = np.nonzero((cur_n > 0) & (b.f64[:, 0] <= t_last))[0]
-        for i in late.tolist():
-            n = min(int(cur_n[i]), int(round((t_last - b.f64[i, 0]) / self.step)) + 1)
-            groups.setdefault(("win", float(b.f64[i, 0]), n), []).append(i)
-        if not groups:
-            return
+        if len(late):
+            n_late = np.minimum(cur_n[late], np.round((t_last - b.f64[late, 0]) / self.step).astype(np.int64) + 1)
+            specs.append(("win", late, b.f64[late, 0], n_late, b.u64[late, 1], 2))
+        for dst, idx, starts, ns_, fkeys, pc in specs:
+            # group by (start, points); families within a group by their key
+            gk = np.stack([starts.view(np.int64), ns_])
+            _, ginv = np.unique(gk, axis=1, return_inverse=True)
+            for g in range(int(ginv.max()) + 1 if len(ginv) else 0):
+                sel = idx[ginv == g]
+                start, n = float(starts[ginv == g][0]), int(ns_[ginv == g][0])
+                await self._load_group(b, dst, sel, start, n, fkeys[ginv == g], pc)
 
-        def fam_of(i, dst):
-            c, s = b.cols_of(i), b.s_of(i)
-            return c.base_fam[s] if dst == "base" else c.fam[s]
+    def _pods_strs(self, b: "_Batch", i: int, pc: int) -> Tuple[str, ...]:
+        c, s = b.cols_of(i), b.s_of(i)
+        return c.pods(int(c.i32[s, pc]), min(int(c.i32[s, pc + 1]), self.P))
 
-        def pods_of(i, dst):
+    async def _load_group(self, b: "_Batch", dst: str, sel: np.ndarray, start: float, n: int, fkeys: np.ndarray,
+                          pc: int) -> None:
+        P, Wc = self.P, self.Wc
+        H, valid = b.pod_keys(pc, sel)                         # [k, P] keys of the rows' first P pods
+        uk, inv = np.unique(H[valid], return_inverse=True)     # the group's distinct pods
+        nl = len(uk)
+        pos = np.full(H.shape, -1, dtype=np.int64)
+        pos[valid] = inv
+        ufk, fidx = np.unique(fkeys, return_inverse=True)      # families of the group
+        fams = []
+        for j in range(len(ufk)):
+            i = int(sel[np.nonzero(fidx == j)[0][0]])
             c, s = b.cols_of(i), b.s_of(i)
-            return (c.base_pods(s) if dst == "base" else c.cur_pods(s))[:P]
-
-        def pod_keys(i, dst):
-            c, s = b.cols_of(i), b.s_of(i)
-            q0, nq = (int(c.i32[s, 4]), int(c.i32[s, 5])) if dst == "base" else (int(c.i32[s, 2]), int(c.i32[s, 3]))
-            return c.pod_u64[q0:q0 + min(nq, P)]
+            fams.append(c.base_fam[s] if dst == "base" else c.fam[s])
         if self.router is not None:  # windows of other ranks' clusters: requested, not fetched
-            for key, grp in list(groups.items()):
-                dst, start, n = key
-                remote = [i for i in grp if not self.router.local(fam_of(i, dst)[0])]
-                if not remote:
-                    continue
-                groups[key] = [i for i in grp if self.router.local(fam_of(i, dst)[0])]
-                for f in dict.fromkeys(fam_of(i, dst) for i in remote):
-                    part = [(int(b.rows[i]), b.ns_of(i), pods_of(i, dst)) for i in remote if fam_of(i, dst) == f]
+            remote = np.array([not self.router.local(fams[j][0]) for j in range(len(fams))])
+            if remote.any():
+                for j in np.nonzero(remote)[0].tolist():
+                    rows_j = sel[fidx == j]
+                    part = [(int(b.rows[i]), b.ns_of(int(i)), self._pods_strs(b, int(i), pc)) for i in rows_j]
                     pods = list(dict.fromkeys((ns, pod) for _, ns, ps in part for pod in ps))
-                    self._remote.append((dst, f, start, n, part, pods))
-            groups = {k: v for k, v in groups.items() if v}
-        for (dst, start, n), grp in groups.items():
-            # every (row, pod) of the group: keys, then one index over the group's distinct pods
-            keys = [pod_keys(i, dst) for i in grp]
-            allk = np.concatenate(keys) if keys else np.zeros(0, np.uint64)
-            uk, inv = np.unique(allk, return_inverse=True)
-            nl = len(uk)
-            fams = list(dict.fromkeys(fam_of(i, dst) for i in grp))
-            fidx = {f: j for j, f in enumerate(fams)}
-            rowfam = np.array([fidx[fam_of(i, dst)] for i in grp], dtype=np.int64)
-            block_t = torch.full((len(fams) * nl, Wc), float("nan"), dtype=torch.float32)
-            if self.gpu:
-                block_t = block_t.pin_memory()
-            tables = {f: native.KeyTable.indexed(uk, j * nl + np.arange(nl), "namespace", "pod")
-                      for f, j in fidx.items()}
-            reqs, tabs = [], []
-            for f in fams:
-                mine = [i for i in grp if fam_of(i, dst) == f]
-                for g in range(0, len(mine), self.apps_per_query):
-                    part = mine[g:g + self.apps_per_query]
-                    sel = (f'{f[1]}{{namespace=~"{re_alt({b.ns_of(i) for i in part})}",'
-                           f'pod=~"{re_alt({pod for i in part for pod in pods_of(i, dst)})}"}}')
-                    reqs.append((range_url(f[0], sel, start, n, self.step), start, n, 0))
-                    tabs.append(tables[f])
-            ok = await fetch_decode(self.prom, reqs, tabs, block_t.numpy(), self.step, self.decode_threads)
-            if not all(ok):
-                log.warning("%d of %d window queries failed (%s from %d)", ok.count(False), len(ok), dst, start)
-            # gather map: (group row, pod) -> block row
-            lens = np.array([len(k) for k in keys], dtype=np.int64)
-            gidx = np.full((len(grp), P), -1, dtype=np.int64)
-            rr = np.repeat(np.arange(len(grp)), lens)
-            cc = np.arange(len(allk)) - np.repeat(np.cumsum(lens) - lens, lens)
-            gidx[rr, cc] = rowfam[rr] * nl + inv
-            blk = block_t.to(self.device, non_blocking=True)
-            gi = torch.from_numpy(gidx).to(self.device)
-            vals = blk[gi.clamp(min=0)]                       # [k, P, Wc]
-            vals = torch.where((gi >= 0)[:, :, None], vals, torch.full_like(vals, float("nan")))
-            rows = torch.from_numpy(b.rows[np.asarray(grp, dtype=np.int64)]).to(self.device)
-            (self.base if dst == "base" else self.win).index_copy_(0, rows, vals.reshape(len(grp), P * Wc))
+                    self._remote.append((dst, fams[j], start, n, part, pods))
+                keep = ~remote[fidx]
+                if not keep.any():
+                    return
+                return await self._load_group(b, dst, sel[keep], start, n, fkeys[keep], pc)
+        F = len(fams)
+        block_t = torch.full((max(nl, 1), F * Wc), float("nan"), dtype=torch.float32)
+        if self.gpu:
+            block_t = block_t.pin_memory()
+        index = native.KeyTable.indexed(uk, np.arange(nl, dtype=np.int64), "namespace", "pod")
+        reqs = []
+        base = dst == "base"
+        for j, f in enumerate(fams):
+            mine = sel[fidx == j]
+            for g0 in range(0, len(mine), self.apps_per_query):
+                chunk = mine[g0:g0 + self.apps_per_query]
+                nss, alts, loose = set(), set(), set()
+                pk, ss = b._part_of[chunk], b.s[chunk]
+                for k in np.unique(pk).tolist():
+                    cols = b.parts[k][0]
+                    for s_ in ss[pk == k].tolist():
+                        nss.add(cols.ns_at(s_))
+                        alt = cols.pods_alt(s_, base)
+                        if alt:                 # the job decoder's "a|b|c" of the row's pods
+                            alts.add(alt)
+                        else:                   # rows of the Python parser
+                            loose.update((cols.base_pods(s_) if base else cols.cur_pods(s_))[:P])
+                pod_re = b"|".join(sorted(alts)).decode()
+                if "." in pod_re:  # the one RE2 metacharacter a plain pod name can hold
+                    pod_re = pod_re.replace(".", "\\\\.")
+                if loose:
+                    pod_re = "|".join(x for x in (pod_re, re_alt(loose)) if x)
+                q = f'{f[1]}{{namespace=~"{re_alt(nss)}",pod=~"{pod_re}"}}'
+                reqs.append((range_url(f[0], q, start, n, self.step), start, n, j * Wc))
+        ok = await fetch_decode(self.prom, reqs, [index] * len(reqs), block_t.numpy(), self.step,
+                                self.decode_threads)
+        if not all(ok):
+            log.warning("%d of %d window queries failed (%s from %d)", ok.count(False), len(ok), dst, start)
+        # gather: (group row, pod) -> block[pod, family]
+        blk = block_t.to(self.device, non_blocking=True).view(max(nl, 1) * F, Wc)
+        gi = torch.from_numpy(np.where(pos >= 0, pos * F + fidx[:, None], -1)).to(self.device)
+        vals = blk[gi.clamp(min=0)]                            # [k, P, Wc]
+        vals = torch.where((gi >= 0)[:, :, None], vals, torch.full_like(vals, float("nan")))
+        rows = torch.from_numpy(b.rows[sel]).to(self.device)
+        (self.base if dst == "base" else self.win).index_copy_(0, rows, vals.reshape(len(sel), P * Wc))
 
     async def _serve_windows(self, requests) -> List[np.ndarray]:
         """Fetch + decode window requests of this rank's clusters (cluster-affine mode)."""
@@ -814,13 +854,14 @@ class RolloutMonitor:
         P = self.P
         F = max(1, len(self.fams))
         S = self.slots.cap
+        t0 = time.perf_counter()
         srcmap = self._srcmap()
         # the tick block is [slot, family x minute]: ONE pod index serves every family's body
         block_t, block = self._tick_block(S, F * k)
+        self.timings["ingest_prep_ms"] = (time.perf_counter() - t0) * 1e3
         self.timings["points"] = k
         index = self.slots.table(F)
-        used = {int(f) for f in np.unique(self.row_fam[self.row_fam >= 0]).tolist()}
-        fams = [(fam, fi) for fam, fi in self.fams.items() if fi in used]
+        fams = [(fam, fi) for fam, fi in self.fams.items() if fi < len(self._fam_rows) and self._fam_rows[fi] > 0]
         reqs = [(range_url(fam[0], fam[1], first, k, self.step), first, k, fi * k) for fam, fi in fams]
         self.tick_queries += len(reqs)
         t0 = time.perf_counter()
@@ -1026,18 +1067,25 @@ class RolloutMonitor:
                                                    "values": vals}
                 self._last_anom[row] = pts[-1][0] if pts else now
             finish[jid] = (r.ST_COMPLETED_UNHEALTH, "anomaly detected in " + ",".join(sorted(anomaly)), anomaly)
+        ending = []
         while self._ends and self._ends[0][0] <= now:
             _, jid = heapq.heappop(self._ends)
             p = self.jobs.get(jid)
-            if p is None or jid in finish:
-                continue
-            seen = bool(npts[p.rows].sum() > 0)
-            if seen and bool(self.model_ok[p.rows].any()):
-                finish[jid] = (r.ST_COMPLETED_HEALTH, "", None)
-            elif seen:
-                finish[jid] = (r.ST_COMPLETED_UNKNOWN, "missing historical data", None)
-            else:
-                finish[jid] = (r.ST_COMPLETED_UNKNOWN, "no current metric data", None)
+            if p is not None and jid not in finish:
+                ending.append(p)
+        if ending:  # past endTime: seen / model checks over every ending job's rows at once
+            rr = np.fromiter((row for p in ending for row in p.rows), dtype=np.int64)
+            lens = np.fromiter((len(p.rows) for p in ending), dtype=np.int64, count=len(ending))
+            starts = np.concatenate([[0], np.cumsum(lens)[:-1]])
+            seen = np.add.reduceat((npts[rr] > 0).astype(np.int64), starts) > 0
+            mok = np.add.reduceat(self.model_ok[rr].astype(np.int64), starts) > 0
+            for p, sn, mk in zip(ending, seen.tolist(), mok.tolist()):
+                if sn and mk:
+                    finish[p.doc_id] = (r.ST_COMPLETED_HEALTH, "", None)
+                elif sn:
+                    finish[p.doc_id] = (r.ST_COMPLETED_UNKNOWN, "missing historical data", None)
+                else:
+                    finish[p.doc_id] = (r.ST_COMPLETED_UNKNOWN, "no current metric data", None)
         if not finish:
             return {}
         items = []
@@ -1050,29 +1098,43 @@ class RolloutMonitor:
             items.append((jid, fields))
         res = self.store.update_many(items, expect_claimed_by=self.worker_id)
         written = {}
-        freed: List[int] = []  # every finished job's rows, released in ONE batch of device fills
-        gone_keys: List[np.ndarray] = []
-        up, lo, _ = self._bands
-        done = self._done_bands
+        counts: Dict[str, int] = {}
+        done_plans: List[RolloutPlan] = []
         for (jid, fields), ok in zip(items, res):
             if ok:
-                self.metrics.jobs.labels(status=fields["status"]).inc()
+                counts[fields["status"]] = counts.get(fields["status"], 0) + 1
                 written[jid] = fields["status"]
             p = self.jobs.pop(jid, None)
-            if p is None:
-                continue
-            hk = p.cols.u64[p.s0:p.s0 + p.n, 0].tolist()
-            for k, (row, h) in enumerate(zip(p.rows, hk)):  # the finished job's last band stays exported
-                if row < len(up) and up[row] == up[row]:
-                    done[h] = (p.cols, p.s0 + k, float(up[row]), float(lo[row]), self._last_anom.pop(row, None))
-            self.history.unwant_h(hk, now)
-            freed += p.rows
-            gone_keys.append(p.pod_keys)
-            self._app_ref(p, -1)
-        if gone_keys:
-            self.slots.release(np.concatenate(gone_keys))
-        self._free_rows(freed)
+            if p is not None:
+                done_plans.append(p)
+                self._app_ref(p, -1)
+        for st, n in counts.items():
+            self.metrics.jobs.labels(status=st).inc(n)
+        if done_plans:
+            self._retire(done_plans, now)
         return written
+
+    def _retire(self, plans: List[RolloutPlan], now: float) -> None:
+        """Release the finished jobs' rows, pod slots and history references in batches;
+        their last bands stay exported (read at scrape time)."""
+        up, lo, _ = self._bands
+        freed = np.fromiter((row for p in plans for row in p.rows), dtype=np.int64)
+        hk = np.concatenate([p.cols.u64[p.s0:p.s0 + p.n, 0] for p in plans])
+        srow = np.concatenate([np.arange(p.s0, p.s0 + p.n) for p in plans])
+        cols = [p.cols for p in plans for _ in range(p.n)]
+        if len(up) >= self.cap and len(freed):
+            u, l_ = up[freed], lo[freed]
+            ok = ~np.isnan(u)
+            done, la = self._done_bands, self._last_anom
+            for h, c, s, uu, ll, row in zip(hk[ok].tolist(), [c for c, k in zip(cols, ok) if k], srow[ok].tolist(),
+                                            u[ok].tolist(), l_[ok].tolist(), freed[ok].tolist()):
+                done[h] = (c, s, uu, ll, la.pop(row, None))
+        if self._last_anom:
+            for row in freed.tolist():
+                self._last_anom.pop(row, None)
+        self.history.unwant_h(hk.tolist(), now)
+        self.slots.release(np.concatenate([p.pod_keys for p in plans]))
+        self._free_rows(freed.tolist())
 
     # ------------------------------------------------------------------ node integration
     def app_table(self) -> Tuple[List[Optional[Tuple[str, str]]], torch.Tensor]:
@@ -1148,17 +1210,33 @@ class _Batch:
             for s in self.s[lo:hi].tolist():
                 yield cols.alias[s], cols.hfam[s][1]
 
-    def cur_pod_keys(self) -> Tuple[np.ndarray, np.ndarray]:
-        """``[n, P]`` keys of each row's first P current pods and the valid mask."""
+    def pod_keys(self, pc: int = 2, sel: Optional[np.ndarray] = None) -> Tuple[np.ndarray, np.ndarray]:
+        """``[n, P]`` keys of each row's first P pods (``pc`` 2: current, 4: baseline)
+        and the valid mask; ``sel``: only these batch rows."""
         P = self.P
-        H = np.zeros((self.n, P), dtype=np.uint64)
-        valid = np.zeros((self.n, P), dtype=bool)
+        sel = np.arange(self.n) if sel is None else np.asarray(sel, dtype=np.int64)
+        H = np.zeros((len(sel), P), dtype=np.uint64)
+        valid = np.zeros((len(sel), P), dtype=bool)
         K = np.arange(P)[None, :]
-        for cols, lo, hi in self.parts:
-            q0 = self.i32[lo:hi, 2].astype(np.int64)[:, None]
-            nq = np.minimum(self.i32[lo:hi, 3], P)[:, None]
+        part = self._part_of[sel]
+        for k, (cols, _lo, _hi) in enumerate(self.parts):
+            m = np.nonzero(part == k)[0]
+            if not len(m):
+                continue
+            rows = sel[m]
+            q0 = self.i32[rows, pc].astype(np.int64)[:, None]
+            nq = np.minimum(self.i32[rows, pc + 1], P)[:, None]
             v = K < nq
             idx = np.where(v, q0 + K, 0)
-            H[lo:hi] = np.where(v, cols.pod_u64[idx] if len(cols.pod_u64) else 0, 0)
-            valid[lo:hi] = v
+            H[m] = np.where(v, cols.pod_u64[idx] if len(cols.pod_u64) else 0, 0)
+            valid[m] = v
         return H, valid
+
+    def cur_pod_keys(self) -> Tuple[np.ndarray, np.ndarray]:
+        return self.pod_keys(2)
+
+    def pod_key_bytes(self, i: int, pc: int) -> bytes:
+        """Identity of a row's first P pods (its pod keys), for caching their names."""
+        c, s = self.cols_of(i), self.s_of(i)
+        q0, nq = int(c.i32[s, pc]), min(int(c.i32[s, pc + 1]), self.P)
+        return c.pod_u64[q0:q0 + nq].tobytes()

@@ -360,6 +360,16 @@ struct Out {
     used += (long long)s.n;
     return off;
   }
+  // "a|b|c": the pods as one RE2 alternation (plain names: no metacharacters but '.')
+  long long put_join(const std::vector<Span>& v, long long& len) {
+    const long long off = used;
+    for (size_t i = 0; i < v.size(); ++i) {
+      if (i) put(Span{"|", 1});
+      put(v[i]);
+    }
+    len = used - off;
+    return off;
+  }
 };
 
 inline uint64_t key2(Span a, Span b) { return fm_series_key(a.p, a.p + a.n, b.p, b.p + b.n); }
@@ -388,10 +398,11 @@ inline double pyround(double x) { return std::nearbyint(x); }  // round-half-eve
 //   ser_f64[s] = {cur_start, base_start, hist_end}
 //   ser_i32[s] = {cur_n, base_n, cur pod0, cur npod, base pod0, base npod, has_base}
 //   ser_span[s] = {alias, hist endpoint, hist metric, hist namespace, hist app, cur metric,
-//                  base endpoint, base metric} as (off, len) pairs
+//                  base endpoint, base metric, cur pods "a|b", base pods "c|d"} as (off, len) pairs
 //   ser_u64[s] = {history key (endpoint\x1fmetric, namespace\x1fapp), family key
 //                 (endpoint, cur metric), baseline family key (0 without baseline),
-//                 history family key (endpoint, hist metric), app key (namespace, app)}
+//                 history family key (endpoint, hist metric), app key (namespace, app),
+//                 alias key (alias, hist metric): the threshold class of the row}
 // per pod p: pod_span[p] = (off, len), pod_u64[p] = series_key(namespace, pod).
 // Returns the number of series rows, or -1 when an output capacity was too small.
 extern "C" long long fm_plan_rollout(const char* blob, const long long* str_off, long long n_docs, double step,
@@ -503,8 +514,8 @@ extern "C" long long fm_plan_rollout(const char* blob, const long long* str_off,
       const long long s = ns_rows++;
       double* sf = ser_f64 + 3 * s;
       int* si = ser_i32 + 7 * s;
-      long long* ss = ser_span + 16 * s;
-      uint64_t* su = ser_u64 + 5 * s;
+      long long* ss = ser_span + 20 * s;
+      uint64_t* su = ser_u64 + 6 * s;
       sf[0] = gc.start;
       sf[1] = b_start;
       sf[2] = gh.end;
@@ -533,11 +544,14 @@ extern "C" long long fm_plan_rollout(const char* blob, const long long* str_off,
         ss[2 * k] = out.put(parts[k]);
         ss[2 * k + 1] = (long long)parts[k].n;
       }
+      ss[16] = out.put_join(pc, ss[17]);
+      ss[18] = out.put_join(pb, ss[19]);
       su[0] = key4(gh.ep, nh, hns, happ);
       su[1] = key2(gc.ep, nc);
       su[2] = be ? key2(gb.ep, nb) : 0;
       su[3] = key2(gh.ep, nh);
       su[4] = key2(hns, happ);
+      su[5] = key2(alias, nh);
     }
     if (out.overflow) return -1;
     if (!ok) {  // roll this document back: Python plans it

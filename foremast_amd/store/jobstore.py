@@ -169,10 +169,27 @@ def _filter(cand: List[Dict[str, Any]], only, only_batch) -> List[Dict[str, Any]
     return cand
 
 
+_STAMP_CACHE: Dict[float, str] = {}
+
+
+def _flat_copy(fields: Dict[str, Any]) -> Dict[str, Any]:
+    """A copy that shares nothing mutable: job documents are flat (str / number
+    values), so a dict copy suffices; nested values are deep-copied."""
+    if all(isinstance(v, (str, int, float, bool, type(None))) for v in fields.values()):
+        return dict(fields)
+    return copy.deepcopy(fields)
+
+
 def _stamp(d: Dict[str, Any], fields: Dict[str, Any]) -> None:
     d.update(fields)
-    d["modified_ts"] = fields.get("modified_ts", time.time())
-    d["modified_at"] = format_rfc3339_nano(d["modified_ts"])
+    ts = fields.get("modified_ts", time.time())
+    d["modified_ts"] = ts
+    at = _STAMP_CACHE.get(ts)
+    if at is None:  # a tick's writes share one timestamp: format it once
+        if len(_STAMP_CACHE) > 64:
+            _STAMP_CACHE.clear()
+        at = _STAMP_CACHE[ts] = format_rfc3339_nano(ts)
+    d["modified_at"] = at
 
 
 class MemoryJobStore(JobStore):
@@ -230,7 +247,7 @@ class MemoryJobStore(JobStore):
         if expect_claimed_by is not None and d.get("claimed_by") != expect_claimed_by:
             return False
         before = (d.get("status"), d.get("claimed_by"))
-        _stamp(d, copy.deepcopy(fields))
+        _stamp(d, _flat_copy(fields))
         self._index(d, before)
         return True
 
