@@ -118,9 +118,20 @@ class NodeBrain:
         cluster-affine mode — by the cluster of the job's new pods."""
         return m.owns_affine if getattr(m, "router", None) is not None else self.owns
 
+    def _suffixes(self) -> Set[str]:
+        """Worker-id suffixes of this rank's monitors (``node-<member>`` + "", "-rollout",
+        "-lstm"): a dead member's leases are held under each of them."""
+        base = worker_id_of(self.world.id) if self.world is not None else ""
+        out = {""}
+        for m in self.monitors:
+            wid = getattr(m, "worker_id", "")
+            if base and wid.startswith(base):
+                out.add(wid[len(base):])
+        return out
+
     def _after_reform(self, before: List[str]) -> None:
         gone = set(before) - set(self.world.members)
-        self.dead |= {worker_id_of(m) for m in gone}
+        self.dead |= {worker_id_of(m) + sfx for m in gone for sfx in self._suffixes()}
         moved = sum(m.release(lambda d, o=self._owns_for(m): not o(d)) for m in self.monitors)
         for m in self.monitors:
             if hasattr(m, "after_reform"):

@@ -1,0 +1,165 @@
+"""The product path at N ranks equals the product path at one rank.
+
+Canary jobs are registered through the service into ONE shared SQLite job
+store; N rank processes (gloo, ElasticWorld) each run the production node brain
+(streaming + rollout monitors) with app ownership by ``owner_of`` over the
+members, against the same deterministic fake Prometheus and a lockstep virtual
+clock.  The final job statuses, anomaly payloads and anomalous-app sets must be
+identical for N = 1, 2, 4, 8 (reference design: shared-nothing brains meeting in
+the job table, ``docs/guides/design.md:37-41``).  A second test freezes one rank
+inside a tick (SIGSTOP), then kills it: the survivors re-form and finish every
+one of its jobs with the statuses of the undisturbed run (takeover,
+``deploy/foremast/3_brain/foremast-brain.yaml:80-81`` — here at re-formation
+instead of after 90 s)."""
+
+import datetime
+import json
+import os
+import signal
+import subprocess
+import sys
+import time
+
+import pytest
+
+from foremast_amd.api import crd
+from foremast_amd.api import rest as r
+from foremast_amd.controller import queries
+from foremast_amd.promql import synth
+from foremast_amd.promql.fake import FakePrometheus
+from foremast_amd.utils.config import BrainConfig, reference_default_env
+from foremast_amd.utils.timeutil import format_rfc3339
+
+T0 = 1_700_000_040.0
+EP = "http://prometheus:9090/api/v1/"
+NS = "ns"
+METRICS = (("http_server_requests_error_5xx", "error5xx"), ("http_server_requests_latency", "latency"))
+APPS = [f"app{i}" for i in range(12)]
+SPIKED = {"app2", "app7", "app9"}
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HELPER = os.path.join(ROOT, "tests", "helpers", "node_rank.py")
+TICKS = 13
+
+
+def config() -> BrainConfig:
+    env = reference_default_env()
+    env.update(MIN_HISTORICAL_DATA_POINT_TO_MEASURE="10", threshold0="4", threshold1="4",
+               ML_ALGORITHM="moving_average_all")
+    cfg = BrainConfig.from_env(env)
+    cfg.ring_len = 1440
+    return cfg
+
+
+def pods(app):
+    return [f"{app}-v2-{k}" for k in range(2)], [f"{app}-v1-{k}" for k in range(3)]
+
+
+def world_prometheus(clock) -> FakePrometheus:
+    """Every series a function of (app, metric, pod): identical on every rank."""
+    prom = FakePrometheus(clock=clock)
+    for i, app in enumerate(APPS):
+        new, old = pods(app)
+        for j, (m, _a) in enumerate(METRICS):
+            base = 0.3 + 0.05 * i + j
+            prom.add("namespace_app_per_pod:" + m, {"namespace": NS, "app": app},
+                     synth.error_rate(base=base, spread=0.05, seed=100 * i + j))
+            for k, pod in enumerate(new + old):
+                gen = synth.error_rate(base=base, spread=0.05, seed=10_000 + 100 * i + 10 * j + k)
+                if app in SPIKED and pod in new and j == 0:
+                    gen = synth.step_change(gen, at=T0 + 60 * (3 + i % 4), factor=0.0, add=40.0)
+                prom.add("namespace_pod:" + m, {"namespace": NS, "pod": pod}, gen)
+    return prom
+
+
+def request(app):
+    mets = crd.Metrics(data_source_type="prometheus", endpoint=EP,
+                       monitoring=[crd.Monitoring(metric_name=m, metric_alias=a) for m, a in METRICS])
+    info = queries.create_metrics_info(NS, app, list(pods(app)), mets, 10, "canary", now=T0)
+    return r.ApplicationHealthAnalyzeRequest(app_name=app, start_time=format_rfc3339(T0),
+                                             end_time=format_rfc3339(T0 + 600), metrics=info,
+                                             strategy="canary").to_dict()
+
+
+def run_node(tmp_path, n, stop=None, hb=3.0):
+    """Register the jobs, run n ranks for TICKS ticks; returns (statuses, per-rank lines)."""
+    import torch.distributed as dist
+    from foremast_amd.service import app as svc
+    from foremast_amd.store.jobstore import SqliteJobStore
+    db = str(tmp_path / f"jobs{n}.db")
+    store = SqliteJobStore(db)
+    ids = {a: svc.register(store, request(a))[1]["jobId"] for a in APPS}
+    kv = dist.TCPStore("127.0.0.1", 0, is_master=True, wait_for_workers=False, timeout=datetime.timedelta(seconds=90))
+    procs, outs = [], []
+    for i in range(n):
+        out = tmp_path / f"n{n}_rank{i}.jsonl"
+        env = dict(os.environ, OMP_NUM_THREADS="1", CUDA_VISIBLE_DEVICES="", GLOO_SOCKET_IFNAME="lo")
+        if stop is not None and i == stop[0]:
+            env["NODE_RANK_STOP_AT"] = str(stop[1])
+        procs.append(subprocess.Popen([sys.executable, HELPER, str(kv.port), str(i), str(n), db, str(out),
+                                       str(TICKS), str(hb)], env=env, cwd=ROOT, stderr=subprocess.PIPE, text=True))
+        outs.append(out)
+    try:
+        if stop is not None:
+            victim = procs[stop[0]]
+            t_end = time.time() + 180
+            while time.time() < t_end:
+                with open(f"/proc/{victim.pid}/stat") as f:
+                    if f.read().split(") ", 1)[1].split()[0] == "T":
+                        break
+                time.sleep(0.05)
+            else:
+                raise AssertionError("victim never reached its fault point")
+            time.sleep(1.0)
+            victim.send_signal(signal.SIGKILL)
+            victim.wait()
+        errs = []
+        for i, p in enumerate(procs):
+            if stop is not None and i == stop[0]:
+                continue
+            _, err = p.communicate(timeout=600)
+            errs.append(err)
+            assert p.returncode == 0, err[-4000:]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    lines = [[json.loads(x) for x in o.read_text().splitlines()] if o.exists() else [] for o in outs]
+    docs = {a: store.get(j) for a, j in ids.items()}
+    return docs, lines
+
+
+def verdicts(docs):
+    out = {}
+    for a, d in docs.items():
+        info = json.loads(d["anomalyInfo"]) if d.get("anomalyInfo") else {}
+        out[a] = (d["status"], {k: v["values"] for k, v in info.items()})
+    return out
+
+
+@pytest.mark.slow
+def test_node_product_n_rank_equals_one_rank(tmp_path):
+    ref_docs, ref_lines = run_node(tmp_path, 1)
+    ref = verdicts(ref_docs)
+    assert {a for a, (st, _) in ref.items() if st == r.ST_COMPLETED_UNHEALTH} == SPIKED
+    assert all(st == r.ST_COMPLETED_HEALTH for a, (st, _) in ref.items() if a not in SPIKED)
+    ref_anom = [sorted(x["anomalous"]) for x in ref_lines[0]]
+    for n in (2, 4, 8):
+        docs, lines = run_node(tmp_path, n)
+        assert verdicts(docs) == ref, n
+        # the node table names the same anomalous apps on every tick, on every rank
+        for rank_lines in lines:
+            assert [sorted(x["anomalous"]) for x in rank_lines] == ref_anom, n
+        # every job was held by exactly one rank
+        for k in range(TICKS):
+            held = [j for ls in lines for j in ls[k]["jobs"]]
+            assert len(held) == len(set(held)), (n, k)
+
+
+@pytest.mark.slow
+def test_node_product_rank_killed_mid_tick_survivors_finish(tmp_path):
+    ref = verdicts(run_node(tmp_path, 1)[0])
+    docs, lines = run_node(tmp_path, 3, stop=(1, 4))
+    got = verdicts(docs)
+    assert got == ref
+    survivors = [ls for i, ls in enumerate(lines) if i != 1]
+    assert all(ls[-1]["generation"] >= 1 and len(ls[-1]["members"]) == 2 for ls in survivors)
