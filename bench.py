@@ -329,23 +329,32 @@ def setup_canary(args, world, rank, dev):
     truth_apps = sorted(set(((bad.cpu() + s) // METRICS_PER_APP).tolist()))
     exch = None
     if args.multi_cluster:
-        # this rank scrapes the baseline pods of the neighbour's shard
-        from foremast_amd.parallel import canary
-        r_ids = canary.remote_baseline_ids(args.series, world, rank, align=METRICS_PER_APP).to(dev)
-        r0 = int(r_ids[0]) if r_ids.numel() else 0
-        r_params = synthetic_params(args.series, dev, seed=1234, rows=(r0, r0 + int(r_ids.numel())))
+        # each rank scrapes ONE cluster: rank r's canaries run in cluster r, their baselines in
+        # cluster r-1, whose rank decodes them and ships them through the product's ClusterRouter
+        # (parallel/affine.py: published requests, one all_to_all per tick)
+        import asyncio
+        from foremast_amd.parallel.affine import ClusterRouter
+        served = (rank + 1) % world               # this rank's cluster holds the baselines of that shard
+        r0, r1, _ = shard_range(args.series, world, served, METRICS_PER_APP)
+        r_params = synthetic_params(args.series, dev, seed=1234, rows=(r0, r1))
         base_t = make_ticks(r_params, P, total_ticks + W, args.season, args.ring, 7, 0.0, row0=r0,
                             n_global=args.series)
-        owner = canary.owner_of(r_ids, canary.shard_starts(args.series, world, METRICS_PER_APP, dev))
-        exch = canary.WindowExchanger(r_ids, owner, P)
-        local_rows = (exch.recv_ids - s).long()
-        if int(local_rows.numel()) != n_local:
-            raise RuntimeError("multi-cluster exchange does not cover the shard")
+        router = ClusterRouter(lambda ep, w: int(ep[len("cluster"):]) % w, dev)
+        loop = asyncio.new_event_loop()
+        family = (f"cluster{(rank - 1) % world}", "namespace_pod:baseline")
+        shard_pod = [("bench", f"shard{rank}")]
+
+        async def serve(reqs):
+            # every request for this cluster's baselines comes from the shard it holds
+            return [base_host[int(q[1])].reshape(1, -1).numpy() for q in reqs]
+
+        def exch(k):
+            (vals,) = loop.run_until_complete(router.exchange([(family, float(k), n_local * P, shard_pod)], serve))
+            return torch.from_numpy(vals).view(n_local, P)
         ticks = cur_t
         base_host = base_t.cpu()
         if dev.type == "cuda":
             base_host = base_host.pin_memory()
-        base_dev = torch.empty((base_t.shape[1], P), dtype=torch.float32, device=dev)
         del base_t
     else:
         base_t = make_ticks(params, P, total_ticks + W, args.season, args.ring, 7, 0.0, row0=s, n_global=args.series)
@@ -425,8 +434,7 @@ def setup_canary(args, world, rank, dev):
             return
         newvb.copy_(host_ticks[k], non_blocking=pin)
         if exch is not None:
-            base_dev.copy_(base_host[k], non_blocking=pin)
-            newb.index_copy_(0, local_rows, exch(base_dev))  # RC5: baseline windows to their owners
+            newb.copy_(exch(k), non_blocking=pin)  # RC5: baseline windows to their owners
     # host copy of the node health table (fused: the whole gathered record buffer)
     health_src = agg.recv if agg.fused else shard.app_stats
     # two host copies of the node health table: tick k+1's D2H may be enqueued while the
@@ -477,6 +485,7 @@ def setup_canary(args, world, rank, dev):
         "current_window": W,
         "grid_points": int(shard.grid.shape[0]),
         "multi_cluster": bool(args.multi_cluster),
+        "affine_exchanges": router.exchanges if args.multi_cluster else 0,
         "gap_frac": args.gap_frac,
         "pairwise_shift_sigma": cfg.pairwise_shift,
         "health_collectives": "1 fused all_gather" if agg.fused else ("all_reduce + all_gather" if agg.active else "none"),
