@@ -943,6 +943,9 @@ def main():
                 "tick_total_ms_p50_p99_max": [pct("tick_total_ms", 50), pct("tick_total_ms", 99),
                                               pct("tick_total_ms", 100)],
                 "intake_ms_p50_p99_max": [pct("intake_ms", 50), pct("intake_ms", 99), pct("intake_ms", 100)],
+                # the same phases without the in-process Prometheus stand-in's own serving time
+                "net_of_standin": {k: [pct(k, 50), pct(k, 99), pct(k, 100)]
+                                   for k in ("detect_net_ms", "intake_net_ms", "tick_net_ms")},
                 "admitted_per_tick_mean": round(float(np.mean([b.get("admitted", 0) for b in bds])), 1) if bds else 0,
                 "admission_ms_p50": {k: (round(float(np.percentile([b.get(k, 0.0) for b in adm], 50)), 3)
                                          if adm else None)

@@ -361,11 +361,20 @@ class ArrivalServer:
         self.requests = 0
         self.bytes_served = 0
         self.serve_s = 0.0
+        self.serve_tick_s = 0.0     # the tick's family bodies (scoring half)
+        self.serve_window_s = 0.0   # selector queries: baseline windows of admissions (intake half)
 
     async def fetch_raw_many(self, urls) -> List[object]:
-        t0 = time.perf_counter()
-        out = [self._one(u) for u in urls]
-        self.serve_s += time.perf_counter() - t0
+        out = []
+        for u in urls:
+            t0 = time.perf_counter()
+            out.append(self._one(u))
+            dt = time.perf_counter() - t0
+            self.serve_s += dt
+            if "%7B" in u:
+                self.serve_window_s += dt
+            else:
+                self.serve_tick_s += dt
         return out
 
     def _one(self, url: str):
@@ -565,7 +574,7 @@ def setup_arrival(args, world, rank, dev):
         n_rows = roll.n_live
         gc_pause["t"], gc_pause["n"] = 0.0, 0
         gc.callbacks.append(_gc_cb)
-        serve0 = server.serve_s
+        serve0, st0, sw0 = server.serve_s, server.serve_tick_s, server.serve_window_s
         t0 = time.perf_counter()
         try:
             table = loop.run_until_complete(node.tick())
@@ -578,6 +587,13 @@ def setup_arrival(args, world, rank, dev):
         bd.update({kk: round(v, 3) for kk, v in node.timings.items()})
         bd["tick_total_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
         bd["prometheus_standin_ms"] = round((server.serve_s - serve0) * 1e3, 3)
+        # the stand-in runs inside this process: the brain's own time is the phase minus its share
+        st_ms, sw_ms = (server.serve_tick_s - st0) * 1e3, (server.serve_window_s - sw0) * 1e3
+        if "detect_ms" in bd:
+            bd["detect_net_ms"] = round(bd["detect_ms"] - st_ms, 3)
+        if "intake_ms" in bd:
+            bd["intake_net_ms"] = round(bd["intake_ms"] - sw_ms, 3)
+        bd["tick_net_ms"] = round(bd["tick_total_ms"] - st_ms - sw_ms, 3)
         bd["live_rows"] = roll.n_live
         bd["gc_ms"], bd["gc_runs"] = round(gc_pause["t"] * 1e3, 2), gc_pause["n"]
         breakdowns.append(bd)

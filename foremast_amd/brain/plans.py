@@ -189,15 +189,16 @@ def hkey_hash(k: Key) -> int:
 class RolloutPlan:
     """A job's plan: its series are rows ``[s0, s0 + n)`` of ``cols``."""
 
-    __slots__ = ("doc_id", "app", "end_ts", "doc", "rows", "cols", "s0", "n", "pod_keys", "_series")
+    __slots__ = ("doc_id", "app", "end_ts", "doc", "rows", "cols", "s0", "n", "pod_keys", "_series", "jslot")
 
     def __init__(self, doc_id: str, app: Tuple[str, str], end_ts: float, cols: PlanCols, s0: int, n: int,
                  doc: Optional[Dict] = None) -> None:
         self.doc_id, self.app, self.end_ts = doc_id, app, end_ts
         self.cols, self.s0, self.n = cols, s0, n
         self.doc: Dict = doc if doc is not None else {}
-        self.rows: List[int] = []
+        self.rows = np.zeros(0, dtype=np.int64)        # table rows of the admitted job's series
         self.pod_keys = np.zeros(0, dtype=np.uint64)   # pod slots the admitted job holds
+        self.jslot = -1                                # the admitted job's slot in the engine's job table
         self._series: Optional[List[RolloutSeries]] = None
 
     @property

@@ -52,6 +52,7 @@ algorithms) stay with :class:`~foremast_amd.brain.worker.BrainWorker`
 
 from __future__ import annotations
 
+import collections
 import heapq
 import json
 import logging
@@ -73,7 +74,7 @@ from ..utils.config import BrainConfig
 from ..utils.metrics import BrainMetrics
 from . import plans as pl
 from .plans import ALGORITHMS, STRATEGIES, PlanCols, RolloutPlan, RolloutSeries  # noqa: F401 (re-exported)
-from .resident import Key, ResidentHistory, fetch_decode, range_url, re_alt
+from .resident import Key, ResidentHistory, fetch_decode, quote_selector, range_url, range_url_quoted, re_alt
 
 log = logging.getLogger("foremast.rollout")
 
@@ -94,21 +95,32 @@ class PodSlots:
     """``(namespace, pod)`` key -> slot: a pod's row in the per-tick decode block
     (``[slot, family x minute]``: one slot serves every metric family).  Slots are
     reference counted by the jobs watching the pod (two jobs on one pod share it).
-    Keys are the 64-bit pod keys of the job decoder, and the native decode index
-    is updated in place when pods come and go (a released pod's key is retired, so
-    a pod that keeps reporting after its job can never land in a reused slot)."""
+    Keys are the 64-bit pod keys of the job decoder; the map is the native decode
+    index itself, updated in place when pods come and go (a released pod's key is
+    retired, so a pod that keeps reporting after its job can never land in a
+    reused slot), and looked up in batches (a dict stands in without the native
+    library)."""
 
     def __init__(self, cap: int = 1024) -> None:
-        self.index: Dict[int, int] = {}
         self.cap = int(cap)
         self.refs = np.zeros(self.cap, dtype=np.int32)
         self.hash = np.zeros(self.cap, dtype=np.uint64)
         self.free: List[int] = list(range(self.cap - 1, -1, -1))
         self.grown = 0     # bumps when cap grows
         self.live = native.LiveKeyIndex("namespace", "pod") if native.available() else None
+        self.index: Dict[int, int] = {}   # the map when the native library is missing
+        self._n = 0
 
     def __len__(self) -> int:
-        return len(self.index)
+        return self._n
+
+    def slot_of(self, keys: np.ndarray) -> np.ndarray:
+        """Slot of each key (-1: not held)."""
+        u = np.ascontiguousarray(keys, dtype=np.uint64)
+        if self.live is not None:
+            return self.live.lookup(u)
+        idx = self.index
+        return np.fromiter((idx.get(h, -1) for h in u.tolist()), dtype=np.int64, count=len(u))
 
     def acquire(self, hashes: np.ndarray) -> np.ndarray:
         """One reference per occurrence of each key; returns the slot of each."""
@@ -116,9 +128,7 @@ class PodSlots:
             return np.zeros(0, dtype=np.int64)
         u, first, inv, cnt = np.unique(np.asarray(hashes, dtype=np.uint64), return_index=True, return_inverse=True,
                                        return_counts=True)
-        ul = u.tolist()
-        idx = self.index
-        slots = np.fromiter((idx.get(h, -1) for h in ul), dtype=np.int64, count=len(ul))
+        slots = self.slot_of(u)
         new = np.nonzero(slots < 0)[0]
         # new keys in the order they were given (jobs in admission order, pods in row order:
         # the order the tick's bodies list them), so the native index's entries -- and its
@@ -132,13 +142,16 @@ class PodSlots:
                 self.hash = np.concatenate([self.hash, np.zeros(old, dtype=np.uint64)])
                 self.free = list(range(self.cap - 1, old - 1, -1)) + self.free
                 self.grown += 1
-            got = [self.free.pop() for _ in range(len(new))]
+            k = len(new)
+            got = np.asarray(self.free[len(self.free) - k:][::-1], dtype=np.int64)
+            del self.free[len(self.free) - k:]
             slots[new] = got
-            for k, s in zip(new.tolist(), got):
-                idx[ul[k]] = s
             self.hash[got] = u[new]
             if self.live is not None:
-                self.live.set(u[new], np.asarray(got, dtype=np.int64))
+                self.live.set(u[new], got)
+            else:
+                self.index.update(zip(u[new].tolist(), got.tolist()))
+            self._n += k
         np.add.at(self.refs, slots, cnt.astype(np.int32))
         return slots[inv]
 
@@ -146,21 +159,21 @@ class PodSlots:
         if not len(hashes):
             return
         u, cnt = np.unique(np.asarray(hashes, dtype=np.uint64), return_counts=True)
-        idx = self.index
-        ul = u.tolist()
-        slots = np.fromiter((idx.get(h, -1) for h in ul), dtype=np.int64, count=len(ul))
+        slots = self.slot_of(u)
         ok = slots >= 0
         slots, cnt, u = slots[ok], cnt[ok], u[ok]
-        self.refs[slots] -= cnt.astype(np.int32)
+        np.subtract.at(self.refs, slots, cnt.astype(np.int32))
         gone = np.nonzero(self.refs[slots] <= 0)[0]
         if len(gone):
             gs = slots[gone]
             self.refs[gs] = 0
-            for h in u[gone].tolist():
-                del idx[h]
-            self.free.extend(gs.tolist())
             if self.live is not None:
                 self.live.retire(u[gone])
+            else:
+                for h in u[gone].tolist():
+                    del self.index[h]
+            self.free.extend(gs.tolist())
+            self._n -= len(gone)
 
     def table(self, fams: int):
         """The decode index (native): key -> slot."""
@@ -197,8 +210,10 @@ class RolloutMonitor:
         self.min_capacity = max(1, int(min_capacity))
         self.jobs: Dict[str, RolloutPlan] = {}        # admitted (rows assigned)
         self.waiting: Dict[str, RolloutPlan] = {}     # claimed, history not resident yet
-        self._ends: List[Tuple[float, str]] = []      # (end_ts, job) heap of admitted jobs
-        self.row_plan: List[Optional[Tuple[str, int]]] = []   # row -> (job id, series index)
+        self._ends: Dict[int, List[RolloutPlan]] = {}  # end minute -> admitted jobs ending in it
+        self._end_keys: List[int] = []                 # heap of the minutes of _ends
+        self._jplan: List[Optional[RolloutPlan]] = []  # job slot -> admitted plan (row_job indexes it)
+        self._jfree: List[int] = []
         self.apps: Dict[Tuple[str, str], int] = {}
         self.roster_version = 0
         self.t_cur = 0.0                               # newest minute ingested into the windows
@@ -222,8 +237,12 @@ class RolloutMonitor:
         self._remote: List[Tuple[str, Tuple[str, str], float, int, List]] = []
         self.timings: Dict[str, float] = {}
         self._bands: Tuple[np.ndarray, np.ndarray, np.ndarray] = (np.zeros(0), np.zeros(0), np.zeros(0))
-        self._done_bands: Dict[int, Tuple[PlanCols, int, float, float, Optional[float]]] = {}
-        self._last_anom: Dict[int, float] = {}
+        # last bands of finished jobs' series, exported until their series come back: one entry
+        # per retirement batch (plans, rows' plan index, series index, hash, upper, lower, last anomaly)
+        self._done_chunks: "collections.deque" = collections.deque()
+        self._done_n = 0
+        self._ending: Dict[str, Tuple[str, str, Optional[Dict]]] = {}   # settled at scoring, written at intake
+        self.written_late: Dict[str, str] = {}                          # statuses the last intake wrote
         self._apps_dirty = False
         self._app_refs: Dict[Tuple[str, str], int] = {}
         self._app_names: List[Optional[Tuple[str, str]]] = []   # app index -> name (None: free index)
@@ -285,7 +304,6 @@ class RolloutMonitor:
         self.app_stats = torch.zeros((max(1, len(self._app_names)), 2), dtype=torch.int32, device=dev)
         if n:  # rows keep their app index across growth
             self.app_id[:n].copy_(old_app_id)
-        self.row_plan.extend([None] * (cap - len(self.row_plan)))
         grow = cap - n
 
         def ext(name, fill, dtype, shape=()):
@@ -296,7 +314,9 @@ class RolloutMonitor:
         ext("row_slot", -1, np.int64, (self.P,))
         ext("row_cs", 0.0, np.float64)      # cur_start of the row (anomaly timestamps)
         ext("row_s", -1, np.int64)          # series index in its PlanCols
-        self.row_cols: List[Optional[PlanCols]] = getattr(self, "row_cols", []) + [None] * grow
+        ext("row_job", -1, np.int64)        # job slot of the row (-1: free)
+        ext("row_k", -1, np.int64)          # series index of the row within its job
+        ext("last_anom", np.nan, np.float64)  # timestamp of the row's last anomalous point (band export)
         self._free = list(range(cap - 1, n - 1, -1)) + self._free
         self._srcmap_geom = None
         self.cap = cap
@@ -304,25 +324,24 @@ class RolloutMonitor:
             from ..ops import kernels as K
             self.anomalies = K.AnomalyBuffer(max(1024, 4 * cap), dev)
 
-    def _free_rows(self, rows: List[int]) -> None:
-        if not rows:
+    def _free_rows(self, rows) -> None:
+        ra = np.asarray(rows, dtype=np.int64)
+        if not len(ra):
             return
-        idx = torch.tensor(rows, dtype=torch.long, device=self.device)
+        idx = torch.from_numpy(ra).to(self.device)
         self.win.index_fill_(0, idx, float("nan"))
         self.base.index_fill_(0, idx, float("nan"))
         self.app_id.index_fill_(0, idx, 0)
-        ra = np.asarray(rows, dtype=np.int64)
-        for row in rows:
-            self.row_plan[row] = None
-            self.row_cols[row] = None
+        self.row_job[ra] = -1
+        self.row_k[ra] = -1
         self.model_ok[ra] = False
         self._fam_count(self.row_fam[ra], -1)
         self.row_fam[ra] = -1
         self.row_slot[ra] = -1
         self.row_s[ra] = -1
         self._srcmap_dirty.append(ra)
-        self._free.extend(rows)
-        self._n_live -= len(rows)
+        self._free.extend(ra.tolist())
+        self._n_live -= len(ra)
 
     def _take_rows(self, n: int) -> np.ndarray:
         if len(self._free) < n:
@@ -339,6 +358,54 @@ class RolloutMonitor:
     @property
     def n_live(self) -> int:
         return self._n_live
+
+    def _take_jslots(self, n: int) -> np.ndarray:
+        while len(self._jfree) < n:
+            old = len(self._jplan)
+            grow = max(64, old)
+            self._jplan.extend([None] * grow)
+            self._jfree = list(range(old + grow - 1, old - 1, -1)) + self._jfree
+        out = self._jfree[len(self._jfree) - n:][::-1] if n else []
+        del self._jfree[len(self._jfree) - n:]
+        return np.asarray(out, dtype=np.int64)
+
+    def _release_jslot(self, p: RolloutPlan) -> None:
+        if p.jslot >= 0 and self._jplan[p.jslot] is p:
+            self._jplan[p.jslot] = None
+            self._jfree.append(p.jslot)
+        p.jslot = -1
+
+    def _end_push(self, p: RolloutPlan) -> None:
+        """File an admitted job under the minute of its endTime (a job without a
+        finite endTime never ends by time)."""
+        if not np.isfinite(p.end_ts):
+            return
+        k = int(np.floor(p.end_ts / self.step))
+        b = self._ends.get(k)
+        if b is None:
+            b = self._ends[k] = []
+            heapq.heappush(self._end_keys, k)
+        b.append(p)
+
+    def _pop_ending(self, now: float, skip) -> List[RolloutPlan]:
+        """Admitted jobs whose endTime has passed (not in ``skip``): whole minutes
+        at once; the current minute's jobs one by one."""
+        out: List[RolloutPlan] = []
+        kn = int(np.floor(now / self.step))
+        keys, jobs = self._end_keys, self.jobs
+        while keys and keys[0] <= kn:
+            k = keys[0]
+            keep = []
+            for p in self._ends[k]:
+                if jobs.get(p.doc_id) is not p or p.doc_id in skip:
+                    continue  # dropped / released, or finishing with an anomaly this tick
+                (out if p.end_ts <= now else keep).append(p)
+            if keep:
+                self._ends[k] = keep
+                break
+            heapq.heappop(keys)
+            del self._ends[k]
+        return out
 
     # ------------------------------------------------------------------ membership
     def owns_affine(self, d) -> bool:
@@ -369,14 +436,17 @@ class RolloutMonitor:
         plans = pl.plan_many(docs, self.cfg.algorithm, self.step, self.Wc)
         hist = self.history
         n = 0
+        groups: Dict[int, Tuple[PlanCols, List[RolloutPlan]]] = {}
         for d, p in zip(docs, plans):
             if p is None or d["id"] in self.jobs or d["id"] in self.waiting:
                 continue
             p.doc = d
             self.waiting[d["id"]] = p
-            c, s0 = p.cols, p.s0
-            hist.want_h(c.u64[s0:s0 + p.n, 0].tolist(), now, lambda i, c=c, s0=s0: c.hkey_at(s0 + i))
+            groups.setdefault(id(p.cols), (p.cols, []))[1].append(p)
             n += 1
+        for c, ps in groups.values():  # history references: one call per decoded batch
+            idx = np.concatenate([np.arange(p.s0, p.s0 + p.n) for p in ps])
+            hist.want_h(c.u64[idx, 0].tolist(), now, lambda i, c=c, idx=idx: c.hkey_at(int(idx[i])))
         self.timings["claim_ms"] = (t1 - t0) * 1e3
         self.timings["plan_ms"] = (time.perf_counter() - t1) * 1e3
         self.timings["claimed"] = n
@@ -401,10 +471,11 @@ class RolloutMonitor:
             return
         self.history.unwant_h(p.cols.u64[p.s0:p.s0 + p.n, 0].tolist(), now)
         self._free_rows(p.rows)
-        if p.rows:
+        if len(p.rows):
             self._app_ref(p, -1)
             self.slots.release(p.pod_keys)
-        p.rows = []
+        self._release_jslot(p)
+        p.rows = np.zeros(0, dtype=np.int64)
 
     def _refresh_apps(self) -> None:
         """Apply the app-roster changes of the last admissions / verdicts.  App
@@ -420,22 +491,23 @@ class RolloutMonitor:
                 self._app_names[i] = None
                 self._app_free.append(i)
         self._app_gone = []
-        rows_all, ids_all = [], []
-        for a, rows in self._app_new:
-            i = self.apps.get(a)
+        ids = np.empty(len(self._app_new), dtype=np.int32)
+        apps, names, free = self.apps, self._app_names, self._app_free
+        for k, (a, _rows) in enumerate(self._app_new):
+            i = apps.get(a)
             if i is None:
-                i = self._app_free.pop() if self._app_free else len(self._app_names)
-                if i == len(self._app_names):
-                    self._app_names.append(a)
+                i = free.pop() if free else len(names)
+                if i == len(names):
+                    names.append(a)
                 else:
-                    self._app_names[i] = a
-                self.apps[a] = i
-            if len(rows):
-                rows_all.append(np.asarray(rows, dtype=np.int64))
-                ids_all.append(np.full(len(rows), i, dtype=np.int32))
-        if rows_all:  # one device scatter for every admitted row
-            rr = torch.from_numpy(np.concatenate(rows_all)).to(self.device)
-            self.app_id[rr] = torch.from_numpy(np.concatenate(ids_all)).to(self.device)
+                    names[i] = a
+                apps[a] = i
+            ids[k] = i
+        if len(self._app_new):  # one device scatter for every admitted row
+            lens = np.fromiter((len(rows) for _a, rows in self._app_new), dtype=np.int64, count=len(self._app_new))
+            if lens.sum():
+                rr = torch.from_numpy(np.concatenate([rows for _a, rows in self._app_new]).astype(np.int64))
+                self.app_id[rr.to(self.device)] = torch.from_numpy(np.repeat(ids, lens)).to(self.device)
         self._app_new = []
         if self.cap and self.app_stats.shape[0] < max(1, len(self._app_names)):
             cap = self.app_stats.shape[0]
@@ -469,20 +541,18 @@ class RolloutMonitor:
         b = _Batch(ready, self.P)
         rows = self._take_rows(b.n)
         b.rows = rows
-        off = 0
-        for p in b.plans:
+        starts = np.concatenate([[0], np.cumsum(b.lens)]).astype(np.int64)
+        js = self._take_jslots(len(b.plans))
+        for i, (p, j) in enumerate(zip(b.plans, js.tolist())):
             del self.waiting[p.doc_id]
-            p.rows = rows[off:off + p.n].tolist()
-            for k, row in enumerate(p.rows):
-                self.row_plan[row] = (p.doc_id, k)
-            off += p.n
+            p.rows = rows[starts[i]:starts[i + 1]]
+            p.jslot = j
+            self._jplan[j] = p
             self.jobs[p.doc_id] = p
-            heapq.heappush(self._ends, (p.end_ts, p.doc_id))
+            self._end_push(p)
         self._n_live += b.n
-        for cols, lo, hi in b.parts:
-            rr = rows[lo:hi]
-            for row in rr.tolist():
-                self.row_cols[row] = cols
+        self.row_job[rows] = np.repeat(js, b.lens)
+        self.row_k[rows] = np.arange(b.n) - np.repeat(starts[:-1], b.lens)
         self.row_s[rows] = b.s
         self.row_cs[rows] = b.f64[:, 0]
         t1 = time.perf_counter()
@@ -637,8 +707,7 @@ class RolloutMonitor:
         job holds one reference per distinct pod (released when it finishes)."""
         P = self.P
         H, valid = b.cur_pod_keys()                           # [n, P] pod keys, mask
-        job = np.repeat(np.arange(len(b.plans)), b.lens)      # plan index of each row
-        jk = np.repeat(job, P)[valid.reshape(-1)]
+        jk = np.repeat(b.job, P)[valid.reshape(-1)]
         hk = H.reshape(-1)[valid.reshape(-1)]
         # distinct (job, pod): one reference each (sort by job then key, drop repeats)
         order = np.lexsort((hk, jk))
@@ -652,7 +721,7 @@ class RolloutMonitor:
             p.pod_keys = hk_u[starts[i]:starts[i + 1]]
         # slot of every (row, pod): the keys are all live now
         u = np.unique(hk_u)
-        us = np.fromiter((self.slots.index[h] for h in u.tolist()), dtype=np.int64, count=len(u))
+        us = self.slots.slot_of(u)
         pos = np.searchsorted(u, H.reshape(-1)).clip(0, max(len(u) - 1, 0))
         sl = np.where(valid.reshape(-1), us[pos] if len(u) else -1, -1).reshape(b.n, P)
         self.row_slot[b.rows] = sl
@@ -725,6 +794,27 @@ class RolloutMonitor:
         c, s = b.cols_of(i), b.s_of(i)
         return c.pods(int(c.i32[s, pc]), min(int(c.i32[s, pc + 1]), self.P))
 
+    def _pod_matchers(self, b: "_Batch", chunk: np.ndarray, base: bool) -> str:
+        """``{namespace=~"...",pod=~"..."}`` of the rows ``chunk`` (their jobs' pods)."""
+        P = self.P
+        nss, alts, loose = set(), set(), set()
+        pk, ss = b._part_of[chunk], b.s[chunk]
+        for k in np.unique(pk).tolist():
+            cols = b.parts[k][0]
+            for s_ in ss[pk == k].tolist():
+                nss.add(cols.ns_at(s_))
+                alt = cols.pods_alt(s_, base)
+                if alt:                 # the job decoder's "a|b|c" of the row's pods
+                    alts.add(alt)
+                else:                   # rows of the Python parser
+                    loose.update((cols.base_pods(s_) if base else cols.cur_pods(s_))[:P])
+        pod_re = b"|".join(sorted(alts)).decode()
+        if "." in pod_re:  # the one RE2 metacharacter a plain pod name can hold
+            pod_re = pod_re.replace(".", "\\\\.")
+        if loose:
+            pod_re = "|".join(x for x in (pod_re, re_alt(loose)) if x)
+        return f'{{namespace=~"{re_alt(nss)}",pod=~"{pod_re}"}}'
+
     async def _load_group(self, b: "_Batch", dst: str, sel: np.ndarray, start: float, n: int, fkeys: np.ndarray,
                           pc: int) -> None:
         P, Wc = self.P, self.Wc
@@ -758,28 +848,21 @@ class RolloutMonitor:
         index = native.KeyTable.indexed(uk, np.arange(nl, dtype=np.int64), "namespace", "pod")
         reqs = []
         base = dst == "base"
+        # a job's rows share its namespace and pods: the selector of a chunk of jobs is built and
+        # URL-quoted once, and every family whose rows are the same jobs reuses it
+        sel_of: Dict[bytes, str] = {}
+        job = b.job[sel]
         for j, f in enumerate(fams):
-            mine = sel[fidx == j]
+            m_j = np.nonzero(fidx == j)[0]
+            mine, jobs_j = sel[m_j], job[m_j]
             for g0 in range(0, len(mine), self.apps_per_query):
                 chunk = mine[g0:g0 + self.apps_per_query]
-                nss, alts, loose = set(), set(), set()
-                pk, ss = b._part_of[chunk], b.s[chunk]
-                for k in np.unique(pk).tolist():
-                    cols = b.parts[k][0]
-                    for s_ in ss[pk == k].tolist():
-                        nss.add(cols.ns_at(s_))
-                        alt = cols.pods_alt(s_, base)
-                        if alt:                 # the job decoder's "a|b|c" of the row's pods
-                            alts.add(alt)
-                        else:                   # rows of the Python parser
-                            loose.update((cols.base_pods(s_) if base else cols.cur_pods(s_))[:P])
-                pod_re = b"|".join(sorted(alts)).decode()
-                if "." in pod_re:  # the one RE2 metacharacter a plain pod name can hold
-                    pod_re = pod_re.replace(".", "\\\\.")
-                if loose:
-                    pod_re = "|".join(x for x in (pod_re, re_alt(loose)) if x)
-                q = f'{f[1]}{{namespace=~"{re_alt(nss)}",pod=~"{pod_re}"}}'
-                reqs.append((range_url(f[0], q, start, n, self.step), start, n, j * Wc))
+                ck = jobs_j[g0:g0 + self.apps_per_query].tobytes()
+                qsel = sel_of.get(ck)
+                if qsel is None:
+                    qsel = sel_of[ck] = quote_selector(self._pod_matchers(b, chunk, base))
+                reqs.append((range_url_quoted(f[0], quote_selector(f[1]) + qsel, start, n, self.step), start, n,
+                             j * Wc))
         ok = await fetch_decode(self.prom, reqs, [index] * len(reqs), block_t.numpy(), self.step,
                                 self.decode_threads)
         if not all(ok):
@@ -825,7 +908,7 @@ class RolloutMonitor:
                     block[i, p, :n] = v[local[(ns, pod)]]
             rows = torch.tensor([row for row, _, _ in part], dtype=torch.long, device=self.device)
             tgt = self.base if dst == "base" else self.win
-            if all(0 <= row < len(self.row_plan) and self.row_plan[row] is not None for row in rows.tolist()):
+            if all(0 <= row < self.cap and self.row_job[row] >= 0 for row in rows.tolist()):
                 tgt.index_copy_(0, rows, torch.from_numpy(block.reshape(len(part), P * Wc)).to(self.device))
 
     def _tick_block(self, S: int, k: int):
@@ -1006,7 +1089,10 @@ class RolloutMonitor:
         t0 = time.perf_counter()
         now = self.clock()
         n = 0
+        self.written_late = {}
         try:
+            self.written_late = self._finish_ending()
+            self.timings["ending_ms"] = (time.perf_counter() - t0) * 1e3
             await self.history.load_pending(now)
             n = await self._admit(now)
         except Exception:  # noqa: BLE001
@@ -1023,6 +1109,7 @@ class RolloutMonitor:
         the jobs claimed by :meth:`sync`."""
         written = await self.score_tick()
         await self.intake()
+        written.update(self.written_late)
         return written
 
     def _anomalies_from_band(self, verdict):
@@ -1040,23 +1127,24 @@ class RolloutMonitor:
         Wc = self.Wc
         bad_rows = np.nonzero(verdict == 1)[0]
         points: Dict[int, List[Tuple[float, float, str]]] = {}
+        row_job, jplan = self.row_job, self._jplan
         for rr, cc, vv in zip(np.asarray(a_rows).tolist(), np.asarray(a_cols).tolist(), np.asarray(a_vals).tolist()):
-            if self.row_plan[rr] is None:
+            j = row_job[rr]
+            if j < 0:
                 continue
-            cols, s = self.row_cols[rr], int(self.row_s[rr])
-            p, c = divmod(int(cc), Wc)
-            pods = cols.cur_pods(s)
+            p = jplan[j]
+            pc, c = divmod(int(cc), Wc)
+            pods = p.cols.cur_pods(p.s0 + int(self.row_k[rr]))
             points.setdefault(rr, []).append((float(self.row_cs[rr]) + c * self.step, float(vv),
-                                              pods[p] if p < len(pods) else ""))
+                                              pods[pc] if pc < len(pods) else ""))
         finish: Dict[str, Tuple[str, str, Optional[Dict]]] = {}
         for rr in bad_rows.tolist():
-            plan_ref = self.row_plan[rr]
-            if plan_ref is None or plan_ref[0] in finish:
+            j = row_job[rr]
+            if j < 0 or jplan[j].doc_id in finish:
                 continue
-            jid = plan_ref[0]
-            p = self.jobs[jid]
+            p = jplan[j]
             anomaly = {}
-            for k, row in enumerate(p.rows):
+            for k, row in enumerate(p.rows.tolist()):
                 if verdict[row] != 1:
                     continue
                 pts = sorted(points.get(row, []))
@@ -1065,27 +1153,36 @@ class RolloutMonitor:
                     vals += [ts, v]
                 anomaly[p.cols.alias[p.s0 + k]] = {"tags": ",".join(sorted({t for _, _, t in pts if t})),
                                                    "values": vals}
-                self._last_anom[row] = pts[-1][0] if pts else now
-            finish[jid] = (r.ST_COMPLETED_UNHEALTH, "anomaly detected in " + ",".join(sorted(anomaly)), anomaly)
-        ending = []
-        while self._ends and self._ends[0][0] <= now:
-            _, jid = heapq.heappop(self._ends)
-            p = self.jobs.get(jid)
-            if p is not None and jid not in finish:
-                ending.append(p)
+                self.last_anom[row] = pts[-1][0] if pts else now
+            finish[p.doc_id] = (r.ST_COMPLETED_UNHEALTH, "anomaly detected in " + ",".join(sorted(anomaly)), anomaly)
+        ending = self._pop_ending(now, finish)
         if ending:  # past endTime: seen / model checks over every ending job's rows at once
-            rr = np.fromiter((row for p in ending for row in p.rows), dtype=np.int64)
+            rr = np.concatenate([p.rows for p in ending])
             lens = np.fromiter((len(p.rows) for p in ending), dtype=np.int64, count=len(ending))
             starts = np.concatenate([[0], np.cumsum(lens)[:-1]])
             seen = np.add.reduceat((npts[rr] > 0).astype(np.int64), starts) > 0
             mok = np.add.reduceat(self.model_ok[rr].astype(np.int64), starts) > 0
+            late: Dict[str, Tuple[str, str, Optional[Dict]]] = {}
             for p, sn, mk in zip(ending, seen.tolist(), mok.tolist()):
                 if sn and mk:
-                    finish[p.doc_id] = (r.ST_COMPLETED_HEALTH, "", None)
+                    late[p.doc_id] = (r.ST_COMPLETED_HEALTH, "", None)
                 elif sn:
-                    finish[p.doc_id] = (r.ST_COMPLETED_UNKNOWN, "missing historical data", None)
+                    late[p.doc_id] = (r.ST_COMPLETED_UNKNOWN, "missing historical data", None)
                 else:
-                    finish[p.doc_id] = (r.ST_COMPLETED_UNKNOWN, "no current metric data", None)
+                    late[p.doc_id] = (r.ST_COMPLETED_UNKNOWN, "no current metric data", None)
+            # the verdicts of jobs that ran out their watch are settled now; their writes and
+            # the release of their rows wait for the intake half (after the node exchange):
+            # nothing about them is news, and the fail-fast verdicts go out first
+            self._ending.update(late)
+        return self._finish(finish, now)
+
+    def _finish_ending(self) -> Dict[str, str]:
+        late, self._ending = self._ending, {}
+        return self._finish(late, self.clock()) if late else {}
+
+    def _finish(self, finish: Dict[str, Tuple[str, str, Optional[Dict]]], now: float) -> Dict[str, str]:
+        """Write the final status of ``finish`` (job -> (status, reason, anomaly)) and
+        retire the jobs."""
         if not finish:
             return {}
         items = []
@@ -1114,27 +1211,34 @@ class RolloutMonitor:
             self._retire(done_plans, now)
         return written
 
+    DONE_BANDS_MAX = 1 << 20   # rows of finished jobs whose last band stays exported
+
     def _retire(self, plans: List[RolloutPlan], now: float) -> None:
         """Release the finished jobs' rows, pod slots and history references in batches;
         their last bands stay exported (read at scrape time)."""
         up, lo, _ = self._bands
-        freed = np.fromiter((row for p in plans for row in p.rows), dtype=np.int64)
-        hk = np.concatenate([p.cols.u64[p.s0:p.s0 + p.n, 0] for p in plans])
-        srow = np.concatenate([np.arange(p.s0, p.s0 + p.n) for p in plans])
-        cols = [p.cols for p in plans for _ in range(p.n)]
+        freed = np.concatenate([p.rows for p in plans])
+        lens = np.fromiter((len(p.rows) for p in plans), dtype=np.int64, count=len(plans))
+        hk_all = np.concatenate([p.cols.u64[p.s0:p.s0 + p.n, 0] for p in plans])
         if len(up) >= self.cap and len(freed):
             u, l_ = up[freed], lo[freed]
             ok = ~np.isnan(u)
-            done, la = self._done_bands, self._last_anom
-            for h, c, s, uu, ll, row in zip(hk[ok].tolist(), [c for c, k in zip(cols, ok) if k], srow[ok].tolist(),
-                                            u[ok].tolist(), l_[ok].tolist(), freed[ok].tolist()):
-                done[h] = (c, s, uu, ll, la.pop(row, None))
-        if self._last_anom:
-            for row in freed.tolist():
-                self._last_anom.pop(row, None)
-        self.history.unwant_h(hk.tolist(), now)
+            if ok.any():
+                pidx = np.repeat(np.arange(len(plans)), lens)[ok]
+                k = self.row_k[freed][ok]
+                s0 = np.fromiter((p.s0 for p in plans), dtype=np.int64, count=len(plans))
+                srow = s0[pidx] + k
+                hk = hk_all[ok]
+                self._done_chunks.append((plans, pidx, srow, hk, u[ok], l_[ok], self.last_anom[freed][ok]))
+                self._done_n += len(srow)
+                while self._done_n > self.DONE_BANDS_MAX and len(self._done_chunks) > 1:
+                    self._done_n -= len(self._done_chunks.popleft()[1])
+        self.last_anom[freed] = np.nan
+        self.history.unwant_h(hk_all.tolist(), now)
         self.slots.release(np.concatenate([p.pod_keys for p in plans]))
-        self._free_rows(freed.tolist())
+        self._free_rows(freed)
+        for p in plans:
+            self._release_jslot(p)
 
     # ------------------------------------------------------------------ node integration
     def app_table(self) -> Tuple[List[Optional[Tuple[str, str]]], torch.Tensor]:
@@ -1147,18 +1251,25 @@ class RolloutMonitor:
 
     def _band_rows(self):
         up, lo, verdict = self._bands
-        live = set()
+        seen = set()
+        la = self.last_anom
         for jid, p in list(self.jobs.items()):
             hk = p.cols.u64[p.s0:p.s0 + p.n, 0].tolist()
-            for k, row in enumerate(p.rows):
+            for k, row in enumerate(p.rows.tolist()):
                 if row < len(up) and up[row] == up[row]:
-                    live.add(hk[k])
+                    seen.add(hk[k])
                     key = p.cols.hkey_at(p.s0 + k)
-                    yield (key[1], key[2], key[3], float(up[row]), float(lo[row]), self._last_anom.get(row))
-        for h, (cols, s, u, l_, an) in list(self._done_bands.items()):
-            if h not in live:
-                key = cols.hkey_at(s)
-                yield (key[1], key[2], key[3], u, l_, an)
+                    an = float(la[row])
+                    yield (key[1], key[2], key[3], float(up[row]), float(lo[row]), an if an == an else None)
+        # finished jobs: the newest band of each series that is not live again
+        for plans, pidx, srow, hk, u, l_, an in reversed(list(self._done_chunks)):
+            for i, s, h, uu, ll, aa in zip(pidx.tolist(), srow.tolist(), hk.tolist(), u.tolist(), l_.tolist(),
+                                           an.tolist()):
+                if h in seen:
+                    continue
+                seen.add(h)
+                key = plans[i].cols.hkey_at(s)
+                yield (key[1], key[2], key[3], uu, ll, aa if aa == aa else None)
 
 
 class _Batch:
@@ -1192,6 +1303,7 @@ class _Batch:
         self.i32 = np.concatenate(i32) if i32 else np.zeros((0, 7), np.int32)
         self.u64 = np.concatenate(u64) if u64 else np.zeros((0, 6), np.uint64)
         self.lens = np.fromiter((p.n for p in self.plans), dtype=np.int64, count=len(self.plans))
+        self.job = np.repeat(np.arange(len(self.plans)), self.lens)   # batch row -> plan index
         self._part_of = np.concatenate([np.full(hi - lo, k, dtype=np.int64) for k, (_, lo, hi) in
                                         enumerate(self.parts)]) if self.parts else np.zeros(0, np.int64)
         self.rows = np.zeros(0, np.int64)

@@ -172,12 +172,16 @@ def _filter(cand: List[Dict[str, Any]], only, only_batch) -> List[Dict[str, Any]
 _STAMP_CACHE: Dict[float, str] = {}
 
 
+_FLAT = frozenset((str, int, float, bool, type(None)))
+
+
 def _flat_copy(fields: Dict[str, Any]) -> Dict[str, Any]:
     """A copy that shares nothing mutable: job documents are flat (str / number
     values), so a dict copy suffices; nested values are deep-copied."""
-    if all(isinstance(v, (str, int, float, bool, type(None))) for v in fields.values()):
-        return dict(fields)
-    return copy.deepcopy(fields)
+    for v in fields.values():
+        if type(v) not in _FLAT:
+            return copy.deepcopy(fields)
+    return dict(fields)
 
 
 def _stamp(d: Dict[str, Any], fields: Dict[str, Any]) -> None:

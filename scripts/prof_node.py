@@ -33,14 +33,16 @@ def main() -> None:
         ticks = int(argv[i + 1])
         del argv[i:i + 2]
     os.makedirs(out, exist_ok=True)
-    sys.argv = ["bench.py", "--config", "node", "--steps", str(ticks), "--warmup", "1"] + argv
+    warm = [] if "--warmup" in argv else ["--warmup", "1"]
+    sys.argv = ["bench.py", "--config", "node", "--steps", str(ticks)] + warm + argv
     import torch
 
     import bench
     args = bench.parse()
     world, rank, dev = bench.init_dist(args)
-    from foremast_amd.benchmarks.node import setup_node
-    tick, _health, meta, _dt, _n = setup_node(args, world, rank, dev)
+    from foremast_amd.benchmarks.node import setup_arrival, setup_node
+    setup = setup_arrival if getattr(args, "arrival_per_tick", 0) else setup_node
+    tick, _health, meta, _dt, _n = setup(args, world, rank, dev)
     for k in range(args.warmup):
         tick(k)
     prof = cProfile.Profile()
@@ -58,6 +60,7 @@ def main() -> None:
         buf.write(f"==== sorted by {key} over {args.steps} ticks ====\n")
         st = pstats.Stats(prof, stream=buf)
         st.sort_stats(key).print_stats(45)
+    prof.dump_stats(os.path.join(out, "node_host.prof"))
     with open(os.path.join(out, "node_host.pstats.txt"), "w") as f:
         f.write(buf.getvalue())
     rec = {"tick_ms": [round(x, 2) for x in wall], "breakdowns": meta["_breakdowns"],
