@@ -255,9 +255,12 @@ class BatchScorer:
         return out_res
 
     # ------------------------------------------------------------------ multivariate
-    def score_bivariate(self, pairs: List[Tuple[MetricTask, MetricTask]]) -> List[Tuple[int, List[int]]]:
-        """Score aligned metric pairs (same job).  Returns per pair (verdict,
-        anomalous indices into the first task's current points)."""
+    def score_bivariate(self, pairs: List[Tuple[MetricTask, MetricTask]]) -> List[Tuple[int, List[Tuple[float, float]]]]:
+        """Score metric pairs of one job each: the current points of each metric are
+        averaged across pods per timestamp and restricted to the timestamps both have
+        (:func:`~.multivariate.align_job`).  Returns per pair (verdict, anomalous
+        points as (timestamp, first metric's value))."""
+        from .multivariate import align_job
         if not pairs:
             return []
         B = len(pairs)
@@ -269,13 +272,12 @@ class BatchScorer:
         for i, (a, b) in enumerate(pairs):
             hx[i, T - len(a.hist):] = a.hist
             hy[i, T - len(b.hist):] = b.hist
-            common, ia, ib = np.intersect1d(a.cur_ts, b.cur_ts, return_indices=True)
-            aligned.append((ia, ib))
-            C = max(C, len(common))
+            _h, cts, cur2 = align_job([a, b])
+            aligned.append((cts, cur2))
+            C = max(C, len(cts))
         cur = np.full((B, C, 2), np.nan, dtype=np.float32)
-        for i, ((a, b), (ia, ib)) in enumerate(zip(pairs, aligned)):
-            cur[i, :len(ia), 0] = a.cur_vals[ia]
-            cur[i, :len(ib), 1] = b.cur_vals[ib]
+        for i, (cts, cur2) in enumerate(aligned):
+            cur[i, :len(cts)] = cur2
         thr = torch.tensor([a.threshold for a, _ in pairs], dtype=torch.float32, device=self.device)
         if self.gpu:
             from ..ops import kernels as K
@@ -293,8 +295,8 @@ class BatchScorer:
             verdict = np.where(an.any(1), 1, np.where((~np.isnan(d2)).any(1) & ok, 0, -1))
         res = []
         t2 = (thr.cpu().numpy() ** 2)
-        for i, (ia, _) in enumerate(aligned):
-            idx = [int(ia[j]) for j in range(len(ia)) if d2[i, j] > t2[i]]
-            res.append((int(verdict[i]) if not idx else 1, idx))
+        for i, (cts, cur2) in enumerate(aligned):
+            pts = [(float(cts[j]), float(cur2[j, 0])) for j in range(len(cts)) if d2[i, j] > t2[i]]
+            res.append((int(verdict[i]) if not pts else 1, pts))
         self.series_scored += 2 * B
         return res

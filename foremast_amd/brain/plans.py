@@ -24,6 +24,7 @@ decoder accepts.
 
 from __future__ import annotations
 
+import ctypes
 import os
 import re
 from collections import OrderedDict
@@ -40,8 +41,27 @@ from ..service import urls
 from ..utils.timeutil import TimeFormatError, parse_rfc3339
 
 STRATEGIES = ("canary", "rollingupdate")
-ALGORITHMS = ("holt_winters", "exponential_smoothing", "double_exponential_smoothing", "moving_average",
+UNIVARIATE = ("holt_winters", "exponential_smoothing", "double_exponential_smoothing", "moving_average",
               "moving_average_all", "seasonal_decompose")
+# multi-metric algorithms (docs/guides/design.md:53-89): every metric keeps a univariate
+# row (moving_average_all, as brain/batch.py scores it), and the job gets a joint model
+JOINT_ALGORITHMS = ("bivariate_normal", "lstm", "auto")
+ALGORITHMS = UNIVARIATE + JOINT_ALGORITHMS
+JOINT_SERVED = ("biv",)   # joint models the resident engine serves (others: BrainWorker)
+
+
+def joint_kind(algorithm: str, n_metrics: int) -> Optional[str]:
+    """The joint model of a job with ``n_metrics`` aliases: ``"biv"`` (bivariate
+    normal over its first two aliases), ``"lstm"`` (LSTM autoencoder over all) or
+    None — the dispatch of ``brain/worker.py`` ``_multivariate``: ``auto`` sends 2
+    metrics to the bivariate normal and 3+ to the LSTM (``design.md:76-84``)."""
+    if algorithm == "auto":
+        return "biv" if n_metrics == 2 else ("lstm" if n_metrics >= 3 else None)
+    if algorithm == "bivariate_normal":
+        return "biv" if n_metrics >= 2 else None
+    if algorithm == "lstm":
+        return "lstm" if n_metrics >= 2 else None
+    return None
 _SPLIT = ("namespace_pod_caller:", "namespace_app_caller:", "namespace_app_caller_per_pod:",
           "namespace_pod_uri:", "namespace_app_uri:", "namespace_app_uri_per_pod:")
 _REGEX_META = re.compile(r"[*+?()\[\]{}^$\\]")
@@ -66,6 +86,25 @@ class RolloutSeries:
     base_n: int
     hist_end: float
     base_fam: Tuple[str, str] = ("", "")  # (endpoint, pod metric) of the baseline window (may be another cluster)
+
+
+class Interned:
+    """A per-row column of a few distinct values, stored as row -> index into them
+    (a decoded batch of 10k rows has a handful of aliases and families)."""
+
+    __slots__ = ("vals", "idx")
+
+    def __init__(self, vals: List, idx: np.ndarray) -> None:
+        self.vals, self.idx = vals, idx
+
+    def __getitem__(self, s):
+        return self.vals[self.idx[s]]
+
+    def __len__(self) -> int:
+        return len(self.idx)
+
+    def __iter__(self):
+        return (self.vals[i] for i in self.idx.tolist())
 
 
 class PlanCols:
@@ -128,7 +167,7 @@ class PlanCols:
             return b""
         a = self.span[s]
         k = 18 if base else 16
-        return self.text[a[k]:a[k] + a[k + 1]]
+        return bytes(self.text[a[k]:a[k] + a[k + 1]])
 
     def cur_pods(self, s: int) -> Tuple[str, ...]:
         return self.pods(int(self.i32[s, 2]), int(self.i32[s, 3]))
@@ -375,11 +414,12 @@ def _native_call(lib, blob, off, N, step, window_cols, ser_cap, pod_cap, text_ca
     u64 = np.empty((ser_cap, 6), dtype=np.uint64)
     pod_span = np.empty((pod_cap, 2), dtype=np.int64)
     pod_u64 = np.empty(pod_cap, dtype=np.uint64)
-    text = np.empty(text_cap, dtype=np.uint8)
+    text = bytearray(text_cap)  # kept as the PlanCols text (no copy of the decoded strings)
+    text_ptr = ctypes.addressof((ctypes.c_char * text_cap).from_buffer(text))
     S = lib.fm_plan_rollout(blob, off.ctypes.data, N, float(step), int(window_cols), job_i32.ctypes.data,
                             job_f64.ctypes.data, job_span.ctypes.data, f64.ctypes.data, i32.ctypes.data,
                             span.ctypes.data, u64.ctypes.data, ser_cap, pod_span.ctypes.data, pod_u64.ctypes.data,
-                            pod_cap, text.ctypes.data, text_cap)
+                            pod_cap, text_ptr, text_cap)
     if S < 0:
         return None
     return S, job_i32, job_f64, job_span, f64, i32, span, u64, pod_span, pod_u64, text
@@ -448,11 +488,12 @@ def _pool():
 def _columns(got, docs: Sequence[Dict]) -> Tuple[np.ndarray, List]:
     """PlanCols and plans of one decoded chunk."""
     S, job_i32, job_f64, job_span, f64, i32, span, u64, pod_span, pod_u64, text = got
-    tb = text.tobytes()
+    tb = text
     sp = span[:S]
 
-    def interned(col: int, table: Dict, make) -> List:
-        """Per row, the interned value of its key column (one decode per distinct key)."""
+    def interned(col: int, table: Dict, make, mask=None) -> Interned:
+        """Per row, the interned value of its key column (one decode per distinct key);
+        rows outside ``mask`` get ("", "")."""
         u, first, inv = np.unique(u64[:S, col], return_index=True, return_inverse=True)
         vals = []
         for k, r0 in zip(u.tolist(), first.tolist()):
@@ -460,7 +501,11 @@ def _columns(got, docs: Sequence[Dict]) -> Tuple[np.ndarray, List]:
             if v is None:
                 v = table[k] = make(sp[r0].tolist())
             vals.append(v)
-        return [vals[i] for i in inv.tolist()]
+        inv = inv.reshape(-1).astype(np.int32)
+        if mask is not None and not mask.all():
+            vals.append(("", ""))
+            inv = np.where(mask, inv, len(vals) - 1).astype(np.int32)
+        return Interned(vals, inv)
 
     def st(a, k):
         return tb[a[2 * k]:a[2 * k] + a[2 * k + 1]].decode()
@@ -468,9 +513,7 @@ def _columns(got, docs: Sequence[Dict]) -> Tuple[np.ndarray, List]:
     hfam = interned(3, _INTERN_H, lambda a: (st(a, 1), st(a, 2)))
     fam = interned(1, _INTERN_F, lambda a: (st(a, 1), st(a, 5)))
     has_b = i32[:S, 6] > 0
-    bfam = interned(2, _INTERN_F, lambda a: (st(a, 6), st(a, 7)) if a[13] or a[15] else ("", ""))
-    if not has_b.all():
-        bfam = [x if h else ("", "") for x, h in zip(bfam, has_b.tolist())]
+    bfam = interned(2, _INTERN_F, lambda a: (st(a, 6), st(a, 7)) if a[13] or a[15] else ("", ""), has_b)
     for d in (_INTERN_A, _INTERN_H, _INTERN_F):
         if len(d) > 1 << 16:
             d.clear()
@@ -512,14 +555,19 @@ def plan_many(docs: Sequence[Dict], algorithm: str, step: float = 60.0,
             out[i] = _PLANS[ck]
         else:
             todo.append(i)
-    if not todo:
-        return out
-    got = _native_batch([docs[i] for i in todo], step, window_cols)
-    for k, i in enumerate(todo):
-        d = docs[i]
-        p = got[1][k] if got is not None and got[0][k] else _plan(d, step, window_cols)
-        out[i] = p
-        _remember((d.get("id", ""), step, window_cols), p)
+    if todo:
+        got = _native_batch([docs[i] for i in todo], step, window_cols)
+        for k, i in enumerate(todo):
+            d = docs[i]
+            p = got[1][k] if got is not None and got[0][k] else _plan(d, step, window_cols)
+            out[i] = p
+            _remember((d.get("id", ""), step, window_cols), p)
+    if algorithm in JOINT_ALGORITHMS:  # jobs whose joint model the engine does not serve stay with BrainWorker
+        for i, p in enumerate(out):
+            if p is not None:
+                k = joint_kind(algorithm, p.n)
+                if k is not None and k not in JOINT_SERVED:
+                    out[i] = None
     return out
 
 

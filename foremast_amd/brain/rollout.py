@@ -64,6 +64,7 @@ import torch
 
 from ..api import rest as r
 from ..ingest import native
+from ..models import bivariate as biv_ref
 from ..models import decompose as dec_ref
 from ..models import detect as det_ref
 from ..models import moving_average as ma_ref
@@ -221,7 +222,8 @@ class RolloutMonitor:
         self.tick_queries = 0
         self.admitted = 0
         self.cap = 0
-        self._free: List[int] = []                     # free rows (stack)
+        self._row_free = np.zeros(0, dtype=bool)       # free-row mask (admission takes the lowest)
+        self._n_free = 0
         self.slots = PodSlots()
         self.fams: Dict[Tuple[str, str], int] = {}     # pod metric family -> index in the decode block
         self._fam_of_key: Dict[int, int] = {}          # family key (job decoder) -> index
@@ -287,6 +289,10 @@ class RolloutMonitor:
             "min_lower": torch.zeros(cap, **f32),
             "app_id": torch.zeros(cap, dtype=torch.int32, device=dev),
             "start_min": torch.zeros(cap, dtype=torch.int32, device=dev),
+            # joint bivariate model of a 2-metric job, kept on its first alias's row
+            "biv_mean": torch.zeros((cap, 2), **f32),
+            "biv_cov": torch.zeros((cap, 3), **f32),
+            "biv_ok": torch.zeros(cap, dtype=torch.bool, device=dev),
         }
         st = {k: torch.zeros(cap, **f32) for k in ("level", "trend", "sigma", "nvalid")}
         st["best"] = torch.full((cap,), -1, dtype=torch.int32, device=dev)
@@ -317,7 +323,9 @@ class RolloutMonitor:
         ext("row_job", -1, np.int64)        # job slot of the row (-1: free)
         ext("row_k", -1, np.int64)          # series index of the row within its job
         ext("last_anom", np.nan, np.float64)  # timestamp of the row's last anomalous point (band export)
-        self._free = list(range(cap - 1, n - 1, -1)) + self._free
+        ext("biv_b", -1, np.int64)          # first-alias row of a bivariate job -> its second alias's row
+        self._row_free = np.concatenate([self._row_free, np.ones(grow, dtype=bool)])
+        self._n_free += grow
         self._srcmap_geom = None
         self.cap = cap
         if self.gpu:
@@ -334,26 +342,28 @@ class RolloutMonitor:
         self.app_id.index_fill_(0, idx, 0)
         self.row_job[ra] = -1
         self.row_k[ra] = -1
+        self.biv_b[ra] = -1
         self.model_ok[ra] = False
         self._fam_count(self.row_fam[ra], -1)
         self.row_fam[ra] = -1
         self.row_slot[ra] = -1
         self.row_s[ra] = -1
         self._srcmap_dirty.append(ra)
-        self._free.extend(ra.tolist())
+        self._row_free[ra] = True
+        self._n_free += len(ra)
         self._n_live -= len(ra)
 
     def _take_rows(self, n: int) -> np.ndarray:
-        if len(self._free) < n:
-            used = self.cap - len(self._free)
+        if self._n_free < n:
+            used = self.cap - self._n_free
             cap = max(self.min_capacity, self.cap or 1)
             while cap < used + n:
                 cap *= 2
             self._alloc(cap)
-        self._free.sort(reverse=True)
-        out = self._free[-n:][::-1] if n else []
-        del self._free[len(self._free) - n:]
-        return np.asarray(out, dtype=np.int64)
+        out = np.flatnonzero(self._row_free)[:n]
+        self._row_free[out] = False
+        self._n_free -= len(out)
+        return out.astype(np.int64)
 
     @property
     def n_live(self) -> int:
@@ -560,6 +570,7 @@ class RolloutMonitor:
         self._assign_slots(b)
         t2 = time.perf_counter()
         self._fit(b)
+        self._fit_joint(b)
         t3 = time.perf_counter()
         await self._load_windows(b)
         t4 = time.perf_counter()
@@ -615,8 +626,76 @@ class RolloutMonitor:
             hz = off[:, None] + tiles
             self.hz[idx] = torch.from_numpy(np.clip(hz, 1, 1 << 20).astype(np.int32)).to(self.device)
 
+    def _fit_joint(self, b: "_Batch") -> None:
+        """Joint models of the admitted multi-metric jobs (``ML_ALGORITHM`` bivariate_normal
+        / auto): the bivariate normal of a job's first two aliases (sorted, as
+        ``brain/worker.py`` pairs them), fitted on their 7-day histories ending at the
+        job's start (K8 ``bivariate`` kernel on the GPU), kept on the first alias's row."""
+        algo = self.cfg.algorithm
+        if algo not in pl.JOINT_ALGORITHMS:
+            return
+        hist = self.history
+        starts = np.concatenate([[0], np.cumsum(b.lens)]).astype(np.int64)
+        ia, ib = [], []   # batch rows of each bivariate job's two aliases
+        for i, p in enumerate(b.plans):
+            if pl.joint_kind(algo, p.n) != "biv":
+                continue
+            al = [p.cols.alias[p.s0 + k] for k in range(p.n)]
+            ka, kb = sorted(range(p.n), key=al.__getitem__)[:2]
+            ia.append(starts[i] + ka)
+            ib.append(starts[i] + kb)
+        if not ia:
+            return
+        ia, ib = np.asarray(ia, dtype=np.int64), np.asarray(ib, dtype=np.int64)
+        ha = np.fromiter((hist.rows[h] for h in b.u64[ia, 0].tolist()), dtype=np.int64, count=len(ia))
+        hb = np.fromiter((hist.rows[h] for h in b.u64[ib, 0].tolist()), dtype=np.int64, count=len(ib))
+        drop = np.maximum(0, np.round((hist.t_last - b.f64[ia, 2]) / self.step).astype(np.int64))
+        dev = self.device
+        for dv in np.unique(drop).tolist():
+            sel = np.nonzero(drop == dv)[0]
+            xa, head, length = hist.gather(ha[sel].tolist(), dv)
+            xb, _, _ = hist.gather(hb[sel].tolist(), dv)
+            k = len(sel)
+            if self.gpu:
+                from ..ops import kernels as K
+                out = K.bivariate(xa, xb, head, length, torch.full((k, 1, 2), float("nan"), device=dev),
+                                  torch.ones(k, device=dev), min_valid=self.cfg.min_historical_points)
+                mean, cov, count = out["mean"], out["cov"], out["count"]
+            else:
+                idx = (torch.arange(length) + head) % xa.shape[1]
+                fit = biv_ref.fit_bivariate(torch.stack([xa.index_select(1, idx), xb.index_select(1, idx)], 2))
+                mean, cov, count = fit.mean, fit.cov, fit.count
+            ra = torch.from_numpy(b.rows[ia[sel]]).to(dev)
+            self.biv_mean[ra] = mean.float()
+            self.biv_cov[ra] = cov.float()
+            self.biv_ok[ra] = count.to(dev) >= self.cfg.min_historical_points
+        self.biv_b[b.rows[ia]] = b.rows[ib]
+
+    def _score_joint(self):
+        """Bivariate jobs' points this tick: (first-alias rows, window columns, pod-mean
+        values) where the squared Mahalanobis distance of the two aliases' pod-mean
+        current values exceeds threshold^2 (``brain/batch.py`` ``score_bivariate``)."""
+        rows = np.nonzero(self.biv_b >= 0)[0]
+        if not len(rows):
+            return None
+        dev, P, Wc = self.device, self.P, self.Wc
+        ra = torch.from_numpy(rows).to(dev)
+        rb = torch.from_numpy(self.biv_b[rows]).to(dev)
+        x = torch.nanmean(self.win[ra].view(-1, P, Wc), 1)
+        y = torch.nanmean(self.win[rb].view(-1, P, Wc), 1)
+        fit = biv_ref.BivariateFit(mean=self.biv_mean[ra], cov=self.biv_cov[ra], count=None)
+        d2 = biv_ref.mahalanobis2(fit, torch.stack([x, y], 2))
+        thr = self.threshold[ra]
+        hit = (d2 > (thr * thr)[:, None]) & self.biv_ok[ra][:, None]
+        i, c = torch.nonzero(hit, as_tuple=True)
+        vals = x[i, c]
+        i, c, vals = i.cpu().numpy(), c.cpu().numpy(), vals.cpu().numpy()
+        return rows[i], c, vals
+
     def _algo_for(self, length: int) -> str:
         algo, m = self.cfg.algorithm, self.season
+        if algo in pl.JOINT_ALGORITHMS:
+            return "moving_average_all"   # the per-metric part; the joint model is _fit_joint's
         if algo == "holt_winters" and length < 2 * m:
             algo = "double_exponential_smoothing"
         if algo == "seasonal_decompose" and length < 2 * m + 1:
@@ -1073,8 +1152,9 @@ class RolloutMonitor:
             a_vals = self.win.numpy()[a_rows, a_cols]
         self.timings["score_ms"] = (time.perf_counter() - t0) * 1e3
         t0 = time.perf_counter()
+        joint = self._score_joint() if self.cfg.algorithm in pl.JOINT_ALGORITHMS else None
         self._bands = (host[2], host[3], verdict)
-        written = self._verdicts(now, verdict, npts, a_rows, a_cols, a_vals)
+        written = self._verdicts(now, verdict, npts, a_rows, a_cols, a_vals, joint)
         self.timings["verdict_ms"] = (time.perf_counter() - t0) * 1e3
         self.ticks += 1
         self.metrics.tick.observe(time.perf_counter() - t_tick)
@@ -1121,11 +1201,19 @@ class RolloutMonitor:
         rr, cc = np.nonzero(flag)
         return rr, cc, x[rr, cc]
 
-    def _verdicts(self, now: float, verdict: np.ndarray, npts: np.ndarray, a_rows, a_cols, a_vals) -> Dict[str, str]:
+    def _verdicts(self, now: float, verdict: np.ndarray, npts: np.ndarray, a_rows, a_cols, a_vals,
+                  joint=None) -> Dict[str, str]:
         """Jobs with an anomalous metric (fail fast) and jobs past endTime finish;
-        the others stay leased and untouched."""
+        the others stay leased and untouched.  ``joint``: (rows, columns, values) of the
+        joint model's anomalous points; they flag the job and replace the anomalies of
+        the first alias (``brain/worker.py`` ``_multivariate``)."""
         Wc = self.Wc
         bad_rows = np.nonzero(verdict == 1)[0]
+        jpts: Dict[int, List[Tuple[float, float]]] = {}
+        if joint is not None and len(joint[0]):
+            for rr, cc, vv in zip(joint[0].tolist(), joint[1].tolist(), joint[2].tolist()):
+                jpts.setdefault(rr, []).append((float(self.row_cs[rr]) + cc * self.step, float(vv)))
+            bad_rows = np.union1d(bad_rows, np.fromiter(jpts, dtype=np.int64, count=len(jpts)))
         points: Dict[int, List[Tuple[float, float, str]]] = {}
         row_job, jplan = self.row_job, self._jplan
         for rr, cc, vv in zip(np.asarray(a_rows).tolist(), np.asarray(a_cols).tolist(), np.asarray(a_vals).tolist()):
@@ -1145,6 +1233,11 @@ class RolloutMonitor:
             p = jplan[j]
             anomaly = {}
             for k, row in enumerate(p.rows.tolist()):
+                if row in jpts:  # the joint model's points replace this alias's own
+                    jp = sorted(jpts[row])
+                    anomaly[p.cols.alias[p.s0 + k]] = {"tags": "", "values": [x for tv in jp for x in tv]}
+                    self.last_anom[row] = jp[-1][0]
+                    continue
                 if verdict[row] != 1:
                     continue
                 pts = sorted(points.get(row, []))

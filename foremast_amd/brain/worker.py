@@ -262,13 +262,12 @@ class BrainWorker:
                 (ta, _), (tb, _) = items[0], items[1]
                 pairs.append((ta, tb))
                 owners.append(i)
-        for i, (verdict, idx) in zip(owners, self.scorer.score_bivariate(pairs)):
+        for i, (verdict, pts) in zip(owners, self.scorer.score_bivariate(pairs)):
             ta, ra = per_job[i][0]
             tb, rb = per_job[i][1]
             if verdict == 1:
                 ra.verdict = max(ra.verdict, 1)
-                ra.anomalies = [(float(ta.cur_ts[j]), float(ta.cur_vals[j]),
-                                 ta.cur_tags[j] if j < len(ta.cur_tags) else "") for j in idx]
+                ra.anomalies = [(ts, v, "") for ts, v in pts]
                 ra.model = rb.model = "bivariate_normal"
 
     def _downstream(self, per_job) -> None:

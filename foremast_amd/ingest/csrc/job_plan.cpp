@@ -153,6 +153,19 @@ bool plain_number(Span s, double& v) {
   bool neg = false;
   if (s.p[0] == '-') { neg = true; i = 1; }
   if (i >= s.n) return false;
+  if (s.n - i <= 15) {  // the common case, an integer below 1e15: one pass, exact
+    long long x = 0;
+    size_t k = i;
+    for (; k < s.n; ++k) {
+      const unsigned d = (unsigned)(s.p[k] - '0');
+      if (d > 9) break;
+      x = x * 10 + (long long)d;
+    }
+    if (k == s.n) {
+      v = neg ? -(double)x : (double)x;
+      return true;
+    }
+  }
   bool digit = false, dot = false;
   for (size_t k = i; k < s.n; ++k) {
     const char c = s.p[k];
@@ -262,10 +275,18 @@ bool parse_selector(const std::string& s, Span& name, std::vector<Matcher>& ms) 
   return true;
 }
 
+struct MetaTable {
+  bool t[256] = {};
+  MetaTable() {
+    for (const char* c = "*+?()[]{}^$\\"; *c; ++c) t[(unsigned char)*c] = true;
+  }
+};
+const MetaTable kMeta;
+
 inline bool regex_meta(Span v) {
-  for (size_t i = 0; i < v.n; ++i)
-    if (strchr("*+?()[]{}^$\\", v.p[i])) return true;
-  return false;
+  bool any = false;
+  for (size_t i = 0; i < v.n; ++i) any |= kMeta.t[(unsigned char)v.p[i]];
+  return any;
 }
 
 // rollout._pods_of: (namespace, sorted distinct pods) of namespace= / pod= / pod=~ "a|b"
