@@ -92,6 +92,18 @@ class BodyServer:
         return body
 
 
+def _brainworker_share(docs, cfg) -> int:
+    """Jobs no resident monitor keys (they would reach BrainWorker); the plan memo is
+    reset afterwards so the timed claims decode as in production."""
+    from ..brain import plans as pl
+    from ..brain.lstm_monitor import lstm_features
+    from ..brain.streaming import is_continuous
+    ps = pl.plan_many(list(docs), cfg.algorithm)
+    pl._PLANS.clear()
+    return sum(1 for d, p in zip(docs, ps)
+               if p is None and not (is_continuous(d) and lstm_features(d, cfg) is not None))
+
+
 def setup_node(args, world, rank, dev):
     from ..brain.node import NodeBrain, owner_of
     from ..brain.rollout import RolloutMonitor
@@ -217,6 +229,7 @@ def setup_node(args, world, rank, dev):
         job_of[resp["jobId"]] = mine[i]
     register_s = time.perf_counter() - t0
     del reqs
+    n_worker = _brainworker_share(list(store._docs.values()), cfg)
 
     stream = StreamingMonitor(store, cfg, prom=server, device=dev, worker_id=f"node-m{rank}", ring_len=R,
                               window=W, clock=lambda: clock["t"])
@@ -307,6 +320,7 @@ def setup_node(args, world, rank, dev):
         "setup_s": round(setup_s, 2),
         "register_s": round(register_s, 3),
         "register_jobs_per_s": round(na / max(register_s, 1e-9), 1),
+        "jobs_to_brainworker": n_worker,
         "intake_s": round(intake_s, 3),
         "intake_breakdown_ms": {k: round(v, 2) for k, v in intake_timings.items()},
         "_scored_rows": scored,
@@ -642,6 +656,7 @@ def setup_arrival(args, world, rank, dev):
         "setup_s": round(setup_s, 2),
         "register_s": round(register_s, 3),
         "register_jobs_per_s": round(sum(len(a) for a in arrivals) / max(register_s, 1e-9), 1),
+        "jobs_to_brainworker": _brainworker_share([d for a in arrivals for d in a], cfg),
         "_scored_rows": scored,
         "_breakdowns": breakdowns,
         "_arrival_finish": finish,

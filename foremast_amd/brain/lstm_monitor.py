@@ -73,6 +73,7 @@ class Entity:
     end_ts: float
     feats: List[Tuple[str, Key]]
     row: int = -1
+    external: bool = False   # a rollout job's joint model (brain/rollout.py): fed, verdicts read back
 
 
 class LstmMonitor:
@@ -142,6 +143,11 @@ class LstmMonitor:
         self._digest: Optional[str] = None
         self._digest_tick = -1
         self.timings: Dict[str, float] = {}
+        # external entities (rollout jobs' joint models): the newest value of each is fed by
+        # the rollout engine (its canary pods' mean), and their verdicts are read back
+        self.sync_history = True     # False: another monitor drives the shared history
+        self._feed: Dict[str, np.ndarray] = {}
+        self.hits: Dict[str, Tuple[float, np.ndarray]] = {}
 
     # ------------------------------------------------------------------ membership
     def is_mine(self, d) -> bool:
@@ -172,6 +178,24 @@ class LstmMonitor:
         if back:
             self.store.update_many(back, expect_claimed_by=self.worker_id)
         return len(back)
+
+    def attach(self, jid: str, feats: List[Tuple[str, Key]], end_ts: float, now: float) -> None:
+        """Score a rollout job's metrics jointly (its first ``F`` aliases, sorted):
+        the entity's rows hold the app's history, then the values :meth:`feed` gives."""
+        if jid in self.jobs or jid in self.waiting:
+            return
+        e = Entity(doc={"id": jid}, end_ts=end_ts, feats=list(feats)[:self.F], external=True)
+        self.waiting[jid] = e
+        self.history.want([k for _, k in e.feats], now)
+
+    def detach(self, jids, now: float) -> None:
+        for jid in jids:
+            self.hits.pop(jid, None)
+            self._drop(jid, now)
+
+    def feed(self, values: Dict[str, np.ndarray]) -> None:
+        """Newest value of each external entity's features (NaN: keep the history's)."""
+        self._feed = values
 
     def after_reform(self) -> None:
         """RC4: every rank adopts rank 0's weights and optimizer state after the
@@ -289,10 +313,30 @@ class LstmMonitor:
             col = (hist.ring.head + R - 1 - age) % R
             v = hist.ring.data[:, col].float()
             x = v[self.feat_rows.clamp(min=0)]
+            if age == 0 and self._feed:  # external entities: the fed values of the newest minute
+                x = self._fed(x)
             x = torch.where(self.padded, torch.zeros_like(x), x)
             x = torch.where((self.feat_rows >= 0) | self.padded, x, torch.full_like(x, float("nan")))
             self.shard.ingest_tick(x.contiguous())
         self.t_cur = hist.t_last
+
+    def _fed(self, x: torch.Tensor) -> torch.Tensor:
+        rows, vals = [], []
+        for jid, v in self._feed.items():
+            e = self.jobs.get(jid)
+            if e is not None and e.row >= 0:
+                w = np.full(self.F, np.nan, dtype=np.float32)
+                w[:min(self.F, len(v))] = np.asarray(v, dtype=np.float32)[:self.F]
+                rows.append(e.row)
+                vals.append(w)
+        self._feed = {}
+        if not rows:
+            return x
+        idx = torch.tensor(rows, dtype=torch.long, device=self.device)
+        fv = torch.from_numpy(np.stack(vals)).to(self.device)
+        x = x.clone()
+        x[idx] = torch.where(torch.isnan(fv), x[idx], fv)
+        return x
 
     # ------------------------------------------------------------------ tick
     async def tick(self) -> Dict[str, str]:
@@ -301,8 +345,9 @@ class LstmMonitor:
         now = self.clock()
         admitted: List[int] = []
         try:
-            self.store.heartbeat(self.worker_id, now)
-            await self.history.sync(now)
+            if self.sync_history:
+                self.store.heartbeat(self.worker_id, now)
+                await self.history.sync(now)
             self._ingest()
             admitted = self._admit()
             if admitted:
@@ -346,9 +391,14 @@ class LstmMonitor:
         v = out["verdict"].cpu().numpy()
         newest = self._newest()
         items = []
+        self.hits = {}
         for jid, e in list(self.jobs.items()):
             if not self._calibrated[e.row]:
                 continue  # admitted while the model was pretraining: scored once calibrated
+            if e.external:  # the rollout engine owns the job: it reads the verdict back
+                if v[e.row] == 1:
+                    self.hits[jid] = (self.history.t_last, newest[e.row])
+                continue
             if v[e.row] == 1:
                 anomaly = {}
                 for f, (alias, _k) in enumerate(e.feats):

@@ -47,7 +47,7 @@ UNIVARIATE = ("holt_winters", "exponential_smoothing", "double_exponential_smoot
 # row (moving_average_all, as brain/batch.py scores it), and the job gets a joint model
 JOINT_ALGORITHMS = ("bivariate_normal", "lstm", "auto")
 ALGORITHMS = UNIVARIATE + JOINT_ALGORITHMS
-JOINT_SERVED = ("biv",)   # joint models the resident engine serves (others: BrainWorker)
+JOINT_SERVED = ("biv", "lstm")   # joint models the resident engine serves
 
 
 def joint_kind(algorithm: str, n_metrics: int) -> Optional[str]:

@@ -44,10 +44,16 @@ state instead:
   finished jobs; band gauges are read from the last tick's host arrays at
   scrape time.
 
+Multi-metric algorithms (``ML_ALGORITHM`` bivariate_normal / lstm / auto,
+``docs/guides/design.md:53-89``) keep a moving_average_all row per metric and
+add the job's joint model: the bivariate normal of its first two aliases (K8
+fit at admission, Mahalanobis on the pod-mean windows every tick) or the LSTM
+autoencoder over all of them (the node's resident LSTM engine,
+:mod:`.lstm_monitor`, fed each tick with the canary pods' mean).
+
 Jobs the resident engine cannot key (non-Prometheus sources, per-caller /
-per-uri families, selectors that are not plain pod lists, multi-metric
-algorithms) stay with :class:`~foremast_amd.brain.worker.BrainWorker`
-(:func:`is_rollout_keyable`).
+per-uri families, selectors that are not plain pod lists) stay with
+:class:`~foremast_amd.brain.worker.BrainWorker` (:func:`is_rollout_keyable`).
 """
 
 from __future__ import annotations
@@ -256,6 +262,19 @@ class RolloutMonitor:
         self._build_grid()
         self.anomalies = None
         self.metrics.add_band_source(f"rollout:{worker_id}", self._band_rows)
+        # the joint LSTM autoencoder of 3+-metric jobs (ML_ALGORITHM lstm / auto): the node's
+        # resident LSTM engine (brain/lstm_monitor.py) on this engine's history, data-parallel
+        # across the ranks; every rank ticks it in lockstep
+        self.joint_lstm = None
+        self._lstm_rows: Dict[str, np.ndarray] = {}   # job -> its rows in feature (sorted alias) order
+        if self.cfg.algorithm in ("lstm", "auto"):
+            from .lstm_monitor import LstmMonitor
+            self.joint_lstm = LstmMonitor(store, self.cfg, prom=self.prom, device=self.device,
+                                          worker_id=worker_id + "-joint", metrics=self.metrics, step=step,
+                                          clock=clock, history=self.history, ring_len=self.history.R,
+                                          min_capacity=min_capacity,
+                                          decode_threads=decode_threads)
+            self.joint_lstm.sync_history = False
 
     # ------------------------------------------------------------------ model grid
     def _build_grid(self) -> None:
@@ -485,6 +504,8 @@ class RolloutMonitor:
             self._app_ref(p, -1)
             self.slots.release(p.pod_keys)
         self._release_jslot(p)
+        if self._lstm_rows.pop(jid, None) is not None:
+            self.joint_lstm.detach([jid], now)
         p.rows = np.zeros(0, dtype=np.int64)
 
     def _refresh_apps(self) -> None:
@@ -637,13 +658,20 @@ class RolloutMonitor:
         hist = self.history
         starts = np.concatenate([[0], np.cumsum(b.lens)]).astype(np.int64)
         ia, ib = [], []   # batch rows of each bivariate job's two aliases
+        now = self.clock()
         for i, p in enumerate(b.plans):
-            if pl.joint_kind(algo, p.n) != "biv":
+            kind = pl.joint_kind(algo, p.n)
+            if kind is None:
                 continue
             al = [p.cols.alias[p.s0 + k] for k in range(p.n)]
-            ka, kb = sorted(range(p.n), key=al.__getitem__)[:2]
-            ia.append(starts[i] + ka)
-            ib.append(starts[i] + kb)
+            order = sorted(range(p.n), key=al.__getitem__)
+            if kind == "lstm" and self.joint_lstm is not None:
+                order = order[:self.joint_lstm.F]
+                self._lstm_rows[p.doc_id] = p.rows[order]
+                self.joint_lstm.attach(p.doc_id, [(al[k], p.cols.hkey_at(p.s0 + k)) for k in order], p.end_ts, now)
+                continue
+            ia.append(starts[i] + order[0])
+            ib.append(starts[i] + order[1])
         if not ia:
             return
         ia, ib = np.asarray(ia, dtype=np.int64), np.asarray(ib, dtype=np.int64)
@@ -1133,6 +1161,7 @@ class RolloutMonitor:
             self._bands = (np.zeros(0), np.zeros(0), np.zeros(0))
             if self.cap:
                 self.app_stats.zero_()
+            await self._tick_lstm(None)  # lockstep: the joint model's collectives run on every rank
             return written
         await self._ingest(t_new)
         t0 = time.perf_counter()
@@ -1153,8 +1182,9 @@ class RolloutMonitor:
         self.timings["score_ms"] = (time.perf_counter() - t0) * 1e3
         t0 = time.perf_counter()
         joint = self._score_joint() if self.cfg.algorithm in pl.JOINT_ALGORITHMS else None
+        lstm_hits = await self._tick_lstm(last_c)
         self._bands = (host[2], host[3], verdict)
-        written = self._verdicts(now, verdict, npts, a_rows, a_cols, a_vals, joint)
+        written = self._verdicts(now, verdict, npts, a_rows, a_cols, a_vals, joint, lstm_hits)
         self.timings["verdict_ms"] = (time.perf_counter() - t0) * 1e3
         self.ticks += 1
         self.metrics.tick.observe(time.perf_counter() - t_tick)
@@ -1201,8 +1231,38 @@ class RolloutMonitor:
         rr, cc = np.nonzero(flag)
         return rr, cc, x[rr, cc]
 
+    async def _tick_lstm(self, last_c: torch.Tensor) -> Dict[str, Tuple[float, np.ndarray]]:
+        """The joint LSTM's tick (lockstep: every rank, every tick, jobs or not): feed
+        each LSTM job's newest canary minute (pod mean per metric), one data-parallel
+        step, score; returns job -> (time, values) of the jobs it flags."""
+        if self.joint_lstm is None:
+            return {}
+        feed = {}
+        if self._lstm_rows:
+            jids = list(self._lstm_rows)
+            rows = np.concatenate([self._lstm_rows[j] for j in jids])
+            ra = torch.from_numpy(rows).to(self.device)
+            col = last_c[ra]
+            win = self.win[ra].view(len(rows), self.P, self.Wc)
+            v = torch.nanmean(win.gather(2, col.view(-1, 1, 1).expand(-1, self.P, 1))[:, :, 0], 1).cpu().numpy()
+            off = 0
+            for j in jids:
+                n = len(self._lstm_rows[j])
+                feed[j] = v[off:off + n]
+                off += n
+        self.joint_lstm.feed(feed)
+        await self.joint_lstm.tick()
+        return dict(self.joint_lstm.hits)
+
+    def after_reform(self) -> None:
+        if self.joint_lstm is not None:
+            self.joint_lstm.after_reform()
+
+    def model_digest(self) -> str:
+        return self.joint_lstm.model_digest() if self.joint_lstm is not None else ""
+
     def _verdicts(self, now: float, verdict: np.ndarray, npts: np.ndarray, a_rows, a_cols, a_vals,
-                  joint=None) -> Dict[str, str]:
+                  joint=None, lstm_hits=None) -> Dict[str, str]:
         """Jobs with an anomalous metric (fail fast) and jobs past endTime finish;
         the others stay leased and untouched.  ``joint``: (rows, columns, values) of the
         joint model's anomalous points; they flag the job and replace the anomalies of
@@ -1214,6 +1274,9 @@ class RolloutMonitor:
             for rr, cc, vv in zip(joint[0].tolist(), joint[1].tolist(), joint[2].tolist()):
                 jpts.setdefault(rr, []).append((float(self.row_cs[rr]) + cc * self.step, float(vv)))
             bad_rows = np.union1d(bad_rows, np.fromiter(jpts, dtype=np.int64, count=len(jpts)))
+        lstm_hits = {j: h for j, h in (lstm_hits or {}).items() if j in self.jobs}
+        if lstm_hits:
+            bad_rows = np.union1d(bad_rows, np.asarray([int(self.jobs[j].rows[0]) for j in lstm_hits], dtype=np.int64))
         points: Dict[int, List[Tuple[float, float, str]]] = {}
         row_job, jplan = self.row_job, self._jplan
         for rr, cc, vv in zip(np.asarray(a_rows).tolist(), np.asarray(a_cols).tolist(), np.asarray(a_vals).tolist()):
@@ -1232,6 +1295,16 @@ class RolloutMonitor:
                 continue
             p = jplan[j]
             anomaly = {}
+            hit = lstm_hits.get(p.doc_id)
+            if hit is not None:  # the joint LSTM flags every metric at the scored minute (worker: _score_lstm)
+                t_hit, vals_hit = hit
+                al = [p.cols.alias[p.s0 + k] for k in range(p.n)]
+                for f, k in enumerate(sorted(range(p.n), key=al.__getitem__)[:len(vals_hit)]):
+                    anomaly[al[k]] = {"tags": "", "values": [float(t_hit), float(vals_hit[f])]}
+                    self.last_anom[p.rows[k]] = float(t_hit)
+                finish[p.doc_id] = (r.ST_COMPLETED_UNHEALTH, "anomaly detected in " + ",".join(sorted(anomaly)),
+                                    anomaly)
+                continue
             for k, row in enumerate(p.rows.tolist()):
                 if row in jpts:  # the joint model's points replace this alias's own
                     jp = sorted(jpts[row])
@@ -1332,6 +1405,10 @@ class RolloutMonitor:
         self._free_rows(freed)
         for p in plans:
             self._release_jslot(p)
+        if self.joint_lstm is not None and self._lstm_rows:
+            gone = [p.doc_id for p in plans if self._lstm_rows.pop(p.doc_id, None) is not None]
+            if gone:
+                self.joint_lstm.detach(gone, now)
 
     # ------------------------------------------------------------------ node integration
     def app_table(self) -> Tuple[List[Optional[Tuple[str, str]]], torch.Tensor]:

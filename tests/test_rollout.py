@@ -96,10 +96,11 @@ def test_plan_matches_barrelman_queries():
     assert s.base_start == T0 - 600 and s.base_n == 11
     b = plan_rollout(store.get(ids["b"]), config())
     assert b is not None and b.series[0].base_pods == ()           # rollingUpdate: no baseline
-    # not keyable: continuous, a wavefront source, a multi-metric algorithm
+    # not keyable: continuous, a wavefront source; multi-metric algorithms are (joint models,
+    # tests/test_rollout_joint.py)
     assert not is_rollout_keyable(dict(doc, strategy="continuous", id="x1"), config())
     assert not is_rollout_keyable(dict(doc, id="x2", currentMetricStore="error5xx== wavefront"), config())
-    assert not is_rollout_keyable(doc, config("lstm"))
+    assert is_rollout_keyable(doc, config("lstm")) and is_rollout_keyable(doc, config("auto"))
 
 
 def _run(device, algorithm):

@@ -167,6 +167,62 @@ def test_bivariate_rollout_matches_worker(device, algorithm):
                 common = sorted(set(gp) & set(wp))
                 assert common, (app, alias)
                 np.testing.assert_allclose([gp[t] for t in common], [wp[t] for t in common], rtol=1e-5)
-    if algorithm == "auto":
-        assert docs["d"]["status"] == r.ST_PREPROCESS_INPROGRESS or "resident" not in docs["d"].get(
-            "processingContent", "")  # 3 metrics under auto: the LSTM path, not the bivariate
+    # 3 metrics under auto: the joint LSTM's job (test_lstm_rollout_jobs_on_the_resident_lstm), still resident
+    assert "resident engine" in docs["d"]["processingContent"]
+
+
+def lstm_world(bad_app="d3"):
+    """3-metric canary jobs on apps whose metrics move together; the new pods of
+    ``bad_app`` triple every metric from the third minute on."""
+    clock = Clock(T0)
+    prom = FakePrometheus(clock=clock)
+    store = MemoryJobStore()
+    ids = {}
+    from foremast_amd.promql import synth
+    for i in range(4):
+        app = f"d{i}"
+        new, old = [f"{app}-v2-{k}" for k in range(2)], [f"{app}-v1-{k}" for k in range(3)]
+        for j, (m, _a) in enumerate(M3):
+            base = synth.seasonal(level=10.0 + i + 5 * j, amp=2.0, noise=0.2, seed=10 * i + j)
+            prom.add("namespace_app_per_pod:" + m, {"namespace": NS, "app": app}, base)
+            for k, pod in enumerate(new + old):
+                g = synth.seasonal(level=10.0 + i + 5 * j, amp=2.0, noise=0.2, seed=10 * i + j + 100 * (k + 1))
+                if app == bad_app and pod in new:
+                    g = synth.step_change(g, at=T0 + 120, factor=3.0)
+                prom.add("namespace_pod:" + m, {"namespace": NS, "pod": pod}, g)
+        ids[app] = svc.register(store, request(app, new, old, M3))[1]["jobId"]
+    return clock, prom, store, ids
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_lstm_rollout_jobs_on_the_resident_lstm(device, monkeypatch):
+    """ML_ALGORITHM=auto, 3-metric canary jobs: keyed by the resident engine (none reach
+    BrainWorker); per-metric rows cannot fire (threshold 1000), the joint LSTM over the
+    three metrics — the node's resident LSTM engine fed with the canary pods' mean —
+    fails the degraded rollout and names every metric."""
+    monkeypatch.setenv("FOREMAST_LSTM_PRETRAIN", "40")
+    monkeypatch.setenv("FOREMAST_LSTM_PRETRAIN_PER_TICK", "40")
+    clock, prom, store, ids = lstm_world()
+    env = reference_default_env()
+    env.update(MIN_HISTORICAL_DATA_POINT_TO_MEASURE="10", ML_ALGORITHM="auto", ML_PAIRWISE_ALGORITHM="none",
+               threshold="1000", threshold0="1000", threshold1="1000", threshold2="1000", ML_LSTM_THRESHOLD="4",
+               FOREMAST_LSTM_WINDOW="8", FOREMAST_LSTM_HIDDEN="16")
+    cfg = BrainConfig.from_env(env)
+    assert all(is_rollout_keyable(store.get(j), cfg) for j in ids.values())
+    mon = RolloutMonitor(store, cfg, prom=PromClient(transport=httpx.ASGITransport(app=prom.asgi_app())),
+                         device=torch.device(device), metrics=BrainMetrics(), window=10, pods=5, clock=clock,
+                         ring_len=2880, min_capacity=4)
+    assert mon.joint_lstm is not None
+    written = {}
+
+    async def go():
+        for k in range(12):
+            clock.t = T0 + 60 * k
+            mon.sync()
+            written.update(await mon.tick())
+    asyncio.run(go())
+    assert written.get(ids["d3"]) == r.ST_COMPLETED_UNHEALTH, written
+    info = json.loads(store.get(ids["d3"])["anomalyInfo"])
+    assert set(info) == {a for _m, a in M3}
+    assert all(written.get(ids[a]) == r.ST_COMPLETED_HEALTH for a in ("d0", "d1", "d2")), written
+    assert not mon.jobs and not mon.joint_lstm.jobs
