@@ -130,7 +130,7 @@ def parse():
     p.add_argument("--baseline-model", default="canary", choices=["canary", "lstm", "multivariate"],
                    help="cpu_baseline: which GPU config's scorer the per-series CPU loop re-creates")
     p.add_argument("--config", default="canary",
-                   choices=["canary", "single", "hw10k", "lstm", "multivariate", "cpu_baseline", "node"],
+                   choices=["canary", "single", "hw10k", "lstm", "multivariate", "cpu_baseline", "node", "node-lstm"],
                    help="canary = headline (BASELINE configs 2/4 at 100k); single = config 1 (one latency "
                         "series, moving average, CPU brain plumbing end to end); hw10k = config 2 (10k series); "
                         "lstm = config 3; multivariate = config 5 (fp8 LSTM, latency + error-rate); node = the product "
@@ -144,6 +144,9 @@ def parse():
                    help="config 4 layout: each rank scrapes the baseline cluster of its neighbour's shard; "
                         "baseline windows reach their owner through one RCCL all-to-all per tick")
     p.add_argument("--lstm-window", type=int, default=32)
+    p.add_argument("--lstm-features", type=int, default=5,
+                   help="node-lstm config: metrics per continuous job (5: the 3+-metric LSTM dispatch over --series "
+                        "series = config 3 through the product; 2: latency + error-rate entities = config 5)")
     p.add_argument("--lstm-train-batch", type=int, default=4096)
     p.add_argument("--lstm-train-every", type=int, default=1)
     p.add_argument("--lstm-pretrain", type=int, default=800,
@@ -165,6 +168,12 @@ def parse():
         a.steps = (60 if a.arrival_per_tick else 8) if a.config == "node" else 20
     if a.warmup is None:
         a.warmup = (a.window + 1 if a.arrival_per_tick else 1) if a.config == "node" else 5
+        if a.config == "node-lstm":  # a fresh node pretrains its shared model over the warmup ticks
+            import os as _os
+            gpu = not a.cpu
+            pre = int(_os.environ.get("FOREMAST_LSTM_PRETRAIN", "800" if gpu else "20"))
+            per = int(_os.environ.get("FOREMAST_LSTM_PRETRAIN_PER_TICK", "100" if gpu else "20"))
+            a.warmup = -(-pre // max(1, per)) + 2
     if a.zero_copy or a.prefetch:
         a.graph = False  # these modes stage the tick's I/O from the host: eager launches
     return a
@@ -798,6 +807,9 @@ def main():
     elif args.config == "node" and args.arrival_per_tick > 0:
         from foremast_amd.benchmarks.node import setup_arrival
         tick, health_host, meta, dtype_name, n_series = setup_arrival(args, world, rank, dev)
+    elif args.config == "node-lstm":
+        from foremast_amd.benchmarks.node import setup_node_lstm
+        tick, health_host, meta, dtype_name, n_series = setup_node_lstm(args, world, rank, dev)
     elif args.config == "node":
         from foremast_amd.benchmarks.node import setup_node
         tick, health_host, meta, dtype_name, n_series = setup_node(args, world, rank, dev)
@@ -885,7 +897,7 @@ def main():
         if world > 1:
             dist.all_reduce(rows_t)
         timed_rows = float(rows_t.item())
-        tick_breakdown = {k: round(v, 3) for k, v in node_roll.timings.items()}
+        tick_breakdown = {k: round(v, 3) for k, v in node_roll.timings.items()} if node_roll is not None else {}
         if arrival_finish is not None:
             fin_s, statuses, arrival_det = arrival_finish()
         else:

@@ -664,3 +664,168 @@ def setup_arrival(args, world, rank, dev):
         "_server": server,
     }
     return tick, health, meta, "bf16" if dev.type == "cuda" else "fp32", J * W * M
+
+
+def setup_node_lstm(args, world, rank, dev):
+    """``--config node-lstm``: BASELINE configs 3 / 5 through the product path.
+    Continuous multi-metric jobs (``--lstm-features F`` metrics each: 5 = the design
+    doc's 3+-metric LSTM dispatch over 100k series; 2 = config 5's latency +
+    error-rate entities) are registered through the service's create handler and
+    scored by the production node brain: ``NodeBrain`` + :class:`LstmMonitor` — the
+    resident 7-day history of every (app, metric) advanced each tick from
+    ``query_range`` JSON (native decode), one data-parallel Adam step of the node's
+    shared LSTM autoencoder, calibration of joining entities, fused MFMA scoring of
+    every entity's newest window, fail-fast verdicts into the job store.  A fresh
+    node pretrains the model over the warmup ticks (``FOREMAST_LSTM_PRETRAIN`` steps,
+    ``FOREMAST_LSTM_PRETRAIN_PER_TICK`` per tick), as in production.  ``--anomaly-frac``
+    of the jobs triple every metric two minutes into the timed ticks."""
+    from ..api import rest as r
+    from ..brain.engine import synthetic_eval, synthetic_params
+    from ..brain.lstm_monitor import LstmMonitor
+    from ..brain.node import NodeBrain, owner_of
+    from ..brain.resident import ResidentHistory
+    from ..brain.streaming import StreamingMonitor
+    from ..ingest import native
+    from ..service import app as svc
+    from ..store import MemoryJobStore
+    from ..utils.config import BrainConfig, reference_default_env
+    from ..utils.timeutil import format_rfc3339
+
+    F = max(2, int(args.lstm_features))
+    mets = METRICS[:F]
+    R, season = args.ring, args.season
+    n_jobs = max(1, args.series // F)
+    if dev.type == "cpu" and not os.environ.get("FOREMAST_BENCH_CPU_FULL"):
+        n_jobs, R, season = min(n_jobs, 64), min(R, 2880), min(season, 1440)
+    pre = int(os.environ.get("FOREMAST_LSTM_PRETRAIN", "800" if dev.type == "cuda" else "20"))
+    per = int(os.environ.get("FOREMAST_LSTM_PRETRAIN_PER_TICK", "100" if dev.type == "cuda" else "20"))
+    ticks = args.warmup + args.steps + 1
+    mine = [a for a in range(n_jobs) if owner_of(f"ns{a % 200}", f"app{a}", world) == rank]
+    na = len(mine)
+    clock = {"t": T0}
+    t_setup = time.perf_counter()
+    env = reference_default_env()
+    env.update(ML_ALGORITHM="lstm", ML_LSTM_THRESHOLD=str(args.lstm_threshold),
+               FOREMAST_LSTM_LEVEL_THRESHOLD=str(args.lstm_level_threshold), FOREMAST_LSTM_WINDOW=str(args.lstm_window))
+    cfg = BrainConfig.from_env(env)
+    cfg.ring_len, cfg.season = R, season
+    store = MemoryJobStore()
+    server = ArrivalServer()
+    ns = [f"ns{a % 200}" for a in mine]
+    app = [f"app{a}" for a in mine]
+    # every job's F series: synthetic seasonal weeks (the history the node holds), continued by the ticks
+    gid = torch.tensor([a * F + j for a in mine for j in range(F)], dtype=torch.int64)
+    params = {k: v[gid] for k, v in synthetic_params(n_jobs * F, torch.device("cpu"), seed=4321).items()}
+    hist = ResidentHistory(server, dev, R, STEP, clock=lambda: clock["t"], decode_threads=args.decode_threads)
+    keys = [(ENDPOINT, "namespace_app_per_pod:" + m, ns[i], app[i]) for i in range(na) for m in mets]
+    hist.want(keys, T0)
+    asyncio.run(hist.assign_only(T0))
+    dparams = {k: v.to(dev) for k, v in params.items()}
+    for c0 in range(0, len(keys), 16384):
+        c1 = min(len(keys), c0 + 16384)
+        hist.load_rows(keys[c0:c1], synthetic_eval({k: v[c0:c1] for k, v in dparams.items()}, 0, R, season,
+                                                   noise_seed=77 + c0))
+    hist.unwant(keys, T0)
+    # per-tick bodies: the newest minute of every (app, metric); injected jobs x3 from tick `at`
+    rng = np.random.default_rng(5 + rank)
+    n_bad = int(round(args.anomaly_frac * na))
+    bad = set(rng.choice(na, size=n_bad, replace=False).tolist()) if n_bad else set()
+    at = args.warmup + 2
+    cont = synthetic_eval(params, R, ticks + 2, season, None).numpy()          # [na * F, ticks] no noise
+    noise = 0.03 * params["lvl"][:, 0].numpy()
+    badm = np.zeros(na * F, dtype=bool)
+    for i in bad:
+        badm[i * F:(i + 1) * F] = True
+    labels = {m: native.label_blob([f'"__name__":"namespace_app_per_pod:{m}","namespace":"{ns[i]}","app":"{app[i]}"'
+                                    for i in range(na)]) for m in mets}
+    for k in range(ticks + 1):
+        tk = T0 + STEP * k
+        v = cont[:, k] + rng.standard_normal(na * F) * noise
+        if k >= at:
+            v = np.where(badm, v * 3.0, v)
+        v = v.astype(np.float32).reshape(na, F)
+        for j, m in enumerate(mets):
+            server.tick_bodies[("namespace_app_per_pod:" + m, tk)] = native.render_matrix(labels[m], v[:, j:j + 1],
+                                                                                          tk, STEP)
+    del cont
+    # --- jobs through the service: continuous, F metrics each -------------------------------------
+    truth: Dict[str, bool] = {}
+    t_reg = time.perf_counter()
+    for i in range(na):
+        cur, hst = {}, {}
+        for m in mets:
+            q = f'namespace_app_per_pod:{m}{{namespace="{ns[i]}",app="{app[i]}"}}'
+            p = {"endpoint": ENDPOINT, "query": q, "step": int(STEP)}
+            cur[m] = {"dataSourceType": "prometheus", "parameters": dict(p, start=int(T0), end=int(T0 + 86400))}
+            hst[m] = {"dataSourceType": "prometheus", "parameters": dict(p, start=int(T0 - 7 * 86400), end=int(T0))}
+        code, resp = svc.register(store, {"appName": app[i], "startTime": format_rfc3339(T0),
+                                          "endTime": format_rfc3339(T0 + 86400), "strategy": "continuous",
+                                          "metrics": {"current": cur, "historical": hst}})
+        assert code == 200, resp
+        truth[resp["jobId"]] = i in bad
+    register_s = time.perf_counter() - t_reg
+    lstm = LstmMonitor(store, cfg, prom=server, device=dev, worker_id=f"node-m{rank}-lstm", step=STEP,
+                       clock=lambda: clock["t"], ring_len=R, features=F, window=args.lstm_window,
+                       train_batch=args.lstm_train_batch, min_capacity=max(64, na), history=hist,
+                       decode_threads=args.decode_threads)
+    stream = StreamingMonitor(store, cfg, prom=server, device=dev, worker_id=f"node-m{rank}", ring_len=R,
+                              window=10, clock=lambda: clock["t"])
+    stream.exclude = lstm.is_mine
+    node = NodeBrain(stream, None, store, dev, publish=False, extra=(lstm,))
+    node.owns = lambda d: True
+    for mon in node.monitors:
+        mon.owns = None
+    loop = asyncio.new_event_loop()
+    setup_s = time.perf_counter() - t_setup
+    breakdowns: List[Dict[str, float]] = []
+    scored: List[int] = []
+
+    def tick(k):
+        clock["t"] = T0 + STEP * k
+        n_live = sum(len(e.feats) for e in lstm.jobs.values())
+        t0 = time.perf_counter()
+        loop.run_until_complete(node.tick())
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        bd = {kk: round(v, 3) for kk, v in lstm.timings.items()}
+        bd.update({kk: round(v, 3) for kk, v in node.timings.items()})
+        bd["tick_total_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
+        bd["entities"] = len(lstm.jobs)
+        breakdowns.append(bd)
+        scored.append(n_live)
+
+    def finish():
+        st: Dict[str, int] = {}
+        tp = fp = fn = 0
+        for jid, b in truth.items():
+            s = store._docs[jid]["status"]
+            st[s] = st.get(s, 0) + 1
+            hit = s == r.ST_COMPLETED_UNHEALTH
+            tp += b and hit
+            fp += (not b) and hit
+            fn += b and not hit
+        return 0.0, st, {"jobs": len(truth), "injected_jobs": sum(truth.values()), "tp": tp, "fp": fp, "fn": fn,
+                         "recall": round(tp / max(1, tp + fn), 4),
+                         "false_positive_rate": round(fp / max(1, len(truth) - sum(truth.values())), 6)}
+
+    meta = {
+        "model": f"continuous {F}-metric jobs on the production node brain: NodeBrain + LstmMonitor (shared LSTM "
+                 f"autoencoder F={F}, H={lstm.shard.model.H}, window {args.lstm_window}, one DP Adam step per tick, "
+                 f"fused {'fp8' if lstm.shard.fp8 else 'bf16'} MFMA scoring)",
+        "global_batch": n_jobs * F,
+        "seq_len": args.lstm_window,
+        "history": R,
+        "entities": n_jobs,
+        "features": F,
+        "path": "service.register (continuous) -> claim -> resident 7-day history -> per tick: query_range JSON of "
+                "every (app, metric) -> native decode -> ring append -> DP train step -> fused scoring -> verdicts",
+        "pretrain_steps": pre, "pretrain_per_tick": per,
+        "warm_node": "resident 7-day history of every (app, metric) in HBM before the jobs arrive",
+        "setup_s": round(setup_s, 2),
+        "register_s": round(register_s, 3),
+        "jobs_to_brainworker": _brainworker_share(list(store._docs.values()), cfg),
+        "_scored_rows": scored,
+        "_breakdowns": breakdowns,
+        "_arrival_finish": finish,
+    }
+    return tick, torch.zeros((1, 2), dtype=torch.int32), meta, "bf16" if dev.type == "cuda" else "fp32", n_jobs * F
