@@ -688,7 +688,10 @@ class RolloutMonitor:
                 from ..ops import kernels as K
                 out = K.bivariate(xa, xb, head, length, torch.full((k, 1, 2), float("nan"), device=dev),
                                   torch.ones(k, device=dev), min_valid=self.cfg.min_historical_points)
-                mean, cov, count = out["mean"], out["cov"], out["count"]
+                mean, cov = out["mean"], out["cov"]
+                # jointly valid history points (the kernel's "count" is its count of anomalous current points)
+                idx = (torch.arange(length, device=dev) + head) % xa.shape[1]
+                count = (~(torch.isnan(xa.index_select(1, idx)) | torch.isnan(xb.index_select(1, idx)))).sum(1)
             else:
                 idx = (torch.arange(length) + head) % xa.shape[1]
                 fit = biv_ref.fit_bivariate(torch.stack([xa.index_select(1, idx), xb.index_select(1, idx)], 2))
