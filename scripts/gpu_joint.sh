@@ -19,6 +19,8 @@ for s in $STEPS; do
     tests) run joint_tests 600 python -u -m pytest tests/test_rollout_joint.py tests/test_rollout.py tests/test_lstm_monitor.py tests/test_node.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
     burst_auto) run burst_auto 600 python bench.py --config node --steps 8 --warmup 1 --algorithm auto ;;
     arrival) run arrival 900 python bench.py --config node --arrival-per-tick ${J:-2000} --steps ${T:-60} ;;
+    nodelstm) run node_lstm 900 python bench.py --config node-lstm --steps ${T:-30} ;;
+    nodemv) run node_mv 900 python bench.py --config node-lstm --lstm-features 2 --steps ${T:-30} ;;
     arrival_auto) run arrival_auto 900 python bench.py --config node --arrival-per-tick ${J:-2000} --steps ${T:-60} --algorithm auto ;;
   esac
 done
