@@ -201,12 +201,17 @@ class LstmMonitor:
         """RC4: every rank adopts rank 0's weights and optimizer state after the
         node re-formed (a step may have been applied on some ranks only)."""
         if comm.active():
-            for p in self.shard.model.parameters():
-                dist.broadcast(p.data, src=0)
+            # every weight and optimizer tensor in flight at once, each waited for with the
+            # exchange deadline: a peer lost here raises CollectiveTimeout (the node re-forms)
+            works = [(dist.broadcast(p.data, src=0, async_op=True), "weights")
+                     for p in self.shard.model.parameters()]
             for st in self.shard.trainer.opt.state.values():
                 for v in st.values():
                     if torch.is_tensor(v):
-                        dist.broadcast(v.data if v.device == self.device else v, src=0)
+                        works.append((dist.broadcast(v.data if v.device == self.device else v, src=0,
+                                                     async_op=True), "optimizer state"))
+            for w, what in works:
+                comm.wait_bounded(w, self.exchange_timeout, f"re-formation broadcast of the LSTM {what}")
             self.shard.packed = None
         self._digest = None
 

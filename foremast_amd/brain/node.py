@@ -130,17 +130,31 @@ class NodeBrain:
         return out
 
     def _after_reform(self, before: List[str]) -> None:
-        gone = set(before) - set(self.world.members)
-        self.dead |= {worker_id_of(m) + sfx for m in gone for sfx in self._suffixes()}
-        moved = sum(m.release(lambda d, o=self._owns_for(m): not o(d)) for m in self.monitors)
+        """The node re-formed: dead members' leases become stealable, jobs whose owner
+        moved are released, per-generation stores are reset, and the monitors' re-formation
+        collectives (the LSTM replicas adopt rank 0's weights, RC4) run under the world's
+        deadline-and-re-form guard — a member lost during them re-forms the node again,
+        and this repeats over the newer membership."""
+        gen = None
+        while gen != self.world.generation:
+            gen = self.world.generation
+            members = list(self.world.members)
+            gone = set(before) - set(members)
+            self.dead |= {worker_id_of(m) + sfx for m in gone for sfx in self._suffixes()}
+            moved = sum(m.release(lambda d, o=self._owns_for(m): not o(d)) for m in self.monitors)
+            for m in self.monitors:
+                if getattr(m, "router", None) is not None:
+                    m.router.reset(kv=dist.PrefixStore("affine", self.world.pstore))
+            self.health.reset(kv=self.world.pstore)
+            log.warning("node re-formed: generation %d, members %s (lost %s); released %d moved jobs",
+                        self.world.generation, members, sorted(gone), moved)
+            self.world.run_tick(self._reform_collectives)
+            before = members
+
+    def _reform_collectives(self) -> None:
         for m in self.monitors:
             if hasattr(m, "after_reform"):
                 m.after_reform()
-            if getattr(m, "router", None) is not None:
-                m.router.reset(kv=dist.PrefixStore("affine", self.world.pstore))
-        self.health.reset(kv=self.world.pstore)
-        log.warning("node re-formed: generation %d, members %s (lost %s); released %d moved jobs",
-                    self.world.generation, self.world.members, sorted(gone), moved)
 
     def app_table(self):
         """(app roster, ``[A, 2]`` device counters, roster version, live series)
