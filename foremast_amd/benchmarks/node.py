@@ -782,7 +782,7 @@ def setup_node_lstm(args, world, rank, dev):
 
     def tick(k):
         clock["t"] = T0 + STEP * k
-        n_live = sum(len(e.feats) for e in lstm.jobs.values())
+        n_live = lstm._n_series
         t0 = time.perf_counter()
         loop.run_until_complete(node.tick())
         if dev.type == "cuda":

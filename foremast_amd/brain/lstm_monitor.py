@@ -138,6 +138,8 @@ class LstmMonitor:
         self._pending_cal = False   # some rank admitted entities while the model was pretraining
         self._pretraining = False
         self._calibrated = np.zeros(self.shard.n, dtype=bool)
+        self._row_end = np.full(self.shard.n, np.inf)   # endTime per row (inf: free, external or open-ended)
+        self._n_series = 0
         # the weights' CRC in the node table: every digest_every ticks and after a re-formation
         self.digest_every = int(os.environ.get("FOREMAST_LSTM_DIGEST_EVERY", "60"))
         self._digest: Optional[str] = None
@@ -222,6 +224,7 @@ class LstmMonitor:
         self.history.unwant([k for _, k in e.feats], now)
         if e.row >= 0:
             self._free_row(e.row)
+            self._n_series -= len(e.feats)
 
     @property
     def n_live(self) -> int:
@@ -238,10 +241,12 @@ class LstmMonitor:
         pd[:n] = self.padded
         self.feat_rows, self.padded = fr, pd
         self._calibrated = np.concatenate([self._calibrated, np.zeros(cap - n, dtype=bool)])
+        self._row_end = np.concatenate([self._row_end, np.full(cap - n, np.inf)])
 
     def _free_row(self, row: int) -> None:
         self.row_job[row] = None
         self._calibrated[row] = False
+        self._row_end[row] = np.inf
         self.feat_rows[row] = -1
         self.padded[row] = False
         self.shard.app_id[row] = 0
@@ -281,6 +286,8 @@ class LstmMonitor:
             e.row = row
             self.jobs[e.doc["id"]] = e
             self.row_job[row] = e.doc["id"]
+            self._row_end[row] = np.inf if e.external else e.end_ts
+            self._n_series += len(e.feats)
             rows.append(row)
             for f, (_, k) in enumerate(e.feats):
                 fr[i, f] = hist.row_of(k)
@@ -394,12 +401,20 @@ class LstmMonitor:
             return written
         out = self.shard.score()
         v = out["verdict"].cpu().numpy()
-        newest = self._newest()
+        n = len(v)
+        # only rows that flag or reach their endTime are visited (entities admitted while the
+        # model was pretraining are scored once calibrated)
+        cal = self._calibrated[:n]
+        hit = (v == 1) & cal
+        rows = np.nonzero(hit | (cal & (self._row_end[:n] <= now)))[0]
+        newest = self._newest() if hit.any() else None
         items = []
         self.hits = {}
-        for jid, e in list(self.jobs.items()):
-            if not self._calibrated[e.row]:
-                continue  # admitted while the model was pretraining: scored once calibrated
+        for row in rows.tolist():
+            jid = self.row_job[row]
+            e = self.jobs.get(jid) if jid is not None else None
+            if e is None:
+                continue
             if e.external:  # the rollout engine owns the job: it reads the verdict back
                 if v[e.row] == 1:
                     self.hits[jid] = (self.history.t_last, newest[e.row])
@@ -423,7 +438,7 @@ class LstmMonitor:
                     self.metrics.jobs.labels(status=fields["status"]).inc()
                 self._drop(jid, now)
         self.ticks += 1
-        self.metrics.series_scored.inc(sum(len(e.feats) for e in self.jobs.values()))
+        self.metrics.series_scored.inc(self._n_series)
         self.timings["tick_ms"] = (time.perf_counter() - t0) * 1e3
         return written
 

@@ -59,6 +59,8 @@ class ClusterHealth:
         self._versions: Optional[List[int]] = None
         self._rosters: List[Dict[str, Any]] = []
         self._published: Optional[int] = None
+        self._mine: Optional[Dict[str, Any]] = None   # roster record of _mine_version
+        self._mine_version: Optional[int] = None
         self.roster_exchanges = 0
         self.last_ms = 0.0
 
@@ -95,7 +97,12 @@ class ClusterHealth:
         send[:HDR].copy_(hdr.to(self.device, non_blocking=True))
         if k:
             send[HDR:HDR + 2 * k].copy_(counts[:k].reshape(-1))
-        mine = dict(info or {}, names=[list(n) if n else None for n in names], version=roster_version)
+        # this rank's roster record, built only when the roster changed (O(apps) per change,
+        # not per tick: a node holds tens of thousands of apps)
+        if self._mine is None or self._mine_version != roster_version:
+            self._mine = {"names": [list(n) if n else None for n in names], "version": roster_version}
+            self._mine_version = roster_version
+        mine = dict(info or {}, **self._mine)
         if self.kv is not None and comm.active(self.group) and self._published != roster_version:
             # publish before the gather that announces the version: a peer that sees it can read it
             self.kv.set(f"roster/{rank}/{roster_version}", json.dumps(mine))

@@ -34,14 +34,18 @@ def main() -> None:
         del argv[i:i + 2]
     os.makedirs(out, exist_ok=True)
     warm = [] if "--warmup" in argv else ["--warmup", "1"]
-    sys.argv = ["bench.py", "--config", "node", "--steps", str(ticks)] + warm + argv
+    lstm = "--lstm" in argv
+    argv = [a for a in argv if a != "--lstm"]
+    sys.argv = ["bench.py", "--config", "node-lstm" if lstm else "node", "--steps", str(ticks)] + warm + argv
     import torch
 
     import bench
     args = bench.parse()
     world, rank, dev = bench.init_dist(args)
-    from foremast_amd.benchmarks.node import setup_arrival, setup_node
+    from foremast_amd.benchmarks.node import setup_arrival, setup_node, setup_node_lstm
     setup = setup_arrival if getattr(args, "arrival_per_tick", 0) else setup_node
+    if lstm:
+        setup = setup_node_lstm
     tick, _health, meta, _dt, _n = setup(args, world, rank, dev)
     for k in range(args.warmup):
         tick(k)
