@@ -136,6 +136,12 @@ def parse():
                         "lstm = config 3; multivariate = config 5 (fp8 LSTM, latency + error-rate); node = the product "
                         "path: canary jobs registered through the service and scored by the production node brain "
                         "from Prometheus JSON (foremast_amd/benchmarks/node.py)")
+    p.add_argument("--cold", action="store_true",
+                   help="node config: a cold node -- only --cold-warm-jobs apps are resident; the week of every other "
+                        "(app, metric) loads from Prometheus JSON through the node's history path, within "
+                        "--cold-budget-s per tick, while the warm jobs keep scoring (record under config.cold)")
+    p.add_argument("--cold-warm-jobs", type=int, default=2000)
+    p.add_argument("--cold-budget-s", type=float, default=2.0)
     p.add_argument("--arrival-per-tick", type=int, default=0,
                    help="node config: steady arrivals -- this many canary rollouts start every minute and finish at "
                         "endTime (--window minutes later); ~J x window jobs live at steady state "

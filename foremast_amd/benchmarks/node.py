@@ -75,9 +75,15 @@ class BodyServer:
         self.fragments: Dict[Tuple[str, float], Dict[str, str]] = {}
         self.requests = 0
         self.bytes_served = 0
+        # cold node: week loads rendered on request -- history(metric, apps, start, n) -> body
+        self.history = None
+        self.serve_s = 0.0
 
     async def fetch_raw_many(self, urls) -> List[object]:
-        return [self._one(u) for u in urls]
+        t0 = time.perf_counter()
+        out = [self._one(u) for u in urls]
+        self.serve_s += time.perf_counter() - t0
+        return out
 
     def _one(self, url: str):
         self.requests += 1
@@ -86,8 +92,11 @@ class BodyServer:
             body = self.tick_bodies.get((unquote(q), end), _body([]))
         else:
             name = unquote(q.split("%7B", 1)[0])
-            frags = self.fragments.get((name, start), {})
-            body = _body([frags[p] for p in _encoded_pods(q) if p in frags])
+            if self.history is not None and name.startswith("namespace_app_per_pod:"):
+                body = self.history(name, _encoded_values(q, "app"), start, int(round((end - start) / STEP)) + 1)
+            else:
+                frags = self.fragments.get((name, start), {})
+                body = _body([frags[p] for p in _encoded_pods(q) if p in frags])
         self.bytes_served += len(body)
         return body
 
@@ -104,11 +113,29 @@ def _brainworker_share(docs, cfg) -> int:
                if p is None and not (is_continuous(d) and lstm_features(d, cfg) is not None))
 
 
+def _cold_record(st, intake_s, standin_s, ticks, n_cold, M, R, n_warm) -> Dict:
+    """Cold-node history ingest: the week of n_cold x M series loaded from Prometheus
+    JSON by the node's history path while its warm jobs keep scoring."""
+    brain_s = intake_s - standin_s
+    return {"cold_jobs": n_cold, "warm_jobs": n_warm, "series": n_cold * M, "points_per_series": R,
+            "json_gb": round(st["body_bytes"] / 1e9, 3),
+            "decode_gb_per_s": round(st["body_bytes"] / 1e9 / max(st["decode_s"], 1e-9), 2),
+            "decode_s": round(st["decode_s"], 3),
+            "h2d_gb_per_s": round(st["h2d_bytes"] / 1e9 / max(st["h2d_s"], 1e-9), 2),
+            "load_batches": st["batches"],
+            "seconds_to_admission_brain": round(brain_s, 2),
+            "seconds_to_admission_wall": round(intake_s, 2),
+            "standin_render_s": round(standin_s, 2),
+            "intake_ticks": len(ticks) + 1,
+            "ticks": ticks}
+
+
 def setup_node(args, world, rank, dev):
     from ..brain.node import NodeBrain, owner_of
     from ..brain.rollout import RolloutMonitor
     from ..brain.streaming import StreamingMonitor
     from ..brain.engine import synthetic_eval, synthetic_params
+    from ..ingest import native
     from ..api import crd
     from ..api import rest as r
     from ..controller import queries
@@ -166,14 +193,39 @@ def setup_node(args, world, rank, dev):
     keys = [(ENDPOINT, "namespace_app_per_pod:" + m, ns[i], app[i]) for i in range(na) for m in METRICS]
     hist = roll.history
     hist.clock = lambda: clock["t"]
-    hist.want(keys, T0)
+    # --cold: only the first cold_warm apps are resident; the week of every other (app, metric)
+    # is loaded through the node's history path from Prometheus JSON (rendered on request)
+    n_warm = na if not getattr(args, "cold", False) else min(na, int(args.cold_warm_jobs))
+    warm_keys = keys[:n_warm * M]
+    hist.want(warm_keys, T0)
     asyncio.run(hist.assign_only(T0))
     dparams = {k: v.to(dev) for k, v in params.items()}
-    for c0 in range(0, len(keys), 16384):
-        c1 = min(len(keys), c0 + 16384)
+    for c0 in range(0, len(warm_keys), 16384):
+        c1 = min(len(warm_keys), c0 + 16384)
         sub = {k: v[c0:c1] for k, v in dparams.items()}
-        hist.load_rows(keys[c0:c1], synthetic_eval(sub, 0, R, season, noise_seed=4321 + c0))
-    hist.unwant(keys, T0)  # retained for retain_s after their last job: the jobs re-reference them
+        hist.load_rows(warm_keys[c0:c1], synthetic_eval(sub, 0, R, season, noise_seed=4321 + c0))
+    hist.unwant(warm_keys, T0)  # retained for retain_s after their last job: the jobs re-reference them
+    if n_warm < na:
+        if args.cold_budget_s > 0:
+            hist.load_budget_s = args.cold_budget_s
+        row_of = {(f"namespace_app_per_pod:{m}", app[i]): i * M + j for i in range(na) for j, m in enumerate(METRICS)}
+        lab_of = {(f"namespace_app_per_pod:{m}", app[i]): f'"__name__":"namespace_app_per_pod:{m}","namespace":'
+                                                         f'"{ns[i]}","app":"{app[i]}"'
+                  for i in range(na) for m in METRICS}
+
+        def history(name, apps, start, n):
+            """The week of the named apps as query_range JSON (model time R - 1 is T0)."""
+            hit = [(row_of[(name, a)], lab_of[(name, a)]) for a in apps if (name, a) in row_of]
+            if not hit:
+                return _body([])
+            rr = torch.tensor([h for h, _ in hit])
+            sub = {k: v[rr] for k, v in params.items()}
+            t0c = int(round((start - T0) / STEP)) + R - 1
+            # noise seeded by the time chunk: a seed repeated per chunk would repeat the noise with
+            # the season's period, which a seasonal model fits exactly
+            vals = synthetic_eval(sub, t0c, n, season, noise_seed=4321 + t0c).numpy()
+            return native.render_matrix(native.label_blob([lab for _, lab in hit]), vals, start, STEP)
+        server.history = history
 
     # --- Prometheus bodies -------------------------------------------------------------------
     # the newest point of minute T0 + 60 k is model time R - 1 + k; the job's baseline window
@@ -248,10 +300,27 @@ def setup_node(args, world, rank, dev):
     if dev.type == "cuda":
         torch.cuda.synchronize()
     t0 = time.perf_counter()
+    cold_ticks: List[Dict[str, float]] = []
+    cold = n_warm < na
+    serve0 = server.serve_s
     run_tick()
     if dev.type == "cuda":
         torch.cuda.synchronize()
+    if cold:
+        # the node keeps ticking while the week loads: every intake loads within its budget and
+        # admits the jobs whose history is complete; the admitted jobs are scored every tick
+        for k in range(1, 100000):  # (the intake ticks stay at the deploy minute: no window time passes)
+            st = dict(hist.load_stats)
+            cold_ticks.append({"tick": k - 1, "admitted_total": len(roll.jobs), "live_rows": roll.n_live,
+                               **{kk: round(v, 3) for kk, v in node.timings.items()}})
+            if len(roll.jobs) == na:
+                break
+            clock["t"] = T0 + STEP * 0  # the intake ticks all run at the deploy minute
+            run_tick()
+            if dev.type == "cuda":
+                torch.cuda.synchronize()
     intake_s = time.perf_counter() - t0
+    standin_s = server.serve_s - serve0
     assert len(roll.jobs) == na, f"admitted {len(roll.jobs)} of {na} jobs"
     intake_timings = dict(roll.timings)
 
@@ -323,6 +392,8 @@ def setup_node(args, world, rank, dev):
         "jobs_to_brainworker": n_worker,
         "intake_s": round(intake_s, 3),
         "intake_breakdown_ms": {k: round(v, 2) for k, v in intake_timings.items()},
+        **({"cold": _cold_record(hist.load_stats, intake_s, standin_s, cold_ticks, na - n_warm, M, R, n_warm)}
+           if cold else {}),
         "_scored_rows": scored,
         "_breakdowns": breakdowns,
         "_finish": finish,
@@ -355,10 +426,16 @@ def _split_range_url(url: str) -> Tuple[str, float, float]:
 
 def _encoded_pods(q: str) -> List[str]:
     """Pod names of an encoded ``pod=~"a|b"`` matcher."""
-    i = q.find("pod%3D~%22")
+    return _encoded_values(q, "pod")
+
+
+def _encoded_values(q: str, label: str) -> List[str]:
+    """Values of an encoded ``<label>=~"a|b"`` matcher."""
+    key = label + "%3D~%22"
+    i = q.find(key)
     if i < 0:
         return []
-    body = q[i + 10:q.find("%22", i + 10)]
+    body = q[i + len(key):q.find("%22", i + len(key))]
     return [unquote(p) if "%" in p else p for p in body.split("%7C")]
 
 

@@ -31,6 +31,7 @@ from __future__ import annotations
 import asyncio
 import collections
 import logging
+import os
 import re
 import time
 from typing import Dict, Iterable, List, Optional, Sequence, Set, Tuple
@@ -179,6 +180,14 @@ class ResidentHistory:
         self.tick_queries = 0
         self.failed_queries = 0
         self.reloads = 0
+        # cold loads: at most load_budget_s of week loads per call (in batches of load_batch
+        # keys), the rest stays pending for the next tick, so a node filling up with
+        # thousands of new apps keeps scoring the jobs it already holds every tick
+        self.load_batch = max(1, int(os.environ.get("FOREMAST_HISTORY_LOAD_BATCH", "4096")))
+        env_budget = os.environ.get("FOREMAST_HISTORY_LOAD_BUDGET_S", "")
+        self.load_budget_s: Optional[float] = float(env_budget) if env_budget else None
+        self.load_stats = {"keys": 0, "body_bytes": 0, "fetch_s": 0.0, "decode_s": 0.0, "h2d_s": 0.0, "h2d_bytes": 0,
+                           "batches": 0}
 
     # ------------------------------------------------------------------ references
     def key_hash(self, k: Key) -> int:
@@ -341,14 +350,20 @@ class ResidentHistory:
         if load:
             await self.load_pending(now)
 
-    async def load_pending(self, now: Optional[float] = None) -> None:
-        """Free expired rows, give pending keys rows and load their week."""
+    async def load_pending(self, now: Optional[float] = None, budget_s: Optional[float] = None) -> None:
+        """Free expired rows, give pending keys rows and load their week: batches of
+        ``load_batch`` keys while the time budget (``budget_s`` / ``load_budget_s``,
+        None: no limit) lasts; keys left over stay pending for the next call."""
         now = self.clock() if now is None else now
         if self.t_last == 0.0:
             self.t_last = float(np.floor(now / self.step) * self.step)
         todo = self._assign(now)
-        if todo:
-            await self._load(todo)
+        budget = self.load_budget_s if budget_s is None else budget_s
+        t0 = time.perf_counter()
+        for i in range(0, len(todo), self.load_batch):
+            await self._load(todo[i:i + self.load_batch])
+            if budget is not None and time.perf_counter() - t0 >= budget:
+                break
 
     async def _advance(self, t_new: float) -> None:
         n_new = int(round((t_new - self.t_last) / self.step))
@@ -411,16 +426,28 @@ class ResidentHistory:
                     tabs.append(table)
                     groups.append([k for k, _ in grp])
         self.history_queries += len(reqs)
-        ok = await fetch_decode(self.prom, reqs, tabs, block, self.step, self.decode_threads)
+        tm: Dict[str, float] = {}
+        ok = await fetch_decode(self.prom, reqs, tabs, block, self.step, self.decode_threads, timings=tm)
         failed: Set[Key] = set()
         for good, keys in zip(ok, groups):
             if not good:
                 failed.update(keys)
         self.failed_queries += ok.count(False)
         rows = torch.tensor([row for _, row in todo], dtype=torch.long)
+        t0 = time.perf_counter()
         self._write_rows(rows, block_t)
-        failed_rows = {row for k, row in todo if k in failed}
-        self.pending = {h for h in self.pending if self.rows.get(h) in failed_rows}
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
+        st = self.load_stats
+        st["h2d_s"] += time.perf_counter() - t0
+        st["h2d_bytes"] += int(block_t.numel()) * 4
+        st["keys"] += len(todo) - len(failed)
+        st["body_bytes"] += int(tm.get("body_mb", 0.0) * 1e6)
+        st["fetch_s"] += tm.get("fetch_ms", 0.0) / 1e3
+        st["decode_s"] += tm.get("native_ms", 0.0) / 1e3
+        st["batches"] += 1
+        # this batch's keys are loaded, except those of a failed query (retried next call)
+        self.pending -= {self.key_hash(k) for k, _row in todo if k not in failed}
 
     def _write_rows(self, rows: torch.Tensor, values: torch.Tensor) -> None:
         """``values [k, R]`` oldest first into the rotated ring (two column slices)."""
