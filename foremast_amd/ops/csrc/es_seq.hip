@@ -84,12 +84,15 @@ template <int MODE, typename TIN, int TPC, bool PARTIAL>
 __global__ __launch_bounds__(256) void es_seq_kernel(const SmoothArgs a) {
   constexpr int SW = 256 / TPC;             // series per workgroup
   constexpr int PER = SW * ES_TC / 256;     // staged elements per thread per chunk
+  // double-buffered tile (one barrier per chunk) when it stays small: <= 64 series, 33 KB;
+  // the 128-series single tile keeps four workgroups on a CU
+  constexpr int NB = SW <= 64 ? 2 : 1;
   const int tid = threadIdx.x;
   const int s = tid / TPC, gp = tid - s * TPC;
   const int n0 = PARTIAL ? 0 : min((int)blockIdx.x * SW, a.N - SW);
   const int n = n0 + s;
-  float* tile = (float*)fm_es_smem;               // [SW][ES_LD]  the chunk being walked
-  int* nanc = (int*)(tile + SW * ES_LD);          // [SW]         missing points of the chunk
+  float* tiles = (float*)fm_es_smem;              // [NB][SW][ES_LD]  chunks (walked / being staged)
+  int* nancs = (int*)(tiles + NB * SW * ES_LD);   // [NB][SW]         missing points of each chunk
   const int T = a.T, R = a.ring_len;
   const int nch = (T + ES_TC - 1) / ES_TC;
   const TIN* base = (const TIN*)a.hist;
@@ -129,6 +132,8 @@ __global__ __launch_bounds__(256) void es_seq_kernel(const SmoothArgs a) {
   };
   // chunk ch into the tile; steps past T become 0 (not NaN: never walked or counted)
   auto store_chunk = [&](int ch, const unsigned (&v)[PER]) {
+    float* tile = tiles + (ch % NB) * SW * ES_LD;
+    int* nanc = nancs + (ch % NB) * SW;
     const int t = tid % ES_TC;
     const bool okt = ch * ES_TC + t < T;
 #pragma unroll
@@ -150,12 +155,15 @@ __global__ __launch_bounds__(256) void es_seq_kernel(const SmoothArgs a) {
   v2f l = splat2(0.f), b = splat2(0.f), sse = splat2(0.f);
   bool started = false;
   int nv = 0;
-  const float* row = tile + s * ES_LD;
-  // walk chunk ch from the tile while nx (chunk ch + 1) and pf (chunk ch + 2) load
+  // walk chunk ch from its tile while nx (chunk ch + 1) and pf (chunk ch + 2) load
   auto body = [&](int ch, unsigned (&nx)[PER], unsigned (&pf)[PER]) {
     load_chunk(ch + 2, pf);
+    // double-buffered: chunk ch + 1 goes to the other tile now (its last reader, the walk
+    // of chunk ch - 1, finished before the previous barrier)
+    if (NB == 2 && ch + 1 < nch) store_chunk(ch + 1, nx);
+    const float* row = tiles + (ch % NB) * SW * ES_LD + s * ES_LD;
     const int nt = min(ES_TC, T - ch * ES_TC);
-    const int miss = nanc[s];
+    const int miss = nancs[(ch % NB) * SW + s];
     nv += nt - miss;
     if (miss == 0 && !started) {
       l = splat2(row[0]);
@@ -163,9 +171,11 @@ __global__ __launch_bounds__(256) void es_seq_kernel(const SmoothArgs a) {
     }
     if (__all(miss == 0)) es_walk<MODE, false>(row, nt, al, c2, l, b, sse, started);
     else es_walk<MODE, true>(row, nt, al, c2, l, b, sse, started);
-    __syncthreads();                                // tile and counts free
-    if (ch + 1 < nch) store_chunk(ch + 1, nx);
-    __syncthreads();
+    __syncthreads();                                // tile and counts free (NB = 2: chunk ch + 1 staged)
+    if (NB == 1) {
+      if (ch + 1 < nch) store_chunk(ch + 1, nx);
+      __syncthreads();
+    }
   };
   for (int ch = 0; ch < nch; ch += 2) {
     body(ch, va, vb);
@@ -194,7 +204,8 @@ __global__ __launch_bounds__(256) void es_seq_kernel(const SmoothArgs a) {
 template <int MODE, typename TIN>
 hipError_t launch_es(const SmoothArgs& a, int tpc, hipStream_t st) {
   const int sw = 256 / tpc;
-  const size_t lds = (size_t)sw * ES_LD * 4 + (size_t)sw * 4;
+  const int nb = sw <= 64 ? 2 : 1;  // the kernel's NB
+  const size_t lds = (size_t)nb * sw * ES_LD * 4 + (size_t)nb * sw * 4;
   const dim3 grid((a.N + sw - 1) / sw), block(256);
   if (a.N < sw) {
     switch (tpc) {

@@ -17,9 +17,10 @@ run() {
 STEPS=${STEPS:-"tests ab"}
 for s in $STEPS; do
   case $s in
-    tests) run tests 600 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread -k "hw or holt or smoothing" ;;
+    tests) run tests 600 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread -k "hw or holt or smoothing or es_ or des or decompose" ;;
     ab) run ab 600 python scripts/hw_prune_ab.py --iters ${ITERS:-8} ${AB_ARGS:-} ;;
     abmix) run abmix 600 python scripts/hw_prune_ab.py --iters ${ITERS:-8} --mix ${AB_ARGS:-} ;;
+    kern) run kern 600 python scripts/bench_kernels.py --only es,decompose --variants "" --rounds 3 ;;
     canary) run canary 600 python bench.py --steps 20 --warmup 5 ;;
     canary6) FOREMAST_HW_WAVES=6 run canary6 600 python bench.py --steps 20 --warmup 5 ;;
   esac
