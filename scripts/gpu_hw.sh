@@ -22,6 +22,5 @@ for s in $STEPS; do
     abmix) run abmix 600 python scripts/hw_prune_ab.py --iters ${ITERS:-8} --mix ${AB_ARGS:-} ;;
     kern) run kern 600 python scripts/bench_kernels.py --only es,decompose --variants "" --rounds 3 ;;
     canary) run canary 600 python bench.py --steps 20 --warmup 5 ;;
-    canary6) FOREMAST_HW_WAVES=6 run canary6 600 python bench.py --steps 20 --warmup 5 ;;
   esac
 done
