@@ -165,6 +165,64 @@ inline bool fast_decimal(const char* p, const char* b, double& out) {
   return true;
 }
 
+// ---- 8 digits at a time (SWAR) ------------------------------------------------
+constexpr uint64_t kOnes = 0x0101010101010101ull;
+constexpr uint64_t kPow10u[9] = {1, 10, 100, 1000, 10000, 100000, 1000000, 10000000, 100000000};
+
+// k (1..8) ASCII digits ending at `end`, read as one 8-byte load from end - 8
+// (the caller guarantees those bytes exist); false unless all k are digits.
+inline bool digits8(const char* end, int k, uint64_t& out) {
+  uint64_t x;
+  memcpy(&x, end - 8, 8);
+  const int sh = 8 * (8 - k);  // the leading 8 - k bytes (low bytes, little endian) read as '0'
+  const uint64_t keep = sh ? ~0ull << sh : ~0ull;
+  x = (x & keep) | (0x30 * kOnes & ~keep);
+  // every byte in '0'..'9': high nibble 3, and adding 6 does not carry out of the low nibble
+  if ((x & 0xF0 * kOnes) != 0x30 * kOnes || ((x + 6 * kOnes) & 0xF0 * kOnes) != 0x30 * kOnes) return false;
+  x -= 0x30 * kOnes;
+  x = x * 10 + (x >> 8);  // pairs
+  x = (((x & 0x000000FF000000FFull) * (100 + (1000000ull << 32))) +
+       (((x >> 16) & 0x000000FF000000FFull) * (1 + (10000ull << 32)))) >> 32;
+  out = x;
+  return true;
+}
+
+// fast_decimal for the common shape — [-]int[.frac] in <= 16 bytes, <= 8
+// fraction digits — without a loop per digit: the same mantissa and power of
+// ten, so the same double (one correctly rounded division).  Reads the 16
+// bytes ending at b, so needs p - lo >= 16 (lo: start of the buffer); false =
+// use fast_decimal / from_chars.
+inline bool swar_decimal(const char* p, const char* b, const char* lo, double& out) {
+  bool neg = false;
+  if (p < b && *p == '-') { neg = true; ++p; }
+  const long long n = b - p;
+  if (n <= 0 || n > 16 || p - lo < 16) return false;
+  // the dot among the last n of the 16 bytes ending at b
+  const unsigned dm = (unsigned)_mm_movemask_epi8(
+                          _mm_cmpeq_epi8(_mm_loadu_si128((const __m128i*)(b - 16)), _mm_set1_epi8('.'))) >>
+                      (16 - n);
+  if (dm & (dm - 1)) return false;  // two dots
+  const char* dot = dm ? p + __builtin_ctz(dm) : nullptr;
+  const char* ie = dot ? dot : b;
+  const int ki = (int)(ie - p), kf = dot ? (int)(b - dot - 1) : 0;
+  if (ki + kf == 0 || ki > 16 || kf > 8 || ki + kf > 18) return false;
+  uint64_t ip = 0, fp = 0;
+  if (ki > 8) {
+    uint64_t hi, lo8;
+    if (!digits8(ie - 8, ki - 8, hi) || !digits8(ie, 8, lo8)) return false;
+    ip = hi * 100000000ull + lo8;
+  } else if (ki > 0 && !digits8(ie, ki, ip)) {
+    return false;
+  }
+  if (kf > 0 && !digits8(b, kf, fp)) return false;
+  const uint64_t m = ip * kPow10u[kf] + fp;
+  if (m > (1ull << 53)) return false;
+  double v = (double)m;
+  if (kf) v /= kPow10[kf];
+  out = neg ? -v : v;
+  return true;
+}
+
 bool parse_number(const char* a, const char* b, double& out) {
   while (a < b && (*a == ' ' || *a == '"')) ++a;
   while (b > a && (b[-1] == ' ' || b[-1] == '"')) --b;
@@ -522,7 +580,57 @@ struct KeyedOut {
   float* out;
   long long ld, max_rows;
   Label la, lb;
+  const char* lo;  // start of the body (swar_decimal reads up to 8 bytes before a number)
 };
+
+// Timestamp text -> grid column by the sample's ordinal in its series: every
+// series of a range response carries the same timestamps, so point j of a
+// series almost always repeats the text of point j of the previous one.  One
+// per decoding thread, reset per chunk (a chunk has one grid).
+struct TsCache {
+  struct Ent {
+    char txt[23];
+    uint8_t len;  // 0: empty
+    int8_t ok;
+    long long col;
+  };
+  static constexpr long long kCap = 1 << 14;
+  std::vector<Ent> ents;
+  long long used = 0;
+  void reset() {
+    for (long long i = 0; i < used; ++i) ents[i].len = 0;
+    used = 0;
+  }
+  // point `j` of a series starting at `a`: on a hit, the column and the end of the text
+  const Ent* hit(long long j, const char* a, const char* e) const {
+    if (j >= used) return nullptr;
+    const Ent& t = ents[j];
+    if (!t.len || e - a <= t.len) return nullptr;
+    if (t.len < 16 && e - a >= 16) {  // text and its ',' in one 16-byte compare
+      const unsigned eq = (unsigned)_mm_movemask_epi8(
+          _mm_cmpeq_epi8(_mm_loadu_si128((const __m128i*)a), _mm_loadu_si128((const __m128i*)t.txt)));
+      const unsigned want = (2u << t.len) - 1;
+      return (eq & want) == want ? &t : nullptr;
+    }
+    return a[t.len] == ',' && memcmp(a, t.txt, t.len) == 0 ? &t : nullptr;
+  }
+  void put(long long j, const char* a, long long n, long long col, bool ok) {
+    if (j >= kCap || n <= 0 || n >= (long long)sizeof(Ent::txt)) return;
+    if ((long long)ents.size() <= j) ents.resize((size_t)std::min(kCap, 2 * j + 64));
+    while (used <= j) ents[used++].len = 0;
+    Ent& t = ents[j];
+    memcpy(t.txt, a, (size_t)n);
+    t.txt[n] = ',';  // n < sizeof(txt): the separator that follows, compared with the text
+    t.len = (uint8_t)n;
+    t.ok = ok;
+    t.col = col;
+  }
+};
+
+TsCache& ts_cache() {
+  thread_local TsCache c;
+  return c;
+}
 
 struct KeyedCounts {
   long long series = 0, dropped = 0, unmatched = 0;
@@ -536,9 +644,9 @@ struct KeyedCounts {
 // overlaps the sample parsing.
 long long keyed_elements(Cursor& c, const char* stop, const KeyedOut& o, KeyIndex& ix, KeyedCounts& k) {
   long long prev_slot = -1;  // slot of the previous element of this chunk (-1: unknown / not flat)
-  const char* ts_txt = nullptr;  // last parsed timestamp text and its grid column
-  long long ts_len = 0, ts_col = 0;
-  bool ts_ok = false;
+  TsCache& tsc = ts_cache();
+  tsc.reset();
+  const bool swar_ok = o.lo != nullptr;
   while (true) {
     if (!c.eat('{')) return -4;
     long long row = -1, cur_slot = -1;
@@ -612,38 +720,59 @@ long long keyed_elements(Cursor& c, const char* stop, const KeyedOut& o, KeyInde
         if (many && !c.eat('[')) return -7;
         c.ws();
         if (!(many && c.eat(']'))) {
-          while (true) {
-            if (!c.eat('[')) return -8;
-            c.ws();
-            const char* a = c.p;
-            while (c.p < c.e && *c.p != ',') ++c.p;
-            // every series of a tick carries the same timestamps: reuse the grid
-            // column of the last timestamp text when the bytes repeat
+          for (long long pt = 0;; ++pt) {
+            // every series of a response carries the same timestamps: point pt
+            // reuses the grid column of point pt of the previous series when the
+            // bytes repeat
             long long gi;
             bool on_grid;
-            if (ts_len > 0 && c.p - a == ts_len && memcmp(a, ts_txt, (size_t)ts_len) == 0) {
-              gi = ts_col;
-              on_grid = ts_ok;
-            } else {
-              double ts;
-              if (!parse_number(a, c.p, ts)) return -9;
-              const double fi = (ts - o.start) / o.step;
-              gi = (long long)llround(fi);
-              on_grid = !(gi < 0 || gi >= o.T || std::fabs(fi - (double)gi) > 1e-6);
-              if (c.p - a <= 32) { ts_txt = a; ts_len = c.p - a; ts_col = gi; ts_ok = on_grid; }
-            }
-            if (!c.eat(',')) return -10;
-            c.ws();
-            const char* v0 = c.p;
-            if (c.p >= c.e) return -11;
-            if (*c.p == '"') { if (!skip_string(c)) return -11; } else { while (c.p < c.e && *c.p != ']') ++c.p; }
             double v;
-            if (!parse_number(v0, c.p, v)) return -12;
-            if (!c.eat(']')) return -13;
+            const TsCache::Ent* t;
+            const char* q1;
+            if (c.e - c.p > 1 && c.p[0] == '[' && (t = tsc.hit(pt, c.p + 1, c.e)) && c.e - c.p > t->len + 3 &&
+                c.p[t->len + 2] == '"' && (q1 = find_quote_or_bs(c.p + t->len + 3, c.e)) < c.e - 1 &&
+                *q1 == '"' && q1[1] == ']') {
+              // compact [ts,"v"] with a known timestamp: no whitespace or token walk
+              const char* q0 = c.p + t->len + 3;
+              gi = t->col;
+              on_grid = t->ok;
+              if (!((swar_ok && swar_decimal(q0, q1, o.lo, v)) || parse_number(q0 - 1, q1 + 1, v))) return -12;
+              c.p = q1 + 2;
+            } else {
+              if (!c.eat('[')) return -8;
+              c.ws();
+              const char* a = c.p;
+              if ((t = tsc.hit(pt, a, c.e))) {
+                gi = t->col;
+                on_grid = t->ok;
+                c.p = a + t->len;
+              } else {
+                while (c.p < c.e && *c.p != ',') ++c.p;
+                double ts;
+                if (!((swar_ok && swar_decimal(a, c.p, o.lo, ts)) || parse_number(a, c.p, ts))) return -9;
+                const double fi = (ts - o.start) / o.step;
+                gi = (long long)llround(fi);
+                on_grid = !(gi < 0 || gi >= o.T || std::fabs(fi - (double)gi) > 1e-6);
+                tsc.put(pt, a, c.p - a, gi, on_grid);
+              }
+              if (!c.eat(',')) return -10;
+              c.ws();
+              const char* v0 = c.p;
+              if (c.p >= c.e) return -11;
+              if (*c.p == '"') {
+                if (!skip_string(c)) return -11;
+                if (!((swar_ok && swar_decimal(v0 + 1, c.p - 1, o.lo, v)) || parse_number(v0, c.p, v))) return -12;
+              } else {
+                while (c.p < c.e && *c.p != ']') ++c.p;
+                if (!parse_number(v0, c.p, v)) return -12;
+              }
+              if (!c.eat(']')) return -13;
+            }
             resolve();
             if (row < 0 || !on_grid) ++k.dropped;
             else o.out[row * o.ld + gi] = (float)v;
             if (!many) break;
+            if (c.p < c.e && *c.p == ',') { ++c.p; continue; }
             if (c.eat(',')) continue;
             if (c.eat(']')) break;
             return -14;
@@ -878,7 +1007,8 @@ long long fm_prom_dense_indexed(const char* buf, long long len, double start, do
   if (c.eat(']')) {
     r = 0;
   } else {
-    const KeyedOut o{start, step, T, out, ld, max_rows, {label_a, strlen(label_a)}, {label_b, strlen(label_b)}};
+    const KeyedOut o{start, step, T, out, ld, max_rows, {label_a, strlen(label_a)}, {label_b, strlen(label_b)},
+                     buf};
     r = keyed_elements(c, buf + len + 1, o, *ix, k);
   }
   if (dropped) *dropped = k.dropped;
@@ -1022,7 +1152,7 @@ long long fm_prom_decode_bodies(int nb, const char* const* bufs, const long long
       KeyIndex* ix = (KeyIndex*)index[j];
       Cursor c{tk.p, bufs[j] + lens[j]};
       KeyedCounts k;
-      const KeyedOut o{st_of(j), step, T_of(j), out + c0_of(j), ld, max_rows, la, lb};
+      const KeyedOut o{st_of(j), step, T_of(j), out + c0_of(j), ld, max_rows, la, lb, bufs[j]};
       const long long r = keyed_elements(c, tk.stop, o, *ix, k);
       if (r < 0) { err[j].store(1); continue; }
       tk.end = c.p;

@@ -177,3 +177,40 @@ def test_decode_bodies_matches_per_body_decode_and_learns_layout():
         assert stats[bad][0] < 0
         assert all(s[0] == len(groups[j % 2]) and s[2] == 0 for j, s in enumerate(stats) if j != bad)
         np.testing.assert_array_equal(out, ref)
+
+
+def test_keyed_decoder_number_shapes_match_python_float():
+    """The keyed decoder's number paths — the 8-digits-at-a-time decimal path, the
+    per-digit exact path, ``from_chars``, the special values — and the per-ordinal
+    timestamp cache (compact and spaced samples, repeated and fresh timestamp text)
+    give exactly ``float32(float(text))`` for every sample shape."""
+    from foremast_amd.ingest import native
+    texts = ["12", "-3.5", "0.000123", "5.", ".5", "-0", "00012.50", "1234567890123456", "12345678.12345678",
+             "1e5", "-2.5E-3", "9007199254740993", "NaN", "+Inf", "-Inf", "49.6630936", "-0.000000001",
+             "123456789.5", "7", "99999999.99999999"]
+    t0, step, T = 1_700_000_000, 60.0, len(texts)
+    keys = [("ns", f"app{a}") for a in range(6)]
+    table = native.KeyTable([(k, i) for i, k in enumerate(keys)])
+    items, want = [], np.full((len(keys), T), np.nan, dtype=np.float32)
+    for a in range(len(keys)):
+        rot = texts[a:] + texts[:a]
+        ts_txt = [str(t0 + int(step) * j) if a % 3 else f"{t0 + int(step) * j}.000" for j in range(T)]
+        if a == 4:
+            pts = ", ".join(f'[ {ts_txt[j]} , "{rot[j]}" ]' for j in range(T))
+        else:
+            pts = ",".join(f'[{ts_txt[j]},"{rot[j]}"]' for j in range(T))
+        items.append(f'{{"metric":{{"namespace":"ns","app":"app{a}"}},"values":[{pts}]}}')
+        want[a] = [np.float32(float(x)) for x in rot]
+    body = ('{"status":"success","data":{"resultType":"matrix","result":[' + ",".join(items) + "]}}").encode()
+    for _ in range(2):  # the second pass runs on the learned layout
+        out = np.full_like(want, np.nan)
+        assert native.parse_dense_keyed(body, t0, step, T, out, table) == (len(keys), 0, 0)
+        np.testing.assert_array_equal(out, want)
+        out = np.full_like(want, np.nan)
+        stats = native.decode_bodies([body], [table], [t0], step, [T], [0], out, threads=2)
+        assert stats == [(len(keys), 0, 0)]
+        np.testing.assert_array_equal(out, want)
+    for bad in ("1.2.3", "12a", "-", "."):
+        b = body.replace(b'"49.6630936"', f'"{bad}"'.encode(), 1)
+        with pytest.raises(native.ParseError):
+            native.parse_dense_keyed(b, t0, step, T, np.full_like(want, np.nan), table)
