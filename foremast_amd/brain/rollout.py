@@ -1280,17 +1280,26 @@ class RolloutMonitor:
         lstm_hits = {j: h for j, h in (lstm_hits or {}).items() if j in self.jobs}
         if lstm_hits:
             bad_rows = np.union1d(bad_rows, np.asarray([int(self.jobs[j].rows[0]) for j in lstm_hits], dtype=np.int64))
-        points: Dict[int, List[Tuple[float, float, str]]] = {}
         row_job, jplan = self.row_job, self._jplan
-        for rr, cc, vv in zip(np.asarray(a_rows).tolist(), np.asarray(a_cols).tolist(), np.asarray(a_vals).tolist()):
-            j = row_job[rr]
-            if j < 0:
-                continue
-            p = jplan[j]
-            pc, c = divmod(int(cc), Wc)
-            pods = p.cols.cur_pods(p.s0 + int(self.row_k[rr]))
-            points.setdefault(rr, []).append((float(self.row_cs[rr]) + c * self.step, float(vv),
-                                              pods[pc] if pc < len(pods) else ""))
+        # anomalous points grouped by row in array form, each row's points ordered by
+        # (time, value): its anomaly payload is one slice of an interleaved [t, v, ...] list
+        ar = np.asarray(a_rows, dtype=np.int64)
+        ac = np.asarray(a_cols, dtype=np.int64)
+        av = np.asarray(a_vals, dtype=np.float64)
+        keep = row_job[ar] >= 0 if len(ar) else np.zeros(0, dtype=bool)
+        ar, ac, av = ar[keep], ac[keep], av[keep]
+        pcs, cs = np.divmod(ac, Wc)
+        ts = self.row_cs[ar] + cs * self.step
+        order = np.lexsort((av, ts, ar))
+        ar, ts, av, pcs = ar[order], ts[order], av[order], pcs[order]
+        inter = np.empty(2 * len(ar), dtype=np.float64)
+        inter[0::2], inter[1::2] = ts, av
+        inter_l = inter.tolist()
+        span: Dict[int, Tuple[int, int]] = {}
+        if len(ar):
+            st = np.flatnonzero(np.r_[True, ar[1:] != ar[:-1]])
+            en = np.r_[st[1:], len(ar)]
+            span = dict(zip(ar[st].tolist(), zip(st.tolist(), en.tolist())))
         finish: Dict[str, Tuple[str, str, Optional[Dict]]] = {}
         for rr in bad_rows.tolist():
             j = row_job[rr]
@@ -1316,13 +1325,17 @@ class RolloutMonitor:
                     continue
                 if verdict[row] != 1:
                     continue
-                pts = sorted(points.get(row, []))
-                vals: List[float] = []
-                for ts, v, _ in pts:
-                    vals += [ts, v]
-                anomaly[p.cols.alias[p.s0 + k]] = {"tags": ",".join(sorted({t for _, _, t in pts if t})),
-                                                   "values": vals}
-                self.last_anom[row] = pts[-1][0] if pts else now
+                sp = span.get(row)
+                if sp is None:
+                    anomaly[p.cols.alias[p.s0 + k]] = {"tags": "", "values": []}
+                    self.last_anom[row] = now
+                    continue
+                lo_, hi_ = sp
+                pods = p.cols.cur_pods(p.s0 + int(self.row_k[row]))
+                names = {pods[q] for q in np.unique(pcs[lo_:hi_]).tolist() if q < len(pods)}
+                anomaly[p.cols.alias[p.s0 + k]] = {"tags": ",".join(sorted(n for n in names if n)),
+                                                   "values": inter_l[2 * lo_:2 * hi_]}
+                self.last_anom[row] = float(ts[hi_ - 1])
             finish[p.doc_id] = (r.ST_COMPLETED_UNHEALTH, "anomaly detected in " + ",".join(sorted(anomaly)), anomaly)
         ending = self._pop_ending(now, finish)
         if ending:  # past endTime: seen / model checks over every ending job's rows at once
