@@ -449,11 +449,14 @@ def _native_batch(docs: Sequence[Dict], step: float, window_cols: int) -> Option
     def run(c):
         d0, d1 = bounds[c], bounds[c + 1]
         o = off[8 * d0:8 * d1 + 1]
-        piece = joined[off[8 * d0]:off[8 * d1]] if nchunk > 1 else joined
-        # capacities (grown and retried if short): series <= entries of the configs, pods <=
-        # escaped pod separators + one per series and kind
-        ser_cap = max(16, piece.count("== "))
-        pod_cap = max(64, piece.count("%7C") + piece.count("|") + 2 * ser_cap)
+        # capacities (grown and retried if short), scaled from the chunk's first document
+        # (a batch is one shape of job; counting the whole chunk's text cost more than the
+        # decode): series <= entries of the configs, pods <= escaped pod separators + one
+        # per series and kind
+        first = joined[off[8 * d0]:off[8 * d0 + 8]]
+        scale = 1.25 * (int(o[-1] - o[0]) + 1) / (len(first) + 1)  # chunk text / first document's
+        ser_cap = max(16, int(first.count("== ") * scale) + 16)
+        pod_cap = max(64, int((first.count("%7C") + first.count("|")) * scale) + 2 * ser_cap)
         text_cap = int(o[-1] - o[0]) + 1024
         for _ in range(4):
             got = _native_call(lib, blob, o, d1 - d0, step, window_cols, ser_cap, pod_cap, text_cap)

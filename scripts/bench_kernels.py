@@ -102,7 +102,7 @@ def main():
                          "series_per_s": round(N / (med / 1e3), 1), "n_series": N, "T": R}
         print(json.dumps({"kernel": name, **results[name]}), flush=True)
     # agreement between variants
-    ref_v = -1 if -1 in variants else variants[0]
+    ref_v = -1 if -1 in variants else (variants[0] if variants else None)
     ref = outs.get((ref_v, sm.MODE_HW))
     if ref is not None:
         for v in variants:

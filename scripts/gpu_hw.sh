@@ -21,6 +21,9 @@ for s in $STEPS; do
     ab) run ab 600 python scripts/hw_prune_ab.py --iters ${ITERS:-8} ${AB_ARGS:-} ;;
     abmix) run abmix 600 python scripts/hw_prune_ab.py --iters ${ITERS:-8} --mix ${AB_ARGS:-} ;;
     kern) run kern 600 python scripts/bench_kernels.py --only es,decompose --variants "" --rounds 3 ;;
+    k4) run k4_tests 300 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread -k "decompose"
+        run k4_bench 300 python scripts/bench_kernels.py --only decompose --variants "" --rounds 5 ;;
+    lstmsweep) SKIP_TRAIN=1 N=${LSTM_N:-24576,49152,73728,98304,100000,122880} run lstm_sweep 300 python scripts/bench_lstm_kernels.py ;;
     canary) run canary 600 python bench.py --steps 20 --warmup 5 ;;
   esac
 done

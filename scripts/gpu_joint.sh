@@ -22,6 +22,7 @@ for s in $STEPS; do
     nodelstm) run node_lstm 900 python bench.py --config node-lstm --steps ${T:-30} ;;
     nodemv) run node_mv 900 python bench.py --config node-lstm --lstm-features 2 --steps ${T:-30} ;;
     cold) run cold 900 python bench.py --config node --cold --steps 8 --warmup 1 ;;
+    prof) run prof 900 python scripts/prof_node.py --out gpurun_out/node_r4/prof --ticks 20 --warmup 12 --arrival-per-tick ${J:-2000} ;;
     arrival_auto) run arrival_auto 900 python bench.py --config node --arrival-per-tick ${J:-2000} --steps ${T:-60} --algorithm auto ;;
   esac
 done

@@ -116,7 +116,9 @@ def test_plan_many_memoises_and_mixes_paths():
     assert got[-1] is None and got[5] is not None and got[5].series[0].cur_n == 11
     again = P.plan_many(docs, "holt_winters")
     assert all(a is b for a, b in zip(again, got[:5]))
-    assert P.plan_many(docs, "lstm") == [None] * 5
+    # lstm / auto / bivariate_normal jobs are keyed too (joint models on the resident engine)
+    assert all(p is not None for p in P.plan_many(docs, "lstm"))
+    assert P.plan_many(docs, "no_such_algorithm") == [None] * 5
 
 
 def test_native_plan_throughput():
