@@ -31,9 +31,11 @@ from __future__ import annotations
 import asyncio
 import collections
 import logging
+import operator
 import os
 import re
 import time
+from collections import _count_elements  # the C helper of Counter.update
 from typing import Dict, Iterable, List, Optional, Sequence, Set, Tuple
 from urllib.parse import quote
 
@@ -204,11 +206,15 @@ class ResidentHistory:
 
     def want_h(self, hashes: Sequence[int], now: float, key_of) -> None:
         """Reference history keys; ``key_of(i)`` gives the tuple of ``hashes[i]``
-        (asked only for keys without a row)."""
-        refs, last, rows = self.refs, self.last_used, self.rows
+        (asked only for keys without a row).  Bulk dict operations in C: a deploy
+        burst references thousands of keys per tick, nearly all with rows."""
+        hashes = list(hashes)
+        _count_elements(self.refs, hashes)
+        self.last_used.update(dict.fromkeys(hashes, now))
+        rows = self.rows
+        if rows.keys() >= set(hashes):
+            return
         for i, h in enumerate(hashes):
-            refs[h] = refs.get(h, 0) + 1
-            last[h] = now
             if h not in rows:
                 self.pending.add(h)
                 if h not in self._tuples:
@@ -233,6 +239,26 @@ class ResidentHistory:
 
     def ready_h(self, h: int) -> bool:
         return h in self.rows and h not in self.pending
+
+    def ready_mask(self, hashes: np.ndarray) -> np.ndarray:
+        """:meth:`ready_h` of every key (uint64 array) at once: set operations in C
+        for the common case of every key ready."""
+        hs = hashes.tolist()
+        bad = set(hs) - self.rows.keys()
+        if self.pending:
+            bad |= self.pending.intersection(hs)
+        if not bad:
+            return np.ones(len(hs), dtype=bool)
+        return ~np.isin(hashes, np.fromiter(bad, dtype=np.uint64, count=len(bad)))
+
+    def rows_of_h(self, hashes: Sequence[int]) -> np.ndarray:
+        """Rows of keys that have one (KeyError otherwise), one C-level lookup."""
+        hashes = list(hashes)
+        if not hashes:
+            return np.zeros(0, dtype=np.int64)
+        if len(hashes) == 1:
+            return np.array([self.rows[hashes[0]]], dtype=np.int64)
+        return np.array(operator.itemgetter(*hashes)(self.rows), dtype=np.int64)
 
     def row_of(self, key: Key) -> int:
         return self.rows[self.key_hash(key)]

@@ -561,11 +561,18 @@ class RolloutMonitor:
     # ------------------------------------------------------------------ admission
     async def _admit(self, now: float) -> int:
         hist = self.history
-        ready = []
-        for p in self.waiting.values():
-            ks = p.cols.u64[p.s0:p.s0 + p.n, 0].tolist()
-            if all(hist.ready_h(h) for h in ks):
-                ready.append(p)
+        waiting = list(self.waiting.values())
+        if not waiting:
+            return 0
+        lens = np.fromiter((p.n for p in waiting), dtype=np.int64, count=len(waiting))
+        ok = hist.ready_mask(np.concatenate([p.cols.u64[p.s0:p.s0 + p.n, 0] for p in waiting]))
+        if not ok.all():  # per job: every one of its keys ready
+            cb = np.concatenate([[0], np.cumsum(~ok)])
+            ends = np.cumsum(lens)
+            n_bad = cb[ends] - cb[ends - lens]
+            ready = [p for p, nb in zip(waiting, n_bad.tolist()) if nb == 0]
+        else:
+            ready = waiting
         if not ready:
             return 0
         t0 = time.perf_counter()
@@ -631,7 +638,7 @@ class RolloutMonitor:
         store the forecast state + per-column horizons."""
         hist = self.history
         drop = np.maximum(0, np.round((hist.t_last - b.f64[:, 2]) / self.step).astype(np.int64))
-        hrows = np.fromiter((hist.rows[h] for h in b.u64[:, 0].tolist()), dtype=np.int64, count=b.n)
+        hrows = hist.rows_of_h(b.u64[:, 0].tolist())
         Wc = self.Wc
         tiles = np.tile(np.arange(Wc), self.P)[None, :]
         for dv in np.unique(drop).tolist():
@@ -675,8 +682,8 @@ class RolloutMonitor:
         if not ia:
             return
         ia, ib = np.asarray(ia, dtype=np.int64), np.asarray(ib, dtype=np.int64)
-        ha = np.fromiter((hist.rows[h] for h in b.u64[ia, 0].tolist()), dtype=np.int64, count=len(ia))
-        hb = np.fromiter((hist.rows[h] for h in b.u64[ib, 0].tolist()), dtype=np.int64, count=len(ib))
+        ha = hist.rows_of_h(b.u64[ia, 0].tolist())
+        hb = hist.rows_of_h(b.u64[ib, 0].tolist())
         drop = np.maximum(0, np.round((hist.t_last - b.f64[ia, 2]) / self.step).astype(np.int64))
         dev = self.device
         for dv in np.unique(drop).tolist():

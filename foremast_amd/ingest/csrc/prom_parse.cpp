@@ -663,11 +663,37 @@ long long keyed_elements(Cursor& c, const char* stop, const KeyedOut& o, KeyInde
       if (row < 0) { ++k.unmatched; cur_slot = -1; return; }
       if (flat && prev_slot >= 0) ix.learn(prev_slot, bytes_hash(lab0, lab_len), lab_len, (int32_t)cur_slot);
     };
+    // whole-element prediction: {"metric":<the label object that followed the previous
+    // element last time>,"values": -- both key scans and the label branch skipped, the
+    // same checks as the label branch's prediction below
+    bool pre = false;
+    if (prev_slot >= 0 && c.e - c.p >= 9 && memcmp(c.p, "\"metric\":", 9) == 0) {
+      uint32_t plen;
+      int32_t pslot, prow;
+      uint64_t ptag;
+      const char* m0 = c.p + 9;
+      if (ix.predict(prev_slot, plen, pslot, prow, ptag) && (size_t)(c.e - m0) >= (size_t)plen + 10 &&
+          m0[plen - 1] == '}' && memcmp(m0 + plen, ",\"values\":", 10) == 0 &&
+          __atomic_load_n(&ix.slots[pslot].row, __ATOMIC_RELAXED) == prow &&
+          KeyIndex::tag_of(bytes_hash(m0, plen), plen, pslot, prow) == ptag) {
+        c.p = m0 + plen + 10;
+        cur_slot = pslot;
+        ix.prefetch_slot(pslot);
+        row = prow;
+        if (row >= o.max_rows) { row = -1; ++k.unmatched; cur_slot = -1; }
+        resolved = flat = have_labels = pre = true;
+      }
+    }
     while (true) {
       const char *k0, *k1;
-      // the two keys of every element, byte-exact and unspaced: no string scan
-      if (c.e - c.p >= 9 && c.p[0] == '"' && c.p[7] == '"' && c.p[8] == ':' &&
-          (memcmp(c.p + 1, "metric", 6) == 0 || memcmp(c.p + 1, "values", 6) == 0)) {
+      static const char kValues[] = "values";
+      if (pre) {  // positioned after "values":
+        k0 = kValues;
+        k1 = kValues + 6;
+        pre = false;
+      } else if (c.e - c.p >= 9 && c.p[0] == '"' && c.p[7] == '"' && c.p[8] == ':' &&
+                 (memcmp(c.p + 1, "metric", 6) == 0 || memcmp(c.p + 1, "values", 6) == 0)) {
+        // the two keys of every element, byte-exact and unspaced: no string scan
         k0 = c.p + 1;
         k1 = c.p + 7;
         c.p += 9;
