@@ -36,7 +36,7 @@ import logging
 import os
 import time
 from dataclasses import dataclass
-from typing import Callable, Dict, List, Optional, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -148,7 +148,7 @@ class LstmMonitor:
         # external entities (rollout jobs' joint models): the newest value of each is fed by
         # the rollout engine (its canary pods' mean), and their verdicts are read back
         self.sync_history = True     # False: another monitor drives the shared history
-        self._feed: Dict[str, np.ndarray] = {}
+        self._feed: Optional[Tuple[List[str], np.ndarray]] = None
         self.hits: Dict[str, Tuple[float, np.ndarray]] = {}
 
     # ------------------------------------------------------------------ membership
@@ -197,7 +197,16 @@ class LstmMonitor:
 
     def feed(self, values: Dict[str, np.ndarray]) -> None:
         """Newest value of each external entity's features (NaN: keep the history's)."""
-        self._feed = values
+        jids = list(values)
+        vals = np.full((len(jids), self.F), np.nan, dtype=np.float32)
+        for i, j in enumerate(jids):
+            v = np.asarray(values[j], dtype=np.float32)[:self.F]
+            vals[i, :len(v)] = v
+        self.feed_matrix(jids, vals)
+
+    def feed_matrix(self, jids: Sequence[str], vals: np.ndarray) -> None:
+        """:meth:`feed` as one ``[len(jids), F]`` float32 matrix (row i: job ``jids[i]``)."""
+        self._feed = (list(jids), vals) if len(jids) else None
 
     def after_reform(self) -> None:
         """RC4: every rank adopts rank 0's weights and optimizer state after the
@@ -333,19 +342,15 @@ class LstmMonitor:
         self.t_cur = hist.t_last
 
     def _fed(self, x: torch.Tensor) -> torch.Tensor:
-        rows, vals = [], []
-        for jid, v in self._feed.items():
-            e = self.jobs.get(jid)
-            if e is not None and e.row >= 0:
-                w = np.full(self.F, np.nan, dtype=np.float32)
-                w[:min(self.F, len(v))] = np.asarray(v, dtype=np.float32)[:self.F]
-                rows.append(e.row)
-                vals.append(w)
-        self._feed = {}
-        if not rows:
+        jids, vals = self._feed
+        self._feed = None
+        jobs = self.jobs
+        rows = np.fromiter(((jobs[j].row if j in jobs else -1) for j in jids), dtype=np.int64, count=len(jids))
+        ok = rows >= 0
+        if not ok.any():
             return x
-        idx = torch.tensor(rows, dtype=torch.long, device=self.device)
-        fv = torch.from_numpy(np.stack(vals)).to(self.device)
+        idx = torch.from_numpy(rows[ok]).to(self.device)
+        fv = torch.from_numpy(np.ascontiguousarray(vals[ok])).to(self.device)
         x = x.clone()
         x[idx] = torch.where(torch.isnan(fv), x[idx], fv)
         return x

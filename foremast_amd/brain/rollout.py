@@ -267,6 +267,7 @@ class RolloutMonitor:
         # across the ranks; every rank ticks it in lockstep
         self.joint_lstm = None
         self._lstm_rows: Dict[str, np.ndarray] = {}   # job -> its rows in feature (sorted alias) order
+        self._lstm_cat = None   # (jobs, their rows concatenated, job / feature index per row); None: stale
         if self.cfg.algorithm in ("lstm", "auto"):
             from .lstm_monitor import LstmMonitor
             self.joint_lstm = LstmMonitor(store, self.cfg, prom=self.prom, device=self.device,
@@ -505,6 +506,7 @@ class RolloutMonitor:
             self.slots.release(p.pod_keys)
         self._release_jslot(p)
         if self._lstm_rows.pop(jid, None) is not None:
+            self._lstm_cat = None
             self.joint_lstm.detach([jid], now)
         p.rows = np.zeros(0, dtype=np.int64)
 
@@ -675,6 +677,7 @@ class RolloutMonitor:
             if kind == "lstm" and self.joint_lstm is not None:
                 order = order[:self.joint_lstm.F]
                 self._lstm_rows[p.doc_id] = p.rows[order]
+                self._lstm_cat = None
                 self.joint_lstm.attach(p.doc_id, [(al[k], p.cols.hkey_at(p.s0 + k)) for k in order], p.end_ts, now)
                 continue
             ia.append(starts[i] + order[0])
@@ -1247,20 +1250,26 @@ class RolloutMonitor:
         step, score; returns job -> (time, values) of the jobs it flags."""
         if self.joint_lstm is None:
             return {}
-        feed = {}
         if self._lstm_rows:
-            jids = list(self._lstm_rows)
-            rows = np.concatenate([self._lstm_rows[j] for j in jids])
-            ra = torch.from_numpy(rows).to(self.device)
+            # the jobs' rows, concatenated once per change of the job set
+            if self._lstm_cat is None:
+                jids = list(self._lstm_rows)
+                lens = np.fromiter((len(self._lstm_rows[j]) for j in jids), dtype=np.int64, count=len(jids))
+                rows = np.concatenate([self._lstm_rows[j] for j in jids])
+                job = np.repeat(np.arange(len(jids)), lens)
+                feat = np.arange(len(rows)) - np.repeat(np.cumsum(lens) - lens, lens)
+                self._lstm_cat = (jids, torch.from_numpy(rows).to(self.device), job, feat)
+            jids, ra, job, feat = self._lstm_cat
             col = last_c[ra]
-            win = self.win[ra].view(len(rows), self.P, self.Wc)
+            win = self.win[ra].view(len(ra), self.P, self.Wc)
             v = torch.nanmean(win.gather(2, col.view(-1, 1, 1).expand(-1, self.P, 1))[:, :, 0], 1).cpu().numpy()
-            off = 0
-            for j in jids:
-                n = len(self._lstm_rows[j])
-                feed[j] = v[off:off + n]
-                off += n
-        self.joint_lstm.feed(feed)
+            F = self.joint_lstm.F
+            vals = np.full((len(jids), F), np.nan, dtype=np.float32)
+            keep = feat < F
+            vals[job[keep], feat[keep]] = v[keep]
+            self.joint_lstm.feed_matrix(jids, vals)
+        else:
+            self.joint_lstm.feed_matrix([], np.zeros((0, self.joint_lstm.F), dtype=np.float32))
         await self.joint_lstm.tick()
         return dict(self.joint_lstm.hits)
 
@@ -1430,6 +1439,8 @@ class RolloutMonitor:
             self._release_jslot(p)
         if self.joint_lstm is not None and self._lstm_rows:
             gone = [p.doc_id for p in plans if self._lstm_rows.pop(p.doc_id, None) is not None]
+            if gone:
+                self._lstm_cat = None
             if gone:
                 self.joint_lstm.detach(gone, now)
 
