@@ -224,7 +224,6 @@ class NodeBrain:
                     split.append(m)
                     await m.score_tick()
                 else:
-                    m.sync(steal_from=self.dead or None)
                     await m.tick()
             except Exception as e:  # noqa: BLE001 - a scoring failure must not desynchronise the collectives
                 log.exception("%s tick failed: %s", type(m).__name__, e)
@@ -236,6 +235,15 @@ class NodeBrain:
             if self.world.generation != gen:
                 self._after_reform(before)
         t1 = time.perf_counter()
+        # claims are intake: a monitor's new jobs are leased after the verdicts are out (a
+        # claim scans the store's open documents, e.g. a burst of another monitor's jobs)
+        # and admitted by its next tick
+        for m in self.monitors:
+            if m not in split:
+                try:
+                    m.sync(steal_from=self.dead or None)
+                except Exception as e:  # noqa: BLE001 - the store may be briefly unavailable
+                    log.exception("%s claim failed: %s", type(m).__name__, e)
         for m in split:
             try:
                 m.sync(steal_from=self.dead or None)
