@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import asyncio
 import collections
+import itertools
 import logging
 import operator
 import os
@@ -224,15 +225,24 @@ class ResidentHistory:
         self.unwant_h([self.key_hash(k) for k in keys], now)
 
     def unwant_h(self, hashes: Iterable[int], now: float) -> None:
-        refs, last = self.refs, self.last_used
-        for h in hashes:
-            n = refs.get(h, 0) - 1
-            if n > 0:
-                refs[h] = n
-            else:
-                refs.pop(h, None)
-                self._idle.append((now, h))  # expiry candidate (checked in time order)
-            last[h] = now
+        """Release references (bulk: counts, lookups and updates in C; Python touches
+        only the keys whose last reference goes)."""
+        dec: Dict[int, int] = {}
+        _count_elements(dec, hashes)
+        if not dec:
+            return
+        refs = self.refs
+        keys = list(dec)
+        left = (np.fromiter(map(refs.get, keys, itertools.repeat(0)), dtype=np.int64, count=len(keys))
+                - np.fromiter(dec.values(), dtype=np.int64, count=len(keys)))
+        keep = left > 0
+        if keep.any():
+            refs.update(zip(itertools.compress(keys, keep), left[keep].tolist()))
+        gone = list(itertools.compress(keys, ~keep))
+        for h in gone:
+            refs.pop(h, None)
+        self._idle.extend(zip(itertools.repeat(now), gone))  # expiry candidates (checked in time order)
+        self.last_used.update(dict.fromkeys(keys, now))
 
     def ready(self, key: Key) -> bool:
         return self.ready_h(self.key_hash(key))
