@@ -376,7 +376,7 @@ class LstmMonitor:
             self.shard.live = torch.tensor(live, dtype=torch.int64, device=self.device)
             self._live_dirty = False
         has = int(self.shard.live.numel() > 0)
-        flags = torch.tensor([float(len(admitted))], device=self.device)
+        flags = torch.full((1,), float(len(admitted)), dtype=torch.float32, device=self.device)
         self.shard.train_step(weight=float(has), flags=flags,
                               timeout_s=self.exchange_timeout if comm.active() else None)
         red = self.shard.trainer.last_flags

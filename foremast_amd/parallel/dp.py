@@ -94,7 +94,10 @@ class GradBuckets:
         if weight is not None and self.overlap and any(b["ready"] for b in self.buckets):
             raise ValueError("weighted steps need GradBuckets(overlap=False): hooks reduce before the weight applies")
         if weight is not None or flags is not None:
-            parts = [torch.tensor([1.0 if weight is None else float(weight)], device=self.buckets[-1]["flat"].device)]
+            # a device-side fill, not torch.tensor([...], device=...): a pageable host copy
+            # would block the host until the GPU drained every step queued before it
+            parts = [torch.full((1,), 1.0 if weight is None else float(weight), dtype=torch.float32,
+                                device=self.buckets[-1]["flat"].device)]
             if flags is not None:
                 parts.append(flags.to(parts[0].device, torch.float32).reshape(-1))
             extra = torch.cat(parts)

@@ -17,7 +17,8 @@ STEPS=${STEPS:-"tests burst_auto arrival"}
 for s in $STEPS; do
   case $s in
     tests) run joint_tests 600 python -u -m pytest tests/test_rollout_joint.py tests/test_rollout.py tests/test_lstm_monitor.py tests/test_node.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
-    burst) run burst 900 python bench.py --config node --steps 30 --warmup 2 ;;
+    burst) run burst 900 python bench.py --config node --steps 8 --warmup 1 ;;
+    lstmcfg) run lstm_cfg 600 python bench.py --config lstm --steps 20 --warmup 5 ;;
     burst_auto) run burst_auto 600 python bench.py --config node --steps 8 --warmup 1 --algorithm auto ;;
     arrival) run arrival 900 python bench.py --config node --arrival-per-tick ${J:-2000} --steps ${T:-60} ;;
     nodelstm) run node_lstm 900 python bench.py --config node-lstm --steps ${T:-30} ;;
