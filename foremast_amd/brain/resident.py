@@ -100,11 +100,13 @@ def range_url(endpoint: str, selector: str, start: float, n: int, step: float) -
 
 async def fetch_decode(prom, reqs: Sequence[Tuple[str, float, int, int]], tables: Sequence[native.KeyTable],
                        out: np.ndarray, step: float, threads: int,
-                       timings: Optional[Dict[str, float]] = None) -> List[bool]:
+                       timings: Optional[Dict[str, float]] = None, fill_nan: bool = False) -> List[bool]:
     """Fetch ``reqs`` = (url, start, n_points, col0) and scatter every body through
     its key table into ``out`` (one native call on a thread pool, off the event
     loop).  Returns per request whether it was fetched and decoded; ``timings``
-    receives ``fetch_ms`` / ``native_ms`` / ``resume_ms`` (executor hand-back)."""
+    receives ``fetch_ms`` / ``native_ms`` / ``resume_ms`` (executor hand-back).
+    ``fill_nan``: the native threads first set the bodies' column span of every
+    row of ``out`` to NaN (the caller did not pre-fill it)."""
     t0 = time.perf_counter()
     bodies = await prom.fetch_raw_many([u for u, *_ in reqs])
     t1 = time.perf_counter()
@@ -121,7 +123,8 @@ async def fetch_decode(prom, reqs: Sequence[Tuple[str, float, int, int]], tables
 
     def run():
         span[0] = time.perf_counter()
-        r = native.decode_bodies(args[0], args[1], args[2], step, args[3], args[4], out, threads=threads)
+        r = native.decode_bodies(args[0], args[1], args[2], step, args[3], args[4], out, threads=threads,
+                                 fill_nan=fill_nan)
         span[1] = time.perf_counter()
         return r
     stats = await asyncio.get_running_loop().run_in_executor(None, run)

@@ -1031,8 +1031,9 @@ class RolloutMonitor:
             if all(0 <= row < self.cap and self.row_job[row] >= 0 for row in rows.tolist()):
                 tgt.index_copy_(0, rows, torch.from_numpy(block.reshape(len(part), P * Wc)).to(self.device))
 
-    def _tick_block(self, S: int, k: int):
-        """NaN-filled pinned decode block of the tick, one of two kept across ticks."""
+    def _tick_block(self, S: int, k: int, fill: bool = True):
+        """Pinned decode block of the tick (NaN-filled unless ``fill`` is False: the
+        decoder's threads fill it), one of two kept across ticks."""
         bufs = self._blocks.get((S, k))
         if bufs is None:
             bufs = [torch.empty((S, k), dtype=torch.float32) for _ in range(2)]
@@ -1042,7 +1043,8 @@ class RolloutMonitor:
         self._block_i ^= 1
         t = bufs[self._block_i]
         a = t.numpy()
-        a.fill(np.nan)
+        if fill:
+            a.fill(np.nan)
         return t, a
 
     async def _ingest(self, t_new: float) -> None:
@@ -1059,17 +1061,19 @@ class RolloutMonitor:
         S = self.slots.cap
         t0 = time.perf_counter()
         srcmap = self._srcmap()
-        # the tick block is [slot, family x minute]: ONE pod index serves every family's body
-        block_t, block = self._tick_block(S, F * k)
+        fams = [(fam, fi) for fam, fi in self.fams.items() if fi < len(self._fam_rows) and self._fam_rows[fi] > 0]
+        # the tick block is [slot, family x minute]: ONE pod index serves every family's body.
+        # When the bodies cover every column the decoder's threads NaN-fill it in parallel
+        native_fill = len({fi for _, fi in fams}) == F
+        block_t, block = self._tick_block(S, F * k, fill=not native_fill)
         self.timings["ingest_prep_ms"] = (time.perf_counter() - t0) * 1e3
         self.timings["points"] = k
         index = self.slots.table(F)
-        fams = [(fam, fi) for fam, fi in self.fams.items() if fi < len(self._fam_rows) and self._fam_rows[fi] > 0]
         reqs = [(range_url(fam[0], fam[1], first, k, self.step), first, k, fi * k) for fam, fi in fams]
         self.tick_queries += len(reqs)
         t0 = time.perf_counter()
         ok = await fetch_decode(self.prom, reqs, [index] * len(reqs), block, self.step, self.decode_threads,
-                                timings=self.timings)
+                                timings=self.timings, fill_nan=native_fill)
         self.timings["decode_ms"] = (time.perf_counter() - t0) * 1e3
         if not all(ok):
             return  # t_cur stays: the next tick fetches these minutes again
