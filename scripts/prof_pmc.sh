@@ -4,6 +4,7 @@
 #   hw    — Holt-Winters scan kernel (default variant) on 20k x 10080
 #   lstm  — LSTM training (per phase) + scoring kernels
 #   dec   — seasonal decomposition
+#   es    — ES / DES sequential fit (and the time-parallel scan variants)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TARGET=${TARGET:-hw}
@@ -13,6 +14,7 @@ export TMPDIR=/tmp
 case $TARGET in
   hw)   CMD=("$PWD/scripts/bench_kernels.py" --series 20000 --rounds 1 --only hw --variants=${VARIANTS:-3,4}) ;;
   dec)  CMD=("$PWD/scripts/bench_kernels.py" --series 20000 --rounds 1 --only decompose --variants=3) ;;
+  es)   CMD=("$PWD/scripts/bench_kernels.py" --series 20000 --rounds 1 --only es --variants=) ;;
   lstm) CMD=("$PWD/scripts/bench_lstm_kernels.py") ;;
 esac
 SETS=("SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS"
