@@ -513,9 +513,10 @@ class RolloutMonitor:
     def _refresh_apps(self) -> None:
         """Apply the app-roster changes of the last admissions / verdicts.  App
         indices are stable (a freed index is reused by a later app), so a job
-        finishing never renumbers the other rows; called only before scoring,
-        so the roster :meth:`app_table` reports is the one the last tick's
-        counters were accumulated under."""
+        finishing never renumbers the other rows; called at the end of the intake
+        half and before scoring (a no-op then unless something changed since), so
+        the roster :meth:`app_table` reports is the one the last tick's counters
+        were accumulated under."""
         if not self._apps_dirty:
             return
         for a in self._app_gone:
@@ -1228,6 +1229,10 @@ class RolloutMonitor:
             log.exception("rollout admission failed (the affine exchange still runs)")
         if self.router is not None:
             await self._route()  # every rank, every tick (collectives)
+        # the roster changes of this tick's completions and admissions, applied here rather
+        # than at the start of the next scoring half (the node table reported in between is
+        # built before the intake half: the same roster either way)
+        self._refresh_apps()
         self.timings["intake_ms"] = (time.perf_counter() - t0) * 1e3
         return n
 
