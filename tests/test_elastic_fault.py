@@ -41,6 +41,7 @@ def test_rank_stopped_inside_exchange_survivors_reform(tmp_path):
         t_end = time.time() + 90
         stopped_at = None
         while time.time() < t_end:
+            assert victim.poll() is None, f"victim exited (rc {victim.returncode}) before its fault point"
             with open(f"/proc/{victim.pid}/stat") as f:
                 if f.read().split(") ", 1)[1].split()[0] == "T":
                     stopped_at = time.time()

@@ -103,6 +103,8 @@ def run_node(tmp_path, n, stop=None, hb=3.0):
             victim = procs[stop[0]]
             t_end = time.time() + 180
             while time.time() < t_end:
+                if victim.poll() is not None:  # exited before its fault point: show why
+                    raise AssertionError("victim exited before its fault point:\n" + victim.stderr.read()[-4000:])
                 with open(f"/proc/{victim.pid}/stat") as f:
                     if f.read().split(") ", 1)[1].split()[0] == "T":
                         break
