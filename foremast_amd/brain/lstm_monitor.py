@@ -118,6 +118,7 @@ class LstmMonitor:
         self.jobs: Dict[str, Entity] = {}
         self.waiting: Dict[str, Entity] = {}
         self.row_job: List[Optional[str]] = [None] * self.shard.n
+        self._used = np.zeros(self.shard.n, dtype=bool)   # row holds an entity (free / live lists in numpy)
         self.feat_rows = torch.full((self.shard.n, self.F), -1, dtype=torch.int64, device=self.device)
         self.padded = torch.zeros((self.shard.n, self.F), dtype=torch.bool, device=self.device)
         self.apps: Dict[Tuple[str, str], int] = {}
@@ -191,9 +192,14 @@ class LstmMonitor:
         self.history.want([k for _, k in e.feats], now)
 
     def detach(self, jids, now: float) -> None:
+        """Drop external entities (their rows freed in one batch of device fills)."""
+        rows = []
         for jid in jids:
             self.hits.pop(jid, None)
-            self._drop(jid, now)
+            row = self._drop(jid, now, free_row=False)
+            if row >= 0:
+                rows.append(row)
+        self._free_rows(rows)
 
     def feed(self, values: Dict[str, np.ndarray]) -> None:
         """Newest value of each external entity's features (NaN: keep the history's)."""
@@ -226,14 +232,19 @@ class LstmMonitor:
             self.shard.packed = None
         self._digest = None
 
-    def _drop(self, jid: str, now: float) -> None:
+    def _drop(self, jid: str, now: float, free_row: bool = True) -> int:
+        """Forget an entity; returns its row (-1: none), freed here unless ``free_row``
+        is False (the caller frees a batch)."""
         e = self.jobs.pop(jid, None) or self.waiting.pop(jid, None)
         if e is None:
-            return
+            return -1
         self.history.unwant([k for _, k in e.feats], now)
-        if e.row >= 0:
-            self._free_row(e.row)
-            self._n_series -= len(e.feats)
+        if e.row < 0:
+            return -1
+        self._n_series -= len(e.feats)
+        if free_row:
+            self._free_rows([e.row])
+        return e.row
 
     @property
     def n_live(self) -> int:
@@ -244,6 +255,7 @@ class LstmMonitor:
         n = self.shard.n
         self.shard.grow(cap)
         self.row_job.extend([None] * (cap - n))
+        self._used = np.concatenate([self._used, np.zeros(cap - n, dtype=bool)])
         fr = torch.full((cap, self.F), -1, dtype=torch.int64, device=self.device)
         fr[:n] = self.feat_rows
         pd = torch.zeros((cap, self.F), dtype=torch.bool, device=self.device)
@@ -252,15 +264,22 @@ class LstmMonitor:
         self._calibrated = np.concatenate([self._calibrated, np.zeros(cap - n, dtype=bool)])
         self._row_end = np.concatenate([self._row_end, np.full(cap - n, np.inf)])
 
-    def _free_row(self, row: int) -> None:
-        self.row_job[row] = None
-        self._calibrated[row] = False
-        self._row_end[row] = np.inf
-        self.feat_rows[row] = -1
-        self.padded[row] = False
-        self.shard.app_id[row] = 0
+    def _free_rows(self, rows: List[int]) -> None:
+        """Free rows in one batch: host bookkeeping, then one index fill per device array."""
+        if not rows:
+            return
+        for row in rows:
+            self.row_job[row] = None
+        ra = np.asarray(rows, dtype=np.int64)
+        self._used[ra] = False
+        self._calibrated[ra] = False
+        self._row_end[ra] = np.inf
+        idx = torch.from_numpy(ra).to(self.device)
+        self.feat_rows[idx] = -1
+        self.padded[idx] = False
+        self.shard.app_id[idx] = 0
         for ring in self.shard.rings:
-            ring.data[row].fill_(float("nan"))
+            ring.data.index_fill_(0, idx, float("nan"))
         self._live_dirty = True
 
     def _app_index(self, app: Tuple[str, str]) -> int:
@@ -281,13 +300,14 @@ class LstmMonitor:
         ready = [e for e in self.waiting.values() if all(hist.ready(k) for _, k in e.feats)]
         if not ready:
             return []
-        free = [i for i, j in enumerate(self.row_job) if j is None]
+        free = np.flatnonzero(~self._used)
         if len(free) < len(ready):
             cap = self.shard.n
             while cap - (self.shard.n - len(free)) < len(ready):
                 cap *= 2
             self._grow(cap)
-            free = [i for i, j in enumerate(self.row_job) if j is None]
+            free = np.flatnonzero(~self._used)
+        free = free[:len(ready)].tolist()
         rows = []
         fr = np.full((len(ready), self.F), -1, dtype=np.int64)
         for i, (e, row) in enumerate(zip(ready, free)):
@@ -295,6 +315,7 @@ class LstmMonitor:
             e.row = row
             self.jobs[e.doc["id"]] = e
             self.row_job[row] = e.doc["id"]
+            self._used[row] = True
             self._row_end[row] = np.inf if e.external else e.end_ts
             self._n_series += len(e.feats)
             rows.append(row)
@@ -372,8 +393,7 @@ class LstmMonitor:
         except Exception as e:  # noqa: BLE001 - the collectives below must still run on this rank
             log.exception("lstm data step failed: %s", e)
         if getattr(self, "_live_dirty", True):
-            live = [i for i, j in enumerate(self.row_job) if j is not None]
-            self.shard.live = torch.tensor(live, dtype=torch.int64, device=self.device)
+            self.shard.live = torch.from_numpy(np.flatnonzero(self._used).astype(np.int64)).to(self.device)
             self._live_dirty = False
         has = int(self.shard.live.numel() > 0)
         flags = torch.full((1,), float(len(admitted)), dtype=torch.float32, device=self.device)
@@ -437,11 +457,15 @@ class LstmMonitor:
                                     "modified_ts": now,
                                     "processingContent": f"scored by {self.worker_id} (resident lstm)"}))
         if items:
+            freed = []
             for (jid, fields), ok in zip(items, self.store.update_many(items, expect_claimed_by=self.worker_id)):
                 if ok:
                     written[jid] = fields["status"]
                     self.metrics.jobs.labels(status=fields["status"]).inc()
-                self._drop(jid, now)
+                row = self._drop(jid, now, free_row=False)
+                if row >= 0:
+                    freed.append(row)
+            self._free_rows(freed)
         self.ticks += 1
         self.metrics.series_scored.inc(self._n_series)
         self.timings["tick_ms"] = (time.perf_counter() - t0) * 1e3

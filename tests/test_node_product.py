@@ -80,18 +80,32 @@ def request(app):
                                              strategy="canary").to_dict()
 
 
+class _RendezvousFlake(Exception):
+    """A gloo pair could not connect while the ranks formed (8 processes on a loaded
+    8-CPU host): not the code under test; the run is repeated on a fresh store."""
+
+
 def run_node(tmp_path, n, stop=None, hb=3.0):
     """Register the jobs, run n ranks for TICKS ticks; returns (statuses, per-rank lines)."""
+    for attempt in range(3):
+        try:
+            return _run_node(tmp_path, n, stop, hb, attempt)
+        except _RendezvousFlake:
+            if attempt == 2:
+                raise
+
+
+def _run_node(tmp_path, n, stop, hb, attempt):
     import torch.distributed as dist
     from foremast_amd.service import app as svc
     from foremast_amd.store.jobstore import SqliteJobStore
-    db = str(tmp_path / f"jobs{n}.db")
+    db = str(tmp_path / f"jobs{n}_{attempt}.db")
     store = SqliteJobStore(db)
     ids = {a: svc.register(store, request(a))[1]["jobId"] for a in APPS}
     kv = dist.TCPStore("127.0.0.1", 0, is_master=True, wait_for_workers=False, timeout=datetime.timedelta(seconds=90))
     procs, outs = [], []
     for i in range(n):
-        out = tmp_path / f"n{n}_rank{i}.jsonl"
+        out = tmp_path / f"n{n}_{attempt}_rank{i}.jsonl"
         env = dict(os.environ, OMP_NUM_THREADS="1", CUDA_VISIBLE_DEVICES="", GLOO_SOCKET_IFNAME="lo")
         if stop is not None and i == stop[0]:
             env["NODE_RANK_STOP_AT"] = str(stop[1])
@@ -120,6 +134,8 @@ def run_node(tmp_path, n, stop=None, hb=3.0):
                 continue
             _, err = p.communicate(timeout=600)
             errs.append(err)
+            if p.returncode != 0 and "connectFullMesh failed" in err:
+                raise _RendezvousFlake(err[-2000:])
             assert p.returncode == 0, err[-4000:]
     finally:
         for p in procs:
