@@ -26,6 +26,7 @@ for s in $STEPS; do
     cold) run cold 900 python bench.py --config node --cold --steps 8 --warmup 1 ;;
     prof) run prof 900 python scripts/prof_node.py --out gpurun_out/node_r4/prof --ticks 20 --warmup 12 --arrival-per-tick ${J:-2000} ;;
     profauto) run prof_auto 900 python scripts/prof_node.py --out gpurun_out/node_r4/prof_auto --ticks 8 --algorithm auto ;;
+    profarrauto) run prof_arr_auto 900 python scripts/prof_node.py --out gpurun_out/node_r4/prof_arr_auto --ticks 10 --warmup 12 --arrival-per-tick ${J:-2000} --algorithm auto ;;
     arrival_auto) run arrival_auto 900 python bench.py --config node --arrival-per-tick ${J:-2000} --steps ${T:-60} --algorithm auto ;;
   esac
 done
