@@ -71,9 +71,11 @@ def lstm_features(doc, cfg: BrainConfig) -> Optional[List[Tuple[str, Key]]]:
 class Entity:
     doc: Dict
     end_ts: float
-    feats: List[Tuple[str, Key]]
+    feats: List[Tuple[str, Key]]   # (alias, history key); the key may be None when ``hk`` is given
     row: int = -1
     external: bool = False   # a rollout job's joint model (brain/rollout.py): fed, verdicts read back
+    hk: Optional[List[int]] = None          # history key hashes of the features
+    app: Optional[Tuple[str, str]] = None   # (namespace, app)
 
 
 class LstmMonitor:
@@ -168,8 +170,10 @@ class LstmMonitor:
             except TimeFormatError:
                 end_ts = float("inf")
             feats = lstm_features(d, self.cfg)[:self.F]
-            self.waiting[d["id"]] = Entity(doc=d, end_ts=end_ts, feats=feats)
-            self.history.want([k for _, k in feats], now)
+            hk = [self.history.key_hash(k) for _, k in feats]
+            self.waiting[d["id"]] = Entity(doc=d, end_ts=end_ts, feats=feats, hk=hk,
+                                           app=(feats[0][1][2], feats[0][1][3]))
+            self.history.want_h(hk, now, lambda i, feats=feats: feats[i][1])
         return len(docs)
 
     def release(self, pred: Callable[[Dict], bool]) -> int:
@@ -185,11 +189,22 @@ class LstmMonitor:
     def attach(self, jid: str, feats: List[Tuple[str, Key]], end_ts: float, now: float) -> None:
         """Score a rollout job's metrics jointly (its first ``F`` aliases, sorted):
         the entity's rows hold the app's history, then the values :meth:`feed` gives."""
+        feats = list(feats)[:self.F]
+        self.attach_h(jid, [a for a, _ in feats], [self.history.key_hash(k) for _, k in feats],
+                      (feats[0][1][2], feats[0][1][3]), end_ts, now, key_of=lambda i: feats[i][1])
+
+    def attach_h(self, jid: str, aliases: Sequence[str], hk: Sequence[int], app: Tuple[str, str], end_ts: float,
+                 now: float, key_of) -> None:
+        """:meth:`attach` by history key hash (the rollout engine's plan columns carry
+        them); ``key_of(i)``: the key tuple of feature i (asked only for keys without a
+        history row yet)."""
         if jid in self.jobs or jid in self.waiting:
             return
-        e = Entity(doc={"id": jid}, end_ts=end_ts, feats=list(feats)[:self.F], external=True)
+        n = min(self.F, len(hk))
+        e = Entity(doc={"id": jid}, end_ts=end_ts, feats=[(a, None) for a in list(aliases)[:n]], external=True,
+                   hk=list(hk)[:n], app=app)
         self.waiting[jid] = e
-        self.history.want([k for _, k in e.feats], now)
+        self.history.want_h(e.hk, now, key_of)
 
     def detach(self, jids, now: float) -> None:
         """Drop external entities (their rows freed in one batch of device fills)."""
@@ -238,7 +253,7 @@ class LstmMonitor:
         e = self.jobs.pop(jid, None) or self.waiting.pop(jid, None)
         if e is None:
             return -1
-        self.history.unwant([k for _, k in e.feats], now)
+        self.history.unwant_h(e.hk, now)
         if e.row < 0:
             return -1
         self._n_series -= len(e.feats)
@@ -297,7 +312,18 @@ class LstmMonitor:
 
     def _admit(self) -> List[int]:
         hist = self.history
-        ready = [e for e in self.waiting.values() if all(hist.ready(k) for _, k in e.feats)]
+        waiting = list(self.waiting.values())
+        if not waiting:
+            return []
+        lens = np.fromiter((len(e.hk) for e in waiting), dtype=np.int64, count=len(waiting))
+        allk = np.fromiter((h for e in waiting for h in e.hk), dtype=np.uint64, count=int(lens.sum()))
+        ok = hist.ready_mask(allk)
+        if ok.all():
+            ready = waiting
+        else:  # per entity: every feature's history ready
+            cb = np.concatenate([[0], np.cumsum(~ok)])
+            ends = np.cumsum(lens)
+            ready = [e for e, nb in zip(waiting, (cb[ends] - cb[ends - lens]).tolist()) if nb == 0]
         if not ready:
             return []
         free = np.flatnonzero(~self._used)
@@ -308,22 +334,28 @@ class LstmMonitor:
             self._grow(cap)
             free = np.flatnonzero(~self._used)
         free = free[:len(ready)].tolist()
-        rows = []
+        rows = free
         fr = np.full((len(ready), self.F), -1, dtype=np.int64)
+        app_ids = np.empty(len(ready), dtype=np.int64)
         for i, (e, row) in enumerate(zip(ready, free)):
             del self.waiting[e.doc["id"]]
             e.row = row
             self.jobs[e.doc["id"]] = e
             self.row_job[row] = e.doc["id"]
-            self._used[row] = True
-            self._row_end[row] = np.inf if e.external else e.end_ts
-            self._n_series += len(e.feats)
-            rows.append(row)
-            for f, (_, k) in enumerate(e.feats):
-                fr[i, f] = hist.row_of(k)
-            ns, app = e.feats[0][1][2], e.feats[0][1][3]
-            self.shard.app_id[row] = self._app_index((ns, app))
-        idx = torch.tensor(rows, dtype=torch.long, device=self.device)
+            self._n_series += len(e.hk)
+            app_ids[i] = self._app_index(e.app)
+        ra = np.asarray(rows, dtype=np.int64)
+        self._used[ra] = True
+        self._row_end[ra] = np.fromiter((np.inf if e.external else e.end_ts for e in ready), dtype=np.float64,
+                                        count=len(ready))
+        # feature rows of the resident history: one lookup for the whole batch
+        flat = hist.rows_of_h([h for e in ready for h in e.hk])
+        lens_r = np.fromiter((len(e.hk) for e in ready), dtype=np.int64, count=len(ready))
+        ent = np.repeat(np.arange(len(ready)), lens_r)
+        fi = np.arange(len(flat)) - np.repeat(np.cumsum(lens_r) - lens_r, lens_r)
+        fr[ent, fi] = flat
+        idx = torch.from_numpy(ra).to(self.device)
+        self.shard.app_id[idx] = torch.from_numpy(app_ids).to(self.shard.app_id.device, self.shard.app_id.dtype)
         fr_t = torch.from_numpy(fr).to(self.device)
         self.feat_rows[idx] = fr_t
         self.padded[idx] = fr_t < 0
