@@ -410,15 +410,23 @@ class LstmMonitor:
 
     # ------------------------------------------------------------------ tick
     async def tick(self) -> Dict[str, str]:
-        """One lockstep tick (every rank runs it: the DP step is a collective)."""
+        """One standalone tick: the scoring half, then the lockstep intake half (the
+        entities admitted there are scored from the next tick on)."""
+        written = await self.score_tick()
+        await self.intake()
+        return written
+
+    async def intake(self) -> int:
+        """The lockstep half (every rank runs it: the DP step and the calibration are
+        collectives): week loads of new keys, admission, one training step (plus the
+        initial training while it lasts), calibration of the admitted rows.  The next
+        scoring half uses the model and the rows left here.  Returns the rows admitted."""
         t0 = time.perf_counter()
         now = self.clock()
         admitted: List[int] = []
         try:
             if self.sync_history:
-                self.store.heartbeat(self.worker_id, now)
-                await self.history.sync(now)
-            self._ingest()
+                await self.history.load_pending(now)
             admitted = self._admit()
             if admitted:
                 self.shard.refresh_stats()
@@ -451,8 +459,24 @@ class LstmMonitor:
             self._pending_cal = False
         elif not pre_done and red is not None and float(red[0]) > 0:
             self._pending_cal = True
-        self.timings["train_ms"] = (time.perf_counter() - t0) * 1e3
+        self.timings["intake_ms"] = self.timings["train_ms"] = (time.perf_counter() - t0) * 1e3
+        return len(admitted)
+
+    async def score_tick(self) -> Dict[str, str]:
+        """The scoring half: history advance, the newest minute into every row (fed
+        values for external entities), scoring with the model of the last intake,
+        verdicts; returns job -> status written."""
+        t0 = time.perf_counter()
+        now = self.clock()
+        try:
+            if self.sync_history:
+                self.store.heartbeat(self.worker_id, now)
+                await self.history.sync(now, load=False)
+            self._ingest()
+        except Exception as e:  # noqa: BLE001 - the lockstep intake half must still run on this rank
+            log.exception("lstm ingest failed: %s", e)
         written: Dict[str, str] = {}
+        self.hits = {}
         if not self.jobs:
             self.shard.app_stats.zero_()
             return written
@@ -466,7 +490,6 @@ class LstmMonitor:
         rows = np.nonzero(hit | (cal & (self._row_end[:n] <= now)))[0]
         newest = self._newest() if hit.any() else None
         items = []
-        self.hits = {}
         for row in rows.tolist():
             jid = self.row_job[row]
             e = self.jobs.get(jid) if jid is not None else None

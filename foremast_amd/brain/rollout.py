@@ -1231,6 +1231,8 @@ class RolloutMonitor:
             log.exception("rollout admission failed (the affine exchange still runs)")
         if self.router is not None:
             await self._route()  # every rank, every tick (collectives)
+        if self.joint_lstm is not None:  # every rank, every tick: admission, DP step, calibration
+            await self.joint_lstm.intake()
         # the roster changes of this tick's completions and admissions, applied here rather
         # than at the start of the next scoring half (the node table reported in between is
         # built before the intake half: the same roster either way)
@@ -1281,7 +1283,7 @@ class RolloutMonitor:
             self.joint_lstm.feed_matrix(jids, vals)
         else:
             self.joint_lstm.feed_matrix([], np.zeros((0, self.joint_lstm.F), dtype=np.float32))
-        await self.joint_lstm.tick()
+        await self.joint_lstm.score_tick()  # the lockstep half runs in intake()
         return dict(self.joint_lstm.hits)
 
     def after_reform(self) -> None:
