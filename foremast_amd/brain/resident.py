@@ -216,7 +216,7 @@ class ResidentHistory:
         _count_elements(self.refs, hashes)
         self.last_used.update(dict.fromkeys(hashes, now))
         rows = self.rows
-        if rows.keys() >= set(hashes):
+        if all(map(rows.__contains__, hashes)):
             return
         for i, h in enumerate(hashes):
             if h not in rows:
@@ -254,15 +254,14 @@ class ResidentHistory:
         return h in self.rows and h not in self.pending
 
     def ready_mask(self, hashes: np.ndarray) -> np.ndarray:
-        """:meth:`ready_h` of every key (uint64 array) at once: set operations in C
-        for the common case of every key ready."""
+        """:meth:`ready_h` of every key (uint64 array) at once."""
         hs = hashes.tolist()
-        bad = set(hs) - self.rows.keys()
+        # membership through map(dict.__contains__) in C (a set difference against the
+        # keys view would first copy every resident key into a set)
+        ok = np.fromiter(map(self.rows.__contains__, hs), dtype=bool, count=len(hs))
         if self.pending:
-            bad |= self.pending.intersection(hs)
-        if not bad:
-            return np.ones(len(hs), dtype=bool)
-        return ~np.isin(hashes, np.fromiter(bad, dtype=np.uint64, count=len(bad)))
+            ok &= ~np.fromiter(map(self.pending.__contains__, hs), dtype=bool, count=len(hs))
+        return ok
 
     def rows_of_h(self, hashes: Sequence[int]) -> np.ndarray:
         """Rows of keys that have one (KeyError otherwise), one C-level lookup."""
