@@ -198,13 +198,24 @@ class LstmMonitor:
         """:meth:`attach` by history key hash (the rollout engine's plan columns carry
         them); ``key_of(i)``: the key tuple of feature i (asked only for keys without a
         history row yet)."""
-        if jid in self.jobs or jid in self.waiting:
-            return
-        n = min(self.F, len(hk))
-        e = Entity(doc={"id": jid}, end_ts=end_ts, feats=[(a, None) for a in list(aliases)[:n]], external=True,
-                   hk=list(hk)[:n], app=app)
-        self.waiting[jid] = e
-        self.history.want_h(e.hk, now, key_of)
+        self.attach_many([(jid, aliases, hk, app, end_ts, key_of)], now)
+
+    def attach_many(self, items, now: float) -> None:
+        """:meth:`attach_h` of many jobs, ``items`` = (jid, aliases, hk, app, end_ts, key_of)
+        tuples: one history reference call for all of them."""
+        hks: List[int] = []
+        owners: List[Tuple[int, int]] = []  # (item, feature) of each referenced key
+        for t, (jid, aliases, hk, app, end_ts, _key_of) in enumerate(items):
+            if jid in self.jobs or jid in self.waiting:
+                continue
+            n = min(self.F, len(hk))
+            e = Entity(doc={"id": jid}, end_ts=end_ts, feats=[(a, None) for a in list(aliases)[:n]],
+                       external=True, hk=list(hk)[:n], app=app)
+            self.waiting[jid] = e
+            hks += e.hk
+            owners += [(t, f) for f in range(n)]
+        if hks:
+            self.history.want_h(hks, now, lambda i: items[owners[i][0]][5](owners[i][1]))
 
     def detach(self, jids, now: float) -> None:
         """Drop external entities (their rows freed in one batch of device fills)."""

@@ -669,6 +669,7 @@ class RolloutMonitor:
         starts = np.concatenate([[0], np.cumsum(b.lens)]).astype(np.int64)
         ia, ib = [], []   # batch rows of each bivariate job's two aliases
         now = self.clock()
+        attach = []       # the joint LSTM's new entities, referenced in one call
         for i, p in enumerate(b.plans):
             kind = pl.joint_kind(algo, p.n)
             if kind is None:
@@ -679,12 +680,13 @@ class RolloutMonitor:
                 order = order[:self.joint_lstm.F]
                 self._lstm_rows[p.doc_id] = p.rows[order]
                 self._lstm_cat = None
-                self.joint_lstm.attach_h(p.doc_id, [al[k] for k in order],
-                                         p.cols.u64[p.s0 + np.asarray(order), 0].tolist(), p.app, p.end_ts, now,
-                                         key_of=lambda i, p=p, order=order: p.cols.hkey_at(p.s0 + order[i]))
+                attach.append((p.doc_id, [al[k] for k in order], p.cols.u64[p.s0 + np.asarray(order), 0].tolist(),
+                               p.app, p.end_ts, lambda i, p=p, order=order: p.cols.hkey_at(p.s0 + order[i])))
                 continue
             ia.append(starts[i] + order[0])
             ib.append(starts[i] + order[1])
+        if attach:
+            self.joint_lstm.attach_many(attach, now)
         if not ia:
             return
         ia, ib = np.asarray(ia, dtype=np.int64), np.asarray(ib, dtype=np.int64)
