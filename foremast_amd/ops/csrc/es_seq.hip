@@ -136,14 +136,19 @@ __global__ __launch_bounds__(256) void es_seq_kernel(const SmoothArgs a) {
     int* nanc = nancs + (ch % NB) * SW;
     const int t = tid % ES_TC;
     const bool okt = ch * ES_TC + t < T;
+    // the missing count of load k (row se's whole chunk: one ballot) goes to lane k of one
+    // register (v_writelane), and lanes 0..PER-1 store them once: no single-lane LDS store
+    // and exec-mask round trip per row
+    int cnt = 0;
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const int se = tid / ES_TC + k * (256 / ES_TC);
       const float x = okt ? bits_f32<TIN>(v[k]) : 0.f;
       tile[se * ES_LD + t] = x;
-      const unsigned long long nb = __ballot(x != x);  // this wave's load k is row se's whole chunk
-      if (t == 0) nanc[se] = __popcll(nb);
+      const int miss = __popcll(__ballot(x != x));  // wave-uniform (an SGPR)
+      asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(cnt) : "s"(miss), "i"(k));
     }
+    if (t < PER) nanc[tid / ES_TC + t * (256 / ES_TC)] = cnt;
   };
 
   unsigned va[PER], vb[PER];
