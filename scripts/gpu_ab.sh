@@ -23,6 +23,10 @@ for s in $STEPS; do
     hw) run hw_base 300 python scripts/bench_kernels.py --only hw --variants 5 --rounds 3
         FOREMAST_HIP_LIB=$ALT run hw_alt 300 python scripts/bench_kernels.py --only hw --variants 5 --rounds 3 ;;
     tests) FOREMAST_HIP_LIB=$ALT run tests_alt 600 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread -k "hw or holt or smoothing or es_ or des" ;;
+    lstm) SKIP_TRAIN=1 N=98304,100000 run lstm_base 300 python scripts/bench_lstm_kernels.py
+          SKIP_TRAIN=1 N=98304,100000 FOREMAST_HIP_LIB=$ALT run lstm_alt 300 python scripts/bench_lstm_kernels.py
+          SKIP_TRAIN=1 N=98304,100000 run lstm_base2 300 python scripts/bench_lstm_kernels.py ;;
+    lstmtests) FOREMAST_HIP_LIB=$ALT run lstmtests_alt 600 python -u -m pytest tests/test_lstm.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
     canary) FOREMAST_HIP_LIB=$ALT run canary_alt 600 python bench.py --steps 20 --warmup 5 ;;
   esac
 done
