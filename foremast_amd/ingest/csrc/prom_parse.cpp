@@ -581,7 +581,20 @@ struct KeyedOut {
   long long ld, max_rows;
   Label la, lb;
   const char* lo;  // start of the body (swar_decimal reads up to 8 bytes before a number)
+  bool skip_name;  // neither key label is __name__: predictions ignore a leading __name__
 };
+
+// Start of the span of a label object (cursor at its '{') that the layout prediction
+// hashes: after a leading "__name__":"<metric>", when `skip` — the families of one
+// tick (one body per metric, same series order, one shared index) then predict each
+// other's elements; their label objects differ only in the metric name.  The label
+// object itself otherwise (a name with an escape is not skipped).
+inline const char* pred_span(const char* m0, const char* e, bool skip) {
+  static const char kName[] = "{\"__name__\":\"";
+  if (!skip || e - m0 < 14 || memcmp(m0, kName, 13) != 0) return m0;
+  const char* q = find_quote_or_bs(m0 + 13, e);
+  return (q + 1 < e && *q == '"' && q[1] == ',') ? q + 2 : m0;
+}
 
 // Timestamp text -> grid column by the sample's ordinal in its series: every
 // series of a range response carries the same timestamps, so point j of a
@@ -671,7 +684,7 @@ long long keyed_elements(Cursor& c, const char* stop, const KeyedOut& o, KeyInde
       uint32_t plen;
       int32_t pslot, prow;
       uint64_t ptag;
-      const char* m0 = c.p + 9;
+      const char* m0 = pred_span(c.p + 9, c.e, o.skip_name);
       if (ix.predict(prev_slot, plen, pslot, prow, ptag) && (size_t)(c.e - m0) >= (size_t)plen + 10 &&
           m0[plen - 1] == '}' && memcmp(m0 + plen, ",\"values\":", 10) == 0 &&
           __atomic_load_n(&ix.slots[pslot].row, __ATOMIC_RELAXED) == prow &&
@@ -710,10 +723,11 @@ long long keyed_elements(Cursor& c, const char* stop, const KeyedOut& o, KeyInde
         uint32_t plen;
         int32_t pslot, prow;
         uint64_t ptag;
-        if (prev_slot >= 0 && ix.predict(prev_slot, plen, pslot, prow, ptag) && (size_t)(c.e - m0) >= plen &&
-            m0[plen - 1] == '}' && __atomic_load_n(&ix.slots[pslot].row, __ATOMIC_RELAXED) == prow &&
-            KeyIndex::tag_of(bytes_hash(m0, plen), plen, pslot, prow) == ptag) {
-          c.p = m0 + plen;
+        const char* s0 = pred_span(m0, c.e, o.skip_name);
+        if (prev_slot >= 0 && ix.predict(prev_slot, plen, pslot, prow, ptag) && (size_t)(c.e - s0) >= plen &&
+            s0[plen - 1] == '}' && __atomic_load_n(&ix.slots[pslot].row, __ATOMIC_RELAXED) == prow &&
+            KeyIndex::tag_of(bytes_hash(s0, plen), plen, pslot, prow) == ptag) {
+          c.p = s0 + plen;
           cur_slot = pslot;
           ix.prefetch_slot(pslot);  // the next element's prediction, needed after the samples
           row = prow;
@@ -723,8 +737,8 @@ long long keyed_elements(Cursor& c, const char* stop, const KeyedOut& o, KeyInde
         } else {
           if (scan_labels(c, o.la, o.lb, a0, a1, b0, b1)) {
             flat = true;  // learnable: the next tick can predict this label object
-            lab0 = m0;
-            lab_len = (uint32_t)(c.p - m0);
+            lab0 = s0;
+            lab_len = (uint32_t)(c.p - s0);
           } else {
             // not flat: brace matching for the extent, then the lenient lookup
             // of fm_prom_dense_keyed, so both decoders agree on any input
@@ -1034,7 +1048,7 @@ long long fm_prom_dense_indexed(const char* buf, long long len, double start, do
     r = 0;
   } else {
     const KeyedOut o{start, step, T, out, ld, max_rows, {label_a, strlen(label_a)}, {label_b, strlen(label_b)},
-                     buf};
+                     buf, strcmp(label_a, "__name__") != 0 && strcmp(label_b, "__name__") != 0};
     r = keyed_elements(c, buf + len + 1, o, *ix, k);
   }
   if (dropped) *dropped = k.dropped;
@@ -1150,6 +1164,7 @@ long long fm_prom_decode_bodies(int nb, const char* const* bufs, const long long
       tasks.push_back(Task{j, cut[i], i + 1 < n ? cut[i + 1] : bufs[j] + lens[j] + 1});
   }
   const Label la{label_a, strlen(label_a)}, lb{label_b, strlen(label_b)};
+  const bool skip_name = strcmp(label_a, "__name__") != 0 && strcmp(label_b, "__name__") != 0;
   std::vector<std::atomic<long long>> acc(3 * (size_t)std::max(nb, 1));
   for (auto& a : acc) a.store(0);
   std::vector<std::atomic<long long>> err(std::max(nb, 1));
@@ -1178,7 +1193,7 @@ long long fm_prom_decode_bodies(int nb, const char* const* bufs, const long long
       KeyIndex* ix = (KeyIndex*)index[j];
       Cursor c{tk.p, bufs[j] + lens[j]};
       KeyedCounts k;
-      const KeyedOut o{st_of(j), step, T_of(j), out + c0_of(j), ld, max_rows, la, lb, bufs[j]};
+      const KeyedOut o{st_of(j), step, T_of(j), out + c0_of(j), ld, max_rows, la, lb, bufs[j], skip_name};
       const long long r = keyed_elements(c, tk.stop, o, *ix, k);
       if (r < 0) { err[j].store(1); continue; }
       tk.end = c.p;

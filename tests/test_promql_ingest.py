@@ -179,6 +179,49 @@ def test_decode_bodies_matches_per_body_decode_and_learns_layout():
         np.testing.assert_array_equal(out, ref)
 
 
+def test_family_bodies_share_one_index_layout():
+    """One tick's family bodies (same pods, label objects that differ only in the
+    leading ``__name__``) through ONE shared pod index: each pass decodes exactly,
+    including after the pod order of one family changes, a pod leaves, a metric name
+    carries an escape, and with ``__name__`` as a key label (then no name is skipped)."""
+    from foremast_amd.ingest import native
+    rng = np.random.default_rng(5)
+    n, F = 300, 4
+    pods = [(f"ns{i % 7}", f"app{i // 3}-v2-{i % 3}-7d9f") for i in range(n)]
+    ix = native.LiveKeyIndex("namespace", "pod")
+    ix.set(native.key_hashes([a for a, _ in pods], [b for _, b in pods]), np.arange(n))
+
+    def body(name, order, vals):
+        items = [f'{{"metric":{{"__name__":"{name}","namespace":"{pods[i][0]}","pod":"{pods[i][1]}"}},'
+                 f'"values":[[600000,"{float(vals[i]):.9g}"]]}}' for i in order]
+        return ('{"status":"success","data":{"resultType":"matrix","result":[' + ",".join(items) + "]}}").encode()
+
+    names = [f"namespace_pod:m{f}" for f in range(F - 1)] + ['namespace_pod:m\\"q']
+    for rnd in range(4):
+        vals = rng.normal(50, 9, (F, n)).astype(np.float32)
+        orders = [list(range(n)) for _ in range(F)]
+        if rnd == 2:
+            orders[1] = list(rng.permutation(n))   # one family lists its pods in another order
+            orders[3] = orders[3][:100] + orders[3][101:]  # a pod missing from one family
+        bodies = [body(names[f], orders[f], vals[f]) for f in range(F)]
+        out = np.full((n, F), np.nan, dtype=np.float32)
+        stats = native.decode_bodies(bodies, [ix] * F, [600000.0] * F, 60.0, [1] * F, list(range(F)), out, threads=3)
+        assert [s[0] for s in stats] == [len(o) for o in orders] and all(s[2] == 0 for s in stats)
+        ref = vals.T.copy()
+        if rnd == 2:
+            ref[100, 3] = np.nan
+        np.testing.assert_array_equal(out, ref)
+    # keyed on __name__ itself: the metric name is part of the key and is never skipped
+    t = native.KeyTable([((names[f], pods[0][1]), f) for f in range(F)], "__name__", "pod")
+    for _ in range(2):
+        out = np.full((F, 1), np.nan, dtype=np.float32)
+        one = np.full(n, 7.0, dtype=np.float32)
+        for f in range(F):
+            one[0] = 10 + f
+            native.decode_bodies([body(names[f], [0], one)], [t], [600000.0], 60.0, [1], [0], out, threads=1)
+        np.testing.assert_array_equal(out[:, 0], 10 + np.arange(F, dtype=np.float32))
+
+
 def test_keyed_decoder_number_shapes_match_python_float():
     """The keyed decoder's number paths — the 8-digits-at-a-time decimal path, the
     per-digit exact path, ``from_chars``, the special values — and the per-ordinal
