@@ -18,8 +18,23 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HELPER = os.path.join(ROOT, "tests", "helpers", "elastic_rank.py")
 
 
+class _RendezvousFlake(Exception):
+    """A gloo pair could not connect while the ranks formed (a loaded host): not the
+    code under test; the run is repeated on a fresh store."""
+
+
 @pytest.mark.slow
 def test_rank_stopped_inside_exchange_survivors_reform(tmp_path):
+    for attempt in range(3):
+        try:
+            return _run(tmp_path / f"a{attempt}")
+        except _RendezvousFlake:
+            if attempt == 2:
+                raise
+
+
+def _run(tmp_path):
+    tmp_path.mkdir()
     hb, n, ticks = 3.0, 3, 25  # heartbeat: under a loaded CI host the first exchange alone can take 4 s
     kv = dist.TCPStore("127.0.0.1", 0, is_master=True, wait_for_workers=False,
                        timeout=datetime.timedelta(seconds=60))
@@ -33,7 +48,8 @@ def test_rank_stopped_inside_exchange_survivors_reform(tmp_path):
         if i == 2:
             env["FOREMAST_FAULT"] = "exchange:3"
         procs.append(subprocess.Popen([sys.executable, HELPER, str(port), str(i), str(n), str(hb), str(ticks),
-                                       str(out)], env=env, cwd=ROOT))
+                                       str(out)], env=env, cwd=ROOT,
+                                      stderr=open(tmp_path / f"rank{i}.err", "w")))
         outs.append(out)
     try:
         # wait until the victim froze itself inside its 3rd exchange
@@ -41,6 +57,10 @@ def test_rank_stopped_inside_exchange_survivors_reform(tmp_path):
         t_end = time.time() + 90
         stopped_at = None
         while time.time() < t_end:
+            if victim.poll() is not None:
+                err = (tmp_path / "rank2.err").read_text()
+                if "connectFullMesh failed" in err or "Connection refused" in err:
+                    raise _RendezvousFlake(err[-2000:])
             assert victim.poll() is None, f"victim exited (rc {victim.returncode}) before its fault point"
             with open(f"/proc/{victim.pid}/stat") as f:
                 if f.read().split(") ", 1)[1].split()[0] == "T":
