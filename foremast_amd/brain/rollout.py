@@ -112,7 +112,13 @@ class PodSlots:
         self.cap = int(cap)
         self.refs = np.zeros(self.cap, dtype=np.int32)
         self.hash = np.zeros(self.cap, dtype=np.uint64)
-        self.free: List[int] = list(range(self.cap - 1, -1, -1))
+        # next-fit allocation: new pods take the free slots at and after a cursor, in order.
+        # Rollouts end roughly in the order they started, so the slots after the cursor are
+        # the longest free and a tick's pods sit in slot order as its bodies list them: the
+        # decode's writes to the tick block walk it forwards (a last-in-first-out free list
+        # handed out slots in key-hash order, and the decode's random row writes cost ~3x)
+        self.freemask = np.ones(self.cap, dtype=bool)
+        self.cursor = 0
         self.grown = 0     # bumps when cap grows
         self.live = native.LiveKeyIndex("namespace", "pod") if native.available() else None
         self.index: Dict[int, int] = {}   # the map when the native library is missing
@@ -142,16 +148,21 @@ class PodSlots:
         # next-element predictions -- are walked sequentially by the decode
         new = new[np.argsort(first[new], kind="stable")]
         if len(new):
-            while len(self.free) < len(new):
+            k = len(new)
+            while self.cap - self._n < k:
                 old = self.cap
                 self.cap *= 2
                 self.refs = np.concatenate([self.refs, np.zeros(old, dtype=np.int32)])
                 self.hash = np.concatenate([self.hash, np.zeros(old, dtype=np.uint64)])
-                self.free = list(range(self.cap - 1, old - 1, -1)) + self.free
+                self.freemask = np.concatenate([self.freemask, np.ones(old, dtype=bool)])
+                self.cursor = old  # the fresh half is contiguous
                 self.grown += 1
-            k = len(new)
-            got = np.asarray(self.free[len(self.free) - k:][::-1], dtype=np.int64)
-            del self.free[len(self.free) - k:]
+            c = self.cursor
+            got = np.flatnonzero(self.freemask[c:])[:k] + c
+            if len(got) < k:
+                got = np.concatenate([got, np.flatnonzero(self.freemask[:c])[:k - len(got)]])
+            self.freemask[got] = False
+            self.cursor = int(got[-1]) + 1 if int(got[-1]) + 1 < self.cap else 0
             slots[new] = got
             self.hash[got] = u[new]
             if self.live is not None:
@@ -179,7 +190,7 @@ class PodSlots:
             else:
                 for h in u[gone].tolist():
                     del self.index[h]
-            self.free.extend(gs.tolist())
+            self.freemask[gs] = True
             self._n -= len(gone)
 
     def table(self, fams: int):
@@ -250,6 +261,8 @@ class RolloutMonitor:
         self._done_chunks: "collections.deque" = collections.deque()
         self._done_n = 0
         self._ending: Dict[str, Tuple[str, str, Optional[Dict]]] = {}   # settled at scoring, written at intake
+        self._end_ctx: Optional[Tuple[float, np.ndarray]] = None       # (scoring time, points seen) of the last scoring
+        self._retire_pending: List[RolloutPlan] = []                   # fail-fast jobs written at scoring
         self.written_late: Dict[str, str] = {}                          # statuses the last intake wrote
         self._apps_dirty = False
         self._app_refs: Dict[Tuple[str, str], int] = {}
@@ -1223,6 +1236,8 @@ class RolloutMonitor:
         n = 0
         self.written_late = {}
         try:
+            self._settle_ending()
+            self._retire_deferred()
             self.written_late = self._finish_ending()
             self.timings["ending_ms"] = (time.perf_counter() - t0) * 1e3
             await self.history.load_pending(now)
@@ -1368,7 +1383,19 @@ class RolloutMonitor:
                                                    "values": inter_l[2 * lo_:2 * hi_]}
                 self.last_anom[row] = float(ts[hi_ - 1])
             finish[p.doc_id] = (r.ST_COMPLETED_UNHEALTH, "anomaly detected in " + ",".join(sorted(anomaly)), anomaly)
-        ending = self._pop_ending(now, finish)
+        # the jobs past endTime are settled in the intake half (after the node exchange):
+        # nothing about them is news, and the fail-fast verdicts go out first
+        self._end_ctx = (now, npts)
+        return self._finish(finish, now, defer_retire=True)
+
+    def _settle_ending(self) -> None:
+        """Verdicts of the jobs whose endTime passed by the last scoring (points seen and
+        model state of that scoring); written by :meth:`_finish_ending`."""
+        ctx, self._end_ctx = self._end_ctx, None
+        if ctx is None:
+            return
+        now, npts = ctx
+        ending = self._pop_ending(now, ())  # this scoring's fail-fast jobs have left self.jobs
         if ending:  # past endTime: seen / model checks over every ending job's rows at once
             rr = np.concatenate([p.rows for p in ending])
             lens = np.fromiter((len(p.rows) for p in ending), dtype=np.int64, count=len(ending))
@@ -1383,19 +1410,17 @@ class RolloutMonitor:
                     late[p.doc_id] = (r.ST_COMPLETED_UNKNOWN, "missing historical data", None)
                 else:
                     late[p.doc_id] = (r.ST_COMPLETED_UNKNOWN, "no current metric data", None)
-            # the verdicts of jobs that ran out their watch are settled now; their writes and
-            # the release of their rows wait for the intake half (after the node exchange):
-            # nothing about them is news, and the fail-fast verdicts go out first
             self._ending.update(late)
-        return self._finish(finish, now)
 
     def _finish_ending(self) -> Dict[str, str]:
         late, self._ending = self._ending, {}
         return self._finish(late, self.clock()) if late else {}
 
-    def _finish(self, finish: Dict[str, Tuple[str, str, Optional[Dict]]], now: float) -> Dict[str, str]:
+    def _finish(self, finish: Dict[str, Tuple[str, str, Optional[Dict]]], now: float,
+                defer_retire: bool = False) -> Dict[str, str]:
         """Write the final status of ``finish`` (job -> (status, reason, anomaly)) and
-        retire the jobs."""
+        retire the jobs (``defer_retire``: their rows, slots and history references are
+        released at the next intake half, :meth:`_retire_deferred`)."""
         if not finish:
             return {}
         items = []
@@ -1421,8 +1446,16 @@ class RolloutMonitor:
         for st, n in counts.items():
             self.metrics.jobs.labels(status=st).inc(n)
         if done_plans:
-            self._retire(done_plans, now)
+            if defer_retire:
+                self._retire_pending.extend(done_plans)
+            else:
+                self._retire(done_plans, now)
         return written
+
+    def _retire_deferred(self) -> None:
+        plans, self._retire_pending = self._retire_pending, []
+        if plans:
+            self._retire(plans, self.clock())
 
     DONE_BANDS_MAX = 1 << 20   # rows of finished jobs whose last band stays exported
 

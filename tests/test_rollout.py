@@ -247,3 +247,24 @@ def test_node_brain_serves_rollout_jobs(device):
 
 def store_status(docs):
     return {app: d["status"] for app, d in docs.items()}
+
+
+def test_pod_slots_next_fit_and_refcounts():
+    """Pod slots: shared pods are reference counted, a released pod's key is retired,
+    and new pods take the free slots after the cursor in order (a tick's pods sit in
+    slot order, so the decode's block writes walk forwards), wrapping and growing."""
+    from foremast_amd.brain.rollout import PodSlots
+    ps = PodSlots(cap=8)
+    h = np.arange(1, 100, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+    a = ps.acquire(h[:6])
+    assert a.tolist() == list(range(6))
+    assert ps.acquire(h[[2, 3]]).tolist() == [2, 3]          # shared: same slots, two references
+    ps.release(h[:4])                                          # 0, 1 free; 2, 3 still referenced
+    assert ps.slot_of(h[:4]).tolist() == [-1, -1, 2, 3] and len(ps) == 4
+    assert ps.acquire(h[6:9]).tolist() == [6, 7, 0]            # after the cursor, then wrap
+    assert ps.acquire(h[9:13]).tolist() == [8, 9, 10, 11]      # grown: the fresh half, in order
+    assert ps.cap == 16 and len(ps) == 11
+    ps.release(h[[2, 3, 4, 5, 6]])
+    ps.release(h[[2, 3]])
+    assert ps.slot_of(h[[2, 3, 4]]).tolist() == [-1, -1, -1]
+    assert ps.acquire(h[20:25]).tolist() == [12, 13, 14, 15, 1]  # after the cursor, then wrap
