@@ -100,7 +100,9 @@ class ClusterHealth:
         # this rank's roster record, built only when the roster changed (O(apps) per change,
         # not per tick: a node holds tens of thousands of apps)
         if self._mine is None or self._mine_version != roster_version:
-            self._mine = {"names": [list(n) if n else None for n in names], "version": roster_version}
+            # (namespace, app) tuples as given (JSON writes them as lists; a C-level copy,
+            # not a Python loop: the roster of a node with arrivals changes every tick)
+            self._mine = {"names": list(names), "version": roster_version}
             self._mine_version = roster_version
         mine = dict(info or {}, **self._mine)
         if self.kv is not None and comm.active(self.group) and self._published != roster_version:
