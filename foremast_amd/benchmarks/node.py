@@ -383,8 +383,9 @@ def setup_node(args, world, rank, dev):
         "pods_new_old": [P, P],
         "watch_window_min": W,
         "path": "service.register -> store claim -> plan -> resident history -> fit at admission -> per tick: "
-                "history advance + pod windows as query_range JSON -> native decode -> H2D -> scatter -> rank tests "
-                "-> cached-state band/verdict -> D2H -> fail-fast writes -> node health exchange",
+                "pod windows as query_range JSON -> native decode -> H2D -> scatter -> rank tests "
+                "-> cached-state band/verdict -> D2H -> fail-fast writes -> node health exchange [detect latency] "
+                "-> endTime writes, history advance, claims, admission",
         "warm_node": "resident 7-day history of every (app, metric) in HBM before the jobs arrive",
         "setup_s": round(setup_s, 2),
         "register_s": round(register_s, 3),
@@ -725,10 +726,11 @@ def setup_arrival(args, world, rank, dev):
         "metrics_per_job": M,
         "pods_new_old": [P, P],
         "app_pool": A_all,
-        "path": "per tick: score running jobs (history advance + pod windows as query_range JSON -> native decode "
-                "-> H2D -> scatter -> rank tests -> cached-state band/verdict -> D2H -> fail-fast / endTime writes) "
-                "-> node health exchange [detect latency] -> claim + native job decode + admission (rows, slots, "
-                "HW fit of the new rows, baseline windows) of this minute's arrivals",
+        "path": "per tick: score running jobs (pod windows as query_range JSON -> native decode "
+                "-> H2D -> scatter -> rank tests -> cached-state band/verdict -> D2H -> fail-fast writes) "
+                "-> node health exchange [detect latency] -> endTime writes + row release, history advance, "
+                "claim + native job decode + admission (rows, slots, HW fit of the new rows, baseline windows) "
+                "of this minute's arrivals",
         "warm_node": "resident 7-day history of every (app, metric) in HBM",
         "setup_s": round(setup_s, 2),
         "register_s": round(register_s, 3),

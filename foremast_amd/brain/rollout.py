@@ -1172,23 +1172,22 @@ class RolloutMonitor:
 
     # ------------------------------------------------------------------ ticks
     async def score_tick(self) -> Dict[str, str]:
-        """The scoring half of a tick: heartbeat, history advance, window ingest,
-        scoring, verdicts of the running jobs; returns job -> status written."""
+        """The scoring half of a tick: heartbeat, window ingest, scoring, verdicts of
+        the running jobs; returns job -> status written.  (The resident history is
+        advanced in the intake half: scoring reads the admission-time model and the
+        windows, not the week; admission needs the newest minute.)"""
         t_tick = time.perf_counter()
         now = self.clock()
         t_new = float(np.floor(now / self.step) * self.step)
-        t0 = time.perf_counter()
         try:
             # inside the guard: a store error on this rank must not skip the lockstep
             # exchange of the intake half, or its peers' all_to_all would pair with another
             # collective
             self.store.heartbeat(self.worker_id, now)
-            await self.history.sync(now, load=False)
         except Exception:  # noqa: BLE001
             if self.router is None:
                 raise
-            log.exception("rollout history step failed (the affine exchange still runs)")
-        self.timings["history_ms"] = (time.perf_counter() - t0) * 1e3
+            log.exception("rollout heartbeat failed (the affine exchange still runs)")
         self._refresh_apps()
         written: Dict[str, str] = {}
         if not self.jobs:
@@ -1240,6 +1239,9 @@ class RolloutMonitor:
             self._retire_deferred()
             self.written_late = self._finish_ending()
             self.timings["ending_ms"] = (time.perf_counter() - t0) * 1e3
+            t1 = time.perf_counter()
+            await self.history.sync(now, load=False)  # the newest minute of every resident week
+            self.timings["history_ms"] = (time.perf_counter() - t1) * 1e3
             await self.history.load_pending(now)
             n = await self._admit(now)
         except Exception:  # noqa: BLE001
