@@ -827,7 +827,11 @@ long long keyed_elements(Cursor& c, const char* stop, const KeyedOut& o, KeyInde
     }
     if (!have_labels) key = series_key("", "", "", "");
     resolve();
-    prev_slot = flat ? cur_slot : -1;
+    // an unmatched series (a pod the node does not watch, e.g. of a job not admitted yet)
+    // keeps the chain: the next element is predicted from the last matched one, so only
+    // the unmatched element itself takes the full parse
+    if (!flat) prev_slot = -1;
+    else if (cur_slot >= 0) prev_slot = cur_slot;
     ++k.series;
     if (c.eat(',')) {
       c.ws();
