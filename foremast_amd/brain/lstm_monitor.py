@@ -31,6 +31,7 @@ LSTM-autoencoder per node, trained data-parallel across the ranks
 
 from __future__ import annotations
 
+import itertools
 import json
 import logging
 import os
@@ -152,6 +153,7 @@ class LstmMonitor:
         # the rollout engine (its canary pods' mean), and their verdicts are read back
         self.sync_history = True     # False: another monitor drives the shared history
         self._feed: Optional[Tuple[List[str], np.ndarray]] = None
+        self._row_of: Dict[str, int] = {}   # admitted entity -> row (C-level lookups of a fed batch)
         self.hits: Dict[str, Tuple[float, np.ndarray]] = {}
 
     # ------------------------------------------------------------------ membership
@@ -238,7 +240,7 @@ class LstmMonitor:
 
     def feed_matrix(self, jids: Sequence[str], vals: np.ndarray) -> None:
         """:meth:`feed` as one ``[len(jids), F]`` float32 matrix (row i: job ``jids[i]``)."""
-        self._feed = (list(jids), vals) if len(jids) else None
+        self._feed = (jids, vals) if len(jids) else None
 
     def after_reform(self) -> None:
         """RC4: every rank adopts rank 0's weights and optimizer state after the
@@ -264,6 +266,7 @@ class LstmMonitor:
         e = self.jobs.pop(jid, None) or self.waiting.pop(jid, None)
         if e is None:
             return -1
+        self._row_of.pop(jid, None)
         self.history.unwant_h(e.hk, now)
         if e.row < 0:
             return -1
@@ -350,6 +353,7 @@ class LstmMonitor:
         app_ids = np.empty(len(ready), dtype=np.int64)
         for i, (e, row) in enumerate(zip(ready, free)):
             del self.waiting[e.doc["id"]]
+            self._row_of[e.doc["id"]] = row
             e.row = row
             self.jobs[e.doc["id"]] = e
             self.row_job[row] = e.doc["id"]
@@ -408,8 +412,7 @@ class LstmMonitor:
     def _fed(self, x: torch.Tensor) -> torch.Tensor:
         jids, vals = self._feed
         self._feed = None
-        jobs = self.jobs
-        rows = np.fromiter(((jobs[j].row if j in jobs else -1) for j in jids), dtype=np.int64, count=len(jids))
+        rows = np.fromiter(map(self._row_of.get, jids, itertools.repeat(-1)), dtype=np.int64, count=len(jids))
         ok = rows >= 0
         if not ok.any():
             return x

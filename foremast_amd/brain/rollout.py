@@ -1286,8 +1286,9 @@ class RolloutMonitor:
             # the jobs' rows, concatenated once per change of the job set
             if self._lstm_cat is None:
                 jids = list(self._lstm_rows)
-                lens = np.fromiter((len(self._lstm_rows[j]) for j in jids), dtype=np.int64, count=len(jids))
-                rows = np.concatenate([self._lstm_rows[j] for j in jids])
+                per = list(self._lstm_rows.values())
+                lens = np.fromiter(map(len, per), dtype=np.int64, count=len(per))
+                rows = np.concatenate(per)
                 job = np.repeat(np.arange(len(jids)), lens)
                 feat = np.arange(len(rows)) - np.repeat(np.cumsum(lens) - lens, lens)
                 self._lstm_cat = (jids, torch.from_numpy(rows).to(self.device), job, feat)
