@@ -280,7 +280,13 @@ class RolloutMonitor:
         # across the ranks; every rank ticks it in lockstep
         self.joint_lstm = None
         self._lstm_rows: Dict[str, np.ndarray] = {}   # job -> its rows in feature (sorted alias) order
-        self._lstm_cat = None   # (jobs, their rows concatenated, job / feature index per row); None: stale
+        # the LSTM jobs' rows as one [slots, F] matrix (a slot per job, -1: no row / free slot),
+        # updated per attach / detach; its device copy is refreshed when it changed
+        self._lstm_slot: Dict[str, int] = {}
+        self._lstm_jids: List[Optional[str]] = []
+        self._lstm_free: List[int] = []
+        self._lstm_mat = np.zeros((0, 1), dtype=np.int64)
+        self._lstm_cat = None   # device copy of the used part of _lstm_mat; None: stale
         if self.cfg.algorithm in ("lstm", "auto"):
             from .lstm_monitor import LstmMonitor
             self.joint_lstm = LstmMonitor(store, self.cfg, prom=self.prom, device=self.device,
@@ -519,7 +525,7 @@ class RolloutMonitor:
             self.slots.release(p.pod_keys)
         self._release_jslot(p)
         if self._lstm_rows.pop(jid, None) is not None:
-            self._lstm_cat = None
+            self._lstm_unslot([jid])
             self.joint_lstm.detach([jid], now)
         p.rows = np.zeros(0, dtype=np.int64)
 
@@ -692,7 +698,7 @@ class RolloutMonitor:
             if kind == "lstm" and self.joint_lstm is not None:
                 order = order[:self.joint_lstm.F]
                 self._lstm_rows[p.doc_id] = p.rows[order]
-                self._lstm_cat = None
+                self._lstm_put(p.doc_id, p.rows[order])
                 attach.append((p.doc_id, [al[k] for k in order], p.cols.u64[p.s0 + np.asarray(order), 0].tolist(),
                                p.app, p.end_ts, lambda i, p=p, order=order: p.cols.hkey_at(p.s0 + order[i])))
                 continue
@@ -1276,6 +1282,32 @@ class RolloutMonitor:
         rr, cc = np.nonzero(flag)
         return rr, cc, x[rr, cc]
 
+    def _lstm_put(self, jid: str, rows: np.ndarray) -> None:
+        F = self.joint_lstm.F
+        if self._lstm_mat.shape[1] != F:
+            self._lstm_mat = np.full((max(64, len(self._lstm_mat)), F), -1, dtype=np.int64)
+        if self._lstm_free:
+            k = self._lstm_free.pop()
+            self._lstm_jids[k] = jid
+        else:
+            k = len(self._lstm_jids)
+            self._lstm_jids.append(jid)
+            if k >= len(self._lstm_mat):
+                self._lstm_mat = np.concatenate([self._lstm_mat, np.full_like(self._lstm_mat, -1)])
+        self._lstm_slot[jid] = k
+        self._lstm_mat[k] = -1
+        self._lstm_mat[k, :min(F, len(rows))] = rows[:F]
+        self._lstm_cat = None
+
+    def _lstm_unslot(self, jids: Sequence[str]) -> None:
+        ks = [self._lstm_slot.pop(j) for j in jids if j in self._lstm_slot]
+        if ks:
+            self._lstm_mat[ks] = -1
+            for k in ks:
+                self._lstm_jids[k] = None
+            self._lstm_free.extend(ks)
+            self._lstm_cat = None
+
     async def _tick_lstm(self, last_c: torch.Tensor) -> Dict[str, Tuple[float, np.ndarray]]:
         """The joint LSTM's tick (lockstep: every rank, every tick, jobs or not): feed
         each LSTM job's newest canary minute (pod mean per metric), one data-parallel
@@ -1283,24 +1315,19 @@ class RolloutMonitor:
         if self.joint_lstm is None:
             return {}
         if self._lstm_rows:
-            # the jobs' rows, concatenated once per change of the job set
+            # [slots, F] rows of the jobs (one H2D per change of the job set); free slots and
+            # missing features read NaN, and a free slot's job is None (not fed)
+            n = len(self._lstm_jids)
             if self._lstm_cat is None:
-                jids = list(self._lstm_rows)
-                per = list(self._lstm_rows.values())
-                lens = np.fromiter(map(len, per), dtype=np.int64, count=len(per))
-                rows = np.concatenate(per)
-                job = np.repeat(np.arange(len(jids)), lens)
-                feat = np.arange(len(rows)) - np.repeat(np.cumsum(lens) - lens, lens)
-                self._lstm_cat = (jids, torch.from_numpy(rows).to(self.device), job, feat)
-            jids, ra, job, feat = self._lstm_cat
+                self._lstm_cat = torch.from_numpy(self._lstm_mat[:n].copy()).to(self.device)
+            m = self._lstm_cat
+            F = m.shape[1]
+            ra = m.clamp(min=0).view(-1)
             col = last_c[ra]
             win = self.win[ra].view(len(ra), self.P, self.Wc)
-            v = torch.nanmean(win.gather(2, col.view(-1, 1, 1).expand(-1, self.P, 1))[:, :, 0], 1).cpu().numpy()
-            F = self.joint_lstm.F
-            vals = np.full((len(jids), F), np.nan, dtype=np.float32)
-            keep = feat < F
-            vals[job[keep], feat[keep]] = v[keep]
-            self.joint_lstm.feed_matrix(jids, vals)
+            v = torch.nanmean(win.gather(2, col.view(-1, 1, 1).expand(-1, self.P, 1))[:, :, 0], 1)
+            v = torch.where(m.view(-1) >= 0, v, torch.full_like(v, float("nan")))
+            self.joint_lstm.feed_matrix(self._lstm_jids, v.view(n, F).float().cpu().numpy())
         else:
             self.joint_lstm.feed_matrix([], np.zeros((0, self.joint_lstm.F), dtype=np.float32))
         await self.joint_lstm.score_tick()  # the lockstep half runs in intake()
@@ -1491,8 +1518,7 @@ class RolloutMonitor:
         if self.joint_lstm is not None and self._lstm_rows:
             gone = [p.doc_id for p in plans if self._lstm_rows.pop(p.doc_id, None) is not None]
             if gone:
-                self._lstm_cat = None
-            if gone:
+                self._lstm_unslot(gone)
                 self.joint_lstm.detach(gone, now)
 
     # ------------------------------------------------------------------ node integration
