@@ -25,6 +25,7 @@ decoder accepts.
 from __future__ import annotations
 
 import ctypes
+import itertools
 import os
 import re
 from collections import OrderedDict
@@ -225,6 +226,12 @@ def hkey_hash(k: Key) -> int:
     return native.key_hash(k[0] + "\x1f" + k[1], k[2] + "\x1f" + k[3])
 
 
+_NO_ROWS = np.zeros(0, dtype=np.int64)
+_NO_KEYS = np.zeros(0, dtype=np.uint64)
+_NO_ROWS.flags.writeable = False   # shared by every unadmitted plan: replaced, never written
+_NO_KEYS.flags.writeable = False
+
+
 class RolloutPlan:
     """A job's plan: its series are rows ``[s0, s0 + n)`` of ``cols``."""
 
@@ -235,8 +242,8 @@ class RolloutPlan:
         self.doc_id, self.app, self.end_ts = doc_id, app, end_ts
         self.cols, self.s0, self.n = cols, s0, n
         self.doc: Dict = doc if doc is not None else {}
-        self.rows = np.zeros(0, dtype=np.int64)        # table rows of the admitted job's series
-        self.pod_keys = np.zeros(0, dtype=np.uint64)   # pod slots the admitted job holds
+        self.rows = _NO_ROWS        # table rows of the admitted job's series
+        self.pod_keys = _NO_KEYS    # pod slots the admitted job holds
         self.jslot = -1                                # the admitted job's slot in the engine's job table
         self._series: Optional[List[RolloutSeries]] = None
 
@@ -430,8 +437,12 @@ def _native_batch(docs: Sequence[Dict], step: float, window_cols: int) -> Option
     lib = native._load()
     if lib is None or not docs:
         return None
-    fields = [d.get(k) for d in docs for k in DOC_FIELDS]
-    fields = [f if isinstance(f, str) else "" for f in fields]
+    # document-major [d0.f0, d0.f1, ..., d1.f0, ...] with C-level loops (one map per field)
+    n_d = len(docs)
+    fields = list(itertools.chain.from_iterable(zip(*[map(dict.get, docs, itertools.repeat(k, n_d),
+                                                          itertools.repeat("", n_d)) for k in DOC_FIELDS])))
+    if set(map(type, fields)) != {str}:
+        fields = [f if isinstance(f, str) else "" for f in fields]
     joined = "".join(fields)
     if joined.isascii():  # one encode; byte offsets = character offsets
         lens = np.fromiter(map(len, fields), dtype=np.int64, count=len(fields))
