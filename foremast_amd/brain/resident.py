@@ -242,8 +242,7 @@ class ResidentHistory:
         if keep.any():
             refs.update(zip(itertools.compress(keys, keep), left[keep].tolist()))
         gone = list(itertools.compress(keys, ~keep))
-        for h in gone:
-            refs.pop(h, None)
+        collections.deque(map(refs.pop, gone, itertools.repeat(None)), maxlen=0)  # pops in C
         self._idle.extend(zip(itertools.repeat(now), gone))  # expiry candidates (checked in time order)
         self.last_used.update(dict.fromkeys(keys, now))
 
