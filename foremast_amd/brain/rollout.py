@@ -1371,6 +1371,7 @@ class RolloutMonitor:
         inter = np.empty(2 * len(ar), dtype=np.float64)
         inter[0::2], inter[1::2] = ts, av
         inter_l = inter.tolist()
+        pcs_l = pcs.tolist()
         span: Dict[int, Tuple[int, int]] = {}
         if len(ar):
             st = np.flatnonzero(np.r_[True, ar[1:] != ar[:-1]])
@@ -1408,7 +1409,7 @@ class RolloutMonitor:
                     continue
                 lo_, hi_ = sp
                 pods = p.cols.cur_pods(p.s0 + int(self.row_k[row]))
-                names = {pods[q] for q in np.unique(pcs[lo_:hi_]).tolist() if q < len(pods)}
+                names = {pods[q] for q in set(pcs_l[lo_:hi_]) if q < len(pods)}
                 anomaly[p.cols.alias[p.s0 + k]] = {"tags": ",".join(sorted(n for n in names if n)),
                                                    "values": inter_l[2 * lo_:2 * hi_]}
                 self.last_anom[row] = float(ts[hi_ - 1])
