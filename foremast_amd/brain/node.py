@@ -249,7 +249,10 @@ class NodeBrain:
                 m.sync(steal_from=self.dead or None)
             except Exception as e:  # noqa: BLE001 - the store may be briefly unavailable
                 log.exception("%s claim failed: %s", type(m).__name__, e)
-            await m.intake()  # every rank, every tick: it may run the lockstep window exchange
+            try:
+                await m.intake()  # every rank, every tick: it may run the lockstep window exchange
+            except Exception as e:  # noqa: BLE001 - e.g. the job store is briefly unavailable
+                log.exception("%s intake failed: %s", type(m).__name__, e)
         self._freeze_admitted()
         self.timings = {"detect_ms": (t1 - t0) * 1e3, "intake_ms": (time.perf_counter() - t1) * 1e3}
         table["generation"] = self.world.generation if self.world else 0

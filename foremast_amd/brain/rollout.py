@@ -86,6 +86,8 @@ from .resident import Key, ResidentHistory, fetch_decode, quote_selector, range_
 log = logging.getLogger("foremast.rollout")
 
 HB = 16  # forecast offsets kept per row (kernels.HALF_HB): horizons 1..16 of the current window
+_NO_ROWS = np.zeros(0, dtype=np.int64)
+_NO_KEYS = np.zeros(0, dtype=np.uint64)
 
 
 def plan_rollout(doc: Dict, cfg: BrainConfig, step: float = 60.0, window_cols: int = 11) -> Optional[RolloutPlan]:
@@ -527,7 +529,8 @@ class RolloutMonitor:
         if self._lstm_rows.pop(jid, None) is not None:
             self._lstm_unslot([jid])
             self.joint_lstm.detach([jid], now)
-        p.rows = np.zeros(0, dtype=np.int64)
+        p.rows = _NO_ROWS
+        p.pod_keys = _NO_KEYS
 
     def _refresh_apps(self) -> None:
         """Apply the app-roster changes of the last admissions / verdicts.  App
@@ -1250,10 +1253,8 @@ class RolloutMonitor:
             self.timings["history_ms"] = (time.perf_counter() - t1) * 1e3
             await self.history.load_pending(now)
             n = await self._admit(now)
-        except Exception:  # noqa: BLE001
-            if self.router is None:
-                raise
-            log.exception("rollout admission failed (the affine exchange still runs)")
+        except Exception:  # noqa: BLE001 - a store / Prometheus error: the lockstep parts below still run
+            log.exception("rollout intake failed (retried next tick; the lockstep exchanges still run)")
         if self.router is not None:
             await self._route()  # every rank, every tick (collectives)
         if self.joint_lstm is not None:  # every rank, every tick: admission, DP step, calibration
@@ -1444,8 +1445,15 @@ class RolloutMonitor:
             self._ending.update(late)
 
     def _finish_ending(self) -> Dict[str, str]:
-        late, self._ending = self._ending, {}
-        return self._finish(late, self.clock()) if late else {}
+        """Write the settled endTime verdicts; they are forgotten only once written
+        (a failing store write keeps them for the next intake, as it keeps the jobs)."""
+        late = {j: v for j, v in self._ending.items() if j in self.jobs}
+        if not late:
+            self._ending = {}
+            return {}
+        written = self._finish(late, self.clock())
+        self._ending = {}
+        return written
 
     def _finish(self, finish: Dict[str, Tuple[str, str, Optional[Dict]]], now: float,
                 defer_retire: bool = False) -> Dict[str, str]:
@@ -1516,6 +1524,10 @@ class RolloutMonitor:
         self._free_rows(freed)
         for p in plans:
             self._release_jslot(p)
+            # the plan object is memoised per job id (plans._PLANS): a later claim of the same
+            # job must not find these rows and pod references, which may belong to others now
+            p.rows = _NO_ROWS
+            p.pod_keys = _NO_KEYS
         if self.joint_lstm is not None and self._lstm_rows:
             gone = [p.doc_id for p in plans if self._lstm_rows.pop(p.doc_id, None) is not None]
             if gone:

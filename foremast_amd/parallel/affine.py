@@ -70,10 +70,11 @@ class ClusterRouter:
         self.seq = 0        # exchanges with requests so far (lockstep: equal on every rank)
         self.exchanges = 0
         self.values_moved = 0
+        self._stale: Optional[str] = None   # this rank's request key of the last exchange
 
     def reset(self, kv=None) -> None:
         """After a re-formation: the new generation's store, sequence from zero."""
-        self.kv, self.seq = kv, 0
+        self.kv, self.seq, self._stale = kv, 0, None
 
     def _store(self):
         if self.kv is None:
@@ -120,6 +121,16 @@ class ClusterRouter:
         counts = torch.empty(world, dtype=torch.int64, device=self.device)
         work = dist.all_gather_into_tensor(counts, cnt, group=self.group, async_op=True)
         comm.wait_bounded(work, self.timeout_s, "affine request counts")
+        if self._stale is not None:
+            # every rank has entered this tick's count gather, so every rank is done reading the
+            # last exchange's requests (a peer that exchanged no bytes with this rank in the
+            # all-to-all may not have synchronised with it there: deleting the key right after
+            # it could pull it from under that peer's read)
+            try:
+                self._store().delete_key(self._stale)
+            except Exception:  # noqa: BLE001 - best-effort cleanup
+                pass
+            self._stale = None
         if int(counts.sum()) == 0:
             return []
         gathered = self._gather_requests(mine, world, rank)
@@ -143,11 +154,7 @@ class ClusterRouter:
         work = dist.all_to_all_single(recv_t, send_t, output_split_sizes=recv_sizes, input_split_sizes=send_sizes,
                                       group=self.group, async_op=True)
         comm.wait_bounded(work, self.timeout_s, "affine window all-to-all")
-        # every peer entered the all-to-all, so every peer has read this exchange's requests
-        try:
-            self._store().delete_key(f"req/{self.seq}/{rank}")
-        except Exception:  # noqa: BLE001 - best-effort cleanup
-            pass
+        self._stale = f"req/{self.seq}/{rank}"   # deleted after the next tick's count gather
         self.seq += 1
         self.values_moved += int(recv_t.numel())
         recv = recv_t.cpu().numpy()

@@ -41,13 +41,25 @@ BEAT_INDEX = "foremast-workers"
 PAGE = 1000  # hits per search page
 
 
-def _kw(field: str) -> str:
-    """Exact-match name of a string field.  Under ES dynamic mapping (how the reference
-    service creates ``documents``: ``elasticsearchstore.go:54-59`` indexes without a
-    mapping) a string is analysed ``text`` — ``node-m0-rollout`` is stored as the tokens
-    ``node`` / ``m0`` / ``rollout`` — with an exact ``.keyword`` sub-field; ``terms``
-    filters must use the latter."""
-    return field + ".keyword"
+def _kw_of(mapping: Dict[str, Any], field: str) -> Optional[str]:
+    """Exact-match name of a string field under an index mapping (the ``properties``
+    of its one type), or None when the mapping does not say yet.  Under ES dynamic
+    mapping (how the reference service creates ``documents``:
+    ``elasticsearchstore.go:54-59`` indexes without a mapping) a string is analysed
+    ``text`` — ``node-m0-rollout`` is stored as the tokens ``node`` / ``m0`` /
+    ``rollout`` — with an exact ``.keyword`` sub-field, which ``terms`` filters must
+    use; an operator-created index that maps the field as ``keyword`` has no such
+    sub-field and is matched on the bare field."""
+    spec = mapping.get(field)
+    if not isinstance(spec, dict):
+        return None
+    if spec.get("type") == "keyword":
+        return field
+    sub = spec.get("fields") or {}
+    for name, f in sub.items():
+        if isinstance(f, dict) and f.get("type") == "keyword":
+            return f"{field}.{name}"
+    return None
 
 
 class ElasticJobStore(JobStore):
@@ -60,6 +72,29 @@ class ElasticJobStore(JobStore):
         if transport is not None:
             kw["transport"] = transport
         self.http = httpx.Client(**kw)
+        self._kw_cache: Dict[str, str] = {}
+
+    def _kw(self, field: str) -> str:
+        """Exact-match name of ``field`` in the job index, read from the index mapping
+        once it names the field (dynamic mapping: ``<field>.keyword``; an explicit
+        ``keyword`` mapping: the bare field).  Until then the dynamic-mapping name is
+        used and the mapping is asked again next time."""
+        got = self._kw_cache.get(field)
+        if got is not None:
+            return got
+        name = None
+        try:
+            resp = self.http.get(f"{self.base}/{self.index}/_mapping")
+            if resp.status_code == 200:
+                for idx in resp.json().values():
+                    for typ in (idx.get("mappings") or {}).values():
+                        name = name or _kw_of((typ or {}).get("properties") or {}, field)
+        except (httpx.HTTPError, ValueError, AttributeError):
+            name = None
+        if name is None:
+            return field + ".keyword"
+        self._kw_cache[field] = name
+        return name
 
     # ------------------------------------------------------------------ plumbing
     def _doc_url(self, job_id: str, suffix: str = "") -> str:
@@ -123,7 +158,7 @@ class ElasticJobStore(JobStore):
 
     def _search(self, statuses, size: int = PAGE, extra=(), must_not=(), index: Optional[str] = None,
                 doc_type: Optional[str] = None, offset: int = 0) -> List[Tuple[Dict[str, Any], int]]:
-        filt = ([{"terms": {_kw("status"): list(statuses)}}] if statuses else []) + list(extra)
+        filt = ([{"terms": {self._kw("status"): list(statuses)}}] if statuses else []) + list(extra)
         body = {"query": {"bool": {"filter": filt, "must_not": list(must_not)}}, "from": offset,
                 "size": size, "version": True, "sort": [{"modified_ts": {"order": "asc"}}]}
         resp = self.http.post(f"{self.base}/{index or self.index}/{doc_type or self.doc_type}/_search",
@@ -170,10 +205,10 @@ class ElasticJobStore(JobStore):
         # crowded out of the oldest-first window
         cand += self._search_pages(r.INPROGRESS_STATUSES, 4 * PAGE,
                                    extra=[{"range": {"modified_ts": {"lt": cutoff}}}],
-                                   must_not=[{"terms": {_kw("claimed_by"): sorted(beats)}}] if beats else [])
+                                   must_not=[{"terms": {self._kw("claimed_by"): sorted(beats)}}] if beats else [])
         if steal_from:
             cand += self._search_pages(r.INPROGRESS_STATUSES, 4 * PAGE,
-                                       extra=[{"terms": {_kw("claimed_by"): sorted(steal_from)}}])
+                                       extra=[{"terms": {self._kw("claimed_by"): sorted(steal_from)}}])
         seen, keep = set(), []
         for d, ver in sorted(cand, key=lambda dv: dv[0].get("modified_ts", 0.0)):
             if d["id"] in seen:

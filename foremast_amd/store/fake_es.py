@@ -16,6 +16,11 @@ only works against a lenient fake:
 * dynamic mapping of strings: a string field is analysed ``text`` (lower-cased,
   split on anything but letters, digits and ``_``) with an exact ``<field>.keyword``
   sub-field, so ``term`` / ``terms`` on the bare field match single tokens only.
+
+An index created with explicit mappings (``PUT /<index>`` with ``{"mappings": {type:
+{"properties": ...}}}``, as an operator might) keeps them: a field mapped ``keyword``
+is matched exactly on its bare name and has no ``.keyword`` sub-field.
+``GET /<index>/_mapping`` reports both kinds.
 """
 
 from __future__ import annotations
@@ -31,6 +36,7 @@ class FakeElasticsearch:
     def __init__(self) -> None:
         self.docs: Dict[Tuple[str, str], Tuple[Dict[str, Any], int]] = {}
         self.types: Dict[str, str] = {}  # index -> its one mapping type
+        self.explicit: Dict[str, Dict[str, Dict[str, Any]]] = {}  # index -> explicit field mappings
         self.lock = threading.Lock()
         self.requests: List[str] = []
         self.fail_next = 0  # fault injection: return 503 for the next N requests
@@ -66,6 +72,10 @@ class FakeElasticsearch:
         parts = [p for p in path.split("/") if p]
         if not parts:
             return 200, {"version": {"number": "6.4.2"}, "tagline": "You Know, for Search"}
+        if len(parts) == 1 and method == "PUT":
+            return self._create_index(parts[0], body or {})
+        if len(parts) == 2 and parts[1] == "_mapping" and method == "GET":
+            return self._mapping(parts[0])
         if len(parts) == 3 and parts[2] == "_search" and method in ("GET", "POST"):
             return self._search(parts[0], body or {})
         if len(parts) == 4 and parts[3] == "_create" and method in ("PUT", "POST"):
@@ -83,6 +93,36 @@ class FakeElasticsearch:
                 ver = int(qs["version"]) if "version" in qs else None
                 return self._put(idx, did, body, create=False, version=ver, typ=_typ)
         return 400, {"error": f"unsupported {method} {path}"}
+
+    def _create_index(self, idx: str, body: Dict[str, Any]):
+        with self.lock:
+            if idx in self.types:
+                return 400, {"error": {"type": "resource_already_exists_exception"}}
+            maps = body.get("mappings") or {}
+            for typ, m in maps.items():
+                self.types[idx] = typ
+                self.explicit[idx] = dict((m or {}).get("properties") or {})
+        return 200, {"acknowledged": True, "index": idx}
+
+    def _mapping(self, idx: str):
+        with self.lock:
+            if idx not in self.types:
+                return 404, {"error": {"type": "index_not_found_exception"}}
+            props: Dict[str, Any] = {}
+            for (i, _did), (d, _v) in self.docs.items():
+                if i != idx:
+                    continue
+                for k, v in d.items():
+                    if k in props:
+                        continue
+                    if isinstance(v, str):
+                        props[k] = {"type": "text", "fields": {"keyword": {"type": "keyword", "ignore_above": 256}}}
+                    elif isinstance(v, bool):
+                        props[k] = {"type": "boolean"}
+                    elif isinstance(v, (int, float)):
+                        props[k] = {"type": "float" if isinstance(v, float) else "long"}
+            props.update(self.explicit.get(idx, {}))
+            return 200, {idx: {"mappings": {self.types[idx]: {"properties": props}}}}
 
     def _put(self, idx: str, did: str, doc: Any, create: bool, version, typ: str):
         with self.lock:
@@ -103,18 +143,19 @@ class FakeElasticsearch:
     def _search(self, idx: str, body: Dict[str, Any]):
         with self.lock:
             items = [(did, d, v) for (i, did), (d, v) in self.docs.items() if i == idx]
-        if not any(True for (i, _d) in self.docs if i == idx):
+        if idx not in self.types:
             return 404, {"error": {"type": "index_not_found_exception"}}
+        explicit = self.explicit.get(idx, {})
         q = body.get("query", {"match_all": {}})
         b = q.get("bool", {})
 
         def hit(doc, f) -> bool:
             if "terms" in f:
                 (key, vals), = f["terms"].items()
-                return any(_matches(doc, key, v) for v in vals)
+                return any(_matches(doc, key, v, explicit) for v in vals)
             if "term" in f:
                 (key, val), = f["term"].items()
-                return _matches(doc, key, val)
+                return _matches(doc, key, val, explicit)
             if "range" in f:
                 (key, ops), = f["range"].items()
                 v = doc.get(key, 0)
@@ -139,9 +180,16 @@ class FakeElasticsearch:
 _TOKEN = re.compile(r"[0-9A-Za-z_]+")
 
 
-def _matches(doc: Dict[str, Any], key: str, want: Any) -> bool:
+def _matches(doc: Dict[str, Any], key: str, want: Any, explicit: Dict[str, Dict[str, Any]] = None) -> bool:
     """ES term-level match under dynamic mapping: ``x.keyword`` is exact; a bare string
-    field holds analysed tokens (a term query is not analysed, so it must equal one)."""
+    field holds analysed tokens (a term query is not analysed, so it must equal one).
+    A field mapped ``keyword`` explicitly is exact on its bare name and has no
+    ``.keyword`` sub-field."""
+    explicit = explicit or {}
+    if key.endswith(".keyword") and key[: -len(".keyword")] in explicit:
+        return False  # no such sub-field: matches nothing, silently (as ES does)
+    if explicit.get(key, {}).get("type") == "keyword":
+        return doc.get(key) == want
     if key.endswith(".keyword"):
         v = doc.get(key[: -len(".keyword")])
         return isinstance(v, str) and v == want

@@ -268,3 +268,63 @@ def test_pod_slots_next_fit_and_refcounts():
     ps.release(h[[2, 3]])
     assert ps.slot_of(h[[2, 3, 4]]).tolist() == [-1, -1, -1]
     assert ps.acquire(h[20:25]).tolist() == [12, 13, 14, 15, 1]  # after the cursor, then wrap
+
+
+class _FlakyStore:
+    """Wraps a job store; ``fail`` names methods that raise until cleared."""
+
+    def __init__(self, inner):
+        self.inner, self.fail = inner, set()
+
+    def __getattr__(self, name):
+        f = getattr(self.inner, name)
+        if name in self.fail:
+            def boom(*a, **k):
+                raise ConnectionError(f"store down ({name})")
+            return boom
+        return f
+
+
+def test_node_keeps_ticking_when_the_store_fails_during_intake():
+    """a store error inside the intake half (the endTime writes) is
+    logged, the node keeps ticking, and the settled endTime verdicts are written by a
+    later intake once the store is back (nothing is lost)."""
+    from foremast_amd.brain.node import NodeBrain
+    from foremast_amd.brain.streaming import StreamingMonitor
+    clock, prom, raw, ids = world(spike_app=None)
+    store = _FlakyStore(raw)
+    cfg = config()
+    stream = StreamingMonitor(store, cfg, prom=PromClient(transport=httpx.ASGITransport(app=prom.asgi_app())),
+                              device=torch.device("cpu"), ring_len=2880, window=10, clock=clock)
+    roll = monitor(store, prom, clock, "cpu", cfg)
+    node = NodeBrain(stream, None, store, torch.device("cpu"), publish=False, extra=(roll,))
+
+    async def go():
+        for t in (T0, T0 + 60, T0 + 120):
+            clock.t = t
+            await node.tick()
+        assert len(roll.jobs) == 3
+        store.fail = {"update_many", "update"}
+        for t in (T0 + 660, T0 + 720):          # every job past endTime; its writes fail
+            clock.t = t
+            await node.tick()
+        assert {raw.get(j)["status"] for j in ids.values()} == {r.ST_PREPROCESS_INPROGRESS}
+        assert len(roll.jobs) == 3 and roll._ending   # kept: written when the store is back
+        store.fail = set()
+        clock.t = T0 + 780
+        await node.tick()
+    asyncio.run(go())
+    assert {app: raw.get(j)["status"] for app, j in ids.items()} == {
+        "a": r.ST_COMPLETED_HEALTH, "b": r.ST_COMPLETED_HEALTH, "c": r.ST_COMPLETED_HEALTH}
+    assert not roll.jobs and roll.n_live == 0
+
+
+def test_retired_plan_holds_no_rows():
+    """a finished job's memoised plan keeps no rows or pod
+    references, so a later claim of the same job id cannot free another job's."""
+    out, docs, ids, _ = _run("cpu", "moving_average_all")
+    from foremast_amd.brain import plans as pl
+    for jid in ids.values():
+        p = pl._PLANS.get(jid)
+        if p is not None:
+            assert len(p.rows) == 0 and len(p.pod_keys) == 0 and p.jslot == -1

@@ -14,7 +14,15 @@ def _store(kind, tmp_path):
         return MemoryJobStore()
     if kind == "sqlite":
         return SqliteJobStore(str(tmp_path / "jobs.db"))
-    return ElasticJobStore("http://es:9200", transport=httpx.WSGITransport(app=FakeElasticsearch()))
+    es = FakeElasticsearch()
+    if kind == "es-keyword":  # an operator-created index: the lease fields mapped `keyword` explicitly
+        status, _ = es.handle("PUT", "/documents", {}, {"mappings": {"document": {"properties": {
+            "status": {"type": "keyword"}, "claimed_by": {"type": "keyword"}, "id": {"type": "keyword"}}}}})
+        assert status == 200
+    return ElasticJobStore("http://es:9200", transport=httpx.WSGITransport(app=es))
+
+
+KINDS = ["memory", "sqlite", "es", "es-keyword"]
 
 
 def _req(i):
@@ -22,7 +30,7 @@ def _req(i):
                              current_config=f"m== http://p/api/v1/query_range?query=x{i}", strategy="canary")
 
 
-@pytest.mark.parametrize("kind", ["memory", "sqlite", "es"])
+@pytest.mark.parametrize("kind", KINDS)
 def test_heartbeat_keeps_leases_alive(kind, tmp_path):
     st = _store(kind, tmp_path)
     ids = [st.create(_req(i), now=1000.0) for i in range(6)]
@@ -40,7 +48,7 @@ def test_heartbeat_keeps_leases_alive(kind, tmp_path):
     assert sorted(x["id"] for x in d) == sorted(x["id"] for x in b)
 
 
-@pytest.mark.parametrize("kind", ["memory", "sqlite", "es"])
+@pytest.mark.parametrize("kind", KINDS)
 def test_update_many_respects_leases(kind, tmp_path):
     st = _store(kind, tmp_path)
     ids = [st.create(_req(i), now=1000.0) for i in range(3)]
@@ -69,7 +77,7 @@ def test_memory_claim_does_not_scan_live_leases():
     assert len(got) == 1 and len(calls) == 1
 
 
-@pytest.mark.parametrize("kind", ["memory", "sqlite", "es"])
+@pytest.mark.parametrize("kind", KINDS)
 def test_hyphenated_worker_ids(kind, tmp_path):
     """Worker ids like ``node-m0-rollout``: ES dynamic mapping analyses them into tokens,
     so lease filters must match the exact keyword (the fake analyses strings as ES does)."""
@@ -113,3 +121,20 @@ def test_fake_es_one_mapping_type_per_index():
     st.put_meta("cluster_health", {"ok": 1})
     assert st.get_meta("cluster_health") == {"ok": 1}
     assert len(st.claim("node-m0", now=1000.0)) == 1
+
+
+def test_fake_es_explicit_keyword_mapping_has_no_subfield():
+    """On an explicitly keyword-mapped index a `.keyword` filter silently matches
+    nothing (as on ES): the store must read the mapping and use the bare field."""
+    es = FakeElasticsearch()
+    es.handle("PUT", "/documents", {}, {"mappings": {"document": {"properties": {"status": {"type": "keyword"}}}}})
+    es.handle("PUT", "/documents/document/a", {}, {"id": "a", "status": "initial"})
+    q = {"query": {"bool": {"filter": [{"terms": {"status.keyword": ["initial"]}}]}}, "size": 10}
+    assert es.handle("POST", "/documents/document/_search", {}, q)[1]["hits"]["hits"] == []
+    q["query"]["bool"]["filter"] = [{"terms": {"status": ["initial"]}}]
+    assert len(es.handle("POST", "/documents/document/_search", {}, q)[1]["hits"]["hits"]) == 1
+    st = ElasticJobStore("http://es:9200", transport=httpx.WSGITransport(app=es))
+    assert st._kw("status") == "status"
+    dyn = ElasticJobStore("http://es:9200", transport=httpx.WSGITransport(app=FakeElasticsearch()))
+    dyn.create(_req(1), now=1000.0)
+    assert dyn._kw("status") == "status.keyword"
