@@ -171,7 +171,7 @@ def parse():
                    help="run the training step and scoring back to back instead of on two HIP streams")
     a = p.parse_args()
     if a.steps is None:
-        a.steps = (60 if a.arrival_per_tick else 8) if a.config == "node" else 20
+        a.steps = (100 if a.arrival_per_tick else 8) if a.config == "node" else 20
     if a.warmup is None:
         a.warmup = (a.window + 1 if a.arrival_per_tick else 1) if a.config == "node" else 5
         if a.config == "node-lstm":  # a fresh node pretrains its shared model over the warmup ticks
@@ -208,6 +208,37 @@ def self_launch(args, argv) -> int:
     return subprocess.call(cmd, env=env)
 
 
+P99_MIN = 100   # samples below which a p99 is not reported (the max is)
+
+
+def _sum_detection(parts) -> dict:
+    """Detection records of every rank summed into the node's."""
+    out = {k: sum(p[k] for p in parts) for k in ("jobs", "injected_jobs", "tp", "fp", "fn")}
+    out["recall"] = round(out["tp"] / max(1, out["tp"] + out["fn"]), 4)
+    out["false_positive_rate"] = round(out["fp"] / max(1, out["jobs"] - out["injected_jobs"]), 6)
+    out["misses"] = [m for p in parts for m in p.get("misses", [])][:50]
+    out["ranks"] = len(parts)
+    return out
+
+
+def _exchange_summary(bds, steps: int, world: int, config: str) -> dict:
+    """The node health exchange over the timed ticks (rank 0's view): deployed path
+    (ElasticWorld under N ranks), generation, collective time, roster bytes."""
+    xs = [b for b in bds[-steps:] if "exchange_ms" in b]
+    ms = [b["exchange_ms"] for b in xs]
+    by = [b["roster_bytes"] for b in xs]
+
+    def q(v, p):
+        if not v or (p == 99 and len(v) < P99_MIN):
+            return None
+        return round(float(np.percentile(v, p)), 3)
+    return {"path": "ElasticWorld run_tick + ClusterHealth roster deltas" if world > 1 or comm.force_collectives()
+            else "single rank (no collectives)", "ranks": world,
+            "generation": max((b.get("generation", 0) for b in xs), default=0),
+            "exchange_ms_p50_p99_max": [q(ms, 50), q(ms, 99), q(ms, 100)],
+            "roster_bytes_p50_max": [q(by, 50), q(by, 100)], "samples": len(xs)}
+
+
 def init_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
@@ -221,6 +252,10 @@ def init_dist(args):
         dev = torch.device("cuda", local)
     else:
         dev = torch.device("cpu")
+    if args.config in ("node", "node-lstm"):
+        # the product configs join the node as a deployed rank does: an ElasticWorld on the
+        # launcher's store forms the process group (benchmarks/node.py node_world)
+        return world, rank, dev
     # FOREMAST_FORCE_COLLECTIVES=1 (tests/test_rccl_gpu.py): a 1-rank group that still runs
     # every collective, so one GPU exercises the RCCL path of the N-GPU tick
     if world > 1 or comm.force_collectives():
@@ -906,6 +941,10 @@ def main():
         tick_breakdown = {k: round(v, 3) for k, v in node_roll.timings.items()} if node_roll is not None else {}
         if arrival_finish is not None:
             fin_s, statuses, arrival_det = arrival_finish()
+            if world > 1:  # every rank's jobs: the node's detection, not rank 0's share
+                parts = [None] * world
+                dist.all_gather_object(parts, arrival_det)
+                arrival_det = _sum_detection(parts)
         else:
             fin_s, statuses = node_finish()
     coll_ms = agg.flush_timings() if agg is not None else []
@@ -937,7 +976,11 @@ def main():
             "data": "synthetic (seasonal Prometheus-like range-vectors, random per-series params; random-init weights)",
             "config": config,
             "p50_detect_latency_ms": round(float(np.percentile(lat_ms, 50)), 3),
-            "p99_detect_latency_ms": round(float(np.percentile(lat_ms, 99)), 3),
+            # a p99 needs >= 100 samples; with fewer only the max is a statistic worth printing
+            "p99_detect_latency_ms": (round(float(np.percentile(lat_ms, 99)), 3) if len(lat_ms) >= P99_MIN
+                                      else None),
+            "max_detect_latency_ms": round(float(np.max(lat_ms)), 3) if len(lat_ms) else None,
+            "latency_samples": int(len(lat_ms)),
             # device time of the per-tick health collectives (fused all-gather, or RC2 all-reduce +
             # RC1 all-gather), rank 0
             "collective_ms_p50": round(float(np.percentile(coll_ms, 50)), 4) if coll_ms else None,
@@ -951,10 +994,14 @@ def main():
 
             def pct(key, q):
                 xs = [b[key] for b in bds if key in b]
+                if q == 99 and len(xs) < P99_MIN:
+                    return None
                 return round(float(np.percentile(xs, q)), 3) if xs else None
             adm = [b for b in bds if b.get("admitted")]
             res["p50_detect_latency_ms"] = pct("detect_ms", 50)
             res["p99_detect_latency_ms"] = pct("detect_ms", 99)
+            res["max_detect_latency_ms"] = pct("detect_ms", 100)
+            res["latency_samples"] = len([b for b in bds if "detect_ms" in b])
             res["node"] = {
                 "series_scored_timed": int(timed_rows),
                 "detect_ms_p50_p99_max": [pct("detect_ms", 50), pct("detect_ms", 99), pct("detect_ms", 100)],
@@ -973,11 +1020,13 @@ def main():
                 "tick_breakdown_ms": bds,
                 "completion_ticks_s": round(fin_s, 3), "job_statuses_rank0": statuses}
             res["detection"] = arrival_det
-        elif timed_rows is not None:
+        if timed_rows is not None and arrival_finish is None:
             res["node"] = {"series_scored_timed": int(timed_rows), "tick_breakdown_ms_last": tick_breakdown,
                            "tick_breakdown_ms": (node_breakdowns or [])[-args.steps:],
                            "tick_ms": [round(float(x), 2) for x in lat_ms.tolist()],
                            "completion_tick_s": round(fin_s, 3), "job_statuses_rank0": statuses}
+        if timed_rows is not None:
+            res["node"]["exchange"] = _exchange_summary(node_breakdowns or [], args.steps, world, args.config)
         if args.config == "canary" and args.refit_every > 1:
             flags = np.array([REFIT_FLAGS.get(args.warmup + k, True) for k in range(args.steps)])
             res["refit_ticks_timed"] = int(flags.sum())

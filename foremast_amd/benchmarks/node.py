@@ -101,6 +101,37 @@ class BodyServer:
         return body
 
 
+def node_world(world: int, rank: int, dev):
+    """The deployed exchange for an N-rank node bench: under ``torch.distributed.run``
+    (``WORLD_SIZE`` > 1) every rank joins an :class:`~foremast_amd.parallel.elastic.ElasticWorld`
+    on the launcher's store, exactly as a production rank does
+    (:func:`~foremast_amd.brain.node.elastic_world_from_env`): heartbeats, the
+    deadline-guarded ``run_tick``, generation-prefixed roster deltas, re-formation.
+    ``FOREMAST_FORCE_COLLECTIVES=1`` gives a 1-member world (one GPU, real RCCL).
+    None for a plain 1-rank run."""
+    from ..brain.node import elastic_world_from_env
+    from ..parallel import comm
+    if world <= 1 and not comm.force_collectives():
+        return None
+    ew = elastic_world_from_env(dev, force=comm.force_collectives())
+    if ew is not None and f"m{rank}" != ew.members[rank]:
+        raise SystemExit(f"node bench: member order {ew.members} does not put m{rank} at rank {rank}")
+    return ew
+
+
+def _exchange_bd(node, bd: Dict) -> None:
+    """The node health exchange of the tick into its breakdown record."""
+    t = node.table or {}
+    bd["exchange_ms"] = round(float(t.get("collective_ms", 0.0)), 3)
+    bd["roster_bytes"] = int(t.get("roster_bytes", 0))
+    bd["generation"] = int(t.get("generation", 0))
+
+
+def _start_node(node, ew) -> None:
+    if ew is not None:
+        node.start()
+
+
 def _brainworker_share(docs, cfg) -> int:
     """Jobs no resident monitor keys (they would reach BrainWorker); the plan memo is
     reset afterwards so the timed claims decode as in production."""
@@ -285,10 +316,12 @@ def setup_node(args, world, rank, dev):
 
     stream = StreamingMonitor(store, cfg, prom=server, device=dev, worker_id=f"node-m{rank}", ring_len=R,
                               window=W, clock=lambda: clock["t"])
-    node = NodeBrain(stream, None, store, dev, publish=False, extra=(roll,))
+    ew = node_world(world, rank, dev)
+    node = NodeBrain(stream, ew, store, dev, publish=False, extra=(roll,))
     node.owns = lambda d: True  # the rank-local store holds exactly this rank's share
     for mon in node.monitors:
         mon.owns = None
+    _start_node(node, ew)
     loop = asyncio.new_event_loop()
     flagged = set()
 
@@ -313,7 +346,12 @@ def setup_node(args, world, rank, dev):
             st = dict(hist.load_stats)
             cold_ticks.append({"tick": k - 1, "admitted_total": len(roll.jobs), "live_rows": roll.n_live,
                                **{kk: round(v, 3) for kk, v in node.timings.items()}})
-            if len(roll.jobs) == na:
+            done = len(roll.jobs) == na
+            if ew is not None:  # lockstep: every rank runs the same number of intake ticks
+                flag = torch.tensor([int(done)], dtype=torch.int32, device=dev)
+                torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MIN)
+                done = bool(flag.item())
+            if done:
                 break
             clock["t"] = T0 + STEP * 0  # the intake ticks all run at the deploy minute
             run_tick()
@@ -352,6 +390,7 @@ def setup_node(args, world, rank, dev):
         scored.append(n_rows)
         bd = {k: round(v, 2) for k, v in roll.timings.items() if k != "admit_ms"}
         bd["gc_ms"], bd["gc_runs"] = round(gc_pause["t"] * 1e3, 2), gc_pause["n"]
+        _exchange_bd(node, bd)
         breakdowns.append(bd)
         for a in table["anomalous_apps"]:
             flagged.add(int(a.split("/app")[1]))
@@ -637,10 +676,12 @@ def setup_arrival(args, world, rank, dev):
 
     stream = StreamingMonitor(store, cfg, prom=server, device=dev, worker_id=f"node-m{rank}", ring_len=R,
                               window=W, clock=lambda: clock["t"])
-    node = NodeBrain(stream, None, store, dev, publish=False, extra=(roll,))
+    ew = node_world(world, rank, dev)
+    node = NodeBrain(stream, ew, store, dev, publish=False, extra=(roll,))
     node.owns = lambda d: True  # the rank-local store holds exactly this rank's share
     for mon in node.monitors:
         mon.owns = None
+    _start_node(node, ew)
     loop = asyncio.new_event_loop()
     flagged: set = set()
     scored: List[int] = []
@@ -693,6 +734,7 @@ def setup_arrival(args, world, rank, dev):
         bd["tick_net_ms"] = round(bd["tick_total_ms"] - st_ms - sw_ms, 3)
         bd["live_rows"] = roll.n_live
         bd["gc_ms"], bd["gc_runs"] = round(gc_pause["t"] * 1e3, 2), gc_pause["n"]
+        _exchange_bd(node, bd)
         breakdowns.append(bd)
         for a in table["anomalous_apps"]:
             flagged.add(a)
@@ -863,10 +905,12 @@ def setup_node_lstm(args, world, rank, dev):
     stream = StreamingMonitor(store, cfg, prom=server, device=dev, worker_id=f"node-m{rank}", ring_len=R,
                               window=10, clock=lambda: clock["t"])
     stream.exclude = lstm.is_mine
-    node = NodeBrain(stream, None, store, dev, publish=False, extra=(lstm,))
+    ew = node_world(world, rank, dev)
+    node = NodeBrain(stream, ew, store, dev, publish=False, extra=(lstm,))
     node.owns = lambda d: True
     for mon in node.monitors:
         mon.owns = None
+    _start_node(node, ew)
     loop = asyncio.new_event_loop()
     setup_s = time.perf_counter() - t_setup
     breakdowns: List[Dict[str, float]] = []
@@ -883,6 +927,7 @@ def setup_node_lstm(args, world, rank, dev):
         bd.update({kk: round(v, 3) for kk, v in node.timings.items()})
         bd["tick_total_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
         bd["entities"] = len(lstm.jobs)
+        _exchange_bd(node, bd)
         breakdowns.append(bd)
         scored.append(n_live)
 

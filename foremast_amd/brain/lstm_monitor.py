@@ -43,6 +43,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from ..parallel.roster import ChangeLog
 from ..api import rest as r
 from ..parallel import comm
 from ..store.jobstore import JobStore
@@ -126,6 +127,7 @@ class LstmMonitor:
         self.padded = torch.zeros((self.shard.n, self.F), dtype=torch.bool, device=self.device)
         self.apps: Dict[Tuple[str, str], int] = {}
         self._app_names: List[Optional[Tuple[str, str]]] = [None]  # app 0: free rows (never reported)
+        self.roster_log = ChangeLog()                               # (index, name) changes, drained by the node
         self.roster_version = 0
         self.t_cur = 0.0
         self.ticks = 0
@@ -316,6 +318,7 @@ class LstmMonitor:
         if i is None:
             i = self.apps[app] = len(self._app_names)
             self._app_names.append(app)
+            self.roster_log.note(i, app)
             self.roster_version += 1
             if self.shard.app_stats.shape[0] < len(self._app_names):
                 cap = self.shard.app_stats.shape[0]
@@ -559,5 +562,10 @@ class LstmMonitor:
         return self._digest
 
     def app_table(self):
-        names = list(self._app_names)
-        return names, self.shard.app_stats[:len(names)]
+        return list(self._app_names), self.app_counts()
+
+    def roster_names(self):
+        return self._app_names
+
+    def app_counts(self) -> torch.Tensor:
+        return self.shard.app_stats[:len(self._app_names)]

@@ -45,6 +45,7 @@ import torch
 import torch.distributed as dist
 
 from ..parallel.cluster import ClusterHealth
+from ..parallel.roster import NodeRoster
 from ..parallel import comm
 from ..parallel.elastic import ElasticWorld
 from .streaming import StreamingMonitor, app_of
@@ -77,6 +78,8 @@ class NodeBrain:
         self.store = store
         self.device = torch.device(device)
         self.health = ClusterHealth(self.device)
+        self.roster = NodeRoster(len(self.monitors), self.device)
+        self._mver: Dict[int, int] = {}
         self.publish = publish
         self.dead: Set[str] = set()
         self.table: Dict = {}
@@ -157,25 +160,29 @@ class NodeBrain:
                 m.after_reform()
 
     def app_table(self):
-        """(app roster, ``[A, 2]`` device counters, roster version, live series)
-        of every monitor of this rank, merged per app."""
-        tables = [m.app_table() for m in self.monitors]
-        used = [i for i, (ns, _) in enumerate(tables) if any(ns)]
-        if len(used) <= 1:  # one engine holds every app of this rank: no merge
-            names, counts = tables[used[0]] if used else tables[0]
-            return (names, counts, sum(m.roster_version for m in self.monitors) + 1_000_000 * (used[0] if used else 0),
-                    sum(m.n_live for m in self.monitors))
-        names = sorted({n for ns, _ in tables for n in ns if n})
-        idx = {n: i for i, n in enumerate(names)}
-        counts = torch.zeros((len(names), 2), dtype=torch.int32, device=self.device)
-        for ns, c in tables:
-            keep = [i for i, n in enumerate(ns) if n]
-            if keep:
-                at = torch.tensor([idx[ns[i]] for i in keep], dtype=torch.long, device=self.device)
-                sel = torch.tensor(keep, dtype=torch.long, device=self.device)
-                counts.index_add_(0, at, c.index_select(0, sel).to(self.device))
-        return (names, counts, sum(m.roster_version for m in self.monitors),
-                sum(m.n_live for m in self.monitors))
+        """(node app roster, ``[A, 2]`` device counters, roster version, live series)
+        of every monitor of this rank, merged per app.  The merged roster is kept
+        from the monitors' change logs (:class:`~foremast_amd.parallel.roster.NodeRoster`):
+        O(apps that changed) per tick, one ``index_add_`` per monitor on the device."""
+        engines, tables = [], []
+        for k, m in enumerate(self.monitors):
+            log = getattr(m, "roster_log", None)
+            if log is not None:
+                reset, items = log.drain()
+            else:  # a monitor without a change log: re-read its table when its version moves
+                v = getattr(m, "roster_version", 0)
+                reset, items = v != self._mver.get(k), []
+                self._mver[k] = v
+            if hasattr(m, "app_counts"):
+                names = m.roster_names() if reset else ()
+                tables.append(m.app_counts())
+            else:
+                names, c = m.app_table()
+                tables.append(c)
+            engines.append((reset, items, names))
+        self.roster.update(engines)
+        counts = self.roster.counts(tables)
+        return self.roster.names, counts, self.roster.version, sum(m.n_live for m in self.monitors)
 
     def _exchange(self) -> Dict:
         names, counts, version, n_live = self.app_table()
@@ -183,7 +190,7 @@ class NodeBrain:
         for m in self.monitors:
             if hasattr(m, "model_digest"):
                 info["lstm_model"] = m.model_digest()
-        return self.health.exchange(names, counts, version, n_live, info)
+        return self.health.exchange(names, counts, version, n_live, info, changes=self.roster.log.drain())
 
     def _freeze_admitted(self) -> None:
         """Admission builds long-lived per-job state (plans, slot maps, documents):
@@ -271,14 +278,28 @@ class NodeBrain:
                 log.warning("publishing the node health table failed: %s", e)
         return table
 
-    async def run_forever(self, stop: asyncio.Event, period: float) -> None:
-        if self.world is not None and not dist.is_initialized():
+    def start(self) -> None:
+        """Join the node: form the elastic world's process group (a no-op if it is
+        formed), point the health exchange and the affine router at the
+        generation's key-value store, start heartbeating.  Every rank of a
+        multi-GPU node runs this once before its first tick (``run_forever``, and
+        the node benches under ``torch.distributed.run``)."""
+        if self.world is None:
+            return
+        if not dist.is_initialized():
             self.world.form()
-            self.health.reset(kv=self.world.pstore)
-            for m in self.monitors:
-                if getattr(m, "router", None) is not None:
-                    m.router.reset(kv=dist.PrefixStore("affine", self.world.pstore))
-            self.world.start_heartbeat()
+        self.health.reset(kv=self.world.pstore)
+        for m in self.monitors:
+            if getattr(m, "router", None) is not None:
+                m.router.reset(kv=dist.PrefixStore("affine", self.world.pstore))
+        self.world.start_heartbeat()
+
+    def stop(self) -> None:
+        if self.world is not None:
+            self.world.stop_heartbeat()
+
+    async def run_forever(self, stop: asyncio.Event, period: float) -> None:
+        self.start()
         try:
             while not stop.is_set():
                 t0 = time.monotonic()
@@ -288,14 +309,15 @@ class NodeBrain:
                 except asyncio.TimeoutError:
                     pass
         finally:
-            if self.world is not None:
-                self.world.stop_heartbeat()
+            self.stop()
 
 
-def elastic_world_from_env(device: torch.device) -> Optional[ElasticWorld]:
+def elastic_world_from_env(device: torch.device, force: bool = False) -> Optional[ElasticWorld]:
     """The rank's ElasticWorld: under :func:`launch_node` (``FOREMAST_NODE_STORE``)
     or under torchrun (``WORLD_SIZE`` > 1: the agent's store at MASTER_ADDR:PORT);
-    None for a single brain process."""
+    None for a single brain process — unless ``force`` (``FOREMAST_FORCE_COLLECTIVES=1``
+    runs: a 1-member world on a store this process hosts, so one GPU exercises
+    the deployed RCCL exchange, its deadlines and its re-formation)."""
     hb = float(os.environ.get("FOREMAST_HEARTBEAT_S", "5"))
     backend = os.environ.get("FOREMAST_DIST_BACKEND", "nccl" if device.type == "cuda" else "gloo")
     # RCCL aborts a wedged communicator at once (ncclCommAbort); gloo's teardown waits for
@@ -308,6 +330,11 @@ def elastic_world_from_env(device: torch.device) -> Optional[ElasticWorld]:
     elif int(os.environ.get("WORLD_SIZE", "1")) > 1:
         host, port = os.environ.get("MASTER_ADDR", "127.0.0.1"), os.environ["MASTER_PORT"]
         n, me = int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"])
+    elif force:
+        kv = dist.TCPStore("127.0.0.1", 0, is_master=True, wait_for_workers=False,
+                           timeout=datetime.timedelta(seconds=60))
+        return ElasticWorld(kv, "m0", ["m0"], backend=backend, heartbeat_timeout_s=hb, collective_timeout_s=coll,
+                            device_id=device if backend == "nccl" else None)
     else:
         return None
     kv = dist.TCPStore(host, int(port), is_master=False, timeout=datetime.timedelta(seconds=60))

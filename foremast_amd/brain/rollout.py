@@ -76,6 +76,7 @@ from ..models import detect as det_ref
 from ..models import moving_average as ma_ref
 from ..models import pairwise as pw_ref
 from ..models import smoothing as sm_ref
+from ..parallel.roster import ChangeLog
 from ..store.jobstore import JobStore
 from ..utils.config import BrainConfig
 from ..utils.metrics import BrainMetrics
@@ -269,6 +270,7 @@ class RolloutMonitor:
         self._apps_dirty = False
         self._app_refs: Dict[Tuple[str, str], int] = {}
         self._app_names: List[Optional[Tuple[str, str]]] = []   # app index -> name (None: free index)
+        self.roster_log = ChangeLog()                            # (index, name) changes, drained by the node
         self._app_free: List[int] = []
         self._app_new: List[Tuple[Tuple[str, str], List[int]]] = []
         self._app_gone: List[Tuple[str, str]] = []
@@ -541,11 +543,13 @@ class RolloutMonitor:
         were accumulated under."""
         if not self._apps_dirty:
             return
+        log = self.roster_log
         for a in self._app_gone:
             if self._app_refs.get(a, 0) <= 0 and a in self.apps:
                 i = self.apps.pop(a)
                 self._app_names[i] = None
                 self._app_free.append(i)
+                log.note(i, None)
         self._app_gone = []
         ids = np.empty(len(self._app_new), dtype=np.int32)
         apps, names, free = self.apps, self._app_names, self._app_free
@@ -558,6 +562,7 @@ class RolloutMonitor:
                 else:
                     names[i] = a
                 apps[a] = i
+                log.note(i, a)
             ids[k] = i
         if len(self._app_new):  # one device scatter for every admitted row
             lens = np.fromiter((len(rows) for _a, rows in self._app_new), dtype=np.int64, count=len(self._app_new))
@@ -1538,10 +1543,16 @@ class RolloutMonitor:
     def app_table(self) -> Tuple[List[Optional[Tuple[str, str]]], torch.Tensor]:
         """(app index -> name, None for a free index; ``[A, 2]`` device counters
         of the last tick: anomalous series, scored series)."""
-        names = list(self._app_names)
+        return list(self._app_names), self.app_counts()
+
+    def roster_names(self) -> List[Optional[Tuple[str, str]]]:
+        return self._app_names
+
+    def app_counts(self) -> torch.Tensor:
+        n = len(self._app_names)
         if not self.cap:
-            return names, torch.zeros((len(names), 2), dtype=torch.int32, device=self.device)
-        return names, self.app_stats[:len(names)]
+            return torch.zeros((n, 2), dtype=torch.int32, device=self.device)
+        return self.app_stats[:n]
 
     def _band_rows(self):
         up, lo, verdict = self._bands

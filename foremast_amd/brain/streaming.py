@@ -42,6 +42,7 @@ from urllib.parse import quote
 import numpy as np
 import torch
 
+from ..parallel.roster import ChangeLog
 from ..api import rest as r
 from ..ingest import native
 from ..promql.client import PromClient
@@ -142,6 +143,7 @@ class StreamingMonitor:
         self.pending: Set[Key] = set()               # live keys whose history is not loaded yet
         self.apps: Dict[Tuple[str, str], int] = {}   # (namespace, app) -> app index (node health table)
         self.roster_version = 0
+        self.roster_log = ChangeLog()
         self.shard: Optional[StreamingShard] = None
         self.t_last: float = 0.0
         self.ticks = 0
@@ -268,6 +270,7 @@ class StreamingMonitor:
         if list(self.apps) != names:
             self.apps = {a: i for i, a in enumerate(names)}
             self.roster_version += 1
+            self.roster_log.mark_reset()  # renumbered: consumers re-read the table
         sh = self.shard
         if sh.app_stats.shape[0] < max(1, len(self.apps)):
             cap = sh.app_stats.shape[0]
@@ -471,10 +474,15 @@ class StreamingMonitor:
     def app_table(self) -> Tuple[List[Tuple[str, str]], torch.Tensor]:
         """(app roster, ``[A, 2]`` int32 device counters of the last tick:
         anomalous series, scored series)."""
-        names = list(self.apps)
+        return list(self.apps), self.app_counts()
+
+    def roster_names(self) -> List[Tuple[str, str]]:
+        return list(self.apps)
+
+    def app_counts(self) -> torch.Tensor:
         if self.shard is None:
-            return names, torch.zeros((len(names), 2), dtype=torch.int32, device=self.device)
-        return names, self.shard.app_stats[:len(names)]
+            return torch.zeros((len(self.apps), 2), dtype=torch.int32, device=self.device)
+        return self.shard.app_stats[:len(self.apps)]
 
     # ------------------------------------------------------------------ checkpoint / resume
     def save_snapshot(self, path: str) -> bool:

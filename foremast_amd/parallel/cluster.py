@@ -5,24 +5,31 @@ Every brain rank (one process per GPU) owns a disjoint set of apps
 per-app counters need no reduction: rank r contributes the fixed-size int32
 record
 
-    [roster_version, n_apps, cap_request, n_series | anomalous_0, scored_0, ...]
+    [roster_seq, n_apps, cap_request, n_series, full_seq | anomalous_0, scored_0, ...]
 
 and ONE ``all_gather_into_tensor`` (RCCL over xGMI on the GPU, gloo on CPU)
 gives every rank the whole node's table.  The records carry counters only;
-the app NAMES behind each rank's rows travel in a control-plane
-``all_gather_object`` that runs only when some rank's roster version changed
-(jobs started or finished) — every rank sees the same gathered headers, so
-all take that branch together and the collective sequence stays matched.
-When a rank needs more rows than the record holds it asks for a larger
-``cap`` in its header; every rank adopts the maximum on the next tick.
+the app NAMES behind each rank's rows travel through the node's key-value
+store as DELTAS: when a rank's roster changes it publishes the ``(index,
+name)`` changes since its last publication under ``roster/<rank>/d/<seq>``
+(a full roster ``roster/<rank>/f/<seq>`` the first time, after a reset, when
+the changes exceed half the roster, or every ``FULL_EVERY`` publications),
+then announces ``seq`` and the seq of its last full roster in its header.  A
+peer one publication behind reads one delta; one that lost track reads the
+full roster and the deltas after it.  Under a steady deployment stream (the
+roster changes every tick) the host work and the bytes per tick are
+O(apps that changed), not O(apps).  Keys older than the previous full roster
+are deleted.  When a rank needs more rows than the record holds it asks for a
+larger ``cap`` in its header; every rank adopts the maximum on the next tick.
 
 Failure handling: the all-gather is issued ``async_op=True`` and waited for
 on the host with a deadline (:func:`~foremast_amd.parallel.comm.wait_bounded`),
 so a dead or SIGSTOPped peer raises :class:`~foremast_amd.parallel.comm.CollectiveTimeout`
 instead of wedging the rank in a D2H copy until the RCCL watchdog kills it;
-with a key-value store (``kv``: the generation's prefix store of the elastic
-world) the app rosters travel through the store, read with the same deadline,
-instead of an object collective.
+roster reads wait on the store with the same deadline.  ``kv`` is the
+generation's prefix store of the elastic world (``parallel/elastic.py``), or
+the default process group's store; only without any store do full rosters
+travel as objects.
 
 At 100k series over 8 ranks (~2.5k apps per rank) the record is ~20 KB, so the
 exchange is latency bound (one collective, tens of microseconds on xGMI).
@@ -40,7 +47,8 @@ import torch.distributed as dist
 
 from . import comm
 
-HDR = 4
+HDR = 5          # [roster seq, n_apps, cap_req, n_series, seq of the last full roster]
+FULL_EVERY = 256  # a full roster at least every this many publications (bounds a reader's catch-up)
 
 
 def _world(group=None) -> Tuple[int, int]:
@@ -49,72 +57,159 @@ def _world(group=None) -> Tuple[int, int]:
     return 1, 0
 
 
+def _diff(old: Sequence, new: Sequence) -> List[Tuple[int, Any]]:
+    """Index changes turning roster ``old`` into ``new`` (the fallback when the
+    caller keeps no change log)."""
+    out = [(i, n) for i, (o, n) in enumerate(zip(old, new)) if o != n]
+    out += [(i, new[i]) for i in range(len(old), len(new))]
+    out += [(i, None) for i in range(len(new), len(old)) if old[i] is not None]
+    return out
+
+
+class _Peer:
+    __slots__ = ("seq", "names", "info")
+
+    def __init__(self) -> None:
+        self.seq = -1
+        self.names: List[Any] = []
+        self.info: Dict[str, Any] = {}
+
+
 class ClusterHealth:
     def __init__(self, device, cap: int = 256, group=None, kv=None, timeout_s: Optional[float] = None) -> None:
         self.device = torch.device(device)
         self.cap = max(1, int(cap))
         self.group = group
-        self.kv = kv                       # roster store (None: all_gather_object)
+        self.kv = kv                       # roster store (None: the default group's store)
         self.timeout_s = comm.exchange_timeout_s() if timeout_s is None else float(timeout_s)
-        self._versions: Optional[List[int]] = None
-        self._rosters: List[Dict[str, Any]] = []
-        self._published: Optional[int] = None
-        self._mine: Optional[Dict[str, Any]] = None   # roster record of _mine_version
-        self._mine_version: Optional[int] = None
-        self.roster_exchanges = 0
+        self.roster_exchanges = 0          # ticks on which some peer's roster had to be read
+        self.roster_full_reads = 0
         self.last_ms = 0.0
+        self.last_roster_bytes = 0         # roster bytes written + read by the last exchange
+        self._reset_state()
+
+    def _reset_state(self) -> None:
+        self._peers: Dict[int, _Peer] = {}
+        self._seq = 0                      # roster publications of this rank
+        self._fseq = -1                    # seq of its last full roster (-1: none yet)
+        self._delta_n = 0                  # delta entries published since that full roster
+        self._mine_version: Optional[int] = None
+        self._pub_names: Optional[List[Any]] = None   # roster as last published (diff fallback only)
+        self._keys: List[Tuple[int, str]] = []        # (seq, key) this rank published, oldest first
+        self._info: Dict[str, Any] = {}
 
     def reset(self, kv=None) -> None:
         """Forget the peers' rosters (after the process group was re-formed);
-        ``kv``: the new generation's roster store."""
-        self._versions = None
-        self._rosters = []
-        self._published = None
+        ``kv``: the new generation's roster store.  The next exchange publishes a
+        full roster."""
+        self._reset_state()
         if kv is not None:
             self.kv = kv
 
-    def _read_roster(self, r: int, version: int) -> Dict[str, Any]:
-        key = f"roster/{r}/{version}"
+    def _store(self):
+        if self.kv is None:
+            try:
+                self.kv = dist.PrefixStore("health", dist.distributed_c10d._get_default_store())
+            except Exception:  # noqa: BLE001 - no default store: rosters travel as objects
+                return None
+        return self.kv
+
+    def _read(self, key: str, what: str) -> Dict[str, Any]:
         try:
             self.kv.wait([key], datetime.timedelta(seconds=self.timeout_s))
-            return json.loads(self.kv.get(key))
+            raw = self.kv.get(key)
         except Exception as e:  # noqa: BLE001 - store timeout: the peer is gone
-            raise comm.CollectiveTimeout(f"roster of rank {r} (version {version}) not published: {e}") from e
+            raise comm.CollectiveTimeout(f"{what} not published: {e}") from e
+        self.last_roster_bytes += len(raw)
+        return json.loads(raw)
+
+    def _publish(self, kv, rank: int, names: Sequence, version: int, info: Dict[str, Any],
+                 changes: Optional[Tuple[bool, List[Tuple[int, Any]]]]) -> None:
+        """Roster publication of this tick (only when the roster changed): the
+        changes since the last publication, or a full roster when a reader could
+        not catch up cheaply (first publication, a reset of the caller's table,
+        more changes than half the roster, or every FULL_EVERY publications)."""
+        if changes is None:
+            items = _diff(self._pub_names or [], names)
+            reset = self._pub_names is None
+            self._pub_names = list(names)
+        else:
+            reset, items = changes
+        self._seq += 1
+        seq = self._seq
+        full = (reset or self._fseq < 0 or seq - self._fseq >= FULL_EVERY
+                or self._delta_n + len(items) > max(64, len(names) // 2))
+        if full:
+            key, rec = f"roster/{rank}/f/{seq}", {"names": list(names), "info": info}
+        else:
+            key, rec = f"roster/{rank}/d/{seq}", {"c": items, "info": info}
+        raw = json.dumps(rec)
+        kv.set(key, raw)   # published before the gather that announces it: a peer that sees it can read it
+        self.last_roster_bytes += len(raw)
+        self._keys.append((seq, key))
+        if full:
+            # readers still finishing the last tick need keys from the previous full roster on
+            old_f, self._fseq, self._delta_n = self._fseq, seq, 0
+            while self._keys and self._keys[0][0] < old_f:
+                try:
+                    kv.delete_key(self._keys.pop(0)[1])
+                except Exception:  # noqa: BLE001 - best-effort cleanup
+                    pass
+        else:
+            self._delta_n += len(items)
+
+    def _catch_up(self, r: int, seq: int, fseq: int) -> _Peer:
+        """Bring peer ``r``'s roster to publication ``seq``: its deltas, or its last
+        full roster plus the deltas after it."""
+        p = self._peers.setdefault(r, _Peer())
+        if p.seq == seq:
+            return p
+        if p.seq < fseq:
+            rec = self._read(f"roster/{r}/f/{fseq}", f"roster of rank {r} (full {fseq})")
+            p.names, p.info, p.seq = [tuple(n) if n else None for n in rec["names"]], rec.get("info", {}), fseq
+            self.roster_full_reads += 1
+        names = p.names
+        for q in range(p.seq + 1, seq + 1):
+            rec = self._read(f"roster/{r}/d/{q}", f"roster delta {q} of rank {r}")
+            for i, n in rec["c"]:
+                if i >= len(names):
+                    names.extend([None] * (i + 1 - len(names)))
+                names[i] = tuple(n) if n else None
+            p.info = rec.get("info", p.info)
+        p.seq = seq
+        return p
 
     def exchange(self, names: Sequence[Tuple[str, str]], counts: torch.Tensor, roster_version: int,
-                 n_series: int, info: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
+                 n_series: int, info: Optional[Dict[str, Any]] = None,
+                 changes: Optional[Tuple[bool, List[Tuple[int, Any]]]] = None) -> Dict[str, Any]:
         """One tick: gather every rank's per-app counters; returns the node table
-        ``{"ranks", "members", "apps": {"ns/app": {anomalous, scored, rank}}, ...}``."""
+        ``{"ranks", "members", "apps": {"ns/app": {anomalous, scored, rank}}, ...}``.
+        ``names``: this rank's roster (index -> (namespace, app), None for a free
+        index); ``changes``: its ``(reset, [(index, name)])`` since the last call
+        (:class:`~foremast_amd.parallel.roster.ChangeLog`; None: diffed here)."""
         world, rank = _world(self.group)
         t0 = time.perf_counter()
+        self.last_roster_bytes = 0
+        active = comm.active(self.group)
         cap_req = 1
         while cap_req < len(names):
             cap_req *= 2
+        info = dict(info or {})
+        kv = self._store() if active else None
+        if roster_version != self._mine_version or info != self._info:
+            if active and kv is not None:
+                self._publish(kv, rank, names, roster_version, info, changes)
+            elif changes is None:
+                self._pub_names = None
+            self._mine_version, self._info = roster_version, info
         chunk = HDR + 2 * self.cap
         send = torch.zeros(chunk, dtype=torch.int32, device=self.device)
         k = min(len(names), self.cap)
-        hdr = torch.tensor([roster_version, len(names), cap_req, n_series], dtype=torch.int32)
+        hdr = torch.tensor([self._seq, len(names), cap_req, n_series, self._fseq], dtype=torch.int32)
         send[:HDR].copy_(hdr.to(self.device, non_blocking=True))
         if k:
             send[HDR:HDR + 2 * k].copy_(counts[:k].reshape(-1))
-        # this rank's roster record, built only when the roster changed (O(apps) per change,
-        # not per tick: a node holds tens of thousands of apps)
-        if self._mine is None or self._mine_version != roster_version:
-            # (namespace, app) tuples as given (JSON writes them as lists; a C-level copy,
-            # not a Python loop: the roster of a node with arrivals changes every tick)
-            self._mine = {"names": list(names), "version": roster_version}
-            self._mine_version = roster_version
-        mine = dict(info or {}, **self._mine)
-        if self.kv is not None and comm.active(self.group) and self._published != roster_version:
-            # publish before the gather that announces the version: a peer that sees it can read it
-            self.kv.set(f"roster/{rank}/{roster_version}", json.dumps(mine))
-            if self._published is not None:
-                try:
-                    self.kv.delete_key(f"roster/{rank}/{self._published}")
-                except Exception:  # noqa: BLE001 - best effort cleanup
-                    pass
-            self._published = roster_version
-        if comm.active(self.group):
+        if active:
             recv = torch.empty(world * chunk, dtype=torch.int32, device=self.device)
             work = dist.all_gather_into_tensor(recv, send, group=self.group, async_op=True)
             comm.fault_point("exchange")
@@ -122,30 +217,39 @@ class ClusterHealth:
         else:
             recv = send
         host = recv.cpu().view(world, chunk)
-        versions = host[:, 0].tolist()
-        if versions != self._versions or len(self._rosters) != world:
-            if not comm.active(self.group):
-                rosters: List[Any] = [mine]
-            elif self.kv is not None:
-                rosters = [mine if r == rank else self._read_roster(r, int(versions[r])) for r in range(world)]
-            else:
-                rosters = [None] * world
-                dist.all_gather_object(rosters, mine, group=self.group)
-            self._rosters, self._versions = rosters, versions
+        rosters: List[Tuple[Sequence, Dict[str, Any]]] = []
+        read = False
+        if active and kv is None:  # no store at all: full rosters as objects, every tick
+            objs: List[Any] = [None] * world
+            dist.all_gather_object(objs, {"names": list(names), "info": info}, group=self.group)
+            rosters = [(o["names"], o["info"]) for o in objs]
+            read = True
+        else:
+            seqs, fseqs = host[:, 0].tolist(), host[:, 4].tolist()
+            for r in range(world):
+                if r == rank:
+                    rosters.append((names, info))
+                    continue
+                p = self._peers.get(r)
+                if p is None or p.seq != seqs[r]:
+                    p = self._catch_up(r, int(seqs[r]), int(fseqs[r]))
+                    read = True
+                rosters.append((p.names, p.info))
+        if read:
             self.roster_exchanges += 1
         self.cap = max(self.cap, int(host[:, 2].max()))  # every rank adopts the same cap next tick
         self.last_ms = (time.perf_counter() - t0) * 1e3
         members, anomalous = [], []
         for r in range(world):
-            ro = self._rosters[r]
-            n = min(int(host[r, 1]), (chunk - HDR) // 2, len(ro["names"]))
+            ro, inf = rosters[r]
+            n = min(int(host[r, 1]), (chunk - HDR) // 2, len(ro))
             bad = torch.nonzero(host[r, HDR:HDR + 2 * n:2] > 0).flatten().tolist()
-            anomalous += [f"{ro['names'][i][0]}/{ro['names'][i][1]}" for i in bad if ro["names"][i]]
-            members.append({k: v for k, v in ro.items() if k not in ("names", "version")}
-                           | {"rank": r, "apps": int(host[r, 1]), "series": int(host[r, 3])})
+            anomalous += [f"{ro[i][0]}/{ro[i][1]}" for i in bad if ro[i]]
+            members.append(dict(inf) | {"rank": r, "apps": int(host[r, 1]), "series": int(host[r, 3])})
         return NodeTable({"ranks": world, "members": members, "anomalous_apps": sorted(anomalous),
-                          "collective_ms": round(self.last_ms, 3), "updated": time.time()},
-                         host, self._rosters, chunk)
+                          "collective_ms": round(self.last_ms, 3), "roster_bytes": self.last_roster_bytes,
+                          "updated": time.time()},
+                         host, [ro for ro, _ in rosters], chunk)
 
 
 class NodeTable(dict):
@@ -155,7 +259,7 @@ class NodeTable(dict):
     of milliseconds of Python, and the tick itself needs just the anomalous
     apps (computed vectorised)."""
 
-    def __init__(self, base: Dict[str, Any], host: torch.Tensor, rosters: List[Dict[str, Any]], chunk: int) -> None:
+    def __init__(self, base: Dict[str, Any], host: torch.Tensor, rosters: List[Sequence], chunk: int) -> None:
         super().__init__(base)
         self._host, self._rosters, self._chunk = host, rosters, chunk
 
@@ -164,9 +268,9 @@ class NodeTable(dict):
             raise KeyError(key)
         apps: Dict[str, Dict[str, int]] = {}
         for r, ro in enumerate(self._rosters):
-            n = min(int(self._host[r, 1]), (self._chunk - HDR) // 2, len(ro["names"]))
+            n = min(int(self._host[r, 1]), (self._chunk - HDR) // 2, len(ro))
             cnt = self._host[r, HDR:HDR + 2 * n].view(n, 2).tolist()
-            for name, (an, sc) in zip(ro["names"][:n], cnt):
+            for name, (an, sc) in zip(ro[:n], cnt):
                 if name:  # None: a free index of the rank's stable app table
                     apps[f"{name[0]}/{name[1]}"] = {"anomalous": an, "scored": sc, "rank": r}
         self["apps"] = apps

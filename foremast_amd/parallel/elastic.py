@@ -96,9 +96,24 @@ class ElasticWorld:
         except Exception:  # noqa: BLE001 - store hiccup counts as stale
             return 0.0
 
+    def _beats(self, members: Sequence[str]) -> List[float]:
+        """Last beat of each member in two store round trips (an existence check of
+        every key, then one multi-get) instead of two per member: the check runs
+        before every tick."""
+        keys = [f"hb/{m}" for m in members]
+        try:
+            if keys and hasattr(self.store, "multi_get") and self.store.check(keys):
+                return [float(v.decode() if isinstance(v, (bytes, bytearray)) else bytes(v).decode())
+                        for v in self.store.multi_get(keys)]
+        except Exception:  # noqa: BLE001 - fall back to one member at a time
+            pass
+        return [self.last_beat(m) for m in members]
+
     def live(self, now: Optional[float] = None) -> List[str]:
         now = time.time() if now is None else now
-        return [m for m in self.members if m == self.id or now - self.last_beat(m) <= self.hb_timeout]
+        others = [m for m in self.members if m != self.id]
+        beats = dict(zip(others, self._beats(others)))
+        return [m for m in self.members if m == self.id or now - beats[m] <= self.hb_timeout]
 
     # ------------------------------------------------------------------ group management
     def _agree(self, proposal: List[str]) -> List[str]:
@@ -130,7 +145,8 @@ class ElasticWorld:
                                 timeout=self.coll_timeout, **kw)
 
     def changed(self) -> bool:
-        self.beat()
+        if getattr(self, "_hb_stop", None) is None or self._hb_stop.is_set():
+            self.beat()  # no heartbeat thread: this call is the beat
         return len(self.live()) != len(self.members)
 
     def reform(self, settle_s: float = 0.0) -> None:

@@ -60,7 +60,7 @@ def test_cluster_health_single_rank_table():
     t = h.exchange(names, counts, 1, 13, {"member": "m0"})
     assert t["apps"]["ns/c"] == {"anomalous": 0, "scored": 3, "rank": 0}
     assert t["anomalous_apps"] == ["ns/a"] and t["members"][0]["series"] == 13
-    assert h.roster_exchanges == 1  # same roster version: names are not re-sent
+    assert h.roster_exchanges == 0 and h.last_roster_bytes == 0  # one rank: no peer roster to read
 
 
 def _serve(app, port):
