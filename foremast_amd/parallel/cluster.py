@@ -42,6 +42,7 @@ import json
 import time
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -86,6 +87,7 @@ class ClusterHealth:
         self.roster_full_reads = 0
         self.last_ms = 0.0
         self.last_roster_bytes = 0         # roster bytes written + read by the last exchange
+        self.last_phases_ms: Dict[str, float] = {}
         self._reset_state()
 
     def _reset_state(self) -> None:
@@ -113,15 +115,6 @@ class ClusterHealth:
             except Exception:  # noqa: BLE001 - no default store: rosters travel as objects
                 return None
         return self.kv
-
-    def _read(self, key: str, what: str) -> Dict[str, Any]:
-        try:
-            self.kv.wait([key], datetime.timedelta(seconds=self.timeout_s))
-            raw = self.kv.get(key)
-        except Exception as e:  # noqa: BLE001 - store timeout: the peer is gone
-            raise comm.CollectiveTimeout(f"{what} not published: {e}") from e
-        self.last_roster_bytes += len(raw)
-        return json.loads(raw)
 
     def _publish(self, kv, rank: int, names: Sequence, version: int, info: Dict[str, Any],
                  changes: Optional[Tuple[bool, List[Tuple[int, Any]]]]) -> None:
@@ -158,26 +151,45 @@ class ClusterHealth:
         else:
             self._delta_n += len(items)
 
-    def _catch_up(self, r: int, seq: int, fseq: int) -> _Peer:
-        """Bring peer ``r``'s roster to publication ``seq``: its deltas, or its last
-        full roster plus the deltas after it."""
-        p = self._peers.setdefault(r, _Peer())
-        if p.seq == seq:
-            return p
-        if p.seq < fseq:
-            rec = self._read(f"roster/{r}/f/{fseq}", f"roster of rank {r} (full {fseq})")
-            p.names, p.info, p.seq = [tuple(n) if n else None for n in rec["names"]], rec.get("info", {}), fseq
-            self.roster_full_reads += 1
-        names = p.names
-        for q in range(p.seq + 1, seq + 1):
-            rec = self._read(f"roster/{r}/d/{q}", f"roster delta {q} of rank {r}")
-            for i, n in rec["c"]:
-                if i >= len(names):
-                    names.extend([None] * (i + 1 - len(names)))
-                names[i] = tuple(n) if n else None
-            p.info = rec.get("info", p.info)
-        p.seq = seq
-        return p
+    def _read_many(self, keys: List[str]) -> List[Dict[str, Any]]:
+        """Records under ``keys`` in two store round trips (one wait for all, one
+        multi-get), however many peers they come from."""
+        try:
+            self.kv.wait(keys, datetime.timedelta(seconds=self.timeout_s))
+            raws = self.kv.multi_get(keys) if hasattr(self.kv, "multi_get") else [self.kv.get(k) for k in keys]
+        except Exception as e:  # noqa: BLE001 - store timeout: a peer is gone
+            raise comm.CollectiveTimeout(f"peer rosters {keys[:4]}... not published: {e}") from e
+        self.last_roster_bytes += sum(len(x) for x in raws)
+        return [json.loads(x) for x in raws]
+
+    def _catch_up(self, want: Dict[int, Tuple[int, int]]) -> None:
+        """Bring each peer ``r`` of ``want`` (r -> (seq, full seq)) to publication
+        ``seq``: its deltas, or its last full roster plus the deltas after it — all
+        peers' records in one batched read."""
+        plan: List[Tuple[int, int, str]] = []   # (peer, seq, kind) in apply order
+        for r, (seq, fseq) in want.items():
+            p = self._peers.setdefault(r, _Peer())
+            q0 = p.seq
+            if q0 < fseq:
+                plan.append((r, fseq, "f"))
+                q0 = fseq
+            plan += [(r, q, "d") for q in range(q0 + 1, seq + 1)]
+        recs = self._read_many([f"roster/{r}/{k}/{q}" for r, q, k in plan]) if plan else []
+        for (r, q, kind), rec in zip(plan, recs):
+            p = self._peers[r]
+            if kind == "f":
+                p.names, p.info = [tuple(n) if n else None for n in rec["names"]], rec.get("info", {})
+                self.roster_full_reads += 1
+            else:
+                names = p.names
+                for i, n in rec["c"]:
+                    if i >= len(names):
+                        names.extend([None] * (i + 1 - len(names)))
+                    names[i] = tuple(n) if n else None
+                p.info = rec.get("info", p.info)
+            p.seq = q
+        for r, (seq, _f) in want.items():
+            self._peers[r].seq = seq
 
     def exchange(self, names: Sequence[Tuple[str, str]], counts: torch.Tensor, roster_version: int,
                  n_series: int, info: Optional[Dict[str, Any]] = None,
@@ -209,6 +221,7 @@ class ClusterHealth:
         send[:HDR].copy_(hdr.to(self.device, non_blocking=True))
         if k:
             send[HDR:HDR + 2 * k].copy_(counts[:k].reshape(-1))
+        t1 = time.perf_counter()
         if active:
             recv = torch.empty(world * chunk, dtype=torch.int32, device=self.device)
             work = dist.all_gather_into_tensor(recv, send, group=self.group, async_op=True)
@@ -217,6 +230,7 @@ class ClusterHealth:
         else:
             recv = send
         host = recv.cpu().view(world, chunk)
+        t2 = time.perf_counter()
         rosters: List[Tuple[Sequence, Dict[str, Any]]] = []
         read = False
         if active and kv is None:  # no store at all: full rosters as objects, every tick
@@ -226,29 +240,36 @@ class ClusterHealth:
             read = True
         else:
             seqs, fseqs = host[:, 0].tolist(), host[:, 4].tolist()
+            want = {r: (int(seqs[r]), int(fseqs[r])) for r in range(world) if r != rank
+                    and (r not in self._peers or self._peers[r].seq != seqs[r])}
+            if want:
+                self._catch_up(want)
+                read = True
             for r in range(world):
-                if r == rank:
-                    rosters.append((names, info))
-                    continue
                 p = self._peers.get(r)
-                if p is None or p.seq != seqs[r]:
-                    p = self._catch_up(r, int(seqs[r]), int(fseqs[r]))
-                    read = True
-                rosters.append((p.names, p.info))
+                rosters.append((names, info) if r == rank else (p.names, p.info))
+        t3 = time.perf_counter()
         if read:
             self.roster_exchanges += 1
         self.cap = max(self.cap, int(host[:, 2].max()))  # every rank adopts the same cap next tick
         self.last_ms = (time.perf_counter() - t0) * 1e3
-        members, anomalous = [], []
-        for r in range(world):
-            ro, inf = rosters[r]
-            n = min(int(host[r, 1]), (chunk - HDR) // 2, len(ro))
-            bad = torch.nonzero(host[r, HDR:HDR + 2 * n:2] > 0).flatten().tolist()
-            anomalous += [f"{ro[i][0]}/{ro[i][1]}" for i in bad if ro[i]]
-            members.append(dict(inf) | {"rank": r, "apps": int(host[r, 1]), "series": int(host[r, 3])})
+        # anomalous apps of every rank in one pass over the gathered counters
+        hn = host.numpy()
+        lim = np.minimum(np.minimum(hn[:, 1], (chunk - HDR) // 2), [len(ro) for ro, _ in rosters])
+        bad = hn[:, HDR::2] > 0
+        bad &= np.arange(bad.shape[1])[None, :] < lim[:, None]
+        anomalous = [f"{rosters[r][0][i][0]}/{rosters[r][0][i][1]}" for r, i in zip(*np.nonzero(bad))
+                     if rosters[r][0][i]]
+        members = [dict(rosters[r][1]) | {"rank": r, "apps": int(hn[r, 1]), "series": int(hn[r, 3])}
+                   for r in range(world)]
+        t4 = time.perf_counter()
+        # where the exchange's time went: roster publication, the counter all-gather (includes
+        # waiting for the slowest rank to reach it), peer roster reads, the table
+        self.last_phases_ms = {"publish": round((t1 - t0) * 1e3, 3), "gather": round((t2 - t1) * 1e3, 3),
+                               "rosters": round((t3 - t2) * 1e3, 3), "table": round((t4 - t3) * 1e3, 3)}
         return NodeTable({"ranks": world, "members": members, "anomalous_apps": sorted(anomalous),
                           "collective_ms": round(self.last_ms, 3), "roster_bytes": self.last_roster_bytes,
-                          "updated": time.time()},
+                          "exchange_phases_ms": self.last_phases_ms, "updated": time.time()},
                          host, [ro for ro, _ in rosters], chunk)
 
 

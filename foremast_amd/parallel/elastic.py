@@ -141,6 +141,9 @@ class ElasticWorld:
             kw["device_id"] = self.device_id
         if self.backend == "nccl":
             os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")  # abort comms, keep the process
+        # beat before the group's rendezvous: once any member is past it, every member has a
+        # fresh beat (a peer still between form() and start_heartbeat() must not look dead)
+        self.beat()
         dist.init_process_group(self.backend, store=pstore, rank=self.rank, world_size=self.world,
                                 timeout=self.coll_timeout, **kw)
 

@@ -85,3 +85,36 @@ def test_forced_collectives_gloo_one_rank_cpu():
     got = _bench(args, force=True, launcher=True, cpu=True)
     assert got["config"]["health_collectives"] == "1 fused all_gather"
     assert got["health"] == ref["health"] and got["detection"] == ref["detection"]
+
+
+def _reform(cpu: bool) -> dict:
+    env = dict(os.environ, OMP_NUM_THREADS="4", HSA_ENABLE_IPC_MODE_LEGACY="0", FOREMAST_HEARTBEAT_S="0.5")
+    for k in ("WORLD_SIZE", "RANK", "MASTER_PORT", "FOREMAST_NODE_STORE"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "tests", "helpers", "reform_rank.py")] + (["--cpu"] if cpu else [])
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=180, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stdout[-1000:] + out.stderr[-3000:]
+    lines = [x for x in out.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    return json.loads(lines[-1])
+
+
+def _check_reform(got: dict, backend: str) -> None:
+    assert got["backend"] == backend and got["backend_after"] == backend
+    assert got["injected"] == 1 and got["reforms"] == 1 and got["generation"] == 1 and got["new_group"]
+    gens = [t["generation"] for t in got["ticks"]]
+    assert gens == [0, 0, 1, 1, 1], gens          # the failed tick completed on the new communicator
+    assert all(t["apps"] == t["want_apps"] and t["collectives"] for t in got["ticks"])
+    assert got["grads_ok"] and got["allreduce_ok"] and got["flags"] == [1.0, 5.0]
+
+
+@pytest.mark.gpu
+def test_rccl_abort_and_reform_in_process():
+    """ElasticWorld on RCCL: a collective deadline inside run_tick aborts the
+    communicator, the group is re-formed (generation 1) in the same process, and
+    the node exchange and a DP gradient all-reduce run on the new communicator."""
+    _check_reform(_reform(cpu=False), "nccl")
+
+
+def test_gloo_abort_and_reform_in_process():
+    _check_reform(_reform(cpu=True), "gloo")

@@ -1,0 +1,90 @@
+"""Node health exchange under churn: N ranks equal one rank, every tick.
+
+Every tick apps start and finish (a sliding window of the app pool; finished
+apps' table indices are reused), each rank holds its apps in two engines (some
+apps in both: the merged roster's reference counts), and the node brain runs
+the deployed exchange — ElasticWorld.run_tick, one all-gather of counters,
+roster DELTAS through the generation's store (``parallel/cluster.py``).  The
+node table (every app's counters and the anomalous apps) must equal the 1-rank
+table and the analytic one on every tick, on every rank, at 2, 4 and 8 gloo
+ranks; the roster bytes per tick must follow the changes, not the roster size.
+Reference: brains scale out and aggregate health across clusters
+(``/root/reference/docs/guides/design.md:37-41``, ``/root/reference/README.md:27``).
+"""
+
+import datetime
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from foremast_amd.brain.node import owner_of
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HELPER = os.path.join(ROOT, "tests", "helpers", "roster_rank.py")
+sys.path.insert(0, os.path.join(ROOT, "tests", "helpers"))
+from roster_rank import counts_of, engines_of, live_apps  # noqa: E402
+
+TICKS, PER_TICK, SPAN = 24, 12, 180
+
+
+def run(tmp_path, n):
+    import torch.distributed as dist
+    kv = dist.TCPStore("127.0.0.1", 0, is_master=True, wait_for_workers=False, timeout=datetime.timedelta(seconds=90))
+    procs, outs = [], []
+    for i in range(n):
+        out = tmp_path / f"roster_n{n}_r{i}.jsonl"
+        env = dict(os.environ, OMP_NUM_THREADS="1", CUDA_VISIBLE_DEVICES="", GLOO_SOCKET_IFNAME="lo")
+        procs.append(subprocess.Popen([sys.executable, HELPER, str(kv.port), str(i), str(n), str(TICKS),
+                                       str(PER_TICK), str(SPAN), str(out)], env=env, cwd=ROOT,
+                                      stderr=subprocess.PIPE, text=True))
+        outs.append(out)
+    try:
+        for p in procs:
+            _, err = p.communicate(timeout=300)
+            assert p.returncode == 0, err[-4000:]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return [[json.loads(x) for x in o.read_text().splitlines()] for o in outs]
+
+
+def expected(k, n):
+    apps = {}
+    for a in live_apps(k, PER_TICK, SPAN):
+        c = np.sum([counts_of(a, k, e) for e in engines_of(a)], axis=0).tolist()
+        apps[f"ns/app{a}"] = (c, owner_of("ns", f"app{a}", n))
+    return apps
+
+
+@pytest.mark.slow
+def test_churning_roster_n_ranks_equal_one_rank(tmp_path):
+    ref = run(tmp_path, 1)[0]
+    for k, line in enumerate(ref):
+        want = expected(k, 1)
+        assert {a: v for a, v in line["apps"].items()} == {a: c for a, (c, _) in want.items()}, k
+    rec = {}
+    for n in (2, 4, 8):
+        lines = run(tmp_path, n)
+        for rank_lines in lines:
+            assert len(rank_lines) == TICKS
+            for k, (line, r1) in enumerate(zip(rank_lines, ref)):
+                assert line["apps"] == r1["apps"], (n, k)
+                assert line["anomalous"] == r1["anomalous"], (n, k)
+                assert line["generation"] == 0
+        # bytes through the store per tick follow the changes: after the first full rosters,
+        # each rank publishes ~(2 x PER_TICK / n) changes and reads the other ranks' deltas
+        steady = [ln["roster_bytes"] for ln in lines[0][2:]]
+        full = max(ln["roster_bytes"] for ln in lines[0][:1])
+        assert np.median(steady) < 0.5 * full or full < 2000, (n, steady, full)
+        ms = [ln["exchange_ms"] for ls in lines for ln in ls[2:]]
+        own = [ln["phases"]["publish"] + ln["phases"]["rosters"] + ln["phases"]["table"] for ls in lines for ln in ls[2:]]
+        rec[n] = {"exchange_ms_p50": float(np.percentile(ms, 50)), "exchange_ms_p90": float(np.percentile(ms, 90)),
+                  "roster_and_table_ms_p50": float(np.percentile(own, 50)),
+                  "roster_bytes_p50": float(np.median(steady)), "first_tick_bytes": full}
+    (tmp_path / "exchange_record.json").write_text(json.dumps(rec))
+    print("exchange record", json.dumps(rec))
