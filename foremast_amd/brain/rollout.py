@@ -62,6 +62,7 @@ import collections
 import heapq
 import json
 import logging
+import os
 import time
 from typing import Callable, Dict, List, Optional, Tuple
 
@@ -274,7 +275,23 @@ class RolloutMonitor:
         self._app_free: List[int] = []
         self._app_new: List[Tuple[Tuple[str, str], List[int]]] = []
         self._app_gone: List[Tuple[str, str]] = []
-        self._thr_cache: Dict[int, Tuple[float, int, float]] = {}   # (alias, metric) key -> threshold
+        self._thr_cache: Dict[int, Tuple[float, int, float, int]] = {}   # (alias, metric) key -> threshold
+        # window-corrected thresholds by (class, valid points): ONE table per distinct
+        # (threshold, bound), built on the host in fp64 when a class first appears, read by
+        # the detect kernel (no per-tick fp64 work on the device)
+        self._thr_classes: Dict[Tuple[float, int], int] = {}
+        self._lut: Optional[torch.Tensor] = None
+        self._lut_n = self.P * self.Wc + 1
+        # GPU scoring half: decoded block waiting for the device, tick scalars, record buffers,
+        # captured HIP graphs of the scoring launches (FOREMAST_ROLLOUT_GRAPH=0: eager)
+        self._pending: Optional[Tuple[torch.Tensor, int, int]] = None
+        self._graphs: Dict[tuple, object] = {}
+        self._src_devs: Dict[Tuple[int, int], torch.Tensor] = {}
+        self.graph_on = os.environ.get("FOREMAST_ROLLOUT_GRAPH", "1") != "0"
+        self.graph_replays = 0
+        if self.gpu:
+            self._tick_host = torch.zeros(4, dtype=torch.int32).pin_memory()
+            self._tick_dev = torch.zeros(4, dtype=torch.int32, device=self.device)
         self._n_live = 0
         self._build_grid()
         self.anomalies = None
@@ -332,6 +349,7 @@ class RolloutMonitor:
             "min_lower": torch.zeros(cap, **f32),
             "app_id": torch.zeros(cap, dtype=torch.int32, device=dev),
             "start_min": torch.zeros(cap, dtype=torch.int32, device=dev),
+            "thr_cls": torch.zeros(cap, dtype=torch.int16, device=dev),
             # joint bivariate model of a 2-metric job, kept on its first alias's row
             "biv_mean": torch.zeros((cap, 2), **f32),
             "biv_cov": torch.zeros((cap, 3), **f32),
@@ -373,7 +391,12 @@ class RolloutMonitor:
         self.cap = cap
         if self.gpu:
             from ..ops import kernels as K
-            self.anomalies = K.AnomalyBuffer(max(1024, 4 * cap), dev)
+            # the scoring half's ONE copy back: [cap, 4] row records + the K9 list count
+            self._rec_dev = torch.zeros(cap * 4 + 4, dtype=torch.float32, device=dev)
+            self._rec_host = torch.zeros(cap * 4 + 4, dtype=torch.float32).pin_memory()
+            self.anomalies = K.AnomalyBuffer(max(1024, 4 * cap), dev,
+                                             count=self._rec_dev[cap * 4:cap * 4 + 1].view(torch.int32))
+            self._graphs = {}
 
     def _free_rows(self, rows) -> None:
         ra = np.asarray(rows, dtype=np.int64)
@@ -645,15 +668,16 @@ class RolloutMonitor:
         # thresholds per (alias, metric) class: one lookup per distinct class of the batch
         u, first, inv = np.unique(b.u64[:, 5], return_index=True, return_inverse=True)
         cache = self._thr_cache
-        tab = np.empty((len(u), 3), dtype=np.float64)
+        tab = np.empty((len(u), 4), dtype=np.float64)
         for k, (key, i) in enumerate(zip(u.tolist(), first.tolist())):
             t = cache.get(key)
             if t is None:
                 c, s_ = b.cols_of(i), b.s_of(i)
                 m = self.cfg.for_metric(c.alias[s_], c.hfam[s_][1])
-                t = cache[key] = (m.threshold, m.bound, m.min_lower_bound)
+                t = cache[key] = (m.threshold, m.bound, m.min_lower_bound, self._thr_class(m.threshold, m.bound))
             tab[k] = t
         thr = tab[inv]
+        self.thr_cls[torch.from_numpy(b.rows).to(dev)] = torch.from_numpy(thr[:, 3].astype(np.int16)).to(dev)
         rows = torch.from_numpy(b.rows).to(dev)
         self.threshold[rows] = torch.from_numpy(thr[:, 0].astype(np.float32)).to(dev)
         self.bound[rows] = torch.from_numpy(thr[:, 1].astype(np.int8)).to(dev)
@@ -661,6 +685,31 @@ class RolloutMonitor:
         self.start_min[rows] = torch.from_numpy(np.round(b.f64[:, 0] / self.step).astype(np.int32)).to(dev)
         self.win[rows] = float("nan")
         self.base[rows] = float("nan")
+
+    def _thr_class(self, threshold: float, bound: int) -> int:
+        """Class of (threshold, bound) in the device threshold table: row ``[cls, 0, n]``
+        is the Sidak-corrected per-point level of a window of n valid points,
+        ``[cls, 1, n]`` the lowered (pairwise) one (``models/detect.py``
+        ``window_threshold``, computed in fp64 on the host once per class)."""
+        key = (float(np.float32(threshold)), int(bound))
+        k = self._thr_classes.get(key)
+        if k is not None:
+            return k
+        k = self._thr_classes[key] = len(self._thr_classes)
+        cfg, n = self.cfg, self._lut_n
+        pts = torch.arange(n, dtype=torch.float64)
+        thr = torch.full((n,), key[0], dtype=torch.float32)
+        bnd = torch.full((n,), key[1], dtype=torch.int8)
+        full, low = det_ref.effective_thresholds(thr, bnd, pts, cfg.pairwise_scale, cfg.window_correction)
+        row = torch.stack([full, low]).float()
+        if self._lut is None or self._lut.shape[0] <= k:
+            cap = 8 if self._lut is None else 2 * self._lut.shape[0]
+            lut = torch.zeros((cap, 2, n), dtype=torch.float32, device=self.device)
+            if self._lut is not None:
+                lut[:self._lut.shape[0]].copy_(self._lut)
+            self._lut = lut
+        self._lut[k].copy_(row.to(self.device))
+        return k
 
     def _fit(self, b: "_Batch") -> None:
         """Fit every admitted row's model on its history ending at the job's
@@ -1109,12 +1158,11 @@ class RolloutMonitor:
         self.timings["decode_ms"] = (time.perf_counter() - t0) * 1e3
         if not all(ok):
             return  # t_cur stays: the next tick fetches these minutes again
-        col0 = (int(round(first / self.step)) - self.start_min).to(torch.int32).contiguous()
         src = block_t.view(S * F, k)
-        if self.gpu:
-            from ..ops import kernels as K
-            K.rollout_scatter(self.win, P, self.Wc, src.to(self.device, non_blocking=True), col0, srcmap)
+        if self.gpu:  # H2D + scatter are the first launches of the scoring half (_score_dev)
+            self._pending = (src, int(round(first / self.step)), k)
         else:
+            col0 = (int(round(first / self.step)) - self.start_min).to(torch.int32).contiguous()
             win = self.win.view(self.cap, P, self.Wc)
             sm = srcmap.view(self.cap, P).long()
             for j in range(k):
@@ -1126,62 +1174,134 @@ class RolloutMonitor:
                 win[rr, pp, c[rr]] = vals[rr, pp]
         self.t_cur = t_new
 
+    # ------------------------------------------------------------------ GPU scoring half
+    def _src_dev(self, rows: int, k: int) -> torch.Tensor:
+        t = self._src_devs.get((rows, k))
+        if t is None:
+            t = torch.empty((rows, k), dtype=torch.float32, device=self.device)
+            self._src_devs = {(rows, k): t}
+        return t
+
+    def _score_launch(self, pend) -> None:
+        """Every device operation of the scoring half, stream-ordered and without a
+        host synchronisation (captured once as a HIP graph and replayed): tick
+        scalars H2D, tick block H2D, scatter into the windows (zeroing the per-app
+        counters and the K9 count), rank tests, band / verdict / counters / K9 list
+        / per-row record from the cached model state with the tabulated thresholds,
+        record D2H.  Four copies and three kernels."""
+        from ..ops import kernels as K
+        cfg, P, Wc = self.cfg, self.P, self.Wc
+        self._tick_dev.copy_(self._tick_host, non_blocking=True)
+        zero = (self.app_stats.view(-1), self.anomalies.count)
+        if pend is not None:
+            src_host, _first, k = pend
+            src = self._src_dev(src_host.shape[0], k)
+            src.copy_(src_host, non_blocking=True)
+            K.rollout_tick_scatter(self.win, P, Wc, src, self.start_min, self._tick_dev[0:1], self._srcmap_t, zero)
+        else:
+            K.rollout_tick_scatter(self.win[:0], P, Wc, self._src_dev(1, 1), self.start_min[:0], self._tick_dev[0:1],
+                                   None, zero)
+        pw_mode = pw_ref.PW_BY_NAME.get(cfg.pairwise_algorithm.upper(), pw_ref.PW_ALL)
+        differs = None
+        if pw_mode != pw_ref.PW_NONE:
+            self.pw_out = K.rank_tests(self.base, self.win, pw_mode, cfg.pairwise_threshold, cfg.min_mann_white,
+                                       cfg.min_wilcoxon, cfg.min_kruskal, want_pvals=False, out=self.pw_out,
+                                       pods=(P, P), min_friedman=cfg.min_friedman)
+            differs = self.pw_out["differs"]
+        cap = self.cap
+        spec = K.DetectSpec(horizons=self.hz, threshold=self.threshold, bound=self.bound, min_lower=self.min_lower,
+                            cur=self.win, differs=differs, pw_scale=cfg.pairwise_scale,
+                            min_valid=cfg.min_historical_points, want_band=True, app_id=self.app_id,
+                            app_stats=self.app_stats, anomalies=self.anomalies,
+                            pw_min_points=cfg.pairwise_min_points, shift_threshold=cfg.pairwise_shift,
+                            shift_min_points=cfg.pairwise_shift_min_points,
+                            base_mean=self.pw_out["base_mean"] if differs is not None else None,
+                            horizon_variance=cfg.horizon_variance, thr_lut=self._lut, thr_cls=self.thr_cls,
+                            row_out=self._rec_dev[:cap * 4].view(cap, 4), start_min=self.start_min,
+                            tick_min=self._tick_dev[1:2], last_ncol=Wc)
+        st = dict(self.state)
+        st.update(self.out)
+        out = K.hw_detect_deferred(st, spec, self.m_detect, self.m_detect,
+                                   grid=self.grid_all if cfg.horizon_variance else None)
+        self.out = {k: out[k] for k in ("forecast", "upper", "lower", "count", "verdict", "score")}
+        self._rec_host.copy_(self._rec_dev, non_blocking=True)
+
+    def _score_dev(self):
+        """The scoring half on the GPU: one graph replay (or the eager launches),
+        one synchronisation, the host record; returns (verdict, points seen, upper,
+        lower at the newest column, anomaly rows, columns, values)."""
+        pend, self._pending = self._pending, None
+        if self._lut is None:  # no class yet (rows admitted without _set_row_params): one neutral class
+            self._thr_class(self.cfg.threshold, self.cfg.bound)
+        th = self._tick_host.numpy()
+        th[0] = pend[1] if pend is not None else 0
+        th[1] = int(round(self.t_cur / self.step))
+        self._srcmap()  # row map in sync with this tick's admissions / releases (in place)
+        use_graph = self.graph_on and pend is not None and pend[2] == 1
+        if use_graph:
+            key = (self.cap, tuple(pend[0].shape), pend[0].data_ptr(), self._srcmap_t.data_ptr(),
+                   self._lut.data_ptr(), self.app_stats.data_ptr(), self.win.data_ptr(),
+                   self.cfg.pairwise_algorithm)
+            g = self._graphs.get(key)
+            if g is None:
+                self._score_launch(pend)          # this tick eagerly (allocates any outputs) ...
+                torch.cuda.current_stream(self.device).synchronize()
+                g = torch.cuda.CUDAGraph()        # ... and the next ones as one replay
+                with torch.cuda.graph(g):
+                    self._score_launch(pend)
+                if len(self._graphs) >= 4:
+                    self._graphs.clear()
+                self._graphs[key] = g
+            else:
+                g.replay()
+                self.graph_replays += 1
+        else:
+            self._score_launch(pend)
+        torch.cuda.current_stream(self.device).synchronize()
+        cap = self.cap
+        rec = self._rec_host.numpy()
+        rows = rec[:cap * 4].reshape(cap, 4)
+        n_anom = int(rec[cap * 4:cap * 4 + 1].view(np.int32)[0])
+        verdict = rows[:, 0].astype(np.int8)
+        a_rows, a_cols, a_vals, overflow = self.anomalies.fetch(n_anom)
+        if overflow:  # more anomalous points than the list holds: re-derive from the band
+            a_rows, a_cols, a_vals = self._anomalies_from_band(verdict)
+        return verdict, rows[:, 1], rows[:, 2].copy(), rows[:, 3].copy(), a_rows, a_cols, a_vals
+
     def _score(self) -> Dict[str, torch.Tensor]:
-        cfg, dev = self.cfg, self.device
+        """The scoring half on the CPU: the PyTorch reference models (fp64 Sidak
+        thresholds per row, as the device table holds them)."""
+        cfg = self.cfg
         valid = ~torch.isnan(self.win)
         npts = valid.sum(1)
         thr_f, thr_l = det_ref.effective_thresholds(self.threshold, self.bound, npts, cfg.pairwise_scale,
                                                     cfg.window_correction)
-        thr_f, thr_l = thr_f.contiguous(), thr_l.contiguous()
         pw_mode = pw_ref.PW_BY_NAME.get(cfg.pairwise_algorithm.upper(), pw_ref.PW_ALL)
         self.app_stats.zero_()
         differs = None
-        if self.gpu:
-            from ..ops import kernels as K
-            if pw_mode != pw_ref.PW_NONE:
-                self.pw_out = K.rank_tests(self.base, self.win, pw_mode, cfg.pairwise_threshold, cfg.min_mann_white,
-                                           cfg.min_wilcoxon, cfg.min_kruskal, want_pvals=False, out=self.pw_out,
-                                           pods=(self.P, self.P), min_friedman=cfg.min_friedman)
-                differs = self.pw_out["differs"]
-            self.anomalies.reset()
-            spec = K.DetectSpec(horizons=self.hz, threshold=thr_f, bound=self.bound, min_lower=self.min_lower,
-                                cur=self.win, differs=differs, pw_scale=cfg.pairwise_scale,
-                                min_valid=cfg.min_historical_points, want_band=True, app_id=self.app_id,
-                                app_stats=self.app_stats, anomalies=self.anomalies, threshold_low=thr_l,
-                                pw_min_points=cfg.pairwise_min_points,
-                                shift_threshold=cfg.pairwise_shift, shift_min_points=cfg.pairwise_shift_min_points,
-                                base_mean=self.pw_out["base_mean"] if differs is not None else None,
-                                horizon_variance=cfg.horizon_variance)
-            st = dict(self.state)
-            st.update(self.out)
-            out = K.hw_detect_deferred(st, spec, self.m_detect, self.m_detect,
-                                       grid=self.grid_all if cfg.horizon_variance else None)
-            self.out = {k: out[k] for k in ("forecast", "upper", "lower", "count", "verdict", "score")}
-        else:
-            if pw_mode != pw_ref.PW_NONE:
-                res = pw_ref.rank_tests(self.base, self.win, pods=(self.P, self.P))
-                differs = pw_ref.pairwise_differs(res, pw_mode, cfg.pairwise_threshold, cfg.min_mann_white,
-                                                  cfg.min_wilcoxon, cfg.min_kruskal, cfg.min_friedman)
-            s = self.state
-            h = self.hz.long()
-            f = s["level"][:, None] + h * s["trend"][:, None] + s["season_hb"].gather(1, (h.clamp(max=HB) - 1))
-            sigma = s["sigma"][:, None].expand_as(f)
-            if cfg.horizon_variance:
-                best = s["best"].long()
-                params = torch.where((best >= 0)[:, None], self.grid_all[best.clamp(min=0)],
-                                     torch.zeros((best.shape[0], 3)))
-                sigma = sigma * det_ref.horizon_sigma_factor(params, sm_ref.MODE_HW, self.m_detect, h)
-            d = det_ref.detect(f, sigma, self.win, thr_f, self.bound, self.min_lower, differs=differs,
-                               pairwise_scale=cfg.pairwise_scale, model_ok=s["nvalid"] >= cfg.min_historical_points,
-                               threshold_low=thr_l, pw_min_points=cfg.pairwise_min_points,
-                               shift_threshold=cfg.pairwise_shift, shift_min_points=cfg.pairwise_shift_min_points,
-                               base_mean=torch.nanmean(self.base.float(), 1) if differs is not None else None)
-            v = d.verdict.long()
-            self.app_stats.index_put_((self.app_id.long(), torch.zeros_like(v)), (v == 1).int(), accumulate=True)
-            self.app_stats.index_put_((self.app_id.long(), torch.ones_like(v)), (v >= 0).int(), accumulate=True)
-            self.out = {"forecast": f, "upper": d.upper, "lower": d.lower, "count": d.count, "verdict": d.verdict,
-                        "score": d.score, "_anomaly": d.anomaly}
-        self.out["npts"] = npts
+        if pw_mode != pw_ref.PW_NONE:
+            res = pw_ref.rank_tests(self.base, self.win, pods=(self.P, self.P))
+            differs = pw_ref.pairwise_differs(res, pw_mode, cfg.pairwise_threshold, cfg.min_mann_white,
+                                              cfg.min_wilcoxon, cfg.min_kruskal, cfg.min_friedman)
+        s = self.state
+        h = self.hz.long()
+        f = s["level"][:, None] + h * s["trend"][:, None] + s["season_hb"].gather(1, (h.clamp(max=HB) - 1))
+        sigma = s["sigma"][:, None].expand_as(f)
+        if cfg.horizon_variance:
+            best = s["best"].long()
+            params = torch.where((best >= 0)[:, None], self.grid_all[best.clamp(min=0)],
+                                 torch.zeros((best.shape[0], 3)))
+            sigma = sigma * det_ref.horizon_sigma_factor(params, sm_ref.MODE_HW, self.m_detect, h)
+        d = det_ref.detect(f, sigma, self.win, thr_f, self.bound, self.min_lower, differs=differs,
+                           pairwise_scale=cfg.pairwise_scale, model_ok=s["nvalid"] >= cfg.min_historical_points,
+                           threshold_low=thr_l, pw_min_points=cfg.pairwise_min_points,
+                           shift_threshold=cfg.pairwise_shift, shift_min_points=cfg.pairwise_shift_min_points,
+                           base_mean=torch.nanmean(self.base.float(), 1) if differs is not None else None)
+        v = d.verdict.long()
+        self.app_stats.index_put_((self.app_id.long(), torch.zeros_like(v)), (v == 1).int(), accumulate=True)
+        self.app_stats.index_put_((self.app_id.long(), torch.ones_like(v)), (v >= 0).int(), accumulate=True)
+        self.out = {"forecast": f, "upper": d.upper, "lower": d.lower, "count": d.count, "verdict": d.verdict,
+                    "score": d.score, "_anomaly": d.anomaly, "npts": npts}
         return self.out
 
     # ------------------------------------------------------------------ ticks
@@ -1213,25 +1333,24 @@ class RolloutMonitor:
             return written
         await self._ingest(t_new)
         t0 = time.perf_counter()
-        out = self._score()
-        # ONE device->host copy of the per-row results (verdict, points seen, band at the newest column)
-        last_c = ((int(round(self.t_cur / self.step)) - self.start_min).clamp(0, self.Wc - 1)).long()
-        up = out["upper"].gather(1, last_c[:, None])[:, 0]
-        lo = out["lower"].gather(1, last_c[:, None])[:, 0]
-        host = torch.stack([out["verdict"].float(), out["npts"].float(), up, lo]).cpu().numpy()
-        verdict, npts = host[0].astype(np.int8), host[1]
+        last_c = None
         if self.gpu:
-            a_rows, a_cols, a_vals, overflow = self.anomalies.fetch()
-            if overflow:  # more anomalous points than the list holds: re-derive from the band
-                a_rows, a_cols, a_vals = self._anomalies_from_band(verdict)
+            verdict, npts, up, lo, a_rows, a_cols, a_vals = self._score_dev()
         else:
+            out = self._score()
+            last_c = ((int(round(self.t_cur / self.step)) - self.start_min).clamp(0, self.Wc - 1)).long()
+            up = out["upper"].gather(1, last_c[:, None])[:, 0].numpy()
+            lo = out["lower"].gather(1, last_c[:, None])[:, 0].numpy()
+            verdict, npts = out["verdict"].numpy().astype(np.int8), out["npts"].float().numpy()
             a_rows, a_cols = np.nonzero(out["_anomaly"].numpy() & (out["verdict"] == 1).numpy()[:, None])
             a_vals = self.win.numpy()[a_rows, a_cols]
         self.timings["score_ms"] = (time.perf_counter() - t0) * 1e3
         t0 = time.perf_counter()
         joint = self._score_joint() if self.cfg.algorithm in pl.JOINT_ALGORITHMS else None
+        if self.joint_lstm is not None and last_c is None:
+            last_c = ((int(round(self.t_cur / self.step)) - self.start_min).clamp(0, self.Wc - 1)).long()
         lstm_hits = await self._tick_lstm(last_c)
-        self._bands = (host[2], host[3], verdict)
+        self._bands = (up, lo, verdict)
         written = self._verdicts(now, verdict, npts, a_rows, a_cols, a_vals, joint, lstm_hits)
         self.timings["verdict_ms"] = (time.perf_counter() - t0) * 1e3
         self.ticks += 1

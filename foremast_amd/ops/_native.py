@@ -41,6 +41,8 @@ class DetectArgs(C.Structure):
         ("score", P), ("app_id", P), ("app_stats", P),
         ("anom_count", P), ("anom_series", P), ("anom_col", P), ("anom_val", P), ("anom_cap", I), ("shift_thr", F), ("base_mean", P),
         ("shift_min_points", I), ("_pad1", I),
+        ("thr_lut", P), ("thr_cls", P), ("lut_n", I), ("last_ncol", I), ("row_out", P), ("start_min", P),
+        ("tick_min", P),
     ]
 
 

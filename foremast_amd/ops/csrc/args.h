@@ -45,6 +45,18 @@ struct DetectArgs {
   const float* base_mean;       // [N] mean of the baseline pods' window (NaN: none) or null
   int shift_min_points;         // the mean-shift rule needs this many valid canary points
   int _pad1;
+  // per-point thresholds by (class, valid points of the window): the Sidak window
+  // correction of models/detect.py window_threshold, tabulated on the host in fp64 (no
+  // per-tick fp64 on the device).  Null: threshold / threshold_low as given.
+  const float* thr_lut;          // [classes, 2, lut_n] (full, lowered)
+  const unsigned short* thr_cls; // [N] class of each series
+  int lut_n;                     // valid-point counts covered: 0 .. lut_n - 1 (larger: clamped)
+  int last_ncol;                 // columns per pod window (row_out's newest column is in 0 .. last_ncol - 1)
+  // per-series record for the host's ONE copy back (or null): verdict, valid points,
+  // upper and lower at the newest column clamp(tick_min[0] - start_min[n], 0, last_ncol - 1)
+  float* row_out;                // [N, 4]
+  const int* start_min;          // [N] minute of each series' first window column
+  const int* tick_min;           // [1] newest minute (device scalar: HIP-graph replays read it)
 };
 
 struct SmoothArgs {

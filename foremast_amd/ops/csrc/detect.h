@@ -63,11 +63,18 @@ struct DetThr {
   float full, low, shift, bm;
   bool differs, shift_on;
 };
-__device__ __forceinline__ DetThr det_thresholds(const DetectArgs& d, int n) {
+__device__ __forceinline__ DetThr det_thresholds(const DetectArgs& d, int n, int npts) {
   DetThr t;
-  t.full = d.threshold[n];
   t.differs = d.differs && d.differs[n];
-  t.low = d.threshold_low ? d.threshold_low[n] : t.full * d.pw_scale;
+  if (d.thr_lut) {  // window-corrected levels of the series' class at its valid-point count
+    const int k = npts < d.lut_n ? npts : d.lut_n - 1;
+    const float* row = d.thr_lut + (long long)d.thr_cls[n] * 2 * d.lut_n;
+    t.full = row[k];
+    t.low = row[d.lut_n + k];
+  } else {
+    t.full = d.threshold[n];
+    t.low = d.threshold_low ? d.threshold_low[n] : t.full * d.pw_scale;
+  }
   t.shift = d.shift_thr;
   t.bm = (d.base_mean && t.differs) ? d.base_mean[n] : fm_nan();
   t.shift_on = t.differs && d.shift_thr > 0.f && t.bm == t.bm;
@@ -81,6 +88,18 @@ struct DetSums {
 
 __device__ __forceinline__ bool det_outside(float x, float f, float thr, float s, float mlow, int bnd) {
   return ((bnd & 1) && x > f + thr * s) || ((bnd & 2) && x < fmaxf(f - thr * s, mlow));
+}
+
+// Newest window column of series n for the host record (row_out).
+__device__ __forceinline__ int det_last_col(const DetectArgs& d, int n) {
+  int c = d.tick_min[0] - d.start_min[n];
+  return c < 0 ? 0 : (c >= d.last_ncol ? d.last_ncol - 1 : c);
+}
+
+// Valid (non-NaN) points of column c, for the threshold table's pre-pass.
+__device__ __forceinline__ float det_valid_col(const DetectArgs& d, int n, int c) {
+  const float x = d.cur[(long long)n * d.ld_cur + c];
+  return x == x ? 1.f : 0.f;
 }
 
 // Pass 1 of a column: counts against both bands (the caller reduces them).
@@ -121,6 +140,10 @@ __device__ __forceinline__ void det_emit_col(const DetectArgs& d, int n, int c, 
   if (d.forecast) d.forecast[o] = f;
   if (d.upper) d.upper[o] = up;
   if (d.lower) d.lower[o] = lo;
+  if (d.row_out && c == det_last_col(d, n)) {
+    d.row_out[4 * (long long)n + 2] = up;
+    d.row_out[4 * (long long)n + 3] = lo;
+  }
   if (emit) {
     const float x = d.cur[(long long)n * d.ld_cur + c];
     if (x == x && (((bnd & 1) && x > up) || ((bnd & 2) && x < lo))) {
@@ -157,11 +180,16 @@ __device__ __forceinline__ float det_decide(const DetectArgs& d, const DetThr& t
   return t.full;
 }
 
-__device__ __forceinline__ void det_write(const DetectArgs& d, int n, int ic, float anyv, bool model_ok, float sc) {
+__device__ __forceinline__ void det_write(const DetectArgs& d, int n, int ic, float anyv, bool model_ok, float sc,
+                                          float npts) {
   const int v = ic > 0 ? 1 : ((anyv > 0.f && model_ok) ? 0 : -1);
   d.count[n] = ic;
   d.verdict[n] = (signed char)v;
   d.score[n] = sc;
+  if (d.row_out) {
+    d.row_out[4 * (long long)n] = (float)v;
+    d.row_out[4 * (long long)n + 1] = npts;
+  }
   if (d.app_id) {
     const int app = d.app_id[n];
     if (v == 1) atomicAdd(&d.app_stats[2 * app], 1);
@@ -178,7 +206,12 @@ __device__ __forceinline__ void detect_epilogue_wave(const DetectArgs& d, int n,
                                                      ForecastFn fcast, int gidx = -1) {
   if (d.C <= 0) return;
   const int lane = lane_id();
-  const DetThr t = det_thresholds(d, n);
+  float npts = 0.f;
+  if (d.cur && (d.thr_lut || d.row_out)) {
+    for (int c = lane; c < d.C; c += FM_WAVE) npts += det_valid_col(d, n, c);
+    npts = wave_allsum(npts);
+  }
+  const DetThr t = det_thresholds(d, n, (int)npts);
   const int bnd = d.bound[n];
   const float mlow = d.min_lower[n];
   const bool model_ok = n_valid >= (float)d.min_valid;
@@ -200,9 +233,9 @@ __device__ __forceinline__ void detect_epilogue_wave(const DetectArgs& d, int n,
   }
   const float anyv = u.anyv, sc = u.sc;
   const bool emit = d.anom_count && ic > 0;
-  if (d.forecast || d.upper || d.lower || emit)
+  if (d.forecast || d.upper || d.lower || d.row_out || emit)
     for (int c = lane; c < d.C; c += FM_WAVE) det_emit_col(d, n, c, thr, sig, gidx, bnd, mlow, emit, fcast, center);
-  if (d.cur && lane == 0) det_write(d, n, ic, anyv, model_ok, sc);
+  if (d.cur && lane == 0) det_write(d, n, ic, anyv, model_ok, sc, npts);
 }
 
 // One WORKGROUP owns series n: threads stride the columns, block reductions.
@@ -211,7 +244,12 @@ __device__ __forceinline__ void detect_epilogue(const DetectArgs& d, int n, floa
                                                 ForecastFn fcast, float* red, int gidx = -1) {
   if (d.C <= 0) return;
   const int tid = threadIdx.x;
-  const DetThr t = det_thresholds(d, n);
+  float npts = 0.f;
+  if (d.cur && (d.thr_lut || d.row_out)) {
+    for (int c = tid; c < d.C; c += blockDim.x) npts += det_valid_col(d, n, c);
+    npts = blk_sum(npts, red);
+  }
+  const DetThr t = det_thresholds(d, n, (int)npts);
   const int bnd = d.bound[n];
   const float mlow = d.min_lower[n];
   const bool model_ok = n_valid >= (float)d.min_valid;
@@ -233,7 +271,7 @@ __device__ __forceinline__ void detect_epilogue(const DetectArgs& d, int n, floa
   }
   const float anyv = u.anyv, sc = u.sc;
   const bool emit = d.anom_count && ic > 0;
-  if (d.forecast || d.upper || d.lower || emit)
+  if (d.forecast || d.upper || d.lower || d.row_out || emit)
     for (int c = tid; c < d.C; c += blockDim.x) det_emit_col(d, n, c, thr, sig, gidx, bnd, mlow, emit, fcast, center);
-  if (d.cur && tid == 0) det_write(d, n, ic, anyv, model_ok, sc);
+  if (d.cur && tid == 0) det_write(d, n, ic, anyv, model_ok, sc, npts);
 }

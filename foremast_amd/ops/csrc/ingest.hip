@@ -169,6 +169,48 @@ __global__ __launch_bounds__(256) void rollout_scatter_kernel(float* __restrict_
   if (v == v) win[(long long)n * ld_w + p * Wc + c] = v;
 }
 
+// The product tick's first kernel (brain/rollout.py): the same scatter with the window
+// column computed in-kernel from the tick's first minute (a device scalar, so a captured
+// HIP graph replays it unchanged) and the row's first-column minute, and the per-tick
+// counters of the detection epilogue zeroed on the way (per-app counters, the K9 list
+// count): one launch instead of four.
+__global__ __launch_bounds__(256) void rollout_tick_scatter_kernel(float* __restrict__ win, long long ld_w, int P,
+                                                                   int Wc, const float* __restrict__ src,
+                                                                   long long ld_s, int k, long long S,
+                                                                   const int* __restrict__ srcmap,
+                                                                   const int* __restrict__ start_min,
+                                                                   const int* __restrict__ tick, int N,
+                                                                   int* __restrict__ zero_a, int n_a,
+                                                                   int* __restrict__ zero_b, int n_b) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_a) zero_a[i] = 0;
+  if (i < n_b) zero_b[i] = 0;
+  const long long total = (long long)N * P * k;
+  if (i >= total) return;
+  const int j = (int)(i % k);
+  const long long np = i / k;  // n * P + p
+  const int n = (int)(np / P), p = (int)(np % P);
+  const int c = tick[0] - start_min[n] + j;
+  if (c < 0 || c >= Wc) return;
+  const long long sr = srcmap ? (long long)srcmap[np] : np;
+  if (sr < 0 || sr >= S) return;
+  const float v = src[sr * ld_s + j];
+  if (v == v) win[(long long)n * ld_w + p * Wc + c] = v;
+}
+
+extern "C" int fm_rollout_tick_scatter(float* win, long long ld_w, int P, int Wc, const float* src, long long ld_s,
+                                       int k, long long S, const int* srcmap, const int* start_min, const int* tick,
+                                       int N, int* zero_a, int n_a, int* zero_b, int n_b, hipStream_t st) {
+  if (P <= 0 || Wc <= 0 || k <= 0 || N < 0 || n_a < 0 || n_b < 0) return (int)hipErrorInvalidValue;
+  long long total = (long long)N * P * k;
+  if (total < n_a) total = n_a;
+  if (total < n_b) total = n_b;
+  if (total <= 0) return 0;
+  hipLaunchKernelGGL(rollout_tick_scatter_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, win, ld_w,
+                     P, Wc, src, ld_s, k, S, srcmap, start_min, tick, N, zero_a, n_a, zero_b, n_b);
+  return (int)hipGetLastError();
+}
+
 extern "C" int fm_rollout_scatter(float* win, long long ld_w, int P, int Wc, const float* src, long long ld_s, int k,
                                   long long S, const int* srcmap, const int* col0, int N, hipStream_t st) {
   if (N <= 0 || k <= 0) return 0;

@@ -10,7 +10,18 @@
 // sum_i (eq_i^2 - 1) in the same sweep.  All lanes read the same x_j per
 // iteration (an LDS broadcast), so the sweep is conflict-free.  For canary
 // windows (n ~ 20-200) this beats a sort: no data-dependent control flow.
+//
+// Small windows (nb, nc <= 64: the product's 5 pods x 11 minutes = 55 per side) take a
+// sort-and-search path instead (rank_tests_kernel<true>): each lane holds ONE baseline,
+// ONE canary and ONE |d| value; the three 64-element arrays are sorted together by a
+// register bitonic network (21 steps, DPP / ds_swizzle / bpermute exchanges), written to
+// the wave's LDS slice, and every lane finds the pooled rank and tie count of its own
+// values by branchless binary searches (lower / upper bound, 7 LDS reads each) in the
+// sorted arrays: rank = #less(base) + #less(cur) + (#eq(base) + #eq(cur) + 1) / 2.
+// O(n log n) per series with all 64 lanes busy, against the sweep's O(n^2) with
+// 112 of 128 lane slots (the sweep is VALU-issue bound: ~5.6 instructions per pair).
 #include "common.h"
+#include <stdlib.h>
 #include "args.h"
 
 
@@ -124,6 +135,98 @@ __device__ __forceinline__ void friedman_wave(const RankArgs& a, const float* x,
   }
 }
 
+// ---- small-window path: register bitonic sort + binary searches ------------------
+// lane ^ J exchange: DPP quad permutes for 1 / 2, ds_swizzle (bit mode, 32-lane groups)
+// for 4..16, a bpermute for 32.
+template <int J>
+__device__ __forceinline__ float xor_lane(float v) {
+  const int x = __float_as_int(v);
+  if constexpr (J == 1) return __int_as_float(__builtin_amdgcn_mov_dpp(x, 0xB1, 0xf, 0xf, false));
+  else if constexpr (J == 2) return __int_as_float(__builtin_amdgcn_mov_dpp(x, 0x4E, 0xf, 0xf, false));
+  else if constexpr (J < 32) return __int_as_float(__builtin_amdgcn_ds_swizzle(x, (J << 10) | 0x1F));
+  else return __shfl_xor(v, 32, FM_WAVE);
+}
+
+template <int K, int J>
+__device__ __forceinline__ void bitonic_step3(float& a, float& b, float& c, int lane) {
+  const bool take_min = ((lane & J) == 0) == ((lane & K) == 0);
+  const float pa = xor_lane<J>(a), pb = xor_lane<J>(b), pc = xor_lane<J>(c);
+  a = take_min ? fminf(a, pa) : fmaxf(a, pa);
+  b = take_min ? fminf(b, pb) : fmaxf(b, pb);
+  c = take_min ? fminf(c, pc) : fmaxf(c, pc);
+}
+
+template <int K, int J>
+__device__ __forceinline__ void bitonic_merge3(float& a, float& b, float& c, int lane) {
+  bitonic_step3<K, J>(a, b, c, lane);
+  if constexpr (J > 1) bitonic_merge3<K, J / 2>(a, b, c, lane);
+}
+
+template <int K>
+__device__ __forceinline__ void bitonic_sort3(float& a, float& b, float& c, int lane) {
+  if constexpr (K > 2) bitonic_sort3<K / 2>(a, b, c, lane);
+  bitonic_merge3<K, K / 2>(a, b, c, lane);
+}
+
+// Elements of the ascending 64-array s (+inf padded) that are < v (LE: <= v).
+template <bool LE>
+__device__ __forceinline__ int bound64(const float* s, float v) {
+  int pos = 0;
+#pragma unroll
+  for (int h = 32; h > 0; h >>= 1) {
+    const float q = s[pos + h - 1];
+    pos += (LE ? q <= v : q < v) ? h : 0;
+  }
+  const float q = s[pos];
+  return pos + ((LE ? q <= v : q < v) ? 1 : 0);
+}
+
+// Pooled-rank statistics of the small path (returned wave-uniform): baseline rank sum
+// R1, pooled tie term sum(t^3 - t), Wilcoxon positive / negative rank sums and its tie
+// term.  bv / cv / dv: this lane's baseline, canary and signed difference (NaN: none).
+__device__ __forceinline__ void small_ranks(float bv, float cv, float dv, float* s, int lane, int n1, int n2, int nd,
+                                            float& R1, float& tie, float& Tp, float& Tm, float& wtie) {
+  const float inf = __builtin_huge_valf();
+  const float ad = fabsf(dv);
+  float kb = bv == bv ? bv : inf, kc = cv == cv ? cv : inf, kd = ad == ad ? ad : inf;
+  bitonic_sort3<64>(kb, kc, kd, lane);
+  s[lane] = kb;
+  s[FM_WAVE + lane] = kc;
+  s[2 * FM_WAVE + lane] = kd;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  const float* sb = s;
+  const float* sc = s + FM_WAVE;
+  const float* sd = s + 2 * FM_WAVE;
+  float r1 = 0.f, t = 0.f, tp = 0.f, tm = 0.f, wt = 0.f;
+  if (bv == bv) {
+    const int lb = bound64<false>(sb, bv), ub = min(bound64<true>(sb, bv), n1);
+    const int lc = bound64<false>(sc, bv), uc = min(bound64<true>(sc, bv), n2);
+    const int eq = (ub - lb) + (uc - lc);
+    r1 = (float)(lb + lc) + 0.5f * (float)(eq + 1);
+    t += (float)(eq * eq - 1);
+  }
+  if (cv == cv) {
+    const int lb = bound64<false>(sb, cv), ub = min(bound64<true>(sb, cv), n1);
+    const int lc = bound64<false>(sc, cv), uc = min(bound64<true>(sc, cv), n2);
+    const int eq = (ub - lb) + (uc - lc);
+    t += (float)(eq * eq - 1);
+  }
+  if (ad == ad) {
+    const int lb = bound64<false>(sd, ad), ub = min(bound64<true>(sd, ad), nd);
+    const int eq = ub - lb;
+    const float r = (float)lb + 0.5f * (float)(eq + 1);
+    if (dv > 0.f) tp = r; else tm = r;
+    wt = (float)(eq * eq - 1);
+  }
+  R1 = wave_allsum(r1);
+  tie = wave_allsum(t);
+  Tp = wave_allsum(tp);
+  Tm = wave_allsum(tm);
+  wtie = wave_allsum(wt);
+}
+
+template <bool SMALL>
 __global__ __launch_bounds__(256) void rank_tests_kernel(const RankArgs a) {
   const int w = wave_id(), lane = lane_id();
   const int n = blockIdx.x * (blockDim.x / FM_WAVE) + w;
@@ -131,14 +234,40 @@ __global__ __launch_bounds__(256) void rank_tests_kernel(const RankArgs a) {
   const int npool4 = (npool + 3) & ~3;
   const int k = a.nb < a.nc ? a.nb : a.nc;
   const int k4 = (k + 3) & ~3;
-  float* x = (float*)fm_rank_smem + (size_t)w * (npool4 + k4 + FM_WAVE);
+  const int small_sz = SMALL ? 3 * FM_WAVE : 0;
+  float* x = (float*)fm_rank_smem + (size_t)w * (small_sz + npool4 + k4 + FM_WAVE) + small_sz;
   float* dabs = x + npool4;
   float* Rf = dabs + k4;  // Friedman rank sums (<= 64 treatments)
   if (n >= a.N) return;  // wave-uniform; no block barrier below
-
-  // stage pooled sample (NaN pads the vector tail) and |d| of aligned pairs
   const float* b = a.base + (long long)n * a.ld_base;
   const float* c = a.cur + (long long)n * a.ld_cur;
+  const bool want_fr = a.mode == 6 || a.p_friedman != nullptr;
+  float R1, tie, R2, Tp, wtie, Tm, n1, n2, np, sb;
+  float p_fr = 1.f, nblk = 0.f;
+  if constexpr (SMALL) {
+    const float bv = lane < a.nb ? b[lane] : fm_nan();
+    const float cv = lane < a.nc ? c[lane] : fm_nan();
+    float dv = fm_nan();
+    if (lane < k) {
+      const float d = cv - bv;
+      if (d == d && d != 0.f) dv = d;
+    }
+    n1 = wave_allsum(bv == bv ? 1.f : 0.f);
+    n2 = wave_allsum(cv == cv ? 1.f : 0.f);
+    np = wave_allsum(dv == dv ? 1.f : 0.f);
+    sb = a.base_mean ? wave_allsum(bv == bv ? bv : 0.f) : 0.f;
+    if (want_fr) {  // Friedman reads the pooled windows staged as the sweep stages them
+      for (int i = lane; i < npool4; i += FM_WAVE) x[i] = i < a.nb ? b[i] : (i < npool ? c[i - a.nb] : fm_nan());
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      friedman_wave(a, x, Rf, p_fr, nblk);
+    }
+    small_ranks(bv, cv, dv, x - small_sz, lane, (int)n1, (int)n2, (int)np, R1, tie, Tp, Tm, wtie);
+    const float nn = n1 + n2;
+    R2 = nn * (nn + 1.f) * 0.5f - R1;
+  } else {
+
+  // stage pooled sample (NaN pads the vector tail) and |d| of aligned pairs
   float cnt_b = 0.f, cnt_c = 0.f, sum_b = 0.f;
   for (int i = lane; i < npool4; i += FM_WAVE) {
     float v = fm_nan();
@@ -161,22 +290,22 @@ __global__ __launch_bounds__(256) void rank_tests_kernel(const RankArgs a) {
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  const float n1 = wave_sum(cnt_b), n2 = wave_sum(cnt_c), np = wave_sum(npairs);
-  const float sb = a.base_mean ? wave_sum(sum_b) : 0.f;
-  const float nn = n1 + n2;
+  n1 = wave_sum(cnt_b);
+  n2 = wave_sum(cnt_c);
+  np = wave_sum(npairs);
+  sb = a.base_mean ? wave_sum(sum_b) : 0.f;
 
   // --- Friedman (time blocks x pods) on the staged windows
-  float p_fr = 1.f, nblk = 0.f;
-  if (a.mode == 6 || a.p_friedman != nullptr) friedman_wave(a, x, Rf, p_fr, nblk);
+  if (want_fr) friedman_wave(a, x, Rf, p_fr, nblk);
 
   // --- MW / Kruskal share the pooled ranks
-  float R1, tie, R2;
   const int nbv = a.nb;
   rank_sweep(x, npool4, [nbv](int i) { return i < nbv; }, R1, tie, R2);
 
   // --- Wilcoxon: ranks of |d| over nonzero pairs, group = positive d
-  float Tp, wtie, Tm;
   rank_sweep(dabs, k4, [c, b](int i) { return (c[i] - b[i]) > 0.f; }, Tp, wtie, Tm);
+  }
+  const float nn = n1 + n2;
 
   if (lane != 0) return;
   // Mann-Whitney U (two-sided, continuity, tie-corrected)
@@ -240,11 +369,16 @@ __global__ __launch_bounds__(256) void rank_tests_kernel(const RankArgs a) {
   }
 }
 
+static bool rank_small(int nb, int nc) {
+  return nb <= FM_WAVE && nc <= FM_WAVE && !getenv("FOREMAST_RANK_SWEEP");
+}
+
 extern "C" size_t fm_rank_lds_bytes(int nb, int nc) {
   const int npool4 = (nb + nc + 3) & ~3;
   const int k = nb < nc ? nb : nc;
   const int k4 = (k + 3) & ~3;
-  return (size_t)4 * (npool4 + k4 + FM_WAVE) * 4;
+  const int small_sz = rank_small(nb, nc) ? 3 * FM_WAVE : 0;
+  return (size_t)4 * (small_sz + npool4 + k4 + FM_WAVE) * 4;
 }
 
 extern "C" int fm_rank_tests(const RankArgs* a, hipStream_t st) {
@@ -255,6 +389,9 @@ extern "C" int fm_rank_tests(const RankArgs* a, hipStream_t st) {
       (a->pods_b <= 0 || a->pods_c <= 0 || a->nb % a->pods_b || a->nc % a->pods_c || a->pods_b + a->pods_c > FM_WAVE))
     return (int)hipErrorInvalidValue;
   dim3 grid((a->N + 3) / 4), block(256);
-  hipLaunchKernelGGL(rank_tests_kernel, grid, block, lds, st, *a);
+  if (rank_small(a->nb, a->nc))
+    hipLaunchKernelGGL(rank_tests_kernel<true>, grid, block, lds, st, *a);
+  else
+    hipLaunchKernelGGL(rank_tests_kernel<false>, grid, block, lds, st, *a);
   return (int)hipGetLastError();
 }

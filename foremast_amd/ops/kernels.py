@@ -78,6 +78,16 @@ class DetectSpec:
     shift_threshold: float = 0.0
     base_mean: Optional[torch.Tensor] = None
     shift_min_points: int = 1
+    # window-corrected thresholds tabulated by (class, valid points) (detect.h det_thresholds):
+    # float32 [classes, 2, n] and uint16-in-int16 [N] classes; replaces threshold / threshold_low
+    thr_lut: Optional[torch.Tensor] = None
+    thr_cls: Optional[torch.Tensor] = None
+    # per-series host record [N, 4] (verdict, valid points, upper / lower at the newest column
+    # clamp(tick_min[0] - start_min[n], 0, last_ncol - 1))
+    row_out: Optional[torch.Tensor] = None
+    start_min: Optional[torch.Tensor] = None
+    tick_min: Optional[torch.Tensor] = None
+    last_ncol: int = 0
 
 
 class AnomalyBuffer:
@@ -85,10 +95,14 @@ class AnomalyBuffer:
     epilogue appends ``(series, column, value)`` triples; the host copies back
     only ``count`` and the used prefix instead of whole ``[N, C]`` bands."""
 
-    def __init__(self, cap: int, device) -> None:
+    def __init__(self, cap: int, device, count: Optional[torch.Tensor] = None) -> None:
+        """``count``: an int32 [1] device tensor to count in (e.g. the tail of a
+        per-tick record copied back in one piece); default: its own."""
         dev = torch.device(device)
         self.cap = int(cap)
-        self.count = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.count = torch.zeros(1, dtype=torch.int32, device=dev) if count is None else count
+        _need(self.count.dtype == torch.int32 and self.count.numel() == 1 and self.count.device == dev,
+              "count must be an int32 [1] tensor on the device")
         self.series = torch.empty(self.cap, dtype=torch.int32, device=dev)
         self.col = torch.empty(self.cap, dtype=torch.int32, device=dev)
         self.val = torch.empty(self.cap, dtype=torch.float32, device=dev)
@@ -96,12 +110,17 @@ class AnomalyBuffer:
     def reset(self) -> None:
         self.count.zero_()
 
-    def fetch(self):
+    def fetch(self, n_all: Optional[int] = None):
         """(series, col, val) numpy arrays sorted by (series, col), and whether
-        the buffer overflowed (more anomalies than ``cap``)."""
+        the buffer overflowed (more anomalies than ``cap``).  ``n_all``: the count
+        when the caller already copied it back."""
         import numpy as np
-        n_all = int(self.count.item())
+        if n_all is None:
+            n_all = int(self.count.item())
         n = min(n_all, self.cap)
+        if n == 0:
+            z = np.zeros(0, dtype=np.int32)
+            return z, z, np.zeros(0, dtype=np.float32), False
         s = self.series[:n].cpu().numpy()
         c = self.col[:n].cpu().numpy()
         v = self.val[:n].cpu().numpy()
@@ -175,6 +194,24 @@ def _fill_detect(d: nat.DetectArgs, spec: DetectSpec, N: int, device, out: Dict[
     d.score = nat.ptr(out["score"])
     d.app_id = nat.ptr(spec.app_id)
     d.app_stats = nat.ptr(spec.app_stats)
+    d.thr_lut, d.thr_cls, d.lut_n = None, None, 0
+    if spec.thr_lut is not None:
+        lut = spec.thr_lut
+        _need(lut.dim() == 3 and lut.shape[1] == 2 and lut.dtype == torch.float32 and lut.is_contiguous()
+              and lut.device == device and lut.shape[2] >= 1, "thr_lut must be contiguous float32 [K, 2, n]")
+        _vec(spec.thr_cls, N, torch.int16, "thr_cls", device)
+        d.thr_lut, d.thr_cls, d.lut_n = nat.ptr(lut), nat.ptr(spec.thr_cls), int(lut.shape[2])
+    d.row_out, d.start_min, d.tick_min, d.last_ncol = None, None, None, 0
+    if spec.row_out is not None:
+        ro = spec.row_out
+        _need(ro.dim() == 2 and ro.shape == (N, 4) and ro.dtype == torch.float32 and ro.is_contiguous()
+              and ro.device == device, f"row_out must be contiguous float32 [{N}, 4]")
+        _vec(spec.start_min, N, torch.int32, "start_min", device)
+        _need(spec.tick_min is not None and spec.tick_min.dtype == torch.int32 and spec.tick_min.device == device,
+              "row_out needs tick_min (int32 device scalar)")
+        _need(1 <= spec.last_ncol <= C, "last_ncol must be in 1..C")
+        d.row_out, d.start_min, d.tick_min = nat.ptr(ro), nat.ptr(spec.start_min), nat.ptr(spec.tick_min)
+        d.last_ncol = int(spec.last_ncol)
 
 
 def _set_hvar(d: nat.DetectArgs, spec: DetectSpec, grid: torch.Tensor, mode: int, m: int) -> None:
@@ -999,3 +1036,44 @@ def rollout_scatter(win: torch.Tensor, P: int, Wc: int, src: torch.Tensor, col0:
     nat.check(lib.fm_rollout_scatter(nat.ptr(win), win.stride(0), int(P), int(Wc), nat.ptr(src), src.stride(0),
                                      int(src.shape[1]), int(src.shape[0]), nat.ptr(srcmap), nat.ptr(col0), N,
                                      nat.stream_handle(win.device)), "fm_rollout_scatter")
+
+
+nat.register("fm_rollout_tick_scatter", [C.c_void_p, C.c_longlong, C.c_int, C.c_int, C.c_void_p, C.c_longlong,
+                                         C.c_int, C.c_longlong, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                         C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p])
+
+
+def rollout_tick_scatter(win: torch.Tensor, P: int, Wc: int, src: torch.Tensor, start_min: torch.Tensor,
+                         tick: torch.Tensor, srcmap: Optional[torch.Tensor] = None,
+                         zero: Tuple[torch.Tensor, ...] = ()) -> None:
+    """The product tick's scatter (csrc/ingest.hip ``rollout_tick_scatter_kernel``):
+    ``win[n, p*Wc + tick[0] - start_min[n] + j] = src[srcmap[n*P + p], j]`` inside the
+    window, and every int32 tensor of ``zero`` (at most two: the per-app counters, the
+    K9 list count) zeroed in the same launch.  ``tick``: int32 device tensor whose
+    element 0 is the block's first minute (read on the device: graph-capturable)."""
+    lib = nat.require()
+    _cuda(win, "win")
+    N = win.shape[0]
+    dev = win.device
+    _need(win.dim() == 2 and win.dtype == torch.float32 and win.stride(1) == 1 and win.shape[1] == P * Wc,
+          f"win must be float32 [N, {P * Wc}] with unit inner stride")
+    _need(src.dim() == 2 and src.dtype == torch.float32 and src.stride(1) == 1 and src.device == dev,
+          "src must be float32 [S, k] on the device")
+    if srcmap is None:
+        _need(src.shape[0] >= N * P, f"src must have >= {N * P} rows without a srcmap")
+    else:
+        _vec(srcmap, N * P, torch.int32, "srcmap", dev)
+    _vec(start_min, N, torch.int32, "start_min", dev)
+    _need(tick.dtype == torch.int32 and tick.numel() >= 1 and tick.device == dev, "tick must be int32 on the device")
+    _need(len(zero) <= 2, "at most two tensors to zero")
+    zs = []
+    for z in zero:
+        _need(z.dtype == torch.int32 and z.is_contiguous() and z.device == dev, "zeroed tensors: contiguous int32")
+        zs.append((nat.ptr(z), int(z.numel())))
+    while len(zs) < 2:
+        zs.append((None, 0))
+    nat.check(lib.fm_rollout_tick_scatter(nat.ptr(win), win.stride(0), int(P), int(Wc), nat.ptr(src), src.stride(0),
+                                          int(src.shape[1]), int(src.shape[0]), nat.ptr(srcmap), nat.ptr(start_min),
+                                          nat.ptr(tick), N, zs[0][0], zs[0][1], zs[1][0], zs[1][1],
+                                          nat.stream_handle(dev)), "fm_rollout_tick_scatter")
+
