@@ -25,7 +25,7 @@ from foremast_amd.brain.streaming import StreamingMonitor  # noqa: E402
 from foremast_amd.parallel.elastic import ElasticWorld  # noqa: E402
 from foremast_amd.promql.client import PromClient  # noqa: E402
 from foremast_amd.store.jobstore import SqliteJobStore  # noqa: E402
-from tests.test_node_product import T0, config, world_prometheus  # noqa: E402
+from tests.test_node_product import T0, config, scenario, world_prometheus  # noqa: E402
 
 
 class Clock:
@@ -44,7 +44,7 @@ def main():
     world = ElasticWorld(kv, f"m{me}", [f"m{i}" for i in range(n)], backend="gloo", heartbeat_timeout_s=hb,
                          collective_timeout_s=2 * hb)
     clock = Clock(T0)
-    prom = world_prometheus(clock)
+    prom = world_prometheus(clock, scenario())
     client = PromClient(transport=httpx.ASGITransport(app=prom.asgi_app()))
     cfg = config()
     store = SqliteJobStore(db)
@@ -69,8 +69,12 @@ def main():
                     return orig()
                 node._exchange = frozen
             table = await node.tick()
+            lstm = roll.joint_lstm
             f.write(json.dumps({"tick": k, "generation": world.generation, "members": world.members,
-                                "anomalous": table["anomalous_apps"], "jobs": sorted(roll.jobs)}) + "\n")
+                                "anomalous": table["anomalous_apps"], "jobs": sorted(roll.jobs),
+                                "lstm_jobs": len(lstm.jobs) if lstm is not None else 0,
+                                "lstm_steps": int(lstm.shard.trainer.steps) if lstm is not None and lstm.shard is not None else 0,
+                                "biv_rows": int((roll.biv_b >= 0).sum()) if roll.cap else 0}) + "\n")
             f.flush()
     with open(out, "w") as f:
         asyncio.run(go(f))

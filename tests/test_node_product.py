@@ -34,19 +34,40 @@ T0 = 1_700_000_040.0
 EP = "http://prometheus:9090/api/v1/"
 NS = "ns"
 METRICS = (("http_server_requests_error_5xx", "error5xx"), ("http_server_requests_latency", "latency"))
+METRICS3 = METRICS + (("http_server_requests_error_4xx", "error4xx"),)
 APPS = [f"app{i}" for i in range(12)]
 SPIKED = {"app2", "app7", "app9"}
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HELPER = os.path.join(ROOT, "tests", "helpers", "node_rank.py")
 TICKS = 13
+# the product's algorithms (docs/guides/design.md:53-92 of the reference):
+#   ma   -- moving_average_all (per metric);
+#   hw   -- Holt-Winters + pairwise ALL, the default (fit at admission on a 2-day resident history);
+#   auto -- per-metric rows + the joint models: bivariate normal of the 2-metric jobs (K8 fit at
+#           admission) and the node's shared LSTM autoencoder over the 3-metric jobs (every third
+#           app), trained data-parallel with a gradient all-reduce every tick
+SCENARIOS = ("ma", "hw", "auto")
 
 
-def config() -> BrainConfig:
+def scenario() -> str:
+    return os.environ.get("NODE_SCENARIO", "ma")
+
+
+def metrics_of(app: str, sc: str):
+    return METRICS3 if sc == "auto" and int(app[3:]) % 3 == 0 else METRICS
+
+
+def config(sc: str = None) -> BrainConfig:
+    sc = sc or scenario()
     env = reference_default_env()
-    env.update(MIN_HISTORICAL_DATA_POINT_TO_MEASURE="10", threshold0="4", threshold1="4",
-               ML_ALGORITHM="moving_average_all")
+    env.update(MIN_HISTORICAL_DATA_POINT_TO_MEASURE="10", threshold0="4", threshold1="4", threshold2="4",
+               ML_ALGORITHM={"ma": "moving_average_all", "hw": "holt_winters", "auto": "auto"}[sc])
+    if sc == "hw":
+        env.update(ML_PAIRWISE_ALGORITHM="ALL")
+    if sc == "auto":
+        env.update(ML_LSTM_THRESHOLD="50", FOREMAST_LSTM_WINDOW="8", FOREMAST_LSTM_HIDDEN="16")
     cfg = BrainConfig.from_env(env)
-    cfg.ring_len = 1440
+    cfg.ring_len = 1440 if sc == "ma" else 2880
     return cfg
 
 
@@ -54,12 +75,13 @@ def pods(app):
     return [f"{app}-v2-{k}" for k in range(2)], [f"{app}-v1-{k}" for k in range(3)]
 
 
-def world_prometheus(clock) -> FakePrometheus:
+def world_prometheus(clock, sc: str = None) -> FakePrometheus:
     """Every series a function of (app, metric, pod): identical on every rank."""
+    sc = sc or scenario()
     prom = FakePrometheus(clock=clock)
     for i, app in enumerate(APPS):
         new, old = pods(app)
-        for j, (m, _a) in enumerate(METRICS):
+        for j, (m, _a) in enumerate(metrics_of(app, sc)):
             base = 0.3 + 0.05 * i + j
             prom.add("namespace_app_per_pod:" + m, {"namespace": NS, "app": app},
                      synth.error_rate(base=base, spread=0.05, seed=100 * i + j))
@@ -71,9 +93,9 @@ def world_prometheus(clock) -> FakePrometheus:
     return prom
 
 
-def request(app):
+def request(app, sc: str = "ma"):
     mets = crd.Metrics(data_source_type="prometheus", endpoint=EP,
-                       monitoring=[crd.Monitoring(metric_name=m, metric_alias=a) for m, a in METRICS])
+                       monitoring=[crd.Monitoring(metric_name=m, metric_alias=a) for m, a in metrics_of(app, sc)])
     info = queries.create_metrics_info(NS, app, list(pods(app)), mets, 10, "canary", now=T0)
     return r.ApplicationHealthAnalyzeRequest(app_name=app, start_time=format_rfc3339(T0),
                                              end_time=format_rfc3339(T0 + 600), metrics=info,
@@ -85,28 +107,29 @@ class _RendezvousFlake(Exception):
     8-CPU host): not the code under test; the run is repeated on a fresh store."""
 
 
-def run_node(tmp_path, n, stop=None, hb=3.0):
+def run_node(tmp_path, n, stop=None, hb=3.0, sc="ma"):
     """Register the jobs, run n ranks for TICKS ticks; returns (statuses, per-rank lines)."""
     for attempt in range(3):
         try:
-            return _run_node(tmp_path, n, stop, hb, attempt)
+            return _run_node(tmp_path, n, stop, hb, attempt, sc)
         except _RendezvousFlake:
             if attempt == 2:
                 raise
 
 
-def _run_node(tmp_path, n, stop, hb, attempt):
+def _run_node(tmp_path, n, stop, hb, attempt, sc):
     import torch.distributed as dist
     from foremast_amd.service import app as svc
     from foremast_amd.store.jobstore import SqliteJobStore
-    db = str(tmp_path / f"jobs{n}_{attempt}.db")
+    db = str(tmp_path / f"jobs{sc}{n}_{attempt}{'_stop' if stop else ''}.db")
     store = SqliteJobStore(db)
-    ids = {a: svc.register(store, request(a))[1]["jobId"] for a in APPS}
+    ids = {a: svc.register(store, request(a, sc))[1]["jobId"] for a in APPS}
     kv = dist.TCPStore("127.0.0.1", 0, is_master=True, wait_for_workers=False, timeout=datetime.timedelta(seconds=90))
     procs, outs = [], []
     for i in range(n):
-        out = tmp_path / f"n{n}_{attempt}_rank{i}.jsonl"
-        env = dict(os.environ, OMP_NUM_THREADS="1", CUDA_VISIBLE_DEVICES="", GLOO_SOCKET_IFNAME="lo")
+        out = tmp_path / f"{sc}_n{n}_{attempt}{'_stop' if stop else ''}_rank{i}.jsonl"
+        env = dict(os.environ, OMP_NUM_THREADS="1", CUDA_VISIBLE_DEVICES="", GLOO_SOCKET_IFNAME="lo",
+                   NODE_SCENARIO=sc, FOREMAST_LSTM_PRETRAIN="10", FOREMAST_LSTM_PRETRAIN_PER_TICK="10")
         if stop is not None and i == stop[0]:
             env["NODE_RANK_STOP_AT"] = str(stop[1])
         procs.append(subprocess.Popen([sys.executable, HELPER, str(kv.port), str(i), str(n), db, str(out),
@@ -155,18 +178,23 @@ def verdicts(docs):
 
 
 @pytest.mark.slow
-def test_node_product_n_rank_equals_one_rank(tmp_path):
-    ref_docs, ref_lines = run_node(tmp_path, 1)
+@pytest.mark.parametrize("sc", SCENARIOS)
+def test_node_product_n_rank_equals_one_rank(tmp_path, sc):
+    ref_docs, ref_lines = run_node(tmp_path, 1, sc=sc)
     ref = verdicts(ref_docs)
     assert {a for a, (st, _) in ref.items() if st == r.ST_COMPLETED_UNHEALTH} == SPIKED
     assert all(st == r.ST_COMPLETED_HEALTH for a, (st, _) in ref.items() if a not in SPIKED)
     ref_anom = [sorted(x["anomalous"]) for x in ref_lines[0]]
-    for n in (2, 4, 8):
-        docs, lines = run_node(tmp_path, n)
+    for n in ((2, 4, 8) if sc == "ma" else (2, 4)):
+        docs, lines = run_node(tmp_path, n, sc=sc)
         assert verdicts(docs) == ref, n
         # the node table names the same anomalous apps on every tick, on every rank
         for rank_lines in lines:
             assert [sorted(x["anomalous"]) for x in rank_lines] == ref_anom, n
+        if sc == "auto":  # the joint models really ran on the ranks: bivariate rows, LSTM entities
+            assert max(x["biv_rows"] for ls in lines for x in ls) > 0, n
+            assert max(x["lstm_jobs"] for ls in lines for x in ls) > 0, n
+            assert min(ls[-1]["lstm_steps"] for ls in lines) > 0, n   # DP steps (all-reduce) on every rank
         # every job was held by exactly one rank
         for k in range(TICKS):
             held = [j for ls in lines for j in ls[k]["jobs"]]
@@ -174,9 +202,10 @@ def test_node_product_n_rank_equals_one_rank(tmp_path):
 
 
 @pytest.mark.slow
-def test_node_product_rank_killed_mid_tick_survivors_finish(tmp_path):
-    ref = verdicts(run_node(tmp_path, 1)[0])
-    docs, lines = run_node(tmp_path, 3, stop=(1, 4))
+@pytest.mark.parametrize("sc", ("ma", "auto"))
+def test_node_product_rank_killed_mid_tick_survivors_finish(tmp_path, sc):
+    ref = verdicts(run_node(tmp_path, 1, sc=sc)[0])
+    docs, lines = run_node(tmp_path, 3, stop=(1, 4), sc=sc)
     got = verdicts(docs)
     assert got == ref
     survivors = [ls for i, ls in enumerate(lines) if i != 1]
