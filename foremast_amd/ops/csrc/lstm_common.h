@@ -117,6 +117,26 @@ __device__ __forceinline__ unsigned pack_fp8x4(float a, float b, float c, float 
   return (unsigned)v;
 }
 
+// ---- CDNA4 block-scaled fp8: v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3 A and B) ----------
+// lane l holds row (A) / column (B) l & 31 and k = 32 (l >> 5) + j in byte j of its 8-VGPR
+// fragment; each lane's 32-element k block has ONE E8M0 scale (2^(s - 127)) per operand.
+typedef int f8x32 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f8x32 pack_fp8x32(const float (&v)[32]) {
+  f8x32 r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r[i] = (int)pack_fp8x4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+  return r;
+}
+
+// SEL: which byte of the two scale registers holds this MFMA's E8M0 scales (op_sel), so one
+// VGPR carries the scales of four k blocks
+template <int SEL>
+__device__ __forceinline__ f32x16 mfma_scaled(const f8x32& a, const f8x32& b, f32x16 c, int scale_a, int scale_b) {
+  // format codes 0 / 0: e4m3 (OCP fp8) for A and B
+  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, SEL, scale_a, SEL, scale_b);
+}
+
 template <bool FP8>
 struct Frag {
   // bf16: 8 x bf16 = uint4; fp8: 8 x fp8 = uint2

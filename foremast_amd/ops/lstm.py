@@ -88,6 +88,8 @@ nat.register("fm_lstm_ae", [C.POINTER(LstmArgs), C.c_void_p])
 nat.register("fm_lstm_lds_bytes", [C.c_int, C.c_int], C.c_size_t)
 nat.register("fm_lstm_args_size", [], C.c_longlong)
 nat.register("fm_fp8_convert", [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p])
+nat.register("fm_mfma_scale_probe", [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                     C.c_void_p])
 
 
 def gate_row_perm() -> torch.Tensor:
@@ -386,3 +388,20 @@ def device_fp8(values: torch.Tensor) -> torch.Tensor:
     nat.check(lib.fm_fp8_convert(v.data_ptr(), out.data_ptr(), v.numel(), nat.stream_handle(v.device)),
               "fm_fp8_convert")
     return out
+
+
+def mfma_scale_probe(A: torch.Tensor, B: torch.Tensor, sa: torch.Tensor, sb: torch.Tensor, sel: int = 0) -> torch.Tensor:
+    """``D = (A 2^(sa-127)) (B 2^(sb-127))`` through ONE ``v_mfma_scale_f32_32x32x64_f8f6f4``
+    with the lane map the fp8 LSTM kernels use (``A [32, 64]``, ``B [64, 32]`` float32
+    converted to e4m3 on the device; ``sa [32, 2]`` / ``sb [32, 2]`` uint8 E8M0 scales of
+    row / column r and k block h, passed in byte ``sel`` of the scale registers)."""
+    lib = nat.require()
+    _need(A.shape == (32, 64) and B.shape == (64, 32) and sa.shape == (32, 2) and sb.shape == (32, 2),
+          "probe shapes: A [32, 64], B [64, 32], scales [32, 2]")
+    A, B = A.float().contiguous(), B.float().contiguous()
+    sa, sb = sa.to(torch.uint8).contiguous(), sb.to(torch.uint8).contiguous()
+    _need(A.is_cuda and all(t.device == A.device for t in (B, sa, sb)), "probe tensors on one GPU")
+    D = torch.empty((32, 32), dtype=torch.float32, device=A.device)
+    nat.check(lib.fm_mfma_scale_probe(A.data_ptr(), B.data_ptr(), sa.data_ptr(), sb.data_ptr(), D.data_ptr(),
+                                      int(sel), nat.stream_handle(A.device)), "fm_mfma_scale_probe")
+    return D

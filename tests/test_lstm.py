@@ -500,3 +500,25 @@ def test_lstm_level_kernel_matches_cpu():
     shard.gpu = True
     torch.testing.assert_close(zl.cpu(), zref.cpu(), rtol=1e-4, atol=1e-4)
     assert bool((zl.abs().amax(1)[shifted] > 5.5).all())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sel", [0, 1, 2, 3])
+def test_block_scaled_fp8_mfma_lane_map(sel):
+    """The CDNA4 block-scaled MFMA (v_mfma_scale_f32_32x32x64_f8f6f4, e4m3) under the lane
+    map and scale bytes the fp8 LSTM kernel assumes, on exact data: small integers (exact
+    in e4m3) and a different power-of-two scale per (row, k block) of A and (column,
+    k block) of B; asymmetric so a transposed map cannot pass."""
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(7 + sel)
+    A = torch.randint(-8, 9, (32, 64), generator=g).float()
+    B = torch.randint(-8, 9, (64, 32), generator=g).float()
+    A[3, :] += torch.arange(64) % 5           # asymmetric rows / columns
+    B[:, 5] += torch.arange(64) % 3
+    sa = torch.randint(120, 135, (32, 2), generator=g).to(torch.uint8)
+    sb = torch.randint(120, 135, (32, 2), generator=g).to(torch.uint8)
+    got = L.mfma_scale_probe(A.to(dev), B.to(dev), sa.to(dev), sb.to(dev), sel).cpu().double()
+    fa = torch.exp2(sa.double() - 127).repeat_interleave(32, dim=1)          # [32, 64]
+    fb = torch.exp2(sb.double() - 127).repeat_interleave(32, dim=1).t()      # [64, 32]
+    want = (A.double() * fa) @ (B.double() * fb)
+    torch.testing.assert_close(got, want, rtol=1e-6, atol=1e-6)
