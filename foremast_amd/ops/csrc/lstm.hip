@@ -1,4 +1,5 @@
-// K6: fused LSTM-autoencoder inference on MFMA (bf16, or fp8 e4m3 OCP).
+// K6: fused LSTM-autoencoder inference on MFMA (bf16, or fp8 e4m3 OCP on the CDNA4
+// block-scaled v_mfma_scale_f32_32x32x64_f8f6f4).
 //
 // Semantics: foremast_amd/models/lstm_ae.py (encoder LSTM(F→H), decoder with
 // zero input starting from the encoder's final (h, c), linear read-out,
@@ -6,9 +7,11 @@
 //
 // Layout (one 64-lane wave = 32 series, a workgroup = 4 waves = 128 series):
 //  * gates^T [256 x 32] = Waug^T [256 x 80] · [h; x_t; 1] [80 x 32] on
-//    v_mfma_f32_32x32x16 (8 row tiles x 5 k-steps = 40 MFMAs per step).  The
-//    input projection and bias ride in the 5th k-step (x at k=64..64+F-1,
-//    bias at k=71), so no VALU matmul is needed for them.
+//    v_mfma_f32_32x32x16_bf16 (8 row tiles x 5 k-steps = 40 MFMAs per step), or in
+//    fp8 on v_mfma_scale_f32_32x32x64_f8f6f4 (8 row tiles x 2 k-steps of K = 64 =
+//    16 MFMAs per step, an E8M0 scale per (gate row, 32-element k block) of the
+//    weights).  The input projection and bias ride in the last k-step (x at
+//    k=64..64+F-1, bias at k=71), so no VALU matmul is needed for them.
 //  * The 256 gate rows are permuted host-side so that in tile t, accumulator
 //    register 4*gate+q of lane half hh holds gate `gate` of hidden unit
 //    u = 16(t>>1) + 8hh + 4(t&1) + q: each lane has i,f,g,o of its units
@@ -27,14 +30,11 @@ struct LstmArgs {
   int N;
   int T;
   int F;                   // 1..7
-  int fp8;                 // 0 bf16, 1 fp8 e4m3
-  const void* w_enc;       // packed A fragments [8][5][64][8] (bf16 or fp8)
+  int fp8;                 // 0 bf16, 1 fp8 e4m3 (CDNA4 block-scaled MFMA)
+  const void* w_enc;       // packed A fragments: bf16 [8][5][64][8]; fp8 [8][2][64][32] e4m3 + [64][16] E8M0
   const void* w_dec;
   const float* w_out;      // [F][64]
   const float* b_out;      // [F]
-  float scale_w_enc;       // fp8 dequant scales (1 for bf16)
-  float scale_w_dec;
-  float scale_act;         // fp8 activation scale for h / x (1 for bf16)
   float mu;                // calibration
   float sigma;
   const float* threshold;  // [N] or null (→ thr_default)
@@ -45,7 +45,6 @@ struct LstmArgs {
   float* recon;            // [N, T, F] or null
   const int* app_id;       // [N] or null
   int* app_stats;          // [A, 2] or null
-  const float* wmax;       // fp8: device absmax [enc, dec] of the packed weights (overrides scale_w_*) or null
   LstmRingSrc src;         // ring-direct input (x == null)
   float* cal;              // [N, 2] per-series (mu, 1/sigma) of the reconstruction error, or null (global only)
   float cal_ewma;          // > 0: mu_i tracks healthy errors, mu_i += cal_ewma * (err - mu_i) when verdict 0
@@ -90,75 +89,126 @@ namespace {
 
 using namespace fm_lstm;
 
+// Cell update of two gate tiles (lane-local): unit (tt, q) <-> acc[4*gate + q]; packed-FP32
+// activation arithmetic, two units per step.
+__device__ __forceinline__ void cell_update(const f32x16& acc0, const f32x16& acc1, int tp, float deq,
+                                            float (&hreg)[32], float (&creg)[32]) {
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const f32x16& acc = e ? acc1 : acc0;
+#pragma unroll
+    for (int q = 0; q < 4; q += 2) {
+      const f32x2_t gi = (f32x2_t){acc[q], acc[q + 1]} * deq, gf = (f32x2_t){acc[4 + q], acc[5 + q]} * deq;
+      const f32x2_t gg = (f32x2_t){acc[8 + q], acc[9 + q]} * deq;
+      const f32x2_t go = (f32x2_t){acc[12 + q], acc[13 + q]} * deq;
+      const int u = (tp + e) * 4 + q;
+      const f32x2_t c = sigm2(gf) * (f32x2_t){creg[u], creg[u + 1]} + sigm2(gi) * tanh2(gg);
+      creg[u] = c.x;
+      creg[u + 1] = c.y;
+      const f32x2_t h = sigm2(go) * tanh2(c);
+      hreg[u] = h.x;
+      hreg[u + 1] = h.y;
+    }
+  }
+}
+
+// E8M0 scale register (4 scale bytes) and op_sel byte of fp8 fragment (tile, k-step)
+template <int TS>
+__device__ __forceinline__ f32x16 mfma_fp8(const f8x32& a, const f8x32& b, f32x16 c, const int4& sc, int scale_b) {
+  const int sreg = (TS >> 2) == 0 ? sc.x : (TS >> 2) == 1 ? sc.y : (TS >> 2) == 2 ? sc.z : sc.w;
+  return mfma_scaled<TS & 3>(a, b, c, sreg, scale_b);
+}
+
+template <int TP>
+__device__ __forceinline__ void gates_fp8(const f8x32* wl, int lo, const f8x32& hb, const f8x32& xb, const int4& sc,
+                                          f32x16& acc0, f32x16& acc1) {
+  acc0 = mfma_fp8<(TP * KSTEPS_FP8)>(wl[(TP * KSTEPS_FP8) * 64 + lo], hb, (f32x16){}, sc, SCALE_H);
+  acc1 = mfma_fp8<((TP + 1) * KSTEPS_FP8)>(wl[((TP + 1) * KSTEPS_FP8) * 64 + lo], hb, (f32x16){}, sc, SCALE_H);
+  acc0 = mfma_fp8<(TP * KSTEPS_FP8 + 1)>(wl[(TP * KSTEPS_FP8 + 1) * 64 + lo], xb, acc0, sc, SCALE_ONE);
+  acc1 = mfma_fp8<((TP + 1) * KSTEPS_FP8 + 1)>(wl[((TP + 1) * KSTEPS_FP8 + 1) * 64 + lo], xb, acc1, sc, SCALE_ONE);
+}
+
 // One LSTM recurrence over T steps for this wave's 32 series.
-// ENC: input x_t at k=64..64+F-1; DEC: zero input, read-out + error.
+// ENC: input x_t (and the bias) in the last k-step; DEC: zero input, read-out + error.
+// bf16: v_mfma_f32_32x32x16_bf16, 5 k-steps (h: 4, input + bias: 1).  fp8: CDNA4
+// v_mfma_scale_f32_32x32x64_f8f6f4 on e4m3 with per-(row, 32-k block) E8M0 weight scales
+// (ops/lstm.py pack_fp8), 2 k-steps: the lane's 32 hidden units, then input + bias.
 template <bool FP8, bool ENC>
-__device__ __forceinline__ void run_phase(const LstmArgs& a, const typename Frag<FP8>::T* wlds,
-                                          const float* wout_lds, long long series, bool valid, int hh,
-                                          float (&hreg)[32], float (&creg)[32], float& errsum) {
-  using FT = typename Frag<FP8>::T;
-  const float sw = a.wmax ? fp8_scale(a.wmax[ENC ? 0 : 1]) : (ENC ? a.scale_w_enc : a.scale_w_dec);
-  // bf16: unit scales by construction (ops/lstm.py pack), so the compiler drops the multiplies
-  const float sa = FP8 ? a.scale_act : 1.f;
-  const float deq = FP8 ? sw * sa : 1.f;  // acc → real gates
+__device__ __forceinline__ void run_phase(const LstmArgs& a, const void* wlds_v, const float* wout_lds,
+                                          long long series, bool valid, int hh, float (&hreg)[32],
+                                          float (&creg)[32], float& errsum) {
   const int lane = lane_id();
   const XPos xp = make_xpos(a.x, a.src, valid ? series : 0, a.T, a.F);  // tail lanes never index past N
+  int4 sc = make_int4(0, 0, 0, 0);
+  if constexpr (FP8) sc = ((const int4*)((const char*)wlds_v + FRAG_BYTES_FP8))[lane];
   for (int t = 0; t < a.T; ++t) {
-    // B fragments: h (4 k-steps) and the input/bias k-step
-    FT hb[4];
+    // the A fragments stay in LDS: an opaque lane offset per step stops the compiler hoisting
+    // them (bf16: 40 fragments = 160 VGPRs; fp8: 16 x 8 = 128) out of the time loop
+    int lo = lane;
+    asm volatile("" : "+v"(lo));
+    if constexpr (FP8) {
+      const f8x32* wl = (const f8x32*)wlds_v;
+      constexpr float HS = (float)(1 << ACT_SHIFT);
+      f8x32 hb;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = hreg[(2 * s + (j >> 2)) * 4 + (j & 3)] * (1.f / sa);
-      hb[s] = make_b<FP8>(v);
-    }
-    FT xb;
-    {
-      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < 8; ++i)
+        hb[i] = (int)pack_fp8x4(hreg[4 * i] * HS, hreg[4 * i + 1] * HS, hreg[4 * i + 2] * HS, hreg[4 * i + 3] * HS);
+      // input + bias k-step: lane half 0, bytes 0..F-1 and 7; everything else zero
+      f8x32 xb = (f8x32){0, 0, 0, 0, 0, 0, 0, 0};
       if (hh == 0) {
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 1.f};
         if (ENC && valid) {
 #pragma unroll
           for (int f = 0; f < 7; ++f)
-            if (f < a.F) v[f] = sat_input<FP8>(load_x(a.src, xp, t, f, a.F) * (1.f / sa));
+            if (f < a.F) v[f] = sat_fp8(load_x(a.src, xp, t, f, a.F));
         }
-        v[7] = 1.f / sa;
+        xb[0] = (int)pack_fp8x4(v[0], v[1], v[2], v[3]);
+        xb[1] = (int)pack_fp8x4(v[4], v[5], v[6], v[7]);
       }
-      xb = make_b<FP8>(v);
-    }
-    // tiles in pairs: two independent accumulator chains, 32 accumulator regs live.
-    // bf16: keep the A fragments in LDS (an opaque lane offset per step stops the
-    // compiler hoisting all 40 fragments = 160 VGPRs out of the time loop);
-    // fp8 fragments (80 VGPRs) may stay register-resident.
-    int lo = lane;
-    if constexpr (!FP8) asm volatile("" : "+v"(lo));
+      f32x16 acc0, acc1;
+      gates_fp8<0>(wl, lo, hb, xb, sc, acc0, acc1);
+      cell_update(acc0, acc1, 0, 1.f, hreg, creg);
+      gates_fp8<2>(wl, lo, hb, xb, sc, acc0, acc1);
+      cell_update(acc0, acc1, 2, 1.f, hreg, creg);
+      gates_fp8<4>(wl, lo, hb, xb, sc, acc0, acc1);
+      cell_update(acc0, acc1, 4, 1.f, hreg, creg);
+      gates_fp8<6>(wl, lo, hb, xb, sc, acc0, acc1);
+      cell_update(acc0, acc1, 6, 1.f, hreg, creg);
+    } else {
+      const FragBF16* wlds = (const FragBF16*)wlds_v;
+      // B fragments: h (4 k-steps) and the input/bias k-step
+      FragBF16 hb[4];
 #pragma unroll
-    for (int tp = 0; tp < TILES; tp += 2) {
-      f32x16 acc0 = (f32x16){}, acc1 = (f32x16){};
+      for (int s = 0; s < 4; ++s) {
+        float v[8];
 #pragma unroll
-      for (int s = 0; s < KSTEPS; ++s) {
-        const FT bfr = (s < 4) ? hb[s] : xb;
-        acc0 = mfma<FP8>(wlds[(tp * KSTEPS + s) * 64 + lo], bfr, acc0);
-        acc1 = mfma<FP8>(wlds[((tp + 1) * KSTEPS + s) * 64 + lo], bfr, acc1);
+        for (int j = 0; j < 8; ++j) v[j] = hreg[(2 * s + (j >> 2)) * 4 + (j & 3)];
+        hb[s] = make_b_bf16(v);
       }
-      // cell update (lane-local): unit (tt, q) <-> acc[4*gate + q]
+      FragBF16 xb;
+      {
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (hh == 0) {
+          if (ENC && valid) {
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const f32x16& acc = e ? acc1 : acc0;
-        // two units per step of the loop: packed-FP32 activation arithmetic
-#pragma unroll
-        for (int q = 0; q < 4; q += 2) {
-          const f32x2_t gi = (f32x2_t){acc[q], acc[q + 1]} * deq, gf = (f32x2_t){acc[4 + q], acc[5 + q]} * deq;
-          const f32x2_t gg = (f32x2_t){acc[8 + q], acc[9 + q]} * deq;
-          const f32x2_t go = (f32x2_t){acc[12 + q], acc[13 + q]} * deq;
-          const int u = (tp + e) * 4 + q;
-          const f32x2_t c = sigm2(gf) * (f32x2_t){creg[u], creg[u + 1]} + sigm2(gi) * tanh2(gg);
-          creg[u] = c.x;
-          creg[u + 1] = c.y;
-          const f32x2_t h = sigm2(go) * tanh2(c);
-          hreg[u] = h.x;
-          hreg[u + 1] = h.y;
+            for (int f = 0; f < 7; ++f)
+              if (f < a.F) v[f] = load_x(a.src, xp, t, f, a.F);
+          }
+          v[7] = 1.f;
         }
+        xb = make_b_bf16(v);
+      }
+      // tiles in pairs: two independent accumulator chains, 32 accumulator regs live
+#pragma unroll
+      for (int tp = 0; tp < TILES; tp += 2) {
+        f32x16 acc0 = (f32x16){}, acc1 = (f32x16){};
+#pragma unroll
+        for (int s = 0; s < KSTEPS; ++s) {
+          const FragBF16 bfr = (s < 4) ? hb[s] : xb;
+          acc0 = mfma_bf16(wlds[(tp * KSTEPS + s) * 64 + lo], bfr, acc0);
+          acc1 = mfma_bf16(wlds[((tp + 1) * KSTEPS + s) * 64 + lo], bfr, acc1);
+        }
+        cell_update(acc0, acc1, tp, 1.f, hreg, creg);
       }
     }
     if (!ENC) {
@@ -188,17 +238,15 @@ __device__ __forceinline__ void run_phase(const LstmArgs& a, const typename Frag
 
 template <bool FP8>
 __global__ __launch_bounds__(256, 2) void lstm_ae_kernel(const LstmArgs a) {
-  using FT = typename Frag<FP8>::T;
   const int w = wave_id(), lane = lane_id();
   const int hh = lane >> 5;
   const long long series = ((long long)blockIdx.x * 4 + w) * 32 + (lane & 31);
   const bool valid = series < a.N;
   const long long sidx = valid ? series : 0;
-  constexpr int FB = FP8 ? FRAG_BYTES_FP8 : FRAG_BYTES_BF16;
-  FT* wlds = (FT*)fm_lstm_smem;
+  constexpr int FB = FP8 ? FRAG_BYTES_FP8 + SCALE_BYTES_FP8 : FRAG_BYTES_BF16;
   float* wout = (float*)(fm_lstm_smem + FB);
 
-  // stage encoder weights + read-out
+  // stage encoder weights (+ fp8 scales) + read-out
   {
     const uint4* src = (const uint4*)a.w_enc;
     uint4* dst = (uint4*)fm_lstm_smem;
@@ -210,7 +258,7 @@ __global__ __launch_bounds__(256, 2) void lstm_ae_kernel(const LstmArgs a) {
 #pragma unroll
   for (int i = 0; i < 32; ++i) { hreg[i] = 0.f; creg[i] = 0.f; }
   float errsum = 0.f;
-  run_phase<FP8, true>(a, wlds, wout, sidx, valid, hh, hreg, creg, errsum);
+  run_phase<FP8, true>(a, fm_lstm_smem, wout, sidx, valid, hh, hreg, creg, errsum);
   __syncthreads();
   {
     const uint4* src = (const uint4*)a.w_dec;
@@ -218,7 +266,7 @@ __global__ __launch_bounds__(256, 2) void lstm_ae_kernel(const LstmArgs a) {
     for (int i = threadIdx.x; i < FB / 16; i += blockDim.x) dst[i] = src[i];
   }
   __syncthreads();
-  run_phase<FP8, false>(a, wlds, wout, sidx, valid, hh, hreg, creg, errsum);
+  run_phase<FP8, false>(a, fm_lstm_smem, wout, sidx, valid, hh, hreg, creg, errsum);
   if (valid && hh == 0) {
     const float err = errsum / (float)(a.T * a.F);
     a.err[series] = err;
@@ -333,7 +381,7 @@ extern "C" int fm_lstm_level(const LevelArgs* a, hipStream_t st) {
 extern "C" long long fm_lstm_level_args_size() { return (long long)sizeof(LevelArgs); }
 
 extern "C" size_t fm_lstm_lds_bytes(int F, int fp8) {
-  return (size_t)(fp8 ? FRAG_BYTES_FP8 : FRAG_BYTES_BF16) + (size_t)F * H * 4;
+  return (size_t)(fp8 ? FRAG_BYTES_FP8 + SCALE_BYTES_FP8 : FRAG_BYTES_BF16) + (size_t)F * H * 4;
 }
 
 extern "C" int fm_lstm_ae(const LstmArgs* a, hipStream_t st) {

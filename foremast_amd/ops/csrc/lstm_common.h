@@ -1,6 +1,7 @@
 // Shared device pieces of the fused LSTM-AE kernels (inference: lstm.hip,
 // training: lstm_train.hip): MFMA operand types, activation functions and
-// B-fragment packing for v_mfma_f32_32x32x16_{bf16,fp8}.
+// B-fragment packing for v_mfma_f32_32x32x16_bf16 and the CDNA4 block-scaled
+// v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3).
 #pragma once
 
 #include "common.h"
@@ -57,14 +58,23 @@ __device__ __forceinline__ float load_x(const LstmRingSrc& s, const XPos& p, int
   const float v = s.bf16 ? bf16_to_f32(((const bf16_t*)s.ring[f])[o]) : ((const float*)s.ring[f])[o];
   return (v - s.mean[p.row * F + f]) * s.rstd[p.row * F + f];
 }
-// dequantisation scale of a pack.hip fp8 segment with absolute maximum m
-__device__ __forceinline__ float fp8_scale(float m) { return m > 0.f ? m * (1.f / 448.f) : 1.f; }
 
 constexpr int H = 64;
 constexpr int TILES = 8;
 constexpr int KSTEPS = 5;
 constexpr int FRAG_BYTES_BF16 = TILES * KSTEPS * 64 * 16;  // 40 KB
-constexpr int FRAG_BYTES_FP8 = TILES * KSTEPS * 64 * 8;    // 20 KB
+// fp8: CDNA4 block-scaled MFMA, K = 64 per instruction: k-step 0 holds the 64 hidden units
+// (each lane half's 32 units in its h-register order), k-step 1 the input and the bias (lane
+// half 0, bytes 0..F-1 and 7), so 2 MFMAs per gate tile instead of 5
+constexpr int KSTEPS_FP8 = 2;
+constexpr int FRAG_BYTES_FP8 = TILES * KSTEPS_FP8 * 64 * 32;    // 32 KB of e4m3
+constexpr int SCALE_BYTES_FP8 = TILES * KSTEPS_FP8 * 64;        // E8M0 per (tile, k-step, lane): [lane][16]
+// h enters the B operand as h * 2^8 (|h| <= 1: e4m3 normals reach down to |h| = 2^-14), scaled
+// back by the MFMA (E8M0 127 - 8); inputs and bias enter unscaled (127).  Replicated in all
+// four bytes: any op_sel byte reads it.
+constexpr int ACT_SHIFT = 8;
+constexpr int SCALE_H = 0x77777777;   // 119 = 127 - ACT_SHIFT
+constexpr int SCALE_ONE = 0x7f7f7f7f;
 
 // v_exp_f32 (2^x) + v_rcp_f32 (1 ulp): two transcendental issues per
 // activation.  (__frcp_rn / '/' lower to the ~10-instruction IEEE division
@@ -137,49 +147,28 @@ __device__ __forceinline__ f32x16 mfma_scaled(const f8x32& a, const f8x32& b, f3
   return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, SEL, scale_a, SEL, scale_b);
 }
 
-template <bool FP8>
-struct Frag {
-  // bf16: 8 x bf16 = uint4; fp8: 8 x fp8 = uint2
-  typedef typename std::conditional<FP8, uint2, uint4>::type T;
-};
+// bf16 A / B fragment of v_mfma_f32_32x32x16_bf16: 8 x bf16 = uint4
+typedef uint4 FragBF16;
 
-template <bool FP8>
-__device__ __forceinline__ f32x16 mfma(const typename Frag<FP8>::T& a, const typename Frag<FP8>::T& b, f32x16 c) {
-  if constexpr (FP8) {
-    long av, bv;
-    __builtin_memcpy(&av, &a, 8);
-    __builtin_memcpy(&bv, &b, 8);
-    return __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(av, bv, c, 0, 0, 0);
-  } else {
-    bf16x8_t av, bv;
-    __builtin_memcpy(&av, &a, 16);
-    __builtin_memcpy(&bv, &b, 16);
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, c, 0, 0, 0);
-  }
+__device__ __forceinline__ f32x16 mfma_bf16(const FragBF16& a, const FragBF16& b, f32x16 c) {
+  bf16x8_t av, bv;
+  __builtin_memcpy(&av, &a, 16);
+  __builtin_memcpy(&bv, &b, 16);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, c, 0, 0, 0);
 }
 
-// Model inputs enter the fp8 B operand saturated to the e4m3 range (±448):
-// the conversion would turn an out-of-range z-score — a regressed series,
-// the very thing being detected — into NaN.  bf16 covers the fp32 range.
-template <bool FP8>
-__device__ __forceinline__ float sat_input(float v) {
-  if constexpr (FP8) return fminf(fmaxf(v, -448.f), 448.f);
-  return v;
-}
+// Model inputs enter the fp8 B operand saturated to the e4m3 range (+-448):
+// the conversion would turn an out-of-range z-score -- a regressed series,
+// the very thing being detected -- into NaN.  bf16 covers the fp32 range.
+__device__ __forceinline__ float sat_fp8(float v) { return fminf(fmaxf(v, -448.f), 448.f); }
 
-// Build the B fragment for a k-step from 8 fp32 values (already scaled).
-template <bool FP8>
-__device__ __forceinline__ typename Frag<FP8>::T make_b(const float (&v)[8]) {
-  typename Frag<FP8>::T r;
-  if constexpr (FP8) {
-    r.x = pack_fp8x4(v[0], v[1], v[2], v[3]);
-    r.y = pack_fp8x4(v[4], v[5], v[6], v[7]);
-  } else {
-    r.x = pack_bf16x2(v[0], v[1]);
-    r.y = pack_bf16x2(v[2], v[3]);
-    r.z = pack_bf16x2(v[4], v[5]);
-    r.w = pack_bf16x2(v[6], v[7]);
-  }
+// Build the bf16 B fragment for a k-step from 8 fp32 values.
+__device__ __forceinline__ FragBF16 make_b_bf16(const float (&v)[8]) {
+  FragBF16 r;
+  r.x = pack_bf16x2(v[0], v[1]);
+  r.y = pack_bf16x2(v[2], v[3]);
+  r.z = pack_bf16x2(v[4], v[5]);
+  r.w = pack_bf16x2(v[6], v[7]);
   return r;
 }
 

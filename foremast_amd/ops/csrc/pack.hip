@@ -11,10 +11,12 @@
 // The codes are built once on the host (foremast_amd/ops/pack.py) from the
 // same index maps the PyTorch reference layouts use.
 //
-// fp8 (OCP e4m3) segments are scaled per segment by 448 / absmax: pass 0
-// (which also writes every non-fp8 segment) reduces absmax with one atomic
-// per wave, pass 1 quantises.  Consumers recompute the scale from the same
-// absmax on the device (fp8_scale in lstm_common.h): no host round trip.
+// fp8 (OCP e4m3) segments are block-scaled for the CDNA4 block-scaled MFMA: every
+// 32 consecutive codes (one lane's k block of an A fragment) share the E8M0
+// exponent e = the smallest integer with absmax <= 448 * 2^e (exact, from frexp);
+// the codes are v * 2^-e in e4m3 and the scale bytes (e + 127) follow the codes,
+// lane-major (block b at n + (b % 64) * (n / 2048) + b / 64), so a kernel lane
+// reads its scales as one vector.  One pass: a block is a half wave.
 #include "common.h"
 
 struct PackSeg {
@@ -29,8 +31,7 @@ struct PackArgs {
   const float* src[8];
   PackSeg seg[8];
   int nseg;
-  int pass;
-  float* absmax;  // [8] per segment (fp8 only)
+  int _pad;
 };
 
 namespace {
@@ -41,30 +42,40 @@ __device__ __forceinline__ float fetch(const PackArgs& a, const PackSeg& s, int 
   return a.src[(c >> 26) & 7][c & 0xffffff] * s.mul[(c >> 24) & 3];
 }
 
+// E8M0 exponent of a block with absolute maximum m (m = f 2^x, f in [0.5, 1); 448 = 0.875 2^9)
+__device__ __forceinline__ int e8m0_exp(float m) {
+  if (!(m > 0.f)) return 0;
+  int x;
+  const float f = frexpf(m, &x);
+  const int e = x - 9 + (f > 0.875f ? 1 : 0);
+  return e < -127 ? -127 : (e > 127 ? 127 : e);
+}
+
 __global__ __launch_bounds__(256) void pack_kernel(const PackArgs a) {
   const PackSeg& s = a.seg[blockIdx.y];
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (a.pass == 0) {
-    if (s.kind == 2) {
-      const float v = i < s.n ? fabsf(fetch(a, s, i)) : 0.f;
-      const float m = wave_max(v);
-      if (lane_id() == 0 && m > 0.f)  // non-negative floats order like their bits
-        atomicMax((unsigned*)&a.absmax[blockIdx.y], __float_as_uint(m));
-      return;
-    }
+  if (s.kind == 2) {  // block-scaled fp8: 32-lane halves of the wave are blocks (n % 2048 == 0)
+    const float v = i < s.n ? fetch(a, s, i) : 0.f;
+    float m = fabsf(v);
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, FM_WAVE));
+    const int e = e8m0_exp(m);
     if (i >= s.n) return;
-    const float v = fetch(a, s, i);
-    if (s.kind == 0)
-      ((float*)s.out)[i] = v;
-    else
-      ((bf16_t*)s.out)[i] = f32_to_bf16(v);
+    const int q = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v, -e), 0.f, 0, false);
+    unsigned char* out = (unsigned char*)s.out;
+    out[i] = (unsigned char)(q & 0xff);
+    if ((i & 31) == 0) {
+      const int b = i >> 5, per_lane = s.n >> 11;
+      out[s.n + (b & 63) * per_lane + (b >> 6)] = (unsigned char)(e + 127);
+    }
     return;
   }
-  if (s.kind != 2 || i >= s.n) return;
-  const float m = a.absmax[blockIdx.y];
-  const float inv = m > 0.f ? 448.f / m : 1.f;
-  const int q = __builtin_amdgcn_cvt_pk_fp8_f32(fetch(a, s, i) * inv, 0.f, 0, false);
-  ((unsigned char*)s.out)[i] = (unsigned char)(q & 0xff);
+  if (i >= s.n) return;
+  const float v = fetch(a, s, i);
+  if (s.kind == 0)
+    ((float*)s.out)[i] = v;
+  else
+    ((bf16_t*)s.out)[i] = f32_to_bf16(v);
 }
 
 }  // namespace
@@ -72,25 +83,13 @@ __global__ __launch_bounds__(256) void pack_kernel(const PackArgs a) {
 extern "C" int fm_pack(const PackArgs* a, hipStream_t st) {
   if (a->nseg <= 0 || a->nseg > 8) return (int)hipErrorInvalidValue;
   int maxn = 0;
-  bool fp8 = false;
   for (int s = 0; s < a->nseg; ++s) {
+    if (a->seg[s].kind == 2 && a->seg[s].n % 2048) return (int)hipErrorInvalidValue;
     if (a->seg[s].n > maxn) maxn = a->seg[s].n;
-    fp8 |= a->seg[s].kind == 2;
   }
   if (maxn == 0) return 0;
-  if (fp8) {
-    if (!a->absmax) return (int)hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(a->absmax, 0, 8 * sizeof(float), st);
-    if (e != hipSuccess) return (int)e;
-  }
   dim3 grid((unsigned)((maxn + 255) / 256), (unsigned)a->nseg), block(256);
-  PackArgs p = *a;
-  p.pass = 0;
-  hipLaunchKernelGGL(pack_kernel, grid, block, 0, st, p);
-  if (fp8) {
-    p.pass = 1;
-    hipLaunchKernelGGL(pack_kernel, grid, block, 0, st, p);
-  }
+  hipLaunchKernelGGL(pack_kernel, grid, block, 0, st, *a);
   return (int)hipGetLastError();
 }
 

@@ -15,7 +15,11 @@ from .kernels import KernelShapeError, _need
 H = 64
 TILES, KSTEPS, KAUG = 8, 5, 80
 BIAS_K = 71  # bias column of the augmented weight (k-step 4, lane half 0, element 7)
-FP8_MAX = 448.0
+# fp8 scoring (CDNA4 v_mfma_scale_f32_32x32x64_f8f6f4): 2 k-steps of K = 64 per gate tile,
+# fragments [TILES][2][64][32] e4m3 + one E8M0 scale per (tile, k-step, lane), lane-major
+KSTEPS_FP8 = 2
+FP8_FRAG_BYTES = TILES * KSTEPS_FP8 * 64 * 32
+FP8_SCALE_BYTES = TILES * KSTEPS_FP8 * 64
 
 
 class LstmRingSrc(C.Structure):
@@ -66,10 +70,9 @@ class LstmArgs(C.Structure):
     _fields_ = [
         ("x", C.c_void_p), ("N", C.c_int), ("T", C.c_int), ("F", C.c_int), ("fp8", C.c_int),
         ("w_enc", C.c_void_p), ("w_dec", C.c_void_p), ("w_out", C.c_void_p), ("b_out", C.c_void_p),
-        ("scale_w_enc", C.c_float), ("scale_w_dec", C.c_float), ("scale_act", C.c_float),
         ("mu", C.c_float), ("sigma", C.c_float), ("threshold", C.c_void_p), ("thr_default", C.c_float),
         ("err", C.c_void_p), ("zscore", C.c_void_p), ("verdict", C.c_void_p), ("recon", C.c_void_p),
-        ("app_id", C.c_void_p), ("app_stats", C.c_void_p), ("wmax", C.c_void_p), ("src", LstmRingSrc),
+        ("app_id", C.c_void_p), ("app_stats", C.c_void_p), ("src", LstmRingSrc),
         ("cal", C.c_void_p), ("cal_ewma", C.c_float), ("zlvl", C.c_void_p), ("thr_level", C.c_float),
         ("_pad2", C.c_int),
     ]
@@ -130,6 +133,49 @@ def pack_fragments(A: torch.Tensor) -> torch.Tensor:
 _IDX_CACHE: Dict[str, torch.Tensor] = {}
 
 
+def h_units(hh: torch.Tensor) -> torch.Tensor:
+    """``[len(hh), 32]`` hidden unit held in h-register j of a lane of half ``hh``
+    (unit 16 (tt >> 1) + 8 hh + 4 (tt & 1) + q for j = 4 tt + q): the fp8 B
+    fragment's k order, so h never moves between lanes."""
+    j = torch.arange(32)
+    tt, q = j // 4, j % 4
+    return 16 * (tt >> 1)[None, :] + 8 * hh[:, None] + 4 * (tt & 1)[None, :] + q[None, :]
+
+
+def _fp8_index(device) -> torch.Tensor:
+    """Flat gather index into a row-major [256, 80] augmented weight giving the
+    block-scaled fp8 fragments ``[TILES, 2, 64, 32]`` (-1: zero): lane l holds
+    permuted gate row 32 t + (l & 31); k-step 0, byte j: the unit of h-register j
+    of lane half l >> 5; k-step 1, lane half 0: inputs at bytes 0..6 (zero weights
+    past F), the bias at byte 7."""
+    key = f"fp8:{device}"
+    idx = _IDX_CACHE.get(key)
+    if idx is None:
+        rows = gate_row_perm()
+        lanes = torch.arange(64)
+        hh = lanes >> 5
+        unit = h_units(hh)                                  # [64, 32]
+        j = torch.arange(32)[None, :]
+        out = torch.empty(TILES, KSTEPS_FP8, 64, 32, dtype=torch.long)
+        for t in range(TILES):
+            r = rows[32 * t + (lanes & 31)][:, None]         # [64, 1]
+            out[t, 0] = r * KAUG + unit
+            out[t, 1] = torch.where((hh[:, None] == 0) & (j < 8), r * KAUG + H + j, torch.full_like(j, -1))
+        idx = out.flatten().to(device)
+        _IDX_CACHE[key] = idx
+    return idx
+
+
+def pack_fp8(A: torch.Tensor) -> torch.Tensor:
+    """``[256, 80]`` augmented weight → the fp8 kernel's uint8 buffer: block-scaled
+    e4m3 fragments ``[TILES, 2, 64, 32]``, then the E8M0 scales ``[64 lanes, 16]``
+    (:func:`~foremast_amd.ops.pack.fp8_blocks_lane_major`)."""
+    from .pack import fp8_blocks_lane_major
+    idx = _fp8_index(A.device)
+    v = torch.where(idx >= 0, A.float().flatten()[idx.clamp(min=0)], torch.zeros((), device=A.device))
+    return fp8_blocks_lane_major(v)
+
+
 def _frag_index(device) -> torch.Tensor:
     """Flat gather index into a row-major [256, 80] augmented weight that
     produces the A-fragment layout (device-side repacking every train step)."""
@@ -166,14 +212,17 @@ def model_srcs(model) -> List[torch.Tensor]:
     return [getattr(model, n).data for n in LSTM_SRCS]
 
 
-def augmented_codes(F: int, enc: bool) -> torch.Tensor:
+def augmented_codes(F: int, enc: bool, fp8: bool = False) -> torch.Tensor:
     """Pack codes of the A-fragment layout of ``[W_hh | W_ih | b]`` (the
-    ``_augment`` + ``pack_fragments`` reference, as a table)."""
+    ``_augment`` + ``pack_fragments`` reference, as a table; ``fp8``: the
+    block-scaled layout of :func:`_fp8_index`)."""
     from .pack import make_codes
-    idx = _frag_index("cpu")
+    idx = _fp8_index("cpu") if fp8 else _frag_index("cpu")
+    used = idx >= 0
+    idx = idx.clamp(min=0)
     r, k = idx // KAUG, idx % KAUG
-    is_h, is_b = k < H, k == BIAS_K
-    is_x = (k >= H) & (k < H + F) & torch.tensor(enc)
+    is_h, is_b = (k < H) & used, (k == BIAS_K) & used
+    is_x = (k >= H) & (k < H + F) & torch.tensor(enc) & used
     src = torch.where(is_h, LSTM_SRCS.index("enc_w_hh" if enc else "dec_w_hh"),
                       torch.where(is_b, LSTM_SRCS.index("enc_b" if enc else "dec_b"), LSTM_SRCS.index("enc_w_ih")))
     off = torch.where(is_h, r * H + k, torch.where(is_b, r, r * F + (k - H)))
@@ -191,8 +240,8 @@ def scoring_packer(p: "LstmPacked", model):
     F = model.F
     kind = KIND_FP8 if p.fp8 else KIND_BF16
     pk = Packer(model_srcs(model))
-    pk.add(augmented_codes(F, True), p.w_enc.view(-1), kind)
-    pk.add(augmented_codes(F, False), p.w_dec.view(-1), kind)
+    pk.add(augmented_codes(F, True, p.fp8), p.w_enc.view(-1), kind)
+    pk.add(augmented_codes(F, False, p.fp8), p.w_dec.view(-1), kind)
     pk.add(identity_codes("out_w", F * H), p.w_out.view(-1), KIND_F32)
     pk.add(identity_codes("out_b", F), p.b_out.view(-1), KIND_F32)
     return pk
@@ -200,26 +249,21 @@ def scoring_packer(p: "LstmPacked", model):
 
 def repack_into(p: "LstmPacked", model) -> "LstmPacked":
     """Refresh ``p`` in place from (device) model parameters.  With the native
-    library: one table-driven pack launch (fp8 scales stay on the device,
-    ``p.wmax``); otherwise one torch gather per matrix."""
+    library: one table-driven pack launch (fp8: block scales computed on the
+    device); otherwise torch gathers (:func:`pack_fp8` for fp8)."""
     if p.w_enc.is_cuda and nat.available():
         if p.packer is None or p.packer_model is not model:
             p.packer, p.packer_model = scoring_packer(p, model), model
         p.packer.run()
-        if p.fp8:
-            p.wmax = p.packer.absmax
         return p
     F = model.F
-    idx = _frag_index(p.w_enc.device)
-    Ae = _augment_dev(model.enc_w_hh, model.enc_b, model.enc_w_ih, F).flatten()[idx]
-    Ad = _augment_dev(model.dec_w_hh, model.dec_b, None, F).flatten()[idx]
     if p.fp8:
-        m = torch.stack([Ae.abs().max(), Ad.abs().max()]).clamp(min=1e-30) / FP8_MAX
-        se, sd = m.tolist()
-        p.w_enc.copy_((Ae / se).to(torch.float8_e4m3fn).view(torch.uint8).view_as(p.w_enc))
-        p.w_dec.copy_((Ad / sd).to(torch.float8_e4m3fn).view(torch.uint8).view_as(p.w_dec))
-        p.scale_w_enc, p.scale_w_dec = se, sd
+        p.w_enc.copy_(pack_fp8(_augment_dev(model.enc_w_hh, model.enc_b, model.enc_w_ih, F)))
+        p.w_dec.copy_(pack_fp8(_augment_dev(model.dec_w_hh, model.dec_b, None, F)))
     else:
+        idx = _frag_index(p.w_enc.device)
+        Ae = _augment_dev(model.enc_w_hh, model.enc_b, model.enc_w_ih, F).flatten()[idx]
+        Ad = _augment_dev(model.dec_w_hh, model.dec_b, None, F).flatten()[idx]
         p.w_enc.copy_(Ae.to(torch.bfloat16).view_as(p.w_enc))
         p.w_dec.copy_(Ad.to(torch.bfloat16).view_as(p.w_dec))
     p.w_out.copy_(model.out_w.detach())
@@ -231,35 +275,28 @@ def repack_into(p: "LstmPacked", model) -> "LstmPacked":
 class LstmPacked:
     F: int
     fp8: bool
-    w_enc: torch.Tensor
+    w_enc: torch.Tensor   # bf16 fragments, or the fp8 buffer (block-scaled fragments + E8M0 scales)
     w_dec: torch.Tensor
     w_out: torch.Tensor
     b_out: torch.Tensor
-    scale_w_enc: float = 1.0
-    scale_w_dec: float = 1.0
-    scale_act: float = 1.0
-    wmax: Optional[torch.Tensor] = None  # device absmax [enc, dec] of the fp8 weights (overrides scale_w_*)
     packer: Optional[object] = None
     packer_model: Optional[object] = None
 
 
-def pack(model, fp8: bool = False, device="cuda", act_scale: float = 1.0 / 32) -> LstmPacked:
+def pack(model, fp8: bool = False, device="cuda") -> LstmPacked:
     F = model.F
     if model.H != H:
         raise KernelShapeError(f"fused LSTM kernel is built for H={H}")
     if not 1 <= F <= 7:
         raise KernelShapeError("fused LSTM kernel supports 1..7 features")
-    Ae = pack_fragments(_augment(model.enc_w_hh, model.enc_b, model.enc_w_ih, F))
-    Ad = pack_fragments(_augment(model.dec_w_hh, model.dec_b, None, F))
     if fp8:
-        se = float(Ae.abs().max()) / FP8_MAX or 1.0
-        sd = float(Ad.abs().max()) / FP8_MAX or 1.0
-        qe = (Ae / se).to(torch.float8_e4m3fn).view(torch.uint8)
-        qd = (Ad / sd).to(torch.float8_e4m3fn).view(torch.uint8)
+        qe = pack_fp8(_augment(model.enc_w_hh, model.enc_b, model.enc_w_ih, F))
+        qd = pack_fp8(_augment(model.dec_w_hh, model.dec_b, None, F))
         return LstmPacked(F=F, fp8=True, w_enc=qe.contiguous().to(device), w_dec=qd.contiguous().to(device),
                           w_out=model.out_w.detach().float().contiguous().to(device),
-                          b_out=model.out_b.detach().float().contiguous().to(device),
-                          scale_w_enc=se, scale_w_dec=sd, scale_act=act_scale)
+                          b_out=model.out_b.detach().float().contiguous().to(device))
+    Ae = pack_fragments(_augment(model.enc_w_hh, model.enc_b, model.enc_w_ih, F))
+    Ad = pack_fragments(_augment(model.dec_w_hh, model.dec_b, None, F))
     return LstmPacked(F=F, fp8=False, w_enc=Ae.to(torch.bfloat16).contiguous().to(device),
                       w_dec=Ad.to(torch.bfloat16).contiguous().to(device),
                       w_out=model.out_w.detach().float().contiguous().to(device),
@@ -318,14 +355,12 @@ def lstm_score(p: LstmPacked, x: Optional[torch.Tensor], mu: float = 0.0, sigma:
     a.N, a.T, a.F, a.fp8 = N, T, F, int(p.fp8)
     a.w_enc, a.w_dec = p.w_enc.data_ptr(), p.w_dec.data_ptr()
     a.w_out, a.b_out = p.w_out.data_ptr(), p.b_out.data_ptr()
-    a.scale_w_enc, a.scale_w_dec, a.scale_act = p.scale_w_enc, p.scale_w_dec, p.scale_act
     a.mu, a.sigma = float(mu), float(sigma)
     a.threshold = nat.ptr(threshold)
     a.thr_default = float(thr_default)
     a.err, a.zscore, a.verdict = nat.ptr(out["err"]), nat.ptr(out["zscore"]), nat.ptr(out["verdict"])
     a.recon = nat.ptr(out.get("recon")) if want_recon else 0
     a.app_id, a.app_stats = nat.ptr(app_id), nat.ptr(app_stats)
-    a.wmax = nat.ptr(p.wmax) if p.fp8 else 0
     a.cal, a.cal_ewma = nat.ptr(cal), float(cal_ewma)
     if zlvl is not None:
         _need(zlvl.shape == (N, F) and zlvl.dtype == torch.float32 and zlvl.is_contiguous() and zlvl.device == dev,

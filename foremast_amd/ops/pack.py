@@ -7,7 +7,10 @@ fragments).  Doing that with torch index/convert ops costs ~15 launches per
 step, each longer on the host than on the GPU.  Here every output element is
 described by one int32 *code* (which parameter, which offset, which
 multiplier class) built once from the reference index maps, and one native
-launch (two for fp8: absmax, then quantise) produces every segment.
+launch produces every segment.  fp8 segments are block-scaled for the CDNA4
+``v_mfma_scale_f32_32x32x64_f8f6f4``: every 32 consecutive elements (one lane's
+k block of an A fragment) share an E8M0 scale, the smallest power of two that
+brings the block's absolute maximum within e4m3's 448 (:func:`e8m0_blocks`).
 
 :func:`reference_gather` evaluates the same codes with torch (CPU tests and
 the non-GPU path).
@@ -33,8 +36,30 @@ class PackSeg(C.Structure):
 
 
 class PackArgs(C.Structure):
-    _fields_ = [("src", C.c_void_p * 8), ("seg", PackSeg * 8), ("nseg", C.c_int), ("pass_", C.c_int),
-                ("absmax", C.c_void_p)]
+    _fields_ = [("src", C.c_void_p * 8), ("seg", PackSeg * 8), ("nseg", C.c_int), ("_pad", C.c_int)]
+
+
+FP8_BLOCK = 32
+FP8_LANES = 64   # scales are stored lane-major: block b's at (b % 64) * (blocks / 64) + b // 64
+
+
+def e8m0_blocks(v: torch.Tensor):
+    """Block-scaled e4m3 of ``v [blocks, 32]``: (codes uint8 ``[blocks, 32]``, E8M0
+    uint8 ``[blocks]``).  The block exponent e is the smallest integer with
+    ``absmax <= 448 * 2^e`` (from the exact frexp of absmax, as csrc/pack.hip
+    computes it), the codes are ``v * 2^-e`` rounded to e4m3, the scale byte
+    ``e + 127``; an all-zero block gets e = 0."""
+    v = v.float()
+    amax = v.abs().amax(1)
+    m, x = torch.frexp(amax)
+    e = torch.where(amax > 0, x - 9 + (m > 0.875).to(x.dtype), torch.zeros_like(x)).clamp(-127, 127)
+    q = torch.ldexp(v, -e[:, None].to(v.dtype)).to(torch.float8_e4m3fn).view(torch.uint8)
+    return q, (e + 127).to(torch.uint8)
+
+
+def fp8_segment_bytes(n: int) -> int:
+    """Bytes of a block-scaled fp8 segment of n codes: the codes, then one scale per block."""
+    return n + n // FP8_BLOCK
 
 
 nat.register("fm_pack", [C.POINTER(PackArgs), C.c_void_p])
@@ -71,11 +96,6 @@ def reference_gather(code: torch.Tensor, srcs: Sequence[torch.Tensor], mul=(1.0,
     return out
 
 
-def fp8_scale(absmax: float) -> float:
-    """Dequantisation scale of an fp8 segment (the kernels use the same rule)."""
-    return absmax / 448.0 if absmax > 0 else 1.0
-
-
 @dataclass
 class _Seg:
     code: torch.Tensor
@@ -90,14 +110,17 @@ class Packer:
     ctypes argument block is built once, so :meth:`run` costs one C call."""
     srcs: List[torch.Tensor]
     segs: List[_Seg] = field(default_factory=list)
-    absmax: Optional[torch.Tensor] = None
     _args: Optional[PackArgs] = None
 
     def add(self, code: torch.Tensor, out: torch.Tensor, kind: int, mul=(1.0, 1.0, 1.0, 1.0)) -> "Packer":
         if len(self.segs) == 8:
             raise ValueError("at most 8 pack segments")
-        if out.numel() != code.numel() or not out.is_contiguous():
-            raise ValueError("pack output must be contiguous with one element per code")
+        n = code.numel()
+        if kind == KIND_FP8 and n % (FP8_BLOCK * FP8_LANES):
+            raise ValueError(f"an fp8 segment holds whole lanes of {FP8_BLOCK}-element blocks")
+        want_n = fp8_segment_bytes(n) if kind == KIND_FP8 else n
+        if out.numel() != want_n or not out.is_contiguous():
+            raise ValueError("pack output must be contiguous with one element per code (fp8: plus the scales)")
         want = {KIND_F32: torch.float32, KIND_BF16: torch.bfloat16, KIND_FP8: torch.uint8}[kind]
         if out.dtype != want:
             raise ValueError(f"pack kind {kind} writes {want}, got {out.dtype}")
@@ -125,10 +148,6 @@ class Packer:
             for j in range(4):
                 a.seg[i].mul[j] = s.mul[j]
         a.nseg = len(self.segs)
-        if any(s.kind == KIND_FP8 for s in self.segs):
-            if self.absmax is None:
-                self.absmax = torch.zeros(8, dtype=torch.float32, device=self.segs[0].out.device)
-            a.absmax = self.absmax.data_ptr()
         return a
 
     def run(self) -> None:
@@ -145,8 +164,11 @@ class Packer:
             elif s.kind == KIND_BF16:
                 s.out.copy_(v.to(torch.bfloat16))
             else:
-                m = float(v.abs().max()) if v.numel() else 0.0
-                if self.absmax is None:
-                    self.absmax = torch.zeros(8, dtype=torch.float32, device=s.out.device)
-                self.absmax[i] = m
-                s.out.copy_((v * (448.0 / m if m > 0 else 1.0)).to(torch.float8_e4m3fn).view(torch.uint8))
+                s.out.copy_(fp8_blocks_lane_major(v))
+
+
+def fp8_blocks_lane_major(v: torch.Tensor) -> torch.Tensor:
+    """A block-scaled fp8 segment of the values ``v`` (codes, then the scales lane-major)."""
+    q, sc = e8m0_blocks(v.reshape(-1, FP8_BLOCK))
+    per_lane = sc.numel() // FP8_LANES
+    return torch.cat([q.reshape(-1), sc.view(per_lane, FP8_LANES).t().reshape(-1)])
