@@ -163,6 +163,9 @@ def parse():
     p.add_argument("--lstm-threshold", type=float, default=5.0,
                    help="AE reconstruction z threshold (5: the level term carries the small shifts)")
     p.add_argument("--mv-bf16", action="store_true", help="multivariate config: bf16 scoring instead of fp8")
+    p.add_argument("--lstm-precision", default="auto", choices=["auto", "bf16", "fp8"],
+                   help="node-lstm scoring precision; auto: fp8 (CDNA4 block-scaled MFMA) for the 2-feature "
+                        "config 5 (BASELINE.json: 'fp8 LSTM on CDNA4 MFMA'), bf16 otherwise")
     p.add_argument("--lstm-cal-ewma", type=float, default=1.0 / 32,
                    help="per-series calibration refresh rate of healthy windows")
     p.add_argument("--lstm-level-threshold", type=float, default=5.5,

@@ -898,10 +898,12 @@ def setup_node_lstm(args, world, rank, dev):
         assert code == 200, resp
         truth[resp["jobId"]] = i in bad
     register_s = time.perf_counter() - t_reg
+    prec = getattr(args, "lstm_precision", "auto")
+    fp8 = prec == "fp8" or (prec == "auto" and F == 2)   # config 5: fp8 on the CDNA4 block-scaled MFMA
     lstm = LstmMonitor(store, cfg, prom=server, device=dev, worker_id=f"node-m{rank}-lstm", step=STEP,
                        clock=lambda: clock["t"], ring_len=R, features=F, window=args.lstm_window,
                        train_batch=args.lstm_train_batch, min_capacity=max(64, na), history=hist,
-                       decode_threads=args.decode_threads)
+                       decode_threads=args.decode_threads, fp8=fp8)
     stream = StreamingMonitor(store, cfg, prom=server, device=dev, worker_id=f"node-m{rank}", ring_len=R,
                               window=10, clock=lambda: clock["t"])
     stream.exclude = lstm.is_mine
@@ -948,7 +950,8 @@ def setup_node_lstm(args, world, rank, dev):
     meta = {
         "model": f"continuous {F}-metric jobs on the production node brain: NodeBrain + LstmMonitor (shared LSTM "
                  f"autoencoder F={F}, H={lstm.shard.model.H}, window {args.lstm_window}, one DP Adam step per tick, "
-                 f"fused {'fp8' if lstm.shard.fp8 else 'bf16'} MFMA scoring)",
+                 f"fused {'fp8 block-scaled (v_mfma_scale_f32_32x32x64_f8f6f4)' if lstm.shard.fp8 else 'bf16'} "
+                 f"MFMA scoring)",
         "global_batch": n_jobs * F,
         "seq_len": args.lstm_window,
         "history": R,
