@@ -118,3 +118,43 @@ def test_rccl_abort_and_reform_in_process():
 
 def test_gloo_abort_and_reform_in_process():
     _check_reform(_reform(cpu=True), "gloo")
+
+
+def _node_bench(gpus: int, cpu: bool, force: bool = False, extra=()) -> dict:
+    env = dict(os.environ, OMP_NUM_THREADS="2", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for k in ("WORLD_SIZE", "RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    if force:
+        env["FOREMAST_FORCE_COLLECTIVES"] = "1"
+    else:
+        env.pop("FOREMAST_FORCE_COLLECTIVES", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--config", "node",
+           "--arrival-per-tick", "8", "--steps", "4", "--warmup", "11"] + list(extra) + (["--cpu"] if cpu else [])
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stdout[-1000:] + out.stderr[-3000:]
+    lines = [x for x in out.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.slow
+def test_node_bench_two_ranks_runs_the_deployed_exchange_cpu():
+    """``bench.py --gpus 2 --config node`` (arrivals) under torch.distributed.run: the
+    ranks join an ElasticWorld on the launcher's store and exchange roster deltas, as a
+    deployed node does; the record says so and counts every rank's jobs."""
+    got = _node_bench(2, cpu=True)
+    ex = got["node"]["exchange"]
+    assert got["n_gpus"] == 2 and ex["ranks"] == 2 and ex["path"].startswith("ElasticWorld")
+    assert ex["generation"] == 0 and ex["samples"] == 4 and ex["exchange_ms_p50_p99_max"][0] is not None
+    det = got["detection"]
+    assert det["ranks"] == 2 and det["fn"] == 0 and det["jobs"] > 0
+
+
+@pytest.mark.gpu
+def test_node_bench_forced_rccl_exchange_one_gpu():
+    """The node bench's deployed exchange on RCCL (a 1-member ElasticWorld with forced
+    collectives): roster deltas through the store, health all-gather on the GPU."""
+    got = _node_bench(1, cpu=False, force=True)
+    ex = got["node"]["exchange"]
+    assert ex["path"].startswith("ElasticWorld") and ex["generation"] == 0
+    assert got["detection"]["fn"] == 0
