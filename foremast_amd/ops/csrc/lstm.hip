@@ -413,39 +413,34 @@ extern "C" int fm_fp8_convert(const float* in, unsigned char* out, int n, hipStr
   return (int)hipGetLastError();
 }
 
-// Probe of the CDNA4 block-scaled MFMA (v_mfma_scale_f32_32x32x64_f8f6f4, e4m3 A / B, one
-// E8M0 scale per 32-element k block): D[32 x 32] = (A * 2^(sa - 127)) [32 x 64] . (B * 2^(sb - 127))
-// [64 x 32] with the lane map the fp8 LSTM kernels assume -- lane l holds row / column l & 31,
-// k = 32 (l >> 5) + j in byte j of its 8-VGPR fragment, and the scale of that 32-element block
-// (tests/test_lstm.py checks it against exact integer data).
+// Probe of the CDNA4 block-scaled MFMA (v_mfma_scale_f32_32x32x64_f8f6f4, e4m3 A / B): lane l
+// loads row (A) / column (B) l & 31, k = 32 (l >> 5) + j into byte j of its 8-VGPR fragment
+// (converted on the device), and passes the 32-bit scale registers it is given (sa_reg /
+// sb_reg [64]) with op_sel SEL; D [32 x 32] is written with the standard 32x32 C map.
+// scripts/probe_mfma_scale.py and tests/test_lstm.py decode which lane / byte scales what.
 template <int SEL>
-__global__ void mfma_scale_probe_kernel(const float* A, const float* B, const unsigned char* sa,
-                                        const unsigned char* sb, float* D) {
+__global__ void mfma_scale_probe_kernel(const float* A, const float* B, const int* sa_reg, const int* sb_reg,
+                                        float* D) {
   const int l = threadIdx.x, r = l & 31, hh = l >> 5;
-  fm_lstm::f8x32 af, bf;
   float av[32], bv[32];
 #pragma unroll
   for (int j = 0; j < 32; ++j) {
     av[j] = A[r * 64 + 32 * hh + j];
     bv[j] = B[(32 * hh + j) * 32 + r];
   }
-  af = fm_lstm::pack_fp8x32(av);
-  bf = fm_lstm::pack_fp8x32(bv);
-  // the scale bytes sit in byte SEL of their registers (the other bytes hold decoys)
-  const int fa = ((int)sa[r * 2 + hh] << (8 * SEL)) | (SEL ? 0x55 : 0x5500);
-  const int fb = ((int)sb[r * 2 + hh] << (8 * SEL)) | (SEL ? 0x66 : 0x6600);
-  const f32x16 d = fm_lstm::mfma_scaled<SEL>(af, bf, (f32x16){}, fa, fb);
+  const fm_lstm::f8x32 af = fm_lstm::pack_fp8x32(av), bf = fm_lstm::pack_fp8x32(bv);
+  const f32x16 d = fm_lstm::mfma_scaled<SEL>(af, bf, (f32x16){}, sa_reg[l], sb_reg[l]);
 #pragma unroll
   for (int i = 0; i < 16; ++i) D[((i & 3) + 8 * (i >> 2) + 4 * hh) * 32 + r] = d[i];
 }
 
-extern "C" int fm_mfma_scale_probe(const float* A, const float* B, const unsigned char* sa, const unsigned char* sb,
-                                   float* D, int sel, hipStream_t st) {
+extern "C" int fm_mfma_scale_probe(const float* A, const float* B, const int* sa_reg, const int* sb_reg, float* D,
+                                   int sel, hipStream_t st) {
   switch (sel) {
-    case 0: hipLaunchKernelGGL(mfma_scale_probe_kernel<0>, dim3(1), dim3(64), 0, st, A, B, sa, sb, D); break;
-    case 1: hipLaunchKernelGGL(mfma_scale_probe_kernel<1>, dim3(1), dim3(64), 0, st, A, B, sa, sb, D); break;
-    case 2: hipLaunchKernelGGL(mfma_scale_probe_kernel<2>, dim3(1), dim3(64), 0, st, A, B, sa, sb, D); break;
-    case 3: hipLaunchKernelGGL(mfma_scale_probe_kernel<3>, dim3(1), dim3(64), 0, st, A, B, sa, sb, D); break;
+    case 0: hipLaunchKernelGGL(mfma_scale_probe_kernel<0>, dim3(1), dim3(64), 0, st, A, B, sa_reg, sb_reg, D); break;
+    case 1: hipLaunchKernelGGL(mfma_scale_probe_kernel<1>, dim3(1), dim3(64), 0, st, A, B, sa_reg, sb_reg, D); break;
+    case 2: hipLaunchKernelGGL(mfma_scale_probe_kernel<2>, dim3(1), dim3(64), 0, st, A, B, sa_reg, sb_reg, D); break;
+    case 3: hipLaunchKernelGGL(mfma_scale_probe_kernel<3>, dim3(1), dim3(64), 0, st, A, B, sa_reg, sb_reg, D); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();

@@ -101,8 +101,9 @@ class AnomalyBuffer:
         dev = torch.device(device)
         self.cap = int(cap)
         self.count = torch.zeros(1, dtype=torch.int32, device=dev) if count is None else count
-        _need(self.count.dtype == torch.int32 and self.count.numel() == 1 and self.count.device == dev,
-              "count must be an int32 [1] tensor on the device")
+        dev = self.count.device  # "cuda" -> "cuda:<current>"
+        _need(self.count.dtype == torch.int32 and self.count.numel() == 1 and self.count.is_cuda,
+              "count must be an int32 [1] GPU tensor")
         self.series = torch.empty(self.cap, dtype=torch.int32, device=dev)
         self.col = torch.empty(self.cap, dtype=torch.int32, device=dev)
         self.val = torch.empty(self.cap, dtype=torch.float32, device=dev)

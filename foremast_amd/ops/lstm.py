@@ -425,16 +425,17 @@ def device_fp8(values: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def mfma_scale_probe(A: torch.Tensor, B: torch.Tensor, sa: torch.Tensor, sb: torch.Tensor, sel: int = 0) -> torch.Tensor:
-    """``D = (A 2^(sa-127)) (B 2^(sb-127))`` through ONE ``v_mfma_scale_f32_32x32x64_f8f6f4``
-    with the lane map the fp8 LSTM kernels use (``A [32, 64]``, ``B [64, 32]`` float32
-    converted to e4m3 on the device; ``sa [32, 2]`` / ``sb [32, 2]`` uint8 E8M0 scales of
-    row / column r and k block h, passed in byte ``sel`` of the scale registers)."""
+def mfma_scale_probe(A: torch.Tensor, B: torch.Tensor, sa_reg: torch.Tensor, sb_reg: torch.Tensor,
+                     sel: int = 0) -> torch.Tensor:
+    """ONE ``v_mfma_scale_f32_32x32x64_f8f6f4`` on e4m3 data: lane l holds row / column
+    ``l & 31`` of ``A [32, 64]`` / ``B [64, 32]`` (float32, converted on the device) at
+    k = 32 (l >> 5) + j, and passes ``sa_reg[l]`` / ``sb_reg[l]`` (int32 [64]) as its
+    scale registers with op_sel ``sel``; returns D [32, 32]."""
     lib = nat.require()
-    _need(A.shape == (32, 64) and B.shape == (64, 32) and sa.shape == (32, 2) and sb.shape == (32, 2),
-          "probe shapes: A [32, 64], B [64, 32], scales [32, 2]")
+    _need(A.shape == (32, 64) and B.shape == (64, 32) and sa_reg.shape == (64,) and sb_reg.shape == (64,),
+          "probe shapes: A [32, 64], B [64, 32], scale registers [64]")
     A, B = A.float().contiguous(), B.float().contiguous()
-    sa, sb = sa.to(torch.uint8).contiguous(), sb.to(torch.uint8).contiguous()
+    sa, sb = sa_reg.to(torch.int32).contiguous(), sb_reg.to(torch.int32).contiguous()
     _need(A.is_cuda and all(t.device == A.device for t in (B, sa, sb)), "probe tensors on one GPU")
     D = torch.empty((32, 32), dtype=torch.float32, device=A.device)
     nat.check(lib.fm_mfma_scale_probe(A.data_ptr(), B.data_ptr(), sa.data_ptr(), sb.data_ptr(), D.data_ptr(),

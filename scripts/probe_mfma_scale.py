@@ -1,0 +1,91 @@
+"""Decode the operand and scale maps of v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3) on the GPU.
+
+1. unity scales, integer data: D == A @ B under the assumed data map (lane l: row / column
+   l & 31, k = 32 (l >> 5) + j in byte j)?
+2. which lane and which byte of the scale registers scale (row r, k block kb) of A and
+   (column c, k block kb) of B, for each op_sel: one-hot probes read the applied power of
+   two off D (every byte of every lane holds a distinct exponent, in two passes).
+
+    python scripts/probe_mfma_scale.py   # prints one JSON line per finding
+"""
+
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from foremast_amd.ops import lstm as L  # noqa: E402
+
+ONE = 0x7F7F7F7F
+
+
+def regs(code) -> torch.Tensor:
+    """int32 [64] scale registers, byte j of lane l = code(l, j)."""
+    out = []
+    for lane in range(64):
+        v = 0
+        for j in range(4):
+            v |= (int(code(lane, j)) & 0xFF) << (8 * j)
+        out.append(v - (1 << 32) if v >= 1 << 31 else v)
+    return torch.tensor(out, dtype=torch.int32)
+
+
+def decode(dev, side: str, sel: int):
+    """(lane, byte) whose scale applied to each (row or column, k block) of ``side``."""
+    found = {}
+    for kb in (0, 1):
+        k0 = 32 * kb + 3
+        exps = []
+        for pas in (0, 1):   # pass 0: exponent = 64 + 2 lane + (byte & 1); pass 1: ... + (byte >> 1)
+            code = (lambda l, j, p=pas: 64 + 2 * l + ((j & 1) if p == 0 else (j >> 1)))
+            A = torch.zeros(32, 64)
+            B = torch.zeros(64, 32)
+            if side == "A":
+                A[:, :] = 1.0
+                B[k0, 5] = 1.0
+                sa, sb = regs(code), torch.full((64,), ONE, dtype=torch.int32)
+            else:
+                B[:, :] = 1.0
+                A[7, k0] = 1.0
+                sa, sb = torch.full((64,), ONE, dtype=torch.int32), regs(code)
+            D = L.mfma_scale_probe(A.to(dev), B.to(dev), sa.to(dev), sb.to(dev), sel).cpu().double()
+            vals = D[:, 5] if side == "A" else D[7, :]
+            exps.append([int(round(float(torch.log2(v)))) + 127 if v > 0 else None for v in vals.tolist()])
+        for i in range(32):
+            e0, e1 = exps[0][i], exps[1][i]
+            if e0 is None or e1 is None:
+                found[(i, kb)] = None
+                continue
+            lane0, b0 = divmod(e0 - 64, 2)
+            lane1, b1 = divmod(e1 - 64, 2)
+            found[(i, kb)] = (lane0, b0 + 2 * b1) if lane0 == lane1 else ("?", e0, e1)
+    return found
+
+
+def main():
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(1)
+    A = torch.randint(-8, 9, (32, 64), generator=g).float()
+    B = torch.randint(-8, 9, (64, 32), generator=g).float()
+    one = torch.full((64,), ONE, dtype=torch.int32, device=dev)
+    D = L.mfma_scale_probe(A.to(dev), B.to(dev), one, one, 0).cpu().double()
+    ref = A.double() @ B.double()
+    print(json.dumps({"unity_scales_max_abs_err": float((D - ref).abs().max()),
+                      "vs_transposed_B_err": float((D - A.double() @ B.double().reshape(32, 64).t()).abs().max())
+                      if False else None}), flush=True)
+    for sel in range(4):
+        for side in ("A", "B"):
+            f = decode(dev, side, sel)
+            expect = {(i, kb): (i + 32 * kb, sel) for i in range(32) for kb in (0, 1)}
+            ok = sum(f[k] == expect[k] for k in expect)
+            sample = {f"{i},{kb}": f[(i, kb)] for i in (0, 1, 5, 31) for kb in (0, 1)}
+            print(json.dumps({"sel": sel, "side": side, "matches_assumed_map": ok, "of": len(expect),
+                              "sample_(index,kblock)->(lane,byte)": {k: v for k, v in sample.items()}},
+                             default=str), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -550,9 +550,18 @@ def test_block_scaled_fp8_mfma_lane_map(sel):
     B = torch.randint(-8, 9, (64, 32), generator=g).float()
     A[3, :] += torch.arange(64) % 5           # asymmetric rows / columns
     B[:, 5] += torch.arange(64) % 3
-    sa = torch.randint(120, 135, (32, 2), generator=g).to(torch.uint8)
-    sb = torch.randint(120, 135, (32, 2), generator=g).to(torch.uint8)
-    got = L.mfma_scale_probe(A.to(dev), B.to(dev), sa.to(dev), sb.to(dev), sel).cpu().double()
+    sa = torch.randint(120, 135, (32, 2), generator=g)
+    sb = torch.randint(120, 135, (32, 2), generator=g)
+
+    def regs(s, decoy):  # lane l: the scale of (l & 31, k block l >> 5) in byte sel, decoys elsewhere
+        out = []
+        for lane in range(64):
+            v = 0
+            for j in range(4):
+                v |= (int(s[lane & 31, lane >> 5]) if j == sel else decoy) << (8 * j)
+            out.append(v - (1 << 32) if v >= 1 << 31 else v)
+        return torch.tensor(out, dtype=torch.int32, device=dev)
+    got = L.mfma_scale_probe(A.to(dev), B.to(dev), regs(sa, 0x55), regs(sb, 0x66), sel).cpu().double()
     fa = torch.exp2(sa.double() - 127).repeat_interleave(32, dim=1)          # [32, 64]
     fb = torch.exp2(sb.double() - 127).repeat_interleave(32, dim=1).t()      # [64, 32]
     want = (A.double() * fa) @ (B.double() * fb)
