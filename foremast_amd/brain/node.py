@@ -173,13 +173,15 @@ class NodeBrain:
                 v = getattr(m, "roster_version", 0)
                 reset, items = v != self._mver.get(k), []
                 self._mver[k] = v
+            apps = getattr(m, "apps", None)
+            n_apps = len(apps) if isinstance(apps, dict) else None
             if hasattr(m, "app_counts"):
-                names = m.roster_names() if reset else ()
                 tables.append(m.app_counts())
+                engines.append((reset, items, m.roster_names, n_apps))
             else:
                 names, c = m.app_table()
                 tables.append(c)
-            engines.append((reset, items, names))
+                engines.append((reset, items, lambda names=names: names, n_apps))
         self.roster.update(engines)
         counts = self.roster.counts(tables)
         return self.roster.names, counts, self.roster.version, sum(m.n_live for m in self.monitors)

@@ -11,12 +11,16 @@ change logs, never rebuilt:
   slot of its app table is set or freed; a consumer drains it once per tick.
   An engine that renumbers its table (or a log that grew past its bound without
   a consumer) marks a reset: the consumer then re-reads the whole table once.
-* :class:`NodeRoster` — the rank's merged table: node index per app with a
-  reference count over the engines, an index map per engine (engine index →
-  node index) mirrored on the device, so the merged counters are one
-  ``index_add_`` per engine.  Its own change log feeds the exchange's roster
-  deltas (:class:`~foremast_amd.parallel.cluster.ClusterHealth`), so the host
-  work per tick is O(apps that changed), not O(apps).
+* :class:`NodeRoster` — the rank's merged table.  While at most one engine
+  holds apps (a rollout-only or continuous-only node, the common case) it IS
+  that engine's table: same indices, the engine's changes forwarded as they
+  are, its counters used as they are — no per-change work at all.  When a
+  second engine holds apps it switches to a merged table: node index per app
+  with a reference count over the engines, an index map per engine (engine
+  index → node index) mirrored on the device, so the merged counters are one
+  ``index_add_`` per engine.  Either way its change log feeds the exchange's
+  roster deltas (:class:`~foremast_amd.parallel.cluster.ClusterHealth`), so the
+  host work per tick is O(apps that changed), not O(apps).
 
 The reference brain has no such table; it is what "aggregate service health
 check across multiple K8s clusters" (``/root/reference/README.md:27``) needs
@@ -80,6 +84,7 @@ class NodeRoster:
         self.version = 0
         self.n_apps = 0
         self._changes = 0
+        self.mode: Optional[Tuple[str, int]] = None   # ("pass", engine) or ("merged", -1)
 
     # ------------------------------------------------------------------ node index refcounts
     def _ref(self, name: Name) -> int:
@@ -126,15 +131,52 @@ class NodeRoster:
         m[i] = self._ref(name) if name is not None else -1
 
     # ------------------------------------------------------------------ per tick
-    def update(self, engines: Sequence[Tuple[bool, List[Tuple[int, Optional[Name]]], Sequence[Optional[Name]]]]) -> bool:
-        """Apply each engine's drained change log ``(reset, items, current names)``;
-        returns whether the merged roster changed."""
+    def _clear(self) -> None:
+        self.names = []
+        self.index, self.refs, self.free = {}, {}, []
+        self.maps = [np.zeros(0, dtype=np.int64) for _ in self.maps]
+        self._dev_maps = [None] * len(self.maps)
+        self.n_apps = 0
+
+    def update(self, engines: Sequence[Tuple[bool, List[Tuple[int, Optional[Name]]], object, Optional[int]]]) -> bool:
+        """Apply each engine's drained change log ``(reset, items, names, n_apps)``
+        (``names``: a callable returning the engine's current table, called only
+        when needed; ``n_apps``: its app count, None if unknown); returns whether
+        the node roster changed."""
+        active = [k for k, e in enumerate(engines) if e[3] is None or e[3] > 0]
+        if len(active) <= 1:  # one engine holds every app: its table is the node's
+            k = active[0] if active else 0
+            reset, items, names_fn, n = engines[k]
+            changed = False
+            if self.mode != ("pass", k):
+                self._clear()
+                self.mode = ("pass", k)
+                self.log.mark_reset()
+                changed = True
+            self.names = names_fn()
+            self.n_apps = int(n or 0)
+            if reset:
+                self.log.mark_reset()
+                changed = True
+            elif items:
+                self.log.note_many(items)
+                changed = True
+            if changed:
+                self.version += 1
+            return changed
         c0 = self._changes
-        for k, (reset, items, names) in enumerate(engines):
+        if self.mode != ("merged", -1):  # rebuild from every engine's whole table
+            self._clear()
+            self.mode = ("merged", -1)
+            self.log.mark_reset()
+            self._changes += 1
+            engines = [(True, [], names_fn, n) for _r, _i, names_fn, n in engines]
+        for k, (reset, items, names_fn, _n) in enumerate(engines):
             if reset:
                 m = self.maps[k]
                 for i in np.flatnonzero(m >= 0).tolist():
                     self._unref(int(m[i]))
+                names = names_fn()
                 self.maps[k] = np.full(max(64, len(names)), -1, dtype=np.int64)
                 for i, nm in enumerate(names):
                     if nm is not None:
@@ -150,8 +192,11 @@ class NodeRoster:
         return changed
 
     def counts(self, tables: Sequence[torch.Tensor]) -> torch.Tensor:
-        """``[A, 2]`` int32 merged counters from each engine's ``[A_k, 2]`` counters."""
+        """``[A, 2]`` int32 node counters from each engine's ``[A_k, 2]`` counters."""
         A = len(self.names)
+        if self.mode is not None and self.mode[0] == "pass":
+            c = tables[self.mode[1]]
+            return c[:A]
         out = torch.zeros((max(A, 1), 2), dtype=torch.int32, device=self.device)
         for k, c in enumerate(tables):
             m = self.maps[k]

@@ -59,6 +59,10 @@ class FakeEngine:
     def n_live(self):
         return len(self.index)
 
+    @property
+    def apps(self):
+        return self.index
+
     def set_apps(self, apps, k):
         want = {("ns", f"app{a}"): a for a in apps}
         for name in [n for n in self.index if n not in want]:

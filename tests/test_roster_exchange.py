@@ -88,3 +88,71 @@ def test_churning_roster_n_ranks_equal_one_rank(tmp_path):
                   "roster_bytes_p50": float(np.median(steady)), "first_tick_bytes": full}
     (tmp_path / "exchange_record.json").write_text(json.dumps(rec))
     print("exchange record", json.dumps(rec))
+
+
+def test_node_roster_pass_and_merged_modes_match_the_engines():
+    """NodeRoster over two engines whose apps come and go (indices reused), passing
+    through one engine's table while the other is empty and merging when both hold
+    apps: every tick the node table (name -> summed counters) equals the engines',
+    and a peer replaying the node's change log (resets: a full copy) holds the same
+    roster -- what ClusterHealth's deltas rely on."""
+    import random
+    import torch
+    from foremast_amd.parallel.roster import ChangeLog, NodeRoster
+
+    class Eng:
+        def __init__(self):
+            self.names, self.index, self.free, self.log = [], {}, [], ChangeLog()
+
+        def set(self, apps):
+            for nm in [n for n in self.index if n not in apps]:
+                i = self.index.pop(nm)
+                self.names[i] = None
+                self.free.append(i)
+                self.log.note(i, None)
+            for nm in apps:
+                if nm not in self.index:
+                    i = self.free.pop() if self.free else len(self.names)
+                    if i == len(self.names):
+                        self.names.append(nm)
+                    else:
+                        self.names[i] = nm
+                    self.index[nm] = i
+                    self.log.note(i, nm)
+
+    rng = random.Random(5)
+    eng = [Eng(), Eng()]
+    nr = NodeRoster(2, "cpu")
+    mirror = []
+    modes = set()
+    for tick in range(60):
+        phase = (tick // 12) % 3        # 0: engine 0 only, 1: both, 2: engine 1 only
+        pool = [("ns", f"a{i}") for i in range(40)]
+        for k, e in enumerate(eng):
+            on = (phase == 0 and k == 0) or phase == 1 or (phase == 2 and k == 1)
+            e.set(set(rng.sample(pool, rng.randint(3, 25))) if on else set())
+        tables = [torch.tensor([[rng.randint(0, 1), rng.randint(1, 4)] if n else [0, 0] for n in e.names],
+                               dtype=torch.int32).reshape(-1, 2) for e in eng]
+        engines = []
+        for e in eng:
+            reset, items = e.log.drain()
+            engines.append((reset, items, (lambda e=e: e.names), len(e.index)))
+        nr.update(engines)
+        modes.add(nr.mode[0])
+        got = {n: nr.counts(tables)[i].tolist() for i, n in enumerate(nr.names) if n}
+        want = {}
+        for e, t in zip(eng, tables):
+            for n, i in e.index.items():
+                c = want.setdefault(n, [0, 0])
+                c[0] += int(t[i, 0])
+                c[1] += int(t[i, 1])
+        assert got == want, tick
+        reset, items = nr.log.drain()
+        if reset:
+            mirror = list(nr.names)
+        for i, n in items:
+            mirror.extend([None] * (i + 1 - len(mirror)))
+            mirror[i] = n
+        assert [n for n in mirror if n] == [n for n in nr.names if n] and \
+            {i: n for i, n in enumerate(mirror) if n} == {i: n for i, n in enumerate(nr.names) if n}, tick
+    assert modes == {"pass", "merged"}
