@@ -58,6 +58,14 @@ def _world(group=None) -> Tuple[int, int]:
     return 1, 0
 
 
+def _label(name) -> str:
+    """``"namespace/app"`` of a roster entry: a (namespace, app) tuple (this rank's
+    engines) or the label itself (a peer's roster, as published); "" for a free index."""
+    if not name:
+        return ""
+    return name if isinstance(name, str) else f"{name[0]}/{name[1]}"
+
+
 def _diff(old: Sequence, new: Sequence) -> List[Tuple[int, Any]]:
     """Index changes turning roster ``old`` into ``new`` (the fallback when the
     caller keeps no change log)."""
@@ -133,9 +141,10 @@ class ClusterHealth:
         full = (reset or self._fseq < 0 or seq - self._fseq >= FULL_EVERY
                 or self._delta_n + len(items) > max(64, len(names) // 2))
         if full:
-            key, rec = f"roster/{rank}/f/{seq}", {"names": list(names), "info": info}
+            key, rec = f"roster/{rank}/f/{seq}", {"n": [_label(n) for n in names], "info": info}
         else:
-            key, rec = f"roster/{rank}/d/{seq}", {"c": items, "info": info}
+            key, rec = f"roster/{rank}/d/{seq}", {"i": [i for i, _ in items], "n": [_label(n) for _, n in items],
+                                                  "info": info}
         raw = json.dumps(rec)
         kv.set(key, raw)   # published before the gather that announces it: a peer that sees it can read it
         self.last_roster_bytes += len(raw)
@@ -178,14 +187,15 @@ class ClusterHealth:
         for (r, q, kind), rec in zip(plan, recs):
             p = self._peers[r]
             if kind == "f":
-                p.names, p.info = [tuple(n) if n else None for n in rec["names"]], rec.get("info", {})
+                p.names, p.info = [n or None for n in rec["n"]], rec.get("info", {})
                 self.roster_full_reads += 1
             else:
                 names = p.names
-                for i, n in rec["c"]:
-                    if i >= len(names):
-                        names.extend([None] * (i + 1 - len(names)))
-                    names[i] = tuple(n) if n else None
+                idx = rec["i"]
+                if idx and max(idx) >= len(names):
+                    names.extend([None] * (max(idx) + 1 - len(names)))
+                for i, n in zip(idx, rec["n"]):
+                    names[i] = n or None
                 p.info = rec.get("info", p.info)
             p.seq = q
         for r, (seq, _f) in want.items():
@@ -258,8 +268,7 @@ class ClusterHealth:
         lim = np.minimum(np.minimum(hn[:, 1], (chunk - HDR) // 2), [len(ro) for ro, _ in rosters])
         bad = hn[:, HDR::2] > 0
         bad &= np.arange(bad.shape[1])[None, :] < lim[:, None]
-        anomalous = [f"{rosters[r][0][i][0]}/{rosters[r][0][i][1]}" for r, i in zip(*np.nonzero(bad))
-                     if rosters[r][0][i]]
+        anomalous = [_label(rosters[r][0][i]) for r, i in zip(*np.nonzero(bad)) if rosters[r][0][i]]
         members = [dict(rosters[r][1]) | {"rank": r, "apps": int(hn[r, 1]), "series": int(hn[r, 3])}
                    for r in range(world)]
         t4 = time.perf_counter()
@@ -293,7 +302,7 @@ class NodeTable(dict):
             cnt = self._host[r, HDR:HDR + 2 * n].view(n, 2).tolist()
             for name, (an, sc) in zip(ro[:n], cnt):
                 if name:  # None: a free index of the rank's stable app table
-                    apps[f"{name[0]}/{name[1]}"] = {"anomalous": an, "scored": sc, "rank": r}
+                    apps[_label(name)] = {"anomalous": an, "scored": sc, "rank": r}
         self["apps"] = apps
         return apps
 
