@@ -10,6 +10,7 @@
 """
 
 import json
+import math
 import os
 import sys
 
@@ -53,7 +54,7 @@ def decode(dev, side: str, sel: int):
                 sa, sb = torch.full((64,), ONE, dtype=torch.int32), regs(code)
             D = L.mfma_scale_probe(A.to(dev), B.to(dev), sa.to(dev), sb.to(dev), sel).cpu().double()
             vals = D[:, 5] if side == "A" else D[7, :]
-            exps.append([int(round(float(torch.log2(v)))) + 127 if v > 0 else None for v in vals.tolist()])
+            exps.append([int(round(math.log2(v))) + 127 if v > 0 else None for v in vals.tolist()])
         for i in range(32):
             e0, e1 = exps[0][i], exps[1][i]
             if e0 is None or e1 is None:
