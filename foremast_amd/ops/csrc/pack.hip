@@ -11,12 +11,14 @@
 // The codes are built once on the host (foremast_amd/ops/pack.py) from the
 // same index maps the PyTorch reference layouts use.
 //
-// fp8 (OCP e4m3) segments are block-scaled for the CDNA4 block-scaled MFMA: every
-// 32 consecutive codes (one lane's k block of an A fragment) share the E8M0
-// exponent e = the smallest integer with absmax <= 448 * 2^e (exact, from frexp);
-// the codes are v * 2^-e in e4m3 and the scale bytes (e + 127) follow the codes,
-// lane-major (block b at n + (b % 64) * (n / 2048) + b / 64), so a kernel lane
-// reads its scales as one vector.  One pass: a block is a half wave.
+// fp8 (OCP e4m3) segments are block-scaled for v_mfma_scale_f32_32x32x64_f8f6f4 A
+// fragments laid out [k-step][64 lanes][32 bytes]: the hardware scales row r of a
+// k-step with the E8M0 byte of lane r (measured: scripts/probe_mfma_scale.py), for
+// all 64 k values of the row (lanes r and r + 32), so a block is those two lanes'
+// values.  Its exponent e is the smallest integer with absmax <= 448 * 2^e (exact,
+// from frexp); the codes are v * 2^-e in e4m3, and the scale bytes (e + 127) follow
+// the codes lane-major (k-step s of lane l at n + l * (n / 2048) + s), both lanes of
+// a block carrying it.  One pass: a block is one wave.
 #include "common.h"
 
 struct PackSeg {
@@ -54,20 +56,17 @@ __device__ __forceinline__ int e8m0_exp(float m) {
 __global__ __launch_bounds__(256) void pack_kernel(const PackArgs a) {
   const PackSeg& s = a.seg[blockIdx.y];
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (s.kind == 2) {  // block-scaled fp8: 32-lane halves of the wave are blocks (n % 2048 == 0)
-    const float v = i < s.n ? fetch(a, s, i) : 0.f;
-    float m = fabsf(v);
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, FM_WAVE));
-    const int e = e8m0_exp(m);
-    if (i >= s.n) return;
+  if (s.kind == 2) {  // block-scaled fp8 (n % 2048 == 0): wave w = (k-step w / 32, row w % 32)
+    const int w = i >> 6, t = i & 63;
+    const int step = w >> 5, lane = (w & 31) + 32 * (t >> 5);
+    const int e_idx = ((step << 6) + lane) * 32 + (t & 31);
+    const float v = e_idx < s.n ? fetch(a, s, e_idx) : 0.f;
+    const int e = e8m0_exp(wave_max(fabsf(v)));
+    if (e_idx >= s.n) return;
     const int q = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v, -e), 0.f, 0, false);
     unsigned char* out = (unsigned char*)s.out;
-    out[i] = (unsigned char)(q & 0xff);
-    if ((i & 31) == 0) {
-      const int b = i >> 5, per_lane = s.n >> 11;
-      out[s.n + (b & 63) * per_lane + (b >> 6)] = (unsigned char)(e + 127);
-    }
+    out[e_idx] = (unsigned char)(q & 0xff);
+    if ((t & 31) == 0) out[s.n + lane * (s.n >> 11) + step] = (unsigned char)(e + 127);
     return;
   }
   if (i >= s.n) return;

@@ -8,9 +8,9 @@ step, each longer on the host than on the GPU.  Here every output element is
 described by one int32 *code* (which parameter, which offset, which
 multiplier class) built once from the reference index maps, and one native
 launch produces every segment.  fp8 segments are block-scaled for the CDNA4
-``v_mfma_scale_f32_32x32x64_f8f6f4``: every 32 consecutive elements (one lane's
-k block of an A fragment) share an E8M0 scale, the smallest power of two that
-brings the block's absolute maximum within e4m3's 448 (:func:`e8m0_blocks`).
+``v_mfma_scale_f32_32x32x64_f8f6f4``: the 64 values of one A-fragment row in one
+k-step (lanes r and r + 32) share an E8M0 scale, the smallest power of two that
+brings their absolute maximum within e4m3's 448 (:func:`e8m0_blocks`).
 
 :func:`reference_gather` evaluates the same codes with torch (CPU tests and
 the non-GPU path).
@@ -39,12 +39,12 @@ class PackArgs(C.Structure):
     _fields_ = [("src", C.c_void_p * 8), ("seg", PackSeg * 8), ("nseg", C.c_int), ("_pad", C.c_int)]
 
 
-FP8_BLOCK = 32
-FP8_LANES = 64   # scales are stored lane-major: block b's at (b % 64) * (blocks / 64) + b // 64
+FP8_CHUNK = 32   # e4m3 bytes one lane holds per MFMA k-step (v_mfma_scale_f32_32x32x64_f8f6f4: K = 64)
+FP8_LANES = 64   # scales are stored lane-major: step s of lane l at (l * steps + s)
 
 
 def e8m0_blocks(v: torch.Tensor):
-    """Block-scaled e4m3 of ``v [blocks, 32]``: (codes uint8 ``[blocks, 32]``, E8M0
+    """Block-scaled e4m3 of ``v [blocks, k]``: (codes uint8 ``[blocks, k]``, E8M0
     uint8 ``[blocks]``).  The block exponent e is the smallest integer with
     ``absmax <= 448 * 2^e`` (from the exact frexp of absmax, as csrc/pack.hip
     computes it), the codes are ``v * 2^-e`` rounded to e4m3, the scale byte
@@ -57,9 +57,24 @@ def e8m0_blocks(v: torch.Tensor):
     return q, (e + 127).to(torch.uint8)
 
 
+def fp8_blocks_lane_major(v: torch.Tensor) -> torch.Tensor:
+    """A block-scaled fp8 segment of the values ``v`` laid out as MFMA A fragments
+    ``[steps, 64 lanes, 32]`` (codes, then the scales lane-major).  The hardware takes
+    row r's scale of a k-step from lane r (measured: ``scripts/probe_mfma_scale.py``),
+    for the row's whole K = 64 -- lanes r and r + 32 -- so a scale block is those two
+    lanes' 64 values; both lanes carry its byte."""
+    steps = v.numel() // (FP8_LANES * FP8_CHUNK)
+    g = v.reshape(steps, 2, 32, FP8_CHUNK).permute(0, 2, 1, 3).reshape(steps * 32, 2 * FP8_CHUNK)
+    q, sc = e8m0_blocks(g)
+    q = q.view(steps, 32, 2, FP8_CHUNK).permute(0, 2, 1, 3).reshape(-1)
+    lane_sc = sc.view(steps, 1, 32).expand(steps, 2, 32).reshape(steps, FP8_LANES)   # [steps, lane]
+    return torch.cat([q, lane_sc.t().reshape(-1)])
+
+
 def fp8_segment_bytes(n: int) -> int:
-    """Bytes of a block-scaled fp8 segment of n codes: the codes, then one scale per block."""
-    return n + n // FP8_BLOCK
+    """Bytes of a block-scaled fp8 segment of n codes: the codes, then one scale byte per
+    (k-step, lane)."""
+    return n + n // FP8_CHUNK
 
 
 nat.register("fm_pack", [C.POINTER(PackArgs), C.c_void_p])
@@ -116,8 +131,8 @@ class Packer:
         if len(self.segs) == 8:
             raise ValueError("at most 8 pack segments")
         n = code.numel()
-        if kind == KIND_FP8 and n % (FP8_BLOCK * FP8_LANES):
-            raise ValueError(f"an fp8 segment holds whole lanes of {FP8_BLOCK}-element blocks")
+        if kind == KIND_FP8 and n % (FP8_CHUNK * FP8_LANES):
+            raise ValueError(f"an fp8 segment holds whole k-steps of {FP8_LANES} x {FP8_CHUNK} A-fragment bytes")
         want_n = fp8_segment_bytes(n) if kind == KIND_FP8 else n
         if out.numel() != want_n or not out.is_contiguous():
             raise ValueError("pack output must be contiguous with one element per code (fp8: plus the scales)")
@@ -165,10 +180,3 @@ class Packer:
                 s.out.copy_(v.to(torch.bfloat16))
             else:
                 s.out.copy_(fp8_blocks_lane_major(v))
-
-
-def fp8_blocks_lane_major(v: torch.Tensor) -> torch.Tensor:
-    """A block-scaled fp8 segment of the values ``v`` (codes, then the scales lane-major)."""
-    q, sc = e8m0_blocks(v.reshape(-1, FP8_BLOCK))
-    per_lane = sc.numel() // FP8_LANES
-    return torch.cat([q.reshape(-1), sc.view(per_lane, FP8_LANES).t().reshape(-1)])
