@@ -90,3 +90,47 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def configs():
+    """Max |D - want| for full-data products under several scale-register fillings."""
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(3)
+    A = torch.randint(-8, 9, (32, 64), generator=g).float()
+    B = torch.randint(-8, 9, (64, 32), generator=g).float()
+    sa = torch.randint(120, 135, (32,), generator=g)
+    sb = torch.randint(120, 135, (32,), generator=g)
+
+    def regs(s, sel, other, hi):
+        out = []
+        for lane in range(64):
+            v = 0
+            for j in range(4):
+                if lane < 32:
+                    b = int(s[lane]) if j == sel else other
+                else:
+                    b = hi if hi is not None else (int(s[lane - 32]) if j == sel else other)
+                v |= (b & 0xFF) << (8 * j)
+            out.append(v - (1 << 32) if v >= 1 << 31 else v)
+        return torch.tensor(out, dtype=torch.int32, device=dev)
+    one = torch.full((64,), ONE, dtype=torch.int32, device=dev)
+    for sel in (0, 1):
+        fa = torch.exp2(sa.double() - 127)[:, None]
+        fb = torch.exp2(sb.double() - 127)[None, :]
+        cases = {
+            "A_rows_other127_hi_same": (regs(sa, sel, 127, None), one, A.double() * fa @ B.double()),
+            "A_rows_other127_hi127": (regs(sa, sel, 127, 127), one, A.double() * fa @ B.double()),
+            "A_rows_decoy_hi_decoy": (regs(sa, sel, 0x55, 0x55), one, A.double() * fa @ B.double()),
+            "B_cols_other127_hi127": (one, regs(sb, sel, 127, 127), A.double() @ (B.double() * fb)),
+            "both_other127_hi127": (regs(sa, sel, 127, 127), regs(sb, sel, 127, 127), (A.double() * fa) @ (B.double() * fb)),
+            "both_decoys": (regs(sa, sel, 0x55, 0x55), regs(sb, sel, 0x66, 0x66), (A.double() * fa) @ (B.double() * fb)),
+        }
+        for name, (ra, rb, want) in cases.items():
+            D = L.mfma_scale_probe(A.to(dev), B.to(dev), ra, rb, sel).cpu().double()
+            err = float((D - want).abs().max())
+            ratio = (D / want.where(want != 0, torch.ones(()))).flatten()[:6].tolist()
+            print(json.dumps({"sel": sel, "case": name, "max_abs_err": err, "ratio_sample": ratio}), flush=True)
+
+
+if __name__ == "__main__" and os.environ.get("PROBE_CONFIGS"):
+    configs()
