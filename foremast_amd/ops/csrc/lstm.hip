@@ -9,7 +9,7 @@
 //  * gates^T [256 x 32] = Waug^T [256 x 80] · [h; x_t; 1] [80 x 32] on
 //    v_mfma_f32_32x32x16_bf16 (8 row tiles x 5 k-steps = 40 MFMAs per step), or in
 //    fp8 on v_mfma_scale_f32_32x32x64_f8f6f4 (8 row tiles x 2 k-steps of K = 64 =
-//    16 MFMAs per step, an E8M0 scale per (gate row, k-step of 64) of the
+//    16 MFMAs per step, an E8M0 scale per (gate row, 32-k block) of the
 //    weights).  The input projection and bias ride in the last k-step (x at
 //    k=64..64+F-1, bias at k=71), so no VALU matmul is needed for them.
 //  * The 256 gate rows are permuted host-side so that in tile t, accumulator

@@ -69,7 +69,7 @@ constexpr int FRAG_BYTES_BF16 = TILES * KSTEPS * 64 * 16;  // 40 KB
 constexpr int KSTEPS_FP8 = 2;
 constexpr int FRAG_BYTES_FP8 = TILES * KSTEPS_FP8 * 64 * 32;    // 32 KB of e4m3
 constexpr int SCALE_BYTES_FP8 = TILES * KSTEPS_FP8 * 64;        // E8M0 per (tile, k-step, lane): [lane][16]
-                                                                // (lane r and r + 32: row r's scale)
+                                                                // (lane r + 32 b: k block b of row r)
 // h enters the B operand as h * 2^8 (|h| <= 1: e4m3 normals reach down to |h| = 2^-14), scaled
 // back by the MFMA (E8M0 127 - 8); inputs and bias enter unscaled (127).  Replicated in all
 // four bytes: any op_sel byte reads it.
@@ -129,10 +129,11 @@ __device__ __forceinline__ unsigned pack_fp8x4(float a, float b, float c, float 
 }
 
 // ---- CDNA4 block-scaled fp8: v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3 A and B) ----------
-// lane l holds row (A) / column (B) l & 31 and k = 32 (l >> 5) + j in byte j of its 8-VGPR
-// fragment; row r (column c) is scaled by 2^(s - 127), s = byte op_sel of LANE r's (c's)
-// scale register, for all 64 k of the instruction (lanes 32..63's scale registers are
-// not read) -- measured by scripts/probe_mfma_scale.py, pinned by tests/test_lstm.py.
+// lane l holds row (A) / column (B) l & 31 in its 8-VGPR fragment, A and B with the same
+// byte <-> k order; measured on the MI355X (scripts/probe_mfma_scale.py, pinned by
+// tests/test_lstm.py): bytes 16 b .. 16 b + 15 of lanes r and r + 32 form k block b of
+// row r (column c), scaled by 2^(s - 127), s = byte op_sel of lane r + 32 b's (c + 32 b's)
+// scale register.
 typedef int f8x32 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ f8x32 pack_fp8x32(const float (&v)[32]) {

@@ -12,13 +12,12 @@
 // same index maps the PyTorch reference layouts use.
 //
 // fp8 (OCP e4m3) segments are block-scaled for v_mfma_scale_f32_32x32x64_f8f6f4 A
-// fragments laid out [k-step][64 lanes][32 bytes]: the hardware scales row r of a
-// k-step with the E8M0 byte of lane r (measured: scripts/probe_mfma_scale.py), for
-// all 64 k values of the row (lanes r and r + 32), so a block is those two lanes'
-// values.  Its exponent e is the smallest integer with absmax <= 448 * 2^e (exact,
-// from frexp); the codes are v * 2^-e in e4m3, and the scale bytes (e + 127) follow
-// the codes lane-major (k-step s of lane l at n + l * (n / 2048) + s), both lanes of
-// a block carrying it.  One pass: a block is one wave.
+// fragments laid out [k-step][64 lanes][32 bytes].  Measured on the MI355X
+// (scripts/probe_mfma_scale.py): bytes 16 b .. 16 b + 15 of lanes r and r + 32 are one
+// 32-value k block of row r, scaled by the E8M0 byte of lane r + 32 b.  A block's
+// exponent e is the smallest integer with absmax <= 448 * 2^e (exact, from frexp); the
+// codes are v * 2^-e in e4m3, and the scale bytes (e + 127) follow the codes lane-major
+// (k-step s of lane l at n + l * (n / 2048) + s).  One pass: a block is a half wave.
 #include "common.h"
 
 struct PackSeg {
@@ -56,17 +55,21 @@ __device__ __forceinline__ int e8m0_exp(float m) {
 __global__ __launch_bounds__(256) void pack_kernel(const PackArgs a) {
   const PackSeg& s = a.seg[blockIdx.y];
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (s.kind == 2) {  // block-scaled fp8 (n % 2048 == 0): wave w = (k-step w / 32, row w % 32)
-    const int w = i >> 6, t = i & 63;
-    const int step = w >> 5, lane = (w & 31) + 32 * (t >> 5);
-    const int e_idx = ((step << 6) + lane) * 32 + (t & 31);
+  if (s.kind == 2) {  // block-scaled fp8 (n % 2048 == 0): half wave = block (k-step, row r, k block b)
+    const int blk = i >> 5, u = i & 31;
+    const int step = blk >> 6, r = blk & 31, b = (blk >> 5) & 1;
+    const int lane = r + 32 * (u >> 4), j = 16 * b + (u & 15);
+    const int e_idx = ((step << 6) + lane) * 32 + j;
     const float v = e_idx < s.n ? fetch(a, s, e_idx) : 0.f;
-    const int e = e8m0_exp(wave_max(fabsf(v)));
+    float m = fabsf(v);
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, FM_WAVE));
+    const int e = e8m0_exp(m);
     if (e_idx >= s.n) return;
     const int q = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v, -e), 0.f, 0, false);
     unsigned char* out = (unsigned char*)s.out;
     out[e_idx] = (unsigned char)(q & 0xff);
-    if ((t & 31) == 0) out[s.n + lane * (s.n >> 11) + step] = (unsigned char)(e + 127);
+    if (u == 0) out[s.n + (r + 32 * b) * (s.n >> 11) + step] = (unsigned char)(e + 127);
     return;
   }
   if (i >= s.n) return;

@@ -16,8 +16,8 @@ H = 64
 TILES, KSTEPS, KAUG = 8, 5, 80
 BIAS_K = 71  # bias column of the augmented weight (k-step 4, lane half 0, element 7)
 # fp8 scoring (CDNA4 v_mfma_scale_f32_32x32x64_f8f6f4): 2 k-steps of K = 64 per gate tile,
-# fragments [TILES][2][64][32] e4m3 + one E8M0 scale per (tile, k-step, gate row), stored
-# lane-major [64 lanes][16] (lanes r and r + 32 both carry row r's byte)
+# fragments [TILES][2][64][32] e4m3 + one E8M0 scale per (tile, k-step, gate row, 32-k block),
+# stored lane-major [64 lanes][16] (block b of row r in lane r + 32 b)
 KSTEPS_FP8 = 2
 FP8_FRAG_BYTES = TILES * KSTEPS_FP8 * 64 * 32
 FP8_SCALE_BYTES = TILES * KSTEPS_FP8 * 64
@@ -169,7 +169,7 @@ def _fp8_index(device) -> torch.Tensor:
 
 def pack_fp8(A: torch.Tensor) -> torch.Tensor:
     """``[256, 80]`` augmented weight → the fp8 kernel's uint8 buffer: block-scaled
-    e4m3 fragments ``[TILES, 2, 64, 32]`` (one scale per gate row and k-step of 64),
+    e4m3 fragments ``[TILES, 2, 64, 32]`` (one scale per gate row and 32-k block),
     then the E8M0 scales ``[64 lanes, 16]``
     (:func:`~foremast_amd.ops.pack.fp8_blocks_lane_major`)."""
     from .pack import fp8_blocks_lane_major

@@ -8,9 +8,9 @@ step, each longer on the host than on the GPU.  Here every output element is
 described by one int32 *code* (which parameter, which offset, which
 multiplier class) built once from the reference index maps, and one native
 launch produces every segment.  fp8 segments are block-scaled for the CDNA4
-``v_mfma_scale_f32_32x32x64_f8f6f4``: the 64 values of one A-fragment row in one
-k-step (lanes r and r + 32) share an E8M0 scale, the smallest power of two that
-brings their absolute maximum within e4m3's 448 (:func:`e8m0_blocks`).
+``v_mfma_scale_f32_32x32x64_f8f6f4``: each 32-value k block of an A-fragment row
+shares an E8M0 scale, the smallest power of two that brings its absolute maximum
+within e4m3's 448 (:func:`e8m0_blocks`, :func:`fp8_blocks_lane_major`).
 
 :func:`reference_gather` evaluates the same codes with torch (CPU tests and
 the non-GPU path).
@@ -59,15 +59,15 @@ def e8m0_blocks(v: torch.Tensor):
 
 def fp8_blocks_lane_major(v: torch.Tensor) -> torch.Tensor:
     """A block-scaled fp8 segment of the values ``v`` laid out as MFMA A fragments
-    ``[steps, 64 lanes, 32]`` (codes, then the scales lane-major).  The hardware takes
-    row r's scale of a k-step from lane r (measured: ``scripts/probe_mfma_scale.py``),
-    for the row's whole K = 64 -- lanes r and r + 32 -- so a scale block is those two
-    lanes' 64 values; both lanes carry its byte."""
+    ``[steps, 64 lanes, 32 bytes]`` (codes, then the scales lane-major).  Measured on
+    the MI355X (``scripts/probe_mfma_scale.py``): bytes 16 b .. 16 b + 15 of lanes r
+    AND r + 32 form one 32-value k block of row r, scaled by the byte in lane r + 32 b's
+    scale register; so each block's E8M0 is stored in lane r + 32 b."""
     steps = v.numel() // (FP8_LANES * FP8_CHUNK)
-    g = v.reshape(steps, 2, 32, FP8_CHUNK).permute(0, 2, 1, 3).reshape(steps * 32, 2 * FP8_CHUNK)
+    g = v.reshape(steps, 2, 32, 2, 16).permute(0, 2, 3, 1, 4).reshape(steps * 64, 32)   # [(step, r, b), (h, j)]
     q, sc = e8m0_blocks(g)
-    q = q.view(steps, 32, 2, FP8_CHUNK).permute(0, 2, 1, 3).reshape(-1)
-    lane_sc = sc.view(steps, 1, 32).expand(steps, 2, 32).reshape(steps, FP8_LANES)   # [steps, lane]
+    q = q.view(steps, 32, 2, 2, 16).permute(0, 3, 1, 2, 4).reshape(-1)
+    lane_sc = sc.view(steps, 32, 2).permute(0, 2, 1).reshape(steps, FP8_LANES)         # lane = r + 32 b
     return torch.cat([q, lane_sc.t().reshape(-1)])
 
 

@@ -406,8 +406,8 @@ def test_block_scaled_fp8_pack_layout_and_precision(F):
     uses (k-step 0: the lane half's 32 h-register units; k-step 1: inputs, then the bias
     at byte 7); dequantised with their lane-major E8M0 scales they reproduce the weights
     within e4m3's half-ulp (2^-4 relative; subnormals: a 2^-10 share of the row's
-    maximum), and every (k-step, row) scale is the smallest power of two that fits the
-    row's maximum in 448."""
+    maximum), and every (row, 32-k block) scale is the smallest power of two that fits
+    the block's maximum in 448."""
     torch.manual_seed(11)
     m = lstm_ae.LSTMAutoencoder(F, 64)
     A = L._augment(m.enc_w_hh, m.enc_b, m.enc_w_ih, F)
@@ -416,8 +416,10 @@ def test_block_scaled_fp8_pack_layout_and_precision(F):
     buf = L.pack_fp8(A)
     assert buf.dtype == torch.uint8 and buf.numel() == L.FP8_FRAG_BYTES + L.FP8_SCALE_BYTES
     q = buf[:L.FP8_FRAG_BYTES].view(torch.float8_e4m3fn).float().view(L.TILES, 2, 64, 32)
-    sc = buf[L.FP8_FRAG_BYTES:].view(64, L.TILES * 2).t().reshape(L.TILES, 2, 64).float()
-    deq = q * torch.exp2(sc - 127)[..., None]
+    sc = buf[L.FP8_FRAG_BYTES:].view(64, L.TILES * 2).t().reshape(L.TILES, 2, 2, 32).float()  # [t, s, b, r]
+    lanes = torch.arange(64)
+    f = torch.exp2(sc - 127)[:, :, (torch.arange(32) // 16)[None, :], (lanes & 31)[:, None]]   # [t, s, lane, j]
+    deq = q * f
     rows = L.gate_row_perm()
     units = L.h_units(torch.arange(64) >> 5)
     for t in (0, 3, 7):
@@ -429,14 +431,12 @@ def test_block_scaled_fp8_pack_layout_and_precision(F):
             np.testing.assert_allclose(deq[t, 1, lane, :8].numpy(), want1.numpy(), rtol=2 ** -4,
                                        atol=float(want1.abs().max()) * 2 ** -10 + 1e-30)
             assert float(deq[t, 1, lane, 8:].abs().max()) == 0.0
-    # one scale per (tile, k-step, row): lanes r and r + 32 carry the same byte, the smallest
-    # power of two with the row's 64-value absmax <= 448 * scale
+    # one scale per (tile, k-step, row r, block b) in lane r + 32 b: bytes 16 b .. 16 b + 15 of
+    # lanes r and r + 32; the smallest power of two with the block's absmax <= 448 * scale
     vals = torch.where(L._fp8_index("cpu") >= 0, A.flatten()[L._fp8_index("cpu").clamp(min=0)],
-                       torch.zeros(())).view(L.TILES * 2, 2, 32, 32)
-    blk = vals.abs().amax(dim=(1, 3)).reshape(-1)                               # [(t, s), r]
-    sc_ts = buf[L.FP8_FRAG_BYTES:].view(64, L.TILES * 2).t().float() - 127       # [(t, s), lane]
-    assert torch.equal(sc_ts[:, :32], sc_ts[:, 32:])
-    s_flat = sc_ts[:, :32].reshape(-1)
+                       torch.zeros(())).view(L.TILES * 2, 2, 32, 2, 16)        # [(t, s), h, r, b, j]
+    blk = vals.abs().amax(dim=(1, 4)).permute(0, 2, 1).reshape(-1)             # [(t, s), b, r]
+    s_flat = (buf[L.FP8_FRAG_BYTES:].view(64, L.TILES * 2).t().float() - 127).reshape(-1)  # [(t, s), lane]
     nz = blk > 0
     assert bool((blk[nz] <= 448 * torch.exp2(s_flat[nz])).all())
     assert bool((blk[nz] > 448 * torch.exp2(s_flat[nz] - 1)).all())
@@ -547,28 +547,31 @@ def test_lstm_level_kernel_matches_cpu():
 def test_block_scaled_fp8_mfma_lane_map(sel):
     """The CDNA4 block-scaled MFMA (v_mfma_scale_f32_32x32x64_f8f6f4, e4m3) under the maps
     the fp8 LSTM kernel relies on, on exact data (small integers, exact in e4m3; a
-    different power of two per row of A and per column of B; asymmetric, so a transposed
-    map cannot pass): lane l holds row / column l & 31 at k = 32 (l >> 5) + j, and the
-    scale of row r (column c) for the whole K = 64 is byte ``sel`` of lane r's (c's)
-    scale register -- lanes 32..63 hold decoys that must not matter
-    (scripts/probe_mfma_scale.py decoded this map)."""
+    different power of two per (row, k block) of A and (column, k block) of B; asymmetric,
+    so a transposed map cannot pass): lane l holds row / column l & 31 (byte j at
+    k = 32 (l >> 5) + j, the same for A and B), and bytes 16 b .. 16 b + 15 of lanes r and
+    r + 32 form k block b, scaled by byte ``sel`` of lane r + 32 b's scale register
+    (scripts/probe_mfma_scale.py decoded this map; the other bytes hold decoys)."""
     dev = torch.device("cuda")
     g = torch.Generator().manual_seed(7 + sel)
     A = torch.randint(-8, 9, (32, 64), generator=g).float()
     B = torch.randint(-8, 9, (64, 32), generator=g).float()
     A[3, :] += torch.arange(64) % 5           # asymmetric rows / columns
     B[:, 5] += torch.arange(64) % 3
-    sa = torch.randint(120, 135, (32,), generator=g)
-    sb = torch.randint(120, 135, (32,), generator=g)
+    sa = torch.randint(120, 135, (32, 2), generator=g)   # [row, block]
+    sb = torch.randint(120, 135, (32, 2), generator=g)   # [column, block]
 
-    def regs(s, decoy):
+    def regs(s, decoy):   # lane r + 32 b: the scale of (r, b) in byte sel
         out = []
         for lane in range(64):
             v = 0
             for j in range(4):
-                v |= (int(s[lane]) if (j == sel and lane < 32) else decoy) << (8 * j)
+                v |= (int(s[lane & 31, lane >> 5]) if j == sel else decoy) << (8 * j)
             out.append(v - (1 << 32) if v >= 1 << 31 else v)
         return torch.tensor(out, dtype=torch.int32, device=dev)
     got = L.mfma_scale_probe(A.to(dev), B.to(dev), regs(sa, 0x55), regs(sb, 0x66), sel).cpu().double()
-    want = (A.double() * torch.exp2(sa.double() - 127)[:, None]) @ (B.double() * torch.exp2(sb.double() - 127)[None, :])
+    blk = (torch.arange(64) % 32) // 16                    # k block of probe index k
+    fa = torch.exp2(sa.double() - 127)[:, blk]             # [32, 64]
+    fb = torch.exp2(sb.double() - 127)[:, blk].t()         # [64, 32]
+    want = (A.double() * fa) @ (B.double() * fb)
     torch.testing.assert_close(got, want, rtol=1e-6, atol=1e-6)
