@@ -62,6 +62,7 @@ class RankArgs(C.Structure):
         ("min_mw", I), ("min_wilcoxon", I), ("min_kruskal", I),
         ("pvals", P), ("differs", P), ("counts", P),
         ("pods_b", I), ("pods_c", I), ("min_friedman", I), ("p_friedman", P), ("base_mean", P),
+        ("z_crit", F), ("_pad", I),
     ]
 
 

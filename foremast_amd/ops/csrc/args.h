@@ -112,6 +112,10 @@ struct RankArgs {
   int min_friedman;        // complete blocks needed
   float* p_friedman;       // [N, 2] (p, complete blocks) or null; computed when set or mode == 6
   float* base_mean;        // [N] mean of the valid baseline values (NaN if none) or null
+  // > 0: two-sided normal quantile of alpha (isf(alpha / 2), fp64 on the host).  Without
+  // pvals, MW / Wilcoxon / Kruskal decide by |z| > z_crit (H > z_crit^2) -- no erfc
+  float z_crit;
+  int _pad;
 };
 
 struct WindowArgs {

@@ -82,6 +82,20 @@ __device__ __forceinline__ float wave_allsum(float v) {
   v += dpp_f<0x143, 0xc, false>(0.f, v);  // row_bcast:31 -> rows 2, 3
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), FM_WAVE - 1));
 }
+template <int CTRL, int RM>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, RM, 0xf, false);
+}
+// integer all-lane sum (exact; the same DPP pattern as wave_allsum)
+__device__ __forceinline__ int wave_allsum_i(int v) {
+  v += dpp_i<0x111, 0xf>(v);
+  v += dpp_i<0x112, 0xf>(v);
+  v += dpp_i<0x114, 0xf>(v);
+  v += dpp_i<0x118, 0xf>(v);
+  v += dpp_i<0x142, 0xa>(v);
+  v += dpp_i<0x143, 0xc>(v);
+  return __builtin_amdgcn_readlane(v, FM_WAVE - 1);
+}
 __device__ __forceinline__ float wave_allmax(float v) {
   const float lo = -__builtin_huge_valf();
   v = fmaxf(v, dpp_f<0x111, 0xf, false>(lo, v));

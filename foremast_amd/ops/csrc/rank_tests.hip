@@ -198,32 +198,34 @@ __device__ __forceinline__ void small_ranks(float bv, float cv, float dv, float*
   const float* sb = s;
   const float* sc = s + FM_WAVE;
   const float* sd = s + 2 * FM_WAVE;
-  float r1 = 0.f, t = 0.f, tp = 0.f, tm = 0.f, wt = 0.f;
+  // integer accumulators (ranks doubled): 2 R1 <= 12210 and 2 Tp <= 4160 share one exact
+  // reduction; Tm = np (np + 1) / 2 - Tp needs none
+  int r1x2 = 0, t = 0, tpx2 = 0, wt = 0;
   if (bv == bv) {
     const int lb = bound64<false>(sb, bv), ub = min(bound64<true>(sb, bv), n1);
     const int lc = bound64<false>(sc, bv), uc = min(bound64<true>(sc, bv), n2);
     const int eq = (ub - lb) + (uc - lc);
-    r1 = (float)(lb + lc) + 0.5f * (float)(eq + 1);
-    t += (float)(eq * eq - 1);
+    r1x2 = 2 * (lb + lc) + eq + 1;
+    t += eq * eq - 1;
   }
   if (cv == cv) {
     const int lb = bound64<false>(sb, cv), ub = min(bound64<true>(sb, cv), n1);
     const int lc = bound64<false>(sc, cv), uc = min(bound64<true>(sc, cv), n2);
     const int eq = (ub - lb) + (uc - lc);
-    t += (float)(eq * eq - 1);
+    t += eq * eq - 1;
   }
   if (ad == ad) {
     const int lb = bound64<false>(sd, ad), ub = min(bound64<true>(sd, ad), nd);
     const int eq = ub - lb;
-    const float r = (float)lb + 0.5f * (float)(eq + 1);
-    if (dv > 0.f) tp = r; else tm = r;
-    wt = (float)(eq * eq - 1);
+    if (dv > 0.f) tpx2 = 2 * lb + eq + 1;
+    wt = eq * eq - 1;
   }
-  R1 = wave_allsum(r1);
-  tie = wave_allsum(t);
-  Tp = wave_allsum(tp);
-  Tm = wave_allsum(tm);
-  wtie = wave_allsum(wt);
+  const int rr = wave_allsum_i(r1x2 | (tpx2 << 16));
+  R1 = 0.5f * (float)(rr & 0xffff);
+  Tp = 0.5f * (float)(rr >> 16);
+  Tm = 0.5f * (float)(nd * (nd + 1)) - Tp;
+  tie = (float)wave_allsum_i(t);
+  wtie = (float)wave_allsum_i(wt);
 }
 
 template <bool SMALL>
@@ -252,9 +254,11 @@ __global__ __launch_bounds__(256) void rank_tests_kernel(const RankArgs a) {
       const float d = cv - bv;
       if (d == d && d != 0.f) dv = d;
     }
-    n1 = wave_allsum(bv == bv ? 1.f : 0.f);
-    n2 = wave_allsum(cv == cv ? 1.f : 0.f);
-    np = wave_allsum(dv == dv ? 1.f : 0.f);
+    // one exact integer reduction for the three counts (7 bits each)
+    const int cnt = wave_allsum_i((bv == bv ? 1 : 0) | (cv == cv ? 1 << 8 : 0) | (dv == dv ? 1 << 16 : 0));
+    n1 = (float)(cnt & 0xff);
+    n2 = (float)((cnt >> 8) & 0xff);
+    np = (float)((cnt >> 16) & 0xff);
     sb = a.base_mean ? wave_allsum(bv == bv ? bv : 0.f) : 0.f;
     if (want_fr) {  // Friedman reads the pooled windows staged as the sweep stages them
       for (int i = lane; i < npool4; i += FM_WAVE) x[i] = i < a.nb ? b[i] : (i < npool ? c[i - a.nb] : fm_nan());
@@ -308,6 +312,53 @@ __global__ __launch_bounds__(256) void rank_tests_kernel(const RankArgs a) {
   const float nn = n1 + n2;
 
   if (lane != 0) return;
+  if (!a.pvals && a.z_crit > 0.f && a.mode >= 1 && a.mode <= 5) {
+    // decisions only (the product tick): p < alpha <=> |z| > z_crit, no erfc
+    const float zc = a.z_crit;
+    bool rej_mw = false, rej_w = false, rej_k = false;
+    if (n1 > 0.f && n2 > 0.f) {
+      const float U1 = R1 - n1 * (n1 + 1.f) * 0.5f;
+      const float U = fmaxf(U1, n1 * n2 - U1);
+      const float var = n1 * n2 / 12.f * ((nn + 1.f) - tie / fmaxf(nn * (nn - 1.f), 1.f));
+      const float sd = sqrtf(fmaxf(var, 0.f));
+      rej_mw = sd > 0.f && (U - n1 * n2 * 0.5f - 0.5f) > zc * sd;
+      const float H = 12.f / fmaxf(nn * (nn + 1.f), 1.f) * (R1 * R1 / n1 + R2 * R2 / n2) - 3.f * (nn + 1.f);
+      const float corr = 1.f - tie / fmaxf(nn * nn * nn - nn, 1.f);
+      rej_k = corr > 0.f && fmaxf(H / corr, 0.f) > zc * zc;
+    }
+    if (np > 0.f) {
+      const float T = fminf(Tp, Tm);
+      const float var = np * (np + 1.f) * (2.f * np + 1.f) / 24.f - wtie / 48.f;
+      const float sd = sqrtf(fmaxf(var, 0.f));
+      rej_w = sd > 0.f && fabsf(T - np * (np + 1.f) * 0.25f) > zc * sd;
+    }
+    const float nsmall = fminf(n1, n2);
+    const bool ran_mw = nsmall >= (float)a.min_mw, ran_w = np >= (float)a.min_wilcoxon;
+    const bool ran_k = nsmall >= (float)a.min_kruskal;
+    rej_mw &= ran_mw;
+    rej_w &= ran_w;
+    rej_k &= ran_k;
+    bool d = false;
+    switch (a.mode) {
+      case 1: d = (ran_mw || ran_w || ran_k) && (!ran_mw || rej_mw) && (!ran_w || rej_w) && (!ran_k || rej_k); break;
+      case 2: d = rej_mw || rej_w || rej_k; break;
+      case 3: d = rej_mw; break;
+      case 4: d = rej_w; break;
+      default: d = rej_k; break;
+    }
+    a.differs[n] = d ? 1 : 0;
+    if (a.base_mean) a.base_mean[n] = n1 > 0.f ? sb / n1 : fm_nan();
+    if (a.p_friedman) {
+      a.p_friedman[2 * (long long)n + 0] = p_fr;
+      a.p_friedman[2 * (long long)n + 1] = nblk;
+    }
+    if (a.counts) {
+      a.counts[3 * (long long)n + 0] = n1;
+      a.counts[3 * (long long)n + 1] = n2;
+      a.counts[3 * (long long)n + 2] = np;
+    }
+    return;
+  }
   // Mann-Whitney U (two-sided, continuity, tie-corrected)
   float p_mw = 1.f;
   if (n1 > 0.f && n2 > 0.f) {

@@ -623,6 +623,18 @@ def window_stats(hist: torch.Tensor, head: int, length: int, det: DetectSpec,
     return out
 
 
+_ZC: Dict[float, float] = {}
+
+
+def _z_crit(alpha: float) -> float:
+    """Two-sided normal quantile isf(alpha / 2) (fp64): p < alpha  <=>  |z| > z_crit."""
+    z = _ZC.get(alpha)
+    if z is None:
+        z = _ZC[alpha] = (float(-torch.special.ndtri(torch.tensor(alpha / 2, dtype=torch.float64)))
+                          if 0.0 < alpha < 1.0 else 0.0)
+    return z
+
+
 def rank_tests(base: torch.Tensor, cur: torch.Tensor, mode: int, alpha: float, min_mw: int = 20,
                min_wilcoxon: int = 20, min_kruskal: int = 5, want_pvals: bool = True,
                out: Optional[Dict[str, torch.Tensor]] = None, pods: Optional[Tuple[int, int]] = None,
@@ -674,6 +686,7 @@ def rank_tests(base: torch.Tensor, cur: torch.Tensor, mode: int, alpha: float, m
             out["friedman"] = torch.empty((N, 2), dtype=torch.float32, device=dev)
     a.pods_b, a.pods_c, a.min_friedman = int(pb), int(pc), int(min_friedman)
     a.p_friedman = nat.ptr(out["friedman"]) if fr else 0
+    a.z_crit = _z_crit(float(alpha))
     nat.check(lib.fm_rank_tests(a, nat.stream_handle(dev)), "fm_rank_tests")
     return out
 

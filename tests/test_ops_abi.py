@@ -33,7 +33,7 @@ def test_struct_sizes(lib, name):
     ("DetectArgs", "pw_scale"), ("DetectArgs", "app_stats"), ("DetectArgs", "ld_cur"),
     ("DetectArgs", "anom_count"), ("DetectArgs", "anom_cap"), ("DetectArgs", "thr_lut"), ("DetectArgs", "lut_n"),
     ("DetectArgs", "row_out"), ("DetectArgs", "tick_min"),
-    ("RankArgs", "pvals"), ("RankArgs", "alpha"), ("RankArgs", "p_friedman"), ("RankArgs", "pods_b"), ("WindowArgs", "det"),
+    ("RankArgs", "pvals"), ("RankArgs", "alpha"), ("RankArgs", "p_friedman"), ("RankArgs", "pods_b"), ("RankArgs", "z_crit"), ("WindowArgs", "det"),
     ("BivArgs", "eps"), ("BivArgs", "app_stats"),
 ])
 def test_struct_offsets(lib, name, field):
