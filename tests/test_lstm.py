@@ -574,4 +574,5 @@ def test_block_scaled_fp8_mfma_lane_map(sel):
     fa = torch.exp2(sa.double() - 127)[:, blk]             # [32, 64]
     fb = torch.exp2(sb.double() - 127)[:, blk].t()         # [64, 32]
     want = (A.double() * fa) @ (B.double() * fb)
-    torch.testing.assert_close(got, want, rtol=1e-6, atol=1e-6)
+    # products of different powers of two: the fp32 accumulation rounds (2^-23 relative)
+    torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-6)
