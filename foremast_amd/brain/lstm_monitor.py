@@ -86,7 +86,7 @@ class LstmMonitor:
                  clock=time.time, owns: Optional[Callable[[Dict], bool]] = None, ring_len: Optional[int] = None,
                  features: int = 5, window: Optional[int] = None, hidden: Optional[int] = None,
                  fp8: Optional[bool] = None, train_batch: int = 4096, min_capacity: int = 64, seed: int = 0,
-                 history: Optional[ResidentHistory] = None, decode_threads: int = 8) -> None:
+                 history: Optional[ResidentHistory] = None, decode_threads: Optional[int] = None) -> None:
         from ..promql.client import PromClient
         self.store = store
         self.cfg = cfg or BrainConfig.from_env()

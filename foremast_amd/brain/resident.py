@@ -154,14 +154,14 @@ class ResidentHistory:
     :meth:`row_of`) hashes once per distinct key."""
 
     def __init__(self, prom, device, ring_len: int = 10080, step: float = 60.0, clock=time.time,
-                 chunk_points: int = 1440, apps_per_query: int = 256, decode_threads: int = 8,
+                 chunk_points: int = 1440, apps_per_query: int = 256, decode_threads: Optional[int] = None,
                  min_capacity: int = 64, retain_s: float = 86400.0, dtype: Optional[torch.dtype] = None) -> None:
         self.prom = prom
         self.device = torch.device(device)
         self.R, self.step, self.clock = int(ring_len), float(step), clock
         self.chunk_pts = max(1, int(chunk_points))
         self.apps_per_query = max(1, int(apps_per_query))
-        self.decode_threads = max(1, int(decode_threads))
+        self.decode_threads = max(1, int(decode_threads or native.default_threads()))
         self.min_capacity = max(1, int(min_capacity))
         self.retain_s = float(retain_s)
         self.dtype = dtype or (torch.bfloat16 if self.device.type == "cuda" else torch.float32)

@@ -207,7 +207,7 @@ class RolloutMonitor:
                  worker_id: str = "rollout-0", metrics: Optional[BrainMetrics] = None, step: float = 60.0,
                  window: int = 10, pods: int = 5, clock=time.time, owns: Optional[Callable[[Dict], bool]] = None,
                  history: Optional[ResidentHistory] = None, ring_len: Optional[int] = None,
-                 min_capacity: int = 64, decode_threads: int = 8, apps_per_query: int = 256,
+                 min_capacity: int = 64, decode_threads: Optional[int] = None, apps_per_query: int = 256,
                  claim_limit: int = 100_000) -> None:
         from ..promql.client import PromClient
         self.store = store
@@ -223,7 +223,7 @@ class RolloutMonitor:
         self.P = max(1, int(pods))
         self.season = max(2, int(round(86400.0 / self.step)))
         self.m_detect = max(self.season, HB)
-        self.decode_threads = max(1, int(decode_threads))
+        self.decode_threads = max(1, int(decode_threads or native.default_threads()))
         self.apps_per_query = max(1, int(apps_per_query))
         self.claim_limit = claim_limit
         self.history = history or ResidentHistory(self.prom, self.device, ring_len or self.cfg.ring_len, self.step,

@@ -121,7 +121,7 @@ class StreamingMonitor:
                  device=None, worker_id: str = "stream-0", metrics: Optional[BrainMetrics] = None,
                  ring_len: int = 10080, step: float = 60.0, window: int = 10, clock=time.time,
                  owns: Optional[Callable[[Dict], bool]] = None, history_chunk_points: int = 1440,
-                 apps_per_query: int = 256, min_capacity: int = 64, decode_threads: int = 8) -> None:
+                 apps_per_query: int = 256, min_capacity: int = 64, decode_threads: Optional[int] = None) -> None:
         self.store = store
         self.cfg = cfg or BrainConfig.from_env()
         self.prom = prom or PromClient()
@@ -135,7 +135,7 @@ class StreamingMonitor:
         self.exclude: Optional[Callable[[Dict], bool]] = None  # jobs another resident engine serves (LSTM)
         self.chunk_pts = max(1, int(history_chunk_points))
         self.apps_per_query = max(1, int(apps_per_query))
-        self.decode_threads = max(1, int(decode_threads))  # native threads decoding the responses
+        self.decode_threads = max(1, int(decode_threads or native.default_threads()))  # native threads decoding the responses
         self.min_capacity = min_capacity
         self.jobs: Dict[str, StreamJob] = {}
         self.keys: List[Optional[Key]] = []          # row -> key (None: free row)

@@ -103,6 +103,16 @@ def _load() -> Optional[C.CDLL]:
         return lib
 
 
+def default_threads() -> int:
+    """Native decode threads of a rank: ``FOREMAST_DECODE_THREADS`` (at most 16), else 8.
+    Measured on the MI355X box (16-CPU share): the 77 MB tick of the 100k-series node
+    bench decodes in 1.40 ms on 8 threads and 1.41 ms on 16."""
+    v = os.environ.get("FOREMAST_DECODE_THREADS", "")
+    if v.isdigit() and int(v) > 0:
+        return min(16, int(v))
+    return 8
+
+
 def available() -> bool:
     return _load() is not None
 

@@ -61,8 +61,9 @@ def _ranks_with_ties(x: torch.Tensor, valid: torch.Tensor):
     xi = big[:, :, None]
     xj = big[:, None, :]
     vj = valid[:, None, :]
-    less = ((xj < xi) & vj).sum(2).float()
-    eq = ((xj == xi) & vj).sum(2).float()  # includes self
+    rt = torch.promote_types(x.dtype, torch.float32)
+    less = ((xj < xi) & vj).sum(2).to(rt)
+    eq = ((xj == xi) & vj).sum(2).to(rt)  # includes self
     rank = less + (eq + 1.0) / 2.0
     rank = torch.where(valid, rank, torch.zeros_like(rank))
     # sum over elements of (t_i^2 - 1) equals sum over tie groups of (t^3 - t)
@@ -121,8 +122,9 @@ def friedman_pods(baseline: torch.Tensor, current: torch.Tensor, pods_b: int = 1
 def rank_tests(baseline: torch.Tensor, current: torch.Tensor, pods=None) -> PairwiseResult:
     """All four tests; ``pods = (pods_b, pods_c)`` is the pod-major layout the
     Friedman test blocks on (default: one pod per side)."""
-    b = baseline.float()
-    c = current.float()
+    dt = torch.promote_types(torch.promote_types(baseline.dtype, current.dtype), torch.float32)
+    b = baseline.to(dt)
+    c = current.to(dt)
     N, nb = b.shape
     nc = c.shape[1]
     x = torch.cat([b, c], 1)
@@ -130,11 +132,10 @@ def rank_tests(baseline: torch.Tensor, current: torch.Tensor, pods=None) -> Pair
     in_b = torch.zeros_like(valid)
     in_b[:, :nb] = True
     rank, tie = _ranks_with_ties(x, valid)
-    n1 = valid[:, :nb].sum(1).float()
-    n2 = valid[:, nb:].sum(1).float()
+    n1 = valid[:, :nb].sum(1).to(dt)
+    n2 = valid[:, nb:].sum(1).to(dt)
     n = n1 + n2
     R1 = torch.where(in_b, rank, torch.zeros_like(rank)).sum(1)
-    R2 = torch.where(~in_b, rank, torch.zeros_like(rank)).sum(1)
     one = torch.ones_like(n)
 
     # --- Mann-Whitney U -----------------------------------------------------------
@@ -149,8 +150,10 @@ def rank_tests(baseline: torch.Tensor, current: torch.Tensor, pods=None) -> Pair
     p_mw = torch.where((sd > 0) & (n1 > 0) & (n2 > 0), p_mw, one)
 
     # --- Kruskal-Wallis (2 groups) ------------------------------------------------
-    H = 12.0 / (n * (n + 1)).clamp(min=1) * (R1 * R1 / n1.clamp(min=1) + R2 * R2 / n2.clamp(min=1)) \
-        - 3 * (n + 1)
+    # 12 / (n (n + 1)) sum R_i^2 / n_i - 3 (n + 1) without its cancellation: with
+    # D = R1 - n1 (n + 1) / 2 = -(R2 - n2 (n + 1) / 2), H = 12 D^2 / ((n + 1) n1 n2)
+    D = R1 - n1 * (n + 1) / 2
+    H = 12.0 * D * D / ((n + 1) * n1 * n2).clamp(min=1)
     corr = 1 - tie / (n * n * n - n).clamp(min=1)
     Hc = H / corr.clamp(min=1e-30)
     p_kw = torch.erfc(torch.sqrt(Hc.clamp(min=0) / 2))
@@ -162,7 +165,7 @@ def rank_tests(baseline: torch.Tensor, current: torch.Tensor, pods=None) -> Pair
     dvalid = ~torch.isnan(d) & (d != 0)
     ad = torch.where(dvalid, d.abs(), torch.zeros_like(d))
     wr, wtie = _ranks_with_ties(ad, dvalid)
-    npairs = dvalid.sum(1).float()
+    npairs = dvalid.sum(1).to(dt)
     Tplus = torch.where(dvalid & (d > 0), wr, torch.zeros_like(wr)).sum(1)
     Tminus = torch.where(dvalid & (d < 0), wr, torch.zeros_like(wr)).sum(1)
     Tw = torch.minimum(Tplus, Tminus)

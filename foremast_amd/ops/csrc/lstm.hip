@@ -119,13 +119,22 @@ __device__ __forceinline__ f32x16 mfma_fp8(const f8x32& a, const f8x32& b, f32x1
   return mfma_scaled<TS & 3>(a, b, c, sreg, scale_b);
 }
 
+// fp8 A fragment i: its two 16-byte halves are stored half-major ([i][half][64 lanes][16 B],
+// ops/pack.py fp8_blocks_lane_major), so each ds_read_b128 covers 64 consecutive 16-byte
+// slots; a 32-byte lane stride would conflict 2-way on every fragment read.
+__device__ __forceinline__ f8x32 frag_fp8(const char* w, int i, int lo) {
+  const int4 p = ((const int4*)(w + i * 2048))[lo];
+  const int4 q = ((const int4*)(w + i * 2048 + 1024))[lo];
+  return (f8x32){p.x, p.y, p.z, p.w, q.x, q.y, q.z, q.w};
+}
+
 template <int TP>
-__device__ __forceinline__ void gates_fp8(const f8x32* wl, int lo, const f8x32& hb, const f8x32& xb, const int4& sc,
+__device__ __forceinline__ void gates_fp8(const char* wl, int lo, const f8x32& hb, const f8x32& xb, const int4& sc,
                                           f32x16& acc0, f32x16& acc1) {
-  acc0 = mfma_fp8<(TP * KSTEPS_FP8)>(wl[(TP * KSTEPS_FP8) * 64 + lo], hb, (f32x16){}, sc, SCALE_H);
-  acc1 = mfma_fp8<((TP + 1) * KSTEPS_FP8)>(wl[((TP + 1) * KSTEPS_FP8) * 64 + lo], hb, (f32x16){}, sc, SCALE_H);
-  acc0 = mfma_fp8<(TP * KSTEPS_FP8 + 1)>(wl[(TP * KSTEPS_FP8 + 1) * 64 + lo], xb, acc0, sc, SCALE_ONE);
-  acc1 = mfma_fp8<((TP + 1) * KSTEPS_FP8 + 1)>(wl[((TP + 1) * KSTEPS_FP8 + 1) * 64 + lo], xb, acc1, sc, SCALE_ONE);
+  acc0 = mfma_fp8<(TP * KSTEPS_FP8)>(frag_fp8(wl, TP * KSTEPS_FP8, lo), hb, (f32x16){}, sc, SCALE_H);
+  acc1 = mfma_fp8<((TP + 1) * KSTEPS_FP8)>(frag_fp8(wl, (TP + 1) * KSTEPS_FP8, lo), hb, (f32x16){}, sc, SCALE_H);
+  acc0 = mfma_fp8<(TP * KSTEPS_FP8 + 1)>(frag_fp8(wl, TP * KSTEPS_FP8 + 1, lo), xb, acc0, sc, SCALE_ONE);
+  acc1 = mfma_fp8<((TP + 1) * KSTEPS_FP8 + 1)>(frag_fp8(wl, (TP + 1) * KSTEPS_FP8 + 1, lo), xb, acc1, sc, SCALE_ONE);
 }
 
 // One LSTM recurrence over T steps for this wave's 32 series.
@@ -147,7 +156,7 @@ __device__ __forceinline__ void run_phase(const LstmArgs& a, const void* wlds_v,
     int lo = lane;
     asm volatile("" : "+v"(lo));
     if constexpr (FP8) {
-      const f8x32* wl = (const f8x32*)wlds_v;
+      const char* wl = (const char*)wlds_v;
       constexpr float HS = (float)(1 << ACT_SHIFT);
       f8x32 hb;
 #pragma unroll

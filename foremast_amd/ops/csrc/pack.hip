@@ -12,7 +12,9 @@
 // same index maps the PyTorch reference layouts use.
 //
 // fp8 (OCP e4m3) segments are block-scaled for v_mfma_scale_f32_32x32x64_f8f6f4 A
-// fragments laid out [k-step][64 lanes][32 bytes].  Measured on the MI355X
+// fragments: codes index the logical [k-step][64 lanes][32 bytes]; the output is stored
+// half-major, [k-step][16-byte half][64 lanes][16 bytes], so the kernel's 16-byte LDS
+// reads of a fragment are lane-contiguous (conflict-free).  Measured on the MI355X
 // (scripts/probe_mfma_scale.py): bytes 16 b .. 16 b + 15 of lanes r and r + 32 are one
 // 32-value k block of row r, scaled by the E8M0 byte of lane r + 32 b.  A block's
 // exponent e is the smallest integer with absmax <= 448 * 2^e (exact, from frexp); the
@@ -59,7 +61,8 @@ __global__ __launch_bounds__(256) void pack_kernel(const PackArgs a) {
     const int blk = i >> 5, u = i & 31;
     const int step = blk >> 6, r = blk & 31, b = (blk >> 5) & 1;
     const int lane = r + 32 * (u >> 4), j = 16 * b + (u & 15);
-    const int e_idx = ((step << 6) + lane) * 32 + j;
+    const int e_idx = ((step << 6) + lane) * 32 + j;                       // logical [step][lane][32]
+    const int o_idx = (step << 11) + (b << 10) + lane * 16 + (u & 15);     // stored half-major
     const float v = e_idx < s.n ? fetch(a, s, e_idx) : 0.f;
     float m = fabsf(v);
 #pragma unroll
@@ -68,7 +71,7 @@ __global__ __launch_bounds__(256) void pack_kernel(const PackArgs a) {
     if (e_idx >= s.n) return;
     const int q = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v, -e), 0.f, 0, false);
     unsigned char* out = (unsigned char*)s.out;
-    out[e_idx] = (unsigned char)(q & 0xff);
+    out[o_idx] = (unsigned char)(q & 0xff);
     if (u == 0) out[s.n + (r + 32 * b) * (s.n >> 11) + step] = (unsigned char)(e + 127);
     return;
   }

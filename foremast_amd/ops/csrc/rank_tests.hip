@@ -12,14 +12,15 @@
 // windows (n ~ 20-200) this beats a sort: no data-dependent control flow.
 //
 // Small windows (nb, nc <= 64: the product's 5 pods x 11 minutes = 55 per side) take a
-// sort-and-search path instead (rank_tests_kernel<true>): each lane holds ONE baseline,
-// ONE canary and ONE |d| value; the three 64-element arrays are sorted together by a
-// register bitonic network (21 steps, DPP / ds_swizzle / bpermute exchanges), written to
-// the wave's LDS slice, and every lane finds the pooled rank and tie count of its own
-// values by branchless binary searches (lower / upper bound, 7 LDS reads each) in the
-// sorted arrays: rank = #less(base) + #less(cur) + (#eq(base) + #eq(cur) + 1) / 2.
-// O(n log n) per series with all 64 lanes busy, against the sweep's O(n^2) with
-// 112 of 128 lane slots (the sweep is VALU-issue bound: ~5.6 instructions per pair).
+// sort-and-scan path instead (rank_tests_kernel<true>): each lane holds ONE baseline,
+// ONE canary and ONE |d| key; the three 64-key arrays are sorted together by a register
+// bitonic network (21 steps of one exchange + one v_med3_u32 per array), and every
+// statistic is summed per run of equal keys at the run's last lane (run starts by a
+// DPP max-scan): R1 from n1 (n1 + 1) / 2 plus the baseline runs' canary counts (one
+// lower / upper bound search in the sorted canary keys), the pooled tie term from the
+// runs' lengths, Wilcoxon's rank sums from run positions and a prefix count of the
+// positive differences.  Integer and exact; ~100 us per 100k rows where the sweep below
+// takes 250 (scripts/bench_rank.py).
 #include "common.h"
 #include <stdlib.h>
 #include "args.h"
@@ -135,97 +136,161 @@ __device__ __forceinline__ void friedman_wave(const RankArgs& a, const float* x,
   }
 }
 
-// ---- small-window path: register bitonic sort + binary searches ------------------
+// ---- small-window path: register bitonic sort, run scans, one cross search -------------
+// All three arrays are sorted as monotone u32 keys: a float v maps to its bit pattern
+// with the sign bit flipped (negatives: all bits), -0 folded onto +0; the |d| array is
+// keyed (bits(|d|) << 1) | (d > 0) so equal magnitudes stay adjacent whatever their
+// signs.  Padding is 0xffffffff, above every key.
+__device__ __forceinline__ unsigned fkey(float v) {
+  const unsigned u = __float_as_uint(v == 0.f ? 0.f : v);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__device__ __forceinline__ unsigned med3u(unsigned a, unsigned b, unsigned c) {
+  unsigned r;
+  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 // lane ^ J exchange: DPP quad permutes for 1 / 2, ds_swizzle (bit mode, 32-lane groups)
 // for 4..16, a bpermute for 32.
 template <int J>
-__device__ __forceinline__ float xor_lane(float v) {
-  const int x = __float_as_int(v);
-  if constexpr (J == 1) return __int_as_float(__builtin_amdgcn_mov_dpp(x, 0xB1, 0xf, 0xf, false));
-  else if constexpr (J == 2) return __int_as_float(__builtin_amdgcn_mov_dpp(x, 0x4E, 0xf, 0xf, false));
-  else if constexpr (J < 32) return __int_as_float(__builtin_amdgcn_ds_swizzle(x, (J << 10) | 0x1F));
-  else return __shfl_xor(v, 32, FM_WAVE);
+__device__ __forceinline__ unsigned xor_lane(unsigned v) {
+  const int x = (int)v;
+  if constexpr (J == 1) return (unsigned)__builtin_amdgcn_mov_dpp(x, 0xB1, 0xf, 0xf, false);
+  else if constexpr (J == 2) return (unsigned)__builtin_amdgcn_mov_dpp(x, 0x4E, 0xf, 0xf, false);
+  else if constexpr (J < 32) return (unsigned)__builtin_amdgcn_ds_swizzle(x, (J << 10) | 0x1F);
+  else return (unsigned)__shfl_xor(x, 32, FM_WAVE);
 }
 
+// One compare-exchange step of the bitonic network on three arrays: med3(a, partner, 0)
+// is the min and med3(a, partner, ~0) the max, so a step is one VALU per array plus the
+// exchange; the direction mask is shared.
 template <int K, int J>
-__device__ __forceinline__ void bitonic_step3(float& a, float& b, float& c, int lane) {
+__device__ __forceinline__ void bitonic_step3(unsigned& a, unsigned& b, unsigned& c, int lane) {
   const bool take_min = ((lane & J) == 0) == ((lane & K) == 0);
-  const float pa = xor_lane<J>(a), pb = xor_lane<J>(b), pc = xor_lane<J>(c);
-  a = take_min ? fminf(a, pa) : fmaxf(a, pa);
-  b = take_min ? fminf(b, pb) : fmaxf(b, pb);
-  c = take_min ? fminf(c, pc) : fmaxf(c, pc);
+  const unsigned sel = take_min ? 0u : ~0u;
+  const unsigned pa = xor_lane<J>(a), pb = xor_lane<J>(b), pc = xor_lane<J>(c);
+  a = med3u(a, pa, sel);
+  b = med3u(b, pb, sel);
+  c = med3u(c, pc, sel);
 }
 
 template <int K, int J>
-__device__ __forceinline__ void bitonic_merge3(float& a, float& b, float& c, int lane) {
+__device__ __forceinline__ void bitonic_merge3(unsigned& a, unsigned& b, unsigned& c, int lane) {
   bitonic_step3<K, J>(a, b, c, lane);
   if constexpr (J > 1) bitonic_merge3<K, J / 2>(a, b, c, lane);
 }
 
 template <int K>
-__device__ __forceinline__ void bitonic_sort3(float& a, float& b, float& c, int lane) {
+__device__ __forceinline__ void bitonic_sort3(unsigned& a, unsigned& b, unsigned& c, int lane) {
   if constexpr (K > 2) bitonic_sort3<K / 2>(a, b, c, lane);
   bitonic_merge3<K, K / 2>(a, b, c, lane);
 }
 
-// Elements of the ascending 64-array s (+inf padded) that are < v (LE: <= v).
+// inclusive lane-order scan (sum or max; every value >= 0) by DPP row shifts + row broadcasts
+template <bool MAX>
+__device__ __forceinline__ int wave_scan_i(int v) {
+#define FM_SCAN_STEP(C, RM)                                              \
+  {                                                                      \
+    const int t = __builtin_amdgcn_update_dpp(0, v, C, RM, 0xf, false); \
+    v = MAX ? max(v, t) : v + t;                                         \
+  }
+  FM_SCAN_STEP(0x111, 0xf) FM_SCAN_STEP(0x112, 0xf) FM_SCAN_STEP(0x114, 0xf) FM_SCAN_STEP(0x118, 0xf)
+  FM_SCAN_STEP(0x142, 0xa) FM_SCAN_STEP(0x143, 0xc)
+#undef FM_SCAN_STEP
+  return v;
+}
+
+// neighbour keys in lane order (wave_shr:1 / wave_shl:1); the edge lanes get ``edge``
+__device__ __forceinline__ unsigned prev_lane(unsigned v, unsigned edge) {
+  return (unsigned)__builtin_amdgcn_update_dpp((int)edge, (int)v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ unsigned next_lane(unsigned v, unsigned edge) {
+  return (unsigned)__builtin_amdgcn_update_dpp((int)edge, (int)v, 0x130, 0xf, 0xf, false);
+}
+
+// Keys of the ascending 64-array s that are < v (LE: <= v).
 template <bool LE>
-__device__ __forceinline__ int bound64(const float* s, float v) {
+__device__ __forceinline__ int bound64(const unsigned* s, unsigned v) {
   int pos = 0;
 #pragma unroll
   for (int h = 32; h > 0; h >>= 1) {
-    const float q = s[pos + h - 1];
+    const unsigned q = s[pos + h - 1];
     pos += (LE ? q <= v : q < v) ? h : 0;
   }
-  const float q = s[pos];
+  const unsigned q = s[pos];
   return pos + ((LE ? q <= v : q < v) ? 1 : 0);
 }
 
 // Pooled-rank statistics of the small path (returned wave-uniform): baseline rank sum
 // R1, pooled tie term sum(t^3 - t), Wilcoxon positive / negative rank sums and its tie
 // term.  bv / cv / dv: this lane's baseline, canary and signed difference (NaN: none).
-__device__ __forceinline__ void small_ranks(float bv, float cv, float dv, float* s, int lane, int n1, int n2, int nd,
+//
+// Everything is counted per RUN of equal keys in the sorted arrays, at the run's last
+// lane: its first lane f comes from a max-scan of run starts, its length t = i - f + 1.
+//  * R1 = n1 (n1 + 1) / 2 + U1 (ranks within the baseline sum to that whatever the ties),
+//    U1 = sum over baseline runs of t_b (#(c < v) + #(c == v) / 2): one lower / upper
+//    bound search of the run's key in the sorted canary keys (LDS).
+//  * pooled ties: (t_b + t_c)^3 - (t_b + t_c) = (t_b^3 - t_b) + (t_c^3 - t_c)
+//    + 3 t_b t_c (t_b + t_c): baseline runs add the first and last terms (t_c from the
+//    same search), canary runs their own t_c^3 - t_c.
+//  * Wilcoxon: a |d| run starting at f of length t holds average rank f + (t + 1) / 2;
+//    its positive members are counted by a prefix sum carried through the run-start scan.
+// All integer: exact, and independent of the summation order.
+__device__ __forceinline__ void small_ranks(float bv, float cv, float dv, unsigned* s, int lane, int n1, int n2, int nd,
                                             float& R1, float& tie, float& Tp, float& Tm, float& wtie) {
-  const float inf = __builtin_huge_valf();
+  const unsigned PAD = ~0u;
   const float ad = fabsf(dv);
-  float kb = bv == bv ? bv : inf, kc = cv == cv ? cv : inf, kd = ad == ad ? ad : inf;
+  unsigned kb = bv == bv ? fkey(bv) : PAD, kc = cv == cv ? fkey(cv) : PAD;
+  unsigned kd = ad == ad ? ((__float_as_uint(ad) << 1) | (dv > 0.f ? 1u : 0u)) : PAD;
   bitonic_sort3<64>(kb, kc, kd, lane);
-  s[lane] = kb;
-  s[FM_WAVE + lane] = kc;
-  s[2 * FM_WAVE + lane] = kd;
+  s[lane] = kc;
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  const float* sb = s;
-  const float* sc = s + FM_WAVE;
-  const float* sd = s + 2 * FM_WAVE;
-  // integer accumulators (ranks doubled): 2 R1 <= 12210 and 2 Tp <= 4160 share one exact
-  // reduction; Tm = np (np + 1) / 2 - Tp needs none
-  int r1x2 = 0, t = 0, tpx2 = 0, wt = 0;
-  if (bv == bv) {
-    const int lb = bound64<false>(sb, bv), ub = min(bound64<true>(sb, bv), n1);
-    const int lc = bound64<false>(sc, bv), uc = min(bound64<true>(sc, bv), n2);
-    const int eq = (ub - lb) + (uc - lc);
-    r1x2 = 2 * (lb + lc) + eq + 1;
-    t += eq * eq - 1;
+  const unsigned vd = kd >> 1;
+  // run starts / ends (the edge values differ from every key of their array)
+  const bool sb_ = kb != prev_lane(kb, ~kb), eb = kb != next_lane(kb, ~kb);
+  const bool sc_ = kc != prev_lane(kc, ~kc), ec = kc != next_lane(kc, ~kc);
+  const bool sd_ = vd != prev_lane(vd, ~vd), ed = vd != next_lane(vd, ~vd);
+  const int pos = (lane < nd && (kd & 1u)) ? 1 : 0;
+  const int P = wave_scan_i<false>(pos);
+  const int fb = wave_scan_i<true>(sb_ ? lane : 0);
+  const int fc = wave_scan_i<true>(sc_ ? lane : 0);
+  const int fd = wave_scan_i<true>(sd_ ? (lane << 8) | (P - pos) : 0);
+  int u1x2 = 0, tpx2 = 0, t = 0, wt = 0;
+  if (lane < n1 && eb) {
+    const int tb = lane - fb + 1;
+    const int lc = bound64<false>(s, kb), tc = bound64<true>(s, kb) - lc;
+    u1x2 = tb * (2 * lc + tc);
+    t = tb * tb * tb - tb + 3 * tb * tc * (tb + tc);
   }
-  if (cv == cv) {
-    const int lb = bound64<false>(sb, cv), ub = min(bound64<true>(sb, cv), n1);
-    const int lc = bound64<false>(sc, cv), uc = min(bound64<true>(sc, cv), n2);
-    const int eq = (ub - lb) + (uc - lc);
-    t += eq * eq - 1;
+  if (lane < n2 && ec) {
+    const int tc = lane - fc + 1;
+    t += tc * tc * tc - tc;
   }
-  if (ad == ad) {
-    const int lb = bound64<false>(sd, ad), ub = min(bound64<true>(sd, ad), nd);
-    const int eq = ub - lb;
-    if (dv > 0.f) tpx2 = 2 * lb + eq + 1;
-    wt = eq * eq - 1;
+  if (lane < nd && ed) {
+    const int f = fd >> 8, td = lane - f + 1, npos = P - (fd & 0xff);
+    tpx2 = npos * (2 * f + td + 1);
+    wt = td * td * td - td;
   }
-  const int rr = wave_allsum_i(r1x2 | (tpx2 << 16));
-  R1 = 0.5f * (float)(rr & 0xffff);
+  // 2 U1 <= 8192 and 2 Tp <= 4160 share one exact reduction; Tm = np (np + 1) / 2 - Tp
+  const int rr = wave_allsum_i(u1x2 | (tpx2 << 16));
+  R1 = 0.5f * (float)(n1 * (n1 + 1) + (rr & 0xffff));
   Tp = 0.5f * (float)(rr >> 16);
   Tm = 0.5f * (float)(nd * (nd + 1)) - Tp;
   tie = (float)wave_allsum_i(t);
   wtie = (float)wave_allsum_i(wt);
+}
+
+// Kruskal-Wallis H of two groups without cancellation: with D = R1 - n1 (n + 1) / 2 (exact:
+// a half-integer), R2 - n2 (n + 1) / 2 = -D and H = 12 / (n (n + 1)) sum R_i^2 / n_i - 3 (n + 1)
+// = 12 D^2 / ((n + 1) n1 n2).  The textbook form subtracts two ~3 (n + 1) terms, and near
+// H = 0 its fp32 rounding moved p by up to 3e-3.
+__device__ __forceinline__ float kruskal_h(float R1, float n1, float n2) {
+  const float n = n1 + n2;
+  const float D = R1 - n1 * (n + 1.f) * 0.5f;
+  return 12.f * D * D / ((n + 1.f) * n1 * n2);
 }
 
 template <bool SMALL>
@@ -236,7 +301,7 @@ __global__ __launch_bounds__(256) void rank_tests_kernel(const RankArgs a) {
   const int npool4 = (npool + 3) & ~3;
   const int k = a.nb < a.nc ? a.nb : a.nc;
   const int k4 = (k + 3) & ~3;
-  const int small_sz = SMALL ? 3 * FM_WAVE : 0;
+  const int small_sz = SMALL ? FM_WAVE : 0;
   float* x = (float*)fm_rank_smem + (size_t)w * (small_sz + npool4 + k4 + FM_WAVE) + small_sz;
   float* dabs = x + npool4;
   float* Rf = dabs + k4;  // Friedman rank sums (<= 64 treatments)
@@ -244,7 +309,7 @@ __global__ __launch_bounds__(256) void rank_tests_kernel(const RankArgs a) {
   const float* b = a.base + (long long)n * a.ld_base;
   const float* c = a.cur + (long long)n * a.ld_cur;
   const bool want_fr = a.mode == 6 || a.p_friedman != nullptr;
-  float R1, tie, R2, Tp, wtie, Tm, n1, n2, np, sb;
+  float R1, tie, R2, Tp, wtie, Tm, n1, n2, np, sb;  // R2: the sweep's (Kruskal needs R1 only)
   float p_fr = 1.f, nblk = 0.f;
   if constexpr (SMALL) {
     const float bv = lane < a.nb ? b[lane] : fm_nan();
@@ -266,9 +331,7 @@ __global__ __launch_bounds__(256) void rank_tests_kernel(const RankArgs a) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       friedman_wave(a, x, Rf, p_fr, nblk);
     }
-    small_ranks(bv, cv, dv, x - small_sz, lane, (int)n1, (int)n2, (int)np, R1, tie, Tp, Tm, wtie);
-    const float nn = n1 + n2;
-    R2 = nn * (nn + 1.f) * 0.5f - R1;
+    small_ranks(bv, cv, dv, (unsigned*)(x - small_sz), lane, (int)n1, (int)n2, (int)np, R1, tie, Tp, Tm, wtie);
   } else {
 
   // stage pooled sample (NaN pads the vector tail) and |d| of aligned pairs
@@ -322,9 +385,9 @@ __global__ __launch_bounds__(256) void rank_tests_kernel(const RankArgs a) {
       const float var = n1 * n2 / 12.f * ((nn + 1.f) - tie / fmaxf(nn * (nn - 1.f), 1.f));
       const float sd = sqrtf(fmaxf(var, 0.f));
       rej_mw = sd > 0.f && (U - n1 * n2 * 0.5f - 0.5f) > zc * sd;
-      const float H = 12.f / fmaxf(nn * (nn + 1.f), 1.f) * (R1 * R1 / n1 + R2 * R2 / n2) - 3.f * (nn + 1.f);
+      const float H = kruskal_h(R1, n1, n2);
       const float corr = 1.f - tie / fmaxf(nn * nn * nn - nn, 1.f);
-      rej_k = corr > 0.f && fmaxf(H / corr, 0.f) > zc * zc;
+      rej_k = corr > 0.f && H / corr > zc * zc;
     }
     if (np > 0.f) {
       const float T = fminf(Tp, Tm);
@@ -372,9 +435,9 @@ __global__ __launch_bounds__(256) void rank_tests_kernel(const RankArgs a) {
   // Kruskal-Wallis, 2 groups → chi^2(1)
   float p_kw = 1.f;
   if (n1 > 0.f && n2 > 0.f) {
-    const float H = 12.f / fmaxf(nn * (nn + 1.f), 1.f) * (R1 * R1 / n1 + R2 * R2 / n2) - 3.f * (nn + 1.f);
+    const float H = kruskal_h(R1, n1, n2);
     const float corr = 1.f - tie / fmaxf(nn * nn * nn - nn, 1.f);
-    if (corr > 0.f) p_kw = fminf(erfcf(sqrtf(fmaxf(H / corr, 0.f) * 0.5f)), 1.f);
+    if (corr > 0.f) p_kw = fminf(erfcf(sqrtf(H / corr * 0.5f)), 1.f);
   }
   // Wilcoxon signed-rank (approx, no continuity correction)
   float p_w = 1.f;
@@ -428,7 +491,7 @@ extern "C" size_t fm_rank_lds_bytes(int nb, int nc) {
   const int npool4 = (nb + nc + 3) & ~3;
   const int k = nb < nc ? nb : nc;
   const int k4 = (k + 3) & ~3;
-  const int small_sz = rank_small(nb, nc) ? 3 * FM_WAVE : 0;
+  const int small_sz = rank_small(nb, nc) ? FM_WAVE : 0;
   return (size_t)4 * (small_sz + npool4 + k4 + FM_WAVE) * 4;
 }
 

@@ -169,7 +169,8 @@ def _fp8_index(device) -> torch.Tensor:
 
 def pack_fp8(A: torch.Tensor) -> torch.Tensor:
     """``[256, 80]`` augmented weight → the fp8 kernel's uint8 buffer: block-scaled
-    e4m3 fragments ``[TILES, 2, 64, 32]`` (one scale per gate row and 32-k block),
+    e4m3 fragments ``[TILES, 2, 64, 32]`` stored half-major (one scale per gate row and
+    32-k block),
     then the E8M0 scales ``[64 lanes, 16]``
     (:func:`~foremast_amd.ops.pack.fp8_blocks_lane_major`)."""
     from .pack import fp8_blocks_lane_major

@@ -58,15 +58,17 @@ def e8m0_blocks(v: torch.Tensor):
 
 
 def fp8_blocks_lane_major(v: torch.Tensor) -> torch.Tensor:
-    """A block-scaled fp8 segment of the values ``v`` laid out as MFMA A fragments
-    ``[steps, 64 lanes, 32 bytes]`` (codes, then the scales lane-major).  Measured on
+    """A block-scaled fp8 segment of the values ``v`` (logical MFMA A fragments
+    ``[steps, 64 lanes, 32 bytes]``), stored half-major ``[steps, 2 halves, 64 lanes, 16
+    bytes]`` so the kernel's 16-byte LDS reads are lane-contiguous (no bank conflicts),
+    then the scales lane-major.  Measured on
     the MI355X (``scripts/probe_mfma_scale.py``): bytes 16 b .. 16 b + 15 of lanes r
     AND r + 32 form one 32-value k block of row r, scaled by the byte in lane r + 32 b's
     scale register; so each block's E8M0 is stored in lane r + 32 b."""
     steps = v.numel() // (FP8_LANES * FP8_CHUNK)
     g = v.reshape(steps, 2, 32, 2, 16).permute(0, 2, 3, 1, 4).reshape(steps * 64, 32)   # [(step, r, b), (h, j)]
     q, sc = e8m0_blocks(g)
-    q = q.view(steps, 32, 2, 2, 16).permute(0, 3, 1, 2, 4).reshape(-1)
+    q = q.view(steps, 32, 2, 2, 16).permute(0, 2, 3, 1, 4).reshape(-1)                 # [step, b, h, r, j]
     lane_sc = sc.view(steps, 32, 2).permute(0, 2, 1).reshape(steps, FP8_LANES)         # lane = r + 32 b
     return torch.cat([q, lane_sc.t().reshape(-1)])
 

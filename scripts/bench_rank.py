@@ -34,19 +34,19 @@ def windows(N, nb, nc, dev, seed=0):
     return base.to(dev).contiguous(), cur.to(dev).contiguous()
 
 
-def run(base, cur, sweep, reps):
+def run(base, cur, sweep, reps, want_pvals=True):
     if sweep:
         os.environ["FOREMAST_RANK_SWEEP"] = "1"
     else:
         os.environ.pop("FOREMAST_RANK_SWEEP", None)
     out = {}
-    K.rank_tests(base, cur, 1, 0.05, want_pvals=True, out=out)
+    K.rank_tests(base, cur, 1, 0.05, want_pvals=want_pvals, out=out)
     torch.cuda.synchronize()
     ts = []
     for _ in range(reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        K.rank_tests(base, cur, 1, 0.05, want_pvals=True, out=out)
+        K.rank_tests(base, cur, 1, 0.05, want_pvals=want_pvals, out=out)
         e1.record()
         e1.synchronize()
         ts.append(e0.elapsed_time(e1))
@@ -64,7 +64,11 @@ def main():
     base, cur = windows(a.rows, a.nb, a.nc, dev)
     small, t_small, m_small = run(base, cur, False, a.reps)
     sweep, t_sweep, m_sweep = run(base, cur, True, a.reps)
+    # the product tick's form: decisions only (|z| > z_crit, no p-values)
+    zsmall, tz_small, _ = run(base, cur, False, a.reps, want_pvals=False)
+    zsweep, tz_sweep, _ = run(base, cur, True, a.reps, want_pvals=False)
     os.environ.pop("FOREMAST_RANK_SWEEP", None)
+    rows_differ = int(((small["pvals"] - sweep["pvals"]).abs() > 1e-6).any(1).sum())
     diff = {k: float((small[k] - sweep[k]).abs().max()) for k in ("pvals", "counts")}
     same = float((small["differs"] == sweep["differs"]).float().mean())
     bm = float(torch.nan_to_num((small["base_mean"] - sweep["base_mean"]).abs()).max())
@@ -75,11 +79,21 @@ def main():
     want = torch.stack([ref.p_mw, ref.p_wilcoxon, ref.p_kruskal], 1)
     ok = torch.isfinite(want)
     ref_err = float((got[ok] - want[ok]).abs().max())
+    got_sw = sweep["pvals"][idx].double().cpu()
+    ref_err_sweep = float((got_sw[ok] - want[ok]).abs().max())
+    # per test: sampled rows further than 1e-4 from the fp64 reference, each path
+    far = {name: [int(((g[:, j] - want[:, j]).abs() > 1e-4).sum()) for g in (got, got_sw)]
+           for j, name in enumerate(("mw", "wilcoxon", "kruskal"))}
     print(json.dumps({"rows": a.rows, "nb": a.nb, "nc": a.nc, "small_ms": round(t_small, 4),
                       "small_min_ms": round(m_small, 4), "sweep_ms": round(t_sweep, 4),
                       "sweep_min_ms": round(m_sweep, 4), "speedup": round(t_sweep / t_small, 2),
+                      "decisions_only_small_ms": round(tz_small, 4), "decisions_only_sweep_ms": round(tz_sweep, 4),
+                      "decisions_only_agree_with_pvals": float((zsmall["differs"] == small["differs"]).float().mean()),
+                      "decisions_only_small_vs_sweep": float((zsmall["differs"] == zsweep["differs"]).float().mean()),
+                      "rows_pvals_differ_gt_1e-6": rows_differ,
                       "differs_agree": same, "max_abs_diff": diff, "base_mean_diff": bm,
-                      "max_abs_err_vs_fp64_ref": ref_err}), flush=True)
+                      "max_abs_err_vs_fp64_ref": ref_err, "sweep_max_abs_err_vs_fp64_ref": ref_err_sweep,
+                      "sampled_rows": int(idx.numel()), "rows_off_ref_gt_1e-4_small_sweep": far}), flush=True)
 
 
 if __name__ == "__main__":

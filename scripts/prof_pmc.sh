@@ -5,6 +5,7 @@
 #   lstm  — LSTM training (per phase) + scoring kernels
 #   dec   — seasonal decomposition
 #   es    — ES / DES sequential fit (and the time-parallel scan variants)
+#   rank  — rank tests, small-window sort path and the pairwise sweep (100k x 55 + 55)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TARGET=${TARGET:-hw}
@@ -16,6 +17,7 @@ case $TARGET in
   dec)  CMD=("$PWD/scripts/bench_kernels.py" --series 20000 --rounds 1 --only decompose --variants=3) ;;
   es)   CMD=("$PWD/scripts/bench_kernels.py" --series 20000 --rounds 1 --only es --variants=) ;;
   lstm) CMD=("$PWD/scripts/bench_lstm_kernels.py") ;;
+  rank) CMD=("$PWD/scripts/bench_rank.py") ;;
 esac
 SETS=("SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS"
       "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU"

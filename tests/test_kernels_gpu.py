@@ -254,6 +254,52 @@ def test_rank_tests_kernel(K):
     np.testing.assert_allclose(out["base_mean"].cpu().numpy(), np.nanmean(b, 1), rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("nb,nc", [(55, 55), (64, 37), (20, 64)])
+def test_rank_small_path_equals_sweep(K, nb, nc, monkeypatch):
+    """The small-window path (sorted keys, run scans, one cross search) against the O(n^2)
+    sweep on heavy ties, signed zeros, negative values, NaN gaps and partly filled canary
+    windows: identical counts and decisions, p-values equal to fp32 rounding, and the
+    decisions-only form (|z| > z_crit) identical to the p-value decisions."""
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(7)
+    N = 4000
+    b = torch.randn(N, nb, generator=g)
+    c = torch.randn(N, nc, generator=g) + (torch.rand(N, 1, generator=g) < 0.3) * 0.7
+    b[: N // 2] = torch.round(b[: N // 2] * 3) / 3        # heavy ties, many exact zeros
+    c[: N // 2] = torch.round(c[: N // 2] * 3) / 3
+    c[::5] = -c[::5]                                      # -0.0 next to +0.0
+    fill = torch.randint(1, nc + 1, (N,), generator=g)
+    c[torch.arange(nc)[None, :] >= fill[:, None]] = float("nan")
+    b[torch.rand(N, nb, generator=g) < 0.05] = float("nan")
+    c[3, :] = b[3, :nc] if nc <= nb else c[3, :]          # all pairs tied: no Wilcoxon pairs
+    tb, tc = b.to(dev).contiguous(), c.to(dev).contiguous()
+    outs = {}
+    for path in ("small", "sweep"):
+        if path == "sweep":
+            monkeypatch.setenv("FOREMAST_RANK_SWEEP", "1")
+        else:
+            monkeypatch.delenv("FOREMAST_RANK_SWEEP", raising=False)
+        for pv in (True, False):
+            o = {}
+            K.rank_tests(tb, tc, pw_ref.PW_ALL, 0.05, want_pvals=pv, out=o)
+            outs[path, pv] = {k: v.clone() for k, v in o.items()}
+    torch.cuda.synchronize()
+    sm, sw = outs["small", True], outs["sweep", True]
+    assert torch.equal(sm["counts"], sw["counts"])
+    np.testing.assert_allclose(sm["pvals"].cpu().numpy(), sw["pvals"].cpu().numpy(), rtol=1e-5, atol=1e-6)
+    assert torch.equal(sm["differs"], sw["differs"])
+    assert torch.equal(outs["small", False]["differs"], sm["differs"])
+    assert torch.equal(outs["sweep", False]["differs"], sw["differs"])
+    # the reference on the same fp32 windows (c - b rounds in fp32 as in the kernel, so the
+    # Wilcoxon ties are the same), its statistics exact and its tails in fp32
+    ref = pw_ref.rank_tests(b, c)
+    dref = pw_ref.pairwise_differs(ref, pw_ref.PW_ALL, 0.05)
+    assert torch.equal(sm["differs"].cpu().bool(), dref)
+    want = torch.stack([ref.p_mw, ref.p_wilcoxon, ref.p_kruskal], 1)
+    ok = torch.isfinite(want)
+    assert float((sm["pvals"].cpu().double()[ok] - want[ok]).abs().max()) < 2e-4
+
+
 def test_rank_tests_kernel_friedman(K):
     """Friedman mode (time slots x pods) against the reference, with ties,
     incomplete blocks and a shifted canary."""

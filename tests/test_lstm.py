@@ -415,7 +415,8 @@ def test_block_scaled_fp8_pack_layout_and_precision(F):
     A[9, :] *= 300.0
     buf = L.pack_fp8(A)
     assert buf.dtype == torch.uint8 and buf.numel() == L.FP8_FRAG_BYTES + L.FP8_SCALE_BYTES
-    q = buf[:L.FP8_FRAG_BYTES].view(torch.float8_e4m3fn).float().view(L.TILES, 2, 64, 32)
+    q = buf[:L.FP8_FRAG_BYTES].view(torch.float8_e4m3fn).float().view(L.TILES, 2, 2, 64, 16)  # half-major
+    q = q.permute(0, 1, 3, 2, 4).reshape(L.TILES, 2, 64, 32)
     sc = buf[L.FP8_FRAG_BYTES:].view(64, L.TILES * 2).t().reshape(L.TILES, 2, 2, 32).float()  # [t, s, b, r]
     lanes = torch.arange(64)
     f = torch.exp2(sc - 127)[:, :, (torch.arange(32) // 16)[None, :], (lanes & 31)[:, None]]   # [t, s, lane, j]
