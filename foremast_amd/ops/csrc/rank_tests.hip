@@ -283,14 +283,31 @@ __device__ __forceinline__ void small_ranks(float bv, float cv, float dv, unsign
   wtie = (float)wave_allsum_i(wt);
 }
 
-// Kruskal-Wallis H of two groups without cancellation: with D = R1 - n1 (n + 1) / 2 (exact:
-// a half-integer), R2 - n2 (n + 1) / 2 = -D and H = 12 / (n (n + 1)) sum R_i^2 / n_i - 3 (n + 1)
-// = 12 D^2 / ((n + 1) n1 n2).  The textbook form subtracts two ~3 (n + 1) terms, and near
-// H = 0 its fp32 rounding moved p by up to 3e-3.
-__device__ __forceinline__ float kruskal_h(float R1, float n1, float n2) {
-  const float n = n1 + n2;
-  const float D = R1 - n1 * (n + 1.f) * 0.5f;
-  return 12.f * D * D / ((n + 1.f) * n1 * n2);
+// The three two-sample tests as z statistics, shared by the p-value and the decisions-only
+// forms (so their verdicts agree by construction):
+//  * Mann-Whitney: |U1 - n1 n2 / 2| with the tie-corrected sd; two-sided with continuity
+//    correction, p = 2 sf((|U1 - mu| - 1/2) / sd).
+//  * Kruskal-Wallis of two groups is the same statistic squared without the continuity
+//    correction: H = 12 D^2 / ((n + 1) n1 n2) with D = R1 - n1 (n + 1) / 2 = U1 - n1 n2 / 2,
+//    and its tie correction 1 - T / (n^3 - n) turns (n + 1) n1 n2 / 12 into the MW variance,
+//    so H / corr = (U1 - mu)^2 / var and p = erfc(sqrt(H / corr / 2)) = 2 sf(|U1 - mu| / sd).
+//    (The textbook form 12 / (n (n + 1)) sum R_i^2 / n_i - 3 (n + 1) subtracts two ~3 (n + 1)
+//    terms; near H = 0 its fp32 rounding moved p by up to 3e-3.)
+//  * Wilcoxon signed rank: |T - np (np + 1) / 4| with its tie-corrected sd.
+struct RankZ {
+  float dU, sd_u, dT, sd_t;
+};
+__device__ __forceinline__ RankZ rank_z(float R1, float tie, float Tp, float Tm, float wtie, float n1, float n2,
+                                        float np) {
+  RankZ z;
+  const float nn = n1 + n2, nm = n1 * n2;
+  z.dU = fabsf(R1 - n1 * (n1 + 1.f) * 0.5f - nm * 0.5f);
+  const float var = nm * (1.f / 12.f) * ((nn + 1.f) - tie / fmaxf(nn * (nn - 1.f), 1.f));
+  z.sd_u = (n1 > 0.f && n2 > 0.f) ? sqrtf(fmaxf(var, 0.f)) : 0.f;
+  z.dT = fabsf(fminf(Tp, Tm) - np * (np + 1.f) * 0.25f);
+  const float wvar = np * (np + 1.f) * (2.f * np + 1.f) * (1.f / 24.f) - wtie * (1.f / 48.f);
+  z.sd_t = np > 0.f ? sqrtf(fmaxf(wvar, 0.f)) : 0.f;
+  return z;
 }
 
 template <bool SMALL>
@@ -309,7 +326,7 @@ __global__ __launch_bounds__(256) void rank_tests_kernel(const RankArgs a) {
   const float* b = a.base + (long long)n * a.ld_base;
   const float* c = a.cur + (long long)n * a.ld_cur;
   const bool want_fr = a.mode == 6 || a.p_friedman != nullptr;
-  float R1, tie, R2, Tp, wtie, Tm, n1, n2, np, sb;  // R2: the sweep's (Kruskal needs R1 only)
+  float R1, tie, R2, Tp, wtie, Tm, n1, n2, np, sb;  // R2: the sweep's (the tests need R1 only)
   float p_fr = 1.f, nblk = 0.f;
   if constexpr (SMALL) {
     const float bv = lane < a.nb ? b[lane] : fm_nan();
@@ -378,23 +395,10 @@ __global__ __launch_bounds__(256) void rank_tests_kernel(const RankArgs a) {
   if (!a.pvals && a.z_crit > 0.f && a.mode >= 1 && a.mode <= 5) {
     // decisions only (the product tick): p < alpha <=> |z| > z_crit, no erfc
     const float zc = a.z_crit;
-    bool rej_mw = false, rej_w = false, rej_k = false;
-    if (n1 > 0.f && n2 > 0.f) {
-      const float U1 = R1 - n1 * (n1 + 1.f) * 0.5f;
-      const float U = fmaxf(U1, n1 * n2 - U1);
-      const float var = n1 * n2 / 12.f * ((nn + 1.f) - tie / fmaxf(nn * (nn - 1.f), 1.f));
-      const float sd = sqrtf(fmaxf(var, 0.f));
-      rej_mw = sd > 0.f && (U - n1 * n2 * 0.5f - 0.5f) > zc * sd;
-      const float H = kruskal_h(R1, n1, n2);
-      const float corr = 1.f - tie / fmaxf(nn * nn * nn - nn, 1.f);
-      rej_k = corr > 0.f && H / corr > zc * zc;
-    }
-    if (np > 0.f) {
-      const float T = fminf(Tp, Tm);
-      const float var = np * (np + 1.f) * (2.f * np + 1.f) / 24.f - wtie / 48.f;
-      const float sd = sqrtf(fmaxf(var, 0.f));
-      rej_w = sd > 0.f && fabsf(T - np * (np + 1.f) * 0.25f) > zc * sd;
-    }
+    const RankZ z = rank_z(R1, tie, Tp, Tm, wtie, n1, n2, np);
+    bool rej_mw = z.sd_u > 0.f && z.dU - 0.5f > zc * z.sd_u;
+    bool rej_k = z.sd_u > 0.f && z.dU > zc * z.sd_u;
+    bool rej_w = z.sd_t > 0.f && z.dT > zc * z.sd_t;
     const float nsmall = fminf(n1, n2);
     const bool ran_mw = nsmall >= (float)a.min_mw, ran_w = np >= (float)a.min_wilcoxon;
     const bool ran_k = nsmall >= (float)a.min_kruskal;
@@ -422,32 +426,12 @@ __global__ __launch_bounds__(256) void rank_tests_kernel(const RankArgs a) {
     }
     return;
   }
-  // Mann-Whitney U (two-sided, continuity, tie-corrected)
-  float p_mw = 1.f;
-  if (n1 > 0.f && n2 > 0.f) {
-    const float U1 = R1 - n1 * (n1 + 1.f) * 0.5f;
-    const float U = fmaxf(U1, n1 * n2 - U1);
-    const float mu = n1 * n2 * 0.5f;
-    const float var = n1 * n2 / 12.f * ((nn + 1.f) - tie / fmaxf(nn * (nn - 1.f), 1.f));
-    const float sd = sqrtf(fmaxf(var, 0.f));
-    if (sd > 0.f) p_mw = fminf(2.f * norm_sf((U - mu - 0.5f) / sd), 1.f);
-  }
-  // Kruskal-Wallis, 2 groups → chi^2(1)
-  float p_kw = 1.f;
-  if (n1 > 0.f && n2 > 0.f) {
-    const float H = kruskal_h(R1, n1, n2);
-    const float corr = 1.f - tie / fmaxf(nn * nn * nn - nn, 1.f);
-    if (corr > 0.f) p_kw = fminf(erfcf(sqrtf(H / corr * 0.5f)), 1.f);
-  }
-  // Wilcoxon signed-rank (approx, no continuity correction)
-  float p_w = 1.f;
-  if (np > 0.f) {
-    const float T = fminf(Tp, Tm);
-    const float mu = np * (np + 1.f) * 0.25f;
-    const float var = np * (np + 1.f) * (2.f * np + 1.f) / 24.f - wtie / 48.f;
-    const float sd = sqrtf(fmaxf(var, 0.f));
-    if (sd > 0.f) p_w = fminf(2.f * norm_sf(fabsf((T - mu) / sd)), 1.f);
-  }
+  // Mann-Whitney U (two-sided, continuity, tie-corrected), Kruskal-Wallis (2 groups, chi^2(1)),
+  // Wilcoxon signed rank (no continuity correction): see rank_z
+  const RankZ z = rank_z(R1, tie, Tp, Tm, wtie, n1, n2, np);
+  const float p_mw = z.sd_u > 0.f ? fminf(2.f * norm_sf((z.dU - 0.5f) / z.sd_u), 1.f) : 1.f;
+  const float p_kw = z.sd_u > 0.f ? fminf(2.f * norm_sf(z.dU / z.sd_u), 1.f) : 1.f;
+  const float p_w = z.sd_t > 0.f ? fminf(2.f * norm_sf(z.dT / z.sd_t), 1.f) : 1.f;
   const float nsmall = fminf(n1, n2);
   const bool ran_mw = nsmall >= (float)a.min_mw;
   const bool ran_w = np >= (float)a.min_wilcoxon;
