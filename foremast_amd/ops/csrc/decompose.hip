@@ -724,18 +724,18 @@ __global__ __launch_bounds__(SB, M > 0 ? 6 : 4) void decompose_score_kernel(cons
   }
 }
 
-// split epilogue of the fast path: one wave per series, the band / verdict from the forecast
-// parameters and the seasonal terms the score kernel left (deferred series: NaN marker,
-// the general kernel has done their epilogue)
+// split epilogue of the fast path: one 16-lane row per series, the band / verdict from the
+// forecast parameters and the seasonal terms the score kernel left (deferred series: NaN
+// marker, the general kernel has done their epilogue)
 __global__ __launch_bounds__(256) void decompose_detect_kernel(const DecompArgs a) {
-  const int n = blockIdx.x * (blockDim.x / FM_WAVE) + wave_id();
-  if (n >= a.N) return;  // wave-uniform
+  const int n = blockIdx.x * (blockDim.x / 16) + (threadIdx.x >> 4);
+  if (n >= a.N) return;  // row-uniform
   const float* sf = a.sfc + (long long)n * a.hmax;
   const float s0 = sf[0];
   if (s0 != s0) return;
   const float lvl = a.fc_level[n], slope = a.fc_slope[n], sig = a.sigma[n], nv = a.nvalid[n];
   const int h = a.m >> 1, hm = a.hmax;
-  detect_epilogue_wave(a.det, n, sig, nv, [&](int hz) {
+  detect_epilogue_row(a.det, n, sig, nv, [&](int hz) {
     const int i = min(max(hz, 1), hm) - 1;  // the host guarantees 1 <= hz <= hmax
     return lvl + slope * (float)(h + hz) + sf[i];
   });
@@ -815,7 +815,7 @@ extern "C" int fm_seasonal_decompose(const DecompArgs* a, hipStream_t st) {
   if (fast && a->sfc && a->det.C > 0) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(decompose_detect_kernel, dim3((a->N + 3) / 4), dim3(256), 0, st, *a);
+    hipLaunchKernelGGL(decompose_detect_kernel, dim3((a->N + 15) / 16), dim3(256), 0, st, *a);
   }
   return (int)hipGetLastError();
 }

@@ -238,6 +238,59 @@ __device__ __forceinline__ void detect_epilogue_wave(const DetectArgs& d, int n,
   if (d.cur && lane == 0) det_write(d, n, ic, anyv, model_ok, sc, npts);
 }
 
+// All-reduce over the 16 lanes of a DPP row: quad butterflies, then row rotations by 4
+// and 8 (every lane ends with the row's total; rows never mix).
+template <bool MAX>
+__device__ __forceinline__ float row16_all(float v) {
+  auto op = [](float a, float b) { return MAX ? fmaxf(a, b) : a + b; };
+  v = op(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xf, 0xf, false)));   // xor 1
+  v = op(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xf, 0xf, false)));   // xor 2
+  v = op(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x124, 0xf, 0xf, false)));  // row_ror:4
+  v = op(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xf, 0xf, false)));  // row_ror:8
+  return v;
+}
+
+// Same semantics as detect_epilogue_wave for kernels where ONE 16-LANE ROW owns series n
+// (four series per wave): the deferred epilogues, whose work per series is a window of
+// ~10 columns, would leave 54 of 64 lanes idle with a wave per series.  Every branch
+// below is uniform over a row (one series), so the row reductions see only active lanes.
+template <typename ForecastFn>
+__device__ __forceinline__ void detect_epilogue_row(const DetectArgs& d, int n, float sig, float n_valid,
+                                                    ForecastFn fcast, int gidx = -1) {
+  if (d.C <= 0) return;
+  const int gl = lane_id() & 15;
+  float npts = 0.f;
+  if (d.cur && (d.thr_lut || d.row_out)) {
+    for (int c = gl; c < d.C; c += 16) npts += det_valid_col(d, n, c);
+    npts = row16_all<false>(npts);
+  }
+  const DetThr t = det_thresholds(d, n, (int)npts);
+  const int bnd = d.bound[n];
+  const float mlow = d.min_lower[n];
+  const bool model_ok = n_valid >= (float)d.min_valid;
+  float thr = t.full, center = fm_nan();
+  int ic = 0;
+  DetSums u;
+  if (d.cur) {
+    for (int c = gl; c < d.C; c += 16) det_count_col(d, n, c, t, sig, gidx, bnd, mlow, model_ok, fcast, u);
+    u.cnt_f = row16_all<false>(u.cnt_f);
+    if (t.differs) u.cnt_l = row16_all<false>(u.cnt_l);
+    if (t.shift_on) {
+      u.cnt_s = row16_all<false>(u.cnt_s);
+      u.zsum = row16_all<false>(u.zsum);
+      u.nz = row16_all<false>(u.nz);
+    }
+    u.anyv = row16_all<true>(u.anyv);
+    u.sc = row16_all<true>(u.sc);
+    thr = det_decide(d, t, u, bnd, &ic, &center);
+  }
+  const float anyv = u.anyv, sc = u.sc;
+  const bool emit = d.anom_count && ic > 0;
+  if (d.forecast || d.upper || d.lower || d.row_out || emit)
+    for (int c = gl; c < d.C; c += 16) det_emit_col(d, n, c, thr, sig, gidx, bnd, mlow, emit, fcast, center);
+  if (d.cur && gl == 0) det_write(d, n, ic, anyv, model_ok, sc, npts);
+}
+
 // One WORKGROUP owns series n: threads stride the columns, block reductions.
 template <typename ForecastFn>
 __device__ __forceinline__ void detect_epilogue(const DetectArgs& d, int n, float sig, float n_valid,

@@ -1428,15 +1428,15 @@ extern "C" size_t fm_hw_d_lds_bytes(int Tp, int seg, int K) {
 }
 
 // Deferred detection for HW variants 4/5: band, verdict, per-app counters and the K9
-// anomaly list from the fitted parameters (one wave per series), with the same
+// anomaly list from the fitted parameters (one 16-lane row per series), with the same
 // forecast as the fused epilogue: level + h * trend + season[(Tp - 1 + h) mod m].
 __global__ __launch_bounds__(256) void hw_detect_params_kernel(const SmoothArgs a) {
-  const int n = blockIdx.x * (blockDim.x / FM_WAVE) + wave_id();
-  if (n >= a.N) return;  // wave-uniform
+  const int n = blockIdx.x * (blockDim.x / 16) + (threadIdx.x >> 4);
+  if (n >= a.N) return;  // row-uniform
   const float gL = a.level[n], gB = a.trend[n], sig = a.sigma[n], nvr = a.nvalid_out[n];
   const float* sb = a.season_hb + (long long)n * HALF_HB;
   const int Tp = a.Tp, m = a.m;
-  detect_epilogue_wave(a.det, n, sig, nvr, [&](int h) {
+  detect_epilogue_row(a.det, n, sig, nvr, [&](int h) {
     int ph = (Tp - 1 + h) % m;
     if (ph < 0) ph += m;
     ph = ph < HALF_HB ? ph : HALF_HB - 1;
@@ -1448,7 +1448,7 @@ extern "C" int fm_hw_detect_params(const SmoothArgs* a, hipStream_t st) {
   if (a->N <= 0 || a->det.C <= 0) return 0;
   if (!a->season_hb || !a->nvalid_out || !a->level || !a->trend || !a->sigma || a->m <= 0)
     return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(hw_detect_params_kernel, dim3((a->N + 3) / 4), dim3(256), 0, st, *a);
+  hipLaunchKernelGGL(hw_detect_params_kernel, dim3((a->N + 15) / 16), dim3(256), 0, st, *a);
   return (int)hipGetLastError();
 }
 

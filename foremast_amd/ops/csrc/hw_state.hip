@@ -259,8 +259,8 @@ __global__ __launch_bounds__(HS_SW) void hw_state_kernel(const HwStateArgs a) {
 
 template <typename TIN>
 __global__ __launch_bounds__(256) void hw_update_detect_kernel(const HwUpdateArgs a) {
-  const int n = blockIdx.x * (256 / FM_WAVE) + wave_id();
-  if (n >= a.N) return;  // wave-uniform
+  const int n = blockIdx.x * 16 + (threadIdx.x >> 4);  // one 16-lane row per series
+  if (n >= a.N) return;  // row-uniform
   const int N = a.N, m = a.m, R = a.ring_len;
   const int gi = a.best[n];
   const float al = a.grid[3 * gi];
@@ -269,7 +269,7 @@ __global__ __launch_bounds__(256) void hw_update_detect_kernel(const HwUpdateArg
   float lvl = a.level[n], trd = a.trend[n];
   int t = a.t_last;
   const TIN* base = (const TIN*)a.hist;
-  // every lane runs the (scalar) update on the same values; lane 0 stores the state
+  // every lane of the row runs the (scalar) update on the same values; its first stores the state
   for (int k = 0; k < a.npts; ++k) {
     ++t;
     const int p = t % m;
@@ -281,14 +281,14 @@ __global__ __launch_bounds__(256) void hw_update_detect_kernel(const HwUpdateArg
     const float e = (y == y) ? y - s - lvl - trd : 0.f;
     lvl = lvl + trd + al * e;
     trd = trd + ab * e;
-    if (lane_id() == 0) *sp = s + g1a * e;
+    if ((lane_id() & 15) == 0) *sp = s + g1a * e;
   }
-  if (lane_id() == 0) {
+  if ((lane_id() & 15) == 0) {
     a.level[n] = lvl;
     a.trend[n] = trd;
   }
   const float* sn = a.season + n;
-  detect_epilogue_wave(a.det, n, a.sigma[n], a.nvalid[n], [&](int h) {
+  detect_epilogue_row(a.det, n, a.sigma[n], a.nvalid[n], [&](int h) {
     return lvl + (float)h * trd + sn[(long long)((t + h) % m) * N];
   }, gi);
 }
@@ -323,7 +323,7 @@ extern "C" int fm_hw_update_detect(const HwUpdateArgs* a, hipStream_t st) {
       a->t_last < 0 || a->ld < a->ring_len || !a->grid || !a->best || !a->level || !a->trend || !a->season ||
       !a->sigma || !a->nvalid)
     return (int)hipErrorInvalidValue;
-  const dim3 grid((a->N + 3) / 4), block(256);
+  const dim3 grid((a->N + 15) / 16), block(256);
   if (a->bf16)
     hipLaunchKernelGGL(hw_update_detect_kernel<bf16_t>, grid, block, 0, st, *a);
   else
