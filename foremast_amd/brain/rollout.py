@@ -1239,9 +1239,12 @@ class RolloutMonitor:
         self._srcmap()  # row map in sync with this tick's admissions / releases (in place)
         use_graph = self.graph_on and pend is not None and pend[2] == 1
         if use_graph:
-            key = (self.cap, tuple(pend[0].shape), pend[0].data_ptr(), self._srcmap_t.data_ptr(),
-                   self._lut.data_ptr(), self.app_stats.data_ptr(), self.win.data_ptr(),
-                   self.cfg.pairwise_algorithm)
+            # every buffer the captured launches address that can be reallocated without a
+            # capacity change (a replay would otherwise read a freed one)
+            src_dev = self._src_dev(pend[0].shape[0], pend[2])
+            key = (self.cap, tuple(pend[0].shape), pend[0].data_ptr(), src_dev.data_ptr(),
+                   self._srcmap_t.data_ptr(), self._lut.data_ptr(), self.app_stats.data_ptr(),
+                   self.win.data_ptr(), self.cfg.pairwise_algorithm)
             g = self._graphs.get(key)
             if g is None:
                 self._score_launch(pend)          # this tick eagerly (allocates any outputs) ...
