@@ -87,7 +87,10 @@ class ElasticJobStore(JobStore):
             resp = self.http.get(f"{self.base}/{self.index}/_mapping")
             if resp.status_code == 200:
                 for idx in resp.json().values():
-                    for typ in (idx.get("mappings") or {}).values():
+                    mappings = idx.get("mappings") or {}
+                    # ES 6.x: {type: {properties}}; a typeless (7.x) index: {properties}
+                    types = [mappings] if "properties" in mappings else list(mappings.values())
+                    for typ in types:
                         name = name or _kw_of((typ or {}).get("properties") or {}, field)
         except (httpx.HTTPError, ValueError, AttributeError):
             name = None

@@ -138,3 +138,18 @@ def test_fake_es_explicit_keyword_mapping_has_no_subfield():
     dyn = ElasticJobStore("http://es:9200", transport=httpx.WSGITransport(app=FakeElasticsearch()))
     dyn.create(_req(1), now=1000.0)
     assert dyn._kw("status") == "status.keyword"
+
+
+def test_es_keyword_detection_reads_typeless_mappings():
+    """A typeless (ES 7) mapping response puts `properties` straight under `mappings`;
+    the store finds the exact-match field there too."""
+    def app(request):
+        if request.url.path.endswith("/_mapping"):
+            body = {"documents": {"mappings": {"properties": {
+                "status": {"type": "keyword"},
+                "claimed_by": {"type": "text", "fields": {"keyword": {"type": "keyword"}}}}}}}
+            return httpx.Response(200, json=body)
+        return httpx.Response(404, json={})
+    st = ElasticJobStore("http://es:9200", transport=httpx.MockTransport(app))
+    assert st._kw("status") == "status"
+    assert st._kw("claimed_by") == "claimed_by.keyword"
