@@ -453,10 +453,13 @@ class LstmShard:
         else:
             L.repack_into(self.packed, self.model)
 
-    def _score_packed(self) -> Dict[str, torch.Tensor]:
+    def _score_packed(self, zl=None, level_done: bool = False) -> Dict[str, torch.Tensor]:
+        """The fused scoring kernel; ``level_done``: the caller has already zeroed the
+        per-app counters and launched the level term (``zl``) on this stream."""
         from ..ops import lstm as L
-        self.app_stats.zero_()
-        zl = self.level_z()
+        if not level_done:
+            self.app_stats.zero_()
+            zl = self.level_z()
         self.out = L.lstm_score(self.packed, None, self.mu, self.sigma, thr_default=self.threshold,
                                 app_id=self.app_id, app_stats=self.app_stats, out=self.out,
                                 ring=self._ring_src(), T=self.T, cal=self.cal, cal_ewma=self.cal_ewma,
@@ -486,19 +489,24 @@ class LstmShard:
             # (N/32 waves, enough to fill the GPU) takes them all
             self._side = torch.cuda.Stream(self.device, priority=-1)
         self._side.wait_stream(main)
+        # the level term (a short kernel the scoring epilogue reads) goes out on the main stream
+        # right after the fork: it runs while the host launches the training step, instead of
+        # delaying the scoring kernel behind it
+        self.app_stats.zero_()
+        zl = self.level_z()
         if self.fused_train:
             # host order: training kernel, scoring kernel, then the training
             # tail (GEMMs, grad scatter, all-reduce, Adam) whose host cost now
             # overlaps both kernels instead of delaying the scoring launch
             with torch.cuda.stream(self._side):
                 self.fg.launch(self.model, None, self._sample_ring(self.train_batch))
-            out = self._score_packed()
+            out = self._score_packed(zl, level_done=True)
             with torch.cuda.stream(self._side):
                 self.trainer.step(None, grad_fn=lambda m, _w: self.fg.finish(m))
         else:
             with torch.cuda.stream(self._side):
                 self.train_step()
-            out = self._score_packed()
+            out = self._score_packed(zl, level_done=True)
         main.wait_stream(self._side)
         return out
 

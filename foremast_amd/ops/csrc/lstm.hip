@@ -316,7 +316,18 @@ __global__ __launch_bounds__(256, 2) void lstm_ae_kernel(const LstmArgs a) {
 }
 
 // one wave per (series, feature): lane = 8 d + q holds points 4q .. 4q+3 of day d's 32-point
-// window (today: only the newest 8 of them)
+// window (today: only the newest 8 of them).  Day sums: two DPP quad butterflies and one
+// ds_swizzle (xor 4) inside each 8-lane day group; the eight day means are then read out with
+// v_readlane (lanes 0, 8, .., 56) and the least squares over the days runs wave-uniform.  Every
+// window of the D <= 7 usable days lies within the newest `avail` samples, so a column needs
+// one conditional wrap, not a modulo.
+__device__ __forceinline__ float day_sum8(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xf, 0xf, false));  // xor 1
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xf, 0xf, false));  // xor 2
+  v += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), (4 << 10) | 0x1F));     // xor 4
+  return v;
+}
+
 __global__ __launch_bounds__(256) void lstm_level_kernel(const LevelArgs a) {
   const long long gw = (long long)blockIdx.x * (blockDim.x / FM_WAVE) + wave_id();
   if (gw >= (long long)a.N * a.F) return;  // wave-uniform
@@ -330,34 +341,32 @@ __global__ __launch_bounds__(256) void lstm_level_kernel(const LevelArgs a) {
   float s = 0.f, c = 0.f;
   if (D >= 1 && d <= D) {
     const long long row = (long long)n * a.src.ld;
+    int col0 = a.newest - back - (LVL_L + E - 1) - d * a.m;
+    col0 += col0 < 0 ? R : 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int p = 4 * q + j;
       if (p >= W || (d == 0 && (p < E || p >= E + LVL_L))) continue;
-      int col = (a.newest - back - (LVL_L + E - 1) + p - d * a.m) % R;
-      col += col < 0 ? R : 0;
+      int col = col0 + p;
+      col -= col >= R ? R : 0;
       const float x = a.src.bf16 ? bf16_to_f32(((const bf16_t*)a.src.ring[f])[row + col])
                                  : ((const float*)a.src.ring[f])[row + col];
       if (x == x) { s += x; c += 1.f; }
     }
   }
+  s = day_sum8(s);
+  c = day_sum8(c);
+  const float mean = c > 0.f ? s / c : fm_nan();  // day d's mean in every lane of its group
+  // least squares of the day means b_d over d = 1..D, extrapolated to d = 0 (wave-uniform)
+  const float today = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mean), 0));
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, sb = 0.f, sdb = 0.f;
 #pragma unroll
-  for (int o = 1; o < 8; o <<= 1) {  // per day
-    s += __shfl_xor(s, o, FM_WAVE);
-    c += __shfl_xor(c, o, FM_WAVE);
-  }
-  const float today = __shfl(c > 0.f ? s / c : fm_nan(), 0, FM_WAVE);
-  // least squares of the day means b_d over d = 1..D (lanes 8d), extrapolated to d = 0
-  const bool use = q == 0 && d >= 1 && d <= D && c > 0.f;
-  const float b = use ? s / c : 0.f, fd = (float)d;
-  float s0 = use ? 1.f : 0.f, s1 = use ? fd : 0.f, s2 = use ? fd * fd : 0.f, sb = b, sdb = use ? fd * b : 0.f;
-#pragma unroll
-  for (int o = 8; o < FM_WAVE; o <<= 1) {
-    s0 += __shfl_xor(s0, o, FM_WAVE);
-    s1 += __shfl_xor(s1, o, FM_WAVE);
-    s2 += __shfl_xor(s2, o, FM_WAVE);
-    sb += __shfl_xor(sb, o, FM_WAVE);
-    sdb += __shfl_xor(sdb, o, FM_WAVE);
+  for (int dd = 1; dd <= 7; ++dd) {
+    const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mean), 8 * dd));
+    if (dd <= D && b == b) {
+      const float fd = (float)dd;
+      s0 += 1.f; s1 += fd; s2 += fd * fd; sb += b; sdb += fd * b;
+    }
   }
   if (lane != 0) return;
   float st = fm_nan();
