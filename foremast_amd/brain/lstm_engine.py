@@ -47,6 +47,7 @@ epilogue also keeps such windows out of the calibration refresh).
 
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -117,6 +118,15 @@ class LstmShard:
         self._ws: Dict[str, torch.Tensor] = {}
         self._all = torch.arange(n_series, device=self.device)
         self._zero_off = torch.zeros(n_series, dtype=torch.long, device=self.device)
+        # whole-tick HIP graph (tick_graph): ring positions travel in a device record
+        # [append column, head after the append] copied from pinned memory by the replay
+        self.graph_on = self.gpu and os.environ.get("FOREMAST_LSTM_GRAPH", "1") != "0"
+        self._graph = None
+        self._graph_key = None
+        self.graph_replays = 0
+        if self.gpu:
+            self._grec_host = torch.zeros(2, dtype=torch.int32).pin_memory()
+            self._grec_dev = torch.zeros(2, dtype=torch.int32, device=self.device)
 
     # ------------------------------------------------------------------ rows (resident monitor)
     def grow(self, capacity: int) -> None:
@@ -219,6 +229,15 @@ class LstmShard:
         x = torch.stack(feats, 2)  # [B, T, F]
         return ((x - self.mean[series_idx][:, None, :]) / self.std[series_idx][:, None, :]).contiguous()
 
+    def _ring_src_dev(self, win_series: Optional[torch.Tensor] = None,
+                      win_start: Optional[torch.Tensor] = None):
+        """:meth:`_ring_src` with the head on the device (graph ticks): the scoring
+        window starts ``length - T`` after it, sampled windows ``win_start`` after it."""
+        from ..ops.lstm import RingSource
+        r0 = self.rings[0]
+        return RingSource(rings=[r.data for r in self.rings], start_col=r0.length - self.T, mean=self.mean,
+                          rstd=self.rstd, win_series=win_series, win_start=win_start, head_dev=self._grec_dev[1:2])
+
     def _ring_src(self, win_series: Optional[torch.Tensor] = None, win_start: Optional[torch.Tensor] = None):
         """Kernel-side input: the kernels read the bf16 rings directly and
         z-score on the fly, so no ``[B, T, F]`` window tensor is materialised.
@@ -227,6 +246,13 @@ class LstmShard:
         r0 = self.rings[0]
         return RingSource(rings=[r.data for r in self.rings], start_col=(r0.head + r0.length - self.T) % r0.R,
                           mean=self.mean, rstd=self.rstd, win_series=win_series, win_start=win_start)
+
+    def _sample_ring_dev(self, B: int):
+        """:meth:`_sample_ring` with starts as offsets from the device head (same draws)."""
+        L = self.rings[0].length
+        si = self._draw_rows(B, torch.int32)
+        st = torch.randint(1, L - self.T + 1, (B,), generator=self.gen, device=self.device, dtype=torch.int32)
+        return self._ring_src_dev(si, st)
 
     def _sample_ring(self, B: int):
         """``B`` random history windows as ring coordinates (two RNG launches):
@@ -414,8 +440,9 @@ class LstmShard:
             sel = rows.to(self.device, torch.long)
             self.lvl_sig[sel] = sig[sel]
 
-    def level_z(self) -> Optional[torch.Tensor]:
-        """``[n, F]`` level z of every series' newest points (None: no level term)."""
+    def level_z(self, head_dev: bool = False) -> Optional[torch.Tensor]:
+        """``[n, F]`` level z of every series' newest points (None: no level term);
+        ``head_dev``: the newest column relative to the graph record's device head."""
         if self.lvl_sig is None or self.level_threshold is None:
             return None
         r0 = self.rings[0]
@@ -423,8 +450,10 @@ class LstmShard:
             return None
         if self.gpu:
             from ..ops import lstm as L
-            self._zl = L.lstm_level([r.data for r in self.rings], (r0.head + r0.length - 1) % r0.R, r0.length,
-                                    self.season, self.level_points, sig=self.lvl_sig, out=self._zl)
+            newest = r0.length - 1 if head_dev else (r0.head + r0.length - 1) % r0.R
+            self._zl = L.lstm_level([r.data for r in self.rings], newest, r0.length, self.season,
+                                    self.level_points, sig=self.lvl_sig, out=self._zl,
+                                    head_dev=self._grec_dev[1:2] if head_dev else None)
             return self._zl
         st = self._level_stat_cpu(0)
         return torch.where(torch.isfinite(st) & (self.lvl_sig > 0), st / self.lvl_sig, 0.0)
@@ -453,7 +482,7 @@ class LstmShard:
         else:
             L.repack_into(self.packed, self.model)
 
-    def _score_packed(self, zl=None, level_done: bool = False) -> Dict[str, torch.Tensor]:
+    def _score_packed(self, zl=None, level_done: bool = False, ring=None) -> Dict[str, torch.Tensor]:
         """The fused scoring kernel; ``level_done``: the caller has already zeroed the
         per-app counters and launched the level term (``zl``) on this stream."""
         from ..ops import lstm as L
@@ -462,7 +491,8 @@ class LstmShard:
             zl = self.level_z()
         self.out = L.lstm_score(self.packed, None, self.mu, self.sigma, thr_default=self.threshold,
                                 app_id=self.app_id, app_stats=self.app_stats, out=self.out,
-                                ring=self._ring_src(), T=self.T, cal=self.cal, cal_ewma=self.cal_ewma,
+                                ring=ring if ring is not None else self._ring_src(), T=self.T, cal=self.cal,
+                                cal_ewma=self.cal_ewma,
                                 zlvl=zl, thr_level=float(self.level_threshold or float("inf")))
         return self.out
 
@@ -476,6 +506,8 @@ class LstmShard:
         are repacked on the main stream before the side stream forks, so
         scoring uses the weights from before this tick's update (a one-step
         model lag) and never races the Adam step; the tick joins both streams."""
+        if self._graph_ready(train, overlap):
+            return self._tick_graph(newx)
         self.ingest_tick(newx)
         if not (train and overlap and self.gpu):
             if train:
@@ -483,12 +515,7 @@ class LstmShard:
             return self.score()
         self._pack_scoring()  # before the wait: the side stream's Adam step must not race the repack
         main = torch.cuda.current_stream(self.device)
-        if self._side is None:
-            # high-priority side stream: the long, latency-bound training kernel
-            # (B/32 wave pairs) must get its CU slots before the scoring grid
-            # (N/32 waves, enough to fill the GPU) takes them all
-            self._side = torch.cuda.Stream(self.device, priority=-1)
-        self._side.wait_stream(main)
+        self._side_stream().wait_stream(main)
         # the level term (a short kernel the scoring epilogue reads) goes out on the main stream
         # right after the fork: it runs while the host launches the training step, instead of
         # delaying the scoring kernel behind it
@@ -509,6 +536,80 @@ class LstmShard:
             out = self._score_packed(zl, level_done=True)
         main.wait_stream(self._side)
         return out
+
+    # ------------------------------------------------------------------ whole-tick HIP graph
+    def _graph_ready(self, train: bool, overlap: bool) -> bool:
+        """Steady-state training ticks on one GPU run as ONE graph replay: the ring is
+        full (the window offsets from the head are constant), this tick does not
+        refresh the series statistics, no collective is involved."""
+        if not (self.graph_on and train and overlap and self.fused_train):
+            return False
+        r0 = self.rings[0]
+        return (r0.length == r0.R and r0.R > self.T and (self.ticks + 1) % self.restat_every != 0
+                and not comm.active())
+
+    def _tick_body(self, newx: torch.Tensor) -> Dict[str, torch.Tensor]:
+        """The graph's launches, in :meth:`tick`'s order: record H2D, ring appends at
+        the device column, repack, fork; level term (main), training kernel (side),
+        scoring (main), training tail + Adam (side); join."""
+        from ..ops import kernels as K
+        main = torch.cuda.current_stream(self.device)
+        self._grec_dev.copy_(self._grec_host, non_blocking=True)
+        for f, ring in enumerate(self.rings):
+            K.ring_append(ring.data, 0, newx[:, f:f + 1], col_dev=self._grec_dev[0:1])
+        self._pack_scoring()
+        side = self._side_stream()
+        side.wait_stream(main)
+        self.app_stats.zero_()
+        zl = self.level_z(head_dev=True)
+        with torch.cuda.stream(side):
+            self.fg.launch(self.model, None, self._sample_ring_dev(self.train_batch))
+        out = self._score_packed(zl, level_done=True, ring=self._ring_src_dev())
+        with torch.cuda.stream(side):
+            self.trainer.step(None, grad_fn=lambda m, _w: self.fg.finish(m))
+        main.wait_stream(side)
+        return out
+
+    def _tick_graph(self, newx: torch.Tensor) -> Dict[str, torch.Tensor]:
+        """One steady-state tick as a HIP-graph replay (captured on the first such tick,
+        whose work runs eagerly; re-captured when anything the graph bakes in moved:
+        buffers, the calibration constants, the sampled rows).  The host mirrors the
+        ring bookkeeping and writes the tick's ring positions into the pinned record."""
+        r0 = self.rings[0]
+        col = r0.next_col()
+        for ring in self.rings:
+            ring.advance(1)
+        self.ticks += 1
+        rec = self._grec_host.numpy()
+        rec[0], rec[1] = col, r0.head
+        live = None if self.live is None else (self.live.data_ptr(), self.live.numel())
+        key = (newx.data_ptr(), tuple(newx.shape), tuple(r.data.data_ptr() for r in self.rings), live,
+               None if self.lvl_sig is None else self.lvl_sig.data_ptr(), self.level_threshold,
+               None if self.cal is None else self.cal.data_ptr(), self.cal_ewma, self.mu, self.sigma,
+               self.threshold, self.app_stats.data_ptr(), self.app_id.data_ptr(), id(self.packed))
+        if self._graph is not None and key == self._graph_key:
+            self._graph.replay()
+            self.graph_replays += 1
+            self.trainer.steps += 1
+            return self.out
+        out = self._tick_body(newx)            # this tick eagerly (builds every buffer) ...
+        torch.cuda.current_stream(self.device).synchronize()
+        g = torch.cuda.CUDAGraph()             # ... the next ones as one replay
+        g.register_generator_state(self.gen)
+        steps = self.trainer.steps
+        with torch.cuda.graph(g):
+            self._tick_body(newx)
+        self.trainer.steps = steps             # the capture ran no step
+        self._graph, self._graph_key = g, key
+        return out
+
+    def _side_stream(self):
+        if self._side is None:
+            # high-priority side stream: the long, latency-bound training kernel
+            # (B/32 wave pairs) must get its CU slots before the scoring grid
+            # (N/32 waves, enough to fill the GPU) takes them all
+            self._side = torch.cuda.Stream(self.device, priority=-1)
+        return self._side
 
     def score(self) -> Dict[str, torch.Tensor]:
         if self.gpu:

@@ -121,6 +121,8 @@ def _declare(lib: C.CDLL) -> None:
     lib.fm_bivariate.restype = I
     lib.fm_ring_append.argtypes = [P, LL, I, I, I, P, LL, LL, I, P]
     lib.fm_ring_append.restype = I
+    lib.fm_ring_append_dev.argtypes = [P, LL, I, I, P, I, P, LL, LL, I, P]
+    lib.fm_ring_append_dev.restype = I
     lib.fm_tick_ingest.argtypes = [P, LL, I, P, LL, I, I, I, P, LL, I, I, P, P, I, P, I, P]
     lib.fm_tick_ingest.restype = I
     lib.fm_tick_ingest_dev.argtypes = [P, LL, P, LL, I, I, P, LL, I, P, P, I, P, P, I, P]

@@ -79,6 +79,7 @@ struct LevelArgs {
   int back_step;     // calibration: offset k ends (k + 1) * back_step samples before the newest
   const float* sig;  // scoring: [N, F] spread of the statistic
   float* out;        // scoring: [N, F] z; calibration: [K, N, F] raw statistic (NaN: not enough data)
+  const int* head_dev;  // optional device ring head: `newest` is then an offset from it
 };
 
 extern __shared__ __attribute__((aligned(16))) char fm_lstm_smem[];
@@ -341,7 +342,8 @@ __global__ __launch_bounds__(256) void lstm_level_kernel(const LevelArgs a) {
   float s = 0.f, c = 0.f;
   if (D >= 1 && d <= D) {
     const long long row = (long long)n * a.src.ld;
-    int col0 = a.newest - back - (LVL_L + E - 1) - d * a.m;
+    const int newest = a.head_dev ? (a.head_dev[0] + a.newest) % R : a.newest;
+    int col0 = newest - back - (LVL_L + E - 1) - d * a.m;
     col0 += col0 < 0 ? R : 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {

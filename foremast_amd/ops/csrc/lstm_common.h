@@ -25,6 +25,7 @@ struct LstmRingSrc {
   const int* win_start;    // [B] start column per window (taken mod ring_len) or null
   const float* mean;       // [N, F]
   const float* rstd;       // [N, F]
+  const int* head_dev;     // optional device ring head: start columns are then offsets from it
 };
 
 namespace fm_lstm {
@@ -45,7 +46,8 @@ __device__ __forceinline__ XPos make_xpos(const float* x, const LstmRingSrc& s, 
   } else {
     p.xrow = nullptr;
     p.row = s.win_series ? s.win_series[w] : w;
-    p.start = (s.win_start ? s.win_start[w] : s.start_col) % s.ring_len;  // any non-negative start
+    const int off = s.win_start ? s.win_start[w] : s.start_col;
+    p.start = ((s.head_dev ? s.head_dev[0] : 0) + off) % s.ring_len;  // any non-negative start
   }
   return p;
 }

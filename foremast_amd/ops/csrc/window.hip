@@ -10,10 +10,14 @@
 // ---------------------------------------------------------------------------------
 // ring append: dst[n, (col0 + j) % R] = src[n, j]   (j < S)
 // ---------------------------------------------------------------------------------
+// col_dev (optional): a device int added to col0 (graph-captured ticks: the column moves
+// every replay, the kernel argument cannot)
 template <typename TOUT>
 __global__ __launch_bounds__(256) void ring_append_kernel(TOUT* __restrict__ dst, long long ld_dst, int R,
-                                                          int col0, int S, const float* __restrict__ src,
-                                                          long long ld_src, long long N) {
+                                                          int col0, const int* __restrict__ col_dev, int S,
+                                                          const float* __restrict__ src, long long ld_src,
+                                                          long long N) {
+  if (col_dev) col0 = (col0 + col_dev[0]) % R;
   const long long total = N * (long long)S;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
@@ -25,20 +29,25 @@ __global__ __launch_bounds__(256) void ring_append_kernel(TOUT* __restrict__ dst
   }
 }
 
-extern "C" int fm_ring_append(void* dst, long long ld_dst, int R, int col0, int S, const float* src,
-                              long long ld_src, long long N, int bf16, hipStream_t st) {
+extern "C" int fm_ring_append_dev(void* dst, long long ld_dst, int R, int col0, const int* col_dev, int S,
+                                  const float* src, long long ld_src, long long N, int bf16, hipStream_t st) {
   if (N <= 0 || S <= 0) return 0;
-  if (R <= 0 || col0 < 0) return (int)hipErrorInvalidValue;
+  if (R <= 0 || col0 < 0 || col0 >= R) return (int)hipErrorInvalidValue;
   long long total = N * (long long)S;
   long long blocks = (total + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   if (bf16)
     hipLaunchKernelGGL(ring_append_kernel<bf16_t>, dim3((unsigned)blocks), dim3(256), 0, st,
-                       (bf16_t*)dst, ld_dst, R, col0, S, src, ld_src, N);
+                       (bf16_t*)dst, ld_dst, R, col0, col_dev, S, src, ld_src, N);
   else
     hipLaunchKernelGGL(ring_append_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, st,
-                       (float*)dst, ld_dst, R, col0, S, src, ld_src, N);
+                       (float*)dst, ld_dst, R, col0, col_dev, S, src, ld_src, N);
   return (int)hipGetLastError();
+}
+
+extern "C" int fm_ring_append(void* dst, long long ld_dst, int R, int col0, int S, const float* src,
+                              long long ld_src, long long N, int bf16, hipStream_t st) {
+  return fm_ring_append_dev(dst, ld_dst, R, col0, nullptr, S, src, ld_src, N, bf16, st);
 }
 
 // ---------------------------------------------------------------------------------

@@ -734,8 +734,9 @@ def bivariate(hx: torch.Tensor, hy: torch.Tensor, head: int, length: int, cur: t
     return out
 
 
-def ring_append(dst: torch.Tensor, col0: int, src: torch.Tensor) -> None:
-    """``dst[n, (col0 + j) % R] = src[n, j]`` (dst may be float32 or bf16)."""
+def ring_append(dst: torch.Tensor, col0: int, src: torch.Tensor, col_dev: Optional[torch.Tensor] = None) -> None:
+    """``dst[n, (col0 + j) % R] = src[n, j]`` (dst may be float32 or bf16); ``col_dev``
+    (int32 device scalar): added to ``col0`` on the device (graph-captured ticks)."""
     lib = nat.require()
     _cuda(dst, "dst")
     _need(dst.dim() == 2 and src.dim() == 2 and dst.shape[0] == src.shape[0], "shape mismatch")
@@ -744,9 +745,12 @@ def ring_append(dst: torch.Tensor, col0: int, src: torch.Tensor) -> None:
     _need(src.device == dst.device, "device mismatch")
     R = dst.shape[1]
     _need(src.shape[1] <= R, "append wider than the ring")
-    nat.check(lib.fm_ring_append(nat.ptr(dst), dst.stride(0), R, int(col0) % R, src.shape[1],
-                                 nat.ptr(src), src.stride(0), dst.shape[0],
-                                 int(dst.dtype == torch.bfloat16), nat.stream_handle(dst.device)),
+    if col_dev is not None:
+        _need(col_dev.dtype == torch.int32 and col_dev.numel() >= 1 and col_dev.device == dst.device,
+              "col_dev must be an int32 device scalar")
+    nat.check(lib.fm_ring_append_dev(nat.ptr(dst), dst.stride(0), R, int(col0) % R, nat.ptr(col_dev), src.shape[1],
+                                     nat.ptr(src), src.stride(0), dst.shape[0],
+                                     int(dst.dtype == torch.bfloat16), nat.stream_handle(dst.device)),
               "fm_ring_append")
 
 

@@ -26,7 +26,7 @@ FP8_SCALE_BYTES = TILES * KSTEPS_FP8 * 64
 class LstmRingSrc(C.Structure):
     _fields_ = [("ring", C.c_void_p * 7), ("ld", C.c_longlong), ("ring_len", C.c_int), ("bf16", C.c_int),
                 ("start_col", C.c_int), ("_pad", C.c_int), ("win_series", C.c_void_p), ("win_start", C.c_void_p),
-                ("mean", C.c_void_p), ("rstd", C.c_void_p)]
+                ("mean", C.c_void_p), ("rstd", C.c_void_p), ("head_dev", C.c_void_p)]
 
 
 @dataclass
@@ -40,6 +40,7 @@ class RingSource:
     rstd: Optional[torch.Tensor] = None          # float32 [N, F]
     win_series: Optional[torch.Tensor] = None    # int32 [B]
     win_start: Optional[torch.Tensor] = None     # int32 [B]
+    head_dev: Optional[torch.Tensor] = None      # int32 device scalar: start_col / win_start are offsets from it
 
     def fill(self, src: "LstmRingSrc", n_windows: int, F: int) -> None:
         r0 = self.rings[0]
@@ -65,6 +66,10 @@ class RingSource:
         src.win_series = nat.ptr(self.win_series)
         src.win_start = nat.ptr(self.win_start)
         src.mean, src.rstd = self.mean.data_ptr(), self.rstd.data_ptr()
+        if self.head_dev is not None:
+            _need(self.head_dev.dtype == torch.int32 and self.head_dev.numel() >= 1
+                  and self.head_dev.device == r0.device, "head_dev must be an int32 device scalar")
+        src.head_dev = nat.ptr(self.head_dev)
 
 
 class LstmArgs(C.Structure):
@@ -83,7 +88,7 @@ class LevelArgs(C.Structure):
     _fields_ = [("src", LstmRingSrc), ("N", C.c_int), ("F", C.c_int), ("newest", C.c_int), ("avail", C.c_int),
                 ("m", C.c_int), ("L", C.c_int), ("E", C.c_int), ("K", C.c_int), ("back_step", C.c_int),
                 ("sig", C.c_void_p),
-                ("out", C.c_void_p)]
+                ("out", C.c_void_p), ("head_dev", C.c_void_p)]
 
 
 nat.register("fm_lstm_level", [C.POINTER(LevelArgs), C.c_void_p])
@@ -382,7 +387,8 @@ def level_extension(m: int) -> int:
 
 def lstm_level(rings: List[torch.Tensor], newest: int, avail: int, m: int, L: int = 8,
                sig: Optional[torch.Tensor] = None, K: int = 0, back_step: int = 0,
-               out: Optional[torch.Tensor] = None, E: Optional[int] = None) -> torch.Tensor:
+               out: Optional[torch.Tensor] = None, E: Optional[int] = None,
+               head_dev: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Level statistic of every (row, feature) (see ``LevelArgs`` in csrc/lstm.hip):
     the mean over the newest ``L`` samples of x_t minus the same minutes' mean over
     up to 7 earlier days.  Scoring (``K == 0``): ``[N, F]`` statistic / ``sig``.
@@ -414,6 +420,10 @@ def lstm_level(rings: List[torch.Tensor], newest: int, avail: int, m: int, L: in
     a.N, a.F, a.newest, a.avail, a.m, a.L, a.E, a.K, a.back_step = N, F, int(newest), int(avail), int(m), int(L), \
         E, int(K), int(back_step)
     a.sig, a.out = nat.ptr(sig), out.data_ptr()
+    if head_dev is not None:  # graph-captured ticks: `newest` is an offset from the device head
+        _need(head_dev.dtype == torch.int32 and head_dev.numel() >= 1 and head_dev.device == dev,
+              "head_dev must be an int32 device scalar")
+    a.head_dev = nat.ptr(head_dev)
     nat.check(lib.fm_lstm_level(C.byref(a), nat.stream_handle(dev)), "fm_lstm_level")
     return out
 

@@ -241,7 +241,12 @@ class FusedLstmGrad:
         else:
             dwe = _mm_f32(self.g_enc, self.h_enc.t())
             dwd = _mm_f32(self.g_dec, self.h_dec[:, :KB].t())
-        dwo = _mm_f32(self.dy.to(torch.bfloat16), self.h_dec[:H, B:].t())  # [F, 64]
+        # [F, 64]: M = F rows over K = T*B is a GEMV that one GEMM tile cannot spread (58 us as
+        # a single hipBLASLt launch at B = 4096); batched over the T slices like dwe / dwd
+        if self.batched_gemm:
+            dwo = _bmm_sum_f32(self.dy.to(torch.bfloat16), self.h_dec[:H, B:].t(), T)
+        else:
+            dwo = _mm_f32(self.dy.to(torch.bfloat16), self.h_dec[:H, B:].t())
         if nat.available():
             self._scatter_grads(model, dwe, dwd, dwo)
             return err.mean()

@@ -167,8 +167,9 @@ class DPTrainer:
         broadcast_params(model, 0, group)
         self.buckets = GradBuckets(list(model.parameters()), bucket_bytes, group, overlap)
         on_gpu = next(model.parameters()).is_cuda
-        # fused multi-tensor Adam on the GPU: one launch for all parameters
-        self.opt = torch.optim.Adam(model.parameters(), lr=lr, fused=on_gpu or None)
+        # fused multi-tensor Adam on the GPU: one launch for all parameters; capturable (its
+        # step counters on the device) so a training step can be part of a HIP graph
+        self.opt = torch.optim.Adam(model.parameters(), lr=lr, fused=on_gpu or None, capturable=on_gpu)
         self.steps = 0
 
     def step(self, windows, grad_fn=None, weight: Optional[float] = None, flags: Optional[torch.Tensor] = None,

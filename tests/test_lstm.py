@@ -275,6 +275,45 @@ def test_lstm_shard_gpu_matches_model(fp8):
     assert any(not torch.equal(b, p) for b, p in zip(before, sh.model.parameters()))
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("fp8", [False, True])
+def test_lstm_tick_graph_matches_eager(fp8, monkeypatch):
+    """A steady-state training tick as ONE HIP-graph replay (ring appends at the device
+    column, repack, level term, training kernel + tail + Adam on the side stream,
+    scoring with the device head) gives the eager tick's outputs and weights, over
+    ticks that cross a statistics refresh (an eager tick inside the graph run)."""
+    from foremast_amd.brain.lstm_engine import LstmShard
+    dev = torch.device("cuda:0")
+    n, R, F = 512, 300, 2
+
+    def make(graph):
+        monkeypatch.setenv("FOREMAST_LSTM_GRAPH", "1" if graph else "0")
+        sh = LstmShard(n, R, F, window=16, device=dev, fp8=fp8, app_id=(torch.arange(n, device=dev) // 4).int(),
+                       n_apps=128, train_batch=256, lr=1e-2, restat_every=4, seed=3)
+        sh.load_history([h.to(dev) for h in _toy_history(n, R, F)])
+        for _ in range(3):
+            sh.train_step()
+        sh.calibrate(512)
+        return sh
+    a, b = make(False), make(True)
+    xa = torch.empty((n, F), device=dev)
+    xb = torch.empty((n, F), device=dev)
+    g = torch.Generator().manual_seed(5)
+    for k in range(9):
+        x = torch.randn(n, F, generator=g) + 10.0
+        xa.copy_(x)
+        xb.copy_(x)
+        oa, ob = a.tick(xa), b.tick(xb)
+        torch.cuda.synchronize()
+        assert torch.equal(oa["verdict"], ob["verdict"]), k
+        torch.testing.assert_close(ob["err"], oa["err"], rtol=1e-6, atol=1e-7)
+        for pa, pb in zip(a.model.parameters(), b.model.parameters()):
+            torch.testing.assert_close(pb, pa, rtol=1e-6, atol=1e-7)
+        assert torch.equal(a.app_stats, b.app_stats)
+    assert b.graph_replays >= 4 and a.graph_replays == 0
+    assert a.trainer.steps == b.trainer.steps
+
+
 def test_backward_register_plan_matches_wT_dgates():
     """CPU emulation of the K7 backward recurrence step: dh_{t-1} = W_hh^T dgates
     from lane-local dgates (forward accumulator order) through the packed W^T
