@@ -482,18 +482,27 @@ class LstmShard:
         else:
             L.repack_into(self.packed, self.model)
 
-    def _score_packed(self, zl=None, level_done: bool = False, ring=None) -> Dict[str, torch.Tensor]:
-        """The fused scoring kernel; ``level_done``: the caller has already zeroed the
-        per-app counters and launched the level term (``zl``) on this stream."""
+    def _level_args(self, ring) -> Optional[Dict]:
+        """The scoring kernel's fused level term (None: no level term yet)."""
+        if self.lvl_sig is None or self.level_threshold is None:
+            return None
+        r0 = self.rings[0]
+        if r0.length < self.level_points + self.LVL_E + self.season:
+            return None
+        newest = r0.length - 1 if ring.head_dev is not None else (r0.head + r0.length - 1) % r0.R
+        return {"sig": self.lvl_sig, "m": self.season, "E": self.LVL_E, "newest": newest, "avail": r0.length}
+
+    def _score_packed(self, zeroed: bool = False, ring=None) -> Dict[str, torch.Tensor]:
+        """The fused scoring kernel, the level term computed inside it; ``zeroed``: the
+        caller has already zeroed the per-app counters on this stream."""
         from ..ops import lstm as L
-        if not level_done:
+        if not zeroed:
             self.app_stats.zero_()
-            zl = self.level_z()
+        ring = ring if ring is not None else self._ring_src()
         self.out = L.lstm_score(self.packed, None, self.mu, self.sigma, thr_default=self.threshold,
                                 app_id=self.app_id, app_stats=self.app_stats, out=self.out,
-                                ring=ring if ring is not None else self._ring_src(), T=self.T, cal=self.cal,
-                                cal_ewma=self.cal_ewma,
-                                zlvl=zl, thr_level=float(self.level_threshold or float("inf")))
+                                ring=ring, T=self.T, cal=self.cal, cal_ewma=self.cal_ewma,
+                                thr_level=float(self.level_threshold or float("inf")), level=self._level_args(ring))
         return self.out
 
     def tick(self, newx: torch.Tensor, train: bool = True, overlap: bool = True) -> Dict[str, torch.Tensor]:
@@ -516,24 +525,20 @@ class LstmShard:
         self._pack_scoring()  # before the wait: the side stream's Adam step must not race the repack
         main = torch.cuda.current_stream(self.device)
         self._side_stream().wait_stream(main)
-        # the level term (a short kernel the scoring epilogue reads) goes out on the main stream
-        # right after the fork: it runs while the host launches the training step, instead of
-        # delaying the scoring kernel behind it
         self.app_stats.zero_()
-        zl = self.level_z()
         if self.fused_train:
             # host order: training kernel, scoring kernel, then the training
             # tail (GEMMs, grad scatter, all-reduce, Adam) whose host cost now
             # overlaps both kernels instead of delaying the scoring launch
             with torch.cuda.stream(self._side):
                 self.fg.launch(self.model, None, self._sample_ring(self.train_batch))
-            out = self._score_packed(zl, level_done=True)
+            out = self._score_packed(zeroed=True)
             with torch.cuda.stream(self._side):
                 self.trainer.step(None, grad_fn=lambda m, _w: self.fg.finish(m))
         else:
             with torch.cuda.stream(self._side):
                 self.train_step()
-            out = self._score_packed(zl, level_done=True)
+            out = self._score_packed(zeroed=True)
         main.wait_stream(self._side)
         return out
 
@@ -549,22 +554,27 @@ class LstmShard:
                 and not comm.active())
 
     def _tick_body(self, newx: torch.Tensor) -> Dict[str, torch.Tensor]:
-        """The graph's launches, in :meth:`tick`'s order: record H2D, ring appends at
-        the device column, repack, fork; level term (main), training kernel (side),
-        scoring (main), training tail + Adam (side); join."""
+        """The graph's launches: record H2D, ring appends at the device column, repacks,
+        training windows sampled, counters zeroed, fork; training kernel (side), scoring
+        with the fused level term (main), training tail + Adam (side); join."""
         from ..ops import kernels as K
         main = torch.cuda.current_stream(self.device)
         self._grec_dev.copy_(self._grec_host, non_blocking=True)
         for f, ring in enumerate(self.rings):
             K.ring_append(ring.data, 0, newx[:, f:f + 1], col_dev=self._grec_dev[0:1])
         self._pack_scoring()
+        # the training step's sampling and packing before the fork: after it each branch
+        # starts with its big kernel, the training kernel created first, so its waves are
+        # resident before scoring fills the GPU (in a graph the stream priority does not order
+        # the branches; a starved training kernel runs after the scoring grid, not beside it)
+        ring_tr = self._sample_ring_dev(self.train_batch)
+        self.fg.pack(self.model)
+        self.app_stats.zero_()
         side = self._side_stream()
         side.wait_stream(main)
-        self.app_stats.zero_()
-        zl = self.level_z(head_dev=True)
         with torch.cuda.stream(side):
-            self.fg.launch(self.model, None, self._sample_ring_dev(self.train_batch))
-        out = self._score_packed(zl, level_done=True, ring=self._ring_src_dev())
+            self.fg.launch(self.model, None, ring_tr, pack=False)
+        out = self._score_packed(zeroed=True, ring=self._ring_src_dev())
         with torch.cuda.stream(side):
             self.trainer.step(None, grad_fn=lambda m, _w: self.fg.finish(m))
         main.wait_stream(side)

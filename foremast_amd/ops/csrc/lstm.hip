@@ -51,6 +51,15 @@ struct LstmArgs {
   const float* zlvl;       // [N, F] level z-scores (lstm_level_kernel) or null
   float thr_level;         // a window is also anomalous when any |zlvl| exceeds this
   int _pad2;
+  // fused level term (ring input, one window per row): with lvl_sig the kernel computes the
+  // level z of its series itself, in a prologue whose loads the other waves' MFMA work hides
+  // (the separate lstm_level_kernel is ~100k tiny waves on the scoring kernel's critical path)
+  const float* lvl_sig;    // [N, F] spread of the level statistic, or null
+  int lvl_m;               // samples per day
+  int lvl_E;               // extra points each side of the earlier days' windows
+  int lvl_newest;          // newest column (an offset from src.head_dev when that is set)
+  int lvl_avail;           // valid samples in the rings
+  float* lvl_out;          // optional [N, F] level z written out, or null
 };
 
 // Level term of the LSTM-AE verdict (lstm_level_kernel): the autoencoder scores the SHAPE
@@ -246,6 +255,78 @@ __device__ __forceinline__ void run_phase(const LstmArgs& a, const void* wlds_v,
   }
 }
 
+// Level z of series n (same statistic as lstm_level_kernel): the two lanes of the series split
+// the days (lane half hh: days hh, hh + 2, hh + 4, hh + 6), exchange their day means, and both
+// fit the least squares over days 1..D.  Returns max_f |z_f|.  Every lane calls it (the
+// exchange is a cross-half shuffle); rows past N compute on row 0 and write nothing.
+__device__ __forceinline__ float fused_level_z(const LstmArgs& a, long long n, bool valid, int hh) {
+  const LstmRingSrc& s = a.src;
+  const int R = s.ring_len, m = a.lvl_m, E = a.lvl_E, W = LVL_L + 2 * E;
+  const int newest = s.head_dev ? (s.head_dev[0] + a.lvl_newest) % R : a.lvl_newest;
+  const int D = min(7, (a.lvl_avail - (LVL_L + E)) / m);
+  const long long row = n * s.ld;
+  float zmax = 0.f;
+  for (int f = 0; f < a.F; ++f) {
+    // a day's points are all loaded before any is summed (fixed trip count, predicated): one
+    // memory latency per day window, not one per point
+    float bm[4];
+#pragma unroll 1
+    for (int i = 0; i < 4; ++i) {
+      const int d = hh + 2 * i;
+      const bool day_ok = D >= 1 && d <= D;
+      int col0 = newest - (LVL_L + E - 1) - d * m;
+      col0 += col0 < 0 ? R : 0;
+      const int p0 = d == 0 ? E : 0, p1 = d == 0 ? E + LVL_L : W;
+      float v[2 * LVL_EMAX + LVL_L];
+#pragma unroll
+      for (int p = 0; p < 2 * LVL_EMAX + LVL_L; ++p) {
+        float x = fm_nan();
+        if (day_ok && p >= p0 && p < p1) {
+          int col = col0 + p;
+          col -= col >= R ? R : 0;
+          x = s.bf16 ? bf16_to_f32(((const bf16_t*)s.ring[f])[row + col]) : ((const float*)s.ring[f])[row + col];
+        }
+        v[p] = x;
+      }
+      float sx = 0.f, cx = 0.f;
+#pragma unroll
+      for (int p = 0; p < 2 * LVL_EMAX + LVL_L; ++p)
+        if (v[p] == v[p]) { sx += v[p]; cx += 1.f; }
+      const float mean = cx > 0.f ? sx / cx : fm_nan();
+      bm[0] = i == 0 ? mean : bm[0];
+      bm[1] = i == 1 ? mean : bm[1];
+      bm[2] = i == 2 ? mean : bm[2];
+      bm[3] = i == 3 ? mean : bm[3];
+    }
+    float ob[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ob[i] = __shfl_xor(bm[i], 32, FM_WAVE);
+    // day d's mean: even days from lane half 0, odd days from half 1
+    auto day = [&](int d) { const int i = d >> 1; return ((d & 1) == hh) ? bm[i] : ob[i]; };
+    const float today = day(0);
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, sb = 0.f, sdb = 0.f;
+#pragma unroll
+    for (int d = 1; d <= 7; ++d) {
+      const float b = day(d);
+      if (d <= D && b == b) {
+        const float fd = (float)d;
+        s0 += 1.f; s1 += fd; s2 += fd * fd; sb += b; sdb += fd * b;
+      }
+    }
+    float st = fm_nan();
+    if (s0 > 0.f && today == today) {
+      const float dbar = s1 / s0, bbar = sb / s0, sdd = s2 - s1 * dbar;
+      const float slope = sdd > 1e-6f ? (sdb - s1 * bbar) / sdd : 0.f;
+      st = today - (bbar - slope * dbar);
+    }
+    const float sg = a.lvl_sig[n * a.F + f];
+    const float z = (st == st && sg > 0.f) ? st / sg : 0.f;
+    if (valid && hh == 0 && a.lvl_out) a.lvl_out[n * a.F + f] = z;
+    zmax = fmaxf(zmax, fabsf(z));
+  }
+  return zmax;
+}
+
 template <bool FP8>
 __global__ __launch_bounds__(256, 2) void lstm_ae_kernel(const LstmArgs a) {
   const int w = wave_id(), lane = lane_id();
@@ -264,6 +345,7 @@ __global__ __launch_bounds__(256, 2) void lstm_ae_kernel(const LstmArgs a) {
     for (int i = threadIdx.x; i < a.F * H; i += blockDim.x) wout[i] = a.w_out[i];
   }
   __syncthreads();
+  const float zl_fused = a.lvl_sig ? fused_level_z(a, sidx, valid, hh) : 0.f;
   float hreg[32], creg[32];
 #pragma unroll
   for (int i = 0; i < 32; ++i) { hreg[i] = 0.f; creg[i] = 0.f; }
@@ -292,7 +374,7 @@ __global__ __launch_bounds__(256, 2) void lstm_ae_kernel(const LstmArgs a) {
     }
     if (a.zscore) a.zscore[series] = z;
     const float thr = a.threshold ? a.threshold[series] : a.thr_default;
-    float zl = 0.f;  // level term: the largest |z| of the series' features
+    float zl = zl_fused;  // level term: the largest |z| of the series' features
     if (a.zlvl)
       for (int f = 0; f < a.F; ++f) zl = fmaxf(zl, fabsf(a.zlvl[series * a.F + f]));
     const int v = (z > thr || zl > a.thr_level) ? 1 : 0;
@@ -407,6 +489,10 @@ extern "C" size_t fm_lstm_lds_bytes(int F, int fp8) {
 extern "C" int fm_lstm_ae(const LstmArgs* a, hipStream_t st) {
   if (a->N <= 0) return 0;
   if (a->F < 1 || a->F > 7 || a->T < 1) return (int)hipErrorInvalidValue;
+  if (a->lvl_sig && (!a->src.ring[0] || a->src.win_series || a->lvl_m < LVL_L + 2 * a->lvl_E || a->lvl_E < 0 ||
+                     a->lvl_E > LVL_EMAX || a->lvl_newest < 0 || a->lvl_newest >= a->src.ring_len ||
+                     a->lvl_avail > a->src.ring_len))
+    return (int)hipErrorInvalidValue;
   const size_t lds = fm_lstm_lds_bytes(a->F, a->fp8);
   dim3 grid((unsigned)((a->N + 127) / 128)), block(256);
   if (a->fp8)

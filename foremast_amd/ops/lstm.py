@@ -81,6 +81,8 @@ class LstmArgs(C.Structure):
         ("app_id", C.c_void_p), ("app_stats", C.c_void_p), ("src", LstmRingSrc),
         ("cal", C.c_void_p), ("cal_ewma", C.c_float), ("zlvl", C.c_void_p), ("thr_level", C.c_float),
         ("_pad2", C.c_int),
+        ("lvl_sig", C.c_void_p), ("lvl_m", C.c_int), ("lvl_E", C.c_int), ("lvl_newest", C.c_int),
+        ("lvl_avail", C.c_int), ("lvl_out", C.c_void_p),
     ]
 
 
@@ -317,7 +319,7 @@ def lstm_score(p: LstmPacked, x: Optional[torch.Tensor], mu: float = 0.0, sigma:
                out: Optional[Dict[str, torch.Tensor]] = None, ring: Optional[RingSource] = None,
                T: Optional[int] = None, cal: Optional[torch.Tensor] = None,
                cal_ewma: float = 0.0, zlvl: Optional[torch.Tensor] = None,
-               thr_level: float = float("inf")) -> Dict[str, torch.Tensor]:
+               thr_level: float = float("inf"), level: Optional[Dict] = None) -> Dict[str, torch.Tensor]:
     """Score windows ``x [N, T, F]`` — or, with ``ring`` (and ``T``), the last
     ``T`` samples of every ring row (or the ``ring.win_series`` / ``win_start``
     windows) read directly by the kernel.
@@ -328,7 +330,11 @@ def lstm_score(p: LstmPacked, x: Optional[torch.Tensor], mu: float = 0.0, sigma:
     terms; with ``cal_ewma > 0`` the kernel moves ``mu`` toward every
     non-anomalous error (relative dispersion kept).  ``zlvl`` ``[N, F]`` (from
     :func:`lstm_level`): a window is also anomalous when any ``|zlvl|`` exceeds
-    ``thr_level``."""
+    ``thr_level``.  ``level`` (ring input, one window per row): the kernel computes the
+    level z itself (:func:`lstm_level`'s statistic) — ``{"sig": [N, F] spread, "m":
+    samples per day, "newest": newest column (an offset from ``ring.head_dev`` when set),
+    "avail": valid samples, "E": extra points (default :func:`level_extension`),
+    "out": optional [N, F] z}``."""
     lib = nat.require()
     if ring is None:
         _need(x is not None and x.is_cuda and x.dtype == torch.float32 and x.dim() == 3 and x.is_contiguous(),
@@ -370,6 +376,19 @@ def lstm_score(p: LstmPacked, x: Optional[torch.Tensor], mu: float = 0.0, sigma:
     a.recon = nat.ptr(out.get("recon")) if want_recon else 0
     a.app_id, a.app_stats = nat.ptr(app_id), nat.ptr(app_stats)
     a.cal, a.cal_ewma = nat.ptr(cal), float(cal_ewma)
+    if level is not None:
+        _need(ring is not None and ring.win_series is None, "the fused level term reads the rings, one window per row")
+        sig, R = level["sig"], ring.rings[0].shape[1]
+        _need(sig.shape == (N, F) and sig.dtype == torch.float32 and sig.is_contiguous() and sig.device == dev,
+              "level sig must be float32 [N, F]")
+        m, newest, avail = int(level["m"]), int(level["newest"]), int(level["avail"])
+        E = level_extension(m) if level.get("E") is None else int(level["E"])
+        _need(0 <= newest < R and 0 < avail <= R and 0 <= E <= 12 and m >= 8 + 2 * E, "level geometry")
+        lo = level.get("out")
+        if lo is not None:
+            _need(lo.shape == (N, F) and lo.dtype == torch.float32 and lo.is_contiguous(), "level out [N, F]")
+        a.lvl_sig, a.lvl_m, a.lvl_E, a.lvl_newest, a.lvl_avail = sig.data_ptr(), m, E, newest, avail
+        a.lvl_out = nat.ptr(lo)
     if zlvl is not None:
         _need(zlvl.shape == (N, F) and zlvl.dtype == torch.float32 and zlvl.is_contiguous() and zlvl.device == dev,
               "zlvl must be float32 [N, F]")

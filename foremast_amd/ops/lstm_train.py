@@ -188,7 +188,13 @@ class FusedLstmGrad:
     phases = 0  # profiling only: restrict the kernel to a subset of its four phases
     batched_gemm = True  # weight-grad reduction as a strided-batched GEMM over time slices
 
-    def launch(self, model, x: Optional[torch.Tensor], ring: Optional[RingSource] = None) -> torch.Tensor:
+    def pack(self, model) -> None:
+        """The weight fragments of the next :meth:`launch` (``launch(..., pack=False)``
+        then skips it: a caller can enqueue the packing ahead, e.g. before a stream fork)."""
+        self._pack(model)
+
+    def launch(self, model, x: Optional[torch.Tensor], ring: Optional[RingSource] = None,
+               pack: bool = True) -> torch.Tensor:
         """Run the fused forward+backward; returns per-window errors ``[B]``.
         ``x [B, T, F]`` windows, or ``ring`` (windows sampled by
         ``win_series``/``win_start``, read straight from the history rings)."""
@@ -199,7 +205,8 @@ class FusedLstmGrad:
         else:
             _need(ring.win_series is not None, "ring training needs sampled windows (win_series/win_start)")
         _need(model.H == H and model.F == self.F, "model shape mismatch")
-        self._pack(model)
+        if pack:
+            self._pack(model)
         w_out = model.out_w.detach().contiguous()
         b_out = model.out_b.detach().contiguous()
         a = LstmTrainArgs()

@@ -583,6 +583,34 @@ def test_lstm_level_kernel_matches_cpu():
 
 
 @pytest.mark.gpu
+def test_fused_level_term_matches_level_kernel():
+    """The scoring kernel's fused level term (its prologue) gives the standalone
+    lstm_level kernel's z, with the head absolute or on the device, and flags the
+    shifted series."""
+    shard, g, m = _level_shard("cuda", torch.bfloat16, n=300, F=3)
+    shifted = torch.arange(0, 300, 7)
+    _level_ticks(shard, g, m, shifted, k=8)
+    shard.calibrate(256)
+    zl = shard.level_z()
+    r0 = shard.rings[0]
+    shard._pack_scoring()
+    for dev_head in (False, True):
+        if dev_head:
+            shard._grec_dev[1] = r0.head
+            ring = shard._ring_src_dev()
+        else:
+            ring = shard._ring_src()
+        lv = shard._level_args(ring)
+        assert lv is not None
+        lv["out"] = torch.full_like(zl, float("nan"))
+        out = L.lstm_score(shard.packed, None, shard.mu, shard.sigma, thr_default=shard.threshold, ring=ring,
+                           T=shard.T, thr_level=float(shard.level_threshold), level=lv)
+        torch.cuda.synchronize()
+        torch.testing.assert_close(lv["out"], zl, rtol=1e-5, atol=1e-5)
+        assert bool((out["verdict"][shifted] == 1).all())
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("sel", [0, 1, 2, 3])
 def test_block_scaled_fp8_mfma_lane_map(sel):
     """The CDNA4 block-scaled MFMA (v_mfma_scale_f32_32x32x64_f8f6f4, e4m3) under the maps
