@@ -174,11 +174,13 @@ def test_lstm_node_two_ranks_dp_replicas_identical(tmp_path):
     try:
         t_end = time.time() + 240
         seen_two = None
+        owners = {}  # app -> owning rank, over every two-rank snapshot (finished apps leave the table)
         while time.time() < t_end and proc.poll() is None:
             t = store.get_meta("cluster_health") or {}
             mem = t.get("members", [])
             if t.get("ranks") == 2 and all(m.get("lstm_model") for m in mem):
                 seen_two = t
+                owners.update({a.split("/")[1]: v["rank"] for a, v in t.get("apps", {}).items()})
                 if store.get(ids["app3"])["status"] == "completed_unhealth":
                     break
             time.sleep(0.5)
@@ -186,8 +188,7 @@ def test_lstm_node_two_ranks_dp_replicas_identical(tmp_path):
         assert seen_two is not None, log
         digests = {m["lstm_model"] for m in seen_two["members"]}
         assert len(digests) == 1, seen_two["members"]              # bit-identical replicas
-        owners = {a.split("/")[1]: v["rank"] for a, v in seen_two["apps"].items()}
-        assert set(owners.values()) == {0, 1}
+        assert set(owners.values()) == {0, 1}, owners
         d = store.get(ids["app3"])
         assert d["status"] == "completed_unhealth", (d["status"], log)
         assert set(json.loads(d["anomalyInfo"])) == {"latency", "error5xx"}
