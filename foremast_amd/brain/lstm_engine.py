@@ -119,13 +119,17 @@ class LstmShard:
         self._all = torch.arange(n_series, device=self.device)
         self._zero_off = torch.zeros(n_series, dtype=torch.long, device=self.device)
         # whole-tick HIP graph (tick_graph): ring positions travel in a device record
-        # [append column, head after the append] copied from pinned memory by the replay
+        # [append column, head after the append] that the replay steps by one tick; the
+        # host writes it only when the rings moved without it (eager ticks, reloads)
         self.graph_on = self.gpu and os.environ.get("FOREMAST_LSTM_GRAPH", "1") != "0"
         self._graph = None
         self._graph_key = None
         self.graph_replays = 0
+        self._grec_last = None  # positions the device record holds after the last graph tick
+        self._grec_k = 0
         if self.gpu:
-            self._grec_host = torch.zeros(2, dtype=torch.int32).pin_memory()
+            # a ring of pinned sources: a re-sync's copy may still be in flight at the next one
+            self._grec_host = torch.zeros((4, 2), dtype=torch.int32).pin_memory()
             self._grec_dev = torch.zeros(2, dtype=torch.int32, device=self.device)
 
     # ------------------------------------------------------------------ rows (resident monitor)
@@ -554,12 +558,12 @@ class LstmShard:
                 and not comm.active())
 
     def _tick_body(self, newx: torch.Tensor) -> Dict[str, torch.Tensor]:
-        """The graph's launches: record H2D, ring appends at the device column, repacks,
+        """The graph's launches: record step, ring appends at the device column, repacks,
         training windows sampled, counters zeroed, fork; training kernel (side), scoring
         with the fused level term (main), training tail + Adam (side); join."""
         from ..ops import kernels as K
         main = torch.cuda.current_stream(self.device)
-        self._grec_dev.copy_(self._grec_host, non_blocking=True)
+        self._grec_dev.add_(1).remainder_(self.rings[0].R)  # the previous tick's positions -> this tick's
         for f, ring in enumerate(self.rings):
             K.ring_append(ring.data, 0, newx[:, f:f + 1], col_dev=self._grec_dev[0:1])
         self._pack_scoring()
@@ -584,14 +588,24 @@ class LstmShard:
         """One steady-state tick as a HIP-graph replay (captured on the first such tick,
         whose work runs eagerly; re-captured when anything the graph bakes in moved:
         buffers, the calibration constants, the sampled rows).  The host mirrors the
-        ring bookkeeping and writes the tick's ring positions into the pinned record."""
+        ring bookkeeping; the replay steps the device record of ring positions itself, so
+        the host writes nothing per tick and a caller may enqueue the next tick before
+        this one ran.  The record is re-written (as the previous tick's positions) only
+        when the rings moved since the last graph tick by anything but one step."""
         r0 = self.rings[0]
+        R = r0.R
         col = r0.next_col()
         for ring in self.rings:
             ring.advance(1)
         self.ticks += 1
-        rec = self._grec_host.numpy()
-        rec[0], rec[1] = col, r0.head
+        now = (col, r0.head)
+        last = self._grec_last
+        if last is None or ((last[0] + 1) % R, (last[1] + 1) % R) != now:
+            rec = self._grec_host[self._grec_k % 4]
+            self._grec_k += 1
+            rec[0], rec[1] = (col - 1) % R, (r0.head - 1) % R
+            self._grec_dev.copy_(rec, non_blocking=True)
+        self._grec_last = now
         live = None if self.live is None else (self.live.data_ptr(), self.live.numel())
         key = (newx.data_ptr(), tuple(newx.shape), tuple(r.data.data_ptr() for r in self.rings), live,
                None if self.lvl_sig is None else self.lvl_sig.data_ptr(), self.level_threshold,

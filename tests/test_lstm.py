@@ -314,6 +314,41 @@ def test_lstm_tick_graph_matches_eager(fp8, monkeypatch):
     assert a.trainer.steps == b.trainer.steps
 
 
+@pytest.mark.gpu
+def test_lstm_tick_graph_enqueued_back_to_back(monkeypatch):
+    """Graph ticks enqueued without a host wait between them (the replay steps the
+    device ring record itself, the host writes nothing per tick) end in the eager
+    shard's rings, weights and counters, across a statistics refresh."""
+    from foremast_amd.brain.lstm_engine import LstmShard
+    dev = torch.device("cuda:0")
+    n, R, F = 512, 300, 2
+
+    def make(graph):
+        monkeypatch.setenv("FOREMAST_LSTM_GRAPH", "1" if graph else "0")
+        sh = LstmShard(n, R, F, window=16, device=dev, fp8=False, app_id=(torch.arange(n, device=dev) // 4).int(),
+                       n_apps=128, train_batch=256, lr=1e-2, restat_every=5, seed=3)
+        sh.load_history([h.to(dev) for h in _toy_history(n, R, F)])
+        sh.train_step()
+        sh.calibrate(512)
+        return sh
+    a, b = make(False), make(True)
+    g = torch.Generator().manual_seed(9)
+    xs = [(torch.randn(n, F, generator=g) + 10.0).pin_memory() for _ in range(9)]
+    for sh in (a, b):
+        x = torch.empty((n, F), device=dev)
+        for xk in xs:
+            x.copy_(xk, non_blocking=True)  # stream-ordered: lands after the previous tick's replay
+            sh.tick(x)
+    torch.cuda.synchronize()
+    assert b.graph_replays >= 4
+    for ra, rb in zip(a.rings, b.rings):
+        assert ra.head == rb.head
+        assert torch.equal(ra.data, rb.data)
+    for pa, pb in zip(a.model.parameters(), b.model.parameters()):
+        torch.testing.assert_close(pb, pa, rtol=1e-6, atol=1e-7)
+    assert torch.equal(a.app_stats, b.app_stats)
+
+
 def test_backward_register_plan_matches_wT_dgates():
     """CPU emulation of the K7 backward recurrence step: dh_{t-1} = W_hh^T dgates
     from lane-local dgates (forward accumulator order) through the packed W^T
