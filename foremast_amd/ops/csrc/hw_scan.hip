@@ -937,29 +937,51 @@ __device__ __forceinline__ v2f half_sum_last(v2f v) {
   return v;
 }
 
-// pass 1 of season 1: D_i = splat(D1_i), v = sum_i W_i D1_i
+// {pair[SEL], pair[SEL]} in one v_pk_mov_b32 (two v_mov_b32 otherwise); the result is a
+// 64-bit register pair from the start: left as one 32-bit value used twice, the season
+// loop's D registers were re-paired by 48 copies on every iteration
+template <int SEL>
+__device__ __forceinline__ v2f pk_splat(v2f pair) {
+  v2f r;
+  if (SEL == 0) asm volatile("v_pk_mov_b32 %0, %1, %1 op_sel:[0,0]" : "=v"(r) : "v"(pair));
+  else asm volatile("v_pk_mov_b32 %0, %1, %1 op_sel:[1,1]" : "=v"(r) : "v"(pair));
+  return r;
+}
+template <int K, int R>
+__device__ __forceinline__ void d_pass1_steps(int q, const Chunk8f& cc, const v2f* wc, v2f* D, v2f& p1, v2f& p2) {
+  if constexpr (R < 8) {
+    const int i = 8 * q + R;
+    if (i < K) {
+      D[i] = pk_splat<R & 1>(chunk_pair<R>(cc));
+      p1 = p1 + wc[2 * R] * D[i];
+      p2 = p2 + wc[2 * R + 1] * D[i];
+    }
+    d_pass1_steps<K, R + 1>(q, cc, wc, D, p1, p2);
+  }
+}
+
+// pass 1 of season 1: D_i = splat(D1_i), v = sum_i W_i D1_i.  A chunk's 16 weight pairs
+// are requested together (one wait per chunk; loaded one at a time, each waited for
+// before the next, they left the pass on the scalar cache's latency) and the next LDS
+// chunk is in flight while this one is summed
 template <int K>
 __device__ __forceinline__ void d_pass1(const float* blk, cfp W, v2f* D, v2f& p1, v2f& p2) {
   constexpr int NCH = (K + 7) / 8;
   p1 = splat2(0.f);
   p2 = splat2(0.f);
+  Chunk8f cc, cn;
+  cn.load(blk);
 #pragma unroll
   for (int q = 0; q < NCH; ++q) {
-    Chunk8f c;
-    c.load(blk + q * D_CHUNK);
+    v2f wc[16];
+    W = launder(W);
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int i = 8 * q + r;
-      if (i < K) {
-        const float d = c.get(r);
-        D[i] = splat2(d);
-        // a 64-bit register pair from the start: left as one 32-bit value used twice, the
-        // season loop's D registers were re-paired by 48 copies on every iteration
-        asm volatile("" : "+v"(D[i]));
-        p1 = p1 + ldv2(W + 4 * i) * D[i];
-        p2 = p2 + ldv2(W + 4 * i + 2) * D[i];
-      }
-    }
+    for (int r = 0; r < 16; ++r)
+      if (16 * q + r < 2 * K) wc[r] = ldv2(W + 32 * q + 2 * r);
+    cc = cn;
+    if (q + 1 < NCH) cn.load(blk + (q + 1) * D_CHUNK);
+    fence_sched();
+    d_pass1_steps<K, 0>(q, cc, wc, D, p1, p2);
     fence_sched();
   }
 }
