@@ -1016,21 +1016,33 @@ __device__ __forceinline__ void d_steps(int q, const Chunk8f& cc, v2f* D, v2f c1
 // FUSE also prefetches the next scan's B^1, B^2, B^4, B^8 (scalar loads) during the last
 // chunk, when the pass-1 weight registers of a next chunk are not needed: the scan then
 // starts without waiting on the scalar cache.
+// chunk 0 of a fused season (its dy chunk and pass-1 weights)
+template <int K>
+__device__ __forceinline__ void d_chunk0(const float* blk, cfp W, Chunk8f& c, v2f* w) {
+  c.load(blk);
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    if (r < 2 * K) w[r] = ldv2(W + 2 * r);
+}
+
 template <int K, bool FUSE>
 __device__ __forceinline__ void d_pass2(const float* blk, v2f* D, v2f c1, v2f c2, v2f g1a, cfp W, v2f& x1,
                                         v2f& x2, v2f& sse, v2f& p1, v2f& p2, cfp tb = nullptr,
                                         Mat2* Bn = nullptr, bool chk = false, const unsigned* ubp = nullptr,
-                                        int* alive = nullptr) {
+                                        int* alive = nullptr, const Chunk8f* c0 = nullptr, const v2f* w0 = nullptr) {
   constexpr int NCH = (K + 7) / 8;
   if (FUSE) { p1 = splat2(0.f); p2 = splat2(0.f); }
   fence_sched();
   Chunk8f cc, cn;
   v2f wc[16], wn[16];
   if (FUSE) {
-    cn.load(blk);
+    if (c0) {  // chunk 0 was requested before the scan (its latency hides under it)
+      cn = *c0;
 #pragma unroll
-    for (int r = 0; r < 16; ++r)
-      if (r < 2 * K) wn[r] = ldv2(W + 2 * r);
+      for (int r = 0; r < 16; ++r) wn[r] = w0[r];
+    } else {
+      d_chunk0<K>(blk, W, cn, wn);
+    }
   }
 #pragma unroll
   for (int q = 0; q < NCH; ++q) {
@@ -1287,8 +1299,10 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
   // argmin or tie it: the wave drops it and takes the next pair from the block's queue.
   // Queue order: the hint pairs (previous winners), then the rest in grid order.
   const int npb = pi_hi - pi_lo;
+  // the hint pairs are fixed for the block: read once (an LDS round trip per pair otherwise)
+  const unsigned hints_pp = (unsigned)__builtin_amdgcn_readfirstlane((int)ubound[3]);
   for (int k = w; k < npb;) {
-    const int pi = hint_pair_at(k, pi_lo, ubound[3]);
+    const int pi = hint_pair_at(k, pi_lo, hints_pp);
     const int c0 = 2 * pi;
     const int c1i = (2 * pi + 1 < a.G) ? 2 * pi + 1 : c0;
     const cfp tab = const_ptr(a.pair_tab + (size_t)pi * TS);
@@ -1300,8 +1314,10 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
     Mat2 Bp[4];  // B^1, B^2, B^4, B^8 of the next scan
     Bj.a = one; Bj.b = zero; Bj.c = zero; Bj.d = one;
 #pragma unroll
+    for (int bit = 0; bit < 4; ++bit) Bp[bit] = ldmat(tb + 8 * bit);
+    fence_sched();  // all four requested before the first is used: one scalar-cache wait, not four
+#pragma unroll
     for (int bit = 0; bit < 4; ++bit) {
-      Bp[bit] = ldmat(tb + 8 * bit);
       const Mat2 r = matmul(Bj, Bp[bit]);
       if ((lane >> bit) & 1) Bj = r;
     }
@@ -1312,10 +1328,12 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
     int alive = 1;  // per lane: 0 once this lane's partial SSEs exceed the bound (read wave-wide)
     for (int sg = 1; sg < nseg - 1; ++sg) {
       v2f x1, x2;
+      Chunk8f c0;
+      v2f w0[16];
+      d_chunk0<K>(mydl + (size_t)sg * SEA, launder(W), c0, w0);  // in flight during the scan
       half_uniform_scan_pre(Bp, launder(tb), p1, p2, X1, X2, Bj, odd_row, x1, x2);
-      // checked in seasons max(2, nseg - 4) .. nseg - 2
       d_pass2<K, true>(mydl + (size_t)sg * SEA, D, c1, c2, g1a, launder(W), x1, x2, sse, p1, p2, tb, Bp,
-                       PRUNE, ubound + half, &alive);
+                       PRUNE, ubound + half, &alive, &c0, w0);
       X1 = half_last_bp(x1, last_addr);
       X2 = half_last_bp(x2, last_addr);
       if (PRUNE && !__any(alive)) break;
