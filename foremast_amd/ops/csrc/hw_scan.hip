@@ -1035,6 +1035,11 @@ __device__ __forceinline__ void d_pass2(const float* blk, v2f* D, v2f c1, v2f c2
   fence_sched();
   Chunk8f cc, cn;
   v2f wc[16], wn[16];
+  // the prune bound, read at the season's start and compared at its last chunk (its LDS
+  // round trip hides under the walk; a bound read early is only larger: it prunes less,
+  // never wrongly)
+  unsigned ub = 0x7f800000u;
+  if (FUSE && chk) ub = __hip_atomic_load(ubp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   if (FUSE) {
     if (c0) {  // chunk 0 was requested before the scan (its latency hides under it)
       cn = *c0;
@@ -1053,7 +1058,7 @@ __device__ __forceinline__ void d_pass2(const float* blk, v2f* D, v2f c1, v2f c2
       // Only lanes 31 / 63 hold their half's sum and vote; the wave keeps the pair while
       // either of them does (the caller's __any).
       const v2f s = half_sum_last(sse);  // the same sum as the final SSE
-      const float U = __uint_as_float(__hip_atomic_load(ubp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+      const float U = __uint_as_float(ub);
       int v = ((lane_id() & 31) == 31 && !(s.x > U && s.y > U)) ? 1 : 0;
       asm volatile("" : "+v"(v));  // the flag lives in a VGPR: no scalar register across the loop
       *alive = v;
