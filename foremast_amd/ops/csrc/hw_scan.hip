@@ -461,33 +461,9 @@ __device__ __forceinline__ void row_round_z(v2f& w1, v2f& w2, const Mat2& Bd) {
   w1 = w1 + Bd.a * q1 + Bd.b * q2;
   w2 = w2 + Bd.c * q1 + Bd.d * q2;
 }
-// half_uniform_scan with BOUND_CTRL moves (rows 0 / 2 never read the row_bcast result)
-__device__ __forceinline__ void half_uniform_scan_z(cfp tab_b, v2f v1, v2f v2, v2f x01, v2f x02,
-                                                    const Mat2& Bj, bool odd_row, v2f& s1, v2f& s2) {
-  const Mat2 B1 = ldmat(tab_b), B2 = ldmat(tab_b + 8), B4 = ldmat(tab_b + 16), B8 = ldmat(tab_b + 24),
-             B16 = ldmat(tab_b + 32);
-  v2f w1 = dppz2<0x111, 0xf>(v1);
-  v2f w2 = dppz2<0x111, 0xf>(v2);
-  row_round_z<0x111>(w1, w2, B1);
-  row_round_z<0x112>(w1, w2, B2);
-  row_round_z<0x114>(w1, w2, B4);
-  row_round_z<0x118>(w1, w2, B8);
-  v2f e1, e2;
-  matvec(B1, w1, w2, e1, e2);
-  e1 = e1 + v1;
-  e2 = e2 + v2;
-  const v2f E1 = dppz2<0x142, 0xa>(e1), E2 = dppz2<0x142, 0xa>(e2);
-  v2f y1, y2;
-  matvec(B16, x01, x02, y1, y2);
-  y1 = odd_row ? y1 + E1 : x01;
-  y2 = odd_row ? y2 + E2 : x02;
-  matvec(Bj, y1, y2, s1, s2);
-  s1 = s1 + w1;
-  s2 = s2 + w2;
-}
-
-// half_uniform_scan_z with B^1..B^8 already in registers (only B^16 is loaded here; it is
-// first used after the four row rounds)
+// half_uniform_scan with BOUND_CTRL moves (rows 0 / 2 never read the row_bcast result) and
+// B^1..B^8 already in registers (only B^16 is loaded here; it is first used after the four
+// row rounds)
 __device__ __forceinline__ void half_uniform_scan_pre(const Mat2* Bp, cfp tab_b, v2f v1, v2f v2, v2f x01, v2f x02,
                                                       const Mat2& Bj, bool odd_row, v2f& s1, v2f& s2) {
   const Mat2 B16 = ldmat(tab_b + 32);

@@ -83,9 +83,6 @@ constexpr int SCALE_ONE = 0x7f7f7f7f;
 // activation.  (__frcp_rn / '/' lower to the ~10-instruction IEEE division
 // sequence.)  Saturates cleanly: exp2 → inf gives rcp → 0.
 constexpr float LOG2E = 1.4426950408889634f;
-__device__ __forceinline__ float sigm(float v) {
-  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-LOG2E * v));
-}
 __device__ __forceinline__ float tanh_f(float v) {
   return 2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-2.f * LOG2E * v)) - 1.f;
 }
