@@ -348,7 +348,10 @@ __device__ __forceinline__ void fwd_phase2(const LstmTrainArgs& a, const uint4* 
   bf16_t* hbuf = ENC ? a.h_enc : a.h_dec;
   const long long ldh = ENC ? KB : KB + a.B;
   // prologue: publish the initial h (zeros for the encoder, the encoder's final h for the decoder)
-  uint4 hb[4];
+  // h as MFMA B fragments: k-steps 2w, 2w + 1 are this wave's units (hm), the other two the
+  // other wave's (ho).  Kept as two arrays with compile-time indices: one array indexed by
+  // the run-time wave id lived in scratch (four 16-byte scratch loads per time step)
+  uint4 hm[2], ho[2];
   auto publish_h = [&](int buf) {
 #pragma unroll
     for (int sl = 0; sl < 2; ++sl) {
@@ -356,14 +359,14 @@ __device__ __forceinline__ void fwd_phase2(const LstmTrainArgs& a, const uint4* 
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = hreg[(2 * sl + (j >> 2)) * 4 + (j & 3)];
       const uint4 f = pack8(v);
-      hb[2 * w + sl] = f;
+      hm[sl] = f;
       x.hb[((buf * 2 + w) * 2 + sl) * 64 + lane] = f;
     }
   };
   auto collect_h = [&](int buf) {
     const int o = 1 - w;
 #pragma unroll
-    for (int sl = 0; sl < 2; ++sl) hb[2 * o + sl] = x.hb[((buf * 2 + o) * 2 + sl) * 64 + lane];
+    for (int sl = 0; sl < 2; ++sl) ho[sl] = x.hb[((buf * 2 + o) * 2 + sl) * 64 + lane];
   };
   publish_h(1);
   __syncthreads();
@@ -401,8 +404,11 @@ __device__ __forceinline__ void fwd_phase2(const LstmTrainArgs& a, const uint4* 
     for (int tp = 0; tp < 4; tp += 2) {
       f32x16 acc0 = (f32x16){}, acc1 = (f32x16){};
 #pragma unroll
-      for (int s = 0; s < KSTEPS; ++s) {
-        const uint4 bfr = (s < 4) ? hb[s] : xb;
+      for (int k = 0; k < KSTEPS; ++k) {
+        // k-step order: this wave's two h steps, the other wave's two, then x (h steps are
+        // summed in a wave-dependent order; the weight fragment follows the step)
+        const uint4 bfr = k < 2 ? hm[k] : k < 4 ? ho[k - 2] : xb;
+        const int s = k < 4 ? ((k + 2 * w) & 3) : k;
         acc0 = mfma_bf16(wlds[((TB + tp) * KSTEPS + s) * 64 + lo], bfr, acc0);
         acc1 = mfma_bf16(wlds[((TB + tp + 1) * KSTEPS + s) * 64 + lo], bfr, acc1);
       }
