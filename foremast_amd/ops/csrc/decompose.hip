@@ -700,22 +700,29 @@ __global__ __launch_bounds__(SB, M > 0 ? 6 : 4) void decompose_score_kernel(cons
     //    next series, whose first LDS writes cannot touch pmv before wave 0 has joined them).
     //    Split epilogue (sfc): only the seasonal terms of horizons 1..hmax leave here.
     if (w == 0) {
+      // (float) T and the lane's seasonal-term address are derived here, per series: hoisted
+      // out of the loop they were spilled, and the reload's vmcnt(0) drained the next
+      // series' prefetched samples (the trap the argument / tid laundering above avoids)
+      int Tn = T;
+      asm volatile("" : "+s"(Tn));
+      const float Tf = (float)Tn;
+      const int ln = tid & (FM_WAVE - 1);
       const float Ks = fmaxf((float)(T - 2 * h) / (float)m, 1.5f);
       const float sig = sqrtf(rss / fmaxf(tcnt, 1.f)) * sqrtf((Ks + 1.f) / (Ks - 1.f));
       const float slope = (tr_e - tr_p) / (float)m;
-      if (lane == 0) {
+      if (ln == 0) {
         if (a->fc_level) a->fc_level[n] = tr_e;
         if (a->fc_slope) a->fc_slope[n] = slope;
         if (a->sigma) a->sigma[n] = sig;
-        if (a->nvalid) a->nvalid[n] = (float)T;
+        if (a->nvalid) a->nvalid[n] = Tf;
       }
-      const int tlast = T - 1;
+      const int tlast = Tn - 1;
       if (a->sfc) {
-        if (lane < a->hmax) a->sfc[(long long)n * a->hmax + lane] = pmv[(tlast + 1 + lane) % m] - pmean;
+        if (ln < a->hmax) a->sfc[(long long)n * a->hmax + ln] = pmv[(tlast + 1 + ln) % m] - pmean;
         continue;
       }
       const DetectArgs det = kdet(a);
-      detect_epilogue_wave(det, n, sig, (float)T, [&](int hz) {
+      detect_epilogue_wave(det, n, sig, Tf, [&](int hz) {
         int p = (tlast + hz) % m;
         p += p < 0 ? m : 0;
         return tr_e + slope * (float)(tlast + hz - te) + (pmv[p] - pmean);
