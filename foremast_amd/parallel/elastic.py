@@ -69,13 +69,23 @@ class ElasticWorld:
         long kernel or a blocked collective)."""
         period = period_s if period_s is not None else self.hb_timeout / 4
         self._hb_stop = threading.Event()
+        self._hb_dead = threading.Event()
+        # a transient store error must not silence a healthy rank: retry on the next
+        # period; only after errors spanning a whole heartbeat timeout does the thread
+        # give up, and then it says so (changed() beats on the main thread instead)
+        give_up_after = max(3, int(self.hb_timeout / max(period, 1e-3)) + 1)
 
         def loop():
+            fails = 0
             while not self._hb_stop.wait(period):
                 try:
                     self.beat(self.hb_store)
-                except Exception:  # noqa: BLE001 - store gone: stop beating
-                    return
+                    fails = 0
+                except Exception:  # noqa: BLE001 - store hiccup: retry next period
+                    fails += 1
+                    if fails >= give_up_after:
+                        self._hb_dead.set()
+                        return
 
         self.beat()
         th = threading.Thread(target=loop, daemon=True, name=f"heartbeat-{self.id}")
@@ -148,8 +158,9 @@ class ElasticWorld:
                                 timeout=self.coll_timeout, **kw)
 
     def changed(self) -> bool:
-        if getattr(self, "_hb_stop", None) is None or self._hb_stop.is_set():
-            self.beat()  # no heartbeat thread: this call is the beat
+        if (getattr(self, "_hb_stop", None) is None or self._hb_stop.is_set()
+                or self._hb_dead.is_set()):
+            self.beat()  # no (live) heartbeat thread: this call is the beat
         return len(self.live()) != len(self.members)
 
     def reform(self, settle_s: float = 0.0) -> None:

@@ -153,12 +153,21 @@ class NodeRoster:
                 self.mode = ("pass", k)
                 self.log.mark_reset()
                 changed = True
-            self.names = names_fn()
+                reset = True
             self.n_apps = int(n or 0)
+            # the node's names are this rank's OWN list, as of this exchange: the engine
+            # frees and reuses indices in place later in the tick (intake), so aliasing its
+            # list would pair this tick's counters with the next tick's names
             if reset:
+                self.names = list(names_fn())
                 self.log.mark_reset()
                 changed = True
             elif items:
+                names = self.names
+                for i, nm in items:
+                    if i >= len(names):
+                        names.extend([None] * (i + 1 - len(names)))
+                    names[i] = nm
                 self.log.note_many(items)
                 changed = True
             if changed:

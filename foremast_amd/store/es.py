@@ -73,15 +73,22 @@ class ElasticJobStore(JobStore):
             kw["transport"] = transport
         self.http = httpx.Client(**kw)
         self._kw_cache: Dict[str, str] = {}
+        self._kw_miss: Dict[str, float] = {}   # field -> time of the last mapping read that did not name it
+        self.kw_miss_ttl_s = 30.0
 
     def _kw(self, field: str) -> str:
         """Exact-match name of ``field`` in the job index, read from the index mapping
         once it names the field (dynamic mapping: ``<field>.keyword``; an explicit
         ``keyword`` mapping: the bare field).  Until then the dynamic-mapping name is
-        used and the mapping is asked again next time."""
+        used, and the mapping is asked again only after ``kw_miss_ttl_s`` (a negative
+        answer is cached too: otherwise every search before the field's first write
+        would cost one more round trip)."""
         got = self._kw_cache.get(field)
         if got is not None:
             return got
+        miss = self._kw_miss.get(field)
+        if miss is not None and time.monotonic() - miss < self.kw_miss_ttl_s:
+            return field + ".keyword"
         name = None
         try:
             resp = self.http.get(f"{self.base}/{self.index}/_mapping")
@@ -95,7 +102,9 @@ class ElasticJobStore(JobStore):
         except (httpx.HTTPError, ValueError, AttributeError):
             name = None
         if name is None:
+            self._kw_miss[field] = time.monotonic()
             return field + ".keyword"
+        self._kw_miss.pop(field, None)
         self._kw_cache[field] = name
         return name
 
@@ -229,6 +238,8 @@ class ElasticJobStore(JobStore):
                      modified_ts=now, modified_at=stamp)
             if self._put_versioned(d, vers[id(d)]):  # lost races simply drop out
                 out.append(d)
+        if out:  # this process just wrote claimed_by: the mapping names it now
+            self._kw_miss.pop("claimed_by", None)
         return out
 
     def all(self):

@@ -300,3 +300,47 @@ def test_bench_n_rank_equals_one_rank(extra):
         assert d["n_gpus"] == n and d["config"]["parallelism"] == f"dp{n}"
         assert d["health"] == ref["health"], n
         assert d["detection"] == ref["detection"], n
+
+
+class _FlakyStore:
+    """A store whose ``set`` fails ``fail`` times, then works (a transient TCPStore error)."""
+
+    def __init__(self, fail: int) -> None:
+        self.kv, self.fail, self.calls = {}, fail, 0
+
+    def set(self, k, v):
+        self.calls += 1
+        if self.fail > 0:
+            self.fail -= 1
+            raise RuntimeError("store hiccup")
+        self.kv[k] = v.encode() if isinstance(v, str) else v
+
+    def check(self, keys):
+        return all(k in self.kv for k in keys)
+
+    def get(self, k):
+        return self.kv[k]
+
+
+def test_heartbeat_thread_survives_a_transient_store_error():
+    """one failing ``hb_store.set`` must not end the heartbeat (the rank
+    would be voted out while healthy); a thread that does give up is recorded so
+    ``changed()`` beats on the main thread."""
+    from foremast_amd.parallel.elastic import ElasticWorld
+    main, hb = _FlakyStore(0), _FlakyStore(1)
+    ew = ElasticWorld(main, "a", ["a"], heartbeat_timeout_s=0.4, heartbeat_store=hb)
+    ew.start_heartbeat(period_s=0.02)
+    t_end = time.time() + 5
+    while "hb/a" not in hb.kv and time.time() < t_end:
+        time.sleep(0.01)
+    assert "hb/a" in hb.kv and hb.calls >= 2   # the first set failed, a later one landed
+    assert not ew._hb_dead.is_set()
+    ew.stop_heartbeat()
+    # a store that stays down: the thread gives up and says so; changed() then beats itself
+    dead = _FlakyStore(10 ** 6)
+    ew2 = ElasticWorld(main, "b", ["b"], heartbeat_timeout_s=0.1, heartbeat_store=dead)
+    ew2.start_heartbeat(period_s=0.01)
+    assert ew2._hb_dead.wait(5.0)
+    main.kv.pop("hb/b", None)
+    assert not ew2.changed()
+    assert "hb/b" in main.kv

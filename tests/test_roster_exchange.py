@@ -156,3 +156,31 @@ def test_node_roster_pass_and_merged_modes_match_the_engines():
         assert [n for n in mirror if n] == [n for n in nr.names if n] and \
             {i: n for i, n in enumerate(mirror) if n} == {i: n for i, n in enumerate(nr.names) if n}, tick
     assert modes == {"pass", "merged"}
+
+
+def test_pass_through_roster_is_a_snapshot_of_the_exchange():
+    """in pass-through mode the node's names are the rank's own list as of the
+    exchange: an engine that frees an app and admits another at the same index AFTER the
+    exchange (intake runs later in the tick) must not rename the published counters."""
+    import torch
+    from foremast_amd.parallel.roster import ChangeLog, NodeRoster
+    names, log = [("ns", "a"), ("ns", "b")], ChangeLog()
+    log.note(0, names[0])
+    log.note(1, names[1])
+    nr = NodeRoster(1, "cpu")
+    reset, items = log.drain()
+    nr.update([(reset, items, lambda: names, 2)])
+    table = torch.tensor([[1, 5], [0, 5]], dtype=torch.int32)
+    before = list(nr.names)
+    # intake after the exchange: "a" finishes, "c" is admitted into its index
+    names[0] = None
+    log.note(0, None)
+    names[0] = ("ns", "c")
+    log.note(0, ("ns", "c"))
+    assert nr.names == before and nr.names[0] == ("ns", "a")
+    assert nr.counts([table])[0].tolist() == [1, 5]
+    # the next exchange applies the changes (O(changes), no full copy)
+    reset, items = log.drain()
+    assert not reset
+    assert nr.update([(reset, items, lambda: names, 2)])
+    assert nr.names == [("ns", "c"), ("ns", "b")] and nr.names is not names

@@ -153,3 +153,25 @@ def test_es_keyword_detection_reads_typeless_mappings():
     st = ElasticJobStore("http://es:9200", transport=httpx.MockTransport(app))
     assert st._kw("status") == "status"
     assert st._kw("claimed_by") == "claimed_by.keyword"
+
+
+def test_es_keyword_negative_answer_is_cached():
+    """until the mapping names a field, the fallback is cached for a TTL instead of
+    costing one GET /_mapping per search; the mapping is read again after the TTL or once this
+    process has written the field."""
+    gets = []
+    props = {}
+
+    def app(request):
+        if request.url.path.endswith("/_mapping"):
+            gets.append(1)
+            return httpx.Response(200, json={"documents": {"mappings": {"properties": dict(props)}}})
+        return httpx.Response(404, json={})
+    st = ElasticJobStore("http://es:9200", transport=httpx.MockTransport(app))
+    for _ in range(5):
+        assert st._kw("claimed_by") == "claimed_by.keyword"
+    assert len(gets) == 1
+    props["claimed_by"] = {"type": "keyword"}
+    st.kw_miss_ttl_s = 0.0            # TTL over: asked again, and the positive answer sticks
+    assert st._kw("claimed_by") == "claimed_by"
+    assert st._kw("claimed_by") == "claimed_by" and len(gets) == 2
