@@ -92,6 +92,9 @@ def parse():
     p.add_argument("--gap-frac", type=float, default=0.0,
                    help="canary: fraction of series whose 7-day history has a 30-minute scrape outage (NaN run) "
                         "after the first season (production-like gaps; those series take the masked kernels)")
+    p.add_argument("--miss-rate", type=float, default=0.0,
+                   help="canary: probability of an isolated missed scrape per history point (NaN; e.g. 1e-3 = "
+                        "~10 per series-week); gapped series pairs take the masked-season Holt-Winters kernel")
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--graph", dest="graph", action="store_true", default=True,
                    help="(default) canary: the GPU part of a steady-state tick (ring advance, ingest, rank tests, "
@@ -371,6 +374,14 @@ def setup_canary(args, world, rank, dev):
         rows, starts = grows[mine] - s, gstarts[mine]
         cols = (starts[:, None] + torch.arange(30)[None, :]).reshape(-1)
         hist[rows.repeat_interleave(30).to(hist.device), cols.to(hist.device)] = float("nan")
+    if args.miss_rate > 0:
+        # isolated misses at a hash of the GLOBAL (series, column): every sharding drops the same points
+        gr = torch.arange(s, e, device=hist.device, dtype=torch.int64)[:, None]
+        gc = torch.arange(hist.shape[1], device=hist.device, dtype=torch.int64)[None, :]
+        h = (gr * 1_000_003 + gc) * 6364136223846793005 + 1442695040888963407
+        u = ((h >> 33) & 0xFFFFFF).double() / float(1 << 24)
+        hist[u < args.miss_rate] = float("nan")
+        del gr, gc, h, u
     shard.load_history(hist)
     del hist
     W, P = args.window, args.pods
@@ -540,6 +551,9 @@ def setup_canary(args, world, rank, dev):
         "multi_cluster": bool(args.multi_cluster),
         "affine_exchanges": router.exchanges if args.multi_cluster else 0,
         "gap_frac": args.gap_frac,
+        "miss_rate": args.miss_rate,
+        "prune_hints": ("previous winners first (exact: the branch and bound's order only)"
+                        if os.environ.get("FOREMAST_HW_HINTS", "1") != "0" else "off (grid order)"),
         "pairwise_shift_sigma": cfg.pairwise_shift,
         "health_collectives": "1 fused all_gather" if agg.fused else ("all_reduce + all_gather" if agg.active else "none"),
         "hip_graph": bool(args.graph and dev.type == "cuda"),
@@ -559,6 +573,12 @@ def setup_canary(args, world, rank, dev):
     meta["_agg"] = agg
     meta["_truth"] = (truth_apps, n_apps)
     meta["_graph_used"] = lambda: shard._graph is not None  # captured (vs eager fallback)
+    if dev.type == "cuda" and args.algorithm == "holt_winters":
+        from foremast_amd.ops import kernels as K
+        d0 = K.hw_deferred_total(dev)
+        # series pairs per fit that took the gapped-series kernel (a pair with a missing point
+        # past season 0), averaged over every tick run
+        meta["_deferred"] = lambda ticks: round((K.hw_deferred_total(dev) - d0) / max(1, ticks), 2)
     return tick, health_host, meta, dt, args.series
 
 
@@ -872,6 +892,7 @@ def main():
     node_roll = meta.pop("_roll", None)
     node_breakdowns = meta.pop("_breakdowns", None)
     graph_used = meta.pop("_graph_used", None)
+    deferred = meta.pop("_deferred", None)
     for k in [k for k in meta if k.startswith("_")]:
         meta.pop(k)
     if truth is not None and world > 1:
@@ -928,6 +949,8 @@ def main():
     elapsed = time.perf_counter() - t0
     if graph_used is not None:
         meta["hip_graph"] = bool(graph_used())
+    if deferred is not None:
+        meta["gapped_pairs_per_tick"] = deferred(args.warmup + args.steps)
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     lat_t = torch.tensor(lat, dtype=torch.float64, device=dev)
     if world > 1:

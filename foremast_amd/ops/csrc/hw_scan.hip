@@ -962,27 +962,51 @@ __device__ __forceinline__ void d_pass1(const float* blk, cfp W, v2f* D, v2f& p1
   }
 }
 
-// the 8 steps of chunk q (compile-time r: the Δ operand's register half is static)
-template <int K, bool FUSE, int R>
+// e with both grid points' components zeroed where bit `bit` of `keep` is clear (keep:
+// the lane's valid-step bits): a missing observation's step carries the forecast
+// (e = 0: no SSE term, no seasonal update).  v_bfe_i32 + two v_and_b32.
+__device__ __forceinline__ v2f keep_if(v2f e, unsigned keep, int bit) {
+  const int mk = ((int)(keep << (31 - bit))) >> 31;  // -1: observed, 0: missing
+  v2f r;
+  r.x = __int_as_float(__float_as_int(e.x) & mk);
+  r.y = __int_as_float(__float_as_int(e.y) & mk);
+  return r;
+}
+
+// the 8 steps of chunk q (compile-time r: the Δ operand's register half is static).
+// Gapped seasons (hw_dg_block): M2 masks this season's missing steps (keep bits k2 of the
+// chunk's word); R1 runs the next season's pass 1 as the masked recurrence from a zero
+// state (p = the lane's end state from zero: its affine offset, exact with gaps) instead
+// of the table sum, whose uniform weights assume every step observed (keep bits k1).
+template <int K, bool FUSE, int R, bool M2 = false, bool R1 = false>
 __device__ __forceinline__ void d_steps(int q, const Chunk8f& cc, v2f* D, v2f c1, v2f c2, v2f g1a, const v2f* wc,
-                                        v2f& x1, v2f& x2, v2f& sse, v2f& p1, v2f& p2) {
+                                        v2f& x1, v2f& x2, v2f& sse, v2f& p1, v2f& p2, unsigned k2 = 0u,
+                                        unsigned k1 = 0u) {
   if constexpr (R < 8) {
     const int i = 8 * q + R;
     if (i < K) {
-      const v2f e = D[i] - x1;
+      v2f e = D[i] - x1;
+      if (M2) e = keep_if(e, k2, i & 31);
       const v2f t = x1 + x2;
       x1 = t + c1 * e;
       x2 = x2 + c2 * e;
       sse = sse + e * e;
       if (FUSE) {
         D[i] = add_dy<R>(D[i], cc) - g1a * e;
-        p1 = p1 + wc[2 * R] * D[i];
-        p2 = p2 + wc[2 * R + 1] * D[i];
+        if (R1) {
+          const v2f tz = p1 + p2;
+          const v2f ez = keep_if(D[i] - p1, k1, i & 31);
+          p1 = tz + c1 * ez;
+          p2 = p2 + c2 * ez;
+        } else {
+          p1 = p1 + wc[2 * R] * D[i];
+          p2 = p2 + wc[2 * R + 1] * D[i];
+        }
       } else if (i < HALF_HB) {
         D[i] = D[i] - g1a * e;
       }
     }
-    d_steps<K, FUSE, R + 1>(q, cc, D, c1, c2, g1a, wc, x1, x2, sse, p1, p2);
+    d_steps<K, FUSE, R + 1, M2, R1>(q, cc, D, c1, c2, g1a, wc, x1, x2, sse, p1, p2, k2, k1);
   }
 }
 
@@ -1001,12 +1025,15 @@ __device__ __forceinline__ void d_chunk0(const float* blk, cfp W, Chunk8f& c, v2
     if (r < 2 * K) w[r] = ldv2(W + 2 * r);
 }
 
-template <int K, bool FUSE>
+template <int K, bool FUSE, bool M2 = false, bool R1 = false>
 __device__ __forceinline__ void d_pass2(const float* blk, v2f* D, v2f c1, v2f c2, v2f g1a, cfp W, v2f& x1,
                                         v2f& x2, v2f& sse, v2f& p1, v2f& p2, cfp tb = nullptr,
                                         Mat2* Bn = nullptr, bool chk = false, const unsigned* ubp = nullptr,
-                                        int* alive = nullptr, const Chunk8f* c0 = nullptr, const v2f* w0 = nullptr) {
+                                        int* alive = nullptr, const Chunk8f* c0 = nullptr, const v2f* w0 = nullptr,
+                                        unsigned k2lo = 0u, unsigned k2hi = 0u, unsigned k1lo = 0u,
+                                        unsigned k1hi = 0u) {
   constexpr int NCH = (K + 7) / 8;
+  constexpr bool WTS = FUSE && !R1;  // table pass 1: the chunk's weights
   if (FUSE) { p1 = splat2(0.f); p2 = splat2(0.f); }
   fence_sched();
   Chunk8f cc, cn;
@@ -1016,7 +1043,7 @@ __device__ __forceinline__ void d_pass2(const float* blk, v2f* D, v2f c1, v2f c2
   // never wrongly)
   unsigned ub = 0x7f800000u;
   if (FUSE && chk) ub = __hip_atomic_load(ubp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  if (FUSE) {
+  if (WTS) {
     if (c0) {  // chunk 0 was requested before the scan (its latency hides under it)
       cn = *c0;
 #pragma unroll
@@ -1024,6 +1051,8 @@ __device__ __forceinline__ void d_pass2(const float* blk, v2f* D, v2f c1, v2f c2
     } else {
       d_chunk0<K>(blk, W, cn, wn);
     }
+  } else if (FUSE) {
+    cn.load(blk);
   }
 #pragma unroll
   for (int q = 0; q < NCH; ++q) {
@@ -1039,7 +1068,7 @@ __device__ __forceinline__ void d_pass2(const float* blk, v2f* D, v2f c1, v2f c2
       asm volatile("" : "+v"(v));  // the flag lives in a VGPR: no scalar register across the loop
       *alive = v;
     }
-    if (FUSE) {
+    if (WTS) {
       cc = cn;
 #pragma unroll
       for (int r = 0; r < 16; ++r) wc[r] = wn[r];
@@ -1055,14 +1084,20 @@ __device__ __forceinline__ void d_pass2(const float* blk, v2f* D, v2f c1, v2f c2
 #pragma unroll
         for (int b = 0; b < 4; ++b) Bn[b] = ldmat(tb + 8 * b);
       }
+    } else if (FUSE) {  // recurrence pass 1: dy chunks only (the next scan is the general one)
+      cc = cn;
+      asm volatile("" ::"v"(cc.lo.x), "v"(cc.hi.x));
+      if (q + 1 < NCH) cn.load(blk + (q + 1) * D_CHUNK);
     }
     fence_sched();
-    d_steps<K, FUSE, 0>(q, cc, D, c1, c2, g1a, wc, x1, x2, sse, p1, p2);
+    // chunk q's steps 8q .. 8q + 7 lie in one 32-bit word of the lane's keep bits
+    d_steps<K, FUSE, 0, M2, R1>(q, cc, D, c1, c2, g1a, wc, x1, x2, sse, p1, p2, q < 4 ? k2lo : k2hi,
+                                q < 4 ? k1lo : k1hi);
     fence_sched();
   }
   // retire the B prefetch here (it landed during the last chunk) so the wait the compiler
   // needs for it is not placed after the caller's end-state ds_bpermutes
-  if (FUSE && Bn) {
+  if (WTS && Bn) {
     asm volatile("" ::"s"(Bn[0].a.x), "s"(Bn[3].d.y));
     fence_sched();
   }
@@ -1439,6 +1474,471 @@ __global__ __launch_bounds__(256, 2) void hw_d_kernel(const SmoothArgs a, int hm
                        hints);
 }
 
+// ---- variant 5, gapped series: hw_dg_kernel ------------------------------------------------
+// A series pair with a missing observation past season 0 leaves hw_d_kernel (which keeps its
+// straight-line dense walk) for this kernel, persistent over the deferred list.  Same
+// residual-state walk, same semantics as the fp64 reference (models/smoothing.py): a missing
+// step carries the forecast (e = 0: no SSE term, no seasonal update) and sigma divides by the
+// valid points.  Per season the pair takes the dense code unless that season has a gap:
+//  * a missing y is imputed as 0 in the season-difference image (D = y* - s stays the exact
+//    residual chain: y* never reaches an error, the step is masked) and flagged in a 64-bit
+//    per-(series, season, lane) miss mask;
+//  * pass 2 of a gapped season masks e at its missing steps (keep_if: 3 VALU per step);
+//  * pass 1 of a gapped NEXT season runs as the masked recurrence from a zero state (4 ops per
+//    step instead of the 2 of the table sum, whose uniform weights assume no gap): its end
+//    state is the lane map's exact offset v; the map's matrix M is the product of the lane's
+//    step matrices, A for an observed step and A_m = [[1, 1], [0, 1]] for a missing one,
+//    assembled run by run from a table of A^0 .. A^K (lane_map);
+//  * the season after such a pass 1 takes the general affine scan (per-lane M, v), the
+//    others the uniform-matrix scan.
+// So a pair pays the gap code only in the seasons that hold a gap (a 30-minute outage: one
+// season), and the dense kernel is untouched.
+template <int K>
+__device__ __forceinline__ Mat2 pow_at(const float* pw, int n) {
+  const float4 lo = *(const float4*)(pw + 8 * n), hi = *(const float4*)(pw + 8 * n + 4);
+  Mat2 m;
+  m.a.x = lo.x; m.a.y = lo.y; m.b.x = lo.z; m.b.y = lo.w;
+  m.c.x = hi.x; m.c.y = hi.y; m.d.x = hi.z; m.d.y = hi.w;
+  return m;
+}
+
+// The lane's season map matrix from its miss bits (bit i: step i missing): runs of observed
+// steps are table powers A^n, a run of r missing steps is A_m^r = [[1, r], [0, 1]].  The
+// loop runs as often as the lane of the wave with the most miss runs (usually 1-3).
+template <int K>
+__device__ __forceinline__ Mat2 lane_map(const float* pw, unsigned lo, unsigned hi) {
+  unsigned long long b = ((unsigned long long)hi << 32) | lo;
+  Mat2 M;
+  M.a = splat2(1.f); M.b = splat2(0.f); M.c = splat2(0.f); M.d = splat2(1.f);
+  int pos = 0;
+  while (__any(b != 0ull)) {
+    if (b != 0ull) {
+      const int i0 = __builtin_ctzll(b);
+      const unsigned long long rest = ~(b >> i0);
+      const int r = rest ? __builtin_ctzll(rest) : 64 - i0;
+      M = matmul(pow_at<K>(pw, i0 - pos), M);
+      const v2f rr = splat2((float)r);
+      M.a = M.a + rr * M.c;
+      M.b = M.b + rr * M.d;
+      pos = i0 + r;
+      b = pos >= 64 ? 0ull : (b >> pos) << pos;
+    }
+  }
+  return matmul(pow_at<K>(pw, K - pos), M);
+}
+
+// pass 1 of season 1 as the masked recurrence (D^(1) from LDS into the D registers)
+template <int K, int R>
+__device__ __forceinline__ void dg_pass1_steps(int q, const Chunk8f& cc, v2f* D, v2f c1, v2f c2, unsigned kw, v2f& p1,
+                                               v2f& p2) {
+  if constexpr (R < 8) {
+    const int i = 8 * q + R;
+    if (i < K) {
+      D[i] = pk_splat<R & 1>(chunk_pair<R>(cc));
+      const v2f t = p1 + p2;
+      const v2f e = keep_if(D[i] - p1, kw, i & 31);
+      p1 = t + c1 * e;
+      p2 = p2 + c2 * e;
+    }
+    dg_pass1_steps<K, R + 1>(q, cc, D, c1, c2, kw, p1, p2);
+  }
+}
+template <int K>
+__device__ __forceinline__ void dg_pass1_rec(const float* blk, v2f* D, v2f c1, v2f c2, unsigned klo, unsigned khi,
+                                             v2f& p1, v2f& p2) {
+  constexpr int NCH = (K + 7) / 8;
+  p1 = splat2(0.f);
+  p2 = splat2(0.f);
+  Chunk8f cc, cn;
+  cn.load(blk);
+#pragma unroll
+  for (int q = 0; q < NCH; ++q) {
+    cc = cn;
+    if (q + 1 < NCH) cn.load(blk + (q + 1) * D_CHUNK);
+    fence_sched();
+    dg_pass1_steps<K, 0>(q, cc, D, c1, c2, q < 4 ? klo : khi, p1, p2);
+    fence_sched();
+  }
+}
+
+// one fused season of the gapped walk: pass 2 of season sg (masked if it has a gap) + pass 1
+// of season sg + 1 (recurrence if IT has a gap); returns whether the next scan is general
+template <int K>
+__device__ __forceinline__ void dg_season(bool m2, bool r1, const float* blk, v2f* D, v2f c1, v2f c2, v2f g1a, cfp W,
+                                          v2f& x1, v2f& x2, v2f& sse, v2f& p1, v2f& p2, cfp tb, Mat2* Bp,
+                                          bool chk, const unsigned* ubp, int* alive, unsigned k2lo, unsigned k2hi,
+                                          unsigned k1lo, unsigned k1hi) {
+  // two variants, not four: a third or fourth copy of the 45-step walk spilled into the hot
+  // blocks (-Rpass-analysis); a season that needs only one of the two masks runs the other
+  // with every keep bit set (exact, a few ops per step dearer)
+  if (!m2 && !r1)
+    d_pass2<K, true, false, false>(blk, D, c1, c2, g1a, W, x1, x2, sse, p1, p2, tb, Bp, chk, ubp, alive);
+  else
+    d_pass2<K, true, true, true>(blk, D, c1, c2, g1a, W, x1, x2, sse, p1, p2, tb, nullptr, chk, ubp, alive, nullptr,
+                                 nullptr, k2lo, k2hi, k1lo, k1hi);
+}
+
+template <int K, bool PRUNE>
+__device__ __forceinline__ void hw_dg_block(const SmoothArgs& a, int hmax, int n0, int hints) {
+  constexpr int SEA = DLay<K>::SEASON;
+  constexpr int TS = PairTab<K>::SIZE;
+  constexpr int NMW = (32 * K + 31) / 32;
+  const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+  const int half = lane >> 5, j = lane & 31;
+  const bool odd_row = ((lane >> 4) & 1) != 0;
+  const int nseg = a.Tp / a.seg, m = a.m, ns1 = nseg - 1;
+  const int npairs = (a.G + 1) / 2;
+
+  // ---- LDS: the hw_d_block layout, then mbits[2][ns1][32][2] | segm[2][ns1] | nvc[2]
+  float* dl = (float*)fm_hw_smem;
+  unsigned* vmask = (unsigned*)(dl + (size_t)2 * ns1 * SEA);
+  float* stat = (float*)(vmask + 2 * NMW);
+  int* flag = (int*)(stat + 8 * D_WAVES);
+  float* ylast = (float*)(flag + 4);
+  float* bests = ylast + 2 * HALF_HB;
+  float* wbest = bests + 4 * 2 * HALF_HB;
+  unsigned* ubound = (unsigned*)(wbest + 4 * 2 * 4);
+  unsigned* mbits = ubound + 4;
+  int* segm = (int*)(mbits + 2 * ns1 * 64);
+  float* nvc = (float*)(segm + 2 * ns1);
+
+  for (int i = tid; i < 2 * NMW + 8 * D_WAVES + 4; i += blockDim.x) vmask[i] = 0u;
+  for (int i = tid; i < 2 * ns1 * 64 + 2 * ns1 + 2; i += blockDim.x) mbits[i] = 0u;  // mbits, segm, nvc = 0.f
+  if (tid < 3) ubound[tid] = tid < 2 ? 0x7f800000u : 0u;
+  if (tid == 3) {
+    unsigned hp[2] = {0xffffu, 0xffffu};
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int b = (hints && n0 + r < a.N) ? a.best[n0 + r] : -1;
+      const int q = (b >= 0 && b < a.G) ? b / 2 : -1;
+      if (q >= 0 && q < npairs && (r == 0 || (unsigned)q != hp[0])) hp[r] = (unsigned)q;
+    }
+    ubound[3] = hp[0] | (hp[1] << 16);
+  }
+  const int head = a.head_dev ? *a.head_dev : a.head;
+  __syncthreads();
+
+  // ---- stage (as hw_d_block: aligned rings in 16-byte season chunks, else per element) -----
+  {
+    constexpr int GRP = 8;
+    const int R = a.ring_len;
+    const bool al = (R % GRP == 0) && (m % GRP == 0) && (a.ld % GRP == 0) &&
+                    ((((unsigned long long)a.hist) & 15ull) == 0);
+    const int phi = al ? (((a.pad - head) % GRP) + GRP) % GRP : 0;
+    const int ostart = phi ? phi - GRP : 0;
+    const int ngrp = (m - ostart + GRP - 1) / GRP;
+    float s0 = 0.f, c0 = 0.f, s1 = 0.f, c1 = 0.f, s0b = 0.f, c0b = 0.f, s1b = 0.f, c1b = 0.f;
+    float nv0 = 0.f, nv1 = 0.f;
+    for (int g = tid; g < 2 * ngrp; g += blockDim.x) {
+      const int r = g >= ngrp ? 1 : 0, o0 = ostart + (g - r * ngrp) * GRP;
+      const int n = n0 + r;
+      const bool real = n < a.N;
+      const bf16_t* row = (const bf16_t*)a.hist + (long long)(real ? n : 0) * a.ld;
+      float y[D_MAXSEG][GRP];
+      if (al) {
+#pragma unroll
+        for (int k = 0; k < D_MAXSEG; ++k) {
+          const int t0 = k * m + o0 - a.pad;
+          int c = (head + t0) % R;
+          c += c < 0 ? R : 0;
+          uint4 wv = make_uint4(0u, 0u, 0u, 0u);
+          if (k < nseg) wv = *(const uint4*)(row + c);
+          const unsigned ww[4] = {wv.x, wv.y, wv.z, wv.w};
+#pragma unroll
+          for (int u = 0; u < GRP; ++u) {
+            const unsigned x = ww[u >> 1];
+            const float v = __uint_as_float((u & 1) ? (x & 0xffff0000u) : (x << 16));
+            const bool ok = real && k < nseg;
+            y[k][u] = ok ? (t0 + u >= 0 ? v : fm_nan()) : 0.f;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < D_MAXSEG; ++k) {
+#pragma unroll
+          for (int u = 0; u < GRP; ++u) {
+            const bool ok = real && k < nseg && o0 + u < m;
+            const int t = k * m + o0 + u - a.pad;
+            const bool pos = t >= 0;
+            int c = head + ((ok && pos) ? t : 0);
+            c -= (c >= R) ? R : 0;
+            const float v = bf16_to_f32(row[c]);
+            y[k][u] = ok ? (pos ? v : fm_nan()) : 0.f;
+          }
+        }
+      }
+      const int ob = o0 > 0 ? o0 : 0;
+      const int jjb = ob / K, ib = ob - jjb * K;
+      unsigned vlo = 0u, vhi = 0u;
+#pragma unroll
+      for (int u = 0; u < GRP; ++u) {
+        const int o = o0 + u;
+        if (o >= 0 && o < m) {
+          int i = ib + (o - ob), jj = jjb;
+          if (i >= K) { i -= K; ++jj; }
+          const bool v0 = y[0][u] == y[0][u];
+          // seasons >= 1: a missing y is flagged and imputed as 0 (y*), see above
+#pragma unroll
+          for (int k = 1; k < D_MAXSEG; ++k) {
+            if (k < nseg) {
+              if (y[k][u] != y[k][u]) {
+                y[k][u] = 0.f;
+                atomicOr(&mbits[((r * ns1 + (k - 1)) * 32 + jj) * 2 + (i >> 5)], 1u << (i & 31));
+                segm[r * ns1 + (k - 1)] = 1;
+              } else {
+                if (r == 0) nv0 += 1.f; else nv1 += 1.f;
+              }
+            }
+          }
+          float* blk = dl + (size_t)r * ns1 * SEA + dl_off(i, jj);
+          blk[0] = v0 ? y[1][u] - y[0][u] : y[1][u];  // D^(1) = y1* - s0; + l0 for valid y0 below
+          if (v0) {
+            if ((o >> 5) == ((o0 < 0 ? 0 : o0) >> 5)) vlo |= 1u << (o & 31);
+            else vhi |= 1u << (o & 31);
+          }
+#pragma unroll
+          for (int k = 1; k < D_MAXSEG - 1; ++k)
+            if (k < ns1) blk[(size_t)k * SEA] = y[k + 1][u] - y[k][u];
+          if (o < HALF_HB) {
+            float yl = y[1][u];
+#pragma unroll
+            for (int k = 2; k < D_MAXSEG; ++k)
+              if (k == ns1) yl = y[k][u];
+            ylast[r * HALF_HB + o] = yl;
+          }
+          // season-1 mean: observed points only (the imputed 0s are not data)
+          const bool v1 = !((mbits[((r * ns1) * 32 + jj) * 2 + (i >> 5)] >> (i & 31)) & 1u);
+          const float y0v = v0 ? y[0][u] : 0.f, y0c = v0 ? 1.f : 0.f;
+          const float y1v = v1 ? y[1][u] : 0.f, y1c = v1 ? 1.f : 0.f;
+          if (r == 0) { s0 += y0v; c0 += y0c; s1 += y1v; c1 += y1c; }
+          else { s0b += y0v; c0b += y0c; s1b += y1v; c1b += y1c; }
+        }
+      }
+      const int wlo = (o0 < 0 ? 0 : o0) >> 5;
+      if (vlo) atomicOr(&vmask[r * NMW + wlo], vlo);
+      if (vhi) atomicOr(&vmask[r * NMW + wlo + 1], vhi);
+    }
+    s0 = wave_sum(s0); c0 = wave_sum(c0); s1 = wave_sum(s1); c1 = wave_sum(c1);
+    s0b = wave_sum(s0b); c0b = wave_sum(c0b); s1b = wave_sum(s1b); c1b = wave_sum(c1b);
+    nv0 = wave_sum(nv0); nv1 = wave_sum(nv1);
+    if (lane == 0) {
+      float* sw = stat + 8 * w;
+      sw[0] = s0; sw[1] = c0; sw[2] = s1; sw[3] = c1;
+      sw[4] = s0b; sw[5] = c0b; sw[6] = s1b; sw[7] = c1b;
+      atomicAdd(&nvc[0], nv0);  // integer-valued: exact in any order
+      atomicAdd(&nvc[1], nv1);
+    }
+  }
+  __syncthreads();
+  float l0r[2], b0r[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    float st[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int v = 0; v < D_WAVES; ++v)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) st[u] += stat[8 * v + 4 * r + u];
+    l0r[r] = st[1] > 0.f ? st[0] / st[1] : 0.f;
+    b0r[r] = ((st[3] > 0.f ? st[2] / st[3] : 0.f) - l0r[r]) / (float)m;
+  }
+  for (int col = tid; col < 2 * m; col += blockDim.x) {
+    const int r = col >= m ? 1 : 0, o = col - r * m;
+    if ((vmask[r * NMW + (o >> 5)] >> (o & 31)) & 1u) {
+      const int jj = o / K, i = o - jj * K;
+      dl[(size_t)r * ns1 * SEA + dl_off(i, jj)] += l0r[r];
+    }
+  }
+  // gapped seasons of the pair (either series): bit sg for season sg (1 .. ns1)
+  int segbits = 0;
+  for (int k = 0; k < ns1; ++k) segbits |= (segm[k] | segm[ns1 + k]) ? (2 << k) : 0;
+  segbits = __builtin_amdgcn_readfirstlane(segbits);
+  __syncthreads();
+
+  const float l0 = half ? l0r[1] : l0r[0], b0 = half ? b0r[1] : b0r[0];
+  const float* mydl = dl + (size_t)half * ns1 * SEA + j * 4;
+  const unsigned* mymb = mbits + ((size_t)half * ns1 * 32 + j) * 2;  // + (sg - 1) * 64
+  const int last_addr = ((lane & 32) | 31) << 2;
+  float bestSSE = __builtin_huge_valf();
+  int bestIdx = 0x7fffffff;
+  float bestL = l0, bestB = b0;
+  float* mybest = bests + (w * 2 + half) * HALF_HB;
+  const int nwaves = blockDim.x / FM_WAVE;
+  const float* powbase = a.pair_tab + (size_t)npairs * TS;  // [npairs][K + 1][8]: A^0 .. A^K
+  const unsigned hints_pp = (unsigned)__builtin_amdgcn_readfirstlane((int)ubound[3]);
+  for (int k = w; k < npairs;) {
+    const int pi = hint_pair_at(k, 0, hints_pp);
+    const int c0 = 2 * pi;
+    const int c1i = (2 * pi + 1 < a.G) ? 2 * pi + 1 : c0;
+    const cfp tab = const_ptr(a.pair_tab + (size_t)pi * TS);
+    const v2f c1 = ldv2(tab), c2 = ldv2(tab + 2), g1a = ldv2(tab + 4);
+    const cfp W = tab + PairTab<K>::W0;
+    const cfp tb = tab + PairTab<K>::B0;
+    const float* pw = powbase + (size_t)pi * (K + 1) * 8;
+    const v2f one = splat2(1.f), zero = splat2(0.f);
+    Mat2 Bj;
+    Mat2 Bp[4];
+    Bj.a = one; Bj.b = zero; Bj.c = zero; Bj.d = one;
+#pragma unroll
+    for (int bit = 0; bit < 4; ++bit) Bp[bit] = ldmat(tb + 8 * bit);
+    fence_sched();
+#pragma unroll
+    for (int bit = 0; bit < 4; ++bit) {
+      const Mat2 r = matmul(Bj, Bp[bit]);
+      if ((lane >> bit) & 1) Bj = r;
+    }
+    v2f D[K];
+    v2f X1 = splat2(l0 + b0), X2 = splat2(b0), sse = zero;
+    v2f p1, p2;
+    Aff<v2f> loc;
+    bool general = (segbits & 2) != 0;
+    if (general) {
+      const unsigned mlo = mymb[0], mhi = mymb[1];
+      dg_pass1_rec<K>(mydl, D, c1, c2, ~mlo, ~mhi, p1, p2);
+      const Mat2 M = lane_map<K>(pw, mlo, mhi);
+      loc.m11 = M.a; loc.m12 = M.b; loc.m21 = M.c; loc.m22 = M.d; loc.v1 = p1; loc.v2 = p2;
+    } else {
+      d_pass1<K>(mydl, W, D, p1, p2);
+    }
+    int alive = 1;
+    for (int sg = 1; sg < ns1; ++sg) {
+      v2f x1, x2;
+      if (general) {
+        half_exclusive_scan(loc, j);
+        x1 = loc.m11 * X1 + loc.m12 * X2 + loc.v1;
+        x2 = loc.m21 * X1 + loc.m22 * X2 + loc.v2;
+      } else {
+        half_uniform_scan_pre(Bp, launder(tb), p1, p2, X1, X2, Bj, odd_row, x1, x2);
+      }
+      const bool m2 = (segbits >> sg) & 1, r1 = (segbits >> (sg + 1)) & 1;
+      const unsigned* mb2 = mymb + (size_t)(sg - 1) * 64;
+      const unsigned* mb1 = mb2 + 64;
+      const unsigned n2lo = mb2[0], n2hi = mb2[1], n1lo = mb1[0], n1hi = mb1[1];
+      dg_season<K>(m2, r1, mydl + (size_t)sg * SEA, D, c1, c2, g1a, launder(W), x1, x2, sse, p1, p2, tb, Bp,
+                   PRUNE, ubound + half, &alive, ~n2lo, ~n2hi, ~n1lo, ~n1hi);
+      // the gapped variant ran pass 1 as the recurrence (whichever of its masks it needed):
+      // the next scan takes the general lane maps
+      general = m2 || r1;
+      if (general) {
+        const Mat2 M = lane_map<K>(pw, n1lo, n1hi);
+        loc.m11 = M.a; loc.m12 = M.b; loc.m21 = M.c; loc.m22 = M.d; loc.v1 = p1; loc.v2 = p2;
+      }
+      X1 = half_last_bp(x1, last_addr);
+      X2 = half_last_bp(x2, last_addr);
+      if (PRUNE && !__any(alive)) break;
+    }
+    if (!PRUNE || __any(alive)) {
+      v2f x1, x2, d1, d2;
+      if (general) {
+        half_exclusive_scan(loc, j);
+        x1 = loc.m11 * X1 + loc.m12 * X2 + loc.v1;
+        x2 = loc.m21 * X1 + loc.m22 * X2 + loc.v2;
+      } else {
+        half_uniform_scan_pre(Bp, tb, p1, p2, X1, X2, Bj, odd_row, x1, x2);
+      }
+      if ((segbits >> ns1) & 1) {
+        const unsigned* mb2 = mymb + (size_t)(ns1 - 1) * 64;
+        d_pass2<K, false, true, false>(mydl, D, c1, c2, g1a, W, x1, x2, sse, d1, d2, nullptr, nullptr, false,
+                                       nullptr, nullptr, nullptr, nullptr, ~mb2[0], ~mb2[1]);
+      } else {
+        d_pass2<K, false>(mydl, D, c1, c2, g1a, W, x1, x2, sse, d1, d2);
+      }
+      X1 = half_last_bp(x1, last_addr);
+      X2 = half_last_bp(x2, last_addr);
+      sse = half_sum_last(sse);
+      sse = half_last_bp(sse, last_addr);
+      const bool upd0 = (sse.x < bestSSE || (sse.x == bestSSE && c0 < bestIdx));
+      if (upd0) { bestSSE = sse.x; bestIdx = c0; bestL = X1.x - X2.x; bestB = X2.x; }
+      const bool upd1 = (c1i != c0) && (sse.y < bestSSE || (sse.y == bestSSE && c1i < bestIdx));
+      if (upd1) { bestSSE = sse.y; bestIdx = c1i; bestL = X1.y - X2.y; bestB = X2.y; }
+      if (j == 0 && (upd0 || upd1)) {
+        const float* yl = ylast + half * HALF_HB;
+#pragma unroll
+        for (int i = 0; i < K && i < HALF_HB; ++i)
+          if (i < hmax) mybest[i] = yl[i] - (upd1 ? D[i].y : D[i].x);
+      }
+      if (PRUNE && j == 0 && (upd0 || upd1))
+        __hip_atomic_fetch_min(ubound + half, __float_as_uint(bestSSE), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    int q = 0;
+    if (lane == 0)
+      q = __hip_atomic_fetch_add(ubound + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    k = nwaves + __builtin_amdgcn_readfirstlane(q);
+  }
+
+  // ---- arg-min across the 4 waves; wave r finishes series n0 + r ----------------------
+  if (j == 0) {
+    float* wb = wbest + (w * 2 + half) * 4;
+    wb[0] = bestSSE;
+    wb[1] = __int_as_float(bestIdx);
+    wb[2] = bestL;
+    wb[3] = bestB;
+  }
+  __syncthreads();
+  if (w >= 2) return;
+  const int r = w, n = n0 + r;
+  if (n >= a.N) return;
+  int win = 0;
+  for (int q = 1; q < nwaves; ++q) {
+    const float sq = wbest[(q * 2 + r) * 4], sw = wbest[(win * 2 + r) * 4];
+    const int iq = __float_as_int(wbest[(q * 2 + r) * 4 + 1]), iw = __float_as_int(wbest[(win * 2 + r) * 4 + 1]);
+    if (sq < sw || (sq == sw && iq < iw)) win = q;
+  }
+  const float* wb = wbest + (win * 2 + r) * 4;
+  const float gSSE = wb[0], gL = wb[2], gB = wb[3];
+  const int gIdx = __float_as_int(wb[1]);
+  const float* sb = bests + (win * 2 + r) * HALF_HB;
+  const float nvr = nvc[r];
+  const float sig = sqrtf(gSSE / fmaxf(nvr, 1.f));
+  if (lane == 0) {
+    a.level[n] = gL;
+    a.trend[n] = gB;
+    a.sigma[n] = sig;
+    a.best[n] = gIdx;
+  }
+  const int Tp = a.Tp;
+  if (a.season_hb && lane < hmax) a.season_hb[(long long)n * HALF_HB + lane] = sb[lane];
+  if (a.nvalid_out && lane == 0) a.nvalid_out[n] = nvr;
+  detect_epilogue_wave(a.det, n, sig, nvr, [&](int h) {
+    int ph = (Tp - 1 + h) % m;
+    if (ph < 0) ph += m;
+    ph = ph < HALF_HB ? ph : HALF_HB - 1;
+    return gL + (float)h * gB + sb[ph];
+  }, gIdx);
+}
+
+// Persistent over the pairs hw_d_kernel deferred (count in deferred[0]); self-cleaning like
+// hw_half_general_kernel: workspace int32 [3 + ceil(N / 2)] = {count, pairs..., done, total};
+// the last workgroup out adds the count to `total` (deferred pairs since allocation, for the
+// records) and resets count and done.
+template <int K, bool PRUNE>
+__global__ __launch_bounds__(256, 2) void hw_dg_kernel(const SmoothArgs a, int hmax, int* deferred, int hints) {
+  const int cnt = min(deferred[0], (a.N + 1) / 2);
+  if (cnt == 0) return;  // gap-free shard: count and done are already 0
+  for (int q = blockIdx.x; q < cnt; q += gridDim.x) {
+    hw_dg_block<K, PRUNE>(a, hmax, deferred[1 + q], hints);
+    __syncthreads();  // LDS is reused by the next pair
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int* done = deferred + 1 + (a.N + 1) / 2;
+    if (atomicAdd(done, 1) == (int)gridDim.x - 1) {
+      done[1] += cnt;
+      *done = 0;
+      deferred[0] = 0;
+    }
+  }
+}
+
+extern "C" size_t fm_hw_dg_lds_bytes(int Tp, int seg, int K);
+
+// A/B instrument (FOREMAST_HW_DG_ALL=1): every pair is listed for the gapped kernel, so its
+// cost on gap-free seasons can be timed against hw_d_kernel's on the same data
+__global__ void hw_dg_list_all_kernel(int* deferred, int pairs) {
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < pairs; q += gridDim.x * blockDim.x) deferred[1 + q] = 2 * q;
+  if (blockIdx.x == 0 && threadIdx.x == 0) deferred[0] = pairs;
+}
+
 extern "C" size_t fm_hw_d_lds_bytes(int Tp, int seg, int K) {
   if (K != 45 || seg <= 0) return (size_t)-1;
   const int nseg = Tp / seg;
@@ -1446,6 +1946,15 @@ extern "C" size_t fm_hw_d_lds_bytes(int Tp, int seg, int K) {
   const int NMW = (32 * K + 31) / 32;
   return ((size_t)2 * (nseg - 1) * DLay<45>::SEASON + 2 * NMW + 8 * D_WAVES + 4 + 2 * HALF_HB + 4 * 2 * HALF_HB + 4 * 2 * 4 +
           4) * 4;
+}
+
+// hw_dg_block: the hw_d_block layout + per-(series, season, lane) 64-bit miss masks, per
+// (series, season) gap flags and the two valid-point counts
+extern "C" size_t fm_hw_dg_lds_bytes(int Tp, int seg, int K) {
+  const size_t base = fm_hw_d_lds_bytes(Tp, seg, K);
+  if (base == (size_t)-1) return base;
+  const int ns1 = Tp / seg - 1;
+  return base + ((size_t)2 * ns1 * 64 + 2 * ns1 + 2) * 4;
 }
 
 // Deferred detection for HW variants 4/5: band, verdict, per-app counters and the K9
@@ -1548,7 +2057,8 @@ extern "C" int fm_hw_d_fit_split(const SmoothArgs* a, int hmax, int* deferred, i
   if (a->N <= 0) return 0;
   const size_t lds = fm_hw_d_lds_bytes(a->Tp, a->seg, K);
   const size_t glds = fm_hw_half_lds_bytes(a->Tp, a->seg, K);
-  if (lds > 80 * 1024 || glds > 64 * 1024) return (int)hipErrorNotSupported;
+  if (lds > 80 * 1024 || glds > 64 * 1024 || fm_hw_dg_lds_bytes(a->Tp, a->seg, K) > 80 * 1024)
+    return (int)hipErrorNotSupported;
   if (!deferred) return (int)hipErrorInvalidValue;
   const int pairs = (a->N + 1) / 2;
   const int S = (split_ws && max_split > 0 && a->G >= 2) ? fm_hw_d_split_plan(pairs, slots, max_split) : 0;
@@ -1561,7 +2071,10 @@ extern "C" int fm_hw_d_fit_split(const SmoothArgs* a, int hmax, int* deferred, i
   const bool prune = !(pe && pe[0] == '0');
   const char* he = getenv("FOREMAST_HW_HINTS");  // previous winners first (=0: grid order)
   const int hints = (prune && !(he && he[0] == '0')) ? 1 : 0;
-  if (prune)
+  const char* da = getenv("FOREMAST_HW_DG_ALL");
+  if (da && da[0] == '1')
+    hipLaunchKernelGGL(hw_dg_list_all_kernel, dim3((pairs + 255) / 256), dim3(256), 0, st, deferred, pairs);
+  else if (prune)
     hipLaunchKernelGGL((hw_d_kernel<45, true>), dim3(pairs - S + 2 * S), dim3(256), lds, st, *a, hmax, deferred,
                        pairs - S, cnt, cand, hints);
   else
@@ -1569,8 +2082,20 @@ extern "C" int fm_hw_d_fit_split(const SmoothArgs* a, int hmax, int* deferred, i
                        pairs - S, cnt, cand, hints);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL((hw_half_general_kernel<45>), dim3(pairs < 512 ? pairs : 512), dim3(256), glds, st, *a, hmax,
-                     deferred);
+  // gapped pairs: the variant-5 walk with masked seasons (FOREMAST_HW_GAPS=v4: the variant-4
+  // general kernel instead, for A/B runs)
+  const char* ge = getenv("FOREMAST_HW_GAPS");
+  if (ge && ge[0] == 'v') {
+    hipLaunchKernelGGL((hw_half_general_kernel<45>), dim3(pairs < 512 ? pairs : 512), dim3(256), glds, st, *a, hmax,
+                       deferred);
+    return (int)hipGetLastError();
+  }
+  const size_t dlds = fm_hw_dg_lds_bytes(a->Tp, a->seg, K);
+  const int grid = pairs < 512 ? pairs : 512;
+  if (prune)
+    hipLaunchKernelGGL((hw_dg_kernel<45, true>), dim3(grid), dim3(256), dlds, st, *a, hmax, deferred, hints);
+  else
+    hipLaunchKernelGGL((hw_dg_kernel<45, false>), dim3(grid), dim3(256), dlds, st, *a, hmax, deferred, hints);
   return (int)hipGetLastError();
 }
 

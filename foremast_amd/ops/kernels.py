@@ -307,7 +307,23 @@ def pair_table(grid: torch.Tensor, K: int) -> torch.Tensor:
                 for q, v in enumerate((Bp[0, 0], Bp[0, 1], Bp[1, 0], Bp[1, 1])):
                     tab[p, base + 2 * q + comp] = v
                 Bp = Bp @ Bp
-    t = torch.tensor(tab, dtype=torch.float32, device=grid.device).contiguous()
+    # then A^0 .. A^K per pair ([npairs][K + 1][8], Mat2 of v2f: m11, m12, m21, m22 with the
+    # two combos interleaved): the gapped-series kernel (hw_dg_kernel) assembles a lane's
+    # season map from them run by run
+    pw = np.zeros((npairs, K + 1, 8), dtype=np.float64)
+    for p in range(npairs):
+        for comp, ci in enumerate((2 * p, 2 * p + 1 if 2 * p + 1 < G else 2 * p)):
+            al, be, ga = g[ci]
+            c2 = al * be
+            c1 = al + c2
+            A = np.array([[1 - c1, 1.0], [-c2, 1.0]])
+            Ap = np.eye(2)
+            for n in range(K + 1):
+                for q, v in enumerate((Ap[0, 0], Ap[0, 1], Ap[1, 0], Ap[1, 1])):
+                    pw[p, n, 2 * q + comp] = v
+                Ap = A @ Ap
+    t = torch.tensor(np.concatenate([tab.reshape(-1), pw.reshape(-1)]), dtype=torch.float32,
+                     device=grid.device).contiguous()
     if len(_PAIR_TAB_CACHE) > 64:
         _PAIR_TAB_CACHE.clear()
     _PAIR_TAB_CACHE[key] = t
@@ -430,9 +446,21 @@ def _half_workspace(dev, N: int) -> torch.Tensor:
     key = (dev.index, N, nat.stream_handle(dev))
     ws = _HALF_WS.get(key)
     if ws is None:
-        ws = torch.zeros(2 + (N + 1) // 2, dtype=torch.int32, device=dev)  # {count, pairs..., done}
+        # {count, pairs..., done, total}: total = pairs deferred to the gapped-series kernel
+        # since allocation (hw_dg_kernel adds each launch's count)
+        ws = torch.zeros(3 + (N + 1) // 2, dtype=torch.int32, device=dev)
         _HALF_WS[key] = ws
     return ws
+
+
+def hw_deferred_total(dev=None) -> int:
+    """Series pairs the variant-5 fit has handed to the gapped-series kernel since the
+    workspaces were allocated, over every workspace of ``dev`` (one device sync)."""
+    tot = 0
+    for (di, _n, _s), ws in _HALF_WS.items():
+        if dev is None or di == torch.device(dev).index:
+            tot += int(ws[-1].item())
+    return tot
 
 
 SPLIT_MAX = 4096       # HW variant 5 split tail: at most this many series pairs split in two halves

@@ -18,6 +18,7 @@ case $TARGET in
   es)   CMD=("$PWD/scripts/bench_kernels.py" --series 20000 --rounds 1 --only es --variants=) ;;
   lstm) CMD=("$PWD/scripts/bench_lstm_kernels.py") ;;
   rank) CMD=("$PWD/scripts/bench_rank.py") ;;
+  gaps) CMD=("$PWD/scripts/bench_hw_gaps.py" --series 20000 --rounds 1 --cases ${CASES:-dense,dgall,miss1e-3}) ;;
 esac
 SETS=("SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS"
       "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU"
