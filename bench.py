@@ -696,7 +696,9 @@ def setup_lstm(args, world, rank, dev, n_features, fp8):
                    "one univariate metric-series"),
         "train_score_overlap": not args.lstm_no_overlap,
     }
-    dt = "bf16"  # training fp32 master / bf16 MFMA scoring (fp8 weights+activations for config 5)
+    # compute dtype of the scoring (the metric's work): fp8 e4m3 block-scaled MFMA for config 5,
+    # bf16 MFMA otherwise (training: fp32 master weights either way)
+    dt = "fp8_e4m3" if fp8 else "bf16"
     meta["_agg"] = agg
     meta["_truth"] = (truth_apps, n_apps)
     meta["_shard"], meta["_bad"], meta["_ticks"], meta["_params"] = shard, bad_local, host_ticks, params

@@ -968,4 +968,5 @@ def setup_node_lstm(args, world, rank, dev):
         "_breakdowns": breakdowns,
         "_arrival_finish": finish,
     }
-    return tick, torch.zeros((1, 2), dtype=torch.int32), meta, "bf16" if dev.type == "cuda" else "fp32", n_jobs * F
+    dt = ("fp8_e4m3" if lstm.shard.fp8 else "bf16") if dev.type == "cuda" else "fp32"
+    return tick, torch.zeros((1, 2), dtype=torch.int32), meta, dt, n_jobs * F

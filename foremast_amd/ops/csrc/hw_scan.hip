@@ -1144,6 +1144,16 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
   // [0..1] per-series SSE bound, [2] pair queue, [3] hint pairs (lo16 | hi16, 0xffff = none)
   unsigned* ubound = (unsigned*)(wbest + 4 * 2 * 4);
 
+  // a pair the gapped kernel took in the last fit (its gap is almost always still in the
+  // window: the ring moved a few columns) goes straight back to it, without staging here
+  int* gflags = deferred + 4 + (a.N + 1) / 2;
+  if (__builtin_amdgcn_readfirstlane(gflags[n0 >> 1])) {
+    if (tid == 0 && hid == 0) {
+      const int q = atomicAdd(deferred, 1);
+      if (q < (a.N + 1) / 2) deferred[1 + q] = n0;
+    }
+    return;
+  }
   for (int i = tid; i < 2 * NMW + 8 * D_WAVES + 4; i += blockDim.x) vmask[i] = 0u;  // vmask, stat, flag
   if (tid < 3) ubound[tid] = tid < 2 ? 0x7f800000u : 0u;  // +inf, +inf, queue 0
   if (tid == 3) {
@@ -1271,10 +1281,11 @@ __device__ __forceinline__ void hw_d_block(const SmoothArgs& a, int hmax, int n0
     if (bad) atomicOr(flag, 1);
   }
   __syncthreads();
-  if (*flag) {  // block-uniform: a gap past season 0 — the general kernel takes the pair
+  if (*flag) {  // block-uniform: a gap past season 0 — the gapped kernel takes the pair
     if (tid == 0 && hid == 0) {
       const int q = atomicAdd(deferred, 1);
       if (q < (a.N + 1) / 2) deferred[1 + q] = n0;  // a stale count can never write past the pair list
+      gflags[n0 >> 1] = 1;
     }
     return;
   }
@@ -1579,7 +1590,7 @@ __device__ __forceinline__ void dg_season(bool m2, bool r1, const float* blk, v2
 }
 
 template <int K, bool PRUNE>
-__device__ __forceinline__ void hw_dg_block(const SmoothArgs& a, int hmax, int n0, int hints) {
+__device__ __forceinline__ void hw_dg_block(const SmoothArgs& a, int hmax, int n0, int hints, int* gflags) {
   constexpr int SEA = DLay<K>::SEASON;
   constexpr int TS = PairTab<K>::SIZE;
   constexpr int NMW = (32 * K + 31) / 32;
@@ -1677,6 +1688,7 @@ __device__ __forceinline__ void hw_dg_block(const SmoothArgs& a, int hmax, int n
           int i = ib + (o - ob), jj = jjb;
           if (i >= K) { i -= K; ++jj; }
           const bool v0 = y[0][u] == y[0][u];
+          const bool v1 = y[1][u] == y[1][u];
           // seasons >= 1: a missing y is flagged and imputed as 0 (y*), see above
 #pragma unroll
           for (int k = 1; k < D_MAXSEG; ++k) {
@@ -1707,7 +1719,6 @@ __device__ __forceinline__ void hw_dg_block(const SmoothArgs& a, int hmax, int n
             ylast[r * HALF_HB + o] = yl;
           }
           // season-1 mean: observed points only (the imputed 0s are not data)
-          const bool v1 = !((mbits[((r * ns1) * 32 + jj) * 2 + (i >> 5)] >> (i & 31)) & 1u);
           const float y0v = v0 ? y[0][u] : 0.f, y0c = v0 ? 1.f : 0.f;
           const float y1v = v1 ? y[1][u] : 0.f, y1c = v1 ? 1.f : 0.f;
           if (r == 0) { s0 += y0v; c0 += y0c; s1 += y1v; c1 += y1c; }
@@ -1752,6 +1763,7 @@ __device__ __forceinline__ void hw_dg_block(const SmoothArgs& a, int hmax, int n
   int segbits = 0;
   for (int k = 0; k < ns1; ++k) segbits |= (segm[k] | segm[ns1 + k]) ? (2 << k) : 0;
   segbits = __builtin_amdgcn_readfirstlane(segbits);
+  if (segbits == 0 && tid == 0) gflags[n0 >> 1] = 0;  // gap-free now: hw_d_kernel stages it next time
   __syncthreads();
 
   const float l0 = half ? l0r[1] : l0r[0], b0 = half ? b0r[1] : b0r[0];
@@ -1908,22 +1920,31 @@ __device__ __forceinline__ void hw_dg_block(const SmoothArgs& a, int hmax, int n
 }
 
 // Persistent over the pairs hw_d_kernel deferred (count in deferred[0]); self-cleaning like
-// hw_half_general_kernel: workspace int32 [3 + ceil(N / 2)] = {count, pairs..., done, total};
-// the last workgroup out adds the count to `total` (deferred pairs since allocation, for the
-// records) and resets count and done.
+// hw_half_general_kernel: workspace int32 [4 + 2 ceil(N / 2)] = {count, pairs..., done, total,
+// queue, per-pair gap flags...}; the last workgroup out adds the count to `total` (deferred
+// pairs since allocation, for the records) and resets count, done and the queue.  A pair's
+// flag is set by hw_d_kernel when it defers the pair and cleared here when the pair is found
+// gap-free; hw_d_kernel hands flagged pairs over without staging them.
 template <int K, bool PRUNE>
 __global__ __launch_bounds__(256, 2) void hw_dg_kernel(const SmoothArgs a, int hmax, int* deferred, int hints) {
   const int cnt = min(deferred[0], (a.N + 1) / 2);
   if (cnt == 0) return;  // gap-free shard: count and done are already 0
-  for (int q = blockIdx.x; q < cnt; q += gridDim.x) {
-    hw_dg_block<K, PRUNE>(a, hmax, deferred[1 + q], hints);
+  int* done = deferred + 1 + (a.N + 1) / 2;  // {done, total, queue}
+  __shared__ int next;
+  // pairs from a queue, not a static stride: their cost varies (gapped seasons, pruning)
+  for (;;) {
+    if (threadIdx.x == 0) next = atomicAdd(done + 2, 1);
+    __syncthreads();
+    const int q = next;
+    __syncthreads();  // every thread has read `next` before thread 0 overwrites it
+    if (q >= cnt) break;
+    hw_dg_block<K, PRUNE>(a, hmax, deferred[1 + q], hints, done + 3);
     __syncthreads();  // LDS is reused by the next pair
   }
-  __syncthreads();
   if (threadIdx.x == 0) {
-    int* done = deferred + 1 + (a.N + 1) / 2;
-    if (atomicAdd(done, 1) == (int)gridDim.x - 1) {
+    if (atomicAdd(done, 1) == (int)gridDim.x - 1) {  // the last workgroup out resets the workspace
       done[1] += cnt;
+      done[2] = 0;
       *done = 0;
       deferred[0] = 0;
     }
@@ -2091,7 +2112,9 @@ extern "C" int fm_hw_d_fit_split(const SmoothArgs* a, int hmax, int* deferred, i
     return (int)hipGetLastError();
   }
   const size_t dlds = fm_hw_dg_lds_bytes(a->Tp, a->seg, K);
-  const int grid = pairs < 512 ? pairs : 512;
+  int grid = pairs < 512 ? pairs : 512;
+  const char* gg = getenv("FOREMAST_HW_DG_GRID");  // A/B: workgroups of the gapped kernel
+  if (gg && atoi(gg) > 0) grid = atoi(gg) < pairs ? atoi(gg) : pairs;
   if (prune)
     hipLaunchKernelGGL((hw_dg_kernel<45, true>), dim3(grid), dim3(256), dlds, st, *a, hmax, deferred, hints);
   else

@@ -446,9 +446,11 @@ def _half_workspace(dev, N: int) -> torch.Tensor:
     key = (dev.index, N, nat.stream_handle(dev))
     ws = _HALF_WS.get(key)
     if ws is None:
-        # {count, pairs..., done, total}: total = pairs deferred to the gapped-series kernel
-        # since allocation (hw_dg_kernel adds each launch's count)
-        ws = torch.zeros(3 + (N + 1) // 2, dtype=torch.int32, device=dev)
+        # {count, pairs..., done, total, queue, gap flags...}: total = pairs deferred to the
+        # gapped-series kernel since allocation (hw_dg_kernel adds each launch's count); queue =
+        # its pair queue; a pair's gap flag sends it straight to that kernel in the next fit
+        P = (N + 1) // 2
+        ws = torch.zeros(4 + 2 * P, dtype=torch.int32, device=dev)
         _HALF_WS[key] = ws
     return ws
 
@@ -459,8 +461,16 @@ def hw_deferred_total(dev=None) -> int:
     tot = 0
     for (di, _n, _s), ws in _HALF_WS.items():
         if dev is None or di == torch.device(dev).index:
-            tot += int(ws[-1].item())
+            tot += int(ws[(ws.numel() - 4) // 2 + 2].item())
     return tot
+
+
+def hw_clear_gap_flags() -> None:
+    """Forget which series pairs the last fits found gapped (each is re-staged by the dense
+    kernel and re-classified); tests that reuse a shard size with new data call this."""
+    for ws in _HALF_WS.values():
+        P = (ws.numel() - 4) // 2
+        ws[P + 4:].zero_()
 
 
 SPLIT_MAX = 4096       # HW variant 5 split tail: at most this many series pairs split in two halves

@@ -313,6 +313,64 @@ def pack(model, fp8: bool = False, device="cuda") -> LstmPacked:
                       b_out=model.out_b.detach().float().contiguous().to(device))
 
 
+def fp8_emulated_forward(model, x: torch.Tensor):
+    """The fp8 scoring kernel's arithmetic in PyTorch (fp32 everywhere else): what the
+    block-scaled ``v_mfma_scale_f32_32x32x64_f8f6f4`` path quantises, it quantises the
+    same way, so a comparison against it measures only accumulation order and the
+    hardware transcendentals.
+
+    * weights: e4m3 codes of ``w * 2^-e`` with one E8M0 exponent per (gate row, 32-k
+      block), :func:`~foremast_amd.ops.pack.e8m0_blocks`: ``W_hh`` blocks are hidden
+      units 0..31 and 32..63; the input k-step's block 0 is ``(W_ih[row, :F], 0.., b[row]
+      at byte 7)`` (decoder: the bias alone);
+    * the hidden state enters as ``e4m3(h * 2^8) * 2^-8``, the inputs as
+      ``e4m3(clamp(x, +-448))``, the bias input as 1;
+    * gates, cell, read-out (unquantised h, fp32 ``W_out``) and the error against the
+      unquantised x in fp32.
+    Returns ``(y [N, T, F], err [N])``."""
+    from .pack import e8m0_blocks
+    F = model.F
+    e4 = torch.float8_e4m3fn
+
+    def deq(blocks: torch.Tensor) -> torch.Tensor:
+        q, sc = e8m0_blocks(blocks)
+        return q.view(e4).float() * torch.ldexp(torch.ones_like(sc, dtype=torch.float32),
+                                                 (sc.int() - 127))[:, None]
+
+    def hh_hat(w):  # [4H, H] -> per (row, 32-unit block)
+        return deq(w.detach().float().cpu().reshape(4 * H * 2, 32)).reshape(4 * H, H)
+
+    def in_block(w_ih, b):  # [4H, 32]: inputs at 0..F-1, bias at 7
+        blk = torch.zeros(4 * H, 32)
+        if w_ih is not None:
+            blk[:, :F] = w_ih.detach().float().cpu()
+        blk[:, 7] = b.detach().float().cpu()
+        d = deq(blk)
+        return (d[:, :F] if w_ih is not None else None), d[:, 7]
+
+    we_hh, wd_hh = hh_hat(model.enc_w_hh), hh_hat(model.dec_w_hh)
+    we_ih, be = in_block(model.enc_w_ih, model.enc_b)
+    _, bd = in_block(None, model.dec_b)
+    x = x.detach().float().cpu()
+    N, T, _ = x.shape
+    xq = x.clamp(-448.0, 448.0).to(e4).float()
+
+    def hq(h):
+        return (h * 256.0).to(e4).float() / 256.0
+
+    cell = type(model)._cell
+    h = torch.zeros(N, H)
+    c = torch.zeros(N, H)
+    for t in range(T):
+        h, c = cell(hq(h) @ we_hh.t() + xq[:, t] @ we_ih.t() + be, c)
+    ys = []
+    for t in range(T):
+        h, c = cell(hq(h) @ wd_hh.t() + bd, c)
+        ys.append(h)
+    y = torch.stack(ys, 1) @ model.out_w.detach().float().cpu().t() + model.out_b.detach().float().cpu()
+    return y, ((y - x) ** 2).mean(dim=(1, 2))
+
+
 def lstm_score(p: LstmPacked, x: Optional[torch.Tensor], mu: float = 0.0, sigma: float = 1.0,
                threshold: Optional[torch.Tensor] = None, thr_default: float = 3.0, want_recon: bool = False,
                app_id: Optional[torch.Tensor] = None, app_stats: Optional[torch.Tensor] = None,

@@ -65,12 +65,20 @@ def test_gapped_pairs_match_reference(K, case):
     spec = K.DetectSpec(horizons=hz.to(dev), threshold=torch.full((N,), 2.0, device=dev),
                         bound=torch.full((N,), 3, dtype=torch.int8, device=dev),
                         min_lower=torch.full((N,), -1e30, device=dev), cur=cur, max_horizon=10)
+    K.hw_clear_gap_flags()  # earlier cases of this size flagged other pairs
     before = K.hw_deferred_total(dev)
     out = K.smoothing_fit(ring, head, T, sm_ref.MODE_HW, M, GRID.to(dev), spec, variant=5, defer_detect=False)
     torch.cuda.synchronize()
     assert K.last_hw_variant == 5
     gapped_pairs = int(np.isnan(yl[:, M:]).reshape(N // 2, -1).any(1).sum())
     assert K.hw_deferred_total(dev) - before == gapped_pairs > 0
+    # the next fit of the same data: the flagged pairs skip the dense kernel's staging and the
+    # gapped kernel gives the same result bit for bit
+    again = {k: v.clone() for k, v in K.smoothing_fit(ring, head, T, sm_ref.MODE_HW, M, GRID.to(dev), spec,
+                                                      variant=5).items()}
+    torch.cuda.synchronize()
+    for key in ("best", "level", "trend", "sigma", "verdict", "forecast"):
+        assert torch.equal(again[key], out[key]), key
     ref = sm_ref.fit_smoothing(torch.tensor(yl, dtype=torch.float64), sm_ref.MODE_HW, GRID.double(), m=M)
     kb = out["best"].cpu().long()
     same = (kb == ref.best).numpy()

@@ -142,6 +142,42 @@ def test_fused_lstm_kernel_matches_reference(fp8):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("F", [2, 3])
+def test_fp8_kernel_matches_emulated_fp8_reference(F):
+    """The fp8 kernel against a PyTorch reference that applies the SAME e4m3 rounding
+    (per-(row, 32-k) E8M0 weight scales, h entering as e4m3(h * 2^8) * 2^-8, saturated
+    e4m3 inputs; ops/lstm.py fp8_emulated_forward): what is left is accumulation order and
+    the hardware exp / rcp, so the reconstruction error agrees to rtol 1e-2 on every
+    window -- a wrong scale map or a bias would not pass."""
+    torch.manual_seed(11 + F)
+    dev = torch.device("cuda:0")
+    N, T = 512, 24
+    m = lstm_ae.LSTMAutoencoder(F, 64)
+    with torch.no_grad():  # a trained-like spread of weights: some blocks far from the others
+        m.enc_w_hh[:, :32] *= 3.0
+        m.dec_w_hh[64:128] *= 0.05
+        m.enc_b[::5] *= 6.0
+        m.out_w *= 8.0       # a read-out that carries the hidden state into y
+    x = torch.randn(N, T, F)
+    x[:40, 10:14] += 4.0
+    ref_y, ref_err = L.fp8_emulated_forward(m, x)
+    p = L.pack(m, fp8=True, device=dev)
+    out = L.lstm_score(p, x.to(dev).contiguous(), mu=float(ref_err.mean()), sigma=float(ref_err.std()),
+                       want_recon=True)
+    torch.cuda.synchronize()
+    err, y = out["err"].cpu(), out["recon"].cpu()
+    np.testing.assert_allclose(err.numpy(), ref_err.numpy(), rtol=1e-2, atol=1e-5)
+    # the reconstruction is the sensitive output (the error is dominated by x): kernel vs
+    # emulated fp8 must be far closer than emulated fp8 vs the unquantised model
+    d_kernel = (y - ref_y).abs()
+    with torch.no_grad():
+        d_quant = (m(x) - ref_y).abs()
+    assert float(d_quant.mean()) > 1e-3                       # the test can tell fp8 from fp32
+    assert float(d_kernel.mean()) < 0.1 * float(d_quant.mean()), (float(d_kernel.mean()), float(d_quant.mean()))
+    assert float(np.percentile(d_kernel.numpy(), 99.9)) < 0.25 * float(np.percentile(d_quant.numpy(), 99.9))
+
+
+@pytest.mark.gpu
 def test_fp8_scoring_saturates_out_of_range_inputs():
     """A regressed window's z-scored inputs can exceed the fp8 e4m3 range
     (|x| > 448): the kernel saturates them, so the error stays
