@@ -516,14 +516,28 @@ def setup_canary(args, world, rank, dev):
         shard.ingest_tick(nv, nb)
         released(k, b)
 
+    def graph_tail():
+        """Captured at the end of the tick graph: the fused health all-gather (RCCL, when
+        collectives run) and the copy of the node health table to pinned host memory."""
+        if agg.fused:
+            agg._gather_fused(shard.app_stats, shard.out["verdict"])
+        health_hosts[0].copy_(agg.recv if agg.fused else shard.app_stats, non_blocking=pin)
+
     def tick(k):
         nv, nb, b = load_tick(W + k)
         if args.graph:
-            out = shard.tick_graph(nv, nb)  # ingest + score as one HIP-graph replay
+            # ingest + score (+ the health collective and the table's copy back) as one replay
+            out = shard.tick_graph(nv, nb, post=graph_tail if (pin and not pipelined) else None)
         else:
             shard.ingest_tick(nv, nb)
             released(W + k, b)
             out = shard.score()
+        REFIT_FLAGS[k] = shard.last_refit
+        if out.get("post_in_graph"):
+            GRAPH_TAIL[0] = True
+            if dev.type == "cuda":
+                torch.cuda.current_stream().synchronize()
+            return out
         stats, _ = agg.tick(shard.app_stats, out["verdict"])
         hh = health_hosts[k % 2 if pipelined else 0]
         if zero_copy:
@@ -531,7 +545,6 @@ def setup_canary(args, world, rank, dev):
             K.copy_to_host(hh.view(-1), (agg.recv if agg.fused else stats).view(-1))
         else:
             hh.copy_(agg.recv if agg.fused else stats, non_blocking=pin)
-        REFIT_FLAGS[k] = shard.last_refit
         if pipelined:
             ev = torch.cuda.Event()
             ev.record()
@@ -591,6 +604,7 @@ class InFlight(NamedTuple):
     host: torch.Tensor
 LAT_START = {}  # timed tick -> perf_counter time its data arrived (set by the prom ingest path)
 REFIT_FLAGS = {}  # tick -> whether it refit the model (canary --refit-every)
+GRAPH_TAIL = [False]  # canary: the health collective + copy back ran inside the tick graph
 
 
 def prom_bodies(host_ticks, s, P, ring, threads, pin):
@@ -953,6 +967,10 @@ def main():
         meta["hip_graph"] = bool(graph_used())
     if deferred is not None:
         meta["gapped_pairs_per_tick"] = deferred(args.warmup + args.steps)
+    if args.config in ("canary", "hw10k") or getattr(args, "config_name", "") == "hw10k":
+        meta["health_tail_in_graph"] = GRAPH_TAIL[0]
+        if GRAPH_TAIL[0] and meta.get("health_collectives", "none") != "none":
+            meta["health_collectives"] += " (captured in the tick graph)"
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     lat_t = torch.tensor(lat, dtype=torch.float64, device=dev)
     if world > 1:

@@ -257,7 +257,8 @@ class StreamingShard:
                 and self.cur.ticks >= self.cur.W and self.anomalies is None
                 and getattr(self, "_hw_variant", None) in (4, 5) and bool(self.out))
 
-    def tick_graph(self, newv: torch.Tensor, newb: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+    def tick_graph(self, newv: torch.Tensor, newb: Optional[torch.Tensor] = None,
+                   post=None) -> Dict[str, torch.Tensor]:
         """``ingest_tick`` + ``score`` as ONE HIP-graph replay with no host-to-device copy.
 
         The graph (captured on the first steady-state call) holds a tick-advance
@@ -270,10 +271,16 @@ class StreamingShard:
         written from the host once, when the graph path (re)starts after eager
         ticks.  Falls back to the eager calls until :meth:`graph_ready`.
         ``newv`` / ``newb`` must be the same buffers on every call (their
-        addresses are baked into the graph)."""
+        addresses are baked into the graph).  ``post`` (optional, called once, inside the
+        capture): the tick's own tail -- the node health collective and the copy of the
+        health table to pinned host memory -- so one replay is the whole GPU side of the
+        tick; on the eager ticks before capture the caller runs its tail itself (the
+        return value's ``"post_in_graph"`` says which happened)."""
         if not self.graph_ready():
             self.ingest_tick(newv, newb)
-            return self.score()
+            out = self.score()
+            out["post_in_graph"] = False
+            return out
         from ..ops import kernels as K
         io = (newv.data_ptr(), None if newb is None else newb.data_ptr())
         if self._graph is not None and io != self._graph_io:
@@ -297,17 +304,31 @@ class StreamingShard:
         self._new_pts += 1
         self.horizons = self._h_buf
         if self._graph is None:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                K.tick_advance(self._state_dev, R, W, self._h_dev, self._h_buf)
-                K.tick_ingest(self.hist.data, 0, self.cur.data, self.cur.P, self.cur.W, 0, newv,
-                              base=self.base if newb is not None else None, newb=newb, state=self._state_dev,
-                              zero=self.app_stats.view(-1))
-                self._score_gpu(head_dev=self._state_dev[3:4])
+            def capture(with_post: bool):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    K.tick_advance(self._state_dev, R, W, self._h_dev, self._h_buf)
+                    K.tick_ingest(self.hist.data, 0, self.cur.data, self.cur.P, self.cur.W, 0, newv,
+                                  base=self.base if newb is not None else None, newb=newb, state=self._state_dev,
+                                  zero=self.app_stats.view(-1))
+                    self._score_gpu(head_dev=self._state_dev[3:4])
+                    if with_post:
+                        post()
+                return g
+            g, self._post_in_graph = None, False
+            if post is not None:
+                try:
+                    g, self._post_in_graph = capture(True), True
+                except RuntimeError:  # e.g. a collective backend that cannot be captured
+                    torch.cuda.synchronize()
+                    g = None
+            if g is None:
+                g = capture(False)
             self._graph, self._graph_io = g, io
         self._graph.replay()
         self._stats_zeroed = False
         self.last_refit = True
+        self.out["post_in_graph"] = self._post_in_graph
         return self.out
 
     # ------------------------------------------------------------------ scoring
