@@ -413,8 +413,9 @@ def setup_canary(args, world, rank, dev):
             return [base_host[int(q[1])].reshape(1, -1).numpy() for q in reqs]
 
         def exch(k):
+            # device values: the all-to-all's output is the owner's baseline block (no host copy)
             (vals,) = loop.run_until_complete(router.exchange([(family, float(k), n_local * P, shard_pod)], serve))
-            return torch.from_numpy(vals).view(n_local, P)
+            return vals.view(n_local, P)
         ticks = cur_t
         base_host = base_t.cpu()
         if dev.type == "cuda":
@@ -498,7 +499,7 @@ def setup_canary(args, world, rank, dev):
             return
         newvb.copy_(host_ticks[k], non_blocking=pin)
         if exch is not None:
-            newb.copy_(exch(k), non_blocking=pin)  # RC5: baseline windows to their owners
+            newb.copy_(exch(k), non_blocking=True)  # RC5: baseline windows to their owners (D2D)
     # host copy of the node health table (fused: the whole gathered record buffer)
     health_src = agg.recv if agg.fused else shard.app_stats
     # two host copies of the node health table: tick k+1's D2H may be enqueued while the

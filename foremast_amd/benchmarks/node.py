@@ -177,6 +177,18 @@ def setup_node(args, world, rank, dev):
 
     if dev.type == "cpu" and args.series > 20000:
         args.series, args.ring = 500, 2880
+    # --multi-cluster (BASELINE config 4 through the product): cluster c is scraped by rank
+    # c mod world; a rank's jobs run their new pods in its own cluster, and every other app's
+    # baseline pods run in the next cluster, so those baseline windows are fetched and decoded
+    # by the rank serving that cluster and cross ranks in the rollout engine's lockstep
+    # exchange (parallel/affine.py) -- at one rank the same exchange runs through the
+    # collectives with FOREMAST_FORCE_COLLECTIVES=1 (the rank serves the other cluster itself)
+    multi = bool(getattr(args, "multi_cluster", False))
+    n_clusters = max(world, 2)
+
+    def cluster_ep(c: int) -> str:
+        return f"http://prom-{c}:9090/api/v1/"
+    home_ep = cluster_ep(rank) if multi else ENDPOINT
     M = len(METRICS)
     n_apps = args.series // M
     P = args.pods
@@ -188,8 +200,14 @@ def setup_node(args, world, rank, dev):
                          f"(jobs finish at endTime); raise --window or lower --steps")
     # this rank's apps: the node brain's ownership function (the shared store sees all jobs;
     # each rank keeps its share, so a rank-local store holds exactly what that rank claims)
-    mine = [a for a in range(n_apps) if owner_of(f"ns{a % 200}", f"app{a}", world) == rank]
+    owner = [owner_of(f"ns{a % 200}", f"app{a}", world) for a in range(n_apps)]
+    mine = [a for a in range(n_apps) if owner[a] == rank]
     na = len(mine)
+
+    def base_cluster(a: int) -> int:  # cluster of app a's baseline pods
+        return (owner[a] + (a & 1)) % n_clusters if multi else owner[a]
+    # apps whose baseline windows this rank's Prometheus serves
+    served = [a for a in range(n_apps) if base_cluster(a) % world == rank] if multi else mine
     t_setup = time.perf_counter()
     clock = {"t": T0}
     server = BodyServer()
@@ -221,7 +239,11 @@ def setup_node(args, world, rank, dev):
     roll = RolloutMonitor(store, cfg, prom=server, device=dev, worker_id=f"node-m{rank}-rollout", step=STEP,
                           window=W, pods=P, clock=lambda: clock["t"], ring_len=R, min_capacity=na * M,
                           decode_threads=args.decode_threads, apps_per_query=256)
-    keys = [(ENDPOINT, "namespace_app_per_pod:" + m, ns[i], app[i]) for i in range(na) for m in METRICS]
+    if multi:
+        from ..parallel.affine import ClusterRouter
+        roll.router = ClusterRouter(lambda ep, w: int(ep.split("prom-")[1].split(":")[0]) % max(w, 1), dev,
+                                    home=[home_ep])
+    keys = [(home_ep, "namespace_app_per_pod:" + m, ns[i], app[i]) for i in range(na) for m in METRICS]
     hist = roll.history
     hist.clock = lambda: clock["t"]
     # --cold: only the first cold_warm apps are resident; the week of every other (app, metric)
@@ -266,6 +288,14 @@ def setup_node(args, world, rank, dev):
     app_lab = [f'"namespace":"{ns[i]}","app":"{app[i]}"' for i in range(na)]
     newp_lab = [f'"namespace":"{ns[i]}","pod":"{pod}"' for i in range(na) for pod in new_pods[i]]
     model = synthetic_eval(params, R - 1 - W, W + 1 + ticks + 1, season, None).numpy()   # [na*M, T] no noise
+    # the baseline model of the served apps (rows of other ranks' apps too, under --multi-cluster)
+    sgid = torch.tensor([a * M + j for a in served for j in range(M)], dtype=torch.int64)
+    sparams = {k: v[sgid] for k, v in synthetic_params(args.series, torch.device("cpu"), seed=1234).items()}
+    smodel = synthetic_eval(sparams, R - 1 - W, W + 1, season, None).numpy().reshape(len(served), M, W + 1)
+    base_model = [smodel[:, j, :] for j in range(M)]
+    snoise = 0.03 * sparams["lvl"][:, 0].numpy().reshape(len(served), M)
+    base_noise = [dict(zip(served, snoise[:, j].tolist())) for j in range(M)]
+    del smodel, sparams
     t_axis = T0 + STEP * (np.arange(model.shape[1]) - W)                                   # time of each column
     col = {float(t): i for i, t in enumerate(t_axis.tolist())}
     bad_m = bad.reshape(na, M)
@@ -283,26 +313,34 @@ def setup_node(args, world, rank, dev):
             server.tick_bodies[("namespace_pod:" + m, ts)] = _body(
                 [f'{{"metric":{{"__name__":"namespace_pod:{m}",{lab}}},"values":[[{int(ts)},"{v}"]]}}'
                  for lab, v in zip(newp_lab, _fmt(pv.reshape(-1)))])
-        # baseline windows of the old pods: [T0 - W min, T0]
+        # baseline windows of the old pods: [T0 - W min, T0], for the apps whose baselines this
+        # rank's cluster serves; noise seeded per (app, metric): every layout serves the same data
         bt = t_axis[:W + 1]
-        base = model[rows, :W + 1][:, None, :] + rng.standard_normal((na, P, W + 1)) * noise[rows][:, None, None]
         frags = {}
-        for i in range(na):
-            for p, pod in enumerate(old_pods[i]):
-                frags[pod] = _series("namespace_pod:" + m, f'"namespace":"{ns[i]}","pod":"{pod}"', bt,
-                                     _fmt(base[i, p]))
+        for a, bm in zip(served, base_model[j]):
+            bg = np.random.default_rng(7_000_003 + a * M + j)
+            base = bm[None, :] + bg.standard_normal((P, W + 1)) * base_noise[j][a]
+            for p in range(P):
+                pod = f"app{a}-v1-{p}-5b6c7d8e9f"
+                frags[pod] = _series("namespace_pod:" + m, f'"namespace":"ns{a % 200}","pod":"{pod}"', bt,
+                                     _fmt(base[p]))
         server.fragments[("namespace_pod:" + m, float(bt[0]))] = frags
     del model
 
     # --- jobs: the barrelman request of a canary rollout per app, through the service ---------
-    mets = crd.Metrics(data_source_type="prometheus", endpoint=ENDPOINT,
+    mets = crd.Metrics(data_source_type="prometheus", endpoint=home_ep,
                        monitoring=[crd.Monitoring(metric_name=m, metric_alias=f"m{j}") for j, m in enumerate(METRICS)])
     reqs = []
     for i in range(na):
         info = queries.create_metrics_info(ns[i], app[i], [new_pods[i], old_pods[i]], mets, W, "canary", now=T0)
-        reqs.append(r.ApplicationHealthAnalyzeRequest(app_name=app[i], start_time=format_rfc3339(T0),
-                                                      end_time=format_rfc3339(T0 + W * STEP), metrics=info,
-                                                      strategy="canary").to_dict())
+        body = r.ApplicationHealthAnalyzeRequest(app_name=app[i], start_time=format_rfc3339(T0),
+                                                 end_time=format_rfc3339(T0 + W * STEP), metrics=info,
+                                                 strategy="canary").to_dict()
+        bc = base_cluster(mine[i])
+        if multi and bc != rank:  # this app's baseline pods run in another cluster
+            for q in body["metrics"]["baseline"].values():
+                q["parameters"]["endpoint"] = cluster_ep(bc)
+        reqs.append(body)
     setup_s = time.perf_counter() - t_setup
     t0 = time.perf_counter()
     job_of = {}
@@ -426,6 +464,14 @@ def setup_node(args, world, rank, dev):
                 "-> cached-state band/verdict -> D2H -> fail-fast writes -> node health exchange [detect latency] "
                 "-> endTime writes, history advance, claims, admission",
         "warm_node": "resident 7-day history of every (app, metric) in HBM before the jobs arrive",
+        "multi_cluster": ({"clusters": n_clusters, "cross_cluster_baselines": "every other app",
+                           "exchange": "rollout engine: baseline windows requested at admission, served by the "
+                                       "cluster's rank, one all_to_all into a device buffer, scattered on the device",
+                           "admission": {k: intake_timings.get(k) for k in ("affine_ms", "affine_bytes",
+                                                                            "affine_requests")},
+                           "values_moved": int(roll.router.values_moved),
+                           "request_bytes": int(roll.router.request_bytes),
+                           "exchanges_with_requests": int(roll.router.exchanges)} if multi else False),
         "setup_s": round(setup_s, 2),
         "register_s": round(register_s, 3),
         "register_jobs_per_s": round(na / max(register_s, 1e-9), 1),
@@ -586,7 +632,11 @@ def setup_arrival(args, world, rank, dev):
     roll = RolloutMonitor(store, cfg, prom=server, device=dev, worker_id=f"node-m{rank}-rollout", step=STEP,
                           window=W, pods=P, clock=lambda: clock["t"], ring_len=R, min_capacity=max(64, J * W * M),
                           decode_threads=args.decode_threads, apps_per_query=256)
-    keys = [(ENDPOINT, "namespace_app_per_pod:" + m, ns[i], app[i]) for i in range(na) for m in METRICS]
+    if multi:
+        from ..parallel.affine import ClusterRouter
+        roll.router = ClusterRouter(lambda ep, w: int(ep.split("prom-")[1].split(":")[0]) % max(w, 1), dev,
+                                    home=[home_ep])
+    keys = [(home_ep, "namespace_app_per_pod:" + m, ns[i], app[i]) for i in range(na) for m in METRICS]
     hist = roll.history
     hist.clock = lambda: clock["t"]
     hist.want(keys, T0)

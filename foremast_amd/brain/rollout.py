@@ -1034,10 +1034,20 @@ class RolloutMonitor:
             remote = np.array([not self.router.local(fams[j][0]) for j in range(len(fams))])
             if remote.any():
                 for j in np.nonzero(remote)[0].tolist():
-                    rows_j = sel[fidx == j]
-                    part = [(int(b.rows[i]), b.ns_of(int(i)), self._pods_strs(b, int(i), pc)) for i in rows_j]
-                    pods = list(dict.fromkeys((ns, pod) for _, ns, ps in part for pod in ps))
-                    self._remote.append((dst, fams[j], start, n, part, pods))
+                    mj = fidx == j
+                    rows_j = sel[mj]
+                    # the request names the pods (the serving rank builds its query from them) ...
+                    pods = list(dict.fromkeys((b.ns_of(int(i)), pod) for i in rows_j
+                                              for pod in self._pods_strs(b, int(i), pc)))
+                    # ... and the owner's scatter map is computed here once, from the rows' pod keys:
+                    # (row, pod column) -> index of that pod in the request (-1: none)
+                    ph = native.key_hashes([k[0] for k in pods], [k[1] for k in pods])
+                    order = np.argsort(ph, kind="stable")
+                    Hj, vj = H[mj], valid[mj]
+                    at = np.searchsorted(ph[order], Hj).clip(0, max(len(pods) - 1, 0))
+                    idx = np.where(vj & (ph[order][at] == Hj), order[at], -1) if len(pods) else \
+                        np.full(Hj.shape, -1, dtype=np.int64)
+                    self._remote.append((dst, fams[j], start, n, b.rows[rows_j].astype(np.int64), idx, pods))
                 keep = ~remote[fidx]
                 if not keep.any():
                     return
@@ -1096,21 +1106,32 @@ class RolloutMonitor:
         return out
 
     async def _route(self) -> None:
-        """Cluster-affine lockstep exchange of this tick's remote window requests."""
+        """Cluster-affine lockstep exchange of this tick's remote window requests (the
+        route changes of this tick's admissions; nothing when none was admitted).  The
+        values arrive in one device buffer and are scattered into the rows' windows
+        on the device through the scatter maps built at admission."""
+        t0 = time.perf_counter()
         mine, self._remote = self._remote, []
-        vals = await self.router.exchange([(f, st, n, pods) for _dst, f, st, n, _part, pods in mine],
+        vals = await self.router.exchange([(f, st, n, pods) for _dst, f, st, n, _rows, _idx, pods in mine],
                                           self._serve_windows)
         P, Wc = self.P, self.Wc
-        for (dst, f, st, n, part, pods), v in zip(mine, vals):
-            local = {k: i for i, k in enumerate(pods)}
-            block = np.full((len(part), P, Wc), np.nan, dtype=np.float32)
-            for i, (_row, ns, ps) in enumerate(part):
-                for p, pod in enumerate(ps[:P]):
-                    block[i, p, :n] = v[local[(ns, pod)]]
-            rows = torch.tensor([row for row, _, _ in part], dtype=torch.long, device=self.device)
+        for (dst, f, st, n, rows, idx, pods), v in zip(mine, vals):
+            ok = (rows >= 0) & (rows < self.cap)
+            ok[ok] &= self.row_job[rows[ok]] >= 0      # rows retired since the request: skipped
+            if not ok.any():
+                continue
+            rows_k, idx_k = rows[ok], idx[ok]
+            gi = torch.from_numpy(idx_k).to(self.device)
+            g = v[gi.clamp(min=0)]                                          # [k, P, n]
+            g = torch.where((gi >= 0)[:, :, None], g, torch.full_like(g, float("nan")))
+            block = torch.full((len(rows_k), P, Wc), float("nan"), dtype=torch.float32, device=self.device)
+            m = min(n, Wc)
+            block[:, :, :m] = g[:, :, :m]
             tgt = self.base if dst == "base" else self.win
-            if all(0 <= row < self.cap and self.row_job[row] >= 0 for row in rows.tolist()):
-                tgt.index_copy_(0, rows, torch.from_numpy(block.reshape(len(part), P * Wc)).to(self.device))
+            tgt.index_copy_(0, torch.from_numpy(rows_k).to(self.device), block.view(len(rows_k), P * Wc))
+        self.timings["affine_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
+        self.timings["affine_bytes"] = float(self.router.last.get("bytes", 0))
+        self.timings["affine_requests"] = float(self.router.last.get("requests", 0))
 
     def _tick_block(self, S: int, k: int, fill: bool = True):
         """Pinned decode block of the tick (NaN-filled unless ``fill`` is False: the

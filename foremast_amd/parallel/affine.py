@@ -32,6 +32,7 @@ from __future__ import annotations
 import datetime
 import json
 import os
+import time
 import zlib
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -61,8 +62,12 @@ def affinity_from_env() -> Callable[[str, int], int]:
 
 class ClusterRouter:
     def __init__(self, rank_of: Callable[[str, int], int], device, group=None,
-                 timeout_s: Optional[float] = None, kv=None) -> None:
+                 timeout_s: Optional[float] = None, kv=None, home: Optional[Sequence[str]] = None) -> None:
         self.rank_of = rank_of
+        # home: the endpoints this rank scrapes itself (default: those rank_of maps to it).  A
+        # 1-rank rehearsal of the N-rank layout names its own cluster here, so the windows of
+        # the "other" clusters still travel through the collective exchange (served by itself)
+        self.home = set(home) if home is not None else None
         self.device = torch.device(device)
         self.group = group
         self.timeout_s = comm.exchange_timeout_s() if timeout_s is None else float(timeout_s)
@@ -70,6 +75,8 @@ class ClusterRouter:
         self.seq = 0        # exchanges with requests so far (lockstep: equal on every rank)
         self.exchanges = 0
         self.values_moved = 0
+        self.request_bytes = 0      # request payloads this rank published (pod lists, at admission)
+        self.last = {"ms": 0.0, "bytes": 0, "requests": 0}   # the last exchange (tick record)
         self._stale: Optional[str] = None   # this rank's request key of the last exchange
 
     def reset(self, kv=None) -> None:
@@ -82,20 +89,25 @@ class ClusterRouter:
         return self.kv
 
     def _gather_requests(self, mine: Sequence[Request], world: int, rank: int) -> List[List[Request]]:
+        """Publish this rank's requests and read every peer's: one set, one wait on all the
+        peers' keys, one multi-get (two store round trips at any world size)."""
         kv, seq = self._store(), self.seq
-        kv.set(f"req/{seq}/{rank}", json.dumps([[list(q[0]), q[1], q[2], [list(p) for p in q[3]]] for q in mine]))
-        out: List[List[Request]] = []
-        for r in range(world):
-            if r == rank:
-                out.append(list(mine))
-                continue
-            key = f"req/{seq}/{r}"
-            try:
-                kv.wait([key], datetime.timedelta(seconds=self.timeout_s))
-                raw = json.loads(kv.get(key))
-            except Exception as e:  # noqa: BLE001 - store timeout: the peer is gone
-                raise comm.CollectiveTimeout(f"affine requests of rank {r} (exchange {seq}) not published: {e}") from e
-            out.append([(tuple(q[0]), float(q[1]), int(q[2]), [tuple(p) for p in q[3]]) for q in raw])
+        payload = json.dumps([[list(q[0]), q[1], q[2], [list(p) for p in q[3]]] for q in mine])
+        kv.set(f"req/{seq}/{rank}", payload)
+        self.request_bytes += len(payload)
+        peers = [r for r in range(world) if r != rank]
+        keys = [f"req/{seq}/{r}" for r in peers]
+        try:
+            raws = []
+            if keys:
+                kv.wait(keys, datetime.timedelta(seconds=self.timeout_s))
+                raws = kv.multi_get(keys) if hasattr(kv, "multi_get") else [kv.get(k) for k in keys]
+        except Exception as e:  # noqa: BLE001 - store timeout: a peer is gone
+            raise comm.CollectiveTimeout(f"affine requests of ranks {peers} (exchange {seq}) not published: {e}") from e
+        out: List[List[Request]] = [list(mine) if r == rank else [] for r in range(world)]
+        for r, raw in zip(peers, raws):
+            raw = raw.decode() if isinstance(raw, (bytes, bytearray)) else bytes(raw).decode()
+            out[r] = [(tuple(q[0]), float(q[1]), int(q[2]), [tuple(p) for p in q[3]]) for q in json.loads(raw)]
         return out
 
     @property
@@ -107,16 +119,30 @@ class ClusterRouter:
         return dist.get_world_size(self.group) if comm.active(self.group) else 1
 
     def local(self, endpoint: str) -> bool:
+        if self.home is not None:
+            return endpoint in self.home
         return self.rank_of(endpoint, self.world) == self.rank
 
-    async def exchange(self, mine: Sequence[Request], serve) -> List[np.ndarray]:
+    async def exchange(self, mine: Sequence[Request], serve) -> List[torch.Tensor]:
         """Lockstep (every rank calls it once per tick).  ``mine``: this rank's
         requests for windows of other ranks' clusters; ``serve(requests) ->
         [values [pods, n]]`` fetches and decodes requests of this rank's own
-        clusters (awaitable).  Returns the values of ``mine``, in order."""
+        clusters (awaitable).  Returns the values of ``mine``, in order, as views of ONE
+        device buffer (the all-to-all's output: the caller scatters them on the device;
+        nothing is copied back to the host).
+
+        Requests are route changes, not per-tick traffic: a job's remote window is
+        requested once, at admission, and a tick without admissions costs one gather of
+        request counts.  ``FOREMAST_FORCE_COLLECTIVES=1`` runs the collective path at one
+        rank too (the 1-GPU rehearsal of the N-rank exchange)."""
         world, rank = self.world, self.rank
-        if world <= 1:
-            return list(await serve(list(mine))) if mine else []
+        t_start = time.perf_counter()
+        if world <= 1 and not (comm.force_collectives() and comm.active(self.group)):
+            if not mine:
+                return []
+            vals = list(await serve(list(mine)))
+            self.last = {"ms": round((time.perf_counter() - t_start) * 1e3, 3), "bytes": 0, "requests": len(mine)}
+            return [torch.from_numpy(np.ascontiguousarray(v, dtype=np.float32)).to(self.device) for v in vals]
         cnt = torch.tensor([len(mine)], dtype=torch.int64, device=self.device)
         counts = torch.empty(world, dtype=torch.int64, device=self.device)
         work = dist.all_gather_into_tensor(counts, cnt, group=self.group, async_op=True)
@@ -132,6 +158,7 @@ class ClusterRouter:
                 pass
             self._stale = None
         if int(counts.sum()) == 0:
+            self.last = {"ms": round((time.perf_counter() - t_start) * 1e3, 3), "bytes": 0, "requests": 0}
             return []
         gathered = self._gather_requests(mine, world, rank)
         self.exchanges += 1
@@ -149,7 +176,9 @@ class ClusterRouter:
                       for a in range(world)]
         send = np.concatenate([p.reshape(-1) for parts in send_parts for p in parts]) if sum(send_sizes) else \
             np.zeros(0, dtype=np.float32)
-        send_t = torch.from_numpy(send).to(self.device)
+        send_t = torch.from_numpy(send)
+        if self.device.type == "cuda":  # one pinned staging copy, one H2D
+            send_t = send_t.pin_memory().to(self.device, non_blocking=True)
         recv_t = torch.empty(sum(recv_sizes), dtype=torch.float32, device=self.device)
         work = dist.all_to_all_single(recv_t, send_t, output_split_sizes=recv_sizes, input_split_sizes=send_sizes,
                                       group=self.group, async_op=True)
@@ -157,13 +186,15 @@ class ClusterRouter:
         self._stale = f"req/{self.seq}/{rank}"   # deleted after the next tick's count gather
         self.seq += 1
         self.values_moved += int(recv_t.numel())
-        recv = recv_t.cpu().numpy()
         offs = np.concatenate([[0], np.cumsum(recv_sizes)])
-        out: List[Optional[np.ndarray]] = [None] * len(mine)
+        out: List[Optional[torch.Tensor]] = [None] * len(mine)
         pos = {a: int(offs[a]) for a in range(world)}
         for i, req in enumerate(mine):  # rank a's part holds my requests to a, in index order
             a = served_by[rank][i]
             sz = len(req[3]) * req[2]
-            out[i] = recv[pos[a]:pos[a] + sz].reshape(len(req[3]), req[2])
+            out[i] = recv_t[pos[a]:pos[a] + sz].view(len(req[3]), req[2])
             pos[a] += sz
+        self.last = {"ms": round((time.perf_counter() - t_start) * 1e3, 3),
+                     "bytes": int(recv_t.numel() + send_t.numel()) * 4,
+                     "requests": int(sum(len(g or []) for g in gathered))}
         return out  # type: ignore[return-value]
