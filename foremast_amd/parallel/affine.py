@@ -43,6 +43,7 @@ import torch.distributed as dist
 from . import comm
 
 Request = Tuple[Tuple[str, str], float, int, List[Tuple[str, str]]]  # (family, start, n, pods)
+CHUNK = 4 << 20   # bytes per store value of a published request list
 
 
 def affinity_from_env() -> Callable[[str, int], int]:
@@ -77,7 +78,8 @@ class ClusterRouter:
         self.values_moved = 0
         self.request_bytes = 0      # request payloads this rank published (pod lists, at admission)
         self.last = {"ms": 0.0, "bytes": 0, "requests": 0}   # the last exchange (tick record)
-        self._stale: Optional[str] = None   # this rank's request key of the last exchange
+        self._stale: Optional[List[str]] = None   # this rank's request keys of the last exchange
+        self._mine_keys: List[str] = []
 
     def reset(self, kv=None) -> None:
         """After a re-formation: the new generation's store, sequence from zero."""
@@ -92,22 +94,37 @@ class ClusterRouter:
         """Publish this rank's requests and read every peer's: one set, one wait on all the
         peers' keys, one multi-get (two store round trips at any world size)."""
         kv, seq = self._store(), self.seq
-        payload = json.dumps([[list(q[0]), q[1], q[2], [list(p) for p in q[3]]] for q in mine])
-        kv.set(f"req/{seq}/{rank}", payload)
+        payload = json.dumps([[list(q[0]), q[1], q[2], [list(p) for p in q[3]]] for q in mine]).encode()
+        # the store caps one value at 8 MiB: a burst of admissions is published in chunks, the
+        # chunk count last (a reader that sees it sees every chunk)
+        chunks = [payload[i:i + CHUNK] for i in range(0, len(payload), CHUNK)] or [b""]
+        for i, c in enumerate(chunks):
+            kv.set(f"req/{seq}/{rank}/{i}", c)
+        kv.set(f"req/{seq}/{rank}", str(len(chunks)))
+        self._mine_keys = [f"req/{seq}/{rank}"] + [f"req/{seq}/{rank}/{i}" for i in range(len(chunks))]
         self.request_bytes += len(payload)
         peers = [r for r in range(world) if r != rank]
         keys = [f"req/{seq}/{r}" for r in peers]
+
+        def dec(v) -> str:
+            return v.decode() if isinstance(v, (bytes, bytearray)) else bytes(v).decode()
         try:
             raws = []
             if keys:
                 kv.wait(keys, datetime.timedelta(seconds=self.timeout_s))
-                raws = kv.multi_get(keys) if hasattr(kv, "multi_get") else [kv.get(k) for k in keys]
+                mget = kv.multi_get if hasattr(kv, "multi_get") else (lambda ks: [kv.get(k) for k in ks])
+                counts = [int(dec(v)) for v in mget(keys)]
+                ckeys = [f"req/{seq}/{r}/{i}" for r, n in zip(peers, counts) for i in range(n)]
+                parts = mget(ckeys)
+                pos = 0
+                for n in counts:
+                    raws.append(b"".join(bytes(v) for v in parts[pos:pos + n]))
+                    pos += n
         except Exception as e:  # noqa: BLE001 - store timeout: a peer is gone
             raise comm.CollectiveTimeout(f"affine requests of ranks {peers} (exchange {seq}) not published: {e}") from e
         out: List[List[Request]] = [list(mine) if r == rank else [] for r in range(world)]
         for r, raw in zip(peers, raws):
-            raw = raw.decode() if isinstance(raw, (bytes, bytearray)) else bytes(raw).decode()
-            out[r] = [(tuple(q[0]), float(q[1]), int(q[2]), [tuple(p) for p in q[3]]) for q in json.loads(raw)]
+            out[r] = [(tuple(q[0]), float(q[1]), int(q[2]), [tuple(p) for p in q[3]]) for q in json.loads(raw.decode())]
         return out
 
     @property
@@ -153,7 +170,8 @@ class ClusterRouter:
             # all-to-all may not have synchronised with it there: deleting the key right after
             # it could pull it from under that peer's read)
             try:
-                self._store().delete_key(self._stale)
+                for k in self._stale:
+                    self._store().delete_key(k)
             except Exception:  # noqa: BLE001 - best-effort cleanup
                 pass
             self._stale = None
@@ -183,7 +201,7 @@ class ClusterRouter:
         work = dist.all_to_all_single(recv_t, send_t, output_split_sizes=recv_sizes, input_split_sizes=send_sizes,
                                       group=self.group, async_op=True)
         comm.wait_bounded(work, self.timeout_s, "affine window all-to-all")
-        self._stale = f"req/{self.seq}/{rank}"   # deleted after the next tick's count gather
+        self._stale = list(self._mine_keys)   # deleted after the next tick's count gather
         self.seq += 1
         self.values_moved += int(recv_t.numel())
         offs = np.concatenate([[0], np.cumsum(recv_sizes)])

@@ -95,3 +95,31 @@ def test_multi_cluster_canary_crosses_ranks(tmp_path, fail_beat):
     vals = json.loads(st["shop"]["anomalyInfo"])["error5xx"]["values"]
     assert vals[1] > 30
     assert st["cart"]["status"] == r.ST_COMPLETED_HEALTH and st["inv"]["status"] == r.ST_COMPLETED_HEALTH
+
+
+def test_request_lists_larger_than_a_store_value_are_chunked():
+    """A burst of admissions publishes more than the store's 8 MiB value cap: the
+    requests go in chunks and every peer reassembles them (two ranks sharing one store)."""
+    import threading
+
+    import torch
+    import torch.distributed as dist
+    from foremast_amd.parallel.affine import CHUNK, ClusterRouter
+    kv = dist.HashStore()
+    reqs = {r: [(("http://prom-%d/" % r, "namespace_pod:m"), 1.7e9, 11,
+                 [("ns%d" % (i % 7), "app%d-v1-%d-5b6c7d8e9f" % (i, r)) for i in range(j * 500, (j + 1) * 500)])
+                for j in range(2 * CHUNK // 20000)] for r in range(2)}
+    got = {}
+
+    def rank(r):
+        rt = ClusterRouter(lambda ep, w: 0, torch.device("cpu"), kv=kv)
+        got[r] = rt._gather_requests(reqs[r], 2, r)
+    ts = [threading.Thread(target=rank, args=(r,)) for r in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(60)
+    assert len(json_size := str(reqs[0])) > CHUNK and json_size
+    for r in range(2):
+        assert [(q[0], q[1], q[2], list(q[3])) for q in got[r][1 - r]] == \
+            [(q[0], q[1], q[2], list(q[3])) for q in reqs[1 - r]]
