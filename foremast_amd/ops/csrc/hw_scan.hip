@@ -1960,12 +1960,17 @@ __global__ void hw_dg_list_all_kernel(int* deferred, int pairs) {
   if (blockIdx.x == 0 && threadIdx.x == 0) deferred[0] = pairs;
 }
 
+// the seasons variant 5 is instantiated for: m = 32 K, K steps per lane
+// (1440 = 32 x 45: the 60 s step; 288 = 32 x 9: the 300 s step)
+static bool d_supported_k(int K) { return K == 45 || K == 9; }
+
 extern "C" size_t fm_hw_d_lds_bytes(int Tp, int seg, int K) {
-  if (K != 45 || seg <= 0) return (size_t)-1;
+  if (!d_supported_k(K) || seg <= 0) return (size_t)-1;
   const int nseg = Tp / seg;
   if (nseg < 2 || nseg > D_MAXSEG) return (size_t)-1;
   const int NMW = (32 * K + 31) / 32;
-  return ((size_t)2 * (nseg - 1) * DLay<45>::SEASON + 2 * NMW + 8 * D_WAVES + 4 + 2 * HALF_HB + 4 * 2 * HALF_HB + 4 * 2 * 4 +
+  const int season = D_CHUNK * ((K + 7) / 8);  // DLay<K>::SEASON
+  return ((size_t)2 * (nseg - 1) * season + 2 * NMW + 8 * D_WAVES + 4 + 2 * HALF_HB + 4 * 2 * HALF_HB + 4 * 2 * 4 +
           4) * 4;
 }
 
@@ -2069,18 +2074,28 @@ extern "C" int fm_hw_d_fit(const SmoothArgs* a, int hmax, int* deferred, hipStre
   return fm_hw_d_fit_split(a, hmax, deferred, nullptr, 0, 0, st);
 }
 
+template <int K>
+static hipError_t launch_d_fit(const SmoothArgs* a, int hmax, int* deferred, int* split_ws, int max_split, int slots,
+                               hipStream_t st);
+
 extern "C" int fm_hw_d_fit_split(const SmoothArgs* a, int hmax, int* deferred, int* split_ws, int max_split,
                                  int slots, hipStream_t st) {
   const int K = a->K;
-  if (K != 45 || a->seg != 32 * K || a->m != a->seg || a->Tp % a->seg != 0 || a->Tp / a->seg < 2 ||
+  if (!d_supported_k(K) || a->seg != 32 * K || a->m != a->seg || a->Tp % a->seg != 0 || a->Tp / a->seg < 2 ||
       a->Tp / a->seg > D_MAXSEG || !a->pair_tab || a->season_out || hmax < 1 || hmax > K || hmax > HALF_HB)
     return (int)hipErrorNotSupported;
   if (a->N <= 0) return 0;
-  const size_t lds = fm_hw_d_lds_bytes(a->Tp, a->seg, K);
-  const size_t glds = fm_hw_half_lds_bytes(a->Tp, a->seg, K);
-  if (lds > 80 * 1024 || glds > 64 * 1024 || fm_hw_dg_lds_bytes(a->Tp, a->seg, K) > 80 * 1024)
+  if (fm_hw_d_lds_bytes(a->Tp, a->seg, K) > 80 * 1024 || fm_hw_dg_lds_bytes(a->Tp, a->seg, K) > 80 * 1024)
     return (int)hipErrorNotSupported;
   if (!deferred) return (int)hipErrorInvalidValue;
+  return (int)(K == 45 ? launch_d_fit<45>(a, hmax, deferred, split_ws, max_split, slots, st)
+                       : launch_d_fit<9>(a, hmax, deferred, split_ws, max_split, slots, st));
+}
+
+template <int K>
+static hipError_t launch_d_fit(const SmoothArgs* a, int hmax, int* deferred, int* split_ws, int max_split, int slots,
+                               hipStream_t st) {
+  const size_t lds = fm_hw_d_lds_bytes(a->Tp, a->seg, K);
   const int pairs = (a->N + 1) / 2;
   const int S = (split_ws && max_split > 0 && a->G >= 2) ? fm_hw_d_split_plan(pairs, slots, max_split) : 0;
   // arrival counters are zero between launches: allocated zeroed, and the second arriver
@@ -2096,30 +2111,32 @@ extern "C" int fm_hw_d_fit_split(const SmoothArgs* a, int hmax, int* deferred, i
   if (da && da[0] == '1')
     hipLaunchKernelGGL(hw_dg_list_all_kernel, dim3((pairs + 255) / 256), dim3(256), 0, st, deferred, pairs);
   else if (prune)
-    hipLaunchKernelGGL((hw_d_kernel<45, true>), dim3(pairs - S + 2 * S), dim3(256), lds, st, *a, hmax, deferred,
+    hipLaunchKernelGGL((hw_d_kernel<K, true>), dim3(pairs - S + 2 * S), dim3(256), lds, st, *a, hmax, deferred,
                        pairs - S, cnt, cand, hints);
   else
-    hipLaunchKernelGGL((hw_d_kernel<45, false>), dim3(pairs - S + 2 * S), dim3(256), lds, st, *a, hmax, deferred,
+    hipLaunchKernelGGL((hw_d_kernel<K, false>), dim3(pairs - S + 2 * S), dim3(256), lds, st, *a, hmax, deferred,
                        pairs - S, cnt, cand, hints);
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return (int)e;
+  if (e != hipSuccess) return e;
   // gapped pairs: the variant-5 walk with masked seasons (FOREMAST_HW_GAPS=v4: the variant-4
-  // general kernel instead, for A/B runs)
+  // general kernel instead, for A/B runs; daily season at 60 s only)
   const char* ge = getenv("FOREMAST_HW_GAPS");
-  if (ge && ge[0] == 'v') {
+  if (K == 45 && ge && ge[0] == 'v') {
+    const size_t glds = fm_hw_half_lds_bytes(a->Tp, a->seg, K);
+    if (glds > 64 * 1024) return hipErrorNotSupported;
     hipLaunchKernelGGL((hw_half_general_kernel<45>), dim3(pairs < 512 ? pairs : 512), dim3(256), glds, st, *a, hmax,
                        deferred);
-    return (int)hipGetLastError();
+    return hipGetLastError();
   }
   const size_t dlds = fm_hw_dg_lds_bytes(a->Tp, a->seg, K);
   int grid = pairs < 512 ? pairs : 512;
   const char* gg = getenv("FOREMAST_HW_DG_GRID");  // A/B: workgroups of the gapped kernel
   if (gg && atoi(gg) > 0) grid = atoi(gg) < pairs ? atoi(gg) : pairs;
   if (prune)
-    hipLaunchKernelGGL((hw_dg_kernel<45, true>), dim3(grid), dim3(256), dlds, st, *a, hmax, deferred, hints);
+    hipLaunchKernelGGL((hw_dg_kernel<K, true>), dim3(grid), dim3(256), dlds, st, *a, hmax, deferred, hints);
   else
-    hipLaunchKernelGGL((hw_dg_kernel<45, false>), dim3(grid), dim3(256), dlds, st, *a, hmax, deferred, hints);
-  return (int)hipGetLastError();
+    hipLaunchKernelGGL((hw_dg_kernel<K, false>), dim3(grid), dim3(256), dlds, st, *a, hmax, deferred, hints);
+  return hipGetLastError();
 }
 
 template <int K, int MODE, typename TIN, int NC, int MINW, bool TAB = false>

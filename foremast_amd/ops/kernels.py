@@ -235,7 +235,7 @@ def _hist_check(hist: torch.Tensor, head: int, length: int) -> None:
 
 
 UNIFORM_K = (8, 12, 16, 24, 32)
-HALF_K = (45,)        # variant 4 (two series per wave): season = 32 * K
+HALF_K = (45, 9)      # variants 4 / 5 (two series per wave): season = 32 * K (variant 4: K = 45 only)
 HALF_HB = 16          # seasonal phases kept per series by variant 4 (max forecast horizon)
 last_hw_variant: Optional[int] = None  # variant actually launched by the last smoothing_fit (tests/bench)
 DEFAULT_HW_VARIANT = 5
@@ -377,13 +377,13 @@ def smoothing_fit(hist: torch.Tensor, head: int, length: int, mode: int, m: int,
     if variant in (4, 5):
         hmax = det.max_horizon
         if (mode == MODE_HW and bf16 and mm % 32 == 0 and mm // 32 in HALF_K and not want_season
-                and hmax is not None and 1 <= hmax <= min(mm // 32, HALF_HB) and K is None
-                and lib.fm_hw_half_lds_bytes(Tp, mm, mm // 32) <= LDS_LIMIT):
+                and hmax is not None and 1 <= hmax <= min(mm // 32, HALF_HB) and K is None):
             if variant == 5 and lib.fm_hw_d_lds_bytes(Tp, mm, mm // 32) <= D_LDS_LIMIT:
                 return _hw_half_fit(lib, hist, head, length, mm, grid, det, Tp, pad, hmax, out, residual=True,
                                     head_dev=head_dev, defer=defer_detect)
-            return _hw_half_fit(lib, hist, head, length, mm, grid, det, Tp, pad, hmax, out, head_dev=head_dev,
-                                defer=defer_detect)
+            if mm // 32 == 45 and lib.fm_hw_half_lds_bytes(Tp, mm, mm // 32) <= LDS_LIMIT:
+                return _hw_half_fit(lib, hist, head, length, mm, grid, det, Tp, pad, hmax, out, head_dev=head_dev,
+                                    defer=defer_detect)
         variant = 3
     if detect_after is not None:
         torch.cuda.current_stream(dev).wait_stream(detect_after)

@@ -27,13 +27,17 @@ def main():
     p.add_argument("--series", type=int, default=100_000)
     p.add_argument("--rounds", type=int, default=3)
     p.add_argument("--cases", default="dense,dgall,gap20,miss1e-4,miss1e-3")
+    p.add_argument("--season", type=int, default=1440, help="points per day: 1440 (60 s step) or 288 (300 s)")
     args = p.parse_args()
     dev = torch.device("cuda:0")
-    N, R, m, C = args.series, 10080, 1440, 50
+    N, m = args.series, args.season
+    R, C = 7 * m, 50 if m >= 1440 else 10
     base = synthetic_history(N, R, m, dev, seed=3).to(torch.bfloat16)
     grid = sm.make_grid(sm.MODE_HW, (0.1, 0.3, 0.5, 0.8), (0.0, 0.01, 0.05, 0.1), (0.05, 0.1, 0.3, 0.5)).to(dev)
     cur = base[:, -C:].float().contiguous()
-    spec = K.DetectSpec(horizons=torch.arange(1, 11, dtype=torch.int32, device=dev).repeat(C // 10), max_horizon=10,
+    hz = min(10, m // 32)
+    spec = K.DetectSpec(horizons=torch.arange(1, hz + 1, dtype=torch.int32, device=dev).repeat(C // hz + 1)[:C],
+                        max_horizon=hz,
                         threshold=torch.full((N,), 3.0, device=dev), bound=torch.full((N,), 3, dtype=torch.int8, device=dev),
                         min_lower=torch.zeros(N, device=dev), cur=cur)
     g = torch.Generator(device=dev).manual_seed(5)
@@ -71,7 +75,8 @@ def main():
     dense = sorted(x[0] for x in res.get("dense", [(float("nan"), 0)]))
     for case, xs in res.items():
         ms = sorted(x[0] for x in xs)
-        rec = {"case": case, "ms_median": round(ms[len(ms) // 2], 3), "ms_all": [round(x, 3) for x in ms],
+        rec = {"case": case, "season": m, "points": R, "ms_median": round(ms[len(ms) // 2], 3),
+               "ns_per_point": round(ms[len(ms) // 2] * 1e6 / (N * R), 4), "ms_all": [round(x, 3) for x in ms],
                "gapped_pairs_per_fit": xs[-1][1], "pairs": (N + 1) // 2,
                "vs_dense": round(ms[len(ms) // 2] / dense[len(dense) // 2], 3) if "dense" in res else None}
         print(json.dumps(rec), flush=True)

@@ -166,3 +166,49 @@ def test_gapped_kernel_agrees_with_general_kernel(K, monkeypatch):
         outs.append({k: v.clone() for k, v in o.items()})
     assert (outs[0]["best"] == outs[1]["best"]).float().mean() >= 0.9
     np.testing.assert_allclose(outs[0]["sigma"].cpu().numpy(), outs[1]["sigma"].cpu().numpy(), rtol=2e-3)
+
+
+@pytest.mark.parametrize("case", ["dense", "miss1e-3", "outage"])
+def test_variant5_at_the_300s_step_matches_reference(K, case, monkeypatch):
+    """Variant 5 at the 300 s step (a daily season of 288 = 32 lanes x 9 steps, the week =
+    2,016 points): the same fit as the fp64 reference, dense and gapped (the gapped kernel
+    at K = 9), and the branch and bound exact."""
+    dev = torch.device("cuda:0")
+    m, N = 288, 22
+    T = 7 * m
+    y = _series(N, T, m, seed=41)
+    rng = np.random.default_rng(42)
+    if case == "miss1e-3":
+        y[rng.random(y.shape) < 2e-3] = np.nan
+    elif case == "outage":
+        y[::3, 3 * m + 17:3 * m + 23] = np.nan           # 30 minutes = 6 points
+    ring = torch.tensor(y, device=dev).to(torch.bfloat16)
+    yl = ring.float().cpu().numpy()
+    C = 8
+    hz = torch.tensor([1, 2, 1, 2, 1, 2, 1, 2], dtype=torch.int32)
+    cur = torch.tensor(np.nan_to_num(y[:, -C:], nan=20.0) * 1.05, device=dev)
+    spec = K.DetectSpec(horizons=hz.to(dev), threshold=torch.full((N,), 2.0, device=dev),
+                        bound=torch.full((N,), 3, dtype=torch.int8, device=dev),
+                        min_lower=torch.full((N,), -1e30, device=dev), cur=cur, max_horizon=2)
+    K.hw_clear_gap_flags()
+    outs = []
+    for prune in ("1", "0"):
+        monkeypatch.setenv("FOREMAST_HW_PRUNE", prune)
+        o = K.smoothing_fit(ring, 0, T, sm_ref.MODE_HW, m, GRID.to(dev), spec, variant=5)
+        torch.cuda.synchronize()
+        assert K.last_hw_variant == 5
+        outs.append({k: v.clone() for k, v in o.items()})
+    for key in ("best", "level", "trend", "sigma", "verdict", "forecast"):
+        assert torch.equal(outs[0][key], outs[1][key]), key
+    out = outs[0]
+    ref = sm_ref.fit_smoothing(torch.tensor(yl, dtype=torch.float64), sm_ref.MODE_HW, GRID.double(), m=m)
+    kb = out["best"].cpu().long()
+    same = (kb == ref.best).numpy()
+    assert same.mean() >= 0.75
+    _assert_near_optimal(yl, GRID, sm_ref.MODE_HW, m, kb)
+    np.testing.assert_allclose(out["sigma"].cpu().numpy(), ref.sigma.numpy(), rtol=5e-3)
+    np.testing.assert_allclose(out["level"].cpu().numpy()[same], ref.level.numpy()[same], rtol=2e-3, atol=5e-3)
+    f_ref = sm_ref.forecast(ref, hz.long())
+    np.testing.assert_allclose(out["forecast"].cpu().numpy()[same], f_ref.numpy()[same], rtol=5e-3, atol=2e-2)
+    d = _ref_detect(out, GRID, sm_ref.MODE_HW, m, hz, cur)
+    assert torch.equal(d.verdict, out["verdict"].cpu())
