@@ -245,6 +245,35 @@ def _exchange_summary(bds, steps: int, world: int, config: str) -> dict:
             "roster_bytes_p50_max": [q(by, 50), q(by, 100)], "samples": len(xs)}
 
 
+def _tail_attribution(bds, factor: float = 2.5) -> dict:
+    """Ticks slower than ``factor`` x the p50 tick, each with what it did besides the
+    steady-state work: a statistics refresh (window_stats over every ring), cyclic-GC
+    pauses, new device segments from the caching allocator (hipMalloc) or allocator
+    retries, verdict writes, the node exchange."""
+    tt = [b.get("tick_total_ms") for b in bds if b.get("tick_total_ms") is not None]
+    if not tt:
+        return {}
+    p50 = float(np.percentile(tt, 50))
+    out = []
+    for i, b in enumerate(bds):
+        t = b.get("tick_total_ms")
+        if t is None or t <= factor * p50:
+            continue
+        why = []
+        if b.get("restat"):
+            why.append("restat")
+        if b.get("gc_ms", 0) > 0.2 * (t - p50):
+            why.append(f"gc {b['gc_ms']} ms")
+        if b.get("hip_mallocs", 0) or b.get("alloc_retries", 0):
+            why.append(f"allocator ({b.get('hip_mallocs', 0)} new segments, {b.get('alloc_retries', 0)} retries)")
+        if b.get("exchange_ms", 0) > 0.2 * (t - p50):
+            why.append(f"exchange {b['exchange_ms']} ms")
+        out.append({"tick": i, "ms": t, "x_p50": round(t / p50, 2), "causes": why or ["unattributed"],
+                    **{k: b[k] for k in ("intake_ms", "tick_ms", "gc_ms") if k in b}})
+    return {"p50_ms": round(p50, 3), "max_ms": round(max(tt), 3), "max_over_p50": round(max(tt) / p50, 2),
+            "threshold_x_p50": factor, "outliers": out, "samples": len(tt)}
+
+
 def init_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
@@ -1036,6 +1065,8 @@ def main():
         }
         if decoder is not None:
             res["decode_ms_last_tick"] = round(decoder.last_decode_ms, 3)
+        if timed_rows is not None and arrival_finish is not None and args.config == "node-lstm":
+            res["tails"] = _tail_attribution((node_breakdowns or [])[-args.steps:])
         if timed_rows is not None and arrival_finish is not None:
             bds = (node_breakdowns or [])[-args.steps:]
 

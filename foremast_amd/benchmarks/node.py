@@ -968,17 +968,45 @@ def setup_node_lstm(args, world, rank, dev):
     breakdowns: List[Dict[str, float]] = []
     scored: List[int] = []
 
+    gc_pause = {"t": 0.0, "t0": 0.0, "n": 0}
+
+    def _gc_cb(phase, info):  # cyclic-GC pauses inside a tick
+        if phase == "start":
+            gc_pause["t0"] = time.perf_counter()
+        else:
+            gc_pause["t"] += time.perf_counter() - gc_pause["t0"]
+            gc_pause["n"] += 1
+
+    def _mem():
+        if dev.type != "cuda":
+            return 0, 0
+        ms = torch.cuda.memory_stats(dev)
+        return int(ms.get("segment.all.allocated", 0)), int(ms.get("num_alloc_retries", 0))
+
     def tick(k):
         clock["t"] = T0 + STEP * k
         n_live = lstm._n_series
+        seg0, retry0 = _mem()
+        gc_pause["t"], gc_pause["n"] = 0.0, 0
+        st0 = lstm.shard.ticks
         t0 = time.perf_counter()
-        loop.run_until_complete(node.tick())
+        gc.callbacks.append(_gc_cb)
+        try:
+            loop.run_until_complete(node.tick())
+        finally:
+            gc.callbacks.remove(_gc_cb)
         if dev.type == "cuda":
             torch.cuda.synchronize()
         bd = {kk: round(v, 3) for kk, v in lstm.timings.items()}
         bd.update({kk: round(v, 3) for kk, v in node.timings.items()})
         bd["tick_total_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
         bd["entities"] = len(lstm.jobs)
+        # what a slow tick did besides the steady-state work (the tail attribution below)
+        seg1, retry1 = _mem()
+        re = lstm.shard.restat_every
+        bd["restat"] = any((t + 1) % re == 0 for t in range(st0, lstm.shard.ticks)) if re else False
+        bd["gc_ms"], bd["gc_runs"] = round(gc_pause["t"] * 1e3, 2), gc_pause["n"]
+        bd["hip_mallocs"], bd["alloc_retries"] = seg1 - seg0, retry1 - retry0
         _exchange_bd(node, bd)
         breakdowns.append(bd)
         scored.append(n_live)
