@@ -268,6 +268,9 @@ def _tail_attribution(bds, factor: float = 2.5) -> dict:
             why.append(f"allocator ({b.get('hip_mallocs', 0)} new segments, {b.get('alloc_retries', 0)} retries)")
         if b.get("exchange_ms", 0) > 0.2 * (t - p50):
             why.append(f"exchange {b['exchange_ms']} ms")
+        nw = int(b.get("verdicts_written", 0))
+        if nw >= 20:  # a burst of fail-fast / endTime writes to the job store
+            why.append(f"{nw} verdict writes")
         out.append({"tick": i, "ms": t, "x_p50": round(t / p50, 2), "causes": why or ["unattributed"],
                     **{k: b[k] for k in ("intake_ms", "tick_ms", "gc_ms") if k in b}})
     return {"p50_ms": round(p50, 3), "max_ms": round(max(tt), 3), "max_over_p50": round(max(tt) / p50, 2),

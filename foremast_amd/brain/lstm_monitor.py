@@ -541,6 +541,7 @@ class LstmMonitor:
         self.ticks += 1
         self.metrics.series_scored.inc(self._n_series)
         self.timings["tick_ms"] = (time.perf_counter() - t0) * 1e3
+        self.timings["verdicts_written"] = float(len(items))
         return written
 
     def _newest(self) -> np.ndarray:
