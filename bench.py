@@ -124,6 +124,14 @@ def parse():
                    help="pinned ingest: prefetch tick k+1's points H2D on a copy stream during tick k "
                         "(double-buffered) instead of copying them on the main stream at the start of the tick; "
                         "measured neutral at 12.5k series per GPU (1.458 vs 1.436 ms), so off by default")
+    p.add_argument("--graph-prefetch", dest="graph_prefetch", action="store_true", default=True,
+                   help="(default) canary graph ticks: the points of tick k+1 are copied H2D on a copy stream into "
+                        "the second of two input buffers (one captured graph each) while tick k runs, so a tick "
+                        "starts with its input on the device; the tick itself is never queued behind the previous")
+    p.add_argument("--no-graph-prefetch", dest="graph_prefetch", action="store_false")
+    p.add_argument("--spin-wait", dest="spin_wait", action="store_true", default=False,
+                   help="canary: wait for a tick's completion by polling its event instead of a blocking stream "
+                        "synchronize (shorter host wake-up between ticks)")
     p.add_argument("--serial-pairwise", action="store_true",
                    help="run the rank tests on the main stream before the fit (fused detect epilogue) "
                         "instead of on a side stream concurrently with it")
@@ -556,7 +564,53 @@ def setup_canary(args, world, rank, dev):
             agg._gather_fused(shard.app_stats, shard.out["verdict"])
         health_hosts[0].copy_(agg.recv if agg.fused else shard.app_stats, non_blocking=pin)
 
+    # double-buffered graph input: tick k+1's points are copied into the other buffer while
+    # tick k runs (each buffer has its own captured graph)
+    gpf = (args.graph and args.graph_prefetch and pin and exch is None and args.ingest == "pinned"
+           and not pipelined)
+    if gpf:
+        gbufs = [newvb, torch.empty_like(newvb)]
+        cstream = torch.cuda.Stream(dev)
+        gready, gstaged = [None, None], [None, None]
+
+        def gstage(i):
+            b = i % 2
+            with torch.cuda.stream(cstream):
+                gbufs[b].copy_(host_ticks[i], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(cstream)
+            gready[b], gstaged[b] = ev, i
+
+    def wait_tick():
+        if dev.type != "cuda":
+            return
+        if args.spin_wait:
+            ev = torch.cuda.Event()
+            ev.record()
+            while not ev.query():
+                pass
+        else:
+            torch.cuda.current_stream().synchronize()
+
     def tick(k):
+        if gpf and shard.graph_ready():
+            i = W + k
+            b = i % 2
+            if gstaged[b] != i:
+                gstage(i)
+            torch.cuda.current_stream().wait_event(gready[b])
+            out = shard.tick_graph(gbufs[b][:, :P], gbufs[b][:, P:], post=graph_tail)
+            if i + 1 < host_ticks.shape[0]:
+                gstage(i + 1)  # the other buffer's reader (tick i - 1) has completed
+            REFIT_FLAGS[k] = shard.last_refit
+            if out.get("post_in_graph"):
+                GRAPH_TAIL[0] = True
+                wait_tick()
+                return out
+            stats, _ = agg.tick(shard.app_stats, out["verdict"])
+            health_hosts[0].copy_(agg.recv if agg.fused else stats, non_blocking=pin)
+            wait_tick()
+            return out
         nv, nb, b = load_tick(W + k)
         if args.graph:
             # ingest + score (+ the health collective and the table's copy back) as one replay
@@ -568,8 +622,7 @@ def setup_canary(args, world, rank, dev):
         REFIT_FLAGS[k] = shard.last_refit
         if out.get("post_in_graph"):
             GRAPH_TAIL[0] = True
-            if dev.type == "cuda":
-                torch.cuda.current_stream().synchronize()
+            wait_tick()
             return out
         stats, _ = agg.tick(shard.app_stats, out["verdict"])
         hh = health_hosts[k % 2 if pipelined else 0]
@@ -605,7 +658,8 @@ def setup_canary(args, world, rank, dev):
         "hip_graph": bool(args.graph and dev.type == "cuda"),
         "ingest": args.ingest,
         "pipelined_ticks": pipelined,
-        "input_prefetch": prefetch,
+        "input_prefetch": prefetch or ("double-buffered H2D of tick k+1 during tick k (graph ticks)" if gpf else False),
+        "spin_wait": bool(args.spin_wait),
         "zero_copy": zero_copy,
         "model_cache": ("none: every tick refits every series" if args.refit_every <= 1 else
                         f"refit every {args.refit_every} ticks, O(1) Holt-Winters state update + detect in between"),

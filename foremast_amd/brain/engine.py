@@ -113,6 +113,7 @@ class StreamingShard:
         # HIP-graph tick (tick_graph): per-tick ring state lives in device memory
         self._graph = None
         self._graph_io = None
+        self._graphs: Dict[tuple, tuple] = {}   # io buffers -> (graph, post captured, outputs)
         self._side = None                # side HIP stream for the rank tests (overlap_pairwise)
         self.overlap_pairwise = self.gpu
         if self.gpu:
@@ -270,8 +271,9 @@ class StreamingShard:
         same kernel; the host only mirrors the ring bookkeeping.  The record is
         written from the host once, when the graph path (re)starts after eager
         ticks.  Falls back to the eager calls until :meth:`graph_ready`.
-        ``newv`` / ``newb`` must be the same buffers on every call (their
-        addresses are baked into the graph).  ``post`` (optional, called once, inside the
+        ``newv`` / ``newb``: one of at most two buffer sets (each set's addresses are baked
+        into its own graph: a double-buffered input whose next tick is copied while this
+        one runs).  ``post`` (optional, called once, inside the
         capture): the tick's own tail -- the node health collective and the copy of the
         health table to pinned host memory -- so one replay is the whole GPU side of the
         tick; on the eager ticks before capture the caller runs its tail itself (the
@@ -283,8 +285,8 @@ class StreamingShard:
             return out
         from ..ops import kernels as K
         io = (newv.data_ptr(), None if newb is None else newb.data_ptr())
-        if self._graph is not None and io != self._graph_io:
-            raise ValueError("tick_graph needs the same newv/newb buffers on every call")
+        if io not in self._graphs and len(self._graphs) >= 2:
+            raise ValueError("tick_graph takes at most two sets of newv/newb buffers (double-buffered input)")
         W, R = self.cur.W, self.hist.R
         if self._h_slots is None:
             self._refresh_horizons()  # builds the per-slot horizon table (host + device)
@@ -303,7 +305,11 @@ class StreamingShard:
         self.cur.ticks += 1
         self._new_pts += 1
         self.horizons = self._h_buf
-        if self._graph is None:
+        hit = self._graphs.get(io)
+        if hit is not None:
+            self._graph, self._post_in_graph, outs = hit
+            self.out = dict(outs)
+        else:
             def capture(with_post: bool):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
@@ -325,6 +331,7 @@ class StreamingShard:
             if g is None:
                 g = capture(False)
             self._graph, self._graph_io = g, io
+            self._graphs[io] = (g, self._post_in_graph, dict(self.out))
         self._graph.replay()
         self._stats_zeroed = False
         self.last_refit = True

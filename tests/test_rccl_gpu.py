@@ -214,3 +214,16 @@ def test_node_multi_cluster_forced_rccl_one_gpu():
     the one-cluster run, values delivered device to device."""
     mc = _check_mc(_mc_bench(1, cpu=False, multi=False, force=True), _mc_bench(1, cpu=False, multi=True, force=True))
     assert mc["admission"]["affine_bytes"] > 0
+
+
+@pytest.mark.gpu
+def test_double_buffered_graph_input_matches_single_buffer():
+    """The canary's graph ticks with the next tick's input copied during the current one
+    (two input buffers, one captured graph each) and a spin-wait give the same health
+    table and detection as one buffer copied at the start of each tick."""
+    args = CANARY + ["--steps", "6"]
+    ref = _bench(args + ["--no-graph-prefetch"], force=False, launcher=False, cpu=False)
+    got = _bench(args + ["--spin-wait"], force=False, launcher=False, cpu=False)
+    assert got["config"]["input_prefetch"] and not ref["config"]["input_prefetch"]
+    assert got["config"]["hip_graph"] and ref["config"]["hip_graph"]
+    assert got["health"] == ref["health"] and got["detection"] == ref["detection"]
