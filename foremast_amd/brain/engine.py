@@ -311,6 +311,7 @@ class StreamingShard:
             self.out = dict(outs)
         else:
             def capture(with_post: bool):
+                K.reserve_graph_workspace(self.device, self.hist.data.shape[0])
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     K.tick_advance(self._state_dev, R, W, self._h_dev, self._h_buf)

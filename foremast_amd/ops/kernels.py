@@ -443,8 +443,15 @@ def _half_workspace(dev, N: int) -> torch.Tensor:
     (device, N, stream): fits on two streams never share a count; the kernels
     bound every append by the pair list and the caller zeroes the workspace when a
     launch on this path fails (``_hw_half_fit``)."""
-    key = (dev.index, N, nat.stream_handle(dev))
+    # inside a HIP-graph capture the workspace must already exist: allocated there it would
+    # come from the graph's pool with its zero-fill captured, i.e. re-zeroed at every replay
+    # (the gap flags and the deferred-pair total would never survive a tick).  A captured fit
+    # uses the (device, N) "graph" workspace that reserve_graph_workspace made beforehand.
+    capturing = dev.type == "cuda" and torch.cuda.is_current_stream_capturing()
+    key = (dev.index, N, "graph") if capturing else (dev.index, N, nat.stream_handle(dev))
     ws = _HALF_WS.get(key)
+    if ws is None and capturing:
+        raise RuntimeError("HW workspace allocated inside a graph capture: call reserve_graph_workspace first")
     if ws is None:
         # {count, pairs..., done, total, queue, gap flags...}: total = pairs deferred to the
         # gapped-series kernel since allocation (hw_dg_kernel adds each launch's count); queue =
@@ -453,6 +460,15 @@ def _half_workspace(dev, N: int) -> torch.Tensor:
         ws = torch.zeros(4 + 2 * P, dtype=torch.int32, device=dev)
         _HALF_WS[key] = ws
     return ws
+
+
+def reserve_graph_workspace(dev, N: int) -> None:
+    """Allocate the deferred-pair workspace a captured Holt-Winters fit of N series uses
+    (outside the capture; see :func:`_half_workspace`)."""
+    dev = torch.device(dev)
+    key = (dev.index, N, "graph")
+    if key not in _HALF_WS:
+        _HALF_WS[key] = torch.zeros(4 + 2 * ((N + 1) // 2), dtype=torch.int32, device=dev)
 
 
 def hw_deferred_total(dev=None) -> int:
