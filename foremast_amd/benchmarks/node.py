@@ -632,11 +632,7 @@ def setup_arrival(args, world, rank, dev):
     roll = RolloutMonitor(store, cfg, prom=server, device=dev, worker_id=f"node-m{rank}-rollout", step=STEP,
                           window=W, pods=P, clock=lambda: clock["t"], ring_len=R, min_capacity=max(64, J * W * M),
                           decode_threads=args.decode_threads, apps_per_query=256)
-    if multi:
-        from ..parallel.affine import ClusterRouter
-        roll.router = ClusterRouter(lambda ep, w: int(ep.split("prom-")[1].split(":")[0]) % max(w, 1), dev,
-                                    home=[home_ep])
-    keys = [(home_ep, "namespace_app_per_pod:" + m, ns[i], app[i]) for i in range(na) for m in METRICS]
+    keys = [(ENDPOINT, "namespace_app_per_pod:" + m, ns[i], app[i]) for i in range(na) for m in METRICS]
     hist = roll.history
     hist.clock = lambda: clock["t"]
     hist.want(keys, T0)
