@@ -31,6 +31,7 @@ LSTM-autoencoder per node, trained data-parallel across the ranks
 
 from __future__ import annotations
 
+import collections
 import itertools
 import json
 import logging
@@ -55,6 +56,26 @@ from .resident import Key, ResidentHistory
 from .streaming import CALLER_SPLIT, is_continuous, series_of
 
 log = logging.getLogger("foremast.lstm_monitor")
+
+_ENC_STR = json.encoder.encode_basestring_ascii
+
+
+def _jfloat(x: float) -> str:
+    """``json.dumps`` of one float (repr; NaN / Infinity spelled as the json module does)."""
+    if x != x:
+        return "NaN"
+    if x in (float("inf"), float("-inf")):
+        return "Infinity" if x > 0 else "-Infinity"
+    return repr(x)
+
+
+def anomaly_info(t: float, pairs) -> str:
+    """``json.dumps({alias: {"tags": "lstm", "values": [t, v]}, ...})`` for (alias, v) pairs,
+    string-equal to it, without the encoder's per-call setup (~8 us a call: a tick on which
+    500 jobs fail at once wrote 500 of these inside the detect latency)."""
+    ts = _jfloat(float(t))
+    return "{" + ", ".join(f'{_ENC_STR(a)}: {{"tags": "lstm", "values": [{ts}, {_jfloat(float(v))}]}}'
+                           for a, v in pairs) + "}"
 
 
 def lstm_features(doc, cfg: BrainConfig) -> Optional[List[Tuple[str, Key]]]:
@@ -262,14 +283,18 @@ class LstmMonitor:
             self.shard.packed = None
         self._digest = None
 
-    def _drop(self, jid: str, now: float, free_row: bool = True) -> int:
+    def _drop(self, jid: str, now: float, free_row: bool = True, hks: Optional[list] = None) -> int:
         """Forget an entity; returns its row (-1: none), freed here unless ``free_row``
-        is False (the caller frees a batch)."""
+        is False (the caller frees a batch).  ``hks``: collect the history references to
+        release instead of releasing them here (the caller releases a batch in one call)."""
         e = self.jobs.pop(jid, None) or self.waiting.pop(jid, None)
         if e is None:
             return -1
         self._row_of.pop(jid, None)
-        self.history.unwant_h(e.hk, now)
+        if hks is None:
+            self.history.unwant_h(e.hk, now)
+        else:
+            hks.extend(e.hk)
         if e.row < 0:
             return -1
         self._n_series -= len(e.feats)
@@ -517,26 +542,27 @@ class LstmMonitor:
                     self.hits[jid] = (self.history.t_last, newest[e.row])
                 continue
             if v[e.row] == 1:
-                anomaly = {}
-                for f, (alias, _k) in enumerate(e.feats):
-                    anomaly[alias] = {"tags": "lstm", "values": [self.history.t_last, float(newest[e.row, f])]}
+                nv = newest[e.row].tolist()
+                aliases = [alias for alias, _k in e.feats]
                 items.append((jid, {"status": r.ST_COMPLETED_UNHEALTH, "claimed_by": "", "modified_ts": now,
-                                    "reason": "anomaly detected in " + ",".join(sorted(anomaly)) + " (lstm)",
-                                    "anomalyInfo": json.dumps(anomaly),
+                                    "reason": "anomaly detected in " + ",".join(sorted(set(aliases))) + " (lstm)",
+                                    "anomalyInfo": anomaly_info(self.history.t_last, dict(zip(aliases, nv)).items()),
                                     "processingContent": f"scored by {self.worker_id} (resident lstm)"}))
             elif now >= e.end_ts:
                 items.append((jid, {"status": r.ST_COMPLETED_HEALTH, "claimed_by": "", "reason": "",
                                     "modified_ts": now,
                                     "processingContent": f"scored by {self.worker_id} (resident lstm)"}))
         if items:
-            freed = []
+            freed, hks = [], []
             for (jid, fields), ok in zip(items, self.store.update_many(items, expect_claimed_by=self.worker_id)):
                 if ok:
                     written[jid] = fields["status"]
-                    self.metrics.jobs.labels(status=fields["status"]).inc()
-                row = self._drop(jid, now, free_row=False)
+                row = self._drop(jid, now, free_row=False, hks=hks)
                 if row >= 0:
                     freed.append(row)
+            for st, n_st in collections.Counter(written.values()).items():
+                self.metrics.jobs.labels(status=st).inc(n_st)
+            self.history.unwant_h(hks, now)  # one bulk release (18 us a call per job before)
             self._free_rows(freed)
         self.ticks += 1
         self.metrics.series_scored.inc(self._n_series)

@@ -218,3 +218,15 @@ def test_lstm_node_gpu_forced_collectives(tmp_path):
         assert t["members"][0].get("lstm_model")
     finally:
         _stop(proc, server)
+
+
+def test_anomaly_info_is_json_dumps():
+    """The verdict's anomalyInfo string is built without the json encoder's per-call
+    setup; it must stay string-equal to json.dumps (NaN / Infinity / escapes included)."""
+    import json
+    from foremast_amd.brain.lstm_monitor import anomaly_info
+    cases = [(1.7e9, [("latency", 1.5), ("error_rate", float("nan"))]),
+             (0.0, [('a"b', float("inf")), ("é", -0.0), ("c", float("-inf"))]),
+             (60.0, [("x", 3.0000001192092896)])]
+    for t, pairs in cases:
+        assert anomaly_info(t, pairs) == json.dumps({k: {"tags": "lstm", "values": [t, v]} for k, v in pairs})
