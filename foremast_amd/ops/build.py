@@ -35,7 +35,7 @@ def hipcc() -> str:
 
 def _flags() -> List[str]:
     return ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-ffp-contract=fast",
-            "-munsafe-fp-atomics", "-Wno-unused-result"]
+            "-munsafe-fp-atomics", "-Wno-unused-result", "-Werror=return-type"]
 
 
 def sources() -> List[str]:
