@@ -568,18 +568,24 @@ def setup_canary(args, world, rank, dev):
     # tick k runs (each buffer has its own captured graph)
     gpf = (args.graph and args.graph_prefetch and pin and exch is None and args.ingest == "pinned"
            and not pipelined)
+    main_stream = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
     if gpf:
         gbufs = [newvb, torch.empty_like(newvb)]
+        gviews = [(g[:, :P], g[:, P:]) for g in gbufs]
         cstream = torch.cuda.Stream(dev)
-        gready, gstaged = [None, None], [None, None]
+        gstaged = [None, None]
 
         def gstage(i):
+            """Copy tick i's points into its buffer on the copy stream and order the main
+            stream after the copy (enqueued now, behind the tick in flight: the next tick's
+            launch then has no wait to enqueue on the host's critical path)."""
             b = i % 2
             with torch.cuda.stream(cstream):
                 gbufs[b].copy_(host_ticks[i], non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(cstream)
-            gready[b], gstaged[b] = ev, i
+            main_stream.wait_event(ev)
+            gstaged[b] = i
 
     def wait_tick():
         if dev.type != "cuda":
@@ -590,7 +596,7 @@ def setup_canary(args, world, rank, dev):
             while not ev.query():
                 pass
         else:
-            torch.cuda.current_stream().synchronize()
+            main_stream.synchronize()
 
     def tick(k):
         if gpf and shard.graph_ready():
@@ -598,8 +604,7 @@ def setup_canary(args, world, rank, dev):
             b = i % 2
             if gstaged[b] != i:
                 gstage(i)
-            torch.cuda.current_stream().wait_event(gready[b])
-            out = shard.tick_graph(gbufs[b][:, :P], gbufs[b][:, P:], post=graph_tail)
+            out = shard.tick_graph(gviews[b][0], gviews[b][1], post=graph_tail)
             if i + 1 < host_ticks.shape[0]:
                 gstage(i + 1)  # the other buffer's reader (tick i - 1) has completed
             REFIT_FLAGS[k] = shard.last_refit

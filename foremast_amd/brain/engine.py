@@ -283,7 +283,6 @@ class StreamingShard:
             out = self.score()
             out["post_in_graph"] = False
             return out
-        from ..ops import kernels as K
         io = (newv.data_ptr(), None if newb is None else newb.data_ptr())
         if io not in self._graphs and len(self._graphs) >= 2:
             raise ValueError("tick_graph takes at most two sets of newv/newb buffers (double-buffered input)")
@@ -310,6 +309,8 @@ class StreamingShard:
             self._graph, self._post_in_graph, outs = hit
             self.out = dict(outs)
         else:
+            from ..ops import kernels as K
+
             def capture(with_post: bool):
                 K.reserve_graph_workspace(self.device, self.hist.data.shape[0])
                 g = torch.cuda.CUDAGraph()
