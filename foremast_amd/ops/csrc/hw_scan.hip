@@ -1594,7 +1594,11 @@ __device__ __forceinline__ void hw_dg_block(const SmoothArgs& a, int hmax, int n
   constexpr int SEA = DLay<K>::SEASON;
   constexpr int TS = PairTab<K>::SIZE;
   constexpr int NMW = (32 * K + 31) / 32;
-  const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+  // thread / lane ids re-derived through an opaque asm per pair: the queue loop of
+  // hw_dg_kernel then holds no lane-derived addresses across pairs (they spilled)
+  int tid = threadIdx.x, lane = lane_id();
+  asm volatile("" : "+v"(tid), "+v"(lane));
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int half = lane >> 5, j = lane & 31;
   const bool odd_row = ((lane >> 4) & 1) != 0;
   const int nseg = a.Tp / a.seg, m = a.m, ns1 = nseg - 1;
@@ -1938,7 +1942,14 @@ __global__ __launch_bounds__(256, 2) void hw_dg_kernel(const SmoothArgs a, int h
     const int q = next;
     __syncthreads();  // every thread has read `next` before thread 0 overwrites it
     if (q >= cnt) break;
-    hw_dg_block<K, PRUNE>(a, hmax, deferred[1 + q], hints, done + 3);
+    // the arguments through a pointer re-derived per pair (opaque to LLVM): values computed
+    // from them inside the block are not hoisted out of the queue loop (held across it, they
+    // spilled)
+    const __attribute__((address_space(4))) SmoothArgs* ap =
+        (const __attribute__((address_space(4))) SmoothArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    int hm = hmax, hi = hints;
+    asm volatile("" : "+s"(ap), "+s"(hm), "+s"(hi));
+    hw_dg_block<K, PRUNE>(*(const SmoothArgs*)ap, hm, deferred[1 + q], hi, done + 3);
     __syncthreads();  // LDS is reused by the next pair
   }
   if (threadIdx.x == 0) {
