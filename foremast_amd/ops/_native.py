@@ -103,6 +103,10 @@ def _declare(lib: C.CDLL) -> None:
     lib.fm_hw_d_fit.restype = I
     lib.fm_hw_d_fit_split.argtypes = [C.POINTER(SmoothArgs), I, P, P, I, I, P]
     lib.fm_hw_d_fit_split.restype = I
+    lib.fm_hw_q_lds_bytes.argtypes = [I, I, I]
+    lib.fm_hw_q_lds_bytes.restype = C.c_size_t
+    lib.fm_hw_q_fit.argtypes = [C.POINTER(SmoothArgs), P, I, P, P]
+    lib.fm_hw_q_fit.restype = I
     lib.fm_hw_d_split_plan.argtypes = [I, I, I]
     lib.fm_hw_d_split_plan.restype = I
     lib.fm_es_seq_fit.argtypes = [C.POINTER(SmoothArgs), I, I, P]

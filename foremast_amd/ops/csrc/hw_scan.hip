@@ -487,6 +487,21 @@ __device__ __forceinline__ void half_uniform_scan_pre(const Mat2* Bp, cfp tab_b,
   s2 = s2 + w2;
 }
 
+// hw_q_block's scan: one series per 16-lane row, so the four row rounds are the whole scan
+// (X_{-1} = x0 of the row's series; Bj = B^(lane & 15))
+__device__ __forceinline__ void row_uniform_scan_pre(const Mat2* Bp, v2f v1, v2f v2, v2f x01, v2f x02,
+                                                     const Mat2& Bj, v2f& s1, v2f& s2) {
+  v2f w1 = dppz2<0x111, 0xf>(v1);
+  v2f w2 = dppz2<0x111, 0xf>(v2);
+  row_round_z<0x111>(w1, w2, Bp[0]);
+  row_round_z<0x112>(w1, w2, Bp[1]);
+  row_round_z<0x114>(w1, w2, Bp[2]);
+  row_round_z<0x118>(w1, w2, Bp[3]);
+  matvec(Bj, x01, x02, s1, s2);
+  s1 = s1 + w1;
+  s2 = s2 + w2;
+}
+
 // General (per-lane matrix) exclusive affine scan within each 32-lane half.
 template <typename V>
 __device__ __forceinline__ void half_exclusive_scan(Aff<V>& a, int j) {
@@ -913,6 +928,27 @@ __device__ __forceinline__ v2f half_sum_last(v2f v) {
   return v;
 }
 
+// sum over each 16-lane row, valid in lanes 15 / 31 / 47 / 63 (hw_q_block: a series per
+// row): the first four rounds of half_sum_last, the same fixed tree within a row
+__device__ __forceinline__ v2f row_sum_last(v2f v) {
+  asm volatile(
+      "s_nop 1\n"
+      "v_add_f32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "v_add_f32_dpp %1, %1, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "s_nop 1\n"
+      "v_add_f32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "v_add_f32_dpp %1, %1, %1 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "s_nop 1\n"
+      "v_add_f32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "v_add_f32_dpp %1, %1, %1 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "s_nop 1\n"
+      "v_add_f32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "v_add_f32_dpp %1, %1, %1 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "s_nop 1"
+      : "+v"(v.x), "+v"(v.y));
+  return v;
+}
+
 // {pair[SEL], pair[SEL]} in one v_pk_mov_b32 (two v_mov_b32 otherwise); the result is a
 // 64-bit register pair from the start: left as one 32-bit value used twice, the season
 // loop's D registers were re-paired by 48 copies on every iteration
@@ -1025,7 +1061,7 @@ __device__ __forceinline__ void d_chunk0(const float* blk, cfp W, Chunk8f& c, v2
     if (r < 2 * K) w[r] = ldv2(W + 2 * r);
 }
 
-template <int K, bool FUSE, bool M2 = false, bool R1 = false>
+template <int K, bool FUSE, bool M2 = false, bool R1 = false, int L = 32>
 __device__ __forceinline__ void d_pass2(const float* blk, v2f* D, v2f c1, v2f c2, v2f g1a, cfp W, v2f& x1,
                                         v2f& x2, v2f& sse, v2f& p1, v2f& p2, cfp tb = nullptr,
                                         Mat2* Bn = nullptr, bool chk = false, const unsigned* ubp = nullptr,
@@ -1062,9 +1098,9 @@ __device__ __forceinline__ void d_pass2(const float* blk, v2f* D, v2f c1, v2f c2
       // the scalar registers of the next chunk's weights are free.
       // Only lanes 31 / 63 hold their half's sum and vote; the wave keeps the pair while
       // either of them does (the caller's __any).
-      const v2f s = half_sum_last(sse);  // the same sum as the final SSE
+      const v2f s = L == 32 ? half_sum_last(sse) : row_sum_last(sse);  // the same sum as the final SSE
       const float U = __uint_as_float(ub);
-      int v = ((lane_id() & 31) == 31 && !(s.x > U && s.y > U)) ? 1 : 0;
+      int v = ((lane_id() & (L - 1)) == L - 1 && !(s.x > U && s.y > U)) ? 1 : 0;
       asm volatile("" : "+v"(v));  // the flag lives in a VGPR: no scalar register across the loop
       *alive = v;
     }
@@ -1483,6 +1519,319 @@ __global__ __launch_bounds__(256, 2) void hw_d_kernel(const SmoothArgs a, int hm
   const int item = b - n_full, slot = item >> 1, h = item & 1, mid = npairs / 2;
   hw_d_block<K, PRUNE>(a, hmax, 2 * (n_full + slot), deferred, h ? mid : 0, h ? npairs : mid, slot, h, cnt, cand,
                        hints);
+}
+
+
+// ---- variant 5 at short seasons: hw_q_kernel (four series per wave) ---------------------------
+// A daily season m = 16 K (the 300 s step: 288 = 16 x 18) walked by 16 lanes per series, four
+// series per wave (one per DPP row) and per workgroup.  Against the 32-lane layout at K = 9
+// the per-season fixed work -- the lane scan, its B loads, the end-state broadcast, the prune
+// vote -- is spread over 18 steps instead of 9 and the scan loses its cross-row stage.  Same
+// residual-state walk and table pass 1 as hw_d_block (d_pass1 / d_pass2 are lane-count
+// agnostic; the prune vote sums over a row, L = 16), same outputs.  A quad with a gap past
+// season 0 goes, as its two series pairs, to the 32-lane gapped kernel (hw_dg_kernel<m / 32>,
+// launched with its own pair table); the hints are those of the first two series (the
+// branch and bound is exact in any order).
+constexpr int Q_S = 4;  // series per wave / workgroup
+template <int K, bool PRUNE>
+__device__ __forceinline__ void hw_q_block(const SmoothArgs& a, int hmax, int n0, int* deferred, int hints) {
+  constexpr int SEA = DLay<K>::SEASON;
+  constexpr int TS = PairTab<K>::SIZE;
+  constexpr int M = 16 * K;
+  constexpr int NMW = (M + 31) / 32;
+  const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+  const int sid = lane >> 4, j = lane & 15;
+  const int nseg = a.Tp / a.seg, m = a.m, ns1 = nseg - 1;
+
+  // ---- LDS: dl[4][ns1][SEA] | vmask[4][NMW] | stat[4 waves][4][4] | flag | ylast[4][HB] | bests[4][4][HB]
+  //          | wbest[4][4][4] | ubound[4] | queue | hints
+  float* dl = (float*)fm_hw_smem;
+  unsigned* vmask = (unsigned*)(dl + (size_t)Q_S * ns1 * SEA);
+  float* stat = (float*)(vmask + Q_S * NMW);
+  int* flag = (int*)(stat + 4 * Q_S * D_WAVES);
+  float* ylast = (float*)(flag + 4);
+  float* bests = ylast + Q_S * HALF_HB;
+  float* wbest = bests + 4 * Q_S * HALF_HB;
+  unsigned* ubound = (unsigned*)(wbest + 4 * Q_S * 4);  // [0..3] bounds, [4] queue, [5] hints
+
+  const int P = (a.N + 1) / 2;
+  int* gflags = deferred + 4 + P;
+  const int pa = n0 >> 1, pb = (n0 + 2 < a.N) ? pa + 1 : -1;  // the quad's two series pairs
+  const auto defer = [&]() {
+    if (tid == 0) {
+      const int q = atomicAdd(deferred, pb >= 0 ? 2 : 1);
+      if (q < P) deferred[1 + q] = n0;
+      if (pb >= 0 && q + 1 < P) deferred[2 + q] = n0 + 2;
+      gflags[pa] = 1;
+      if (pb >= 0) gflags[pb] = 1;
+    }
+  };
+  if (__builtin_amdgcn_readfirstlane(gflags[pa] | (pb >= 0 ? gflags[pb] : 0))) {
+    defer();
+    return;
+  }
+  for (int i = tid; i < Q_S * NMW + 4 * Q_S * D_WAVES + 4; i += blockDim.x) vmask[i] = 0u;  // vmask, stat, flag
+  if (tid < Q_S + 1) ubound[tid] = tid < Q_S ? 0x7f800000u : 0u;  // +inf per series, queue 0
+  if (tid == Q_S + 1) {
+    unsigned hp[2] = {0xffffu, 0xffffu};
+    const int npairs = (a.G + 1) / 2;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int b = (hints && n0 + r < a.N) ? a.best[n0 + r] : -1;
+      const int q = (b >= 0 && b < a.G) ? b / 2 : -1;
+      if (q >= 0 && q < npairs && (r == 0 || (unsigned)q != hp[0])) hp[r] = (unsigned)q;
+    }
+    ubound[Q_S + 1] = hp[0] | (hp[1] << 16);
+  }
+  const int head = a.head_dev ? *a.head_dev : a.head;
+  __syncthreads();
+
+  // ---- stage: one thread per (series, 8 consecutive phases), all seasons of them in flight
+  {
+    constexpr int GRP = 8;
+    const int R = a.ring_len;
+    const bool al = (R % GRP == 0) && (m % GRP == 0) && (a.ld % GRP == 0) &&
+                    ((((unsigned long long)a.hist) & 15ull) == 0);
+    const int phi = al ? (((a.pad - head) % GRP) + GRP) % GRP : 0;
+    const int ostart = phi ? phi - GRP : 0;
+    const int ngrp = (m - ostart + GRP - 1) / GRP;
+    float acc[Q_S][4];
+#pragma unroll
+    for (int r = 0; r < Q_S; ++r)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[r][u] = 0.f;
+    int bad = 0;
+    for (int g = tid; g < Q_S * ngrp; g += blockDim.x) {
+      const int r = g / ngrp, o0 = ostart + (g - r * ngrp) * GRP;
+      const int n = n0 + r;
+      const bool real = n < a.N;
+      const bf16_t* row = (const bf16_t*)a.hist + (long long)(real ? n : 0) * a.ld;
+      float y[D_MAXSEG][GRP];
+      if (al) {
+#pragma unroll
+        for (int k = 0; k < D_MAXSEG; ++k) {
+          const int t0 = k * m + o0 - a.pad;
+          int c = (head + t0) % R;
+          c += c < 0 ? R : 0;
+          uint4 wv = make_uint4(0u, 0u, 0u, 0u);
+          if (k < nseg) wv = *(const uint4*)(row + c);
+          const unsigned ww[4] = {wv.x, wv.y, wv.z, wv.w};
+#pragma unroll
+          for (int u = 0; u < GRP; ++u) {
+            const unsigned x = ww[u >> 1];
+            const float v = __uint_as_float((u & 1) ? (x & 0xffff0000u) : (x << 16));
+            const bool ok = real && k < nseg;
+            y[k][u] = ok ? (t0 + u >= 0 ? v : fm_nan()) : 0.f;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < D_MAXSEG; ++k) {
+#pragma unroll
+          for (int u = 0; u < GRP; ++u) {
+            const bool ok = real && k < nseg && o0 + u < m;
+            const int t = k * m + o0 + u - a.pad;
+            const bool pos = t >= 0;
+            int c = head + ((ok && pos) ? t : 0);
+            c -= (c >= R) ? R : 0;
+            const float v = bf16_to_f32(row[c]);
+            y[k][u] = ok ? (pos ? v : fm_nan()) : 0.f;
+          }
+        }
+      }
+      float s0 = 0.f, c0 = 0.f, s1 = 0.f, c1 = 0.f;
+#pragma unroll
+      for (int u = 0; u < GRP; ++u) {
+        const int o = o0 + u;
+        if (o >= 0 && o < m) {
+          const int jj = o / K, i = o - jj * K;
+          const bool v0 = y[0][u] == y[0][u];
+          float* blk = dl + (size_t)r * ns1 * SEA + dl_off(i, jj);
+          blk[0] = v0 ? y[1][u] - y[0][u] : y[1][u];  // + l0 for valid y0 once the means are known
+          if (v0) atomicOr(&vmask[r * NMW + (o >> 5)], 1u << (o & 31));
+#pragma unroll
+          for (int k = 1; k < D_MAXSEG - 1; ++k)
+            if (k < ns1) blk[(size_t)k * SEA] = y[k + 1][u] - y[k][u];
+#pragma unroll
+          for (int k = 1; k < D_MAXSEG; ++k)
+            if (k < nseg && y[k][u] != y[k][u]) bad = 1;
+          if (o < HALF_HB) {
+            float yl = y[1][u];
+#pragma unroll
+            for (int k = 2; k < D_MAXSEG; ++k)
+              if (k == ns1) yl = y[k][u];
+            ylast[r * HALF_HB + o] = yl;
+          }
+          const bool v1 = y[1][u] == y[1][u];
+          s0 += v0 ? y[0][u] : 0.f;
+          c0 += v0 ? 1.f : 0.f;
+          s1 += v1 ? y[1][u] : 0.f;
+          c1 += v1 ? 1.f : 0.f;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < Q_S; ++q)
+        if (q == r) { acc[q][0] += s0; acc[q][1] += c0; acc[q][2] += s1; acc[q][3] += c1; }
+    }
+    // per-wave slots summed in wave order below (deterministic, see hw_d_block)
+#pragma unroll
+    for (int q = 0; q < Q_S; ++q)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[q][u] = wave_sum(acc[q][u]);
+    if (lane == 0) {
+      float* sw = stat + 4 * Q_S * w;
+#pragma unroll
+      for (int q = 0; q < Q_S; ++q)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) sw[4 * q + u] = acc[q][u];
+    }
+    if (bad) atomicOr(flag, 1);
+  }
+  __syncthreads();
+  if (*flag) {  // block-uniform: a gap past season 0 — the 32-lane gapped kernel takes both pairs
+    defer();
+    return;
+  }
+  float l0r[Q_S], b0r[Q_S];
+#pragma unroll
+  for (int r = 0; r < Q_S; ++r) {
+    float st[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int v = 0; v < D_WAVES; ++v)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) st[u] += stat[4 * Q_S * v + 4 * r + u];
+    l0r[r] = st[1] > 0.f ? st[0] / st[1] : 0.f;
+    b0r[r] = ((st[3] > 0.f ? st[2] / st[3] : 0.f) - l0r[r]) / (float)m;
+  }
+  for (int col = tid; col < Q_S * m; col += blockDim.x) {
+    const int r = col / m, o = col - r * m;
+    if ((vmask[r * NMW + (o >> 5)] >> (o & 31)) & 1u) {
+      const int jj = o / K, i = o - jj * K;
+      dl[(size_t)r * ns1 * SEA + dl_off(i, jj)] += l0r[r];
+    }
+  }
+  __syncthreads();
+
+  const float l0 = sid == 0 ? l0r[0] : sid == 1 ? l0r[1] : sid == 2 ? l0r[2] : l0r[3];
+  const float b0 = sid == 0 ? b0r[0] : sid == 1 ? b0r[1] : sid == 2 ? b0r[2] : b0r[3];
+  const float* mydl = dl + (size_t)sid * ns1 * SEA + j * 4;
+  const int last_addr = ((lane & 48) | 15) << 2;  // bpermute source: lane 15 of the row
+  float bestSSE = __builtin_huge_valf();
+  int bestIdx = 0x7fffffff;
+  float bestL = l0, bestB = b0;
+  float* mybest = bests + (w * Q_S + sid) * HALF_HB;
+  const int nwaves = blockDim.x / FM_WAVE;
+  const int npb = (a.G + 1) / 2;
+  const unsigned hints_pp = (unsigned)__builtin_amdgcn_readfirstlane((int)ubound[Q_S + 1]);
+  for (int k = w; k < npb;) {
+    const int pi = hint_pair_at(k, 0, hints_pp);
+    const int c0 = 2 * pi;
+    const int c1i = (2 * pi + 1 < a.G) ? 2 * pi + 1 : c0;
+    const cfp tab = const_ptr(a.pair_tab + (size_t)pi * TS);
+    const v2f c1 = ldv2(tab), c2 = ldv2(tab + 2), g1a = ldv2(tab + 4);
+    const cfp W = tab + PairTab<K>::W0;
+    const cfp tb = tab + PairTab<K>::B0;
+    const v2f one = splat2(1.f), zero = splat2(0.f);
+    Mat2 Bj;
+    Mat2 Bp[4];
+    Bj.a = one; Bj.b = zero; Bj.c = zero; Bj.d = one;
+#pragma unroll
+    for (int bit = 0; bit < 4; ++bit) Bp[bit] = ldmat(tb + 8 * bit);
+    fence_sched();
+#pragma unroll
+    for (int bit = 0; bit < 4; ++bit) {
+      const Mat2 r = matmul(Bj, Bp[bit]);
+      if ((lane >> bit) & 1) Bj = r;
+    }
+    v2f D[K];
+    v2f X1 = splat2(l0 + b0), X2 = splat2(b0), sse = zero;
+    v2f p1, p2;
+    d_pass1<K>(mydl, W, D, p1, p2);
+    int alive = 1;
+    for (int sg = 1; sg < nseg - 1; ++sg) {
+      v2f x1, x2;
+      Chunk8f c0;
+      v2f w0[16];
+      d_chunk0<K>(mydl + (size_t)sg * SEA, launder(W), c0, w0);
+      row_uniform_scan_pre(Bp, p1, p2, X1, X2, Bj, x1, x2);
+      d_pass2<K, true, false, false, 16>(mydl + (size_t)sg * SEA, D, c1, c2, g1a, launder(W), x1, x2, sse, p1, p2,
+                                         tb, Bp, PRUNE, ubound + sid, &alive, &c0, w0);
+      X1 = half_last_bp(x1, last_addr);
+      X2 = half_last_bp(x2, last_addr);
+      if (PRUNE && !__any(alive)) break;
+    }
+    if (!PRUNE || __any(alive)) {
+      v2f x1, x2, d1, d2;
+      row_uniform_scan_pre(Bp, p1, p2, X1, X2, Bj, x1, x2);
+      d_pass2<K, false, false, false, 16>(mydl, D, c1, c2, g1a, W, x1, x2, sse, d1, d2);
+      X1 = half_last_bp(x1, last_addr);
+      X2 = half_last_bp(x2, last_addr);
+      sse = row_sum_last(sse);
+      sse = half_last_bp(sse, last_addr);  // lane 15 of the row -> the whole row
+      const bool upd0 = (sse.x < bestSSE || (sse.x == bestSSE && c0 < bestIdx));
+      if (upd0) { bestSSE = sse.x; bestIdx = c0; bestL = X1.x - X2.x; bestB = X2.x; }
+      const bool upd1 = (c1i != c0) && (sse.y < bestSSE || (sse.y == bestSSE && c1i < bestIdx));
+      if (upd1) { bestSSE = sse.y; bestIdx = c1i; bestL = X1.y - X2.y; bestB = X2.y; }
+      if (j == 0 && (upd0 || upd1)) {
+        const float* yl = ylast + sid * HALF_HB;
+#pragma unroll
+        for (int i = 0; i < K && i < HALF_HB; ++i)
+          if (i < hmax) mybest[i] = yl[i] - (upd1 ? D[i].y : D[i].x);
+      }
+      if (PRUNE && j == 0 && (upd0 || upd1))
+        __hip_atomic_fetch_min(ubound + sid, __float_as_uint(bestSSE), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    int q = 0;
+    if (lane == 0)
+      q = __hip_atomic_fetch_add(ubound + Q_S, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    k = nwaves + __builtin_amdgcn_readfirstlane(q);
+  }
+
+  // ---- arg-min across the 4 waves; wave r finishes series n0 + r ----------------------
+  if (j == 0) {
+    float* wb = wbest + (w * Q_S + sid) * 4;
+    wb[0] = bestSSE;
+    wb[1] = __int_as_float(bestIdx);
+    wb[2] = bestL;
+    wb[3] = bestB;
+  }
+  __syncthreads();
+  if (w >= Q_S) return;
+  const int r = w, n = n0 + r;
+  if (n >= a.N) return;
+  int win = 0;
+  for (int q = 1; q < nwaves; ++q) {
+    const float sq = wbest[(q * Q_S + r) * 4], sw = wbest[(win * Q_S + r) * 4];
+    const int iq = __float_as_int(wbest[(q * Q_S + r) * 4 + 1]), iw = __float_as_int(wbest[(win * Q_S + r) * 4 + 1]);
+    if (sq < sw || (sq == sw && iq < iw)) win = q;
+  }
+  const float* wb = wbest + (win * Q_S + r) * 4;
+  const float gSSE = wb[0], gL = wb[2], gB = wb[3];
+  const int gIdx = __float_as_int(wb[1]);
+  const float* sb = bests + (win * Q_S + r) * HALF_HB;
+  const float nvr = (float)(ns1 * m);  // fast path: every sample past season 0 is valid
+  const float sig = sqrtf(gSSE / fmaxf(nvr, 1.f));
+  if (lane == 0) {
+    a.level[n] = gL;
+    a.trend[n] = gB;
+    a.sigma[n] = sig;
+    a.best[n] = gIdx;
+  }
+  const int Tp = a.Tp;
+  if (a.season_hb && lane < hmax) a.season_hb[(long long)n * HALF_HB + lane] = sb[lane];
+  if (a.nvalid_out && lane == 0) a.nvalid_out[n] = nvr;
+  detect_epilogue_wave(a.det, n, sig, nvr, [&](int h) {
+    int ph = (Tp - 1 + h) % m;
+    if (ph < 0) ph += m;
+    ph = ph < HALF_HB ? ph : HALF_HB - 1;
+    return gL + (float)h * gB + sb[ph];
+  }, gIdx);
+}
+
+template <int K, bool PRUNE>
+__global__ __launch_bounds__(256, 2) void hw_q_kernel(const SmoothArgs a, int hmax, int* deferred, int hints) {
+  hw_q_block<K, PRUNE>(a, hmax, 4 * blockIdx.x, deferred, hints);
 }
 
 // ---- variant 5, gapped series: hw_dg_kernel ------------------------------------------------
@@ -1987,6 +2336,56 @@ extern "C" size_t fm_hw_d_lds_bytes(int Tp, int seg, int K) {
 
 // hw_dg_block: the hw_d_block layout + per-(series, season, lane) 64-bit miss masks, per
 // (series, season) gap flags and the two valid-point counts
+// hw_q_kernel: seasons m = 16 K (K = 18: the 300 s step)
+static bool q_supported_k(int K) { return K == 18; }
+
+extern "C" size_t fm_hw_q_lds_bytes(int Tp, int seg, int K) {
+  if (!q_supported_k(K) || seg != 16 * K) return (size_t)-1;
+  const int nseg = Tp / seg;
+  if (nseg < 2 || nseg > D_MAXSEG) return (size_t)-1;
+  const int NMW = (16 * K + 31) / 32;
+  const int season = D_CHUNK * ((K + 7) / 8);
+  return ((size_t)Q_S * (nseg - 1) * season + Q_S * NMW + 4 * Q_S * D_WAVES + 4 + Q_S * HALF_HB +
+          4 * Q_S * HALF_HB + 4 * Q_S * 4 + 8) * 4;
+}
+
+// Variant 5 at m = 16 K: hw_q_kernel over quads, then the gapped kernel at K / 2 (32 lanes x
+// K / 2 steps) over the pairs it deferred, with `tab_g` = pair_table(grid, K / 2) (the
+// 32-lane kernel's weights and powers).  Same workspace and contract as fm_hw_d_fit.
+extern "C" int fm_hw_q_fit(const SmoothArgs* a, const float* tab_g, int hmax, int* deferred, hipStream_t st) {
+  const int K = a->K;
+  if (!q_supported_k(K) || a->seg != 16 * K || a->m != a->seg || a->Tp % a->seg != 0 || a->Tp / a->seg < 2 ||
+      a->Tp / a->seg > D_MAXSEG || !a->pair_tab || !tab_g || a->season_out || hmax < 1 || hmax > K ||
+      hmax > HALF_HB)
+    return (int)hipErrorNotSupported;
+  if (a->N <= 0) return 0;
+  const size_t lds = fm_hw_q_lds_bytes(a->Tp, a->seg, K);
+  const size_t dlds = fm_hw_dg_lds_bytes(a->Tp, a->seg, K / 2);
+  if (lds > 80 * 1024 || dlds > 80 * 1024) return (int)hipErrorNotSupported;
+  if (!deferred) return (int)hipErrorInvalidValue;
+  const char* pe = getenv("FOREMAST_HW_PRUNE");
+  const bool prune = !(pe && pe[0] == '0');
+  const char* he = getenv("FOREMAST_HW_HINTS");
+  const int hints = (prune && !(he && he[0] == '0')) ? 1 : 0;
+  const int quads = (a->N + 3) / 4;
+  if (prune)
+    hipLaunchKernelGGL((hw_q_kernel<18, true>), dim3(quads), dim3(256), lds, st, *a, hmax, deferred, hints);
+  else
+    hipLaunchKernelGGL((hw_q_kernel<18, false>), dim3(quads), dim3(256), lds, st, *a, hmax, deferred, hints);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  SmoothArgs ag = *a;
+  ag.pair_tab = tab_g;
+  ag.K = K / 2;
+  const int pairs = (a->N + 1) / 2;
+  const int grid = pairs < 512 ? pairs : 512;
+  if (prune)
+    hipLaunchKernelGGL((hw_dg_kernel<9, true>), dim3(grid), dim3(256), dlds, st, ag, hmax, deferred, hints);
+  else
+    hipLaunchKernelGGL((hw_dg_kernel<9, false>), dim3(grid), dim3(256), dlds, st, ag, hmax, deferred, hints);
+  return (int)hipGetLastError();
+}
+
 extern "C" size_t fm_hw_dg_lds_bytes(int Tp, int seg, int K) {
   const size_t base = fm_hw_d_lds_bytes(Tp, seg, K);
   if (base == (size_t)-1) return base;

@@ -236,6 +236,7 @@ def _hist_check(hist: torch.Tensor, head: int, length: int) -> None:
 
 UNIFORM_K = (8, 12, 16, 24, 32)
 HALF_K = (45, 9)      # variants 4 / 5 (two series per wave): season = 32 * K (variant 4: K = 45 only)
+QUAD_K = (18,)        # variant 5, four series per wave (hw_q_kernel): season = 16 * K (288: the 300 s step)
 HALF_HB = 16          # seasonal phases kept per series by variant 4 (max forecast horizon)
 last_hw_variant: Optional[int] = None  # variant actually launched by the last smoothing_fit (tests/bench)
 DEFAULT_HW_VARIANT = 5
@@ -376,6 +377,12 @@ def smoothing_fit(hist: torch.Tensor, head: int, length: int, mode: int, m: int,
         return _es_seq_fit(lib, hist, head, length, mode, grid, det, out, head_dev=head_dev, defer=defer_detect)
     if variant in (4, 5):
         hmax = det.max_horizon
+        if (variant == 5 and mode == MODE_HW and bf16 and mm % 16 == 0 and mm // 16 in QUAD_K
+                and not want_season and K is None and hmax is not None and 1 <= hmax <= min(mm // 16, HALF_HB)
+                and os.environ.get("FOREMAST_HW_QUAD", "1") != "0"
+                and lib.fm_hw_q_lds_bytes(Tp, mm, mm // 16) <= D_LDS_LIMIT):
+            return _hw_half_fit(lib, hist, head, length, mm, grid, det, Tp, pad, hmax, out, residual=True,
+                                head_dev=head_dev, defer=defer_detect, quad=True)
         if (mode == MODE_HW and bf16 and mm % 32 == 0 and mm // 32 in HALF_K and not want_season
                 and hmax is not None and 1 <= hmax <= min(mm // 32, HALF_HB) and K is None):
             if variant == 5 and lib.fm_hw_d_lds_bytes(Tp, mm, mm // 32) <= D_LDS_LIMIT:
@@ -508,7 +515,7 @@ def _split_workspace(dev) -> tuple:
 
 
 def _hw_half_fit(lib, hist, head, length, m, grid, det, Tp, pad, hmax, out, residual: bool = False,
-                 head_dev: Optional[torch.Tensor] = None, defer: bool = False):
+                 head_dev: Optional[torch.Tensor] = None, defer: bool = False, quad: bool = False):
     """Variants 4/5 of the Holt-Winters fit: two series per wave, season = 32
     lanes x K steps.  Variant 4 (hw_scan.hip ``hw_half_kernel``) walks the
     seasonal state over a bf16 image; variant 5 (``residual``, ``hw_d_kernel``)
@@ -517,7 +524,7 @@ def _hw_half_fit(lib, hist, head, length, m, grid, det, Tp, pad, hmax, out, resi
     kernel in both."""
     dev = hist.device
     N = hist.shape[0]
-    k = m // 32
+    k = m // 16 if quad else m // 32
     out = {} if out is None else out
     f32 = dict(dtype=torch.float32, device=dev)
     for kname in ("level", "trend", "sigma"):
@@ -561,6 +568,14 @@ def _hw_half_fit(lib, hist, head, length, m, grid, det, Tp, pad, hmax, out, resi
     ws = _half_workspace(dev, N)
     global last_hw_variant, last_detect_deferred
     last_detect_deferred = defer
+    if quad:
+        # four series per wave at K = m / 16; gapped pairs go to the 32-lane kernel at m / 32
+        rc = lib.fm_hw_q_fit(a, nat.ptr(pair_table(grid, m // 32)), int(hmax), nat.ptr(ws), nat.stream_handle(dev))
+        if rc != 0:
+            ws.zero_()
+        nat.check(rc, "fm_hw_q_fit")
+        last_hw_variant = 5
+        return out
     if residual:
         sws, slots = _split_workspace(dev)
         if os.environ.get("FOREMAST_HW_SPLIT", "1") == "0":

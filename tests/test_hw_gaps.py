@@ -212,3 +212,47 @@ def test_variant5_at_the_300s_step_matches_reference(K, case, monkeypatch):
     np.testing.assert_allclose(out["forecast"].cpu().numpy()[same], f_ref.numpy()[same], rtol=5e-3, atol=2e-2)
     d = _ref_detect(out, GRID, sm_ref.MODE_HW, m, hz, cur)
     assert torch.equal(d.verdict, out["verdict"].cpu())
+
+
+@pytest.mark.parametrize("case", ["dense", "outage"])
+def test_quad_kernel_matches_pair_kernel_at_300s(K, case, monkeypatch):
+    """At m = 288 variant 5 walks four series per wave (hw_q_kernel, 16 lanes x 18 steps);
+    FOREMAST_HW_QUAD=0 runs the 32-lane K = 9 kernel.  Same fits up to the summation order
+    of the SSE (row vs half sums): the same grid point almost everywhere, sigma to float
+    rounding.  The outage case defers gapped quads to the 32-lane gapped kernel.  N = 23
+    leaves a partial quad (padding series)."""
+    dev = torch.device("cuda:0")
+    m, N = 288, 23
+    T = 7 * m
+    y = _series(N, T, m, seed=43)
+    if case == "outage":
+        y[::4, 2 * m + 100:2 * m + 106] = np.nan
+    ring = torch.tensor(y, device=dev).to(torch.bfloat16)
+    C = 10
+    spec = K.DetectSpec(horizons=torch.arange(1, C + 1, dtype=torch.int32, device=dev),
+                        threshold=torch.full((N,), 2.0, device=dev),
+                        bound=torch.full((N,), 3, dtype=torch.int8, device=dev),
+                        min_lower=torch.full((N,), -1e30, device=dev),
+                        cur=torch.tensor(np.nan_to_num(y[:, -C:], nan=20.0) * 1.05, device=dev), max_horizon=C)
+    K.hw_clear_gap_flags()
+    outs = []
+    for quad in ("1", "0"):
+        monkeypatch.setenv("FOREMAST_HW_QUAD", quad)
+        if quad == "0":
+            # the 32-lane kernel takes horizons <= K = 9 only
+            spec = K.DetectSpec(horizons=torch.arange(1, 10, dtype=torch.int32, device=dev),
+                                threshold=spec.threshold, bound=spec.bound, min_lower=spec.min_lower,
+                                cur=spec.cur[:, :9].contiguous(), max_horizon=9)
+        o = K.smoothing_fit(ring, 0, T, sm_ref.MODE_HW, m, GRID.to(dev), spec, variant=5)
+        torch.cuda.synchronize()
+        assert K.last_hw_variant == 5
+        outs.append({k: v.clone() for k, v in o.items()})
+    assert (outs[0]["best"] == outs[1]["best"]).float().mean() >= 0.95
+    same = (outs[0]["best"] == outs[1]["best"]).cpu().numpy()
+    np.testing.assert_allclose(outs[0]["sigma"].cpu().numpy(), outs[1]["sigma"].cpu().numpy(), rtol=1e-3)
+    np.testing.assert_allclose(outs[0]["level"].cpu().numpy()[same], outs[1]["level"].cpu().numpy()[same],
+                               rtol=1e-4, atol=1e-3)
+    # and against the fp64 reference
+    ref = sm_ref.fit_smoothing(torch.tensor(ring.float().cpu().numpy(), dtype=torch.float64), sm_ref.MODE_HW,
+                               GRID.double(), m=m)
+    np.testing.assert_allclose(outs[0]["sigma"].cpu().numpy(), ref.sigma.numpy(), rtol=5e-3)
