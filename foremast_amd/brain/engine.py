@@ -252,11 +252,12 @@ class StreamingShard:
     def graph_ready(self) -> bool:
         """The steady state a captured tick assumes: GPU, full ring (head
         advances by one per tick), warm window (every tick graduates), the
-        two-series-per-wave Holt-Winters path, no anomaly list."""
+        Holt-Winters paths that read the ring head from the device (variants 4 / 5, and 6
+        at the short seasons), no anomaly list."""
         return (self.gpu and self.mode == sm_ref.MODE_HW and self.refit_every == 1
                 and self.hist.length == self.hist.R
                 and self.cur.ticks >= self.cur.W and self.anomalies is None
-                and getattr(self, "_hw_variant", None) in (4, 5) and bool(self.out))
+                and getattr(self, "_hw_variant", None) in (4, 5, 6) and bool(self.out))
 
     def tick_graph(self, newv: torch.Tensor, newb: Optional[torch.Tensor] = None,
                    post=None) -> Dict[str, torch.Tensor]:

@@ -113,6 +113,12 @@ def _declare(lib: C.CDLL) -> None:
     lib.fm_es_seq_fit.restype = I
     lib.fm_es_seq_tpc.argtypes = [I]
     lib.fm_es_seq_tpc.restype = I
+    lib.fm_hw_seq_fit.argtypes = [C.POINTER(SmoothArgs), I, P]
+    lib.fm_hw_seq_fit.restype = I
+    lib.fm_hw_seq_lds_bytes.argtypes = [I, I, I]
+    lib.fm_hw_seq_lds_bytes.restype = C.c_size_t
+    lib.fm_hw_seq_tpc.argtypes = [I, I]
+    lib.fm_hw_seq_tpc.restype = I
     lib.fm_hw_detect_params.argtypes = [C.POINTER(SmoothArgs), P]
     lib.fm_hw_detect_params.restype = I
     lib.fm_rank_tests.argtypes = [C.POINTER(RankArgs), P]

@@ -237,6 +237,9 @@ def _hist_check(hist: torch.Tensor, head: int, length: int) -> None:
 UNIFORM_K = (8, 12, 16, 24, 32)
 HALF_K = (45, 9)      # variants 4 / 5 (two series per wave): season = 32 * K (variant 4: K = 45 only)
 QUAD_K = (18,)        # variant 5, four series per wave (hw_q_kernel): season = 16 * K (288: the 300 s step)
+# variant 6 (hw_seq.hip): sequential fit with the season in registers, one (series, grid pair)
+# per thread, at the short daily seasons of the 3600 / 1800 / 1200 / 900 / 600 s steps
+SEQ_M = (24, 48, 72, 96, 144)
 HALF_HB = 16          # seasonal phases kept per series by variant 4 (max forecast horizon)
 last_hw_variant: Optional[int] = None  # variant actually launched by the last smoothing_fit (tests/bench)
 DEFAULT_HW_VARIANT = 5
@@ -375,6 +378,12 @@ def smoothing_fit(hist: torch.Tensor, head: int, length: int, mode: int, m: int,
         variant = int(os.environ.get("FOREMAST_HW_VARIANT", str(DEFAULT_HW_VARIANT)))
     if mode in (MODE_ES, MODE_DES) and variant in (4, 5) and K is None and G <= 64:
         return _es_seq_fit(lib, hist, head, length, mode, grid, det, out, head_dev=head_dev, defer=defer_detect)
+    if (mode == MODE_HW and variant in (4, 5) and mm in SEQ_M and K is None and G <= 64
+            and os.environ.get("FOREMAST_HW_SEQ", "1") != "0"
+            and (det.horizons.shape[-1] == 0 or (det.max_horizon is not None and 1 <= det.max_horizon <= HALF_HB))
+            and lib.fm_hw_seq_lds_bytes(Tp, mm, G) <= LDS_LIMIT):
+        return _hw_seq_fit(lib, hist, head, length, mm, grid, det, Tp, pad, out, want_season,
+                           head_dev=head_dev, defer=defer_detect, detect_after=detect_after)
     if variant in (4, 5):
         hmax = det.max_horizon
         if (variant == 5 and mode == MODE_HW and bf16 and mm % 16 == 0 and mm // 16 in QUAD_K
@@ -592,6 +601,61 @@ def _hw_half_fit(lib, hist, head, length, m, grid, det, Tp, pad, hmax, out, resi
         ws.zero_()
     nat.check(rc, "fm_hw_half_fit")
     last_hw_variant = 4
+    return out
+
+
+def _hw_seq_fit(lib, hist, head, length, m, grid, det, Tp, pad, out, want_season: bool,
+                head_dev: Optional[torch.Tensor] = None, defer: bool = False, detect_after=None):
+    """Variant 6 of the Holt-Winters fit (csrc/hw_seq.hip): short daily seasons (``SEQ_M``),
+    one (series, pair of grid points) per thread walking its series from LDS with the m
+    seasonal terms in registers; gaps through keep factors on the same path.  The band /
+    verdict epilogue is fm_hw_detect_params (inline, or deferred like variants 4 / 5)."""
+    dev = hist.device
+    N = hist.shape[0]
+    out = {} if out is None else out
+    f32 = dict(dtype=torch.float32, device=dev)
+    for kname in ("level", "trend", "sigma", "nvalid"):
+        if kname not in out:
+            out[kname] = torch.empty(N, **f32)
+    if "best" not in out:
+        out["best"] = torch.empty(N, dtype=torch.int32, device=dev)
+    if "season_hb" not in out:
+        out["season_hb"] = torch.empty((N, HALF_HB), **f32)
+    if want_season and "season" not in out:
+        out["season"] = torch.empty((N, m), **f32)
+    if not defer and detect_after is not None:
+        torch.cuda.current_stream(dev).wait_stream(detect_after)  # the inline epilogue reads det.differs
+    a = nat.SmoothArgs()
+    a.hist = nat.ptr(hist)
+    a.ld = hist.stride(0)
+    a.ring_len = hist.shape[1]
+    a.head = int(head)
+    a.T = int(length)
+    a.Tp = int(Tp)
+    a.pad = int(pad)
+    a.m = int(m)
+    a.K = 1
+    a.seg = int(m)
+    a.grid = nat.ptr(grid)
+    a.G = grid.shape[0]
+    a.N = N
+    a.level, a.trend, a.sigma = nat.ptr(out["level"]), nat.ptr(out["trend"]), nat.ptr(out["sigma"])
+    a.best = nat.ptr(out["best"])
+    a.season_out = nat.ptr(out["season"]) if want_season else 0
+    a.nvalid_out = nat.ptr(out["nvalid"])
+    a.season_hb = nat.ptr(out["season_hb"])
+    if head_dev is not None:
+        _need(head_dev.dtype == torch.int32 and head_dev.device == dev and head_dev.numel() >= 1,
+              "head_dev must be an int32 device scalar")
+        a.head_dev = nat.ptr(head_dev)
+    _fill_detect(a.det, det, N, dev, out)
+    _set_hvar(a.det, det, grid, MODE_HW, m)
+    if defer:
+        a.det.C = 0
+    global last_hw_variant, last_detect_deferred
+    nat.check(lib.fm_hw_seq_fit(a, int(hist.dtype == torch.bfloat16), nat.stream_handle(dev)), "fm_hw_seq_fit")
+    last_hw_variant = 6
+    last_detect_deferred = defer
     return out
 
 

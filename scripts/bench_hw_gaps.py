@@ -2,7 +2,9 @@
 """Holt-Winters variant-5 fit on gapped inputs (the masked-season kernel, hw_dg_kernel):
 kernel time per 100k x 10,080 x 64 fit for dense series, a 30-minute outage in a fraction
 of the series, isolated scrape misses at a rate, and (FOREMAST_HW_DG_ALL=1 rows) every pair
-through the gapped kernel.  One JSON line per case; interleaved rounds."""
+through the gapped kernel.  At the short seasons of variant 6 (hw_seq.hip, e.g. --season 72:
+the 1200 s step) the ``v3dense`` / ``v3miss1e-3`` cases run the time-parallel variant 3 on the
+same data (FOREMAST_HW_SEQ=0).  One JSON line per case; interleaved rounds."""
 
 from __future__ import annotations
 
@@ -35,7 +37,7 @@ def main():
     base = synthetic_history(N, R, m, dev, seed=3).to(torch.bfloat16)
     grid = sm.make_grid(sm.MODE_HW, (0.1, 0.3, 0.5, 0.8), (0.0, 0.01, 0.05, 0.1), (0.05, 0.1, 0.3, 0.5)).to(dev)
     cur = base[:, -C:].float().contiguous()
-    hz = min(10, m // 32)
+    hz = 10 if m in K.SEQ_M else min(10, m // 32)
     spec = K.DetectSpec(horizons=torch.arange(1, hz + 1, dtype=torch.int32, device=dev).repeat(C // hz + 1)[:C],
                         max_horizon=hz,
                         threshold=torch.full((N,), 3.0, device=dev), bound=torch.full((N,), 3, dtype=torch.int8, device=dev),
@@ -44,21 +46,25 @@ def main():
     hists = {}
     for case in args.cases.split(","):
         h = base.clone()
-        if case.startswith("gap"):
-            frac = int(case[3:]) / 100
+        kind = case[2:] if case.startswith("v3") else case
+        if kind.startswith("gap"):
+            frac = int(kind[3:]) / 100
             rows = torch.randperm(N, device=dev, generator=g)[: int(frac * N)]
             starts = torch.randint(m, R - 30, (rows.numel(),), device=dev, generator=g)
             cols = starts[:, None] + torch.arange(30, device=dev)[None, :]
             h[rows[:, None].expand(-1, 30), cols] = float("nan")
-        elif case.startswith("miss"):
-            rate = float(case[4:])
+        elif kind.startswith("miss"):
+            rate = float(kind[4:])
             h[torch.rand(h.shape, device=dev, generator=g) < rate] = float("nan")
         hists[case] = h
     res = {c: [] for c in hists}
-    out = {}
+    variant = {}
+    outs = {}
     for _ in range(args.rounds):
         for case, h in hists.items():
             os.environ["FOREMAST_HW_DG_ALL"] = "1" if case == "dgall" else "0"
+            os.environ["FOREMAST_HW_SEQ"] = "0" if case.startswith("v3") else "1"
+            out = outs.setdefault(case.startswith("v3"), {})
             for _w in range(2):
                 K.smoothing_fit(h, 0, R, sm.MODE_HW, m, grid, spec, variant=5, out=out)
             torch.cuda.synchronize()
@@ -71,11 +77,13 @@ def main():
                 torch.cuda.synchronize()
                 ts.append((time.perf_counter() - t) * 1e3)
             res[case].append((sorted(ts)[2], (K.hw_deferred_total(dev) - d0) / 5))
+            variant[case] = K.last_hw_variant
     os.environ["FOREMAST_HW_DG_ALL"] = "0"
+    os.environ["FOREMAST_HW_SEQ"] = "1"
     dense = sorted(x[0] for x in res.get("dense", [(float("nan"), 0)]))
     for case, xs in res.items():
         ms = sorted(x[0] for x in xs)
-        rec = {"case": case, "season": m, "points": R, "ms_median": round(ms[len(ms) // 2], 3),
+        rec = {"case": case, "season": m, "variant": variant[case], "points": R, "ms_median": round(ms[len(ms) // 2], 3),
                "ns_per_point": round(ms[len(ms) // 2] * 1e6 / (N * R), 4), "ms_all": [round(x, 3) for x in ms],
                "gapped_pairs_per_fit": xs[-1][1], "pairs": (N + 1) // 2,
                "vs_dense": round(ms[len(ms) // 2] / dense[len(dense) // 2], 3) if "dense" in res else None}
