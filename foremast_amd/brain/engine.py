@@ -285,6 +285,22 @@ class StreamingShard:
             out["post_in_graph"] = False
             return out
         io = (newv.data_ptr(), None if newb is None else newb.data_ptr())
+        hit = self._graphs.get(io)
+        if hit is not None and self._state_synced and self._h_slots is not None:
+            # steady state: the replay goes first and the host mirror of the ring bookkeeping
+            # (nothing the replay reads) follows it, off the path from the previous tick's
+            # completion to this tick's first kernel
+            self._graph, self._post_in_graph, outs = hit
+            self._graph.replay()
+            self.hist.advance(1)
+            self.cur.ticks += 1
+            self._new_pts += 1
+            self.horizons = self._h_buf
+            self.out = dict(outs)
+            self._stats_zeroed = False
+            self.last_refit = True
+            self.out["post_in_graph"] = self._post_in_graph
+            return self.out
         if io not in self._graphs and len(self._graphs) >= 2:
             raise ValueError("tick_graph takes at most two sets of newv/newb buffers (double-buffered input)")
         W, R = self.cur.W, self.hist.R
