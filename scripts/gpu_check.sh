@@ -24,6 +24,8 @@ for s in $STEPS; do
     bench0) run bench_frac0 600 python bench.py --steps 20 --warmup 5 --anomaly-frac 0 ;;
     benchshift) run bench_shift 600 python bench.py --steps 20 --warmup 5 --anomaly-kind shift3sigma ;;
     hw10k) run bench_hw10k 600 python bench.py --config hw10k --steps 20 --warmup 5 ;;
+    hw10k100) run bench_hw10k100 600 python bench.py --config hw10k --steps 100 --warmup 10 ;;
+    b12k) run bench_12k5 600 python bench.py --series 12500 --steps 100 --warmup 10 ;;
     graph) run bench_graph 600 python bench.py --steps 20 --warmup 5 --graph ;;
     kbench) run kbench 600 python scripts/bench_kernels.py ;;
     lstm) run bench_lstm 600 python bench.py --config lstm --steps 20 --warmup 5 ;;
