@@ -88,7 +88,7 @@ template <typename TIN> __device__ __forceinline__ float ld_elem(const TIN* p) {
 // and exit before the walk (a series' TPC threads are whole lane groups, so the shuffles of
 // the remaining series never read an exited lane).
 template <int M, int GPT, int TPC, typename TIN>
-__global__ __launch_bounds__(256, 2) void hw_seq_kernel(const SmoothArgs a) {
+__global__ __launch_bounds__(256, M > 144 ? 1 : 2) void hw_seq_kernel(const SmoothArgs a) {
   using V = typename SeqVec<GPT>::type;
   constexpr int SW = 256 / TPC;
   static_assert(M % 4 == 0, "16-byte LDS reads of four steps");
@@ -208,7 +208,11 @@ __global__ __launch_bounds__(256, 2) void hw_seq_kernel(const SmoothArgs a) {
 }
 
 // grid points per thread at season M: two (packed) while 2 M VGPRs of season fit beside
-// the walk's ~30, else one
+// the walk's ~30, else one.  M = 288 (opt-in, kernels.py FOREMAST_HW_SEQ288=1): one grid
+// point per thread at one wave per SIMD, 133 of the season's registers in AGPRs; its cost
+// does not depend on gaps (5.89 ms per 100k x 2016 x 64 dense or at 1e-3 misses), so it
+// beats variant 5 (2.59 dense, 4.78 with 20 % outages, 7.71 at 1e-3 misses) only when most
+// series pairs are gapped (profiles/hw_r6/seq/fit_k288_quad_vs_seq.jsonl)
 constexpr int seq_gpt(int M) { return M <= 96 ? 2 : 1; }
 
 int seq_tpc(int M, int G) {
@@ -218,7 +222,7 @@ int seq_tpc(int M, int G) {
   return t;
 }
 
-bool seq_supported_m(int M) { return M == 24 || M == 48 || M == 72 || M == 96 || M == 144; }
+bool seq_supported_m(int M) { return M == 24 || M == 48 || M == 72 || M == 96 || M == 144 || M == 288; }
 
 template <int M, typename TIN>
 hipError_t launch_seq(const SmoothArgs& a, int tpc, size_t lds, hipStream_t st) {
@@ -242,7 +246,8 @@ hipError_t launch_seq_m(const SmoothArgs& a, int tpc, size_t lds, hipStream_t st
     case 48: return launch_seq<48, TIN>(a, tpc, lds, st);
     case 72: return launch_seq<72, TIN>(a, tpc, lds, st);
     case 96: return launch_seq<96, TIN>(a, tpc, lds, st);
-    default: return launch_seq<144, TIN>(a, tpc, lds, st);
+    case 144: return launch_seq<144, TIN>(a, tpc, lds, st);
+    default: return launch_seq<288, TIN>(a, tpc, lds, st);
   }
 }
 

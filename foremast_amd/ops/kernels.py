@@ -238,7 +238,9 @@ UNIFORM_K = (8, 12, 16, 24, 32)
 HALF_K = (45, 9)      # variants 4 / 5 (two series per wave): season = 32 * K (variant 4: K = 45 only)
 QUAD_K = (18,)        # variant 5, four series per wave (hw_q_kernel): season = 16 * K (288: the 300 s step)
 # variant 6 (hw_seq.hip): sequential fit with the season in registers, one (series, grid pair)
-# per thread, at the short daily seasons of the 3600 / 1800 / 1200 / 900 / 600 s steps
+# per thread, at the short daily seasons of the 3600 / 1800 / 1200 / 900 / 600 s steps; at the
+# 300 s step (m = 288) only with FOREMAST_HW_SEQ288=1 (gap-independent cost: faster than variant 5
+# once most series pairs are gapped, slower on dense data)
 SEQ_M = (24, 48, 72, 96, 144)
 HALF_HB = 16          # seasonal phases kept per series by variant 4 (max forecast horizon)
 last_hw_variant: Optional[int] = None  # variant actually launched by the last smoothing_fit (tests/bench)
@@ -378,7 +380,8 @@ def smoothing_fit(hist: torch.Tensor, head: int, length: int, mode: int, m: int,
         variant = int(os.environ.get("FOREMAST_HW_VARIANT", str(DEFAULT_HW_VARIANT)))
     if mode in (MODE_ES, MODE_DES) and variant in (4, 5) and K is None and G <= 64:
         return _es_seq_fit(lib, hist, head, length, mode, grid, det, out, head_dev=head_dev, defer=defer_detect)
-    if (mode == MODE_HW and variant in (4, 5) and mm in SEQ_M and K is None and G <= 64
+    if (mode == MODE_HW and variant in (4, 5) and K is None and G <= 64
+            and (mm in SEQ_M or (mm == 288 and os.environ.get("FOREMAST_HW_SEQ288", "0") == "1"))
             and os.environ.get("FOREMAST_HW_SEQ", "1") != "0"
             and (det.horizons.shape[-1] == 0 or (det.max_horizon is not None and 1 <= det.max_horizon <= HALF_HB))
             and lib.fm_hw_seq_lds_bytes(Tp, mm, G) <= LDS_LIMIT):

@@ -169,3 +169,21 @@ def test_seq_season_output_and_variant3_agree(K, monkeypatch):
     assert K.last_hw_variant == 3
     assert (v3["best"] == out["best"]).float().mean() >= 0.9
     np.testing.assert_allclose(v3["sigma"].cpu().numpy(), out["sigma"].cpu().numpy(), rtol=2e-3)
+
+
+@pytest.mark.parametrize("case", ["dense", "miss", "outage"])
+def test_seq_at_the_300s_step_matches_reference(K, case, monkeypatch):
+    """Variant 6 at m = 288 (FOREMAST_HW_SEQ288=1): one grid point per thread, the 288 season
+    registers partly in AGPRs (one wave per SIMD)."""
+    monkeypatch.setenv("FOREMAST_HW_SEQ288", "1")
+    dev = torch.device("cuda:0")
+    m, N = 288, 9
+    T = 7 * m
+    y = _gapped(case, N, T, m, seed=288)
+    ring = torch.tensor(y, device=dev).to(torch.bfloat16)
+    yl = ring.float().cpu().numpy()
+    spec, hz, cur = _spec(K, N, 10, dev, y)
+    out = K.smoothing_fit(ring, 0, T, sm_ref.MODE_HW, m, GRID.to(dev), spec)
+    torch.cuda.synchronize()
+    assert K.last_hw_variant == 6
+    _check(K, out, yl, m, hz, cur)

@@ -60,10 +60,10 @@ def test_hw_seq_geometry(lib):
     nat.load()  # argtypes / restype
     assert lib.fm_hw_seq_tpc(72, 64) == 32 and lib.fm_hw_seq_tpc(72, 16) == 16 and lib.fm_hw_seq_tpc(72, 33) == 32
     assert lib.fm_hw_seq_tpc(144, 64) == 64 and lib.fm_hw_seq_tpc(144, 5) == 32
-    assert lib.fm_hw_seq_tpc(72, 65) == 0 and lib.fm_hw_seq_tpc(288, 64) == 0 and lib.fm_hw_seq_tpc(70, 8) == 0
+    assert lib.fm_hw_seq_tpc(72, 65) == 0 and lib.fm_hw_seq_tpc(1440, 64) == 0 and lib.fm_hw_seq_tpc(70, 8) == 0
     assert lib.fm_hw_seq_lds_bytes(504, 72, 64) == (2 * 8 * (504 + 4) + 8) * 4
     assert lib.fm_hw_seq_lds_bytes(504, 72, 16) == (2 * 16 * (504 + 4) + 16) * 4
     none = C.c_size_t(-1).value
     assert lib.fm_hw_seq_lds_bytes(500, 72, 64) == none       # not a whole number of seasons
     assert lib.fm_hw_seq_lds_bytes(72, 72, 64) == none        # one season: nothing to fit
-    assert lib.fm_hw_seq_lds_bytes(2016, 288, 64) == none     # m = 288 is variant 5's
+    assert lib.fm_hw_seq_lds_bytes(2016, 288, 64) == (2 * 4 * (2016 + 4) + 4) * 4  # one grid point per thread
