@@ -31,6 +31,8 @@
 #include "common.h"
 #include "args.h"
 
+#include <cstdlib>
+
 extern __shared__ __attribute__((aligned(16))) char fm_hws_smem[];
 
 extern "C" int fm_hw_detect_params(const SmoothArgs* a, hipStream_t st);
@@ -88,7 +90,7 @@ template <typename TIN> __device__ __forceinline__ float ld_elem(const TIN* p) {
 // and exit before the walk (a series' TPC threads are whole lane groups, so the shuffles of
 // the remaining series never read an exited lane).
 template <int M, int GPT, int TPC, typename TIN>
-__global__ __launch_bounds__(256, M > 144 ? 1 : 2) void hw_seq_kernel(const SmoothArgs a) {
+__global__ __launch_bounds__(256, (M > 144 || (M > 96 && GPT == 2)) ? 1 : 2) void hw_seq_kernel(const SmoothArgs a) {
   using V = typename SeqVec<GPT>::type;
   constexpr int SW = 256 / TPC;
   static_assert(M % 4 == 0, "16-byte LDS reads of four steps");
@@ -213,10 +215,19 @@ __global__ __launch_bounds__(256, M > 144 ? 1 : 2) void hw_seq_kernel(const Smoo
 // does not depend on gaps (5.89 ms per 100k x 2016 x 64 dense or at 1e-3 misses), so it
 // beats variant 5 (2.59 dense, 4.78 with 20 % outages, 7.71 at 1e-3 misses) only when most
 // series pairs are gapped (profiles/hw_r6/seq/fit_k288_quad_vs_seq.jsonl)
-constexpr int seq_gpt(int M) { return M <= 96 ? 2 : 1; }
+// (A/B: FOREMAST_HW_SEQ_GPT144=2 runs m = 144 with two grid points per thread at one wave
+// per SIMD, part of the 288 season registers in AGPRs)
+int seq_gpt(int M) {
+  if (M <= 96) return 2;
+  if (M == 144) {
+    const char* e = getenv("FOREMAST_HW_SEQ_GPT144");
+    return (e && e[0] == '2') ? 2 : 1;
+  }
+  return 1;
+}
 
 int seq_tpc(int M, int G) {
-  const int gpt = M <= 96 ? 2 : 1;
+  const int gpt = seq_gpt(M);
   int t = gpt == 2 ? 16 : 32;  // instantiated: 16 / 32 (two per thread), 32 / 64 (one)
   while (t * gpt < G) t *= 2;
   return t;
@@ -224,9 +235,8 @@ int seq_tpc(int M, int G) {
 
 bool seq_supported_m(int M) { return M == 24 || M == 48 || M == 72 || M == 96 || M == 144 || M == 288; }
 
-template <int M, typename TIN>
+template <int M, int GPT, typename TIN>
 hipError_t launch_seq(const SmoothArgs& a, int tpc, size_t lds, hipStream_t st) {
-  constexpr int GPT = seq_gpt(M);
   const int sw = 256 / tpc;
   const dim3 grid((a.N + sw - 1) / sw), block(256);
   if constexpr (GPT == 2) {
@@ -242,12 +252,13 @@ hipError_t launch_seq(const SmoothArgs& a, int tpc, size_t lds, hipStream_t st) 
 template <typename TIN>
 hipError_t launch_seq_m(const SmoothArgs& a, int tpc, size_t lds, hipStream_t st) {
   switch (a.m) {
-    case 24: return launch_seq<24, TIN>(a, tpc, lds, st);
-    case 48: return launch_seq<48, TIN>(a, tpc, lds, st);
-    case 72: return launch_seq<72, TIN>(a, tpc, lds, st);
-    case 96: return launch_seq<96, TIN>(a, tpc, lds, st);
-    case 144: return launch_seq<144, TIN>(a, tpc, lds, st);
-    default: return launch_seq<288, TIN>(a, tpc, lds, st);
+    case 24: return launch_seq<24, 2, TIN>(a, tpc, lds, st);
+    case 48: return launch_seq<48, 2, TIN>(a, tpc, lds, st);
+    case 72: return launch_seq<72, 2, TIN>(a, tpc, lds, st);
+    case 96: return launch_seq<96, 2, TIN>(a, tpc, lds, st);
+    case 144:
+      return seq_gpt(144) == 2 ? launch_seq<144, 2, TIN>(a, tpc, lds, st) : launch_seq<144, 1, TIN>(a, tpc, lds, st);
+    default: return launch_seq<288, 1, TIN>(a, tpc, lds, st);
   }
 }
 

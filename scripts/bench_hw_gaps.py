@@ -4,7 +4,8 @@ kernel time per 100k x 10,080 x 64 fit for dense series, a 30-minute outage in a
 of the series, isolated scrape misses at a rate, and (FOREMAST_HW_DG_ALL=1 rows) every pair
 through the gapped kernel.  At the short seasons of variant 6 (hw_seq.hip, e.g. --season 72:
 the 1200 s step) the ``v3dense`` / ``v3miss1e-3`` cases run the time-parallel variant 3 on the
-same data (FOREMAST_HW_SEQ=0); ``s6*`` cases run variant 6 at m = 288 (FOREMAST_HW_SEQ288=1).  One JSON line per case; interleaved rounds."""
+same data (FOREMAST_HW_SEQ=0); ``s6*`` cases run variant 6 at m = 288 (FOREMAST_HW_SEQ288=1), ``g2*`` cases m = 144 with two grid
+points per thread (FOREMAST_HW_SEQ_GPT144=2).  One JSON line per case; interleaved rounds."""
 
 from __future__ import annotations
 
@@ -46,7 +47,7 @@ def main():
     hists = {}
     for case in args.cases.split(","):
         h = base.clone()
-        kind = case[2:] if case[:2] in ("v3", "s6") else case
+        kind = case[2:] if case[:2] in ("v3", "s6", "g2") else case
         if kind.startswith("gap"):
             frac = int(kind[3:]) / 100
             rows = torch.randperm(N, device=dev, generator=g)[: int(frac * N)]
@@ -65,6 +66,7 @@ def main():
             os.environ["FOREMAST_HW_DG_ALL"] = "1" if case == "dgall" else "0"
             os.environ["FOREMAST_HW_SEQ"] = "0" if case.startswith("v3") else "1"
             os.environ["FOREMAST_HW_SEQ288"] = "1" if case.startswith("s6") else "0"
+            os.environ["FOREMAST_HW_SEQ_GPT144"] = "2" if case.startswith("g2") else "1"
             out = outs.setdefault(case[:2], {})
             for _w in range(2):
                 K.smoothing_fit(h, 0, R, sm.MODE_HW, m, grid, spec, variant=5, out=out)
