@@ -659,6 +659,7 @@ def setup_canary(args, world, rank, dev):
         "prune_hints": ("previous winners first (exact: the branch and bound's order only)"
                         if os.environ.get("FOREMAST_HW_HINTS", "1") != "0" else "off (grid order)"),
         "pairwise_shift_sigma": cfg.pairwise_shift,
+        "pairwise_shift_spread": "one-step sigma" if cfg.pairwise_shift_one_step else "horizon-scaled sigma",
         "health_collectives": "1 fused all_gather" if agg.fused else ("all_reduce + all_gather" if agg.active else "none"),
         "hip_graph": bool(args.graph and dev.type == "cuda"),
         "ingest": args.ingest,
@@ -942,7 +943,8 @@ def run_cpu_baseline(args) -> None:
                                 alpha=cfg.pairwise_threshold, pairwise_scale=cfg.pairwise_scale,
                                 pw_min_points=cfg.pairwise_min_points,
                                 shift_threshold=cfg.pairwise_shift,
-                                shift_min_points=cfg.pairwise_shift_min_points).verdict for i in range(n)]
+                                shift_min_points=cfg.pairwise_shift_min_points,
+                                shift_one_step=cfg.pairwise_shift_one_step).verdict for i in range(n)]
     dt = time.perf_counter() - t0
     truth = set(bad.tolist())
     flagged = {i for i, v in enumerate(verdicts) if v == 1}

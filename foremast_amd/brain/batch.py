@@ -186,14 +186,15 @@ class BatchScorer:
             f = pl_ref.forecast(fit, torch.from_numpy(cts).to(dev))
             d = det_ref.detect(f, fit.sigma.float(), t_cur, t_thr, t_bnd, t_low, differs=differs,
                                pairwise_scale=cfg.pairwise_scale,
-                               model_ok=fit.n_valid >= cfg.min_historical_points, **dkw)
+                               model_ok=fit.n_valid >= cfg.min_historical_points, **dkw)  # no horizon factor
             upper, lower, verdict, anom = d.upper, d.lower, d.verdict, d.anomaly
         elif self.gpu:
             from ..ops import kernels as K
             spec = K.DetectSpec(horizons=t_hz, threshold=t_thr, bound=t_bnd, min_lower=t_low, cur=t_cur,
                                 differs=differs, pw_scale=cfg.pairwise_scale, min_valid=cfg.min_historical_points,
                                 max_horizon=int(hz.max()) if hz.size and hz.min() >= 1 else None,
-                                horizon_variance=cfg.horizon_variance, **dkw)
+                                horizon_variance=cfg.horizon_variance,
+                                shift_one_step=cfg.pairwise_shift_one_step, **dkw)
             T = t_hist.shape[1]
             if algo == "seasonal_decompose":
                 out = K.decompose_score(t_hist, 0, T, m, spec)
@@ -215,20 +216,23 @@ class BatchScorer:
                 fc = dec_ref.decompose_forecast(t_hist, m)
                 f = dec_ref.forecast_decomposition(fc, t_hz)
                 sigma, n_valid = fc.sigma, fc.n_valid
+                sigma1 = sigma
             elif mode is not None:
                 grid = sm_ref.make_grid(mode, cfg.hw_alpha, cfg.hw_beta, cfg.hw_gamma)
                 fit = sm_ref.fit_smoothing(t_hist, mode, grid, m=max(m, 1))
                 f = sm_ref.forecast(fit, t_hz)
                 sigma, n_valid = fit.sigma, fit.n_valid
+                sigma1 = sigma
                 if cfg.horizon_variance:
                     sigma = sigma[:, None] * det_ref.horizon_sigma_factor(grid[fit.best.long()], mode, max(m, 1), t_hz)
             else:
                 st = ma_ref.window_stats(t_hist, cfg.ma_window if algo == "moving_average" else None)
                 f = st.mean[:, None].expand(B, t_cur.shape[1])
                 sigma, n_valid = st.std, st.count
+                sigma1 = sigma
             d = det_ref.detect(f, sigma, t_cur, t_thr, t_bnd, t_low, differs=differs,
                                pairwise_scale=cfg.pairwise_scale, model_ok=n_valid >= cfg.min_historical_points,
-                               **dkw)
+                               shift_sigma=sigma1 if cfg.pairwise_shift_one_step else None, **dkw)
             upper, lower, verdict, anom = d.upper, d.lower, d.verdict, d.anomaly
         upper_np = upper.float().cpu().numpy()
         lower_np = lower.float().cpu().numpy()

@@ -405,6 +405,7 @@ class StreamingShard:
                             anomalies=self.anomalies, max_horizon=self.cur.W, threshold_low=self.thr_low,
                             pw_min_points=cfg.pairwise_min_points,
                             shift_threshold=cfg.pairwise_shift, shift_min_points=cfg.pairwise_shift_min_points,
+                            shift_one_step=cfg.pairwise_shift_one_step,
                             base_mean=self.pw_out["base_mean"] if differs is not None else None,
                             horizon_variance=cfg.horizon_variance)
 
@@ -466,6 +467,7 @@ class StreamingShard:
                             anomalies=self.anomalies, max_horizon=self.cur.W, threshold_low=self.thr_low,
                             pw_min_points=cfg.pairwise_min_points,
                             shift_threshold=cfg.pairwise_shift, shift_min_points=cfg.pairwise_shift_min_points,
+                            shift_one_step=cfg.pairwise_shift_one_step,
                             base_mean=self.pw_out["base_mean"] if differs is not None else None,
                             horizon_variance=cfg.horizon_variance)
         if self.anomalies is not None:
@@ -552,11 +554,13 @@ class StreamingShard:
             n_valid = st.count
             extra = {"mean": st.mean, "std": st.std}
         ok = n_valid >= cfg.min_historical_points
+        sigma1 = extra["sigma"] if "sigma" in extra else extra["std"]  # one-step (the mean-shift rule's spread)
         d = det_ref.detect(f, sigma, self.cur.data, self.thr_full, self.bound, self.min_lower,
                            differs=differs, pairwise_scale=cfg.pairwise_scale, model_ok=ok,
                            threshold_low=self.thr_low, pw_min_points=cfg.pairwise_min_points,
                            shift_threshold=cfg.pairwise_shift, shift_min_points=cfg.pairwise_shift_min_points,
-                           base_mean=torch.nanmean(self.base.float(), 1) if differs is not None else None)
+                           base_mean=torch.nanmean(self.base.float(), 1) if differs is not None else None,
+                           shift_sigma=sigma1 if cfg.pairwise_shift_one_step else None)
         v = d.verdict.long()
         self.app_stats.index_put_((self.app_id.long(), torch.zeros_like(v)), (v == 1).int(), accumulate=True)
         self.app_stats.index_put_((self.app_id.long(), torch.ones_like(v)), (v >= 0).int(), accumulate=True)

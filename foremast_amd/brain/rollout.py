@@ -1235,7 +1235,7 @@ class RolloutMonitor:
                             min_valid=cfg.min_historical_points, want_band=True, app_id=self.app_id,
                             app_stats=self.app_stats, anomalies=self.anomalies,
                             pw_min_points=cfg.pairwise_min_points, shift_threshold=cfg.pairwise_shift,
-                            shift_min_points=cfg.pairwise_shift_min_points,
+                            shift_min_points=cfg.pairwise_shift_min_points, shift_one_step=cfg.pairwise_shift_one_step,
                             base_mean=self.pw_out["base_mean"] if differs is not None else None,
                             horizon_variance=cfg.horizon_variance, thr_lut=self._lut, thr_cls=self.thr_cls,
                             row_out=self._rec_dev[:cap * 4].view(cap, 4), start_min=self.start_min,
@@ -1320,7 +1320,8 @@ class RolloutMonitor:
                            pairwise_scale=cfg.pairwise_scale, model_ok=s["nvalid"] >= cfg.min_historical_points,
                            threshold_low=thr_l, pw_min_points=cfg.pairwise_min_points,
                            shift_threshold=cfg.pairwise_shift, shift_min_points=cfg.pairwise_shift_min_points,
-                           base_mean=torch.nanmean(self.base.float(), 1) if differs is not None else None)
+                           base_mean=torch.nanmean(self.base.float(), 1) if differs is not None else None,
+                           shift_sigma=s["sigma"] if cfg.pairwise_shift_one_step else None)
         v = d.verdict.long()
         self.app_stats.index_put_((self.app_id.long(), torch.zeros_like(v)), (v == 1).int(), accumulate=True)
         self.app_stats.index_put_((self.app_id.long(), torch.ones_like(v)), (v >= 0).int(), accumulate=True)

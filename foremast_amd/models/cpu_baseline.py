@@ -77,7 +77,8 @@ def hw_fit(y: np.ndarray, m: int, grid: np.ndarray):
 def score_series(hist: np.ndarray, cur: np.ndarray, base: Optional[np.ndarray], horizons: np.ndarray, m: int,
                  grid: np.ndarray, threshold: float = 4.0, bound: int = 3, alpha: float = 0.05,
                  pairwise_scale: float = 0.5, pw_min_points: int = 3, min_mw: int = 20, min_w: int = 20,
-                 min_k: int = 5, shift_threshold: float = 0.0, shift_min_points: int = 1) -> CpuVerdict:
+                 min_k: int = 5, shift_threshold: float = 0.0, shift_min_points: int = 1,
+                 shift_one_step: bool = False) -> CpuVerdict:
     """Score ONE series: pairwise tests, HW fit, forecast, band, verdict."""
     differs = False
     if base is not None:
@@ -114,10 +115,12 @@ def score_series(hist: np.ndarray, cur: np.ndarray, base: Optional[np.ndarray], 
     bm = float(np.nanmean(base)) if base is not None and np.any(~np.isnan(base)) else float("nan")
     if (shift_threshold > 0 and differs and bm == bm and n_full == 0 and not n_low >= pw_min_points
             and np.count_nonzero(ok) >= max(shift_min_points, 1)):
-        # the mean-shift rule (models/detect.py): canary window against the baseline mean
-        mz = float(np.mean((cur[ok] - bm) / np.maximum(s[ok], 1e-12)))
+        # the mean-shift rule (models/detect.py): canary window against the baseline mean, in
+        # units of the one-step sigma (shift_one_step) or of the horizon-scaled band sigma
+        ss = np.full(len(cur), sigma) if shift_one_step else s
+        mz = float(np.mean((cur[ok] - bm) / np.maximum(ss[ok], 1e-12)))
         if ((bound & 1) and mz > shift_threshold) or ((bound & 2) and mz < -shift_threshold):
-            hi = (cur > bm + shift_threshold * s) if bound & 1 else np.zeros(len(cur), bool)
-            lo = (cur < bm - shift_threshold * s) if bound & 2 else np.zeros(len(cur), bool)
+            hi = (cur > bm + shift_threshold * ss) if bound & 1 else np.zeros(len(cur), bool)
+            lo = (cur < bm - shift_threshold * ss) if bound & 2 else np.zeros(len(cur), bool)
             count = int(np.count_nonzero((hi | lo) & ok))
     return CpuVerdict(verdict=1 if count else 0, count=count, differs=differs, best=best, sigma=sigma)

@@ -123,11 +123,14 @@ def detect(forecast: torch.Tensor, sigma: torch.Tensor, x: torch.Tensor,
            differs: Optional[torch.Tensor] = None, pairwise_scale: float = 0.5,
            model_ok: Optional[torch.Tensor] = None, threshold_low: Optional[torch.Tensor] = None,
            pw_min_points: int = 1, shift_threshold: float = 0.0,
-           base_mean: Optional[torch.Tensor] = None, shift_min_points: int = 1) -> Detection:
+           base_mean: Optional[torch.Tensor] = None, shift_min_points: int = 1,
+           shift_sigma: Optional[torch.Tensor] = None) -> Detection:
     """``sigma``: ``[N]`` or per point ``[N, C]`` (horizon-scaled).  ``threshold``
     / ``threshold_low`` are per-point levels (already window-corrected, see
     :func:`effective_thresholds`); ``threshold_low`` defaults to
-    ``threshold * pairwise_scale``."""
+    ``threshold * pairwise_scale``.  ``shift_sigma`` (``[N]``, optional): the spread of
+    the mean-shift rule (the model's one-step sigma, config ``pairwise_shift_one_step``);
+    default ``sigma``."""
     f = forecast.float()
     N, C = f.shape
     thr = threshold.float().expand(N) if threshold.dim() == 0 else threshold.float()
@@ -157,10 +160,11 @@ def detect(forecast: torch.Tensor, sigma: torch.Tensor, x: torch.Tensor,
     if use_shift:
         bm = base_mean.float().to(f.device).view(-1, 1)
         st = float(shift_threshold)
-        up_s = bm + st * sig
-        lo_s = torch.maximum(bm - st * sig, mlow)
+        ss = sig if shift_sigma is None else shift_sigma.float().to(f.device).view(-1, 1).expand(N, C)
+        up_s = bm + st * ss
+        lo_s = torch.maximum(bm - st * ss, mlow)
         an_s = (((xv > up_s) & ((bnd & 1) != 0)) | ((xv < lo_s) & ((bnd & 2) != 0))) & valid & ok[:, None]
-        zb = torch.where(valid & ok[:, None], (xv - bm) / sig.clamp(min=1e-12), torch.zeros_like(xv))
+        zb = torch.where(valid & ok[:, None], (xv - bm) / ss.clamp(min=1e-12), torch.zeros_like(xv))
         nz = (valid & ok[:, None]).sum(1)
         mz = zb.sum(1) / nz.clamp(min=1)
         side = (((bnd[:, 0] & 1) != 0) & (mz > st)) | (((bnd[:, 0] & 2) != 0) & (mz < -st))

@@ -40,7 +40,7 @@ class DetectArgs(C.Structure):
         ("forecast", P), ("upper", P), ("lower", P), ("count", P), ("verdict", P),
         ("score", P), ("app_id", P), ("app_stats", P),
         ("anom_count", P), ("anom_series", P), ("anom_col", P), ("anom_val", P), ("anom_cap", I), ("shift_thr", F), ("base_mean", P),
-        ("shift_min_points", I), ("_pad1", I),
+        ("shift_min_points", I), ("shift_one_step", I),
         ("thr_lut", P), ("thr_cls", P), ("lut_n", I), ("last_ncol", I), ("row_out", P), ("start_min", P),
         ("tick_min", P),
     ]

@@ -44,7 +44,7 @@ struct DetectArgs {
   float shift_thr;
   const float* base_mean;       // [N] mean of the baseline pods' window (NaN: none) or null
   int shift_min_points;         // the mean-shift rule needs this many valid canary points
-  int _pad1;
+  int shift_one_step;           // 1: the mean-shift rule's spread is the one-step sigma (no horizon factor)
   // per-point thresholds by (class, valid points of the window): the Sidak window
   // correction of models/detect.py window_threshold, tabulated on the host in fp64 (no
   // per-tick fp64 on the device).  Null: threshold / threshold_low as given.

@@ -58,7 +58,8 @@ __device__ __forceinline__ float hstep_factor(const DetectArgs& d, int gidx, int
 // the lowered band (threshold_low, or threshold * pw_scale) — which only counts
 // when at least pw_min_points points fall outside it — and the mean-shift rule
 // (shift_thr > 0): the window's mean deviation from the baseline pods' mean, in
-// units of the spread s, beyond shift_thr on an enabled side.
+// units of the spread s (the one-step sigma with shift_one_step), beyond shift_thr on an
+// enabled side.
 struct DetThr {
   float full, low, shift, bm;
   bool differs, shift_on;
@@ -116,8 +117,9 @@ __device__ __forceinline__ void det_count_col(const DetectArgs& d, int n, int c,
     u.cnt_f += det_outside(x, f, t.full, s, mlow, bnd) ? 1.f : 0.f;
     if (t.differs) u.cnt_l += det_outside(x, f, t.low, s, mlow, bnd) ? 1.f : 0.f;
     if (t.shift_on) {
-      u.cnt_s += det_outside(x, t.bm, t.shift, s, mlow, bnd) ? 1.f : 0.f;
-      u.zsum += (x - t.bm) / fmaxf(s, 1e-12f);
+      const float ss = d.shift_one_step ? sig : s;  // the mean-shift rule's spread
+      u.cnt_s += det_outside(x, t.bm, t.shift, ss, mlow, bnd) ? 1.f : 0.f;
+      u.zsum += (x - t.bm) / fmaxf(ss, 1e-12f);
       u.nz += 1.f;
     }
   }
@@ -132,8 +134,9 @@ __device__ __forceinline__ void det_emit_col(const DetectArgs& d, int n, int c, 
                                              float mlow, bool emit, ForecastFn& fcast, float center) {
   const int h = d.horizons[d.h_ld * n + c];
   const float f = fcast(h);
-  const float s = sig * hstep_factor(d, gidx, h);
-  const float fc = center == center ? center : f;
+  const bool shifted = center == center;  // the mean-shift rule's band
+  const float s = (shifted && d.shift_one_step) ? sig : sig * hstep_factor(d, gidx, h);
+  const float fc = shifted ? center : f;
   const float up = fc + thr * s;
   const float lo = fmaxf(fc - thr * s, mlow);
   const long long o = (long long)n * d.C + c;

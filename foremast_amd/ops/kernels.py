@@ -78,6 +78,9 @@ class DetectSpec:
     shift_threshold: float = 0.0
     base_mean: Optional[torch.Tensor] = None
     shift_min_points: int = 1
+    # the mean-shift rule's spread: the one-step sigma (models/detect.py ``shift_sigma``)
+    # instead of the horizon-scaled band sigma
+    shift_one_step: bool = False
     # window-corrected thresholds tabulated by (class, valid points) (detect.h det_thresholds):
     # float32 [classes, 2, n] and uint16-in-int16 [N] classes; replaces threshold / threshold_low
     thr_lut: Optional[torch.Tensor] = None
@@ -185,6 +188,7 @@ def _fill_detect(d: nat.DetectArgs, spec: DetectSpec, N: int, device, out: Dict[
     d.shift_thr = float(spec.shift_threshold)
     d.base_mean = nat.ptr(spec.base_mean)
     d.shift_min_points = int(spec.shift_min_points)
+    d.shift_one_step = int(bool(spec.shift_one_step))
     d.threshold_low = nat.ptr(spec.threshold_low)
     d.hv_grid, d.hv_mode, d.hv_m = None, 0, 0
     d.forecast = nat.ptr(out.get("forecast"))

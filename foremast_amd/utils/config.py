@@ -88,6 +88,11 @@ class BrainConfig:
     # band semantics (docs/SCORING.md); set ML_PAIRWISE_SHIFT=0 for the per-point rule only
     pairwise_shift: float = 1.5
     pairwise_shift_min_points: int = 20  # ML_PAIRWISE_SHIFT_MIN_POINTS (as MIN_MANN_WHITE_DATA_POINTS)
+    # the mean-shift rule's spread (ML_PAIRWISE_SHIFT_ONE_STEP = 1 | 0): the model's one-step
+    # sigma, not the horizon-scaled band sigma.  The rule compares the canary window with the
+    # baseline pods' window over the same minutes, so the forecast's h-step error growth is not
+    # part of the comparison (docs/SCORING.md)
+    pairwise_shift_one_step: bool = True
     window_correction: str = "sidak"
     horizon_variance: bool = True
     poll_seconds: float = 5.0
@@ -159,6 +164,7 @@ class BrainConfig:
         c.pairwise_min_points = int(f("ML_PAIRWISE_MIN_ANOMALIES", c.pairwise_min_points, int))
         c.pairwise_shift = f("ML_PAIRWISE_SHIFT", c.pairwise_shift)
         c.pairwise_shift_min_points = int(f("ML_PAIRWISE_SHIFT_MIN_POINTS", c.pairwise_shift_min_points, int))
+        c.pairwise_shift_one_step = e.get("ML_PAIRWISE_SHIFT_ONE_STEP", "1").strip().lower() not in ("0", "false", "no")
         c.window_correction = (e.get("FOREMAST_WINDOW_CORRECTION") or c.window_correction).strip().lower()
         c.horizon_variance = e.get("FOREMAST_HORIZON_VARIANCE", "1").strip().lower() not in ("0", "false", "no")
         # FOREMAST_DETECTION_PRESET=reference: the reference brain's documented per-point

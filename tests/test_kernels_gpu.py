@@ -624,13 +624,14 @@ def test_hw_split_plan():
     assert lib.fm_hw_d_split_plan(20, 0, 4096) == 0
 
 
-@pytest.mark.parametrize("shift", [0.0, 1.0])
+@pytest.mark.parametrize("shift,one_step", [(0.0, False), (1.0, False), (1.0, True)])
 @pytest.mark.parametrize("which", ["window_stats", "holt_winters", "hw_deferred"])
-def test_two_rule_detection_matches_reference(K, which, shift):
+def test_two_rule_detection_matches_reference(K, which, shift, one_step):
     """Full band + lowered pairwise band that needs >= pw_min_points points, and
     (shift > 0) the mean-shift rule (detect.h det_decide): kernel verdicts, counts,
     bands and the K9 list equal the reference on series built to sit on each side
-    of every rule."""
+    of every rule.  one_step: the rule's spread is the one-step sigma (DetectSpec
+    shift_one_step / detect's shift_sigma), not the horizon-scaled band sigma."""
     from foremast_amd.brain.engine import synthetic_history
     dev = torch.device("cuda:0")
     N, T, m, C = 2000, 2 * 1440, 1440, 10
@@ -654,12 +655,14 @@ def test_two_rule_detection_matches_reference(K, which, shift):
     spec = K.DetectSpec(horizons=torch.arange(1, C + 1, dtype=torch.int32, device=dev), threshold=full.to(dev),
                         bound=bound, min_lower=torch.full((N,), -1e9, device=dev), cur=cur, differs=differs,
                         threshold_low=low.to(dev), pw_min_points=3, anomalies=K.AnomalyBuffer(N * C, dev),
-                        max_horizon=C, shift_threshold=shift, base_mean=bmean, shift_min_points=5)
+                        max_horizon=C, shift_threshold=shift, base_mean=bmean, shift_min_points=5,
+                        shift_one_step=one_step)
     spec.anomalies.reset()
     grid = sm_ref.make_grid(sm_ref.MODE_HW, (0.1, 0.5), (0.0, 0.1), (0.1, 0.5)).to(dev)
     if which == "window_stats":
         out = K.window_stats(hist, 0, T, spec)
         sig = out["std"].cpu()
+        sig1 = sig
     else:
         if which == "hw_deferred":
             out = K.smoothing_fit(hist, 0, T, sm_ref.MODE_HW, m, grid, spec, defer_detect=True, variant=5)
@@ -669,12 +672,12 @@ def test_two_rule_detection_matches_reference(K, which, shift):
         else:
             out = K.smoothing_fit(hist, 0, T, sm_ref.MODE_HW, m, grid, spec)
         params = grid.cpu()[out["best"].cpu().long()]
-        sig = out["sigma"].cpu()[:, None] * det_ref.horizon_sigma_factor(params, sm_ref.MODE_HW, m,
-                                                                        torch.arange(1, C + 1))
+        sig1 = out["sigma"].cpu()
+        sig = sig1[:, None] * det_ref.horizon_sigma_factor(params, sm_ref.MODE_HW, m, torch.arange(1, C + 1))
     torch.cuda.synchronize()
     d = det_ref.detect(out["forecast"].cpu(), sig, cur.cpu(), full, bound.cpu(), torch.full((N,), -1e9),
                        differs=differs.cpu(), threshold_low=low, pw_min_points=3, shift_threshold=shift,
-                       base_mean=bmean.cpu(), shift_min_points=5)
+                       base_mean=bmean.cpu(), shift_min_points=5, shift_sigma=sig1 if one_step else None)
     assert torch.equal(d.verdict, out["verdict"].cpu())
     assert torch.equal(d.count, out["count"].cpu())
     low_fired = (differs.cpu().bool() & (d.count > 0))

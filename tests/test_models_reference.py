@@ -325,6 +325,29 @@ def test_pairwise_mean_shift_rule():
     assert d.verdict.tolist()[0] == 0
 
 
+def test_mean_shift_rule_one_step_spread():
+    """shift_sigma: the mean-shift rule measures the window against the baseline in units of
+    the one-step sigma, while the bands keep the horizon-scaled sigma.  A +2 sigma shift whose
+    band sigma grows to 1.5x over the window: under the horizon-scaled spread the window's mean
+    z is ~1.3 (below 1.5, healthy); in one-step units it is 2.0 (anomalous)."""
+    N, C = 2, 10
+    f = torch.zeros(N, C)
+    sig1 = torch.ones(N)
+    sig = sig1[:, None] * torch.linspace(1.0, 2.0, C)[None, :]     # horizon-scaled (mean 1.5)
+    x = torch.full((N, C), 2.0)
+    x[1] = 0.5                                                     # a small shift stays healthy
+    thr, low = torch.full((N,), 4.0), torch.full((N,), 3.0)
+    bound = torch.full((N,), 3, dtype=torch.int8)
+    kw = dict(differs=torch.ones(N, dtype=torch.uint8), threshold_low=low, pw_min_points=3, shift_min_points=5,
+              shift_threshold=1.5, base_mean=torch.zeros(N))
+    d_h = detect.detect(f, sig, x, thr, bound, torch.full((N,), -1e9), **kw)
+    d_1 = detect.detect(f, sig, x, thr, bound, torch.full((N,), -1e9), shift_sigma=sig1, **kw)
+    assert d_h.verdict.tolist() == [0, 0] and d_1.verdict.tolist() == [1, 0]
+    assert d_1.count.tolist() == [10, 0]
+    np.testing.assert_allclose(d_1.upper[0].numpy(), 1.5)           # band base_mean + 1.5 * one-step sigma
+    np.testing.assert_allclose(d_1.upper[1].numpy(), (4.0 * sig[1]).numpy())  # others keep the scaled band
+
+
 def test_decompose_forecast_continues_trend_and_season():
     """Decomposition scorer reference: on a noiseless linear trend + sinusoid the
     forecast matches the generating function and the residual RMS is ~0."""

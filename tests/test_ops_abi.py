@@ -32,7 +32,7 @@ def test_struct_sizes(lib, name):
     ("SmoothArgs", "det"), ("SmoothArgs", "season_out"), ("SmoothArgs", "grid"), ("SmoothArgs", "head_dev"), ("SmoothArgs", "season_hb"), ("SmoothArgs", "nvalid_out"),
     ("DetectArgs", "pw_scale"), ("DetectArgs", "app_stats"), ("DetectArgs", "ld_cur"),
     ("DetectArgs", "anom_count"), ("DetectArgs", "anom_cap"), ("DetectArgs", "thr_lut"), ("DetectArgs", "lut_n"),
-    ("DetectArgs", "row_out"), ("DetectArgs", "tick_min"),
+    ("DetectArgs", "row_out"), ("DetectArgs", "tick_min"), ("DetectArgs", "shift_one_step"),
     ("RankArgs", "pvals"), ("RankArgs", "alpha"), ("RankArgs", "p_friedman"), ("RankArgs", "pods_b"), ("RankArgs", "z_crit"), ("WindowArgs", "det"),
     ("BivArgs", "eps"), ("BivArgs", "app_stats"),
 ])
