@@ -83,6 +83,9 @@ def parse():
     p.add_argument("--pairwise-shift", type=float, default=None,
                    help="canary: mean-shift rule threshold in sigmas (ML_PAIRWISE_SHIFT; 0 = off; "
                         "default: the BrainConfig default)")
+    p.add_argument("--pairwise-shift-spread", choices=["one-step", "horizon"], default=None,
+                   help="canary: the mean-shift rule's spread (ML_PAIRWISE_SHIFT_ONE_STEP; default: the "
+                        "BrainConfig default, one-step)")
     p.add_argument("--anomaly-frac", type=float, default=0.01)
     p.add_argument("--anomaly-kind", default="scale3", choices=["scale3", "shift3sigma", "scale", "shift"],
                    help="injected canary regression: values x3, or a level shift of +3 noise sigma; "
@@ -379,6 +382,8 @@ def setup_canary(args, world, rank, dev):
     cfg.min_historical_points = 0
     if args.pairwise_shift is not None:
         cfg.pairwise_shift = args.pairwise_shift
+    if args.pairwise_shift_spread is not None:
+        cfg.pairwise_shift_one_step = args.pairwise_shift_spread == "one-step"
     s, e, per = shard_range(args.series, world, rank, align=METRICS_PER_APP)
     n_local = e - s
     n_apps = (args.series + METRICS_PER_APP - 1) // METRICS_PER_APP

@@ -86,7 +86,7 @@ class BrainConfig:
     # BASELINE pods' mean (not of the forecast) is anomalous even if few of its points
     # leave the window-corrected band.  A departure from the reference brain's per-point
     # band semantics (docs/SCORING.md); set ML_PAIRWISE_SHIFT=0 for the per-point rule only
-    pairwise_shift: float = 1.5
+    pairwise_shift: float = 1.25  # round 6: 1.5 -> 1.25 (docs/SCORING.md, profiles/bench/shift_thr_r6/)
     pairwise_shift_min_points: int = 20  # ML_PAIRWISE_SHIFT_MIN_POINTS (as MIN_MANN_WHITE_DATA_POINTS)
     # the mean-shift rule's spread (ML_PAIRWISE_SHIFT_ONE_STEP = 1 | 0): the model's one-step
     # sigma, not the horizon-scaled band sigma.  The rule compares the canary window with the
