@@ -187,3 +187,38 @@ def test_seq_at_the_300s_step_matches_reference(K, case, monkeypatch):
     torch.cuda.synchronize()
     assert K.last_hw_variant == 6
     _check(K, out, yl, m, hz, cur)
+
+
+def test_batch_scorer_at_the_1200s_step_runs_variant6(K):
+    """The per-job scorer (brain/batch.py, the service's jobs whose queries carry step 1200):
+    the group's season is 86400 / 1200 = 72, so the GPU fit runs variant 6; its verdicts
+    equal the CPU reference scorer's on the same tasks (x3 regressions in some canary
+    windows, isolated misses in the histories)."""
+    from foremast_amd.brain.batch import BatchScorer, MetricTask
+    from foremast_amd.utils.config import BrainConfig
+    step, m, T, C = 1200.0, 72, 504, 10
+    N = 24
+    y = _gapped("miss", N, T + C, m, seed=1200)
+    base = _series(N, T + C, m, seed=77)[:, T:]
+    cfg = BrainConfig()
+    cfg.algorithm = "holt_winters"
+    cfg.min_historical_points = 0
+    t_end = 1_700_000_000.0
+    tasks = []
+    for i in range(N):
+        cur = y[i, T:].copy()
+        cur[np.isnan(cur)] = 20.0
+        if i % 6 == 0:
+            cur *= 3.0                                   # injected regression
+        tasks.append(MetricTask(job_id=f"j{i}", alias="latency", metric="latency", namespace="ns", app=f"a{i}",
+                                step=step, hist=y[i, :T].astype(np.float32), hist_end=t_end,
+                                cur_ts=t_end + step * np.arange(1, C + 1), cur_vals=cur.astype(np.float32),
+                                base_vals=base[i].astype(np.float32), threshold=3.0, bound=3))
+    gpu = BatchScorer(cfg, device=torch.device("cuda:0")).score(tasks)
+    torch.cuda.synchronize()
+    assert K.last_hw_variant == 6
+    cpu = BatchScorer(cfg, device=torch.device("cpu")).score(tasks)
+    vg = np.array([r.verdict for r in gpu])
+    vc = np.array([r.verdict for r in cpu])
+    assert (vg == vc).mean() >= 0.95, (vg, vc)
+    assert (vg[::6] == 1).all()
