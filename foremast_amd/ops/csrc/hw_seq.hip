@@ -40,6 +40,7 @@ extern "C" int fm_hw_detect_params(const SmoothArgs* a, hipStream_t st);
 namespace {
 
 constexpr int SEQ_HB = 16;  // seasonal phases written to season_hb (kernels.py HALF_HB)
+constexpr int SEQ_LD = 8;   // staging loads in flight per thread
 
 template <int GPT> struct SeqVec;
 template <> struct SeqVec<1> { using type = float; };
@@ -83,7 +84,14 @@ __device__ __forceinline__ void seq_season(const float* yr, const float* kr, V (
   }
 }
 
-template <typename TIN> __device__ __forceinline__ float ld_elem(const TIN* p) { return to_f32<TIN>(*p); }
+// raw bits of one element (bf16: zero-extended), converted after the loads are issued
+template <typename TIN> __device__ __forceinline__ unsigned ld_bits(const TIN* p) {
+  if constexpr (sizeof(TIN) == 2) return (unsigned)*(const unsigned short*)p;
+  else return __float_as_uint(*(const float*)p);
+}
+template <typename TIN> __device__ __forceinline__ float bits_f32_(unsigned u) {
+  return __uint_as_float(sizeof(TIN) == 2 ? u << 16 : u);
+}
 
 // A workgroup of 256 threads owns SW = 256 / TPC series; thread gp of a series fits grid
 // points GPT gp .. GPT gp + GPT - 1 (clamped to G - 1).  Rows past N stage missing points
@@ -106,22 +114,39 @@ __global__ __launch_bounds__(256, (M > 144 || (M > 96 && GPT == 2)) ? 1 : 2) voi
 
   if (tid < SW) nanc[tid] = 0;
   __syncthreads();
+  // staging: element i = r Tp + tau of the workgroup's rows, i = tid + 256 j; SEQ_LD loads in
+  // flight per thread before any is converted and stored (issued one row at a time, waiting
+  // on each, the staging was a chain of ~16 global-memory round trips per workgroup)
   const TIN* base = (const TIN*)a.hist;
-  for (int r = 0; r < SW; ++r) {  // row r: consecutive columns over the workgroup (coalesced)
-    const int nn = n0 + r;
-    const TIN* src = base + (long long)(nn < a.N ? nn : 0) * a.ld;
-    for (int tau = tid; tau < Tp; tau += 256) {
-      const int t = tau - pad;
-      float x = fm_nan();
-      if (nn < a.N && t >= 0) {
-        int c = head + t;
-        c -= c >= R ? R : 0;
-        x = ld_elem<TIN>(src + c);
-      }
+  const int total = SW * Tp;
+  for (int i0 = 0; i0 < total; i0 += 256 * SEQ_LD) {
+    unsigned u[SEQ_LD];
+    bool in[SEQ_LD];
+    int at[SEQ_LD];
+#pragma unroll
+    for (int j = 0; j < SEQ_LD; ++j) {
+      const int i = i0 + tid + 256 * j;
+      const int r = (unsigned)i / (unsigned)Tp, tau = i - r * Tp;
+      const int nn = n0 + r, t = tau - pad;
+      in[j] = i < total && nn < a.N && t >= 0;
+      at[j] = i < total ? r * LDY + tau : -1;
+      int c = head + t;
+      c -= c >= R ? R : 0;
+      // unconditional loads (an element past the rows / the padding reads element 0 and is
+      // replaced), held by the asm below: a load the compiler sinks under a branch is waited
+      // for at the branch's join, one global-memory round trip per element
+      u[j] = ld_bits<TIN>(base + (in[j] ? (long long)nn * a.ld + c : 0));
+    }
+#pragma unroll
+    for (int j = 0; j < SEQ_LD; ++j) asm volatile("" : "+v"(u[j]));
+#pragma unroll
+    for (int j = 0; j < SEQ_LD; ++j) {
+      if (at[j] < 0) break;
+      const float x = in[j] ? bits_f32_<TIN>(u[j]) : fm_nan();
       const bool ok = x == x;
-      ys[r * LDY + tau] = ok ? x : 0.f;
-      ks[r * LDY + tau] = ok ? 1.f : 0.f;
-      if (!ok && tau >= M) atomicAdd(&nanc[r], 1);  // rare: gaps (the front padding is in season 0)
+      ys[at[j]] = ok ? x : 0.f;
+      ks[at[j]] = ok ? 1.f : 0.f;
+      if (!ok && at[j] % LDY >= M) atomicAdd(&nanc[at[j] / LDY], 1);  // rare: gaps (padding is in season 0)
     }
   }
   __syncthreads();
