@@ -132,6 +132,12 @@ def parse():
                         "the second of two input buffers (one captured graph each) while tick k runs, so a tick "
                         "starts with its input on the device; the tick itself is never queued behind the previous")
     p.add_argument("--no-graph-prefetch", dest="graph_prefetch", action="store_false")
+    p.add_argument("--doorbell", dest="doorbell", action="store_true", default=False,
+                   help="canary graph ticks: tick k+1's graph is enqueued (with its input copy) while tick k runs "
+                        "and starts by waiting for a doorbell, a pinned host counter the host bumps when it releases "
+                        "the tick after tick k's results are in: the gap between ticks is a PCIe write instead of "
+                        "a graph launch; the detect latency is timed from the doorbell")
+    p.add_argument("--no-doorbell", dest="doorbell", action="store_false")
     p.add_argument("--spin-wait", dest="spin_wait", action="store_true", default=False,
                    help="canary: wait for a tick's completion by polling its event instead of a blocking stream "
                         "synchronize (shorter host wake-up between ticks)")
@@ -603,7 +609,53 @@ def setup_canary(args, world, rank, dev):
         else:
             main_stream.synchronize()
 
+    bell = gpf and args.doorbell and dev.type == "cuda"
+    if bell:
+        shard.enable_doorbell()
+        DOORBELL[0] = shard
+    queued = {}  # doorbell mode: tick index -> (outputs, completion event) of a tick enqueued ahead
+    n_ticks_total = args.warmup + args.steps
+
+    def tick_bell(k):
+        """Doorbell graph tick k: ring the tick enqueued ahead (or enqueue it now), enqueue
+        tick k + 1 behind it, then wait for tick k."""
+        i = W + k
+        b = i % 2
+        hit = queued.pop(k, None)
+        if hit is None:
+            if gstaged[b] != i:
+                gstage(i)
+            out = shard.tick_graph(gviews[b][0], gviews[b][1], post=graph_tail)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            out, ev = hit
+        LAT_START[k] = time.perf_counter()
+        shard.ring()  # tick k starts (its input was copied before it was enqueued)
+        # enqueue tick k + 1 (not across the warmup / timed boundary, whose synchronize would
+        # wait on a tick no one rings)
+        if k + 1 < n_ticks_total and k + 1 != args.warmup and i + 1 < host_ticks.shape[0]:
+            gstage(i + 1)  # the other buffer's reader (tick k - 1) has completed
+            nxt = shard.tick_graph(gviews[1 - b][0], gviews[1 - b][1], post=graph_tail)
+            ev1 = torch.cuda.Event()
+            ev1.record()
+            queued[k + 1] = (nxt, ev1)
+        REFIT_FLAGS[k] = shard.last_refit
+        GRAPH_TAIL[0] = bool(out.get("post_in_graph"))
+        if args.spin_wait:
+            while not ev.query():
+                pass
+        else:
+            ev.synchronize()
+        if not out.get("post_in_graph"):
+            stats, _ = agg.tick(shard.app_stats, out["verdict"])
+            health_hosts[0].copy_(agg.recv if agg.fused else stats, non_blocking=pin)
+            main_stream.synchronize()
+        return out
+
     def tick(k):
+        if bell and shard.graph_ready():  # every replay of a doorbell graph is rung by tick_bell
+            return tick_bell(k)
         if gpf and shard.graph_ready():
             i = W + k
             b = i % 2
@@ -671,6 +723,7 @@ def setup_canary(args, world, rank, dev):
         "pipelined_ticks": pipelined,
         "input_prefetch": prefetch or ("double-buffered H2D of tick k+1 during tick k (graph ticks)" if gpf else False),
         "spin_wait": bool(args.spin_wait),
+        "doorbell": bool(bell),
         "zero_copy": zero_copy,
         "model_cache": ("none: every tick refits every series" if args.refit_every <= 1 else
                         f"refit every {args.refit_every} ticks, O(1) Holt-Winters state update + detect in between"),
@@ -703,6 +756,7 @@ class InFlight(NamedTuple):
 LAT_START = {}  # timed tick -> perf_counter time its data arrived (set by the prom ingest path)
 REFIT_FLAGS = {}  # tick -> whether it refit the model (canary --refit-every)
 GRAPH_TAIL = [False]  # canary: the health collective + copy back ran inside the tick graph
+DOORBELL = [None]     # canary --doorbell: the shard (its doorbell waits that timed out are recorded)
 
 
 def prom_bodies(host_ticks, s, P, ring, threads, pin):
@@ -1068,6 +1122,8 @@ def main():
         meta["gapped_pairs_per_tick"] = deferred(args.warmup + args.steps)
     if args.config in ("canary", "hw10k") or getattr(args, "config_name", "") == "hw10k":
         meta["health_tail_in_graph"] = GRAPH_TAIL[0]
+        if DOORBELL[0] is not None:
+            meta["doorbell_timeouts"] = DOORBELL[0].doorbell_timeouts()
         if GRAPH_TAIL[0] and meta.get("health_collectives", "none") != "none":
             meta["health_collectives"] += " (captured in the tick graph)"
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)

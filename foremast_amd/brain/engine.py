@@ -123,6 +123,10 @@ class StreamingShard:
             self._state_k = 0
             self._state_dev = torch.zeros(8, dtype=torch.int32, device=self.device)
         self._state_synced = False  # the device tick record matches the host ring (graph ticks)
+        # doorbell (enable_doorbell): graph ticks enqueued ahead wait for the host's counter
+        self._bell: Optional[torch.Tensor] = None
+        self._bell_dev: Optional[torch.Tensor] = None
+        self._bell_n = 0
         # cached Holt-Winters model (refit_every > 1): state after the last refit / update
         self.refit_every = max(1, int(spec.refit_every))
         self._cache: Optional[Dict] = None
@@ -249,6 +253,27 @@ class StreamingShard:
         self._refresh_horizons()
 
     # ------------------------------------------------------------------ graph tick
+    def enable_doorbell(self) -> None:
+        """Graph ticks start by waiting for a doorbell (ops/csrc/ingest.hip
+        ``tick_advance_kernel``): a tick can be enqueued before its input is released and
+        starts a PCIe write after :meth:`ring` instead of a graph launch after it.  Every
+        graph replay must be matched by exactly one :meth:`ring`."""
+        if not self.gpu or self._bell is not None:
+            return
+        self._bell = torch.zeros(1, dtype=torch.int32).pin_memory()
+        self._bell_dev = torch.zeros(2, dtype=torch.int32, device=self.device)
+        self._bell_n = 0
+        self._graphs.clear()  # recaptured with the doorbell wait
+
+    def ring(self) -> None:
+        """Release the next enqueued graph tick (doorbell mode)."""
+        self._bell_n += 1
+        self._bell[0] = self._bell_n
+
+    def doorbell_timeouts(self) -> int:
+        """Doorbell waits that gave up (one device sync); 0 when every replay was rung."""
+        return 0 if self._bell_dev is None else int(self._bell_dev[1].item())
+
     def graph_ready(self) -> bool:
         """The steady state a captured tick assumes: GPU, full ring (head
         advances by one per tick), warm window (every tick graduates), the
@@ -332,7 +357,8 @@ class StreamingShard:
                 K.reserve_graph_workspace(self.device, self.hist.data.shape[0])
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
-                    K.tick_advance(self._state_dev, R, W, self._h_dev, self._h_buf)
+                    K.tick_advance(self._state_dev, R, W, self._h_dev, self._h_buf, bell=self._bell,
+                                   bell_dev=self._bell_dev)
                     K.tick_ingest(self.hist.data, 0, self.cur.data, self.cur.P, self.cur.W, 0, newv,
                                   base=self.base if newb is not None else None, newb=newb, state=self._state_dev,
                                   zero=self.app_stats.view(-1))

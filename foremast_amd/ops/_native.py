@@ -139,7 +139,7 @@ def _declare(lib: C.CDLL) -> None:
     lib.fm_tick_ingest_dev.restype = I
     lib.fm_copy_to_host_i32.argtypes = [P, P, LL, P]
     lib.fm_copy_to_host_i32.restype = I
-    lib.fm_tick_advance.argtypes = [P, I, I, P, I, P, P]
+    lib.fm_tick_advance.argtypes = [P, I, I, P, I, P, P, P, LL, P]
     lib.fm_tick_advance.restype = I
     for name, args in _EXTRA.items():
         fn = getattr(lib, name, None)

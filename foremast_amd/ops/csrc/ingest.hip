@@ -117,9 +117,31 @@ extern "C" int fm_copy_to_host_i32(int* dst_host, const int* src, long long n, h
 // `head`, which then moves by one; the window slot cycles mod W) and copies
 // the forecast horizons of the new slot from a device table, so a replay needs
 // no host-to-device copy at all.
+// Doorbell (optional): a tick graph enqueued before its input is released starts with this
+// kernel spinning until the host's pinned counter `bell` reaches the replay's number
+// (bell_dev[0] + 1, kept on the device so one captured graph serves every tick), so the
+// tick starts a PCIe write after the host releases it instead of a graph launch after it.
+// bell_dev[1] counts waits that gave up after `limit` wall-clock ticks (the tick then runs
+// on whatever input it has; the host checks the count).
 __global__ __launch_bounds__(256) void tick_advance_kernel(int* __restrict__ st, int R, int W,
                                                            const int* __restrict__ h_table, int nh,
-                                                           int* __restrict__ h_buf) {
+                                                           int* __restrict__ h_buf, const int* bell,
+                                                           int* __restrict__ bell_dev, long long limit) {
+  if (bell) {
+    if (threadIdx.x == 0) {
+      const int want = bell_dev[0] + 1;
+      const long long t0 = wall_clock64();
+      while (__hip_atomic_load(bell, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
+        if (wall_clock64() - t0 > limit) {
+          bell_dev[1] += 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      bell_dev[0] = want;
+    }
+    __syncthreads();
+  }
   const int head = st[3], slot = st[1];
   __syncthreads();  // every thread has the previous record before thread 0 rewrites it
   const int nslot = slot + 1 < W ? slot + 1 : 0;
@@ -135,9 +157,12 @@ __global__ __launch_bounds__(256) void tick_advance_kernel(int* __restrict__ st,
   }
 }
 
-extern "C" int fm_tick_advance(int* state, int R, int W, const int* h_table, int nh, int* h_buf, hipStream_t st) {
-  if (!state || R <= 0 || W <= 0 || (h_table && (!h_buf || nh <= 0))) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(tick_advance_kernel, dim3(1), dim3(256), 0, st, state, R, W, h_table, nh, h_buf);
+extern "C" int fm_tick_advance(int* state, int R, int W, const int* h_table, int nh, int* h_buf, const int* bell,
+                               int* bell_dev, long long limit, hipStream_t st) {
+  if (!state || R <= 0 || W <= 0 || (h_table && (!h_buf || nh <= 0)) || (bell && (!bell_dev || limit <= 0)))
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(tick_advance_kernel, dim3(1), dim3(256), 0, st, state, R, W, h_table, nh, h_buf, bell, bell_dev,
+                     limit);
   return (int)hipGetLastError();
 }
 

@@ -894,11 +894,17 @@ def ring_append(dst: torch.Tensor, col0: int, src: torch.Tensor, col_dev: Option
               "fm_ring_append")
 
 
+DOORBELL_LIMIT = 200_000_000  # wall-clock ticks a doorbell wait spins before giving up (2 s at 100 MHz)
+
+
 def tick_advance(state: torch.Tensor, R: int, W: int, h_table: Optional[torch.Tensor] = None,
-                 h_buf: Optional[torch.Tensor] = None) -> None:
+                 h_buf: Optional[torch.Tensor] = None, bell: Optional[torch.Tensor] = None,
+                 bell_dev: Optional[torch.Tensor] = None) -> None:
     """Advance the device tick record ``state`` (int32 ``{hist_col, slot,
     graduate, head}``) by one steady-state tick and copy row ``(slot + 1) mod W``
-    of ``h_table`` (int32 ``[W, nh]``) into ``h_buf`` (csrc/ingest.hip)."""
+    of ``h_table`` (int32 ``[W, nh]``) into ``h_buf`` (csrc/ingest.hip).
+    ``bell`` (pinned host int32 [1]) / ``bell_dev`` (device int32 [2]): first wait until
+    the host's counter reaches ``bell_dev[0] + 1`` (the doorbell of a pre-enqueued tick)."""
     lib = nat.require()
     _cuda(state, "state")
     _need(state.dtype == torch.int32 and state.numel() >= 4 and state.is_contiguous(), "state must be int32 [>=4]")
@@ -909,7 +915,12 @@ def tick_advance(state: torch.Tensor, R: int, W: int, h_table: Optional[torch.Te
               and h_buf.numel() == h_table.shape[1] and h_table.device == state.device
               and h_buf.device == state.device, "h_table must be int32 [W, nh] and h_buf int32 [nh]")
         nh = int(h_table.shape[1])
+    if bell is not None:
+        _need(bell.dtype == torch.int32 and bell.numel() >= 1 and not bell.is_cuda and bell.is_pinned()
+              and bell_dev is not None and bell_dev.dtype == torch.int32 and bell_dev.numel() >= 2
+              and bell_dev.device == state.device, "bell must be pinned host int32 [1], bell_dev device int32 [2]")
     nat.check(lib.fm_tick_advance(nat.ptr(state), int(R), int(W), nat.ptr(h_table), nh, nat.ptr(h_buf),
+                                  nat.ptr(bell), nat.ptr(bell_dev), DOORBELL_LIMIT if bell is not None else 0,
                                   nat.stream_handle(state.device)), "fm_tick_advance")
 
 

@@ -227,3 +227,16 @@ def test_double_buffered_graph_input_matches_single_buffer():
     assert got["config"]["input_prefetch"] and not ref["config"]["input_prefetch"]
     assert got["config"]["hip_graph"] and ref["config"]["hip_graph"]
     assert got["health"] == ref["health"] and got["detection"] == ref["detection"]
+
+
+@pytest.mark.gpu
+def test_doorbell_graph_ticks_match_plain_graph_ticks():
+    """--doorbell: tick k+1's graph is enqueued while tick k runs and waits on the device for
+    the host's pinned counter; every wait is rung (no timeout) and the health table and
+    detection equal the plain graph ticks'."""
+    args = CANARY + ["--steps", "6"]
+    ref = _bench(args + ["--no-doorbell"], force=False, launcher=False, cpu=False)
+    got = _bench(args + ["--doorbell"], force=False, launcher=False, cpu=False)
+    assert got["config"]["doorbell"] and not ref["config"]["doorbell"]
+    assert got["config"]["hip_graph"] and got["config"]["doorbell_timeouts"] == 0
+    assert got["health"] == ref["health"] and got["detection"] == ref["detection"]
