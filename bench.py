@@ -141,6 +141,9 @@ def parse():
     p.add_argument("--spin-wait", dest="spin_wait", action="store_true", default=False,
                    help="canary: wait for a tick's completion by polling its event instead of a blocking stream "
                         "synchronize (shorter host wake-up between ticks)")
+    p.add_argument("--overlap-pairwise", action="store_true",
+                   help="run the rank tests on a side stream beside the fit at any shard size (the default from "
+                        "16,384 series per rank, engine.OVERLAP_MIN_SERIES)")
     p.add_argument("--serial-pairwise", action="store_true",
                    help="run the rank tests on the main stream before the fit (fused detect epilogue) "
                         "instead of on a side stream concurrently with it")
@@ -412,6 +415,9 @@ def setup_canary(args, world, rank, dev):
                            bound=torch.full((n_local,), 3, dtype=torch.int8, device=dev), **fused)
     if args.serial_pairwise:
         shard.overlap_pairwise = False
+    elif args.overlap_pairwise:
+        shard.overlap_pairwise = True
+    PW_OVERLAP[0] = bool(shard.overlap_pairwise)
     # --- synthetic data (outside the timed region) ---------------------------------
     # every datum is a function of the GLOBAL series index: N ranks score exactly the
     # series the one-rank run scores (tests/test_parallel.py::test_bench_n_rank_equals_one_rank)
@@ -757,6 +763,7 @@ LAT_START = {}  # timed tick -> perf_counter time its data arrived (set by the p
 REFIT_FLAGS = {}  # tick -> whether it refit the model (canary --refit-every)
 GRAPH_TAIL = [False]  # canary: the health collective + copy back ran inside the tick graph
 DOORBELL = [None]     # canary --doorbell: the shard (its doorbell waits that timed out are recorded)
+PW_OVERLAP = [None]   # canary: rank tests on a side stream beside the fit (True) or before it
 
 
 def prom_bodies(host_ticks, s, P, ring, threads, pin):
@@ -1124,6 +1131,8 @@ def main():
         meta["health_tail_in_graph"] = GRAPH_TAIL[0]
         if DOORBELL[0] is not None:
             meta["doorbell_timeouts"] = DOORBELL[0].doorbell_timeouts()
+        if PW_OVERLAP[0] is not None:
+            meta["pairwise_overlap"] = "side stream beside the fit" if PW_OVERLAP[0] else "before the fit (fused detect)"
         if GRAPH_TAIL[0] and meta.get("health_collectives", "none") != "none":
             meta["health_collectives"] += " (captured in the tick graph)"
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)

@@ -32,6 +32,8 @@ from ..models import pairwise as pw_ref
 from ..models import smoothing as sm_ref
 from ..utils.config import BrainConfig
 
+OVERLAP_MIN_SERIES = 16384  # StreamingShard.overlap_pairwise default threshold
+
 ALGO_MODE = {"exponential_smoothing": sm_ref.MODE_ES, "double_exponential_smoothing": sm_ref.MODE_DES,
              "holt_winters": sm_ref.MODE_HW}
 
@@ -115,7 +117,12 @@ class StreamingShard:
         self._graph_io = None
         self._graphs: Dict[tuple, tuple] = {}   # io buffers -> (graph, post captured, outputs)
         self._side = None                # side HIP stream for the rank tests (overlap_pairwise)
-        self.overlap_pairwise = self.gpu
+        # rank tests on a side stream beside the fit (deferred detection) from OVERLAP_MIN_SERIES
+        # series; below, before the fit on the main stream with the detection fused into the
+        # fit (the side stream's join and the separate detection kernel cost more than the
+        # rank tests of a small shard: 12.5k 1.210 vs 1.218 ms, 25k 2.370 vs 2.360,
+        # profiles/bench/serial_r6/)
+        self.overlap_pairwise = self.gpu and N >= OVERLAP_MIN_SERIES
         if self.gpu:
             # graph-tick ring state: a ring of pinned sources, so a copy still in flight
             # (pipelined ticks, at most two ahead) never sees the next tick's values

@@ -141,11 +141,13 @@ def test_streaming_monitor_resumes_from_snapshot(tmp_path):
 
 
 @pytest.mark.gpu
-def test_graph_tick_matches_eager():
+@pytest.mark.parametrize("overlap", [True, False])
+def test_graph_tick_matches_eager(overlap):
     """tick_graph (ingest + rank tests + HW fit as one HIP-graph replay, ring state
     read from device memory) gives the same outputs as the eager calls, tick for
     tick, through the ring wrap, the window slot cycle and eager ticks in between
-    (the device tick record resyncs)."""
+    (the device tick record resyncs); with the rank tests on a side stream beside the
+    fit (the default from OVERLAP_MIN_SERIES series) and before it on the main stream."""
     from foremast_amd.brain.engine import ShardSpec, StreamingShard, synthetic_history
     from foremast_amd.ingest.ringbuffer import RingState
     from foremast_amd.ops import _native
@@ -160,6 +162,7 @@ def test_graph_tick_matches_eager():
     for _ in range(2):
         sh = StreamingShard(ShardSpec(n_series=n, ring_len=R, season=m, pods=P, window=W, n_apps=8), cfg, dev,
                             app_id=(torch.arange(n, device=dev) % 8).int())
+        sh.overlap_pairwise = overlap
         sh.load_history(hist[:, :R])
         # start near the end of the ring so the head wraps during the run (same data in both)
         sh.hist.state = RingState(head=R - 12, length=R)
