@@ -114,39 +114,40 @@ __global__ __launch_bounds__(256, (M > 144 || (M > 96 && GPT == 2)) ? 1 : 2) voi
 
   if (tid < SW) nanc[tid] = 0;
   __syncthreads();
-  // staging: element i = r Tp + tau of the workgroup's rows, i = tid + 256 j; SEQ_LD loads in
-  // flight per thread before any is converted and stored (issued one row at a time, waiting
-  // on each, the staging was a chain of ~16 global-memory round trips per workgroup)
+  // staging: wave w stages rows w, w + 4, ..; lane l columns l, l + 64, ..  (a row's base
+  // is wave-uniform, so an element costs a 32-bit offset, no division by Tp).  SEQ_LD loads
+  // per lane are in flight before any is converted and stored
   const TIN* base = (const TIN*)a.hist;
-  const int total = SW * Tp;
-  for (int i0 = 0; i0 < total; i0 += 256 * SEQ_LD) {
-    unsigned u[SEQ_LD];
-    bool in[SEQ_LD];
-    int at[SEQ_LD];
+  const int wv = tid >> 6, ln = tid & 63;
+  for (int r = wv; r < SW; r += 256 / 64) {
+    const int nn = n0 + r;
+    const bool rowok = nn < a.N;
+    const TIN* rowp = base + (long long)(rowok ? nn : 0) * a.ld;
+    for (int q0 = 0; q0 < Tp; q0 += 64 * SEQ_LD) {
+      unsigned u[SEQ_LD];
 #pragma unroll
-    for (int j = 0; j < SEQ_LD; ++j) {
-      const int i = i0 + tid + 256 * j;
-      const int r = (unsigned)i / (unsigned)Tp, tau = i - r * Tp;
-      const int nn = n0 + r, t = tau - pad;
-      in[j] = i < total && nn < a.N && t >= 0;
-      at[j] = i < total ? r * LDY + tau : -1;
-      int c = head + t;
-      c -= c >= R ? R : 0;
-      // unconditional loads (an element past the rows / the padding reads element 0 and is
-      // replaced), held by the asm below: a load the compiler sinks under a branch is waited
-      // for at the branch's join, one global-memory round trip per element
-      u[j] = ld_bits<TIN>(base + (in[j] ? (long long)nn * a.ld + c : 0));
-    }
+      for (int j = 0; j < SEQ_LD; ++j) {
+        const int tau = q0 + 64 * j + ln, t = tau - pad;
+        const bool in = rowok && tau < Tp && t >= 0;
+        int c = head + t;
+        c -= c >= R ? R : 0;
+        // unconditional loads (an element outside reads the row's first and is replaced),
+        // held by the asm below: a load under a branch is waited for at the branch's join
+        u[j] = ld_bits<TIN>(rowp + (in ? c : 0));
+      }
 #pragma unroll
-    for (int j = 0; j < SEQ_LD; ++j) asm volatile("" : "+v"(u[j]));
+      for (int j = 0; j < SEQ_LD; ++j) asm volatile("" : "+v"(u[j]));
 #pragma unroll
-    for (int j = 0; j < SEQ_LD; ++j) {
-      if (at[j] < 0) break;
-      const float x = in[j] ? bits_f32_<TIN>(u[j]) : fm_nan();
-      const bool ok = x == x;
-      ys[at[j]] = ok ? x : 0.f;
-      ks[at[j]] = ok ? 1.f : 0.f;
-      if (!ok && at[j] % LDY >= M) atomicAdd(&nanc[at[j] / LDY], 1);  // rare: gaps (padding is in season 0)
+      for (int j = 0; j < SEQ_LD; ++j) {
+        const int tau = q0 + 64 * j + ln, t = tau - pad;
+        if (tau < Tp) {
+          const float x = (rowok && t >= 0) ? bits_f32_<TIN>(u[j]) : fm_nan();
+          const bool ok = x == x;
+          ys[r * LDY + tau] = ok ? x : 0.f;
+          ks[r * LDY + tau] = ok ? 1.f : 0.f;
+          if (!ok && tau >= M) atomicAdd(&nanc[r], 1);  // rare: gaps (the front padding is in season 0)
+        }
+      }
     }
   }
   __syncthreads();

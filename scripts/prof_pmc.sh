@@ -6,6 +6,7 @@
 #   dec   — seasonal decomposition
 #   es    — ES / DES sequential fit (and the time-parallel scan variants)
 #   rank  — rank tests, small-window sort path and the pairwise sweep (100k x 55 + 55)
+#   seq   — Holt-Winters variant 6 (hw_seq.hip) at a short season (SEASON, default 72)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TARGET=${TARGET:-hw}
@@ -19,6 +20,7 @@ case $TARGET in
   lstm) CMD=("$PWD/scripts/bench_lstm_kernels.py") ;;
   rank) CMD=("$PWD/scripts/bench_rank.py") ;;
   gaps) CMD=("$PWD/scripts/bench_hw_gaps.py" --series 20000 --rounds 1 --cases ${CASES:-dense,dgall,miss1e-3}) ;;
+  seq)  CMD=("$PWD/scripts/bench_hw_gaps.py" --series 100000 --rounds 1 --season ${SEASON:-72} --cases dense) ;;
 esac
 SETS=("SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS"
       "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU"
