@@ -20,14 +20,17 @@
 // coordinates: e = (y - s) - f;  f' = (f + b) + c1 e;  b' = b + c2 e;  s' = s + g e, with
 // c1 = alpha (1 + beta), c2 = alpha beta, g = gamma (1 - alpha); level = f - b at the end.
 //
-// Per step and grid-point pair: 6 packed FP32 ops, a dependency chain of two (e, f), gaps
-// included: the staging (one coalesced pass of each workgroup's rows) writes two fp32 LDS
-// images, y with a missing point as 0 and a keep factor k (row stride Tp + 4: 16-byte
-// ds_reads of four steps), and e = k (y - s - f) costs the same two fmas as (y - s) - f
-// (seq_step).  One code path: a branch between a plain and a masked season walk kept two
-// copies of the 2 m season registers live (234 VGPRs at m = 48, spills from m = 72).  The band / verdict
-// epilogue is fm_hw_detect_params (the fit writes the first HALF_HB seasonal phases and the
-// valid count), as for every deferred HW fit.
+// Per step and grid-point pair: 7 packed FP32 ops (6 fmas and f + b), a dependency chain of
+// two (e, f), gaps included: the staging (one coalesced pass of each workgroup's rows) writes
+// two fp32 LDS images, y with a missing point as 0 and a keep factor k (row stride Tp + 4:
+// 16-byte ds_reads of four steps), and e = k (y - s - f) costs the same two fmas as
+// (y - s) - f (seq_step).  One code path: a branch between a plain and a masked season walk
+// kept two copies of the 2 m season registers live (234 VGPRs at m = 48, spills from
+// m = 72).  The band / verdict epilogue is fm_hw_detect_params (the fit writes the first
+// HALF_HB seasonal phases and the valid count), as for every deferred HW fit.  m = 288 (the
+// 300 s step) is instantiated as an opt-in (see seq_gpt).  PMC at m = 72: the season walk is
+// ~80 % of the kernel's VALU, which issues in ~83 % of the slots
+// (profiles/hw_r6/seq/pmc/).
 #include "common.h"
 #include "args.h"
 
