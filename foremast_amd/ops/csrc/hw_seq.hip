@@ -44,6 +44,7 @@ namespace {
 
 constexpr int SEQ_HB = 16;  // seasonal phases written to season_hb (kernels.py HALF_HB)
 constexpr int SEQ_LD = 8;   // staging loads in flight per thread
+constexpr int SEQ_BUF_DW3 = 0x00020000;  // buffer resource word 3 (raw access) on gfx950
 
 template <int GPT> struct SeqVec;
 template <> struct SeqVec<1> { using type = float; };
@@ -121,11 +122,13 @@ __global__ __launch_bounds__(256, (M > 144 || (M > 96 && GPT == 2)) ? 1 : 2) voi
   // is wave-uniform, so an element costs a 32-bit offset, no division by Tp).  SEQ_LD loads
   // per lane are in flight before any is converted and stored
   const TIN* base = (const TIN*)a.hist;
-  const int wv = tid >> 6, ln = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), ln = tid & 63;  // wave-uniform row
   for (int r = wv; r < SW; r += 256 / 64) {
     const int nn = n0 + r;
     const bool rowok = nn < a.N;
-    const TIN* rowp = base + (long long)(rowok ? nn : 0) * a.ld;
+    // the row as a raw buffer (wave-uniform descriptor): an element costs a 32-bit offset
+    const __amdgpu_buffer_rsrc_t rowb = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(base + (long long)(rowok ? nn : 0) * a.ld), (short)0, (int)(R * (int)sizeof(TIN)), SEQ_BUF_DW3);
     for (int q0 = 0; q0 < Tp; q0 += 64 * SEQ_LD) {
       unsigned u[SEQ_LD];
 #pragma unroll
@@ -136,7 +139,9 @@ __global__ __launch_bounds__(256, (M > 144 || (M > 96 && GPT == 2)) ? 1 : 2) voi
         c -= c >= R ? R : 0;
         // unconditional loads (an element outside reads the row's first and is replaced),
         // held by the asm below: a load under a branch is waited for at the branch's join
-        u[j] = ld_bits<TIN>(rowp + (in ? c : 0));
+        const unsigned off = (unsigned)(in ? c : 0) * (unsigned)sizeof(TIN);
+        if constexpr (sizeof(TIN) == 2) u[j] = (unsigned)__builtin_amdgcn_raw_buffer_load_b16(rowb, off, 0u, 0);
+        else u[j] = __builtin_amdgcn_raw_buffer_load_b32(rowb, off, 0u, 0);
       }
 #pragma unroll
       for (int j = 0; j < SEQ_LD; ++j) asm volatile("" : "+v"(u[j]));
