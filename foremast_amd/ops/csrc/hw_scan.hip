@@ -2215,11 +2215,16 @@ __device__ __forceinline__ void hw_dg_block(const SmoothArgs& a, int hmax, int n
       if (upd0) { bestSSE = sse.x; bestIdx = c0; bestL = X1.x - X2.x; bestB = X2.x; }
       const bool upd1 = (c1i != c0) && (sse.y < bestSSE || (sse.y == bestSSE && c1i < bestIdx));
       if (upd1) { bestSSE = sse.y; bestIdx = c1i; bestL = X1.y - X2.y; bestB = X2.y; }
-      if (j == 0 && (upd0 || upd1)) {
+      // the forecast's seasonal phases 0 .. hmax - 1 from the lanes that own them: lane 0 alone
+      // while hmax <= K; at K = 9 (the gapped pairs of the 300 s step's quad path, which takes
+      // horizons up to 16) phases 9 .. 15 are lane 1's
+      if ((upd0 || upd1) && j * K < hmax) {
         const float* yl = ylast + half * HALF_HB;
 #pragma unroll
-        for (int i = 0; i < K && i < HALF_HB; ++i)
-          if (i < hmax) mybest[i] = yl[i] - (upd1 ? D[i].y : D[i].x);
+        for (int i = 0; i < K && i < HALF_HB; ++i) {
+          const int ph = j * K + i;
+          if (ph < hmax && ph < HALF_HB) mybest[ph] = yl[ph] - (upd1 ? D[i].y : D[i].x);
+        }
       }
       if (PRUNE && j == 0 && (upd0 || upd1))
         __hip_atomic_fetch_min(ubound + half, __float_as_uint(bestSSE), __ATOMIC_RELAXED,

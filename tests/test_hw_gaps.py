@@ -256,3 +256,40 @@ def test_quad_kernel_matches_pair_kernel_at_300s(K, case, monkeypatch):
     ref = sm_ref.fit_smoothing(torch.tensor(ring.float().cpu().numpy(), dtype=torch.float64), sm_ref.MODE_HW,
                                GRID.double(), m=m)
     np.testing.assert_allclose(outs[0]["sigma"].cpu().numpy(), ref.sigma.numpy(), rtol=5e-3)
+
+
+@pytest.mark.parametrize("case", ["miss", "outage"])
+def test_quad_path_gapped_pairs_forecast_long_horizons(K, case):
+    """At m = 288 the quad path takes forecast horizons up to 16 while its gapped pairs run the
+    32-lane K = 9 gapped kernel: the seasonal phases 9..15 of a series come from the lane that
+    owns them (lane 1).  Before the fix they were never written, so horizons >= 10 read stale
+    LDS (the 300 s canary with isolated misses flagged 17,459 of 20,000 healthy apps)."""
+    dev = torch.device("cuda:0")
+    m, N = 288, 24
+    T = 7 * m
+    y = _series(N, T, m, seed=77)
+    rng = np.random.default_rng(78)
+    if case == "miss":
+        y[rng.random(y.shape) < 2e-3] = np.nan
+    else:
+        y[::2, 4 * m + 30:4 * m + 36] = np.nan
+    ring = torch.tensor(y, device=dev).to(torch.bfloat16)
+    yl = ring.float().cpu().numpy()
+    C = 16
+    hz = torch.arange(1, C + 1, dtype=torch.int32)
+    cur = torch.tensor(np.nan_to_num(y[:, -C:], nan=20.0), device=dev)
+    spec = K.DetectSpec(horizons=hz.to(dev), threshold=torch.full((N,), 4.0, device=dev),
+                        bound=torch.full((N,), 3, dtype=torch.int8, device=dev),
+                        min_lower=torch.full((N,), -1e30, device=dev), cur=cur, max_horizon=C)
+    K.hw_clear_gap_flags()
+    before = K.hw_deferred_total(dev)
+    out = K.smoothing_fit(ring, 0, T, sm_ref.MODE_HW, m, GRID.to(dev), spec, variant=5)
+    torch.cuda.synchronize()
+    assert K.last_hw_variant == 5 and K.hw_deferred_total(dev) > before   # gapped pairs took the K = 9 kernel
+    ref = sm_ref.fit_smoothing(torch.tensor(yl, dtype=torch.float64), sm_ref.MODE_HW, GRID.double(), m=m)
+    same = (out["best"].cpu().long() == ref.best).numpy()
+    assert same.mean() >= 0.75
+    f_ref = sm_ref.forecast(ref, hz.long())
+    np.testing.assert_allclose(out["forecast"].cpu().numpy()[same], f_ref.numpy()[same], rtol=5e-3, atol=2e-2)
+    d = _ref_detect(out, GRID, sm_ref.MODE_HW, m, hz, cur, thr=4.0)
+    assert torch.equal(d.verdict, out["verdict"].cpu())
